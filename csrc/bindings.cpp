@@ -1,0 +1,242 @@
+// dalgo torch-op registrations (TORCH_LIBRARY "dalgo").
+//
+// Every op validates shapes/dtypes/devices on the host (a kernel is never
+// launched on operands whose shape disagrees with what its grid assumes), then
+// calls the extern "C" launcher of the gfx950 kernel on the caller's current HIP
+// stream, so ops compose with torch streams and hipGraph capture. Launch
+// failures surface as c10::Error with the op name.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "launchers.h"
+
+namespace {
+
+using at::Tensor;
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define DALGO_CHECK_HIP(expr, name)                                                   \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    TORCH_CHECK(_e == hipSuccess, "dalgo::" name " launch failed: ", hipGetErrorString(_e)); \
+  } while (0)
+
+inline void check_dev(const Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda(), "dalgo: ", what, " must be a GPU (HIP) tensor");
+}
+inline void check_f32(const Tensor& t, const char* what) {
+  check_dev(t, what);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, "dalgo: ", what, " must be float32");
+  TORCH_CHECK(t.is_contiguous(), "dalgo: ", what, " must be contiguous");
+}
+
+inline uint32_t frac_threshold(double frac) {
+  if (frac <= 0.0) return 0u;
+  if (frac >= 1.0) return 0xffffffffu;
+  double t = std::floor(frac * 4294967296.0);
+  return t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+}
+
+void check_lr_inputs(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& seg,
+                     int64_t D, bool has_bias) {
+  check_dev(X, "X");
+  TORCH_CHECK(X.dim() == 2, "X must be 2-D");
+  TORCH_CHECK(X.scalar_type() == at::kBFloat16 || X.scalar_type() == at::kFloat,
+              "X must be bf16 or f32");
+  TORCH_CHECK(X.stride(1) == 1, "X rows must be contiguous");
+  const int vec = X.scalar_type() == at::kBFloat16 ? 8 : 4;
+  const int64_t ld = X.stride(0);
+  TORCH_CHECK(ld % vec == 0, "X row stride must be a multiple of ", vec, " elements (16 B)");
+  TORCH_CHECK(X.size(1) >= D && ld >= X.size(1), "X has fewer columns than D");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0, "X must be 16-B aligned");
+  TORCH_CHECK(ld <= dalgo_lr_max_cols(vec == 8), "row stride too large for lr kernels");
+  check_f32(y, "y");
+  TORCH_CHECK(y.numel() >= X.size(0), "y shorter than X");
+  check_f32(W, "W");
+  TORCH_CHECK(W.dim() == 2 && W.size(1) >= D + (has_bias ? 1 : 0), "W shape");
+  check_dev(seg, "seg");
+  TORCH_CHECK(seg.scalar_type() == at::kLong && seg.dim() == 1 && seg.numel() == W.size(0) + 1,
+              "seg must be int64 [n_seg+1]");
+  TORCH_CHECK(X.get_device() == W.get_device() && X.get_device() == y.get_device(),
+              "device mismatch");
+}
+
+// ---------------------------------------------------------------------------
+void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& seg,
+             int64_t row_offset, int64_t D, bool has_bias, double eps, int64_t seed, int64_t step,
+             double frac, int64_t gx, int64_t rows_per_block, Tensor slab, Tensor gslab,
+             Tensor cnt1, Tensor cnt2, Tensor G, Tensor C) {
+  check_lr_inputs(X, y, W, seg, D, has_bias);
+  const int64_t nseg = W.size(0);
+  TORCH_CHECK(gx >= 1 && gx <= 65535, "gx");
+  TORCH_CHECK(rows_per_block > 0 && rows_per_block % 256 == 0, "rows_per_block % 256");
+  const int64_t ngroups = (gx + 15) / 16;
+  check_f32(slab, "slab"); check_f32(gslab, "gslab"); check_f32(G, "G"); check_f32(C, "C");
+  const int64_t S = slab.size(1);
+  TORCH_CHECK(S >= D + 2, "slab stride");
+  TORCH_CHECK(slab.size(0) >= nseg * gx && gslab.size(0) >= nseg * ngroups &&
+              gslab.size(1) == S, "slab/gslab shape");
+  TORCH_CHECK(cnt1.scalar_type() == at::kInt && cnt1.numel() >= nseg * ngroups, "cnt1");
+  TORCH_CHECK(cnt2.scalar_type() == at::kInt && cnt2.numel() >= nseg, "cnt2");
+  TORCH_CHECK(G.dim() == 2 && G.size(0) == nseg && G.size(1) == W.size(1), "G shape");
+  TORCH_CHECK(C.numel() >= nseg, "C shape");
+  c10::hip::HIPGuard guard(X.device());
+  const bool full = frac >= 1.0;
+  DALGO_CHECK_HIP(
+      dalgo_lr_grad(X.data_ptr(), y.data_ptr<float>(), W.data_ptr<float>(), seg.data_ptr<int64_t>(),
+                    X.stride(0), row_offset, (int)D, (int)W.size(1), has_bias ? 1 : 0, (float)eps,
+                    (uint64_t)seed, (uint64_t)step, frac_threshold(frac), full ? 1 : 0,
+                    X.scalar_type() == at::kBFloat16 ? 1 : 0, (int)gx, (int)nseg,
+                    (int)rows_per_block, slab.data_ptr<float>(), gslab.data_ptr<float>(),
+                    reinterpret_cast<unsigned*>(cnt1.data_ptr<int>()),
+                    reinterpret_cast<unsigned*>(cnt2.data_ptr<int>()), G.data_ptr<float>(),
+                    C.data_ptr<float>(), (int)S, cur_stream()),
+      "lr_grad");
+}
+
+void lr_eval(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& seg, int64_t D,
+             bool has_bias, double eps, int64_t gx, int64_t rows_per_block, Tensor correct,
+             Tensor loss) {
+  check_lr_inputs(X, y, W, seg, D, has_bias);
+  const int64_t nseg = W.size(0);
+  TORCH_CHECK(rows_per_block > 0 && rows_per_block % 256 == 0, "rows_per_block % 256");
+  TORCH_CHECK(correct.scalar_type() == at::kLong && correct.numel() >= nseg, "correct");
+  check_f32(loss, "loss");
+  TORCH_CHECK(loss.numel() >= nseg, "loss");
+  c10::hip::HIPGuard guard(X.device());
+  DALGO_CHECK_HIP(
+      dalgo_lr_eval(X.data_ptr(), y.data_ptr<float>(), W.data_ptr<float>(), seg.data_ptr<int64_t>(),
+                    X.stride(0), (int)D, (int)W.size(1), has_bias ? 1 : 0, (float)eps,
+                    X.scalar_type() == at::kBFloat16 ? 1 : 0, (int)gx, (int)nseg,
+                    (int)rows_per_block,
+                    reinterpret_cast<unsigned long long*>(correct.data_ptr<int64_t>()),
+                    loss.data_ptr<float>(), cur_stream()),
+      "lr_eval");
+}
+
+// ---------------------------------------------------------------------------
+void sync_update(Tensor W, const std::optional<Tensor>& G, const std::optional<Tensor>& C,
+                 const std::optional<Tensor>& center, const std::optional<Tensor>& S,
+                 const std::optional<Tensor>& Dl, const std::optional<Tensor>& count_acc, int64_t n,
+                 int64_t mode, int64_t reg, double eta, double lam, double alpha, double reg_alpha,
+                 double mu, double zeta, double beta, double inv_p) {
+  check_f32(W, "W");
+  TORCH_CHECK(W.dim() == 2 && n <= W.size(1), "W must be [rows, ld] with n <= ld");
+  const int64_t nrow = W.size(0), ld = W.size(1);
+  auto ptr = [&](const std::optional<Tensor>& t, const char* nm, int64_t need) -> float* {
+    if (!t.has_value()) return nullptr;
+    check_f32(*t, nm);
+    TORCH_CHECK(t->numel() >= need, "dalgo::sync_update: ", nm, " too small");
+    return t->data_ptr<float>();
+  };
+  float* g = ptr(G, "G", nrow * ld);
+  float* c = ptr(C, "C", nrow);
+  float* ce = ptr(center, "center", n);
+  float* s = ptr(S, "S", n);
+  float* dl = ptr(Dl, "Dl", n);
+  double* cacc = nullptr;
+  if (count_acc.has_value()) {
+    check_dev(*count_acc, "count_acc");
+    TORCH_CHECK(count_acc->scalar_type() == at::kDouble && count_acc->numel() >= 1, "count_acc f64");
+    TORCH_CHECK(c, "count_acc needs C");
+    cacc = count_acc->data_ptr<double>();
+  }
+  switch (mode) {
+    case 0: TORCH_CHECK(g && c, "SSGD needs G, C"); break;
+    case 1: TORCH_CHECK(g, "GD needs G"); break;
+    case 2: TORCH_CHECK(g && c, "local needs G, C"); break;
+    case 3: TORCH_CHECK(g && c && ce, "elastic local needs G, C, center"); break;
+    case 4: case 6: TORCH_CHECK(s && nrow == 1, "sync needs S and one row"); break;
+    case 5: TORCH_CHECK(s && dl && nrow == 1, "BMUF needs S, Dl and one row"); break;
+    default: TORCH_CHECK(false, "unknown update mode ", mode);
+  }
+  c10::hip::HIPGuard guard(W.device());
+  DALGO_CHECK_HIP(dalgo_sync_update(W.data_ptr<float>(), g, c, ce, s, dl, cacc, (int)n, (int)ld,
+                                    (int)nrow, (int)mode, (int)reg, (float)eta, (float)lam,
+                                    (float)alpha, (float)reg_alpha, (float)mu, (float)zeta,
+                                    (float)beta, (float)inv_p, cur_stream()),
+                  "sync_update");
+}
+
+void rows_sum(const Tensor& W, int64_t n, Tensor out) {
+  check_f32(W, "W");
+  check_f32(out, "out");
+  TORCH_CHECK(W.dim() == 2 && n <= W.size(1) && out.numel() >= n, "rows_sum shapes");
+  c10::hip::HIPGuard guard(W.device());
+  DALGO_CHECK_HIP(dalgo_rows_sum(W.data_ptr<float>(), (int)W.size(0), (int)W.size(1), (int)n,
+                                 out.data_ptr<float>(), cur_stream()),
+                  "rows_sum");
+}
+
+void rows_broadcast(Tensor W, int64_t n, const Tensor& src) {
+  check_f32(W, "W");
+  check_f32(src, "src");
+  TORCH_CHECK(W.dim() == 2 && n <= W.size(1) && src.numel() >= n, "rows_broadcast shapes");
+  c10::hip::HIPGuard guard(W.device());
+  DALGO_CHECK_HIP(dalgo_rows_broadcast(W.data_ptr<float>(), (int)W.size(0), (int)W.size(1),
+                                       (int)n, src.data_ptr<float>(), cur_stream()),
+                  "rows_broadcast");
+}
+
+// ---------------------------------------------------------------------------
+void philox_fill(Tensor out, int64_t D, int64_t row_offset, int64_t seed, int64_t stream,
+                 int64_t dist, double a, double b) {
+  check_dev(out, "out");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1, "philox_fill: out must be 2-D, row-contiguous");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat,
+              "philox_fill: bf16 or f32");
+  TORCH_CHECK(out.stride(0) == out.size(1), "philox_fill: out must be contiguous");
+  TORCH_CHECK(D <= out.size(1), "philox_fill: D > columns");
+  TORCH_CHECK(dist == 0 || dist == 1, "philox_fill: dist");
+  c10::hip::HIPGuard guard(out.device());
+  DALGO_CHECK_HIP(dalgo_philox_fill(out.data_ptr(), out.scalar_type() == at::kBFloat16 ? 1 : 0,
+                                    out.size(0), D, out.size(1), row_offset, (uint64_t)seed,
+                                    (uint64_t)stream, (int)dist, (float)a, (float)b, cur_stream()),
+                  "philox_fill");
+}
+
+void mc_pi(int64_t seed, int64_t stream, int64_t offset, int64_t n, Tensor count) {
+  check_dev(count, "count");
+  TORCH_CHECK(count.scalar_type() == at::kLong && count.numel() >= 1, "mc_pi: count int64[1]");
+  TORCH_CHECK(offset % 2 == 0 && n >= 0, "mc_pi: offset must be even");
+  c10::hip::HIPGuard guard(count.device());
+  DALGO_CHECK_HIP(dalgo_mc_pi((uint64_t)seed, (uint64_t)stream, (uint64_t)offset, (uint64_t)n,
+                              reinterpret_cast<unsigned long long*>(count.data_ptr<int64_t>()),
+                              cur_stream()),
+                  "mc_pi");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(dalgo, m) {
+  m.def("lr_grad(Tensor X, Tensor y, Tensor W, Tensor seg, int row_offset, int D, bool has_bias, "
+        "float eps, int seed, int step, float frac, int gx, int rows_per_block, Tensor(a!) slab, "
+        "Tensor(b!) gslab, Tensor(c!) cnt1, Tensor(d!) cnt2, Tensor(e!) G, Tensor(f!) C) -> ()");
+  m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
+        "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss) -> ()");
+  m.def("sync_update(Tensor(a!) W, Tensor? G, Tensor? C, Tensor? center, Tensor? S, "
+        "Tensor(b!)? Dl, Tensor(c!)? count_acc, int n, int mode, int reg, float eta, float lam, float alpha, "
+        "float reg_alpha, float mu, float zeta, float beta, float inv_p) -> ()");
+  m.def("rows_sum(Tensor W, int n, Tensor(a!) out) -> ()");
+  m.def("rows_broadcast(Tensor(a!) W, int n, Tensor src) -> ()");
+  m.def("philox_fill(Tensor(a!) out, int D, int row_offset, int seed, int stream, int dist, "
+        "float a, float b) -> ()");
+  m.def("mc_pi(int seed, int stream, int offset, int n, Tensor(a!) count) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
+  m.impl("lr_grad", &lr_grad);
+  m.impl("lr_eval", &lr_eval);
+  m.impl("sync_update", &sync_update);
+  m.impl("rows_sum", &rows_sum);
+  m.impl("rows_broadcast", &rows_broadcast);
+  m.impl("philox_fill", &philox_fill);
+  m.impl("mc_pi", &mc_pi);   // dispatches on its output counter
+}

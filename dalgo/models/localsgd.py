@@ -1,0 +1,230 @@
+"""Parallel SGD for logistic regression: SSGD, full-batch GD, MA, BMUF, EASGD.
+
+One scaffold for the reference's five LR-family scripts (optimization/ssgd.py,
+optimization/ma.py, optimization/bmuf.py, optimization/easgd.py,
+machine_learning/logistic_regression.py). The Spark driver loop becomes an SPMD
+loop executed identically on every rank:
+
+  SSGD / GD (ssgd.py:93-105, logistic_regression.py:76-85)
+      K1+K7 fused sampled gradient  ->  all_reduce([g || count])  ->  K8 update
+  MA / BMUF (ma.py:93-106, bmuf.py:98-114)
+      reset locals to w (ma.py:96) -> n_local x [K1 on the SAME minibatch (seed 42+t
+      is constant inside a round, ma.py:99) -> K8 local step] -> sum locals ->
+      all_reduce -> K8 average / block-momentum rule
+  EASGD (easgd.py:95-106)
+      K1 -> K8 elastic local step (pull toward the old centre) -> sum locals ->
+      all_reduce -> K8 centre update with the NEW locals (sequential, as the reference)
+
+Logical workers (``n_workers`` = the reference's ``n_slices``) keep their Spark
+partition rows (99/99/99/101 on breast cancer) and are spread over the ranks, so
+a W-rank run and a 1-rank run with the same P compute the same thing. Each rank
+holds only its rows (HBM-resident shard); the model and all sync state are
+replicated, so no driver and no broadcast per iteration.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import asdict, dataclass, field
+
+import torch
+
+from dalgo.data.datasets import LRData
+from dalgo.ops import lr as lr_ops
+from dalgo.ops import update as U
+from dalgo.parallel import comm
+from dalgo.parallel.runtime import Runtime
+from dalgo.parallel.sharding import ShardLayout
+
+ALGOS = ("ssgd", "gd", "ma", "bmuf", "easgd")
+
+
+@dataclass
+class SGDConfig:
+    algo: str = "ssgd"
+    n_workers: int = 4            # n_slices (ssgd.py:17)
+    n_iterations: int = 1500      # ssgd.py:18 (ma/bmuf: 300)
+    eta: float = 0.1              # ssgd.py:19
+    frac: float = 0.1             # mini_batch_fraction (ssgd.py:20)
+    lam: float = 0.0              # ssgd.py:21
+    reg: str = "l2"               # reg_gradient(w, "l2") at ssgd.py:105
+    reg_alpha: float = 0.0
+    n_local: int = 5              # ma.py:23
+    mu: float = 0.9               # bmuf.py:24
+    zeta: float = 0.1             # bmuf.py:25
+    rho: float = 0.1              # easgd.py:23 (alpha = eta*rho, beta = P*alpha)
+    eps: float | None = None      # sigmoid epsilon: 0 (ssgd/gd) or 1e-6 (ma/bmuf/easgd)
+    sample_seed: int = 42         # sample(False, f, 42 + t)
+    init_seed: int = 0            # the reference's np.random.ranf is unseeded
+    reuse_minibatch: bool = True  # MA/BMUF: same sample for all local steps (ma.py:99)
+    eval_every: int = 1           # test accuracy every k rounds (0 = never)
+
+    def __post_init__(self):
+        if self.algo not in ALGOS:
+            raise ValueError(f"algo must be one of {ALGOS}")
+        if self.eps is None:
+            self.eps = 1e-6 if self.algo in ("ma", "bmuf", "easgd") else 0.0
+        if self.algo == "gd":
+            self.frac = 1.0
+
+    @property
+    def alpha(self) -> float:
+        return self.eta * self.rho
+
+    @property
+    def beta(self) -> float:
+        return self.n_workers * self.alpha
+
+
+@dataclass
+class TrainHistory:
+    accs: list = field(default_factory=list)
+    losses: list = field(default_factory=list)
+    iters: list = field(default_factory=list)
+
+
+def init_models(cfg: SGDConfig, ldw: int, dtype=torch.float64):
+    """Deterministic stand-in for the reference's unseeded U[-1, 1) draws.
+
+    Draw order follows the scripts: local models (ma.py:86), then w (ma.py:89),
+    then BMUF's delta_w (bmuf.py:95).
+    """
+    g = torch.Generator().manual_seed(cfg.init_seed)
+    out = {}
+    if cfg.algo in ("ma", "bmuf", "easgd"):
+        out["locals"] = 2 * torch.rand((cfg.n_workers, ldw), generator=g, dtype=dtype) - 1
+    out["w"] = 2 * torch.rand(ldw, generator=g, dtype=dtype) - 1
+    if cfg.algo == "bmuf":
+        out["delta"] = 2 * torch.rand(ldw, generator=g, dtype=dtype) - 1
+    return out
+
+
+class ParallelSGD:
+    def __init__(self, cfg: SGDConfig, data: LRData, layout: ShardLayout, rt: Runtime,
+                 model_dtype: torch.dtype = torch.float32):
+        self.cfg = cfg
+        self.data = data
+        self.layout = layout
+        self.rt = rt
+        dev = data.X_train.device
+        self.device = dev
+        if dev.type == "cuda" and model_dtype != torch.float32:
+            raise ValueError("GPU kernels keep f32 master weights")
+        self.D = data.D
+        self.ldw = self.D + 1
+        self.t = 0
+        self.history = TrainHistory()
+        P = cfg.n_workers
+        init = init_models(cfg, self.ldw)
+        self.w = init["w"].to(model_dtype).to(dev).view(1, -1).contiguous()
+        algo = cfg.algo
+        segs = layout.local_segments()
+        if algo in ("ssgd", "gd"):
+            self.seg = torch.tensor([0, layout.local_rows], dtype=torch.int64, device=dev)
+            self.max_seg = layout.local_rows
+            # fused all-reduce bucket [g (ldw) || count (1)]
+            self.bucket = comm.BucketedAllReduce([(1, self.ldw), (1,)], dtype=model_dtype, device=dev)
+            self.G, self.C = self.bucket.views
+        else:
+            self.seg = torch.tensor(segs, dtype=torch.int64, device=dev)
+            self.max_seg = max(segs[i + 1] - segs[i] for i in range(len(segs) - 1))
+            lo, hi = layout.worker_lo, layout.worker_hi
+            self.W = init["locals"][lo:hi].to(model_dtype).to(dev).contiguous()
+            self.G = torch.zeros((hi - lo, self.ldw), dtype=model_dtype, device=dev)
+            self.C = torch.zeros(hi - lo, dtype=model_dtype, device=dev)
+            self.S = torch.zeros(self.ldw, dtype=model_dtype, device=dev)
+            if algo == "bmuf":
+                self.Dl = init["delta"].to(model_dtype).to(dev).contiguous()
+        self.inv_p = 1.0 / P
+        # optional f64 device accumulator of global minibatch sizes (bench accounting)
+        self.count_acc: torch.Tensor | None = None
+
+    # ------------------------------------------------------------------ steps
+    def _grad(self, W, stream):
+        c = self.cfg
+        lr_ops.lr_grad(self.data.X_train, self.data.y_train, W, self.seg, D=self.D, has_bias=True,
+                       eps=c.eps, seed=c.sample_seed, step=stream, frac=c.frac,
+                       row_offset=self.data.row_offset, G=self.G, C=self.C,
+                       max_seg_rows=self.max_seg)
+
+    def step(self):
+        c = self.cfg
+        t = self.t
+        if c.algo in ("ssgd", "gd"):
+            self._grad(self.w, t)
+            self.bucket.all_reduce()
+            if c.algo == "ssgd":
+                U.sync_update(self.w, U.SSGD, G=self.G, C=self.C, reg=c.reg, eta=c.eta,
+                              lam=c.lam, reg_alpha=c.reg_alpha, count_acc=self.count_acc)
+            else:
+                U.sync_update(self.w, U.GD_SUM, G=self.G, C=self.C, eta=c.eta,
+                              count_acc=self.count_acc)
+        elif c.algo in ("ma", "bmuf"):
+            U.rows_broadcast(self.W, self.w)
+            for l in range(c.n_local):
+                stream = t if c.reuse_minibatch else t * c.n_local + l
+                self._grad(self.W, stream)
+                U.sync_update(self.W, U.LOCAL_MEAN, G=self.G, C=self.C, eta=c.eta)
+            U.rows_sum(self.W, self.S)
+            comm.all_reduce_sum(self.S)
+            if c.algo == "ma":
+                U.sync_update(self.w, U.AVERAGE, S=self.S, inv_p=self.inv_p)
+            else:
+                U.sync_update(self.w, U.BMUF, S=self.S, Dl=self.Dl, mu=c.mu, zeta=c.zeta,
+                              inv_p=self.inv_p)
+        else:  # easgd
+            self._grad(self.W, t)
+            U.sync_update(self.W, U.LOCAL_ELASTIC, G=self.G, C=self.C, center=self.w, eta=c.eta,
+                          alpha=c.alpha)
+            U.rows_sum(self.W, self.S)
+            comm.all_reduce_sum(self.S)
+            U.sync_update(self.w, U.ELASTIC_CENTER, S=self.S, beta=c.beta, inv_p=self.inv_p)
+        self.t += 1
+
+    def evaluate(self):
+        d = self.data
+        if d.X_test.shape[0] == 0:
+            return float("nan"), float("nan")
+        correct, loss = lr_ops.lr_eval(d.X_test, d.y_test, self.w, D=self.D, has_bias=True,
+                                       eps=self.cfg.eps)
+        return int(correct.item()) / d.X_test.shape[0], float(loss.item())
+
+    def fit(self, n_iterations: int | None = None, verbose: bool = False, callback=None):
+        n = self.cfg.n_iterations if n_iterations is None else n_iterations
+        acc = float("nan")
+        for _ in range(n):
+            if verbose:
+                self.rt.log("On iteration %d" % (self.t + 1))
+            self.step()
+            if self.cfg.eval_every and (self.t % self.cfg.eval_every == 0):
+                acc, loss = self.evaluate()
+                self.history.accs.append(acc)
+                self.history.losses.append(loss)
+                self.history.iters.append(self.t)
+                if verbose:
+                    self.rt.log("iterations: %d, accuracy: %f" % (self.t - 1, acc))
+            if callback is not None:
+                callback(self)
+        return self.history
+
+    # --------------------------------------------------------- checkpointing
+    def state_dict(self) -> dict:
+        sd = {"t": self.t, "w": self.w.detach().cpu(), "cfg": asdict(self.cfg),
+              "accs": list(self.history.accs)}
+        if hasattr(self, "W"):
+            sd["locals"] = self.W.detach().cpu()
+            sd["worker_lo"] = self.layout.worker_lo
+        if hasattr(self, "Dl"):
+            sd["delta"] = self.Dl.detach().cpu()
+        return sd
+
+    def load_state_dict(self, sd: dict):
+        self.t = int(sd["t"])
+        self.w.copy_(sd["w"].to(self.w.dtype))
+        if "locals" in sd and hasattr(self, "W"):
+            self.W.copy_(sd["locals"].to(self.W.dtype))
+        if "delta" in sd and hasattr(self, "Dl"):
+            self.Dl.copy_(sd["delta"].to(self.Dl.dtype))
+        self.history.accs = list(sd.get("accs", []))
+
+    def weights(self) -> torch.Tensor:
+        return self.w.view(-1)

@@ -1,0 +1,164 @@
+"""Logistic-regression ops: fused sampled gradient (K1+K7) and evaluation (K10).
+
+GPU tensors run ``csrc/kernels/lr_grad.hip``; CPU tensors run the torch
+reference below, which draws the identical Philox minibatch
+(:mod:`dalgo.utils.philox`) so CPU (gloo) and GPU runs select the same rows.
+
+Reference semantics (all in ``/root/reference``):
+  * ``logistic_f`` = 1/(exp(-x.w) + 1 [+ 1e-6])  — ssgd.py:23-24, ma.py:25-26
+  * ``gradient``   = -(y - sigma) * x            — ssgd.py:27-33
+  * minibatch      = points.sample(False, f, 42+t) — ssgd.py:97 (here: Philox
+    Bernoulli keyed by (seed, step, global row); Spark's per-partition RNG cannot
+    be matched bit-for-bit)
+  * accuracy       = sigma < 0.5 -> 0 else 1       — ssgd.py:107-110
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from dalgo.ops import _ext
+from dalgo.utils import philox
+
+_TARGET_BLOCKS = 512          # ~2 blocks of 8 waves per CU on 256 CUs
+
+
+def padded_cols(D: int, dtype: torch.dtype) -> int:
+    """Row stride (elements) the kernels need: a multiple of 16 bytes."""
+    vec = 8 if dtype == torch.bfloat16 else 4
+    return ((D + vec - 1) // vec) * vec
+
+
+def pad_features(X: torch.Tensor) -> torch.Tensor:
+    """Return X (or a copy) whose rows are 16-B aligned with a 16-B multiple stride.
+
+    Columns in the stride padding are never used: the kernels multiply them by
+    zero weights and never write their gradient, so any view works.
+    """
+    vec = 8 if X.dtype == torch.bfloat16 else 4
+    if X.stride(1) == 1 and X.stride(0) % vec == 0 and X.data_ptr() % 16 == 0:
+        return X
+    ld = padded_cols(X.shape[1], X.dtype)
+    out = torch.zeros((X.shape[0], ld), dtype=X.dtype, device=X.device)
+    out[:, : X.shape[1]] = X
+    return out[:, : X.shape[1]]
+
+
+def _grid(n_rows: int, nseg: int):
+    per_seg = max(1, _TARGET_BLOCKS // max(1, nseg))
+    rpb = max(256, int(math.ceil(n_rows / per_seg / 256.0)) * 256)
+    gx = max(1, int(math.ceil(n_rows / rpb)))
+    return gx, rpb
+
+
+@dataclass
+class _Workspace:
+    slab: torch.Tensor
+    gslab: torch.Tensor
+    cnt1: torch.Tensor
+    cnt2: torch.Tensor
+
+
+_ws_cache: dict = {}
+
+
+def _workspace(device, nseg, gx, S) -> _Workspace:
+    key = (str(device), nseg, gx, S)
+    ws = _ws_cache.get(key)
+    if ws is None:
+        ngroups = (gx + 15) // 16
+        ws = _Workspace(
+            slab=torch.empty((nseg * gx, S), dtype=torch.float32, device=device),
+            gslab=torch.empty((nseg * ngroups, S), dtype=torch.float32, device=device),
+            cnt1=torch.zeros(nseg * ngroups, dtype=torch.int32, device=device),
+            cnt2=torch.zeros(nseg, dtype=torch.int32, device=device),
+        )
+        _ws_cache[key] = ws
+    return ws
+
+
+def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor, *,
+            D: int, has_bias: bool = True, eps: float = 0.0, seed: int = 42, step: int = 0,
+            frac: float = 1.0, row_offset: int = 0, G: torch.Tensor | None = None,
+            C: torch.Tensor | None = None, max_seg_rows: int | None = None):
+    """Per-segment gradient SUM and selected-row COUNT.
+
+    X: [n, >=D] (bf16/f32), y: [n] f32, W: [n_seg, ldw] f32 models,
+    seg: int64 [n_seg+1] local row bounds (segment s uses W[s]).
+    Returns (G [n_seg, ldw], C [n_seg]); G[:, D] is the bias gradient.
+    """
+    nseg, ldw = W.shape
+    if G is None:
+        G = torch.zeros((nseg, ldw), dtype=W.dtype, device=W.device)
+    if C is None:
+        C = torch.zeros(nseg, dtype=W.dtype, device=W.device)
+    if X.is_cuda:
+        if max_seg_rows is None:
+            if nseg == 1:
+                max_seg_rows = int(X.shape[0])
+            else:
+                b = seg.tolist()
+                max_seg_rows = max(b[i + 1] - b[i] for i in range(nseg))
+        gx, rpb = _grid(max(int(max_seg_rows), 1), nseg)
+        S = ((D + 2 + 63) // 64) * 64
+        ws = _workspace(X.device, nseg, gx, S)
+        _ext.ops().lr_grad(X, y, W, seg, int(row_offset), int(D), bool(has_bias), float(eps),
+                           int(seed), int(step), float(frac), gx, rpb, ws.slab, ws.gslab,
+                           ws.cnt1, ws.cnt2, G, C)
+        return G, C
+    return _lr_grad_cpu(X, y, W, seg, D, has_bias, eps, seed, step, frac, row_offset, G, C)
+
+
+def _lr_grad_cpu(X, y, W, seg, D, has_bias, eps, seed, step, frac, row_offset, G, C):
+    segb = seg.tolist()
+    G.zero_()
+    C.zero_()
+    for s in range(W.shape[0]):
+        lo, hi = segb[s], segb[s + 1]
+        if hi <= lo:
+            continue
+        mask = philox.bernoulli_mask(seed, step, np.arange(row_offset + lo, row_offset + hi), frac)
+        idx = torch.from_numpy(np.nonzero(mask)[0] + lo)
+        if idx.numel() == 0:
+            continue
+        Xs = X[idx, :D].to(W.dtype)
+        w = W[s]
+        z = Xs @ w[:D]
+        if has_bias:
+            z = z + w[D]
+        sig = 1.0 / (torch.exp(-z) + 1.0 + eps)
+        r = sig - y[idx].to(W.dtype)
+        G[s, :D] = r @ Xs
+        if has_bias:
+            G[s, D] = r.sum()
+        C[s] = float(idx.numel())
+    return G, C
+
+
+def lr_eval(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, *, D: int,
+            has_bias: bool = True, eps: float = 0.0):
+    """Return (correct_count, mean_logloss) of model w ([ldw] or [1, ldw]) on (X, y)."""
+    W = w.reshape(1, -1)
+    n = int(X.shape[0])
+    if X.is_cuda:
+        gx, rpb = _grid(max(n, 1), 1)
+        seg = torch.tensor([0, n], dtype=torch.int64, device=X.device)
+        correct = torch.zeros(1, dtype=torch.int64, device=X.device)
+        loss = torch.zeros(1, dtype=torch.float32, device=X.device)
+        _ext.ops().lr_eval(X, y, W, seg, int(D), bool(has_bias), float(eps), gx, rpb, correct, loss)
+        return correct, loss / max(n, 1)
+    Xs = X[:, :D].to(W.dtype)
+    z = Xs @ W[0, :D]
+    if has_bias:
+        z = z + W[0, D]
+    with np.errstate(over="ignore"):
+        sig = 1.0 / (torch.exp(-z) + 1.0 + eps)
+    pred = torch.where(sig < 0.5, 0.0, 1.0).to(W.dtype)
+    correct = (pred == y.to(W.dtype)).sum().reshape(1)
+    sc = sig.clamp(1e-7, 1 - 1e-7)
+    yy = y.to(W.dtype)
+    loss = -(yy * torch.log(sc) + (1 - yy) * torch.log(1 - sc)).mean().reshape(1)
+    return correct, loss

@@ -1,0 +1,129 @@
+"""Collectives (replace the reference's Spark data-movement primitives).
+
+Reference call site -> collective here:
+  * ``sc.broadcast(w)`` every iteration (ssgd.py:95)      -> nothing (w is replicated
+    SPMD); :func:`broadcast` once at init
+  * ``treeAggregate`` of (sum g, count) (ssgd.py:99-103)  -> :func:`all_reduce_sum` of
+    one fused ``[g || count]`` buffer (one latency-bound RCCL call per step)
+  * ``reduceByKey`` + ``collect`` (k-means.py:62-67)      -> all_reduce of the fused
+    ``[k*d sums || k counts]`` table
+  * ``reduceByKey`` of PageRank contributions (pagerank.py:57) -> :func:`all_gather_into`
+    of destination-partitioned rank slices (half the bytes of an all-reduce)
+  * ``collect`` of ALS factor rows (matrix_decomposition.py:52-64) -> all_gather
+  * ``count`` / ``reduce(add)`` (pagerank.py:44, monte_carlo.py:28) -> int64 all_reduce
+
+With world size 1 every call is a no-op / identity, so single-GPU runs pay no
+communication. All calls are issued on the current stream (RCCL enqueues on
+its own stream, torch inserts the event dependencies), so they can be captured
+with the surrounding kernels.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from dalgo.parallel import runtime
+
+
+def _active() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def world_size() -> int:
+    return dist.get_world_size() if _active() else 1
+
+
+def rank() -> int:
+    return dist.get_rank() if _active() else 0
+
+
+def all_reduce_sum(t: torch.Tensor, async_op: bool = False):
+    """In-place SUM all-reduce (identity at world size 1)."""
+    if not _active():
+        return t
+    work = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=async_op)
+    return work if async_op else t
+
+
+def all_reduce_max(t: torch.Tensor):
+    if _active():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t
+
+
+def all_reduce_count(n: int | torch.Tensor, device=None) -> int:
+    """Global integer count (``rdd.count()`` / ``reduce(add)`` equivalent)."""
+    if isinstance(n, torch.Tensor):
+        t = n.to(torch.int64).reshape(1).clone()
+    else:
+        dev = device or runtime.get().device
+        t = torch.tensor([int(n)], dtype=torch.int64, device=dev)
+    all_reduce_sum(t)
+    return int(t.item())
+
+
+def broadcast(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    if _active():
+        dist.broadcast(t, src=src)
+    return t
+
+
+def all_gather_into(out: torch.Tensor, local: torch.Tensor) -> torch.Tensor:
+    """Gather equal-sized local shards into ``out`` (concatenated along dim 0)."""
+    if not _active():
+        if out.data_ptr() != local.data_ptr():
+            out.copy_(local.reshape(out.shape))
+        return out
+    dist.all_gather_into_tensor(out, local.contiguous())
+    return out
+
+
+def all_gather_varlen(local: torch.Tensor, counts: list[int]) -> torch.Tensor:
+    """Gather shards of different lengths along dim 0 (padded all_gather + trim)."""
+    if not _active():
+        return local
+    m = max(counts)
+    pad = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    out = torch.empty((m * len(counts),) + tuple(local.shape[1:]), dtype=local.dtype,
+                      device=local.device)
+    dist.all_gather_into_tensor(out, pad)
+    parts = [out[i * m: i * m + c] for i, c in enumerate(counts)]
+    return torch.cat(parts, dim=0)
+
+
+def reduce_scatter_sum(out: torch.Tensor, full: torch.Tensor) -> torch.Tensor:
+    if not _active():
+        out.copy_(full.reshape(out.shape))
+        return out
+    dist.reduce_scatter_tensor(out, full.contiguous(), op=dist.ReduceOp.SUM)
+    return out
+
+
+def gather_to_rank0(local: torch.Tensor, counts: list[int]) -> torch.Tensor | None:
+    """``collect()``: rows of every rank concatenated on rank 0 (None elsewhere)."""
+    full = all_gather_varlen(local, counts)
+    return full if rank() == 0 else None
+
+
+class BucketedAllReduce:
+    """Flatten several tensors into one contiguous bucket and all-reduce once.
+
+    xGMI rings are per-link latency/bandwidth bound; small per-tensor
+    all-reduces (the SGD family's [g||cnt], k-means' [sums||counts]) are fused
+    into one RCCL call. Tensors are views into the bucket, so kernels can write
+    their outputs straight into it (no pack/unpack copies).
+    """
+
+    def __init__(self, shapes: list[tuple[int, ...]], dtype=torch.float32, device=None):
+        device = device or runtime.get().device
+        sizes = [int(torch.Size(s).numel()) for s in shapes]
+        self.buffer = torch.zeros(sum(sizes), dtype=dtype, device=device)
+        self.views = []
+        off = 0
+        for s, n in zip(shapes, sizes):
+            self.views.append(self.buffer[off: off + n].view(s))
+            off += n
+
+    def all_reduce(self, async_op: bool = False):
+        return all_reduce_sum(self.buffer, async_op=async_op)

@@ -1,0 +1,129 @@
+"""Process-group runtime: one rank per GPU (replaces SparkSession / executors).
+
+The reference obtains its workers from an external Spark runtime
+(``SparkSession.builder.appName(..).getOrCreate()``, optimization/ssgd.py:78-81;
+``spark.stop()``, ssgd.py:117). Here every rank is an SPMD process started by
+``torchrun`` (or :func:`dalgo.parallel.launch.spawn`), bound to GPU
+``LOCAL_RANK``, talking RCCL (torch backend ``"nccl"``) over xGMI; on CPU-only
+hosts the same code runs on ``gloo``. A single process without any launcher
+environment is a valid world of size 1 (no process group needed).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class Runtime:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+    app_name: str = "dalgo"
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+    def barrier(self):
+        if self.distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def synchronize(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def log(self, *args, **kw):
+        """print on rank 0 only (the reference prints from the driver)."""
+        if self.is_main:
+            print(*args, **kw, flush=True)
+
+
+_RT: Runtime | None = None
+
+
+def _env_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def init(backend: str | None = None, *, device: str | None = None, app_name: str = "dalgo",
+         timeout_s: float = 600.0) -> Runtime:
+    """Initialise (idempotent) and return the process runtime.
+
+    backend: "nccl" (RCCL, GPU), "gloo" (CPU) or None = auto (nccl when a GPU is
+    requested/available, gloo otherwise). device: "cuda" | "cpu" | None = auto.
+    """
+    global _RT
+    if _RT is not None:
+        return _RT
+    rank = _env_int("RANK", 0)
+    world = _env_int("WORLD_SIZE", 1)
+    local_rank = _env_int("LOCAL_RANK", rank)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+    if device is None:
+        if backend == "gloo":
+            device = "cpu"
+        else:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+    if device == "cuda":
+        ndev = torch.cuda.device_count()
+        if ndev == 0:
+            raise RuntimeError("device='cuda' requested but no GPU is visible")
+        dev = torch.device("cuda", local_rank % ndev)
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    if backend is None:
+        backend = "nccl" if dev.type == "cuda" else "gloo"
+
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kw = dict(backend=backend, rank=rank, world_size=world,
+                  timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = dev
+        dist.init_process_group(**kw)
+    _RT = Runtime(rank=rank, world_size=world, local_rank=local_rank, device=dev,
+                  backend=backend if world > 1 else "none", app_name=app_name)
+    return _RT
+
+
+def get() -> Runtime:
+    return _RT if _RT is not None else init()
+
+
+def shutdown():
+    """Tear down the process group (``spark.stop()`` equivalent)."""
+    global _RT
+    if dist.is_available() and dist.is_initialized():
+        try:
+            dist.barrier()
+        except Exception:
+            pass
+        dist.destroy_process_group()
+    _RT = None
+
+
+def seed_everything(seed: int):
+    import random
+
+    import numpy as np
+    random.seed(seed)
+    np.random.seed(seed % (2 ** 32))
+    torch.manual_seed(seed)

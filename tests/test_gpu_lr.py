@@ -1,0 +1,99 @@
+"""Numerics of the LR kernels (K1/K7/K10) and K8 against the torch fp32/fp64 reference."""
+import numpy as np
+import pytest
+import torch
+
+from dalgo.ops import lr as L
+from dalgo.ops import update as U
+from dalgo.ops.lr import pad_features
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, D, dtype, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = (torch.rand((n, D), generator=g) * 2 - 1).to(dtype)
+    y = (torch.rand(n, generator=g) < 0.5).float()
+    return X, y
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("D", [30, 256, 1000, 1024])
+@pytest.mark.parametrize("frac", [0.1, 1.0])
+def test_lr_grad_matches_reference(cuda, dtype, D, frac):
+    n = 5000
+    X, y = _data(n, D, dtype)
+    Xc = pad_features(X)
+    nseg = 3
+    seg = torch.tensor([0, 1500, 3001, n], dtype=torch.int64)
+    W = torch.randn(nseg, D + 1, generator=torch.Generator().manual_seed(1)) * 0.1
+    kw = dict(D=D, has_bias=True, eps=1e-6, seed=42, step=7, frac=frac, row_offset=12345)
+    G_ref, C_ref = L.lr_grad(Xc.float(), y, W.double(), seg, **kw)
+    Gd, Cd = L.lr_grad(pad_features(X.to(cuda)), y.to(cuda), W.to(cuda), seg.to(cuda), **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(Cd.cpu().double(), C_ref), (Cd, C_ref)
+    err = (Gd.cpu().double() - G_ref).abs().max().item()
+    scale = G_ref.abs().max().item() + 1e-6
+    assert err / scale < 2e-5, (err, scale)
+
+
+def test_lr_grad_single_segment_deterministic(cuda):
+    X, y = _data(200_000, 1024, torch.bfloat16, seed=3)
+    Xd, yd = X.to(cuda), y.to(cuda)
+    W = torch.randn(1, 1025, generator=torch.Generator().manual_seed(2)).to(cuda) * 0.05
+    seg = torch.tensor([0, X.shape[0]], dtype=torch.int64, device=cuda)
+    outs = [L.lr_grad(Xd, yd, W, seg, D=1024, frac=0.1, step=3) for _ in range(3)]
+    for G, C in outs[1:]:
+        assert torch.equal(G, outs[0][0]) and torch.equal(C, outs[0][1])
+    G_ref, C_ref = L.lr_grad(X, y, W.cpu().double(), seg.cpu(), D=1024, frac=0.1, step=3)
+    assert float(outs[0][1].item()) == float(C_ref.item())
+    rel = (outs[0][0].cpu().double() - G_ref).abs().max() / G_ref.abs().max()
+    assert rel < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_lr_eval(cuda, dtype):
+    X, y = _data(7777, 100, dtype, seed=5)
+    w = torch.randn(101, generator=torch.Generator().manual_seed(9))
+    c_ref, l_ref = L.lr_eval(pad_features(X).float(), y, w.double(), D=100)
+    c, l = L.lr_eval(pad_features(X.to(cuda)), y.to(cuda), w.to(cuda), D=100)
+    assert abs(int(c.item()) - int(c_ref.item())) <= 2   # sigma==0.5 ties may flip in f32
+    assert abs(float(l.item()) - float(l_ref.item())) < 1e-3
+
+
+@pytest.mark.parametrize("mode", range(7))
+def test_sync_update_modes(cuda, mode):
+    g = torch.Generator().manual_seed(mode)
+    nrow = 1 if mode in (U.AVERAGE, U.BMUF, U.ELASTIC_CENTER) else 3
+    n = 1025
+    W = torch.randn(nrow, n, generator=g)
+    G = torch.randn(nrow, n, generator=g)
+    C = torch.tensor([5.0, 0.0, 17.0][:nrow])
+    center = torch.randn(n, generator=g)
+    S = torch.randn(n, generator=g)
+    Dl = torch.randn(n, generator=g)
+    kw = dict(reg="elastic_net", eta=0.1, lam=0.01, alpha=0.01, reg_alpha=0.3, mu=0.9,
+              zeta=0.1, beta=0.04, inv_p=0.25)
+    if mode == U.GD_SUM:
+        kw.pop("lam")
+    Wc, Dc = W.clone().double(), Dl.clone().double()
+    U.sync_update(Wc, mode, G=G.double(), C=C.double(), center=center.double(), S=S.double(),
+                  Dl=Dc, **kw)
+    Wd, Dd = W.to(cuda), Dl.to(cuda)
+    U.sync_update(Wd, mode, G=G.to(cuda), C=C.to(cuda), center=center.to(cuda), S=S.to(cuda),
+                  Dl=Dd, **kw)
+    assert torch.allclose(Wd.cpu().double(), Wc, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(Dd.cpu().double(), Dc, rtol=1e-5, atol=1e-5)
+
+
+def test_rows_sum_broadcast(cuda):
+    W = torch.randn(4, 1025)
+    out = torch.zeros(1025)
+    U.rows_sum(W, out)
+    od = torch.zeros(1025, device=cuda)
+    U.rows_sum(W.to(cuda), od)
+    assert torch.allclose(od.cpu(), out, atol=1e-5)
+    src = torch.randn(1025)
+    Wd = W.to(cuda)
+    U.rows_broadcast(Wd, src.to(cuda))
+    assert torch.equal(Wd.cpu(), src.expand(4, -1))

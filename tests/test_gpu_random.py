@@ -1,0 +1,32 @@
+"""Philox fill + Monte-Carlo pi kernels vs the NumPy Philox mirror."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from dalgo.ops import random as R
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dist", [R.UNIFORM, R.NORMAL])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_philox_fill_matches_numpy(cuda, dist, dtype):
+    a, b = (-1.0, 1.0) if dist == R.UNIFORM else (0.5, 2.0)
+    out_c = torch.empty((37, 40), dtype=dtype)
+    R.philox_fill_(out_c, D=33, row_offset=1000, seed=77, stream=5, dist=dist, a=a, b=b)
+    out_d = torch.empty((37, 40), dtype=dtype, device=cuda)
+    R.philox_fill_(out_d, D=33, row_offset=1000, seed=77, stream=5, dist=dist, a=a, b=b)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert torch.allclose(out_d.cpu().float(), out_c.float(), atol=tol * 4, rtol=tol)
+    assert (out_d[:, 33:] == 0).all()
+
+
+def test_mc_pi_exact_count(cuda):
+    n = 1_000_002
+    c_ref = R.mc_pi_count(n, seed=3, stream=1, offset=10)
+    c = R.mc_pi_count(n, seed=3, stream=1, offset=10, device=cuda)
+    assert abs(int(c.item()) - int(c_ref.item())) <= 2   # float rounding at the circle edge
+    pi = 4.0 * int(c.item()) / n
+    assert abs(pi - math.pi) < 0.01
