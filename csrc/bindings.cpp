@@ -7,8 +7,8 @@
 // failures surface as c10::Error with the op name.
 #include <torch/library.h>
 #include <ATen/ATen.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -20,7 +20,10 @@ namespace {
 
 using at::Tensor;
 
-inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+// ROCm torch exposes HIP devices as DeviceType::CUDA ("masquerading"), so the
+// guard/stream helpers are the masquerading variants.
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+using DeviceGuard = c10::hip::HIPGuardMasqueradingAsCUDA;
 
 #define DALGO_CHECK_HIP(expr, name)                                                   \
   do {                                                                                \
@@ -87,7 +90,7 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
   TORCH_CHECK(cnt2.scalar_type() == at::kInt && cnt2.numel() >= nseg, "cnt2");
   TORCH_CHECK(G.dim() == 2 && G.size(0) == nseg && G.size(1) == W.size(1), "G shape");
   TORCH_CHECK(C.numel() >= nseg, "C shape");
-  c10::hip::HIPGuard guard(X.device());
+  DeviceGuard guard(X.device());
   const bool full = frac >= 1.0;
   DALGO_CHECK_HIP(
       dalgo_lr_grad(X.data_ptr(), y.data_ptr<float>(), W.data_ptr<float>(), seg.data_ptr<int64_t>(),
@@ -110,7 +113,7 @@ void lr_eval(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
   TORCH_CHECK(correct.scalar_type() == at::kLong && correct.numel() >= nseg, "correct");
   check_f32(loss, "loss");
   TORCH_CHECK(loss.numel() >= nseg, "loss");
-  c10::hip::HIPGuard guard(X.device());
+  DeviceGuard guard(X.device());
   DALGO_CHECK_HIP(
       dalgo_lr_eval(X.data_ptr(), y.data_ptr<float>(), W.data_ptr<float>(), seg.data_ptr<int64_t>(),
                     X.stride(0), (int)D, (int)W.size(1), has_bias ? 1 : 0, (float)eps,
@@ -157,7 +160,7 @@ void sync_update(Tensor W, const std::optional<Tensor>& G, const std::optional<T
     case 5: TORCH_CHECK(s && dl && nrow == 1, "BMUF needs S, Dl and one row"); break;
     default: TORCH_CHECK(false, "unknown update mode ", mode);
   }
-  c10::hip::HIPGuard guard(W.device());
+  DeviceGuard guard(W.device());
   DALGO_CHECK_HIP(dalgo_sync_update(W.data_ptr<float>(), g, c, ce, s, dl, cacc, (int)n, (int)ld,
                                     (int)nrow, (int)mode, (int)reg, (float)eta, (float)lam,
                                     (float)alpha, (float)reg_alpha, (float)mu, (float)zeta,
@@ -169,7 +172,7 @@ void rows_sum(const Tensor& W, int64_t n, Tensor out) {
   check_f32(W, "W");
   check_f32(out, "out");
   TORCH_CHECK(W.dim() == 2 && n <= W.size(1) && out.numel() >= n, "rows_sum shapes");
-  c10::hip::HIPGuard guard(W.device());
+  DeviceGuard guard(W.device());
   DALGO_CHECK_HIP(dalgo_rows_sum(W.data_ptr<float>(), (int)W.size(0), (int)W.size(1), (int)n,
                                  out.data_ptr<float>(), cur_stream()),
                   "rows_sum");
@@ -179,7 +182,7 @@ void rows_broadcast(Tensor W, int64_t n, const Tensor& src) {
   check_f32(W, "W");
   check_f32(src, "src");
   TORCH_CHECK(W.dim() == 2 && n <= W.size(1) && src.numel() >= n, "rows_broadcast shapes");
-  c10::hip::HIPGuard guard(W.device());
+  DeviceGuard guard(W.device());
   DALGO_CHECK_HIP(dalgo_rows_broadcast(W.data_ptr<float>(), (int)W.size(0), (int)W.size(1),
                                        (int)n, src.data_ptr<float>(), cur_stream()),
                   "rows_broadcast");
@@ -195,7 +198,7 @@ void philox_fill(Tensor out, int64_t D, int64_t row_offset, int64_t seed, int64_
   TORCH_CHECK(out.stride(0) == out.size(1), "philox_fill: out must be contiguous");
   TORCH_CHECK(D <= out.size(1), "philox_fill: D > columns");
   TORCH_CHECK(dist == 0 || dist == 1, "philox_fill: dist");
-  c10::hip::HIPGuard guard(out.device());
+  DeviceGuard guard(out.device());
   DALGO_CHECK_HIP(dalgo_philox_fill(out.data_ptr(), out.scalar_type() == at::kBFloat16 ? 1 : 0,
                                     out.size(0), D, out.size(1), row_offset, (uint64_t)seed,
                                     (uint64_t)stream, (int)dist, (float)a, (float)b, cur_stream()),
@@ -206,7 +209,7 @@ void mc_pi(int64_t seed, int64_t stream, int64_t offset, int64_t n, Tensor count
   check_dev(count, "count");
   TORCH_CHECK(count.scalar_type() == at::kLong && count.numel() >= 1, "mc_pi: count int64[1]");
   TORCH_CHECK(offset % 2 == 0 && n >= 0, "mc_pi: offset must be even");
-  c10::hip::HIPGuard guard(count.device());
+  DeviceGuard guard(count.device());
   DALGO_CHECK_HIP(dalgo_mc_pi((uint64_t)seed, (uint64_t)stream, (uint64_t)offset, (uint64_t)n,
                               reinterpret_cast<unsigned long long*>(count.data_ptr<int64_t>()),
                               cur_stream()),
