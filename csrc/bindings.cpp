@@ -75,7 +75,7 @@ void check_lr_inputs(const Tensor& X, const Tensor& y, const Tensor& W, const Te
 void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& seg,
              int64_t row_offset, int64_t D, bool has_bias, double eps, int64_t seed, int64_t step,
              double frac, int64_t gx, int64_t rows_per_block, Tensor slab, Tensor gslab,
-             Tensor cnt1, Tensor cnt2, Tensor G, Tensor C) {
+             Tensor cnt1, Tensor cnt2, Tensor G, Tensor C, int64_t variant) {
   check_lr_inputs(X, y, W, seg, D, has_bias);
   const int64_t nseg = W.size(0);
   TORCH_CHECK(gx >= 1 && gx <= 65535, "gx");
@@ -100,13 +100,13 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
                     (int)rows_per_block, slab.data_ptr<float>(), gslab.data_ptr<float>(),
                     reinterpret_cast<unsigned*>(cnt1.data_ptr<int>()),
                     reinterpret_cast<unsigned*>(cnt2.data_ptr<int>()), G.data_ptr<float>(),
-                    C.data_ptr<float>(), (int)S, cur_stream()),
+                    C.data_ptr<float>(), (int)S, (int)variant, cur_stream()),
       "lr_grad");
 }
 
 void lr_eval(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& seg, int64_t D,
              bool has_bias, double eps, int64_t gx, int64_t rows_per_block, Tensor correct,
-             Tensor loss) {
+             Tensor loss, int64_t variant) {
   check_lr_inputs(X, y, W, seg, D, has_bias);
   const int64_t nseg = W.size(0);
   TORCH_CHECK(rows_per_block > 0 && rows_per_block % 256 == 0, "rows_per_block % 256");
@@ -120,7 +120,7 @@ void lr_eval(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
                     X.scalar_type() == at::kBFloat16 ? 1 : 0, (int)gx, (int)nseg,
                     (int)rows_per_block,
                     reinterpret_cast<unsigned long long*>(correct.data_ptr<int64_t>()),
-                    loss.data_ptr<float>(), cur_stream()),
+                    loss.data_ptr<float>(), (int)variant, cur_stream()),
       "lr_eval");
 }
 
@@ -216,14 +216,27 @@ void mc_pi(int64_t seed, int64_t stream, int64_t offset, int64_t n, Tensor count
                   "mc_pi");
 }
 
+void hbm_read(const Tensor& src, Tensor out, int64_t unroll) {
+  check_dev(src, "src");
+  check_dev(out, "out");
+  TORCH_CHECK(src.is_contiguous() && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0, "src");
+  TORCH_CHECK(out.scalar_type() == at::kInt && out.numel() >= 1, "out int32[grid]");
+  DeviceGuard guard(src.device());
+  DALGO_CHECK_HIP(dalgo_hbm_read(src.data_ptr(), src.numel() * src.element_size(),
+                                 reinterpret_cast<uint32_t*>(out.data_ptr<int>()), (int)out.numel(),
+                                 (int)unroll, cur_stream()),
+                  "hbm_read");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dalgo, m) {
   m.def("lr_grad(Tensor X, Tensor y, Tensor W, Tensor seg, int row_offset, int D, bool has_bias, "
         "float eps, int seed, int step, float frac, int gx, int rows_per_block, Tensor(a!) slab, "
-        "Tensor(b!) gslab, Tensor(c!) cnt1, Tensor(d!) cnt2, Tensor(e!) G, Tensor(f!) C) -> ()");
+        "Tensor(b!) gslab, Tensor(c!) cnt1, Tensor(d!) cnt2, Tensor(e!) G, Tensor(f!) C, "
+        "int variant=3) -> ()");
   m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
-        "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss) -> ()");
+        "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=3) -> ()");
   m.def("sync_update(Tensor(a!) W, Tensor? G, Tensor? C, Tensor? center, Tensor? S, "
         "Tensor(b!)? Dl, Tensor(c!)? count_acc, int n, int mode, int reg, float eta, float lam, float alpha, "
         "float reg_alpha, float mu, float zeta, float beta, float inv_p) -> ()");
@@ -231,6 +244,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("rows_broadcast(Tensor(a!) W, int n, Tensor src) -> ()");
   m.def("philox_fill(Tensor(a!) out, int D, int row_offset, int seed, int stream, int dist, "
         "float a, float b) -> ()");
+  m.def("hbm_read(Tensor src, Tensor(a!) out, int unroll=8) -> ()");
   m.def("mc_pi(int seed, int stream, int offset, int n, Tensor(a!) count) -> ()");
 }
 
@@ -241,5 +255,6 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("rows_sum", &rows_sum);
   m.impl("rows_broadcast", &rows_broadcast);
   m.impl("philox_fill", &philox_fill);
-  m.impl("mc_pi", &mc_pi);   // dispatches on its output counter
+  m.impl("mc_pi", &mc_pi);
+  m.impl("hbm_read", &hbm_read);   // dispatches on its output counter
 }

@@ -80,14 +80,33 @@ __device__ __forceinline__ void acquire_fence() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// A batch of (up to) U selected rows held in VGPRs (U = 4 or 8). With PIPE the
+// row loads of batch i+1 are issued before batch i is computed (two named
+// register sets, manual unroll); with U = 8 a single set keeps 16 KB per wave
+// in flight. Bytes in flight per wave are bounded by VGPRs (4 B per VGPR-lane),
+// which is what the variants trade against occupancy.
+template <int NC, int U>
+struct Batch {
+  uint4 x[U][NC];
+  float yq[U / 4];  // label of row 4j + (lane >> 4)
+  float v[U];       // 1 = valid row, 0 = padding
+  int n;            // valid rows (0 = no more work)
+};
+
+constexpr int kRing = 512;   // per-wave ring of selected local row indices
+
 // EVAL=false: gradient; EVAL=true: accuracy + log-loss over every row.
-template <typename T, int NC, bool EVAL, int NW>
+// PIPE: software-pipelined (two register sets) vs. single-buffered sweep.
+template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U>
 __global__ void __launch_bounds__(NW * 64)
 lr_rows_kernel(LrParams p) {
   constexpr int VEC = VecTraits<T>::VEC;
   constexpr int COLS = NC * 64 * VEC;  // columns covered per lane-set
-  __shared__ int s_list[NW][256];      // per-wave list of selected rows (local idx)
-  __shared__ float s_red[NW][COLS + 2 + 2];
+  constexpr int RED_FLOATS = NW * (COLS + 4);
+  constexpr int RING_INTS = NW * kRing;
+  // one LDS arena: per-wave selection rings during the sweep, then the
+  // cross-wave reduction buffer
+  __shared__ __attribute__((aligned(16))) float s_arena[(RED_FLOATS > RING_INTS) ? RED_FLOATS : RING_INTS];
   __shared__ int s_flag;
 
   const int lane = threadIdx.x & 63;
@@ -98,8 +117,6 @@ lr_rows_kernel(LrParams p) {
   const int64_t seg_lo = p.seg[seg], seg_hi = p.seg[seg + 1];
   const int64_t lo = seg_lo + (int64_t)bx * p.rows_per_block;
   const int64_t hi = max(lo, min(seg_hi, lo + (int64_t)p.rows_per_block));
-  const int nchunks = (int)(p.ld / VEC);
-
   // model fragment in registers
   const float* w = p.W + (int64_t)seg * p.ldw;
   float wr[NC][VEC];
@@ -126,112 +143,159 @@ lr_rows_kernel(LrParams p) {
   // group walk in global-row space, 256 rows per group, 4 rows per lane
   const int64_t glo = p.row_offset + lo, ghi = p.row_offset + hi;
   const int64_t gstart = glo & ~(int64_t)3;
-  int* list = s_list[wid];
+  int* ring = reinterpret_cast<int*>(s_arena) + wid * kRing;
+  const int q = lane >> 4;
+  uint32_t head = 0, tail = 0;
+  int64_t gnext = gstart + (int64_t)wid * 256;
 
-  for (int64_t g0 = gstart + (int64_t)wid * 256; g0 < ghi; g0 += (int64_t)NW * 256) {
-    // ---- K7: Bernoulli selection, compacted into the wave's LDS list
-    const int64_t r0 = g0 + 4 * lane;
-    u32x4 h{0u, 0u, 0u, 0u};
-    if (!p.full && !EVAL && r0 < ghi) h = philox_block(p.seed, p.step, (uint64_t)r0 >> 2);
-    const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
-    int base = 0;
+  // ---- K7: Bernoulli selection of the next 256-row groups, compacted into the ring
+  auto refill = [&]() {
+    while ((tail - head) < (uint32_t)(2 * U) && gnext < ghi) {
+      const int64_t r0 = gnext + 4 * lane;
+      u32x4 h{0u, 0u, 0u, 0u};
+      if (!p.full && !EVAL && r0 < ghi) h = philox_block(p.seed, p.step, (uint64_t)r0 >> 2);
+      const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t gr = r0 + j;
-      const bool sel = (gr >= glo) && (gr < ghi) && (EVAL || p.full || hv[j] < p.thr);
-      const uint64_t m = __ballot(sel);
-      const int pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      if (sel) list[pos] = (int)(gr - p.row_offset - lo);
-      base += __popcll(m);
+      for (int j = 0; j < 4; ++j) {
+        const int64_t gr = r0 + j;
+        const bool sel = (gr >= glo) && (gr < ghi) && (EVAL || p.full || hv[j] < p.thr);
+        const uint64_t m = __ballot(sel);
+        const uint32_t pos = tail + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (sel) ring[pos & (kRing - 1)] = (int)(gr - p.row_offset - lo);
+        tail += (uint32_t)__popcll(m);
+      }
+      gnext += (int64_t)NW * 256;
     }
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    const int n = base;
+  };
 
-    // ---- row batches of 4: loads first, then dot, reduce, sigmoid, accumulate
-    for (int i = 0; i < n; i += 4) {
-      const int k1 = min(i + 1, n - 1), k2 = min(i + 2, n - 1), k3 = min(i + 3, n - 1);
-      const int64_t ra = lo + __builtin_amdgcn_readfirstlane(list[i]);
-      const int64_t rb = lo + __builtin_amdgcn_readfirstlane(list[k1]);
-      const int64_t rc = lo + __builtin_amdgcn_readfirstlane(list[k2]);
-      const int64_t rd = lo + __builtin_amdgcn_readfirstlane(list[k3]);
-      const float va = 1.f, vb = (i + 1 < n) ? 1.f : 0.f, vc = (i + 2 < n) ? 1.f : 0.f,
-                  vd = (i + 3 < n) ? 1.f : 0.f;
-      uint4 xa[NC], xb[NC], xc[NC], xd[NC];
-      const T* pa = X + ra * p.ld;
-      const T* pb = X + rb * p.ld;
-      const T* pc = X + rc * p.ld;
-      const T* pd = X + rd * p.ld;
+  auto take_and_load = [&](Batch<NC, U>& b) {
+    const uint32_t avail = tail - head;
+    b.n = (int)min(avail, (uint32_t)U);
+    if (b.n == 0) return;
+    const uint32_t last = b.n - 1;
+    int64_t r[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      r[k] = lo + __builtin_amdgcn_readfirstlane(ring[(head + min((uint32_t)k, last)) & (kRing - 1)]);
+      b.v[k] = (k < b.n) ? 1.f : 0.f;
+    }
+    head += b.n;
+    // one buffer descriptor per row (wave-uniform SGPRs, base = row start,
+    // num_records = row bytes): lanes past the row read 0 via the range check
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(X + r[k] * p.ld), (short)0, (int)(p.ld * (int64_t)sizeof(T)), 0x00020000);
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        const int ch = c * 64 + lane;
-        if (ch < nchunks) {
-          xa[c] = *reinterpret_cast<const uint4*>(pa + (int64_t)ch * VEC);
-          xb[c] = *reinterpret_cast<const uint4*>(pb + (int64_t)ch * VEC);
-          xc[c] = *reinterpret_cast<const uint4*>(pc + (int64_t)ch * VEC);
-          xd[c] = *reinterpret_cast<const uint4*>(pd + (int64_t)ch * VEC);
-        } else {
-          xa[c] = xb[c] = xc[c] = xd[c] = make_uint4(0u, 0u, 0u, 0u);
-        }
+        auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (c * 64 + lane) * 16, 0, 0);
+        b.x[k][c] = make_uint4(v[0], v[1], v[2], v[3]);
       }
-      // labels: lane l serves row (l >> 4)
-      const int q = lane >> 4;
-      const int64_t rq = q == 0 ? ra : (q == 1 ? rb : (q == 2 ? rc : rd));
-      const float yq = p.y[rq];
+    }
+#pragma unroll
+    for (int j = 0; j < U / 4; ++j) {
+      const int64_t rq = q == 0 ? r[4 * j] : (q == 1 ? r[4 * j + 1] : (q == 2 ? r[4 * j + 2] : r[4 * j + 3]));
+      b.yq[j] = p.y[rq];
+    }
+  };
 
-      float da = 0.f, db = 0.f, dc = 0.f, dd = 0.f;
+  auto compute = [&](Batch<NC, U>& b) {
+    float d[U];
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        float fa[VEC], fb[VEC], fc[VEC], fd[VEC];
-        unpack<T>(xa[c], fa); unpack<T>(xb[c], fb); unpack<T>(xc[c], fc); unpack<T>(xd[c], fd);
+    for (int k = 0; k < U; ++k) d[k] = 0.f;
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          da = fmaf(fa[e], wr[c][e], da);
-          db = fmaf(fb[e], wr[c][e], db);
-          dc = fmaf(fc[e], wr[c][e], dc);
-          dd = fmaf(fd[e], wr[c][e], dd);
-        }
+    for (int c = 0; c < NC; ++c) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        float f[VEC];
+        unpack<T>(b.x[k][c], f);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) d[k] = fmaf(f[e], wr[c][e], d[k]);
       }
-      const float z = wave_sum4(da, db, dc, dd) + wb;
-      const float sig = 1.f / (__expf(-z) + 1.f + p.eps);
-      const float vq = q == 0 ? va : (q == 1 ? vb : (q == 2 ? vc : vd));
+    }
+    float z[U / 4];
+#pragma unroll
+    for (int j = 0; j < U / 4; ++j)
+      z[j] = wave_sum4(d[4 * j], d[4 * j + 1], d[4 * j + 2], d[4 * j + 3]) + wb;
+    // Opaque re-definition of the raw rows: forces the bf16->f32 unpack to be
+    // recomputed in the rank-1 update instead of keeping U*NC*VEC unpacked
+    // floats live across the reduction (saves ~64 VGPRs -> 2x occupancy).
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        asm volatile("" : "+v"(b.x[k][c].x), "+v"(b.x[k][c].y), "+v"(b.x[k][c].z), "+v"(b.x[k][c].w));
+    float rs[U];
+#pragma unroll
+    for (int j = 0; j < U / 4; ++j) {
+      const float sig = 1.f / (__expf(-z[j]) + 1.f + p.eps);
+      const float vq = q == 0 ? b.v[4 * j] : (q == 1 ? b.v[4 * j + 1] : (q == 2 ? b.v[4 * j + 2] : b.v[4 * j + 3]));
+      const float yq = b.yq[j];
       if constexpr (EVAL) {
         // pred = sigma < 0.5 ? 0 : 1  (ssgd.py:108-109)
         const float pred = sig < 0.5f ? 0.f : 1.f;
-        const float ok = (pred == yq) ? 1.f : 0.f;
+        const float ok = (pred == yq) ? vq : 0.f;
         const float sc = fminf(fmaxf(sig, 1e-7f), 1.f - 1e-7f);
-        const float l = -(yq * __logf(sc) + (1.f - yq) * __logf(1.f - sc));
-        // one lane per row-block contributes
-        const float oka = readlane_f(ok * vq, 0) + readlane_f(ok * vq, 16) +
-                          readlane_f(ok * vq, 32) + readlane_f(ok * vq, 48);
-        lossf += readlane_f(l * vq, 0) + readlane_f(l * vq, 16) + readlane_f(l * vq, 32) +
-                 readlane_f(l * vq, 48);
-        correct += (unsigned)oka;
+        const float l = -(yq * __logf(sc) + (1.f - yq) * __logf(1.f - sc)) * vq;
+        correct += (unsigned)(readlane_f(ok, 0) + readlane_f(ok, 16) + readlane_f(ok, 32) +
+                              readlane_f(ok, 48));
+        lossf += readlane_f(l, 0) + readlane_f(l, 16) + readlane_f(l, 32) + readlane_f(l, 48);
       } else {
         const float r = (sig - yq) * vq;
-        const float ra_ = readlane_f(r, 0), rb_ = readlane_f(r, 16), rc_ = readlane_f(r, 32),
-                    rd_ = readlane_f(r, 48);
-        gb += (ra_ + rb_) + (rc_ + rd_);
-        cntf += va + vb + vc + vd;
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          float fa[VEC], fb[VEC], fc[VEC], fd[VEC];
-          unpack<T>(xa[c], fa); unpack<T>(xb[c], fb); unpack<T>(xc[c], fc); unpack<T>(xd[c], fd);
+        for (int k = 0; k < 4; ++k) rs[4 * j + k] = readlane_f(r, 16 * k);
+      }
+    }
+    if constexpr (!EVAL) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) gb += rs[k];
+      cntf += (float)b.n;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+#pragma unroll
+        for (int k0 = 0; k0 < U; k0 += 4) {
+          float f[4][VEC];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) unpack<T>(b.x[k0 + k][c], f[k]);
 #pragma unroll
           for (int e = 0; e < VEC; ++e) {
             float acc = g[c][e];
-            acc = fmaf(ra_, fa[e], acc);
-            acc = fmaf(rb_, fb[e], acc);
-            acc = fmaf(rc_, fc[e], acc);
-            acc = fmaf(rd_, fd[e], acc);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc = fmaf(rs[k0 + k], f[k][e], acc);
             g[c][e] = acc;
           }
         }
       }
     }
-    __builtin_amdgcn_wave_barrier();
+  };
+
+  // ---- software-pipelined sweep: load(i+1) || compute(i)
+  Batch<NC, U> A;
+  if constexpr (PIPE) {
+    Batch<NC, U> B;
+    refill();
+    take_and_load(A);
+    while (true) {
+      if (A.n == 0) break;
+      refill();
+      take_and_load(B);
+      compute(A);
+      if (B.n == 0) break;
+      refill();
+      take_and_load(A);
+      compute(B);
+    }
+  } else {
+    while (true) {
+      refill();
+      take_and_load(A);
+      if (A.n == 0) break;
+      compute(A);
+    }
   }
+  __syncthreads();   // rings are dead: the arena becomes the reduction buffer
 
   if constexpr (EVAL) {
     __shared__ float s_ev[NW][2];
@@ -246,7 +310,8 @@ lr_rows_kernel(LrParams p) {
     return;
   } else {
     // ---- block reduction across waves (fixed order)
-    float* red = s_red[wid];
+    auto red_row = [&](int k) { return s_arena + k * (COLS + 4); };
+    float* red = red_row(wid);
 #pragma unroll
     for (int c = 0; c < NC; ++c)
 #pragma unroll
@@ -259,12 +324,12 @@ lr_rows_kernel(LrParams p) {
     for (int col = threadIdx.x; col < D; col += NW * 64) {
       float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < NW; ++k) s += s_red[k][col];
+      for (int k = 0; k < NW; ++k) s += red_row(k)[col];
       my[col] = s;
     }
     if (threadIdx.x == 0) {
       float sb = 0.f, sc = 0.f;
-      for (int k = 0; k < NW; ++k) { sb += s_red[k][COLS]; sc += s_red[k][COLS + 1]; }
+      for (int k = 0; k < NW; ++k) { sb += red_row(k)[COLS]; sc += red_row(k)[COLS + 1]; }
       my[D] = sb;       // bias grad slot
       my[D + 1] = sc;   // count slot
     }
@@ -327,32 +392,51 @@ lr_rows_kernel(LrParams p) {
 
 using namespace dalgo;
 
-template <typename T, int NC, bool EVAL>
+template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U>
 static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st) {
-  constexpr int NW = 8;
   dim3 grid(gx, nseg), block(NW * 64);
-  hipLaunchKernelGGL((lr_rows_kernel<T, NC, EVAL, NW>), grid, block, 0, st, p);
+  hipLaunchKernelGGL((lr_rows_kernel<T, NC, EVAL, NW, PIPE, U>), grid, block, 0, st, p);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
 
+// variant bits: bit0 = pipelined sweep (two register sets), bit1 = 8 waves per
+// block (else 4), bit2 = 8-row batches (else 4; not combined with bit0)
+template <typename T, int NC, bool EVAL>
+static hipError_t launch_variant(const LrParams& p, int gx, int nseg, int variant, hipStream_t st) {
+  if constexpr (NC >= 4) {   // register budget: one 4-row set at 4 chunks/lane
+    return (variant & 2) ? launch_lr<T, NC, EVAL, 8, false, 4>(p, gx, nseg, st)
+                         : launch_lr<T, NC, EVAL, 4, false, 4>(p, gx, nseg, st);
+  } else {
+    switch (variant & 7) {
+      case 0: return launch_lr<T, NC, EVAL, 4, false, 4>(p, gx, nseg, st);
+      case 1: return launch_lr<T, NC, EVAL, 4, true, 4>(p, gx, nseg, st);
+      case 2: return launch_lr<T, NC, EVAL, 8, false, 4>(p, gx, nseg, st);
+      case 3: return launch_lr<T, NC, EVAL, 8, true, 4>(p, gx, nseg, st);
+      case 4: case 5: return launch_lr<T, NC, EVAL, 4, false, 8>(p, gx, nseg, st);
+      default: return launch_lr<T, NC, EVAL, 8, false, 8>(p, gx, nseg, st);
+    }
+  }
+}
+
 template <bool EVAL>
-static hipError_t dispatch_lr(const LrParams& p, int is_bf16, int gx, int nseg, hipStream_t st) {
+static hipError_t dispatch_lr(const LrParams& p, int is_bf16, int gx, int nseg, int variant,
+                              hipStream_t st) {
   const int vec = is_bf16 ? 8 : 4;
   const int64_t nchunks = p.ld / vec;
   const int nc = (int)cdiv(nchunks, 64);
   if (is_bf16) {
     switch (nc) {
-      case 1: return launch_lr<uint16_t, 1, EVAL>(p, gx, nseg, st);
-      case 2: return launch_lr<uint16_t, 2, EVAL>(p, gx, nseg, st);
-      case 3: case 4: return launch_lr<uint16_t, 4, EVAL>(p, gx, nseg, st);
+      case 1: return launch_variant<uint16_t, 1, EVAL>(p, gx, nseg, variant, st);
+      case 2: return launch_variant<uint16_t, 2, EVAL>(p, gx, nseg, variant, st);
+      case 3: case 4: return launch_variant<uint16_t, 4, EVAL>(p, gx, nseg, variant, st);
       default: return hipErrorInvalidValue;
     }
   } else {
     switch (nc) {
-      case 1: return launch_lr<float, 1, EVAL>(p, gx, nseg, st);
-      case 2: return launch_lr<float, 2, EVAL>(p, gx, nseg, st);
-      case 3: case 4: return launch_lr<float, 4, EVAL>(p, gx, nseg, st);
+      case 1: return launch_variant<float, 1, EVAL>(p, gx, nseg, variant, st);
+      case 2: return launch_variant<float, 2, EVAL>(p, gx, nseg, variant, st);
+      case 3: case 4: return launch_variant<float, 4, EVAL>(p, gx, nseg, variant, st);
       default: return hipErrorInvalidValue;
     }
   }
@@ -367,25 +451,25 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          int64_t ld, int64_t row_offset, int D, int ldw, int has_bias, float eps,
                          uint64_t seed, uint64_t step, uint32_t thr, int full, int is_bf16,
                          int gx, int nseg, int rows_per_block, float* slab, float* gslab,
-                         unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S,
+                         unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int variant,
                          hipStream_t st) {
   LrParams p{};
   p.X = X; p.y = y; p.W = W; p.seg = seg; p.ld = ld; p.row_offset = row_offset; p.D = D;
   p.ldw = ldw; p.has_bias = has_bias; p.eps = eps; p.seed = seed; p.step = step; p.thr = thr;
   p.full = full; p.rows_per_block = rows_per_block; p.slab = slab; p.gslab = gslab;
   p.cnt1 = cnt1; p.cnt2 = cnt2; p.G = G; p.C = C; p.S = S;
-  return dispatch_lr<false>(p, is_bf16, gx, nseg, st);
+  return dispatch_lr<false>(p, is_bf16, gx, nseg, variant, st);
 }
 
 hipError_t dalgo_lr_eval(const void* X, const float* y, const float* W, const int64_t* seg,
                          int64_t ld, int D, int ldw, int has_bias, float eps, int is_bf16, int gx,
                          int nseg, int rows_per_block, unsigned long long* correct, float* loss,
-                         hipStream_t st) {
+                         int variant, hipStream_t st) {
   LrParams p{};
   p.X = X; p.y = y; p.W = W; p.seg = seg; p.ld = ld; p.row_offset = 0; p.D = D; p.ldw = ldw;
   p.has_bias = has_bias; p.eps = eps; p.full = 1; p.rows_per_block = rows_per_block;
   p.correct = correct; p.loss = loss;
-  return dispatch_lr<true>(p, is_bf16, gx, nseg, st);
+  return dispatch_lr<true>(p, is_bf16, gx, nseg, variant, st);
 }
 
 }  // extern "C"

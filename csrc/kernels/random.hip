@@ -70,6 +70,27 @@ mc_pi_kernel(uint64_t seed, uint64_t stream, uint64_t offset, uint64_t n,
   }
 }
 
+// HBM read-roofline probe (diagnostics): every 16 B of [p, p+n16*16) read once with
+// dwordx4 loads, UNROLL loads in flight per lane, xor-folded into one word per
+// block so the loads cannot be dead-code eliminated.
+template <int UNROLL>
+__global__ void __launch_bounds__(256)
+hbm_read_kernel(const uint4* __restrict__ p, int64_t n16, uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (UNROLL - 1) * stride < n16; i += UNROLL * stride) {
+    uint4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) v[u] = p[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  for (; i < n16; i += stride) { uint4 v = p[i]; acc ^= v.x ^ v.y ^ v.z ^ v.w; }
+  acc = wave_sum_u32(acc);
+  if (threadIdx.x == 0) out[blockIdx.x] = acc;
+}
+
 }  // namespace dalgo
 
 using namespace dalgo;
@@ -99,6 +120,17 @@ hipError_t dalgo_mc_pi(uint64_t seed, uint64_t stream, uint64_t offset, uint64_t
   const int grid = (int)std::min<uint64_t>((nblk + 255) / 256, 256 * 8);
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL(mc_pi_kernel, dim3(grid), dim3(256), 0, st, seed, stream, offset, n, count);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t dalgo_hbm_read(const void* p, int64_t nbytes, uint32_t* out, int grid, int unroll,
+                          hipStream_t st) {
+  const int64_t n16 = nbytes / 16;
+  if (unroll >= 8)
+    hipLaunchKernelGGL(hbm_read_kernel<8>, dim3(grid), dim3(256), 0, st, (const uint4*)p, n16, out);
+  else
+    hipLaunchKernelGGL(hbm_read_kernel<4>, dim3(grid), dim3(256), 0, st, (const uint4*)p, n16, out);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

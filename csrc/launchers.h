@@ -13,12 +13,12 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          int64_t ld, int64_t row_offset, int D, int ldw, int has_bias, float eps,
                          uint64_t seed, uint64_t step, uint32_t thr, int full, int is_bf16,
                          int gx, int nseg, int rows_per_block, float* slab, float* gslab,
-                         unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S,
+                         unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int variant,
                          hipStream_t st);
 hipError_t dalgo_lr_eval(const void* X, const float* y, const float* W, const int64_t* seg,
                          int64_t ld, int D, int ldw, int has_bias, float eps, int is_bf16, int gx,
                          int nseg, int rows_per_block, unsigned long long* correct, float* loss,
-                         hipStream_t st);
+                         int variant, hipStream_t st);
 
 // ---- K8 sync/update rules (sync_update.hip)
 hipError_t dalgo_sync_update(float* W, const float* G, const float* C, const float* center,
@@ -33,6 +33,8 @@ hipError_t dalgo_rows_broadcast(float* W, int nrow, int ld, int n, const float* 
 hipError_t dalgo_philox_fill(void* out, int is_bf16, int64_t nrows, int64_t D, int64_t ld,
                              int64_t row_offset, uint64_t seed, uint64_t stream, int dist, float a,
                              float b, hipStream_t st);
+hipError_t dalgo_hbm_read(const void* p, int64_t nbytes, uint32_t* out, int grid, int unroll,
+                          hipStream_t st);
 hipError_t dalgo_mc_pi(uint64_t seed, uint64_t stream, uint64_t offset, uint64_t n,
                        unsigned long long* count, hipStream_t st);
 

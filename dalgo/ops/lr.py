@@ -23,7 +23,13 @@ import torch
 from dalgo.ops import _ext
 from dalgo.utils import philox
 
-_TARGET_BLOCKS = 512          # ~2 blocks of 8 waves per CU on 256 CUs
+import os
+
+# Launch shape of the row-streaming kernels (tuned on MI355X, see profiles/):
+#   LR_VARIANT bit0 = software-pipelined sweep, bit1 = 8-wave blocks (else 4)
+#   TARGET_BLOCKS   = workgroups per launch (split over segments)
+LR_VARIANT = int(os.environ.get("DALGO_LR_VARIANT", "2"))
+_TARGET_BLOCKS = int(os.environ.get("DALGO_LR_BLOCKS", "256"))
 
 
 def padded_cols(D: int, dtype: torch.dtype) -> int:
@@ -47,8 +53,8 @@ def pad_features(X: torch.Tensor) -> torch.Tensor:
     return out[:, : X.shape[1]]
 
 
-def _grid(n_rows: int, nseg: int):
-    per_seg = max(1, _TARGET_BLOCKS // max(1, nseg))
+def _grid(n_rows: int, nseg: int, target_blocks: int | None = None):
+    per_seg = max(1, (target_blocks or _TARGET_BLOCKS) // max(1, nseg))
     rpb = max(256, int(math.ceil(n_rows / per_seg / 256.0)) * 256)
     gx = max(1, int(math.ceil(n_rows / rpb)))
     return gx, rpb
@@ -83,7 +89,8 @@ def _workspace(device, nseg, gx, S) -> _Workspace:
 def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor, *,
             D: int, has_bias: bool = True, eps: float = 0.0, seed: int = 42, step: int = 0,
             frac: float = 1.0, row_offset: int = 0, G: torch.Tensor | None = None,
-            C: torch.Tensor | None = None, max_seg_rows: int | None = None):
+            C: torch.Tensor | None = None, max_seg_rows: int | None = None,
+            variant: int | None = None, target_blocks: int | None = None):
     """Per-segment gradient SUM and selected-row COUNT.
 
     X: [n, >=D] (bf16/f32), y: [n] f32, W: [n_seg, ldw] f32 models,
@@ -102,12 +109,12 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
             else:
                 b = seg.tolist()
                 max_seg_rows = max(b[i + 1] - b[i] for i in range(nseg))
-        gx, rpb = _grid(max(int(max_seg_rows), 1), nseg)
+        gx, rpb = _grid(max(int(max_seg_rows), 1), nseg, target_blocks)
         S = ((D + 2 + 63) // 64) * 64
         ws = _workspace(X.device, nseg, gx, S)
         _ext.ops().lr_grad(X, y, W, seg, int(row_offset), int(D), bool(has_bias), float(eps),
                            int(seed), int(step), float(frac), gx, rpb, ws.slab, ws.gslab,
-                           ws.cnt1, ws.cnt2, G, C)
+                           ws.cnt1, ws.cnt2, G, C, LR_VARIANT if variant is None else int(variant))
         return G, C
     return _lr_grad_cpu(X, y, W, seg, D, has_bias, eps, seed, step, frac, row_offset, G, C)
 
@@ -148,7 +155,8 @@ def lr_eval(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, *, D: int,
         seg = torch.tensor([0, n], dtype=torch.int64, device=X.device)
         correct = torch.zeros(1, dtype=torch.int64, device=X.device)
         loss = torch.zeros(1, dtype=torch.float32, device=X.device)
-        _ext.ops().lr_eval(X, y, W, seg, int(D), bool(has_bias), float(eps), gx, rpb, correct, loss)
+        _ext.ops().lr_eval(X, y, W, seg, int(D), bool(has_bias), float(eps), gx, rpb, correct, loss,
+                           LR_VARIANT)
         return correct, loss / max(n, 1)
     Xs = X[:, :D].to(W.dtype)
     z = Xs @ W[0, :D]
