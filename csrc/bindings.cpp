@@ -228,6 +228,199 @@ void hbm_read(const Tensor& src, Tensor out, int64_t unroll) {
                   "hbm_read");
 }
 
+// ---------------------------------------------------------------------------
+// k-means
+inline int kmeans_dp(int64_t d) {
+  for (int dp : {16, 32, 64, 128})
+    if (d <= dp) return dp;
+  return -1;
+}
+
+void check_points(const Tensor& X, int DP) {
+  check_dev(X, "X");
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "X must be 2-D with contiguous rows");
+  TORCH_CHECK(X.scalar_type() == at::kBFloat16 || X.scalar_type() == at::kFloat, "X bf16/f32");
+  TORCH_CHECK(X.stride(0) >= DP, "X row stride must cover the padded dim ", DP);
+  TORCH_CHECK((X.stride(0) * X.element_size()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0,
+              "X rows must be 16-B aligned");
+}
+
+void kmeans_assign(const Tensor& X, const Tensor& Cq, const Tensor& hn, Tensor assign,
+                   const std::optional<Tensor>& mind, const std::optional<Tensor>& sse) {
+  TORCH_CHECK(Cq.dim() == 2, "Cq [kpad, DP]");
+  const int DP = (int)Cq.size(1);
+  TORCH_CHECK(kmeans_dp(DP) == DP, "Cq columns must be 16/32/64/128");
+  check_points(X, DP);
+  check_dev(Cq, "Cq");
+  TORCH_CHECK(Cq.scalar_type() == X.scalar_type() && Cq.is_contiguous(), "Cq dtype/layout");
+  const int64_t kpad = Cq.size(0);
+  TORCH_CHECK(kpad % 32 == 0 && kpad > 0, "kpad % 32");
+  check_f32(hn, "hn");
+  TORCH_CHECK(hn.numel() >= kpad, "hn");
+  check_dev(assign, "assign");
+  TORCH_CHECK(assign.scalar_type() == at::kInt && assign.numel() >= X.size(0), "assign int32[n]");
+  float* md = nullptr;
+  if (mind.has_value()) {
+    check_f32(*mind, "mind");
+    TORCH_CHECK(mind->numel() >= X.size(0), "mind");
+    md = mind->data_ptr<float>();
+  }
+  double* ss = nullptr;
+  if (sse.has_value()) {
+    check_dev(*sse, "sse");
+    TORCH_CHECK(sse->scalar_type() == at::kDouble && sse->numel() >= 1, "sse f64[1]");
+    ss = sse->data_ptr<double>();
+  }
+  DeviceGuard guard(X.device());
+  DALGO_CHECK_HIP(dalgo_kmeans_assign(X.data_ptr(), X.scalar_type() == at::kBFloat16, X.size(0),
+                                      X.stride(0), DP, Cq.data_ptr(), hn.data_ptr<float>(),
+                                      (int)kpad, assign.data_ptr<int>(), md, ss, cur_stream()),
+                  "kmeans_assign");
+}
+
+void kmeans_accumulate(const Tensor& X, const Tensor& assign, int64_t k, int64_t DP, Tensor S,
+                       Tensor cnt) {
+  TORCH_CHECK(kmeans_dp(DP) == DP, "DP must be 16/32/64/128");
+  check_points(X, (int)DP);
+  check_dev(assign, "assign");
+  TORCH_CHECK(assign.scalar_type() == at::kInt && assign.numel() >= X.size(0), "assign");
+  check_f32(S, "S");
+  TORCH_CHECK(S.numel() >= k * DP, "S [k, DP]");
+  check_dev(cnt, "cnt");
+  TORCH_CHECK(cnt.scalar_type() == at::kLong && cnt.numel() >= k, "cnt int64[k]");
+  DeviceGuard guard(X.device());
+  DALGO_CHECK_HIP(dalgo_kmeans_accumulate(X.data_ptr(), X.scalar_type() == at::kBFloat16,
+                                          X.size(0), X.stride(0), (int)DP,
+                                          assign.data_ptr<int>(), (int)k, S.data_ptr<float>(),
+                                          reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>()),
+                                          cur_stream()),
+                  "kmeans_accumulate");
+}
+
+void kmeans_update(Tensor C, const Tensor& S, const Tensor& cnt, Tensor Cq, Tensor hn,
+                   const std::optional<Tensor>& shift2) {
+  check_f32(C, "C");
+  TORCH_CHECK(C.dim() == 2, "C [k, d]");
+  const int64_t k = C.size(0), d = C.size(1);
+  check_dev(Cq, "Cq");
+  TORCH_CHECK(Cq.dim() == 2 && Cq.is_contiguous() && Cq.size(0) >= k && Cq.size(0) % 32 == 0 &&
+                  Cq.size(1) >= d, "Cq [kpad, DP]");
+  TORCH_CHECK(Cq.scalar_type() == at::kBFloat16 || Cq.scalar_type() == at::kFloat, "Cq dtype");
+  const int64_t DP = Cq.size(1), kpad = Cq.size(0);
+  check_f32(S, "S");
+  TORCH_CHECK(S.numel() >= k * DP, "S");
+  TORCH_CHECK(cnt.scalar_type() == at::kLong && cnt.numel() >= k, "cnt");
+  check_f32(hn, "hn");
+  TORCH_CHECK(hn.numel() >= kpad, "hn");
+  float* sh = nullptr;
+  if (shift2.has_value()) { check_f32(*shift2, "shift2"); sh = shift2->data_ptr<float>(); }
+  DeviceGuard guard(C.device());
+  DALGO_CHECK_HIP(dalgo_kmeans_update(C.data_ptr<float>(), S.data_ptr<float>(),
+                                      reinterpret_cast<const unsigned long long*>(cnt.data_ptr<int64_t>()),
+                                      (int)k, (int)d, (int)DP, Cq.data_ptr(),
+                                      Cq.scalar_type() == at::kBFloat16, hn.data_ptr<float>(),
+                                      (int)kpad, sh, cur_stream()),
+                  "kmeans_update");
+}
+
+// ---------------------------------------------------------------------------
+// PageRank
+inline void check_i32(const Tensor& t, const char* what) {
+  check_dev(t, what);
+  TORCH_CHECK(t.scalar_type() == at::kInt && t.is_contiguous(), "dalgo: ", what, " must be int32");
+}
+
+void rmat_edges(int64_t seed, int64_t scale, int64_t e_off, double a, double b, double c,
+                bool scramble, Tensor src, Tensor dst) {
+  check_i32(src, "src");
+  check_i32(dst, "dst");
+  TORCH_CHECK(src.numel() == dst.numel(), "src/dst size");
+  TORCH_CHECK(scale >= 1 && scale <= 31, "scale in [1, 31]");
+  DeviceGuard guard(src.device());
+  DALGO_CHECK_HIP(dalgo_rmat((uint64_t)seed, (int)scale, e_off, src.numel(), (float)a, (float)b,
+                             (float)c, scramble ? 1 : 0, src.data_ptr<int32_t>(),
+                             dst.data_ptr<int32_t>(), cur_stream()),
+                  "rmat_edges");
+}
+
+void pr_spmv(const Tensor& src, const Tensor& dstl, const Tensor& c, Tensor acc, Tensor pres) {
+  check_i32(src, "src");
+  check_i32(dstl, "dstl");
+  TORCH_CHECK(src.numel() == dstl.numel() && src.numel() % 4 == 0, "edge arrays: equal, % 4");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(dstl.data_ptr()) % 16 == 0, "edge arrays 16-B aligned");
+  check_f32(c, "c");
+  check_f32(acc, "acc");
+  check_i32(pres, "pres");
+  TORCH_CHECK(pres.numel() >= acc.numel(), "pres size");
+  DeviceGuard guard(src.device());
+  DALGO_CHECK_HIP(dalgo_pr_spmv(src.data_ptr<int32_t>(), dstl.data_ptr<int32_t>(), src.numel(),
+                                c.data_ptr<float>(), acc.data_ptr<float>(), pres.data_ptr<int32_t>(),
+                                cur_stream()),
+                  "pr_spmv");
+}
+
+void pr_update(const Tensor& acc, const Tensor& pres, const Tensor& outdeg, double q, double invN,
+               int64_t mode, const std::optional<Tensor>& dangling_in, Tensor r, Tensor c,
+               const std::optional<Tensor>& dangling_out) {
+  check_f32(acc, "acc");
+  check_i32(pres, "pres");
+  check_i32(outdeg, "outdeg");
+  check_f32(r, "r");
+  check_f32(c, "c");
+  const int64_t n = acc.numel();
+  TORCH_CHECK(pres.numel() >= n && outdeg.numel() >= n && r.numel() >= n && c.numel() >= n,
+              "pr_update sizes");
+  const float* di = nullptr;
+  float* dout = nullptr;
+  if (dangling_in.has_value()) { check_f32(*dangling_in, "dangling_in"); di = dangling_in->data_ptr<float>(); }
+  if (dangling_out.has_value()) { check_f32(*dangling_out, "dangling_out"); dout = dangling_out->data_ptr<float>(); }
+  DeviceGuard guard(acc.device());
+  DALGO_CHECK_HIP(dalgo_pr_update(acc.data_ptr<float>(), pres.data_ptr<int32_t>(),
+                                  outdeg.data_ptr<int32_t>(), n, (float)q, (float)invN, (int)mode,
+                                  di, r.data_ptr<float>(), c.data_ptr<float>(), dout, cur_stream()),
+                  "pr_update");
+}
+
+// ---------------------------------------------------------------------------
+// transitive closure
+void tc_step(const Tensor& A, const Tensor& Told, Tensor Tnew, Tensor count) {
+  for (const Tensor* t : {&A, &Told, static_cast<const Tensor*>(&Tnew)}) {
+    check_dev(*t, "tc operand");
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->stride(1) == 1,
+                "tc operands: 2-D bf16 with contiguous rows");
+  }
+  const int64_t npad = A.size(0);
+  TORCH_CHECK(A.size(1) >= npad && Told.size(1) >= npad && Tnew.sizes() == Told.sizes(),
+              "tc shapes");
+  TORCH_CHECK(npad % 64 == 0 && Told.size(0) % 64 == 0, "tc: dims must be multiples of 64");
+  TORCH_CHECK(Told.stride(0) == Tnew.stride(0), "tc: T strides");
+  TORCH_CHECK(count.scalar_type() == at::kLong && count.numel() >= 1, "count int64[1]");
+  DeviceGuard guard(A.device());
+  DALGO_CHECK_HIP(dalgo_tc_step(A.data_ptr(), A.stride(0), Told.data_ptr(), Tnew.data_ptr(),
+                                Told.stride(0), (int)npad, (int)Told.size(0),
+                                reinterpret_cast<unsigned long long*>(count.data_ptr<int64_t>()),
+                                cur_stream()),
+                  "tc_step");
+}
+
+// ---------------------------------------------------------------------------
+// ALS
+void spd_inverse(const Tensor& G, double ridge, Tensor out, const std::optional<Tensor>& status) {
+  check_f32(G, "G");
+  check_f32(out, "out");
+  TORCH_CHECK(G.dim() == 2 && G.size(0) == G.size(1) && out.sizes() == G.sizes(), "square k x k");
+  TORCH_CHECK(G.size(0) >= 1 && G.size(0) <= 128, "spd_inverse: k <= 128");
+  int* st = nullptr;
+  if (status.has_value()) { check_i32(*status, "status"); st = status->data_ptr<int32_t>(); }
+  DeviceGuard guard(G.device());
+  DALGO_CHECK_HIP(dalgo_spd_inverse(G.data_ptr<float>(), (int)G.size(0), (int)G.stride(0),
+                                    (float)ridge, out.data_ptr<float>(), (int)out.stride(0), st,
+                                    cur_stream()),
+                  "spd_inverse");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dalgo, m) {
@@ -244,6 +437,18 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("rows_broadcast(Tensor(a!) W, int n, Tensor src) -> ()");
   m.def("philox_fill(Tensor(a!) out, int D, int row_offset, int seed, int stream, int dist, "
         "float a, float b) -> ()");
+  m.def("kmeans_assign(Tensor X, Tensor Cq, Tensor hn, Tensor(a!) assign, Tensor(b!)? mind, "
+        "Tensor(c!)? sse) -> ()");
+  m.def("kmeans_accumulate(Tensor X, Tensor assign, int k, int DP, Tensor(a!) S, Tensor(b!) cnt) -> ()");
+  m.def("kmeans_update(Tensor(a!) C, Tensor S, Tensor cnt, Tensor(b!) Cq, Tensor(c!) hn, "
+        "Tensor(d!)? shift2) -> ()");
+  m.def("rmat_edges(int seed, int scale, int e_off, float a, float b, float c, bool scramble, "
+        "Tensor(a!) src, Tensor(b!) dst) -> ()");
+  m.def("pr_spmv(Tensor src, Tensor dstl, Tensor c, Tensor(a!) acc, Tensor(b!) pres) -> ()");
+  m.def("pr_update(Tensor acc, Tensor pres, Tensor outdeg, float q, float invN, int mode, "
+        "Tensor? dangling_in, Tensor(a!) r, Tensor(b!) c, Tensor(c!)? dangling_out) -> ()");
+  m.def("tc_step(Tensor A, Tensor Told, Tensor(a!) Tnew, Tensor(b!) count) -> ()");
+  m.def("spd_inverse(Tensor G, float ridge, Tensor(a!) out, Tensor(b!)? status) -> ()");
   m.def("hbm_read(Tensor src, Tensor(a!) out, int unroll=8) -> ()");
   m.def("mc_pi(int seed, int stream, int offset, int n, Tensor(a!) count) -> ()");
 }
@@ -256,5 +461,13 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("rows_broadcast", &rows_broadcast);
   m.impl("philox_fill", &philox_fill);
   m.impl("mc_pi", &mc_pi);
-  m.impl("hbm_read", &hbm_read);   // dispatches on its output counter
+  m.impl("hbm_read", &hbm_read);
+  m.impl("spd_inverse", &spd_inverse);
+  m.impl("tc_step", &tc_step);
+  m.impl("rmat_edges", &rmat_edges);
+  m.impl("pr_spmv", &pr_spmv);
+  m.impl("pr_update", &pr_update);
+  m.impl("kmeans_assign", &kmeans_assign);
+  m.impl("kmeans_accumulate", &kmeans_accumulate);
+  m.impl("kmeans_update", &kmeans_update);   // dispatches on its output counter
 }

@@ -1,0 +1,440 @@
+// K2 + K3 + centroid update: distributed Lloyd k-means on MFMA.
+//
+// Reference: machine_learning/k-means.py — closest_center (:20-28) is an O(k*d)
+// Python loop per point, reduceByKey (:62-63) sums (point, 1) per cluster and
+// the driver replaces non-empty centres (:66-71).
+//
+// K2 kmeans_assign  — fused distance GEMM + argmin, never materialising N x k:
+//   score(x, c) = x.c - 0.5*|c|^2  (argmax score == argmin |x-c|^2).
+//   MFMA 32x32x16 bf16 (or 32x32x2 f32): A = 32 centres (rows of D), B = 32 points
+//   (columns of D), so each lane owns ONE point and 16 of the 32 centres of the
+//   tile in its accumulator registers -> the argmin is a per-lane register scan
+//   (no cross-lane work until one final permlane32 swap). The accumulator is
+//   initialised with -0.5|c|^2 (row constants as the initial accumulator) so the
+//   epilogue is one compare + two selects per element. Centres stream through a
+//   double-buffered, XOR-swizzled LDS chunk (32 centres) shared by the block's
+//   NW*PT*32 points; point fragments stay in VGPRs for the whole sweep.
+//   Ties resolve to the lowest centre id (the reference's strict '<', :25).
+// K3 kmeans_accumulate — per-cluster sums and counts without global float
+//   atomics per row: block (row-chunk r, cluster-range q) gathers only the rows
+//   of chunk r whose cluster lies in range q and accumulates them in an LDS
+//   table (ds_add_f32), then adds the table to the global [k x d] sums once.
+//   Every X row is read exactly once overall.
+// kmeans_update — c = S/n for non-empty clusters, keep the stale centre
+//   otherwise (k-means.py:70-71); writes the f32 master, the padded MFMA copy,
+//   0.5|c~|^2 of the ROUNDED copy (consistent scores) and the squared shift.
+#include "dalgo/common.h"
+#include <algorithm>
+
+namespace dalgo {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <typename T> struct KTraits;
+// bf16: one 16-wide k-step per MFMA, 8 elements (16 B) per lane per k-step
+template <> struct KTraits<uint16_t> { static constexpr int ELEMS_PER_LOAD = 8; static constexpr int KSTEPS_PER_LOAD = 1; };
+// f32: 2-wide k-steps; a 16-B load (4 floats) feeds 4 k-steps with the permuted
+// k order  k(step 4q+u, half h) = 8q + 4h + u  used for BOTH operands
+template <> struct KTraits<float>    { static constexpr int ELEMS_PER_LOAD = 4; static constexpr int KSTEPS_PER_LOAD = 4; };
+
+template <typename T, int DP>
+struct KGeom {
+  static constexpr int ROWB = DP * (int)sizeof(T);       // bytes per centre row
+  static constexpr int NJ = ROWB / 16;                    // 16-B pieces per row
+  static constexpr int SWZ = (NJ >= 16 ? 16 : NJ) - 1;    // XOR swizzle mask
+  static constexpr int CHUNKB = 32 * ROWB;                // one 32-centre chunk
+  static constexpr int NLOAD = DP / (2 * KTraits<T>::ELEMS_PER_LOAD);  // 16-B loads per lane per point
+};
+
+__device__ __forceinline__ f32x16 mfma_step(const uint4& a, const uint4& b, f32x16 c, uint16_t) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma_step(const uint4& a, const uint4& b, f32x16 c, float) {
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.x), __uint_as_float(b.x), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.y), __uint_as_float(b.y), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.z), __uint_as_float(b.z), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.w), __uint_as_float(b.w), c, 0, 0, 0);
+  return c;
+}
+
+__device__ __forceinline__ float sq_sum(const uint4& v, uint16_t) {
+  float s = 0.f, f;
+  f = bf16lo(v.x); s = fmaf(f, f, s); f = bf16hi(v.x); s = fmaf(f, f, s);
+  f = bf16lo(v.y); s = fmaf(f, f, s); f = bf16hi(v.y); s = fmaf(f, f, s);
+  f = bf16lo(v.z); s = fmaf(f, f, s); f = bf16hi(v.z); s = fmaf(f, f, s);
+  f = bf16lo(v.w); s = fmaf(f, f, s); f = bf16hi(v.w); s = fmaf(f, f, s);
+  return s;
+}
+__device__ __forceinline__ float sq_sum(const uint4& v, float) {
+  float a = __uint_as_float(v.x), b = __uint_as_float(v.y), c = __uint_as_float(v.z),
+        d = __uint_as_float(v.w);
+  return a * a + b * b + c * c + d * d;
+}
+
+// X: [n, ldx] (columns [d, DP) must be zero), Cq: [kpad, DP] (rows >= k zero),
+// hn: [kpad] = 0.5|c|^2 (1e30 for padding centres).
+template <typename T, int DP, int PT, int NW>
+__global__ void __launch_bounds__(NW * 64)
+kmeans_assign_kernel(const T* __restrict__ X, int64_t n, int64_t ldx, const T* __restrict__ Cq,
+                     const float* __restrict__ hn, int kpad, int* __restrict__ assign,
+                     float* __restrict__ mind, double* __restrict__ sse) {
+  using G = KGeom<T, DP>;
+  constexpr int NT = NW * 64;
+  constexpr int NPIECE = G::CHUNKB / 16;
+  constexpr int PER_T = (NPIECE + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) unsigned char s_c[2][G::CHUNKB];
+  __shared__ __attribute__((aligned(16))) float s_hn[2][32];
+  __shared__ double s_sse[NW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, cl = lane & 31;
+  const int64_t pbase = ((int64_t)blockIdx.x * NW + wid) * (PT * 32);
+
+  // ---- point fragments (B operand) resident in VGPRs for the whole sweep
+  uint4 bf[PT][G::NLOAD];
+  float xn[PT];
+#pragma unroll
+  for (int t = 0; t < PT; ++t) {
+    const int64_t p = pbase + t * 32 + cl;
+    xn[t] = 0.f;
+#pragma unroll
+    for (int s = 0; s < G::NLOAD; ++s) {
+      if (p < n) {
+        bf[t][s] = *reinterpret_cast<const uint4*>(X + p * ldx + (2 * s + h) * KTraits<T>::ELEMS_PER_LOAD);
+      } else {
+        bf[t][s] = make_uint4(0u, 0u, 0u, 0u);
+      }
+      xn[t] += sq_sum(bf[t][s], T{});
+    }
+  }
+
+  float best[PT];
+  int bidx[PT];
+#pragma unroll
+  for (int t = 0; t < PT; ++t) { best[t] = -3.0e38f; bidx[t] = 0; }
+
+  const int nchunk = kpad / 32;
+  const unsigned char* Cb = reinterpret_cast<const unsigned char*>(Cq);
+  uint4 stg[PER_T];
+  float stg_h = 0.f;
+  auto stage_load = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int piece = tid + i * NT;
+      if (piece < NPIECE)
+        stg[i] = *reinterpret_cast<const uint4*>(Cb + (int64_t)ch * G::CHUNKB + piece * 16);
+    }
+    if (tid < 32) stg_h = hn[ch * 32 + tid];
+  };
+  auto stage_store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int piece = tid + i * NT;
+      if (piece < NPIECE) {
+        const int cc = piece / G::NJ, j = piece % G::NJ;
+        *reinterpret_cast<uint4*>(&s_c[buf][cc * G::ROWB + ((j ^ (cc & G::SWZ)) << 4)]) = stg[i];
+      }
+    }
+    if (tid < 32) s_hn[buf][tid] = stg_h;
+  };
+
+  stage_load(0);
+  stage_store(0);
+  __syncthreads();
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const int buf = ch & 1;
+    if (ch + 1 < nchunk) stage_load(ch + 1);   // in flight under the MFMAs
+    // accumulator init = -0.5|c|^2 of the centre each register holds
+    f32x16 acc[PT];
+    {
+      float4 h4[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) h4[g] = *reinterpret_cast<const float4*>(&s_hn[buf][8 * g + 4 * h]);
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          acc[t][4 * g + 0] = -h4[g].x; acc[t][4 * g + 1] = -h4[g].y;
+          acc[t][4 * g + 2] = -h4[g].z; acc[t][4 * g + 3] = -h4[g].w;
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < G::NLOAD; ++s) {
+      const int j = 2 * s + h;
+      const uint4 a = *reinterpret_cast<const uint4*>(&s_c[buf][cl * G::ROWB + ((j ^ (cl & G::SWZ)) << 4)]);
+#pragma unroll
+      for (int t = 0; t < PT; ++t) acc[t] = mfma_step(a, bf[t][s], acc[t], T{});
+    }
+    // running argmax over this lane's 16 centres, ascending centre order
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c = ch * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float v = acc[t][r];
+        const bool take = v > best[t];
+        best[t] = take ? v : best[t];
+        bidx[t] = take ? c : bidx[t];
+      }
+    }
+    if (ch + 1 < nchunk) {
+      stage_store(buf ^ 1);
+    }
+    __syncthreads();
+  }
+
+  // ---- combine the two lane halves (same point, disjoint centre subsets)
+  double my_sse = 0.0;
+#pragma unroll
+  for (int t = 0; t < PT; ++t) {
+    auto rb = __builtin_amdgcn_permlane32_swap(__float_as_uint(best[t]), __float_as_uint(best[t]), false, false);
+    auto ri = __builtin_amdgcn_permlane32_swap((uint32_t)bidx[t], (uint32_t)bidx[t], false, false);
+    auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(xn[t]), __float_as_uint(xn[t]), false, false);
+    const float pb = __uint_as_float(h ? rb[0] : rb[1]);
+    const int pi = (int)(h ? ri[0] : ri[1]);
+    const float px = __uint_as_float(h ? rx[0] : rx[1]);
+    float b = best[t];
+    int bi = bidx[t];
+    if (pb > b || (pb == b && pi < bi)) { b = pb; bi = pi; }
+    const float x2 = xn[t] + px;
+    const int64_t p = pbase + t * 32 + cl;
+    if (h == 0 && p < n) {
+      const float dist = fmaxf(x2 - 2.f * b, 0.f);
+      assign[p] = bi;
+      if (mind) mind[p] = dist;
+      my_sse += (double)dist;
+    }
+  }
+  if (sse) {
+    // wave sum in f64 via two f32 halves is overkill; a plain LDS pass is enough
+    __shared__ double s_part[NW * 64];
+    s_part[tid] = my_sse;
+    __syncthreads();
+    if (lane == 0) {
+      double s = 0.0;
+      for (int i = 0; i < 64; ++i) s += s_part[wid * 64 + i];
+      s_sse[wid] = s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double s = 0.0;
+      for (int w = 0; w < NW; ++w) s += s_sse[w];
+      atomicAdd(sse, s);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K3: range-partitioned LDS accumulation. grid = (row chunks, cluster ranges).
+template <typename T, int DP, int CR, int NW>
+__global__ void __launch_bounds__(NW * 64)
+kmeans_accumulate_kernel(const T* __restrict__ X, int64_t n, int64_t ldx, const int* __restrict__ assign,
+                         int k, int64_t rows_per_chunk, float* __restrict__ S,
+                         unsigned long long* __restrict__ cnt) {
+  // lane l owns EPL contiguous columns [l*EPL, l*EPL+EPL) of a row (DP >= 64),
+  // or column l (DP < 64, lanes >= DP idle)
+  constexpr int EPL = DP >= 64 ? DP / 64 : 1;
+  __shared__ float s_tab[CR * DP];
+  __shared__ unsigned s_cnt[CR];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int c0 = blockIdx.y * CR;
+  for (int i = tid; i < CR * DP; i += NW * 64) s_tab[i] = 0.f;
+  for (int i = tid; i < CR; i += NW * 64) s_cnt[i] = 0u;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
+  const int64_t r1 = min(n, r0 + rows_per_chunk);
+  const bool lane_on = (DP >= 64) || (lane < DP);
+  for (int64_t base = r0 + (int64_t)wid * 64; base < r1; base += (int64_t)NW * 64) {
+    const int64_t r = base + lane;
+    const int a = (r < r1) ? assign[r] : -1;
+    const bool mine = (a >= c0) && (a < c0 + CR);
+    uint64_t m = __ballot(mine);
+    while (m) {
+      // up to 4 rows per round so their loads overlap
+      int sel[4], cnum[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (m) {
+          const int b = __builtin_ctzll(m);
+          m &= m - 1;
+          sel[u] = b;
+          cnum[u] = __builtin_amdgcn_readlane(a, b) - c0;
+        } else {
+          sel[u] = sel[0];
+          cnum[u] = -1;
+        }
+      }
+      float v[4][EPL];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const T* row = X + (base + sel[u]) * ldx + lane * EPL;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          float x = 0.f;
+          if (lane_on) {
+            if constexpr (sizeof(T) == 2) x = bf16_to_f32(reinterpret_cast<const uint16_t*>(row)[e]);
+            else x = reinterpret_cast<const float*>(row)[e];
+          }
+          v[u][e] = x;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (cnum[u] >= 0) {
+          if (lane_on) {
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) atomicAdd(&s_tab[cnum[u] * DP + lane * EPL + e], v[u][e]);
+          }
+          if (lane == 0) atomicAdd(&s_cnt[cnum[u]], 1u);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < CR * DP; i += NW * 64) {
+    const int c = c0 + i / DP;
+    const float val = s_tab[i];
+    if (c < k && val != 0.f) atomicAdd(&S[(int64_t)c * DP + (i % DP)], val);
+  }
+  for (int i = tid; i < CR; i += NW * 64) {
+    if (c0 + i < k && s_cnt[i] != 0u) atomicAdd(&cnt[c0 + i], (unsigned long long)s_cnt[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256)
+kmeans_update_kernel(float* __restrict__ C, const float* __restrict__ S,
+                     const unsigned long long* __restrict__ cnt,
+                     int k, int d, int DP, T* __restrict__ Cq, float* __restrict__ hn, int kpad,
+                     float* __restrict__ shift2) {
+  // one wave per centre
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (c >= kpad) return;
+  float nrm = 0.f, sh = 0.f;
+  const float nc = (c < k) ? (float)cnt[c] : 0.f;
+  for (int j = lane; j < DP; j += 64) {
+    float v = 0.f;
+    if (c < k && j < d) {
+      const float old = C[(int64_t)c * d + j];
+      v = nc > 0.f ? S[(int64_t)c * DP + j] / nc : old;
+      sh += (v - old) * (v - old);
+      C[(int64_t)c * d + j] = v;
+    }
+    float vr;
+    if constexpr (sizeof(T) == 2) {
+      const uint16_t b = f32_to_bf16(v);
+      Cq[(int64_t)c * DP + j] = b;
+      vr = bf16_to_f32(b);
+    } else {
+      Cq[(int64_t)c * DP + j] = v;
+      vr = v;
+    }
+    nrm = fmaf(vr, vr, nrm);
+  }
+  nrm = wave_sum(nrm);
+  sh = wave_sum(sh);
+  if (lane == 0) {
+    hn[c] = (c < k) ? 0.5f * nrm : 1.0e30f;
+    if (shift2 && c < k) atomicAdd(shift2, sh);
+  }
+}
+
+}  // namespace dalgo
+
+using namespace dalgo;
+
+template <typename T, int DP>
+static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const void* Cq,
+                                   const float* hn, int kpad, int* assign, float* mind, double* sse,
+                                   hipStream_t st) {
+  constexpr int PT = sizeof(T) == 2 ? 2 : 1;
+  constexpr int NW = 8;
+  const int64_t per_block = NW * PT * 32;
+  const int64_t grid = cdiv(n, per_block);
+  if (grid == 0) return hipSuccess;
+  if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((kmeans_assign_kernel<T, DP, PT, NW>), dim3((unsigned)grid), dim3(NW * 64), 0,
+                     st, (const T*)X, n, ldx, (const T*)Cq, hn, kpad, assign, mind, sse);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+template <typename T>
+static hipError_t launch_assign(int DP, const void* X, int64_t n, int64_t ldx, const void* Cq,
+                                const float* hn, int kpad, int* assign, float* mind, double* sse,
+                                hipStream_t st) {
+  switch (DP) {
+    case 16: return launch_assign_dp<T, 16>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 32: return launch_assign_dp<T, 32>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 64: return launch_assign_dp<T, 64>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 128: return launch_assign_dp<T, 128>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <typename T, int DP>
+static hipError_t launch_acc_dp(const void* X, int64_t n, int64_t ldx, const int* assign, int k,
+                                float* S, unsigned long long* cnt, hipStream_t st) {
+  constexpr int NW = 8;
+  constexpr int CR = (DP >= 128) ? 64 : (8192 / DP);   // LDS table <= 32 KB
+  const int q = (int)cdiv(k, CR);
+  // ~2048 blocks in total, at least 2048 rows per chunk
+  int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n, 2048), std::max<int64_t>(1, 2048 / q)));
+  const int64_t rpc = round_up(cdiv(n, chunks), 64);
+  chunks = cdiv(n, rpc);
+  if (chunks == 0) return hipSuccess;
+  hipLaunchKernelGGL((kmeans_accumulate_kernel<T, DP, CR, NW>), dim3((unsigned)chunks, q),
+                     dim3(NW * 64), 0, st, (const T*)X, n, ldx, assign, k, rpc, S, cnt);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+template <typename T>
+static hipError_t launch_acc(int DP, const void* X, int64_t n, int64_t ldx, const int* assign,
+                             int k, float* S, unsigned long long* cnt, hipStream_t st) {
+  switch (DP) {
+    case 16: return launch_acc_dp<T, 16>(X, n, ldx, assign, k, S, cnt, st);
+    case 32: return launch_acc_dp<T, 32>(X, n, ldx, assign, k, S, cnt, st);
+    case 64: return launch_acc_dp<T, 64>(X, n, ldx, assign, k, S, cnt, st);
+    case 128: return launch_acc_dp<T, 128>(X, n, ldx, assign, k, S, cnt, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+extern "C" {
+
+hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
+                               const void* Cq, const float* hn, int kpad, int* assign, float* mind,
+                               double* sse, hipStream_t st) {
+  if (kpad % 32 != 0) return hipErrorInvalidValue;
+  return is_bf16 ? launch_assign<uint16_t>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, st)
+                 : launch_assign<float>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+}
+
+hipError_t dalgo_kmeans_accumulate(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
+                                   const int* assign, int k, float* S, unsigned long long* cnt,
+                                   hipStream_t st) {
+  return is_bf16 ? launch_acc<uint16_t>(DP, X, n, ldx, assign, k, S, cnt, st)
+                 : launch_acc<float>(DP, X, n, ldx, assign, k, S, cnt, st);
+}
+
+hipError_t dalgo_kmeans_update(float* C, const float* S, const unsigned long long* cnt, int k,
+                               int d, int DP,
+                               void* Cq, int is_bf16, float* hn, int kpad, float* shift2,
+                               hipStream_t st) {
+  const int grid = (int)cdiv(kpad, 4);
+  if (is_bf16)
+    hipLaunchKernelGGL(kmeans_update_kernel<uint16_t>, dim3(grid), dim3(256), 0, st, C, S, cnt, k,
+                       d, DP, (uint16_t*)Cq, hn, kpad, shift2);
+  else
+    hipLaunchKernelGGL(kmeans_update_kernel<float>, dim3(grid), dim3(256), 0, st, C, S, cnt, k, d,
+                       DP, (float*)Cq, hn, kpad, shift2);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+}  // extern "C"

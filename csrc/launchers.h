@@ -38,4 +38,32 @@ hipError_t dalgo_hbm_read(const void* p, int64_t nbytes, uint32_t* out, int grid
 hipError_t dalgo_mc_pi(uint64_t seed, uint64_t stream, uint64_t offset, uint64_t n,
                        unsigned long long* count, hipStream_t st);
 
+// ---- K2/K3 k-means (kmeans.hip)
+hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
+                               const void* Cq, const float* hn, int kpad, int* assign, float* mind,
+                               double* sse, hipStream_t st);
+hipError_t dalgo_kmeans_accumulate(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
+                                   const int* assign, int k, float* S, unsigned long long* cnt,
+                                   hipStream_t st);
+hipError_t dalgo_kmeans_update(float* C, const float* S, const unsigned long long* cnt, int k,
+                               int d, int DP, void* Cq, int is_bf16, float* hn, int kpad,
+                               float* shift2, hipStream_t st);
+
+// ---- K4 PageRank + R-MAT generator (pagerank.hip)
+hipError_t dalgo_rmat(uint64_t seed, int scale, int64_t e_off, int64_t n, float a, float b, float c,
+                      int do_scramble, int32_t* src, int32_t* dst, hipStream_t st);
+hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, const float* c,
+                         float* acc, int32_t* pres, hipStream_t st);
+hipError_t dalgo_pr_update(const float* acc, const int32_t* pres, const int32_t* outdeg, int64_t n,
+                           float q, float invN, int mode, const float* dangling_in, float* r,
+                           float* c, float* dangling_out, hipStream_t st);
+
+// ---- K9 transitive closure (closure.hip)
+hipError_t dalgo_tc_step(const void* A, int64_t lda, const void* Told, void* Tnew, int64_t ldt,
+                         int npad, int nz, unsigned long long* count, hipStream_t st);
+
+// ---- K5 ALS ridge SPD inverse (als.hip)
+hipError_t dalgo_spd_inverse(const float* G, int k, int ldg, float ridge, float* out, int ldo,
+                             int* status, hipStream_t st);
+
 }  // extern "C"

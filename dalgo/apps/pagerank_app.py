@@ -1,0 +1,72 @@
+"""graph_computation/pagerank.py entry logic."""
+from __future__ import annotations
+
+import torch
+
+from dalgo.models.pagerank import PageRank, PageRankConfig
+from dalgo.models.transitive_closure import compact_ids
+from dalgo.ops import graph as G
+from dalgo.parallel import runtime
+from dalgo.utils.cli import common_parser, init_from_args
+
+TOY_EDGES = [(1, 2), (1, 3), (2, 3), (3, 1)]   # pagerank.py:35-38
+
+
+def load_edges(path: str):
+    import numpy as np
+    arr = np.loadtxt(path, dtype=np.int64, delimiter=None, ndmin=2)
+    return torch.from_numpy(arr[:, 0]).to(torch.int32), torch.from_numpy(arr[:, 1]).to(torch.int32)
+
+
+def rmat_shard(scale: int, edge_factor: int, rank: int, world: int, device, seed: int = 1,
+               chunk: int = 1 << 26):
+    """Generate the global R-MAT stream in chunks, keep this rank's destinations."""
+    n_vertices = 1 << scale
+    n_edges = edge_factor * n_vertices
+    sl = G.vertex_slices(n_vertices, world)
+    v_lo, v_hi = rank * sl, min(n_vertices, (rank + 1) * sl)
+    parts = []
+    for off in range(0, n_edges, chunk):
+        m = min(chunk, n_edges - off)
+        s, d = G.rmat_edges(m, scale, seed=seed, e_off=off, device=device)
+        keep = (d >= v_lo) & (d < v_hi)
+        parts.append((s[keep], d[keep] - v_lo))
+        del s, d
+    return G.merge_shards(parts, v_lo, v_hi, n_vertices, sl), n_edges
+
+
+def main(argv=None):
+    ap = common_parser("Distributed PageRank (MI355X-native)")
+    ap.add_argument("--n-iterations", type=int, default=10)
+    ap.add_argument("--q", type=float, default=0.15)
+    ap.add_argument("--semantics", choices=["reference", "standard"], default="reference")
+    ap.add_argument("--edges", default=None, help="whitespace-separated 'src dst' edge file")
+    ap.add_argument("--rmat-scale", type=int, default=None, help="synthetic Graph500 R-MAT graph")
+    ap.add_argument("--edge-factor", type=int, default=16)
+    ap.add_argument("--top", type=int, default=20, help="print only the top ranks of large graphs")
+    a = ap.parse_args(argv)
+    rt = init_from_args(a, "PageRank")
+    ids = None
+    if a.rmat_scale:
+        shard, _ = rmat_shard(a.rmat_scale, a.edge_factor, rt.rank, rt.world_size, rt.device, a.seed + 1)
+    else:
+        if a.edges:
+            src, dst = load_edges(a.edges)
+        else:
+            src = torch.tensor([e[0] for e in TOY_EDGES], dtype=torch.int32)
+            dst = torch.tensor([e[1] for e in TOY_EDGES], dtype=torch.int32)
+        s, d, ids = compact_ids(src.long(), dst.long())
+        shard = G.build_shard(s.to(torch.int32).to(rt.device), d.to(torch.int32).to(rt.device),
+                              len(ids), rt.rank, rt.world_size)
+    pr = PageRank(PageRankConfig(q=a.q, n_iterations=a.n_iterations, semantics=a.semantics),
+                  shard, rt.world_size).fit()
+    ranks = pr.collect()
+    if rt.is_main:
+        items = list(ranks.items())
+        if ids is None and len(items) > a.top:
+            items = sorted(items, key=lambda kv: -kv[1])[: a.top]
+        for v, r in items:
+            vid = int(ids[v]) if ids is not None else v
+            print("%s has rank: %s." % (vid, r))
+    runtime.shutdown()
+    return ranks if ids is None else {int(ids[v]): r for v, r in ranks.items()}

@@ -1,0 +1,122 @@
+"""Distributed Lloyd k-means (machine_learning/k-means.py).
+
+Reference loop (k-means.py:53-71): ``takeSample(False, k, 42)`` initial centres,
+then ``n_iterations`` x [map(closest_center) -> reduceByKey((sum, count)) ->
+collect means -> replace non-empty centres]. ``convergeDist`` (:16) is declared
+but never used; here ``tol`` optionally stops when the max squared centre shift
+drops below it (off by default = reference behaviour).
+
+SPMD version per iteration, every rank on its HBM-resident row shard:
+  K2 assign (MFMA distance GEMM + argmin)  ->  K3 per-cluster sums/counts  ->
+  all_reduce(sums [k x DP] f32) + all_reduce(counts int64)  ->  fused update.
+The reduceByKey shuffle + driver collect become two RCCL all-reduces whose size
+is independent of N (528 KB at k=1024, d=128).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from dalgo.ops import kmeans as K
+from dalgo.parallel import comm
+
+
+@dataclass
+class KMeansConfig:
+    k: int = 2                 # k-means.py:15
+    n_iterations: int = 5      # k-means.py:18
+    n_workers: int = 2         # n_slices (k-means.py:17)
+    init: str = "sample"       # "sample": k distinct random rows (takeSample) | "given"
+    seed: int = 42             # takeSample(False, k, 42)
+    tol: float | None = None   # convergeDist-style early stop (reference ignores it)
+
+
+@dataclass
+class KMeansHistory:
+    sse: list = field(default_factory=list)
+    shift: list = field(default_factory=list)
+
+
+def sample_rows(n_global: int, k: int, seed: int) -> np.ndarray:
+    """k distinct global row ids (the takeSample stand-in; deterministic)."""
+    if k > n_global:
+        raise ValueError("k larger than the number of points")
+    rng = np.random.default_rng(seed)
+    return np.sort(rng.choice(n_global, size=k, replace=False))
+
+
+class KMeans:
+    def __init__(self, cfg: KMeansConfig, X_local: torch.Tensor, row_offset: int, n_global: int,
+                 init_centers: torch.Tensor | None = None):
+        self.cfg = cfg
+        self.X = K.prepare_points(X_local)
+        self.dev = self.X.device
+        self.row_offset = row_offset
+        self.n_global = n_global
+        self.d = self.X.shape[1]
+        self.DP = K.kmeans_dp(self.d)
+        k = cfg.k
+        if init_centers is None:
+            init_centers = self._sample_init()
+        self.cen = K.make_centers(init_centers.float(), self.X.dtype, self.dev)
+        self.assign = torch.zeros(self.X.shape[0], dtype=torch.int32, device=self.dev)
+        self.S = torch.zeros((k, self.DP), dtype=torch.float32, device=self.dev)
+        self.cnt = torch.zeros(k, dtype=torch.int64, device=self.dev)
+        self.sse = torch.zeros(1, dtype=torch.float64, device=self.dev)
+        self.shift2 = torch.zeros(1, dtype=torch.float32, device=self.dev)
+        self.history = KMeansHistory()
+        self.t = 0
+
+    def _sample_init(self) -> torch.Tensor:
+        ids = sample_rows(self.n_global, self.cfg.k, self.cfg.seed)
+        C = torch.zeros((self.cfg.k, self.d), dtype=torch.float32, device=self.dev)
+        lo, hi = self.row_offset, self.row_offset + self.X.shape[0]
+        mine = np.nonzero((ids >= lo) & (ids < hi))[0]
+        if len(mine):
+            rows = torch.from_numpy(ids[mine] - lo).to(self.dev)
+            C[torch.from_numpy(mine).to(self.dev)] = self.X[rows].float()
+        comm.all_reduce_sum(C)
+        return C
+
+    def step(self):
+        self.sse.zero_()
+        self.S.zero_()
+        self.cnt.zero_()
+        self.shift2.zero_()
+        K.assign(self.X, self.cen, out=self.assign, sse=self.sse)
+        K.accumulate(self.X, self.assign, self.cfg.k, self.DP, self.S, self.cnt)
+        comm.all_reduce_sum(self.S)
+        comm.all_reduce_sum(self.cnt)
+        K.update(self.cen, self.S, self.cnt, self.shift2)
+        self.t += 1
+
+    def fit(self, n_iterations: int | None = None, track: bool = True):
+        n = self.cfg.n_iterations if n_iterations is None else n_iterations
+        for _ in range(n):
+            self.step()
+            if track or self.cfg.tol is not None:
+                sse = self.sse.clone()
+                comm.all_reduce_sum(sse)
+                self.history.sse.append(float(sse.item()))
+                self.history.shift.append(float(self.shift2.item()))
+                if self.cfg.tol is not None and self.history.shift[-1] < self.cfg.tol:
+                    break
+        return self.history
+
+    def predict(self, X: torch.Tensor) -> torch.Tensor:
+        return K.assign(K.prepare_points(X), self.cen)
+
+    @property
+    def centers(self) -> torch.Tensor:
+        return self.cen.C
+
+    def state_dict(self) -> dict:
+        return {"t": self.t, "centers": self.cen.C.detach().cpu(), "sse": list(self.history.sse)}
+
+    def load_state_dict(self, sd: dict):
+        self.t = int(sd["t"])
+        self.cen.C.copy_(sd["centers"].to(self.dev))
+        K.refresh(self.cen)
+        self.history.sse = list(sd.get("sse", []))

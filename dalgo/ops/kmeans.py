@@ -1,0 +1,125 @@
+"""k-means ops: fused MFMA distance+argmin (K2), per-cluster accumulation (K3)
+and the centroid update (csrc/kernels/kmeans.hip), plus torch-CPU references.
+
+Layouts: points X [n, >=DP] (bf16 or f32, zero in columns [d, DP), rows 16-B
+aligned); centres keep an f32 master ``C [k, d]`` plus the MFMA copy
+``Cq [kpad, DP]`` in X's dtype and ``hn = 0.5*|Cq|^2`` (1e30 for padding rows),
+with DP = d rounded up to 16/32/64/128 and kpad = k rounded up to 32.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from dalgo.ops import _ext
+
+
+def kmeans_dp(d: int) -> int:
+    for dp in (16, 32, 64, 128):
+        if d <= dp:
+            return dp
+    raise ValueError(f"k-means kernels support d <= 128 (got {d})")
+
+
+def prepare_points(X: torch.Tensor) -> torch.Tensor:
+    """Return X as an [n, d] view of a zero-padded [n, DP] buffer (copy if needed)."""
+    n, d = X.shape
+    DP = kmeans_dp(d)
+    if X.stride(1) == 1 and X.stride(0) == DP and X.data_ptr() % 16 == 0:
+        return X
+    buf = torch.zeros((n, DP), dtype=X.dtype, device=X.device)
+    buf[:, :d] = X
+    return buf[:, :d]
+
+
+def _full(X: torch.Tensor) -> torch.Tensor:
+    """The [n, DP] padded rows behind a prepared [n, d] view."""
+    DP = kmeans_dp(X.shape[1])
+    return X.as_strided((X.shape[0], DP), (X.stride(0), 1))
+
+
+@dataclass
+class Centers:
+    C: torch.Tensor      # [k, d] f32 master
+    Cq: torch.Tensor     # [kpad, DP] compute copy (X dtype)
+    hn: torch.Tensor     # [kpad] f32
+    k: int
+    d: int
+
+    @property
+    def DP(self) -> int:
+        return self.Cq.shape[1]
+
+
+def make_centers(C0: torch.Tensor, dtype: torch.dtype, device) -> Centers:
+    k, d = C0.shape
+    DP = kmeans_dp(d)
+    kpad = ((k + 31) // 32) * 32
+    C = C0.to(device=device, dtype=torch.float32).contiguous()
+    Cq = torch.zeros((kpad, DP), dtype=dtype, device=device)
+    hn = torch.zeros(kpad, dtype=torch.float32, device=device)
+    cen = Centers(C, Cq, hn, k, d)
+    refresh(cen)
+    return cen
+
+
+def refresh(cen: Centers):
+    """Recompute Cq / hn from the master C (host-side torch; once per init)."""
+    Cq = cen.Cq
+    Cq.zero_()
+    Cq[: cen.k, : cen.d] = cen.C.to(Cq.dtype)
+    r = Cq[: cen.k].float()
+    cen.hn.fill_(1e30)
+    cen.hn[: cen.k] = 0.5 * (r * r).sum(dim=1)
+
+
+def assign(X: torch.Tensor, cen: Centers, out: torch.Tensor | None = None,
+           mind: torch.Tensor | None = None, sse: torch.Tensor | None = None):
+    """Nearest-centre ids (int32, ties -> lowest id), squared distances, SSE."""
+    n = X.shape[0]
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=X.device)
+    if X.is_cuda:
+        _ext.ops().kmeans_assign(X, cen.Cq, cen.hn, out, mind, sse)
+        return out
+    # CPU reference: exact scores on the ROUNDED centres, f64, first maximum wins
+    Xf = X[:, : cen.d].double()
+    Cr = cen.Cq[: cen.k, : cen.d].double()
+    score = Xf @ Cr.T - 0.5 * (Cr * Cr).sum(dim=1)[None, :]
+    best = torch.argmax(score, dim=1)
+    out.copy_(best.to(torch.int32))
+    dist = ((Xf * Xf).sum(dim=1) - 2 * score.gather(1, best[:, None])[:, 0]).clamp_min(0)
+    if mind is not None:
+        mind.copy_(dist.float())
+    if sse is not None:
+        sse += dist.sum()
+    return out
+
+
+def accumulate(X: torch.Tensor, a: torch.Tensor, k: int, DP: int, S: torch.Tensor,
+               cnt: torch.Tensor):
+    """S[c, :] += sum of rows assigned to c (f32, [k, DP]); cnt[c] += count (int64)."""
+    if X.is_cuda:
+        _ext.ops().kmeans_accumulate(X, a, int(k), int(DP), S, cnt)
+        return S, cnt
+    d = X.shape[1]
+    idx = a.long()
+    S.view(k, DP)[:, :d].index_add_(0, idx, X.to(S.dtype))
+    cnt.index_add_(0, idx, torch.ones_like(idx, dtype=cnt.dtype))
+    return S, cnt
+
+
+def update(cen: Centers, S: torch.Tensor, cnt: torch.Tensor, shift2: torch.Tensor | None = None):
+    """c = S/n (non-empty), stale otherwise (k-means.py:70-71); refreshes Cq / hn."""
+    if cen.C.is_cuda:
+        _ext.ops().kmeans_update(cen.C, S, cnt, cen.Cq, cen.hn, shift2)
+        return cen
+    Sv = S.view(-1, cen.DP)[: cen.k, : cen.d]
+    n = cnt[: cen.k].to(torch.float32).view(-1, 1)
+    new = torch.where(n > 0, Sv / n.clamp_min(1), cen.C)
+    if shift2 is not None:
+        shift2 += ((new - cen.C) ** 2).sum()
+    cen.C.copy_(new)
+    refresh(cen)
+    return cen

@@ -1,0 +1,42 @@
+"""Shared command-line plumbing for the reference-compatible entry scripts.
+
+Every script keeps the reference's constants as argparse defaults and adds the
+common flags below. Launch: ``python <script>.py`` (one rank) or
+``torchrun --nproc-per-node N <script>.py`` (one rank per GPU, RCCL).
+"""
+from __future__ import annotations
+
+import argparse
+
+import torch
+
+from dalgo.parallel import runtime
+
+
+def common_parser(description: str) -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(description=description)
+    ap.add_argument("--device", choices=["auto", "cuda", "cpu"], default="auto",
+                    help="cuda = gfx950 HIP kernels + RCCL, cpu = torch reference + gloo")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default=None)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--metrics-out", default=None, help="JSONL metrics file (rank 0)")
+    ap.add_argument("--quiet", action="store_true", help="suppress per-iteration lines")
+    ap.add_argument("--no-plot", action="store_true")
+    return ap
+
+
+def init_from_args(a, app_name: str) -> runtime.Runtime:
+    dev = None if a.device == "auto" else a.device
+    if dev is None and a.backend == "gloo":
+        dev = "cpu"
+    return runtime.init(backend=a.backend, device=dev, app_name=app_name)
+
+
+def default_dtype(rt: runtime.Runtime, want: str | None = None) -> torch.dtype:
+    if want == "bf16":
+        return torch.bfloat16
+    if want == "f32":
+        return torch.float32
+    if want == "f64":
+        return torch.float64
+    return torch.float32 if rt.device.type == "cuda" else torch.float64
