@@ -1,0 +1,93 @@
+"""Multi-rank (gloo, world_size=2) == single-rank equivalence for every algorithm."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from tests.dist_util import run_world
+
+
+def _lr_family(rt):
+    from dalgo.data.datasets import breast_cancer
+    from dalgo.models.localsgd import ParallelSGD, SGDConfig
+    from dalgo.parallel.sharding import make_layout
+    out = {}
+    for algo in ("ssgd", "gd", "ma", "bmuf", "easgd"):
+        cfg = SGDConfig(algo=algo, n_iterations=12, eval_every=0)
+        lay = make_layout(398, cfg.n_workers, rt.world_size, rt.rank)
+        d = breast_cancer(dtype=torch.float64, row_range=(lay.row_lo, lay.row_hi))
+        m = ParallelSGD(cfg, d, lay, rt, model_dtype=torch.float64)
+        m.fit()
+        out[algo] = m.weights().numpy().copy()
+    return out
+
+
+def _others(rt):
+    from dalgo.models.als import ALS, ALSConfig
+    from dalgo.models.kmeans import KMeans, KMeansConfig
+    from dalgo.models.monte_carlo import MonteCarloConfig, estimate_pi
+    from dalgo.models.pagerank import PageRank, PageRankConfig
+    from dalgo.models.transitive_closure import DenseClosure, SparseClosure
+    from dalgo.data.synthetic import blobs
+    from dalgo.ops import graph as G
+    from dalgo.parallel.sharding import even_slices
+    W, r = rt.world_size, rt.rank
+    out = {}
+    # k-means on blobs
+    n = 3000
+    lo, hi = even_slices(n, W)[r]
+    X = blobs(n, 5, 4, row_range=(lo, hi), seed=3)
+    km = KMeans(KMeansConfig(k=4, n_iterations=4, seed=1), X, lo, n)
+    km.fit()
+    out["kmeans"] = km.centers.numpy().copy()
+    out["kmeans_sse"] = km.history.sse
+    # pagerank on a small R-MAT graph, both semantics
+    s, d = G.rmat_edges(6000, 10, seed=9)
+    for sem in ("reference", "standard"):
+        sh = G.build_shard(s, d, 1024, r, W)
+        out["pr_" + sem] = PageRank(PageRankConfig(semantics=sem), sh, W).fit().collect()
+    # transitive closure
+    g = torch.Generator().manual_seed(4)
+    ts = torch.randint(0, 60, (100,), generator=g)
+    td = torch.randint(0, 60, (100,), generator=g)
+    out["tc_dense"] = DenseClosure(ts, td, 60, r, W).run().counts
+    out["tc_sparse"] = SparseClosure(ts, td, r, W, n=60).run().counts
+    # ALS
+    out["als"] = ALS(ALSConfig(m=40, n=60, k=5, seed=2), r, W).fit().rmse
+    # Monte Carlo
+    out["mc"] = estimate_pi(MonteCarloConfig(n=200_000), r, W)
+    return out
+
+
+@pytest.fixture(scope="module")
+def lr_results():
+    one = run_world(_lr_family, world=1)[0]
+    two = run_world(_lr_family, world=2)
+    return one, two
+
+
+@pytest.mark.parametrize("algo", ["ssgd", "gd", "ma", "bmuf", "easgd"])
+def test_lr_family_two_ranks_equal_one(lr_results, algo):
+    one, two = lr_results
+    assert np.allclose(two[0][algo], two[1][algo], rtol=0, atol=0)        # replicated state
+    ref = one[algo]
+    assert np.allclose(two[0][algo], ref, rtol=1e-10, atol=1e-8 * max(1, np.abs(ref).max()))
+
+
+def test_other_algorithms_two_ranks_equal_one():
+    one = run_world(_others, world=1)[0]
+    two = run_world(_others, world=2)
+    for k in ("kmeans",):
+        assert np.allclose(two[0][k], one[k], atol=1e-4), k
+        assert np.allclose(two[1][k], one[k], atol=1e-4), k
+    assert np.allclose(two[0]["kmeans_sse"], one["kmeans_sse"], rtol=1e-6)
+    for sem in ("pr_reference", "pr_standard"):
+        a, b = one[sem], two[0][sem]
+        assert set(a) == set(b)
+        assert max(abs(a[v] - b[v]) for v in a) < 1e-12
+        assert b == two[1][sem]
+    assert one["tc_dense"] == two[0]["tc_dense"] == one["tc_sparse"] == two[1]["tc_sparse"]
+    assert np.allclose(one["als"], two[0]["als"], rtol=1e-9)
+    assert one["mc"] == two[0]["mc"] == two[1]["mc"]
+    assert abs(one["mc"][0] - math.pi) < 0.02

@@ -1,0 +1,103 @@
+"""The reference-path entry scripts run end-to-end (CPU) and print the reference lines."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, timeout=300):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable] + args, cwd=ROOT, capture_output=True, text=True,
+                       timeout=timeout, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    return r.stdout
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("script,needle", [
+    ("optimization/ssgd.py", "Final acc:"),
+    ("optimization/ma.py", "Final acc:"),
+    ("optimization/bmuf.py", "Final acc:"),
+    ("optimization/easgd.py", "Final acc:"),
+    ("machine_learning/logistic_regression.py", "Final acc:"),
+])
+def test_lr_scripts(script, needle, tmp_path):
+    out = _run([script, "--device", "cpu", "--n-iterations", "30", "--quiet", "--no-plot",
+                "--metrics-out", str(tmp_path / "m.jsonl")])
+    assert "Initial w:" in out and needle in out
+    lines = (tmp_path / "m.jsonl").read_text().splitlines()
+    assert len(lines) == 30 and "accuracy" in json.loads(lines[-1])
+
+
+def test_kmeans_script():
+    out = _run(["machine_learning/k-means.py", "--device", "cpu", "--no-plot"])
+    assert "Final centers: [array([1., 2.]" in out and "array([10.,  2.]" in out
+
+
+def test_pagerank_script():
+    out = _run(["graph_computation/pagerank.py", "--device", "cpu"])
+    assert "1 has rank: 0.38891305880091237." in out
+    assert "2 has rank: 0.214416470596171." in out
+    assert "3 has rank: 0.3966704706029163." in out
+
+
+def test_closure_script():
+    out = _run(["graph_computation/transitive_closure.py", "--device", "cpu"])
+    assert "The original graph has 9 paths" in out
+
+
+def test_als_script():
+    out = _run(["matrix_computation/matrix_decomposition.py", "--device", "cpu"])
+    assert out.count("rmse:") == 5 and "iterations: 4, rmse:" in out
+
+
+def test_monte_carlo_script():
+    out = _run(["randomized_algorithm/monte_carlo.py", "--device", "cpu"])
+    assert "Pi is roughly 3.1" in out
+
+
+def test_torchrun_two_ranks_gloo():
+    out = _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+                "optimization/bmuf.py", "--device", "cpu", "--backend", "gloo",
+                "--n-iterations", "20", "--quiet", "--no-plot"], timeout=400)
+    assert out.count("Final acc:") == 1   # rank 0 prints only
+
+
+def test_checkpoint_resume(tmp_path):
+    ck = str(tmp_path / "ck")
+    full = _run(["optimization/easgd.py", "--device", "cpu", "--n-iterations", "40", "--quiet",
+                 "--no-plot"])
+    _run(["optimization/easgd.py", "--device", "cpu", "--n-iterations", "20", "--quiet",
+          "--no-plot", "--ckpt-dir", ck])
+    resumed = _run(["optimization/easgd.py", "--device", "cpu", "--n-iterations", "40", "--quiet",
+                    "--no-plot", "--ckpt-dir", ck, "--resume"])
+    assert "Resumed from iteration 20" in resumed
+    fw = full.split("Final w:")[1]
+    rw = resumed.split("Final w:")[1]
+    assert fw == rw
+
+
+def test_bench_cpu_contract():
+    out = _run(["bench.py", "--device", "cpu", "--rows", "20000", "--dim", "64", "--steps", "3",
+                "--warmup", "1", "--dtype", "f32"])
+    line = [l for l in out.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0

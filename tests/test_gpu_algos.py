@@ -1,0 +1,205 @@
+"""GPU numerics of K2/K3 (k-means), K4 (PageRank), K5 (ALS), K9 (closure) and the
+end-to-end models against the torch-CPU references."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from dalgo.ops import graph as G
+from dalgo.ops import kmeans as K
+
+pytestmark = pytest.mark.gpu
+
+
+# ------------------------------------------------------------------ k-means
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("d,k,n", [(2, 2, 6), (16, 40, 3000), (50, 33, 4099), (128, 1024, 20000)])
+def test_kmeans_assign_matches_reference(cuda, dtype, d, k, n):
+    g = torch.Generator().manual_seed(d + k)
+    X = (torch.randn(n, d, generator=g) * 3).to(dtype)
+    C0 = torch.randn(k, d, generator=g) * 3
+    Xc = K.prepare_points(X)
+    cen_c = K.make_centers(C0, dtype, "cpu")
+    a_ref = K.assign(Xc, cen_c)
+    Xd = K.prepare_points(X.to(cuda))
+    cen_d = K.make_centers(C0, dtype, cuda)
+    mind = torch.empty(n, device=cuda)
+    sse = torch.zeros(1, dtype=torch.float64, device=cuda)
+    a = K.assign(Xd, cen_d, mind=mind, sse=sse).cpu()
+    # scores computed in f32 on the GPU vs f64 on the CPU: allow rare near-ties
+    agree = (a == a_ref).float().mean().item()
+    assert agree > 0.999, agree
+    # where they differ the two distances must be (nearly) equal
+    Xf = Xc.double()
+    Cr = cen_c.Cq[:k, :d].double()
+    dist = torch.cdist(Xf, Cr) ** 2
+    dd = dist.gather(1, a.long()[:, None]) - dist.gather(1, a_ref.long()[:, None])
+    assert dd.abs().max().item() < 1e-3 * (1 + dist.max().item())
+    assert torch.allclose(mind.cpu().double(), dist.gather(1, a.long()[:, None])[:, 0],
+                          rtol=1e-3, atol=1e-2)
+
+
+def test_kmeans_ties_lowest_index(cuda):
+    X = torch.tensor([[0.0, 0.0]] * 5)
+    C0 = torch.tensor([[1.0, 0.0], [-1.0, 0.0], [0.0, 1.0]])   # all equidistant
+    a = K.assign(K.prepare_points(X.to(cuda)), K.make_centers(C0, torch.float32, cuda)).cpu()
+    assert a.tolist() == [0] * 5
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_kmeans_accumulate_update(cuda, dtype):
+    n, d, k = 50_000, 100, 70
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(n, d, generator=g).to(dtype)
+    a = torch.randint(0, k - 3, (n,), generator=g, dtype=torch.int32)   # last 3 clusters empty
+    DP = K.kmeans_dp(d)
+    S = torch.zeros(k, DP, device=cuda)
+    cnt = torch.zeros(k, dtype=torch.int64, device=cuda)
+    K.accumulate(K.prepare_points(X.to(cuda)), a.to(cuda), k, DP, S, cnt)
+    Sr = torch.zeros(k, DP, dtype=torch.float64)
+    Sr[:, :d].index_add_(0, a.long(), X.double())
+    cr = torch.bincount(a.long(), minlength=k)
+    assert torch.equal(cnt.cpu(), cr)
+    assert torch.allclose(S.cpu().double(), Sr, atol=1e-2, rtol=1e-4)
+    C0 = torch.randn(k, d, generator=g)
+    cen = K.make_centers(C0, dtype, cuda)
+    sh = torch.zeros(1, device=cuda)
+    K.update(cen, S, cnt, sh)
+    exp = torch.where(cr[:, None] > 0, Sr[:, :d] / cr.clamp_min(1)[:, None].double(), C0.double())
+    assert torch.allclose(cen.C.cpu().double(), exp, atol=1e-4)
+    assert torch.equal(cen.C[-3:].cpu(), C0[-3:])   # empty clusters keep the stale centre
+    rq = cen.Cq[:k, :d].float()
+    assert torch.allclose(cen.hn[:k], 0.5 * (rq * rq).sum(1), rtol=1e-5)
+    assert (cen.hn[k:] > 1e29).all()
+
+
+def test_kmeans_model_gpu_vs_cpu(cuda):
+    from dalgo.data.synthetic import blobs
+    from dalgo.models.kmeans import KMeans, KMeansConfig
+    X = blobs(20_000, 16, 8, seed=5)
+    cfg = KMeansConfig(k=8, n_iterations=6, seed=3)
+    kc = KMeans(cfg, X, 0, X.shape[0])
+    kc.fit()
+    kg = KMeans(cfg, X.to(cuda), 0, X.shape[0])
+    kg.fit()
+    assert torch.allclose(kg.centers.cpu(), kc.centers, atol=1e-3)
+    assert kg.history.sse[-1] == pytest.approx(kc.history.sse[-1], rel=1e-4)
+
+
+def test_kmeans_toy_gpu(cuda):
+    from dalgo.models.kmeans import KMeans, KMeansConfig
+    X = torch.tensor([[1, 2], [1, 4], [1, 0], [10, 2], [10, 4], [10, 0]], dtype=torch.float32)
+    km = KMeans(KMeansConfig(k=2), X.to(cuda), 0, 6,
+                init_centers=torch.tensor([[1.0, 4.0], [10.0, 0.0]]))
+    km.fit()
+    assert km.centers.cpu().tolist() == [[1.0, 2.0], [10.0, 2.0]]
+
+
+# ------------------------------------------------------------------ PageRank
+def test_rmat_generator_matches_cpu(cuda):
+    s, d = G.rmat_edges(5000, 14, seed=11, e_off=123, device=cuda)
+    sc, dc = G.rmat_edges(5000, 14, seed=11, e_off=123)
+    assert torch.equal(s.cpu(), sc) and torch.equal(d.cpu(), dc)
+    assert int(s.max()) < (1 << 14) and int(s.min()) >= 0
+
+
+@pytest.mark.parametrize("frac_absent", [0.0, 0.3])
+def test_pr_spmv_matches_reference(cuda, frac_absent):
+    nv = 1 << 13
+    s, d = G.rmat_edges(200_000, 13, seed=3)
+    sh_c = G.build_shard(s, d, nv, 0, 1)
+    sh_d = G.build_shard(s.to(cuda), d.to(cuda), nv, 0, 1)
+    g = torch.Generator().manual_seed(0)
+    c = torch.rand(nv, generator=g)
+    c[torch.rand(nv, generator=g) < frac_absent] = -1.0
+    acc_c = torch.zeros(nv, dtype=torch.float64)
+    pres_c = torch.zeros(nv, dtype=torch.int32)
+    G.pr_spmv(sh_c, c.double(), acc_c, pres_c)
+    acc = torch.zeros(nv, device=cuda)
+    pres = torch.zeros(nv, dtype=torch.int32, device=cuda)
+    G.pr_spmv(sh_d, c.to(cuda), acc, pres)
+    assert torch.equal(pres.cpu(), pres_c)
+    assert torch.allclose(acc.cpu().double(), acc_c, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("sem", ["reference", "standard"])
+def test_pagerank_gpu_vs_cpu(cuda, sem):
+    from dalgo.models.pagerank import PageRank, PageRankConfig
+    s, d = G.rmat_edges(100_000, 12, seed=8)
+    nv = 1 << 12
+    rc = PageRank(PageRankConfig(semantics=sem), G.build_shard(s, d, nv, 0, 1)).fit().collect()
+    rg = PageRank(PageRankConfig(semantics=sem),
+                  G.build_shard(s.to(cuda), d.to(cuda), nv, 0, 1)).fit().collect()
+    assert set(rc) == set(rg)
+    assert max(abs(rc[v] - rg[v]) for v in rc) < 1e-6
+
+
+def test_pagerank_toy_gpu(cuda):
+    from dalgo.models.pagerank import PageRank, PageRankConfig
+    src = torch.tensor([1, 1, 2, 3], dtype=torch.int32, device=cuda)
+    dst = torch.tensor([2, 3, 3, 1], dtype=torch.int32, device=cuda)
+    r = PageRank(PageRankConfig(), G.build_shard(src, dst, 4, 0, 1)).fit().collect()
+    assert r[1] == pytest.approx(0.38891305880091237, abs=1e-6)
+    assert r[2] == pytest.approx(0.214416470596171, abs=1e-6)
+    assert r[3] == pytest.approx(0.3966704706029163, abs=1e-6)
+
+
+# ------------------------------------------------------------------ closure / ALS / MC
+def test_transitive_closure_gpu(cuda):
+    from dalgo.models.transitive_closure import DenseClosure, SparseClosure
+    g = torch.Generator().manual_seed(2)
+    n, e = 300, 420
+    src = torch.randint(0, n, (e,), generator=g)
+    dst = torch.randint(0, n, (e,), generator=g)
+    ref = DenseClosure(src, dst, n).run().counts
+    assert DenseClosure(src, dst, n, device=cuda).run().counts == ref
+    assert SparseClosure(src, dst, n=n, device=cuda).run().counts == ref
+    s4 = torch.tensor([0, 0, 1, 2])
+    d4 = torch.tensor([1, 2, 2, 0])
+    assert DenseClosure(s4, d4, 3, device=cuda).run().counts == [4, 8, 9, 9]
+
+
+def test_spd_inverse_gpu(cuda):
+    from dalgo.models.als import spd_inverse
+    for k in (10, 64, 128):
+        A = torch.rand(200, k, dtype=torch.float64)
+        G_ = (A.T @ A).float()
+        inv = spd_inverse(G_.to(cuda), 5.0).cpu().double()
+        ref = torch.linalg.inv(G_.double() + 5.0 * torch.eye(k, dtype=torch.float64))
+        assert torch.allclose(inv, ref, rtol=1e-4, atol=1e-6)
+
+
+def test_als_gpu(cuda):
+    from dalgo.models.als import ALS, ALSConfig
+    hc = ALS(ALSConfig(seed=3)).fit().rmse
+    hg = ALS(ALSConfig(seed=3), device=cuda).fit().rmse
+    assert hg[-1] < 0.05 and abs(hg[0] - hc[0]) < 1e-3
+
+
+def test_monte_carlo_gpu(cuda):
+    from dalgo.models.monte_carlo import MonteCarloConfig, estimate_pi
+    pi_c, cnt_c = estimate_pi(MonteCarloConfig(n=2_000_000))
+    pi_g, cnt_g = estimate_pi(MonteCarloConfig(n=2_000_000), device=cuda)
+    assert abs(cnt_c - cnt_g) <= 4 and abs(pi_g - math.pi) < 0.01
+
+
+# ------------------------------------------------------------------ LR family end-to-end
+@pytest.mark.parametrize("algo", ["ssgd", "gd", "ma", "bmuf", "easgd"])
+def test_lr_family_gpu_tracks_cpu(cuda, algo):
+    from dalgo.data.datasets import synthetic_logistic
+    from dalgo.models.localsgd import ParallelSGD, SGDConfig
+    from dalgo.parallel import runtime
+    from dalgo.parallel.sharding import make_layout
+    rt = runtime.init(device="cuda")
+    N, D = 40_000, 96
+    cfg = SGDConfig(algo=algo, n_workers=4, n_iterations=15, eta=0.5, eval_every=0)
+    lay = make_layout(N, 4, 1, 0, spark_compatible=False)
+    dc = synthetic_logistic(N, D, dtype=torch.float32, device="cpu")
+    dg = synthetic_logistic(N, D, dtype=torch.float32, device=cuda)
+    assert torch.allclose(dg.X_train.cpu(), dc.X_train, atol=1e-6)
+    mc = ParallelSGD(cfg, dc, lay, rt, model_dtype=torch.float64)
+    mc.fit()
+    mg = ParallelSGD(cfg, dg, lay, rt)
+    mg.fit()
+    assert torch.allclose(mg.weights().cpu().double(), mc.weights(), rtol=1e-3, atol=1e-4)
