@@ -230,6 +230,7 @@ void hbm_read(const Tensor& src, Tensor out, int64_t unroll) {
 
 // ---------------------------------------------------------------------------
 // k-means
+void check_i32(const Tensor& t, const char* what);
 inline int kmeans_dp(int64_t d) {
   for (int dp : {16, 32, 64, 128})
     if (d <= dp) return dp;
@@ -298,6 +299,34 @@ void kmeans_accumulate(const Tensor& X, const Tensor& assign, int64_t k, int64_t
                   "kmeans_accumulate");
 }
 
+void kmeans_accumulate_sorted(const Tensor& X, const Tensor& assign, int64_t k, int64_t DP,
+                              int64_t seg, Tensor block_counts, Tensor cluster_start,
+                              Tensor seg_start, Tensor perm, Tensor S, Tensor cnt) {
+  TORCH_CHECK(kmeans_dp(DP) == DP, "DP must be 16/32/64/128");
+  check_points(X, (int)DP);
+  const int64_t n = X.size(0);
+  TORCH_CHECK(n < 0x7fffffffLL, "kmeans_accumulate_sorted: n must fit int32 (shard larger inputs)");
+  TORCH_CHECK(assign.scalar_type() == at::kInt && assign.numel() >= n, "assign");
+  check_i32(block_counts, "block_counts");
+  TORCH_CHECK(block_counts.numel() % k == 0 && block_counts.numel() >= k, "block_counts [B*k]");
+  const int64_t B = block_counts.numel() / k;
+  TORCH_CHECK(cluster_start.scalar_type() == at::kLong && cluster_start.numel() >= k + 1, "cluster_start");
+  TORCH_CHECK(seg_start.scalar_type() == at::kLong && seg_start.numel() >= k + 1, "seg_start");
+  check_i32(perm, "perm");
+  TORCH_CHECK(perm.numel() >= n, "perm");
+  check_f32(S, "S");
+  TORCH_CHECK(S.numel() >= k * DP, "S");
+  TORCH_CHECK(cnt.scalar_type() == at::kLong && cnt.numel() >= k, "cnt");
+  DeviceGuard guard(X.device());
+  DALGO_CHECK_HIP(dalgo_kmeans_accumulate_sorted(
+                      X.data_ptr(), X.scalar_type() == at::kBFloat16, n, X.stride(0), (int)DP,
+                      assign.data_ptr<int>(), (int)k, (int)B, (int)seg, block_counts.data_ptr<int>(),
+                      cluster_start.data_ptr<int64_t>(), seg_start.data_ptr<int64_t>(),
+                      perm.data_ptr<int>(), S.data_ptr<float>(),
+                      reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>()), cur_stream()),
+                  "kmeans_accumulate_sorted");
+}
+
 void kmeans_update(Tensor C, const Tensor& S, const Tensor& cnt, Tensor Cq, Tensor hn,
                    const std::optional<Tensor>& shift2) {
   check_f32(C, "C");
@@ -326,7 +355,7 @@ void kmeans_update(Tensor C, const Tensor& S, const Tensor& cnt, Tensor Cq, Tens
 
 // ---------------------------------------------------------------------------
 // PageRank
-inline void check_i32(const Tensor& t, const char* what) {
+void check_i32(const Tensor& t, const char* what) {
   check_dev(t, what);
   TORCH_CHECK(t.scalar_type() == at::kInt && t.is_contiguous(), "dalgo: ", what, " must be int32");
 }
@@ -440,6 +469,9 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("kmeans_assign(Tensor X, Tensor Cq, Tensor hn, Tensor(a!) assign, Tensor(b!)? mind, "
         "Tensor(c!)? sse) -> ()");
   m.def("kmeans_accumulate(Tensor X, Tensor assign, int k, int DP, Tensor(a!) S, Tensor(b!) cnt) -> ()");
+  m.def("kmeans_accumulate_sorted(Tensor X, Tensor assign, int k, int DP, int seg, "
+        "Tensor(a!) block_counts, Tensor(b!) cluster_start, Tensor(c!) seg_start, Tensor(d!) perm, "
+        "Tensor(e!) S, Tensor(f!) cnt) -> ()");
   m.def("kmeans_update(Tensor(a!) C, Tensor S, Tensor cnt, Tensor(b!) Cq, Tensor(c!) hn, "
         "Tensor(d!)? shift2) -> ()");
   m.def("rmat_edges(int seed, int scale, int e_off, float a, float b, float c, bool scramble, "
@@ -469,5 +501,6 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("pr_update", &pr_update);
   m.impl("kmeans_assign", &kmeans_assign);
   m.impl("kmeans_accumulate", &kmeans_accumulate);
-  m.impl("kmeans_update", &kmeans_update);   // dispatches on its output counter
+  m.impl("kmeans_update", &kmeans_update);
+  m.impl("kmeans_accumulate_sorted", &kmeans_accumulate_sorted);   // dispatches on its output counter
 }

@@ -343,6 +343,140 @@ kmeans_update_kernel(float* __restrict__ C, const float* __restrict__ S,
   }
 }
 
+// ---------------------------------------------------------------------------
+// K3 (sort-based, default): counting sort of the rows by cluster, then every
+// wave sums a contiguous run of <= SEG rows of one cluster in registers and adds
+// that partial row once to S. Global float atomics: one d-vector per segment
+// (~N/SEG + k of them) instead of one per row; every X row is gathered once.
+//   hist    : per row-chunk LDS histogram -> block_counts[b][c]
+//   scan    : per cluster, exclusive offsets over chunks; cluster starts; segments
+//   scatter : LDS cursors -> perm[pos] = row
+//   segsum  : per segment register accumulation -> atomicAdd into S[c]
+__global__ void __launch_bounds__(256)
+kmeans_hist_kernel(const int* __restrict__ assign, int64_t n, int64_t rpc, int k,
+                   int* __restrict__ block_counts) {
+  extern __shared__ int hist[];
+  for (int c = threadIdx.x; c < k; c += blockDim.x) hist[c] = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rpc, r1 = min(n, r0 + rpc);
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) atomicAdd(&hist[assign[r]], 1);
+  __syncthreads();
+  for (int c = threadIdx.x; c < k; c += blockDim.x) block_counts[(int64_t)blockIdx.x * k + c] = hist[c];
+}
+
+__global__ void __launch_bounds__(1024)
+kmeans_scan_kernel(int* __restrict__ block_counts, int B, int k, int seg,
+                   int64_t* __restrict__ cluster_start, int64_t* __restrict__ seg_start,
+                   unsigned long long* __restrict__ cnt_out) {
+  extern __shared__ int64_t tot[];            // [2k]: counts, then segment counts
+  __shared__ int64_t s_part[2][1024 / 64];
+  for (int c = threadIdx.x; c < k; c += blockDim.x) {
+    int run = 0;
+    for (int b = 0; b < B; ++b) {
+      const int v = block_counts[(int64_t)b * k + c];
+      block_counts[(int64_t)b * k + c] = run;
+      run += v;
+    }
+    tot[c] = run;
+    tot[k + c] = (run + seg - 1) / seg;
+    if (cnt_out) cnt_out[c] += (unsigned long long)run;
+  }
+  __syncthreads();
+  // exclusive scans of tot[0..k) and tot[k..2k) by a single thread per chunk of k/1024
+  const int per = (k + blockDim.x - 1) / blockDim.x;
+  const int c0 = threadIdx.x * per, c1 = min(k, c0 + per);
+  int64_t a = 0, b = 0;
+  for (int c = c0; c < c1; ++c) { a += tot[c]; b += tot[k + c]; }
+  // block-wide exclusive scan of (a, b) via LDS (wave partials)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t ia = a, ib = b;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t ta = __shfl_up(ia, off), tb = __shfl_up(ib, off);
+    if (lane >= off) { ia += ta; ib += tb; }
+  }
+  if (lane == 63) { s_part[0][wid] = ia; s_part[1][wid] = ib; }
+  __syncthreads();
+  int64_t wa = 0, wb = 0;
+  for (int w = 0; w < wid; ++w) { wa += s_part[0][w]; wb += s_part[1][w]; }
+  int64_t ra = wa + ia - a, rb = wb + ib - b;    // exclusive prefix for c0
+  for (int c = c0; c < c1; ++c) {
+    cluster_start[c] = ra;
+    seg_start[c] = rb;
+    ra += tot[c];
+    rb += tot[k + c];
+  }
+  if (c1 == k && c0 < k) { cluster_start[k] = ra; seg_start[k] = rb; }
+  if (k == 0 && threadIdx.x == 0) { cluster_start[0] = 0; seg_start[0] = 0; }
+}
+
+__global__ void __launch_bounds__(256)
+kmeans_scatter_kernel(const int* __restrict__ assign, int64_t n, int64_t rpc, int k,
+                      const int* __restrict__ block_offsets, const int64_t* __restrict__ cluster_start,
+                      int* __restrict__ perm) {
+  extern __shared__ int cursor[];
+  for (int c = threadIdx.x; c < k; c += blockDim.x)
+    cursor[c] = (int)(cluster_start[c] + block_offsets[(int64_t)blockIdx.x * k + c]);
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rpc, r1 = min(n, r0 + rpc);
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+    const int pos = atomicAdd(&cursor[assign[r]], 1);
+    perm[pos] = (int)r;
+  }
+}
+
+template <typename T, int DP, int NW>
+__global__ void __launch_bounds__(NW * 64)
+kmeans_segsum_kernel(const T* __restrict__ X, int64_t ldx, const int* __restrict__ perm,
+                     const int64_t* __restrict__ cluster_start, const int64_t* __restrict__ seg_start,
+                     int k, int seg, float* __restrict__ S) {
+  constexpr int EPL = DP >= 64 ? DP / 64 : 1;
+  const int lane = threadIdx.x & 63;
+  const int64_t nseg = seg_start[k];
+  const bool lane_on = (DP >= 64) || (lane < DP);
+  for (int64_t sid = (int64_t)blockIdx.x * NW + (threadIdx.x >> 6); sid < nseg;
+       sid += (int64_t)gridDim.x * NW) {
+    // cluster of this segment: last c with seg_start[c] <= sid
+    int lo = 0, hi = k - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (seg_start[mid] <= sid) lo = mid; else hi = mid - 1;
+    }
+    const int c = lo;
+    const int64_t r0 = cluster_start[c] + (sid - seg_start[c]) * (int64_t)seg;
+    const int64_t r1 = min(cluster_start[c + 1], r0 + seg);
+    float acc[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
+    for (int64_t i = r0; i < r1; i += 8) {
+      // 8 row ids per round: lanes 0..7 load them, broadcast by readlane
+      const int my = (lane < 8 && i + lane < r1) ? perm[i + lane] : -1;
+      float v[8][EPL];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int row = __builtin_amdgcn_readlane(my, u);
+        const T* rp = X + (int64_t)(row < 0 ? 0 : row) * ldx + lane * EPL;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          float x = 0.f;
+          if (lane_on && row >= 0) {
+            if constexpr (sizeof(T) == 2) x = bf16_to_f32(reinterpret_cast<const uint16_t*>(rp)[e]);
+            else x = reinterpret_cast<const float*>(rp)[e];
+          }
+          v[u][e] = x;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) acc[e] += v[u][e];
+    }
+    if (lane_on) {
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) atomicAdd(&S[(int64_t)c * DP + lane * EPL + e], acc[e]);
+    }
+  }
+}
+
 }  // namespace dalgo
 
 using namespace dalgo;
@@ -405,7 +539,54 @@ static hipError_t launch_acc(int DP, const void* X, int64_t n, int64_t ldx, cons
   }
 }
 
+template <typename T, int DP>
+static hipError_t launch_segsum_dp(const void* X, int64_t ldx, const int* perm, const int64_t* cs,
+                                   const int64_t* ss, int k, int seg, int64_t max_segs, float* S,
+                                   hipStream_t st) {
+  constexpr int NW = 4;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(max_segs, NW), 256 * 16));
+  hipLaunchKernelGGL((kmeans_segsum_kernel<T, DP, NW>), dim3(grid), dim3(NW * 64), 0, st,
+                     (const T*)X, ldx, perm, cs, ss, k, seg, S);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+template <typename T>
+static hipError_t launch_segsum(int DP, const void* X, int64_t ldx, const int* perm,
+                                const int64_t* cs, const int64_t* ss, int k, int seg,
+                                int64_t max_segs, float* S, hipStream_t st) {
+  switch (DP) {
+    case 16: return launch_segsum_dp<T, 16>(X, ldx, perm, cs, ss, k, seg, max_segs, S, st);
+    case 32: return launch_segsum_dp<T, 32>(X, ldx, perm, cs, ss, k, seg, max_segs, S, st);
+    case 64: return launch_segsum_dp<T, 64>(X, ldx, perm, cs, ss, k, seg, max_segs, S, st);
+    case 128: return launch_segsum_dp<T, 128>(X, ldx, perm, cs, ss, k, seg, max_segs, S, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 extern "C" {
+
+// Sort-based K3. Workspace: block_counts int32[B*k], cluster_start/seg_start
+// int64[k+1], perm int32[n]. B = number of row chunks (any >= 1).
+hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
+                                          const int* assign, int k, int B, int seg, int* block_counts,
+                                          int64_t* cluster_start, int64_t* seg_start, int* perm,
+                                          float* S, unsigned long long* cnt, hipStream_t st) {
+  if (k < 1 || k > 16384 || B < 1 || seg < 1 || n >= (int64_t)0x7fffffff) return hipErrorInvalidValue;
+  const int64_t rpc = cdiv(std::max<int64_t>(n, 1), B);
+  const size_t lds_k = (size_t)k * sizeof(int);
+  hipLaunchKernelGGL(kmeans_hist_kernel, dim3(B), dim3(256), lds_k, st, assign, n, rpc, k, block_counts);
+  DALGO_LAUNCH_CHECK();
+  hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), 2 * (size_t)k * sizeof(int64_t), st,
+                     block_counts, B, k, seg, cluster_start, seg_start, cnt);
+  DALGO_LAUNCH_CHECK();
+  hipLaunchKernelGGL(kmeans_scatter_kernel, dim3(B), dim3(256), lds_k, st, assign, n, rpc, k,
+                     (const int*)block_counts, (const int64_t*)cluster_start, perm);
+  DALGO_LAUNCH_CHECK();
+  const int64_t max_segs = cdiv(n, seg) + k;
+  return is_bf16 ? launch_segsum<uint16_t>(DP, X, ldx, perm, cluster_start, seg_start, k, seg, max_segs, S, st)
+                 : launch_segsum<float>(DP, X, ldx, perm, cluster_start, seg_start, k, seg, max_segs, S, st);
+}
 
 hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
                                const void* Cq, const float* hn, int kpad, int* assign, float* mind,

@@ -45,6 +45,10 @@ hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ld
 hipError_t dalgo_kmeans_accumulate(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
                                    const int* assign, int k, float* S, unsigned long long* cnt,
                                    hipStream_t st);
+hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
+                                          const int* assign, int k, int B, int seg, int* block_counts,
+                                          int64_t* cluster_start, int64_t* seg_start, int* perm,
+                                          float* S, unsigned long long* cnt, hipStream_t st);
 hipError_t dalgo_kmeans_update(float* C, const float* S, const unsigned long long* cnt, int k,
                                int d, int DP, void* Cq, int is_bf16, float* hn, int kpad,
                                float* shift2, hipStream_t st);

@@ -97,11 +97,40 @@ def assign(X: torch.Tensor, cen: Centers, out: torch.Tensor | None = None,
     return out
 
 
+_ws: dict = {}
+SEG_ROWS = 2048          # rows summed in registers per wave before one atomic flush
+CHUNK_ROWS = 65536       # rows per histogram / scatter block
+
+
+def _sort_ws(device, n, k):
+    B = max(1, min(4096, (n + CHUNK_ROWS - 1) // CHUNK_ROWS))
+    key = (str(device), n, k)
+    ws = _ws.get(key)
+    if ws is None:
+        ws = dict(block_counts=torch.empty(B * k, dtype=torch.int32, device=device),
+                  cluster_start=torch.empty(k + 1, dtype=torch.int64, device=device),
+                  seg_start=torch.empty(k + 1, dtype=torch.int64, device=device),
+                  perm=torch.empty(max(n, 1), dtype=torch.int32, device=device))
+        _ws.clear()
+        _ws[key] = ws
+    return ws
+
+
 def accumulate(X: torch.Tensor, a: torch.Tensor, k: int, DP: int, S: torch.Tensor,
-               cnt: torch.Tensor):
-    """S[c, :] += sum of rows assigned to c (f32, [k, DP]); cnt[c] += count (int64)."""
+               cnt: torch.Tensor, method: str = "sorted"):
+    """S[c, :] += sum of rows assigned to c (f32, [k, DP]); cnt[c] += count (int64).
+
+    method "sorted" (default): counting sort by cluster + per-segment register
+    sums (one atomic d-vector per 2048 rows). "table": range-partitioned LDS
+    accumulation tables (ds_add_f32 per element) — kept for A/B at small k.
+    """
     if X.is_cuda:
-        _ext.ops().kmeans_accumulate(X, a, int(k), int(DP), S, cnt)
+        if method == "table":
+            _ext.ops().kmeans_accumulate(X, a, int(k), int(DP), S, cnt)
+        else:
+            ws = _sort_ws(X.device, X.shape[0], int(k))
+            _ext.ops().kmeans_accumulate_sorted(X, a, int(k), int(DP), SEG_ROWS, ws["block_counts"],
+                                                ws["cluster_start"], ws["seg_start"], ws["perm"], S, cnt)
         return S, cnt
     d = X.shape[1]
     idx = a.long()

@@ -47,8 +47,9 @@ def test_kmeans_ties_lowest_index(cuda):
     assert a.tolist() == [0] * 5
 
 
+@pytest.mark.parametrize("method", ["sorted", "table"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_kmeans_accumulate_update(cuda, dtype):
+def test_kmeans_accumulate_update(cuda, dtype, method):
     n, d, k = 50_000, 100, 70
     g = torch.Generator().manual_seed(1)
     X = torch.randn(n, d, generator=g).to(dtype)
@@ -56,7 +57,7 @@ def test_kmeans_accumulate_update(cuda, dtype):
     DP = K.kmeans_dp(d)
     S = torch.zeros(k, DP, device=cuda)
     cnt = torch.zeros(k, dtype=torch.int64, device=cuda)
-    K.accumulate(K.prepare_points(X.to(cuda)), a.to(cuda), k, DP, S, cnt)
+    K.accumulate(K.prepare_points(X.to(cuda)), a.to(cuda), k, DP, S, cnt, method=method)
     Sr = torch.zeros(k, DP, dtype=torch.float64)
     Sr[:, :d].index_add_(0, a.long(), X.double())
     cr = torch.bincount(a.long(), minlength=k)
