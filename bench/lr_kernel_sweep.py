@@ -68,8 +68,8 @@ def main():
             mult = 2 if name == "copy" else 1
             print(json.dumps({"ref": name, "GBps": nbytes * mult / dt / 1e9, "ms": dt * 1e3}))
         del buf
-        for grid in (1024, 2048, 4096, 8192):
-            for unroll in (4, 8):
+        for grid in (256, 512, 1024, 2048, 4096, 8192):
+            for unroll in (8, -4, -8):
                 o = torch.zeros(grid, dtype=torch.int32, device=dev)
                 torch.ops.dalgo.hbm_read(X, o, unroll); torch.cuda.synchronize()
                 t0 = time.perf_counter()

@@ -456,9 +456,9 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("lr_grad(Tensor X, Tensor y, Tensor W, Tensor seg, int row_offset, int D, bool has_bias, "
         "float eps, int seed, int step, float frac, int gx, int rows_per_block, Tensor(a!) slab, "
         "Tensor(b!) gslab, Tensor(c!) cnt1, Tensor(d!) cnt2, Tensor(e!) G, Tensor(f!) C, "
-        "int variant=3) -> ()");
+        "int variant=6) -> ()");
   m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
-        "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=3) -> ()");
+        "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=6) -> ()");
   m.def("sync_update(Tensor(a!) W, Tensor? G, Tensor? C, Tensor? center, Tensor? S, "
         "Tensor(b!)? Dl, Tensor(c!)? count_acc, int n, int mode, int reg, float eta, float lam, float alpha, "
         "float reg_alpha, float mu, float zeta, float beta, float inv_p) -> ()");

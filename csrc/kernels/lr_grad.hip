@@ -71,13 +71,30 @@ __device__ __forceinline__ void unpack<float>(const uint4& v, float (&o)[4]) {
   o[2] = __uint_as_float(v.z); o[3] = __uint_as_float(v.w);
 }
 
-__device__ __forceinline__ void publish_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// Cross-workgroup hand-off without L2 writeback/invalidate (guide §6 G16, sc1
+// form): slab words are stored write-through (agent-scope relaxed atomic store =
+// global_store ... sc1), every storing wave drains vmcnt before the block's
+// ticket add, and the reducer reads every handed-off word with sc1 loads. An
+// agent-scope release/acquire fence here costs a full L2 writeback/invalidate
+// per block, which dominated small launches.
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void acquire_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// sum of column `col` over nrows slab rows (stride S): 16 loads issued back to
+// back per round (indices clamped, not branched, so hipcc keeps them in flight)
+__device__ __forceinline__ float sum_slab_col(const float* src, int nrows, int S, int col) {
+  float s = 0.f;
+  for (int k0 = 0; k0 < nrows; k0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = ld_wt(&src[(int64_t)min(k0 + u, nrows - 1) * S + col]);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += (k0 + u < nrows) ? v[u] : 0.f;
+  }
+  return s;
 }
 
 // A batch of (up to) U selected rows held in VGPRs (U = 4 or 8). With PIPE the
@@ -108,6 +125,7 @@ lr_rows_kernel(LrParams p) {
   // cross-wave reduction buffer
   __shared__ __attribute__((aligned(16))) float s_arena[(RED_FLOATS > RING_INTS) ? RED_FLOATS : RING_INTS];
   __shared__ int s_flag;
+  __shared__ int s_next;   // next unclaimed 256-row group of this block (dynamic balancing)
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -146,6 +164,8 @@ lr_rows_kernel(LrParams p) {
   int* ring = reinterpret_cast<int*>(s_arena) + wid * kRing;
   const int q = lane >> 4;
   uint32_t head = 0, tail = 0;
+  if (threadIdx.x == 0) s_next = NW;   // groups 0..NW-1 are pre-assigned to the waves
+  __syncthreads();
   int64_t gnext = gstart + (int64_t)wid * 256;
 
   // ---- K7: Bernoulli selection of the next 256-row groups, compacted into the ring
@@ -165,7 +185,11 @@ lr_rows_kernel(LrParams p) {
         if (sel) ring[pos & (kRing - 1)] = (int)(gr - p.row_offset - lo);
         tail += (uint32_t)__popcll(m);
       }
-      gnext += (int64_t)NW * 256;
+      // claim the next group dynamically: waves that drew few selected rows
+      // take more groups, so the block's waves finish together
+      int gi = 0;
+      if (lane == 0) gi = atomicAdd(&s_next, 1);
+      gnext = gstart + (int64_t)__builtin_amdgcn_readfirstlane(gi) * 256;
     }
     __builtin_amdgcn_wave_barrier();
   };
@@ -325,13 +349,13 @@ lr_rows_kernel(LrParams p) {
       float s = 0.f;
 #pragma unroll
       for (int k = 0; k < NW; ++k) s += red_row(k)[col];
-      my[col] = s;
+      st_wt(&my[col], s);
     }
     if (threadIdx.x == 0) {
       float sb = 0.f, sc = 0.f;
       for (int k = 0; k < NW; ++k) { sb += red_row(k)[COLS]; sc += red_row(k)[COLS + 1]; }
-      my[D] = sb;       // bias grad slot
-      my[D + 1] = sc;   // count slot
+      st_wt(&my[D], sb);       // bias grad slot
+      st_wt(&my[D + 1], sc);   // count slot
     }
     // ---- level 1: last arriver of each 16-block group sums the group's slabs
     const int ngroups = (gx + kGroup - 1) / kGroup;
@@ -340,45 +364,38 @@ lr_rows_kernel(LrParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      publish_fence();
       unsigned t = __hip_atomic_fetch_add(&p.cnt1[seg * ngroups + grp], 1u, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
       s_flag = (t == (unsigned)(gsize - 1));
     }
     __syncthreads();
     if (!s_flag) return;
-    if (threadIdx.x == 0) acquire_fence();
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: keep loads below
     const int nv = D + 2;
     {
       const float* src = p.slab + ((int64_t)seg * gx + grp * kGroup) * S;
       float* dst = p.gslab + ((int64_t)seg * ngroups + grp) * S;
       for (int col = threadIdx.x; col < nv; col += NW * 64) {
-        float s = 0.f;
-        for (int k = 0; k < gsize; ++k) s += src[(int64_t)k * S + col];
-        dst[col] = s;
+        st_wt(&dst[col], sum_slab_col(src, gsize, S, col));
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
       p.cnt1[seg * ngroups + grp] = 0u;   // re-arm for the next launch
-      publish_fence();
       unsigned t = __hip_atomic_fetch_add(&p.cnt2[seg], 1u, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
       s_flag = (t == (unsigned)(ngroups - 1));
     }
     __syncthreads();
     if (!s_flag) return;
-    if (threadIdx.x == 0) acquire_fence();
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // ---- level 2: sum group slabs in order -> G[seg], C[seg]
     {
       const float* src = p.gslab + (int64_t)seg * ngroups * S;
       float* Gs = p.G + (int64_t)seg * p.ldw;
       for (int col = threadIdx.x; col < nv; col += NW * 64) {
-        float s = 0.f;
-        for (int k = 0; k < ngroups; ++k) s += src[(int64_t)k * S + col];
+        const float s = sum_slab_col(src, ngroups, S, col);
         if (col < D) Gs[col] = s;
         else if (col == D) { if (p.has_bias) Gs[D] = s; }
         else p.C[seg] = s;
@@ -400,21 +417,28 @@ static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st)
   return hipSuccess;
 }
 
-// variant bits: bit0 = pipelined sweep (two register sets), bit1 = 8 waves per
-// block (else 4), bit2 = 8-row batches (else 4; not combined with bit0)
+// variants (launch shape x sweep structure), A/B-tested in bench/lr_kernel_sweep.py:
+//   0: 4 waves, single set, 4-row batches   1: 4 waves, pipelined (2 sets)
+//   2: 8 waves, single set                  3: 8 waves, pipelined
+//   4: 4 waves, 8-row batches               5: 8 waves, 8-row batches
+//   6: 12 waves, pipelined (3 waves/SIMD)   7: 16 waves, single set (4 waves/SIMD)
 template <typename T, int NC, bool EVAL>
 static hipError_t launch_variant(const LrParams& p, int gx, int nseg, int variant, hipStream_t st) {
   if constexpr (NC >= 4) {   // register budget: one 4-row set at 4 chunks/lane
-    return (variant & 2) ? launch_lr<T, NC, EVAL, 8, false, 4>(p, gx, nseg, st)
-                         : launch_lr<T, NC, EVAL, 4, false, 4>(p, gx, nseg, st);
+    return (variant == 2 || variant == 3 || variant == 5)
+               ? launch_lr<T, NC, EVAL, 8, false, 4>(p, gx, nseg, st)
+               : launch_lr<T, NC, EVAL, 4, false, 4>(p, gx, nseg, st);
   } else {
-    switch (variant & 7) {
+    switch (variant) {
       case 0: return launch_lr<T, NC, EVAL, 4, false, 4>(p, gx, nseg, st);
       case 1: return launch_lr<T, NC, EVAL, 4, true, 4>(p, gx, nseg, st);
       case 2: return launch_lr<T, NC, EVAL, 8, false, 4>(p, gx, nseg, st);
       case 3: return launch_lr<T, NC, EVAL, 8, true, 4>(p, gx, nseg, st);
-      case 4: case 5: return launch_lr<T, NC, EVAL, 4, false, 8>(p, gx, nseg, st);
-      default: return launch_lr<T, NC, EVAL, 8, false, 8>(p, gx, nseg, st);
+      case 4: return launch_lr<T, NC, EVAL, 4, false, 8>(p, gx, nseg, st);
+      case 5: return launch_lr<T, NC, EVAL, 8, false, 8>(p, gx, nseg, st);
+      case 6: return launch_lr<T, NC, EVAL, 12, true, 4>(p, gx, nseg, st);
+      case 7: return launch_lr<T, NC, EVAL, 16, false, 4>(p, gx, nseg, st);
+      default: return hipErrorInvalidValue;
     }
   }
 }

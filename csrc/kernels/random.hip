@@ -91,6 +91,27 @@ hbm_read_kernel(const uint4* __restrict__ p, int64_t n16, uint32_t* __restrict__
   if (threadIdx.x == 0) out[blockIdx.x] = acc;
 }
 
+// Probe variant: block b streams its own contiguous region [b*n/G, (b+1)*n/G)
+// (the access shape of a row-sharded sweep), UNROLL x 16 B in flight per lane.
+template <int UNROLL>
+__global__ void __launch_bounds__(256)
+hbm_read_blocked_kernel(const uint4* __restrict__ p, int64_t n16, uint32_t* __restrict__ out) {
+  const int64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(n16, lo + per);
+  uint32_t acc = 0;
+  int64_t i = lo + threadIdx.x;
+  for (; i + (UNROLL - 1) * 256 < hi; i += UNROLL * 256) {
+    uint4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) v[u] = p[i + u * 256];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  for (; i < hi; i += 256) { uint4 v = p[i]; acc ^= v.x ^ v.y ^ v.z ^ v.w; }
+  acc = wave_sum_u32(acc);
+  if (threadIdx.x == 0) out[blockIdx.x] = acc;
+}
+
 }  // namespace dalgo
 
 using namespace dalgo;
@@ -127,6 +148,14 @@ hipError_t dalgo_mc_pi(uint64_t seed, uint64_t stream, uint64_t offset, uint64_t
 hipError_t dalgo_hbm_read(const void* p, int64_t nbytes, uint32_t* out, int grid, int unroll,
                           hipStream_t st) {
   const int64_t n16 = nbytes / 16;
+  if (unroll < 0) {   // blocked-region variant
+    if (unroll <= -8)
+      hipLaunchKernelGGL(hbm_read_blocked_kernel<8>, dim3(grid), dim3(256), 0, st, (const uint4*)p, n16, out);
+    else
+      hipLaunchKernelGGL(hbm_read_blocked_kernel<4>, dim3(grid), dim3(256), 0, st, (const uint4*)p, n16, out);
+    DALGO_LAUNCH_CHECK();
+    return hipSuccess;
+  }
   if (unroll >= 8)
     hipLaunchKernelGGL(hbm_read_kernel<8>, dim3(grid), dim3(256), 0, st, (const uint4*)p, n16, out);
   else

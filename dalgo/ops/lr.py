@@ -26,9 +26,9 @@ from dalgo.utils import philox
 import os
 
 # Launch shape of the row-streaming kernels (tuned on MI355X, see profiles/):
-#   LR_VARIANT bit0 = software-pipelined sweep, bit1 = 8-wave blocks (else 4)
+#   LR_VARIANT      = launch-shape variant (table in csrc/kernels/lr_grad.hip)
 #   TARGET_BLOCKS   = workgroups per launch (split over segments)
-LR_VARIANT = int(os.environ.get("DALGO_LR_VARIANT", "2"))
+LR_VARIANT = int(os.environ.get("DALGO_LR_VARIANT", "6"))
 _TARGET_BLOCKS = int(os.environ.get("DALGO_LR_BLOCKS", "256"))
 
 
