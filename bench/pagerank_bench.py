@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--semantics", default="reference")
+    ap.add_argument("--no-reorder", action="store_true", help="keep scrambled R-MAT vertex ids")
     a = ap.parse_args()
     from dalgo.apps.pagerank_app import rmat_shard
     from dalgo.models.pagerank import PageRank, PageRankConfig
@@ -31,7 +32,7 @@ def main():
     rt = runtime.init(device="cuda")
     W = rt.world_size
     t0 = time.time()
-    shard, n_gen = rmat_shard(a.scale, a.edge_factor, rt.rank, W, rt.device)
+    shard, n_gen = rmat_shard(a.scale, a.edge_factor, rt.rank, W, rt.device, reorder=not a.no_reorder)
     torch.cuda.synchronize()
     build_s = time.time() - t0
     E = comm.all_reduce_count(shard.n_edges, device=rt.device)
@@ -62,7 +63,7 @@ def main():
         print(json.dumps({
             "metric": "PageRank edges/sec (whole node)", "value": E / (ms / 1e3), "unit": "edges/s",
             "n_gpus": W, "ms_per_iter": ms, "edges_dedup": E, "edges_generated": n_gen,
-            "vertices": 1 << a.scale, "phases_ms_rank0": phases, "graph_build_s": build_s,
+            "vertices": 1 << a.scale, "degree_reordered": not a.no_reorder, "phases_ms_rank0": phases, "graph_build_s": build_s,
             "spmv_GBps_stream": shard.n_edges * 8 / (phases["spmv"] / 1e3) / 1e9}), flush=True)
     runtime.shutdown()
 

@@ -84,6 +84,7 @@ class GraphShard:
     v_hi: int
     n_vertices: int        # global vertex-id space size
     slice_size: int        # vertices per rank slice (padded, for all_gather)
+    new_id: torch.Tensor | None = None   # old -> new vertex id (degree reordering), if any
 
     @property
     def n_local(self) -> int:
