@@ -248,7 +248,8 @@ void check_points(const Tensor& X, int DP) {
 }
 
 void kmeans_assign(const Tensor& X, const Tensor& Cq, const Tensor& hn, Tensor assign,
-                   const std::optional<Tensor>& mind, const std::optional<Tensor>& sse) {
+                   const std::optional<Tensor>& mind, const std::optional<Tensor>& sse,
+                   int64_t variant) {
   TORCH_CHECK(Cq.dim() == 2, "Cq [kpad, DP]");
   const int DP = (int)Cq.size(1);
   TORCH_CHECK(kmeans_dp(DP) == DP, "Cq columns must be 16/32/64/128");
@@ -276,7 +277,8 @@ void kmeans_assign(const Tensor& X, const Tensor& Cq, const Tensor& hn, Tensor a
   DeviceGuard guard(X.device());
   DALGO_CHECK_HIP(dalgo_kmeans_assign(X.data_ptr(), X.scalar_type() == at::kBFloat16, X.size(0),
                                       X.stride(0), DP, Cq.data_ptr(), hn.data_ptr<float>(),
-                                      (int)kpad, assign.data_ptr<int>(), md, ss, cur_stream()),
+                                      (int)kpad, assign.data_ptr<int>(), md, ss, (int)variant,
+                                      cur_stream()),
                   "kmeans_assign");
 }
 
@@ -467,7 +469,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("philox_fill(Tensor(a!) out, int D, int row_offset, int seed, int stream, int dist, "
         "float a, float b) -> ()");
   m.def("kmeans_assign(Tensor X, Tensor Cq, Tensor hn, Tensor(a!) assign, Tensor(b!)? mind, "
-        "Tensor(c!)? sse) -> ()");
+        "Tensor(c!)? sse, int variant=5) -> ()");
   m.def("kmeans_accumulate(Tensor X, Tensor assign, int k, int DP, Tensor(a!) S, Tensor(b!) cnt) -> ()");
   m.def("kmeans_accumulate_sorted(Tensor X, Tensor assign, int k, int DP, int seg, "
         "Tensor(a!) block_counts, Tensor(b!) cluster_start, Tensor(c!) seg_start, Tensor(d!) perm, "

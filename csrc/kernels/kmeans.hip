@@ -75,17 +75,21 @@ __device__ __forceinline__ float sq_sum(const uint4& v, float) {
 
 // X: [n, ldx] (columns [d, DP) must be zero), Cq: [kpad, DP] (rows >= k zero),
 // hn: [kpad] = 0.5|c|^2 (1e30 for padding centres).
-template <typename T, int DP, int PT, int NW>
-__global__ void __launch_bounds__(NW * 64)
+// NSUB 32-centre sub-tiles are staged per barrier (chunk = 32*NSUB centres);
+// kpad must be a multiple of 32*NSUB.
+template <typename T, int DP, int PT, int NW, int NSUB, int MINW>
+__global__ void __launch_bounds__(NW * 64, MINW)
 kmeans_assign_kernel(const T* __restrict__ X, int64_t n, int64_t ldx, const T* __restrict__ Cq,
                      const float* __restrict__ hn, int kpad, int* __restrict__ assign,
                      float* __restrict__ mind, double* __restrict__ sse) {
   using G = KGeom<T, DP>;
   constexpr int NT = NW * 64;
-  constexpr int NPIECE = G::CHUNKB / 16;
+  constexpr int CH = 32 * NSUB;
+  constexpr int CHUNKB = NSUB * G::CHUNKB;
+  constexpr int NPIECE = CHUNKB / 16;
   constexpr int PER_T = (NPIECE + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) unsigned char s_c[2][G::CHUNKB];
-  __shared__ __attribute__((aligned(16))) float s_hn[2][32];
+  __shared__ __attribute__((aligned(16))) unsigned char s_c[2][CHUNKB];
+  __shared__ __attribute__((aligned(16))) float s_hn[2][CH];
   __shared__ double s_sse[NW];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, cl = lane & 31;
@@ -114,7 +118,7 @@ kmeans_assign_kernel(const T* __restrict__ X, int64_t n, int64_t ldx, const T* _
 #pragma unroll
   for (int t = 0; t < PT; ++t) { best[t] = -3.0e38f; bidx[t] = 0; }
 
-  const int nchunk = kpad / 32;
+  const int nchunk = kpad / CH;
   const unsigned char* Cb = reinterpret_cast<const unsigned char*>(Cq);
   uint4 stg[PER_T];
   float stg_h = 0.f;
@@ -123,20 +127,20 @@ kmeans_assign_kernel(const T* __restrict__ X, int64_t n, int64_t ldx, const T* _
     for (int i = 0; i < PER_T; ++i) {
       const int piece = tid + i * NT;
       if (piece < NPIECE)
-        stg[i] = *reinterpret_cast<const uint4*>(Cb + (int64_t)ch * G::CHUNKB + piece * 16);
+        stg[i] = *reinterpret_cast<const uint4*>(Cb + (int64_t)ch * CHUNKB + piece * 16);
     }
-    if (tid < 32) stg_h = hn[ch * 32 + tid];
+    if (tid < CH) stg_h = hn[ch * CH + tid];
   };
   auto stage_store = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < PER_T; ++i) {
       const int piece = tid + i * NT;
       if (piece < NPIECE) {
-        const int cc = piece / G::NJ, j = piece % G::NJ;
+        const int cc = piece / G::NJ, j = piece % G::NJ;   // centre within chunk (row-major: sub-tiles contiguous)
         *reinterpret_cast<uint4*>(&s_c[buf][cc * G::ROWB + ((j ^ (cc & G::SWZ)) << 4)]) = stg[i];
       }
     }
-    if (tid < 32) s_hn[buf][tid] = stg_h;
+    if (tid < CH) s_hn[buf][tid] = stg_h;
   };
 
   stage_load(0);
@@ -145,38 +149,43 @@ kmeans_assign_kernel(const T* __restrict__ X, int64_t n, int64_t ldx, const T* _
   for (int ch = 0; ch < nchunk; ++ch) {
     const int buf = ch & 1;
     if (ch + 1 < nchunk) stage_load(ch + 1);   // in flight under the MFMAs
-    // accumulator init = -0.5|c|^2 of the centre each register holds
-    f32x16 acc[PT];
-    {
-      float4 h4[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) h4[g] = *reinterpret_cast<const float4*>(&s_hn[buf][8 * g + 4 * h]);
+    for (int sub = 0; sub < NSUB; ++sub) {
+      // accumulator init = -0.5|c|^2 of the centre each register holds
+      f32x16 acc[PT];
+      {
+        float4 h4[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          h4[g] = *reinterpret_cast<const float4*>(&s_hn[buf][32 * sub + 8 * g + 4 * h]);
+#pragma unroll
+        for (int t = 0; t < PT; ++t) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            acc[t][4 * g + 0] = -h4[g].x; acc[t][4 * g + 1] = -h4[g].y;
+            acc[t][4 * g + 2] = -h4[g].z; acc[t][4 * g + 3] = -h4[g].w;
+          }
+        }
+      }
+      const unsigned char* sub_base = &s_c[buf][sub * G::CHUNKB];
+#pragma unroll
+      for (int s = 0; s < G::NLOAD; ++s) {
+        const int j = 2 * s + h;
+        const uint4 a = *reinterpret_cast<const uint4*>(&sub_base[cl * G::ROWB + ((j ^ (cl & G::SWZ)) << 4)]);
+#pragma unroll
+        for (int t = 0; t < PT; ++t) acc[t] = mfma_step(a, bf[t][s], acc[t], T{});
+      }
+      // running argmax over this lane's 16 centres, ascending centre order
 #pragma unroll
       for (int t = 0; t < PT; ++t) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          acc[t][4 * g + 0] = -h4[g].x; acc[t][4 * g + 1] = -h4[g].y;
-          acc[t][4 * g + 2] = -h4[g].z; acc[t][4 * g + 3] = -h4[g].w;
+        for (int r = 0; r < 16; ++r) {
+          const int c = ch * CH + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const float v = acc[t][r];
+          const bool take = v > best[t];
+          best[t] = take ? v : best[t];
+          bidx[t] = take ? c : bidx[t];
         }
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < G::NLOAD; ++s) {
-      const int j = 2 * s + h;
-      const uint4 a = *reinterpret_cast<const uint4*>(&s_c[buf][cl * G::ROWB + ((j ^ (cl & G::SWZ)) << 4)]);
-#pragma unroll
-      for (int t = 0; t < PT; ++t) acc[t] = mfma_step(a, bf[t][s], acc[t], T{});
-    }
-    // running argmax over this lane's 16 centres, ascending centre order
-#pragma unroll
-    for (int t = 0; t < PT; ++t) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int c = ch * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float v = acc[t][r];
-        const bool take = v > best[t];
-        best[t] = take ? v : best[t];
-        bidx[t] = take ? c : bidx[t];
       }
     }
     if (ch + 1 < nchunk) {
@@ -447,28 +456,31 @@ kmeans_segsum_kernel(const T* __restrict__ X, int64_t ldx, const int* __restrict
     float acc[EPL];
 #pragma unroll
     for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
-    for (int64_t i = r0; i < r1; i += 8) {
-      // 8 row ids per round: lanes 0..7 load them, broadcast by readlane
-      const int my = (lane < 8 && i + lane < r1) ? perm[i + lane] : -1;
-      float v[8][EPL];
+    // 64 row ids per coalesced load (next block prefetched), 16 rows in flight
+    int idx = (r0 + lane < r1) ? perm[r0 + lane] : -1;
+    for (int64_t i = r0; i < r1; i += 64) {
+      const int nxt = (i + 64 + lane < r1) ? perm[i + 64 + lane] : -1;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int row = __builtin_amdgcn_readlane(my, u);
-        const T* rp = X + (int64_t)(row < 0 ? 0 : row) * ldx + lane * EPL;
+      for (int u0 = 0; u0 < 64; u0 += 16) {
+        float v[16][EPL];
 #pragma unroll
-        for (int e = 0; e < EPL; ++e) {
-          float x = 0.f;
-          if (lane_on && row >= 0) {
+        for (int u = 0; u < 16; ++u) {
+          const int row = __builtin_amdgcn_readlane(idx, u0 + u);
+          const T* rp = X + (int64_t)(row < 0 ? 0 : row) * ldx + lane * EPL;
+#pragma unroll
+          for (int e = 0; e < EPL; ++e) {
+            float x = 0.f;
             if constexpr (sizeof(T) == 2) x = bf16_to_f32(reinterpret_cast<const uint16_t*>(rp)[e]);
             else x = reinterpret_cast<const float*>(rp)[e];
+            v[u][e] = (lane_on && row >= 0) ? x : 0.f;
           }
-          v[u][e] = x;
         }
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+#pragma unroll
+          for (int e = 0; e < EPL; ++e) acc[e] += v[u][e];
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-#pragma unroll
-        for (int e = 0; e < EPL; ++e) acc[e] += v[u][e];
+      idx = nxt;
     }
     if (lane_on) {
 #pragma unroll
@@ -481,31 +493,58 @@ kmeans_segsum_kernel(const T* __restrict__ X, int64_t ldx, const int* __restrict
 
 using namespace dalgo;
 
-template <typename T, int DP>
-static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const void* Cq,
-                                   const float* hn, int kpad, int* assign, float* mind, double* sse,
-                                   hipStream_t st) {
-  constexpr int PT = sizeof(T) == 2 ? 2 : 1;
-  constexpr int NW = 8;
+template <typename T, int DP, int NW, int NSUB, int PTB = 2, int MINW = 1>
+static hipError_t launch_assign_v(const void* X, int64_t n, int64_t ldx, const void* Cq,
+                                  const float* hn, int kpad, int* assign, float* mind, double* sse,
+                                  hipStream_t st) {
+  constexpr int PT = sizeof(T) == 2 ? PTB : 1;
+  if (kpad % (32 * NSUB)) return hipErrorInvalidValue;
   const int64_t per_block = NW * PT * 32;
   const int64_t grid = cdiv(n, per_block);
   if (grid == 0) return hipSuccess;
   if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((kmeans_assign_kernel<T, DP, PT, NW>), dim3((unsigned)grid), dim3(NW * 64), 0,
-                     st, (const T*)X, n, ldx, (const T*)Cq, hn, kpad, assign, mind, sse);
+  hipLaunchKernelGGL((kmeans_assign_kernel<T, DP, PT, NW, NSUB, MINW>), dim3((unsigned)grid),
+                     dim3(NW * 64), 0, st, (const T*)X, n, ldx, (const T*)Cq, hn, kpad, assign,
+                     mind, sse);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
+}
+
+// variant: 0 = 8 waves x 32-centre chunks, 1 = 4 waves x 32, 2 = 4 waves x 128,
+//          3 = 8 waves x 128, 4 = 4 waves x 64, 5 = variant 0 capped at 128 VGPRs
+//          (4 waves/SIMD: two 8-wave blocks per CU), 6 = 4 waves x 4 point tiles (128
+//          points per wave), 7 = 8 waves x 4 point tiles, 8 = 4 waves capped at 128
+//          VGPRs (four blocks per CU), 9 = variant 5 with 64-centre chunks,
+//          10 = 16 waves (1024 points per block) capped at 128 VGPRs
+template <typename T, int DP>
+static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const void* Cq,
+                                   const float* hn, int kpad, int* assign, float* mind, double* sse,
+                                   int variant, hipStream_t st) {
+  switch (variant) {
+    case 0: return launch_assign_v<T, DP, 8, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 1: return launch_assign_v<T, DP, 4, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 2: return launch_assign_v<T, DP, 4, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 3: return launch_assign_v<T, DP, 8, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 4: return launch_assign_v<T, DP, 4, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 5: return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 6: return launch_assign_v<T, DP, 4, 1, 4, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 7: return launch_assign_v<T, DP, 8, 1, 4, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 8: return launch_assign_v<T, DP, 4, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 9: return launch_assign_v<T, DP, 8, 2, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 10: return launch_assign_v<T, DP, 16, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 template <typename T>
 static hipError_t launch_assign(int DP, const void* X, int64_t n, int64_t ldx, const void* Cq,
                                 const float* hn, int kpad, int* assign, float* mind, double* sse,
-                                hipStream_t st) {
+                                int variant, hipStream_t st) {
   switch (DP) {
-    case 16: return launch_assign_dp<T, 16>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 32: return launch_assign_dp<T, 32>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 64: return launch_assign_dp<T, 64>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 128: return launch_assign_dp<T, 128>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 16: return launch_assign_dp<T, 16>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, variant, st);
+    case 32: return launch_assign_dp<T, 32>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, variant, st);
+    case 64: return launch_assign_dp<T, 64>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, variant, st);
+    case 128: return launch_assign_dp<T, 128>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, variant, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -590,10 +629,10 @@ hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n,
 
 hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
                                const void* Cq, const float* hn, int kpad, int* assign, float* mind,
-                               double* sse, hipStream_t st) {
+                               double* sse, int variant, hipStream_t st) {
   if (kpad % 32 != 0) return hipErrorInvalidValue;
-  return is_bf16 ? launch_assign<uint16_t>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, st)
-                 : launch_assign<float>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+  return is_bf16 ? launch_assign<uint16_t>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, variant, st)
+                 : launch_assign<float>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, variant, st);
 }
 
 hipError_t dalgo_kmeans_accumulate(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,

@@ -55,7 +55,7 @@ class Centers:
 def make_centers(C0: torch.Tensor, dtype: torch.dtype, device) -> Centers:
     k, d = C0.shape
     DP = kmeans_dp(d)
-    kpad = ((k + 31) // 32) * 32
+    kpad = ((k + 127) // 128) * 128     # multiple of every chunk width of the assign kernel
     C = C0.to(device=device, dtype=torch.float32).contiguous()
     Cq = torch.zeros((kpad, DP), dtype=dtype, device=device)
     hn = torch.zeros(kpad, dtype=torch.float32, device=device)
@@ -74,14 +74,23 @@ def refresh(cen: Centers):
     cen.hn[: cen.k] = 0.5 * (r * r).sum(dim=1)
 
 
+import os
+
+# launch variant of the assign kernel (table in csrc/kernels/kmeans.hip); 5 = 8-wave
+# blocks capped at 128 VGPRs so two blocks share a CU (measured best on MI355X)
+ASSIGN_VARIANT = int(os.environ.get("DALGO_KM_VARIANT", "5"))
+
+
 def assign(X: torch.Tensor, cen: Centers, out: torch.Tensor | None = None,
-           mind: torch.Tensor | None = None, sse: torch.Tensor | None = None):
+           mind: torch.Tensor | None = None, sse: torch.Tensor | None = None,
+           variant: int | None = None):
     """Nearest-centre ids (int32, ties -> lowest id), squared distances, SSE."""
     n = X.shape[0]
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=X.device)
     if X.is_cuda:
-        _ext.ops().kmeans_assign(X, cen.Cq, cen.hn, out, mind, sse)
+        _ext.ops().kmeans_assign(X, cen.Cq, cen.hn, out, mind, sse,
+                                 ASSIGN_VARIANT if variant is None else int(variant))
         return out
     # CPU reference: exact scores on the ROUNDED centres, f64, first maximum wins
     Xf = X[:, : cen.d].double()
