@@ -40,6 +40,8 @@ def parse(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--backend", default=None, choices=["nccl", "gloo"],
+                    help="collective backend (default: nccl = RCCL on GPU, gloo on CPU)")
     ap.add_argument("--eval", action="store_true", help="report held-out accuracy after timing")
     return ap.parse_args(argv)
 
@@ -52,7 +54,7 @@ def main(argv=None):
     from dalgo.parallel import comm, runtime
     from dalgo.parallel.sharding import make_layout
 
-    rt = runtime.init(device=a.device, app_name="bench-ssgd")
+    rt = runtime.init(backend=a.backend, device=a.device, app_name="bench-ssgd")
     W = rt.world_size
     if a.gpus != W and rt.is_main:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={W}; using {W}", file=sys.stderr)

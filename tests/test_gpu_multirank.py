@@ -1,0 +1,55 @@
+"""Multi-rank GPU rehearsal on ONE device: 2 ranks share cuda:0 over gloo.
+
+RCCL refuses two ranks on one GPU, so this exercises everything of the N-GPU path
+except the transport: sharded on-device data, HIP kernels per rank, collectives on
+GPU tensors, rank-0 reporting and the bench JSON contract.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _torchrun(args, n=2, timeout=600):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-5000:]
+    return r.stdout
+
+
+def test_bench_two_ranks_gloo_on_one_gpu(cuda):
+    out = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--rows", "200000",
+                     "--steps", "5", "--warmup", "2"])
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0
+
+
+@pytest.mark.parametrize("script,extra,needle", [
+    ("optimization/bmuf.py", ["--synthetic", "50000,128", "--n-iterations", "5", "--quiet"], "Final acc:"),
+    ("optimization/easgd.py", ["--synthetic", "50000,128", "--n-iterations", "5", "--quiet"], "Final acc:"),
+    ("machine_learning/k-means.py", ["--synthetic", "20000,16", "--k", "8"], "Final centers:"),
+    ("graph_computation/pagerank.py", ["--rmat-scale", "12", "--top", "3"], "has rank:"),
+    ("matrix_computation/matrix_decomposition.py", [], "iterations: 4, rmse:"),
+    ("randomized_algorithm/monte_carlo.py", ["--n", "1000000"], "Pi is roughly"),
+])
+def test_scripts_two_ranks_gloo_on_one_gpu(cuda, script, extra, needle):
+    out = _torchrun([script, "--device", "cuda", "--backend", "gloo", "--no-plot"] + extra)
+    assert needle in out
