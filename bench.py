@@ -38,7 +38,6 @@ def parse(argv=None):
     ap.add_argument("--frac", type=float, default=0.1)
     ap.add_argument("--algo", default="ssgd", choices=["ssgd", "gd", "ma", "bmuf", "easgd"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
-    ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--backend", default=None, choices=["nccl", "gloo"],
                     help="collective backend (default: nccl = RCCL on GPU, gloo on CPU)")
@@ -72,12 +71,6 @@ def main(argv=None):
     count = torch.zeros(1, dtype=torch.float64, device=rt.device)
 
     step_fn = model.step
-    graph = None
-    if a.graph and rt.device.type == "cuda":
-        # warm up on a side stream, then capture one step; replays advance model.t
-        # via the captured sampling stream index, so we capture K distinct steps.
-        pass
-
     for _ in range(a.warmup):
         step_fn()
     rt.synchronize()

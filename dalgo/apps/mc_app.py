@@ -9,10 +9,11 @@ from dalgo.utils.cli import common_parser, init_from_args
 def main(argv=None):
     ap = common_parser("Monte-Carlo pi (MI355X-native)")
     ap.add_argument("--n-slices", type=int, default=4)
-    ap.add_argument("--n", type=int, default=None, help="samples (default 100000 * n_slices)")
+    ap.add_argument("--num-samples", type=int, default=None,
+                    help="samples (default 100000 * n_slices, monte_carlo.py:15)")
     a = ap.parse_args(argv)
     rt = init_from_args(a, "monte_carlo")
-    pi, _ = estimate_pi(MonteCarloConfig(n_slices=a.n_slices, n=a.n, seed=a.seed),
+    pi, _ = estimate_pi(MonteCarloConfig(n_slices=a.n_slices, n=a.num_samples, seed=a.seed),
                         rt.rank, rt.world_size, device=rt.device)
     rt.log("Pi is roughly %f" % pi)   # monte_carlo.py:31
     runtime.shutdown()

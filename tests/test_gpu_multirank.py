@@ -48,7 +48,7 @@ def test_bench_two_ranks_gloo_on_one_gpu(cuda):
     ("machine_learning/k-means.py", ["--synthetic", "20000,16", "--k", "8"], "Final centers:"),
     ("graph_computation/pagerank.py", ["--rmat-scale", "12", "--top", "3"], "has rank:"),
     ("matrix_computation/matrix_decomposition.py", [], "iterations: 4, rmse:"),
-    ("randomized_algorithm/monte_carlo.py", ["--n", "1000000"], "Pi is roughly"),
+    ("randomized_algorithm/monte_carlo.py", ["--num-samples", "1000000"], "Pi is roughly"),
 ])
 def test_scripts_two_ranks_gloo_on_one_gpu(cuda, script, extra, needle):
     out = _torchrun([script, "--device", "cuda", "--backend", "gloo", "--no-plot"] + extra)
