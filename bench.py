@@ -84,12 +84,12 @@ def main(argv=None):
     rt.barrier()
     rt.synchronize()
     elapsed = time.perf_counter() - t_start
+    samples = model.global_sample_count()
     model.count_acc = None
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=rt.device)
     comm.all_reduce_max(el)
     elapsed = float(el.item())
-    samples = float(count.item())
     if cfg.algo not in ("ssgd", "gd"):
         samples = a.rows * a.frac * a.steps * (cfg.n_local if cfg.algo in ("ma", "bmuf") else 1)
     value = samples / elapsed

@@ -75,8 +75,24 @@ void check_lr_inputs(const Tensor& X, const Tensor& y, const Tensor& W, const Te
 void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& seg,
              int64_t row_offset, int64_t D, bool has_bias, double eps, int64_t seed, int64_t step,
              double frac, int64_t gx, int64_t rows_per_block, Tensor slab, Tensor gslab,
-             Tensor cnt1, Tensor cnt2, Tensor G, Tensor C, int64_t variant) {
+             Tensor cnt1, Tensor cnt2, Tensor G, Tensor C, int64_t variant,
+             const std::optional<Tensor>& Wprev, int64_t upd_mode, int64_t upd_reg, double upd_eta,
+             double upd_lam, double upd_reg_alpha, const std::optional<Tensor>& count_acc) {
   check_lr_inputs(X, y, W, seg, D, has_bias);
+  const float* wprev = nullptr;
+  if (Wprev.has_value()) {
+    check_f32(*Wprev, "Wprev");
+    TORCH_CHECK(W.size(0) == 1 && Wprev->numel() >= W.size(1), "fused update: one model, Wprev [1, ldw]");
+    TORCH_CHECK(Wprev->data_ptr() != W.data_ptr(), "fused update: Wprev and W must differ (ping-pong)");
+    TORCH_CHECK(upd_mode == 0 || upd_mode == 1, "fused update mode: 0 SSGD, 1 GD");
+    wprev = Wprev->data_ptr<float>();
+  }
+  double* cacc = nullptr;
+  if (count_acc.has_value()) {
+    check_dev(*count_acc, "count_acc");
+    TORCH_CHECK(count_acc->scalar_type() == at::kDouble, "count_acc f64");
+    cacc = count_acc->data_ptr<double>();
+  }
   const int64_t nseg = W.size(0);
   TORCH_CHECK(gx >= 1 && gx <= 65535, "gx");
   TORCH_CHECK(rows_per_block > 0 && rows_per_block % 256 == 0, "rows_per_block % 256");
@@ -100,7 +116,8 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
                     (int)rows_per_block, slab.data_ptr<float>(), gslab.data_ptr<float>(),
                     reinterpret_cast<unsigned*>(cnt1.data_ptr<int>()),
                     reinterpret_cast<unsigned*>(cnt2.data_ptr<int>()), G.data_ptr<float>(),
-                    C.data_ptr<float>(), (int)S, (int)variant, cur_stream()),
+                    C.data_ptr<float>(), (int)S, (int)variant, wprev, (int)upd_mode, (int)upd_reg,
+                    (float)upd_eta, (float)upd_lam, (float)upd_reg_alpha, cacc, cur_stream()),
       "lr_grad");
 }
 
@@ -455,10 +472,11 @@ void spd_inverse(const Tensor& G, double ridge, Tensor out, const std::optional<
 }  // namespace
 
 TORCH_LIBRARY(dalgo, m) {
-  m.def("lr_grad(Tensor X, Tensor y, Tensor W, Tensor seg, int row_offset, int D, bool has_bias, "
+  m.def("lr_grad(Tensor X, Tensor y, Tensor(z!) W, Tensor seg, int row_offset, int D, bool has_bias, "
         "float eps, int seed, int step, float frac, int gx, int rows_per_block, Tensor(a!) slab, "
         "Tensor(b!) gslab, Tensor(c!) cnt1, Tensor(d!) cnt2, Tensor(e!) G, Tensor(f!) C, "
-        "int variant=6) -> ()");
+        "int variant=6, Tensor? Wprev=None, int upd_mode=0, int upd_reg=0, float upd_eta=0., "
+        "float upd_lam=0., float upd_reg_alpha=0., Tensor(g!)? count_acc=None) -> ()");
   m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
         "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=6) -> ()");
   m.def("sync_update(Tensor(a!) W, Tensor? G, Tensor? C, Tensor? center, Tensor? S, "

@@ -50,7 +50,29 @@ struct LrParams {
   // eval outputs
   unsigned long long* correct;  // [n_seg] (eval mode)
   float* loss;                  // [n_seg] sum of log-loss (eval mode)
+  // fused K8 update of the PREVIOUS step (SSGD / full-batch GD, one segment):
+  // w = upd(Wprev, Gprev, Cprev) is computed by every block for its own register
+  // fragment and written to W by block 0, so a training step is one kernel +
+  // one all-reduce (the separate update launch disappears).
+  const float* Wprev;   // nullptr: no fused update, use W as is
+  const float* Gprev;   // all-reduced gradient sum of the previous step (== G buffer)
+  const float* Cprev;
+  int upd_mode;         // 0 = SSGD (mean + reg), 1 = GD (sum)
+  int upd_reg;          // 0 none, 1 l2, 2 l1, 3 elastic net
+  float upd_eta, upd_lam, upd_reg_alpha;
+  double* count_acc;    // optional: += local selected-row count of THIS step
 };
+
+__device__ __forceinline__ float fused_update(float w, float g, float c, const LrParams& p) {
+  if (p.upd_mode == 1) return w - p.upd_eta * g;
+  const float gm = c > 0.f ? g / c : 0.f;
+  float r = 0.f;
+  if (p.upd_reg == 1) r = w;
+  else if (p.upd_reg == 2) r = (w > 0.f) ? 1.f : (w < 0.f ? -1.f : 0.f);
+  else if (p.upd_reg == 3) r = p.upd_reg_alpha * ((w > 0.f) ? 1.f : (w < 0.f ? -1.f : 0.f)) +
+                               (1.f - p.upd_reg_alpha) * w;
+  return w - p.upd_eta * (gm + p.upd_lam * r);
+}
 
 constexpr int kGroup = 16;   // blocks per first-level reduction group
 
@@ -135,17 +157,41 @@ lr_rows_kernel(LrParams p) {
   const int64_t seg_lo = p.seg[seg], seg_hi = p.seg[seg + 1];
   const int64_t lo = seg_lo + (int64_t)bx * p.rows_per_block;
   const int64_t hi = max(lo, min(seg_hi, lo + (int64_t)p.rows_per_block));
-  // model fragment in registers
-  const float* w = p.W + (int64_t)seg * p.ldw;
+  // model fragment in registers (optionally applying the previous step's update)
   float wr[NC][VEC];
+  float wb;
+  if (p.Wprev == nullptr) {
+    const float* w = p.W + (int64_t)seg * p.ldw;
 #pragma unroll
-  for (int c = 0; c < NC; ++c)
+    for (int c = 0; c < NC; ++c)
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      int col = (c * 64 + lane) * VEC + e;
-      wr[c][e] = (col < p.D) ? w[col] : 0.f;
+      for (int e = 0; e < VEC; ++e) {
+        int col = (c * 64 + lane) * VEC + e;
+        wr[c][e] = (col < p.D) ? w[col] : 0.f;
+      }
+    wb = p.has_bias ? w[p.D] : 0.f;
+  } else {
+    const float cprev = p.Cprev[0];
+    float* wout = const_cast<float*>(p.W);
+    const bool writer = (bx == 0 && wid == 0);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        int col = (c * 64 + lane) * VEC + e;
+        float v = 0.f;
+        if (col < p.D) {
+          v = fused_update(p.Wprev[col], p.Gprev[col], cprev, p);
+          if (writer) wout[col] = v;
+        }
+        wr[c][e] = v;
+      }
+    wb = 0.f;
+    if (p.has_bias) {
+      wb = fused_update(p.Wprev[p.D], p.Gprev[p.D], cprev, p);
+      if (writer && lane == 0) wout[p.D] = wb;
     }
-  const float wb = p.has_bias ? w[p.D] : 0.f;
+  }
 
   float g[NC][VEC];
 #pragma unroll
@@ -398,7 +444,10 @@ lr_rows_kernel(LrParams p) {
         const float s = sum_slab_col(src, ngroups, S, col);
         if (col < D) Gs[col] = s;
         else if (col == D) { if (p.has_bias) Gs[D] = s; }
-        else p.C[seg] = s;
+        else {
+          p.C[seg] = s;
+          if (p.count_acc) p.count_acc[0] += (double)s;
+        }
       }
     }
     if (threadIdx.x == 0) p.cnt2[seg] = 0u;
@@ -476,8 +525,12 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          uint64_t seed, uint64_t step, uint32_t thr, int full, int is_bf16,
                          int gx, int nseg, int rows_per_block, float* slab, float* gslab,
                          unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int variant,
-                         hipStream_t st) {
+                         const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
+                         float upd_reg_alpha, double* count_acc, hipStream_t st) {
   LrParams p{};
+  p.Wprev = Wprev; p.Gprev = G; p.Cprev = C; p.upd_mode = upd_mode; p.upd_reg = upd_reg;
+  p.upd_eta = upd_eta; p.upd_lam = upd_lam; p.upd_reg_alpha = upd_reg_alpha;
+  p.count_acc = count_acc;
   p.X = X; p.y = y; p.W = W; p.seg = seg; p.ld = ld; p.row_offset = row_offset; p.D = D;
   p.ldw = ldw; p.has_bias = has_bias; p.eps = eps; p.seed = seed; p.step = step; p.thr = thr;
   p.full = full; p.rows_per_block = rows_per_block; p.slab = slab; p.gslab = gslab;

@@ -14,7 +14,8 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          uint64_t seed, uint64_t step, uint32_t thr, int full, int is_bf16,
                          int gx, int nseg, int rows_per_block, float* slab, float* gslab,
                          unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int variant,
-                         hipStream_t st);
+                         const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
+                         float upd_reg_alpha, double* count_acc, hipStream_t st);
 hipError_t dalgo_lr_eval(const void* X, const float* y, const float* W, const int64_t* seg,
                          int64_t ld, int D, int ldw, int has_bias, float eps, int is_bf16, int gx,
                          int nseg, int rows_per_block, unsigned long long* correct, float* loss,

@@ -135,8 +135,18 @@ class ParallelSGD:
             if algo == "bmuf":
                 self.Dl = init["delta"].to(model_dtype).to(dev).contiguous()
         self.inv_p = 1.0 / P
-        # optional f64 device accumulator of global minibatch sizes (bench accounting)
+        # optional f64 device accumulator of minibatch sizes (bench accounting);
+        # read it through global_sample_count()
         self.count_acc: torch.Tensor | None = None
+        # SSGD / GD on the GPU: the K8 update is fused into the next step's gradient
+        # kernel (ping-pong model buffers); self._pending = G/C hold an update not
+        # yet applied to self.w (applied lazily by _flush()).
+        self.fused = dev.type == "cuda" and algo in ("ssgd", "gd")
+        self._pending = False
+        if self.fused:
+            self.w_next = torch.empty_like(self.w)
+        self._upd = dict(mode=0 if algo == "ssgd" else 1, reg=U.REG.get(cfg.reg, 0), eta=cfg.eta,
+                         lam=cfg.lam, reg_alpha=cfg.reg_alpha)
 
     # ------------------------------------------------------------------ steps
     def _grad(self, W, stream):
@@ -146,10 +156,45 @@ class ParallelSGD:
                        row_offset=self.data.row_offset, G=self.G, C=self.C,
                        max_seg_rows=self.max_seg)
 
+    def _flush(self):
+        """Apply a pending fused update to self.w (end of training / before reads)."""
+        if self._pending:
+            c = self.cfg
+            if c.algo == "ssgd":
+                U.sync_update(self.w, U.SSGD, G=self.G, C=self.C, reg=c.reg, eta=c.eta,
+                              lam=c.lam, reg_alpha=c.reg_alpha)
+            else:
+                U.sync_update(self.w, U.GD_SUM, G=self.G, C=self.C, eta=c.eta)
+            self._pending = False
+
+    def global_sample_count(self) -> float:
+        """Total minibatch rows accumulated in count_acc, summed over ranks."""
+        if self.count_acc is None:
+            return 0.0
+        cnt = self.count_acc.clone()
+        if self.fused:
+            comm.all_reduce_sum(cnt)   # the fused kernel accumulates LOCAL counts
+        return float(cnt.item())
+
     def step(self):
         c = self.cfg
         t = self.t
-        if c.algo in ("ssgd", "gd"):
+        if self.fused:
+            if self._pending:
+                lr_ops.lr_grad(self.data.X_train, self.data.y_train, self.w_next, self.seg, D=self.D,
+                               has_bias=True, eps=c.eps, seed=c.sample_seed, step=t, frac=c.frac,
+                               row_offset=self.data.row_offset, G=self.G, C=self.C,
+                               max_seg_rows=self.max_seg, w_prev=self.w, update=self._upd,
+                               count_acc=self.count_acc)
+                self.w, self.w_next = self.w_next, self.w
+            else:
+                lr_ops.lr_grad(self.data.X_train, self.data.y_train, self.w, self.seg, D=self.D,
+                               has_bias=True, eps=c.eps, seed=c.sample_seed, step=t, frac=c.frac,
+                               row_offset=self.data.row_offset, G=self.G, C=self.C,
+                               max_seg_rows=self.max_seg, count_acc=self.count_acc)
+            self.bucket.all_reduce()
+            self._pending = True
+        elif c.algo in ("ssgd", "gd"):
             self._grad(self.w, t)
             self.bucket.all_reduce()
             if c.algo == "ssgd":
@@ -181,6 +226,7 @@ class ParallelSGD:
         self.t += 1
 
     def evaluate(self):
+        self._flush()
         d = self.data
         if d.X_test.shape[0] == 0:
             return float("nan"), float("nan")
@@ -208,6 +254,7 @@ class ParallelSGD:
 
     # --------------------------------------------------------- checkpointing
     def state_dict(self) -> dict:
+        self._flush()
         sd = {"t": self.t, "w": self.w.detach().cpu(), "cfg": asdict(self.cfg),
               "accs": list(self.history.accs)}
         if hasattr(self, "W"):
@@ -218,6 +265,7 @@ class ParallelSGD:
         return sd
 
     def load_state_dict(self, sd: dict):
+        self._pending = False
         self.t = int(sd["t"])
         self.w.copy_(sd["w"].to(self.w.dtype))
         if "locals" in sd and hasattr(self, "W"):
@@ -227,4 +275,5 @@ class ParallelSGD:
         self.history.accs = list(sd.get("accs", []))
 
     def weights(self) -> torch.Tensor:
+        self._flush()
         return self.w.view(-1)

@@ -90,12 +90,20 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
             D: int, has_bias: bool = True, eps: float = 0.0, seed: int = 42, step: int = 0,
             frac: float = 1.0, row_offset: int = 0, G: torch.Tensor | None = None,
             C: torch.Tensor | None = None, max_seg_rows: int | None = None,
-            variant: int | None = None, target_blocks: int | None = None):
+            variant: int | None = None, target_blocks: int | None = None,
+            w_prev: torch.Tensor | None = None, update: dict | None = None,
+            count_acc: torch.Tensor | None = None):
     """Per-segment gradient SUM and selected-row COUNT.
 
     X: [n, >=D] (bf16/f32), y: [n] f32, W: [n_seg, ldw] f32 models,
     seg: int64 [n_seg+1] local row bounds (segment s uses W[s]).
     Returns (G [n_seg, ldw], C [n_seg]); G[:, D] is the bias gradient.
+
+    Fused update (GPU, one segment): with ``w_prev`` given, the kernel first applies
+    the previous step's update ``update`` (dict: mode 0 = SSGD / 1 = GD, reg, eta,
+    lam, reg_alpha) using the CURRENT contents of G and C, writes the new model to
+    ``W`` and computes the gradient at it. ``count_acc`` (f64) accumulates the local
+    selected-row count.
     """
     nseg, ldw = W.shape
     if G is None:
@@ -112,11 +120,24 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
         gx, rpb = _grid(max(int(max_seg_rows), 1), nseg, target_blocks)
         S = ((D + 2 + 63) // 64) * 64
         ws = _workspace(X.device, nseg, gx, S)
+        u = update or {}
         _ext.ops().lr_grad(X, y, W, seg, int(row_offset), int(D), bool(has_bias), float(eps),
                            int(seed), int(step), float(frac), gx, rpb, ws.slab, ws.gslab,
-                           ws.cnt1, ws.cnt2, G, C, LR_VARIANT if variant is None else int(variant))
+                           ws.cnt1, ws.cnt2, G, C, LR_VARIANT if variant is None else int(variant),
+                           w_prev, int(u.get("mode", 0)), int(u.get("reg", 0)),
+                           float(u.get("eta", 0.0)), float(u.get("lam", 0.0)),
+                           float(u.get("reg_alpha", 0.0)), count_acc)
         return G, C
-    return _lr_grad_cpu(X, y, W, seg, D, has_bias, eps, seed, step, frac, row_offset, G, C)
+    if w_prev is not None:
+        from dalgo.ops import update as U
+        W.copy_(w_prev.view_as(W))
+        U.sync_update(W, U.SSGD if update.get("mode", 0) == 0 else U.GD_SUM, G=G, C=C,
+                      reg=update.get("reg", 0), eta=update.get("eta", 0.0),
+                      lam=update.get("lam", 0.0), reg_alpha=update.get("reg_alpha", 0.0))
+    G, C = _lr_grad_cpu(X, y, W, seg, D, has_bias, eps, seed, step, frac, row_offset, G, C)
+    if count_acc is not None:
+        count_acc += float(C.sum())
+    return G, C
 
 
 def _lr_grad_cpu(X, y, W, seg, D, has_bias, eps, seed, step, frac, row_offset, G, C):
