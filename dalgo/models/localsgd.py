@@ -24,6 +24,7 @@ replicated, so no driver and no broadcast per iteration.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import asdict, dataclass, field
 
 import torch
@@ -138,10 +139,14 @@ class ParallelSGD:
         # optional f64 device accumulator of minibatch sizes (bench accounting);
         # read it through global_sample_count()
         self.count_acc: torch.Tensor | None = None
-        # SSGD / GD on the GPU: the K8 update is fused into the next step's gradient
-        # kernel (ping-pong model buffers); self._pending = G/C hold an update not
-        # yet applied to self.w (applied lazily by _flush()).
-        self.fused = dev.type == "cuda" and algo in ("ssgd", "gd")
+        # Optional (DALGO_FUSED_UPDATE=1): fuse the K8 update into the next step's
+        # gradient kernel (ping-pong model buffers); self._pending = G/C hold an
+        # update not yet applied to self.w (applied lazily by _flush()). Measured on
+        # MI355X it is ~1.5% (10M rows) to ~8% (1.25M rows) SLOWER than the separate
+        # 2-us update launch, which overlaps the previous kernel's tail, while the
+        # fused prologue lengthens every block's start-up path — so it is off by default.
+        self.fused = (dev.type == "cuda" and algo in ("ssgd", "gd")
+                      and os.environ.get("DALGO_FUSED_UPDATE", "0") == "1")
         self._pending = False
         if self.fused:
             self.w_next = torch.empty_like(self.w)
