@@ -45,8 +45,8 @@ class DenseClosure:
         dev = torch.device(device)
         self.dev = dev
         self.n = n
-        self.npad = _round_up(max(n, 1), 64)
-        sl = _round_up((self.npad + world - 1) // world, 64)
+        self.npad = _round_up(max(n, 1), 128)   # 128 x 128 LDS-tiled K9 blocks
+        sl = _round_up((self.npad + world - 1) // world, 128)
         self.z_lo = min(self.npad, rank * sl)
         self.z_hi = min(self.npad, (rank + 1) * sl)
         self.nz = sl
