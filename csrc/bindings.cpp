@@ -433,21 +433,22 @@ void pr_update(const Tensor& acc, const Tensor& pres, const Tensor& outdeg, doub
 
 // ---------------------------------------------------------------------------
 // transitive closure
-void tc_step(const Tensor& A, const Tensor& Told, Tensor Tnew, Tensor count) {
+void tc_step(const Tensor& A, const Tensor& Told, Tensor Tnew, Tensor count, int64_t variant) {
   for (const Tensor* t : {&A, &Told, static_cast<const Tensor*>(&Tnew)}) {
     check_dev(*t, "tc operand");
-    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->stride(1) == 1,
-                "tc operands: 2-D bf16 with contiguous rows");
+    TORCH_CHECK(t->scalar_type() == at::kByte && t->dim() == 2 && t->stride(1) == 1,
+                "tc operands: 2-D uint8 (0/1) with contiguous rows");
+    TORCH_CHECK(t->stride(0) % 16 == 0, "tc: row strides must be multiples of 16 bytes");
   }
   const int64_t npad = A.size(0);
   TORCH_CHECK(A.size(1) >= npad && Told.size(1) >= npad && Tnew.sizes() == Told.sizes(),
               "tc shapes");
-  TORCH_CHECK(npad % 64 == 0 && Told.size(0) % 64 == 0, "tc: dims must be multiples of 64");
+  TORCH_CHECK(npad % 128 == 0 && Told.size(0) % 128 == 0, "tc: dims must be multiples of 128");
   TORCH_CHECK(Told.stride(0) == Tnew.stride(0), "tc: T strides");
   TORCH_CHECK(count.scalar_type() == at::kLong && count.numel() >= 1, "count int64[1]");
   DeviceGuard guard(A.device());
   DALGO_CHECK_HIP(dalgo_tc_step(A.data_ptr(), A.stride(0), Told.data_ptr(), Tnew.data_ptr(),
-                                Told.stride(0), (int)npad, (int)Told.size(0),
+                                Told.stride(0), (int)npad, (int)Told.size(0), (int)variant,
                                 reinterpret_cast<unsigned long long*>(count.data_ptr<int64_t>()),
                                 cur_stream()),
                   "tc_step");
@@ -499,7 +500,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("pr_spmv(Tensor src, Tensor dstl, Tensor c, Tensor(a!) acc, Tensor(b!) pres) -> ()");
   m.def("pr_update(Tensor acc, Tensor pres, Tensor outdeg, float q, float invN, int mode, "
         "Tensor? dangling_in, Tensor(a!) r, Tensor(b!) c, Tensor(c!)? dangling_out) -> ()");
-  m.def("tc_step(Tensor A, Tensor Told, Tensor(a!) Tnew, Tensor(b!) count) -> ()");
+  m.def("tc_step(Tensor A, Tensor Told, Tensor(a!) Tnew, Tensor(b!) count, int variant=0) -> ()");
   m.def("spd_inverse(Tensor G, float ridge, Tensor(a!) out, Tensor(b!)? status) -> ()");
   m.def("hbm_read(Tensor src, Tensor(a!) out, int unroll=8) -> ()");
   m.def("mc_pi(int seed, int stream, int offset, int n, Tensor(a!) count) -> ()");

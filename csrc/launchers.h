@@ -65,7 +65,7 @@ hipError_t dalgo_pr_update(const float* acc, const int32_t* pres, const int32_t*
 
 // ---- K9 transitive closure (closure.hip)
 hipError_t dalgo_tc_step(const void* A, int64_t lda, const void* Told, void* Tnew, int64_t ldt,
-                         int npad, int nz, unsigned long long* count, hipStream_t st);
+                         int npad, int nz, int variant, unsigned long long* count, hipStream_t st);
 
 // ---- K5 ALS ridge SPD inverse (als.hip)
 hipError_t dalgo_spd_inverse(const float* G, int k, int ldg, float ridge, float* out, int ldo,

@@ -106,7 +106,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     if force or not OUT.exists() or OUT.stat().st_mtime < _newest(objs):
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", OUT,
               f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch",
-              f"-Wl,-rpath,{tlib}", f"-L{ROCM / 'lib'}", "-lamdhip64"], verbose)
+              f"-Wl,-rpath,{tlib}", f"-L{ROCM / 'lib'}", "-lamdhip64",
+              "-Wl,--no-undefined"], verbose)
     return OUT
 
 

@@ -6,14 +6,16 @@ size as "The original graph has %i paths" (:42; the text is the reference's).
 
 Two engines, both partitioned by the path TARGET z (columns of P are
 independent, so ranks need no communication except the int64 count all-reduce):
-  * dense  — P^T as a 0/1 bf16 matrix, one fused MFMA boolean-GEMM round per
-             iteration (K9, csrc/kernels/closure.hip). Best up to ~50k vertices.
+  * dense  — P^T as a 0/1 uint8 matrix, one fused int8-MFMA boolean-GEMM round
+             per iteration (K9, csrc/kernels/closure.hip). Best up to ~100k
+             vertices (n^2 bytes per matrix).
   * sparse — semi-naive set iteration on packed int64 (x<<32|z) keys with
              sort/unique on device: only last round's NEW paths are joined
              (same fixpoint and per-round counts as the reference's naive join).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -35,6 +37,10 @@ def compact_ids(src: torch.Tensor, dst: torch.Tensor):
     return inv[:n], inv[n:], ids
 
 
+# K-staging depth of K9: 0 = 64 B, 1 = 128 B per stage (1.52 vs 1.76 POP/s int8 at n = 16384)
+TC_VARIANT = int(os.environ.get("DALGO_TC_VARIANT", "1"))
+
+
 def _round_up(a, b):
     return (a + b - 1) // b * b
 
@@ -50,7 +56,7 @@ class DenseClosure:
         self.z_lo = min(self.npad, rank * sl)
         self.z_hi = min(self.npad, (rank + 1) * sl)
         self.nz = sl
-        dt = torch.bfloat16 if dev.type == "cuda" else torch.float32
+        dt = torch.uint8 if dev.type == "cuda" else torch.float32
         src = src.to(dev).long()
         dst = dst.to(dev).long()
         self.A = torch.zeros((self.npad, self.npad), dtype=dt, device=dev)
@@ -68,7 +74,7 @@ class DenseClosure:
     def step(self) -> int:
         if self.dev.type == "cuda":
             self.count.zero_()
-            _ext.ops().tc_step(self.A, self.T, self.T2, self.count)
+            _ext.ops().tc_step(self.A, self.T, self.T2, self.count, TC_VARIANT)
         else:
             C = self.T @ self.A.T                           # C^T[z][x] = sum_y T[z][y] A[x][y]
             self.T2.copy_(((self.T != 0) | (C > 0.5)).to(self.T.dtype))

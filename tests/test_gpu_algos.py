@@ -161,6 +161,23 @@ def test_transitive_closure_gpu(cuda):
     assert DenseClosure(s4, d4, 3, device=cuda).run().counts == [4, 8, 9, 9]
 
 
+@pytest.mark.parametrize("variant", [0, 1])
+def test_tc_step_kernel_exact(cuda, variant):
+    """One K9 step (both K-staging depths) == (T | (T A^T > 0)) computed in f32 on the CPU."""
+    from dalgo.ops import _ext
+    g = torch.Generator().manual_seed(3)
+    n, nz = 640, 384
+    A = (torch.rand(n, n, generator=g) < 0.01).to(torch.uint8)
+    T = (torch.rand(nz, n, generator=g) < 0.05).to(torch.uint8)
+    ref = ((T != 0) | ((T.float() @ A.float().T) > 0.5)).to(torch.uint8)
+    Tn = torch.zeros_like(T, device=cuda)
+    cnt = torch.zeros(1, dtype=torch.int64, device=cuda)
+    _ext.ops().tc_step(A.to(cuda), T.to(cuda), Tn, cnt, variant)
+    torch.cuda.synchronize()
+    assert torch.equal(Tn.cpu(), ref)
+    assert int(cnt.item()) == int(ref.sum())
+
+
 def test_spd_inverse_gpu(cuda):
     from dalgo.models.als import spd_inverse
     for k in (10, 64, 128):
