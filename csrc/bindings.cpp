@@ -146,7 +146,7 @@ void sync_update(Tensor W, const std::optional<Tensor>& G, const std::optional<T
                  const std::optional<Tensor>& center, const std::optional<Tensor>& S,
                  const std::optional<Tensor>& Dl, const std::optional<Tensor>& count_acc, int64_t n,
                  int64_t mode, int64_t reg, double eta, double lam, double alpha, double reg_alpha,
-                 double mu, double zeta, double beta, double inv_p) {
+                 double mu, double zeta, double beta, double inv_p, bool zero_grad) {
   check_f32(W, "W");
   TORCH_CHECK(W.dim() == 2 && n <= W.size(1), "W must be [rows, ld] with n <= ld");
   const int64_t nrow = W.size(0), ld = W.size(1);
@@ -181,7 +181,7 @@ void sync_update(Tensor W, const std::optional<Tensor>& G, const std::optional<T
   DALGO_CHECK_HIP(dalgo_sync_update(W.data_ptr<float>(), g, c, ce, s, dl, cacc, (int)n, (int)ld,
                                     (int)nrow, (int)mode, (int)reg, (float)eta, (float)lam,
                                     (float)alpha, (float)reg_alpha, (float)mu, (float)zeta,
-                                    (float)beta, (float)inv_p, cur_stream()),
+                                    (float)beta, (float)inv_p, zero_grad ? 1 : 0, cur_stream()),
                   "sync_update");
 }
 
@@ -480,9 +480,9 @@ TORCH_LIBRARY(dalgo, m) {
         "float upd_lam=0., float upd_reg_alpha=0., Tensor(g!)? count_acc=None) -> ()");
   m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
         "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=6) -> ()");
-  m.def("sync_update(Tensor(a!) W, Tensor? G, Tensor? C, Tensor? center, Tensor? S, "
+  m.def("sync_update(Tensor(a!) W, Tensor(d!)? G, Tensor(e!)? C, Tensor? center, Tensor? S, "
         "Tensor(b!)? Dl, Tensor(c!)? count_acc, int n, int mode, int reg, float eta, float lam, float alpha, "
-        "float reg_alpha, float mu, float zeta, float beta, float inv_p) -> ()");
+        "float reg_alpha, float mu, float zeta, float beta, float inv_p, bool zero_grad=False) -> ()");
   m.def("rows_sum(Tensor W, int n, Tensor(a!) out) -> ()");
   m.def("rows_broadcast(Tensor(a!) W, int n, Tensor src) -> ()");
   m.def("philox_fill(Tensor(a!) out, int D, int row_offset, int seed, int stream, int dist, "

@@ -61,6 +61,8 @@ struct LrParams {
   int upd_reg;          // 0 none, 1 l2, 2 l1, 3 elastic net
   float upd_eta, upd_lam, upd_reg_alpha;
   double* count_acc;    // optional: += local selected-row count of THIS step
+  int atomic_out;       // 1: blocks add their partials to G/C with float atomics
+                        //    (G/C zeroed by the caller; summation order not fixed)
 };
 
 __device__ __forceinline__ float fused_update(float w, float g, float c, const LrParams& p) {
@@ -390,6 +392,24 @@ lr_rows_kernel(LrParams p) {
     __syncthreads();
     const int S = p.S;
     const int D = p.D;
+    if (p.atomic_out) {
+      float* Gs = p.G + (int64_t)seg * p.ldw;
+      for (int col = threadIdx.x; col < D; col += NW * 64) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) s += red_row(k)[col];
+        __hip_atomic_fetch_add(&Gs[col], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (threadIdx.x == 0) {
+        float sb = 0.f, sc = 0.f;
+        for (int k = 0; k < NW; ++k) { sb += red_row(k)[COLS]; sc += red_row(k)[COLS + 1]; }
+        if (p.has_bias) __hip_atomic_fetch_add(&Gs[D], sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&p.C[seg], sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p.count_acc)
+          __hip_atomic_fetch_add(p.count_acc, (double)sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
     float* my = p.slab + ((int64_t)seg * gx + bx) * S;
     for (int col = threadIdx.x; col < D; col += NW * 64) {
       float s = 0.f;
@@ -535,7 +555,8 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
   p.ldw = ldw; p.has_bias = has_bias; p.eps = eps; p.seed = seed; p.step = step; p.thr = thr;
   p.full = full; p.rows_per_block = rows_per_block; p.slab = slab; p.gslab = gslab;
   p.cnt1 = cnt1; p.cnt2 = cnt2; p.G = G; p.C = C; p.S = S;
-  return dispatch_lr<false>(p, is_bf16, gx, nseg, variant, st);
+  p.atomic_out = (variant >> 8) & 1;   // bit 8 of the variant selects the atomic epilogue
+  return dispatch_lr<false>(p, is_bf16, gx, nseg, variant & 0xff, st);
 }
 
 hipError_t dalgo_lr_eval(const void* X, const float* y, const float* W, const int64_t* seg,

@@ -30,8 +30,8 @@ enum RegType : int { kRegNone = 0, kRegL2 = 1, kRegL1 = 2, kRegElastic = 3 };
 
 struct UpdParams {
   float* W;            // [nrow, ld]  model(s) updated in place
-  const float* G;      // [nrow, ld]  gradient sums  (local modes / SSGD)
-  const float* C;      // [nrow]      counts
+  float* G;            // [nrow, ld]  gradient sums  (local modes / SSGD)
+  float* C;            // [nrow]      counts
   const float* center; // [ld]        EASGD centre variable (local elastic)
   const float* S;      // [ld]        all-reduced sum of models (sync modes)
   float* Dl;           // [ld]        BMUF block-momentum buffer
@@ -39,6 +39,8 @@ struct UpdParams {
   int n, ld, nrow;
   int mode, reg;
   float eta, lam, alpha, reg_alpha, mu, zeta, beta, inv_p;
+  int zero_grad;       // 1: leave G[row] and C[row] zeroed after use (one block per row):
+                       //    the next atomic-epilogue gradient launch accumulates into them
 };
 
 __device__ __forceinline__ float reg_grad(float w, int reg, float a) {
@@ -53,7 +55,7 @@ __device__ __forceinline__ float reg_grad(float w, int reg, float a) {
   }
 }
 
-__global__ void __launch_bounds__(256) sync_update_kernel(UpdParams p) {
+__global__ void __launch_bounds__(1024) sync_update_kernel(UpdParams p) {
   const int row = blockIdx.y;
   if (p.count_acc && row == 0 && blockIdx.x == 0 && threadIdx.x == 0) p.count_acc[0] += (double)p.C[0];
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < p.n; j += gridDim.x * blockDim.x) {
@@ -78,6 +80,7 @@ __global__ void __launch_bounds__(256) sync_update_kernel(UpdParams p) {
         w = w - p.eta * gm - p.alpha * (w - p.center[j]);
         break;
       }
+      default: break;
       case kAverage: w = p.S[j] * p.inv_p; break;
       case kBMUF: {
         const float wavg = p.S[j] * p.inv_p;
@@ -89,6 +92,11 @@ __global__ void __launch_bounds__(256) sync_update_kernel(UpdParams p) {
       case kElasticCenter: w = (1.f - p.beta) * w + p.beta * (p.S[j] * p.inv_p); break;
     }
     p.W[o] = w;
+    if (p.zero_grad) p.G[o] = 0.f;
+  }
+  if (p.zero_grad) {
+    __syncthreads();   // every thread of this row's (single) block has read C[row]
+    if (threadIdx.x == 0 && p.C) p.C[row] = 0.f;
   }
 }
 
@@ -117,14 +125,19 @@ using namespace dalgo;
 
 extern "C" {
 
-hipError_t dalgo_sync_update(float* W, const float* G, const float* C, const float* center,
+hipError_t dalgo_sync_update(float* W, float* G, float* C, const float* center,
                              const float* S, float* Dl, double* count_acc, int n, int ld, int nrow,
                              int mode, int reg, float eta, float lam, float alpha, float reg_alpha,
-                             float mu, float zeta, float beta, float inv_p, hipStream_t st) {
+                             float mu, float zeta, float beta, float inv_p, int zero_grad,
+                             hipStream_t st) {
+  zero_grad = (zero_grad && G != nullptr && mode <= kLocalElastic) ? 1 : 0;
   UpdParams p{W, G, C, center, S, Dl, count_acc, n, ld, nrow, mode, reg,
-              eta, lam, alpha, reg_alpha, mu, zeta, beta, inv_p};
-  const int bx = (int)std::min<int64_t>(cdiv(n, 256), 64);
-  hipLaunchKernelGGL(sync_update_kernel, dim3(bx, nrow), dim3(256), 0, st, p);
+              eta, lam, alpha, reg_alpha, mu, zeta, beta, inv_p, zero_grad};
+  // zero_grad needs one block per row (C[row] is cleared after a block barrier):
+  // give that block 1024 threads so the ~1k-float vector is one pass
+  const int bx = zero_grad ? 1 : (int)std::min<int64_t>(cdiv(n, 256), 64);
+  const int nt = zero_grad ? 1024 : 256;
+  hipLaunchKernelGGL(sync_update_kernel, dim3(bx, nrow), dim3(nt), 0, st, p);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

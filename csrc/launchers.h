@@ -22,10 +22,11 @@ hipError_t dalgo_lr_eval(const void* X, const float* y, const float* W, const in
                          int variant, hipStream_t st);
 
 // ---- K8 sync/update rules (sync_update.hip)
-hipError_t dalgo_sync_update(float* W, const float* G, const float* C, const float* center,
+hipError_t dalgo_sync_update(float* W, float* G, float* C, const float* center,
                              const float* S, float* Dl, double* count_acc, int n, int ld, int nrow,
                              int mode, int reg, float eta, float lam, float alpha, float reg_alpha,
-                             float mu, float zeta, float beta, float inv_p, hipStream_t st);
+                             float mu, float zeta, float beta, float inv_p, int zero_grad,
+                             hipStream_t st);
 hipError_t dalgo_rows_sum(const float* W, int nrow, int ld, int n, float* out, hipStream_t st);
 hipError_t dalgo_rows_broadcast(float* W, int nrow, int ld, int n, const float* src,
                                 hipStream_t st);

@@ -148,6 +148,10 @@ class ParallelSGD:
         self.fused = (dev.type == "cuda" and algo in ("ssgd", "gd")
                       and os.environ.get("DALGO_FUSED_UPDATE", "0") == "1")
         self._pending = False
+        # G/C are zero (fresh, or left zeroed by the last gradient-consuming K8), so the
+        # next atomic-epilogue K1 can accumulate into them without a memset launch
+        self._g_zero = True
+        self._zg = not lr_ops.DETERMINISTIC   # deterministic K1 overwrites G: no need to clear
         if self.fused:
             self.w_next = torch.empty_like(self.w)
         self._upd = dict(mode=0 if algo == "ssgd" else 1, reg=U.REG.get(cfg.reg, 0), eta=cfg.eta,
@@ -159,7 +163,8 @@ class ParallelSGD:
         lr_ops.lr_grad(self.data.X_train, self.data.y_train, W, self.seg, D=self.D, has_bias=True,
                        eps=c.eps, seed=c.sample_seed, step=stream, frac=c.frac,
                        row_offset=self.data.row_offset, G=self.G, C=self.C,
-                       max_seg_rows=self.max_seg)
+                       max_seg_rows=self.max_seg, g_is_zero=self._g_zero)
+        self._g_zero = False
 
     def _flush(self):
         """Apply a pending fused update to self.w (end of training / before reads)."""
@@ -204,16 +209,19 @@ class ParallelSGD:
             self.bucket.all_reduce()
             if c.algo == "ssgd":
                 U.sync_update(self.w, U.SSGD, G=self.G, C=self.C, reg=c.reg, eta=c.eta,
-                              lam=c.lam, reg_alpha=c.reg_alpha, count_acc=self.count_acc)
+                              lam=c.lam, reg_alpha=c.reg_alpha, count_acc=self.count_acc,
+                              zero_grad=self._zg)
             else:
                 U.sync_update(self.w, U.GD_SUM, G=self.G, C=self.C, eta=c.eta,
-                              count_acc=self.count_acc)
+                              count_acc=self.count_acc, zero_grad=self._zg)
+            self._g_zero = True
         elif c.algo in ("ma", "bmuf"):
             U.rows_broadcast(self.W, self.w)
             for l in range(c.n_local):
                 stream = t if c.reuse_minibatch else t * c.n_local + l
                 self._grad(self.W, stream)
-                U.sync_update(self.W, U.LOCAL_MEAN, G=self.G, C=self.C, eta=c.eta)
+                U.sync_update(self.W, U.LOCAL_MEAN, G=self.G, C=self.C, eta=c.eta, zero_grad=self._zg)
+                self._g_zero = True
             U.rows_sum(self.W, self.S)
             comm.all_reduce_sum(self.S)
             if c.algo == "ma":
@@ -224,7 +232,8 @@ class ParallelSGD:
         else:  # easgd
             self._grad(self.W, t)
             U.sync_update(self.W, U.LOCAL_ELASTIC, G=self.G, C=self.C, center=self.w, eta=c.eta,
-                          alpha=c.alpha)
+                          alpha=c.alpha, zero_grad=self._zg)
+            self._g_zero = True
             U.rows_sum(self.W, self.S)
             comm.all_reduce_sum(self.S)
             U.sync_update(self.w, U.ELASTIC_CENTER, S=self.S, beta=c.beta, inv_p=self.inv_p)

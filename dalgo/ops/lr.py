@@ -30,6 +30,9 @@ import os
 #   TARGET_BLOCKS   = workgroups per launch (split over segments)
 LR_VARIANT = int(os.environ.get("DALGO_LR_VARIANT", "6"))
 _TARGET_BLOCKS = int(os.environ.get("DALGO_LR_BLOCKS", "256"))
+#   DETERMINISTIC   = combine per-block partials with the fixed-order two-level
+#                     hand-off (bitwise repeatable) instead of float atomics
+DETERMINISTIC = os.environ.get("DALGO_DETERMINISTIC", "0") == "1"
 
 
 def padded_cols(D: int, dtype: torch.dtype) -> int:
@@ -92,7 +95,8 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
             C: torch.Tensor | None = None, max_seg_rows: int | None = None,
             variant: int | None = None, target_blocks: int | None = None,
             w_prev: torch.Tensor | None = None, update: dict | None = None,
-            count_acc: torch.Tensor | None = None):
+            count_acc: torch.Tensor | None = None, g_is_zero: bool = False,
+            deterministic: bool | None = None):
     """Per-segment gradient SUM and selected-row COUNT.
 
     X: [n, >=D] (bf16/f32), y: [n] f32, W: [n_seg, ldw] f32 models,
@@ -104,6 +108,12 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
     lam, reg_alpha) using the CURRENT contents of G and C, writes the new model to
     ``W`` and computes the gradient at it. ``count_acc`` (f64) accumulates the local
     selected-row count.
+
+    Epilogue: by default every block adds its partial sums to G/C with float
+    atomics (G/C are zeroed here unless the caller passes ``g_is_zero=True``, e.g.
+    after a ``sync_update(..., zero_grad=True)``); ``deterministic=True`` (or
+    DALGO_DETERMINISTIC=1) uses the fixed-order two-level reduction instead, which
+    is bitwise repeatable. The fused-update path is always deterministic.
     """
     nseg, ldw = W.shape
     if G is None:
@@ -121,9 +131,16 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
         S = ((D + 2 + 63) // 64) * 64
         ws = _workspace(X.device, nseg, gx, S)
         u = update or {}
+        var = LR_VARIANT if variant is None else int(variant)
+        det = DETERMINISTIC if deterministic is None else bool(deterministic)
+        if not det and w_prev is None:
+            if not g_is_zero:
+                G.zero_()
+                C.zero_()
+            var |= 256                     # atomic epilogue (csrc/kernels/lr_grad.hip)
         _ext.ops().lr_grad(X, y, W, seg, int(row_offset), int(D), bool(has_bias), float(eps),
                            int(seed), int(step), float(frac), gx, rpb, ws.slab, ws.gslab,
-                           ws.cnt1, ws.cnt2, G, C, LR_VARIANT if variant is None else int(variant),
+                           ws.cnt1, ws.cnt2, G, C, var,
                            w_prev, int(u.get("mode", 0)), int(u.get("reg", 0)),
                            float(u.get("eta", 0.0)), float(u.get("lam", 0.0)),
                            float(u.get("reg_alpha", 0.0)), count_acc)

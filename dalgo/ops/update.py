@@ -27,7 +27,9 @@ def _reg_grad(w, reg: int, a: float):
 def sync_update(W: torch.Tensor, mode: int, *, n: int | None = None, G=None, C=None, center=None,
                 S=None, Dl=None, count_acc=None, reg: str | int = "none", eta: float = 0.0, lam: float = 0.0,
                 alpha: float = 0.0, reg_alpha: float = 0.0, mu: float = 0.0, zeta: float = 0.0,
-                beta: float = 0.0, inv_p: float = 1.0) -> torch.Tensor:
+                beta: float = 0.0, inv_p: float = 1.0, zero_grad: bool = False) -> torch.Tensor:
+    """One K8 launch. ``zero_grad``: the gradient-consuming modes (SSGD, GD, local
+    mean/elastic) leave G and C zeroed, ready for the next atomic-epilogue K1."""
     W2 = W if W.dim() == 2 else W.view(1, -1)
     n = W2.shape[1] if n is None else int(n)
     reg_i = REG[reg] if isinstance(reg, str) else int(reg)
@@ -38,7 +40,7 @@ def sync_update(W: torch.Tensor, mode: int, *, n: int | None = None, G=None, C=N
                                None if S is None else S.reshape(-1),
                                None if Dl is None else Dl.reshape(-1), count_acc, n, int(mode), reg_i,
                                float(eta), float(lam), float(alpha), float(reg_alpha), float(mu),
-                               float(zeta), float(beta), float(inv_p))
+                               float(zeta), float(beta), float(inv_p), bool(zero_grad))
         return W
     # ---- CPU reference (same math, W's dtype)
     if count_acc is not None:
@@ -72,6 +74,10 @@ def sync_update(W: torch.Tensor, mode: int, *, n: int | None = None, G=None, C=N
         w.copy_((1 - beta) * w + beta * (S.reshape(1, -1)[:, :n] * inv_p))
     else:
         raise ValueError(f"unknown update mode {mode}")
+    if zero_grad and G is not None and mode in (SSGD, GD_SUM, LOCAL_MEAN, LOCAL_ELASTIC):
+        G.zero_()
+        if C is not None:
+            C.zero_()
     return W
 
 

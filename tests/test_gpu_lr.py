@@ -42,9 +42,20 @@ def test_lr_grad_single_segment_deterministic(cuda):
     Xd, yd = X.to(cuda), y.to(cuda)
     W = torch.randn(1, 1025, generator=torch.Generator().manual_seed(2)).to(cuda) * 0.05
     seg = torch.tensor([0, X.shape[0]], dtype=torch.int64, device=cuda)
-    outs = [L.lr_grad(Xd, yd, W, seg, D=1024, frac=0.1, step=3) for _ in range(3)]
+    outs = [L.lr_grad(Xd, yd, W, seg, D=1024, frac=0.1, step=3, deterministic=True)
+            for _ in range(3)]
     for G, C in outs[1:]:
         assert torch.equal(G, outs[0][0]) and torch.equal(C, outs[0][1])
+    # the default atomic epilogue agrees to f32 rounding (order of the block sums)
+    Ga, Ca = L.lr_grad(Xd, yd, W, seg, D=1024, frac=0.1, step=3, deterministic=False)
+    assert torch.equal(Ca, outs[0][1])
+    assert ((Ga - outs[0][0]).abs().max() / outs[0][0].abs().max()).item() < 1e-5
+    # g_is_zero=True accumulates into the given (zero) buffers without a memset
+    G0 = torch.zeros_like(Ga)
+    C0 = torch.zeros_like(Ca)
+    L.lr_grad(Xd, yd, W, seg, D=1024, frac=0.1, step=3, G=G0, C=C0, g_is_zero=True)
+    assert torch.equal(C0, Ca)
+    assert ((G0 - Ga).abs().max() / Ga.abs().max()).item() < 1e-5
     G_ref, C_ref = L.lr_grad(X, y, W.cpu().double(), seg.cpu(), D=1024, frac=0.1, step=3)
     assert float(outs[0][1].item()) == float(C_ref.item())
     rel = (outs[0][0].cpu().double() - G_ref).abs().max() / G_ref.abs().max()
@@ -84,6 +95,13 @@ def test_sync_update_modes(cuda, mode):
                   Dl=Dd, **kw)
     assert torch.allclose(Wd.cpu().double(), Wc, rtol=1e-5, atol=1e-5)
     assert torch.allclose(Dd.cpu().double(), Dc, rtol=1e-5, atol=1e-5)
+    # zero_grad: same update, and the gradient-consuming modes leave G / C zeroed
+    Wz, Gz, Cz = W.to(cuda), G.to(cuda), C.to(cuda)
+    U.sync_update(Wz, mode, G=Gz, C=Cz, center=center.to(cuda), S=S.to(cuda),
+                  Dl=Dl.to(cuda), zero_grad=True, **kw)
+    assert torch.equal(Wz, Wd)
+    consumes = mode in (U.SSGD, U.GD_SUM, U.LOCAL_MEAN, U.LOCAL_ELASTIC)
+    assert bool((Gz == 0).all()) == consumes and bool((Cz == 0).all()) == consumes
 
 
 def test_rows_sum_broadcast(cuda):
