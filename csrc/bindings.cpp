@@ -432,6 +432,60 @@ void pr_update(const Tensor& acc, const Tensor& pres, const Tensor& outdeg, doub
 }
 
 // ---------------------------------------------------------------------------
+// K11 xGMI one-shot all-reduce: buffers are raw device addresses (int64) owned by
+// dalgo.parallel.xgmi (allocated / IPC-opened through these ops)
+int64_t xgmi_buffer_bytes(int64_t slot) { return (int64_t)dalgo_xgmi_buffer_bytes((int)slot); }
+
+int64_t xgmi_alloc(int64_t bytes, int64_t device) {
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, (int)device));
+  void* p = nullptr;
+  DALGO_CHECK_HIP(dalgo_xgmi_alloc((size_t)bytes, &p), "xgmi_alloc");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void xgmi_free(int64_t ptr) {
+  DALGO_CHECK_HIP(dalgo_xgmi_free(reinterpret_cast<void*>(ptr)), "xgmi_free");
+}
+
+Tensor xgmi_get_handle(int64_t ptr) {
+  Tensor h = at::zeros({64}, at::TensorOptions().dtype(at::kByte));
+  DALGO_CHECK_HIP(dalgo_xgmi_get_handle(reinterpret_cast<void*>(ptr), h.data_ptr()), "xgmi_get_handle");
+  return h;
+}
+
+int64_t xgmi_open(const Tensor& handle, int64_t device) {
+  TORCH_CHECK(!handle.is_cuda() && handle.scalar_type() == at::kByte && handle.numel() == 64 &&
+                  handle.is_contiguous(), "xgmi_open: handle must be a CPU uint8[64]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, (int)device));
+  void* p = nullptr;
+  DALGO_CHECK_HIP(dalgo_xgmi_open(handle.data_ptr(), &p), "xgmi_open");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void xgmi_close(int64_t ptr) {
+  DALGO_CHECK_HIP(dalgo_xgmi_close(reinterpret_cast<void*>(ptr)), "xgmi_close");
+}
+
+void xgmi_allreduce(Tensor x, at::IntArrayRef bufs, int64_t rank, int64_t slot, int64_t epoch,
+                    Tensor err, double timeout_s) {
+  check_f32(x, "x");
+  TORCH_CHECK(x.numel() <= slot, "xgmi_allreduce: vector larger than the slot");
+  TORCH_CHECK(bufs.size() >= 1 && bufs.size() <= 8 && rank >= 0 && rank < (int64_t)bufs.size(),
+              "xgmi_allreduce: 1..8 ranks");
+  TORCH_CHECK(epoch > 0 && epoch <= 0xffffffffLL, "xgmi_allreduce: epoch in [1, 2^32)");
+  check_dev(err, "err");
+  TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() >= 1, "err int32[1]");
+  void* b[8] = {};
+  for (size_t r = 0; r < bufs.size(); ++r) b[r] = reinterpret_cast<void*>(bufs[r]);
+  DeviceGuard guard(x.device());
+  DALGO_CHECK_HIP(dalgo_xgmi_allreduce(x.data_ptr<float>(), x.data_ptr<float>(), (int)x.numel(),
+                                       (int)rank, (int)bufs.size(), b, (int)slot, (uint32_t)epoch,
+                                       reinterpret_cast<unsigned*>(err.data_ptr<int>()), timeout_s,
+                                       cur_stream()),
+                  "xgmi_allreduce");
+}
+
+// ---------------------------------------------------------------------------
 // transitive closure
 void tc_step(const Tensor& A, const Tensor& Told, Tensor Tnew, Tensor count, int64_t variant) {
   for (const Tensor* t : {&A, &Told, static_cast<const Tensor*>(&Tnew)}) {
@@ -500,6 +554,14 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("pr_spmv(Tensor src, Tensor dstl, Tensor c, Tensor(a!) acc, Tensor(b!) pres) -> ()");
   m.def("pr_update(Tensor acc, Tensor pres, Tensor outdeg, float q, float invN, int mode, "
         "Tensor? dangling_in, Tensor(a!) r, Tensor(b!) c, Tensor(c!)? dangling_out) -> ()");
+  m.def("xgmi_buffer_bytes(int slot) -> int", &xgmi_buffer_bytes);
+  m.def("xgmi_alloc(int bytes, int device) -> int", &xgmi_alloc);
+  m.def("xgmi_free(int ptr) -> ()", &xgmi_free);
+  m.def("xgmi_get_handle(int ptr) -> Tensor", &xgmi_get_handle);
+  m.def("xgmi_open(Tensor handle, int device) -> int", &xgmi_open);
+  m.def("xgmi_close(int ptr) -> ()", &xgmi_close);
+  m.def("xgmi_allreduce(Tensor(a!) x, int[] bufs, int rank, int slot, int epoch, Tensor(b!) err, "
+        "float timeout_s) -> ()");
   m.def("tc_step(Tensor A, Tensor Told, Tensor(a!) Tnew, Tensor(b!) count, int variant=0) -> ()");
   m.def("spd_inverse(Tensor G, float ridge, Tensor(a!) out, Tensor(b!)? status) -> ()");
   m.def("hbm_read(Tensor src, Tensor(a!) out, int unroll=8) -> ()");
@@ -517,6 +579,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("hbm_read", &hbm_read);
   m.impl("spd_inverse", &spd_inverse);
   m.impl("tc_step", &tc_step);
+  m.impl("xgmi_allreduce", &xgmi_allreduce);
   m.impl("rmat_edges", &rmat_edges);
   m.impl("pr_spmv", &pr_spmv);
   m.impl("pr_update", &pr_update);

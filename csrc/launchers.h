@@ -72,4 +72,15 @@ hipError_t dalgo_tc_step(const void* A, int64_t lda, const void* Told, void* Tne
 hipError_t dalgo_spd_inverse(const float* G, int k, int ldg, float ridge, float* out, int ldo,
                              int* status, hipStream_t st);
 
+// ---- K11 one-shot xGMI all-reduce (xgmi_allreduce.hip)
+size_t dalgo_xgmi_buffer_bytes(int slot_floats);
+hipError_t dalgo_xgmi_alloc(size_t bytes, void** ptr);
+hipError_t dalgo_xgmi_free(void* ptr);
+hipError_t dalgo_xgmi_get_handle(void* ptr, void* handle);
+hipError_t dalgo_xgmi_open(const void* handle, void** ptr);
+hipError_t dalgo_xgmi_close(void* ptr);
+hipError_t dalgo_xgmi_allreduce(const float* in, float* out, int n, int rank, int world,
+                                void* const* bufs, int slot, uint32_t epoch, unsigned* err,
+                                double timeout_s, hipStream_t st);
+
 }  // extern "C"

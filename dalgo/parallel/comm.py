@@ -115,7 +115,8 @@ class BucketedAllReduce:
     their outputs straight into it (no pack/unpack copies).
     """
 
-    def __init__(self, shapes: list[tuple[int, ...]], dtype=torch.float32, device=None):
+    def __init__(self, shapes: list[tuple[int, ...]], dtype=torch.float32, device=None,
+                 allow_xgmi: bool = True):
         device = device or runtime.get().device
         sizes = [int(torch.Size(s).numel()) for s in shapes]
         self.buffer = torch.zeros(sum(sizes), dtype=dtype, device=device)
@@ -124,6 +125,16 @@ class BucketedAllReduce:
         for s, n in zip(shapes, sizes):
             self.views.append(self.buffer[off: off + n].view(s))
             off += n
+        # latency-bound GPU buckets go through the K11 one-shot xGMI all-reduce
+        # (collective decision: all ranks or none; RCCL otherwise)
+        self.xg = None
+        if (allow_xgmi and _active() and self.buffer.is_cuda and dtype == torch.float32):
+            from dalgo.parallel import xgmi
+            if self.buffer.numel() <= xgmi.SLOT_FLOATS:
+                self.xg = xgmi.shared(self.buffer.device)
 
     def all_reduce(self, async_op: bool = False):
+        if self.xg is not None:
+            self.xg.all_reduce_(self.buffer)   # stream-ordered: nothing to wait for
+            return None if async_op else self.buffer
         return all_reduce_sum(self.buffer, async_op=async_op)

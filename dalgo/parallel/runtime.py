@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import sys
 from dataclasses import dataclass
 
 import torch
@@ -112,6 +113,11 @@ def shutdown():
     """Tear down the process group (``spark.stop()`` equivalent)."""
     global _RT
     if dist.is_available() and dist.is_initialized():
+        try:
+            from dalgo.parallel import xgmi
+            xgmi.close_shared()
+        except Exception as e:
+            print(f"[dalgo] xGMI buffer release failed: {e}", file=sys.stderr)
         try:
             dist.barrier()
         except Exception:

@@ -1,0 +1,188 @@
+"""K11: one-shot xGMI all-reduce for latency-bound vectors (csrc/kernels/xgmi_allreduce.hip).
+
+The SGD family all-reduces a ~4 KB ``[g || count]`` bucket every step
+(treeAggregate, optimization/ssgd.py:99-103); at 8 GPUs that collective is a
+sizeable part of a ~60 us step. MI355X GPUs in a node are fully connected by
+point-to-point xGMI links, so instead of a ring every rank writes its vector
+straight into every peer's exchange buffer (IPC-mapped, uncached), raises one
+flag per peer and sums the W slots of its own buffer in rank order: one hop, all
+links in parallel, bitwise-identical results on every rank.
+
+Safety: the exchange buffers are opened collectively; a self-test checks exact
+sums over back-to-back calls (both buffer phases), and the decision to use K11 is
+itself all-reduced, so either every rank uses it or none does (falls back to
+RCCL). The device-side wait is bounded by a wall-clock timeout that sets an error
+word instead of hanging; :meth:`XgmiAllReduce.check` raises if it ever fired.
+
+Env: ``DALGO_XGMI=0`` disables it; ``DALGO_XGMI_TIMEOUT`` (s, default 60).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+from dalgo.ops import _ext
+
+MAX_RANKS = 8
+SLOT_FLOATS = 4096          # largest vector (floats) handled; larger buckets use RCCL
+
+
+def _agree(ok: bool, device) -> bool:
+    """Collective AND of a per-rank flag."""
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                        device=device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return int(flag.item()) == 1
+
+
+class XgmiAllReduce:
+    """Exchange buffers of all ranks + the K11 launch. Construction is collective and
+    failure-consistent: it raises on EVERY rank if any rank could not allocate or
+    map the buffers (no rank is left waiting in a collective)."""
+
+    def __init__(self, device: torch.device, slot_floats: int = SLOT_FLOATS,
+                 timeout_s: float | None = None, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if self.world > MAX_RANKS:
+            raise ValueError(f"xGMI all-reduce supports at most {MAX_RANKS} ranks")
+        self.device = torch.device(device)
+        self.slot = int(slot_floats)
+        self.timeout_s = float(timeout_s if timeout_s is not None
+                               else os.environ.get("DALGO_XGMI_TIMEOUT", "60"))
+        self.own = 0
+        self.opened = []
+        self.bufs = []
+        dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        handle, err = None, None
+        try:
+            ops = _ext.ops()
+            self._ops = ops
+            self.own = int(ops.xgmi_alloc(int(ops.xgmi_buffer_bytes(self.slot)), dev_index))
+            handle = bytes(ops.xgmi_get_handle(self.own).numpy().tobytes())
+        except Exception as e:
+            err = e
+        handles = [None] * self.world
+        dist.all_gather_object(handles, handle, group=group)   # every rank takes part
+        if any(h is None for h in handles):
+            self._release()
+            raise RuntimeError(f"xGMI buffer allocation failed on some rank ({err!r})")
+        try:
+            for r in range(self.world):
+                if r == self.rank:
+                    self.bufs.append(self.own)
+                else:
+                    h = torch.frombuffer(bytearray(handles[r]), dtype=torch.uint8).clone()
+                    p = int(self._ops.xgmi_open(h, dev_index))
+                    self.opened.append(p)
+                    self.bufs.append(p)
+            ok = True
+        except Exception as e:
+            err, ok = e, False
+        if not _agree(ok, self.device):
+            self._release()
+            raise RuntimeError(f"xGMI IPC mapping failed on some rank ({err!r})")
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.epoch = 0
+
+    def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
+        """In-place SUM over ranks of a contiguous f32 GPU vector (numel <= slot)."""
+        self.epoch += 1
+        if self.epoch >= 1 << 32:
+            raise RuntimeError("xGMI all-reduce epoch space exhausted")
+        self._ops.xgmi_allreduce(x, self.bufs, self.rank, self.slot, self.epoch, self.err,
+                                 self.timeout_s)
+        return x
+
+    def check(self):
+        if int(self.err.item()) != 0:
+            raise RuntimeError("xGMI all-reduce: a peer flag wait timed out (results invalid)")
+
+    def _release(self):
+        for p in self.opened:
+            try:
+                self._ops.xgmi_close(p)
+            except Exception:
+                pass
+        self.opened = []
+        if self.own:
+            try:
+                self._ops.xgmi_free(self.own)
+            except Exception:
+                pass
+            self.own = 0
+
+    def close(self):
+        """Collective: every rank stops using the buffers before any is freed."""
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.group)
+        self._release()
+
+
+def _self_test(xg: XgmiAllReduce) -> bool:
+    """K11 result == exact expected sums for a few back-to-back calls (both phases)."""
+    n = 1031
+    ok = True
+    for it in range(4):
+        base = torch.arange(n, dtype=torch.float32, device=xg.device)
+        x = base * (xg.rank + 1) + it
+        xg.all_reduce_(x)
+        W = xg.world
+        exp = base * (W * (W + 1) / 2) + it * W
+        torch.cuda.synchronize(xg.device)
+        ok = ok and bool(torch.equal(x, exp))
+    return ok and int(xg.err.item()) == 0
+
+
+_shared: dict = {}
+
+
+def shared(device: torch.device) -> XgmiAllReduce | None:
+    """Process-wide K11 instance for the default group (collective on first call).
+
+    Returns None (on every rank) if disabled, unsupported or the self-test fails.
+    """
+    key = str(device)
+    if key in _shared:
+        return _shared[key]
+    inst = None
+    if (os.environ.get("DALGO_XGMI", "1") == "1" and dist.is_initialized()
+            and 1 < dist.get_world_size() <= MAX_RANKS and torch.device(device).type == "cuda"
+            and _ext.available()):
+        try:
+            inst = XgmiAllReduce(device, timeout_s=10.0)
+        except Exception as e:   # consistent on every rank (collective construction)
+            if dist.get_rank() == 0:
+                print(f"[dalgo] xGMI all-reduce unavailable: {e}", file=sys.stderr)
+            inst = None
+        if inst is not None:
+            try:
+                ok = _self_test(inst)
+            except Exception as e:
+                print(f"[dalgo] rank {dist.get_rank()}: xGMI self-test error: {e}", file=sys.stderr)
+                ok = False
+            if _agree(ok, device):
+                inst.timeout_s = float(os.environ.get("DALGO_XGMI_TIMEOUT", "60"))
+            else:
+                inst.close()
+                inst = None
+                if dist.get_rank() == 0:
+                    print("[dalgo] xGMI self-test failed: using the process group's all-reduce",
+                          file=sys.stderr)
+    _shared[key] = inst
+    return inst
+
+
+def close_shared():
+    """Release the shared instances (collective; called by runtime.shutdown)."""
+    for k, inst in list(_shared.items()):
+        if inst is not None:
+            if int(inst.err.item()) != 0:
+                print("[dalgo] warning: an xGMI all-reduce wait timed out during the run",
+                      file=sys.stderr)
+            inst.close()
+        del _shared[k]

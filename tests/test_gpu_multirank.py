@@ -53,3 +53,10 @@ def test_bench_two_ranks_gloo_on_one_gpu(cuda):
 def test_scripts_two_ranks_gloo_on_one_gpu(cuda, script, extra, needle):
     out = _torchrun([script, "--device", "cuda", "--backend", "gloo", "--no-plot"] + extra)
     assert needle in out
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_xgmi_allreduce_ranks_on_one_gpu(cuda, n):
+    """K11: IPC exchange buffers + flag protocol, exact rank-ordered sums on every rank."""
+    out = _torchrun(["tests/helpers/xgmi_check.py"], n=n)
+    assert f"XGMI_OK world={n}" in out
