@@ -9,7 +9,7 @@ from dalgo.models.kmeans import KMeans, KMeansConfig
 from dalgo.parallel import comm, runtime
 from dalgo.parallel.sharding import even_slices, spark_slices
 from dalgo.utils import checkpoint, obs
-from dalgo.utils.cli import common_parser, init_from_args
+from dalgo.utils.cli import add_ckpt_args, common_parser, init_from_args
 
 TOY = [[1, 2], [1, 4], [1, 0], [10, 2], [10, 4], [10, 0]]   # k-means.py:49-50
 
@@ -25,7 +25,7 @@ def main(argv=None):
     ap.add_argument("--synthetic", default=None, metavar="N,D",
                     help="Gaussian blobs instead of the 6 toy points")
     ap.add_argument("--dtype", choices=["bf16", "f32"], default=None)
-    ap.add_argument("--ckpt-dir", default=None)
+    add_ckpt_args(ap)
     a = ap.parse_args(argv)
     rt = init_from_args(a, "K-means")
     if a.synthetic:
@@ -42,7 +42,18 @@ def main(argv=None):
     cfg = KMeansConfig(k=a.k, n_iterations=a.n_iterations, n_workers=a.n_slices, seed=a.init_seed,
                        tol=a.converge_dist)
     km = KMeans(cfg, X, lo, N)
-    hist = km.fit()
+    if a.resume and a.ckpt_dir:
+        sd = checkpoint.load(a.ckpt_dir, "kmeans_state")
+        if sd is not None:
+            km.load_state_dict(sd)
+            rt.log(f"Resumed from iteration {km.t}")
+    while km.t < a.n_iterations:
+        km.fit(1)
+        if a.ckpt_dir and a.ckpt_every and km.t % a.ckpt_every == 0:
+            checkpoint.save(km.state_dict(), a.ckpt_dir, "kmeans_state", rt.rank)
+        if cfg.tol is not None and km.history.shift and km.history.shift[-1] < cfg.tol:
+            break
+    hist = km.history
     sink = obs.MetricsSink(a.metrics_out, rt.rank)
     for i, (s, sh) in enumerate(zip(hist.sse, hist.shift)):
         sink.log(iteration=i + 1, sse=s, shift2=sh)

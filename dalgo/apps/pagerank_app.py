@@ -7,7 +7,8 @@ from dalgo.models.pagerank import PageRank, PageRankConfig
 from dalgo.models.transitive_closure import compact_ids
 from dalgo.ops import graph as G
 from dalgo.parallel import runtime
-from dalgo.utils.cli import common_parser, init_from_args
+from dalgo.utils import checkpoint
+from dalgo.utils.cli import add_ckpt_args, common_parser, init_from_args
 
 TOY_EDGES = [(1, 2), (1, 3), (2, 3), (3, 1)]   # pagerank.py:35-38
 
@@ -80,6 +81,7 @@ def main(argv=None):
     ap.add_argument("--rmat-scale", type=int, default=None, help="synthetic Graph500 R-MAT graph")
     ap.add_argument("--edge-factor", type=int, default=16)
     ap.add_argument("--top", type=int, default=20, help="print only the top ranks of large graphs")
+    add_ckpt_args(ap)
     a = ap.parse_args(argv)
     rt = init_from_args(a, "PageRank")
     ids = None
@@ -95,7 +97,18 @@ def main(argv=None):
         shard = G.build_shard(s.to(torch.int32).to(rt.device), d.to(torch.int32).to(rt.device),
                               len(ids), rt.rank, rt.world_size)
     pr = PageRank(PageRankConfig(q=a.q, n_iterations=a.n_iterations, semantics=a.semantics),
-                  shard, rt.world_size).fit()
+                  shard, rt.world_size)
+    if a.resume and a.ckpt_dir:
+        sd = checkpoint.load(a.ckpt_dir, "pagerank_state", rt.rank, per_rank=True)
+        if sd is not None:
+            pr.load_state_dict(sd)
+            rt.log(f"Resumed from iteration {pr.t}")
+    while pr.t < a.n_iterations:
+        pr.step()
+        if a.ckpt_dir and a.ckpt_every and pr.t % a.ckpt_every == 0:
+            checkpoint.save(pr.state_dict(), a.ckpt_dir, "pagerank_state", rt.rank, per_rank=True)
+    if a.ckpt_dir:
+        checkpoint.save(pr.state_dict(), a.ckpt_dir, "pagerank_state", rt.rank, per_rank=True)
     ranks = pr.collect()
     if rt.is_main:
         items = list(ranks.items())

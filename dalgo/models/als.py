@@ -112,6 +112,16 @@ class ALS:
         sse = float(self.R2.item() + part.sum().item())
         return math.sqrt(max(sse, 0.0) / (self.cfg.m * self.cfg.n))
 
+    def state_dict(self) -> dict:
+        """Replicated state: both factors (full, after the half-sweep gathers)."""
+        return {"t": self.t, "U": self.U.cpu(), "V": self.V.cpu(), "rmse": list(self.history.rmse)}
+
+    def load_state_dict(self, sd: dict):
+        self.t = int(sd["t"])
+        self.U = sd["U"].to(self.dev, self.dtype)
+        self.V = sd["V"].to(self.dev, self.dtype)
+        self.history.rmse = list(sd.get("rmse", []))
+
     def fit(self, n_iterations: int | None = None, callback=None):
         n = self.cfg.n_iterations if n_iterations is None else n_iterations
         for _ in range(n):

@@ -113,10 +113,12 @@ class KMeans:
         return self.cen.C
 
     def state_dict(self) -> dict:
-        return {"t": self.t, "centers": self.cen.C.detach().cpu(), "sse": list(self.history.sse)}
+        return {"t": self.t, "centers": self.cen.C.detach().cpu(), "sse": list(self.history.sse),
+                "shift": list(self.history.shift)}
 
     def load_state_dict(self, sd: dict):
         self.t = int(sd["t"])
         self.cen.C.copy_(sd["centers"].to(self.dev))
         K.refresh(self.cen)
         self.history.sse = list(sd.get("sse", []))
+        self.history.shift = list(sd.get("shift", []))

@@ -95,6 +95,19 @@ class PageRank:
             self.step()
         return self
 
+    def state_dict(self) -> dict:
+        """Per-rank state (this rank's destination slice) for checkpoint / resume."""
+        return {"t": self.t, "r": self.r.cpu(), "c_slice": self.c_slice.cpu(),
+                "dang": self.dang.cpu(), "v_lo": self.g.v_lo, "v_hi": self.g.v_hi}
+
+    def load_state_dict(self, sd: dict):
+        if (int(sd["v_lo"]), int(sd["v_hi"])) != (self.g.v_lo, self.g.v_hi):
+            raise ValueError("checkpoint was written with a different vertex partition")
+        self.t = int(sd["t"])
+        self.r.copy_(sd["r"].to(self.dev))
+        self.c_slice.copy_(sd["c_slice"].to(self.dev))
+        self.dang.copy_(sd["dang"].to(self.dev))
+
     def ranks_local(self):
         """(vertex ids, ranks) of this rank's present vertices."""
         if self.mode == 0:

@@ -25,6 +25,15 @@ def common_parser(description: str) -> argparse.ArgumentParser:
     return ap
 
 
+def add_ckpt_args(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
+    """--ckpt-dir / --ckpt-every / --resume (the reference has none)."""
+    ap.add_argument("--ckpt-dir", default=None, help="checkpoint directory")
+    ap.add_argument("--ckpt-every", type=int, default=0,
+                    help="checkpoint every K iterations (0: only at the end)")
+    ap.add_argument("--resume", action="store_true", help="continue from --ckpt-dir")
+    return ap
+
+
 def init_from_args(a, app_name: str) -> runtime.Runtime:
     dev = None if a.device == "auto" else a.device
     if dev is None and a.backend == "gloo":

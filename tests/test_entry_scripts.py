@@ -92,6 +92,26 @@ def test_checkpoint_resume(tmp_path):
     assert fw == rw
 
 
+@pytest.mark.parametrize("script,args,final", [
+    ("machine_learning/k-means.py", ["--synthetic", "3000,4", "--k", "5", "--n-iterations", "6"],
+     "Final centers:"),
+    ("graph_computation/pagerank.py", ["--rmat-scale", "9", "--top", "5", "--n-iterations", "6"],
+     "has rank:"),
+    ("matrix_computation/matrix_decomposition.py", ["--n-iterations", "6"], "iterations: 5, rmse:"),
+])
+def test_checkpoint_resume_other_apps(tmp_path, script, args, final):
+    """Run 6 iterations straight vs. 3 + resume to 6: identical final output."""
+    ck = str(tmp_path / "ck")
+    base = [script, "--device", "cpu", "--no-plot"]
+    full = _run(base + args)
+    short = [x if x != "6" else "3" for x in args]
+    _run(base + short + ["--ckpt-dir", ck])
+    resumed = _run(base + args + ["--ckpt-dir", ck, "--resume"])
+    assert "Resumed from iteration 3" in resumed
+    tail = lambda out: out[out.index(final):]
+    assert tail(full) == tail(resumed)
+
+
 def test_bench_cpu_contract():
     out = _run(["bench.py", "--device", "cpu", "--rows", "20000", "--dim", "64", "--steps", "3",
                 "--warmup", "1", "--dtype", "f32"])
