@@ -86,6 +86,11 @@ def main(argv=None):
     elapsed = time.perf_counter() - t_start
     samples = model.global_sample_count()
     model.count_acc = None
+    xg = getattr(getattr(model, "bucket", None), "xg", None)
+    if xg is not None:
+        xg.check()   # raise (non-zero exit) if a peer wait ever timed out
+    allreduce = "xgmi-oneshot (K11)" if xg is not None else (
+        f"{rt.backend}" if W > 1 else "none (1 rank)")
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=rt.device)
     comm.all_reduce_max(el)
@@ -112,7 +117,8 @@ def main(argv=None):
             "data": f"synthetic (on-device Philox planted logistic model, {a.rows}x{a.dim}, random-init w)",
             "config": {"model": f"{a.algo.upper()} logistic regression", "global_batch": int(round(samples / a.steps)),
                        "seq_len": None, "features": a.dim, "rows": a.rows,
-                       "minibatch_fraction": a.frac, "parallelism": f"dp{W}"},
+                       "minibatch_fraction": a.frac, "parallelism": f"dp{W}",
+                       "allreduce": allreduce},
             "per_gpu_samples_per_s": value / W,
             "effective_hbm_GBps_per_gpu": value / W * a.dim * (2 if dtype == torch.bfloat16 else 4) / 1e9,
             "datagen_s": gen_s,
