@@ -37,10 +37,29 @@ def rank() -> int:
     return dist.get_rank() if _active() else 0
 
 
+def _xgmi_for(t: torch.Tensor):
+    """The K11 one-shot all-reduce if ``t`` is a small contiguous f32 GPU vector."""
+    if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+        return None
+    from dalgo.parallel import xgmi
+    if t.numel() > xgmi.SLOT_FLOATS:
+        return None
+    return xgmi.shared(t.device)   # collective on first use; None if disabled / failed
+
+
 def all_reduce_sum(t: torch.Tensor, async_op: bool = False):
-    """In-place SUM all-reduce (identity at world size 1)."""
+    """In-place SUM all-reduce (identity at world size 1).
+
+    Latency-bound vectors (f32, <= 4096 floats, on GPU) take the K11 one-shot
+    xGMI path (rank-ordered sum, identical on every rank); everything else RCCL.
+    """
     if not _active():
         return t
+    if not async_op:
+        xg = _xgmi_for(t)
+        if xg is not None:
+            xg.all_reduce_(t)
+            return t
     work = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=async_op)
     return work if async_op else t
 
@@ -127,11 +146,7 @@ class BucketedAllReduce:
             off += n
         # latency-bound GPU buckets go through the K11 one-shot xGMI all-reduce
         # (collective decision: all ranks or none; RCCL otherwise)
-        self.xg = None
-        if (allow_xgmi and _active() and self.buffer.is_cuda and dtype == torch.float32):
-            from dalgo.parallel import xgmi
-            if self.buffer.numel() <= xgmi.SLOT_FLOATS:
-                self.xg = xgmi.shared(self.buffer.device)
+        self.xg = _xgmi_for(self.buffer) if (allow_xgmi and _active()) else None
 
     def all_reduce(self, async_op: bool = False):
         if self.xg is not None:
