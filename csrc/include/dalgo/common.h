@@ -44,13 +44,17 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
 // ---------------------------------------------------------------------------
 struct u32x4 { uint32_t x, y, z, w; };
 
-__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+__host__ __device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)a * b) >> 32);   // v_mul_hi_u32 on the device
+}
+
+__host__ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
   const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
-    uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    uint32_t hi0 = mulhi32(M0, c.x), lo0 = M0 * c.x;
+    uint32_t hi1 = mulhi32(M1, c.z), lo1 = M1 * c.z;
     u32x4 n;
     n.x = hi1 ^ c.y ^ k0;
     n.y = lo1;
@@ -67,7 +71,7 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1
 // draw(seed, stream, i) = philox(counter = {i>>2 (64 bit), stream (64 bit)},
 //                                key = seed (64 bit))[i & 3]
 // One Philox call therefore serves 4 consecutive indices.
-__device__ __forceinline__ u32x4 philox_block(uint64_t seed, uint64_t stream, uint64_t block) {
+__host__ __device__ __forceinline__ u32x4 philox_block(uint64_t seed, uint64_t stream, uint64_t block) {
   u32x4 c{(uint32_t)block, (uint32_t)(block >> 32), (uint32_t)stream, (uint32_t)(stream >> 32)};
   return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
