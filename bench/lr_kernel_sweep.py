@@ -78,6 +78,21 @@ def main():
                 torch.cuda.synchronize()
                 dt = (time.perf_counter() - t0) / 5
                 print(json.dumps({"ref": f"hbm_read grid={grid} unroll={unroll}", "GBps": nbytes / dt / 1e9}))
+    if a.ref:
+        # the minibatch access shape itself: the same Bernoulli(frac) rows, sorted
+        from dalgo.utils import philox  # noqa: F401  (documents the sampling stream)
+        n = X.shape[0]
+        sel = torch.nonzero(torch.rand(n, device=dev) < a.frac).flatten().to(torch.int32)
+        o = torch.zeros(1, dtype=torch.int32, device=dev)
+        for grid in (512, 1024, 2048, 4096, 8192):
+            torch.ops.dalgo.hbm_gather_rows(X, sel, o, grid); torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(10):
+                torch.ops.dalgo.hbm_gather_rows(X, sel, o, grid)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / 10
+            print(json.dumps({"ref": f"gather_rows grid={grid}", "rows": int(sel.numel()),
+                              "GBps": sel.numel() * X.stride(0) * 2 / dt / 1e9, "us": dt * 1e6}))
     out = []
     for arm, ts in res.items():
         ts.sort()

@@ -233,6 +233,25 @@ void mc_pi(int64_t seed, int64_t stream, int64_t offset, int64_t n, Tensor count
                   "mc_pi");
 }
 
+void hbm_gather_rows(const Tensor& X, const Tensor& idx, Tensor out, int64_t grid) {
+  check_dev(X, "X");
+  check_dev(idx, "idx");
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1 && X.stride(0) * X.element_size() >= 2048,
+              "X: 2-D with >= 2 KB rows");
+  TORCH_CHECK(idx.scalar_type() == at::kInt && idx.is_contiguous(), "idx int32");
+  if (idx.numel() > 0) {
+    const int64_t mx = idx.max().item<int>(), mn = idx.min().item<int>();
+    TORCH_CHECK(mn >= 0 && mx < X.size(0), "idx out of range");
+  }
+  TORCH_CHECK(out.scalar_type() == at::kInt && out.numel() >= 1, "out int32[1]");
+  DeviceGuard guard(X.device());
+  DALGO_CHECK_HIP(dalgo_hbm_gather_rows(X.data_ptr(), X.stride(0) * X.element_size(),
+                                        idx.data_ptr<int>(), idx.numel(),
+                                        reinterpret_cast<uint32_t*>(out.data_ptr<int>()), (int)grid,
+                                        cur_stream()),
+                  "hbm_gather_rows");
+}
+
 void hbm_read(const Tensor& src, Tensor out, int64_t unroll) {
   check_dev(src, "src");
   check_dev(out, "out");
@@ -565,6 +584,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("tc_step(Tensor A, Tensor Told, Tensor(a!) Tnew, Tensor(b!) count, int variant=0) -> ()");
   m.def("spd_inverse(Tensor G, float ridge, Tensor(a!) out, Tensor(b!)? status) -> ()");
   m.def("hbm_read(Tensor src, Tensor(a!) out, int unroll=8) -> ()");
+  m.def("hbm_gather_rows(Tensor X, Tensor idx, Tensor(a!) out, int grid=2048) -> ()");
   m.def("mc_pi(int seed, int stream, int offset, int n, Tensor(a!) count) -> ()");
 }
 
@@ -577,6 +597,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("philox_fill", &philox_fill);
   m.impl("mc_pi", &mc_pi);
   m.impl("hbm_read", &hbm_read);
+  m.impl("hbm_gather_rows", &hbm_gather_rows);
   m.impl("spd_inverse", &spd_inverse);
   m.impl("tc_step", &tc_step);
   m.impl("xgmi_allreduce", &xgmi_allreduce);

@@ -112,6 +112,33 @@ hbm_read_blocked_kernel(const uint4* __restrict__ p, int64_t n16, uint32_t* __re
   if (threadIdx.x == 0) out[blockIdx.x] = acc;
 }
 
+// Probe: the access shape of the SGD minibatch (a sorted list of selected 2-KB rows,
+// ~10 % of the matrix): each wave streams whole rows, 4 rows (8 KB) in flight per
+// wave; the ceiling any K1 design can reach for this pattern.
+__global__ void __launch_bounds__(256)
+hbm_gather_rows_kernel(const uint4* __restrict__ X, int64_t ld16, const int* __restrict__ idx,
+                       int64_t nidx, uint32_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  uint32_t acc = 0;
+  for (; w < nidx; w += 4 * nw) {
+    uint4 v[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t k = min(w + u * nw, nidx - 1);
+      const uint4* row = X + (int64_t)idx[k] * ld16;
+      v[u][0] = row[lane];
+      v[u][1] = row[64 + lane];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      acc ^= v[u][0].x ^ v[u][0].w ^ v[u][1].y ^ v[u][1].z;
+  }
+  acc = wave_sum_u32(acc);
+  if ((threadIdx.x & 63) == 0) atomicXor(out, acc);
+}
+
 }  // namespace dalgo
 
 using namespace dalgo;
@@ -141,6 +168,15 @@ hipError_t dalgo_mc_pi(uint64_t seed, uint64_t stream, uint64_t offset, uint64_t
   const int grid = (int)std::min<uint64_t>((nblk + 255) / 256, 256 * 8);
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL(mc_pi_kernel, dim3(grid), dim3(256), 0, st, seed, stream, offset, n, count);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t dalgo_hbm_gather_rows(const void* X, int64_t ld_bytes, const int* idx, int64_t nidx,
+                                 uint32_t* out, int grid, hipStream_t st) {
+  if (ld_bytes % 16 || ld_bytes < 2048) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(hbm_gather_rows_kernel, dim3(grid), dim3(256), 0, st, (const uint4*)X,
+                     ld_bytes / 16, idx, nidx, out);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
