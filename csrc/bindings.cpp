@@ -486,7 +486,9 @@ void xgmi_close(int64_t ptr) {
 }
 
 void xgmi_allreduce(Tensor x, at::IntArrayRef bufs, int64_t rank, int64_t slot, int64_t epoch,
-                    Tensor err, double timeout_s) {
+                    Tensor err, double timeout_s, const std::optional<Tensor>& W, int64_t upd_mode,
+                    int64_t upd_reg, double eta, double lam, double reg_alpha, int64_t count_index,
+                    const std::optional<Tensor>& count_acc) {
   check_f32(x, "x");
   TORCH_CHECK(x.numel() <= slot, "xgmi_allreduce: vector larger than the slot");
   TORCH_CHECK(bufs.size() >= 1 && bufs.size() <= 8 && rank >= 0 && rank < (int64_t)bufs.size(),
@@ -496,11 +498,27 @@ void xgmi_allreduce(Tensor x, at::IntArrayRef bufs, int64_t rank, int64_t slot, 
   TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() >= 1, "err int32[1]");
   void* b[8] = {};
   for (size_t r = 0; r < bufs.size(); ++r) b[r] = reinterpret_cast<void*>(bufs[r]);
+  float* w = nullptr;
+  int nw = 0;
+  if (W.has_value()) {
+    check_f32(*W, "W");
+    nw = (int)W->numel();
+    TORCH_CHECK(count_index >= nw && count_index < x.numel(),
+                "xgmi_allreduce: the count must follow the model-sized gradient in x");
+    w = W->data_ptr<float>();
+  }
+  double* cacc = nullptr;
+  if (count_acc.has_value()) {
+    check_dev(*count_acc, "count_acc");
+    TORCH_CHECK(count_acc->scalar_type() == at::kDouble && count_acc->numel() >= 1, "count_acc f64");
+    cacc = count_acc->data_ptr<double>();
+  }
   DeviceGuard guard(x.device());
   DALGO_CHECK_HIP(dalgo_xgmi_allreduce(x.data_ptr<float>(), x.data_ptr<float>(), (int)x.numel(),
                                        (int)rank, (int)bufs.size(), b, (int)slot, (uint32_t)epoch,
                                        reinterpret_cast<unsigned*>(err.data_ptr<int>()), timeout_s,
-                                       cur_stream()),
+                                       w, nw, (int)count_index, (int)upd_mode, (int)upd_reg,
+                                       (float)eta, (float)lam, (float)reg_alpha, cacc, cur_stream()),
                   "xgmi_allreduce");
 }
 
@@ -580,7 +598,8 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("xgmi_open(Tensor handle, int device) -> int", &xgmi_open);
   m.def("xgmi_close(int ptr) -> ()", &xgmi_close);
   m.def("xgmi_allreduce(Tensor(a!) x, int[] bufs, int rank, int slot, int epoch, Tensor(b!) err, "
-        "float timeout_s) -> ()");
+        "float timeout_s, Tensor(c!)? W=None, int upd_mode=0, int upd_reg=0, float eta=0., "
+        "float lam=0., float reg_alpha=0., int count_index=-1, Tensor(d!)? count_acc=None) -> ()");
   m.def("tc_step(Tensor A, Tensor Told, Tensor(a!) Tnew, Tensor(b!) count, int variant=0) -> ()");
   m.def("spd_inverse(Tensor G, float ridge, Tensor(a!) out, Tensor(b!)? status) -> ()");
   m.def("hbm_read(Tensor src, Tensor(a!) out, int unroll=8) -> ()");

@@ -37,7 +37,25 @@ struct XgParams {
   uint32_t epoch;
   unsigned* err;
   long long timeout_ticks;      // s_memrealtime ticks (100 MHz)
+  // optional fused K8 (SSGD / full-batch GD on the [g (ldw) || count] bucket):
+  // W[0..nw) is updated from the reduced sums and the bucket is left zeroed for
+  // the next atomic-epilogue K1 (one launch instead of all-reduce + update)
+  float* W;                     // nullptr: plain all-reduce
+  int nw, cidx, upd_mode, upd_reg;   // cidx: index of the count in the vector
+  float eta, lam, reg_alpha;
+  double* count_acc;
 };
+
+__device__ __forceinline__ float xg_update(float w, float g, float c, const XgParams& p) {
+  if (p.upd_mode == 1) return w - p.eta * g;                    // GD: sum, not mean
+  const float gm = c > 0.f ? g / c : 0.f;
+  float r = 0.f;
+  const float sg = (w > 0.f) ? 1.f : (w < 0.f ? -1.f : 0.f);
+  if (p.upd_reg == 1) r = w;
+  else if (p.upd_reg == 2) r = sg;
+  else if (p.upd_reg == 3) r = p.reg_alpha * sg + (1.f - p.reg_alpha) * w;
+  return w - p.eta * (gm + p.lam * r);
+}
 
 __device__ __forceinline__ uint32_t* xg_flags(uint8_t* b) { return reinterpret_cast<uint32_t*>(b); }
 __device__ __forceinline__ float* xg_slot(uint8_t* b, int ph, int src, int slot) {
@@ -75,11 +93,19 @@ __global__ void __launch_bounds__(1024) xgmi_allreduce_kernel(XgParams p) {
   __syncthreads();
   // 4. reduce in rank order (identical on every rank)
   uint8_t* mine = p.bufs[p.rank];
-  for (int i = tid; i < p.n; i += blockDim.x) {
+  auto reduced = [&](int i) {
     float s = 0.f;
     for (int r = 0; r < p.world; ++r) s += __builtin_nontemporal_load(xg_slot(mine, ph, r, p.slot) + i);
-    p.out[i] = s;
+    return s;
+  };
+  if (p.W == nullptr) {
+    for (int i = tid; i < p.n; i += blockDim.x) p.out[i] = reduced(i);
+    return;
   }
+  const float c = reduced(p.cidx);                 // the global minibatch size
+  for (int i = tid; i < p.nw; i += blockDim.x) p.W[i] = xg_update(p.W[i], reduced(i), c, p);
+  for (int i = tid; i < p.n; i += blockDim.x) p.out[i] = 0.f;
+  if (tid == 0 && p.count_acc) p.count_acc[0] += (double)c;
 }
 
 }  // namespace dalgo
@@ -115,7 +141,10 @@ hipError_t dalgo_xgmi_close(void* ptr) { return hipIpcCloseMemHandle(ptr); }
 
 hipError_t dalgo_xgmi_allreduce(const float* in, float* out, int n, int rank, int world,
                                 void* const* bufs, int slot, uint32_t epoch, unsigned* err,
-                                double timeout_s, hipStream_t st) {
+                                double timeout_s, float* W, int nw, int cidx, int upd_mode,
+                                int upd_reg, float eta, float lam, float reg_alpha,
+                                double* count_acc, hipStream_t st) {
+  if (W != nullptr && (cidx < 0 || cidx >= n || nw > cidx)) return hipErrorInvalidValue;
   if (world < 1 || world > kXgMaxRanks || rank < 0 || rank >= world || n < 0 || n > slot ||
       epoch == 0)
     return hipErrorInvalidValue;
@@ -127,6 +156,8 @@ hipError_t dalgo_xgmi_allreduce(const float* in, float* out, int n, int rank, in
   p.in = in; p.out = out; p.n = n; p.rank = rank; p.world = world; p.slot = slot;
   p.epoch = epoch; p.err = err;
   p.timeout_ticks = (long long)(timeout_s * 1e8);
+  p.W = W; p.nw = nw; p.cidx = cidx; p.upd_mode = upd_mode; p.upd_reg = upd_reg;
+  p.eta = eta; p.lam = lam; p.reg_alpha = reg_alpha; p.count_acc = count_acc;
   hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(1), dim3(1024), 0, st, p);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;

@@ -83,6 +83,8 @@ hipError_t dalgo_xgmi_open(const void* handle, void** ptr);
 hipError_t dalgo_xgmi_close(void* ptr);
 hipError_t dalgo_xgmi_allreduce(const float* in, float* out, int n, int rank, int world,
                                 void* const* bufs, int slot, uint32_t epoch, unsigned* err,
-                                double timeout_s, hipStream_t st);
+                                double timeout_s, float* W, int nw, int cidx, int upd_mode,
+                                int upd_reg, float eta, float lam, float reg_alpha,
+                                double* count_acc, hipStream_t st);
 
 }  // extern "C"

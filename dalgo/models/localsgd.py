@@ -206,6 +206,16 @@ class ParallelSGD:
             self._pending = True
         elif c.algo in ("ssgd", "gd"):
             self._grad(self.w, t)
+            xg = self.bucket.xg
+            if xg is not None and self._zg:
+                # K11 all-reduce + K8 update in one launch; leaves the bucket zeroed
+                xg.all_reduce_update_(self.bucket.buffer, self.w, mode=0 if c.algo == "ssgd" else 1,
+                                      reg=self._upd["reg"], eta=c.eta, lam=c.lam,
+                                      reg_alpha=c.reg_alpha, count_index=self.ldw,
+                                      count_acc=self.count_acc)
+                self._g_zero = True
+                self.t += 1
+                return
             self.bucket.all_reduce()
             if c.algo == "ssgd":
                 U.sync_update(self.w, U.SSGD, G=self.G, C=self.C, reg=c.reg, eta=c.eta,

@@ -98,6 +98,20 @@ class XgmiAllReduce:
                                  self.timeout_s)
         return x
 
+    def all_reduce_update_(self, x: torch.Tensor, W: torch.Tensor, *, mode: int, reg: int = 0,
+                           eta: float = 0.0, lam: float = 0.0, reg_alpha: float = 0.0,
+                           count_index: int, count_acc: torch.Tensor | None = None) -> torch.Tensor:
+        """All-reduce the ``[g || count]`` bucket ``x`` and apply the SSGD (mode 0) or
+        full-batch GD (mode 1) update to ``W`` in the same launch (fused K8); ``x`` is
+        left ZEROED, ready for the next atomic-epilogue gradient kernel."""
+        self.epoch += 1
+        if self.epoch >= 1 << 32:
+            raise RuntimeError("xGMI all-reduce epoch space exhausted")
+        self._ops.xgmi_allreduce(x, self.bufs, self.rank, self.slot, self.epoch, self.err,
+                                 self.timeout_s, W, int(mode), int(reg), float(eta), float(lam),
+                                 float(reg_alpha), int(count_index), count_acc)
+        return x
+
     def check(self):
         if int(self.err.item()) != 0:
             raise RuntimeError("xGMI all-reduce: a peer flag wait timed out (results invalid)")

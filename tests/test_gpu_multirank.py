@@ -60,3 +60,26 @@ def test_xgmi_allreduce_ranks_on_one_gpu(cuda, n):
     """K11: IPC exchange buffers + flag protocol, exact rank-ordered sums on every rank."""
     out = _torchrun(["tests/helpers/xgmi_check.py"], n=n)
     assert f"XGMI_OK world={n}" in out
+
+
+def _final_w(out):
+    import numpy as np
+    txt = out.split("Final w:")[1].split("Final acc")[0]
+    return np.array([float(v) for v in txt.replace("[", " ").replace("]", " ").split()])
+
+
+@pytest.mark.parametrize("algo", ["ssgd", "logistic_regression"])
+def test_fused_xgmi_update_matches_process_group(cuda, algo):
+    """SSGD / full-batch GD: K11 all-reduce + fused K8 == gloo all-reduce + separate K8."""
+    import numpy as np
+    script = "optimization/ssgd.py" if algo == "ssgd" else "machine_learning/logistic_regression.py"
+    args = [script, "--device", "cuda", "--backend", "gloo", "--no-plot", "--quiet",
+            "--synthetic", "40000,64", "--n-iterations", "30", "--dtype", "f32"]
+    fused = _torchrun(args)
+    os.environ["DALGO_XGMI"] = "0"
+    try:
+        plain = _torchrun(args)
+    finally:
+        del os.environ["DALGO_XGMI"]
+    wf, wp = _final_w(fused), _final_w(plain)
+    assert wf.shape == wp.shape and np.allclose(wf, wp, rtol=1e-4, atol=1e-5), (wf[:5], wp[:5])
