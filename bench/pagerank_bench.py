@@ -24,6 +24,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--semantics", default="reference")
     ap.add_argument("--no-reorder", action="store_true", help="keep scrambled R-MAT vertex ids")
+    ap.add_argument("--spmv", default="pull", choices=["pull", "blocked"])
+    ap.add_argument("--bin-width", type=int, default=16384)
+    ap.add_argument("--chunk", type=int, default=1 << 18)
+    ap.add_argument("--tile", type=int, default=1 << 16)
     a = ap.parse_args()
     from dalgo.apps.pagerank_app import rmat_shard
     from dalgo.models.pagerank import PageRank, PageRankConfig
@@ -36,7 +40,8 @@ def main():
     torch.cuda.synchronize()
     build_s = time.time() - t0
     E = comm.all_reduce_count(shard.n_edges, device=rt.device)
-    pr = PageRank(PageRankConfig(semantics=a.semantics), shard, W)
+    pr = PageRank(PageRankConfig(semantics=a.semantics, spmv=a.spmv, bin_width=a.bin_width,
+                                 chunk=a.chunk, tile=a.tile), shard, W)
     for _ in range(a.warmup):
         pr.step()
     torch.cuda.synchronize()
@@ -45,7 +50,10 @@ def main():
     comm.all_gather_into(pr.c_full, pr.c_slice)
     ev[1].record()
     pr.acc.zero_(); pr.pres.zero_()
-    G.pr_spmv(pr.g, pr.c_full, pr.acc, pr.pres)
+    if pr.layout is not None:
+        G.pb_spmv(pr.layout, pr.c_full, pr.acc, pr.pres)
+    else:
+        G.pr_spmv(pr.g, pr.c_full, pr.acc, pr.pres)
     ev[2].record()
     G.pr_update(pr.acc, pr.pres, pr.outdeg, 0.15, pr.invN, pr.mode, pr.r, pr.c_slice[: shard.n_local])
     ev[3].record()
@@ -63,7 +71,7 @@ def main():
         print(json.dumps({
             "metric": "PageRank edges/sec (whole node)", "value": E / (ms / 1e3), "unit": "edges/s",
             "n_gpus": W, "ms_per_iter": ms, "edges_dedup": E, "edges_generated": n_gen,
-            "vertices": 1 << a.scale, "degree_reordered": not a.no_reorder, "phases_ms_rank0": phases, "graph_build_s": build_s,
+            "vertices": 1 << a.scale, "degree_reordered": not a.no_reorder, "spmv": pr.spmv, "phases_ms_rank0": phases, "graph_build_s": build_s,
             "spmv_GBps_stream": shard.n_edges * 8 / (phases["spmv"] / 1e3) / 1e9}), flush=True)
     runtime.shutdown()
 

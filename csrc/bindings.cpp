@@ -428,6 +428,51 @@ void pr_spmv(const Tensor& src, const Tensor& dstl, const Tensor& c, Tensor acc,
                   "pr_spmv");
 }
 
+// Propagation-blocked SpMV. The layout invariants (slot < val.numel(), src < c.numel(),
+// dloc < bin_width, chunk bounds inside val) are established and asserted once when
+// dalgo.ops.graph.build_blocked() creates the layout; here shapes/dtypes are checked.
+void pb_spmv(const Tensor& psrc, const Tensor& ppos, const Tensor& c, Tensor val, const Tensor& dloc,
+             const Tensor& chunk_lo4, const Tensor& chunk_bin, const Tensor& chunk_slab,
+             int64_t bin_width, Tensor acc, Tensor pres, Tensor slab, const Tensor& split_bin,
+             const Tensor& split_first, const Tensor& split_count) {
+  check_i32(psrc, "psrc");
+  check_i32(ppos, "ppos");
+  TORCH_CHECK(psrc.numel() == ppos.numel() && psrc.numel() % 4 == 0, "pb: src/pos equal, % 4");
+  check_f32(c, "c");
+  check_f32(val, "val");
+  check_dev(dloc, "dloc");
+  TORCH_CHECK(dloc.scalar_type() == at::kShort && dloc.is_contiguous() && dloc.numel() == val.numel() &&
+                  val.numel() % 4 == 0, "pb: dloc int16[len(val)], len % 4 == 0");
+  check_dev(chunk_lo4, "chunk_lo4");
+  TORCH_CHECK(chunk_lo4.scalar_type() == at::kLong && chunk_lo4.is_contiguous(), "chunk_lo4 int64");
+  check_i32(chunk_bin, "chunk_bin");
+  check_i32(chunk_slab, "chunk_slab");
+  const int64_t nch = chunk_bin.numel();
+  TORCH_CHECK(chunk_slab.numel() == nch && chunk_lo4.numel() == nch + 1, "pb: chunk arrays");
+  check_f32(acc, "acc");
+  check_i32(pres, "pres");
+  TORCH_CHECK(pres.numel() >= acc.numel(), "pres size");
+  check_f32(slab, "slab");
+  check_i32(split_bin, "split_bin");
+  check_i32(split_first, "split_first");
+  check_i32(split_count, "split_count");
+  const int64_t nsp = split_bin.numel();
+  TORCH_CHECK(split_first.numel() == nsp && split_count.numel() == nsp, "pb: split arrays");
+  for (const Tensor* t : {&psrc, &ppos, static_cast<const Tensor*>(&val), &dloc})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "pb arrays 16-B aligned");
+  DeviceGuard guard(psrc.device());
+  DALGO_CHECK_HIP(dalgo_pb_spmv(psrc.data_ptr<int32_t>(), ppos.data_ptr<int32_t>(), psrc.numel(),
+                                c.data_ptr<float>(), val.data_ptr<float>(),
+                                reinterpret_cast<const uint16_t*>(dloc.data_ptr<int16_t>()),
+                                chunk_lo4.data_ptr<int64_t>(), chunk_bin.data_ptr<int32_t>(),
+                                chunk_slab.data_ptr<int32_t>(), (int)nch, (int)bin_width,
+                                acc.numel(), acc.data_ptr<float>(), pres.data_ptr<int32_t>(),
+                                slab.data_ptr<float>(), split_bin.data_ptr<int32_t>(),
+                                split_first.data_ptr<int32_t>(), split_count.data_ptr<int32_t>(),
+                                (int)nsp, cur_stream()),
+                  "pb_spmv");
+}
+
 void pr_update(const Tensor& acc, const Tensor& pres, const Tensor& outdeg, double q, double invN,
                int64_t mode, const std::optional<Tensor>& dangling_in, Tensor r, Tensor c,
                const std::optional<Tensor>& dangling_out) {
@@ -588,6 +633,9 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(d!)? shift2) -> ()");
   m.def("rmat_edges(int seed, int scale, int e_off, float a, float b, float c, bool scramble, "
         "Tensor(a!) src, Tensor(b!) dst) -> ()");
+  m.def("pb_spmv(Tensor psrc, Tensor ppos, Tensor c, Tensor(a!) val, Tensor dloc, Tensor chunk_lo4, "
+        "Tensor chunk_bin, Tensor chunk_slab, int bin_width, Tensor(b!) acc, Tensor(c!) pres, "
+        "Tensor(d!) slab, Tensor split_bin, Tensor split_first, Tensor split_count) -> ()");
   m.def("pr_spmv(Tensor src, Tensor dstl, Tensor c, Tensor(a!) acc, Tensor(b!) pres) -> ()");
   m.def("pr_update(Tensor acc, Tensor pres, Tensor outdeg, float q, float invN, int mode, "
         "Tensor? dangling_in, Tensor(a!) r, Tensor(b!) c, Tensor(c!)? dangling_out) -> ()");
@@ -622,6 +670,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("xgmi_allreduce", &xgmi_allreduce);
   m.impl("rmat_edges", &rmat_edges);
   m.impl("pr_spmv", &pr_spmv);
+  m.impl("pb_spmv", &pb_spmv);
   m.impl("pr_update", &pr_update);
   m.impl("kmeans_assign", &kmeans_assign);
   m.impl("kmeans_accumulate", &kmeans_accumulate);

@@ -62,6 +62,12 @@ hipError_t dalgo_rmat(uint64_t seed, int scale, int64_t e_off, int64_t n, float 
                       int do_scramble, int32_t* src, int32_t* dst, hipStream_t st);
 hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, const float* c,
                          float* acc, int32_t* pres, hipStream_t st);
+hipError_t dalgo_pb_spmv(const int32_t* psrc, const int32_t* ppos, int64_t E4, const float* c,
+                         float* val, const uint16_t* dloc, const int64_t* chunk_lo4,
+                         const int32_t* chunk_bin, const int32_t* chunk_slab, int nchunks,
+                         int bin_width, int64_t n_local, float* acc, int32_t* pres, float* slab,
+                         const int32_t* split_bin, const int32_t* split_first,
+                         const int32_t* split_count, int nsplit, hipStream_t st);
 hipError_t dalgo_pr_update(const float* acc, const int32_t* pres, const int32_t* outdeg, int64_t n,
                            float q, float invN, int mode, const float* dangling_in, float* r,
                            float* c, float* dangling_out, hipStream_t st);

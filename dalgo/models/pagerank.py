@@ -14,6 +14,7 @@ vertices and dangling mass redistributed.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -27,6 +28,10 @@ class PageRankConfig:
     q: float = 0.15              # teleport probability (pagerank.py:19)
     n_iterations: int = 10       # pagerank.py:18
     semantics: str = "reference"  # "reference" | "standard"
+    spmv: str = ""               # "pull" | "blocked" ("" = DALGO_PR_SPMV env, default pull)
+    bin_width: int = 16384       # blocked: destination vertices per LDS bin
+    chunk: int = 1 << 18         # blocked: max edge slots per workgroup
+    tile: int = 1 << 16          # blocked: phase-1 edges per slot-sorted tile
 
 
 class PageRank:
@@ -43,6 +48,9 @@ class PageRank:
         comm.all_reduce_sum(od_full)
         self.outdeg = od_full[shard.v_lo: shard.v_hi].contiguous()
         self.mode = 0 if cfg.semantics == "reference" else 1
+        self.spmv = cfg.spmv or os.environ.get("DALGO_PR_SPMV", "pull")
+        self.layout = (Gops.build_blocked(shard, cfg.bin_width, cfg.chunk, cfg.tile)
+                       if self.spmv == "blocked" else None)
         if self.mode == 0:
             self.N = int((od_full > 0).sum().item())
         else:
@@ -77,7 +85,10 @@ class PageRank:
         comm.all_gather_into(self.c_full, self.c_slice)
         self.acc.zero_()
         self.pres.zero_()
-        Gops.pr_spmv(self.g, self.c_full, self.acc, self.pres)
+        if self.layout is not None:
+            Gops.pb_spmv(self.layout, self.c_full, self.acc, self.pres)
+        else:
+            Gops.pr_spmv(self.g, self.c_full, self.acc, self.pres)
         nl = self.g.n_local
         if self.mode == 1:
             self.dang_next.zero_()

@@ -131,6 +131,125 @@ def local_outdeg(shard: GraphShard) -> torch.Tensor:
     return torch.bincount(s, minlength=shard.n_vertices).to(torch.int32)
 
 
+# ------------------------------------------------------------------ propagation blocking
+@dataclass
+class BlockedLayout:
+    """Edge layout of the propagation-blocked SpMV (pb_spmv): see csrc/kernels/pagerank.hip.
+
+    psrc/ppos: phase-1 edge list (global src id, slot in the binned array) in
+    tile order: tiles of ``tile`` consecutive edges in SOURCE order, each tile
+    re-sorted by slot, so the c[src] reads of a tile stay inside a narrow source
+    range while its writes form contiguous runs per bin (coalesced stores).
+    val/dloc: the destination-binned array (value written per iteration, static
+    destination offset inside the bin; slots of a bin are in source order).
+    chunks: contiguous slot ranges of one bin; a bin longer than ``chunk`` slots
+    is split, its chunks write partial slabs that pb_combine sums in order."""
+    psrc: torch.Tensor
+    ppos: torch.Tensor
+    val: torch.Tensor
+    dloc: torch.Tensor
+    chunk_lo4: torch.Tensor
+    chunk_bin: torch.Tensor
+    chunk_slab: torch.Tensor
+    slab: torch.Tensor
+    split_bin: torch.Tensor
+    split_first: torch.Tensor
+    split_count: torch.Tensor
+    bin_width: int
+    n_local: int
+
+
+def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk: int = 1 << 18,
+                  tile: int = 1 << 16) -> BlockedLayout:
+    """One-time construction from a (dst, src)-sorted shard (device sorts)."""
+    if bin_width not in (8192, 16384):
+        raise ValueError("bin_width must be 8192 or 16384 (LDS accumulator sizes of the kernel)")
+    dev = shard.src.device
+    E = shard.n_edges
+    s = shard.src[:E].to(torch.int64)
+    d = shard.dstl[:E].to(torch.int64)
+    nl = shard.n_local
+    nbins = max(1, (nl + bin_width - 1) // bin_width)
+    b = d // bin_width
+    # slots: bins in order, inside a bin edges in source order, each bin padded to 4
+    order2 = torch.argsort(b * (shard.n_vertices + 1) + s, stable=True)
+    inv2 = torch.empty_like(order2)
+    inv2[order2] = torch.arange(E, device=dev)
+    del order2
+    cnt = torch.bincount(b, minlength=nbins)
+    start_u = torch.cumsum(cnt, 0) - cnt
+    cntp = (cnt + 3) // 4 * 4
+    start_p = torch.cumsum(cntp, 0) - cntp
+    Ep = max(int(cntp.sum().item()) if E else 0, 4)
+    pos = start_p[b] + (inv2 - start_u[b])
+    del inv2
+    val = torch.full((Ep,), -1.0, dtype=torch.float32, device=dev)
+    dloc = torch.zeros(Ep, dtype=torch.int16, device=dev)
+    dl = d - b * bin_width
+    dloc[pos] = dl.to(torch.int32).to(torch.int16)        # < 16384: fits int16 as is
+    # phase-1 order: source order, then slot order inside each tile
+    order1 = torch.argsort(s, stable=True)
+    pos1 = pos[order1]
+    t_id = torch.arange(E, device=dev) // max(1, tile)
+    order_t = torch.argsort(t_id * Ep + pos1)
+    E4 = (E + 3) // 4 * 4
+    psrc = torch.full((max(E4, 4),), -1, dtype=torch.int32, device=dev)
+    ppos = torch.zeros(max(E4, 4), dtype=torch.int32, device=dev)
+    psrc[:E] = s[order1][order_t].to(torch.int32)
+    ppos[:E] = pos1[order_t].to(torch.int32)
+    del order1, pos1, t_id, order_t
+    # chunks (host): split each non-empty bin into <= chunk-slot pieces (multiples of 4)
+    cntp_h = cntp.cpu().tolist()
+    start_h = start_p.cpu().tolist()
+    chunk = max(4, chunk // 4 * 4)
+    lo4, bins, slab_of, sp_bin, sp_first, sp_cnt = [], [], [], [], [], []
+    nslab = 0
+    for bi, (st, n) in enumerate(zip(start_h, cntp_h)):
+        if n == 0:
+            continue
+        pieces = list(range(st, st + n, chunk))
+        if len(pieces) > 1:
+            sp_bin.append(bi)
+            sp_first.append(nslab)
+            sp_cnt.append(len(pieces))
+        for p0 in pieces:
+            lo4.append(p0 // 4)
+            bins.append(bi)
+            if len(pieces) > 1:
+                slab_of.append(nslab)
+                nslab += 1
+            else:
+                slab_of.append(-1)
+    lo4.append(Ep // 4 if E else 0)
+    # the invariants the kernels rely on (checked once, here)
+    assert E == 0 or (int(pos.max()) < Ep and int(dl.max()) < bin_width and int(dl.min()) >= 0)
+    assert E == 0 or (int(s.min()) >= 0 and int(s.max()) < shard.n_vertices)
+    i32 = lambda x: torch.tensor(x, dtype=torch.int32, device=dev)
+    return BlockedLayout(psrc, ppos, val, dloc,
+                         torch.tensor(lo4, dtype=torch.int64, device=dev), i32(bins), i32(slab_of),
+                         torch.zeros(max(nslab, 1) * bin_width, dtype=torch.float32, device=dev),
+                         i32(sp_bin), i32(sp_first), i32(sp_cnt), bin_width, nl)
+
+
+def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: torch.Tensor):
+    """Same result as :func:`pr_spmv` (acc/pres zeroed by the caller)."""
+    if c_full.is_cuda:
+        _ext.ops().pb_spmv(lay.psrc, lay.ppos, c_full, lay.val, lay.dloc, lay.chunk_lo4,
+                           lay.chunk_bin, lay.chunk_slab, lay.bin_width, acc, pres, lay.slab,
+                           lay.split_bin, lay.split_first, lay.split_count)
+        return
+    # CPU reference of the two phases
+    m = lay.psrc >= 0
+    lay.val[lay.ppos[m].long()] = c_full[lay.psrc[m].long()]
+    lo = lay.chunk_lo4.tolist()
+    for k, bi in enumerate(lay.chunk_bin.tolist()):
+        v = lay.val[lo[k] * 4: lo[k + 1] * 4]
+        dd = lay.dloc[lo[k] * 4: lo[k + 1] * 4].long() + bi * lay.bin_width
+        keep = v >= 0
+        acc.index_add_(0, dd[keep], v[keep])
+        pres[dd[keep]] = 1
+
+
 # ------------------------------------------------------------------ K4 kernels
 def pr_spmv(shard: GraphShard, c_full: torch.Tensor, acc: torch.Tensor, pres: torch.Tensor):
     """acc[v] = sum_{u->v, c[u] >= 0} c[u];  pres[v] = any such edge  (acc/pres zeroed by caller)."""
