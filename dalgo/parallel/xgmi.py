@@ -14,7 +14,10 @@ itself all-reduced, so either every rank uses it or none does (falls back to
 RCCL). The device-side wait is bounded by a wall-clock timeout that sets an error
 word instead of hanging; :meth:`XgmiAllReduce.check` raises if it ever fired.
 
-Env: ``DALGO_XGMI=0`` disables it; ``DALGO_XGMI_TIMEOUT`` (s, default 60).
+Selection (``DALGO_XGMI``): ``auto`` (default) times K11 against the process
+group's all-reduce on a bucket-sized vector right after the self-test and keeps
+whichever is faster (max over ranks, so all ranks agree); ``1`` forces K11 (if the
+self-test passes), ``0`` disables it. ``DALGO_XGMI_TIMEOUT`` (s, default 60).
 """
 from __future__ import annotations
 
@@ -155,6 +158,27 @@ def _self_test(xg: XgmiAllReduce) -> bool:
 _shared: dict = {}
 
 
+def _race(xg: XgmiAllReduce, n: int = 1025, iters: int = 50) -> tuple[float, float]:
+    """(K11, process group) seconds for ``iters`` back-to-back all-reduces, max over ranks."""
+    import time
+    x = torch.zeros(n, dtype=torch.float32, device=xg.device)
+    out = []
+    for use_k11 in (True, False):
+        for _ in range(5):
+            xg.all_reduce_(x) if use_k11 else dist.all_reduce(x)
+        torch.cuda.synchronize(xg.device)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            xg.all_reduce_(x) if use_k11 else dist.all_reduce(x)
+        torch.cuda.synchronize(xg.device)
+        out.append(time.perf_counter() - t0)
+    t = torch.tensor(out, dtype=torch.float64,
+                     device=xg.device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0]), float(t[1])
+
+
 def shared(device: torch.device) -> XgmiAllReduce | None:
     """Process-wide K11 instance for the default group (collective on first call).
 
@@ -164,7 +188,8 @@ def shared(device: torch.device) -> XgmiAllReduce | None:
     if key in _shared:
         return _shared[key]
     inst = None
-    if (os.environ.get("DALGO_XGMI", "1") == "1" and dist.is_initialized()
+    mode = os.environ.get("DALGO_XGMI", "auto")
+    if (mode in ("1", "auto") and dist.is_initialized()
             and 1 < dist.get_world_size() <= MAX_RANKS and torch.device(device).type == "cuda"
             and _ext.available()):
         try:
@@ -181,6 +206,15 @@ def shared(device: torch.device) -> XgmiAllReduce | None:
                 ok = False
             if _agree(ok, device):
                 inst.timeout_s = float(os.environ.get("DALGO_XGMI_TIMEOUT", "60"))
+                if mode == "auto":
+                    t_k11, t_pg = _race(inst)
+                    if dist.get_rank() == 0:
+                        print(f"[dalgo] small all-reduce: xGMI one-shot {t_k11 / 50 * 1e6:.1f} us, "
+                              f"{dist.get_backend()} {t_pg / 50 * 1e6:.1f} us -> "
+                              f"{'xGMI' if t_k11 < t_pg else dist.get_backend()}", file=sys.stderr)
+                    if not t_k11 < t_pg:
+                        inst.close()
+                        inst = None
             else:
                 inst.close()
                 inst = None

@@ -19,6 +19,7 @@ def vec(it, r, n):
 
 
 def main():
+    os.environ["DALGO_XGMI"] = "1"             # force K11 (no timing race)
     rt = runtime.init(backend="gloo", device="cuda", app_name="xgmi-check")
     xg = xgmi.shared(rt.device)
     assert xg is not None, "xGMI all-reduce did not come up"

@@ -75,7 +75,11 @@ def test_fused_xgmi_update_matches_process_group(cuda, algo):
     script = "optimization/ssgd.py" if algo == "ssgd" else "machine_learning/logistic_regression.py"
     args = [script, "--device", "cuda", "--backend", "gloo", "--no-plot", "--quiet",
             "--synthetic", "40000,64", "--n-iterations", "30", "--dtype", "f32"]
-    fused = _torchrun(args)
+    os.environ["DALGO_XGMI"] = "1"
+    try:
+        fused = _torchrun(args)
+    finally:
+        del os.environ["DALGO_XGMI"]
     os.environ["DALGO_XGMI"] = "0"
     try:
         plain = _torchrun(args)
@@ -83,3 +87,11 @@ def test_fused_xgmi_update_matches_process_group(cuda, algo):
         del os.environ["DALGO_XGMI"]
     wf, wp = _final_w(fused), _final_w(plain)
     assert wf.shape == wp.shape and np.allclose(wf, wp, rtol=1e-4, atol=1e-5), (wf[:5], wp[:5])
+
+
+def test_bench_auto_selects_allreduce(cuda):
+    """DALGO_XGMI=auto (default): the start-up race picks a path and reports it."""
+    out = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--rows", "200000",
+                     "--steps", "5", "--warmup", "2"])
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+    assert d["config"]["allreduce"] in ("xgmi-oneshot (K11)", "gloo")
