@@ -63,6 +63,7 @@ struct LrParams {
   double* count_acc;    // optional: += local selected-row count of THIS step
   int atomic_out;       // 1: blocks add their partials to G/C with float atomics
                         //    (G/C zeroed by the caller; summation order not fixed)
+  int probe_no_epilogue;  // diagnostics only (variant bit 9): skip the block reduction
 };
 
 __device__ __forceinline__ float fused_update(float w, float g, float c, const LrParams& p) {
@@ -368,6 +369,10 @@ lr_rows_kernel(LrParams p) {
     }
   }
   __syncthreads();   // rings are dead: the arena becomes the reduction buffer
+  if (p.probe_no_epilogue) {
+    if (threadIdx.x == 0 && cntf < 0.f) p.C[0] = cntf + gb;   // keep the sweep live
+    return;
+  }
 
   if constexpr (EVAL) {
     __shared__ float s_ev[NW][2];
@@ -556,6 +561,7 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
   p.full = full; p.rows_per_block = rows_per_block; p.slab = slab; p.gslab = gslab;
   p.cnt1 = cnt1; p.cnt2 = cnt2; p.G = G; p.C = C; p.S = S;
   p.atomic_out = (variant >> 8) & 1;   // bit 8 of the variant selects the atomic epilogue
+  p.probe_no_epilogue = (variant >> 9) & 1;
   return dispatch_lr<false>(p, is_bf16, gx, nseg, variant & 0xff, st);
 }
 
