@@ -50,7 +50,7 @@ def main():
             for _ in range(a.reps):
                 step += 1
                 L.lr_grad(X, y, W, seg, D=a.dim, frac=a.frac, step=step, G=G, C=C,
-                          variant=arm[0], target_blocks=arm[1])
+                          variant=arm[0], target_blocks=arm[1], g_is_zero=True)
             torch.cuda.synchronize()
             res[arm].append((time.perf_counter() - t0) / a.reps)
     rows = a.rows * a.frac

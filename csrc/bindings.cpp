@@ -612,10 +612,10 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("lr_grad(Tensor X, Tensor y, Tensor(z!) W, Tensor seg, int row_offset, int D, bool has_bias, "
         "float eps, int seed, int step, float frac, int gx, int rows_per_block, Tensor(a!) slab, "
         "Tensor(b!) gslab, Tensor(c!) cnt1, Tensor(d!) cnt2, Tensor(e!) G, Tensor(f!) C, "
-        "int variant=6, Tensor? Wprev=None, int upd_mode=0, int upd_reg=0, float upd_eta=0., "
+        "int variant=3, Tensor? Wprev=None, int upd_mode=0, int upd_reg=0, float upd_eta=0., "
         "float upd_lam=0., float upd_reg_alpha=0., Tensor(g!)? count_acc=None) -> ()");
   m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
-        "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=6) -> ()");
+        "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=3) -> ()");
   m.def("sync_update(Tensor(a!) W, Tensor(d!)? G, Tensor(e!)? C, Tensor? center, Tensor? S, "
         "Tensor(b!)? Dl, Tensor(c!)? count_acc, int n, int mode, int reg, float eta, float lam, float alpha, "
         "float reg_alpha, float mu, float zeta, float beta, float inv_p, bool zero_grad=False) -> ()");

@@ -28,7 +28,7 @@ import os
 # Launch shape of the row-streaming kernels (tuned on MI355X, see profiles/):
 #   LR_VARIANT      = launch-shape variant (table in csrc/kernels/lr_grad.hip)
 #   TARGET_BLOCKS   = workgroups per launch (split over segments)
-LR_VARIANT = int(os.environ.get("DALGO_LR_VARIANT", "6"))
+LR_VARIANT = int(os.environ.get("DALGO_LR_VARIANT", "3"))   # 8 waves, pipelined (bench sweep)
 _TARGET_BLOCKS = int(os.environ.get("DALGO_LR_BLOCKS", "256"))
 #   DETERMINISTIC   = combine per-block partials with the fixed-order two-level
 #                     hand-off (bitwise repeatable) instead of float atomics
