@@ -77,8 +77,46 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
              double frac, int64_t gx, int64_t rows_per_block, Tensor slab, Tensor gslab,
              Tensor cnt1, Tensor cnt2, Tensor G, Tensor C, int64_t variant,
              const std::optional<Tensor>& Wprev, int64_t upd_mode, int64_t upd_reg, double upd_eta,
-             double upd_lam, double upd_reg_alpha, const std::optional<Tensor>& count_acc) {
+             double upd_lam, double upd_reg_alpha, const std::optional<Tensor>& count_acc,
+             const std::optional<Tensor>& ticket, at::OptionalIntArrayRef xg_bufs, int64_t xg_rank,
+             int64_t xg_slot, int64_t xg_epoch, const std::optional<Tensor>& xg_err,
+             double xg_timeout, int64_t tail_mode, int64_t tail_reg, double tail_eta,
+             double tail_lam, double tail_reg_alpha, const std::optional<Tensor>& tail_count_acc) {
   check_lr_inputs(X, y, W, seg, D, has_bias);
+  DalgoLrTail tail{};
+  const DalgoLrTail* tailp = nullptr;
+  if (ticket.has_value()) {
+    check_dev(*ticket, "ticket");
+    TORCH_CHECK(ticket->scalar_type() == at::kInt && ticket->numel() >= 1, "ticket int32[1]");
+    TORCH_CHECK(W.size(0) == 1 && !Wprev.has_value() && (variant & 256),
+                "fused tail: one model, atomic epilogue, no prologue update");
+    TORCH_CHECK(tail_mode == 0 || tail_mode == 1, "fused tail mode: 0 SSGD, 1 GD");
+    tail.ticket = reinterpret_cast<unsigned*>(ticket->data_ptr<int>());
+    tail.world = 1;
+    if (xg_bufs.has_value() && xg_bufs->size() > 1) {
+      TORCH_CHECK(xg_bufs->size() <= 8 && xg_rank >= 0 && xg_rank < (int64_t)xg_bufs->size(),
+                  "fused tail: 2..8 ranks");
+      TORCH_CHECK(xg_epoch > 0 && xg_epoch <= 0xffffffffLL, "fused tail: epoch in [1, 2^32)");
+      TORCH_CHECK(xg_slot >= W.size(1) + 1, "fused tail: bucket larger than the slot");
+      TORCH_CHECK(xg_err.has_value() && xg_err->scalar_type() == at::kInt, "fused tail: err int32");
+      check_dev(*xg_err, "xg_err");
+      tail.world = (int)xg_bufs->size();
+      for (int r = 0; r < tail.world; ++r) tail.bufs[r] = reinterpret_cast<void*>((*xg_bufs)[r]);
+      tail.rank = (int)xg_rank;
+      tail.slot = (int)xg_slot;
+      tail.epoch = (uint32_t)xg_epoch;
+      tail.err = reinterpret_cast<unsigned*>(xg_err->data_ptr<int>());
+      tail.timeout_s = xg_timeout;
+    }
+    tail.mode = (int)tail_mode; tail.reg = (int)tail_reg; tail.eta = (float)tail_eta;
+    tail.lam = (float)tail_lam; tail.reg_alpha = (float)tail_reg_alpha;
+    if (tail_count_acc.has_value()) {
+      check_dev(*tail_count_acc, "tail_count_acc");
+      TORCH_CHECK(tail_count_acc->scalar_type() == at::kDouble, "tail_count_acc f64");
+      tail.count_acc = tail_count_acc->data_ptr<double>();
+    }
+    tailp = &tail;
+  }
   const float* wprev = nullptr;
   if (Wprev.has_value()) {
     check_f32(*Wprev, "Wprev");
@@ -117,7 +155,7 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
                     reinterpret_cast<unsigned*>(cnt1.data_ptr<int>()),
                     reinterpret_cast<unsigned*>(cnt2.data_ptr<int>()), G.data_ptr<float>(),
                     C.data_ptr<float>(), (int)S, (int)variant, wprev, (int)upd_mode, (int)upd_reg,
-                    (float)upd_eta, (float)upd_lam, (float)upd_reg_alpha, cacc, cur_stream()),
+                    (float)upd_eta, (float)upd_lam, (float)upd_reg_alpha, cacc, tailp, cur_stream()),
       "lr_grad");
 }
 
@@ -613,7 +651,11 @@ TORCH_LIBRARY(dalgo, m) {
         "float eps, int seed, int step, float frac, int gx, int rows_per_block, Tensor(a!) slab, "
         "Tensor(b!) gslab, Tensor(c!) cnt1, Tensor(d!) cnt2, Tensor(e!) G, Tensor(f!) C, "
         "int variant=3, Tensor? Wprev=None, int upd_mode=0, int upd_reg=0, float upd_eta=0., "
-        "float upd_lam=0., float upd_reg_alpha=0., Tensor(g!)? count_acc=None) -> ()");
+        "float upd_lam=0., float upd_reg_alpha=0., Tensor(g!)? count_acc=None, "
+        "Tensor(h!)? ticket=None, int[]? xg_bufs=None, int xg_rank=0, int xg_slot=0, int xg_epoch=0, "
+        "Tensor(i!)? xg_err=None, float xg_timeout=0., int tail_mode=0, int tail_reg=0, "
+        "float tail_eta=0., float tail_lam=0., float tail_reg_alpha=0., "
+        "Tensor(j!)? tail_count_acc=None) -> ()");
   m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
         "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=3) -> ()");
   m.def("sync_update(Tensor(a!) W, Tensor(d!)? G, Tensor(e!)? C, Tensor? center, Tensor? S, "

@@ -21,6 +21,8 @@
 // Segments: rows [seg_lo[s], seg_lo[s+1]) use model s (MA/BMUF/EASGD keep one
 // local model per logical worker, ma.py:86-87); SSGD uses a single segment.
 #include "dalgo/common.h"
+#include "dalgo/xgmi.h"
+#include "launchers.h"
 
 namespace dalgo {
 
@@ -64,7 +66,42 @@ struct LrParams {
   int atomic_out;       // 1: blocks add their partials to G/C with float atomics
                         //    (G/C zeroed by the caller; summation order not fixed)
   int probe_no_epilogue;  // diagnostics only (variant bit 9): skip the block reduction
+  // fused tail (SSGD / GD, one segment, atomic epilogue): the last block to finish
+  // (ticket) exchanges [g || count] with the other ranks over xGMI (xg.world > 1)
+  // and applies the update to W, leaving G / C zeroed: one launch per training step.
+  unsigned* ticket;     // nullptr: no tail; zero on entry, re-armed by the last block
+  XgLink xg;
+  XgUpdate tu;
+  double* tail_count_acc;  // += the GLOBAL minibatch size
 };
+
+// The last block of a fused-tail launch: every other block's atomics are performed
+// (each waited vmcnt(0) before taking its ticket), so agent-scope loads see the
+// complete local sums.
+__device__ __forceinline__ void lr_tail(const LrParams& p) {
+  const int n = p.ldw;                 // G row; index n carries the count
+  float* G = p.G;
+  float* W = const_cast<float*>(p.W);
+  auto get = [&](int i) -> float {
+    return __hip_atomic_load(i < n ? &G[i] : &p.C[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  float c;
+  if (p.xg.world > 1) {
+    xg_push_publish_wait(p.xg, n + 1, get);
+    c = xg_sum(p.xg, n);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) W[i] = xg_update(W[i], xg_sum(p.xg, i), c, p.tu);
+  } else {
+    c = get(n);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) W[i] = xg_update(W[i], get(i), c, p.tu);
+  }
+  for (int i = threadIdx.x; i < n; i += blockDim.x) G[i] = 0.f;
+  __syncthreads();                     // every thread has read the count
+  if (threadIdx.x == 0) {
+    p.C[0] = 0.f;
+    if (p.tail_count_acc) p.tail_count_acc[0] += (double)c;
+    *p.ticket = 0u;
+  }
+}
 
 __device__ __forceinline__ float fused_update(float w, float g, float c, const LrParams& p) {
   if (p.upd_mode == 1) return w - p.upd_eta * g;
@@ -413,6 +450,15 @@ lr_rows_kernel(LrParams p) {
         if (p.count_acc)
           __hip_atomic_fetch_add(p.count_acc, (double)sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (p.ticket == nullptr) return;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this block's adds are performed
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_flag = (t == gridDim.x * gridDim.y - 1u);
+      }
+      __syncthreads();
+      if (s_flag) lr_tail(p);
       return;
     }
     float* my = p.slab + ((int64_t)seg * gx + bx) * S;
@@ -551,8 +597,25 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          int gx, int nseg, int rows_per_block, float* slab, float* gslab,
                          unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int variant,
                          const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
-                         float upd_reg_alpha, double* count_acc, hipStream_t st) {
+                         float upd_reg_alpha, double* count_acc, const DalgoLrTail* tail,
+                         hipStream_t st) {
   LrParams p{};
+  if (tail != nullptr) {
+    if (nseg != 1 || !((variant >> 8) & 1) || Wprev != nullptr || tail->ticket == nullptr ||
+        tail->world < 1 || tail->world > kXgMaxRanks || tail->rank < 0 || tail->rank >= tail->world ||
+        (tail->world > 1 && (tail->epoch == 0 || tail->slot < ldw + 1)))
+      return hipErrorInvalidValue;
+    p.ticket = tail->ticket;
+    for (int r = 0; r < tail->world; ++r) {
+      if (tail->world > 1 && tail->bufs[r] == nullptr) return hipErrorInvalidValue;
+      p.xg.bufs[r] = static_cast<uint8_t*>(tail->bufs[r]);
+    }
+    p.xg.rank = tail->rank; p.xg.world = tail->world; p.xg.slot = tail->slot;
+    p.xg.epoch = tail->epoch; p.xg.err = tail->err;
+    p.xg.timeout_ticks = (long long)(tail->timeout_s * 1e8);
+    p.tu = XgUpdate{tail->mode, tail->reg, tail->eta, tail->lam, tail->reg_alpha};
+    p.tail_count_acc = tail->count_acc;
+  }
   p.Wprev = Wprev; p.Gprev = G; p.Cprev = C; p.upd_mode = upd_mode; p.upd_reg = upd_reg;
   p.upd_eta = upd_eta; p.upd_lam = upd_lam; p.upd_reg_alpha = upd_reg_alpha;
   p.count_acc = count_acc;

@@ -5,6 +5,19 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Fused tail of the LR gradient launch (SSGD / full-batch GD): see lr_grad.hip.
+struct DalgoLrTail {
+  unsigned* ticket;             // device counter, zero
+  void* bufs[8];                // K11 exchange buffers (world > 1)
+  int world, rank, slot;
+  uint32_t epoch;
+  unsigned* err;
+  double timeout_s;
+  int mode, reg;                // 0 SSGD (mean + reg), 1 GD (sum)
+  float eta, lam, reg_alpha;
+  double* count_acc;            // += global minibatch size (optional)
+};
+
 extern "C" {
 
 // ---- K1/K7/K10 logistic regression (lr_grad.hip)
@@ -15,7 +28,8 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          int gx, int nseg, int rows_per_block, float* slab, float* gslab,
                          unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int variant,
                          const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
-                         float upd_reg_alpha, double* count_acc, hipStream_t st);
+                         float upd_reg_alpha, double* count_acc, const DalgoLrTail* tail,
+                         hipStream_t st);
 hipError_t dalgo_lr_eval(const void* X, const float* y, const float* W, const int64_t* seg,
                          int64_t ld, int D, int ldw, int has_bias, float eps, int is_bf16, int gx,
                          int nseg, int rows_per_block, unsigned long long* correct, float* loss,

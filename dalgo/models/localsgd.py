@@ -166,6 +166,18 @@ class ParallelSGD:
                        max_seg_rows=self.max_seg, g_is_zero=self._g_zero)
         self._g_zero = False
 
+    def _one_kernel(self) -> bool:
+        """Fused single-launch step (DALGO_ONE_KERNEL=1): GPU, atomic epilogue, one rank or
+        K11 peers. Measured on MI355X equal to K1 + separate update / K11 launch (361 vs
+        361 us at 10M rows, 59.1 vs 59.7 us at 1.25M, 76.7 vs 76.5 us for 2 ranks on one
+        GPU): back-to-back launches already overlap, and the last-block hand-off adds the
+        latency the launch saves. Off by default; kept tested."""
+        if getattr(self, "_ok1", None) is None:
+            self._ok1 = (self.device.type == "cuda" and self._zg
+                         and os.environ.get("DALGO_ONE_KERNEL", "0") == "1"
+                         and (comm.world_size() == 1 or self.bucket.xg is not None))
+        return self._ok1
+
     def _flush(self):
         """Apply a pending fused update to self.w (end of training / before reads)."""
         if self._pending:
@@ -204,6 +216,16 @@ class ParallelSGD:
                                max_seg_rows=self.max_seg, count_acc=self.count_acc)
             self.bucket.all_reduce()
             self._pending = True
+        elif c.algo in ("ssgd", "gd") and self._one_kernel():
+            # the whole step in ONE launch: gradient, (xGMI exchange,) update
+            lr_ops.lr_grad(self.data.X_train, self.data.y_train, self.w, self.seg, D=self.D,
+                           has_bias=True, eps=c.eps, seed=c.sample_seed, step=t, frac=c.frac,
+                           row_offset=self.data.row_offset, G=self.G, C=self.C,
+                           max_seg_rows=self.max_seg, g_is_zero=self._g_zero,
+                           tail=dict(mode=0 if c.algo == "ssgd" else 1, reg=self._upd["reg"],
+                                     eta=c.eta, lam=c.lam, reg_alpha=c.reg_alpha,
+                                     count_acc=self.count_acc, xg=self.bucket.xg))
+            self._g_zero = True
         elif c.algo in ("ssgd", "gd"):
             self._grad(self.w, t)
             xg = self.bucket.xg

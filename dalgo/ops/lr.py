@@ -69,6 +69,7 @@ class _Workspace:
     gslab: torch.Tensor
     cnt1: torch.Tensor
     cnt2: torch.Tensor
+    ticket: torch.Tensor   # fused-tail arrival counter (re-armed by the kernel)
 
 
 _ws_cache: dict = {}
@@ -84,6 +85,7 @@ def _workspace(device, nseg, gx, S) -> _Workspace:
             gslab=torch.empty((nseg * ngroups, S), dtype=torch.float32, device=device),
             cnt1=torch.zeros(nseg * ngroups, dtype=torch.int32, device=device),
             cnt2=torch.zeros(nseg, dtype=torch.int32, device=device),
+            ticket=torch.zeros(1, dtype=torch.int32, device=device),
         )
         _ws_cache[key] = ws
     return ws
@@ -96,7 +98,7 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
             variant: int | None = None, target_blocks: int | None = None,
             w_prev: torch.Tensor | None = None, update: dict | None = None,
             count_acc: torch.Tensor | None = None, g_is_zero: bool = False,
-            deterministic: bool | None = None):
+            deterministic: bool | None = None, tail: dict | None = None):
     """Per-segment gradient SUM and selected-row COUNT.
 
     X: [n, >=D] (bf16/f32), y: [n] f32, W: [n_seg, ldw] f32 models,
@@ -114,6 +116,13 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
     after a ``sync_update(..., zero_grad=True)``); ``deterministic=True`` (or
     DALGO_DETERMINISTIC=1) uses the fixed-order two-level reduction instead, which
     is bitwise repeatable. The fused-update path is always deterministic.
+
+    Fused tail (GPU, one segment, atomic epilogue): ``tail`` = dict(mode 0 = SSGD /
+    1 = GD, reg, eta, lam, reg_alpha, count_acc, xg) makes the LAST block of the
+    launch all-reduce ``[G || C]`` over xGMI (``xg``: a shared XgmiAllReduce, or None
+    on one rank), apply the update to ``W`` and leave G / C zeroed — a whole
+    synchronous training step in one launch. ``count_acc`` then accumulates the
+    GLOBAL minibatch size.
     """
     nseg, ldw = W.shape
     if G is None:
@@ -133,6 +142,26 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
         u = update or {}
         var = LR_VARIANT if variant is None else int(variant)
         det = DETERMINISTIC if deterministic is None else bool(deterministic)
+        if tail is not None:
+            if det or w_prev is not None or nseg != 1:
+                raise ValueError("fused tail needs the atomic epilogue, one model, no prologue update")
+            if not g_is_zero:
+                G.zero_()
+                C.zero_()
+            xg = tail.get("xg")
+            kw = {}
+            if xg is not None:
+                kw = dict(xg_bufs=xg.bufs, xg_rank=xg.rank, xg_slot=xg.slot,
+                          xg_epoch=xg.next_epoch(), xg_err=xg.err, xg_timeout=xg.timeout_s)
+            _ext.ops().lr_grad(X, y, W, seg, int(row_offset), int(D), bool(has_bias), float(eps),
+                               int(seed), int(step), float(frac), gx, rpb, ws.slab, ws.gslab,
+                               ws.cnt1, ws.cnt2, G, C, var | 256, None, 0, 0, 0.0, 0.0, 0.0,
+                               count_acc, ticket=ws.ticket, tail_mode=int(tail.get("mode", 0)),
+                               tail_reg=int(tail.get("reg", 0)), tail_eta=float(tail.get("eta", 0.0)),
+                               tail_lam=float(tail.get("lam", 0.0)),
+                               tail_reg_alpha=float(tail.get("reg_alpha", 0.0)),
+                               tail_count_acc=tail.get("count_acc"), **kw)
+            return G, C
         if not det and w_prev is None:
             if not g_is_zero:
                 G.zero_()

@@ -115,3 +115,34 @@ def test_rows_sum_broadcast(cuda):
     Wd = W.to(cuda)
     U.rows_broadcast(Wd, src.to(cuda))
     assert torch.equal(Wd.cpu(), src.expand(4, -1))
+
+
+@pytest.mark.parametrize("mode,reg", [(0, 0), (0, 3), (1, 0)])
+def test_lr_grad_fused_tail_single_rank(cuda, mode, reg):
+    """One-launch step (gradient + update in the last block) == lr_grad + K8."""
+    X, y = _data(300_000, 1024, torch.bfloat16, seed=11)
+    Xd, yd = X.to(cuda), y.to(cuda)
+    seg = torch.tensor([0, X.shape[0]], dtype=torch.int64, device=cuda)
+    w0 = torch.randn(1, 1025, generator=torch.Generator().manual_seed(4)).to(cuda) * 0.05
+    kw = dict(D=1024, frac=0.1, eps=0.0, seed=42)
+    upd = dict(eta=0.1, lam=0.01, reg_alpha=0.3)
+    # reference: separate gradient + update launches
+    w_ref = w0.clone()
+    acc_ref = torch.zeros(1, dtype=torch.float64, device=cuda)
+    for t in range(3):
+        G, C = L.lr_grad(Xd, yd, w_ref, seg, step=t, **kw)
+        U.sync_update(w_ref, U.SSGD if mode == 0 else U.GD_SUM, G=G, C=C, reg=reg,
+                      count_acc=acc_ref, **upd)
+    # fused tail
+    w = w0.clone()
+    G = torch.zeros(1, 1025, device=cuda)
+    C = torch.zeros(1, device=cuda)
+    acc = torch.zeros(1, dtype=torch.float64, device=cuda)
+    for t in range(3):
+        L.lr_grad(Xd, yd, w, seg, step=t, G=G, C=C, g_is_zero=(t > 0),
+                  tail=dict(mode=mode, reg=reg, count_acc=acc, xg=None, **upd), **kw)
+    torch.cuda.synchronize()
+    assert float(acc.item()) == float(acc_ref.item())
+    assert bool((G == 0).all()) and bool((C == 0).all())
+    rel = ((w - w_ref).abs().max() / w_ref.abs().max()).item()
+    assert rel < 1e-5, rel
