@@ -30,6 +30,7 @@ namespace dalgo {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 template <typename T> struct KTraits;
 // bf16: one 16-wide k-step per MFMA, 8 elements (16 B) per lane per k-step
@@ -231,6 +232,208 @@ kmeans_assign_kernel(const T* __restrict__ X, int64_t n, int64_t ldx, const T* _
       double s = 0.0;
       for (int w = 0; w < NW; ++w) s += s_sse[w];
       atomicAdd(sse, s);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K2 "resident" form (bf16, default): one block per CU keeps up to 512 centres in
+// LDS for the whole launch — no per-chunk staging, no barriers in the main loop —
+// and its waves stream point tiles straight from HBM into VGPRs (the next tile
+// group is prefetched under the MFMAs). k > 512 runs as several launches (passes)
+// that carry the running (distance, id) per point in the output buffers.
+//
+// Distances, not scores: every centre row gets one extra 16-wide k-step
+// [h_hi, h_mid, h_lo, 1, 1, 1, 0...] (h = 0.5|c|^2 split into three bf16) and every
+// point [1, 1, 1, g_hi, g_mid, g_lo, 0...] (g = 0.5|x|^2), with the point itself
+// negated, so the MFMA (C = inline 0) produces 0.5|x - c|^2 >= 0 directly (f32
+// accumulate, the splits carry ~24 bits). Non-negative floats order like their
+// int bits, so the argmin is an integer min over keys (bits & ~0xff) | (sub << 4 | r):
+// one v_and_or + half a v_min3 per distance instead of compare + two selects.
+// Equal (truncated) distances resolve to the lower key = lower centre id, matching
+// the reference's strict '<' (k-means.py:25); the truncation is 2^-15 relative.
+template <int DP> struct ResGeom {
+  static constexpr int KS = DP / 16;       // data k-steps
+  static constexpr int KE = KS + 1;        // + the norm k-step
+  static constexpr int NJ = 2 * KE;        // 16-B pieces per LDS row
+  static constexpr int CB = 512;           // centres per pass (16 sub-tiles: 4-bit sub id)
+};
+
+__device__ __forceinline__ uint32_t bf16_pack2(float lo, float hi) {
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+// v ~= hi + mid + lo with each part a bf16 (about 24 significant bits in total)
+__device__ __forceinline__ void split3(float v, float& hi, float& mid, float& lo) {
+  hi = bf16_to_f32(f32_to_bf16(v));
+  const float r = v - hi;
+  mid = bf16_to_f32(f32_to_bf16(r));
+  lo = r - mid;
+}
+
+template <int DP, int NW, int PT>
+__global__ void __launch_bounds__(NW * 64, 1)
+kmeans_assign_res_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
+                         const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int c0,
+                         int ncen, int first, int last, int* __restrict__ assign,
+                         float* __restrict__ dist, double* __restrict__ sse) {
+  using G = ResGeom<DP>;
+  constexpr int KS = G::KS, KE = G::KE, NJ = G::NJ;
+  constexpr int NT = NW * 64;
+  __shared__ uint4 s_c[G::CB * NJ];
+  __shared__ double s_sse[NW];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, cl = lane & 31;
+
+  // ---- stage this pass's centres (+ norm step) once; piece j of row c lives at
+  // j ^ ((c >> 4) & 1): conflict-free ds_read_b128 for the 32-row A reads
+  for (int i = tid; i < ncen * 2 * KS; i += NT) {
+    const int c = i / (2 * KS), j = i % (2 * KS);
+    s_c[c * NJ + (j ^ ((c >> 4) & 1))] =
+        *reinterpret_cast<const uint4*>(Cq + (int64_t)(c0 + c) * DP + j * 8);
+  }
+  for (int c = tid; c < ncen; c += NT) {
+    float a, b, d;
+    split3(hn[c0 + c], a, b, d);
+    const uint32_t one = 0x3f80u;
+    s_c[c * NJ + ((2 * KS) ^ ((c >> 4) & 1))] =
+        make_uint4(bf16_pack2(a, b), (uint32_t)f32_to_bf16(d) | (one << 16), one | (one << 16), 0u);
+    s_c[c * NJ + ((2 * KS + 1) ^ ((c >> 4) & 1))] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  __syncthreads();
+
+  const int nsub = ncen / 32;
+  const int64_t ngrp = cdiv(n, (int64_t)PT * 32);
+  const int64_t GW = (int64_t)gridDim.x * NW;
+  double my_sse = 0.0;
+
+  // B fragments of a tile group: negated point pieces + the norm step. Rows past n
+  // re-read row n-1 (unconditional loads keep hipcc from branching around each one;
+  // those lanes' results are never written).
+  uint4 B[PT][KE];
+  auto load_raw = [&](uint4 (&R)[PT][KS], int64_t grp) {
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      const int64_t p = min(grp * (PT * 32) + t * 32 + cl, n - 1);
+      const uint16_t* src = X + p * ldx + h * 8;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) R[t][s] = *reinterpret_cast<const uint4*>(src + 16 * s);
+    }
+  };
+  auto finish = [&](const uint4 (&R)[PT][KS]) {
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      float g = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const uint4 v = R[t][s];
+        g = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, v.x), __builtin_bit_cast(bf16x2, v.x), g, false);
+        g = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, v.y), __builtin_bit_cast(bf16x2, v.y), g, false);
+        g = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, v.z), __builtin_bit_cast(bf16x2, v.z), g, false);
+        g = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, v.w), __builtin_bit_cast(bf16x2, v.w), g, false);
+        B[t][s] = make_uint4(v.x ^ 0x80008000u, v.y ^ 0x80008000u, v.z ^ 0x80008000u, v.w ^ 0x80008000u);
+      }
+      auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(g), __float_as_uint(g), false, false);
+      g = 0.5f * (__uint_as_float(sw[0]) + __uint_as_float(sw[1]));
+      float a, b, d;
+      split3(g, a, b, d);
+      const uint32_t one = 0x3f80u;
+      B[t][KS] = h ? make_uint4(0u, 0u, 0u, 0u)
+                   : make_uint4(one | (one << 16), one | ((uint32_t)f32_to_bf16(a) << 16), bf16_pack2(b, d), 0u);
+    }
+  };
+
+  int64_t grp = (int64_t)blockIdx.x * NW + wid;
+  {
+    uint4 R[PT][KS];
+    load_raw(R, grp);
+    finish(R);
+  }
+  // piece (2s + h) ^ swz == 2s + (h ^ swz): one lane base, immediate offsets per k-step
+  const uint4* arow = &s_c[cl * NJ + (h ^ ((cl >> 4) & 1))];
+  // key mask held in a VGPR so the pack is ONE v_and_or_b32 (VGPR mask, SGPR key)
+  int kmask;
+  asm volatile("v_mov_b32 %0, 0xffffff00" : "=v"(kmask));
+  for (; grp < ngrp; grp += GW) {
+    uint4 Rn[PT][KS];
+    const bool more = grp + GW < ngrp;
+    if (more) load_raw(Rn, grp + GW);   // lands under this group's MFMAs
+
+    int key[PT];
+#pragma unroll
+    for (int t = 0; t < PT; ++t) key[t] = 0x7fffffff;
+    for (int sub = 0; sub < nsub; ++sub) {
+      uint4 a[KE];
+#pragma unroll
+      for (int s = 0; s < KE; ++s) a[s] = arow[sub * 32 * NJ + 2 * s];
+      f32x16 acc[PT];
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        const f32x16 z = {};
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[0]),
+                                                          __builtin_bit_cast(bf16x8, B[t][0]), z, 0, 0, 0);
+      }
+#pragma unroll
+      for (int s = 1; s < KE; ++s)
+#pragma unroll
+        for (int t = 0; t < PT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[s]),
+                                                            __builtin_bit_cast(bf16x8, B[t][s]), acc[t], 0, 0, 0);
+      const int sk = sub << 4;
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        int m = key[t];
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const int k0 = (__float_as_int(acc[t][r]) & kmask) | __builtin_amdgcn_readfirstlane(sk | r);
+          const int k1 = (__float_as_int(acc[t][r + 1]) & kmask) | __builtin_amdgcn_readfirstlane(sk | (r + 1));
+          m = min(min(m, k0), k1);   // one v_min3_i32 per pair
+        }
+        key[t] = m;
+      }
+    }
+
+    // ---- decode, combine the lane halves (same point, disjoint centre rows),
+    // merge with the previous passes, write
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      const int kk = key[t];
+      const float v = __int_as_float(kk & ~0xff);
+      const int r = kk & 15;
+      const int ci = c0 + ((kk >> 4) & 15) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      auto sv = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+      auto si = __builtin_amdgcn_permlane32_swap((uint32_t)ci, (uint32_t)ci, false, false);
+      const float pv = __uint_as_float(h ? sv[0] : sv[1]);
+      const int pi = (int)(h ? si[0] : si[1]);
+      float bv = v;
+      int bi = ci;
+      if (pv < bv || (pv == bv && pi < bi)) { bv = pv; bi = pi; }
+      const int64_t p = grp * (PT * 32) + t * 32 + cl;
+      if (h == 0 && p < n) {
+        if (!first) {
+          const float ov = dist[p];
+          if (!(bv < ov)) { bv = ov; bi = assign[p]; }
+        }
+        assign[p] = bi;
+        if (last) {
+          const float dd = fmaxf(2.f * bv, 0.f);
+          dist[p] = dd;
+          my_sse += (double)dd;
+        } else {
+          dist[p] = bv;
+        }
+      }
+    }
+    if (more) finish(Rn);
+  }
+
+  if (sse && last) {
+    double s = my_sse;
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) s_sse[wid] = s;
+    __syncthreads();
+    if (tid == 0) {
+      double tot = 0.0;
+      for (int w = 0; w < NW; ++w) tot += s_sse[w];
+      atomicAdd(sse, tot);
     }
   }
 }
@@ -510,12 +713,49 @@ static hipError_t launch_assign_v(const void* X, int64_t n, int64_t ldx, const v
   return hipSuccess;
 }
 
+static int device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cached[dev] = v;
+  }
+  return cached[dev];
+}
+
+// resident-centre K2 (bf16): one persistent block per CU, ceil(kpad / 512) passes;
+// `dist` is required (it carries the running distance between passes)
+template <int DP, int NW, int PT>
+static hipError_t launch_assign_res(const void* X, int64_t n, int64_t ldx, const void* Cq,
+                                    const float* hn, int kpad, int* assign, float* dist, double* sse,
+                                    hipStream_t st) {
+  using G = ResGeom<DP>;
+  if (dist == nullptr || kpad % 32) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  const int64_t ngrp = cdiv(n, (int64_t)PT * 32);
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(device_cus(), cdiv(ngrp, NW)));
+  const int npass = (int)cdiv(kpad, G::CB);
+  for (int ps = 0; ps < npass; ++ps) {
+    const int c0 = ps * G::CB;
+    const int ncen = std::min(G::CB, kpad - c0);
+    hipLaunchKernelGGL((kmeans_assign_res_kernel<DP, NW, PT>), dim3(grid), dim3(NW * 64), 0, st,
+                       (const uint16_t*)X, n, ldx, (const uint16_t*)Cq, hn, c0, ncen, ps == 0 ? 1 : 0,
+                       ps == npass - 1 ? 1 : 0, assign, dist, sse);
+    DALGO_LAUNCH_CHECK();
+  }
+  return hipSuccess;
+}
+
 // variant: 0 = 8 waves x 32-centre chunks, 1 = 4 waves x 32, 2 = 4 waves x 128,
 //          3 = 8 waves x 128, 4 = 4 waves x 64, 5 = variant 0 capped at 128 VGPRs
 //          (4 waves/SIMD: two 8-wave blocks per CU), 6 = 4 waves x 4 point tiles (128
 //          points per wave), 7 = 8 waves x 4 point tiles, 8 = 4 waves capped at 128
 //          VGPRs (four blocks per CU), 9 = variant 5 with 64-centre chunks,
-//          10 = 16 waves (1024 points per block) capped at 128 VGPRs
+//          10 = 16 waves (1024 points per block) capped at 128 VGPRs,
+//          11 / 12 / 13 = resident-centre form (bf16; f32 uses 5): 8 waves x 2 point
+//          tiles, 4 waves x 4 tiles, 8 waves x 1 tile
 template <typename T, int DP>
 static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                    const float* hn, int kpad, int* assign, float* mind, double* sse,
@@ -532,6 +772,13 @@ static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const 
     case 8: return launch_assign_v<T, DP, 4, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
     case 9: return launch_assign_v<T, DP, 8, 2, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
     case 10: return launch_assign_v<T, DP, 16, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 11: case 12: case 13:
+      if constexpr (sizeof(T) == 2) {
+        if (variant == 11) return launch_assign_res<DP, 8, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 12) return launch_assign_res<DP, 4, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        return launch_assign_res<DP, 8, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+      }
+      return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
     default: return hipErrorInvalidValue;
   }
 }

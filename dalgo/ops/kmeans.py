@@ -76,9 +76,30 @@ def refresh(cen: Centers):
 
 import os
 
-# launch variant of the assign kernel (table in csrc/kernels/kmeans.hip); 5 = 8-wave
-# blocks capped at 128 VGPRs so two blocks share a CU (measured best on MI355X)
-ASSIGN_VARIANT = int(os.environ.get("DALGO_KM_VARIANT", "5"))
+# launch variant of the assign kernel (table in csrc/kernels/kmeans.hip). -1 = per
+# dtype: f32 -> 5 (8-wave blocks capped at 128 VGPRs, two blocks per CU), bf16 -> 5
+# until the resident-centre form (11/12/13) is measured on the GPU
+ASSIGN_VARIANT = int(os.environ.get("DALGO_KM_VARIANT", "-1"))
+RESIDENT_VARIANTS = (11, 12, 13)
+_BF16_DEFAULT = 5
+_scratch: dict = {}
+
+
+def assign_variant(X: torch.Tensor, variant: int | None = None) -> int:
+    v = ASSIGN_VARIANT if variant is None else int(variant)
+    if v < 0:
+        v = _BF16_DEFAULT if X.dtype == torch.bfloat16 else 5
+    return v
+
+
+def _dist_scratch(n: int, device) -> torch.Tensor:
+    """Per-point distance buffer the multi-pass resident kernel carries between passes."""
+    key = str(device)
+    t = _scratch.get(key)
+    if t is None or t.numel() < n:
+        t = torch.empty(max(n, 1), dtype=torch.float32, device=device)
+        _scratch[key] = t
+    return t
 
 
 def assign(X: torch.Tensor, cen: Centers, out: torch.Tensor | None = None,
@@ -89,8 +110,11 @@ def assign(X: torch.Tensor, cen: Centers, out: torch.Tensor | None = None,
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=X.device)
     if X.is_cuda:
-        _ext.ops().kmeans_assign(X, cen.Cq, cen.hn, out, mind, sse,
-                                 ASSIGN_VARIANT if variant is None else int(variant))
+        v = assign_variant(X, variant)
+        md = mind
+        if md is None and v in RESIDENT_VARIANTS and X.dtype == torch.bfloat16:
+            md = _dist_scratch(n, X.device)
+        _ext.ops().kmeans_assign(X, cen.Cq, cen.hn, out, md, sse, v)
         return out
     # CPU reference: exact scores on the ROUNDED centres, f64, first maximum wins
     Xf = X[:, : cen.d].double()

@@ -16,6 +16,39 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("d,k,n", [(2, 2, 6), (16, 40, 3000), (50, 33, 4099), (128, 1024, 20000)])
 def test_kmeans_assign_matches_reference(cuda, dtype, d, k, n):
+    _check_assign(cuda, dtype, d, k, n, None)
+
+
+# resident-centre K2 (bf16): one and several 512-centre passes, DP = 16/32/64/128,
+# a ragged last tile group, and point counts below one tile group
+@pytest.mark.parametrize("variant", [11, 12, 13])
+@pytest.mark.parametrize("d,k,n", [(2, 2, 6), (16, 40, 3000), (30, 77, 1025), (50, 33, 4099),
+                                   (128, 1024, 20000), (128, 600, 70001), (100, 1500, 9000)])
+def test_kmeans_assign_resident(cuda, variant, d, k, n):
+    _check_assign(cuda, torch.bfloat16, d, k, n, variant)
+
+
+def test_kmeans_resident_ties_and_passes(cuda):
+    """Exact ties resolve to the lowest id inside a pass, across lane halves and across passes."""
+    X = torch.zeros(70, 8)
+    C0 = torch.zeros(1100, 8) + 50.0
+    for c in (3, 7, 12, 515, 1030):      # equidistant from 0: same pass, other half, later passes
+        C0[c] = 0.0
+        C0[c, c % 8] = 1.0
+    for v in (11, 12, 13):
+        a = K.assign(K.prepare_points(X.to(cuda).bfloat16()), K.make_centers(C0, torch.bfloat16, cuda),
+                     variant=v).cpu()
+        assert a.tolist() == [3] * 70, v
+    C0[3, 3] = 2.0                       # now the later passes hold the nearest (ids 7 and 12 stay tied)
+    C0[7, 7] = 2.0
+    C0[12, 4] = 2.0
+    for v in (11, 12, 13):
+        a = K.assign(K.prepare_points(X.to(cuda).bfloat16()), K.make_centers(C0, torch.bfloat16, cuda),
+                     variant=v).cpu()
+        assert a.tolist() == [515] * 70, v
+
+
+def _check_assign(cuda, dtype, d, k, n, variant):
     g = torch.Generator().manual_seed(d + k)
     X = (torch.randn(n, d, generator=g) * 3).to(dtype)
     C0 = torch.randn(k, d, generator=g) * 3
@@ -26,7 +59,7 @@ def test_kmeans_assign_matches_reference(cuda, dtype, d, k, n):
     cen_d = K.make_centers(C0, dtype, cuda)
     mind = torch.empty(n, device=cuda)
     sse = torch.zeros(1, dtype=torch.float64, device=cuda)
-    a = K.assign(Xd, cen_d, mind=mind, sse=sse).cpu()
+    a = K.assign(Xd, cen_d, mind=mind, sse=sse, variant=variant).cpu()
     # scores computed in f32 on the GPU vs f64 on the CPU: allow rare near-ties
     agree = (a == a_ref).float().mean().item()
     assert agree > 0.999, agree
