@@ -81,8 +81,16 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
              const std::optional<Tensor>& ticket, at::OptionalIntArrayRef xg_bufs, int64_t xg_rank,
              int64_t xg_slot, int64_t xg_epoch, const std::optional<Tensor>& xg_err,
              double xg_timeout, int64_t tail_mode, int64_t tail_reg, double tail_eta,
-             double tail_lam, double tail_reg_alpha, const std::optional<Tensor>& tail_count_acc) {
+             double tail_lam, double tail_reg_alpha, const std::optional<Tensor>& tail_count_acc,
+             const std::optional<Tensor>& pool, int64_t pool_parity) {
   check_lr_inputs(X, y, W, seg, D, has_bias);
+  unsigned* poolp = nullptr;
+  if (pool.has_value()) {
+    check_dev(*pool, "pool");
+    TORCH_CHECK(pool->scalar_type() == at::kInt && pool->is_contiguous() &&
+                pool->numel() >= 2 * 8 * W.size(0), "pool: int32 [2 * 8 * n_seg] claim heads");
+    poolp = reinterpret_cast<unsigned*>(pool->data_ptr<int>());
+  }
   DalgoLrTail tail{};
   const DalgoLrTail* tailp = nullptr;
   if (ticket.has_value()) {
@@ -155,7 +163,8 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
                     reinterpret_cast<unsigned*>(cnt1.data_ptr<int>()),
                     reinterpret_cast<unsigned*>(cnt2.data_ptr<int>()), G.data_ptr<float>(),
                     C.data_ptr<float>(), (int)S, (int)variant, wprev, (int)upd_mode, (int)upd_reg,
-                    (float)upd_eta, (float)upd_lam, (float)upd_reg_alpha, cacc, tailp, cur_stream()),
+                    (float)upd_eta, (float)upd_lam, (float)upd_reg_alpha, cacc, tailp, poolp,
+                    (int)(pool_parity & 1), cur_stream()),
       "lr_grad");
 }
 
@@ -288,6 +297,17 @@ void hbm_gather_rows(const Tensor& X, const Tensor& idx, Tensor out, int64_t gri
                                         reinterpret_cast<uint32_t*>(out.data_ptr<int>()), (int)grid,
                                         cur_stream()),
                   "hbm_gather_rows");
+}
+
+// diagnostics: per-wave K1 timeline (u64, 8 per wave) for the following lr_grad launches
+void lr_set_trace(const c10::optional<Tensor>& buf) {
+  if (buf.has_value()) {
+    check_dev(*buf, "trace");
+    TORCH_CHECK(buf->scalar_type() == at::kLong && buf->is_contiguous(), "trace must be contiguous int64");
+    dalgo_lr_set_trace(buf->data_ptr());
+  } else {
+    dalgo_lr_set_trace(nullptr);
+  }
 }
 
 void hbm_read(const Tensor& src, Tensor out, int64_t unroll) {
@@ -655,7 +675,7 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(h!)? ticket=None, int[]? xg_bufs=None, int xg_rank=0, int xg_slot=0, int xg_epoch=0, "
         "Tensor(i!)? xg_err=None, float xg_timeout=0., int tail_mode=0, int tail_reg=0, "
         "float tail_eta=0., float tail_lam=0., float tail_reg_alpha=0., "
-        "Tensor(j!)? tail_count_acc=None) -> ()");
+        "Tensor(j!)? tail_count_acc=None, Tensor(k!)? pool=None, int pool_parity=0) -> ()");
   m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
         "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=3) -> ()");
   m.def("sync_update(Tensor(a!) W, Tensor(d!)? G, Tensor(e!)? C, Tensor? center, Tensor? S, "
@@ -693,6 +713,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("tc_step(Tensor A, Tensor Told, Tensor(a!) Tnew, Tensor(b!) count, int variant=0) -> ()");
   m.def("spd_inverse(Tensor G, float ridge, Tensor(a!) out, Tensor(b!)? status) -> ()");
   m.def("hbm_read(Tensor src, Tensor(a!) out, int unroll=8) -> ()");
+  m.def("lr_set_trace(Tensor? buf) -> ()", &lr_set_trace);
   m.def("hbm_gather_rows(Tensor X, Tensor idx, Tensor(a!) out, int grid=2048) -> ()");
   m.def("mc_pi(int seed, int stream, int offset, int n, Tensor(a!) count) -> ()");
 }

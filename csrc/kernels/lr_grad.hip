@@ -66,6 +66,17 @@ struct LrParams {
   int atomic_out;       // 1: blocks add their partials to G/C with float atomics
                         //    (G/C zeroed by the caller; summation order not fixed)
   int probe_no_epilogue;  // diagnostics only (variant bit 9): skip the block reduction
+  // cross-block work pool: rows past gx * rows_per_block of each segment are claimed
+  // in 128-row units from 8 shard heads (pool[(parity * n_seg + seg) * 8 + shard]);
+  // nullptr: the static block ranges cover everything
+  unsigned* pool;
+  int pool_parity;        // this launch uses set `parity` and re-arms the other one
+  int fine_q;             // work claims switch from 256-row groups to 64-row quarters once
+                          // fewer than fine_q quarters of the block are unclaimed (0 = never)
+  // diagnostics only (dalgo_lr_set_trace): per-wave timeline, 8 u64 per wave at
+  // [(block * NW + wave) * 8]: start, first row batch issued, sweep done, epilogue
+  // done (s_memrealtime, 100 MHz), selected rows, hardware CU/SE id
+  unsigned long long* trace;
   // fused tail (SSGD / GD, one segment, atomic epilogue): the last block to finish
   // (ticket) exchanges [g || count] with the other ranks over xGMI (xg.world > 1)
   // and applies the update to W, leaving G / C zeroed: one launch per training step.
@@ -187,10 +198,13 @@ lr_rows_kernel(LrParams p) {
   // cross-wave reduction buffer
   __shared__ __attribute__((aligned(16))) float s_arena[(RED_FLOATS > RING_INTS) ? RED_FLOATS : RING_INTS];
   __shared__ int s_flag;
-  __shared__ int s_next;   // next unclaimed 256-row group of this block (dynamic balancing)
+  __shared__ int s_next;   // next unclaimed 64-row quarter of this block (dynamic balancing)
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
+  unsigned long long* const tr =
+      p.trace ? p.trace + ((int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * NW + wid) * 8 : nullptr;
+  const unsigned long long t_start = tr ? (unsigned long long)__builtin_amdgcn_s_memrealtime() : 0ull;
   const int seg = blockIdx.y;
   const int bx = blockIdx.x;
   const int gx = gridDim.x;
@@ -250,32 +264,123 @@ lr_rows_kernel(LrParams p) {
   int* ring = reinterpret_cast<int*>(s_arena) + wid * kRing;
   const int q = lane >> 4;
   uint32_t head = 0, tail = 0;
-  if (threadIdx.x == 0) s_next = NW;   // groups 0..NW-1 are pre-assigned to the waves
+  // work units are counted in 64-row quarters; a claim takes a whole 256-row group
+  // (4 quarters) until the block's unclaimed rows fall below fine_q quarters, then
+  // single quarters, so the block's waves finish within ~1.5 row batches of each other
+  if (threadIdx.x == 0) s_next = 4 * NW;   // groups 0..NW-1 are pre-assigned to the waves
+  // cross-block pool (segment rows past the static block ranges): 128-row units j,
+  // shard s = j % 8 holds units s, s + 8, ...; the claim heads are only touched by
+  // agent-scope atomics (performed at memory side). Block (0, 0) re-arms the other
+  // parity set, which the previous launch used and the next one will.
+  if (p.pool != nullptr && bx == 0 && seg == 0)
+    for (int i = threadIdx.x; i < 8 * (int)gridDim.y; i += NW * 64)
+      __hip_atomic_store(p.pool + (int64_t)(p.pool_parity ^ 1) * gridDim.y * 8 + i, 0u,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  int64_t gnext = gstart + (int64_t)wid * 256;
+  constexpr int kPU = 128;
+  const int64_t psl = seg_lo + (int64_t)gx * p.rows_per_block;   // pool start (local row)
+  const bool has_pool = p.pool != nullptr && psl < seg_hi;
+  unsigned* const heads = has_pool ? p.pool + ((int64_t)p.pool_parity * gridDim.y + seg) * 8 : nullptr;
+  const int64_t psg = p.row_offset + psl, psa = psg & ~(int64_t)3, sghi = p.row_offset + seg_hi;
+  const int nj = has_pool ? (int)((sghi - psa + kPU - 1) / kPU) : 0;
+  auto shard_size = [&](int s) { return nj > s ? (nj - s + 7) >> 3 : 0; };
+  int pshard = (bx + seg) & 7;
+  int ahead = 0;            // lane 0: claim issued ahead on `pshard`, consumed by the next pool claim
+  bool ahead_out = false;
+  bool in_pool = false;
 
-  // ---- K7: Bernoulli selection of the next 256-row groups, compacted into the ring
+  const int nq = (int)((ghi - gstart + 63) >> 6);
+  int64_t gnext = gstart + (int64_t)wid * 256;
+  int64_t ulo = glo;                       // current work unit: rows [max(gnext, ulo), uhi)
+  int64_t uhi = min(ghi, gnext + 256);
+  bool more = gnext < ghi;
+  int sclaim = 4 * (NW + wid);             // next group of this wave in the fixed map
+
+  auto pool_next = [&]() {
+    if (!has_pool) { more = false; return; }
+    if (!ahead_out) {
+      if (lane == 0) ahead = (int)atomicAdd(&heads[pshard], 1u);
+      ahead_out = true;
+    }
+    int k = __builtin_amdgcn_readfirstlane(ahead);
+    ahead_out = false;
+    while (true) {
+      if (k < shard_size(pshard)) {
+        gnext = psa + (int64_t)(pshard + 8 * k) * kPU;
+        ulo = psg;
+        uhi = min(sghi, gnext + kPU);
+        more = true;
+        if (lane == 0) ahead = (int)atomicAdd(&heads[pshard], 1u);   // the next claim, ahead
+        ahead_out = true;
+        return;
+      }
+      // this shard is exhausted: read every head (one round trip, at memory side)
+      // and steal from the shard with the most unclaimed units
+      int rem = -1;
+      if (lane < 8) rem = shard_size(lane) - (int)atomicAdd(&heads[lane], 0u);
+      int best = 0, brem = __builtin_amdgcn_readlane(rem, 0);
+#pragma unroll
+      for (int s = 1; s < 8; ++s) {
+        const int r = __builtin_amdgcn_readlane(rem, s);
+        if (r > brem) { brem = r; best = s; }
+      }
+      if (brem <= 0) { more = false; return; }
+      pshard = best;
+      int kk = 0;
+      if (lane == 0) kk = (int)atomicAdd(&heads[pshard], 1u);
+      k = __builtin_amdgcn_readfirstlane(kk);
+    }
+  };
+  if (!more) { in_pool = true; pool_next(); }
+
+  // ---- K7: Bernoulli selection of the next work unit, compacted into the ring
   auto refill = [&]() {
-    while ((tail - head) < (uint32_t)(2 * U) && gnext < ghi) {
+    while ((tail - head) < (uint32_t)(2 * U) && more) {
       const int64_t r0 = gnext + 4 * lane;
       u32x4 h{0u, 0u, 0u, 0u};
-      if (!p.full && !EVAL && r0 < ghi) h = philox_block(p.seed, p.step, (uint64_t)r0 >> 2);
+      if (!p.full && !EVAL && r0 < uhi) h = philox_block(p.seed, p.step, (uint64_t)r0 >> 2);
       const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int64_t gr = r0 + j;
-        const bool sel = (gr >= glo) && (gr < ghi) && (EVAL || p.full || hv[j] < p.thr);
+        const bool sel = (gr >= ulo) && (gr < uhi) && (EVAL || p.full || hv[j] < p.thr);
         const uint64_t m = __ballot(sel);
         const uint32_t pos = tail + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         if (sel) ring[pos & (kRing - 1)] = (int)(gr - p.row_offset - lo);
         tail += (uint32_t)__popcll(m);
       }
-      // claim the next group dynamically: waves that drew few selected rows
-      // take more groups, so the block's waves finish together
-      int gi = 0;
-      if (lane == 0) gi = atomicAdd(&s_next, 1);
-      gnext = gstart + (int64_t)__builtin_amdgcn_readfirstlane(gi) * 256;
+      // claim the next unit dynamically: waves that drew few selected rows
+      // take more units, so the block's waves finish together
+      if (!in_pool) {
+        int gi = 0, w = 4;
+        if (!p.atomic_out) {
+          // fixed-order epilogue: a fixed group -> wave map (wave w takes groups
+          // w, w + NW, ...), so every partial sum is bitwise repeatable
+          gi = sclaim;
+          sclaim += 4 * NW;
+        } else {
+          if (lane == 0) {
+            if (p.fine_q > 0 && nq - *(volatile int*)&s_next <= p.fine_q) w = 1;
+            gi = atomicAdd(&s_next, w);
+          }
+          gi = __builtin_amdgcn_readfirstlane(gi);
+          w = __builtin_amdgcn_readfirstlane(w);
+        }
+        if (gi < nq) {
+          gnext = gstart + (int64_t)gi * 64;
+          uhi = min(ghi, gnext + 64 * w);
+          // the block's last static unit: claim the first pool unit now, so it is
+          // back before it is needed
+          if (has_pool && !ahead_out && gi + w >= nq) {
+            if (lane == 0) ahead = (int)atomicAdd(&heads[pshard], 1u);
+            ahead_out = true;
+          }
+        } else {
+          in_pool = true;
+        }
+      }
+      if (in_pool) pool_next();
     }
     __builtin_amdgcn_wave_barrier();
   };
@@ -383,10 +488,12 @@ lr_rows_kernel(LrParams p) {
 
   // ---- software-pipelined sweep: load(i+1) || compute(i)
   Batch<NC, U> A;
+  unsigned long long t_first = 0ull;
   if constexpr (PIPE) {
     Batch<NC, U> B;
     refill();
     take_and_load(A);
+    if (tr) t_first = __builtin_amdgcn_s_memrealtime();
     while (true) {
       if (A.n == 0) break;
       refill();
@@ -404,6 +511,13 @@ lr_rows_kernel(LrParams p) {
       if (A.n == 0) break;
       compute(A);
     }
+  }
+  if (tr && lane == 0) {
+    tr[0] = t_start;
+    tr[1] = t_first;
+    tr[2] = __builtin_amdgcn_s_memrealtime();
+    tr[4] = (unsigned long long)cntf;
+    tr[5] = __smid();
   }
   __syncthreads();   // rings are dead: the arena becomes the reduction buffer
   if (p.probe_no_epilogue) {
@@ -449,6 +563,10 @@ lr_rows_kernel(LrParams p) {
         __hip_atomic_fetch_add(&p.C[seg], sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (p.count_acc)
           __hip_atomic_fetch_add(p.count_acc, (double)sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (tr) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) tr[3] = __builtin_amdgcn_s_memrealtime();
       }
       if (p.ticket == nullptr) return;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this block's adds are performed
@@ -586,7 +704,13 @@ static hipError_t dispatch_lr(const LrParams& p, int is_bf16, int gx, int nseg, 
   }
 }
 
+static unsigned long long* g_lr_trace = nullptr;
+
 extern "C" {
+
+// diagnostics: route the per-wave timeline of later dalgo_lr_grad launches to `buf`
+// (nullptr: off). Sized by the caller: 8 u64 per wave of the launch.
+void dalgo_lr_set_trace(void* buf) { g_lr_trace = static_cast<unsigned long long*>(buf); }
 
 // Maximum supported row stride: 4 chunks/lane -> 2048 bf16 or 1024 f32 columns.
 int dalgo_lr_max_cols(int is_bf16) { return is_bf16 ? 2048 : 1024; }
@@ -598,7 +722,7 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int variant,
                          const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
                          float upd_reg_alpha, double* count_acc, const DalgoLrTail* tail,
-                         hipStream_t st) {
+                         unsigned* pool, int pool_parity, hipStream_t st) {
   LrParams p{};
   if (tail != nullptr) {
     if (nseg != 1 || !((variant >> 8) & 1) || Wprev != nullptr || tail->ticket == nullptr ||
@@ -625,6 +749,10 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
   p.cnt1 = cnt1; p.cnt2 = cnt2; p.G = G; p.C = C; p.S = S;
   p.atomic_out = (variant >> 8) & 1;   // bit 8 of the variant selects the atomic epilogue
   p.probe_no_epilogue = (variant >> 9) & 1;
+  p.fine_q = 4 * ((variant >> 16) & 0xff);   // bits 16..23: fine-claim threshold in groups
+  p.trace = g_lr_trace;
+  p.pool = pool;
+  p.pool_parity = pool_parity & 1;
   return dispatch_lr<false>(p, is_bf16, gx, nseg, variant & 0xff, st);
 }
 

@@ -22,6 +22,7 @@ extern "C" {
 
 // ---- K1/K7/K10 logistic regression (lr_grad.hip)
 int dalgo_lr_max_cols(int is_bf16);
+void dalgo_lr_set_trace(void* buf);
 hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const int64_t* seg,
                          int64_t ld, int64_t row_offset, int D, int ldw, int has_bias, float eps,
                          uint64_t seed, uint64_t step, uint32_t thr, int full, int is_bf16,
@@ -29,7 +30,7 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int variant,
                          const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
                          float upd_reg_alpha, double* count_acc, const DalgoLrTail* tail,
-                         hipStream_t st);
+                         unsigned* pool, int pool_parity, hipStream_t st);
 hipError_t dalgo_lr_eval(const void* X, const float* y, const float* W, const int64_t* seg,
                          int64_t ld, int D, int ldw, int has_bias, float eps, int is_bf16, int gx,
                          int nseg, int rows_per_block, unsigned long long* correct, float* loss,

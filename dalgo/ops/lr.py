@@ -30,6 +30,12 @@ import os
 #   TARGET_BLOCKS   = workgroups per launch (split over segments)
 LR_VARIANT = int(os.environ.get("DALGO_LR_VARIANT", "3"))   # 8 waves, pipelined (bench sweep)
 _TARGET_BLOCKS = int(os.environ.get("DALGO_LR_BLOCKS", "256"))
+#   FINE_GROUPS     = switch the in-block work claims from 256-row groups to 64-row
+#                     quarters once fewer than this many groups are unclaimed (0 = off)
+LR_FINE_GROUPS = int(os.environ.get("DALGO_LR_FINE", "8"))
+#   POOL_FRAC       = share of each segment's rows left to the cross-block pool that
+#                     blocks claim from once their static range is done (0 = off)
+LR_POOL_FRAC = float(os.environ.get("DALGO_LR_POOL", "0"))
 #   DETERMINISTIC   = combine per-block partials with the fixed-order two-level
 #                     hand-off (bitwise repeatable) instead of float atomics
 DETERMINISTIC = os.environ.get("DALGO_DETERMINISTIC", "0") == "1"
@@ -56,10 +62,15 @@ def pad_features(X: torch.Tensor) -> torch.Tensor:
     return out[:, : X.shape[1]]
 
 
-def _grid(n_rows: int, nseg: int, target_blocks: int | None = None):
+def _grid(n_rows: int, nseg: int, target_blocks: int | None = None, pool_frac: float = 0.0):
+    """Blocks per segment and static rows per block (multiple of 256). With pool_frac > 0
+    the static ranges cover about (1 - pool_frac) of the rows; the rest is the segment's
+    cross-block pool, claimed dynamically (csrc/kernels/lr_grad.hip)."""
     per_seg = max(1, (target_blocks or _TARGET_BLOCKS) // max(1, nseg))
-    rpb = max(256, int(math.ceil(n_rows / per_seg / 256.0)) * 256)
-    gx = max(1, int(math.ceil(n_rows / rpb)))
+    static_rows = n_rows * (1.0 - min(max(pool_frac, 0.0), 0.9))
+    rpb = max(256, int(math.ceil(static_rows / per_seg / 256.0)) * 256)
+    gx = max(1, min(per_seg, int(math.ceil(n_rows / rpb)))) if pool_frac > 0 else \
+        max(1, int(math.ceil(n_rows / rpb)))
     return gx, rpb
 
 
@@ -70,6 +81,8 @@ class _Workspace:
     cnt1: torch.Tensor
     cnt2: torch.Tensor
     ticket: torch.Tensor   # fused-tail arrival counter (re-armed by the kernel)
+    pool: torch.Tensor     # cross-block pool claim heads, 2 parity sets x n_seg x 8 shards
+    launches: int = 0      # parity of the next launch = launches & 1
 
 
 _ws_cache: dict = {}
@@ -86,6 +99,7 @@ def _workspace(device, nseg, gx, S) -> _Workspace:
             cnt1=torch.zeros(nseg * ngroups, dtype=torch.int32, device=device),
             cnt2=torch.zeros(nseg, dtype=torch.int32, device=device),
             ticket=torch.zeros(1, dtype=torch.int32, device=device),
+            pool=torch.zeros(2 * nseg * 8, dtype=torch.int32, device=device),
         )
         _ws_cache[key] = ws
     return ws
@@ -98,7 +112,8 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
             variant: int | None = None, target_blocks: int | None = None,
             w_prev: torch.Tensor | None = None, update: dict | None = None,
             count_acc: torch.Tensor | None = None, g_is_zero: bool = False,
-            deterministic: bool | None = None, tail: dict | None = None):
+            deterministic: bool | None = None, tail: dict | None = None,
+            pool_frac: float | None = None):
     """Per-segment gradient SUM and selected-row COUNT.
 
     X: [n, >=D] (bf16/f32), y: [n] f32, W: [n_seg, ldw] f32 models,
@@ -136,12 +151,22 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
             else:
                 b = seg.tolist()
                 max_seg_rows = max(b[i + 1] - b[i] for i in range(nseg))
-        gx, rpb = _grid(max(int(max_seg_rows), 1), nseg, target_blocks)
+        det = DETERMINISTIC if deterministic is None else bool(deterministic)
+        # dynamic work placement (cross-block pool) only with the atomic epilogue: the
+        # deterministic paths keep a fixed row -> block -> wave assignment
+        pf = (LR_POOL_FRAC if pool_frac is None else float(pool_frac)) \
+            if (not det and w_prev is None) else 0.0
+        gx, rpb = _grid(max(int(max_seg_rows), 1), nseg, target_blocks, pf)
         S = ((D + 2 + 63) // 64) * 64
         ws = _workspace(X.device, nseg, gx, S)
+        pool = {}
+        if pf > 0:
+            pool = dict(pool=ws.pool, pool_parity=ws.launches & 1)
+            ws.launches += 1
         u = update or {}
         var = LR_VARIANT if variant is None else int(variant)
-        det = DETERMINISTIC if deterministic is None else bool(deterministic)
+        if not (var >> 16):
+            var |= (LR_FINE_GROUPS & 0xff) << 16
         if tail is not None:
             if det or w_prev is not None or nseg != 1:
                 raise ValueError("fused tail needs the atomic epilogue, one model, no prologue update")
@@ -160,7 +185,7 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
                                tail_reg=int(tail.get("reg", 0)), tail_eta=float(tail.get("eta", 0.0)),
                                tail_lam=float(tail.get("lam", 0.0)),
                                tail_reg_alpha=float(tail.get("reg_alpha", 0.0)),
-                               tail_count_acc=tail.get("count_acc"), **kw)
+                               tail_count_acc=tail.get("count_acc"), **kw, **pool)
             return G, C
         if not det and w_prev is None:
             if not g_is_zero:
@@ -172,7 +197,7 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
                            ws.cnt1, ws.cnt2, G, C, var,
                            w_prev, int(u.get("mode", 0)), int(u.get("reg", 0)),
                            float(u.get("eta", 0.0)), float(u.get("lam", 0.0)),
-                           float(u.get("reg_alpha", 0.0)), count_acc)
+                           float(u.get("reg_alpha", 0.0)), count_acc, **pool)
         return G, C
     if w_prev is not None:
         from dalgo.ops import update as U

@@ -62,6 +62,27 @@ def test_lr_grad_single_segment_deterministic(cuda):
     assert rel < 1e-4
 
 
+@pytest.mark.parametrize("pool_frac", [0.1, 0.3])
+@pytest.mark.parametrize("fine", [0, 8])
+def test_lr_grad_work_pool(cuda, pool_frac, fine):
+    """Cross-block work pool + fine in-block claims select and sum exactly the same rows
+    (several launches: the two claim-head parity sets alternate and re-arm each other)."""
+    n, D = 300_000, 1024
+    X, y = _data(n, D, torch.bfloat16, seed=5)
+    Xd, yd = X.to(cuda), y.to(cuda)
+    seg = torch.tensor([0, 70_001, 190_000, n], dtype=torch.int64)
+    W = torch.randn(3, D + 1, generator=torch.Generator().manual_seed(4)) * 0.05
+    for step in range(4):
+        kw = dict(D=D, frac=0.1, step=step, seed=11)
+        G_ref, C_ref = L.lr_grad(X, y, W.double(), seg, **kw)
+        Gd, Cd = L.lr_grad(Xd, yd, W.to(cuda), seg.to(cuda), pool_frac=pool_frac,
+                           variant=L.LR_VARIANT | (fine << 16), **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(Cd.cpu().double(), C_ref), (step, Cd, C_ref)
+        rel = (Gd.cpu().double() - G_ref).abs().max() / G_ref.abs().max()
+        assert rel < 1e-4, (step, rel)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_lr_eval(cuda, dtype):
     X, y = _data(7777, 100, dtype, seed=5)
