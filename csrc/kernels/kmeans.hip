@@ -439,6 +439,236 @@ kmeans_assign_res_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
 }
 
 // ---------------------------------------------------------------------------
+// K2 "pipelined" form (bf16): distance keys + LDS-DMA centre chunks, built so the
+// MFMA pipe is not starved by LDS waits, barriers or a long VALU epilogue:
+//  * centre chunks (32*NSUB rows) go global -> LDS by LDS-DMA (global_load_lds_dwordx4,
+//    no staging VGPRs), triple-buffered: chunk ch+2 is in flight while ch is consumed,
+//    and one raw s_barrier per chunk both publishes chunk ch and retires chunk ch-1;
+//  * the MFMA produces a shifted half-distance directly: B = -x (sign bits flipped
+//    once), C = 0.5|c|^2 + M with M = max over the block's points of 0.5|x|^2, so
+//    acc = 0.5|x - c|^2 + (M - 0.5|x|^2) >= 0 for every (point, centre) of the block;
+//    C comes from an LDS-resident copy of 0.5|c|^2 + M (no accumulator-init moves);
+//  * non-negative floats order like their int bits, so the per-sub-tile argmin is an
+//    integer min over keys (bits & ~31) | r: one v_and_or + half a v_min3 per
+//    distance (the compare / two-select form costs 3 VALU); the 5 dropped bits are
+//    2^-18 relative, far below the bf16 operand rounding. A strict compare per
+//    sub-tile keeps ties at the lowest id (ascending centre order per lane);
+//  * the next sub-tile's A fragments and C values are read under the current MFMAs.
+// Two 4-wave blocks per CU (launch_bounds min 2 -> 256 VGPRs, 2 waves/SIMD): one
+// block's point loads and first chunk overlap the other block's MFMAs.
+// The source side of the LDS-DMA carries the XOR swizzle (the LDS image is written
+// lane-linear): slot (row, jj) holds piece jj ^ (row & SWZ) of centre `row`.
+template <int N>
+__device__ __forceinline__ void km_wait_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
+}
+typedef __attribute__((address_space(3))) void km_lds_void;
+
+template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF>
+__global__ void __launch_bounds__(NW * 64, MINB)
+kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
+                          const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int kpad,
+                          int* __restrict__ assign, float* __restrict__ mind,
+                          double* __restrict__ sse) {
+  constexpr int KS = DP / 16;                  // 32x32x16 k-steps per centre row
+  constexpr int NJ = DP * 2 / 16;              // 16-B pieces per row (= 2 KS)
+  constexpr int SWZ = (NJ >= 16 ? 16 : NJ) - 1;
+  constexpr int CH = 32 * NSUB;
+  constexpr int NT = NW * 64;
+  constexpr int CHP = CH * NJ;                 // 16-B pieces per chunk
+  constexpr int GPT = CHP / NT;                // LDS-DMA instructions per thread per chunk
+  static_assert(CHP % NT == 0, "chunk must be a whole number of block-wide DMA rounds");
+  static_assert(NBUF == 2 || NBUF == 3, "double or triple buffered chunks");
+  __shared__ __attribute__((aligned(16))) uint4 s_c[NBUF * CHP];
+  extern __shared__ __attribute__((aligned(16))) float s_hn[];   // [kpad]: 0.5|c|^2 + M
+  __shared__ float s_m[NW];
+  __shared__ double s_sse[NW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, cl = lane & 31;
+  const int64_t pbase = ((int64_t)blockIdx.x * NW + wid) * (PT * 32);
+  const int nchunk = kpad / CH;
+
+  // ---- points (B operand, negated), resident for the whole sweep; rows past n are zero
+  uint4 bf[PT][KS];
+  float x2[PT];                                // |x|^2 of the lane's point (both halves)
+#pragma unroll
+  for (int t = 0; t < PT; ++t) {
+    const int64_t p = pbase + t * 32 + cl;
+    const bool ok = p < n;
+    const uint16_t* src = X + (ok ? p : 0) * ldx + h * 8;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const uint4 v = *reinterpret_cast<const uint4*>(src + 16 * s);
+      bf[t][s] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  // all ordinary loads retired before the DMA stream starts, and the fragments pinned
+  // here, so the compiler's own waits never drain a chunk in flight (vmcnt(0) in-loop)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float mx = 0.f;
+#pragma unroll
+  for (int t = 0; t < PT; ++t) {
+    float q = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      asm volatile("" : "+v"(bf[t][s].x), "+v"(bf[t][s].y), "+v"(bf[t][s].z), "+v"(bf[t][s].w));
+      q += sq_sum(bf[t][s], uint16_t{});
+      bf[t][s] = make_uint4(bf[t][s].x ^ 0x80008000u, bf[t][s].y ^ 0x80008000u,
+                            bf[t][s].z ^ 0x80008000u, bf[t][s].w ^ 0x80008000u);
+    }
+    auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(q), __float_as_uint(q), false, false);
+    x2[t] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    mx = fmaxf(mx, 0.5f * x2[t]);
+  }
+  for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+  if (lane == 0) s_m[wid] = mx;
+  __syncthreads();
+  float M = s_m[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) M = fmaxf(M, s_m[w]);
+  // slack so that rounding of the MFMA sum cannot push a near-zero distance negative
+  M = M * 1.0001f + 1e-6f;
+  for (int c = tid; c < kpad; c += NT) s_hn[c] = hn[c] + M;
+
+  // per-thread DMA sources: slot q = g*NT + tid of the chunk image
+  int src_off[GPT];
+#pragma unroll
+  for (int g = 0; g < GPT; ++g) {
+    const int q = g * NT + tid, row = q / NJ, jj = q % NJ;
+    src_off[g] = row * DP + (jj ^ (row & SWZ)) * 8;
+  }
+  // Issued as inline asm: with the builtin, hipcc cannot tell the DMA target from the
+  // chunk being read and drains vmcnt(0) before every ds_read (the chunk in flight
+  // would then never overlap compute). The counted waits below are the only waits.
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(km_lds_void*)s_c;
+  auto issue = [&](int ch) {
+    const uint16_t* base = Cq + (int64_t)ch * CH * DP;
+    const uint32_t dst = lds0 + (uint32_t)(((ch % NBUF) * CHP) * 16);
+#pragma unroll
+    for (int g = 0; g < GPT; ++g) {
+      const uint32_t m0v = __builtin_amdgcn_readfirstlane(dst + (uint32_t)((g * NT + wid * 64) * 16));
+      const uint16_t* src = base + src_off[g];
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                   :: "s"(m0v), "v"(src) : "memory");
+    }
+  };
+
+  int bkey[PT], bsub[PT];
+#pragma unroll
+  for (int t = 0; t < PT; ++t) { bkey[t] = 0x7fffffff; bsub[t] = 0; }
+  int kmask;   // key mask in a VGPR so each pack is ONE v_and_or_b32 (VGPR mask, inline r)
+  asm volatile("v_mov_b32 %0, 0xffffffe0" : "=v"(kmask));
+
+  // lane's A-row base inside a chunk image: row = sub*32 + cl, piece (2s + h) ^ (cl & SWZ)
+  const int arow = cl * NJ;
+  const int asw = cl & SWZ;
+  auto load_frag = [&](const uint4* img, int sub, int cb, uint4 (&a)[KS], f32x16& hc) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) a[s] = img[sub * 32 * NJ + arow + ((2 * s + h) ^ asw)];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 v = *reinterpret_cast<const float4*>(&s_hn[cb + 8 * g + 4 * h]);
+      hc[4 * g + 0] = v.x; hc[4 * g + 1] = v.y; hc[4 * g + 2] = v.z; hc[4 * g + 3] = v.w;
+    }
+  };
+
+  issue(0);
+  if (NBUF == 3 && nchunk > 1) issue(1);
+  for (int ch = 0; ch < nchunk; ++ch) {
+    if (NBUF == 3 && ch + 1 < nchunk) km_wait_vmcnt<GPT>();   // chunk ch landed, ch+1 in flight
+    else km_wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // s_hn stores (first chunk)
+    // publishes chunk ch to every wave AND retires everyone's reads of chunk ch-1,
+    // whose buffer is refilled next (triple: chunk ch+2 after this chunk's MFMAs;
+    // double: chunk ch+1 right away)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (NBUF == 2 && ch + 1 < nchunk) issue(ch + 1);
+    const uint4* img = s_c + (ch % NBUF) * CHP;
+    uint4 a[KS];
+    f32x16 hc;
+    load_frag(img, 0, ch * CH, a, hc);
+#pragma unroll
+    for (int sub = 0; sub < NSUB; ++sub) {
+      const int cb = ch * CH + sub * 32;
+      uint4 an[KS];
+      f32x16 hn_next;
+      if (PF && sub + 1 < NSUB) load_frag(img, sub + 1, cb + 32, an, hn_next);
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            __builtin_bit_cast(bf16x8, a[0]), __builtin_bit_cast(bf16x8, bf[t][0]), hc, 0, 0, 0);
+#pragma unroll
+        for (int s = 1; s < KS; ++s)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              __builtin_bit_cast(bf16x8, a[s]), __builtin_bit_cast(bf16x8, bf[t][s]), acc, 0, 0, 0);
+        int m = 0x7fffffff;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const int k0 = (__float_as_int(acc[r]) & kmask) | r;
+          const int k1 = (__float_as_int(acc[r + 1]) & kmask) | (r + 1);
+          m = min(min(m, k0), k1);   // one v_min3_i32 per pair
+        }
+        // strict: an equal key of a later sub-tile (higher ids) never displaces
+        const bool take = m < bkey[t];
+        bkey[t] = take ? m : bkey[t];
+        bsub[t] = take ? cb : bsub[t];
+      }
+      if (sub + 1 < NSUB) {
+        if constexpr (PF) {
+#pragma unroll
+          for (int s = 0; s < KS; ++s) a[s] = an[s];
+          hc = hn_next;
+        } else {
+          load_frag(img, sub + 1, cb + 32, a, hc);
+        }
+      }
+    }
+    if (NBUF == 3 && ch + 2 < nchunk) issue(ch + 2);
+  }
+
+  // ---- decode, combine the two lane halves (same point, disjoint centre rows)
+  double my_sse = 0.0;
+#pragma unroll
+  for (int t = 0; t < PT; ++t) {
+    const int r = bkey[t] & 31;
+    const float v = __int_as_float(bkey[t] & ~31);
+    const int mi = bsub[t] + (r & 3) + 8 * (r >> 2) + 4 * h;
+    auto sv = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    auto si = __builtin_amdgcn_permlane32_swap((uint32_t)mi, (uint32_t)mi, false, false);
+    const float pv = __uint_as_float(h ? sv[0] : sv[1]);
+    const int pi = (int)(h ? si[0] : si[1]);
+    float bv = v;
+    int bi = mi;
+    if (pv < bv || (pv == bv && pi < bi)) { bv = pv; bi = pi; }
+    const int64_t p = pbase + t * 32 + cl;
+    if (h == 0 && p < n) {
+      // acc = 0.5|x-c|^2 + M - 0.5|x|^2
+      const float dist = fmaxf(2.f * (bv - M) + x2[t], 0.f);
+      assign[p] = bi;
+      if (mind) mind[p] = dist;
+      my_sse += (double)dist;
+    }
+  }
+  if (sse) {
+    double s = my_sse;
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) s_sse[wid] = s;
+    __syncthreads();
+    if (tid == 0) {
+      double tot = 0.0;
+      for (int w = 0; w < NW; ++w) tot += s_sse[w];
+      atomicAdd(sse, tot);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K3: range-partitioned LDS accumulation. grid = (row chunks, cluster ranges).
 template <typename T, int DP, int CR, int NW>
 __global__ void __launch_bounds__(NW * 64)
@@ -748,6 +978,33 @@ static hipError_t launch_assign_res(const void* X, int64_t n, int64_t ldx, const
   return hipSuccess;
 }
 
+// pipelined K2 (bf16, DP >= 64): grid = one PT-tile group per wave, MINB blocks per CU
+template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF>
+static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, const void* Cq,
+                                     const float* hn, int kpad, int* assign, float* mind,
+                                     double* sse, hipStream_t st) {
+  constexpr int CH = 32 * NSUB;
+  constexpr size_t kStatic = NBUF * (size_t)CH * DP * 2;
+  if (kpad % CH) return hipErrorInvalidValue;
+  const size_t dyn = (size_t)kpad * sizeof(float);
+  if (kStatic + dyn + 1024 > 160 * 1024) return hipErrorInvalidValue;
+  const int64_t grid = cdiv(n, (int64_t)NW * PT * 32);
+  if (grid == 0) return hipSuccess;
+  if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
+  auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF>;
+  static size_t attr_set = 0;   // largest dynamic size this instantiation was enabled for
+  if (dyn > attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)dyn);
+    if (e != hipSuccess) return e;
+    attr_set = dyn;
+  }
+  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(NW * 64), dyn, st, (const uint16_t*)X, n, ldx,
+                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
 // variant: 0 = 8 waves x 32-centre chunks, 1 = 4 waves x 32, 2 = 4 waves x 128,
 //          3 = 8 waves x 128, 4 = 4 waves x 64, 5 = variant 0 capped at 128 VGPRs
 //          (4 waves/SIMD: two 8-wave blocks per CU), 6 = 4 waves x 4 point tiles (128
@@ -755,7 +1012,11 @@ static hipError_t launch_assign_res(const void* X, int64_t n, int64_t ldx, const
 //          VGPRs (four blocks per CU), 9 = variant 5 with 64-centre chunks,
 //          10 = 16 waves (1024 points per block) capped at 128 VGPRs,
 //          11 / 12 / 13 = resident-centre form (bf16; f32 uses 5): 8 waves x 2 point
-//          tiles, 4 waves x 4 tiles, 8 waves x 1 tile
+//          tiles, 4 waves x 4 tiles, 8 waves x 1 tile,
+//          14..17 = pipelined distance-key form (bf16, DP >= 64; otherwise 5), 4 waves x
+//          64-centre chunks: 14 = 2 tiles/wave, 2 blocks/CU, triple-buffered, A prefetch;
+//          15 = 3 blocks/CU, no prefetch; 16 = 1 tile/wave, 4 blocks/CU, double-buffered;
+//          17 = 2 tiles, 3 blocks/CU, double-buffered
 template <typename T, int DP>
 static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                    const float* hn, int kpad, int* assign, float* mind, double* sse,
@@ -777,6 +1038,14 @@ static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const 
         if (variant == 11) return launch_assign_res<DP, 8, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
         if (variant == 12) return launch_assign_res<DP, 4, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
         return launch_assign_res<DP, 8, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+      }
+      return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 14: case 15: case 16: case 17:
+      if constexpr (sizeof(T) == 2 && DP >= 64) {
+        if (variant == 14) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 15) return launch_assign_pipe<DP, 4, 2, 2, 3, 3, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 16) return launch_assign_pipe<DP, 4, 1, 2, 4, 2, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        return launch_assign_pipe<DP, 4, 2, 2, 3, 2, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
       }
       return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
     default: return hipErrorInvalidValue;

@@ -77,11 +77,12 @@ def refresh(cen: Centers):
 import os
 
 # launch variant of the assign kernel (table in csrc/kernels/kmeans.hip). -1 = per
-# dtype: f32 -> 5 (8-wave blocks capped at 128 VGPRs, two blocks per CU), bf16 -> 5
-# until the resident-centre form (11/12/13) is measured on the GPU
+# dtype: f32 -> 5 (8-wave blocks capped at 128 VGPRs, two blocks per CU), bf16 -> 14
+# (pipelined distance-key form: 4.87 vs 5.20 ms for variant 5 at 20M x 128 x 1024 on
+# one MI355X; DP < 64 falls back to 5 inside the launcher)
 ASSIGN_VARIANT = int(os.environ.get("DALGO_KM_VARIANT", "-1"))
 RESIDENT_VARIANTS = (11, 12, 13)
-_BF16_DEFAULT = 5
+_BF16_DEFAULT = 14
 _scratch: dict = {}
 
 

@@ -28,6 +28,28 @@ def test_kmeans_assign_resident(cuda, variant, d, k, n):
     _check_assign(cuda, torch.bfloat16, d, k, n, variant)
 
 
+# pipelined K2 (bf16, LDS-DMA triple-buffered centre chunks): DP = 64 / 128 (smaller DP
+# falls back to variant 5), ragged tile groups, one and many chunks
+@pytest.mark.parametrize("variant", [14, 15, 16, 17])
+@pytest.mark.parametrize("d,k,n", [(2, 2, 6), (50, 33, 4099), (100, 1500, 9000),
+                                   (128, 1024, 20000), (128, 600, 70001), (64, 128, 513)])
+def test_kmeans_assign_pipelined(cuda, variant, d, k, n):
+    _check_assign(cuda, torch.bfloat16, d, k, n, variant)
+
+
+def test_kmeans_pipelined_ties(cuda):
+    """Exact ties resolve to the lowest id across sub-tiles, chunks and lane halves."""
+    X = torch.zeros(300, 128)
+    C0 = torch.zeros(1100, 128) + 50.0
+    for c in (3, 7, 12, 515, 1030):
+        C0[c] = 0.0
+        C0[c, c % 128] = 1.0
+    for v in (14, 15, 16, 17):
+        a = K.assign(K.prepare_points(X.to(cuda).bfloat16()), K.make_centers(C0, torch.bfloat16, cuda),
+                     variant=v).cpu()
+        assert a.tolist() == [3] * 300, v
+
+
 def test_kmeans_resident_ties_and_passes(cuda):
     """Exact ties resolve to the lowest id inside a pass, across lane halves and across passes."""
     X = torch.zeros(70, 8)
