@@ -211,41 +211,46 @@ lr_rows_kernel(LrParams p) {
   const int64_t seg_lo = p.seg[seg], seg_hi = p.seg[seg + 1];
   const int64_t lo = seg_lo + (int64_t)bx * p.rows_per_block;
   const int64_t hi = max(lo, min(seg_hi, lo + (int64_t)p.rows_per_block));
-  // model fragment in registers (optionally applying the previous step's update)
+  // model fragment in registers (optionally applying the previous step's update).
+  // Fetched AFTER the first row batch is issued (see the sweep): the W / Wprev reads
+  // then overlap the first rows' HBM latency instead of preceding them, and the
+  // work-claim barrier below does not wait for them.
   float wr[NC][VEC];
-  float wb;
-  if (p.Wprev == nullptr) {
-    const float* w = p.W + (int64_t)seg * p.ldw;
+  float wb = 0.f;
+  auto load_w = [&]() {
+    if (p.Wprev == nullptr) {
+      const float* w = p.W + (int64_t)seg * p.ldw;
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
+      for (int c = 0; c < NC; ++c)
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        int col = (c * 64 + lane) * VEC + e;
-        wr[c][e] = (col < p.D) ? w[col] : 0.f;
-      }
-    wb = p.has_bias ? w[p.D] : 0.f;
-  } else {
-    const float cprev = p.Cprev[0];
-    float* wout = const_cast<float*>(p.W);
-    const bool writer = (bx == 0 && wid == 0);
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        int col = (c * 64 + lane) * VEC + e;
-        float v = 0.f;
-        if (col < p.D) {
-          v = fused_update(p.Wprev[col], p.Gprev[col], cprev, p);
-          if (writer) wout[col] = v;
+        for (int e = 0; e < VEC; ++e) {
+          int col = (c * 64 + lane) * VEC + e;
+          wr[c][e] = (col < p.D) ? w[col] : 0.f;
         }
-        wr[c][e] = v;
+      wb = p.has_bias ? w[p.D] : 0.f;
+    } else {
+      const float cprev = p.Cprev[0];
+      float* wout = const_cast<float*>(p.W);
+      const bool writer = (bx == 0 && wid == 0);
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          int col = (c * 64 + lane) * VEC + e;
+          float v = 0.f;
+          if (col < p.D) {
+            v = fused_update(p.Wprev[col], p.Gprev[col], cprev, p);
+            if (writer) wout[col] = v;
+          }
+          wr[c][e] = v;
+        }
+      wb = 0.f;
+      if (p.has_bias) {
+        wb = fused_update(p.Wprev[p.D], p.Gprev[p.D], cprev, p);
+        if (writer && lane == 0) wout[p.D] = wb;
       }
-    wb = 0.f;
-    if (p.has_bias) {
-      wb = fused_update(p.Wprev[p.D], p.Gprev[p.D], cprev, p);
-      if (writer && lane == 0) wout[p.D] = wb;
     }
-  }
+  };
 
   float g[NC][VEC];
 #pragma unroll
@@ -493,6 +498,7 @@ lr_rows_kernel(LrParams p) {
     Batch<NC, U> B;
     refill();
     take_and_load(A);
+    load_w();
     if (tr) t_first = __builtin_amdgcn_s_memrealtime();
     while (true) {
       if (A.n == 0) break;
@@ -505,6 +511,7 @@ lr_rows_kernel(LrParams p) {
       compute(B);
     }
   } else {
+    load_w();
     while (true) {
       refill();
       take_and_load(A);
