@@ -70,16 +70,15 @@ def main(argv=None):
     model = ParallelSGD(cfg, data, layout, rt)
     count = torch.zeros(1, dtype=torch.float64, device=rt.device)
 
-    step_fn = model.step
-    for _ in range(a.warmup):
-        step_fn()
+    # model.run_steps(k): k full training steps, either k step() calls or (SSGD / GD with
+    # DALGO_PERSISTENT=1) one persistent K1 launch running all k steps
+    model.run_steps(a.warmup)
     rt.synchronize()
     rt.barrier()
     rt.synchronize()
     model.count_acc = count
     t_start = time.perf_counter()
-    for _ in range(a.steps):
-        step_fn()
+    model.run_steps(a.steps)
     rt.synchronize()
     rt.barrier()
     rt.synchronize()
@@ -89,6 +88,9 @@ def main(argv=None):
     xg = getattr(getattr(model, "bucket", None), "xg", None)
     if xg is not None:
         xg.check()   # raise (non-zero exit) if a peer wait ever timed out
+    from dalgo.ops import lr as lr_ops
+    lr_ops.check_persistent()   # ... or a persistent launch's step-release wait
+    launch = "persistent" if model._persistent() else "per-step"
     allreduce = "xgmi-oneshot (K11)" if xg is not None else (
         f"{rt.backend}" if W > 1 else "none (1 rank)")
 
@@ -118,7 +120,7 @@ def main(argv=None):
             "config": {"model": f"{a.algo.upper()} logistic regression", "global_batch": int(round(samples / a.steps)),
                        "seq_len": None, "features": a.dim, "rows": a.rows,
                        "minibatch_fraction": a.frac, "parallelism": f"dp{W}",
-                       "allreduce": allreduce},
+                       "allreduce": allreduce, "launch": launch},
             "per_gpu_samples_per_s": value / W,
             "effective_hbm_GBps_per_gpu": value / W * a.dim * (2 if dtype == torch.bfloat16 else 4) / 1e9,
             "datagen_s": gen_s,

@@ -82,7 +82,9 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
              int64_t xg_slot, int64_t xg_epoch, const std::optional<Tensor>& xg_err,
              double xg_timeout, int64_t tail_mode, int64_t tail_reg, double tail_eta,
              double tail_lam, double tail_reg_alpha, const std::optional<Tensor>& tail_count_acc,
-             const std::optional<Tensor>& pool, int64_t pool_parity) {
+             const std::optional<Tensor>& pool, int64_t pool_parity, int64_t nsteps,
+             const std::optional<Tensor>& epoch, int64_t epoch_base,
+             const std::optional<Tensor>& perr, double spin_s) {
   check_lr_inputs(X, y, W, seg, D, has_bias);
   unsigned* poolp = nullptr;
   if (pool.has_value()) {
@@ -93,6 +95,7 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
   }
   DalgoLrTail tail{};
   const DalgoLrTail* tailp = nullptr;
+  TORCH_CHECK(nsteps <= 1 || ticket.has_value(), "persistent launch needs the fused tail");
   if (ticket.has_value()) {
     check_dev(*ticket, "ticket");
     TORCH_CHECK(ticket->scalar_type() == at::kInt && ticket->numel() >= 1, "ticket int32[1]");
@@ -122,6 +125,21 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
       check_dev(*tail_count_acc, "tail_count_acc");
       TORCH_CHECK(tail_count_acc->scalar_type() == at::kDouble, "tail_count_acc f64");
       tail.count_acc = tail_count_acc->data_ptr<double>();
+    }
+    if (nsteps > 1) {
+      TORCH_CHECK(epoch.has_value() && perr.has_value() && !pool.has_value(),
+                  "persistent launch: epoch + perr counters, no work pool");
+      check_dev(*epoch, "epoch");
+      check_dev(*perr, "perr");
+      TORCH_CHECK(epoch->scalar_type() == at::kInt && perr->scalar_type() == at::kInt,
+                  "persistent launch: int32 epoch / perr");
+      TORCH_CHECK(nsteps < (1LL << 30) && epoch_base >= 0 && epoch_base <= 0xffffffffLL && spin_s > 0,
+                  "persistent launch: bad nsteps / epoch_base / spin_s");
+      tail.nsteps = (int)nsteps;
+      tail.epoch_ctr = reinterpret_cast<unsigned*>(epoch->data_ptr<int>());
+      tail.epoch_base = (uint32_t)epoch_base;
+      tail.perr = reinterpret_cast<unsigned*>(perr->data_ptr<int>());
+      tail.spin_s = spin_s;
     }
     tailp = &tail;
   }
@@ -675,7 +693,8 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(h!)? ticket=None, int[]? xg_bufs=None, int xg_rank=0, int xg_slot=0, int xg_epoch=0, "
         "Tensor(i!)? xg_err=None, float xg_timeout=0., int tail_mode=0, int tail_reg=0, "
         "float tail_eta=0., float tail_lam=0., float tail_reg_alpha=0., "
-        "Tensor(j!)? tail_count_acc=None, Tensor(k!)? pool=None, int pool_parity=0) -> ()");
+        "Tensor(j!)? tail_count_acc=None, Tensor(k!)? pool=None, int pool_parity=0, int nsteps=1, "
+        "Tensor(l!)? epoch=None, int epoch_base=0, Tensor(m!)? perr=None, float spin_s=2.) -> ()");
   m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
         "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=3) -> ()");
   m.def("sync_update(Tensor(a!) W, Tensor(d!)? G, Tensor(e!)? C, Tensor? center, Tensor? S, "

@@ -43,10 +43,12 @@ __device__ __forceinline__ float xg_update(float w, float g, float c, const XgUp
 // Block-wide: push get(i), i < n, into slot [phase][rank] of every rank's buffer,
 // publish one flag per destination and wait (bounded) until all W sources of this
 // epoch have landed in the local buffer. Every thread of the block must call it.
+// `epoch` is passed separately (a persistent launch walks L.epoch, L.epoch + 1, ...
+// without copying the link, whose pointer array would otherwise land in scratch).
 template <class Get>
-__device__ __forceinline__ void xg_push_publish_wait(const XgLink& L, int n, Get get) {
+__device__ __forceinline__ void xg_push_publish_wait(const XgLink& L, uint32_t epoch, int n, Get get) {
   const int tid = threadIdx.x;
-  const int ph = (int)(L.epoch & 1u);
+  const int ph = (int)(epoch & 1u);
   for (int k = 0; k < L.world; ++k) {            // destinations rotated: links evenly loaded
     const int r = (L.rank + k) % L.world;
     float* dst = xg_slot(L.bufs[r], ph, L.rank, L.slot);
@@ -55,12 +57,12 @@ __device__ __forceinline__ void xg_push_publish_wait(const XgLink& L, int n, Get
   __threadfence_system();
   __syncthreads();
   if (tid < L.world)
-    __hip_atomic_store(&xg_flags(L.bufs[tid])[ph * kXgMaxRanks + L.rank], L.epoch, __ATOMIC_RELAXED,
+    __hip_atomic_store(&xg_flags(L.bufs[tid])[ph * kXgMaxRanks + L.rank], epoch, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid < L.world) {
     uint32_t* f = &xg_flags(L.bufs[L.rank])[ph * kXgMaxRanks + tid];
     const long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != L.epoch) {
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
       __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - t0 > L.timeout_ticks) {
         atomicOr(L.err, 1u);
@@ -72,9 +74,9 @@ __device__ __forceinline__ void xg_push_publish_wait(const XgLink& L, int n, Get
 }
 
 // rank-ordered sum of element i over the W landed slots (identical on every rank)
-__device__ __forceinline__ float xg_sum(const XgLink& L, int i) {
+__device__ __forceinline__ float xg_sum(const XgLink& L, uint32_t epoch, int i) {
   uint8_t* mine = L.bufs[L.rank];
-  const int ph = (int)(L.epoch & 1u);
+  const int ph = (int)(epoch & 1u);
   float s = 0.f;
   for (int r = 0; r < L.world; ++r) s += __builtin_nontemporal_load(xg_slot(mine, ph, r, L.slot) + i);
   return s;

@@ -84,33 +84,58 @@ struct LrParams {
   XgLink xg;
   XgUpdate tu;
   double* tail_count_acc;  // += the GLOBAL minibatch size
+  // persistent multi-step mode (fused tail only): nsteps > 1 runs steps step ..
+  // step + nsteps - 1 in ONE cooperative launch (every block resident). The tail block
+  // of step i writes W / G / C / ticket through to the coherence point, then publishes
+  // epoch_base + i + 1 in *epoch; every block waits for it (bounded by spin_ticks of
+  // s_memrealtime; a timeout sets *perr and ends the launch) before it reads W for step
+  // i + 1 - by then its first row batch of step i + 1 is already in flight.
+  int nsteps;
+  unsigned* epoch;
+  uint32_t epoch_base;
+  unsigned* perr;
+  uint64_t spin_ticks;
 };
+
+__device__ __forceinline__ void wt_store(float* a, float v) {
+  __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // The last block of a fused-tail launch: every other block's atomics are performed
 // (each waited vmcnt(0) before taking its ticket), so agent-scope loads see the
 // complete local sums.
-__device__ __forceinline__ void lr_tail(const LrParams& p) {
+__device__ __forceinline__ void lr_tail(const LrParams& p, uint32_t xg_epoch) {
   const int n = p.ldw;                 // G row; index n carries the count
   float* G = p.G;
   float* W = const_cast<float*>(p.W);
   auto get = [&](int i) -> float {
     return __hip_atomic_load(i < n ? &G[i] : &p.C[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
+  // W is read with agent-scope loads too: in the persistent mode an earlier step's tail
+  // block (another CU / XCD) wrote it, and a plain load could hit a stale L2 line
+  auto getw = [&](int i) -> float {
+    return __hip_atomic_load(&W[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
   float c;
   if (p.xg.world > 1) {
-    xg_push_publish_wait(p.xg, n + 1, get);
-    c = xg_sum(p.xg, n);
-    for (int i = threadIdx.x; i < n; i += blockDim.x) W[i] = xg_update(W[i], xg_sum(p.xg, i), c, p.tu);
+    // persistent mode: one exchange epoch per step (xg_epoch = p.xg.epoch + step index)
+    xg_push_publish_wait(p.xg, xg_epoch, n + 1, get);
+    c = xg_sum(p.xg, xg_epoch, n);
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+      wt_store(&W[i], xg_update(getw(i), xg_sum(p.xg, xg_epoch, i), c, p.tu));
   } else {
     c = get(n);
-    for (int i = threadIdx.x; i < n; i += blockDim.x) W[i] = xg_update(W[i], get(i), c, p.tu);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) wt_store(&W[i], xg_update(getw(i), get(i), c, p.tu));
   }
-  for (int i = threadIdx.x; i < n; i += blockDim.x) G[i] = 0.f;
+  // write-through (agent-scope) stores: in the persistent mode other XCDs' blocks read
+  // W and add into G / C right after the epoch release, without a kernel boundary
+  for (int i = threadIdx.x; i < n; i += blockDim.x) wt_store(&G[i], 0.f);
   __syncthreads();                     // every thread has read the count
   if (threadIdx.x == 0) {
-    p.C[0] = 0.f;
-    if (p.tail_count_acc) p.tail_count_acc[0] += (double)c;
-    *p.ticket = 0u;
+    wt_store(&p.C[0], 0.f);
+    if (p.tail_count_acc)
+      __hip_atomic_fetch_add(p.tail_count_acc, (double)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -187,9 +212,9 @@ constexpr int kRing = 512;   // per-wave ring of selected local row indices
 
 // EVAL=false: gradient; EVAL=true: accuracy + log-loss over every row.
 // PIPE: software-pipelined (two register sets) vs. single-buffered sweep.
-template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U>
+template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, bool PERSIST>
 __global__ void __launch_bounds__(NW * 64)
-lr_rows_kernel(LrParams p) {
+lr_rows_kernel(const LrParams p) {
   constexpr int VEC = VecTraits<T>::VEC;
   constexpr int COLS = NC * 64 * VEC;  // columns covered per lane-set
   constexpr int RED_FLOATS = NW * (COLS + 4);
@@ -199,6 +224,7 @@ lr_rows_kernel(LrParams p) {
   __shared__ __attribute__((aligned(16))) float s_arena[(RED_FLOATS > RING_INTS) ? RED_FLOATS : RING_INTS];
   __shared__ int s_flag;
   __shared__ int s_next;   // next unclaimed 64-row quarter of this block (dynamic balancing)
+  __shared__ int s_ok;     // persistent mode: the epoch wait succeeded
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -211,12 +237,45 @@ lr_rows_kernel(LrParams p) {
   const int64_t seg_lo = p.seg[seg], seg_hi = p.seg[seg + 1];
   const int64_t lo = seg_lo + (int64_t)bx * p.rows_per_block;
   const int64_t hi = max(lo, min(seg_hi, lo + (int64_t)p.rows_per_block));
+  // ---- step loop (one iteration unless persistent: p.nsteps > 1)
+  // (a separate instantiation: the step loop costs registers the one-step kernel keeps)
+  const int nst = PERSIST && p.nsteps > 1 ? p.nsteps : 1;
+  // persistent mode: wait until the tail block of the previous step released W
+  auto wait_epoch = [&](int it) -> bool {
+    if (threadIdx.x == 0) {
+      const uint32_t want = p.epoch_base + (uint32_t)it;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      int ok = 1;
+      while ((int32_t)(__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+        if (__hip_atomic_load(p.perr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+            __builtin_amdgcn_s_memrealtime() - t0 > p.spin_ticks) {
+          __hip_atomic_store(p.perr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok != 0;
+  };
+  for (int it = 0; it < nst; ++it) {
+  // the kernel argument block is never written (a modified copy would live in scratch)
+  const uint64_t step_cur = p.step + (uint64_t)it;
   // model fragment in registers (optionally applying the previous step's update).
   // Fetched AFTER the first row batch is issued (see the sweep): the W / Wprev reads
   // then overlap the first rows' HBM latency instead of preceding them, and the
   // work-claim barrier below does not wait for them.
   float wr[NC][VEC];
   float wb = 0.f;
+  // persistent mode: W was written by another CU in this launch -> agent-scope loads
+  auto ldw_ = [&](const float* a) -> float {
+    if constexpr (PERSIST)
+      return __hip_atomic_load(const_cast<float*>(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      return *a;
+  };
   auto load_w = [&]() {
     if (p.Wprev == nullptr) {
       const float* w = p.W + (int64_t)seg * p.ldw;
@@ -225,9 +284,9 @@ lr_rows_kernel(LrParams p) {
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
           int col = (c * 64 + lane) * VEC + e;
-          wr[c][e] = (col < p.D) ? w[col] : 0.f;
+          wr[c][e] = (col < p.D) ? ldw_(w + col) : 0.f;
         }
-      wb = p.has_bias ? w[p.D] : 0.f;
+      wb = p.has_bias ? ldw_(w + p.D) : 0.f;
     } else {
       const float cprev = p.Cprev[0];
       float* wout = const_cast<float*>(p.W);
@@ -343,7 +402,7 @@ lr_rows_kernel(LrParams p) {
     while ((tail - head) < (uint32_t)(2 * U) && more) {
       const int64_t r0 = gnext + 4 * lane;
       u32x4 h{0u, 0u, 0u, 0u};
-      if (!p.full && !EVAL && r0 < uhi) h = philox_block(p.seed, p.step, (uint64_t)r0 >> 2);
+      if (!p.full && !EVAL && r0 < uhi) h = philox_block(p.seed, step_cur, (uint64_t)r0 >> 2);
       const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -498,6 +557,7 @@ lr_rows_kernel(LrParams p) {
     Batch<NC, U> B;
     refill();
     take_and_load(A);
+    if (PERSIST && it > 0 && !wait_epoch(it)) return;
     load_w();
     if (tr) t_first = __builtin_amdgcn_s_memrealtime();
     while (true) {
@@ -511,6 +571,7 @@ lr_rows_kernel(LrParams p) {
       compute(B);
     }
   } else {
+    if (PERSIST && it > 0 && !wait_epoch(it)) return;
     load_w();
     while (true) {
       refill();
@@ -529,7 +590,7 @@ lr_rows_kernel(LrParams p) {
   __syncthreads();   // rings are dead: the arena becomes the reduction buffer
   if (p.probe_no_epilogue) {
     if (threadIdx.x == 0 && cntf < 0.f) p.C[0] = cntf + gb;   // keep the sweep live
-    return;
+    continue;
   }
 
   if constexpr (EVAL) {
@@ -542,7 +603,7 @@ lr_rows_kernel(LrParams p) {
       atomicAdd(&p.correct[seg], c);
       atomicAdd(&p.loss[seg], l);
     }
-    return;
+    continue;
   } else {
     // ---- block reduction across waves (fixed order)
     auto red_row = [&](int k) { return s_arena + k * (COLS + 4); };
@@ -575,7 +636,7 @@ lr_rows_kernel(LrParams p) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) tr[3] = __builtin_amdgcn_s_memrealtime();
       }
-      if (p.ticket == nullptr) return;
+      if (p.ticket == nullptr) continue;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this block's adds are performed
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -583,8 +644,17 @@ lr_rows_kernel(LrParams p) {
         s_flag = (t == gridDim.x * gridDim.y - 1u);
       }
       __syncthreads();
-      if (s_flag) lr_tail(p);
-      return;
+      if (s_flag) {
+        lr_tail(p, p.xg.epoch + (uint32_t)it);
+        if (PERSIST && nst > 1) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // W / G / C / ticket written through
+          __syncthreads();
+          if (threadIdx.x == 0)
+            __hip_atomic_store(p.epoch, p.epoch_base + (uint32_t)it + 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      continue;
     }
     float* my = p.slab + ((int64_t)seg * gx + bx) * S;
     for (int col = threadIdx.x; col < D; col += NW * 64) {
@@ -611,7 +681,7 @@ lr_rows_kernel(LrParams p) {
       s_flag = (t == (unsigned)(gsize - 1));
     }
     __syncthreads();
-    if (!s_flag) return;
+    if (!s_flag) continue;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: keep loads below
     const int nv = D + 2;
     {
@@ -630,7 +700,7 @@ lr_rows_kernel(LrParams p) {
       s_flag = (t == (unsigned)(ngroups - 1));
     }
     __syncthreads();
-    if (!s_flag) return;
+    if (!s_flag) continue;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // ---- level 2: sum group slabs in order -> G[seg], C[seg]
     {
@@ -648,6 +718,7 @@ lr_rows_kernel(LrParams p) {
     }
     if (threadIdx.x == 0) p.cnt2[seg] = 0u;
   }
+  }  // step loop
 }
 
 }  // namespace dalgo
@@ -657,7 +728,17 @@ using namespace dalgo;
 template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U>
 static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st) {
   dim3 grid(gx, nseg), block(NW * 64);
-  hipLaunchKernelGGL((lr_rows_kernel<T, NC, EVAL, NW, PIPE, U>), grid, block, 0, st, p);
+  if (p.nsteps > 1) {
+    if constexpr (!EVAL) {
+      // persistent mode: every block must be resident (blocks wait on each other);
+      // the cooperative launch refuses a grid that cannot be
+      void* args[] = {const_cast<LrParams*>(&p)};
+      return hipLaunchCooperativeKernel((const void*)lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, true>,
+                                        grid, block, args, 0, st);
+    }
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL((lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, false>), grid, block, 0, st, p);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -746,6 +827,15 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
     p.xg.timeout_ticks = (long long)(tail->timeout_s * 1e8);
     p.tu = XgUpdate{tail->mode, tail->reg, tail->eta, tail->lam, tail->reg_alpha};
     p.tail_count_acc = tail->count_acc;
+    if (tail->nsteps > 1) {
+      if (tail->epoch_ctr == nullptr || tail->perr == nullptr || pool != nullptr)
+        return hipErrorInvalidValue;
+      p.nsteps = tail->nsteps;
+      p.epoch = tail->epoch_ctr;
+      p.epoch_base = tail->epoch_base;
+      p.perr = tail->perr;
+      p.spin_ticks = (uint64_t)(tail->spin_s * 1e8);
+    }
   }
   p.Wprev = Wprev; p.Gprev = G; p.Cprev = C; p.upd_mode = upd_mode; p.upd_reg = upd_reg;
   p.upd_eta = upd_eta; p.upd_lam = upd_lam; p.upd_reg_alpha = upd_reg_alpha;

@@ -42,13 +42,13 @@ struct XgParams {
 
 __global__ void __launch_bounds__(1024) xgmi_allreduce_kernel(XgParams p) {
   const int tid = threadIdx.x;
-  xg_push_publish_wait(p.L, p.n, [&](int i) { return p.in[i]; });
+  xg_push_publish_wait(p.L, p.L.epoch, p.n, [&](int i) { return p.in[i]; });
   if (p.W == nullptr) {
-    for (int i = tid; i < p.n; i += blockDim.x) p.out[i] = xg_sum(p.L, i);
+    for (int i = tid; i < p.n; i += blockDim.x) p.out[i] = xg_sum(p.L, p.L.epoch, i);
     return;
   }
-  const float c = xg_sum(p.L, p.cidx);             // the global minibatch size
-  for (int i = tid; i < p.nw; i += blockDim.x) p.W[i] = xg_update(p.W[i], xg_sum(p.L, i), c, p.u);
+  const float c = xg_sum(p.L, p.L.epoch, p.cidx);             // the global minibatch size
+  for (int i = tid; i < p.nw; i += blockDim.x) p.W[i] = xg_update(p.W[i], xg_sum(p.L, p.L.epoch, i), c, p.u);
   for (int i = tid; i < p.n; i += blockDim.x) p.out[i] = 0.f;
   if (tid == 0 && p.count_acc) p.count_acc[0] += (double)c;
 }

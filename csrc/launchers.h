@@ -16,6 +16,13 @@ struct DalgoLrTail {
   int mode, reg;                // 0 SSGD (mean + reg), 1 GD (sum)
   float eta, lam, reg_alpha;
   double* count_acc;            // += global minibatch size (optional)
+  // persistent multi-step launch (nsteps > 1): device epoch counter (holds epoch_base
+  // on entry, epoch_base + nsteps on exit), error word, per-wait time limit
+  int nsteps;
+  unsigned* epoch_ctr;
+  uint32_t epoch_base;
+  unsigned* perr;
+  double spin_s;
 };
 
 extern "C" {

@@ -178,6 +178,37 @@ class ParallelSGD:
                          and (comm.world_size() == 1 or self.bucket.xg is not None))
         return self._ok1
 
+    def _persistent(self) -> bool:
+        """Persistent multi-step launches (DALGO_PERSISTENT=1): SSGD / GD on GPU, atomic
+        epilogue, one rank or K11 peers. K steps run as ONE cooperative K1 grid whose tail
+        block releases each step's model (csrc/kernels/lr_grad.hip, nsteps)."""
+        if getattr(self, "_okp", None) is None:
+            self._okp = (self.device.type == "cuda" and self._zg and not self.fused
+                         and self.cfg.algo in ("ssgd", "gd")
+                         and os.environ.get("DALGO_PERSISTENT", "0") == "1"
+                         and (comm.world_size() == 1 or self.bucket.xg is not None))
+        return self._okp
+
+    def run_steps(self, k: int):
+        """k training steps (one persistent launch when enabled, else k step() calls)."""
+        k = int(k)
+        if k <= 0:
+            return
+        if not self._persistent():
+            for _ in range(k):
+                self.step()
+            return
+        c = self.cfg
+        lr_ops.lr_grad(self.data.X_train, self.data.y_train, self.w, self.seg, D=self.D,
+                       has_bias=True, eps=c.eps, seed=c.sample_seed, step=self.t, frac=c.frac,
+                       row_offset=self.data.row_offset, G=self.G, C=self.C,
+                       max_seg_rows=self.max_seg, g_is_zero=self._g_zero,
+                       tail=dict(mode=0 if c.algo == "ssgd" else 1, reg=self._upd["reg"],
+                                 eta=c.eta, lam=c.lam, reg_alpha=c.reg_alpha,
+                                 count_acc=self.count_acc, xg=self.bucket.xg, nsteps=k))
+        self._g_zero = True
+        self.t += k
+
     def _flush(self):
         """Apply a pending fused update to self.w (end of training / before reads)."""
         if self._pending:
@@ -283,6 +314,24 @@ class ParallelSGD:
     def fit(self, n_iterations: int | None = None, verbose: bool = False, callback=None):
         n = self.cfg.n_iterations if n_iterations is None else n_iterations
         acc = float("nan")
+        if self._persistent() and not verbose:
+            # persistent launches between evaluation points (the callback runs once per
+            # launch, at the evaluation step)
+            done = 0
+            while done < n:
+                ev = self.cfg.eval_every
+                k = n - done if not ev else min(n - done, ev - self.t % ev)
+                self.run_steps(k)
+                done += k
+                if ev and self.t % ev == 0:
+                    acc, loss = self.evaluate()
+                    self.history.accs.append(acc)
+                    self.history.losses.append(loss)
+                    self.history.iters.append(self.t)
+                if callback is not None:
+                    callback(self)
+            lr_ops.check_persistent()
+            return self.history
         for _ in range(n):
             if verbose:
                 self.rt.log("On iteration %d" % (self.t + 1))

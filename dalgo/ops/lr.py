@@ -82,7 +82,10 @@ class _Workspace:
     cnt2: torch.Tensor
     ticket: torch.Tensor   # fused-tail arrival counter (re-armed by the kernel)
     pool: torch.Tensor     # cross-block pool claim heads, 2 parity sets x n_seg x 8 shards
+    epoch: torch.Tensor    # persistent launches: device step-release counter ...
+    perr: torch.Tensor     # ... and its wait-timeout error word
     launches: int = 0      # parity of the next launch = launches & 1
+    epochs: int = 0        # host mirror of `epoch` (advanced by nsteps per launch)
 
 
 _ws_cache: dict = {}
@@ -100,9 +103,19 @@ def _workspace(device, nseg, gx, S) -> _Workspace:
             cnt2=torch.zeros(nseg, dtype=torch.int32, device=device),
             ticket=torch.zeros(1, dtype=torch.int32, device=device),
             pool=torch.zeros(2 * nseg * 8, dtype=torch.int32, device=device),
+            epoch=torch.zeros(1, dtype=torch.int32, device=device),
+            perr=torch.zeros(1, dtype=torch.int32, device=device),
         )
         _ws_cache[key] = ws
     return ws
+
+
+def check_persistent():
+    """Raise if a persistent launch (tail nsteps > 1) ever timed out waiting for a step
+    release (the launch then ended early and the model is not trustworthy)."""
+    for ws in _ws_cache.values():
+        if ws.epochs and int(ws.perr.item()) != 0:
+            raise RuntimeError("persistent K1 launch: a step-release wait timed out")
 
 
 def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor, *,
@@ -174,10 +187,21 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
                 G.zero_()
                 C.zero_()
             xg = tail.get("xg")
+            nsteps = int(tail.get("nsteps", 1))
             kw = {}
             if xg is not None:
                 kw = dict(xg_bufs=xg.bufs, xg_rank=xg.rank, xg_slot=xg.slot,
-                          xg_epoch=xg.next_epoch(), xg_err=xg.err, xg_timeout=xg.timeout_s)
+                          xg_epoch=xg.next_epoch(nsteps), xg_err=xg.err, xg_timeout=xg.timeout_s)
+            if nsteps > 1:
+                # persistent launch: steps step .. step + nsteps - 1, one cooperative grid
+                if pool:
+                    raise ValueError("persistent launch: no cross-block work pool")
+                if ws.epochs + nsteps >= 1 << 31:
+                    ws.epoch.zero_()
+                    ws.epochs = 0
+                kw.update(nsteps=nsteps, epoch=ws.epoch, epoch_base=ws.epochs, perr=ws.perr,
+                          spin_s=float(tail.get("spin_s", 2.0)))
+                ws.epochs += nsteps
             _ext.ops().lr_grad(X, y, W, seg, int(row_offset), int(D), bool(has_bias), float(eps),
                                int(seed), int(step), float(frac), gx, rpb, ws.slab, ws.gslab,
                                ws.cnt1, ws.cnt2, G, C, var | 256, None, 0, 0, 0.0, 0.0, 0.0,

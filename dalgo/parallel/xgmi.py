@@ -92,12 +92,14 @@ class XgmiAllReduce:
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.epoch = 0
 
-    def next_epoch(self) -> int:
-        """Claim the next exchange epoch (for kernels that run the exchange themselves)."""
-        self.epoch += 1
+    def next_epoch(self, count: int = 1) -> int:
+        """Claim the next `count` exchange epochs (for kernels that run the exchange
+        themselves; a persistent multi-step launch uses first, first + 1, ...)."""
+        first = self.epoch + 1
+        self.epoch += int(count)
         if self.epoch >= 1 << 32:
             raise RuntimeError("xGMI all-reduce epoch space exhausted")
-        return self.epoch
+        return first
 
     def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
         """In-place SUM over ranks of a contiguous f32 GPU vector (numel <= slot)."""

@@ -167,3 +167,38 @@ def test_lr_grad_fused_tail_single_rank(cuda, mode, reg):
     assert bool((G == 0).all()) and bool((C == 0).all())
     rel = ((w - w_ref).abs().max() / w_ref.abs().max()).item()
     assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("mode,reg,n", [(0, 0, 300_000), (0, 3, 1_250_000), (1, 0, 40_000)])
+def test_lr_grad_persistent_steps(cuda, mode, reg, n):
+    """Persistent launch (K steps in one cooperative grid, epoch-released W) == K
+    separate gradient + update steps; the release counter ends at base + K."""
+    X, y = _data(n, 1024, torch.bfloat16, seed=12)
+    Xd, yd = X.to(cuda), y.to(cuda)
+    seg = torch.tensor([0, n], dtype=torch.int64, device=cuda)
+    w0 = torch.randn(1, 1025, generator=torch.Generator().manual_seed(5)).to(cuda) * 0.05
+    kw = dict(D=1024, frac=0.1, eps=0.0, seed=42)
+    # GD applies the gradient SUM: a small step keeps 14 steps from amplifying the
+    # (order-dependent) f32 rounding of the atomic block sums
+    upd = dict(eta=0.1 if mode == 0 else 1e-3, lam=0.01, reg_alpha=0.3)
+    K = 7
+    w_ref = w0.clone()
+    acc_ref = torch.zeros(1, dtype=torch.float64, device=cuda)
+    for t in range(2 * K):
+        G, C = L.lr_grad(Xd, yd, w_ref, seg, step=t, **kw)
+        U.sync_update(w_ref, U.SSGD if mode == 0 else U.GD_SUM, G=G, C=C, reg=reg,
+                      count_acc=acc_ref, **upd)
+    w = w0.clone()
+    G = torch.zeros(1, 1025, device=cuda)
+    C = torch.zeros(1, device=cuda)
+    acc = torch.zeros(1, dtype=torch.float64, device=cuda)
+    for r in range(2):   # two launches: the epoch base carries over
+        L.lr_grad(Xd, yd, w, seg, step=r * K, G=G, C=C, g_is_zero=True,
+                  tail=dict(mode=mode, reg=reg, count_acc=acc, xg=None, nsteps=K, **upd), **kw)
+    torch.cuda.synchronize()
+    L.check_persistent()
+    assert float(acc.item()) == float(acc_ref.item())
+    assert bool((G == 0).all()) and bool((C == 0).all())
+    rel = ((w - w_ref).abs().max() / w_ref.abs().max()).item()
+    assert rel < 1e-4, rel
+

@@ -68,22 +68,25 @@ def _final_w(out):
     return np.array([float(v) for v in txt.replace("[", " ").replace("]", " ").split()])
 
 
-@pytest.mark.parametrize("one_kernel", ["1", "0"])
+@pytest.mark.parametrize("one_kernel", ["1", "0", "persistent"])
 @pytest.mark.parametrize("algo", ["ssgd", "logistic_regression"])
 def test_fused_xgmi_update_matches_process_group(cuda, algo, one_kernel):
-    """SSGD / full-batch GD: one-launch step (K1 tail: xGMI exchange + update) or K1 + K11
-    with the fused K8 == gloo all-reduce + separate K8."""
+    """SSGD / full-batch GD: one-launch step (K1 tail: xGMI exchange + update), a
+    persistent multi-step launch (every step's tail exchanges over K11), or K1 + K11 with
+    the fused K8 == gloo all-reduce + separate K8."""
     import numpy as np
     script = "optimization/ssgd.py" if algo == "ssgd" else "machine_learning/logistic_regression.py"
     args = [script, "--device", "cuda", "--backend", "gloo", "--no-plot", "--quiet",
-            "--synthetic", "40000,64", "--n-iterations", "30", "--dtype", "f32"]
+            "--synthetic", "40000,64", "--n-iterations", "30", "--dtype", "f32",
+            "--eval-every", "10"]   # persistent mode: 10-step launches between evaluations
     os.environ["DALGO_XGMI"] = "1"
-    os.environ["DALGO_ONE_KERNEL"] = one_kernel
+    env_key = "DALGO_PERSISTENT" if one_kernel == "persistent" else "DALGO_ONE_KERNEL"
+    os.environ[env_key] = "1" if one_kernel == "persistent" else one_kernel
     try:
         fused = _torchrun(args)
     finally:
         del os.environ["DALGO_XGMI"]
-        del os.environ["DALGO_ONE_KERNEL"]
+        del os.environ[env_key]
     os.environ["DALGO_XGMI"] = "0"
     try:
         plain = _torchrun(args)
