@@ -90,7 +90,8 @@ def main(argv=None):
         xg.check()   # raise (non-zero exit) if a peer wait ever timed out
     from dalgo.ops import lr as lr_ops
     lr_ops.check_persistent()   # ... or a persistent launch's step-release wait
-    launch = "persistent" if model._persistent() else "per-step"
+    launch = "persistent" if model._persistent() else (
+        "hipgraph-replay" if model._graph_ok() else "per-step")
     allreduce = "xgmi-oneshot (K11)" if xg is not None else (
         f"{rt.backend}" if W > 1 else "none (1 rank)")
 

@@ -84,8 +84,17 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
              double tail_lam, double tail_reg_alpha, const std::optional<Tensor>& tail_count_acc,
              const std::optional<Tensor>& pool, int64_t pool_parity, int64_t nsteps,
              const std::optional<Tensor>& epoch, int64_t epoch_base,
-             const std::optional<Tensor>& perr, double spin_s) {
+             const std::optional<Tensor>& perr, double spin_s,
+             const std::optional<Tensor>& step_dev, int64_t step_mul) {
   check_lr_inputs(X, y, W, seg, D, has_bias);
+  const int64_t* stepp = nullptr;
+  if (step_dev.has_value()) {
+    check_dev(*step_dev, "step_dev");
+    TORCH_CHECK(step_dev->scalar_type() == at::kLong && step_dev->numel() >= 1,
+                "step_dev: int64[1] device step counter");
+    TORCH_CHECK(step_mul >= 0, "step_mul >= 0");
+    stepp = step_dev->data_ptr<int64_t>();
+  }
   unsigned* poolp = nullptr;
   if (pool.has_value()) {
     check_dev(*pool, "pool");
@@ -182,7 +191,7 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
                     reinterpret_cast<unsigned*>(cnt2.data_ptr<int>()), G.data_ptr<float>(),
                     C.data_ptr<float>(), (int)S, (int)variant, wprev, (int)upd_mode, (int)upd_reg,
                     (float)upd_eta, (float)upd_lam, (float)upd_reg_alpha, cacc, tailp, poolp,
-                    (int)(pool_parity & 1), cur_stream()),
+                    (int)(pool_parity & 1), stepp, step_mul, cur_stream()),
       "lr_grad");
 }
 
@@ -694,7 +703,8 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(i!)? xg_err=None, float xg_timeout=0., int tail_mode=0, int tail_reg=0, "
         "float tail_eta=0., float tail_lam=0., float tail_reg_alpha=0., "
         "Tensor(j!)? tail_count_acc=None, Tensor(k!)? pool=None, int pool_parity=0, int nsteps=1, "
-        "Tensor(l!)? epoch=None, int epoch_base=0, Tensor(m!)? perr=None, float spin_s=2.) -> ()");
+        "Tensor(l!)? epoch=None, int epoch_base=0, Tensor(m!)? perr=None, float spin_s=2., "
+        "Tensor? step_dev=None, int step_mul=1) -> ()");
   m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
         "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=3) -> ()");
   m.def("sync_update(Tensor(a!) W, Tensor(d!)? G, Tensor(e!)? C, Tensor? center, Tensor? S, "

@@ -38,6 +38,10 @@ struct LrParams {
   int has_bias;
   float eps;            // 0 (ssgd.py:24) or 1e-6 (ma.py:26)
   uint64_t seed, step;  // sampling stream
+  // graph replay (hipGraph): the stream index is step + step_mul * (*step_dev), read
+  // from device memory so one captured graph serves every training step
+  const int64_t* step_dev;
+  int64_t step_mul;
   uint32_t thr;         // Bernoulli threshold: select iff u32 < thr
   int full;             // 1: every row selected (full-batch GD)
   int rows_per_block;   // multiple of 256
@@ -260,9 +264,11 @@ lr_rows_kernel(const LrParams p) {
     __syncthreads();
     return s_ok != 0;
   };
+  const uint64_t step_base =
+      p.step + (p.step_dev != nullptr ? (uint64_t)(p.step_mul * p.step_dev[0]) : 0ull);
   for (int it = 0; it < nst; ++it) {
   // the kernel argument block is never written (a modified copy would live in scratch)
-  const uint64_t step_cur = p.step + (uint64_t)it;
+  const uint64_t step_cur = step_base + (uint64_t)it;
   // model fragment in registers (optionally applying the previous step's update).
   // Fetched AFTER the first row batch is issued (see the sweep): the W / Wprev reads
   // then overlap the first rows' HBM latency instead of preceding them, and the
@@ -810,8 +816,11 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int variant,
                          const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
                          float upd_reg_alpha, double* count_acc, const DalgoLrTail* tail,
-                         unsigned* pool, int pool_parity, hipStream_t st) {
+                         unsigned* pool, int pool_parity, const int64_t* step_dev,
+                         int64_t step_mul, hipStream_t st) {
   LrParams p{};
+  p.step_dev = step_dev;
+  p.step_mul = step_mul;
   if (tail != nullptr) {
     if (nseg != 1 || !((variant >> 8) & 1) || Wprev != nullptr || tail->ticket == nullptr ||
         tail->world < 1 || tail->world > kXgMaxRanks || tail->rank < 0 || tail->rank >= tail->world ||

@@ -37,7 +37,8 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int variant,
                          const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
                          float upd_reg_alpha, double* count_acc, const DalgoLrTail* tail,
-                         unsigned* pool, int pool_parity, hipStream_t st);
+                         unsigned* pool, int pool_parity, const int64_t* step_dev,
+                         int64_t step_mul, hipStream_t st);
 hipError_t dalgo_lr_eval(const void* X, const float* y, const float* W, const int64_t* seg,
                          int64_t ld, int D, int ldw, int has_bias, float eps, int is_bf16, int gx,
                          int nseg, int rows_per_block, unsigned long long* correct, float* loss,

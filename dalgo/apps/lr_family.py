@@ -48,6 +48,8 @@ def build_parser(algo: str):
     ap.add_argument("--dtype", choices=["bf16", "f32", "f64"], default=None,
                     help="feature storage dtype (default f32 on GPU, f64 on CPU)")
     ap.add_argument("--eval-every", type=int, default=1)
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="hipGraph replay of whole steps (auto: MA/BMUF/EASGD on one rank)")
     ap.add_argument("--ckpt-dir", default=None)
     ap.add_argument("--ckpt-every", type=int, default=0)
     ap.add_argument("--resume", action="store_true")
@@ -80,6 +82,8 @@ def main(algo: str, argv=None):
                     n_local=a.n_local_iterations, mu=a.mu, zeta=a.zeta, rho=a.rho,
                     sample_seed=a.sample_seed, init_seed=a.seed, eval_every=a.eval_every)
     model = ParallelSGD(cfg, data, layout, rt, model_dtype=model_dtype)
+    if a.graph != "auto":
+        model.graph = a.graph == "on"
     sink = obs.MetricsSink(a.metrics_out, rt.rank)
     ck_name = f"{algo}_state"
     if a.resume and a.ckpt_dir:

@@ -99,6 +99,11 @@ def init_models(cfg: SGDConfig, ldw: int, dtype=torch.float64):
     return out
 
 
+# DALGO_GRAPH=auto replays steps as a hipGraph only while the local shard is at most
+# this large (launch-bound regime; see ParallelSGD._graph_ok)
+_GRAPH_AUTO_MAX_BYTES = int(os.environ.get("DALGO_GRAPH_AUTO_MAX_MB", "256")) << 20
+
+
 class ParallelSGD:
     def __init__(self, cfg: SGDConfig, data: LRData, layout: ShardLayout, rt: Runtime,
                  model_dtype: torch.dtype = torch.float32):
@@ -154,16 +159,23 @@ class ParallelSGD:
         self._zg = not lr_ops.DETERMINISTIC   # deterministic K1 overwrites G: no need to clear
         if self.fused:
             self.w_next = torch.empty_like(self.w)
+        # hipGraph replay state (see _graph_ok): None = follow DALGO_GRAPH
+        self.graph: bool | None = None
+        self._graphs: dict = {}
+        self._graph_warm = False
+        self._t_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._t_dev_val = 0
         self._upd = dict(mode=0 if algo == "ssgd" else 1, reg=U.REG.get(cfg.reg, 0), eta=cfg.eta,
                          lam=cfg.lam, reg_alpha=cfg.reg_alpha)
 
     # ------------------------------------------------------------------ steps
-    def _grad(self, W, stream):
+    def _grad(self, W, stream, step_dev=None, step_mul=1):
         c = self.cfg
         lr_ops.lr_grad(self.data.X_train, self.data.y_train, W, self.seg, D=self.D, has_bias=True,
                        eps=c.eps, seed=c.sample_seed, step=stream, frac=c.frac,
                        row_offset=self.data.row_offset, G=self.G, C=self.C,
-                       max_seg_rows=self.max_seg, g_is_zero=self._g_zero)
+                       max_seg_rows=self.max_seg, g_is_zero=self._g_zero,
+                       step_dev=step_dev, step_mul=step_mul)
         self._g_zero = False
 
     def _one_kernel(self) -> bool:
@@ -229,9 +241,74 @@ class ParallelSGD:
             comm.all_reduce_sum(cnt)   # the fused kernel accumulates LOCAL counts
         return float(cnt.item())
 
+    # ------------------------------------------------------- hipGraph replay
+    def _graph_ok(self) -> bool:
+        """Replay whole training steps from one captured hipGraph (DALGO_GRAPH=1 or auto,
+        or ``model.graph = True``). Every kernel of a step (K1 gradient, K8 updates, row
+        sums, the model all-reduce) is recorded once; the sampling stream comes from a
+        device step counter (K1 ``step_dev``) that the graph itself advances, so a replay
+        is one host call per step instead of 2 (SSGD) to 14 (MA/BMUF, 5 local steps)
+        launches. Needs GPU tensors, no persistent / fused-update / one-kernel mode, and
+        no host-sequenced K11 epochs: one rank, or RCCL with DALGO_XGMI=0 (RCCL
+        collectives are graph-capturable)."""
+        if getattr(self, "_okg", None) is None:
+            ws = comm.world_size()
+            env = os.environ.get("DALGO_GRAPH", "auto")
+            # auto: the multi-launch MA / BMUF / EASGD steps on one rank while they are
+            # launch bound (measured 1.05-1.8x faster replayed up to 100k x 256 bf16,
+            # bench/graph_replay.py; 5-7% SLOWER at 10M x 1024, where back-to-back eager
+            # launches overlap better than graph nodes); SSGD / GD (two launches) stay
+            # eager (0.75-0.9x replayed)
+            X = self.data.X_train
+            small = X.numel() * X.element_size() <= _GRAPH_AUTO_MAX_BYTES
+            auto = self.cfg.algo in ("ma", "bmuf", "easgd") and ws == 1 and small
+            want = self.graph if self.graph is not None else (
+                env == "1" or (env == "auto" and auto))
+            ok_comm = ws == 1 or (torch.distributed.get_backend() == "nccl"
+                                  and os.environ.get("DALGO_XGMI", "auto") == "0")
+            self._okg = bool(want and self.device.type == "cuda" and not self.fused
+                             and not self._persistent() and not self._one_kernel() and ok_comm
+                             and getattr(getattr(self, "bucket", None), "xg", None) is None)
+        return self._okg
+
+    def _graph_step(self):
+        # count_acc's address is baked into the captured kernels: one graph per target
+        key = None if self.count_acc is None else self.count_acc.data_ptr()
+        g = self._graphs.get(key)
+        if g is None:
+            if not self._graph_warm:
+                # one eager step allocates the kernel workspaces and reaches the
+                # steady state (G / C zero between steps) the capture assumes
+                self._step_impl(self.t)
+                self.t += 1
+                torch.cuda.synchronize(self.device)
+                self._graph_warm = True
+                return
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._step_impl(0, self._t_dev)
+                self._t_dev.add_(1)
+            self._graphs[key] = g
+        if self._t_dev_val != self.t:
+            self._t_dev.fill_(self.t)
+        g.replay()
+        self.t += 1
+        self._t_dev_val = self.t
+
     def step(self):
+        if self._graph_ok():
+            self._graph_step()
+            return
+        self._step_impl(self.t)
+        self.t += 1
+
+    def _step_impl(self, t: int, step_dev: torch.Tensor | None = None):
+        """One training step at sampling step t (or at the device counter step_dev);
+        does not advance self.t."""
         c = self.cfg
-        t = self.t
+        sd = dict(step_dev=step_dev) if step_dev is not None else {}
+        if step_dev is not None:
+            t = 0
         if self.fused:
             if self._pending:
                 lr_ops.lr_grad(self.data.X_train, self.data.y_train, self.w_next, self.seg, D=self.D,
@@ -258,7 +335,7 @@ class ParallelSGD:
                                      count_acc=self.count_acc, xg=self.bucket.xg))
             self._g_zero = True
         elif c.algo in ("ssgd", "gd"):
-            self._grad(self.w, t)
+            self._grad(self.w, t, **sd)
             xg = self.bucket.xg
             if xg is not None and self._zg:
                 # K11 all-reduce + K8 update in one launch; leaves the bucket zeroed
@@ -267,7 +344,6 @@ class ParallelSGD:
                                       reg_alpha=c.reg_alpha, count_index=self.ldw,
                                       count_acc=self.count_acc)
                 self._g_zero = True
-                self.t += 1
                 return
             self.bucket.all_reduce()
             if c.algo == "ssgd":
@@ -282,7 +358,12 @@ class ParallelSGD:
             U.rows_broadcast(self.W, self.w)
             for l in range(c.n_local):
                 stream = t if c.reuse_minibatch else t * c.n_local + l
-                self._grad(self.W, stream)
+                if step_dev is not None:
+                    # stream = (0 | l) + (1 | n_local) * step_dev
+                    self._grad(self.W, 0 if c.reuse_minibatch else l, step_dev,
+                               1 if c.reuse_minibatch else c.n_local)
+                else:
+                    self._grad(self.W, stream)
                 U.sync_update(self.W, U.LOCAL_MEAN, G=self.G, C=self.C, eta=c.eta, zero_grad=self._zg)
                 self._g_zero = True
             U.rows_sum(self.W, self.S)
@@ -293,14 +374,13 @@ class ParallelSGD:
                 U.sync_update(self.w, U.BMUF, S=self.S, Dl=self.Dl, mu=c.mu, zeta=c.zeta,
                               inv_p=self.inv_p)
         else:  # easgd
-            self._grad(self.W, t)
+            self._grad(self.W, t, **sd)
             U.sync_update(self.W, U.LOCAL_ELASTIC, G=self.G, C=self.C, center=self.w, eta=c.eta,
                           alpha=c.alpha, zero_grad=self._zg)
             self._g_zero = True
             U.rows_sum(self.W, self.S)
             comm.all_reduce_sum(self.S)
             U.sync_update(self.w, U.ELASTIC_CENTER, S=self.S, beta=c.beta, inv_p=self.inv_p)
-        self.t += 1
 
     def evaluate(self):
         self._flush()

@@ -126,7 +126,8 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
             w_prev: torch.Tensor | None = None, update: dict | None = None,
             count_acc: torch.Tensor | None = None, g_is_zero: bool = False,
             deterministic: bool | None = None, tail: dict | None = None,
-            pool_frac: float | None = None):
+            pool_frac: float | None = None, step_dev: torch.Tensor | None = None,
+            step_mul: int = 1):
     """Per-segment gradient SUM and selected-row COUNT.
 
     X: [n, >=D] (bf16/f32), y: [n] f32, W: [n_seg, ldw] f32 models,
@@ -151,6 +152,10 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
     on one rank), apply the update to ``W`` and leave G / C zeroed — a whole
     synchronous training step in one launch. ``count_acc`` then accumulates the
     GLOBAL minibatch size.
+
+    Graph replay: with ``step_dev`` (int64 [1] on the device) the sampling stream is
+    ``step + step_mul * step_dev[0]``, read by the kernel at run time, so a step captured
+    once in a hipGraph keeps drawing fresh minibatches on every replay.
     """
     nseg, ldw = W.shape
     if G is None:
@@ -173,6 +178,11 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
         S = ((D + 2 + 63) // 64) * 64
         ws = _workspace(X.device, nseg, gx, S)
         pool = {}
+        if step_dev is not None:
+            pf = 0.0     # graph replay: no host-side launch parity
+            gx, rpb = _grid(max(int(max_seg_rows), 1), nseg, target_blocks, 0.0)
+            ws = _workspace(X.device, nseg, gx, S)
+            pool = dict(step_dev=step_dev, step_mul=int(step_mul))
         if pf > 0:
             pool = dict(pool=ws.pool, pool_parity=ws.launches & 1)
             ws.launches += 1
@@ -229,6 +239,8 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
         U.sync_update(W, U.SSGD if update.get("mode", 0) == 0 else U.GD_SUM, G=G, C=C,
                       reg=update.get("reg", 0), eta=update.get("eta", 0.0),
                       lam=update.get("lam", 0.0), reg_alpha=update.get("reg_alpha", 0.0))
+    if step_dev is not None:
+        step = int(step) + int(step_mul) * int(step_dev.view(-1)[0])
     G, C = _lr_grad_cpu(X, y, W, seg, D, has_bias, eps, seed, step, frac, row_offset, G, C)
     if count_acc is not None:
         count_acc += float(C.sum())

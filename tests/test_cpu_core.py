@@ -68,3 +68,18 @@ def test_breast_cancer_split():
     d = breast_cancer()
     assert d.X_train.shape == (398, 30) and d.X_test.shape == (171, 30)
     assert d.X_train.stride(0) % 2 == 0   # 16-B padded rows
+
+
+def test_lr_grad_device_step_counter_cpu():
+    """K1's graph-replay stream (step + step_mul * step_dev) selects the same rows as
+    the plain step argument (CPU reference path)."""
+    from dalgo.ops import lr as L
+    g = torch.Generator().manual_seed(3)
+    X = torch.rand((3000, 17), generator=g, dtype=torch.float64)
+    y = (torch.rand(3000, generator=g) < 0.5).double()
+    W = torch.randn(1, 18, generator=g, dtype=torch.float64)
+    seg = torch.tensor([0, 3000])
+    kw = dict(D=17, seed=42, frac=0.1)
+    G1, C1 = L.lr_grad(X, y, W, seg, step=2 + 5 * 7, **kw)
+    G2, C2 = L.lr_grad(X, y, W, seg, step=2, step_dev=torch.tensor([7]), step_mul=5, **kw)
+    assert torch.equal(C1, C2) and torch.equal(G1, G2)

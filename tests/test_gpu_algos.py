@@ -311,3 +311,42 @@ def test_lr_family_gpu_tracks_cpu(cuda, algo):
     mg.fit()
     a, b = mg.weights().cpu().double(), mc.weights()
     assert (a - b).norm() / b.norm() < 1e-4
+
+
+@pytest.mark.parametrize("algo", ["ssgd", "gd", "ma", "bmuf", "easgd"])
+@pytest.mark.parametrize("reuse", [True, False])
+def test_lr_family_graph_replay_matches_eager(cuda, algo, reuse):
+    """hipGraph replay (one captured step, device step counter) == eager launches:
+    same minibatches (exact global sample count), same model up to f32 atomic order,
+    including a checkpoint-style jump of t between replays."""
+    if reuse is False and algo not in ("ma", "bmuf"):
+        pytest.skip("reuse_minibatch only affects MA / BMUF")
+    from dalgo.data.datasets import synthetic_logistic
+    from dalgo.models.localsgd import ParallelSGD, SGDConfig
+    from dalgo.parallel import runtime
+    from dalgo.parallel.sharding import make_layout
+    rt = runtime.init(device="cuda")
+    N, D = 60_000, 200
+    cfg = SGDConfig(algo=algo, n_workers=4, n_iterations=12, eta=0.5 if algo != "gd" else 1e-4,
+                    eval_every=0, reuse_minibatch=reuse)
+    lay = make_layout(N, 4, 1, 0, spark_compatible=False)
+    d = synthetic_logistic(N, D, dtype=torch.bfloat16, device=cuda)
+    runs = []
+    for graph in (False, True):
+        m = ParallelSGD(cfg, d, lay, rt)
+        m.graph = graph
+        m.count_acc = torch.zeros(1, dtype=torch.float64, device=cuda)
+        m.fit(6)
+        m.t += 3          # e.g. a resumed checkpoint: the device counter must follow
+        m.fit(6)
+        torch.cuda.synchronize()
+        assert m._graph_ok() == graph
+        if graph:
+            assert len(m._graphs) == 1
+        runs.append((m.weights().clone(), float(m.count_acc.item()), m.t))
+    (we, ce, te), (wg, cg, tg) = runs
+    assert te == tg == 15
+    if algo in ("ssgd", "gd"):
+        assert ce == cg
+    rel = ((wg - we).norm() / we.norm()).item()
+    assert rel < 1e-4, rel
