@@ -55,7 +55,7 @@ def test_scripts_two_ranks_gloo_on_one_gpu(cuda, script, extra, needle):
     assert needle in out
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_xgmi_allreduce_ranks_on_one_gpu(cuda, n):
     """K11: IPC exchange buffers + flag protocol, exact rank-ordered sums on every rank."""
     out = _torchrun(["tests/helpers/xgmi_check.py"], n=n)
@@ -102,3 +102,15 @@ def test_bench_auto_selects_allreduce(cuda):
                      "--steps", "5", "--warmup", "2"])
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
     assert d["config"]["allreduce"] in ("xgmi-oneshot (K11)", "gloo")
+
+
+def test_bench_eight_ranks_on_one_gpu(cuda):
+    """World size 8 (the driver's largest N), 8 ranks sharing cuda:0: sharding of the
+    10M-row global set into 1.25M-row shards, the 8-peer K11 exchange (or gloo if the
+    start-up race prefers it), rank-0 JSON with the whole-job aggregate."""
+    out = _torchrun(["bench.py", "--gpus", "8", "--backend", "gloo", "--rows", "400000",
+                     "--steps", "5", "--warmup", "2"], n=8)
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+    assert d["n_gpus"] == 8 and d["steps"] == 5 and d["config"]["parallelism"] == "dp8"
+    assert d["config"]["allreduce"] in ("xgmi-oneshot (K11)", "gloo")
+    assert d["value"] > 0 and d["ms_per_step"] > 0
