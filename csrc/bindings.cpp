@@ -168,7 +168,7 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
   }
   const int64_t nseg = W.size(0);
   TORCH_CHECK(gx >= 1 && gx <= 65535, "gx");
-  TORCH_CHECK(rows_per_block > 0 && rows_per_block % 256 == 0, "rows_per_block % 256");
+  TORCH_CHECK(rows_per_block > 0 && rows_per_block % 4 == 0, "rows_per_block % 4");
   const int64_t ngroups = (gx + 15) / 16;
   check_f32(slab, "slab"); check_f32(gslab, "gslab"); check_f32(G, "G"); check_f32(C, "C");
   const int64_t S = slab.size(1);
@@ -200,7 +200,7 @@ void lr_eval(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
              Tensor loss, int64_t variant) {
   check_lr_inputs(X, y, W, seg, D, has_bias);
   const int64_t nseg = W.size(0);
-  TORCH_CHECK(rows_per_block > 0 && rows_per_block % 256 == 0, "rows_per_block % 256");
+  TORCH_CHECK(rows_per_block > 0 && rows_per_block % 4 == 0, "rows_per_block % 4");
   TORCH_CHECK(correct.scalar_type() == at::kLong && correct.numel() >= nseg, "correct");
   check_f32(loss, "loss");
   TORCH_CHECK(loss.numel() >= nseg, "loss");

@@ -44,7 +44,7 @@ struct LrParams {
   int64_t step_mul;
   uint32_t thr;         // Bernoulli threshold: select iff u32 < thr
   int full;             // 1: every row selected (full-batch GD)
-  int rows_per_block;   // multiple of 256
+  int rows_per_block;   // multiple of 4 (the Philox row quad)
   // grad outputs
   float* slab;          // [n_seg * gx, S]
   float* gslab;         // [n_seg * ngroups, S]

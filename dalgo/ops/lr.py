@@ -36,6 +36,12 @@ LR_FINE_GROUPS = int(os.environ.get("DALGO_LR_FINE", "8"))
 #   POOL_FRAC       = share of each segment's rows left to the cross-block pool that
 #                     blocks claim from once their static range is done (0 = off)
 LR_POOL_FRAC = float(os.environ.get("DALGO_LR_POOL", "0"))
+#   RPB_ALIGN       = granularity (rows) of each block's static range. The kernel walks
+#                     any 4-aligned range: 1.25M rows with 256-row ranges is 245 blocks of
+#                     5120 rows (11 CUs idle), with 4-row ranges 256 x 4884. Measured equal
+#                     (1.25M: 59.3/60.2 vs 59.6/59.0 us; 10M: 361.3 vs 361.4/362.9 us,
+#                     profiles/final/README.md), so the profiled 256 stays the default
+LR_RPB_ALIGN = max(4, int(os.environ.get("DALGO_LR_RPB_ALIGN", "256")) // 4 * 4)
 #   DETERMINISTIC   = combine per-block partials with the fixed-order two-level
 #                     hand-off (bitwise repeatable) instead of float atomics
 DETERMINISTIC = os.environ.get("DALGO_DETERMINISTIC", "0") == "1"
@@ -63,12 +69,13 @@ def pad_features(X: torch.Tensor) -> torch.Tensor:
 
 
 def _grid(n_rows: int, nseg: int, target_blocks: int | None = None, pool_frac: float = 0.0):
-    """Blocks per segment and static rows per block (multiple of 256). With pool_frac > 0
+    """Blocks per segment and static rows per block (multiple of LR_RPB_ALIGN). With pool_frac > 0
     the static ranges cover about (1 - pool_frac) of the rows; the rest is the segment's
     cross-block pool, claimed dynamically (csrc/kernels/lr_grad.hip)."""
     per_seg = max(1, (target_blocks or _TARGET_BLOCKS) // max(1, nseg))
     static_rows = n_rows * (1.0 - min(max(pool_frac, 0.0), 0.9))
-    rpb = max(256, int(math.ceil(static_rows / per_seg / 256.0)) * 256)
+    al = LR_RPB_ALIGN
+    rpb = max(256, int(math.ceil(static_rows / per_seg / al)) * al)
     gx = max(1, min(per_seg, int(math.ceil(n_rows / rpb)))) if pool_frac > 0 else \
         max(1, int(math.ceil(n_rows / rpb)))
     return gx, rpb
