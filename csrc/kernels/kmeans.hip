@@ -23,6 +23,7 @@
 // kmeans_update — c = S/n for non-empty clusters, keep the stale centre
 //   otherwise (k-means.py:70-71); writes the f32 master, the padded MFMA copy,
 //   0.5|c~|^2 of the ROUNDED copy (consistent scores) and the squared shift.
+#include <cstdlib>
 #include "dalgo/common.h"
 #include <algorithm>
 
@@ -813,8 +814,19 @@ kmeans_scan_kernel(int* __restrict__ block_counts, int B, int k, int seg,
   extern __shared__ int64_t tot[];            // [2k]: counts, then segment counts
   __shared__ int64_t s_part[2][1024 / 64];
   for (int c = threadIdx.x; c < k; c += blockDim.x) {
+    // the column walk is load-latency bound: issue kBat loads before the stores
+    // that depend on them (one HBM round trip per kBat blocks, not per block)
+    constexpr int kBat = 32;
     int run = 0;
-    for (int b = 0; b < B; ++b) {
+    int b = 0;
+    for (; b + kBat <= B; b += kBat) {
+      int v[kBat];
+#pragma unroll
+      for (int j = 0; j < kBat; ++j) v[j] = __builtin_nontemporal_load(&block_counts[(int64_t)(b + j) * k + c]);
+#pragma unroll
+      for (int j = 0; j < kBat; ++j) { block_counts[(int64_t)(b + j) * k + c] = run; run += v[j]; }
+    }
+    for (; b < B; ++b) {
       const int v = block_counts[(int64_t)b * k + c];
       block_counts[(int64_t)b * k + c] = run;
       run += v;
@@ -863,6 +875,74 @@ kmeans_scatter_kernel(const int* __restrict__ assign, int64_t n, int64_t rpc, in
   for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
     const int pos = atomicAdd(&cursor[assign[r]], 1);
     perm[pos] = (int)r;
+  }
+}
+
+// Coalesced scatter (default for k <= kScKmax): the block's rows are handled in
+// chunks of kScCh; each chunk is counting-sorted by cluster in LDS first (local
+// ranks by LDS atomics, block scan of the local counts, one packed (cluster, row
+// offset) word per slot), then slot i is written to cursor[c] + (i - lstart[c]):
+// consecutive lanes store consecutive perm entries of one cluster run (~kScCh/k
+// rows per run) instead of 64 unrelated 4-byte locations per store instruction.
+constexpr int kScCh = 32768, kScKmax = 2048, kScNT = 1024, kScPer = kScCh / kScNT;
+__global__ void __launch_bounds__(kScNT)
+kmeans_scatter_chunked_kernel(const int* __restrict__ assign, int64_t n, int64_t rpc, int k,
+                              const int* __restrict__ block_offsets,
+                              const int64_t* __restrict__ cluster_start, int* __restrict__ perm) {
+  __shared__ int stage[kScCh];
+  __shared__ int cursor[kScKmax], lcnt[kScKmax], lstart[kScKmax];
+  __shared__ int s_wsum[kScNT / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int c = tid; c < k; c += kScNT)
+    cursor[c] = (int)(cluster_start[c] + block_offsets[(int64_t)blockIdx.x * k + c]);
+  const int64_t r0 = (int64_t)blockIdx.x * rpc, r1 = min(n, r0 + rpc);
+  const int per = (k + kScNT - 1) / kScNT;        // scan entries per thread
+  for (int64_t q0 = r0; q0 < r1; q0 += kScCh) {
+    const int m = (int)min((int64_t)kScCh, r1 - q0);
+    for (int c = tid; c < k; c += kScNT) lcnt[c] = 0;
+    __syncthreads();
+    int packed[kScPer];                            // (cluster << 15) | local rank
+#pragma unroll
+    for (int j = 0; j < kScPer; ++j) {
+      const int o = j * kScNT + tid;
+      packed[j] = -1;
+      if (o < m) {
+        const int c = assign[q0 + o];
+        packed[j] = (c << 15) | atomicAdd(&lcnt[c], 1);
+      }
+    }
+    __syncthreads();
+    // exclusive scan of lcnt -> lstart (per thread: `per` consecutive clusters)
+    const int c0 = tid * per, c1 = min(k, c0 + per);
+    int a = 0;
+    for (int c = c0; c < c1; ++c) a += lcnt[c];
+    int ia = a;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int t = __shfl_up(ia, off);
+      if (lane >= off) ia += t;
+    }
+    if (lane == 63) s_wsum[wid] = ia;
+    __syncthreads();
+    int run = ia - a;
+    for (int w = 0; w < wid; ++w) run += s_wsum[w];
+    for (int c = c0; c < c1; ++c) { lstart[c] = run; run += lcnt[c]; }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kScPer; ++j) {
+      if (packed[j] >= 0) {
+        const int c = packed[j] >> 15;
+        stage[lstart[c] + (packed[j] & 0x7fff)] = (c << 15) | (j * kScNT + tid);
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < m; i += kScNT) {
+      const int v = stage[i];
+      const int c = v >> 15;
+      perm[cursor[c] + (i - lstart[c])] = (int)(q0 + (v & 0x7fff));
+    }
+    __syncthreads();
+    for (int c = tid; c < k; c += kScNT) cursor[c] += lcnt[c];
+    __syncthreads();
   }
 }
 
@@ -1135,8 +1215,13 @@ hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n,
   hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), 2 * (size_t)k * sizeof(int64_t), st,
                      block_counts, B, k, seg, cluster_start, seg_start, cnt);
   DALGO_LAUNCH_CHECK();
-  hipLaunchKernelGGL(kmeans_scatter_kernel, dim3(B), dim3(256), lds_k, st, assign, n, rpc, k,
-                     (const int*)block_counts, (const int64_t*)cluster_start, perm);
+  const char* sc_env = getenv("DALGO_KM_SCATTER");            // "0": per-row LDS-cursor scatter
+  if (k <= kScKmax && !(sc_env && sc_env[0] == '0'))
+    hipLaunchKernelGGL(kmeans_scatter_chunked_kernel, dim3(B), dim3(kScNT), 0, st, assign, n, rpc, k,
+                       (const int*)block_counts, (const int64_t*)cluster_start, perm);
+  else
+    hipLaunchKernelGGL(kmeans_scatter_kernel, dim3(B), dim3(256), lds_k, st, assign, n, rpc, k,
+                       (const int*)block_counts, (const int64_t*)cluster_start, perm);
   DALGO_LAUNCH_CHECK();
   const int64_t max_segs = cdiv(n, seg) + k;
   return is_bf16 ? launch_segsum<uint16_t>(DP, X, ldx, perm, cluster_start, seg_start, k, seg, max_segs, S, st)

@@ -102,6 +102,28 @@ def test_kmeans_ties_lowest_index(cuda):
     assert a.tolist() == [0] * 5
 
 
+@pytest.mark.parametrize("k", [1024, 3000])
+@pytest.mark.parametrize("scatter", ["chunked", "cursor"])
+def test_kmeans_sorted_scatter_variants(cuda, monkeypatch, k, scatter):
+    """K3 sorted accumulate with the coalesced chunked scatter (k <= 2048, default) and the
+    per-row LDS-cursor scatter (DALGO_KM_SCATTER=0, and k > 2048): several blocks, full and
+    partial 32K-row chunks; exact counts, f64-checked sums."""
+    if scatter == "cursor":
+        monkeypatch.setenv("DALGO_KM_SCATTER", "0")
+    n, d = 300_001, 64
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(n, d, generator=g).to(torch.bfloat16)
+    a = torch.randint(0, k, (n,), generator=g, dtype=torch.int32)
+    DP = K.kmeans_dp(d)
+    S = torch.zeros(k, DP, device=cuda)
+    cnt = torch.zeros(k, dtype=torch.int64, device=cuda)
+    K.accumulate(K.prepare_points(X.to(cuda)), a.to(cuda), k, DP, S, cnt, method="sorted")
+    Sr = torch.zeros(k, DP, dtype=torch.float64)
+    Sr[:, :d].index_add_(0, a.long(), X.double())
+    assert torch.equal(cnt.cpu(), torch.bincount(a.long(), minlength=k))
+    assert torch.allclose(S.cpu().double(), Sr, atol=1e-2, rtol=1e-4)
+
+
 @pytest.mark.parametrize("method", ["sorted", "table"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_kmeans_accumulate_update(cuda, dtype, method):
