@@ -86,10 +86,9 @@ def main(argv=None):
     samples = model.global_sample_count()
     model.count_acc = None
     xg = getattr(getattr(model, "bucket", None), "xg", None)
-    if xg is not None:
-        xg.check()   # raise (non-zero exit) if a peer wait ever timed out
-    from dalgo.ops import lr as lr_ops
-    lr_ops.check_persistent()   # ... or a persistent launch's step-release wait
+    # collective: MAX of every rank's device error words (K11 peer waits, persistent
+    # step releases) first, then raise on EVERY rank (non-zero exit everywhere)
+    comm.check_device_errors("bench")
     launch = "persistent" if model._persistent() else (
         "hipgraph-replay" if model._graph_ok() else "per-step")
     allreduce = "xgmi-oneshot (K11)" if xg is not None else (

@@ -470,7 +470,13 @@ __device__ __forceinline__ void km_wait_vmcnt() {
 }
 typedef __attribute__((address_space(3))) void km_lds_void;
 
-template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF>
+// SWP (software-pipelined argmin): the MFMA chains of sub-tile s run in the same basic
+// block as the argmin VALU of sub-tile s-1 (its accumulators stay live one sub-tile
+// longer, +16 VGPRs per point tile), so the key/min work of the LAST sub-tile of a chunk
+// no longer runs MFMA-less after the chunk's final MFMA (s_nop hazard pad + ~50 VALU +
+// DMA issue + barrier + LDS fragment latency per chunk in the plain form): it fills the
+// issue gaps of the next chunk's first MFMAs instead.
+template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, bool SWP = false>
 __global__ void __launch_bounds__(NW * 64, MINB)
 kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
                           const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int kpad,
@@ -578,6 +584,31 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     }
   };
 
+  // SWP: accumulators of the previous sub-tile, reduced one sub-tile late. Initial keys
+  // are NaN bits (0x7fffffe0 | r after masking): larger than any finite distance key,
+  // so the dummy first reduction is displaced by the first real one.
+  f32x16 pacc[PT];
+  int pcb = 0;
+  if constexpr (SWP) {
+#pragma unroll
+    for (int t = 0; t < PT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) pacc[t][r] = __int_as_float(0x7fffffff);
+  }
+  auto reduce_tile = [&](const f32x16& acc, int t, int cb) {
+    int m = 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const int k0 = (__float_as_int(acc[r]) & kmask) | r;
+      const int k1 = (__float_as_int(acc[r + 1]) & kmask) | (r + 1);
+      m = min(min(m, k0), k1);   // one v_min3_i32 per pair
+    }
+    // strict: an equal key of a later sub-tile (higher ids) never displaces
+    const bool take = m < bkey[t];
+    bkey[t] = take ? m : bkey[t];
+    bsub[t] = take ? cb : bsub[t];
+  };
+
   issue(0);
   if (NBUF == 3 && nchunk > 1) issue(1);
   for (int ch = 0; ch < nchunk; ++ch) {
@@ -600,6 +631,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       uint4 an[KS];
       f32x16 hn_next;
       if (PF && sub + 1 < NSUB) load_frag(img, sub + 1, cb + 32, an, hn_next);
+      f32x16 cacc[PT];
 #pragma unroll
       for (int t = 0; t < PT; ++t) {
         f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
@@ -608,17 +640,23 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
         for (int s = 1; s < KS; ++s)
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
               __builtin_bit_cast(bf16x8, a[s]), __builtin_bit_cast(bf16x8, bf[t][s]), acc, 0, 0, 0);
-        int m = 0x7fffffff;
+        if constexpr (SWP) cacc[t] = acc;
+        else reduce_tile(acc, t, cb);
+      }
+      if constexpr (SWP) {
+        // argmin of the previous sub-tile: independent of the MFMAs above, same block
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const int k0 = (__float_as_int(acc[r]) & kmask) | r;
-          const int k1 = (__float_as_int(acc[r + 1]) & kmask) | (r + 1);
-          m = min(min(m, k0), k1);   // one v_min3_i32 per pair
+        for (int t = 0; t < PT; ++t) reduce_tile(pacc[t], t, pcb);
+#pragma unroll
+        for (int t = 0; t < PT; ++t) pacc[t] = cacc[t];
+        pcb = cb;
+        // pin the interleave: one MFMA, then a few argmin VALU ops, for every MFMA of
+        // this sub-tile (hipcc otherwise clusters the MFMAs and sinks the VALU after them)
+#pragma unroll
+        for (int i = 0; i < PT * KS; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // VALU
         }
-        // strict: an equal key of a later sub-tile (higher ids) never displaces
-        const bool take = m < bkey[t];
-        bkey[t] = take ? m : bkey[t];
-        bsub[t] = take ? cb : bsub[t];
       }
       if (sub + 1 < NSUB) {
         if constexpr (PF) {
@@ -631,6 +669,10 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       }
     }
     if (NBUF == 3 && ch + 2 < nchunk) issue(ch + 2);
+  }
+  if constexpr (SWP) {
+#pragma unroll
+    for (int t = 0; t < PT; ++t) reduce_tile(pacc[t], t, pcb);
   }
 
   // ---- decode, combine the two lane halves (same point, disjoint centre rows)
@@ -811,7 +853,9 @@ __global__ void __launch_bounds__(1024)
 kmeans_scan_kernel(int* __restrict__ block_counts, int B, int k, int seg,
                    int64_t* __restrict__ cluster_start, int64_t* __restrict__ seg_start,
                    unsigned long long* __restrict__ cnt_out) {
-  extern __shared__ int64_t tot[];            // [2k]: counts, then segment counts
+  // [2k] int32 (n < 2^31 is checked by the launcher): counts, then segment counts;
+  // 8 B per cluster keeps k = 16384 inside the 160 KB LDS (128 KB dynamic)
+  extern __shared__ int tot[];
   __shared__ int64_t s_part[2][1024 / 64];
   for (int c = threadIdx.x; c < k; c += blockDim.x) {
     // the column walk is load-latency bound: issue kBat loads before the stores
@@ -1059,7 +1103,7 @@ static hipError_t launch_assign_res(const void* X, int64_t n, int64_t ldx, const
 }
 
 // pipelined K2 (bf16, DP >= 64): grid = one PT-tile group per wave, MINB blocks per CU
-template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF>
+template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, bool SWP = false>
 static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                      const float* hn, int kpad, int* assign, float* mind,
                                      double* sse, hipStream_t st) {
@@ -1071,7 +1115,7 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
   const int64_t grid = cdiv(n, (int64_t)NW * PT * 32);
   if (grid == 0) return hipSuccess;
   if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
-  auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF>;
+  auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF, SWP>;
   static size_t attr_set = 0;   // largest dynamic size this instantiation was enabled for
   if (dyn > attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1096,7 +1140,8 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
 //          14..17 = pipelined distance-key form (bf16, DP >= 64; otherwise 5), 4 waves x
 //          64-centre chunks: 14 = 2 tiles/wave, 2 blocks/CU, triple-buffered, A prefetch;
 //          15 = 3 blocks/CU, no prefetch; 16 = 1 tile/wave, 4 blocks/CU, double-buffered;
-//          17 = 2 tiles, 3 blocks/CU, double-buffered
+//          17 = 2 tiles, 3 blocks/CU, double-buffered;
+//          18 = 14 with the software-pipelined argmin (SWP), 19 = 18 without A prefetch
 template <typename T, int DP>
 static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                    const float* hn, int kpad, int* assign, float* mind, double* sse,
@@ -1120,8 +1165,10 @@ static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const 
         return launch_assign_res<DP, 8, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
       }
       return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 14: case 15: case 16: case 17:
+    case 14: case 15: case 16: case 17: case 18: case 19:
       if constexpr (sizeof(T) == 2 && DP >= 64) {
+        if (variant == 18) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 19) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, false, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
         if (variant == 14) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
         if (variant == 15) return launch_assign_pipe<DP, 4, 2, 2, 3, 3, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
         if (variant == 16) return launch_assign_pipe<DP, 4, 1, 2, 4, 2, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
@@ -1212,7 +1259,17 @@ hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n,
   const size_t lds_k = (size_t)k * sizeof(int);
   hipLaunchKernelGGL(kmeans_hist_kernel, dim3(B), dim3(256), lds_k, st, assign, n, rpc, k, block_counts);
   DALGO_LAUNCH_CHECK();
-  hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), 2 * (size_t)k * sizeof(int64_t), st,
+  const size_t scan_lds = 2 * (size_t)k * sizeof(int);
+  if (scan_lds > 64 * 1024) {
+    static size_t scan_attr = 0;   // largest dynamic size enabled so far (k > 8192)
+    if (scan_lds > scan_attr) {
+      hipError_t e = hipFuncSetAttribute((const void*)kmeans_scan_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)scan_lds);
+      if (e != hipSuccess) return e;
+      scan_attr = scan_lds;
+    }
+  }
+  hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), scan_lds, st,
                      block_counts, B, k, seg, cluster_start, seg_start, cnt);
   DALGO_LAUNCH_CHECK();
   const char* sc_env = getenv("DALGO_KM_SCATTER");            // "0": per-row LDS-cursor scatter

@@ -103,6 +103,7 @@ class KMeans:
                 self.history.shift.append(float(self.shift2.item()))
                 if self.cfg.tol is not None and self.history.shift[-1] < self.cfg.tol:
                     break
+        comm.check_device_errors("end of k-means fit")
         return self.history
 
     def predict(self, X: torch.Tensor) -> torch.Tensor:

@@ -404,19 +404,21 @@ class ParallelSGD:
                 self.run_steps(k)
                 done += k
                 if ev and self.t % ev == 0:
+                    comm.check_device_errors("evaluation")
                     acc, loss = self.evaluate()
                     self.history.accs.append(acc)
                     self.history.losses.append(loss)
                     self.history.iters.append(self.t)
                 if callback is not None:
                     callback(self)
-            lr_ops.check_persistent()
+            comm.check_device_errors("end of fit")
             return self.history
         for _ in range(n):
             if verbose:
                 self.rt.log("On iteration %d" % (self.t + 1))
             self.step()
             if self.cfg.eval_every and (self.t % self.cfg.eval_every == 0):
+                comm.check_device_errors("evaluation")
                 acc, loss = self.evaluate()
                 self.history.accs.append(acc)
                 self.history.losses.append(loss)
@@ -425,6 +427,7 @@ class ParallelSGD:
                     self.rt.log("iterations: %d, accuracy: %f" % (self.t - 1, acc))
             if callback is not None:
                 callback(self)
+        comm.check_device_errors("end of fit")
         return self.history
 
     # --------------------------------------------------------- checkpointing

@@ -104,6 +104,7 @@ class PageRank:
         n = self.cfg.n_iterations if n_iterations is None else n_iterations
         for _ in range(n):
             self.step()
+        comm.check_device_errors("end of PageRank fit")
         return self
 
     def state_dict(self) -> dict:

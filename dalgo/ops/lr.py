@@ -117,12 +117,21 @@ def _workspace(device, nseg, gx, S) -> _Workspace:
     return ws
 
 
-def check_persistent():
-    """Raise if a persistent launch (tail nsteps > 1) ever timed out waiting for a step
-    release (the launch then ended early and the model is not trustworthy)."""
+def persistent_error() -> int:
+    """Local error word of the persistent launches (non-zero: a step-release wait
+    timed out, the launch ended early and the model is not trustworthy)."""
+    e = 0
     for ws in _ws_cache.values():
-        if ws.epochs and int(ws.perr.item()) != 0:
-            raise RuntimeError("persistent K1 launch: a step-release wait timed out")
+        if ws.epochs:
+            e = max(e, int(ws.perr.item()))
+    return e
+
+
+def check_persistent():
+    """Local (this rank only) form of the persistent-launch check; multi-rank callers
+    use the collective :func:`dalgo.parallel.comm.check_device_errors`."""
+    if persistent_error() != 0:
+        raise RuntimeError("persistent K1 launch: a step-release wait timed out")
 
 
 def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor, *,

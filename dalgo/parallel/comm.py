@@ -64,6 +64,50 @@ def all_reduce_sum(t: torch.Tensor, async_op: bool = False):
     return work if async_op else t
 
 
+class DeviceCollectiveError(RuntimeError):
+    """A device-side collective wait (K11 peer flag, persistent step release) timed
+    out on some rank: the results since the last check are not trustworthy."""
+
+
+_error_seen = False
+
+
+def error_seen() -> bool:
+    """True once :func:`check_device_errors` has raised in this process."""
+    return _error_seen
+
+
+def _local_error_word() -> int:
+    e = 0
+    from dalgo.parallel import xgmi
+    for inst in list(xgmi._shared.values()):
+        if inst is not None:
+            e = max(e, int(inst.err.item()))
+    from dalgo.ops import lr as lr_ops
+    e = max(e, lr_ops.persistent_error())
+    return e
+
+
+def check_device_errors(where: str = "") -> None:
+    """Collective (EVERY rank must call it at the same point): MAX over ranks of the
+    device error words (K11 bounded peer-flag waits, persistent-launch step releases).
+    Raises :class:`DeviceCollectiveError` on every rank if any rank's word is set, so
+    no rank is left blocked in a later collective. The reduction goes through the
+    process group (never K11, whose failure it reports)."""
+    global _error_seen
+    e = _local_error_word()
+    if _active():
+        dev = runtime.get().device if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor([e], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        e = int(t.item())
+    if e:
+        _error_seen = True
+        at = f" (at {where})" if where else ""
+        raise DeviceCollectiveError(
+            f"a device-side collective wait timed out on some rank{at}: results are invalid")
+
+
 def all_reduce_max(t: torch.Tensor):
     if _active():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

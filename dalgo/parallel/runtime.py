@@ -112,7 +112,16 @@ def get() -> Runtime:
 def shutdown():
     """Tear down the process group (``spark.stop()`` equivalent)."""
     global _RT
+    failed = False
     if dist.is_available() and dist.is_initialized():
+        from dalgo.parallel import comm
+        try:
+            comm.check_device_errors("shutdown")   # collective: every rank learns it
+        except comm.DeviceCollectiveError as e:
+            print(f"[dalgo] rank {dist.get_rank()}: {e}", file=sys.stderr)
+        except Exception as e:
+            print(f"[dalgo] device error check failed: {e}", file=sys.stderr)
+        failed = comm.error_seen()
         try:
             from dalgo.parallel import xgmi
             xgmi.close_shared()
@@ -124,6 +133,10 @@ def shutdown():
             pass
         dist.destroy_process_group()
     _RT = None
+    if failed:
+        # a device collective timed out at some point of the run: exit non-zero on
+        # every rank even if the caller swallowed the exception
+        raise SystemExit(3)
 
 
 def seed_everything(seed: int):

@@ -125,6 +125,8 @@ class XgmiAllReduce:
         return x
 
     def check(self):
+        """Local check of this rank's error word only; training code uses the
+        collective :func:`dalgo.parallel.comm.check_device_errors` (raises on every rank)."""
         if int(self.err.item()) != 0:
             raise RuntimeError("xGMI all-reduce: a peer flag wait timed out (results invalid)")
 

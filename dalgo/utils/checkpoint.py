@@ -17,6 +17,11 @@ def path_for(ckpt_dir: str, name: str, rank: int | None = None) -> str:
 
 
 def save(state: dict, ckpt_dir: str, name: str, rank: int = 0, per_rank: bool = False) -> str | None:
+    """Collective: every rank calls it (rank 0 writes unless ``per_rank``). A device
+    collective that timed out on any rank raises here on every rank, so a poisoned
+    state is never written."""
+    from dalgo.parallel import comm
+    comm.check_device_errors("checkpoint save")
     if not per_rank and rank != 0:
         return None
     os.makedirs(ckpt_dir, exist_ok=True)

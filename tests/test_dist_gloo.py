@@ -91,3 +91,32 @@ def test_other_algorithms_two_ranks_equal_one():
     assert np.allclose(one["als"], two[0]["als"], rtol=1e-9)
     assert one["mc"] == two[0]["mc"] == two[1]["mc"]
     assert abs(one["mc"][0] - math.pi) < 0.02
+
+
+def _error_check_body(rt):
+    """Rank 1 alone carries a set K11 error word; both ranks must raise."""
+    import torch
+
+    from dalgo.parallel import comm, xgmi
+
+    class _Fake:
+        err = torch.ones(1, dtype=torch.int32) if rt.rank == 1 else torch.zeros(1, dtype=torch.int32)
+
+    xgmi._shared["fake"] = _Fake()
+    raised = False
+    try:
+        comm.check_device_errors("test")
+    except comm.DeviceCollectiveError:
+        raised = True
+    finally:
+        del xgmi._shared["fake"]
+        comm._error_seen = False      # let the harness' shutdown exit cleanly
+    # clean words: no raise on any rank
+    comm.check_device_errors("test-clean")
+    return raised
+
+
+def test_device_error_check_raises_on_every_rank():
+    """a peer-wait timeout on ONE rank raises on EVERY rank (collective MAX
+    first), so no rank is left blocked in a later collective."""
+    assert run_world(_error_check_body, world=2) == [True, True]

@@ -102,18 +102,28 @@ def test_kmeans_ties_lowest_index(cuda):
     assert a.tolist() == [0] * 5
 
 
-@pytest.mark.parametrize("k", [1024, 3000])
+@pytest.mark.parametrize("k,skew", [(1024, "uniform"), (1500, "uniform"), (2048, "uniform"),
+                                    (2048, "one-cluster"), (1500, "two-clusters"),
+                                    (3000, "uniform"), (12000, "uniform"), (16384, "uniform")])
 @pytest.mark.parametrize("scatter", ["chunked", "cursor"])
-def test_kmeans_sorted_scatter_variants(cuda, monkeypatch, k, scatter):
+def test_kmeans_sorted_scatter_variants(cuda, monkeypatch, k, skew, scatter):
     """K3 sorted accumulate with the coalesced chunked scatter (k <= 2048, default) and the
     per-row LDS-cursor scatter (DALGO_KM_SCATTER=0, and k > 2048): several blocks, full and
-    partial 32K-row chunks; exact counts, f64-checked sums."""
+    partial 32K-row chunks; exact counts, f64-checked sums. k = 1500 / 2048 run the
+    two-clusters-per-thread scan of the chunked scatter (kScKmax boundary); "one-cluster"
+    puts every row of a 32K chunk in one cluster (15-bit local rank at its limit);
+    k = 12000 / 16384 need the > 64 KB dynamic-LDS scan."""
     if scatter == "cursor":
         monkeypatch.setenv("DALGO_KM_SCATTER", "0")
     n, d = 300_001, 64
     g = torch.Generator().manual_seed(3)
     X = torch.randn(n, d, generator=g).to(torch.bfloat16)
-    a = torch.randint(0, k, (n,), generator=g, dtype=torch.int32)
+    if skew == "one-cluster":
+        a = torch.full((n,), k - 1, dtype=torch.int32)
+    elif skew == "two-clusters":
+        a = torch.where(torch.rand(n, generator=g) < 0.5, 7, k - 2).to(torch.int32)
+    else:
+        a = torch.randint(0, k, (n,), generator=g, dtype=torch.int32)
     DP = K.kmeans_dp(d)
     S = torch.zeros(k, DP, device=cuda)
     cnt = torch.zeros(k, dtype=torch.int64, device=cuda)

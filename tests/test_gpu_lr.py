@@ -83,6 +83,31 @@ def test_lr_grad_work_pool(cuda, pool_frac, fine):
         assert rel < 1e-4, (step, rel)
 
 
+@pytest.mark.parametrize("align", [4, 260])
+@pytest.mark.parametrize("mode", ["atomic", "deterministic", "pool"])
+def test_lr_grad_static_range_alignment(cuda, monkeypatch, align, mode):
+    """K1 with block ranges that are not multiples of 256 rows (LR_RPB_ALIGN 4 / 260):
+    partial 256-row groups at every block end, Philox quads straddling block
+    boundaries, a row_offset that is not a multiple of 4, and the deterministic,
+    atomic and pool epilogues; exact counts and G vs the f64 CPU reference."""
+    monkeypatch.setattr(L, "LR_RPB_ALIGN", align)
+    n, D = 300_001, 256
+    X, y = _data(n, D, torch.bfloat16, seed=8)
+    Xd, yd = X.to(cuda), y.to(cuda)
+    seg = torch.tensor([0, 100_003, n], dtype=torch.int64)
+    W = torch.randn(2, D + 1, generator=torch.Generator().manual_seed(6)) * 0.05
+    for step in range(3):
+        kw = dict(D=D, frac=0.1, step=step, seed=13, row_offset=6)
+        G_ref, C_ref = L.lr_grad(X, y, W.double(), seg, **kw)
+        extra = dict(deterministic=(mode == "deterministic"),
+                     pool_frac=0.2 if mode == "pool" else 0.0)
+        Gd, Cd = L.lr_grad(Xd, yd, W.to(cuda), seg.to(cuda), **extra, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(Cd.cpu().double(), C_ref), (step, Cd, C_ref)
+        rel = (Gd.cpu().double() - G_ref).abs().max() / G_ref.abs().max()
+        assert rel < 1e-4, (step, rel)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_lr_eval(cuda, dtype):
     X, y = _data(7777, 100, dtype, seed=5)

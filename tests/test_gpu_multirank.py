@@ -62,6 +62,20 @@ def test_xgmi_allreduce_ranks_on_one_gpu(cuda, n):
     assert f"XGMI_OK world={n}" in out
 
 
+def test_xgmi_timeout_raises_on_every_rank(cuda):
+    """A K11 peer wait that times out on rank 0 only: the collective check raises on
+    both ranks and shutdown exits non-zero (no rank silently continues)."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           "tests/helpers/xgmi_timeout.py"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    out = r.stdout + r.stderr
+    assert "XG_RAISED rank 0" in out and "XG_RAISED rank 1" in out, out[-3000:]
+    assert "XG_NO_RAISE" not in out and "XG_SHUTDOWN_RETURNED" not in out, out[-3000:]
+    assert r.returncode != 0
+
+
 def _final_w(out):
     import numpy as np
     txt = out.split("Final w:")[1].split("Final acc")[0]
