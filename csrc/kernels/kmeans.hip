@@ -990,7 +990,7 @@ kmeans_scatter_chunked_kernel(const int* __restrict__ assign, int64_t n, int64_t
   }
 }
 
-template <typename T, int DP, int NW>
+template <typename T, int DP, int NW, bool NT>
 __global__ void __launch_bounds__(NW * 64)
 kmeans_segsum_kernel(const T* __restrict__ X, int64_t ldx, const int* __restrict__ perm,
                      const int64_t* __restrict__ cluster_start, const int64_t* __restrict__ seg_start,
@@ -1024,12 +1024,22 @@ kmeans_segsum_kernel(const T* __restrict__ X, int64_t ldx, const int* __restrict
         for (int u = 0; u < 16; ++u) {
           const int row = __builtin_amdgcn_readlane(idx, u0 + u);
           const T* rp = X + (int64_t)(row < 0 ? 0 : row) * ldx + lane * EPL;
+          if constexpr (sizeof(T) == 2 && EPL % 2 == 0) {
+            // rows are gathered exactly once per iteration: nt loads
 #pragma unroll
-          for (int e = 0; e < EPL; ++e) {
-            float x = 0.f;
-            if constexpr (sizeof(T) == 2) x = bf16_to_f32(reinterpret_cast<const uint16_t*>(rp)[e]);
-            else x = reinterpret_cast<const float*>(rp)[e];
-            v[u][e] = (lane_on && row >= 0) ? x : 0.f;
+            for (int e = 0; e < EPL; e += 2) {
+              const uint32_t w2 = ld_u32<NT>(reinterpret_cast<const uint32_t*>(rp) + e / 2);
+              v[u][e] = (lane_on && row >= 0) ? bf16lo(w2) : 0.f;
+              v[u][e + 1] = (lane_on && row >= 0) ? bf16hi(w2) : 0.f;
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+              float x = 0.f;
+              if constexpr (sizeof(T) == 2) x = bf16_to_f32(reinterpret_cast<const uint16_t*>(rp)[e]);
+              else x = reinterpret_cast<const float*>(rp)[e];
+              v[u][e] = (lane_on && row >= 0) ? x : 0.f;
+            }
           }
         }
 #pragma unroll
@@ -1141,7 +1151,9 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
 //          64-centre chunks: 14 = 2 tiles/wave, 2 blocks/CU, triple-buffered, A prefetch;
 //          15 = 3 blocks/CU, no prefetch; 16 = 1 tile/wave, 4 blocks/CU, double-buffered;
 //          17 = 2 tiles, 3 blocks/CU, double-buffered;
-//          18 = 14 with the software-pipelined argmin (SWP), 19 = 18 without A prefetch
+//          18 = 14 with the software-pipelined argmin (SWP), 19 = 18 without A prefetch,
+//          20 = 8-wave blocks (1 per CU, 512 points per chunk), 21 = 20 with 128-centre
+//          chunks, 22 = 20 with SWP, 23 = 14 with 128-centre chunks
 template <typename T, int DP>
 static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                    const float* hn, int kpad, int* assign, float* mind, double* sse,
@@ -1165,8 +1177,14 @@ static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const 
         return launch_assign_res<DP, 8, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
       }
       return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 14: case 15: case 16: case 17: case 18: case 19:
+    case 14: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23:
       if constexpr (sizeof(T) == 2 && DP >= 64) {
+        // one 8-wave block per CU: every centre chunk feeds 512 points (half the L2 -> LDS
+        // centre traffic of two independent 4-wave blocks)
+        if (variant == 20) return launch_assign_pipe<DP, 8, 2, 2, 1, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 21) return launch_assign_pipe<DP, 8, 2, 4, 1, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 22) return launch_assign_pipe<DP, 8, 2, 2, 1, 3, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 23) return launch_assign_pipe<DP, 4, 2, 4, 2, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
         if (variant == 18) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
         if (variant == 19) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, false, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
         if (variant == 14) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
@@ -1227,8 +1245,12 @@ static hipError_t launch_segsum_dp(const void* X, int64_t ldx, const int* perm, 
                                    hipStream_t st) {
   constexpr int NW = 4;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(max_segs, NW), 256 * 16));
-  hipLaunchKernelGGL((kmeans_segsum_kernel<T, DP, NW>), dim3(grid), dim3(NW * 64), 0, st,
-                     (const T*)X, ldx, perm, cs, ss, k, seg, S);
+  if (env_int("DALGO_NT", 1))
+    hipLaunchKernelGGL((kmeans_segsum_kernel<T, DP, NW, true>), dim3(grid), dim3(NW * 64), 0, st,
+                       (const T*)X, ldx, perm, cs, ss, k, seg, S);
+  else
+    hipLaunchKernelGGL((kmeans_segsum_kernel<T, DP, NW, false>), dim3(grid), dim3(NW * 64), 0, st,
+                       (const T*)X, ldx, perm, cs, ss, k, seg, S);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -216,7 +216,7 @@ constexpr int kRing = 512;   // per-wave ring of selected local row indices
 
 // EVAL=false: gradient; EVAL=true: accuracy + log-loss over every row.
 // PIPE: software-pipelined (two register sets) vs. single-buffered sweep.
-template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, bool PERSIST>
+template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, bool PERSIST, int AUX = 0>
 __global__ void __launch_bounds__(NW * 64)
 lr_rows_kernel(const LrParams p) {
   constexpr int VEC = VecTraits<T>::VEC;
@@ -475,7 +475,7 @@ lr_rows_kernel(const LrParams p) {
           (void*)(X + r[k] * p.ld), (short)0, (int)(p.ld * (int64_t)sizeof(T)), 0x00020000);
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (c * 64 + lane) * 16, 0, 0);
+        auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (c * 64 + lane) * 16, 0, AUX);
         b.x[k][c] = make_uint4(v[0], v[1], v[2], v[3]);
       }
     }
@@ -731,7 +731,7 @@ lr_rows_kernel(const LrParams p) {
 
 using namespace dalgo;
 
-template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U>
+template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, int AUX = 0>
 static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st) {
   dim3 grid(gx, nseg), block(NW * 64);
   if (p.nsteps > 1) {
@@ -744,7 +744,7 @@ static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st)
     }
     return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL((lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, false>), grid, block, 0, st, p);
+  hipLaunchKernelGGL((lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, false, AUX>), grid, block, 0, st, p);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -754,9 +754,11 @@ static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st)
 //   2: 8 waves, single set                  3: 8 waves, pipelined
 //   4: 4 waves, 8-row batches               5: 8 waves, 8-row batches
 //   6: 12 waves, pipelined (3 waves/SIMD)   7: 16 waves, single set (4 waves/SIMD)
+//   8: = 3 with nt row loads   9: = 5 with nt   10: = 3 with sc0|nt   11: = 3 with sc0|sc1
 template <typename T, int NC, bool EVAL>
 static hipError_t launch_variant(const LrParams& p, int gx, int nseg, int variant, hipStream_t st) {
   if constexpr (NC >= 4) {   // register budget: one 4-row set at 4 chunks/lane
+    if (variant == 8 || variant == 9) return launch_lr<T, NC, EVAL, 8, false, 4, 2>(p, gx, nseg, st);
     return (variant == 2 || variant == 3 || variant == 5)
                ? launch_lr<T, NC, EVAL, 8, false, 4>(p, gx, nseg, st)
                : launch_lr<T, NC, EVAL, 4, false, 4>(p, gx, nseg, st);
@@ -770,6 +772,11 @@ static hipError_t launch_variant(const LrParams& p, int gx, int nseg, int varian
       case 5: return launch_lr<T, NC, EVAL, 8, false, 8>(p, gx, nseg, st);
       case 6: return launch_lr<T, NC, EVAL, 12, true, 4>(p, gx, nseg, st);
       case 7: return launch_lr<T, NC, EVAL, 16, false, 4>(p, gx, nseg, st);
+      // X-row cache policy (aux bits of the buffer load: 2 = nt, 1 = sc0, 16 = sc1)
+      case 8: return launch_lr<T, NC, EVAL, 8, true, 4, 2>(p, gx, nseg, st);
+      case 9: return launch_lr<T, NC, EVAL, 8, false, 8, 2>(p, gx, nseg, st);
+      case 10: return launch_lr<T, NC, EVAL, 8, true, 4, 3>(p, gx, nseg, st);
+      case 11: return launch_lr<T, NC, EVAL, 8, true, 4, 17>(p, gx, nseg, st);
       default: return hipErrorInvalidValue;
     }
   }

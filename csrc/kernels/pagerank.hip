@@ -83,7 +83,7 @@ __device__ __forceinline__ void flush_run(float* acc, int32_t* pres, int key, fl
   }
 }
 
-template <int NW>
+template <int NW, bool NT>
 __global__ void __launch_bounds__(NW * 64)
 pr_spmv_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dstl, int64_t E,
                const float* __restrict__ c, float* __restrict__ acc, int32_t* __restrict__ pres) {
@@ -97,8 +97,8 @@ pr_spmv_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dstl
     const int64_t e0 = wi * 256 + 4 * lane;
     int4 s4 = make_int4(-1, -1, -1, -1), d4 = make_int4(-1, -1, -1, -1);
     if (e0 < E) {
-      s4 = *reinterpret_cast<const int4*>(src + e0);
-      d4 = *reinterpret_cast<const int4*>(dstl + e0);
+      s4 = ld_int4<NT>(src + e0);
+      d4 = ld_int4<NT>(dstl + e0);
     }
     const int sv[4] = {s4.x, s4.y, s4.z, s4.w};
     const int dv[4] = {d4.x, d4.y, d4.z, d4.w};
@@ -362,8 +362,13 @@ hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, con
   const int64_t nwin = cdiv(E, 256);
   const int grid = (int)std::min<int64_t>(cdiv(nwin, NW), 256 * 16);
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL(pr_spmv_kernel<NW>, dim3(grid), dim3(NW * 64), 0, st, src, dstl, E, c, acc,
-                     pres);
+  // edge stream read once per iteration: nt loads (DALGO_NT=0 restores the default policy)
+  if (env_int("DALGO_NT", 1))
+    hipLaunchKernelGGL((pr_spmv_kernel<NW, true>), dim3(grid), dim3(NW * 64), 0, st, src, dstl, E, c,
+                       acc, pres);
+  else
+    hipLaunchKernelGGL((pr_spmv_kernel<NW, false>), dim3(grid), dim3(NW * 64), 0, st, src, dstl, E, c,
+                       acc, pres);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

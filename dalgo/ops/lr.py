@@ -28,7 +28,7 @@ import os
 # Launch shape of the row-streaming kernels (tuned on MI355X, see profiles/):
 #   LR_VARIANT      = launch-shape variant (table in csrc/kernels/lr_grad.hip)
 #   TARGET_BLOCKS   = workgroups per launch (split over segments)
-LR_VARIANT = int(os.environ.get("DALGO_LR_VARIANT", "3"))   # 8 waves, pipelined (bench sweep)
+LR_VARIANT = int(os.environ.get("DALGO_LR_VARIANT", "8"))   # 8 waves, pipelined, nt row loads (bench sweep)
 _TARGET_BLOCKS = int(os.environ.get("DALGO_LR_BLOCKS", "256"))
 #   FINE_GROUPS     = switch the in-block work claims from 256-row groups to 64-row
 #                     quarters once fewer than this many groups are unclaimed (0 = off)

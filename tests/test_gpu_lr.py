@@ -37,6 +37,25 @@ def test_lr_grad_matches_reference(cuda, dtype, D, frac):
     assert err / scale < 2e-5, (err, scale)
 
 
+@pytest.mark.parametrize("variant", list(range(12)))
+@pytest.mark.parametrize("D", [256, 1024, 2048])
+def test_lr_grad_every_variant(cuda, variant, D):
+    """Every launch-shape / cache-policy variant of K1 selects the same rows and sums
+    the same gradient (variants 8-11 differ only in the X-row load policy bits)."""
+    n = 40_000
+    X, y = _data(n, D, torch.bfloat16, seed=21)
+    seg = torch.tensor([0, 13_331, n], dtype=torch.int64)
+    W = torch.randn(2, D + 1, generator=torch.Generator().manual_seed(3)) * 0.05
+    kw = dict(D=D, frac=0.1, step=5, seed=7)
+    G_ref, C_ref = L.lr_grad(X, y, W.double(), seg, **kw)
+    Gd, Cd = L.lr_grad(X.to(cuda), y.to(cuda), W.to(cuda), seg.to(cuda),
+                       variant=variant | (L.LR_FINE_GROUPS << 16), **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(Cd.cpu().double(), C_ref), (variant, Cd, C_ref)
+    rel = (Gd.cpu().double() - G_ref).abs().max() / G_ref.abs().max()
+    assert rel < 1e-4, (variant, rel)
+
+
 def test_lr_grad_single_segment_deterministic(cuda):
     X, y = _data(200_000, 1024, torch.bfloat16, seed=3)
     Xd, yd = X.to(cuda), y.to(cuda)
