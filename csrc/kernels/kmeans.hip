@@ -490,7 +490,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   constexpr int CHP = CH * NJ;                 // 16-B pieces per chunk
   constexpr int GPT = CHP / NT;                // LDS-DMA instructions per thread per chunk
   static_assert(CHP % NT == 0, "chunk must be a whole number of block-wide DMA rounds");
-  static_assert(NBUF == 2 || NBUF == 3, "double or triple buffered chunks");
+  static_assert(NBUF >= 2 && NBUF <= 4, "double, triple or quadruple buffered chunks");
   __shared__ __attribute__((aligned(16))) uint4 s_c[NBUF * CHP];
   extern __shared__ __attribute__((aligned(16))) float s_hn[];   // [kpad]: 0.5|c|^2 + M
   __shared__ float s_m[NW];
@@ -610,10 +610,21 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   };
 
   issue(0);
-  if (NBUF == 3 && nchunk > 1) issue(1);
+  if (NBUF >= 3 && nchunk > 1) issue(1);
+  if (NBUF >= 4 && nchunk > 2) issue(2);
   for (int ch = 0; ch < nchunk; ++ch) {
-    if (NBUF == 3 && ch + 1 < nchunk) km_wait_vmcnt<GPT>();   // chunk ch landed, ch+1 in flight
-    else km_wait_vmcnt<0>();
+    // chunk ch landed; chunks ch+1 .. ch+NBUF-2 stay in flight
+    const int ahead = NBUF >= 3 ? min(NBUF - 2, nchunk - 1 - ch) : 0;
+    if constexpr (NBUF >= 4) {
+      if (ahead >= 2) km_wait_vmcnt<2 * GPT>();
+      else if (ahead == 1) km_wait_vmcnt<GPT>();
+      else km_wait_vmcnt<0>();
+    } else if constexpr (NBUF == 3) {
+      if (ahead >= 1) km_wait_vmcnt<GPT>();
+      else km_wait_vmcnt<0>();
+    } else {
+      km_wait_vmcnt<0>();
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // s_hn stores (first chunk)
     // publishes chunk ch to every wave AND retires everyone's reads of chunk ch-1,
     // whose buffer is refilled next (triple: chunk ch+2 after this chunk's MFMAs;
@@ -668,7 +679,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
         }
       }
     }
-    if (NBUF == 3 && ch + 2 < nchunk) issue(ch + 2);
+    if (NBUF >= 3 && ch + NBUF - 1 < nchunk) issue(ch + NBUF - 1);
   }
   if constexpr (SWP) {
 #pragma unroll
@@ -1153,7 +1164,13 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
 //          17 = 2 tiles, 3 blocks/CU, double-buffered;
 //          18 = 14 with the software-pipelined argmin (SWP), 19 = 18 without A prefetch,
 //          20 = 8-wave blocks (1 per CU, 512 points per chunk), 21 = 20 with 128-centre
-//          chunks, 22 = 20 with SWP, 23 = 14 with 128-centre chunks
+//          chunks, 22 = 20 with SWP, 23 = 14 quadruple-buffered (chunk ch+3 in flight
+//          while ch is consumed), 24 = 23 with SWP, 25 = 128-centre chunks double-
+//          buffered (64 MFMAs per barrier), 26 = 25 with SWP, 27 = 25 without A prefetch,
+//          28 / 29 = 8-wave blocks, 256- / 128-centre chunks double-buffered, SWP;
+//          30 = 28 without SWP. Measured and removed (profiles/round2/README.md): a
+//          persistent form looping blocks over point groups with next-group L2 prefetch
+//          (2-4 % slower than 26), s_setprio on alternate blocks (within 1 %)
 template <typename T, int DP>
 static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                    const float* hn, int kpad, int* assign, float* mind, double* sse,
@@ -1177,14 +1194,21 @@ static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const 
         return launch_assign_res<DP, 8, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
       }
       return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 14: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23:
+    case 14: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23: case 24: case 25: case 26: case 27: case 28: case 29: case 30:
       if constexpr (sizeof(T) == 2 && DP >= 64) {
         // one 8-wave block per CU: every centre chunk feeds 512 points (half the L2 -> LDS
         // centre traffic of two independent 4-wave blocks)
         if (variant == 20) return launch_assign_pipe<DP, 8, 2, 2, 1, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
         if (variant == 21) return launch_assign_pipe<DP, 8, 2, 4, 1, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
         if (variant == 22) return launch_assign_pipe<DP, 8, 2, 2, 1, 3, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 23) return launch_assign_pipe<DP, 4, 2, 4, 2, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 23) return launch_assign_pipe<DP, 4, 2, 2, 2, 4, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 24) return launch_assign_pipe<DP, 4, 2, 2, 2, 4, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 25) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 26) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 27) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 28) return launch_assign_pipe<DP, 8, 2, 8, 1, 2, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 29) return launch_assign_pipe<DP, 8, 2, 4, 1, 2, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 30) return launch_assign_pipe<DP, 8, 2, 8, 1, 2, true, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
         if (variant == 18) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
         if (variant == 19) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, false, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
         if (variant == 14) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);

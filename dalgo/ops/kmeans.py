@@ -77,12 +77,13 @@ def refresh(cen: Centers):
 import os
 
 # launch variant of the assign kernel (table in csrc/kernels/kmeans.hip). -1 = per
-# dtype: f32 -> 5 (8-wave blocks capped at 128 VGPRs, two blocks per CU), bf16 -> 14
-# (pipelined distance-key form: 4.87 vs 5.20 ms for variant 5 at 20M x 128 x 1024 on
-# one MI355X; DP < 64 falls back to 5 inside the launcher)
+# dtype: f32 -> 5 (8-wave blocks capped at 128 VGPRs, two blocks per CU), bf16 -> 26
+# (pipelined distance-key form with 128-centre double-buffered chunks and the software-
+# pipelined argmin: 4.47-4.63 ms vs 4.73-5.11 ms for the round-1 default 14 at
+# 20M x 128 x 1024, profiles/round2/README.md; DP < 64 falls back to 5 in the launcher)
 ASSIGN_VARIANT = int(os.environ.get("DALGO_KM_VARIANT", "-1"))
 RESIDENT_VARIANTS = (11, 12, 13)
-_BF16_DEFAULT = 14
+_BF16_DEFAULT = 26
 _scratch: dict = {}
 
 
