@@ -390,15 +390,19 @@ void kmeans_assign(const Tensor& X, const Tensor& Cq, const Tensor& hn, Tensor a
     md = mind->data_ptr<float>();
   }
   double* ss = nullptr;
+  int sse_mask = 0;   // blocks add their SSE to slot (block & mask): a power-of-two
+                      // prefix of `sse` (one slot = every block on one address)
   if (sse.has_value()) {
     check_dev(*sse, "sse");
-    TORCH_CHECK(sse->scalar_type() == at::kDouble && sse->numel() >= 1, "sse f64[1]");
+    TORCH_CHECK(sse->scalar_type() == at::kDouble && sse->numel() >= 1 && sse->is_contiguous(),
+                "sse f64[>=1]");
     ss = sse->data_ptr<double>();
+    while (sse_mask < 1023 && 2 * (sse_mask + 1) <= sse->numel()) sse_mask = 2 * sse_mask + 1;
   }
   DeviceGuard guard(X.device());
   DALGO_CHECK_HIP(dalgo_kmeans_assign(X.data_ptr(), X.scalar_type() == at::kBFloat16, X.size(0),
                                       X.stride(0), DP, Cq.data_ptr(), hn.data_ptr<float>(),
-                                      (int)kpad, assign.data_ptr<int>(), md, ss, (int)variant,
+                                      (int)kpad, assign.data_ptr<int>(), md, ss, sse_mask, (int)variant,
                                       cur_stream()),
                   "kmeans_assign");
 }

@@ -83,7 +83,7 @@ template <typename T, int DP, int PT, int NW, int NSUB, int MINW>
 __global__ void __launch_bounds__(NW * 64, MINW)
 kmeans_assign_kernel(const T* __restrict__ X, int64_t n, int64_t ldx, const T* __restrict__ Cq,
                      const float* __restrict__ hn, int kpad, int* __restrict__ assign,
-                     float* __restrict__ mind, double* __restrict__ sse) {
+                     float* __restrict__ mind, double* __restrict__ sse, int sse_mask) {
   using G = KGeom<T, DP>;
   constexpr int NT = NW * 64;
   constexpr int CH = 32 * NSUB;
@@ -232,7 +232,7 @@ kmeans_assign_kernel(const T* __restrict__ X, int64_t n, int64_t ldx, const T* _
     if (tid == 0) {
       double s = 0.0;
       for (int w = 0; w < NW; ++w) s += s_sse[w];
-      atomicAdd(sse, s);
+      atomicAdd(sse + (blockIdx.x & sse_mask), s);
     }
   }
 }
@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(NW * 64, 1)
 kmeans_assign_res_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
                          const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int c0,
                          int ncen, int first, int last, int* __restrict__ assign,
-                         float* __restrict__ dist, double* __restrict__ sse) {
+                         float* __restrict__ dist, double* __restrict__ sse, int sse_mask) {
   using G = ResGeom<DP>;
   constexpr int KS = G::KS, KE = G::KE, NJ = G::NJ;
   constexpr int NT = NW * 64;
@@ -434,7 +434,7 @@ kmeans_assign_res_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
     if (tid == 0) {
       double tot = 0.0;
       for (int w = 0; w < NW; ++w) tot += s_sse[w];
-      atomicAdd(sse, tot);
+      atomicAdd(sse + (blockIdx.x & sse_mask), tot);
     }
   }
 }
@@ -476,12 +476,15 @@ typedef __attribute__((address_space(3))) void km_lds_void;
 // no longer runs MFMA-less after the chunk's final MFMA (s_nop hazard pad + ~50 VALU +
 // DMA issue + barrier + LDS fragment latency per chunk in the plain form): it fills the
 // issue gaps of the next chunk's first MFMAs instead.
-template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, bool SWP = false>
+// DIAG (diagnostics only, wrong assignments): 1 = argmin VALU replaced by one min per
+// tile, 2 = MFMAs removed (accumulator = C input, A fragments folded by XOR), 3 = 2
+// without the C-init LDS reads, 4 = 3 without the A-fragment LDS reads
+template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, int SWP = 0, int DIAG = 0>
 __global__ void __launch_bounds__(NW * 64, MINB)
 kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
                           const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int kpad,
                           int* __restrict__ assign, float* __restrict__ mind,
-                          double* __restrict__ sse) {
+                          double* __restrict__ sse, int sse_mask) {
   constexpr int KS = DP / 16;                  // 32x32x16 k-steps per centre row
   constexpr int NJ = DP * 2 / 16;              // 16-B pieces per row (= 2 KS)
   constexpr int SWZ = (NJ >= 16 ? 16 : NJ) - 1;
@@ -575,27 +578,44 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   const int arow = cl * NJ;
   const int asw = cl & SWZ;
   auto load_frag = [&](const uint4* img, int sub, int cb, uint4 (&a)[KS], f32x16& hc) {
+    if constexpr (DIAG == 4) {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) a[s] = img[sub * 32 * NJ + arow + ((2 * s + h) ^ asw)];
+      for (int s = 0; s < KS; ++s) a[s] = make_uint4(cb + s, sub, 0u, 0u);
+    } else {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float4 v = *reinterpret_cast<const float4*>(&s_hn[cb + 8 * g + 4 * h]);
-      hc[4 * g + 0] = v.x; hc[4 * g + 1] = v.y; hc[4 * g + 2] = v.z; hc[4 * g + 3] = v.w;
+      for (int s = 0; s < KS; ++s) a[s] = img[sub * 32 * NJ + arow + ((2 * s + h) ^ asw)];
+    }
+    if constexpr (DIAG >= 3) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) hc[r] = (float)(cb + r);
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 v = *reinterpret_cast<const float4*>(&s_hn[cb + 8 * g + 4 * h]);
+        hc[4 * g + 0] = v.x; hc[4 * g + 1] = v.y; hc[4 * g + 2] = v.z; hc[4 * g + 3] = v.w;
+      }
     }
   };
 
   // SWP: accumulators of the previous sub-tile, reduced one sub-tile late. Initial keys
   // are NaN bits (0x7fffffe0 | r after masking): larger than any finite distance key,
   // so the dummy first reduction is displaced by the first real one.
+  // SWP = 2 defers only the last point tile's reduction (16 accumulator VGPRs instead
+  // of 16 * PT); the earlier tiles' reductions overlap the later tiles' MFMA chains.
+  constexpr int T0 = SWP == 2 ? PT - 1 : 0;   // first deferred tile
   f32x16 pacc[PT];
   int pcb = 0;
-  if constexpr (SWP) {
+  if constexpr (SWP != 0) {
 #pragma unroll
-    for (int t = 0; t < PT; ++t)
+    for (int t = T0; t < PT; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) pacc[t][r] = __int_as_float(0x7fffffff);
   }
   auto reduce_tile = [&](const f32x16& acc, int t, int cb) {
+    if constexpr (DIAG == 1) {
+      bkey[t] = min(bkey[t], __float_as_int(acc[0]));
+      return;
+    }
     int m = 0x7fffffff;
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {
@@ -645,21 +665,30 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       f32x16 cacc[PT];
 #pragma unroll
       for (int t = 0; t < PT; ++t) {
-        f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            __builtin_bit_cast(bf16x8, a[0]), __builtin_bit_cast(bf16x8, bf[t][0]), hc, 0, 0, 0);
+        f32x16 acc;
+        if constexpr (DIAG >= 2) {
+          uint32_t f = bf[t][0].x;
 #pragma unroll
-        for (int s = 1; s < KS; ++s)
+          for (int s = 0; s < KS; ++s) f ^= a[s].x ^ a[s].w;
+          acc = hc;
+          acc[0] = __int_as_float(__float_as_int(acc[0]) ^ (int)f);
+        } else {
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              __builtin_bit_cast(bf16x8, a[s]), __builtin_bit_cast(bf16x8, bf[t][s]), acc, 0, 0, 0);
-        if constexpr (SWP) cacc[t] = acc;
+              __builtin_bit_cast(bf16x8, a[0]), __builtin_bit_cast(bf16x8, bf[t][0]), hc, 0, 0, 0);
+#pragma unroll
+          for (int s = 1; s < KS; ++s)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                __builtin_bit_cast(bf16x8, a[s]), __builtin_bit_cast(bf16x8, bf[t][s]), acc, 0, 0, 0);
+        }
+        if (SWP != 0 && t >= T0) cacc[t] = acc;
         else reduce_tile(acc, t, cb);
       }
-      if constexpr (SWP) {
+      if constexpr (SWP != 0) {
         // argmin of the previous sub-tile: independent of the MFMAs above, same block
 #pragma unroll
-        for (int t = 0; t < PT; ++t) reduce_tile(pacc[t], t, pcb);
+        for (int t = T0; t < PT; ++t) reduce_tile(pacc[t], t, pcb);
 #pragma unroll
-        for (int t = 0; t < PT; ++t) pacc[t] = cacc[t];
+        for (int t = T0; t < PT; ++t) pacc[t] = cacc[t];
         pcb = cb;
         // pin the interleave: one MFMA, then a few argmin VALU ops, for every MFMA of
         // this sub-tile (hipcc otherwise clusters the MFMAs and sinks the VALU after them)
@@ -681,9 +710,9 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     }
     if (NBUF >= 3 && ch + NBUF - 1 < nchunk) issue(ch + NBUF - 1);
   }
-  if constexpr (SWP) {
+  if constexpr (SWP != 0) {
 #pragma unroll
-    for (int t = 0; t < PT; ++t) reduce_tile(pacc[t], t, pcb);
+    for (int t = T0; t < PT; ++t) reduce_tile(pacc[t], t, pcb);
   }
 
   // ---- decode, combine the two lane halves (same point, disjoint centre rows)
@@ -717,7 +746,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     if (tid == 0) {
       double tot = 0.0;
       for (int w = 0; w < NW; ++w) tot += s_sse[w];
-      atomicAdd(sse, tot);
+      atomicAdd(sse + (blockIdx.x & sse_mask), tot);
     }
   }
 }
@@ -1073,7 +1102,7 @@ using namespace dalgo;
 
 template <typename T, int DP, int NW, int NSUB, int PTB = 2, int MINW = 1>
 static hipError_t launch_assign_v(const void* X, int64_t n, int64_t ldx, const void* Cq,
-                                  const float* hn, int kpad, int* assign, float* mind, double* sse,
+                                  const float* hn, int kpad, int* assign, float* mind, double* sse, int sse_mask,
                                   hipStream_t st) {
   constexpr int PT = sizeof(T) == 2 ? PTB : 1;
   if (kpad % (32 * NSUB)) return hipErrorInvalidValue;
@@ -1083,7 +1112,7 @@ static hipError_t launch_assign_v(const void* X, int64_t n, int64_t ldx, const v
   if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
   hipLaunchKernelGGL((kmeans_assign_kernel<T, DP, PT, NW, NSUB, MINW>), dim3((unsigned)grid),
                      dim3(NW * 64), 0, st, (const T*)X, n, ldx, (const T*)Cq, hn, kpad, assign,
-                     mind, sse);
+                     mind, sse, sse_mask);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -1104,7 +1133,7 @@ static int device_cus() {
 // `dist` is required (it carries the running distance between passes)
 template <int DP, int NW, int PT>
 static hipError_t launch_assign_res(const void* X, int64_t n, int64_t ldx, const void* Cq,
-                                    const float* hn, int kpad, int* assign, float* dist, double* sse,
+                                    const float* hn, int kpad, int* assign, float* dist, double* sse, int sse_mask,
                                     hipStream_t st) {
   using G = ResGeom<DP>;
   if (dist == nullptr || kpad % 32) return hipErrorInvalidValue;
@@ -1117,17 +1146,17 @@ static hipError_t launch_assign_res(const void* X, int64_t n, int64_t ldx, const
     const int ncen = std::min(G::CB, kpad - c0);
     hipLaunchKernelGGL((kmeans_assign_res_kernel<DP, NW, PT>), dim3(grid), dim3(NW * 64), 0, st,
                        (const uint16_t*)X, n, ldx, (const uint16_t*)Cq, hn, c0, ncen, ps == 0 ? 1 : 0,
-                       ps == npass - 1 ? 1 : 0, assign, dist, sse);
+                       ps == npass - 1 ? 1 : 0, assign, dist, sse, sse_mask);
     DALGO_LAUNCH_CHECK();
   }
   return hipSuccess;
 }
 
 // pipelined K2 (bf16, DP >= 64): grid = one PT-tile group per wave, MINB blocks per CU
-template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, bool SWP = false>
+template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, int SWP = 0, int DIAG = 0>
 static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                      const float* hn, int kpad, int* assign, float* mind,
-                                     double* sse, hipStream_t st) {
+                                     double* sse, int sse_mask, hipStream_t st) {
   constexpr int CH = 32 * NSUB;
   constexpr size_t kStatic = NBUF * (size_t)CH * DP * 2;
   if (kpad % CH) return hipErrorInvalidValue;
@@ -1136,7 +1165,7 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
   const int64_t grid = cdiv(n, (int64_t)NW * PT * 32);
   if (grid == 0) return hipSuccess;
   if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
-  auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF, SWP>;
+  auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF, SWP, DIAG>;
   static size_t attr_set = 0;   // largest dynamic size this instantiation was enabled for
   if (dyn > attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1145,7 +1174,7 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
     attr_set = dyn;
   }
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(NW * 64), dyn, st, (const uint16_t*)X, n, ldx,
-                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse);
+                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse, sse_mask);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -1168,68 +1197,88 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
 //          while ch is consumed), 24 = 23 with SWP, 25 = 128-centre chunks double-
 //          buffered (64 MFMAs per barrier), 26 = 25 with SWP, 27 = 25 without A prefetch,
 //          28 / 29 = 8-wave blocks, 256- / 128-centre chunks double-buffered, SWP;
-//          30 = 28 without SWP. Measured and removed (profiles/round2/README.md): a
+//          30 = 28 without SWP, 48 / 49 / 50 = 3 point tiles per wave (96 points: each A
+//          fragment read from LDS feeds 3 MFMAs) without prefetch / with A prefetch / with
+//          SWP, 51 / 52 = 3 tiles with SWP = 2 (only the last tile's reduction deferred)
+//          without / with A prefetch (52: bf16 default), 53 = 26 with SWP = 2, 54 = 4
+//          tiles with SWP = 2 (spills), 40 / 41 / 42 / 43 = diagnostics of 26 (no argmin VALU /
+//          no MFMA / no MFMA + no C-init reads / no MFMA + no LDS fragment reads; wrong
+//          results). Measured and removed (profiles/round2/README.md): a
 //          persistent form looping blocks over point groups with next-group L2 prefetch
-//          (2-4 % slower than 26), s_setprio on alternate blocks (within 1 %)
+//          (2-4 % slower than 26), s_setprio on alternate blocks (within 1 %), a form
+//          with the centres resident in VGPRs and the points streamed through LDS
+//          (4.79-5.30 vs 4.42-4.56 ms: the extra norm k-step costs more than the saved
+//          LDS reads)
 template <typename T, int DP>
 static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const void* Cq,
-                                   const float* hn, int kpad, int* assign, float* mind, double* sse,
+                                   const float* hn, int kpad, int* assign, float* mind, double* sse, int sse_mask,
                                    int variant, hipStream_t st) {
   switch (variant) {
-    case 0: return launch_assign_v<T, DP, 8, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 1: return launch_assign_v<T, DP, 4, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 2: return launch_assign_v<T, DP, 4, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 3: return launch_assign_v<T, DP, 8, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 4: return launch_assign_v<T, DP, 4, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 5: return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 6: return launch_assign_v<T, DP, 4, 1, 4, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 7: return launch_assign_v<T, DP, 8, 1, 4, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 8: return launch_assign_v<T, DP, 4, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 9: return launch_assign_v<T, DP, 8, 2, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 10: return launch_assign_v<T, DP, 16, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+    case 0: return launch_assign_v<T, DP, 8, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 1: return launch_assign_v<T, DP, 4, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 2: return launch_assign_v<T, DP, 4, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 3: return launch_assign_v<T, DP, 8, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 4: return launch_assign_v<T, DP, 4, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 5: return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 6: return launch_assign_v<T, DP, 4, 1, 4, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 7: return launch_assign_v<T, DP, 8, 1, 4, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 8: return launch_assign_v<T, DP, 4, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 9: return launch_assign_v<T, DP, 8, 2, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 10: return launch_assign_v<T, DP, 16, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
     case 11: case 12: case 13:
       if constexpr (sizeof(T) == 2) {
-        if (variant == 11) return launch_assign_res<DP, 8, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 12) return launch_assign_res<DP, 4, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        return launch_assign_res<DP, 8, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 11) return launch_assign_res<DP, 8, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 12) return launch_assign_res<DP, 4, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        return launch_assign_res<DP, 8, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
       }
-      return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-    case 14: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23: case 24: case 25: case 26: case 27: case 28: case 29: case 30:
+      return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 14: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23: case 24: case 25: case 26: case 27: case 28: case 29: case 30: case 40: case 41: case 42: case 43: case 48: case 49: case 50: case 51: case 52: case 53: case 54:
       if constexpr (sizeof(T) == 2 && DP >= 64) {
         // one 8-wave block per CU: every centre chunk feeds 512 points (half the L2 -> LDS
         // centre traffic of two independent 4-wave blocks)
-        if (variant == 20) return launch_assign_pipe<DP, 8, 2, 2, 1, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 21) return launch_assign_pipe<DP, 8, 2, 4, 1, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 22) return launch_assign_pipe<DP, 8, 2, 2, 1, 3, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 23) return launch_assign_pipe<DP, 4, 2, 2, 2, 4, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 24) return launch_assign_pipe<DP, 4, 2, 2, 2, 4, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 25) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 26) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 27) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 28) return launch_assign_pipe<DP, 8, 2, 8, 1, 2, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 29) return launch_assign_pipe<DP, 8, 2, 4, 1, 2, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 30) return launch_assign_pipe<DP, 8, 2, 8, 1, 2, true, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 18) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 19) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, false, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 14) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 15) return launch_assign_pipe<DP, 4, 2, 2, 3, 3, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        if (variant == 16) return launch_assign_pipe<DP, 4, 1, 2, 4, 2, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
-        return launch_assign_pipe<DP, 4, 2, 2, 3, 2, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+        if (variant == 20) return launch_assign_pipe<DP, 8, 2, 2, 1, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 21) return launch_assign_pipe<DP, 8, 2, 4, 1, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 22) return launch_assign_pipe<DP, 8, 2, 2, 1, 3, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 23) return launch_assign_pipe<DP, 4, 2, 2, 2, 4, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 24) return launch_assign_pipe<DP, 4, 2, 2, 2, 4, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 25) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 26) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 27) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 28) return launch_assign_pipe<DP, 8, 2, 8, 1, 2, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 29) return launch_assign_pipe<DP, 8, 2, 4, 1, 2, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 30) return launch_assign_pipe<DP, 8, 2, 8, 1, 2, true, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 48) return launch_assign_pipe<DP, 4, 3, 4, 2, 2, false, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 49) return launch_assign_pipe<DP, 4, 3, 4, 2, 2, true, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 50) return launch_assign_pipe<DP, 4, 3, 4, 2, 2, false, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 51) return launch_assign_pipe<DP, 4, 3, 4, 2, 2, false, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 52) return launch_assign_pipe<DP, 4, 3, 4, 2, 2, true, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 53) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 54) return launch_assign_pipe<DP, 4, 4, 4, 2, 2, false, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 40) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, true, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 41) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, true, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 42) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, true, 3>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 43) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, true, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 18) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 19) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, false, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 14) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 15) return launch_assign_pipe<DP, 4, 2, 2, 3, 3, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        if (variant == 16) return launch_assign_pipe<DP, 4, 1, 2, 4, 2, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+        return launch_assign_pipe<DP, 4, 2, 2, 3, 2, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
       }
-      return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, st);
+      return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
     default: return hipErrorInvalidValue;
   }
 }
 
 template <typename T>
 static hipError_t launch_assign(int DP, const void* X, int64_t n, int64_t ldx, const void* Cq,
-                                const float* hn, int kpad, int* assign, float* mind, double* sse,
+                                const float* hn, int kpad, int* assign, float* mind, double* sse, int sse_mask,
                                 int variant, hipStream_t st) {
   switch (DP) {
-    case 16: return launch_assign_dp<T, 16>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, variant, st);
-    case 32: return launch_assign_dp<T, 32>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, variant, st);
-    case 64: return launch_assign_dp<T, 64>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, variant, st);
-    case 128: return launch_assign_dp<T, 128>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, variant, st);
+    case 16: return launch_assign_dp<T, 16>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st);
+    case 32: return launch_assign_dp<T, 32>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st);
+    case 64: return launch_assign_dp<T, 64>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st);
+    case 128: return launch_assign_dp<T, 128>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1333,10 +1382,10 @@ hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n,
 
 hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
                                const void* Cq, const float* hn, int kpad, int* assign, float* mind,
-                               double* sse, int variant, hipStream_t st) {
+                               double* sse, int sse_mask, int variant, hipStream_t st) {
   if (kpad % 32 != 0) return hipErrorInvalidValue;
-  return is_bf16 ? launch_assign<uint16_t>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, variant, st)
-                 : launch_assign<float>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, variant, st);
+  return is_bf16 ? launch_assign<uint16_t>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st)
+                 : launch_assign<float>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st);
 }
 
 hipError_t dalgo_kmeans_accumulate(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,

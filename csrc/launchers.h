@@ -68,7 +68,7 @@ hipError_t dalgo_mc_pi(uint64_t seed, uint64_t stream, uint64_t offset, uint64_t
 // ---- K2/K3 k-means (kmeans.hip)
 hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
                                const void* Cq, const float* hn, int kpad, int* assign, float* mind,
-                               double* sse, int variant, hipStream_t st);
+                               double* sse, int sse_mask, int variant, hipStream_t st);
 hipError_t dalgo_kmeans_accumulate(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
                                    const int* assign, int k, float* S, unsigned long long* cnt,
                                    hipStream_t st);

@@ -77,13 +77,14 @@ def refresh(cen: Centers):
 import os
 
 # launch variant of the assign kernel (table in csrc/kernels/kmeans.hip). -1 = per
-# dtype: f32 -> 5 (8-wave blocks capped at 128 VGPRs, two blocks per CU), bf16 -> 26
-# (pipelined distance-key form with 128-centre double-buffered chunks and the software-
-# pipelined argmin: 4.47-4.63 ms vs 4.73-5.11 ms for the round-1 default 14 at
-# 20M x 128 x 1024, profiles/round2/README.md; DP < 64 falls back to 5 in the launcher)
+# dtype: f32 -> 5 (8-wave blocks capped at 128 VGPRs, two blocks per CU), bf16 -> 52
+# (pipelined distance-key form: 128-centre double-buffered chunks, 3 point tiles per
+# wave, last-tile software-pipelined argmin: 4.20 ms vs 4.54 ms for 26 and 4.73-5.11 ms
+# for the round-1 default 14 at 20M x 128 x 1024, profiles/round2/README.md; DP < 64
+# falls back to 5 in the launcher)
 ASSIGN_VARIANT = int(os.environ.get("DALGO_KM_VARIANT", "-1"))
 RESIDENT_VARIANTS = (11, 12, 13)
-_BF16_DEFAULT = 26
+_BF16_DEFAULT = 52
 _scratch: dict = {}
 
 
@@ -92,6 +93,18 @@ def assign_variant(X: torch.Tensor, variant: int | None = None) -> int:
     if v < 0:
         v = _BF16_DEFAULT if X.dtype == torch.bfloat16 else 5
     return v
+
+
+def _sse_slots(device) -> torch.Tensor:
+    """Zeroed [256] f64 slots for the assign kernels' per-block SSE partials."""
+    key = ("sse", str(device))
+    t = _scratch.get(key)
+    if t is None:
+        t = torch.zeros(256, dtype=torch.float64, device=device)
+        _scratch[key] = t
+    else:
+        t.zero_()
+    return t
 
 
 def _dist_scratch(n: int, device) -> torch.Tensor:
@@ -116,7 +129,14 @@ def assign(X: torch.Tensor, cen: Centers, out: torch.Tensor | None = None,
         md = mind
         if md is None and v in RESIDENT_VARIANTS and X.dtype == torch.bfloat16:
             md = _dist_scratch(n, X.device)
-        _ext.ops().kmeans_assign(X, cen.Cq, cen.hn, out, md, sse, v)
+        if sse is not None and sse.numel() == 1:
+            # blocks spread their SSE partials over 256 slots (one f64 address hit by
+            # every block serialises ~2 ms of atomics at 100M points), summed here
+            slots = _sse_slots(X.device)
+            _ext.ops().kmeans_assign(X, cen.Cq, cen.hn, out, md, slots, v)
+            sse += slots.sum()
+        else:
+            _ext.ops().kmeans_assign(X, cen.Cq, cen.hn, out, md, sse, v)
         return out
     # CPU reference: exact scores on the ROUNDED centres, f64, first maximum wins
     Xf = X[:, : cen.d].double()

@@ -30,7 +30,8 @@ def test_kmeans_assign_resident(cuda, variant, d, k, n):
 
 # pipelined K2 (bf16, LDS-DMA triple-buffered centre chunks): DP = 64 / 128 (smaller DP
 # falls back to variant 5), ragged tile groups, one and many chunks
-@pytest.mark.parametrize("variant", [14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 29])
+@pytest.mark.parametrize("variant", [14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 29,
+                                     48, 49, 50, 51, 52, 53, 54])
 @pytest.mark.parametrize("d,k,n", [(2, 2, 6), (50, 33, 4099), (100, 1500, 9000),
                                    (128, 1024, 20000), (128, 600, 70001), (64, 128, 513)])
 def test_kmeans_assign_pipelined(cuda, variant, d, k, n):
@@ -51,7 +52,7 @@ def test_kmeans_pipelined_ties(cuda):
     for c in (3, 7, 12, 515, 1030):
         C0[c] = 0.0
         C0[c, c % 128] = 1.0
-    for v in (14, 15, 16, 17, 18, 20, 22, 23, 24, 25, 26, 27, 29):
+    for v in (14, 15, 16, 17, 18, 20, 22, 23, 24, 25, 26, 27, 29, 50, 51, 52, 53, 54):
         a = K.assign(K.prepare_points(X.to(cuda).bfloat16()), K.make_centers(C0, torch.bfloat16, cuda),
                      variant=v).cpu()
         assert a.tolist() == [3] * 300, v
