@@ -47,7 +47,7 @@ def main():
     dst = torch.randint(0, n, (e,), device=dev, generator=g)
     tc = DenseClosure(src, dst, n, device=dev)
     cntb = torch.zeros(1, dtype=torch.int64, device=dev)
-    for v in (0, 1):
+    for v in (0, 1, 2, 3):
         dt = timed(lambda: _ext.ops().tc_step(tc.A, tc.T, tc.T2, cntb, v), 3)
         out[f"closure_step_v{v}"] = {"n": n, "ms": dt * 1e3, "TOPs_int8": 2.0 * tc.npad ** 3 / dt / 1e12}
     # ALS half-sweep

@@ -41,29 +41,39 @@ __device__ __forceinline__ void wait_vmcnt() {
   else static_assert(N == 0, "unsupported vmcnt");
 }
 
-template <int BK>
-__global__ void __launch_bounds__(256)
+// TILE x TILE output tile per block: TILE = 128 -> 4 waves of 64 x 64 (2 x 2 MFMA tiles);
+// TILE = 256 -> 8 waves of 128 x 64 (4 x 2 MFMA tiles, 128 accumulator VGPRs): half the
+// operand bytes per MFMA (the 128 form is bound by L2 / Infinity-Fabric traffic: 38 GB
+// of L2 misses per n = 16384 step for 0.5 GB of unique data).
+template <int BK, int TILE>
+__global__ void __launch_bounds__(TILE == 256 ? 512 : 256)
 tc_step_i8_kernel(const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __restrict__ Told,
                   uint8_t* __restrict__ Tnew, int64_t ldt, int npad, int gx,
                   unsigned long long* __restrict__ count) {
-  constexpr int CPR = BK / 16;          // 16-B chunks per staged row
-  constexpr int RP = 256 / BK;          // rows covering the 64 banks once
-  constexpr int STAGE = 128 * BK;       // bytes per operand per stage
-  constexpr int PPT = STAGE / 16 / 256; // 16-B pieces per thread per operand
+  constexpr int NW = TILE == 256 ? 8 : 4;
+  constexpr int NT = NW * 64;
+  constexpr int WZ = NW / 2;               // waves along z (2 along x)
+  constexpr int MI = TILE / 2 / 32;        // MFMA tiles per wave along x
+  constexpr int MJ = TILE / WZ / 32;       // ... along z
+  constexpr int CPR = BK / 16;             // 16-B chunks per staged row
+  constexpr int RP = 256 / BK;             // rows covering the 64 banks once
+  constexpr int STAGE = TILE * BK;         // bytes per operand per stage
+  constexpr int PPT = STAGE / 16 / NT;     // 16-B pieces per thread per operand
+  static_assert(PPT * 16 * NT == STAGE, "whole DMA rounds per stage");
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 2 * STAGE];   // [buf][A | T]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, cl = lane & 31;
   const int wx = wid & 1, wz = wid >> 1;
-  // tile order: consecutive block ids walk down z inside a column strip of x
-  // tiles so co-resident blocks share their A rows in L2
+  // tile order: consecutive block ids walk down x inside a column strip of z tiles so
+  // co-resident blocks share their T rows in L2
   const int bid = blockIdx.x;
-  const int x0 = (bid % gx) * 128, z0 = (bid / gx) * 128;
+  const int x0 = (bid % gx) * TILE, z0 = (bid / gx) * TILE;
 
   const uint8_t* asrc[PPT];
   const uint8_t* tsrc[PPT];
 #pragma unroll
   for (int q = 0; q < PPT; ++q) {
-    const int p = q * 256 + tid, r = p / CPR, pc = p % CPR;
+    const int p = q * NT + tid, r = p / CPR, pc = p % CPR;
     const int c = pc ^ ((r / RP) & (CPR - 1));
     asrc[q] = A + (int64_t)(x0 + r) * lda + c * 16;
     tsrc[q] = Told + (int64_t)(z0 + r) * ldt + c * 16;
@@ -72,16 +82,16 @@ tc_step_i8_kernel(const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __r
     uint8_t* base = smem + buf * 2 * STAGE;
 #pragma unroll
     for (int q = 0; q < PPT; ++q) {
-      __builtin_amdgcn_global_load_lds((const void*)(asrc[q] + y0), (lds_void*)(base + (q * 256 + wid * 64) * 16), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(tsrc[q] + y0), (lds_void*)(base + STAGE + (q * 256 + wid * 64) * 16), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[q] + y0), (lds_void*)(base + (q * NT + wid * 64) * 16), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(tsrc[q] + y0), (lds_void*)(base + STAGE + (q * NT + wid * 64) * 16), 16, 0, 0);
     }
   };
 
-  i32x16_t acc[2][2];
+  i32x16_t acc[MI][MJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = i32x16_t{};
+    for (int j = 0; j < MJ; ++j) acc[i][j] = i32x16_t{};
 
   const int nst = npad / BK;
   issue(0, 0);
@@ -100,23 +110,23 @@ tc_step_i8_kernel(const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __r
     const uint8_t* stt = sa + STAGE;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
-      i32x4_t a[2], b[2];
+      i32x4_t a[MI], b[MJ];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r = wx * 64 + i * 32 + cl;
+      for (int i = 0; i < MI; ++i) {
+        const int r = wx * (TILE / 2) + i * 32 + cl;
         const int pc = (2 * ks + h) ^ ((r / RP) & (CPR - 1));
         a[i] = *reinterpret_cast<const i32x4_t*>(sa + r * BK + pc * 16);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = wz * 64 + j * 32 + cl;
+      for (int j = 0; j < MJ; ++j) {
+        const int r = wz * (TILE / WZ) + j * 32 + cl;
         const int pc = (2 * ks + h) ^ ((r / RP) & (CPR - 1));
         b[j] = *reinterpret_cast<const i32x4_t*>(stt + r * BK + pc * 16);
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < MJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -127,13 +137,13 @@ tc_step_i8_kernel(const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __r
   // epilogue: T_new[z][x..x+3] = T_old | (C > 0)
   uint32_t ones = 0;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int z = z0 + wz * 64 + j * 32 + cl;
+    for (int j = 0; j < MJ; ++j) {
+      const int z = z0 + wz * (TILE / WZ) + j * 32 + cl;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int x = x0 + wx * 64 + i * 32 + 8 * g + 4 * h;
+        const int x = x0 + wx * (TILE / 2) + i * 32 + 8 * g + 4 * h;
         const uint32_t old = *reinterpret_cast<const uint32_t*>(Told + (int64_t)z * ldt + x);
         uint32_t nv = 0;
 #pragma unroll
@@ -149,11 +159,11 @@ tc_step_i8_kernel(const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __r
   if (lane == 0 && ones) atomicAdd(count, (unsigned long long)ones);
 }
 
-template <int BK>
+template <int BK, int TILE>
 void launch_tc_step(const void* A, int64_t lda, const void* Told, void* Tnew, int64_t ldt, int npad,
                     int gx, int gz, unsigned long long* count, hipStream_t st) {
-  hipLaunchKernelGGL((tc_step_i8_kernel<BK>), dim3(gx * gz), dim3(256), 0, st, (const uint8_t*)A, lda,
-                     (const uint8_t*)Told, (uint8_t*)Tnew, ldt, npad, gx, count);
+  hipLaunchKernelGGL((tc_step_i8_kernel<BK, TILE>), dim3(gx * gz), dim3(TILE == 256 ? 512 : 256), 0, st,
+                     (const uint8_t*)A, lda, (const uint8_t*)Told, (uint8_t*)Tnew, ldt, npad, gx, count);
 }
 
 }  // namespace dalgo
@@ -163,14 +173,23 @@ using namespace dalgo;
 extern "C" {
 
 // A: [npad, lda] uint8 0/1, T_old/T_new: [nz, ldt] uint8 0/1; npad, nz multiples
-// of 128, lda/ldt >= npad and multiples of 16. variant 0: BK = 64, 1: BK = 128.
+// of 128, lda/ldt >= npad and multiples of 16. variant 0: 128-tiles BK = 64, 1: 128-tiles
+// BK = 128, 2: 256-tiles BK = 64, 3: 256-tiles BK = 128 (2 / 3 need npad and nz multiples
+// of 256 and fall back to 0 otherwise).
 hipError_t dalgo_tc_step(const void* A, int64_t lda, const void* Told, void* Tnew, int64_t ldt,
                          int npad, int nz, int variant, unsigned long long* count, hipStream_t st) {
   if (npad % 128 || nz % 128 || lda % 16 || ldt % 16) return hipErrorInvalidValue;
+  if (npad == 0 || nz == 0) return hipSuccess;
+  if ((variant == 2 || variant == 3) && npad % 256 == 0 && nz % 256 == 0) {
+    const int gx = npad / 256, gz = nz / 256;
+    if (variant == 3) launch_tc_step<128, 256>(A, lda, Told, Tnew, ldt, npad, gx, gz, count, st);
+    else launch_tc_step<64, 256>(A, lda, Told, Tnew, ldt, npad, gx, gz, count, st);
+    DALGO_LAUNCH_CHECK();
+    return hipSuccess;
+  }
   const int gx = npad / 128, gz = nz / 128;
-  if (gx == 0 || gz == 0) return hipSuccess;
-  if (variant == 1) launch_tc_step<128>(A, lda, Told, Tnew, ldt, npad, gx, gz, count, st);
-  else launch_tc_step<64>(A, lda, Told, Tnew, ldt, npad, gx, gz, count, st);
+  if (variant == 1) launch_tc_step<128, 128>(A, lda, Told, Tnew, ldt, npad, gx, gz, count, st);
+  else launch_tc_step<64, 128>(A, lda, Told, Tnew, ldt, npad, gx, gz, count, st);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -290,12 +290,13 @@ def test_transitive_closure_gpu(cuda):
     assert DenseClosure(s4, d4, 3, device=cuda).run().counts == [4, 8, 9, 9]
 
 
-@pytest.mark.parametrize("variant", [0, 1])
-def test_tc_step_kernel_exact(cuda, variant):
-    """One K9 step (both K-staging depths) == (T | (T A^T > 0)) computed in f32 on the CPU."""
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("n,nz", [(640, 384), (768, 512)])
+def test_tc_step_kernel_exact(cuda, variant, n, nz):
+    """One K9 step (128 / 256 tiles x both K-staging depths; 256 tiles fall back to 128 when
+    the sizes are not multiples of 256) == (T | (T A^T > 0)) computed in f32 on the CPU."""
     from dalgo.ops import _ext
     g = torch.Generator().manual_seed(3)
-    n, nz = 640, 384
     A = (torch.rand(n, n, generator=g) < 0.01).to(torch.uint8)
     T = (torch.rand(nz, n, generator=g) < 0.05).to(torch.uint8)
     ref = ((T != 0) | ((T.float() @ A.float().T) > 0.5)).to(torch.uint8)
