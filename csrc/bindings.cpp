@@ -695,6 +695,41 @@ void spd_inverse(const Tensor& G, double ridge, Tensor out, const std::optional<
                   "spd_inverse");
 }
 
+// out = (R . F) . Ginv for all rows of R at once (K5 half-sweep). Workspaces (the
+// packed F^T fragments and the K-split partials) come from the torch caching allocator
+// on the current stream.
+void als_solve(const Tensor& R, const Tensor& F, const Tensor& Ginv, Tensor out) {
+  check_dev(R, "R");
+  TORCH_CHECK(R.scalar_type() == at::kFloat && R.dim() == 2 && R.stride(1) == 1,
+              "als_solve: R must be 2-D float32 with contiguous rows");
+  TORCH_CHECK(R.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(R.data_ptr()) % 16 == 0,
+              "als_solve: R rows must be 16-B aligned (row stride a multiple of 4)");
+  check_dev(F, "F");
+  TORCH_CHECK(F.scalar_type() == at::kFloat && F.dim() == 2 && F.stride(1) == 1,
+              "als_solve: F must be 2-D float32 with contiguous rows");
+  check_f32(Ginv, "Ginv");
+  check_f32(out, "out");
+  const int64_t m = R.size(0), n = R.size(1), k = F.size(1);
+  TORCH_CHECK(F.size(0) == n, "als_solve: F must have R.size(1) rows");
+  TORCH_CHECK(k >= 1 && k <= 128, "als_solve: k <= 128");
+  TORCH_CHECK(Ginv.dim() == 2 && Ginv.size(0) == k && Ginv.size(1) == k, "als_solve: Ginv k x k");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == m && out.size(1) == k, "als_solve: out m x k");
+  TORCH_CHECK(m >= 1 && n >= 1, "als_solve: empty R");
+  TORCH_CHECK(R.device() == F.device() && R.device() == Ginv.device() && R.device() == out.device(),
+              "als_solve: operands on different devices");
+  DeviceGuard guard(R.device());
+  const int nsplit = dalgo_als_nsplit(m, n, (int)k);
+  const int64_t kpad = dalgo_als_kpad((int)k);
+  auto opts = R.options();
+  Tensor Fq = at::empty({dalgo_als_fq_bytes(n, (int)k) / 4}, opts);
+  Tensor P = at::empty({(int64_t)nsplit * m * kpad}, opts);
+  DALGO_CHECK_HIP(dalgo_als_solve(R.data_ptr<float>(), m, n, R.stride(0), F.data_ptr<float>(),
+                                  F.stride(0), (int)k, Ginv.data_ptr<float>(), (int)Ginv.stride(0),
+                                  out.data_ptr<float>(), out.stride(0), Fq.data_ptr(),
+                                  P.data_ptr<float>(), nsplit, cur_stream()),
+                  "als_solve");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dalgo, m) {
@@ -745,6 +780,7 @@ TORCH_LIBRARY(dalgo, m) {
         "float lam=0., float reg_alpha=0., int count_index=-1, Tensor(d!)? count_acc=None) -> ()");
   m.def("tc_step(Tensor A, Tensor Told, Tensor(a!) Tnew, Tensor(b!) count, int variant=0) -> ()");
   m.def("spd_inverse(Tensor G, float ridge, Tensor(a!) out, Tensor(b!)? status) -> ()");
+  m.def("als_solve(Tensor R, Tensor F, Tensor Ginv, Tensor(a!) out) -> ()");
   m.def("hbm_read(Tensor src, Tensor(a!) out, int unroll=8) -> ()");
   m.def("lr_set_trace(Tensor? buf) -> ()", &lr_set_trace);
   m.def("hbm_gather_rows(Tensor X, Tensor idx, Tensor(a!) out, int grid=2048) -> ()");
@@ -762,6 +798,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("hbm_read", &hbm_read);
   m.impl("hbm_gather_rows", &hbm_gather_rows);
   m.impl("spd_inverse", &spd_inverse);
+  m.impl("als_solve", &als_solve);
   m.impl("tc_step", &tc_step);
   m.impl("xgmi_allreduce", &xgmi_allreduce);
   m.impl("rmat_edges", &rmat_edges);

@@ -102,6 +102,12 @@ hipError_t dalgo_tc_step(const void* A, int64_t lda, const void* Told, void* Tne
 // ---- K5 ALS ridge SPD inverse (als.hip)
 hipError_t dalgo_spd_inverse(const float* G, int k, int ldg, float ridge, float* out, int ldo,
                              int* status, hipStream_t st);
+int64_t dalgo_als_fq_bytes(int64_t n, int k);
+int dalgo_als_nsplit(int64_t m, int64_t n, int k);
+int dalgo_als_kpad(int k);
+hipError_t dalgo_als_solve(const float* R, int64_t m, int64_t n, int64_t ldr, const float* F,
+                           int64_t ldf, int k, const float* Ginv, int ldg, float* out, int64_t ldo,
+                           void* Fq, float* P, int nsplit, hipStream_t st);
 
 // ---- K11 one-shot xGMI all-reduce (xgmi_allreduce.hip)
 size_t dalgo_xgmi_buffer_bytes(int slot_floats);

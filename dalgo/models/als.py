@@ -10,7 +10,8 @@ Row-partitioned model parallelism: rank r owns rows [m_lo, m_hi) of U with the
 matching R rows, and rows [n_lo, n_hi) of V with the matching R columns. A
 half-sweep is: Gram G = F^T F of the replicated other factor (one GEMM),
 K5 ridge SPD inverse (csrc/kernels/als.hip, f64 in LDS, once — not per row),
-local rows = (R_rows F) G^-1 (one GEMM), all_gather of the factor rows. The
+local rows = (R_rows F) G^-1 (K5 als_solve: one pass over R_rows on the bf16 MFMA with
+a hi/lo split, G^-1 applied in the epilogue), all_gather of the factor rows. The
 RMSE uses ||R - UV^T||^2 = ||R||^2 - 2<U, RV> + <U^T U, V^T V> so U V^T is never
 materialised (f64 partial sums, one scalar all-reduce).
 """
@@ -36,6 +37,26 @@ class ALSConfig:
     n_iterations: int = 5   # (:16)
     n_workers: int = 4      # n_slices (:17)
     seed: int = 7
+
+
+def rows_solve(R: torch.Tensor, F: torch.Tensor, Ginv: torch.Tensor) -> torch.Tensor:
+    """(R F) Ginv for every row of R at once: K5 on the GPU (csrc/kernels/als.hip:
+    R streamed once through a 3-product bf16 split MFMA GEMM, K-split partials reduced
+    and multiplied by Ginv in the epilogue); torch GEMMs on the CPU."""
+    if not R.is_cuda:
+        return (R @ F) @ Ginv
+    if R.stride(1) != 1 or R.stride(0) % 4 or R.data_ptr() % 16:
+        R = _aligned_rows(R)
+    out = torch.empty((R.shape[0], F.shape[1]), dtype=torch.float32, device=R.device)
+    _ext.ops().als_solve(R, F.contiguous(), Ginv.contiguous(), out)
+    return out
+
+
+def _aligned_rows(R: torch.Tensor) -> torch.Tensor:
+    ld = (R.shape[1] + 3) // 4 * 4
+    buf = torch.zeros((R.shape[0], ld), dtype=R.dtype, device=R.device)
+    buf[:, : R.shape[1]] = R
+    return buf[:, : R.shape[1]]
 
 
 def spd_inverse(G: torch.Tensor, ridge: float) -> torch.Tensor:
@@ -93,7 +114,7 @@ class ALS:
     def _half(self, R_local: torch.Tensor, F: torch.Tensor, x_dim: int) -> torch.Tensor:
         G = F.T @ F                                         # Gram, once per half-sweep
         Ginv = spd_inverse(G.contiguous(), self.cfg.lam * x_dim)
-        return (R_local @ F) @ Ginv                         # all local rows at once
+        return rows_solve(R_local, F, Ginv)                 # all local rows at once (K5)
 
     def step(self):
         c = self.cfg

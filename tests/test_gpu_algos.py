@@ -318,6 +318,32 @@ def test_spd_inverse_gpu(cuda):
         assert torch.allclose(inv, ref, rtol=1e-4, atol=1e-6)
 
 
+# K5 als_solve: (R F) Ginv against f64, every launch variant (16x16x32 and 32x32x16 forms),
+# k across 1..8 factor-column tiles, n not a multiple of 16 (tail K-step), rows not a multiple of
+# the block, a strided (non-contiguous rows) R, a K-split count > 1
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("m,n,k", [(100, 500, 10), (1000, 777, 64), (3000, 4096, 33),
+                                   (600, 1000, 128), (513, 100, 96), (7, 5, 1), (20000, 3001, 64)])
+def test_als_solve_gpu(cuda, monkeypatch, variant, m, n, k):
+    from dalgo.models.als import rows_solve
+    monkeypatch.setenv("DALGO_ALS_VARIANT", str(variant))
+    g = torch.Generator().manual_seed(m * 7 + n + k)
+    R = torch.rand(m, n, generator=g, dtype=torch.float64) * 16
+    F = torch.rand(n, k, generator=g, dtype=torch.float64) - 0.3
+    Gi = torch.rand(k, k, generator=g, dtype=torch.float64) - 0.5
+    ref = (R @ F) @ Gi
+    out = rows_solve(R.float().to(cuda), F.float().to(cuda), Gi.float().to(cuda)).cpu().double()
+    # f32 rounding of the inputs + 2^-16 split residual, relative to sum |R||F||Gi|
+    scale = (R.abs() @ F.abs()) @ Gi.abs()
+    err = ((out - ref).abs() / scale).max().item()
+    assert err < 2e-5, err
+    if m > 64:   # strided rows (ld = n + 3 -> realigned copy inside rows_solve)
+        Rs = torch.zeros(m, n + 3, dtype=torch.float32, device=cuda)[:, :n]
+        Rs.copy_(R.float().to(cuda))
+        out2 = rows_solve(Rs, F.float().to(cuda), Gi.float().to(cuda)).cpu().double()
+        assert ((out2 - ref).abs() / scale).max().item() < 2e-5
+
+
 def test_als_gpu(cuda):
     from dalgo.models.als import ALS, ALSConfig
     hc = ALS(ALSConfig(seed=3)).fit().rmse
