@@ -321,7 +321,7 @@ def test_spd_inverse_gpu(cuda):
 # K5 als_solve: (R F) Ginv against f64, every launch variant (16x16x32 and 32x32x16 forms),
 # k across 1..8 factor-column tiles, n not a multiple of 16 (tail K-step), rows not a multiple of
 # the block, a strided (non-contiguous rows) R, a K-split count > 1
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("m,n,k", [(100, 500, 10), (1000, 777, 64), (3000, 4096, 33),
                                    (600, 1000, 128), (513, 100, 96), (7, 5, 1), (20000, 3001, 64)])
 def test_als_solve_gpu(cuda, monkeypatch, variant, m, n, k):
