@@ -120,3 +120,90 @@ def test_device_error_check_raises_on_every_rank():
     """a peer-wait timeout on ONE rank raises on EVERY rank (collective MAX
     first), so no rank is left blocked in a later collective."""
     assert run_world(_error_check_body, world=2) == [True, True]
+
+
+def test_other_algorithms_three_ranks_equal_one():
+    """Odd world size: uneven vertex / row / factor slices (3000 points, 1024-vertex
+    slices of a 6000-vertex graph, 40 / 60 ALS rows over 3 ranks)."""
+    one = run_world(_others, world=1)[0]
+    three = run_world(_others, world=3)
+    for r in range(3):
+        assert np.allclose(three[r]["kmeans"], one["kmeans"], atol=1e-4), r
+        assert three[r]["tc_dense"] == one["tc_dense"] == three[r]["tc_sparse"]
+        assert three[r]["mc"] == three[0]["mc"]
+    assert np.allclose(three[0]["kmeans_sse"], one["kmeans_sse"], rtol=1e-6)
+    for sem in ("pr_reference", "pr_standard"):
+        a, b = one[sem], three[0][sem]
+        assert set(a) == set(b)
+        assert max(abs(a[v] - b[v]) for v in a) < 1e-12
+        assert b == three[1][sem] == three[2][sem]
+    assert np.allclose(one["als"], three[0]["als"], rtol=1e-9)
+
+
+def _lr_four(rt):
+    return _lr_family(rt)
+
+
+def test_lr_family_four_ranks_equal_one(lr_results):
+    """One logical worker (Spark partition) per rank: P = W = 4."""
+    one, _ = lr_results
+    four = run_world(_lr_four, world=4)
+    for algo in ("ssgd", "gd", "ma", "bmuf", "easgd"):
+        ref = one[algo]
+        for r in range(4):
+            assert np.allclose(four[r][algo], ref, rtol=1e-10,
+                               atol=1e-8 * max(1, np.abs(ref).max())), (algo, r)
+
+
+def _comm_body(rt):
+    import torch
+
+    from dalgo.parallel import comm
+    W, r = rt.world_size, rt.rank
+    out = {}
+    x = torch.arange(5, dtype=torch.float64) * (r + 1)
+    comm.all_reduce_sum(x)
+    out["sum"] = x.tolist()
+    m = torch.tensor([float(r * 7 % 5)], dtype=torch.float64)
+    comm.all_reduce_max(m)
+    out["max"] = float(m.item())
+    out["count"] = comm.all_reduce_count(r + 2)
+    b = torch.full((3,), float(r), dtype=torch.float64)
+    comm.broadcast(b, src=W - 1)
+    out["bcast"] = b.tolist()
+    full = torch.empty(2 * W, dtype=torch.float64)
+    comm.all_gather_into(full, torch.tensor([r, 10 * r], dtype=torch.float64))
+    out["gather"] = full.tolist()
+    counts = [i + 1 for i in range(W)]                       # uneven: 1, 2, 3 rows
+    loc = torch.full((counts[r], 2), float(r), dtype=torch.float64)
+    out["varlen"] = comm.all_gather_varlen(loc, counts).tolist()
+    rs = torch.empty(2, dtype=torch.float64)
+    comm.reduce_scatter_sum(rs, torch.arange(2 * W, dtype=torch.float64) + r)
+    out["rs"] = rs.tolist()
+    g0 = comm.gather_to_rank0(torch.full((counts[r],), float(r), dtype=torch.float64), counts)
+    out["g0"] = None if g0 is None else g0.tolist()
+    bk = comm.BucketedAllReduce([(2, 3), (1,)], dtype=torch.float64, device=torch.device("cpu"))
+    a, c = bk.views
+    a.fill_(float(r))
+    c.fill_(1.0)
+    bk.all_reduce()
+    out["bucket"] = (a.tolist(), c.tolist())
+    return out
+
+
+def test_comm_primitives_three_ranks():
+    W = 3
+    res = run_world(_comm_body, world=W)
+    for r, o in enumerate(res):
+        assert o["sum"] == [i * 6.0 for i in range(5)]
+        assert o["max"] == 4.0                                # 0, 7 % 5 = 2, 14 % 5 = 4
+        assert o["count"] == 2 + 3 + 4
+        assert o["bcast"] == [2.0, 2.0, 2.0]
+        assert o["gather"] == [0.0, 0.0, 1.0, 10.0, 2.0, 20.0]
+        assert o["varlen"] == [[0.0, 0.0]] + [[1.0, 1.0]] * 2 + [[2.0, 2.0]] * 3
+        assert o["rs"] == [float(3 * (2 * r) + 3), float(3 * (2 * r + 1) + 3)]
+        assert o["bucket"] == ([[3.0] * 3] * 2, [3.0])
+        if r == 0:
+            assert o["g0"] == [0.0, 1.0, 1.0, 2.0, 2.0, 2.0]
+        else:
+            assert o["g0"] is None
