@@ -108,26 +108,34 @@ tc_step_i8_kernel(const uint8_t* __restrict__ A, int64_t lda, const uint8_t* __r
     asm volatile("" ::: "memory");
     const uint8_t* sa = smem + cur * 2 * STAGE;
     const uint8_t* stt = sa + STAGE;
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      i32x4_t a[MI], b[MJ];
+    // fragments of k-step ks+1 are read while the MFMAs of ks run (register double buffer)
+    i32x4_t a[2][MI], b[2][MJ];
+    auto frags = [&](int ks, i32x4_t (&aa)[MI], i32x4_t (&bb)[MJ]) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int r = wx * (TILE / 2) + i * 32 + cl;
         const int pc = (2 * ks + h) ^ ((r / RP) & (CPR - 1));
-        a[i] = *reinterpret_cast<const i32x4_t*>(sa + r * BK + pc * 16);
+        aa[i] = *reinterpret_cast<const i32x4_t*>(sa + r * BK + pc * 16);
       }
 #pragma unroll
       for (int j = 0; j < MJ; ++j) {
         const int r = wz * (TILE / WZ) + j * 32 + cl;
         const int pc = (2 * ks + h) ^ ((r / RP) & (CPR - 1));
-        b[j] = *reinterpret_cast<const i32x4_t*>(stt + r * BK + pc * 16);
+        bb[j] = *reinterpret_cast<const i32x4_t*>(stt + r * BK + pc * 16);
       }
+    };
+    frags(0, a[0], b[0]);
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      if (ks + 1 < BK / 32) frags(ks + 1, a[(ks + 1) & 1], b[(ks + 1) & 1]);
+      // keep the reads of ks+1 ahead of the MFMAs of ks (hipcc otherwise sinks them to
+      // their use and re-uses one register set: a full LDS latency per k-step)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < MJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1][i], b[ks & 1][j], acc[i][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();     // all reads of `cur` done before it is refilled
@@ -175,7 +183,7 @@ extern "C" {
 // A: [npad, lda] uint8 0/1, T_old/T_new: [nz, ldt] uint8 0/1; npad, nz multiples
 // of 128, lda/ldt >= npad and multiples of 16. variant 0: 128-tiles BK = 64, 1: 128-tiles
 // BK = 128, 2: 256-tiles BK = 64, 3: 256-tiles BK = 128 (2 / 3 need npad and nz multiples
-// of 256 and fall back to 0 otherwise).
+// of 256 and fall back to 1 otherwise).
 hipError_t dalgo_tc_step(const void* A, int64_t lda, const void* Told, void* Tnew, int64_t ldt,
                          int npad, int nz, int variant, unsigned long long* count, hipStream_t st) {
   if (npad % 128 || nz % 128 || lda % 16 || ldt % 16) return hipErrorInvalidValue;
@@ -188,7 +196,8 @@ hipError_t dalgo_tc_step(const void* A, int64_t lda, const void* Told, void* Tne
     return hipSuccess;
   }
   const int gx = npad / 128, gz = nz / 128;
-  if (variant == 1) launch_tc_step<128, 128>(A, lda, Told, Tnew, ldt, npad, gx, gz, count, st);
+  if (variant == 1 || variant == 2 || variant == 3)
+    launch_tc_step<128, 128>(A, lda, Told, Tnew, ldt, npad, gx, gz, count, st);
   else launch_tc_step<64, 128>(A, lda, Told, Tnew, ldt, npad, gx, gz, count, st);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;

@@ -37,8 +37,11 @@ def compact_ids(src: torch.Tensor, dst: torch.Tensor):
     return inv[:n], inv[n:], ids
 
 
-# K-staging depth of K9: 0 = 64 B, 1 = 128 B per stage (1.52 vs 1.76 POP/s int8 at n = 16384)
-TC_VARIANT = int(os.environ.get("DALGO_TC_VARIANT", "1"))
+# K9 launch variant (csrc/kernels/closure.hip): 0 / 1 = 128 x 128 tiles with 64 / 128-B K
+# stages, 2 / 3 = 256 x 256 tiles (8 waves, half the operand bytes per MFMA) with 64 / 128-B
+# stages. n = 16384, 1 x MI355X: 1.51 / 1.73 / 2.14 / 2.33 POP/s int8 (torch._int_mm, the
+# plain library GEMM of the same shape without the OR epilogue: 2.86 POP/s)
+TC_VARIANT = int(os.environ.get("DALGO_TC_VARIANT", "3"))
 
 
 def _round_up(a, b):
@@ -51,8 +54,10 @@ class DenseClosure:
         dev = torch.device(device)
         self.dev = dev
         self.n = n
-        self.npad = _round_up(max(n, 1), 128)   # 128 x 128 LDS-tiled K9 blocks
-        sl = _round_up((self.npad + world - 1) // world, 128)
+        # 256 x 256 K9 tiles once the graph is big enough to fill them, 128 x 128 below
+        al = 256 if n > 128 else 128
+        self.npad = _round_up(max(n, 1), al)
+        sl = _round_up((self.npad + world - 1) // world, al)
         self.z_lo = min(self.npad, rank * sl)
         self.z_hi = min(self.npad, (rank + 1) * sl)
         self.nz = sl
