@@ -121,3 +121,18 @@ def test_bench_cpu_contract():
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in d
     assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0
+
+
+def test_module_dispatcher():
+    """python -m dalgo <algorithm>: every reference script is reachable by name."""
+    out = _run(["-m", "dalgo", "list"])
+    for name in ("ssgd", "ma", "bmuf", "easgd", "logistic_regression", "kmeans", "pagerank",
+                 "transitive_closure", "als", "monte_carlo"):
+        assert name in out
+    out = _run(["-m", "dalgo", "pagerank", "--device", "cpu", "--no-plot"])
+    assert "1 has rank: 0.38891305880091237." in out
+    out = _run(["-m", "dalgo", "closure", "--device", "cpu"])
+    assert "The original graph has 9 paths" in out
+    r = subprocess.run([sys.executable, "-m", "dalgo", "nope"], cwd=ROOT, capture_output=True,
+                       text=True, env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 2
