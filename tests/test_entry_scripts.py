@@ -136,3 +136,25 @@ def test_module_dispatcher():
     r = subprocess.run([sys.executable, "-m", "dalgo", "nope"], cwd=ROOT, capture_output=True,
                        text=True, env=dict(os.environ, PYTHONPATH=ROOT))
     assert r.returncode == 2
+
+
+def _top_ranks(out):
+    res = {}
+    for line in out.splitlines():
+        if " has rank: " in line:
+            v, r = line.split(" has rank: ")
+            res[int(v)] = float(r.rstrip("."))
+    return res
+
+
+def test_pagerank_rmat_world_size_invariant():
+    """R-MAT PageRank with the degree relabeling (dealt over the W slices): 1 rank and 3
+    gloo ranks report the same top vertices (generator ids) and ranks."""
+    args = ["graph_computation/pagerank.py", "--device", "cpu", "--rmat-scale", "10",
+            "--top", "10"]
+    one = _top_ranks(_run(args))
+    three = _top_ranks(_run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+                             "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+                            + ["--backend", "gloo"], timeout=400))
+    assert len(one) == 10 and set(one) == set(three)
+    assert max(abs(one[v] - three[v]) for v in one) < 1e-12
