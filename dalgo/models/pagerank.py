@@ -1,9 +1,14 @@
 """Distributed PageRank (graph_computation/pagerank.py).
 
 Destination-partitioned pull formulation: rank r owns vertex slice r and its
-in-edges; per iteration ONE collective — all_gather of the contribution slices
-c[u] = r[u]/outdeg(u) (half the bytes of an all-reduce of a full vector) —
-then the K4 segmented SpMV and the fused rank/contribution epilogue.
+in-edges; per iteration ONE collective exchange of contributions c[u] = r[u]/outdeg(u),
+then the K4 segmented SpMV and the fused rank/contribution epilogue. The exchange is
+either an all_gather of the full slices (half the bytes of an all-reduce of a full
+vector) or, by default on several ranks, a ghost exchange: each rank receives only the
+c[u] of the remote sources that actually have an edge into its slice (one uneven
+all_to_all; on R-MAT scale 20 with W = 8 that is 25 % of the remote vertices), and its
+edge list is relabeled once into the compact [own slice | ghosts] index space, which
+also shrinks the gather footprint of the SpMV.
 
 semantics="reference" reproduces the join/reduceByKey formulation bit-for-bit
 in structure: N = #vertices with out-edges (pagerank.py:44),
@@ -32,6 +37,8 @@ class PageRankConfig:
     bin_width: int = 16384       # blocked: destination vertices per LDS bin
     chunk: int = 1 << 18         # blocked: max edge slots per workgroup
     tile: int = 1 << 16          # blocked: phase-1 edges per slot-sorted tile
+    exchange: str = ""           # "ghost" | "allgather" ("" = DALGO_PR_EXCHANGE env, default
+                                 # ghost on several ranks with the pull SpMV)
 
 
 class PageRank:
@@ -63,8 +70,17 @@ class PageRank:
         self.acc = torch.zeros(nl, dtype=fdt, device=dev)
         self.pres = torch.zeros(nl, dtype=torch.int32, device=dev)
         self.r = torch.zeros(nl, dtype=fdt, device=dev)
-        self.c_slice = torch.zeros(sl, dtype=fdt, device=dev)   # padded slice
-        self.c_full = torch.zeros(sl * world, dtype=fdt, device=dev)
+        ex = cfg.exchange or os.environ.get("DALGO_PR_EXCHANGE", "ghost")
+        self.exchange = ex if (world > 1 and self.layout is None) else "allgather"
+        if self.exchange == "ghost":
+            self._build_ghosts()
+            # own slice first, then the ghosts: c_slice is a view, so the update kernel's
+            # writes are already in place for the SpMV
+            self.c_full = torch.zeros(sl + self.n_ghost, dtype=fdt, device=dev)
+            self.c_slice = self.c_full[:sl]
+        else:
+            self.c_slice = torch.zeros(sl, dtype=fdt, device=dev)   # padded slice
+            self.c_full = torch.zeros(sl * world, dtype=fdt, device=dev)
         self.dang = torch.zeros(1, dtype=fdt, device=dev)
         self.dang_next = torch.zeros(1, dtype=fdt, device=dev)
         od = self.outdeg.to(fdt)
@@ -81,12 +97,54 @@ class PageRank:
             comm.all_reduce_sum(self.dang)
         self.t = 0
 
+    def _build_ghosts(self):
+        """Relabel this rank's edge sources into [own slice (sl) | ghosts] and agree, with
+        one exchange of request lists, which own c values every peer needs."""
+        g, W, sl = self.g, self.world, self.g.slice_size
+        rank = g.v_lo // sl if sl else 0
+        E = g.n_edges
+        src = g.src[:E].to(torch.int64)
+        owner = src // sl
+        remote = owner != rank
+        ghosts = torch.unique(src[remote])                     # sorted: grouped by owner
+        self.n_ghost = int(ghosts.numel())
+        recv_counts = torch.bincount(ghosts // sl, minlength=W).to(torch.int64)
+        local = torch.where(remote, sl + torch.searchsorted(ghosts, src), src - g.v_lo)
+        src_local = torch.full_like(g.src, -1)
+        src_local[:E] = local.to(torch.int32)
+        if E:
+            assert int(local.max()) < sl + self.n_ghost and int(local.min()) >= 0
+        self.g_local = Gops.GraphShard(src_local, g.dstl, E, g.v_lo, g.v_hi, g.n_vertices, sl,
+                                       g.new_id)
+        # request lists: peer p asks for send_counts[p] of my vertices
+        send_counts = torch.empty_like(recv_counts)
+        comm.all_to_all_single(send_counts, recv_counts)
+        self.recv_split = [int(x) for x in recv_counts.tolist()]
+        self.send_split = [int(x) for x in send_counts.tolist()]
+        req = torch.empty(sum(self.send_split), dtype=torch.int64, device=src.device)
+        comm.all_to_all_single(req, ghosts, out_split=self.send_split, in_split=self.recv_split)
+        self.send_idx = (req - g.v_lo).contiguous()
+        assert bool(((self.send_idx >= 0) & (self.send_idx < g.n_local)).all())
+        self.send_buf = None
+
+    def _exchange(self):
+        if self.exchange == "ghost":
+            if self.send_buf is None:
+                self.send_buf = torch.empty(self.send_idx.numel(), dtype=self.fdt, device=self.dev)
+            torch.index_select(self.c_slice, 0, self.send_idx, out=self.send_buf)
+            comm.all_to_all_single(self.c_full[self.g.slice_size:], self.send_buf,
+                                   out_split=self.recv_split, in_split=self.send_split)
+        else:
+            comm.all_gather_into(self.c_full, self.c_slice)
+
     def step(self):
-        comm.all_gather_into(self.c_full, self.c_slice)
+        self._exchange()
         self.acc.zero_()
         self.pres.zero_()
         if self.layout is not None:
             Gops.pb_spmv(self.layout, self.c_full, self.acc, self.pres)
+        elif self.exchange == "ghost":
+            Gops.pr_spmv(self.g_local, self.c_full, self.acc, self.pres)
         else:
             Gops.pr_spmv(self.g, self.c_full, self.acc, self.pres)
         nl = self.g.n_local

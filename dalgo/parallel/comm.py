@@ -163,6 +163,27 @@ def reduce_scatter_sum(out: torch.Tensor, full: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, out_split: list[int] | None = None,
+                      in_split: list[int] | None = None) -> torch.Tensor:
+    """Personalised exchange along dim 0 (``out_split[p]`` rows arrive from rank p,
+    ``in_split[p]`` rows go to it); RCCL runs it as grouped send/recv over all peers at
+    once. World size 1: a copy."""
+    if not _active():
+        if out.numel():
+            out.copy_(inp.reshape(out.shape))
+        return out
+    if inp.is_cuda and dist.get_backend() == "gloo":
+        # gloo's all_to_all takes host tensors only (the one-GPU multi-rank rehearsal)
+        host = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(host, inp.cpu(), output_split_sizes=out_split,
+                               input_split_sizes=in_split)
+        out.copy_(host)
+        return out
+    dist.all_to_all_single(out, inp.contiguous(), output_split_sizes=out_split,
+                           input_split_sizes=in_split)
+    return out
+
+
 def gather_to_rank0(local: torch.Tensor, counts: list[int]) -> torch.Tensor | None:
     """``collect()``: rows of every rank concatenated on rank 0 (None elsewhere)."""
     full = all_gather_varlen(local, counts)

@@ -47,6 +47,9 @@ def _others(rt):
     for sem in ("reference", "standard"):
         sh = G.build_shard(s, d, 1024, r, W)
         out["pr_" + sem] = PageRank(PageRankConfig(semantics=sem), sh, W).fit().collect()
+        # the all_gather exchange (the default on several ranks is the ghost exchange)
+        out["pr_ag_" + sem] = PageRank(PageRankConfig(semantics=sem, exchange="allgather"), sh,
+                                       W).fit().collect()
     # transitive closure
     g = torch.Generator().manual_seed(4)
     ts = torch.randint(0, 60, (100,), generator=g)
@@ -82,7 +85,7 @@ def test_other_algorithms_two_ranks_equal_one():
         assert np.allclose(two[0][k], one[k], atol=1e-4), k
         assert np.allclose(two[1][k], one[k], atol=1e-4), k
     assert np.allclose(two[0]["kmeans_sse"], one["kmeans_sse"], rtol=1e-6)
-    for sem in ("pr_reference", "pr_standard"):
+    for sem in ("pr_reference", "pr_standard", "pr_ag_reference", "pr_ag_standard"):
         a, b = one[sem], two[0][sem]
         assert set(a) == set(b)
         assert max(abs(a[v] - b[v]) for v in a) < 1e-12
@@ -132,7 +135,7 @@ def test_other_algorithms_three_ranks_equal_one():
         assert three[r]["tc_dense"] == one["tc_dense"] == three[r]["tc_sparse"]
         assert three[r]["mc"] == three[0]["mc"]
     assert np.allclose(three[0]["kmeans_sse"], one["kmeans_sse"], rtol=1e-6)
-    for sem in ("pr_reference", "pr_standard"):
+    for sem in ("pr_reference", "pr_standard", "pr_ag_reference", "pr_ag_standard"):
         a, b = one[sem], three[0][sem]
         assert set(a) == set(b)
         assert max(abs(a[v] - b[v]) for v in a) < 1e-12
