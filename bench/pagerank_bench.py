@@ -47,18 +47,16 @@ def main():
     torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     ev[0].record()
-    comm.all_gather_into(pr.c_full, pr.c_slice)
+    pr._exchange()
     ev[1].record()
-    pr.acc.zero_(); pr.pres.zero_()
-    if pr.layout is not None:
-        G.pb_spmv(pr.layout, pr.c_full, pr.acc, pr.pres)
-    else:
-        G.pr_spmv(pr.g, pr.c_full, pr.acc, pr.pres)
+    pr._spmv()
     ev[2].record()
-    G.pr_update(pr.acc, pr.pres, pr.outdeg, 0.15, pr.invN, pr.mode, pr.r, pr.c_slice[: shard.n_local])
+    pr._update()
     ev[3].record()
     torch.cuda.synchronize()
-    phases = {n: ev[i].elapsed_time(ev[i + 1]) for i, n in enumerate(["allgather", "spmv", "update"])}
+    phases = {n: ev[i].elapsed_time(ev[i + 1]) for i, n in enumerate(["exchange", "spmv", "update"])}
+    xf = torch.tensor([pr.exchange_floats()], dtype=torch.int64, device=rt.device)
+    comm.all_reduce_sum(xf)
     rt.barrier(); torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(a.steps):
@@ -72,7 +70,9 @@ def main():
             "metric": "PageRank edges/sec (whole node)", "value": E / (ms / 1e3), "unit": "edges/s",
             "n_gpus": W, "ms_per_iter": ms, "edges_dedup": E, "edges_generated": n_gen,
             "vertices": 1 << a.scale, "degree_reordered": not a.no_reorder, "spmv": pr.spmv, "phases_ms_rank0": phases, "graph_build_s": build_s,
-            "spmv_GBps_stream": shard.n_edges * 8 / (phases["spmv"] / 1e3) / 1e9}), flush=True)
+            "spmv_GBps_stream": shard.n_edges * 8 / (phases["spmv"] / 1e3) / 1e9,
+            "exchange": pr.exchange, "exchange_MB_per_iter_all_ranks": int(xf.item()) * 4 / 1e6,
+            "allgather_MB_per_iter_all_ranks": (W - 1) * W * shard.slice_size * 4 / 1e6}), flush=True)
     runtime.shutdown()
 
 

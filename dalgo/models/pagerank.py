@@ -137,8 +137,7 @@ class PageRank:
         else:
             comm.all_gather_into(self.c_full, self.c_slice)
 
-    def step(self):
-        self._exchange()
+    def _spmv(self):
         self.acc.zero_()
         self.pres.zero_()
         if self.layout is not None:
@@ -147,6 +146,8 @@ class PageRank:
             Gops.pr_spmv(self.g_local, self.c_full, self.acc, self.pres)
         else:
             Gops.pr_spmv(self.g, self.c_full, self.acc, self.pres)
+
+    def _update(self):
         nl = self.g.n_local
         if self.mode == 1:
             self.dang_next.zero_()
@@ -156,7 +157,20 @@ class PageRank:
         if self.mode == 1:
             comm.all_reduce_sum(self.dang_next)
             self.dang, self.dang_next = self.dang_next, self.dang
+
+    def step(self):
+        self._exchange()      # contributions of the previous iteration
+        self._spmv()          # K4 pull SpMV over the local in-edges
+        self._update()        # ranks + next contributions (fused epilogue kernel)
         self.t += 1
+
+    def exchange_floats(self) -> int:
+        """Contribution floats this rank receives per iteration."""
+        if self.world == 1:
+            return 0
+        if self.exchange == "ghost":
+            return self.n_ghost
+        return self.g.slice_size * (self.world - 1)
 
     def fit(self, n_iterations: int | None = None):
         n = self.cfg.n_iterations if n_iterations is None else n_iterations
