@@ -79,8 +79,11 @@ __host__ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, ui
   const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    uint32_t hi0 = mulhi32(M0, c.x), lo0 = M0 * c.x;
-    uint32_t hi1 = mulhi32(M1, c.z), lo1 = M1 * c.z;
+    // one 32x32->64 product per multiplier (v_mad_u64_u32 on the device) instead of a
+    // separate mul_hi and mul_lo
+    const uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
     u32x4 n;
     n.x = hi1 ^ c.y ^ k0;
     n.y = lo1;
