@@ -58,6 +58,10 @@ class SGDConfig:
     init_seed: int = 0            # the reference's np.random.ranf is unseeded
     reuse_minibatch: bool = True  # MA/BMUF: same sample for all local steps (ma.py:99)
     eval_every: int = 1           # test accuracy every k rounds (0 = never)
+    # EASGD on several ranks: the centre all-reduce of round t runs (async, on the
+    # collective stream) under the gradient kernel of round t+1, which does not read the
+    # centre; the centre update is applied right before the elastic step that needs it
+    overlap_center: bool = True
 
     def __post_init__(self):
         if self.algo not in ALGOS:
@@ -375,15 +379,38 @@ class ParallelSGD:
                               inv_p=self.inv_p)
         else:  # easgd
             self._grad(self.W, t, **sd)
+            # the centre of this round = previous round's locals (easgd.py:104-106): its
+            # all-reduce may still be in flight under the gradient kernel above
+            self._finish_center()
             U.sync_update(self.W, U.LOCAL_ELASTIC, G=self.G, C=self.C, center=self.w, eta=c.eta,
                           alpha=c.alpha, zero_grad=self._zg)
             self._g_zero = True
             U.rows_sum(self.W, self.S)
-            comm.all_reduce_sum(self.S)
-            U.sync_update(self.w, U.ELASTIC_CENTER, S=self.S, beta=c.beta, inv_p=self.inv_p)
+            if self._overlap_ok(step_dev):
+                self._center_work = comm.all_reduce_sum(self.S, async_op=True)
+            else:
+                comm.all_reduce_sum(self.S)
+                U.sync_update(self.w, U.ELASTIC_CENTER, S=self.S, beta=c.beta, inv_p=self.inv_p)
+
+    def _overlap_ok(self, step_dev=None) -> bool:
+        """EASGD centre all-reduce deferred under the next gradient (several ranks, eager)."""
+        return (self.cfg.algo == "easgd" and self.cfg.overlap_center and comm.world_size() > 1
+                and step_dev is None and os.environ.get("DALGO_EASGD_OVERLAP", "1") != "0"
+                and not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()))
+
+    def _finish_center(self):
+        """Complete a deferred EASGD centre update: w = (1-beta) w + beta * sum(locals)/P."""
+        work = getattr(self, "_center_work", None)
+        if work is None:
+            return
+        self._center_work = None
+        work.wait()
+        c = self.cfg
+        U.sync_update(self.w, U.ELASTIC_CENTER, S=self.S, beta=c.beta, inv_p=self.inv_p)
 
     def evaluate(self):
         self._flush()
+        self._finish_center()
         d = self.data
         if d.X_test.shape[0] == 0:
             return float("nan"), float("nan")
@@ -427,12 +454,14 @@ class ParallelSGD:
                     self.rt.log("iterations: %d, accuracy: %f" % (self.t - 1, acc))
             if callback is not None:
                 callback(self)
+        self._finish_center()
         comm.check_device_errors("end of fit")
         return self.history
 
     # --------------------------------------------------------- checkpointing
     def state_dict(self) -> dict:
         self._flush()
+        self._finish_center()
         sd = {"t": self.t, "w": self.w.detach().cpu(), "cfg": asdict(self.cfg),
               "accs": list(self.history.accs)}
         if hasattr(self, "W"):
@@ -454,4 +483,5 @@ class ParallelSGD:
 
     def weights(self) -> torch.Tensor:
         self._flush()
+        self._finish_center()
         return self.w.view(-1)

@@ -210,3 +210,28 @@ def test_comm_primitives_three_ranks():
             assert o["g0"] == [0.0, 1.0, 1.0, 2.0, 2.0, 2.0]
         else:
             assert o["g0"] is None
+
+
+def _easgd_overlap(rt):
+    from dalgo.data.datasets import breast_cancer
+    from dalgo.models.localsgd import ParallelSGD, SGDConfig
+    from dalgo.parallel.sharding import make_layout
+    out = {}
+    for ov in (True, False):
+        cfg = SGDConfig(algo="easgd", n_iterations=15, eval_every=4, overlap_center=ov)
+        lay = make_layout(398, cfg.n_workers, rt.world_size, rt.rank)
+        d = breast_cancer(dtype=torch.float64, row_range=(lay.row_lo, lay.row_hi))
+        m = ParallelSGD(cfg, d, lay, rt, model_dtype=torch.float64)
+        h = m.fit()
+        out[ov] = (m.weights().numpy().copy(), list(h.accs), m.state_dict()["w"].numpy().copy())
+    return out
+
+
+def test_easgd_centre_overlap_is_exact():
+    """The deferred (overlapped) EASGD centre all-reduce computes exactly the sequential
+    rounds of easgd.py:95-106: same weights, same evaluation history, same checkpoint."""
+    for res in run_world(_easgd_overlap, world=2):
+        a, b = res[True], res[False]
+        assert np.array_equal(a[0], b[0])
+        assert a[1] == b[1]
+        assert np.array_equal(a[2], b[2])
