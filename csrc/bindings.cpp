@@ -730,6 +730,49 @@ void als_solve(const Tensor& R, const Tensor& F, const Tensor& Ginv, Tensor out)
                   "als_solve");
 }
 
+// G = F^T F (k x k) of an n x k f32 factor, split-n partials summed in block order
+void als_gram(const Tensor& F, Tensor G) {
+  check_dev(F, "F");
+  TORCH_CHECK(F.scalar_type() == at::kFloat && F.dim() == 2 && F.stride(1) == 1,
+              "als_gram: F must be 2-D float32 with contiguous rows");
+  check_f32(G, "G");
+  const int64_t n = F.size(0), k = F.size(1);
+  TORCH_CHECK(k >= 1 && k <= 128, "als_gram: k <= 128");
+  TORCH_CHECK(G.dim() == 2 && G.size(0) == k && G.size(1) == k, "als_gram: G k x k");
+  TORCH_CHECK(F.device() == G.device(), "als_gram: operands on different devices");
+  DeviceGuard guard(F.device());
+  Tensor part = at::empty({(int64_t)dalgo_als_gram_blocks(n) * k * k}, F.options());
+  DALGO_CHECK_HIP(dalgo_als_gram(F.data_ptr<float>(), n, (int)k, F.stride(0), G.data_ptr<float>(),
+                                 (int)G.stride(0), part.data_ptr<float>(), cur_stream()),
+                  "als_gram");
+}
+
+// sum_ij (R_ij - U_i . V_j)^2 -> out (f64 [1]); R rows 16-B aligned
+void als_residual(const Tensor& R, const Tensor& U, const Tensor& V, Tensor out) {
+  check_dev(R, "R");
+  TORCH_CHECK(R.scalar_type() == at::kFloat && R.dim() == 2 && R.stride(1) == 1,
+              "als_residual: R must be 2-D float32 with contiguous rows");
+  TORCH_CHECK(R.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(R.data_ptr()) % 16 == 0,
+              "als_residual: R rows must be 16-B aligned");
+  for (const Tensor* t : {&U, &V}) {
+    check_dev(*t, "factor");
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->dim() == 2 && t->stride(1) == 1,
+                "als_residual: factors must be 2-D float32 with contiguous rows");
+  }
+  TORCH_CHECK(out.scalar_type() == at::kDouble && out.numel() >= 1 && out.is_cuda(), "out f64[1]");
+  const int64_t m = R.size(0), n = R.size(1), k = U.size(1);
+  TORCH_CHECK(U.size(0) == m && V.size(0) == n && V.size(1) == k, "als_residual: shapes");
+  TORCH_CHECK(k >= 1 && k <= 128 && m >= 1 && n >= 1, "als_residual: k <= 128, non-empty R");
+  DeviceGuard guard(R.device());
+  Tensor Vq = at::empty({dalgo_als_residual_vq_bytes(n, (int)k) / 4}, R.options());
+  Tensor part = at::empty({(int64_t)dalgo_als_residual_blocks(m, n)}, R.options().dtype(at::kDouble));
+  DALGO_CHECK_HIP(dalgo_als_residual(R.data_ptr<float>(), m, n, R.stride(0), U.data_ptr<float>(),
+                                     U.stride(0), V.data_ptr<float>(), V.stride(0), (int)k, Vq.data_ptr(),
+                                     part.data_ptr<double>(), cur_stream()),
+                  "als_residual");
+  out.reshape(-1).narrow(0, 0, 1).copy_(part.sum().reshape(1));
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dalgo, m) {
@@ -781,6 +824,8 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("tc_step(Tensor A, Tensor Told, Tensor(a!) Tnew, Tensor(b!) count, int variant=0) -> ()");
   m.def("spd_inverse(Tensor G, float ridge, Tensor(a!) out, Tensor(b!)? status) -> ()");
   m.def("als_solve(Tensor R, Tensor F, Tensor Ginv, Tensor(a!) out) -> ()");
+  m.def("als_gram(Tensor F, Tensor(a!) G) -> ()");
+  m.def("als_residual(Tensor R, Tensor U, Tensor V, Tensor(a!) out) -> ()");
   m.def("hbm_read(Tensor src, Tensor(a!) out, int unroll=8) -> ()");
   m.def("lr_set_trace(Tensor? buf) -> ()", &lr_set_trace);
   m.def("hbm_gather_rows(Tensor X, Tensor idx, Tensor(a!) out, int grid=2048) -> ()");
@@ -799,6 +844,8 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("hbm_gather_rows", &hbm_gather_rows);
   m.impl("spd_inverse", &spd_inverse);
   m.impl("als_solve", &als_solve);
+  m.impl("als_gram", &als_gram);
+  m.impl("als_residual", &als_residual);
   m.impl("tc_step", &tc_step);
   m.impl("xgmi_allreduce", &xgmi_allreduce);
   m.impl("rmat_edges", &rmat_edges);

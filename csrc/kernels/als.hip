@@ -578,6 +578,153 @@ als_rf16l_kernel(const float* __restrict__ R, int64_t m, int64_t n, int64_t ldr,
   }
 }
 
+// ---- residual sum of squares  sum_ij (R_ij - U_i . V_j)^2  (the ALS RMSE of
+// matrix_decomposition.py:19-21) in one pass over R, never forming U V^T: the closed form
+// ||R||^2 - 2<U, R V> + <U^T U, V^T V> cancels ~5 significant digits at 100k x 50k, where
+// an f32 R V (even with the hi/lo split) moves the RMSE by 0.5 %; here every residual is
+// formed in f32 from an f32-accurate U V^T tile and squared, so nothing cancels.
+// 16x16x32 MFMA with A = V^T tile (16 V rows = columns of R, Vq packed hi/lo fragments),
+// B = U^T tile (16 U rows = rows of R, resident hi/lo fragments): lane l ends with R row
+// (l & 15) and columns 4 (l >> 4) + i, i < 4 — one float4 of R per lane per tile pair.
+// Vq[((ct * KS + s) * 2 + p) * 64 + lane] = part p of V[16 ct + (lane & 15)][32 s + 8 (lane >> 4) + j]
+__global__ void __launch_bounds__(256)
+als_pack_v_kernel(const float* __restrict__ V, int64_t n, int k, int64_t ldv, int KS,
+                  uint4* __restrict__ Vq, int64_t nct) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (ct, s, lane)
+  if (gid >= nct * KS * 64) return;
+  const int lane = (int)(gid & 63);
+  const int64_t t = gid >> 6;
+  const int sidx = (int)(t % KS);
+  const int64_t ct = t / KS;
+  const int64_t row = 16 * ct + (lane & 15);
+  const int k0 = 32 * sidx + 8 * (lane >> 4);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (row < n && k0 + j < k) ? V[row * ldv + k0 + j] : 0.f;
+  uint4 hi, lo;
+  split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), hi, lo);
+  Vq[(t * 2 + 0) * 64 + lane] = hi;
+  Vq[(t * 2 + 1) * 64 + lane] = lo;
+}
+
+template <int RT, int KS>
+__global__ void __launch_bounds__(256, 1)
+als_residual_kernel(const float* __restrict__ R, int64_t m, int64_t n, int64_t ldr,
+                    const float* __restrict__ U, int k, int64_t ldu, const uint4* __restrict__ Vq,
+                    int nrb, int64_t ct_per_split, double* __restrict__ part) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  constexpr int NW = 4;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, rr = lane & 15, g = lane >> 4;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int sp = L / nrb, rb = L % nrb;
+  const int64_t nct = (n + 15) / 16;
+  const int64_t ct0 = (int64_t)sp * ct_per_split;
+  const int64_t ct1 = std::min<int64_t>(nct, ct0 + ct_per_split);
+  const int64_t row0 = ((int64_t)rb * NW + wid) * (RT * 16);
+  // resident U^T fragments (B operand): row row0 + 16 t + rr, k = 32 s + 8 g + j
+  bf16x8 uh[RT][KS], ul[RT][KS];
+  const float* rp[RT];
+  bool rok[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int64_t row = row0 + 16 * t + rr;
+    rok[t] = row < m;
+    const int64_t rs = rok[t] ? row : 0;
+    rp[t] = R + rs * ldr + 4 * g;
+#pragma unroll
+    for (int sidx = 0; sidx < KS; ++sidx) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kk = 32 * sidx + 8 * g + j;
+        v[j] = (kk < k) ? U[rs * ldu + kk] : 0.f;
+      }
+      uint4 hi, lo;
+      split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), hi, lo);
+      uh[t][sidx] = __builtin_bit_cast(bf16x8, hi);
+      ul[t][sidx] = __builtin_bit_cast(bf16x8, lo);
+    }
+  }
+  auto load_v = [&](uint4 (&vf)[KS][2], int64_t ct) {
+    const uint4* vp = Vq + (ct * KS * 2) * 64 + lane;
+#pragma unroll
+    for (int sidx = 0; sidx < KS; ++sidx) {
+      vf[sidx][0] = vp[(2 * sidx) * 64];
+      vf[sidx][1] = vp[(2 * sidx + 1) * 64];
+    }
+  };
+  const bool full_cols = (n % 16) == 0;
+  auto load_r = [&](float4 (&rv)[RT], int64_t ct) {
+    const int64_t c = 16 * ct + 4 * g;
+    if (full_cols || c + 4 <= n) {
+#pragma unroll
+      for (int t = 0; t < RT; ++t) rv[t] = *reinterpret_cast<const float4*>(rp[t] + 16 * ct);
+    } else {
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (c + e < n) ? rp[t][16 * ct + e] : 0.f;
+        rv[t] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  };
+  double dsum = 0.0;
+  float fsum = 0.f;
+  int nacc = 0;
+  auto tile = [&](const float4 (&rv)[RT], const uint4 (&vf)[KS][2], int64_t ct) {
+    const int64_t c = 16 * ct + 4 * g;
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      f32x4 d = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sidx = 0; sidx < KS; ++sidx) {
+        const bf16x8 vh = __builtin_bit_cast(bf16x8, vf[sidx][0]);
+        const bf16x8 vl = __builtin_bit_cast(bf16x8, vf[sidx][1]);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, uh[t][sidx], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl, uh[t][sidx], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, ul[t][sidx], d, 0, 0, 0);
+      }
+      const float r0 = rv[t].x - d[0], r1 = rv[t].y - d[1], r2 = rv[t].z - d[2], r3 = rv[t].w - d[3];
+      float q = 0.f;
+      if (rok[t]) {
+        q = (c + 0 < n ? r0 * r0 : 0.f) + (c + 1 < n ? r1 * r1 : 0.f) +
+            (c + 2 < n ? r2 * r2 : 0.f) + (c + 3 < n ? r3 * r3 : 0.f);
+      }
+      fsum += q;
+    }
+    if (++nacc == 32) { dsum += (double)fsum; fsum = 0.f; nacc = 0; }
+  };
+
+  float4 ra[RT], rb2[RT];
+  uint4 va[KS][2], vb[KS][2];
+  int64_t ct = ct0;
+  if (ct < ct1) { load_v(va, ct); load_r(ra, ct); }
+  for (; ct + 1 < ct1; ct += 2) {
+    load_v(vb, ct + 1);
+    load_r(rb2, ct + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(ra, va, ct);
+    __builtin_amdgcn_sched_barrier(0);
+    if (ct + 2 < ct1) { load_v(va, ct + 2); load_r(ra, ct + 2); }
+    __builtin_amdgcn_sched_barrier(0);
+    tile(rb2, vb, ct + 1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (ct < ct1) tile(ra, va, ct);
+  dsum += (double)fsum;
+  // block sum (wave shuffles in f64, then LDS), one partial per block
+  for (int off = 32; off >= 1; off >>= 1) dsum += __shfl_xor(dsum, off);
+  __shared__ double s_w[NW];
+  if (lane == 0) s_w[wid] = dsum;
+  __syncthreads();
+  if (tid == 0) {
+    double tot = 0.0;
+    for (int w = 0; w < NW; ++w) tot += s_w[w];
+    part[blockIdx.x] = tot;
+  }
+}
+
 // out[i, :k] = (sum_s P[s][i, :]) . Ginv   — 32 rows per block, fixed split order
 __global__ void __launch_bounds__(256)
 als_reduce_solve_kernel(const float* __restrict__ P, int nsplit, int64_t m, int kpad,
@@ -604,6 +751,63 @@ als_reduce_solve_kernel(const float* __restrict__ P, int nsplit, int64_t m, int 
     float s = 0.f;
     for (int c = 0; c < k; ++c) s = fmaf(b[c], s_g[c * k + j], s);
     out[(r0 + i) * ldo + j] = s;
+  }
+}
+
+// Gram matrix G = F^T F of an n x k factor (k <= 128), once per half-sweep. The library
+// GEMM runs this skinny shape (M = N = k, K = n = 50k) on a handful of workgroups (280 us
+// in the round-2 profile); here n is split over up to 256 blocks, each stages 32 rows at a
+// time in LDS and accumulates its k*k partial in registers (thread t owns entries t,
+// t+256, ...), and a second kernel sums the partials in block order (deterministic).
+__global__ void __launch_bounds__(256)
+als_gram_partial_kernel(const float* __restrict__ F, int64_t n, int k, int64_t ldf,
+                        int64_t rows_per_block, float* __restrict__ part) {
+  constexpr int RB = 32;
+  __shared__ float s_f[RB * 128];
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = std::min<int64_t>(n, r0 + rows_per_block);
+  const int kk = k * k;
+  float acc[64];
+  int ei[64], ej[64];
+  const int ne = (kk + 255) / 256;             // entries per thread (<= 64 for k <= 128)
+#pragma unroll
+  for (int q = 0; q < 64; ++q) {
+    acc[q] = 0.f;
+    const int e = tid + 256 * q;
+    ei[q] = e < kk ? e / k : 0;
+    ej[q] = e < kk ? e % k : 0;
+  }
+  for (int64_t rb = r0; rb < r1; rb += RB) {
+    const int nr = (int)std::min<int64_t>(RB, r1 - rb);
+    __syncthreads();
+    for (int e = tid; e < nr * k; e += 256) {
+      const int i = e / k, j = e % k;
+      s_f[i * k + j] = F[(rb + i) * ldf + j];
+    }
+    __syncthreads();
+    for (int i = 0; i < nr; ++i) {
+      const float* row = s_f + i * k;
+#pragma unroll
+      for (int q = 0; q < 64; ++q)
+        if (q < ne) acc[q] = fmaf(row[ei[q]], row[ej[q]], acc[q]);
+    }
+  }
+  float* out = part + (int64_t)blockIdx.x * kk;
+#pragma unroll
+  for (int q = 0; q < 64; ++q) {
+    const int e = tid + 256 * q;
+    if (q < ne && e < kk) out[e] = acc[q];
+  }
+}
+
+__global__ void __launch_bounds__(256)
+als_gram_sum_kernel(const float* __restrict__ part, int nb, int k, float* __restrict__ G, int ldg) {
+  const int kk = k * k;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < kk; e += gridDim.x * 256) {
+    float s = 0.f;
+    for (int b = 0; b < nb; ++b) s += part[(int64_t)b * kk + e];
+    G[(int64_t)(e / k) * ldg + (e % k)] = s;
   }
 }
 
@@ -708,6 +912,70 @@ hipError_t dalgo_spd_inverse(const float* G, int k, int ldg, float ridge, float*
   const int threads = k * k >= 1024 ? 1024 : ((k * k + 63) / 64) * 64;
   hipLaunchKernelGGL(spd_inverse_kernel, dim3(1), dim3(threads), lds, st, G, k, ldg, ridge, out, ldo,
                      status);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+// G[k x k] = F^T F (F: n x k f32, k <= 128); part: dalgo_als_gram_blocks(n) * k * k floats
+int dalgo_als_gram_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(256, cdiv(n, 64))); }
+hipError_t dalgo_als_gram(const float* F, int64_t n, int k, int64_t ldf, float* G, int ldg, float* part,
+                          hipStream_t st) {
+  if (k < 1 || k > 128 || n < 0) return hipErrorInvalidValue;
+  const int nb = dalgo_als_gram_blocks(n);
+  const int64_t rpb = std::max<int64_t>(1, cdiv(n, nb));
+  hipLaunchKernelGGL(als_gram_partial_kernel, dim3(nb), dim3(256), 0, st, F, n, k, ldf, rpb, part);
+  DALGO_LAUNCH_CHECK();
+  hipLaunchKernelGGL(als_gram_sum_kernel, dim3((unsigned)cdiv((int64_t)k * k, 256)), dim3(256), 0, st, part,
+                     nb, k, G, ldg);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+// sum_ij (R_ij - U_i . V_j)^2 over R (m x n f32, ldr % 4 == 0, 16-B aligned), U (m x k),
+// V (n x k), k <= 128. Vq: dalgo_als_residual_vq_bytes(n, k) bytes; part: one double per
+// block, dalgo_als_residual_blocks(m, n) of them (the caller sums them in order).
+static void als_residual_grid(int64_t m, int64_t n, int* nrb, int* nsp, int64_t* ctps) {
+  const int64_t rows = 4 * 8 * 16;
+  *nrb = (int)std::max<int64_t>(1, cdiv(m, rows));
+  const int64_t nct = std::max<int64_t>(1, cdiv(n, 16));
+  const int64_t want = std::max<int64_t>(1, cdiv(4 * (int64_t)als_device_cus(), *nrb));
+  const int64_t s = std::min<int64_t>(want, nct);
+  *ctps = cdiv(nct, s);
+  *nsp = (int)cdiv(nct, *ctps);
+}
+int64_t dalgo_als_residual_vq_bytes(int64_t n, int k) {
+  return std::max<int64_t>(1, cdiv(n, 16)) * ((k + 31) / 32) * 2 * 64 * 16;
+}
+int dalgo_als_residual_blocks(int64_t m, int64_t n) {
+  int nrb, nsp;
+  int64_t ctps;
+  als_residual_grid(m, n, &nrb, &nsp, &ctps);
+  return nrb * nsp;
+}
+hipError_t dalgo_als_residual(const float* R, int64_t m, int64_t n, int64_t ldr, const float* U,
+                              int64_t ldu, const float* V, int64_t ldv, int k, void* Vq, double* part,
+                              hipStream_t st) {
+  if (k < 1 || k > 128 || m < 1 || n < 1 || (ldr & 3)) return hipErrorInvalidValue;
+  if (((uintptr_t)R & 15) || ((uintptr_t)Vq & 15)) return hipErrorInvalidValue;
+  const int KS = (k + 31) / 32;
+  const int64_t nct = cdiv(n, 16);
+  {
+    const int64_t total = nct * KS * 64;
+    hipLaunchKernelGGL(als_pack_v_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, st, V, n, k, ldv,
+                       KS, reinterpret_cast<uint4*>(Vq), nct);
+    DALGO_LAUNCH_CHECK();
+  }
+  int nrb, nsp;
+  int64_t ctps;
+  als_residual_grid(m, n, &nrb, &nsp, &ctps);
+  const uint4* vq = reinterpret_cast<const uint4*>(Vq);
+  const dim3 grid(nrb * nsp), blk(256);
+  switch (KS) {
+    case 1: hipLaunchKernelGGL((als_residual_kernel<8, 1>), grid, blk, 0, st, R, m, n, ldr, U, k, ldu, vq, nrb, ctps, part); break;
+    case 2: hipLaunchKernelGGL((als_residual_kernel<8, 2>), grid, blk, 0, st, R, m, n, ldr, U, k, ldu, vq, nrb, ctps, part); break;
+    case 3: hipLaunchKernelGGL((als_residual_kernel<8, 3>), grid, blk, 0, st, R, m, n, ldr, U, k, ldu, vq, nrb, ctps, part); break;
+    default: hipLaunchKernelGGL((als_residual_kernel<8, 4>), grid, blk, 0, st, R, m, n, ldr, U, k, ldu, vq, nrb, ctps, part); break;
+  }
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -105,6 +105,14 @@ hipError_t dalgo_spd_inverse(const float* G, int k, int ldg, float ridge, float*
 int64_t dalgo_als_fq_bytes(int64_t n, int k);
 int dalgo_als_nsplit(int64_t m, int64_t n, int k);
 int dalgo_als_kpad(int k);
+int dalgo_als_gram_blocks(int64_t n);
+int64_t dalgo_als_residual_vq_bytes(int64_t n, int k);
+int dalgo_als_residual_blocks(int64_t m, int64_t n);
+hipError_t dalgo_als_residual(const float* R, int64_t m, int64_t n, int64_t ldr, const float* U,
+                              int64_t ldu, const float* V, int64_t ldv, int k, void* Vq, double* part,
+                              hipStream_t st);
+hipError_t dalgo_als_gram(const float* F, int64_t n, int k, int64_t ldf, float* G, int ldg, float* part,
+                          hipStream_t st);
 hipError_t dalgo_als_solve(const float* R, int64_t m, int64_t n, int64_t ldr, const float* F,
                            int64_t ldf, int k, const float* Ginv, int ldg, float* out, int64_t ldo,
                            void* Fq, float* P, int nsplit, hipStream_t st);

@@ -12,8 +12,9 @@ half-sweep is: Gram G = F^T F of the replicated other factor (one GEMM),
 K5 ridge SPD inverse (csrc/kernels/als.hip, f64 in LDS, once — not per row),
 local rows = (R_rows F) G^-1 (K5 als_solve: one pass over R_rows on the bf16 MFMA with
 a hi/lo split, G^-1 applied in the epilogue), all_gather of the factor rows. The
-RMSE uses ||R - UV^T||^2 = ||R||^2 - 2<U, RV> + <U^T U, V^T V> so U V^T is never
-materialised (f64 partial sums, one scalar all-reduce).
+RMSE never materialises U V^T: on the GPU the K5 residual kernel squares each f32
+residual in one pass over R; on the CPU the f64 closed form ||R||^2 - 2<U, RV> +
+<U^T U, V^T V> (one scalar all-reduce either way).
 """
 from __future__ import annotations
 
@@ -50,6 +51,17 @@ def rows_solve(R: torch.Tensor, F: torch.Tensor, Ginv: torch.Tensor) -> torch.Te
     out = torch.empty((R.shape[0], F.shape[1]), dtype=torch.float32, device=R.device)
     _ext.ops().als_solve(R, F.contiguous(), Ginv.contiguous(), out)
     return out
+
+
+def gram(F: torch.Tensor) -> torch.Tensor:
+    """F^T F: K5 split-n Gram kernel on the GPU (the library GEMM runs this skinny shape
+    on a handful of workgroups), torch on the CPU."""
+    if not F.is_cuda:
+        return F.T @ F
+    k = F.shape[1]
+    G = torch.empty((k, k), dtype=torch.float32, device=F.device)
+    _ext.ops().als_gram(F.contiguous(), G)
+    return G
 
 
 def _aligned_rows(R: torch.Tensor) -> torch.Tensor:
@@ -96,9 +108,10 @@ class ALS:
         self.n_lo, self.n_hi = self.nrows[rank]
         self.R_rows = (Ut[self.m_lo: self.m_hi] @ Vt.T).contiguous()        # [m_l, n]
         self.R_cols = (Vt[self.n_lo: self.n_hi] @ Ut.T).contiguous()        # [n_l, m] = R^T rows
-        self.R2 = torch.tensor([float((self.R_rows.double() ** 2).sum())], dtype=torch.float64,
-                               device=dev)
-        comm.all_reduce_sum(self.R2)
+        if dev.type != "cuda":   # ||R||^2 of the CPU closed-form RMSE (the GPU squares residuals)
+            self.R2 = torch.tensor([float((self.R_rows.double() ** 2).sum())], dtype=torch.float64,
+                                   device=dev)
+            comm.all_reduce_sum(self.R2)
         self.history = ALSHistory()
         self.t = 0
 
@@ -112,7 +125,7 @@ class ALS:
         return comm.all_gather_varlen(local, counts) if self.world > 1 else local
 
     def _half(self, R_local: torch.Tensor, F: torch.Tensor, x_dim: int) -> torch.Tensor:
-        G = F.T @ F                                         # Gram, once per half-sweep
+        G = gram(F)                                         # Gram, once per half-sweep
         Ginv = spd_inverse(G.contiguous(), self.cfg.lam * x_dim)
         return rows_solve(R_local, F, Ginv)                 # all local rows at once (K5)
 
@@ -125,12 +138,25 @@ class ALS:
         self.t += 1
 
     def rmse(self) -> float:
-        U_l = self.U[self.m_lo: self.m_hi].double()
-        RV = self.R_rows.double() @ self.V.double()
-        part = torch.stack([-2.0 * (U_l * RV).sum(),
-                            ((U_l.T @ U_l) * (self.V.double().T @ self.V.double())).sum()])
-        comm.all_reduce_sum(part)
-        sse = float(self.R2.item() + part.sum().item())
+        """sqrt(||R - U V^T||^2 / (m n)) (matrix_decomposition.py:19-21). GPU: the K5 residual
+        kernel squares every f32 residual of this rank's rows in one pass over R (no m x n
+        product is stored, and nothing cancels); CPU: the f64 closed form
+        ||R||^2 - 2<U, RV> + <U^T U, V^T V>. One scalar all-reduce."""
+        U_l = self.U[self.m_lo: self.m_hi]
+        if self.R_rows.is_cuda:
+            R = self.R_rows
+            if R.stride(1) != 1 or R.stride(0) % 4 or R.data_ptr() % 16:
+                R = _aligned_rows(R)
+            part = torch.zeros(1, dtype=torch.float64, device=self.dev)
+            _ext.ops().als_residual(R, U_l.float().contiguous(), self.V.float().contiguous(), part)
+            comm.all_reduce_sum(part)
+            sse = float(part.item())
+        else:
+            RV = self.R_rows.double() @ self.V.double()
+            Ud, Vd = U_l.double(), self.V.double()
+            part = torch.stack([-2.0 * (Ud * RV).sum(), ((Ud.T @ Ud) * (Vd.T @ Vd)).sum()])
+            comm.all_reduce_sum(part)
+            sse = float(self.R2.item() + part.sum().item())
         return math.sqrt(max(sse, 0.0) / (self.cfg.m * self.cfg.n))
 
     def state_dict(self) -> dict:

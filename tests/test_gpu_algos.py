@@ -344,6 +344,50 @@ def test_als_solve_gpu(cuda, monkeypatch, variant, m, n, k):
         assert ((out2 - ref).abs() / scale).max().item() < 2e-5
 
 
+@pytest.mark.parametrize("n,k", [(5, 1), (1000, 10), (70000, 64), (3000, 100), (2049, 128)])
+def test_als_gram_gpu(cuda, n, k):
+    """K5 split-n Gram F^T F against f64."""
+    from dalgo.models.als import gram
+    g = torch.Generator().manual_seed(n + k)
+    F = torch.rand(n, k, generator=g, dtype=torch.float64) - 0.3
+    ref = F.T @ F
+    G = gram(F.float().to(cuda)).cpu().double()
+    scale = F.abs().T @ F.abs()
+    assert ((G - ref).abs() / scale.clamp_min(1e-30)).max().item() < 1e-5
+
+
+@pytest.mark.parametrize("m,n,k", [(100, 500, 10), (513, 777, 64), (1000, 1001, 33), (7, 5, 1),
+                                   (3000, 2000, 128), (4100, 96, 96)])
+def test_als_residual_gpu(cuda, m, n, k):
+    """K5 residual kernel: sum (R - U V^T)^2 with R close to U V^T (the cancelling regime),
+    row / column tails, every K-step count, against f64."""
+    from dalgo.ops import _ext
+    g = torch.Generator().manual_seed(m + n + k)
+    U = torch.rand(m, k, generator=g, dtype=torch.float64)
+    V = torch.rand(n, k, generator=g, dtype=torch.float64)
+    R = U @ V.T + 0.05 * (torch.rand(m, n, generator=g, dtype=torch.float64) - 0.5)
+    Rf, Uf, Vf = R.float(), U.float(), V.float()
+    ref = float(((Rf.double() - Uf.double() @ Vf.double().T) ** 2).sum())
+    out = torch.zeros(1, dtype=torch.float64, device=cuda)
+    ld = (n + 3) // 4 * 4
+    Rd = torch.zeros(m, ld, dtype=torch.float32, device=cuda)[:, :n]
+    Rd.copy_(Rf.to(cuda))
+    _ext.ops().als_residual(Rd, Uf.to(cuda), Vf.to(cuda), out)
+    assert abs(float(out.item()) - ref) / ref < 1e-3, (float(out.item()), ref)
+
+
+def test_als_rmse_gpu_matches_f64(cuda):
+    """ALS.rmse on the GPU (RV from the K5 GEMM, f64 dot and Grams) == the f64 residual
+    norm of the same factors (m x n residual formed on the CPU)."""
+    from dalgo.models.als import ALS, ALSConfig
+    als = ALS(ALSConfig(m=3000, n=2000, k=16, seed=5), device=cuda)
+    als.fit(2)
+    R = (als.R_rows.cpu().double())
+    res = R - als.U.cpu().double() @ als.V.cpu().double().T
+    ref = math.sqrt(float((res ** 2).sum()) / (3000 * 2000))
+    assert abs(als.rmse() - ref) / ref < 1e-3, (als.rmse(), ref)
+
+
 def test_als_gpu(cuda):
     from dalgo.models.als import ALS, ALSConfig
     hc = ALS(ALSConfig(seed=3)).fit().rmse
