@@ -62,6 +62,8 @@ def main():
             us = lambda v: (v - t0) / 100.0   # noqa: E731
             start = us(t[:, :, 0]).flatten().tolist()
             first = (t[:, :, 1] - t[:, :, 0]).flatten().div(100.0).tolist()
+            bar = (t[:, :, 6] - t[:, :, 0]).flatten().div(100.0).tolist()
+            refl = (t[:, :, 7] - t[:, :, 0]).flatten().div(100.0).tolist()
             done = us(t[:, :, 2]).flatten().tolist()
             epi_end = us(t[:, 0, 3]).tolist()
             epi = ((t[:, 0, 3] - t[:, :, 2].max(dim=1).values) / 100.0).tolist()
@@ -73,6 +75,7 @@ def main():
             last8 = brows[order[-8:]].mean().item()
             res.append({
                 "start_p50": pct(start, 0.5), "start_max": max(start),
+                "barrier_p50": pct(bar, 0.5), "refill_p50": pct(refl, 0.5),
                 "first_issue_p50": pct(first, 0.5), "first_issue_max": max(first),
                 "sweep_done_p10": pct(done, 0.1), "sweep_done_p50": pct(done, 0.5),
                 "sweep_done_p90": pct(done, 0.9), "sweep_done_max": max(done),

@@ -347,6 +347,7 @@ lr_rows_kernel(const LrParams p) {
       __hip_atomic_store(p.pool + (int64_t)(p.pool_parity ^ 1) * gridDim.y * 8 + i, 0u,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
+  const unsigned long long t_bar = tr ? (unsigned long long)__builtin_amdgcn_s_memrealtime() : 0ull;
   constexpr int kPU = 128;
   const int64_t psl = seg_lo + (int64_t)gx * p.rows_per_block;   // pool start (local row)
   const bool has_pool = p.pool != nullptr && psl < seg_hi;
@@ -558,10 +559,11 @@ lr_rows_kernel(const LrParams p) {
 
   // ---- software-pipelined sweep: load(i+1) || compute(i)
   Batch<NC, U> A;
-  unsigned long long t_first = 0ull;
+  unsigned long long t_first = 0ull, t_refill = 0ull;
   if constexpr (PIPE) {
     Batch<NC, U> B;
     refill();
+    if (tr) t_refill = __builtin_amdgcn_s_memrealtime();
     take_and_load(A);
     if (PERSIST && it > 0 && !wait_epoch(it)) return;
     load_w();
@@ -592,6 +594,8 @@ lr_rows_kernel(const LrParams p) {
     tr[2] = __builtin_amdgcn_s_memrealtime();
     tr[4] = (unsigned long long)cntf;
     tr[5] = __smid();
+    tr[6] = t_bar;
+    tr[7] = t_refill;
   }
   __syncthreads();   // rings are dead: the arena becomes the reduction buffer
   if (p.probe_no_epilogue) {
