@@ -29,6 +29,11 @@ def main():
     ops = _ext.ops()
     args = sys.argv[1:]
     fines = [0]
+    frac = 0.1
+    if "--frac" in args:
+        i = args.index("--frac")
+        frac = float(args[i + 1])
+        args = args[:i] + args[i + 2:]
     if "--fine" in args:
         i = args.index("--fine")
         fines = [int(x) for x in args[i + 1:]]
@@ -48,12 +53,12 @@ def main():
         res = []
         for rep in range(6):
             for i in range(5):
-                L.lr_grad(X, y, W, seg, D=1024, frac=0.1, step=100 * rep + i, G=G, C=C, g_is_zero=True,
+                L.lr_grad(X, y, W, seg, D=1024, frac=frac, step=100 * rep + i, G=G, C=C, g_is_zero=True,
                           variant=var)
             buf.zero_()
             torch.cuda.synchronize()
             ops.lr_set_trace(buf)
-            L.lr_grad(X, y, W, seg, D=1024, frac=0.1, step=100 * rep + 50, G=G, C=C, g_is_zero=True,
+            L.lr_grad(X, y, W, seg, D=1024, frac=frac, step=100 * rep + 50, G=G, C=C, g_is_zero=True,
                       variant=var)
             ops.lr_set_trace(None)
             torch.cuda.synchronize()
@@ -88,7 +93,7 @@ def main():
                 "cus": len(set(t[:, :, 5].flatten().tolist())),
             })
         med = {k: round(sorted(r[k] for r in res)[len(res) // 2], 2) for k in res[0]}
-        print(json.dumps({"rows": rows, "fine": fine, "blocks": gx, **med}), flush=True)
+        print(json.dumps({"rows": rows, "frac": frac, "fine": fine, "blocks": gx, **med}), flush=True)
 
 
 if __name__ == "__main__":

@@ -227,7 +227,7 @@ lr_rows_kernel(const LrParams p) {
   // cross-wave reduction buffer
   __shared__ __attribute__((aligned(16))) float s_arena[(RED_FLOATS > RING_INTS) ? RED_FLOATS : RING_INTS];
   __shared__ int s_flag;
-  __shared__ int s_next;   // next unclaimed 64-row quarter of this block (dynamic balancing)
+  __shared__ int s_next;   // next unclaimed work unit of this block (dynamic balancing)
   __shared__ int s_ok;     // persistent mode: the epoch wait succeeded
 
   const int lane = threadIdx.x & 63;
@@ -334,10 +334,19 @@ lr_rows_kernel(const LrParams p) {
   int* ring = reinterpret_cast<int*>(s_arena) + wid * kRing;
   const int q = lane >> 4;
   uint32_t head = 0, tail = 0;
-  // work units are counted in 64-row quarters; a claim takes a whole 256-row group
-  // (4 quarters) until the block's unclaimed rows fall below fine_q quarters, then
-  // single quarters, so the block's waves finish within ~1.5 row batches of each other
-  if (threadIdx.x == 0) s_next = 4 * NW;   // groups 0..NW-1 are pre-assigned to the waves
+  // work units are counted in 2^qs-row units (64 rows when sampling, 8 when every row is
+  // taken: a unit then holds 8x the selected rows); a claim takes a whole 256-row group
+  // (upg units) until fewer than the fine threshold's groups of the block are unclaimed,
+  // then single units, so the block's waves finish within ~1.5 row batches of each other
+  const int qs = (EVAL || p.full) ? 3 : 6;
+  const int upg = 256 >> qs;
+  const int fine_u = (p.fine_q * upg) >> 2;   // fine_q counts 64-row quarters
+  const int nq = (int)((ghi - gstart + (1 << qs) - 1) >> qs);
+  // a block with few rows pre-assigns and claims single units (whole groups would leave
+  // most of its waves idle)
+  const bool small = nq < upg * NW + fine_u;
+  const int w0 = small ? 1 : upg;
+  if (threadIdx.x == 0) s_next = w0 * NW;   // units 0..w0 * NW - 1 are pre-assigned
   // cross-block pool (segment rows past the static block ranges): 128-row units j,
   // shard s = j % 8 holds units s, s + 8, ...; the claim heads are only touched by
   // agent-scope atomics (performed at memory side). Block (0, 0) re-arms the other
@@ -360,12 +369,11 @@ lr_rows_kernel(const LrParams p) {
   bool ahead_out = false;
   bool in_pool = false;
 
-  const int nq = (int)((ghi - gstart + 63) >> 6);
-  int64_t gnext = gstart + (int64_t)wid * 256;
+  int64_t gnext = gstart + ((int64_t)(wid * w0) << qs);
   int64_t ulo = glo;                       // current work unit: rows [max(gnext, ulo), uhi)
-  int64_t uhi = min(ghi, gnext + 256);
+  int64_t uhi = min(ghi, gnext + ((int64_t)w0 << qs));
   bool more = gnext < ghi;
-  int sclaim = 4 * (NW + wid);             // next group of this wave in the fixed map
+  int sclaim = w0 * (NW + wid);            // next unit of this wave in the fixed map
 
   auto pool_next = [&]() {
     if (!has_pool) { more = false; return; }
@@ -424,23 +432,23 @@ lr_rows_kernel(const LrParams p) {
       // claim the next unit dynamically: waves that drew few selected rows
       // take more units, so the block's waves finish together
       if (!in_pool) {
-        int gi = 0, w = 4;
+        int gi = 0, w = w0;
         if (!p.atomic_out) {
           // fixed-order epilogue: a fixed group -> wave map (wave w takes groups
           // w, w + NW, ...), so every partial sum is bitwise repeatable
           gi = sclaim;
-          sclaim += 4 * NW;
+          sclaim += w0 * NW;
         } else {
           if (lane == 0) {
-            if (p.fine_q > 0 && nq - *(volatile int*)&s_next <= p.fine_q) w = 1;
+            if (small || (fine_u > 0 && nq - *(volatile int*)&s_next <= fine_u)) w = 1;
             gi = atomicAdd(&s_next, w);
           }
           gi = __builtin_amdgcn_readfirstlane(gi);
           w = __builtin_amdgcn_readfirstlane(w);
         }
         if (gi < nq) {
-          gnext = gstart + (int64_t)gi * 64;
-          uhi = min(ghi, gnext + 64 * w);
+          gnext = gstart + ((int64_t)gi << qs);
+          uhi = min(ghi, gnext + ((int64_t)w << qs));
           // the block's last static unit: claim the first pool unit now, so it is
           // back before it is needed
           if (has_pool && !ahead_out && gi + w >= nq) {

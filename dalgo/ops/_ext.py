@@ -13,7 +13,9 @@ from pathlib import Path
 
 import torch
 
-_LIB = Path(__file__).resolve().parent.parent / "_dalgo_hip.so"
+# DALGO_EXT_LIB: load another build of the extension (A/B timing of two builds in one run)
+_LIB = Path(os.environ.get("DALGO_EXT_LIB") or
+            Path(__file__).resolve().parent.parent / "_dalgo_hip.so")
 _lock = threading.Lock()
 _state = {"loaded": False, "error": None}
 
