@@ -78,6 +78,13 @@ def main():
             intra = ((t[:, :, 2].max(dim=1).values - t[:, :, 2].min(dim=1).values) / 100.0).tolist()
             bd = bdone.tolist()
             last8 = brows[order[-8:]].mean().item()
+            # blocks are dealt round-robin over the 8 XCDs: per-XCD medians of the block
+            # finish time and of the time per selected row
+            per_row = (bdone - us(t[:, :, 0].min(dim=1).values)) / brows.clamp(min=1)
+            xcd_done = [bdone[i::8].median().item() for i in range(8)]
+            xcd_rate = [per_row[i::8].median().item() * 1e3 for i in range(8)]
+            bc = torch.stack([bdone - bdone.mean(), brows - brows.mean()])
+            corr = (bc[0] * bc[1]).sum() / (bc[0].norm() * bc[1].norm() + 1e-12)
             res.append({
                 "start_p50": pct(start, 0.5), "start_max": max(start),
                 "barrier_p50": pct(bar, 0.5), "refill_p50": pct(refl, 0.5),
@@ -90,6 +97,10 @@ def main():
                 "block_rows_mean": brows.mean().item(), "block_rows_max": brows.max().item(),
                 "rows_last8_blocks": last8,
                 "wave_rows_max": t[:, :, 4].max().item(),
+                "xcd_done_spread": max(xcd_done) - min(xcd_done),
+                "xcd_ns_per_row_min": min(xcd_rate), "xcd_ns_per_row_max": max(xcd_rate),
+                "ns_per_row_cv": (per_row.std() / per_row.mean()).item(),
+                "corr_done_rows": corr.item(),
                 "cus": len(set(t[:, :, 5].flatten().tolist())),
             })
         med = {k: round(sorted(r[k] for r in res)[len(res) // 2], 2) for k in res[0]}
