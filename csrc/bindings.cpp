@@ -99,7 +99,7 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
   if (pool.has_value()) {
     check_dev(*pool, "pool");
     TORCH_CHECK(pool->scalar_type() == at::kInt && pool->is_contiguous() &&
-                pool->numel() >= 2 * 8 * W.size(0), "pool: int32 [2 * 8 * n_seg] claim heads");
+                pool->numel() >= 2 * 64 * W.size(0), "pool: int32 [2 * 64 * n_seg] claim heads");
     poolp = reinterpret_cast<unsigned*>(pool->data_ptr<int>());
   }
   DalgoLrTail tail{};

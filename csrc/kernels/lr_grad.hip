@@ -216,6 +216,12 @@ constexpr int kRing = 512;   // per-wave ring of selected local row indices
 
 // EVAL=false: gradient; EVAL=true: accuracy + log-loss over every row.
 // PIPE: software-pipelined (two register sets) vs. single-buffered sweep.
+// cross-block pool geometry (K1): 512-row units claimed per block, handed to the
+// block's waves as 64-row sub-units; unit claims run kPAhead sub-units ahead of use
+constexpr int kPU = 512, kPSub = 64, kPSubs = kPU / kPSub, kPAhead = 4, kPSlots = 8;
+constexpr int kPHeads = 64;                  // claim heads (shards) per segment; one per lane
+constexpr int64_t kPExh = (1ll << 40) - 1;   // "pool exhausted" marker
+
 template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, bool PERSIST, int AUX = 0>
 __global__ void __launch_bounds__(NW * 64)
 lr_rows_kernel(const LrParams p) {
@@ -229,6 +235,10 @@ lr_rows_kernel(const LrParams p) {
   __shared__ int s_flag;
   __shared__ int s_next;   // next unclaimed work unit of this block (dynamic balancing)
   __shared__ int s_ok;     // persistent mode: the epoch wait succeeded
+  // block-level pool claims: next 64-row pool sub-unit to hand out, next pool unit to
+  // claim (block-local order), and the claimed units ((u + 1) << 40 | first global row)
+  __shared__ int s_pnext, s_pclaim;
+  __shared__ unsigned long long s_punit[kPSlots];
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -347,27 +357,29 @@ lr_rows_kernel(const LrParams p) {
   const bool small = nq < upg * NW + fine_u;
   const int w0 = small ? 1 : upg;
   if (threadIdx.x == 0) s_next = w0 * NW;   // units 0..w0 * NW - 1 are pre-assigned
-  // cross-block pool (segment rows past the static block ranges): 128-row units j,
-  // shard s = j % 8 holds units s, s + 8, ...; the claim heads are only touched by
-  // agent-scope atomics (performed at memory side). Block (0, 0) re-arms the other
-  // parity set, which the previous launch used and the next one will.
+  // cross-block pool (segment rows past the static block ranges): 512-row units, claimed
+  // per BLOCK from 64 shard heads (shard s holds units s, s + 64, ...; the heads are only
+  // touched by agent-scope atomics, performed at memory side, and a block first tries its
+  // own shard, so few blocks share a head) and handed to the block's waves in 64-row
+  // sub-units through LDS. Block (0, 0) re-arms the other parity set, which the previous
+  // launch used and the next one will.
   if (p.pool != nullptr && bx == 0 && seg == 0)
-    for (int i = threadIdx.x; i < 8 * (int)gridDim.y; i += NW * 64)
-      __hip_atomic_store(p.pool + (int64_t)(p.pool_parity ^ 1) * gridDim.y * 8 + i, 0u,
+    for (int i = threadIdx.x; i < kPHeads * (int)gridDim.y; i += NW * 64)
+      __hip_atomic_store(p.pool + (int64_t)(p.pool_parity ^ 1) * gridDim.y * kPHeads + i, 0u,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < kPSlots) s_punit[threadIdx.x] = 0ull;
+  if (threadIdx.x == 0) { s_pnext = 0; s_pclaim = 0; }
   __syncthreads();
   const unsigned long long t_bar = tr ? (unsigned long long)__builtin_amdgcn_s_memrealtime() : 0ull;
-  constexpr int kPU = 128;
   const int64_t psl = seg_lo + (int64_t)gx * p.rows_per_block;   // pool start (local row)
   const bool has_pool = p.pool != nullptr && psl < seg_hi;
-  unsigned* const heads = has_pool ? p.pool + ((int64_t)p.pool_parity * gridDim.y + seg) * 8 : nullptr;
+  unsigned* const heads =
+      has_pool ? p.pool + ((int64_t)p.pool_parity * gridDim.y + seg) * kPHeads : nullptr;
   const int64_t psg = p.row_offset + psl, psa = psg & ~(int64_t)3, sghi = p.row_offset + seg_hi;
   const int nj = has_pool ? (int)((sghi - psa + kPU - 1) / kPU) : 0;
-  auto shard_size = [&](int s) { return nj > s ? (nj - s + 7) >> 3 : 0; };
-  int pshard = (bx + seg) & 7;
-  int ahead = 0;            // lane 0: claim issued ahead on `pshard`, consumed by the next pool claim
-  bool ahead_out = false;
-  bool in_pool = false;
+  auto shard_size = [&](int s) { return nj > s ? (nj - s + kPHeads - 1) / kPHeads : 0; };
+  int pshard = bx & (kPHeads - 1);
+  bool in_pool = false, pool_done = false, pool_err = false;
 
   int64_t gnext = gstart + ((int64_t)(wid * w0) << qs);
   int64_t ulo = glo;                       // current work unit: rows [max(gnext, ulo), uhi)
@@ -375,42 +387,91 @@ lr_rows_kernel(const LrParams p) {
   bool more = gnext < ghi;
   int sclaim = w0 * (NW + wid);            // next unit of this wave in the fixed map
 
-  auto pool_next = [&]() {
-    if (!has_pool) { more = false; return; }
-    if (!ahead_out) {
-      if (lane == 0) ahead = (int)atomicAdd(&heads[pshard], 1u);
-      ahead_out = true;
-    }
-    int k = __builtin_amdgcn_readfirstlane(ahead);
-    ahead_out = false;
-    while (true) {
+  // claim one pool unit for the block (blocking for this wave only) and publish it
+  auto claim_unit = [&](int u) {
+    int64_t start = kPExh;
+    int k = 0;
+    if (lane == 0) k = (int)atomicAdd(&heads[pshard], 1u);
+    k = __builtin_amdgcn_readfirstlane(k);
+    for (int tries = 0;; ++tries) {
       if (k < shard_size(pshard)) {
-        gnext = psa + (int64_t)(pshard + 8 * k) * kPU;
-        ulo = psg;
-        uhi = min(sghi, gnext + kPU);
-        more = true;
-        if (lane == 0) ahead = (int)atomicAdd(&heads[pshard], 1u);   // the next claim, ahead
-        ahead_out = true;
-        return;
+        start = psa + (int64_t)(pshard + kPHeads * k) * kPU;
+        break;
       }
-      // this shard is exhausted: read every head (one round trip, at memory side)
-      // and steal from the shard with the most unclaimed units
-      int rem = -1;
-      if (lane < 8) rem = shard_size(lane) - (int)atomicAdd(&heads[lane], 0u);
-      int best = 0, brem = __builtin_amdgcn_readlane(rem, 0);
-#pragma unroll
-      for (int s = 1; s < 8; ++s) {
-        const int r = __builtin_amdgcn_readlane(rem, s);
-        if (r > brem) { brem = r; best = s; }
-      }
-      if (brem <= 0) { more = false; return; }
-      pshard = best;
+      // this shard is exhausted: read every head (plain agent-scope loads, one per lane:
+      // no read-modify-write traffic on the shared heads) and move to a shard with
+      // unclaimed units, the first one at or after a per-block rotation
+      const unsigned hv = __hip_atomic_load(&heads[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t m = __ballot((int)hv < shard_size(lane));
+      if (m == 0ull) break;                        // every unit has been claimed
+      if (tries > (1 << 16)) { pool_err = true; break; }   // never expected
+      const int rot = (bx * 7 + u) & (kPHeads - 1);
+      const uint64_t mr = (m >> rot) | (rot ? m << (64 - rot) : 0ull);
+      pshard = (rot + (int)__builtin_ctzll(mr)) & (kPHeads - 1);
       int kk = 0;
       if (lane == 0) kk = (int)atomicAdd(&heads[pshard], 1u);
       k = __builtin_amdgcn_readfirstlane(kk);
     }
+    if (lane == 0)
+      __hip_atomic_store(&s_punit[u % kPSlots], ((unsigned long long)(u + 1) << 40) | (unsigned long long)start,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
-  if (!more) { in_pool = true; pool_next(); }
+  // published tag of pool unit u's slot (u + 1 once unit u is published)
+  auto slot_tag = [&](int u) -> int {
+    const unsigned long long raw =
+        __hip_atomic_load(&s_punit[u % kPSlots], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __builtin_amdgcn_readfirstlane((int)(uint32_t)(raw >> 40));
+  };
+  // claim pool units up to u, one at a time and in order: unit c is only claimed once
+  // unit c - 1 is published, so "exhausted" at unit c implies it for every later unit
+  // (a wave that sees it may stop). Returns early while another wave's claim is in flight.
+  auto ensure_claimed = [&](int u) {
+    while (true) {
+      const int c = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(&s_pclaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      if (c > u) return;
+      if (c > 0 && slot_tag(c - 1) != c) return;     // unit c - 1 not published yet
+      int won = 0;
+      if (lane == 0) won = atomicCAS(&s_pclaim, c, c + 1) == c;
+      if (__builtin_amdgcn_readfirstlane(won)) claim_unit(c);
+    }
+  };
+  // next 64-row pool sub-unit of the block (claims run kPAhead sub-units ahead)
+  auto pool_draw = [&]() {
+    while (true) {
+      if (!has_pool || pool_done) { more = false; return; }
+      int j = 0;
+      if (lane == 0) j = atomicAdd(&s_pnext, 1);
+      j = __builtin_amdgcn_readfirstlane(j);
+      const int u = j / kPSubs, sub = j % kPSubs;
+      ensure_claimed((j + kPAhead) / kPSubs);
+      unsigned long long v = 0ull;
+      for (int spin = 0;; ++spin) {
+        const unsigned long long raw =
+            __hip_atomic_load(&s_punit[u % kPSlots], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // (readfirstlane returns int: widen through uint32_t, never sign-extend)
+        v = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(raw >> 32)) << 32) |
+            (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)raw);
+        const unsigned long long tag = v >> 40;
+        if (tag == (unsigned long long)(u + 1)) break;
+        if (tag > (unsigned long long)(u + 1) || spin > (1 << 20)) {   // never expected
+          pool_err = true;
+          v = kPExh;
+          break;
+        }
+        ensure_claimed(u);   // the claim of unit u may be waiting for this wave
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const int64_t start = (int64_t)(v & ((1ull << 40) - 1));
+      if (start == kPExh) { pool_done = true; more = false; return; }
+      gnext = start + (int64_t)sub * kPSub;
+      ulo = psg;
+      uhi = min(sghi, gnext + kPSub);
+      if (gnext < uhi) { more = true; return; }
+      // an empty sub-unit past the segment end: draw again
+    }
+  };
+  if (!more) { in_pool = true; pool_draw(); }
 
   // ---- K7: Bernoulli selection of the next work unit, compacted into the ring
   auto refill = [&]() {
@@ -449,17 +510,14 @@ lr_rows_kernel(const LrParams p) {
         if (gi < nq) {
           gnext = gstart + ((int64_t)gi << qs);
           uhi = min(ghi, gnext + ((int64_t)w << qs));
-          // the block's last static unit: claim the first pool unit now, so it is
-          // back before it is needed
-          if (has_pool && !ahead_out && gi + w >= nq) {
-            if (lane == 0) ahead = (int)atomicAdd(&heads[pshard], 1u);
-            ahead_out = true;
-          }
+          // the block's last static unit: have the first pool unit claimed now, so
+          // it is back before it is needed
+          if (has_pool && gi + w >= nq) ensure_claimed(0);
         } else {
           in_pool = true;
         }
       }
-      if (in_pool) pool_next();
+      if (in_pool) pool_draw();
     }
     __builtin_amdgcn_wave_barrier();
   };
@@ -596,6 +654,7 @@ lr_rows_kernel(const LrParams p) {
       compute(A);
     }
   }
+  if (pool_err) cntf = __builtin_nanf("");   // a pool hand-off failed: poison the count
   if (tr && lane == 0) {
     tr[0] = t_start;
     tr[1] = t_first;

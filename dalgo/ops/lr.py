@@ -88,7 +88,7 @@ class _Workspace:
     cnt1: torch.Tensor
     cnt2: torch.Tensor
     ticket: torch.Tensor   # fused-tail arrival counter (re-armed by the kernel)
-    pool: torch.Tensor     # cross-block pool claim heads, 2 parity sets x n_seg x 8 shards
+    pool: torch.Tensor     # cross-block pool claim heads, 2 parity sets x n_seg x 64 shards
     epoch: torch.Tensor    # persistent launches: device step-release counter ...
     perr: torch.Tensor     # ... and its wait-timeout error word
     launches: int = 0      # parity of the next launch = launches & 1
@@ -109,7 +109,7 @@ def _workspace(device, nseg, gx, S) -> _Workspace:
             cnt1=torch.zeros(nseg * ngroups, dtype=torch.int32, device=device),
             cnt2=torch.zeros(nseg, dtype=torch.int32, device=device),
             ticket=torch.zeros(1, dtype=torch.int32, device=device),
-            pool=torch.zeros(2 * nseg * 8, dtype=torch.int32, device=device),
+            pool=torch.zeros(2 * nseg * 64, dtype=torch.int32, device=device),
             epoch=torch.zeros(1, dtype=torch.int32, device=device),
             perr=torch.zeros(1, dtype=torch.int32, device=device),
         )
