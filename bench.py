@@ -42,7 +42,59 @@ def parse(argv=None):
     ap.add_argument("--backend", default=None, choices=["nccl", "gloo"],
                     help="collective backend (default: nccl = RCCL on GPU, gloo on CPU)")
     ap.add_argument("--eval", action="store_true", help="report held-out accuracy after timing")
+    ap.add_argument("--launch", default=os.environ.get("DALGO_LAUNCH", "auto"),
+                    choices=["auto", "env"],
+                    help="auto: time the equivalent SSGD/GD step launch forms (per-step K1 + "
+                         "update/K11, one fused launch per step, one persistent launch per K "
+                         "steps) after the warmup, untimed, and keep the fastest; env: the "
+                         "DALGO_ONE_KERNEL / DALGO_PERSISTENT settings")
+    ap.add_argument("--cal-steps", type=int, default=20, help="steps per candidate (auto)")
     return ap.parse_args(argv)
+
+
+def calibrate_launch(model, rt, a) -> dict:
+    """Pick the fastest launch form of the SAME training step on this node.
+
+    The three forms compute identical steps (tests/test_gpu_multirank.py::
+    test_fused_xgmi_update_matches_process_group); which one is fastest depends on the
+    node (launch latency vs. the xGMI exchange latency the persistent form hides under
+    the next step's first row loads), so it is measured rather than assumed. Runs after
+    the warmup and before the timed region (untimed); every rank times every candidate,
+    the MAX over ranks decides, so all ranks pick the same form. Returns the per-candidate
+    ms/step."""
+    from dalgo.parallel import comm
+    if (a.algo not in ("ssgd", "gd") or model.device.type != "cuda" or not model._zg
+            or model.fused or model._graph_ok() or a.cal_steps <= 0):
+        return {}
+    if comm.world_size() > 1 and model.bucket.xg is None:
+        return {}   # the fused / persistent forms need the K11 exchange on several ranks
+    # ranks sharing one GPU (the one-GPU rehearsals): a rank's in-kernel wait for its peers'
+    # exchange needs the peers' kernels co-resident on the same CUs, which a persistent grid
+    # does not leave room for; the forms are only raced when every rank has its own GPU
+    # (DALGO_CAL_SHARED=1 forces it, for the 2-rank rehearsal test)
+    local_n = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    if local_n > torch.cuda.device_count() and os.environ.get("DALGO_CAL_SHARED", "0") != "1":
+        return {}
+    cands = {"per-step": (False, False), "one-kernel": (True, False), "persistent": (False, True)}
+    res = {}
+    for name, (one, pers) in cands.items():
+        model._ok1, model._okp = one, pers
+        model.run_steps(2)            # first launch of this form (code objects, workspaces)
+        rt.synchronize()
+        rt.barrier()
+        rt.synchronize()
+        t0 = time.perf_counter()
+        model.run_steps(a.cal_steps)
+        rt.synchronize()
+        rt.barrier()
+        rt.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=rt.device)
+        comm.all_reduce_max(el)
+        res[name] = float(el.item()) / a.cal_steps * 1e3
+    comm.check_device_errors("launch calibration")
+    best = min(res, key=res.get)
+    model._ok1, model._okp = cands[best]
+    return res
 
 
 def main(argv=None):
@@ -74,6 +126,7 @@ def main(argv=None):
     # DALGO_PERSISTENT=1) one persistent K1 launch running all k steps
     model.run_steps(a.warmup)
     rt.synchronize()
+    cal = calibrate_launch(model, rt, a) if a.launch == "auto" else {}
     rt.barrier()
     rt.synchronize()
     model.count_acc = count
@@ -90,7 +143,8 @@ def main(argv=None):
     # step releases) first, then raise on EVERY rank (non-zero exit everywhere)
     comm.check_device_errors("bench")
     launch = "persistent" if model._persistent() else (
-        "hipgraph-replay" if model._graph_ok() else "per-step")
+        "hipgraph-replay" if model._graph_ok() else (
+            "one-kernel" if model._one_kernel() else "per-step"))
     allreduce = "xgmi-oneshot (K11)" if xg is not None else (
         f"{rt.backend}" if W > 1 else "none (1 rank)")
 
@@ -125,6 +179,8 @@ def main(argv=None):
             "effective_hbm_GBps_per_gpu": value / W * a.dim * (2 if dtype == torch.bfloat16 else 4) / 1e9,
             "datagen_s": gen_s,
         }
+        if cal:
+            out["launch_calibration_ms_per_step"] = cal
         if acc is not None:
             out["heldout_accuracy"] = acc
         print(json.dumps(out), flush=True)

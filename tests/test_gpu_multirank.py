@@ -110,6 +110,24 @@ def test_fused_xgmi_update_matches_process_group(cuda, algo, one_kernel):
     assert wf.shape == wp.shape and np.allclose(wf, wp, rtol=1e-4, atol=1e-5), (wf[:5], wp[:5])
 
 
+def test_bench_launch_calibration_two_ranks(cuda):
+    """bench.py --launch auto with the K11 exchange: the per-step, one-kernel and
+    persistent forms are each timed on both ranks and one is kept (same on every rank)."""
+    os.environ["DALGO_XGMI"] = "1"
+    os.environ["DALGO_CAL_SHARED"] = "1"
+    try:
+        out = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--rows", "200000",
+                         "--steps", "5", "--warmup", "2", "--cal-steps", "4"])
+    finally:
+        del os.environ["DALGO_XGMI"]
+        del os.environ["DALGO_CAL_SHARED"]
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+    cal = d["launch_calibration_ms_per_step"]
+    assert set(cal) == {"per-step", "one-kernel", "persistent"}
+    assert d["config"]["launch"] == min(cal, key=cal.get)
+    assert d["config"]["allreduce"] == "xgmi-oneshot (K11)" and d["value"] > 0
+
+
 def test_bench_auto_selects_allreduce(cuda):
     """DALGO_XGMI=auto (default): the start-up race picks a path and reports it."""
     out = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--rows", "200000",
