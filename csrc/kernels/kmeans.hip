@@ -1208,7 +1208,9 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
 //          (2-4 % slower than 26), s_setprio on alternate blocks (within 1 %), a form
 //          with the centres resident in VGPRs and the points streamed through LDS
 //          (4.79-5.30 vs 4.42-4.56 ms: the extra norm k-step costs more than the saved
-//          LDS reads)
+//          LDS reads), one 4-wave block per CU with the whole 512-entry register file per
+//          wave and 4-8 point tiles per wave (5.0-5.5 vs 4.14 ms for 52 at 20M: one wave
+//          per SIMD leaves the barrier / LDS / DMA waits exposed)
 template <typename T, int DP>
 static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                    const float* hn, int kpad, int* assign, float* mind, double* sse, int sse_mask,
