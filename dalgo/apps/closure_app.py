@@ -5,7 +5,8 @@ import torch
 
 from dalgo.models.transitive_closure import DenseClosure, SparseClosure, compact_ids
 from dalgo.parallel import runtime
-from dalgo.utils.cli import common_parser, init_from_args
+from dalgo.utils import checkpoint
+from dalgo.utils.cli import add_ckpt_args, common_parser, init_from_args
 
 TOY_EDGES = [(1, 2), (1, 3), (2, 3), (3, 1)]   # transitive_closure.py:18
 
@@ -15,6 +16,9 @@ def main(argv=None):
     ap.add_argument("--engine", choices=["auto", "dense", "sparse"], default="auto")
     ap.add_argument("--edges", default=None)
     ap.add_argument("--random", default=None, metavar="N,E", help="random graph with N vertices, E edges")
+    ap.add_argument("--max-rounds", type=int, default=1 << 30,
+                    help="stop after this many join rounds (resume later with --resume)")
+    add_ckpt_args(ap)
     a = ap.parse_args(argv)
     rt = init_from_args(a, "Transitive Closure")
     if a.random:
@@ -35,9 +39,29 @@ def main(argv=None):
         tc = DenseClosure(s, d, n, rt.rank, rt.world_size, device=rt.device)
     else:
         tc = SparseClosure(s, d, rt.rank, rt.world_size, n=n, device=rt.device)
-    res = tc.run()
+    # per-rank state (each rank owns the paths of its target slice)
+    name = f"closure_{engine}_w{rt.world_size}"
+    if a.resume and a.ckpt_dir:
+        sd = checkpoint.load(a.ckpt_dir, name, rt.rank, per_rank=True)
+        if sd is not None:
+            tc.load_state_dict(sd)
+            rt.log("resumed after %d rounds" % (len(tc.counts) - 1))
+
+    def save(m):
+        checkpoint.save(m.state_dict(), a.ckpt_dir, name, rt.rank, per_rank=True)
+
+    def cb(m):
+        if a.ckpt_dir and a.ckpt_every and (len(m.counts) - 1) % a.ckpt_every == 0:
+            save(m)
+
+    res = tc.run(a.max_rounds, callback=cb)
+    if a.ckpt_dir:
+        save(tc)
     if not a.quiet:
         rt.log("path counts per round: %s" % res.counts)
+    if not tc.converged:
+        rt.log("stopped after %d rounds before the fixpoint (--max-rounds); continue with --resume"
+               % (len(res.counts) - 1))
     rt.log("The original graph has %i paths" % res.n_paths)   # transitive_closure.py:42 (sic)
     runtime.shutdown()
     return res

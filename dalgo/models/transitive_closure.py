@@ -18,6 +18,7 @@ from __future__ import annotations
 import os
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 
 from dalgo.ops import _ext
@@ -48,7 +49,37 @@ def _round_up(a, b):
     return (a + b - 1) // b * b
 
 
-class DenseClosure:
+class _Fixpoint:
+    """Shared fixpoint driver (transitive_closure.py:31-40) with resumable state: the
+    per-round counts travel with the path set in ``state_dict`` (checkpoint/resume,
+    SURVEY §5), so a resumed run continues the same trajectory."""
+    counts: list
+
+    def _initial_count(self) -> int:
+        raise NotImplementedError
+
+    def run(self, max_rounds: int = 1 << 30, callback=None) -> ClosureResult:
+        if not self.counts:
+            self.counts = [self._initial_count()]
+        cnt = self.counts[-1]
+        done = len(self.counts) > 1 and self.counts[-1] == self.counts[-2]
+        rounds = 0
+        while not done and rounds < max_rounds:
+            nxt = self.step()
+            self.counts.append(nxt)
+            rounds += 1
+            done = nxt == cnt
+            cnt = nxt
+            if callback is not None:
+                callback(self)
+        return ClosureResult(cnt, list(self.counts))
+
+    @property
+    def converged(self) -> bool:
+        return len(self.counts) > 1 and self.counts[-1] == self.counts[-2]
+
+
+class DenseClosure(_Fixpoint):
     def __init__(self, src: torch.Tensor, dst: torch.Tensor, n: int, rank: int = 0, world: int = 1,
                  device="cpu"):
         dev = torch.device(device)
@@ -71,6 +102,7 @@ class DenseClosure:
         self.T[dst[m] - self.z_lo, src[m]] = 1            # T[z][x] = P[x][z]
         self.T2 = torch.zeros_like(self.T)
         self.count = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.counts: list = []
 
     def nnz(self) -> int:
         c = (self.T != 0).sum().reshape(1).to(torch.int64)
@@ -87,20 +119,26 @@ class DenseClosure:
         self.T, self.T2 = self.T2, self.T
         return comm.all_reduce_count(self.count)
 
-    def run(self, max_rounds: int = 1 << 30) -> ClosureResult:
-        cnt = self.nnz()
-        res = ClosureResult(cnt, [cnt])
-        for _ in range(max_rounds):
-            nxt = self.step()
-            res.counts.append(nxt)
-            if nxt == cnt:
-                break
-            cnt = nxt
-        res.n_paths = cnt
-        return res
+    def _initial_count(self) -> int:
+        return self.nnz()
+
+    def state_dict(self) -> dict:
+        """This rank's slice of P^T, bit-packed (n^2 / 8 bytes for the whole graph)."""
+        bits = np.packbits((self.T != 0).cpu().numpy(), axis=1)
+        return {"engine": "dense", "n": self.n, "z_lo": self.z_lo, "z_hi": self.z_hi,
+                "nz": self.nz, "npad": self.npad, "T_bits": torch.from_numpy(bits),
+                "counts": torch.tensor(self.counts, dtype=torch.int64)}
+
+    def load_state_dict(self, sd: dict):
+        if sd.get("engine") != "dense" or (sd["n"], sd["z_lo"], sd["z_hi"], sd["npad"]) != \
+                (self.n, self.z_lo, self.z_hi, self.npad):
+            raise ValueError("checkpoint is for a different graph or rank partition")
+        t = np.unpackbits(sd["T_bits"].numpy(), axis=1, count=self.npad)
+        self.T.copy_(torch.from_numpy(t).to(self.T.dtype))
+        self.counts = [int(c) for c in sd["counts"].tolist()]
 
 
-class SparseClosure:
+class SparseClosure(_Fixpoint):
     def __init__(self, src: torch.Tensor, dst: torch.Tensor, rank: int = 0, world: int = 1,
                  n: int | None = None, device="cpu"):
         dev = torch.device(device)
@@ -120,6 +158,8 @@ class SparseClosure:
         z = keys & 0xFFFFFFFF
         self.P = keys[(z % world) == rank]
         self.delta = self.P
+        self.rank, self.world = rank, world
+        self.counts: list = []
 
     def _join(self, delta: torch.Tensor) -> torch.Tensor:
         y = delta >> 32
@@ -143,14 +183,19 @@ class SparseClosure:
         self.delta = new
         return comm.all_reduce_count(self.P.numel(), device=self.dev)
 
-    def run(self, max_rounds: int = 1 << 30) -> ClosureResult:
-        cnt = comm.all_reduce_count(self.P.numel(), device=self.dev)
-        res = ClosureResult(cnt, [cnt])
-        for _ in range(max_rounds):
-            nxt = self.step()
-            res.counts.append(nxt)
-            if nxt == cnt:
-                break
-            cnt = nxt
-        res.n_paths = cnt
-        return res
+    def _initial_count(self) -> int:
+        return comm.all_reduce_count(self.P.numel(), device=self.dev)
+
+    def state_dict(self) -> dict:
+        """This rank's path set and last round's new paths (semi-naive frontier)."""
+        return {"engine": "sparse", "n": self.n, "rank": self.rank, "world": self.world,
+                "P": self.P.cpu(), "delta": self.delta.cpu(),
+                "counts": torch.tensor(self.counts, dtype=torch.int64)}
+
+    def load_state_dict(self, sd: dict):
+        if sd.get("engine") != "sparse" or (sd["n"], sd["rank"], sd["world"]) != \
+                (self.n, self.rank, self.world):
+            raise ValueError("checkpoint is for a different graph or rank partition")
+        self.P = sd["P"].to(self.dev)
+        self.delta = sd["delta"].to(self.dev)
+        self.counts = [int(c) for c in sd["counts"].tolist()]

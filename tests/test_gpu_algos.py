@@ -288,6 +288,15 @@ def test_transitive_closure_gpu(cuda):
     s4 = torch.tensor([0, 0, 1, 2])
     d4 = torch.tensor([1, 2, 2, 0])
     assert DenseClosure(s4, d4, 3, device=cuda).run().counts == [4, 8, 9, 9]
+    # checkpoint after 3 rounds (bit-packed P^T slice / sparse path set), resume in a fresh
+    # instance: the same trajectory as the uninterrupted run
+    for cls in (DenseClosure, SparseClosure):
+        kw = dict(n=n, device=cuda)
+        a = cls(src, dst, **kw) if cls is SparseClosure else cls(src, dst, n, device=cuda)
+        a.run(max_rounds=3)
+        b = cls(src, dst, **kw) if cls is SparseClosure else cls(src, dst, n, device=cuda)
+        b.load_state_dict(a.state_dict())
+        assert b.run().counts == ref, cls.__name__
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3])
