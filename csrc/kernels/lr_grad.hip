@@ -99,6 +99,25 @@ struct LrParams {
   uint32_t epoch_base;
   unsigned* perr;
   uint64_t spin_ticks;
+  // count-balanced block ranges (SSGD, one segment, atomic epilogue; nullptr = off).
+  // Selection is keyed by (seed, step, row) only, so the minibatch of step t + 2 is known
+  // two steps early: launch t counts it per 64-row bucket (fine, plain stores; every
+  // bucket lies inside one 64-aligned work unit) and per 4096 rows (coarse, atomics into
+  // a buffer the launch before zeroed), and each block's wave 0 turns the counts of step
+  // t + 1 (complete since launch t - 1) into the start row of block bx for step t + 1:
+  // the 64-row bucket holding selected row number bx * T / gx. Launch t + 1 then reads
+  // its range [r_cur[bx], r_cur[bx + 1]) instead of the static rows_per_block split, so
+  // every block streams the same number of selected rows (+- one bucket) instead of
+  // mean +- sqrt(mean).
+  int* bal_fine_w;        // [nf]  step + 2 counts per 64 rows (written)
+  int* bal_coarse_w;      // [nc]  step + 2 counts per 4096 rows (accumulated; zero on entry)
+  int* bal_coarse_z;      // [nc]  zeroed here for step + 3
+  const int* bal_fine_r;  // [nf]  step + 1 counts (read by wave 0)
+  const int* bal_coarse_r;
+  int* bal_r_next;        // [gx + 1] block start rows for step + 1
+  const int* bal_r_cur;   // [gx + 1] block start rows for this step (nullptr: static split)
+  int bal_nf, bal_nc;
+  int64_t bal_n;          // local rows of the segment
 };
 
 __device__ __forceinline__ void wt_store(float* a, float v) {
@@ -249,8 +268,13 @@ lr_rows_kernel(const LrParams p) {
   const int bx = blockIdx.x;
   const int gx = gridDim.x;
   const int64_t seg_lo = p.seg[seg], seg_hi = p.seg[seg + 1];
-  const int64_t lo = seg_lo + (int64_t)bx * p.rows_per_block;
-  const int64_t hi = max(lo, min(seg_hi, lo + (int64_t)p.rows_per_block));
+  const int64_t lo = p.bal_r_cur != nullptr ? seg_lo + p.bal_r_cur[bx]
+                                            : seg_lo + (int64_t)bx * p.rows_per_block;
+  const int64_t hi = p.bal_r_cur != nullptr
+                         ? max(lo, min(seg_hi, seg_lo + (int64_t)p.bal_r_cur[bx + 1]))
+                         : max(lo, min(seg_hi, lo + (int64_t)p.rows_per_block));
+  if (p.bal_coarse_z != nullptr)
+    for (int i = bx * NW * 64 + (int)threadIdx.x; i < p.bal_nc; i += gx * NW * 64) p.bal_coarse_z[i] = 0;
   // ---- step loop (one iteration unless persistent: p.nsteps > 1)
   // (a separate instantiation: the step loop costs registers the one-step kernel keeps)
   const int nst = PERSIST && p.nsteps > 1 ? p.nsteps : 1;
@@ -473,6 +497,83 @@ lr_rows_kernel(const LrParams p) {
   };
   if (!more) { in_pool = true; pool_draw(); }
 
+  // count-balanced ranges: selected rows of step + 2 in this unit, per 64-row bucket (16
+  // lanes x 4 rows; units start 64-aligned in local rows, so a bucket never straddles two)
+  auto bal_count = [&](int64_t r0) {
+    u32x4 h2{0u, 0u, 0u, 0u};
+    if (r0 < uhi) h2 = philox_block(p.seed, step_cur + 2, (uint64_t)r0 >> 2);
+    const uint32_t hv2[4] = {h2.x, h2.y, h2.z, h2.w};
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c += (r0 + j >= ulo && r0 + j < uhi && hv2[j] < p.thr) ? 1 : 0;
+    c += __shfl_xor(c, 1);
+    c += __shfl_xor(c, 2);
+    c += __shfl_xor(c, 4);
+    c += __shfl_xor(c, 8);
+    const int64_t b0 = r0;   // lane 16q: r0 = unit start + 64q
+    if ((lane & 15) == 0 && b0 >= ulo && b0 < uhi) {
+      const int64_t lb = (b0 - p.row_offset) >> 6;
+      if (lb >= 0 && lb < p.bal_nf) {
+        p.bal_fine_w[lb] = c;
+        if (c) atomicAdd(&p.bal_coarse_w[lb >> 6], c);
+      }
+    }
+  };
+  // wave 0: start row of this block for step + 1 from the step + 1 counts (three rounds:
+  // coarse chunk sums per lane, the owning chunk's coarse buckets, its 64 fine buckets)
+  auto bal_boundary = [&]() {
+    const int nc = p.bal_nc, nf = p.bal_nf;
+    const int64_t n = p.bal_n;
+    int64_t R = 0;
+    if (bx > 0) {
+      const int per = (nc + 63) >> 6;   // <= 64 (host check)
+      uint32_t sum = 0;
+      for (int i = 0; i < per; ++i) {
+        const int idx = lane * per + i;
+        if (idx < nc) sum += (uint32_t)p.bal_coarse_r[idx];
+      }
+      auto scan = [&](uint32_t v) {
+        uint32_t inc = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const uint32_t t = __shfl_up(inc, off);
+          if (lane >= off) inc += t;
+        }
+        return inc;
+      };
+      const uint32_t inc = scan(sum);
+      const uint64_t tot = (uint64_t)__shfl(inc, 63);
+      if (tot == 0) {
+        R = min(n, (int64_t)bx * p.rows_per_block);   // nothing selected: static split
+      } else {
+        const uint64_t A = (uint64_t)bx * tot / (uint64_t)gx;   // < tot
+        const uint32_t exc = inc - sum;
+        const uint64_t m1 = __ballot((uint64_t)exc <= A && A < (uint64_t)inc);
+        const int l1 = m1 ? __builtin_ctzll(m1) : 63;
+        const uint32_t base1 = __shfl(exc, l1);
+        const int cidx = l1 * per + lane;
+        const bool cok = lane < per && cidx < nc;
+        const uint32_t v2 = cok ? (uint32_t)p.bal_coarse_r[cidx] : 0u;
+        const uint32_t inc2 = base1 + scan(v2), exc2 = inc2 - v2;
+        const uint64_t m2 = __ballot(cok && (uint64_t)exc2 <= A && A < (uint64_t)inc2);
+        const int l2 = m2 ? __builtin_ctzll(m2) : 0;
+        const int cb = l1 * per + l2;
+        const uint32_t base2 = __shfl(exc2, l2);
+        const int fidx = cb * 64 + lane;
+        const bool fok = fidx < nf;
+        const uint32_t v3 = fok ? (uint32_t)p.bal_fine_r[fidx] : 0u;
+        const uint32_t inc3 = base2 + scan(v3), exc3 = inc3 - v3;
+        const uint64_t m3 = __ballot(fok && (uint64_t)exc3 <= A && A < (uint64_t)inc3);
+        const int l3 = m3 ? __builtin_ctzll(m3) : 0;
+        R = min(n, ((int64_t)cb * 64 + l3) * 64);
+      }
+    }
+    if (lane == 0) {
+      p.bal_r_next[bx] = (int)R;
+      if (bx == gx - 1) p.bal_r_next[gx] = (int)n;
+    }
+  };
+
   // ---- K7: Bernoulli selection of the next work unit, compacted into the ring
   auto refill = [&]() {
     while ((tail - head) < (uint32_t)(2 * U) && more) {
@@ -480,6 +581,9 @@ lr_rows_kernel(const LrParams p) {
       u32x4 h{0u, 0u, 0u, 0u};
       if (!p.full && !EVAL && r0 < uhi) h = philox_block(p.seed, step_cur, (uint64_t)r0 >> 2);
       const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
+      if constexpr (!EVAL && !PERSIST) {
+        if (p.bal_fine_w != nullptr) bal_count(r0);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int64_t gr = r0 + j;
@@ -626,6 +730,9 @@ lr_rows_kernel(const LrParams p) {
   // ---- software-pipelined sweep: load(i+1) || compute(i)
   Batch<NC, U> A;
   unsigned long long t_first = 0ull, t_refill = 0ull;
+  // wave 0 computes the block's step + 1 start row once its first batch is computed (its
+  // loads then overlap the sweep; a wave 0 without rows does it after the loop)
+  bool bal_todo = !EVAL && !PERSIST && p.bal_r_next != nullptr && wid == 0;
   if constexpr (PIPE) {
     Batch<NC, U> B;
     refill();
@@ -639,6 +746,7 @@ lr_rows_kernel(const LrParams p) {
       refill();
       take_and_load(B);
       compute(A);
+      if (bal_todo) { bal_todo = false; bal_boundary(); }
       if (B.n == 0) break;
       refill();
       take_and_load(A);
@@ -654,6 +762,7 @@ lr_rows_kernel(const LrParams p) {
       compute(A);
     }
   }
+  if (bal_todo) bal_boundary();
   if (pool_err) cntf = __builtin_nanf("");   // a pool hand-off failed: poison the count
   if (tr && lane == 0) {
     tr[0] = t_start;
@@ -895,8 +1004,25 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
                          float upd_reg_alpha, double* count_acc, const DalgoLrTail* tail,
                          unsigned* pool, int pool_parity, const int64_t* step_dev,
-                         int64_t step_mul, hipStream_t st) {
+                         int64_t step_mul, const DalgoLrBal* bal, hipStream_t st) {
   LrParams p{};
+  if (bal != nullptr) {
+    // balanced ranges: one segment, sampled rows, atomic epilogue, no pool / graph step /
+    // prologue update / persistent steps; 64-aligned units need 4-aligned global rows
+    const int64_t nf = cdiv(bal->n, (int64_t)64), nc = cdiv(nf, (int64_t)64);
+    if (nseg != 1 || full || !((variant >> 8) & 1) || pool != nullptr || step_dev != nullptr ||
+        Wprev != nullptr || (tail != nullptr && tail->nsteps > 1) || row_offset % 4 != 0 ||
+        rows_per_block % 64 != 0 || bal->n <= 0 || bal->n >= (1ll << 31) || bal->nf != nf ||
+        bal->nc != nc || nc > 4096 || bal->fine_w == nullptr || bal->coarse_w == nullptr ||
+        bal->coarse_z == nullptr || bal->r_next == nullptr ||
+        ((bal->fine_r == nullptr) != (bal->coarse_r == nullptr)))
+      return hipErrorInvalidValue;
+    p.bal_fine_w = bal->fine_w; p.bal_coarse_w = bal->coarse_w; p.bal_coarse_z = bal->coarse_z;
+    p.bal_fine_r = bal->fine_r; p.bal_coarse_r = bal->coarse_r;
+    p.bal_r_next = bal->fine_r != nullptr ? bal->r_next : nullptr;
+    p.bal_r_cur = bal->r_cur;
+    p.bal_nf = (int)nf; p.bal_nc = (int)nc; p.bal_n = bal->n;
+  }
   p.step_dev = step_dev;
   p.step_mul = step_mul;
   if (tail != nullptr) {
