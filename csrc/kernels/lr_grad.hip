@@ -239,6 +239,7 @@ constexpr int kRing = 512;   // per-wave ring of selected local row indices
 // block's waves as 64-row sub-units; unit claims run kPAhead sub-units ahead of use
 constexpr int kPU = 512, kPSub = 64, kPSubs = kPU / kPSub, kPAhead = 4, kPSlots = 8;
 constexpr int kPHeads = 64;                  // claim heads (shards) per segment; one per lane
+constexpr int kBalCap = 2048;                // balanced ranges: LDS bucket counts per block
 constexpr int64_t kPExh = (1ll << 40) - 1;   // "pool exhausted" marker
 
 template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, bool PERSIST, int AUX = 0>
@@ -258,6 +259,8 @@ lr_rows_kernel(const LrParams p) {
   // claim (block-local order), and the claimed units ((u + 1) << 40 | first global row)
   __shared__ int s_pnext, s_pclaim;
   __shared__ unsigned long long s_punit[kPSlots];
+  // balanced ranges: per-64-row selected counts of step + 2 for this block's range
+  __shared__ unsigned s_bcnt[(EVAL || PERSIST) ? 1 : kBalCap];
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -392,6 +395,10 @@ lr_rows_kernel(const LrParams p) {
       __hip_atomic_store(p.pool + (int64_t)(p.pool_parity ^ 1) * gridDim.y * kPHeads + i, 0u,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (threadIdx.x < kPSlots) s_punit[threadIdx.x] = 0ull;
+  if constexpr (!EVAL && !PERSIST) {
+    if (p.bal_fine_w != nullptr)
+      for (int i = threadIdx.x; i < kBalCap; i += NW * 64) s_bcnt[i] = 0u;
+  }
   if (threadIdx.x == 0) { s_pnext = 0; s_pclaim = 0; }
   __syncthreads();
   const unsigned long long t_bar = tr ? (unsigned long long)__builtin_amdgcn_s_memrealtime() : 0ull;
@@ -497,8 +504,12 @@ lr_rows_kernel(const LrParams p) {
   };
   if (!more) { in_pool = true; pool_draw(); }
 
-  // count-balanced ranges: selected rows of step + 2 in this unit, per 64-row bucket (16
-  // lanes x 4 rows; units start 64-aligned in local rows, so a bucket never straddles two)
+  // count-balanced ranges: selected rows of step + 2 in this unit, per 64-row bucket,
+  // accumulated in LDS (s_bcnt, bucket index relative to the 64-aligned block start) and
+  // written out after the sweep: a global store or atomic here would sit in the wave's
+  // in-order vmcnt queue and stall the row pipeline behind it. Buckets past kBalCap (a
+  // block range of > kBalCap * 64 rows, only at very small sampling rates) take the slow
+  // path: 16-lane sum and a direct global store / atomic.
   auto bal_count = [&](int64_t r0) {
     u32x4 h2{0u, 0u, 0u, 0u};
     if (r0 < uhi) h2 = philox_block(p.seed, step_cur + 2, (uint64_t)r0 >> 2);
@@ -506,17 +517,41 @@ lr_rows_kernel(const LrParams p) {
     int c = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) c += (r0 + j >= ulo && r0 + j < uhi && hv2[j] < p.thr) ? 1 : 0;
+    const int64_t lbb = (gnext - glo) >> 6;   // block-local bucket of lanes 0..15
+    if (lbb + 4 <= kBalCap) {
+      if (c) atomicAdd(&s_bcnt[lbb + (lane >> 4)], (unsigned)c);
+      return;
+    }
     c += __shfl_xor(c, 1);
     c += __shfl_xor(c, 2);
     c += __shfl_xor(c, 4);
     c += __shfl_xor(c, 8);
-    const int64_t b0 = r0;   // lane 16q: r0 = unit start + 64q
-    if ((lane & 15) == 0 && b0 >= ulo && b0 < uhi) {
-      const int64_t lb = (b0 - p.row_offset) >> 6;
+    if ((lane & 15) == 0 && r0 >= ulo && r0 < uhi) {
+      const int64_t lb = (r0 - p.row_offset) >> 6;
       if (lb >= 0 && lb < p.bal_nf) {
-        p.bal_fine_w[lb] = c;
-        if (c) atomicAdd(&p.bal_coarse_w[lb >> 6], c);
+        if (lbb + (lane >> 4) < kBalCap) atomicAdd(&s_bcnt[lbb + (lane >> 4)], (unsigned)c);
+        else {
+          p.bal_fine_w[lb] = c;
+          if (c) atomicAdd(&p.bal_coarse_w[lb >> 6], c);
+        }
       }
+    }
+  };
+  // after the sweep: the block's LDS bucket counts -> fine (stores) and coarse (one
+  // wave-reduced atomic per 4096-row bucket the block touches)
+  auto bal_flush = [&]() {
+    const int64_t fb0 = (glo - p.row_offset) >> 6;            // first global fine bucket
+    const int nb = (int)min((int64_t)kBalCap, (ghi - glo + 63) >> 6);
+    for (int i = threadIdx.x; i < nb; i += NW * 64)
+      if (fb0 + i < p.bal_nf) p.bal_fine_w[fb0 + i] = (int)s_bcnt[i];
+    if (nb == 0) return;
+    const int64_t c0 = fb0 >> 6, c1 = (fb0 + nb - 1) >> 6;   // coarse buckets touched
+    for (int64_t c = c0 + wid; c <= c1; c += NW) {
+      const int64_t f = c * 64 + lane - fb0;                  // block-local fine bucket
+      unsigned v = (f >= 0 && f < nb) ? s_bcnt[f] : 0u;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0 && v) atomicAdd(&p.bal_coarse_w[c], (int)v);
     }
   };
   // wave 0: start row of this block for step + 1 from the step + 1 counts (three rounds:
@@ -730,8 +765,7 @@ lr_rows_kernel(const LrParams p) {
   // ---- software-pipelined sweep: load(i+1) || compute(i)
   Batch<NC, U> A;
   unsigned long long t_first = 0ull, t_refill = 0ull;
-  // wave 0 computes the block's step + 1 start row once its first batch is computed (its
-  // loads then overlap the sweep; a wave 0 without rows does it after the loop)
+  // wave 0 computes the block's step + 1 start row right after issuing its first batch
   bool bal_todo = !EVAL && !PERSIST && p.bal_r_next != nullptr && wid == 0;
   if constexpr (PIPE) {
     Batch<NC, U> B;
@@ -741,12 +775,13 @@ lr_rows_kernel(const LrParams p) {
     if (PERSIST && it > 0 && !wait_epoch(it)) return;
     load_w();
     if (tr) t_first = __builtin_amdgcn_s_memrealtime();
+    // wave 0: the block's step + 1 start row, under the first batch's HBM latency
+    if (bal_todo) { bal_todo = false; bal_boundary(); }
     while (true) {
       if (A.n == 0) break;
       refill();
       take_and_load(B);
       compute(A);
-      if (bal_todo) { bal_todo = false; bal_boundary(); }
       if (B.n == 0) break;
       refill();
       take_and_load(A);
@@ -774,6 +809,9 @@ lr_rows_kernel(const LrParams p) {
     tr[7] = t_refill;
   }
   __syncthreads();   // rings are dead: the arena becomes the reduction buffer
+  if constexpr (!EVAL && !PERSIST) {
+    if (p.bal_fine_w != nullptr) bal_flush();
+  }
   if (p.probe_no_epilogue) {
     if (threadIdx.x == 0 && cntf < 0.f) p.C[0] = cntf + gb;   // keep the sweep live
     continue;
