@@ -30,10 +30,6 @@ def main():
     args = sys.argv[1:]
     fines = [0]
     frac = 0.1
-    # --balance: count-balanced block ranges (consecutive steps, so the traced launch
-    # consumes ranges computed by the launch before it)
-    bal = "--balance" in args
-    args = [a for a in args if a != "--balance"]
     if "--frac" in args:
         i = args.index("--frac")
         frac = float(args[i + 1])
@@ -56,14 +52,14 @@ def main():
         gx, _ = L._grid(rows, 1)
         res = []
         for rep in range(6):
-            for i in range(45, 50):
+            for i in range(5):
                 L.lr_grad(X, y, W, seg, D=1024, frac=frac, step=100 * rep + i, G=G, C=C, g_is_zero=True,
-                          variant=var, balance=bal)
+                          variant=var)
             buf.zero_()
             torch.cuda.synchronize()
             ops.lr_set_trace(buf)
             L.lr_grad(X, y, W, seg, D=1024, frac=frac, step=100 * rep + 50, G=G, C=C, g_is_zero=True,
-                      variant=var, balance=bal)
+                      variant=var)
             ops.lr_set_trace(None)
             torch.cuda.synchronize()
             t = buf[: gx * NW * 8].view(gx, NW, 8).cpu().double()
@@ -108,8 +104,7 @@ def main():
                 "cus": len(set(t[:, :, 5].flatten().tolist())),
             })
         med = {k: round(sorted(r[k] for r in res)[len(res) // 2], 2) for k in res[0]}
-        print(json.dumps({"rows": rows, "frac": frac, "fine": fine, "balance": bal, "blocks": gx, **med}),
-              flush=True)
+        print(json.dumps({"rows": rows, "frac": frac, "fine": fine, "blocks": gx, **med}), flush=True)
 
 
 if __name__ == "__main__":

@@ -85,41 +85,8 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
              const std::optional<Tensor>& pool, int64_t pool_parity, int64_t nsteps,
              const std::optional<Tensor>& epoch, int64_t epoch_base,
              const std::optional<Tensor>& perr, double spin_s,
-             const std::optional<Tensor>& step_dev, int64_t step_mul,
-             const std::optional<Tensor>& bal, int64_t bal_flags, int64_t bal_n) {
+             const std::optional<Tensor>& step_dev, int64_t step_mul) {
   check_lr_inputs(X, y, W, seg, D, has_bias);
-  // count-balanced ranges: one int32 workspace [fine x2 | coarse x3 | r x2], slots picked by
-  // the step (fine: written (step+2)%2, read (step+1)%2; coarse: written (step+2)%3, read
-  // (step+1)%3, zeroed step%3; r: read step%2, written (step+1)%2). bal_flags: 1 = use
-  // r_cur, 2 = the step + 1 counts are complete (compute r_next)
-  DalgoLrBal balp{};
-  const DalgoLrBal* balptr = nullptr;
-  if (bal.has_value()) {
-    check_dev(*bal, "bal");
-    TORCH_CHECK(step >= 0, "balanced ranges: step >= 0");
-    const int64_t nf = (bal_n + 63) / 64, nc = (nf + 63) / 64;
-    TORCH_CHECK(bal->scalar_type() == at::kInt && bal->is_contiguous() &&
-                    bal->numel() >= 2 * nf + 3 * nc + 2 * (gx + 1) && bal_n == X.size(0),
-                "bal: int32 workspace [2 nf + 3 nc + 2 (gx + 1)] for X.size(0) rows");
-    int* b = bal->data_ptr<int>();
-    int* fine = b;
-    int* coarse = b + 2 * nf;
-    int* r = coarse + 3 * nc;
-    const int64_t t = step;
-    balp.fine_w = fine + ((t + 2) % 2) * nf;
-    balp.coarse_w = coarse + ((t + 2) % 3) * nc;
-    balp.coarse_z = coarse + (t % 3) * nc;
-    if (bal_flags & 2) {
-      balp.fine_r = fine + ((t + 1) % 2) * nf;
-      balp.coarse_r = coarse + ((t + 1) % 3) * nc;
-    }
-    balp.r_next = r + ((t + 1) % 2) * (gx + 1);
-    balp.r_cur = (bal_flags & 1) ? r + (t % 2) * (gx + 1) : nullptr;
-    balp.nf = (int)nf;
-    balp.nc = (int)nc;
-    balp.n = bal_n;
-    balptr = &balp;
-  }
   const int64_t* stepp = nullptr;
   if (step_dev.has_value()) {
     check_dev(*step_dev, "step_dev");
@@ -224,7 +191,7 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
                     reinterpret_cast<unsigned*>(cnt2.data_ptr<int>()), G.data_ptr<float>(),
                     C.data_ptr<float>(), (int)S, (int)variant, wprev, (int)upd_mode, (int)upd_reg,
                     (float)upd_eta, (float)upd_lam, (float)upd_reg_alpha, cacc, tailp, poolp,
-                    (int)(pool_parity & 1), stepp, step_mul, balptr, cur_stream()),
+                    (int)(pool_parity & 1), stepp, step_mul, cur_stream()),
       "lr_grad");
 }
 
@@ -819,8 +786,7 @@ TORCH_LIBRARY(dalgo, m) {
         "float tail_eta=0., float tail_lam=0., float tail_reg_alpha=0., "
         "Tensor(j!)? tail_count_acc=None, Tensor(k!)? pool=None, int pool_parity=0, int nsteps=1, "
         "Tensor(l!)? epoch=None, int epoch_base=0, Tensor(m!)? perr=None, float spin_s=2., "
-        "Tensor? step_dev=None, int step_mul=1, Tensor(n!)? bal=None, int bal_flags=0, "
-        "int bal_n=0) -> ()");
+        "Tensor? step_dev=None, int step_mul=1) -> ()");
   m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
         "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=3) -> ()");
   m.def("sync_update(Tensor(a!) W, Tensor(d!)? G, Tensor(e!)? C, Tensor? center, Tensor? S, "

@@ -77,6 +77,7 @@ struct LrParams {
   int pool_parity;        // this launch uses set `parity` and re-arms the other one
   int fine_q;             // work claims switch from 256-row groups to 64-row quarters once
                           // fewer than fine_q quarters of the block are unclaimed (0 = never)
+  int unit_shift;         // sampling: work units of 2^unit_shift rows (2..8; fine claims take one)
   // diagnostics only (dalgo_lr_set_trace): per-wave timeline, 8 u64 per wave at
   // [(block * NW + wave) * 8]: start, first row batch issued, sweep done, epilogue
   // done (s_memrealtime, 100 MHz), selected rows, hardware CU/SE id
@@ -99,25 +100,6 @@ struct LrParams {
   uint32_t epoch_base;
   unsigned* perr;
   uint64_t spin_ticks;
-  // count-balanced block ranges (SSGD, one segment, atomic epilogue; nullptr = off).
-  // Selection is keyed by (seed, step, row) only, so the minibatch of step t + 2 is known
-  // two steps early: launch t counts it per 64-row bucket (fine, plain stores; every
-  // bucket lies inside one 64-aligned work unit) and per 4096 rows (coarse, atomics into
-  // a buffer the launch before zeroed), and each block's wave 0 turns the counts of step
-  // t + 1 (complete since launch t - 1) into the start row of block bx for step t + 1:
-  // the 64-row bucket holding selected row number bx * T / gx. Launch t + 1 then reads
-  // its range [r_cur[bx], r_cur[bx + 1]) instead of the static rows_per_block split, so
-  // every block streams the same number of selected rows (+- one bucket) instead of
-  // mean +- sqrt(mean).
-  int* bal_fine_w;        // [nf]  step + 2 counts per 64 rows (written)
-  int* bal_coarse_w;      // [nc]  step + 2 counts per 4096 rows (accumulated; zero on entry)
-  int* bal_coarse_z;      // [nc]  zeroed here for step + 3
-  const int* bal_fine_r;  // [nf]  step + 1 counts (read by wave 0)
-  const int* bal_coarse_r;
-  int* bal_r_next;        // [gx + 1] block start rows for step + 1
-  const int* bal_r_cur;   // [gx + 1] block start rows for this step (nullptr: static split)
-  int bal_nf, bal_nc;
-  int64_t bal_n;          // local rows of the segment
 };
 
 __device__ __forceinline__ void wt_store(float* a, float v) {
@@ -239,7 +221,6 @@ constexpr int kRing = 512;   // per-wave ring of selected local row indices
 // block's waves as 64-row sub-units; unit claims run kPAhead sub-units ahead of use
 constexpr int kPU = 512, kPSub = 64, kPSubs = kPU / kPSub, kPAhead = 4, kPSlots = 8;
 constexpr int kPHeads = 64;                  // claim heads (shards) per segment; one per lane
-constexpr int kBalCap = 2048;                // balanced ranges: LDS bucket counts per block
 constexpr int64_t kPExh = (1ll << 40) - 1;   // "pool exhausted" marker
 
 template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, bool PERSIST, int AUX = 0>
@@ -259,8 +240,6 @@ lr_rows_kernel(const LrParams p) {
   // claim (block-local order), and the claimed units ((u + 1) << 40 | first global row)
   __shared__ int s_pnext, s_pclaim;
   __shared__ unsigned long long s_punit[kPSlots];
-  // balanced ranges: per-64-row selected counts of step + 2 for this block's range
-  __shared__ unsigned s_bcnt[(EVAL || PERSIST) ? 1 : kBalCap];
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -271,13 +250,8 @@ lr_rows_kernel(const LrParams p) {
   const int bx = blockIdx.x;
   const int gx = gridDim.x;
   const int64_t seg_lo = p.seg[seg], seg_hi = p.seg[seg + 1];
-  const int64_t lo = p.bal_r_cur != nullptr ? seg_lo + p.bal_r_cur[bx]
-                                            : seg_lo + (int64_t)bx * p.rows_per_block;
-  const int64_t hi = p.bal_r_cur != nullptr
-                         ? max(lo, min(seg_hi, seg_lo + (int64_t)p.bal_r_cur[bx + 1]))
-                         : max(lo, min(seg_hi, lo + (int64_t)p.rows_per_block));
-  if (p.bal_coarse_z != nullptr)
-    for (int i = bx * NW * 64 + (int)threadIdx.x; i < p.bal_nc; i += gx * NW * 64) p.bal_coarse_z[i] = 0;
+  const int64_t lo = seg_lo + (int64_t)bx * p.rows_per_block;
+  const int64_t hi = max(lo, min(seg_hi, lo + (int64_t)p.rows_per_block));
   // ---- step loop (one iteration unless persistent: p.nsteps > 1)
   // (a separate instantiation: the step loop costs registers the one-step kernel keeps)
   const int nst = PERSIST && p.nsteps > 1 ? p.nsteps : 1;
@@ -375,7 +349,7 @@ lr_rows_kernel(const LrParams p) {
   // taken: a unit then holds 8x the selected rows); a claim takes a whole 256-row group
   // (upg units) until fewer than the fine threshold's groups of the block are unclaimed,
   // then single units, so the block's waves finish within ~1.5 row batches of each other
-  const int qs = (EVAL || p.full) ? 3 : 6;
+  const int qs = (EVAL || p.full) ? 3 : p.unit_shift;
   const int upg = 256 >> qs;
   const int fine_u = (p.fine_q * upg) >> 2;   // fine_q counts 64-row quarters
   const int nq = (int)((ghi - gstart + (1 << qs) - 1) >> qs);
@@ -395,10 +369,6 @@ lr_rows_kernel(const LrParams p) {
       __hip_atomic_store(p.pool + (int64_t)(p.pool_parity ^ 1) * gridDim.y * kPHeads + i, 0u,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (threadIdx.x < kPSlots) s_punit[threadIdx.x] = 0ull;
-  if constexpr (!EVAL && !PERSIST) {
-    if (p.bal_fine_w != nullptr)
-      for (int i = threadIdx.x; i < kBalCap; i += NW * 64) s_bcnt[i] = 0u;
-  }
   if (threadIdx.x == 0) { s_pnext = 0; s_pclaim = 0; }
   __syncthreads();
   const unsigned long long t_bar = tr ? (unsigned long long)__builtin_amdgcn_s_memrealtime() : 0ull;
@@ -504,111 +474,6 @@ lr_rows_kernel(const LrParams p) {
   };
   if (!more) { in_pool = true; pool_draw(); }
 
-  // count-balanced ranges: selected rows of step + 2 in this unit, per 64-row bucket,
-  // accumulated in LDS (s_bcnt, bucket index relative to the 64-aligned block start) and
-  // written out after the sweep: a global store or atomic here would sit in the wave's
-  // in-order vmcnt queue and stall the row pipeline behind it. Buckets past kBalCap (a
-  // block range of > kBalCap * 64 rows, only at very small sampling rates) take the slow
-  // path: 16-lane sum and a direct global store / atomic.
-  auto bal_count = [&](int64_t r0) {
-    u32x4 h2{0u, 0u, 0u, 0u};
-    if (r0 < uhi) h2 = philox_block(p.seed, step_cur + 2, (uint64_t)r0 >> 2);
-    const uint32_t hv2[4] = {h2.x, h2.y, h2.z, h2.w};
-    int c = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) c += (r0 + j >= ulo && r0 + j < uhi && hv2[j] < p.thr) ? 1 : 0;
-    const int64_t lbb = (gnext - glo) >> 6;   // block-local bucket of lanes 0..15
-    if (lbb + 4 <= kBalCap) {
-      if (c) atomicAdd(&s_bcnt[lbb + (lane >> 4)], (unsigned)c);
-      return;
-    }
-    c += __shfl_xor(c, 1);
-    c += __shfl_xor(c, 2);
-    c += __shfl_xor(c, 4);
-    c += __shfl_xor(c, 8);
-    if ((lane & 15) == 0 && r0 >= ulo && r0 < uhi) {
-      const int64_t lb = (r0 - p.row_offset) >> 6;
-      if (lb >= 0 && lb < p.bal_nf) {
-        if (lbb + (lane >> 4) < kBalCap) atomicAdd(&s_bcnt[lbb + (lane >> 4)], (unsigned)c);
-        else {
-          p.bal_fine_w[lb] = c;
-          if (c) atomicAdd(&p.bal_coarse_w[lb >> 6], c);
-        }
-      }
-    }
-  };
-  // after the sweep: the block's LDS bucket counts -> fine (stores) and coarse (one
-  // wave-reduced atomic per 4096-row bucket the block touches)
-  auto bal_flush = [&]() {
-    const int64_t fb0 = (glo - p.row_offset) >> 6;            // first global fine bucket
-    const int nb = (int)min((int64_t)kBalCap, (ghi - glo + 63) >> 6);
-    for (int i = threadIdx.x; i < nb; i += NW * 64)
-      if (fb0 + i < p.bal_nf) p.bal_fine_w[fb0 + i] = (int)s_bcnt[i];
-    if (nb == 0) return;
-    const int64_t c0 = fb0 >> 6, c1 = (fb0 + nb - 1) >> 6;   // coarse buckets touched
-    for (int64_t c = c0 + wid; c <= c1; c += NW) {
-      const int64_t f = c * 64 + lane - fb0;                  // block-local fine bucket
-      unsigned v = (f >= 0 && f < nb) ? s_bcnt[f] : 0u;
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-      if (lane == 0 && v) atomicAdd(&p.bal_coarse_w[c], (int)v);
-    }
-  };
-  // wave 0: start row of this block for step + 1 from the step + 1 counts (three rounds:
-  // coarse chunk sums per lane, the owning chunk's coarse buckets, its 64 fine buckets)
-  auto bal_boundary = [&]() {
-    const int nc = p.bal_nc, nf = p.bal_nf;
-    const int64_t n = p.bal_n;
-    int64_t R = 0;
-    if (bx > 0) {
-      const int per = (nc + 63) >> 6;   // <= 64 (host check)
-      uint32_t sum = 0;
-      for (int i = 0; i < per; ++i) {
-        const int idx = lane * per + i;
-        if (idx < nc) sum += (uint32_t)p.bal_coarse_r[idx];
-      }
-      auto scan = [&](uint32_t v) {
-        uint32_t inc = v;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          const uint32_t t = __shfl_up(inc, off);
-          if (lane >= off) inc += t;
-        }
-        return inc;
-      };
-      const uint32_t inc = scan(sum);
-      const uint64_t tot = (uint64_t)__shfl(inc, 63);
-      if (tot == 0) {
-        R = min(n, (int64_t)bx * p.rows_per_block);   // nothing selected: static split
-      } else {
-        const uint64_t A = (uint64_t)bx * tot / (uint64_t)gx;   // < tot
-        const uint32_t exc = inc - sum;
-        const uint64_t m1 = __ballot((uint64_t)exc <= A && A < (uint64_t)inc);
-        const int l1 = m1 ? __builtin_ctzll(m1) : 63;
-        const uint32_t base1 = __shfl(exc, l1);
-        const int cidx = l1 * per + lane;
-        const bool cok = lane < per && cidx < nc;
-        const uint32_t v2 = cok ? (uint32_t)p.bal_coarse_r[cidx] : 0u;
-        const uint32_t inc2 = base1 + scan(v2), exc2 = inc2 - v2;
-        const uint64_t m2 = __ballot(cok && (uint64_t)exc2 <= A && A < (uint64_t)inc2);
-        const int l2 = m2 ? __builtin_ctzll(m2) : 0;
-        const int cb = l1 * per + l2;
-        const uint32_t base2 = __shfl(exc2, l2);
-        const int fidx = cb * 64 + lane;
-        const bool fok = fidx < nf;
-        const uint32_t v3 = fok ? (uint32_t)p.bal_fine_r[fidx] : 0u;
-        const uint32_t inc3 = base2 + scan(v3), exc3 = inc3 - v3;
-        const uint64_t m3 = __ballot(fok && (uint64_t)exc3 <= A && A < (uint64_t)inc3);
-        const int l3 = m3 ? __builtin_ctzll(m3) : 0;
-        R = min(n, ((int64_t)cb * 64 + l3) * 64);
-      }
-    }
-    if (lane == 0) {
-      p.bal_r_next[bx] = (int)R;
-      if (bx == gx - 1) p.bal_r_next[gx] = (int)n;
-    }
-  };
-
   // ---- K7: Bernoulli selection of the next work unit, compacted into the ring
   auto refill = [&]() {
     while ((tail - head) < (uint32_t)(2 * U) && more) {
@@ -616,9 +481,6 @@ lr_rows_kernel(const LrParams p) {
       u32x4 h{0u, 0u, 0u, 0u};
       if (!p.full && !EVAL && r0 < uhi) h = philox_block(p.seed, step_cur, (uint64_t)r0 >> 2);
       const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
-      if constexpr (!EVAL && !PERSIST) {
-        if (p.bal_fine_w != nullptr) bal_count(r0);
-      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int64_t gr = r0 + j;
@@ -765,8 +627,6 @@ lr_rows_kernel(const LrParams p) {
   // ---- software-pipelined sweep: load(i+1) || compute(i)
   Batch<NC, U> A;
   unsigned long long t_first = 0ull, t_refill = 0ull;
-  // wave 0 computes the block's step + 1 start row right after issuing its first batch
-  bool bal_todo = !EVAL && !PERSIST && p.bal_r_next != nullptr && wid == 0;
   if constexpr (PIPE) {
     Batch<NC, U> B;
     refill();
@@ -775,8 +635,6 @@ lr_rows_kernel(const LrParams p) {
     if (PERSIST && it > 0 && !wait_epoch(it)) return;
     load_w();
     if (tr) t_first = __builtin_amdgcn_s_memrealtime();
-    // wave 0: the block's step + 1 start row, under the first batch's HBM latency
-    if (bal_todo) { bal_todo = false; bal_boundary(); }
     while (true) {
       if (A.n == 0) break;
       refill();
@@ -797,7 +655,6 @@ lr_rows_kernel(const LrParams p) {
       compute(A);
     }
   }
-  if (bal_todo) bal_boundary();
   if (pool_err) cntf = __builtin_nanf("");   // a pool hand-off failed: poison the count
   if (tr && lane == 0) {
     tr[0] = t_start;
@@ -809,9 +666,6 @@ lr_rows_kernel(const LrParams p) {
     tr[7] = t_refill;
   }
   __syncthreads();   // rings are dead: the arena becomes the reduction buffer
-  if constexpr (!EVAL && !PERSIST) {
-    if (p.bal_fine_w != nullptr) bal_flush();
-  }
   if (p.probe_no_epilogue) {
     if (threadIdx.x == 0 && cntf < 0.f) p.C[0] = cntf + gb;   // keep the sweep live
     continue;
@@ -1042,25 +896,8 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
                          float upd_reg_alpha, double* count_acc, const DalgoLrTail* tail,
                          unsigned* pool, int pool_parity, const int64_t* step_dev,
-                         int64_t step_mul, const DalgoLrBal* bal, hipStream_t st) {
+                         int64_t step_mul, hipStream_t st) {
   LrParams p{};
-  if (bal != nullptr) {
-    // balanced ranges: one segment, sampled rows, atomic epilogue, no pool / graph step /
-    // prologue update / persistent steps; 64-aligned units need 4-aligned global rows
-    const int64_t nf = cdiv(bal->n, (int64_t)64), nc = cdiv(nf, (int64_t)64);
-    if (nseg != 1 || full || !((variant >> 8) & 1) || pool != nullptr || step_dev != nullptr ||
-        Wprev != nullptr || (tail != nullptr && tail->nsteps > 1) || row_offset % 4 != 0 ||
-        rows_per_block % 64 != 0 || bal->n <= 0 || bal->n >= (1ll << 31) || bal->nf != nf ||
-        bal->nc != nc || nc > 4096 || bal->fine_w == nullptr || bal->coarse_w == nullptr ||
-        bal->coarse_z == nullptr || bal->r_next == nullptr ||
-        ((bal->fine_r == nullptr) != (bal->coarse_r == nullptr)))
-      return hipErrorInvalidValue;
-    p.bal_fine_w = bal->fine_w; p.bal_coarse_w = bal->coarse_w; p.bal_coarse_z = bal->coarse_z;
-    p.bal_fine_r = bal->fine_r; p.bal_coarse_r = bal->coarse_r;
-    p.bal_r_next = bal->fine_r != nullptr ? bal->r_next : nullptr;
-    p.bal_r_cur = bal->r_cur;
-    p.bal_nf = (int)nf; p.bal_nc = (int)nc; p.bal_n = bal->n;
-  }
   p.step_dev = step_dev;
   p.step_mul = step_mul;
   if (tail != nullptr) {
@@ -1098,6 +935,9 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
   p.atomic_out = (variant >> 8) & 1;   // bit 8 of the variant selects the atomic epilogue
   p.probe_no_epilogue = (variant >> 9) & 1;
   p.fine_q = 4 * ((variant >> 16) & 0xff);   // bits 16..23: fine-claim threshold in groups
+  // bits 24..27: log2 rows per work unit when sampling (0 = 6: 64-row units)
+  p.unit_shift = ((variant >> 24) & 0xf) ? ((variant >> 24) & 0xf) : 6;
+  if (p.unit_shift < 2 || p.unit_shift > 8) return hipErrorInvalidValue;
   p.trace = g_lr_trace;
   p.pool = pool;
   p.pool_parity = pool_parity & 1;

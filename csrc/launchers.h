@@ -25,19 +25,6 @@ struct DalgoLrTail {
   double spin_s;
 };
 
-// Count-balanced K1 block ranges (SSGD, one segment): see LrParams in lr_grad.hip.
-struct DalgoLrBal {
-  int* fine_w;          // step + 2 counts per 64 rows (written)
-  int* coarse_w;        // step + 2 counts per 4096 rows (accumulated; zero on entry)
-  int* coarse_z;        // zeroed for step + 3
-  const int* fine_r;    // step + 1 counts (nullptr: do not compute r_next)
-  const int* coarse_r;
-  int* r_next;          // [gx + 1] block start rows of step + 1
-  const int* r_cur;     // [gx + 1] block start rows of this step (nullptr: static split)
-  int nf, nc;
-  int64_t n;            // local rows
-};
-
 extern "C" {
 
 // ---- K1/K7/K10 logistic regression (lr_grad.hip)
@@ -51,7 +38,7 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
                          float upd_reg_alpha, double* count_acc, const DalgoLrTail* tail,
                          unsigned* pool, int pool_parity, const int64_t* step_dev,
-                         int64_t step_mul, const DalgoLrBal* bal, hipStream_t st);
+                         int64_t step_mul, hipStream_t st);
 hipError_t dalgo_lr_eval(const void* X, const float* y, const float* W, const int64_t* seg,
                          int64_t ld, int D, int ldw, int has_bias, float eps, int is_bf16, int gx,
                          int nseg, int rows_per_block, unsigned long long* correct, float* loss,

@@ -171,9 +171,6 @@ class ParallelSGD:
         self._t_dev_val = 0
         self._upd = dict(mode=0 if algo == "ssgd" else 1, reg=U.REG.get(cfg.reg, 0), eta=cfg.eta,
                          lam=cfg.lam, reg_alpha=cfg.reg_alpha)
-        # SSGD on one segment: count-balanced K1 block ranges handed from step to step
-        # (DALGO_LR_BALANCE, dalgo/ops/lr.py)
-        self._balance = algo == "ssgd" and lr_ops.LR_BALANCE
 
     # ------------------------------------------------------------------ steps
     def _grad(self, W, stream, step_dev=None, step_mul=1):
@@ -182,7 +179,7 @@ class ParallelSGD:
                        eps=c.eps, seed=c.sample_seed, step=stream, frac=c.frac,
                        row_offset=self.data.row_offset, G=self.G, C=self.C,
                        max_seg_rows=self.max_seg, g_is_zero=self._g_zero,
-                       step_dev=step_dev, step_mul=step_mul, balance=self._balance)
+                       step_dev=step_dev, step_mul=step_mul)
         self._g_zero = False
 
     def _one_kernel(self) -> bool:
@@ -339,8 +336,7 @@ class ParallelSGD:
                            max_seg_rows=self.max_seg, g_is_zero=self._g_zero,
                            tail=dict(mode=0 if c.algo == "ssgd" else 1, reg=self._upd["reg"],
                                      eta=c.eta, lam=c.lam, reg_alpha=c.reg_alpha,
-                                     count_acc=self.count_acc, xg=self.bucket.xg),
-                           balance=self._balance)
+                                     count_acc=self.count_acc, xg=self.bucket.xg))
             self._g_zero = True
         elif c.algo in ("ssgd", "gd"):
             self._grad(self.w, t, **sd)

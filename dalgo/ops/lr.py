@@ -33,6 +33,9 @@ _TARGET_BLOCKS = int(os.environ.get("DALGO_LR_BLOCKS", "256"))
 #   FINE_GROUPS     = switch the in-block work claims from 256-row groups to 64-row
 #                     quarters once fewer than this many groups are unclaimed (0 = off)
 LR_FINE_GROUPS = int(os.environ.get("DALGO_LR_FINE", "8"))
+#   UNIT_SHIFT      = sampled steps: work units of 2^UNIT_SHIFT rows; the final (fine) claims
+#                     take one unit, so it sets how closely a block's 8 waves finish together
+LR_UNIT_SHIFT = int(os.environ.get("DALGO_LR_UNIT_SHIFT", "6"))
 #   POOL_FRAC       = share of each segment's rows left to the cross-block pool that
 #                     blocks claim from once their static range is done (0 = off)
 LR_POOL_FRAC = float(os.environ.get("DALGO_LR_POOL", "0"))
@@ -45,12 +48,6 @@ LR_RPB_ALIGN = max(4, int(os.environ.get("DALGO_LR_RPB_ALIGN", "256")) // 4 * 4)
 #   DETERMINISTIC   = combine per-block partials with the fixed-order two-level
 #                     hand-off (bitwise repeatable) instead of float atomics
 DETERMINISTIC = os.environ.get("DALGO_DETERMINISTIC", "0") == "1"
-#   BALANCE         = count-balanced block ranges for sampled one-model steps (SSGD): the
-#                     launch of step t counts the minibatch of step t + 2 per 64 rows and
-#                     turns the step t + 1 counts into block start rows, so from the third
-#                     consecutive step on every block streams the same number of selected
-#                     rows (csrc/kernels/lr_grad.hip, LrParams.bal_*)
-LR_BALANCE = os.environ.get("DALGO_LR_BALANCE", "1") == "1"
 
 
 def padded_cols(D: int, dtype: torch.dtype) -> int:
@@ -88,23 +85,6 @@ def _grid(n_rows: int, nseg: int, target_blocks: int | None = None, pool_frac: f
 
 
 @dataclass
-class _Balance:
-    """Host mirror of the balanced-range workspace (one int32 buffer: fine counts x2,
-    coarse counts x3, block start rows x2; slots chosen from the step by the binding)."""
-    key: tuple                       # (rows, gx, rpb, seed, thr, row_offset)
-    buf: torch.Tensor
-    nf: int
-    nc: int
-    counts_step: int | None = None   # step whose counts are complete in the buffer
-    r_step: int | None = None        # step whose block start rows are complete
-    last_step: int | None = None     # step of the last balanced launch
-
-    def coarse_slot(self, t: int) -> torch.Tensor:
-        off = 2 * self.nf + (t % 3) * self.nc
-        return self.buf[off:off + self.nc]
-
-
-@dataclass
 class _Workspace:
     slab: torch.Tensor
     gslab: torch.Tensor
@@ -116,7 +96,6 @@ class _Workspace:
     perr: torch.Tensor     # ... and its wait-timeout error word
     launches: int = 0      # parity of the next launch = launches & 1
     epochs: int = 0        # host mirror of `epoch` (advanced by nsteps per launch)
-    bal: _Balance | None = None
 
 
 _ws_cache: dict = {}
@@ -139,35 +118,6 @@ def _workspace(device, nseg, gx, S) -> _Workspace:
         )
         _ws_cache[key] = ws
     return ws
-
-
-def _balance_args(ws: _Workspace, X, gx: int, rpb: int, seed: int, step: int, frac: float,
-                  row_offset: int) -> dict:
-    """Workspace + flags of a balanced launch of step `step`; updates the host mirror as if
-    the launch ran (call right before launching it)."""
-    n = int(X.shape[0])
-    nf = (n + 63) // 64
-    nc = (nf + 63) // 64
-    key = (n, gx, rpb, int(seed), float(frac), int(row_offset))
-    b = ws.bal
-    if b is None or b.key != key:
-        b = ws.bal = _Balance(key, torch.zeros(2 * nf + 3 * nc + 2 * (gx + 1), dtype=torch.int32,
-                                               device=X.device), nf, nc)
-    t = int(step)
-    flags = (1 if b.r_step == t else 0) | (2 if b.counts_step == t + 1 else 0)
-    if b.last_step != t - 1:
-        b.coarse_slot(t + 2).zero_()   # normally zeroed by the launch of step t - 1
-    b.counts_step = t + 2
-    b.r_step = t + 1 if flags & 2 else None
-    b.last_step = t
-    return dict(bal=b.buf, bal_flags=flags, bal_n=n)
-
-
-def _balance_ok(X, nseg, frac, row_offset, det, w_prev, step_dev, pool, step) -> bool:
-    n = int(X.shape[0])
-    return (nseg == 1 and 0.0 < frac < 1.0 and not det and w_prev is None and step_dev is None
-            and not pool and int(row_offset) % 4 == 0 and 0 < n < (1 << 31)
-            and (n + 4095) // 4096 <= 4096 and int(step) >= 0 and LR_RPB_ALIGN % 64 == 0)
 
 
 def persistent_error() -> int:
@@ -196,7 +146,7 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
             count_acc: torch.Tensor | None = None, g_is_zero: bool = False,
             deterministic: bool | None = None, tail: dict | None = None,
             pool_frac: float | None = None, step_dev: torch.Tensor | None = None,
-            step_mul: int = 1, balance: bool = False):
+            step_mul: int = 1):
     """Per-segment gradient SUM and selected-row COUNT.
 
     X: [n, >=D] (bf16/f32), y: [n] f32, W: [n_seg, ldw] f32 models,
@@ -208,10 +158,6 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
     lam, reg_alpha) using the CURRENT contents of G and C, writes the new model to
     ``W`` and computes the gradient at it. ``count_acc`` (f64) accumulates the local
     selected-row count.
-
-    Balanced ranges (``balance=True``; GPU, one sampled segment seg = [0, X.shape[0]],
-    atomic epilogue): consecutive calls with steps t, t + 1, ... hand count-balanced block
-    ranges from launch to launch (same rows selected, different block boundaries).
 
     Epilogue: by default every block adds its partial sums to G/C with float
     atomics (G/C are zeroed here unless the caller passes ``g_is_zero=True``, e.g.
@@ -259,17 +205,12 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
         if pf > 0:
             pool = dict(pool=ws.pool, pool_parity=ws.launches & 1)
             ws.launches += 1
-        nst = int(tail.get("nsteps", 1)) if tail is not None else 1
-        bal = {}
-        if balance and nst == 1 and int(max_seg_rows) == int(X.shape[0]) and \
-                _balance_ok(X, nseg, frac, row_offset, det, w_prev, step_dev, pool, step):
-            bal = _balance_args(ws, X, gx, rpb, seed, step, frac, row_offset)
-        elif ws.bal is not None:
-            ws.bal.counts_step = ws.bal.r_step = ws.bal.last_step = None
         u = update or {}
         var = LR_VARIANT if variant is None else int(variant)
-        if not (var >> 16):
+        if not ((var >> 16) & 0xff):
             var |= (LR_FINE_GROUPS & 0xff) << 16
+        if not (var >> 24):
+            var |= (LR_UNIT_SHIFT & 0xf) << 24
         if tail is not None:
             if det or w_prev is not None or nseg != 1:
                 raise ValueError("fused tail needs the atomic epilogue, one model, no prologue update")
@@ -299,7 +240,7 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
                                tail_reg=int(tail.get("reg", 0)), tail_eta=float(tail.get("eta", 0.0)),
                                tail_lam=float(tail.get("lam", 0.0)),
                                tail_reg_alpha=float(tail.get("reg_alpha", 0.0)),
-                               tail_count_acc=tail.get("count_acc"), **kw, **pool, **bal)
+                               tail_count_acc=tail.get("count_acc"), **kw, **pool)
             return G, C
         if not det and w_prev is None:
             if not g_is_zero:
@@ -311,7 +252,7 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
                            ws.cnt1, ws.cnt2, G, C, var,
                            w_prev, int(u.get("mode", 0)), int(u.get("reg", 0)),
                            float(u.get("eta", 0.0)), float(u.get("lam", 0.0)),
-                           float(u.get("reg_alpha", 0.0)), count_acc, **pool, **bal)
+                           float(u.get("reg_alpha", 0.0)), count_acc, **pool)
         return G, C
     if w_prev is not None:
         from dalgo.ops import update as U

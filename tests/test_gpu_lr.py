@@ -246,65 +246,3 @@ def test_lr_grad_persistent_steps(cuda, mode, reg, n):
     rel = ((w - w_ref).abs().max() / w_ref.abs().max()).item()
     assert rel < 1e-4, rel
 
-
-
-def _selected_per_block(R, seed, step, frac, row_offset):
-    from dalgo.utils import philox
-    n = int(R[-1])
-    m = philox.bernoulli_mask(seed, step, np.arange(row_offset, row_offset + n), frac)
-    cs = np.concatenate([[0], np.cumsum(m)])
-    return cs[np.asarray(R[1:])] - cs[np.asarray(R[:-1])]
-
-
-@pytest.mark.parametrize("n,frac,row_offset", [(4113, 0.1, 0), (300_001, 0.1, 12),
-                                               (1_250_000, 0.1, 0), (200_000, 0.5, 4),
-                                               (100_000, 0.1, 6)])
-@pytest.mark.parametrize("tail", [False, True])
-def test_lr_grad_balanced_ranges(cuda, n, frac, row_offset, tail):
-    """Count-balanced block ranges handed from step to step: every step's G / C equals the
-    fp64 reference (same rows selected), and from the third consecutive step the blocks'
-    ranges hold T / gx selected rows +- one 64-row bucket (row_offset 6: not 4-aligned, the
-    static split is kept)."""
-    D = 256
-    X, y = _data(n, D, torch.bfloat16)
-    Xd, yd = pad_features(X.to(cuda)), y.to(cuda)
-    W = torch.randn(1, D + 1, generator=torch.Generator().manual_seed(3)) * 0.1
-    Wd = W.to(cuda)
-    seg = torch.tensor([0, n], dtype=torch.int64)
-    segd = seg.to(cuda)
-    L._ws_cache.clear()
-    for t in range(5, 11):
-        kw = dict(D=D, has_bias=True, eps=0.0, seed=42, step=t, frac=frac, row_offset=row_offset)
-        G_ref, C_ref = L.lr_grad(X.float(), y, W.double(), seg, **kw)
-        if tail:
-            # one-launch step: the tail block applies w -= eta * g / count (SSGD) and counts
-            # the minibatch into count_acc
-            Gd = torch.zeros(1, D + 1, device=cuda)
-            Cd = torch.zeros(1, device=cuda)
-            acc = torch.zeros(1, dtype=torch.float64, device=cuda)
-            Wt = Wd.clone()
-            L.lr_grad(Xd, yd, Wt, segd, **kw, G=Gd, C=Cd, balance=True, g_is_zero=True,
-                      tail=dict(mode=0, eta=0.5, count_acc=acc))
-            torch.cuda.synchronize()
-            assert acc.item() == C_ref.item(), (t, acc.item(), C_ref.item())
-            w_ref = W.double() - 0.5 * G_ref / C_ref.item()
-            err = (Wt.cpu().double() - w_ref).abs().max().item()
-            assert err < 1e-5, (t, err)
-            continue
-        Gd, Cd = L.lr_grad(Xd, yd, Wd, segd, **kw, balance=True)
-        torch.cuda.synchronize()
-        assert torch.equal(Cd.cpu().double(), C_ref), (t, Cd, C_ref)
-        err = (Gd.cpu().double() - G_ref).abs().max().item()
-        assert err / (G_ref.abs().max().item() + 1e-6) < 2e-5, (t, err)
-    ws = [w for w in L._ws_cache.values() if w.bal is not None]
-    if row_offset % 4:
-        assert not ws
-        return
-    b = ws[0].bal
-    gx = b.key[1]
-    assert b.r_step == 11 and b.counts_step == 12
-    off = 2 * b.nf + 3 * b.nc + (11 % 2) * (gx + 1)
-    R = b.buf[off:off + gx + 1].cpu().numpy()
-    assert R[0] == 0 and R[-1] == n and np.all(np.diff(R) >= 0) and np.all(R[:-1] % 64 == 0)
-    cnt = _selected_per_block(R, 42, 11, frac, row_offset)
-    assert np.abs(cnt - cnt.sum() / gx).max() <= 65, (cnt.min(), cnt.max(), cnt.sum() / gx)
