@@ -500,7 +500,8 @@ void rmat_edges(int64_t seed, int64_t scale, int64_t e_off, double a, double b, 
                   "rmat_edges");
 }
 
-void pr_spmv(const Tensor& src, const Tensor& dstl, const Tensor& c, Tensor acc, Tensor pres) {
+void pr_spmv(const Tensor& src, const Tensor& dstl, const Tensor& c, Tensor acc, Tensor pres,
+             bool accumulate) {
   check_i32(src, "src");
   check_i32(dstl, "dstl");
   TORCH_CHECK(src.numel() == dstl.numel() && src.numel() % 4 == 0, "edge arrays: equal, % 4");
@@ -513,7 +514,7 @@ void pr_spmv(const Tensor& src, const Tensor& dstl, const Tensor& c, Tensor acc,
   DeviceGuard guard(src.device());
   DALGO_CHECK_HIP(dalgo_pr_spmv(src.data_ptr<int32_t>(), dstl.data_ptr<int32_t>(), src.numel(),
                                 c.data_ptr<float>(), acc.data_ptr<float>(), pres.data_ptr<int32_t>(),
-                                cur_stream()),
+                                accumulate ? 1 : 0, cur_stream()),
                   "pr_spmv");
 }
 
@@ -809,7 +810,8 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("pb_spmv(Tensor psrc, Tensor ppos, Tensor c, Tensor(a!) val, Tensor dloc, Tensor chunk_lo4, "
         "Tensor chunk_bin, Tensor chunk_slab, int bin_width, Tensor(b!) acc, Tensor(c!) pres, "
         "Tensor(d!) slab, Tensor split_bin, Tensor split_first, Tensor split_count) -> ()");
-  m.def("pr_spmv(Tensor src, Tensor dstl, Tensor c, Tensor(a!) acc, Tensor(b!) pres) -> ()");
+  m.def("pr_spmv(Tensor src, Tensor dstl, Tensor c, Tensor(a!) acc, Tensor(b!) pres, "
+        "bool accumulate=False) -> ()");
   m.def("pr_update(Tensor acc, Tensor pres, Tensor outdeg, float q, float invN, int mode, "
         "Tensor? dangling_in, Tensor(a!) r, Tensor(b!) c, Tensor(c!)? dangling_out) -> ()");
   m.def("xgmi_buffer_bytes(int slot) -> int", &xgmi_buffer_bytes);

@@ -71,19 +71,25 @@ rmat_kernel(uint64_t seed, int scale, int64_t e_off, int64_t n, uint32_t pa, uin
 
 // ---------------------------------------------------------------------------
 // pull SpMV over a (dst, src)-sorted local edge list (reduce-by-key per wave)
+// ACC: a second pass over another edge subset of the same rows (overlapped ghost exchange):
+// complete rows add to acc / set pres instead of overwriting them
+template <bool ACC>
 __device__ __forceinline__ void flush_run(float* acc, int32_t* pres, int key, float v, int f,
                                           bool partial) {
   if (key < 0) return;
   if (partial) {
     atomicAdd(&acc[key], v);
     if (f) atomicOr(&pres[key], 1);
+  } else if constexpr (ACC) {
+    acc[key] += v;
+    if (f) pres[key] = 1;
   } else {
     acc[key] = v;
     pres[key] = f;
   }
 }
 
-template <int NW, bool NT>
+template <int NW, bool NT, bool ACC>
 __global__ void __launch_bounds__(NW * 64)
 pr_spmv_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dstl, int64_t E,
                const float* __restrict__ c, float* __restrict__ acc, int32_t* __restrict__ pres) {
@@ -129,7 +135,7 @@ pr_spmv_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dstl
     for (int j = 0; j < 4; ++j) {
       if (dv[j] != key) {
         if (single) { head = run; headf = runf; single = false; }
-        else flush_run(acc, pres, key, run, runf, false);   // interior: complete row
+        else flush_run<ACC>(acc, pres, key, run, runf, false);   // interior: complete row
         key = dv[j];
         run = 0.f;
         runf = 0;
@@ -168,9 +174,9 @@ pr_spmv_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dstl
       // head run ends inside this lane
       const float hv = head + (cont_left ? S_left : 0.f);
       const int hf = headf | (cont_left ? F_left : 0);
-      flush_run(acc, pres, k0, hv, hf, partial_key(k0));
+      flush_run<ACC>(acc, pres, k0, hv, hf, partial_key(k0));
     }
-    if (!cont_right) flush_run(acc, pres, kt, sv_, sf_, partial_key(kt));
+    if (!cont_right) flush_run<ACC>(acc, pres, kt, sv_, sf_, partial_key(kt));
   }
 }
 
@@ -356,19 +362,26 @@ hipError_t dalgo_rmat(uint64_t seed, int scale, int64_t e_off, int64_t n, float 
 }
 
 hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, const float* c,
-                         float* acc, int32_t* pres, hipStream_t st) {
+                         float* acc, int32_t* pres, int accumulate, hipStream_t st) {
   if (E % 4 != 0) return hipErrorInvalidValue;
   constexpr int NW = 4;
   const int64_t nwin = cdiv(E, 256);
   const int grid = (int)std::min<int64_t>(cdiv(nwin, NW), 256 * 16);
   if (grid == 0) return hipSuccess;
   // edge stream read once per iteration: nt loads (DALGO_NT=0 restores the default policy)
-  if (env_int("DALGO_NT", 1))
-    hipLaunchKernelGGL((pr_spmv_kernel<NW, true>), dim3(grid), dim3(NW * 64), 0, st, src, dstl, E, c,
-                       acc, pres);
+  const bool nt = env_int("DALGO_NT", 1) != 0;
+  if (nt && accumulate)
+    hipLaunchKernelGGL((pr_spmv_kernel<NW, true, true>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
+                       E, c, acc, pres);
+  else if (nt)
+    hipLaunchKernelGGL((pr_spmv_kernel<NW, true, false>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
+                       E, c, acc, pres);
+  else if (accumulate)
+    hipLaunchKernelGGL((pr_spmv_kernel<NW, false, true>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
+                       E, c, acc, pres);
   else
-    hipLaunchKernelGGL((pr_spmv_kernel<NW, false>), dim3(grid), dim3(NW * 64), 0, st, src, dstl, E, c,
-                       acc, pres);
+    hipLaunchKernelGGL((pr_spmv_kernel<NW, false, false>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
+                       E, c, acc, pres);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

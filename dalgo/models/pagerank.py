@@ -116,6 +116,21 @@ class PageRank:
             assert int(local.max()) < sl + self.n_ghost and int(local.min()) >= 0
         self.g_local = Gops.GraphShard(src_local, g.dstl, E, g.v_lo, g.v_hi, g.n_vertices, sl,
                                        g.new_id)
+        # the same edges split by source: own slice (needs no exchange) and ghosts; each
+        # keeps the (dst, src) order, so the ghost pass adds into rows the own pass wrote
+        own = local < sl
+
+        def _part(m):
+            k = int(m.sum().item())
+            kp = (k + 3) // 4 * 4
+            s_ = torch.full((kp,), -1, dtype=torch.int32, device=src.device)
+            d_ = torch.full((kp,), -1, dtype=torch.int32, device=src.device)
+            s_[:k] = local[m].to(torch.int32)
+            d_[:k] = g.dstl[:E][m]
+            return Gops.GraphShard(s_, d_, k, g.v_lo, g.v_hi, g.n_vertices, sl, g.new_id)
+
+        self.g_own, self.g_ghost = _part(own), _part(~own)
+        self.own_share = self.g_own.n_edges / max(E, 1)
         # request lists: peer p asks for send_counts[p] of my vertices
         send_counts = torch.empty_like(recv_counts)
         comm.all_to_all_single(send_counts, recv_counts)
@@ -158,9 +173,35 @@ class PageRank:
             comm.all_reduce_sum(self.dang_next)
             self.dang, self.dang_next = self.dang_next, self.dang
 
+    def _overlap(self) -> bool:
+        """Ghost exchange under the SpMV over own-slice sources: the all_to_all writes only
+        the ghost part of c_full, the first pass reads only the own part, the second adds
+        the ghost-source edges into the same rows. Splitting the SpMV costs ~10 % at the
+        rank-0 share of R-MAT scale 26 (1.41 -> 1.54 ms at W = 8, 5.42 -> 5.80 ms at W = 2,
+        profiles/round2/README.md), so by default (DALGO_PR_OVERLAP=auto) it is only used
+        while the own-source pass is long enough to hide the exchange: at least a quarter
+        of the edges (W <= 4 with the dealt relabeling). 1 / 0 force it on / off."""
+        if self.exchange != "ghost":
+            return False
+        env = os.environ.get("DALGO_PR_OVERLAP", "auto")
+        return env == "1" or (env == "auto" and self.own_share >= 0.25)
+
     def step(self):
-        self._exchange()      # contributions of the previous iteration
-        self._spmv()          # K4 pull SpMV over the local in-edges
+        if self._overlap():
+            if self.send_buf is None:
+                self.send_buf = torch.empty(self.send_idx.numel(), dtype=self.fdt, device=self.dev)
+            torch.index_select(self.c_slice, 0, self.send_idx, out=self.send_buf)
+            work = comm.all_to_all_single(self.c_full[self.g.slice_size:], self.send_buf,
+                                          out_split=self.recv_split, in_split=self.send_split,
+                                          async_op=True)
+            self.acc.zero_()
+            self.pres.zero_()
+            Gops.pr_spmv(self.g_own, self.c_full, self.acc, self.pres)
+            work.wait()
+            Gops.pr_spmv(self.g_ghost, self.c_full, self.acc, self.pres, accumulate=True)
+        else:
+            self._exchange()      # contributions of the previous iteration
+            self._spmv()          # K4 pull SpMV over the local in-edges
         self._update()        # ranks + next contributions (fused epilogue kernel)
         self.t += 1
 

@@ -251,10 +251,13 @@ def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: t
 
 
 # ------------------------------------------------------------------ K4 kernels
-def pr_spmv(shard: GraphShard, c_full: torch.Tensor, acc: torch.Tensor, pres: torch.Tensor):
-    """acc[v] = sum_{u->v, c[u] >= 0} c[u];  pres[v] = any such edge  (acc/pres zeroed by caller)."""
+def pr_spmv(shard: GraphShard, c_full: torch.Tensor, acc: torch.Tensor, pres: torch.Tensor,
+            accumulate: bool = False):
+    """acc[v] = sum_{u->v, c[u] >= 0} c[u];  pres[v] = any such edge  (acc/pres zeroed by caller).
+    ``accumulate``: a further pass over another edge subset of the same rows (adds to acc,
+    ORs pres)."""
     if c_full.is_cuda:
-        _ext.ops().pr_spmv(shard.src, shard.dstl, c_full, acc, pres)
+        _ext.ops().pr_spmv(shard.src, shard.dstl, c_full, acc, pres, bool(accumulate))
         return
     E = shard.n_edges
     s = shard.src[:E].long()
@@ -263,6 +266,8 @@ def pr_spmv(shard: GraphShard, c_full: torch.Tensor, acc: torch.Tensor, pres: to
     acc.index_add_(0, d, cv.clamp_min(0))
     hit = torch.zeros_like(pres)
     hit.index_add_(0, d, (cv >= 0).to(pres.dtype))
+    if accumulate:
+        hit += pres
     pres.copy_((hit > 0).to(pres.dtype))
 
 

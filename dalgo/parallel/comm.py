@@ -163,25 +163,33 @@ def reduce_scatter_sum(out: torch.Tensor, full: torch.Tensor) -> torch.Tensor:
     return out
 
 
+class _Done:
+    """Handle of a collective that already completed (``async_op`` fallbacks)."""
+
+    def wait(self):
+        return True
+
+
 def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, out_split: list[int] | None = None,
-                      in_split: list[int] | None = None) -> torch.Tensor:
+                      in_split: list[int] | None = None, async_op: bool = False):
     """Personalised exchange along dim 0 (``out_split[p]`` rows arrive from rank p,
     ``in_split[p]`` rows go to it); RCCL runs it as grouped send/recv over all peers at
-    once. World size 1: a copy."""
+    once. World size 1: a copy. ``async_op``: returns a handle whose ``wait()`` orders
+    the current stream after the exchange (RCCL runs it on its own stream meanwhile)."""
     if not _active():
         if out.numel():
             out.copy_(inp.reshape(out.shape))
-        return out
+        return _Done() if async_op else out
     if inp.is_cuda and dist.get_backend() == "gloo":
         # gloo's all_to_all takes host tensors only (the one-GPU multi-rank rehearsal)
         host = torch.empty(out.shape, dtype=out.dtype)
         dist.all_to_all_single(host, inp.cpu(), output_split_sizes=out_split,
                                input_split_sizes=in_split)
         out.copy_(host)
-        return out
-    dist.all_to_all_single(out, inp.contiguous(), output_split_sizes=out_split,
-                           input_split_sizes=in_split)
-    return out
+        return _Done() if async_op else out
+    work = dist.all_to_all_single(out, inp.contiguous(), output_split_sizes=out_split,
+                                  input_split_sizes=in_split, async_op=async_op)
+    return work if async_op else out
 
 
 def gather_to_rank0(local: torch.Tensor, counts: list[int]) -> torch.Tensor | None:

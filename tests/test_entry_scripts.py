@@ -191,3 +191,9 @@ def test_pagerank_rmat_world_size_invariant():
                             + ["--backend", "gloo"], timeout=400))
     assert len(one) == 10 and set(one) == set(three)
     assert max(abs(one[v] - three[v]) for v in one) < 1e-12
+    # 3 ranks take the overlapped ghost exchange by default (own-source share 1/3); the
+    # sequential exchange + single SpMV pass gives the same ranks
+    seq = _top_ranks(_run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+                           "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+                          + ["--backend", "gloo"], env_extra={"DALGO_PR_OVERLAP": "0"}, timeout=400))
+    assert set(seq) == set(three) and max(abs(seq[v] - three[v]) for v in seq) < 1e-12

@@ -217,6 +217,26 @@ def test_pr_spmv_matches_reference(cuda, frac_absent):
     G.pr_spmv(sh_d, c.to(cuda), acc, pres)
     assert torch.equal(pres.cpu(), pres_c)
     assert torch.allclose(acc.cpu().double(), acc_c, rtol=1e-5, atol=1e-5)
+    # two passes over a source split of the same edges (the overlapped ghost exchange:
+    # own-slice sources, then the accumulate pass over the rest) == one pass
+    E = sh_d.n_edges
+    m = sh_d.src[:E] < nv // 3
+
+    def part(mask):
+        k = int(mask.sum().item())
+        kp = (k + 3) // 4 * 4
+        s_ = torch.full((kp,), -1, dtype=torch.int32, device=cuda)
+        d_ = torch.full((kp,), -1, dtype=torch.int32, device=cuda)
+        s_[:k] = sh_d.src[:E][mask]
+        d_[:k] = sh_d.dstl[:E][mask]
+        return G.GraphShard(s_, d_, k, sh_d.v_lo, sh_d.v_hi, sh_d.n_vertices, sh_d.slice_size)
+
+    acc2 = torch.zeros(nv, device=cuda)
+    pres2 = torch.zeros(nv, dtype=torch.int32, device=cuda)
+    G.pr_spmv(part(m), c.to(cuda), acc2, pres2)
+    G.pr_spmv(part(~m), c.to(cuda), acc2, pres2, accumulate=True)
+    assert torch.equal(pres2.cpu(), pres_c)
+    assert torch.allclose(acc2.cpu().double(), acc_c, rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("sem", ["reference", "standard"])
