@@ -223,7 +223,15 @@ constexpr int kPU = 512, kPSub = 64, kPSubs = kPU / kPSub, kPAhead = 4, kPSlots 
 constexpr int kPHeads = 64;                  // claim heads (shards) per segment; one per lane
 constexpr int64_t kPExh = (1ll << 40) - 1;   // "pool exhausted" marker
 
-template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, bool PERSIST, int AUX = 0>
+// LEAN compiles out every path the default sampled launch never takes: the cross-block
+// pool, the fixed-order (deterministic) epilogue and claim map, the fused-update prologue
+// and the no-epilogue probe. Each launch starts from a cold instruction cache, and those
+// inlined paths sat between the executed instructions of the start-up path and the
+// refill loop: variant 8 without the pool alone measured 56.5 -> 53.5 us per 1.25M-row
+// step (profiles/round2/README.md). The launcher falls back to the full build when a
+// launch needs any of them.
+template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, bool PERSIST, int AUX = 0,
+          bool LEAN = false>
 __global__ void __launch_bounds__(NW * 64)
 lr_rows_kernel(const LrParams p) {
   constexpr int VEC = VecTraits<T>::VEC;
@@ -294,7 +302,7 @@ lr_rows_kernel(const LrParams p) {
       return *a;
   };
   auto load_w = [&]() {
-    if (p.Wprev == nullptr) {
+    if (LEAN || p.Wprev == nullptr) {
       const float* w = p.W + (int64_t)seg * p.ldw;
 #pragma unroll
       for (int c = 0; c < NC; ++c)
@@ -364,7 +372,7 @@ lr_rows_kernel(const LrParams p) {
   // own shard, so few blocks share a head) and handed to the block's waves in 64-row
   // sub-units through LDS. Block (0, 0) re-arms the other parity set, which the previous
   // launch used and the next one will.
-  if (p.pool != nullptr && bx == 0 && seg == 0)
+  if (!LEAN && p.pool != nullptr && bx == 0 && seg == 0)
     for (int i = threadIdx.x; i < kPHeads * (int)gridDim.y; i += NW * 64)
       __hip_atomic_store(p.pool + (int64_t)(p.pool_parity ^ 1) * gridDim.y * kPHeads + i, 0u,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -373,7 +381,7 @@ lr_rows_kernel(const LrParams p) {
   __syncthreads();
   const unsigned long long t_bar = tr ? (unsigned long long)__builtin_amdgcn_s_memrealtime() : 0ull;
   const int64_t psl = seg_lo + (int64_t)gx * p.rows_per_block;   // pool start (local row)
-  const bool has_pool = p.pool != nullptr && psl < seg_hi;
+  const bool has_pool = !LEAN && p.pool != nullptr && psl < seg_hi;
   unsigned* const heads =
       has_pool ? p.pool + ((int64_t)p.pool_parity * gridDim.y + seg) * kPHeads : nullptr;
   const int64_t psg = p.row_offset + psl, psa = psg & ~(int64_t)3, sghi = p.row_offset + seg_hi;
@@ -495,7 +503,7 @@ lr_rows_kernel(const LrParams p) {
       // take more units, so the block's waves finish together
       if (!in_pool) {
         int gi = 0, w = w0;
-        if (!p.atomic_out) {
+        if (!LEAN && !p.atomic_out) {
           // fixed-order epilogue: a fixed group -> wave map (wave w takes groups
           // w, w + NW, ...), so every partial sum is bitwise repeatable
           gi = sclaim;
@@ -666,7 +674,7 @@ lr_rows_kernel(const LrParams p) {
     tr[7] = t_refill;
   }
   __syncthreads();   // rings are dead: the arena becomes the reduction buffer
-  if (p.probe_no_epilogue) {
+  if (!LEAN && p.probe_no_epilogue) {
     if (threadIdx.x == 0 && cntf < 0.f) p.C[0] = cntf + gb;   // keep the sweep live
     continue;
   }
@@ -694,7 +702,7 @@ lr_rows_kernel(const LrParams p) {
     __syncthreads();
     const int S = p.S;
     const int D = p.D;
-    if (p.atomic_out) {
+    if (LEAN || p.atomic_out) {
       float* Gs = p.G + (int64_t)seg * p.ldw;
       for (int col = threadIdx.x; col < D; col += NW * 64) {
         float s = 0.f;
@@ -803,7 +811,7 @@ lr_rows_kernel(const LrParams p) {
 
 using namespace dalgo;
 
-template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, int AUX = 0>
+template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, int AUX = 0, bool LEAN = false>
 static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st) {
   dim3 grid(gx, nseg), block(NW * 64);
   if (p.nsteps > 1) {
@@ -816,7 +824,7 @@ static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st)
     }
     return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL((lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, false, AUX>), grid, block, 0, st, p);
+  hipLaunchKernelGGL((lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, false, AUX, LEAN>), grid, block, 0, st, p);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -827,6 +835,8 @@ static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st)
 //   4: 4 waves, 8-row batches               5: 8 waves, 8-row batches
 //   6: 12 waves, pipelined (3 waves/SIMD)   7: 16 waves, single set (4 waves/SIMD)
 //   8: = 3 with nt row loads   9: = 5 with nt   10: = 3 with sc0|nt   11: = 3 with sc0|sc1
+//   (8 runs a LEAN build when the launch needs no pool, deterministic epilogue, fused
+//   update prologue or probe, else the full build; 12 = 8 always in the full build)
 template <typename T, int NC, bool EVAL>
 static hipError_t launch_variant(const LrParams& p, int gx, int nseg, int variant, hipStream_t st) {
   if constexpr (NC >= 4) {   // register budget: one 4-row set at 4 chunks/lane
@@ -845,7 +855,13 @@ static hipError_t launch_variant(const LrParams& p, int gx, int nseg, int varian
       case 6: return launch_lr<T, NC, EVAL, 12, true, 4>(p, gx, nseg, st);
       case 7: return launch_lr<T, NC, EVAL, 16, false, 4>(p, gx, nseg, st);
       // X-row cache policy (aux bits of the buffer load: 2 = nt, 1 = sc0, 16 = sc1)
-      case 8: return launch_lr<T, NC, EVAL, 8, true, 4, 2>(p, gx, nseg, st);
+      case 8:
+        if constexpr (!EVAL) {
+          if (p.pool == nullptr && p.atomic_out && p.Wprev == nullptr && !p.probe_no_epilogue)
+            return launch_lr<T, NC, EVAL, 8, true, 4, 2, true>(p, gx, nseg, st);
+        }
+        return launch_lr<T, NC, EVAL, 8, true, 4, 2, false>(p, gx, nseg, st);
+      case 12: return launch_lr<T, NC, EVAL, 8, true, 4, 2, false>(p, gx, nseg, st);   // 8, full build
       case 9: return launch_lr<T, NC, EVAL, 8, false, 8, 2>(p, gx, nseg, st);
       case 10: return launch_lr<T, NC, EVAL, 8, true, 4, 3>(p, gx, nseg, st);
       case 11: return launch_lr<T, NC, EVAL, 8, true, 4, 17>(p, gx, nseg, st);
