@@ -234,6 +234,9 @@ template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, bool PERSIST,
           bool LEAN = false>
 __global__ void __launch_bounds__(NW * 64)
 lr_rows_kernel(const LrParams p) {
+  // the persistent form (fused tail, atomic epilogue, no pool / prologue: host checks)
+  // never takes those paths either
+  constexpr bool kLean = LEAN || PERSIST;
   constexpr int VEC = VecTraits<T>::VEC;
   constexpr int COLS = NC * 64 * VEC;  // columns covered per lane-set
   constexpr int RED_FLOATS = NW * (COLS + 4);
@@ -302,7 +305,7 @@ lr_rows_kernel(const LrParams p) {
       return *a;
   };
   auto load_w = [&]() {
-    if (LEAN || p.Wprev == nullptr) {
+    if (kLean || p.Wprev == nullptr) {
       const float* w = p.W + (int64_t)seg * p.ldw;
 #pragma unroll
       for (int c = 0; c < NC; ++c)
@@ -372,7 +375,7 @@ lr_rows_kernel(const LrParams p) {
   // own shard, so few blocks share a head) and handed to the block's waves in 64-row
   // sub-units through LDS. Block (0, 0) re-arms the other parity set, which the previous
   // launch used and the next one will.
-  if (!LEAN && p.pool != nullptr && bx == 0 && seg == 0)
+  if (!kLean && p.pool != nullptr && bx == 0 && seg == 0)
     for (int i = threadIdx.x; i < kPHeads * (int)gridDim.y; i += NW * 64)
       __hip_atomic_store(p.pool + (int64_t)(p.pool_parity ^ 1) * gridDim.y * kPHeads + i, 0u,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -381,7 +384,7 @@ lr_rows_kernel(const LrParams p) {
   __syncthreads();
   const unsigned long long t_bar = tr ? (unsigned long long)__builtin_amdgcn_s_memrealtime() : 0ull;
   const int64_t psl = seg_lo + (int64_t)gx * p.rows_per_block;   // pool start (local row)
-  const bool has_pool = !LEAN && p.pool != nullptr && psl < seg_hi;
+  const bool has_pool = !kLean && p.pool != nullptr && psl < seg_hi;
   unsigned* const heads =
       has_pool ? p.pool + ((int64_t)p.pool_parity * gridDim.y + seg) * kPHeads : nullptr;
   const int64_t psg = p.row_offset + psl, psa = psg & ~(int64_t)3, sghi = p.row_offset + seg_hi;
@@ -503,7 +506,7 @@ lr_rows_kernel(const LrParams p) {
       // take more units, so the block's waves finish together
       if (!in_pool) {
         int gi = 0, w = w0;
-        if (!LEAN && !p.atomic_out) {
+        if (!kLean && !p.atomic_out) {
           // fixed-order epilogue: a fixed group -> wave map (wave w takes groups
           // w, w + NW, ...), so every partial sum is bitwise repeatable
           gi = sclaim;
@@ -674,7 +677,7 @@ lr_rows_kernel(const LrParams p) {
     tr[7] = t_refill;
   }
   __syncthreads();   // rings are dead: the arena becomes the reduction buffer
-  if (!LEAN && p.probe_no_epilogue) {
+  if (!kLean && p.probe_no_epilogue) {
     if (threadIdx.x == 0 && cntf < 0.f) p.C[0] = cntf + gb;   // keep the sweep live
     continue;
   }
@@ -702,7 +705,7 @@ lr_rows_kernel(const LrParams p) {
     __syncthreads();
     const int S = p.S;
     const int D = p.D;
-    if (LEAN || p.atomic_out) {
+    if (kLean || p.atomic_out) {
       float* Gs = p.G + (int64_t)seg * p.ldw;
       for (int col = threadIdx.x; col < D; col += NW * 64) {
         float s = 0.f;
@@ -932,7 +935,8 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
     p.tu = XgUpdate{tail->mode, tail->reg, tail->eta, tail->lam, tail->reg_alpha};
     p.tail_count_acc = tail->count_acc;
     if (tail->nsteps > 1) {
-      if (tail->epoch_ctr == nullptr || tail->perr == nullptr || pool != nullptr)
+      if (tail->epoch_ctr == nullptr || tail->perr == nullptr || pool != nullptr ||
+          ((variant >> 9) & 1))
         return hipErrorInvalidValue;
       p.nsteps = tail->nsteps;
       p.epoch = tail->epoch_ctr;
