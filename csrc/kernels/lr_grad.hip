@@ -843,6 +843,11 @@ static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st)
 template <typename T, int NC, bool EVAL>
 static hipError_t launch_variant(const LrParams& p, int gx, int nseg, int variant, hipStream_t st) {
   if constexpr (NC >= 4) {   // register budget: one 4-row set at 4 chunks/lane
+    if constexpr (!EVAL) {
+      if (variant == 8 && p.pool == nullptr && p.atomic_out && p.Wprev == nullptr &&
+          !p.probe_no_epilogue)
+        return launch_lr<T, NC, EVAL, 8, false, 4, 2, true>(p, gx, nseg, st);
+    }
     if (variant == 8 || variant == 9) return launch_lr<T, NC, EVAL, 8, false, 4, 2>(p, gx, nseg, st);
     return (variant == 2 || variant == 3 || variant == 5)
                ? launch_lr<T, NC, EVAL, 8, false, 4>(p, gx, nseg, st)
