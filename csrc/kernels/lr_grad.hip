@@ -307,13 +307,34 @@ lr_rows_kernel(const LrParams p) {
   auto load_w = [&]() {
     if (kLean || p.Wprev == nullptr) {
       const float* w = p.W + (int64_t)seg * p.ldw;
+      // 16-B aligned model row (SSGD: one model): each lane's VEC contiguous weights
+      // with VEC / 4 vector loads instead of VEC bounds-checked scalar ones (fewer
+      // instructions on the cold start-up path)
+      const bool vec_ok = !PERSIST && (reinterpret_cast<uintptr_t>(w) & 15) == 0;
+      if (vec_ok) {
 #pragma unroll
-      for (int c = 0; c < NC; ++c)
+        for (int c = 0; c < NC; ++c) {
+          const int col0 = (c * 64 + lane) * VEC;
+          if (col0 + VEC <= p.D) {
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          int col = (c * 64 + lane) * VEC + e;
-          wr[c][e] = (col < p.D) ? ldw_(w + col) : 0.f;
+            for (int v = 0; v < VEC / 4; ++v) {
+              const float4 f = *reinterpret_cast<const float4*>(w + col0 + 4 * v);
+              wr[c][4 * v] = f.x; wr[c][4 * v + 1] = f.y; wr[c][4 * v + 2] = f.z; wr[c][4 * v + 3] = f.w;
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) wr[c][e] = (col0 + e < p.D) ? w[col0 + e] : 0.f;
+          }
         }
+      } else {
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) {
+            int col = (c * 64 + lane) * VEC + e;
+            wr[c][e] = (col < p.D) ? ldw_(w + col) : 0.f;
+          }
+      }
       wb = p.has_bias ? ldw_(w + p.D) : 0.f;
     } else {
       const float cprev = p.Cprev[0];
