@@ -11,8 +11,16 @@ minibatch + fused gradient (K1+K7) -> RCCL all_reduce([g || count]) -> K8 update
 every rank. samples/sec = global minibatch rows processed per second (exact
 count, accumulated on device).
 
-Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch with
-torch.distributed.run (one rank per GPU, RCCL over xGMI).
+Run: python bench.py [--gpus N --steps K --warmup W]. With N > 1 and no launcher
+environment the script starts ``torch.distributed.run --nproc-per-node N`` on itself
+as a CHILD process (before anything touches the GPU; no exec) and exits with its
+code, so one command measures N ranks on N GPUs (RCCL over xGMI); under
+torchrun (the driver's N > 1 launch) it is one of the ranks. The JSON carries the
+evidence that N distinct devices took part (``device_ids``), the RCCL version,
+the small-all-reduce path the start-up race chose with both timings, the
+per-step all-reduce time measured in isolation after the timed region, and the
+held-out accuracy of the trained model (a correctness witness: a fast but wrong
+gradient kernel cannot post a number).
 """
 from __future__ import annotations
 
@@ -41,7 +49,14 @@ def parse(argv=None):
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--backend", default=None, choices=["nccl", "gloo"],
                     help="collective backend (default: nccl = RCCL on GPU, gloo on CPU)")
-    ap.add_argument("--eval", action="store_true", help="report held-out accuracy after timing")
+    ap.add_argument("--eval", dest="eval", action="store_true", default=True,
+                    help="held-out accuracy after the timed region (default on)")
+    ap.add_argument("--no-eval", dest="eval", action="store_false")
+    ap.add_argument("--n-test", type=int, default=100_000, help="held-out rows for the witness")
+    ap.add_argument("--witness-steps", type=int, default=1500,
+                    help="after the timed region, keep training (untimed) up to this many total "
+                         "steps (the reference's n_iterations, optimization/ssgd.py:18) before "
+                         "the held-out evaluation")
     ap.add_argument("--launch", default=os.environ.get("DALGO_LAUNCH", "auto"),
                     choices=["auto", "env"],
                     help="auto: time the equivalent SSGD/GD step launch forms (per-step K1 + "
@@ -71,10 +86,12 @@ def calibrate_launch(model, rt, a) -> dict:
     # ranks sharing one GPU (the one-GPU rehearsals): a rank's in-kernel wait for its peers'
     # exchange needs the peers' kernels co-resident on the same CUs, which a persistent grid
     # does not leave room for; the forms are only raced when every rank has its own GPU
-    # (DALGO_CAL_SHARED=1 forces it, for the 2-rank rehearsal test)
-    local_n = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
-    if local_n > torch.cuda.device_count() and os.environ.get("DALGO_CAL_SHARED", "0") != "1":
+    # (library rule, from the device identities every rank published at init)
+    if not runtime.spin_waits_allowed():
         return {}
+    # the calibration trains extra steps: restore the model afterwards so the timed region
+    # and the held-out witness see exactly warmup + steps training steps
+    snap = model.state_dict()
     cands = {"per-step": (False, False), "one-kernel": (True, False), "persistent": (False, True)}
     res = {}
     for name, (one, pers) in cands.items():
@@ -94,11 +111,70 @@ def calibrate_launch(model, rt, a) -> dict:
     comm.check_device_errors("launch calibration")
     best = min(res, key=res.get)
     model._ok1, model._okp = cands[best]
+    model.load_state_dict(snap)
+    rt.synchronize()
     return res
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def self_launch(a, argv) -> int | None:
+    """``--gpus N`` without a launcher: run N ranks as a torchrun CHILD process.
+
+    Returns the child's exit code, or None when this process is already a rank (or
+    N == 1). Nothing here initialises the GPU (``torch.cuda.device_count()`` does not
+    on this ROCm build), and the child is a new process, never an exec."""
+    if a.gpus <= 1 or "RANK" in os.environ or "WORLD_SIZE" in os.environ:
+        return None
+    backend = a.backend or ("nccl" if a.device == "cuda" else "gloo")
+    if a.device == "cuda":
+        ndev = torch.cuda.device_count()
+        if backend == "nccl" and a.gpus > ndev:
+            print(f"[bench] --gpus {a.gpus} but only {ndev} GPU(s) are visible: RCCL needs one "
+                  f"GPU per rank; refusing to report a {a.gpus}-GPU number", file=sys.stderr)
+            return 2
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def allreduce_probe(model, rt, iters: int = 100) -> float | None:
+    """Per-step all-reduce cost in isolation (us, max over ranks): the SSGD/GD
+    ``[g || count]`` bucket through whatever path the run uses (K11 or the process
+    group). The bucket is all zeros between steps, so the probe leaves it unchanged."""
+    from dalgo.parallel import comm
+    if rt.world_size <= 1 or not hasattr(model, "bucket"):
+        return None
+    for _ in range(10):
+        model.bucket.all_reduce()
+    rt.synchronize()
+    rt.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        model.bucket.all_reduce()
+    rt.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=rt.device)
+    comm.all_reduce_max(el)
+    return float(el.item()) / iters * 1e6
+
+
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     a = parse(argv)
+    rc = self_launch(a, argv)
+    if rc is not None:
+        sys.exit(rc)
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from dalgo.data.datasets import synthetic_logistic
     from dalgo.models.localsgd import ParallelSGD, SGDConfig
@@ -107,14 +183,15 @@ def main(argv=None):
 
     rt = runtime.init(backend=a.backend, device=a.device, app_name="bench-ssgd")
     W = rt.world_size
-    if a.gpus != W and rt.is_main:
-        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={W}; using {W}", file=sys.stderr)
+    if a.gpus != W:
+        raise SystemExit(f"[bench] --gpus {a.gpus} but WORLD_SIZE={W}: launch N ranks "
+                         f"(or let bench.py start them) so N GPUs are measured")
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     n_workers = W
     layout = make_layout(a.rows, n_workers, W, rt.rank, spark_compatible=False)
     t0 = time.time()
     data = synthetic_logistic(a.rows, a.dim, row_range=(layout.row_lo, layout.row_hi),
-                              n_test=100_000 if a.eval else 0, device=rt.device, dtype=dtype)
+                              n_test=a.n_test if a.eval else 0, device=rt.device, dtype=dtype)
     rt.synchronize()
     gen_s = time.time() - t0
     cfg = SGDConfig(algo=a.algo, n_workers=n_workers, frac=a.frac, eval_every=0,
@@ -154,9 +231,31 @@ def main(argv=None):
     if cfg.algo not in ("ssgd", "gd"):
         samples = a.rows * a.frac * a.steps * (cfg.n_local if cfg.algo in ("ma", "bmuf") else 1)
     value = samples / elapsed
+    ar_us = allreduce_probe(model, rt) if cfg.algo in ("ssgd", "gd") else None
     acc = None
+    witness = None
     if a.eval:
-        acc, _ = model.evaluate()
+        # correctness witness (untimed): train on to the reference's 1500 iterations
+        # (ssgd.py:18, 93) and score the held-out split. The planted model's own accuracy
+        # on that split is the Bayes ceiling; a random w scores ~0.5. Passing needs at
+        # least half the way from chance to the ceiling, which a broken gradient kernel
+        # cannot reach (measured in f64 on 200k x 1024: 0.49 @100, 0.81 @1000, 0.83 @1500,
+        # ceiling 0.83)
+        done = a.warmup + a.steps
+        extra = max(0, a.witness_steps - done)
+        model.run_steps(extra)
+        rt.synchronize()
+        comm.check_device_errors("witness training")
+        acc, loss = model.evaluate()
+        from dalgo.data.datasets import planted_model
+        ws = torch.from_numpy(planted_model(a.dim, 1234)).to(rt.device)
+        d = model.data
+        zs = d.X_test.float() @ ws[:a.dim] + ws[a.dim]
+        bayes = float(((zs > 0).float() == d.y_test).float().mean().item())
+        thr = 0.5 + 0.5 * (bayes - 0.5)
+        witness = {"heldout_accuracy": acc, "heldout_logloss": loss, "n_test": a.n_test,
+                   "trained_steps": done + extra, "planted_model_accuracy": bayes,
+                   "threshold": thr, "passed": bool(acc >= thr)}
     if rt.is_main:
         out = {
             "metric": BASELINE_METRIC,
@@ -181,10 +280,27 @@ def main(argv=None):
         }
         if cal:
             out["launch_calibration_ms_per_step"] = cal
-        if acc is not None:
+        from dalgo.parallel import xgmi
+        out["world_size"] = W
+        out["device_ids"] = list(rt.device_ids)
+        out["distinct_devices"] = len(set(rt.device_ids))
+        out["shared_device"] = rt.shared_device
+        out["backend"] = rt.backend
+        if rt.device.type == "cuda":
+            try:
+                out["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
+            except Exception:
+                out["rccl_version"] = None
+        out["small_allreduce_race"] = xgmi.last_race
+        out["allreduce_us_per_step"] = ar_us
+        if witness is not None:
             out["heldout_accuracy"] = acc
+            out["correctness_witness"] = witness
         print(json.dumps(out), flush=True)
     runtime.shutdown()
+    if witness is not None and not witness["passed"]:
+        raise SystemExit(f"[bench] correctness witness failed: held-out accuracy {acc:.4f} < "
+                         f"{witness['threshold']:.4f}")
 
 
 if __name__ == "__main__":

@@ -1,6 +1,8 @@
 """graph_computation/transitive_closure.py entry logic."""
 from __future__ import annotations
 
+import hashlib
+
 import torch
 
 from dalgo.models.transitive_closure import DenseClosure, SparseClosure, compact_ids
@@ -41,14 +43,20 @@ def main(argv=None):
         tc = SparseClosure(s, d, rt.rank, rt.world_size, n=n, device=rt.device)
     # per-rank state (each rank owns the paths of its target slice)
     name = f"closure_{engine}_w{rt.world_size}"
+    # the input graph's identity travels with every per-rank checkpoint
+    fp = hashlib.sha1(s.numpy().astype("int64").tobytes() + b"|" +
+                      d.numpy().astype("int64").tobytes()).hexdigest() + f"/n={n}"
     if a.resume and a.ckpt_dir:
-        sd = checkpoint.load(a.ckpt_dir, name, rt.rank, per_rank=True)
+        sd = checkpoint.load_consistent(a.ckpt_dir, name, rt.rank, fingerprint=fp,
+                                        progress=lambda st: len(st["counts"]))
         if sd is not None:
             tc.load_state_dict(sd)
             rt.log("resumed after %d rounds" % (len(tc.counts) - 1))
 
     def save(m):
-        checkpoint.save(m.state_dict(), a.ckpt_dir, name, rt.rank, per_rank=True)
+        st = m.state_dict()
+        st["fingerprint"] = fp
+        checkpoint.save(st, a.ckpt_dir, name, rt.rank, per_rank=True)
 
     def cb(m):
         if a.ckpt_dir and a.ckpt_every and (len(m.counts) - 1) % a.ckpt_every == 0:

@@ -288,6 +288,9 @@ class ParallelSGD:
                 torch.cuda.synchronize(self.device)
                 self._graph_warm = True
                 return
+            # a deferred EASGD centre update of the warm step must land before capture:
+            # the captured step must not contain (or wait on) a collective issued eagerly
+            self._finish_center()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._step_impl(0, self._t_dev)
@@ -393,10 +396,21 @@ class ParallelSGD:
                 U.sync_update(self.w, U.ELASTIC_CENTER, S=self.S, beta=c.beta, inv_p=self.inv_p)
 
     def _overlap_ok(self, step_dev=None) -> bool:
-        """EASGD centre all-reduce deferred under the next gradient (several ranks, eager)."""
-        return (self.cfg.algo == "easgd" and self.cfg.overlap_center and comm.world_size() > 1
-                and step_dev is None and os.environ.get("DALGO_EASGD_OVERLAP", "1") != "0"
-                and not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()))
+        """EASGD centre all-reduce deferred under the next gradient (several ranks, eager).
+
+        Never under hipGraph replay (the captured step would consume a collective issued
+        outside the graph) and never when the small-vector all-reduce goes through K11:
+        the async form would route the centre through the process group instead of the
+        one-shot exchange the start-up race chose."""
+        if not (self.cfg.algo == "easgd" and self.cfg.overlap_center and comm.world_size() > 1
+                and step_dev is None and os.environ.get("DALGO_EASGD_OVERLAP", "1") != "0"):
+            return False
+        if self._graph_ok():
+            return False
+        if self.device.type == "cuda":
+            if torch.cuda.is_current_stream_capturing() or comm.uses_xgmi(self.S):
+                return False
+        return True
 
     def _finish_center(self):
         """Complete a deferred EASGD centre update: w = (1-beta) w + beta * sum(locals)/P."""
@@ -407,6 +421,15 @@ class ParallelSGD:
         work.wait()
         c = self.cfg
         U.sync_update(self.w, U.ELASTIC_CENTER, S=self.S, beta=c.beta, inv_p=self.inv_p)
+
+    def _maybe_check_errors(self):
+        """Collective device-error check every DALGO_ERRCHECK_EVERY evaluations (default
+        100; also at end of fit, checkpoints and shutdown) instead of every evaluation:
+        each check is an extra collective plus host syncs on a ~50 us step."""
+        self._n_evals = getattr(self, "_n_evals", 0) + 1
+        every = int(os.environ.get("DALGO_ERRCHECK_EVERY", "100"))
+        if every > 0 and self._n_evals % every == 0:
+            comm.check_device_errors("evaluation")
 
     def evaluate(self):
         self._flush()
@@ -431,7 +454,7 @@ class ParallelSGD:
                 self.run_steps(k)
                 done += k
                 if ev and self.t % ev == 0:
-                    comm.check_device_errors("evaluation")
+                    self._maybe_check_errors()
                     acc, loss = self.evaluate()
                     self.history.accs.append(acc)
                     self.history.losses.append(loss)
@@ -445,7 +468,7 @@ class ParallelSGD:
                 self.rt.log("On iteration %d" % (self.t + 1))
             self.step()
             if self.cfg.eval_every and (self.t % self.cfg.eval_every == 0):
-                comm.check_device_errors("evaluation")
+                self._maybe_check_errors()
                 acc, loss = self.evaluate()
                 self.history.accs.append(acc)
                 self.history.losses.append(loss)

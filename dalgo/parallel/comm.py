@@ -47,6 +47,11 @@ def _xgmi_for(t: torch.Tensor):
     return xgmi.shared(t.device)   # collective on first use; None if disabled / failed
 
 
+def uses_xgmi(t: torch.Tensor) -> bool:
+    """Would a synchronous all_reduce_sum of ``t`` take the K11 one-shot path?"""
+    return _active() and _xgmi_for(t) is not None
+
+
 def all_reduce_sum(t: torch.Tensor, async_op: bool = False):
     """In-place SUM all-reduce (identity at world size 1).
 

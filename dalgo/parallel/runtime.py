@@ -3,10 +3,18 @@
 The reference obtains its workers from an external Spark runtime
 (``SparkSession.builder.appName(..).getOrCreate()``, optimization/ssgd.py:78-81;
 ``spark.stop()``, ssgd.py:117). Here every rank is an SPMD process started by
-``torchrun`` (or :func:`dalgo.parallel.launch.spawn`), bound to GPU
-``LOCAL_RANK``, talking RCCL (torch backend ``"nccl"``) over xGMI; on CPU-only
-hosts the same code runs on ``gloo``. A single process without any launcher
-environment is a valid world of size 1 (no process group needed).
+``torchrun`` (``bench.py --gpus N`` starts it as a child process by itself),
+bound to GPU ``LOCAL_RANK``, talking RCCL (torch backend ``"nccl"``) over xGMI;
+on CPU-only hosts the same code runs on ``gloo``. A single process without any
+launcher environment is a valid world of size 1 (no process group needed).
+
+Device sharing rule: at init every rank publishes the identity of its GPU
+(host, PCI domain/bus/device, UUID). When two ranks sit on the same physical
+GPU (the one-GPU multi-rank rehearsals), :attr:`Runtime.shared_device` is True
+on EVERY rank, and the library never builds a kernel that waits on another
+process's kernel (K11 one-shot exchange, persistent / one-kernel K1 forms):
+those need the peer kernels co-resident on other CUs, which one shared device
+does not guarantee.
 """
 from __future__ import annotations
 
@@ -27,6 +35,10 @@ class Runtime:
     device: torch.device = torch.device("cpu")
     backend: str = "none"
     app_name: str = "dalgo"
+    # identity string of every rank's device (index = rank); "cpu" on CPU ranks
+    device_ids: tuple = ()
+    # True on every rank when any two ranks share one physical GPU
+    shared_device: bool = False
 
     @property
     def is_main(self) -> bool:
@@ -100,9 +112,40 @@ def init(backend: str | None = None, *, device: str | None = None, app_name: str
         if backend == "nccl":
             kw["device_id"] = dev
         dist.init_process_group(**kw)
+    ident = device_identity(dev)
+    ids = (ident,)
+    if world > 1:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, ident)
+        ids = tuple(gathered)
+    shared = any(i != "cpu" and ids.count(i) > 1 for i in ids)
     _RT = Runtime(rank=rank, world_size=world, local_rank=local_rank, device=dev,
-                  backend=backend if world > 1 else "none", app_name=app_name)
+                  backend=backend if world > 1 else "none", app_name=app_name,
+                  device_ids=ids, shared_device=shared)
     return _RT
+
+
+def device_identity(dev: torch.device) -> str:
+    """Host-unique identity of a physical device ("cpu" for CPU ranks): hostname plus
+    PCI domain:bus:device plus UUID, so two ranks whose HIP_VISIBLE_DEVICES map
+    different indices to one card still compare equal."""
+    if dev.type != "cuda":
+        return "cpu"
+    import socket
+    p = torch.cuda.get_device_properties(dev)
+    pci = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    return f"{socket.gethostname()}/{pci}/{p.uuid}"
+
+
+def spin_waits_allowed() -> bool:
+    """May this run launch kernels that wait on another process's kernels?
+
+    False whenever ranks share a physical GPU, unless the opt-in rehearsal switch
+    ``DALGO_ALLOW_SHARED_SPIN=1`` is set (tests marked ``gpu_shared`` only)."""
+    rt = _RT
+    if rt is None or not rt.shared_device:
+        return True
+    return os.environ.get("DALGO_ALLOW_SHARED_SPIN", "0") == "1"
 
 
 def get() -> Runtime:

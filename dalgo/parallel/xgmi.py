@@ -17,7 +17,10 @@ word instead of hanging; :meth:`XgmiAllReduce.check` raises if it ever fired.
 Selection (``DALGO_XGMI``): ``auto`` (default) times K11 against the process
 group's all-reduce on a bucket-sized vector right after the self-test and keeps
 whichever is faster (max over ranks, so all ranks agree); ``1`` forces K11 (if the
-self-test passes), ``0`` disables it. ``DALGO_XGMI_TIMEOUT`` (s, default 60).
+self-test passes), ``0`` disables it. ``DALGO_XGMI_TIMEOUT`` (s, default 5; capped
+at 2 s when ranks share a GPU). K11 is never built when two ranks share one
+physical GPU (:func:`dalgo.parallel.runtime.spin_waits_allowed`): its peer wait
+would then depend on another process's kernel being co-resident on the same CUs.
 """
 from __future__ import annotations
 
@@ -31,6 +34,15 @@ from dalgo.ops import _ext
 
 MAX_RANKS = 8
 SLOT_FLOATS = 4096          # largest vector (floats) handled; larger buckets use RCCL
+
+
+def _default_timeout() -> float:
+    from dalgo.parallel import runtime
+    t = float(os.environ.get("DALGO_XGMI_TIMEOUT", "5"))
+    rt = runtime._RT
+    if rt is not None and rt.shared_device:
+        t = min(t, 2.0)
+    return t
 
 
 def _agree(ok: bool, device) -> bool:
@@ -55,8 +67,7 @@ class XgmiAllReduce:
             raise ValueError(f"xGMI all-reduce supports at most {MAX_RANKS} ranks")
         self.device = torch.device(device)
         self.slot = int(slot_floats)
-        self.timeout_s = float(timeout_s if timeout_s is not None
-                               else os.environ.get("DALGO_XGMI_TIMEOUT", "60"))
+        self.timeout_s = float(timeout_s if timeout_s is not None else _default_timeout())
         self.own = 0
         self.opened = []
         self.bufs = []
@@ -167,6 +178,8 @@ def _self_test(xg: XgmiAllReduce) -> bool:
 
 
 _shared: dict = {}
+# outcome of the start-up K11-vs-process-group race (bench JSON): None until a race ran
+last_race: dict | None = None
 
 
 def _race(xg: XgmiAllReduce, n: int = 1025, iters: int = 50) -> tuple[float, float]:
@@ -200,11 +213,14 @@ def shared(device: torch.device) -> XgmiAllReduce | None:
         return _shared[key]
     inst = None
     mode = os.environ.get("DALGO_XGMI", "auto")
+    from dalgo.parallel import runtime
+    if mode in ("1", "auto") and not runtime.spin_waits_allowed():
+        mode = "0"   # ranks share a GPU: no cross-process spin-waiting kernels (collective)
     if (mode in ("1", "auto") and dist.is_initialized()
             and 1 < dist.get_world_size() <= MAX_RANKS and torch.device(device).type == "cuda"
             and _ext.available()):
         try:
-            inst = XgmiAllReduce(device, timeout_s=10.0)
+            inst = XgmiAllReduce(device, timeout_s=min(2.0, _default_timeout()))
         except Exception as e:   # consistent on every rank (collective construction)
             if dist.get_rank() == 0:
                 print(f"[dalgo] xGMI all-reduce unavailable: {e}", file=sys.stderr)
@@ -216,9 +232,12 @@ def shared(device: torch.device) -> XgmiAllReduce | None:
                 print(f"[dalgo] rank {dist.get_rank()}: xGMI self-test error: {e}", file=sys.stderr)
                 ok = False
             if _agree(ok, device):
-                inst.timeout_s = float(os.environ.get("DALGO_XGMI_TIMEOUT", "60"))
+                inst.timeout_s = _default_timeout()
                 if mode == "auto":
                     t_k11, t_pg = _race(inst)
+                    global last_race
+                    last_race = {"k11_us": t_k11 / 50 * 1e6, "process_group_us": t_pg / 50 * 1e6,
+                                 "winner": "k11" if t_k11 < t_pg else dist.get_backend()}
                     if dist.get_rank() == 0:
                         print(f"[dalgo] small all-reduce: xGMI one-shot {t_k11 / 50 * 1e6:.1f} us, "
                               f"{dist.get_backend()} {t_pg / 50 * 1e6:.1f} us -> "

@@ -37,3 +37,35 @@ def load(ckpt_dir: str, name: str, rank: int = 0, per_rank: bool = False) -> dic
     if not os.path.exists(p):
         return None
     return torch.load(p, map_location="cpu", weights_only=True)
+
+
+def load_consistent(ckpt_dir: str, name: str, rank: int, *, fingerprint: str,
+                    progress) -> dict | None:
+    """Collective per-rank resume: every rank loads its own file, then all ranks agree.
+
+    Returns the state on every rank when ALL ranks found a file with the expected
+    ``fingerprint`` (e.g. a hash of the input graph) at the same ``progress(state)``
+    (e.g. the round count); None on every rank when no rank found one; raises on every
+    rank otherwise (a crash between two ranks' saves, a missing file on one rank, a
+    checkpoint of a different input) -- ranks that resumed from different points
+    would enter different numbers of collectives and hang or reach a wrong fixpoint."""
+    from dalgo.parallel import comm, runtime
+    sd = load(ckpt_dir, name, rank, per_rank=True)
+    found = sd is not None
+    match = found and sd.get("fingerprint") == fingerprint
+    prog = int(progress(sd)) if match else -1
+    dev = runtime.get().device if comm._active() and \
+        torch.distributed.get_backend() == "nccl" else torch.device("cpu")
+    hi = torch.tensor([int(found), int(match), prog], dtype=torch.int64, device=dev)
+    lo = -hi.clone()
+    comm.all_reduce_max(hi)
+    comm.all_reduce_max(lo)
+    any_found, all_found = int(hi[0]), -int(lo[0])
+    all_match, p_max, p_min = -int(lo[1]), int(hi[2]), -int(lo[2])
+    if not any_found:
+        return None
+    if not (all_found and all_match and p_min == p_max):
+        raise RuntimeError(
+            f"inconsistent resume of {name!r}: found on all ranks={bool(all_found)}, same input "
+            f"on all ranks={bool(all_match)}, progress min/max={p_min}/{p_max}")
+    return sd

@@ -235,3 +235,24 @@ def test_easgd_centre_overlap_is_exact():
         assert np.array_equal(a[0], b[0])
         assert a[1] == b[1]
         assert np.array_equal(a[2], b[2])
+
+
+def _easgd_overlap_rules(rt):
+    """EASGD's deferred centre all-reduce is never used under hipGraph replay: a captured
+    step must not consume a collective issued outside the graph."""
+    from dalgo.data.datasets import breast_cancer
+    from dalgo.models.localsgd import ParallelSGD, SGDConfig
+    from dalgo.parallel.sharding import make_layout
+    cfg = SGDConfig(algo="easgd", n_iterations=4, eval_every=0)
+    lay = make_layout(398, cfg.n_workers, rt.world_size, rt.rank)
+    d = breast_cancer(dtype=torch.float64, row_range=(lay.row_lo, lay.row_hi))
+    m = ParallelSGD(cfg, d, lay, rt, model_dtype=torch.float64)
+    eager = m._overlap_ok()
+    m._okg = True          # as if graph replay had been selected
+    graphed = m._overlap_ok()
+    return eager, graphed
+
+
+def test_easgd_overlap_off_under_graph_replay():
+    res = run_world(_easgd_overlap_rules, world=2)
+    assert all(r == (True, False) for r in res)

@@ -92,6 +92,22 @@ def test_closure_resume_two_ranks_gloo(tmp_path):
     final = [l for l in full.splitlines() if "The original graph has" in l]
     assert final and final == [l for l in res.splitlines() if "The original graph has" in l]
 
+    # a missing per-rank file, or a checkpoint of another graph: every rank refuses
+    bad = tmp_path / "bad"
+    bad.mkdir()
+    import shutil
+    shutil.copy(tmp_path / "closure_sparse_w2.rank0.pt", bad / "closure_sparse_w2.rank0.pt")
+    base_bad = [x if x != str(tmp_path) else str(bad) for x in base]
+    r = subprocess.run([sys.executable] + tr + ["--master-port", str(_port())] + base_bad
+                       + ["--resume"], cwd=ROOT, capture_output=True, text=True, timeout=400,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode != 0 and "inconsistent resume" in r.stderr
+    other = [x if x != "5" else "6" for x in base]
+    r = subprocess.run([sys.executable] + tr + ["--master-port", str(_port())] + other
+                       + ["--resume"], cwd=ROOT, capture_output=True, text=True, timeout=400,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode != 0 and "same input on all ranks=False" in r.stderr
+
 
 def test_als_script():
     out = _run(["matrix_computation/matrix_decomposition.py", "--device", "cpu"])
@@ -154,6 +170,29 @@ def test_bench_cpu_contract():
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in d
     assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0
+
+
+def test_bench_self_launches_n_ranks():
+    """python bench.py --gpus 2 with no launcher environment starts 2 ranks itself
+    (torchrun child process) and reports dp2 with both ranks' device records."""
+    out = _run(["bench.py", "--gpus", "2", "--device", "cpu", "--backend", "gloo", "--rows", "20000",
+                "--dim", "64", "--steps", "3", "--warmup", "1", "--dtype", "f32", "--n-test", "5000"],
+               timeout=600)
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert len(d["device_ids"]) == 2 and d["allreduce_us_per_step"] > 0
+    assert d["correctness_witness"]["passed"] and d["correctness_witness"]["trained_steps"] == 1500
+
+
+def test_bench_refuses_mismatched_world():
+    """--gpus N under a launcher with WORLD_SIZE != N fails loudly (no silent 1-GPU number)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--device", "cpu", "--rows",
+                        "2000", "--dim", "16", "--steps", "1", "--warmup", "0"], cwd=ROOT,
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stdout + r.stderr)
 
 
 def test_module_dispatcher():

@@ -3,6 +3,12 @@
 RCCL refuses two ranks on one GPU, so this exercises everything of the N-GPU path
 except the transport: sharded on-device data, HIP kernels per rank, collectives on
 GPU tensors, rank-0 reporting and the bench JSON contract.
+
+Default (``-m gpu``) cases never run a kernel that waits on another process's kernel:
+the library sees that the ranks share one device (runtime.shared_device) and builds
+no K11 exchange and no persistent / one-kernel K1 form. The K11 / persistent
+rehearsals, which DO spin across processes on one GPU, are marked ``gpu_shared`` and
+run only when DALGO_GPU_SHARED_TESTS=1 (own gpurun sessions, never the round-end tier).
 """
 import json
 import os
@@ -24,8 +30,9 @@ def _port():
     return p
 
 
-def _torchrun(args, n=2, timeout=600):
+def _torchrun(args, n=2, timeout=600, env_extra=None):
     env = dict(os.environ, PYTHONPATH=ROOT)
+    env.update(env_extra or {})
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
@@ -55,17 +62,33 @@ def test_scripts_two_ranks_gloo_on_one_gpu(cuda, script, extra, needle):
     assert needle in out
 
 
+SPIN = {"DALGO_ALLOW_SHARED_SPIN": "1"}
+
+
+def test_shared_gpu_disables_cross_process_waits(cuda):
+    """Two ranks on one GPU: every rank sees shared_device, K11 is never built (so no
+    persistent / one-kernel form either) and the bench reports the process group."""
+    out = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--rows", "200000",
+                     "--steps", "5", "--warmup", "2"], env_extra={"DALGO_XGMI": "1"})
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+    assert d["shared_device"] is True and d["distinct_devices"] == 1
+    assert d["config"]["allreduce"] == "gloo" and d["config"]["launch"] == "per-step"
+    assert d["correctness_witness"]["passed"]
+
+
+@pytest.mark.gpu_shared
 @pytest.mark.parametrize("n", [2, 4, 8])
 def test_xgmi_allreduce_ranks_on_one_gpu(cuda, n):
     """K11: IPC exchange buffers + flag protocol, exact rank-ordered sums on every rank."""
-    out = _torchrun(["tests/helpers/xgmi_check.py"], n=n)
+    out = _torchrun(["tests/helpers/xgmi_check.py"], n=n, env_extra=SPIN)
     assert f"XGMI_OK world={n}" in out
 
 
+@pytest.mark.gpu_shared
 def test_xgmi_timeout_raises_on_every_rank(cuda):
     """A K11 peer wait that times out on rank 0 only: the collective check raises on
     both ranks and shutdown exits non-zero (no rank silently continues)."""
-    env = dict(os.environ, PYTHONPATH=ROOT)
+    env = dict(os.environ, PYTHONPATH=ROOT, **SPIN)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            "tests/helpers/xgmi_timeout.py"]
@@ -82,6 +105,7 @@ def _final_w(out):
     return np.array([float(v) for v in txt.replace("[", " ").replace("]", " ").split()])
 
 
+@pytest.mark.gpu_shared
 @pytest.mark.parametrize("one_kernel", ["1", "0", "persistent"])
 @pytest.mark.parametrize("algo", ["ssgd", "logistic_regression"])
 def test_fused_xgmi_update_matches_process_group(cuda, algo, one_kernel):
@@ -93,34 +117,21 @@ def test_fused_xgmi_update_matches_process_group(cuda, algo, one_kernel):
     args = [script, "--device", "cuda", "--backend", "gloo", "--no-plot", "--quiet",
             "--synthetic", "40000,64", "--n-iterations", "30", "--dtype", "f32",
             "--eval-every", "10"]   # persistent mode: 10-step launches between evaluations
-    os.environ["DALGO_XGMI"] = "1"
     env_key = "DALGO_PERSISTENT" if one_kernel == "persistent" else "DALGO_ONE_KERNEL"
-    os.environ[env_key] = "1" if one_kernel == "persistent" else one_kernel
-    try:
-        fused = _torchrun(args)
-    finally:
-        del os.environ["DALGO_XGMI"]
-        del os.environ[env_key]
-    os.environ["DALGO_XGMI"] = "0"
-    try:
-        plain = _torchrun(args)
-    finally:
-        del os.environ["DALGO_XGMI"]
+    fused = _torchrun(args, env_extra=dict(SPIN, DALGO_XGMI="1", **{
+        env_key: "1" if one_kernel == "persistent" else one_kernel}))
+    plain = _torchrun(args, env_extra={"DALGO_XGMI": "0"})
     wf, wp = _final_w(fused), _final_w(plain)
     assert wf.shape == wp.shape and np.allclose(wf, wp, rtol=1e-4, atol=1e-5), (wf[:5], wp[:5])
 
 
+@pytest.mark.gpu_shared
 def test_bench_launch_calibration_two_ranks(cuda):
     """bench.py --launch auto with the K11 exchange: the per-step, one-kernel and
     persistent forms are each timed on both ranks and one is kept (same on every rank)."""
-    os.environ["DALGO_XGMI"] = "1"
-    os.environ["DALGO_CAL_SHARED"] = "1"
-    try:
-        out = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--rows", "200000",
-                         "--steps", "5", "--warmup", "2", "--cal-steps", "4"])
-    finally:
-        del os.environ["DALGO_XGMI"]
-        del os.environ["DALGO_CAL_SHARED"]
+    out = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--rows", "200000",
+                     "--steps", "5", "--warmup", "2", "--cal-steps", "4"],
+                    env_extra=dict(SPIN, DALGO_XGMI="1"))
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
     cal = d["launch_calibration_ms_per_step"]
     assert set(cal) == {"per-step", "one-kernel", "persistent"}
@@ -128,20 +139,22 @@ def test_bench_launch_calibration_two_ranks(cuda):
     assert d["config"]["allreduce"] == "xgmi-oneshot (K11)" and d["value"] > 0
 
 
+@pytest.mark.gpu_shared
 def test_bench_auto_selects_allreduce(cuda):
     """DALGO_XGMI=auto (default): the start-up race picks a path and reports it."""
     out = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--rows", "200000",
-                     "--steps", "5", "--warmup", "2"])
+                     "--steps", "5", "--warmup", "2"], env_extra=SPIN)
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
     assert d["config"]["allreduce"] in ("xgmi-oneshot (K11)", "gloo")
 
 
+@pytest.mark.gpu_shared
 def test_bench_eight_ranks_on_one_gpu(cuda):
     """World size 8 (the driver's largest N), 8 ranks sharing cuda:0: sharding of the
     10M-row global set into 1.25M-row shards, the 8-peer K11 exchange (or gloo if the
     start-up race prefers it), rank-0 JSON with the whole-job aggregate."""
     out = _torchrun(["bench.py", "--gpus", "8", "--backend", "gloo", "--rows", "400000",
-                     "--steps", "5", "--warmup", "2"], n=8)
+                     "--steps", "5", "--warmup", "2"], n=8, env_extra=SPIN)
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
     assert d["n_gpus"] == 8 and d["steps"] == 5 and d["config"]["parallelism"] == "dp8"
     assert d["config"]["allreduce"] in ("xgmi-oneshot (K11)", "gloo")
