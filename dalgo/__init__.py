@@ -7,7 +7,7 @@ decomposition and Monte-Carlo pi. See SURVEY.md for the design blueprint.
 
 Layout:
   dalgo.ops       python wrappers of the HIP kernels (+ torch-CPU references)
-  dalgo.parallel  runtime (process group), collectives, sharding, launcher
+  dalgo.parallel  runtime (process group, device-sharing rule), collectives, K11, sharding
   dalgo.models    the algorithms (drivers of the reference scripts)
   dalgo.data      datasets and on-device synthetic generators
   dalgo.utils     Philox mirror, observability, config, checkpoints

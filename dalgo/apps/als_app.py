@@ -22,6 +22,8 @@ def main(argv=None):
                     n_workers=a.n_slices, seed=a.seed + 7)
     als = ALS(cfg, rt.rank, rt.world_size, device=rt.device)
     sink = obs.MetricsSink(a.metrics_out, rt.rank)
+    if sink.enabled or obs.roctx_enabled():
+        als.timer = obs.PhaseTimer(rt.device)
 
     if a.resume and a.ckpt_dir:
         sd = checkpoint.load(a.ckpt_dir, "als_state")
@@ -31,7 +33,9 @@ def main(argv=None):
 
     def cb(m):
         rt.log("iterations: %d, rmse: %f" % (m.t - 1, m.history.rmse[-1]))   # :67
-        sink.log(iteration=m.t, rmse=m.history.rmse[-1])
+        sink.log(phases=m.timer.take() if m.timer else None, iteration=m.t,
+                 rmse=m.history.rmse[-1], bytes_allgathered=m.bytes_gathered,
+                 world_size=rt.world_size)
         if a.ckpt_dir and a.ckpt_every and m.t % a.ckpt_every == 0:
             checkpoint.save(m.state_dict(), a.ckpt_dir, "als_state", rt.rank)
 

@@ -2,12 +2,13 @@
 from __future__ import annotations
 
 import hashlib
+import time
 
 import torch
 
 from dalgo.models.transitive_closure import DenseClosure, SparseClosure, compact_ids
 from dalgo.parallel import runtime
-from dalgo.utils import checkpoint
+from dalgo.utils import checkpoint, obs
 from dalgo.utils.cli import add_ckpt_args, common_parser, init_from_args
 
 TOY_EDGES = [(1, 2), (1, 3), (2, 3), (3, 1)]   # transitive_closure.py:18
@@ -58,11 +59,23 @@ def main(argv=None):
         st["fingerprint"] = fp
         checkpoint.save(st, a.ckpt_dir, name, rt.rank, per_rank=True)
 
+    sink = obs.MetricsSink(a.metrics_out, rt.rank)
+    if sink.enabled or obs.roctx_enabled():
+        tc.timer = obs.PhaseTimer(rt.device)
+    t_last = [time.time()]
+
     def cb(m):
+        now = time.time()
+        sink.log(phases=m.timer.take() if m.timer else None, round=len(m.counts) - 1,
+                 paths=m.counts[-1], round_s=now - t_last[0], engine=engine,
+                 bytes_allreduced=8 * (len(m.counts) - 1) if rt.world_size > 1 else 0,
+                 world_size=rt.world_size)
+        t_last[0] = now
         if a.ckpt_dir and a.ckpt_every and (len(m.counts) - 1) % a.ckpt_every == 0:
             save(m)
 
     res = tc.run(a.max_rounds, callback=cb)
+    sink.close()
     if a.ckpt_dir:
         save(tc)
     if not a.quiet:

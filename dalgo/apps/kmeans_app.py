@@ -47,16 +47,18 @@ def main(argv=None):
         if sd is not None:
             km.load_state_dict(sd)
             rt.log(f"Resumed from iteration {km.t}")
+    sink = obs.MetricsSink(a.metrics_out, rt.rank)
+    if sink.enabled or obs.roctx_enabled():
+        km.timer = obs.PhaseTimer(rt.device)
     while km.t < a.n_iterations:
         km.fit(1)
+        sink.log(phases=km.timer.take() if km.timer else None, iteration=km.t,
+                 sse=km.history.sse[-1], shift2=km.history.shift[-1],
+                 bytes_allreduced=km.bytes_allreduced, world_size=rt.world_size)
         if a.ckpt_dir and a.ckpt_every and km.t % a.ckpt_every == 0:
             checkpoint.save(km.state_dict(), a.ckpt_dir, "kmeans_state", rt.rank)
         if cfg.tol is not None and km.history.shift and km.history.shift[-1] < cfg.tol:
             break
-    hist = km.history
-    sink = obs.MetricsSink(a.metrics_out, rt.rank)
-    for i, (s, sh) in enumerate(zip(hist.sse, hist.shift)):
-        sink.log(iteration=i + 1, sse=s, shift2=sh)
     C = km.centers.cpu().numpy()
     rt.log("Final centers: " + str([np.array(c) for c in C]))
     if a.ckpt_dir:

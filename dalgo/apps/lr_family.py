@@ -85,6 +85,8 @@ def main(algo: str, argv=None):
     if a.graph != "auto":
         model.graph = a.graph == "on"
     sink = obs.MetricsSink(a.metrics_out, rt.rank)
+    if sink.enabled or obs.roctx_enabled():
+        model.timer = obs.PhaseTimer(rt.device)
     ck_name = f"{algo}_state"
     if a.resume and a.ckpt_dir:
         sd = checkpoint.load(a.ckpt_dir, ck_name, rt.rank, per_rank=True)
@@ -97,9 +99,14 @@ def main(algo: str, argv=None):
     remaining = max(0, cfg.n_iterations - model.t)
 
     def cb(m):
-        if sink.path and m.history.accs and m.history.iters[-1] == m.t:
-            sink.log(algo=algo, iteration=m.t, accuracy=m.history.accs[-1],
-                     loss=m.history.losses[-1], elapsed_s=time.time() - t0)
+        if sink.enabled:
+            rec = dict(algo=algo, iteration=m.t, elapsed_s=time.time() - t0,
+                       bytes_allreduced=m.bytes_allreduced, world_size=rt.world_size)
+            if m.history.accs and m.history.iters[-1] == m.t:
+                rec.update(accuracy=m.history.accs[-1], loss=m.history.losses[-1])
+            sink.log(phases=m.timer.take(), **rec)
+        elif m.timer is not None:
+            m.timer.take()
         if a.ckpt_dir and a.ckpt_every and m.t % a.ckpt_every == 0:
             checkpoint.save(m.state_dict(), a.ckpt_dir, ck_name, rt.rank, per_rank=True)
 

@@ -7,7 +7,7 @@ from dalgo.models.pagerank import PageRank, PageRankConfig
 from dalgo.models.transitive_closure import compact_ids
 from dalgo.ops import graph as G
 from dalgo.parallel import runtime
-from dalgo.utils import checkpoint
+from dalgo.utils import checkpoint, obs
 from dalgo.utils.cli import add_ckpt_args, common_parser, init_from_args
 
 TOY_EDGES = [(1, 2), (1, 3), (2, 3), (3, 1)]   # pagerank.py:35-38
@@ -130,8 +130,14 @@ def main(argv=None):
         if sd is not None:
             pr.load_state_dict(sd)
             rt.log(f"Resumed from iteration {pr.t}")
+    sink = obs.MetricsSink(a.metrics_out, rt.rank)
+    if sink.enabled or obs.roctx_enabled():
+        pr.timer = obs.PhaseTimer(rt.device)
     while pr.t < a.n_iterations:
         pr.step()
+        sink.log(phases=pr.timer.take() if pr.timer else None, iteration=pr.t,
+                 bytes_exchanged=getattr(pr, "bytes_exchanged", 0), world_size=rt.world_size,
+                 exchange=pr.exchange)
         if a.ckpt_dir and a.ckpt_every and pr.t % a.ckpt_every == 0:
             checkpoint.save(pr.state_dict(), a.ckpt_dir, "pagerank_state", rt.rank, per_rank=True)
     if a.ckpt_dir:
@@ -150,5 +156,6 @@ def main(argv=None):
         for v, r in items:
             vid = int(ids[v]) if ids is not None else v
             print("%s has rank: %s." % (vid, r))
+    sink.close()
     runtime.shutdown()
     return ranks if ids is None else {int(ids[v]): r for v, r in ranks.items()}

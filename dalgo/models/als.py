@@ -27,6 +27,7 @@ from dalgo.ops import _ext
 from dalgo.ops import random as drandom
 from dalgo.parallel import comm
 from dalgo.parallel.sharding import even_slices
+from dalgo.utils.obs import NULL_PHASE
 
 
 @dataclass
@@ -114,6 +115,11 @@ class ALS:
             comm.all_reduce_sum(self.R2)
         self.history = ALSHistory()
         self.t = 0
+        self.timer = None   # dalgo.utils.obs.PhaseTimer (None = off)
+        self.bytes_gathered = 0
+
+    def _ph(self, name: str):
+        return self.timer.phase(name) if self.timer is not None else NULL_PHASE
 
     def _uniform(self, rows, cols, stream):
         out = torch.empty((rows, cols), dtype=torch.float32, device=self.dev)
@@ -122,12 +128,19 @@ class ALS:
 
     def _gather_rows(self, local: torch.Tensor, slices, full_rows: int) -> torch.Tensor:
         counts = [b - a for a, b in slices]
-        return comm.all_gather_varlen(local, counts) if self.world > 1 else local
+        if self.world == 1:
+            return local
+        with self._ph("allgather"):
+            out = comm.all_gather_varlen(local, counts)
+        self.bytes_gathered += out.numel() * out.element_size()
+        return out
 
     def _half(self, R_local: torch.Tensor, F: torch.Tensor, x_dim: int) -> torch.Tensor:
-        G = gram(F)                                         # Gram, once per half-sweep
-        Ginv = spd_inverse(G.contiguous(), self.cfg.lam * x_dim)
-        return rows_solve(R_local, F, Ginv)                 # all local rows at once (K5)
+        with self._ph("gram+inverse"):
+            G = gram(F)                                     # Gram, once per half-sweep
+            Ginv = spd_inverse(G.contiguous(), self.cfg.lam * x_dim)
+        with self._ph("solve"):
+            return rows_solve(R_local, F, Ginv)             # all local rows at once (K5)
 
     def step(self):
         c = self.cfg
@@ -173,7 +186,8 @@ class ALS:
         n = self.cfg.n_iterations if n_iterations is None else n_iterations
         for _ in range(n):
             self.step()
-            self.history.rmse.append(self.rmse())
+            with self._ph("rmse"):
+                self.history.rmse.append(self.rmse())
             if callback:
                 callback(self)
         return self.history

@@ -8,9 +8,12 @@ drops below it (off by default = reference behaviour).
 
 SPMD version per iteration, every rank on its HBM-resident row shard:
   K2 assign (MFMA distance GEMM + argmin)  ->  K3 per-cluster sums/counts  ->
-  all_reduce(sums [k x DP] f32) + all_reduce(counts int64)  ->  fused update.
-The reduceByKey shuffle + driver collect become two RCCL all-reduces whose size
-is independent of N (528 KB at k=1024, d=128).
+  ONE all_reduce of the fused f32 bucket [sums k x DP || counts as 2 x k exact f32
+  words]  ->  fused update.
+The reduceByKey shuffle + driver collect become one RCCL all-reduce whose size is
+independent of N (520 KB at k=1024, d=128). Counts travel as (cnt mod 2^b,
+cnt >> b) f32 pairs with b = 24 - ceil(log2 W) (21 at 8 ranks): every partial sum
+of the low words stays below 2^24, so the f32 reduction is exact.
 """
 from __future__ import annotations
 
@@ -21,6 +24,7 @@ import torch
 
 from dalgo.ops import kmeans as K
 from dalgo.parallel import comm
+from dalgo.utils.obs import NULL_PHASE
 
 
 @dataclass
@@ -62,12 +66,20 @@ class KMeans:
             init_centers = self._sample_init()
         self.cen = K.make_centers(init_centers.float(), self.X.dtype, self.dev)
         self.assign = torch.zeros(self.X.shape[0], dtype=torch.int32, device=self.dev)
-        self.S = torch.zeros((k, self.DP), dtype=torch.float32, device=self.dev)
+        # [S (k x DP) || count lo (k) || count hi (k)]: one all-reduce per iteration
+        self.bucket = torch.zeros(k * self.DP + 2 * k, dtype=torch.float32, device=self.dev)
+        self.S = self.bucket[: k * self.DP].view(k, self.DP)
+        self._cnt_pair = self.bucket[k * self.DP:].view(2, k)
         self.cnt = torch.zeros(k, dtype=torch.int64, device=self.dev)
+        self.bytes_allreduced = 0
         self.sse = torch.zeros(1, dtype=torch.float64, device=self.dev)
         self.shift2 = torch.zeros(1, dtype=torch.float32, device=self.dev)
         self.history = KMeansHistory()
         self.t = 0
+        self.timer = None   # dalgo.utils.obs.PhaseTimer (None = off)
+
+    def _ph(self, name: str):
+        return self.timer.phase(name) if self.timer is not None else NULL_PHASE
 
     def _sample_init(self) -> torch.Tensor:
         ids = sample_rows(self.n_global, self.cfg.k, self.cfg.seed)
@@ -85,11 +97,22 @@ class KMeans:
         self.S.zero_()
         self.cnt.zero_()
         self.shift2.zero_()
-        K.assign(self.X, self.cen, out=self.assign, sse=self.sse)
-        K.accumulate(self.X, self.assign, self.cfg.k, self.DP, self.S, self.cnt)
-        comm.all_reduce_sum(self.S)
-        comm.all_reduce_sum(self.cnt)
-        K.update(self.cen, self.S, self.cnt, self.shift2)
+        with self._ph("assign"):
+            K.assign(self.X, self.cen, out=self.assign, sse=self.sse)
+        with self._ph("accumulate"):
+            K.accumulate(self.X, self.assign, self.cfg.k, self.DP, self.S, self.cnt)
+        W = comm.world_size()
+        if W > 1:
+            with self._ph("allreduce"):
+                b = 24 - max(1, (W - 1).bit_length())
+                self._cnt_pair[0].copy_(self.cnt & ((1 << b) - 1))
+                self._cnt_pair[1].copy_(self.cnt >> b)
+                comm.all_reduce_sum(self.bucket)
+                torch.add(self._cnt_pair[0].to(torch.int64),
+                          self._cnt_pair[1].to(torch.int64) << b, out=self.cnt)
+            self.bytes_allreduced += self.bucket.numel() * 4
+        with self._ph("update"):
+            K.update(self.cen, self.S, self.cnt, self.shift2)
         self.t += 1
 
     def fit(self, n_iterations: int | None = None, track: bool = True):

@@ -35,6 +35,7 @@ from dalgo.ops import update as U
 from dalgo.parallel import comm
 from dalgo.parallel.runtime import Runtime
 from dalgo.parallel.sharding import ShardLayout
+from dalgo.utils.obs import NULL_PHASE
 
 ALGOS = ("ssgd", "gd", "ma", "bmuf", "easgd")
 
@@ -171,6 +172,19 @@ class ParallelSGD:
         self._t_dev_val = 0
         self._upd = dict(mode=0 if algo == "ssgd" else 1, reg=U.REG.get(cfg.reg, 0), eta=cfg.eta,
                          lam=cfg.lam, reg_alpha=cfg.reg_alpha)
+        # observability (dalgo.utils.obs.PhaseTimer; None = off, no per-step cost) and
+        # the running count of bytes this rank all-reduced
+        self.timer = None
+        self.bytes_allreduced = 0
+        ar = self.bucket.buffer if algo in ("ssgd", "gd") else self.S
+        self._ar_bytes = ar.numel() * ar.element_size()
+
+    def _ph(self, name: str):
+        return self.timer.phase(name) if self.timer is not None else NULL_PHASE
+
+    def _count_ar(self, n: int = 1):
+        if comm.world_size() > 1:
+            self.bytes_allreduced += n * self._ar_bytes
 
     # ------------------------------------------------------------------ steps
     def _grad(self, W, stream, step_dev=None, step_mul=1):
@@ -215,13 +229,15 @@ class ParallelSGD:
                 self.step()
             return
         c = self.cfg
-        lr_ops.lr_grad(self.data.X_train, self.data.y_train, self.w, self.seg, D=self.D,
-                       has_bias=True, eps=c.eps, seed=c.sample_seed, step=self.t, frac=c.frac,
-                       row_offset=self.data.row_offset, G=self.G, C=self.C,
-                       max_seg_rows=self.max_seg, g_is_zero=self._g_zero,
-                       tail=dict(mode=0 if c.algo == "ssgd" else 1, reg=self._upd["reg"],
-                                 eta=c.eta, lam=c.lam, reg_alpha=c.reg_alpha,
-                                 count_acc=self.count_acc, xg=self.bucket.xg, nsteps=k))
+        with self._ph("persistent_launch"):
+            lr_ops.lr_grad(self.data.X_train, self.data.y_train, self.w, self.seg, D=self.D,
+                           has_bias=True, eps=c.eps, seed=c.sample_seed, step=self.t, frac=c.frac,
+                           row_offset=self.data.row_offset, G=self.G, C=self.C,
+                           max_seg_rows=self.max_seg, g_is_zero=self._g_zero,
+                           tail=dict(mode=0 if c.algo == "ssgd" else 1, reg=self._upd["reg"],
+                                     eta=c.eta, lam=c.lam, reg_alpha=c.reg_alpha,
+                                     count_acc=self.count_acc, xg=self.bucket.xg, nsteps=k))
+        self._count_ar(k)
         self._g_zero = True
         self.t += k
 
@@ -292,13 +308,22 @@ class ParallelSGD:
             # the captured step must not contain (or wait on) a collective issued eagerly
             self._finish_center()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._step_impl(0, self._t_dev)
-                self._t_dev.add_(1)
+            timer, self.timer = self.timer, None     # no timing events inside a capture
+            ar = self.bytes_allreduced
+            try:
+                with torch.cuda.graph(g):
+                    self._step_impl(0, self._t_dev)
+                    self._t_dev.add_(1)
+            finally:
+                self.timer = timer
+            self._ar_per_replay = self.bytes_allreduced - ar
+            self.bytes_allreduced = ar
             self._graphs[key] = g
         if self._t_dev_val != self.t:
             self._t_dev.fill_(self.t)
-        g.replay()
+        with self._ph("step_graph"):
+            g.replay()
+        self.bytes_allreduced += getattr(self, "_ar_per_replay", 0)
         self.t += 1
         self._t_dev_val = self.t
 
@@ -330,70 +355,91 @@ class ParallelSGD:
                                row_offset=self.data.row_offset, G=self.G, C=self.C,
                                max_seg_rows=self.max_seg, count_acc=self.count_acc)
             self.bucket.all_reduce()
+            self._count_ar()
             self._pending = True
         elif c.algo in ("ssgd", "gd") and self._one_kernel():
             # the whole step in ONE launch: gradient, (xGMI exchange,) update
-            lr_ops.lr_grad(self.data.X_train, self.data.y_train, self.w, self.seg, D=self.D,
-                           has_bias=True, eps=c.eps, seed=c.sample_seed, step=t, frac=c.frac,
-                           row_offset=self.data.row_offset, G=self.G, C=self.C,
-                           max_seg_rows=self.max_seg, g_is_zero=self._g_zero,
-                           tail=dict(mode=0 if c.algo == "ssgd" else 1, reg=self._upd["reg"],
-                                     eta=c.eta, lam=c.lam, reg_alpha=c.reg_alpha,
-                                     count_acc=self.count_acc, xg=self.bucket.xg))
+            self._count_ar()
+            with self._ph("step_one_kernel"):
+                lr_ops.lr_grad(self.data.X_train, self.data.y_train, self.w, self.seg, D=self.D,
+                               has_bias=True, eps=c.eps, seed=c.sample_seed, step=t, frac=c.frac,
+                               row_offset=self.data.row_offset, G=self.G, C=self.C,
+                               max_seg_rows=self.max_seg, g_is_zero=self._g_zero,
+                               tail=dict(mode=0 if c.algo == "ssgd" else 1, reg=self._upd["reg"],
+                                         eta=c.eta, lam=c.lam, reg_alpha=c.reg_alpha,
+                                         count_acc=self.count_acc, xg=self.bucket.xg))
             self._g_zero = True
         elif c.algo in ("ssgd", "gd"):
-            self._grad(self.w, t, **sd)
+            with self._ph("sample+grad"):
+                self._grad(self.w, t, **sd)
             xg = self.bucket.xg
+            self._count_ar()
             if xg is not None and self._zg:
                 # K11 all-reduce + K8 update in one launch; leaves the bucket zeroed
-                xg.all_reduce_update_(self.bucket.buffer, self.w, mode=0 if c.algo == "ssgd" else 1,
-                                      reg=self._upd["reg"], eta=c.eta, lam=c.lam,
-                                      reg_alpha=c.reg_alpha, count_index=self.ldw,
-                                      count_acc=self.count_acc)
+                with self._ph("allreduce+update"):
+                    xg.all_reduce_update_(self.bucket.buffer, self.w,
+                                          mode=0 if c.algo == "ssgd" else 1,
+                                          reg=self._upd["reg"], eta=c.eta, lam=c.lam,
+                                          reg_alpha=c.reg_alpha, count_index=self.ldw,
+                                          count_acc=self.count_acc)
                 self._g_zero = True
                 return
-            self.bucket.all_reduce()
-            if c.algo == "ssgd":
-                U.sync_update(self.w, U.SSGD, G=self.G, C=self.C, reg=c.reg, eta=c.eta,
-                              lam=c.lam, reg_alpha=c.reg_alpha, count_acc=self.count_acc,
-                              zero_grad=self._zg)
-            else:
-                U.sync_update(self.w, U.GD_SUM, G=self.G, C=self.C, eta=c.eta,
-                              count_acc=self.count_acc, zero_grad=self._zg)
+            with self._ph("allreduce"):
+                self.bucket.all_reduce()
+            with self._ph("update"):
+                if c.algo == "ssgd":
+                    U.sync_update(self.w, U.SSGD, G=self.G, C=self.C, reg=c.reg, eta=c.eta,
+                                  lam=c.lam, reg_alpha=c.reg_alpha, count_acc=self.count_acc,
+                                  zero_grad=self._zg)
+                else:
+                    U.sync_update(self.w, U.GD_SUM, G=self.G, C=self.C, eta=c.eta,
+                                  count_acc=self.count_acc, zero_grad=self._zg)
             self._g_zero = True
         elif c.algo in ("ma", "bmuf"):
             U.rows_broadcast(self.W, self.w)
             for l in range(c.n_local):
                 stream = t if c.reuse_minibatch else t * c.n_local + l
-                if step_dev is not None:
-                    # stream = (0 | l) + (1 | n_local) * step_dev
-                    self._grad(self.W, 0 if c.reuse_minibatch else l, step_dev,
-                               1 if c.reuse_minibatch else c.n_local)
-                else:
-                    self._grad(self.W, stream)
-                U.sync_update(self.W, U.LOCAL_MEAN, G=self.G, C=self.C, eta=c.eta, zero_grad=self._zg)
+                with self._ph("sample+grad"):
+                    if step_dev is not None:
+                        # stream = (0 | l) + (1 | n_local) * step_dev
+                        self._grad(self.W, 0 if c.reuse_minibatch else l, step_dev,
+                                   1 if c.reuse_minibatch else c.n_local)
+                    else:
+                        self._grad(self.W, stream)
+                with self._ph("local_update"):
+                    U.sync_update(self.W, U.LOCAL_MEAN, G=self.G, C=self.C, eta=c.eta,
+                                  zero_grad=self._zg)
                 self._g_zero = True
-            U.rows_sum(self.W, self.S)
-            comm.all_reduce_sum(self.S)
-            if c.algo == "ma":
-                U.sync_update(self.w, U.AVERAGE, S=self.S, inv_p=self.inv_p)
-            else:
-                U.sync_update(self.w, U.BMUF, S=self.S, Dl=self.Dl, mu=c.mu, zeta=c.zeta,
-                              inv_p=self.inv_p)
+            with self._ph("allreduce"):
+                U.rows_sum(self.W, self.S)
+                comm.all_reduce_sum(self.S)
+            self._count_ar()
+            with self._ph("update"):
+                if c.algo == "ma":
+                    U.sync_update(self.w, U.AVERAGE, S=self.S, inv_p=self.inv_p)
+                else:
+                    U.sync_update(self.w, U.BMUF, S=self.S, Dl=self.Dl, mu=c.mu, zeta=c.zeta,
+                                  inv_p=self.inv_p)
         else:  # easgd
-            self._grad(self.W, t, **sd)
+            with self._ph("sample+grad"):
+                self._grad(self.W, t, **sd)
             # the centre of this round = previous round's locals (easgd.py:104-106): its
             # all-reduce may still be in flight under the gradient kernel above
             self._finish_center()
-            U.sync_update(self.W, U.LOCAL_ELASTIC, G=self.G, C=self.C, center=self.w, eta=c.eta,
-                          alpha=c.alpha, zero_grad=self._zg)
+            with self._ph("local_update"):
+                U.sync_update(self.W, U.LOCAL_ELASTIC, G=self.G, C=self.C, center=self.w,
+                              eta=c.eta, alpha=c.alpha, zero_grad=self._zg)
             self._g_zero = True
             U.rows_sum(self.W, self.S)
+            self._count_ar()
             if self._overlap_ok(step_dev):
                 self._center_work = comm.all_reduce_sum(self.S, async_op=True)
             else:
-                comm.all_reduce_sum(self.S)
-                U.sync_update(self.w, U.ELASTIC_CENTER, S=self.S, beta=c.beta, inv_p=self.inv_p)
+                with self._ph("allreduce"):
+                    comm.all_reduce_sum(self.S)
+                with self._ph("update"):
+                    U.sync_update(self.w, U.ELASTIC_CENTER, S=self.S, beta=c.beta,
+                                  inv_p=self.inv_p)
 
     def _overlap_ok(self, step_dev=None) -> bool:
         """EASGD centre all-reduce deferred under the next gradient (several ranks, eager).
@@ -418,9 +464,11 @@ class ParallelSGD:
         if work is None:
             return
         self._center_work = None
-        work.wait()
+        with self._ph("allreduce_wait"):
+            work.wait()
         c = self.cfg
-        U.sync_update(self.w, U.ELASTIC_CENTER, S=self.S, beta=c.beta, inv_p=self.inv_p)
+        with self._ph("update"):
+            U.sync_update(self.w, U.ELASTIC_CENTER, S=self.S, beta=c.beta, inv_p=self.inv_p)
 
     def _maybe_check_errors(self):
         """Collective device-error check every DALGO_ERRCHECK_EVERY evaluations (default
@@ -437,8 +485,9 @@ class ParallelSGD:
         d = self.data
         if d.X_test.shape[0] == 0:
             return float("nan"), float("nan")
-        correct, loss = lr_ops.lr_eval(d.X_test, d.y_test, self.w, D=self.D, has_bias=True,
-                                       eps=self.cfg.eps)
+        with self._ph("eval"):
+            correct, loss = lr_ops.lr_eval(d.X_test, d.y_test, self.w, D=self.D, has_bias=True,
+                                           eps=self.cfg.eps)
         return int(correct.item()) / d.X_test.shape[0], float(loss.item())
 
     def fit(self, n_iterations: int | None = None, verbose: bool = False, callback=None):

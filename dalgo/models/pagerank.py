@@ -26,6 +26,7 @@ import torch
 
 from dalgo.ops import graph as Gops
 from dalgo.parallel import comm
+from dalgo.utils.obs import NULL_PHASE
 
 
 @dataclass
@@ -186,23 +187,36 @@ class PageRank:
         env = os.environ.get("DALGO_PR_OVERLAP", "auto")
         return env == "1" or (env == "auto" and self.own_share >= 0.25)
 
+    def _ph(self, name: str):
+        t = getattr(self, "timer", None)
+        return t.phase(name) if t is not None else NULL_PHASE
+
     def step(self):
         if self._overlap():
             if self.send_buf is None:
                 self.send_buf = torch.empty(self.send_idx.numel(), dtype=self.fdt, device=self.dev)
-            torch.index_select(self.c_slice, 0, self.send_idx, out=self.send_buf)
-            work = comm.all_to_all_single(self.c_full[self.g.slice_size:], self.send_buf,
-                                          out_split=self.recv_split, in_split=self.send_split,
-                                          async_op=True)
-            self.acc.zero_()
-            self.pres.zero_()
-            Gops.pr_spmv(self.g_own, self.c_full, self.acc, self.pres)
-            work.wait()
-            Gops.pr_spmv(self.g_ghost, self.c_full, self.acc, self.pres, accumulate=True)
+            with self._ph("exchange_issue"):
+                torch.index_select(self.c_slice, 0, self.send_idx, out=self.send_buf)
+                work = comm.all_to_all_single(self.c_full[self.g.slice_size:], self.send_buf,
+                                              out_split=self.recv_split,
+                                              in_split=self.send_split, async_op=True)
+            with self._ph("spmv_own"):
+                self.acc.zero_()
+                self.pres.zero_()
+                Gops.pr_spmv(self.g_own, self.c_full, self.acc, self.pres)
+            with self._ph("exchange_wait"):
+                work.wait()
+            with self._ph("spmv_ghost"):
+                Gops.pr_spmv(self.g_ghost, self.c_full, self.acc, self.pres, accumulate=True)
         else:
-            self._exchange()      # contributions of the previous iteration
-            self._spmv()          # K4 pull SpMV over the local in-edges
-        self._update()        # ranks + next contributions (fused epilogue kernel)
+            with self._ph("exchange"):
+                self._exchange()      # contributions of the previous iteration
+            with self._ph("spmv"):
+                self._spmv()          # K4 pull SpMV over the local in-edges
+        with self._ph("update"):
+            self._update()        # ranks + next contributions (fused epilogue kernel)
+        self.bytes_exchanged = getattr(self, "bytes_exchanged", 0) + \
+            self.exchange_floats() * self.c_slice.element_size()
         self.t += 1
 
     def exchange_floats(self) -> int:

@@ -23,6 +23,7 @@ import torch
 
 from dalgo.ops import _ext
 from dalgo.parallel import comm
+from dalgo.utils.obs import NULL_PHASE
 
 
 @dataclass
@@ -54,6 +55,10 @@ class _Fixpoint:
     per-round counts travel with the path set in ``state_dict`` (checkpoint/resume,
     SURVEY §5), so a resumed run continues the same trajectory."""
     counts: list
+    timer = None   # dalgo.utils.obs.PhaseTimer (None = off)
+
+    def _ph(self, name: str):
+        return self.timer.phase(name) if self.timer is not None else NULL_PHASE
 
     def _initial_count(self) -> int:
         raise NotImplementedError
@@ -65,7 +70,8 @@ class _Fixpoint:
         done = len(self.counts) > 1 and self.counts[-1] == self.counts[-2]
         rounds = 0
         while not done and rounds < max_rounds:
-            nxt = self.step()
+            with self._ph("round"):
+                nxt = self.step()
             self.counts.append(nxt)
             rounds += 1
             done = nxt == cnt

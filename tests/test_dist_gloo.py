@@ -256,3 +256,31 @@ def _easgd_overlap_rules(rt):
 def test_easgd_overlap_off_under_graph_replay():
     res = run_world(_easgd_overlap_rules, world=2)
     assert all(r == (True, False) for r in res)
+
+
+def _kmeans_big_counts(rt):
+    """The fused [S || count pairs] bucket is exact for counts beyond 2^24 per rank."""
+    from dalgo.models.kmeans import KMeans, KMeansConfig
+    X = torch.zeros((8, 2))
+    X[4:, 0] = 1.0
+    km = KMeans(KMeansConfig(k=2, n_iterations=1), X, 8 * rt.rank, 8 * rt.world_size,
+                init_centers=torch.tensor([[0.0, 0.0], [1.0, 0.0]]))
+    from dalgo.ops import kmeans as K
+    orig = K.accumulate
+
+    def fake(Xp, a, k, DP, S, cnt, method="sorted"):
+        orig(Xp, a, k, DP, S, cnt)
+        cnt += (1 << 25) + 12345 * (rt.rank + 1)   # pretend huge clusters
+        return S, cnt
+    K.accumulate = fake
+    try:
+        km.step()
+    finally:
+        K.accumulate = orig
+    return km.cnt.tolist()
+
+
+def test_kmeans_fused_bucket_exact_large_counts():
+    res = run_world(_kmeans_big_counts, world=3)
+    extra = 3 * (1 << 25) + 12345 * 6
+    assert all(r == [12 + extra, 12 + extra] for r in res), res

@@ -236,3 +236,26 @@ def test_pagerank_rmat_world_size_invariant():
                            "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
                           + ["--backend", "gloo"], env_extra={"DALGO_PR_OVERLAP": "0"}, timeout=400))
     assert set(seq) == set(three) and max(abs(seq[v] - three[v]) for v in seq) < 1e-12
+
+
+def test_metrics_jsonl_phases_two_ranks(tmp_path):
+    """--metrics-out: one JSONL line per iteration with the phase split and the bytes
+    all-reduced (2 gloo ranks: non-zero bytes)."""
+    m = tmp_path / "m.jsonl"
+    _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+          "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+          "optimization/ssgd.py", "--device", "cpu", "--backend", "gloo", "--n-iterations", "6",
+          "--quiet", "--no-plot", "--metrics-out", str(m)], timeout=400)
+    recs = [json.loads(l) for l in m.read_text().splitlines()]
+    assert [r["iteration"] for r in recs] == list(range(1, 7))
+    assert set(recs[0]["phase_ms"]) >= {"sample+grad", "allreduce", "update", "eval"}
+    assert recs[-1]["bytes_allreduced"] == 6 * 32 * 8 and recs[0]["world_size"] == 2
+    m2 = tmp_path / "k.jsonl"
+    _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+          "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+          "machine_learning/k-means.py", "--device", "cpu", "--backend", "gloo",
+          "--synthetic", "2000,8", "--k", "4", "--no-plot", "--metrics-out", str(m2)], timeout=400)
+    recs = [json.loads(l) for l in m2.read_text().splitlines()]
+    assert len(recs) == 5 and set(recs[0]["phase_ms"]) >= {"assign", "accumulate", "allreduce",
+                                                           "update"}
+    assert recs[-1]["bytes_allreduced"] == 5 * 4 * (4 * 16 + 2 * 4)
