@@ -658,6 +658,75 @@ void xgmi_allreduce(Tensor x, at::IntArrayRef bufs, int64_t rank, int64_t slot, 
 }
 
 // ---------------------------------------------------------------------------
+// transitive closure, sparse mode (K9 sparse: frontier join + hash-set dedup/merge)
+namespace {
+void check_i64_1d(const Tensor& t, const char* what) {
+  check_dev(t, what);
+  TORCH_CHECK(t.scalar_type() == at::kLong && t.dim() == 1 && t.is_contiguous(),
+              what, ": contiguous 1-D int64");
+}
+uint64_t* u64(const Tensor& t) { return reinterpret_cast<uint64_t*>(t.data_ptr<int64_t>()); }
+uint64_t pow2_mask(const Tensor& table) {
+  const uint64_t n = (uint64_t)table.numel();
+  TORCH_CHECK(n >= 2 && (n & (n - 1)) == 0, "tcs: table size must be a power of two");
+  return n - 1;
+}
+}  // namespace
+
+void tcs_degree(const Tensor& keys, int64_t d0, int64_t nd, const Tensor& in_ptr, Tensor deg) {
+  check_i64_1d(keys, "keys");
+  check_i64_1d(in_ptr, "in_ptr");
+  check_i64_1d(deg, "deg");
+  TORCH_CHECK(d0 >= 0 && nd >= 0 && d0 + nd <= keys.numel() && deg.numel() >= nd, "tcs_degree ranges");
+  DeviceGuard guard(keys.device());
+  DALGO_CHECK_HIP(dalgo_tcs_degree(u64(keys), d0, nd, in_ptr.data_ptr<int64_t>(),
+                                   deg.data_ptr<int64_t>(), cur_stream()),
+                  "tcs_degree");
+}
+
+void tcs_expand(Tensor keys, int64_t d0, int64_t nd, const Tensor& excl, int64_t c_lo,
+                int64_t c_hi, const Tensor& in_ptr, const Tensor& in_src, Tensor table,
+                Tensor n_keys, Tensor err) {
+  check_i64_1d(keys, "keys");
+  check_i64_1d(excl, "excl");
+  check_i64_1d(in_ptr, "in_ptr");
+  check_i64_1d(table, "table");
+  check_i64_1d(n_keys, "n_keys");
+  check_dev(in_src, "in_src");
+  TORCH_CHECK(in_src.scalar_type() == at::kInt && in_src.is_contiguous(), "in_src int32");
+  check_dev(err, "err");
+  TORCH_CHECK(err.scalar_type() == at::kInt, "err int32");
+  TORCH_CHECK(d0 >= 0 && nd >= 0 && d0 + nd <= keys.numel() && excl.numel() >= nd + 1,
+              "tcs_expand: frontier range");
+  TORCH_CHECK(0 <= c_lo && c_lo <= c_hi, "tcs_expand: candidate range");
+  DeviceGuard guard(keys.device());
+  DALGO_CHECK_HIP(dalgo_tcs_expand(u64(keys) + d0, nd, excl.data_ptr<int64_t>(), c_lo, c_hi,
+                                   in_ptr.data_ptr<int64_t>(), in_src.data_ptr<int32_t>(),
+                                   u64(table), pow2_mask(table), u64(keys),
+                                   reinterpret_cast<unsigned long long*>(n_keys.data_ptr<int64_t>()),
+                                   (uint64_t)keys.numel(),
+                                   reinterpret_cast<unsigned*>(err.data_ptr<int>()), cur_stream()),
+                  "tcs_expand");
+}
+
+void tcs_insert(const Tensor& src, Tensor table, bool append, Tensor keys, Tensor n_keys,
+                Tensor err) {
+  check_i64_1d(src, "src");
+  check_i64_1d(table, "table");
+  check_i64_1d(keys, "keys");
+  check_i64_1d(n_keys, "n_keys");
+  check_dev(err, "err");
+  TORCH_CHECK(err.scalar_type() == at::kInt, "err int32");
+  DeviceGuard guard(table.device());
+  DALGO_CHECK_HIP(dalgo_tcs_insert(u64(src), src.numel(), u64(table), pow2_mask(table),
+                                   append ? 1 : 0, u64(keys),
+                                   reinterpret_cast<unsigned long long*>(n_keys.data_ptr<int64_t>()),
+                                   (uint64_t)keys.numel(),
+                                   reinterpret_cast<unsigned*>(err.data_ptr<int>()), cur_stream()),
+                  "tcs_insert");
+}
+
+// ---------------------------------------------------------------------------
 // transitive closure
 void tc_step(const Tensor& A, const Tensor& Told, Tensor Tnew, Tensor count, int64_t variant) {
   for (const Tensor* t : {&A, &Told, static_cast<const Tensor*>(&Tnew)}) {
@@ -824,6 +893,11 @@ TORCH_LIBRARY(dalgo, m) {
         "float timeout_s, Tensor(c!)? W=None, int upd_mode=0, int upd_reg=0, float eta=0., "
         "float lam=0., float reg_alpha=0., int count_index=-1, Tensor(d!)? count_acc=None) -> ()");
   m.def("tc_step(Tensor A, Tensor Told, Tensor(a!) Tnew, Tensor(b!) count, int variant=0) -> ()");
+  m.def("tcs_degree(Tensor keys, int d0, int nd, Tensor in_ptr, Tensor(a!) deg) -> ()");
+  m.def("tcs_expand(Tensor(a!) keys, int d0, int nd, Tensor excl, int c_lo, int c_hi, "
+        "Tensor in_ptr, Tensor in_src, Tensor(b!) table, Tensor(c!) n_keys, Tensor(d!) err) -> ()");
+  m.def("tcs_insert(Tensor src, Tensor(a!) table, bool append, Tensor(b!) keys, "
+        "Tensor(c!) n_keys, Tensor(d!) err) -> ()");
   m.def("spd_inverse(Tensor G, float ridge, Tensor(a!) out, Tensor(b!)? status) -> ()");
   m.def("als_solve(Tensor R, Tensor F, Tensor Ginv, Tensor(a!) out) -> ()");
   m.def("als_gram(Tensor F, Tensor(a!) G) -> ()");
@@ -849,6 +923,9 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("als_gram", &als_gram);
   m.impl("als_residual", &als_residual);
   m.impl("tc_step", &tc_step);
+  m.impl("tcs_degree", &tcs_degree);
+  m.impl("tcs_expand", &tcs_expand);
+  m.impl("tcs_insert", &tcs_insert);
   m.impl("xgmi_allreduce", &xgmi_allreduce);
   m.impl("rmat_edges", &rmat_edges);
   m.impl("pr_spmv", &pr_spmv);

@@ -96,6 +96,17 @@ hipError_t dalgo_pr_update(const float* acc, const int32_t* pres, const int32_t*
                            float* c, float* dangling_out, hipStream_t st);
 
 // ---- K9 transitive closure (closure.hip)
+// ---- K9 sparse closure round on a device hash set (tc_sparse.hip)
+hipError_t dalgo_tcs_degree(const uint64_t* keys, int64_t d0, int64_t nd, const int64_t* in_ptr,
+                            int64_t* deg, hipStream_t st);
+hipError_t dalgo_tcs_expand(const uint64_t* fkeys, int64_t nd, const int64_t* excl, int64_t c_lo,
+                            int64_t c_hi, const int64_t* in_ptr, const int32_t* in_src,
+                            uint64_t* table, uint64_t mask, uint64_t* keys,
+                            unsigned long long* n_keys, uint64_t cap, unsigned* err,
+                            hipStream_t st);
+hipError_t dalgo_tcs_insert(const uint64_t* src, int64_t n, uint64_t* table, uint64_t mask,
+                            int append, uint64_t* keys, unsigned long long* n_keys, uint64_t cap,
+                            unsigned* err, hipStream_t st);
 hipError_t dalgo_tc_step(const void* A, int64_t lda, const void* Told, void* Tnew, int64_t ldt,
                          int npad, int nz, int variant, unsigned long long* count, hipStream_t st);
 

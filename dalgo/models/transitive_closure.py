@@ -145,6 +145,17 @@ class DenseClosure(_Fixpoint):
 
 
 class SparseClosure(_Fixpoint):
+    """Semi-naive closure over path keys (x << 32 | z) of this rank's targets
+    (z % world == rank); the edges are replicated as an in-edge CSR (in_ptr / in_src,
+    the reversed edge RDD of transitive_closure.py:27).
+
+    GPU (K9 sparse, csrc/kernels/tc_sparse.hip): the path set is an append-only key
+    array plus a device hash set; a round expands only the last round's new paths
+    (the frontier) through the in-edges and inserts every candidate with one 64-bit
+    CAS -- dedup, the test against earlier paths and the merge into P in one kernel,
+    no sort. CPU: the torch reference (repeat_interleave join, unique, isin, sort).
+    """
+
     def __init__(self, src: torch.Tensor, dst: torch.Tensor, rank: int = 0, world: int = 1,
                  n: int | None = None, device="cpu"):
         dev = torch.device(device)
@@ -152,6 +163,8 @@ class SparseClosure(_Fixpoint):
         dst = dst.to(dev).long()
         self.dev = dev
         n = int(max(src.max().item(), dst.max().item()) + 1) if n is None else n
+        if n >= 1 << 31:
+            raise ValueError("sparse closure: vertex ids must fit in 31 bits")
         self.n = n
         # edges grouped by their TARGET y: in_ptr / in_src (the reversed edge RDD)
         order = torch.argsort(dst * n + src)
@@ -159,14 +172,73 @@ class SparseClosure(_Fixpoint):
         self.in_src = xs
         self.in_ptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
         self.in_ptr[1:] = torch.cumsum(torch.bincount(ys, minlength=n), 0)
-        # this rank's paths: targets z with z % world == rank
-        keys = torch.unique((src << 32) | dst)
-        z = keys & 0xFFFFFFFF
-        self.P = keys[(z % world) == rank]
-        self.delta = self.P
         self.rank, self.world = rank, world
         self.counts: list = []
+        own = (dst % world) == rank
+        init = (src[own] << 32) | dst[own]
+        self.gpu = dev.type == "cuda"
+        if self.gpu:
+            from dalgo.ops import _ext
+            self._ops = _ext.ops()
+            self.in_src32 = xs.to(torch.int32).contiguous()
+            self.n_keys_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+            self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._alloc(max(1024, 4 * init.numel()))
+            self._ops.tcs_insert(init.contiguous(), self.table, True, self.keys, self.n_keys_dev,
+                                 self.err)
+            self.n_keys = int(self.n_keys_dev.item())
+            self.d0 = 0                      # frontier = keys[d0 : n_keys]
+            self.rounds_candidates: list = []
+        else:
+            self.P = torch.unique(init)
+            self.delta = self.P
 
+    # ------------------------------------------------------------------ GPU engine
+    def _alloc(self, want_keys: int):
+        """Table of the next power of two >= 2 x want_keys slots; key array of half that."""
+        size = 1 << max(10, (2 * int(want_keys) - 1).bit_length())
+        self.table = torch.full((size,), -1, dtype=torch.int64, device=self.dev)
+        keys = torch.empty(size // 2, dtype=torch.int64, device=self.dev)
+        if getattr(self, "keys", None) is not None and self.n_keys:
+            keys[: self.n_keys].copy_(self.keys[: self.n_keys])
+        self.keys = keys
+
+    def _grow(self, want_keys: int):
+        self._alloc(want_keys)
+        if self.n_keys:
+            # rehash the existing paths (no append: they are already in `keys`)
+            self._ops.tcs_insert(self.keys[: self.n_keys], self.table, False, self.keys,
+                                 self.n_keys_dev, self.err)
+
+    def _gpu_step(self) -> int:
+        d0, d1 = self.d0, self.n_keys
+        nd = d1 - d0
+        if nd:
+            with self._ph("degrees"):
+                excl = torch.zeros(nd + 1, dtype=torch.int64, device=self.dev)
+                self._ops.tcs_degree(self.keys, d0, nd, self.in_ptr, excl[1:])
+                torch.cumsum(excl[1:], 0, out=excl[1:])
+            total = int(excl[nd].item())
+            self.rounds_candidates.append(total)
+            c = 0
+            while c < total:
+                free = self.table.numel() // 2 - self.n_keys
+                if free < min(total - c, self.table.numel() // 8):
+                    # more room first: the chunk below can add at most its candidate count
+                    self._grow(2 * (self.n_keys + min(total - c, self.n_keys + 1)))
+                    continue
+                m = min(total - c, free)
+                with self._ph("expand+insert"):
+                    self._ops.tcs_expand(self.keys, d0, nd, excl, c, c + m, self.in_ptr,
+                                         self.in_src32, self.table, self.n_keys_dev, self.err)
+                self.n_keys = int(self.n_keys_dev.item())
+                c += m
+            if int(self.err.item()):
+                raise RuntimeError("sparse closure: hash-set capacity invariant broken")
+        self.d0 = d1
+        return comm.all_reduce_count(self.n_keys, device=self.dev)
+
+    # ------------------------------------------------------------------ CPU engine
     def _join(self, delta: torch.Tensor) -> torch.Tensor:
         y = delta >> 32
         z = delta & 0xFFFFFFFF
@@ -182,6 +254,8 @@ class SparseClosure(_Fixpoint):
         return torch.unique((x << 32) | z[rep])
 
     def step(self) -> int:
+        if self.gpu:
+            return self._gpu_step()
         new = self._join(self.delta)
         if new.numel():
             new = new[~torch.isin(new, self.P)]
@@ -190,18 +264,48 @@ class SparseClosure(_Fixpoint):
         return comm.all_reduce_count(self.P.numel(), device=self.dev)
 
     def _initial_count(self) -> int:
-        return comm.all_reduce_count(self.P.numel(), device=self.dev)
+        n = self.n_keys if self.gpu else self.P.numel()
+        return comm.all_reduce_count(n, device=self.dev)
+
+    def paths(self) -> torch.Tensor:
+        """This rank's path keys (x << 32 | z), sorted."""
+        if self.gpu:
+            return torch.sort(self.keys[: self.n_keys]).values
+        return self.P
+
+    def frontier(self) -> torch.Tensor:
+        if self.gpu:
+            return torch.sort(self.keys[self.d0: self.n_keys]).values
+        return self.delta
 
     def state_dict(self) -> dict:
         """This rank's path set and last round's new paths (semi-naive frontier)."""
         return {"engine": "sparse", "n": self.n, "rank": self.rank, "world": self.world,
-                "P": self.P.cpu(), "delta": self.delta.cpu(),
+                "P": self.paths().cpu(), "delta": self.frontier().cpu(),
                 "counts": torch.tensor(self.counts, dtype=torch.int64)}
 
     def load_state_dict(self, sd: dict):
         if sd.get("engine") != "sparse" or (sd["n"], sd["rank"], sd["world"]) != \
                 (self.n, self.rank, self.world):
             raise ValueError("checkpoint is for a different graph or rank partition")
-        self.P = sd["P"].to(self.dev)
-        self.delta = sd["delta"].to(self.dev)
+        P = sd["P"].to(self.dev)
+        delta = sd["delta"].to(self.dev)
         self.counts = [int(c) for c in sd["counts"].tolist()]
+        if not self.gpu:
+            self.P, self.delta = P, delta
+            return
+        # key array = (P \ delta) followed by delta, so the frontier is the contiguous tail
+        old = P[~torch.isin(P, delta)] if delta.numel() else P
+        self.keys = None
+        self.n_keys = 0
+        self._alloc(max(1024, 2 * P.numel()))
+        self.n_keys_dev.zero_()
+        self._ops.tcs_insert(old.contiguous(), self.table, True, self.keys, self.n_keys_dev,
+                             self.err)
+        d0 = int(self.n_keys_dev.item())
+        self._ops.tcs_insert(delta.contiguous(), self.table, True, self.keys, self.n_keys_dev,
+                             self.err)
+        self.n_keys = int(self.n_keys_dev.item())
+        self.d0 = d0
+        if self.n_keys != P.numel():
+            raise ValueError("sparse closure checkpoint: path set is not duplicate-free")

@@ -490,3 +490,53 @@ def test_lr_family_graph_replay_matches_eager(cuda, algo, reuse):
         assert ce == cg
     rel = ((wg - we).norm() / we.norm()).item()
     assert rel < 1e-4, rel
+
+
+@pytest.mark.parametrize("n,e,seed", [(3000, 2600, 1), (20000, 18000, 2), (4000, 6000, 3)])
+def test_sparse_closure_gpu_exact(cuda, n, e, seed):
+    """K9 sparse (hash-set frontier join): per-round path counts == the CPU torch engine,
+    the final path SET equal too; the third graph is supercritical (large closure, the
+    hash set grows several times)."""
+    from dalgo.models.transitive_closure import SparseClosure
+    g = torch.Generator().manual_seed(seed)
+    src = torch.randint(0, n, (e,), generator=g)
+    dst = torch.randint(0, n, (e,), generator=g)
+    cpu = SparseClosure(src, dst, n=n)
+    gpu = SparseClosure(src, dst, n=n, device=cuda)
+    assert gpu.run().counts == cpu.run().counts
+    assert torch.equal(gpu.paths().cpu(), cpu.paths())
+
+
+def test_sparse_closure_expand_skewed_degrees(cuda):
+    """One expansion over a frontier whose candidate prefix has long runs of zero-degree
+    paths (blocks spanning > 2048 frontier entries: global binary search) and hubs with
+    tens of thousands of in-edges (one path spans many blocks) == torch join."""
+    from dalgo.models.transitive_closure import SparseClosure
+    g = torch.Generator().manual_seed(7)
+    n = 100_000
+    hubs = torch.tensor([5, 77, 4242])
+    src = torch.cat([torch.randint(0, n, (60_000,), generator=g),
+                     torch.randint(0, n, (3000,), generator=g)])
+    dst = torch.cat([hubs[torch.randint(0, 3, (60_000,), generator=g)],
+                     torch.randint(0, n, (3000,), generator=g)])
+    # initial paths: the edges; frontier sources mostly have in-degree 0
+    cpu = SparseClosure(src, dst, n=n)
+    gpu = SparseClosure(src, dst, n=n, device=cuda)
+    for _ in range(3):
+        assert gpu.step() == cpu.step()
+        assert torch.equal(gpu.frontier().cpu(), cpu.frontier())
+    assert int(gpu.err.item()) == 0
+
+
+def test_sparse_closure_gpu_resume(cuda):
+    from dalgo.models.transitive_closure import SparseClosure
+    g = torch.Generator().manual_seed(11)
+    n, e = 5000, 4700
+    src = torch.randint(0, n, (e,), generator=g)
+    dst = torch.randint(0, n, (e,), generator=g)
+    ref = SparseClosure(src, dst, n=n, device=cuda).run().counts
+    a = SparseClosure(src, dst, n=n, device=cuda)
+    a.run(max_rounds=4)
+    b = SparseClosure(src, dst, n=n, device=cuda)
+    b.load_state_dict(a.state_dict())
+    assert b.run().counts == ref
