@@ -12,15 +12,19 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("dist", [R.UNIFORM, R.NORMAL])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_philox_fill_matches_numpy(cuda, dist, dtype):
+@pytest.mark.parametrize("D,ld,row_offset", [(33, 40, 1000), (33, 40, 1001), (1, 1, 7),
+                                             (64, 64, 3), (5, 8, 12345)])
+def test_philox_fill_matches_numpy(cuda, dist, dtype, D, ld, row_offset):
+    """4 elements per thread from one Philox block (groups straddle row ends for odd D
+    and unaligned starts) == the NumPy mirror; padding columns zeroed."""
     a, b = (-1.0, 1.0) if dist == R.UNIFORM else (0.5, 2.0)
-    out_c = torch.empty((37, 40), dtype=dtype)
-    R.philox_fill_(out_c, D=33, row_offset=1000, seed=77, stream=5, dist=dist, a=a, b=b)
-    out_d = torch.empty((37, 40), dtype=dtype, device=cuda)
-    R.philox_fill_(out_d, D=33, row_offset=1000, seed=77, stream=5, dist=dist, a=a, b=b)
+    out_c = torch.empty((37, ld), dtype=dtype)
+    R.philox_fill_(out_c, D=D, row_offset=row_offset, seed=77, stream=5, dist=dist, a=a, b=b)
+    out_d = torch.full((37, ld), 7.0, dtype=dtype, device=cuda)
+    R.philox_fill_(out_d, D=D, row_offset=row_offset, seed=77, stream=5, dist=dist, a=a, b=b)
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     assert torch.allclose(out_d.cpu().float(), out_c.float(), atol=tol * 4, rtol=tol)
-    assert (out_d[:, 33:] == 0).all()
+    assert (out_d[:, D:] == 0).all()
 
 
 def test_mc_pi_exact_count(cuda):
