@@ -77,7 +77,7 @@ def calibrate_launch(model, rt, a) -> dict:
     the warmup and before the timed region (untimed); every rank times every candidate,
     the MAX over ranks decides, so all ranks pick the same form. Returns the per-candidate
     ms/step."""
-    from dalgo.parallel import comm
+    from dalgo.parallel import comm, runtime
     if (a.algo not in ("ssgd", "gd") or model.device.type != "cuda" or not model._zg
             or model.fused or model._graph_ok() or a.cal_steps <= 0):
         return {}

@@ -43,9 +43,10 @@ def main():
     for name, ref in engines:
         tc = SparseClosure(src, dst, n=a.n, device=rt.device)
         if ref:
+            P = tc.paths()
             tc.gpu = False                 # same object, torch engine on the GPU tensors
-            tc.P = tc.paths()
-            tc.delta = tc.P
+            tc.P = P
+            tc.delta = P
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         res = tc.run()

@@ -43,6 +43,8 @@ class PageRankConfig:
 
 
 class PageRank:
+    timer = None   # dalgo.utils.obs.PhaseTimer (None = off)
+
     def __init__(self, cfg: PageRankConfig, shard: Gops.GraphShard, world: int = 1):
         self.cfg = cfg
         self.g = shard
@@ -188,8 +190,7 @@ class PageRank:
         return env == "1" or (env == "auto" and self.own_share >= 0.25)
 
     def _ph(self, name: str):
-        t = getattr(self, "timer", None)
-        return t.phase(name) if t is not None else NULL_PHASE
+        return self.timer.phase(name) if self.timer is not None else NULL_PHASE
 
     def step(self):
         if self._overlap():

@@ -2,7 +2,7 @@
 
 The algorithms (ParallelSGD, KMeans, PageRank, ALS, closure, Monte Carlo) time their
 phases through :class:`PhaseTimer` when a timer is attached (the apps attach one when
-``--metrics-out`` is given, or under rocprofv3), and the apps write one JSONL line per
+``--metrics-out`` is given or DALGO_ROCTX=1), and the apps write one JSONL line per
 iteration with the phase split and the bytes all-reduced.
 
 Parity with the reference's R6 layer: ``draw_acc_plot`` / ``ewma_smooth``
@@ -201,10 +201,7 @@ def _roctx():
     global _ROCTX
     if _ROCTX is None:
         _ROCTX = False
-        want = os.environ.get("DALGO_ROCTX")
-        if want is None:
-            want = "1" if any(k.startswith("ROCPROF") for k in os.environ) else "0"
-        if want == "1":
+        if os.environ.get("DALGO_ROCTX") == "1":
             import ctypes
             # the rocprofiler-sdk roctx (what rocprofv3 --marker-trace intercepts) first,
             # the legacy roctracer library second
@@ -224,8 +221,7 @@ def roctx_enabled() -> bool:
 
 @contextlib.contextmanager
 def roctx_range(name: str):
-    """roctx range (visible in rocprofv3 --marker-trace) when DALGO_ROCTX=1 (or when
-    the program runs under rocprofv3, which exports ROCPROF_* variables)."""
+    """roctx range (visible in rocprofv3 --marker-trace) when DALGO_ROCTX=1."""
     lib = _roctx()
     if lib:
         lib.roctxRangePushA(name.encode())
