@@ -454,6 +454,46 @@ void kmeans_accumulate_sorted(const Tensor& X, const Tensor& assign, int64_t k, 
                   "kmeans_accumulate_sorted");
 }
 
+// K3 incremental: changed rows of (a_new vs a_old), then move them between the f64 sums
+void kmeans_diff(const Tensor& a_new, const Tensor& a_old, Tensor changed, Tensor n_changed) {
+  check_dev(a_new, "a_new");
+  check_dev(a_old, "a_old");
+  check_dev(changed, "changed");
+  check_dev(n_changed, "n_changed");
+  TORCH_CHECK(a_new.scalar_type() == at::kInt && a_old.scalar_type() == at::kInt &&
+                  changed.scalar_type() == at::kInt && a_new.is_contiguous() &&
+                  a_old.is_contiguous() && changed.is_contiguous(), "kmeans_diff: int32 vectors");
+  TORCH_CHECK(a_old.numel() == a_new.numel() && a_new.numel() < 0x7fffffffLL, "kmeans_diff: sizes");
+  TORCH_CHECK(n_changed.scalar_type() == at::kLong && n_changed.numel() >= 1, "n_changed int64[1]");
+  DeviceGuard guard(a_new.device());
+  DALGO_CHECK_HIP(dalgo_km_diff(a_new.data_ptr<int32_t>(), a_old.data_ptr<int32_t>(), a_new.numel(),
+                                changed.data_ptr<int32_t>(),
+                                reinterpret_cast<unsigned long long*>(n_changed.data_ptr<int64_t>()),
+                                changed.numel(), cur_stream()),
+                  "kmeans_diff");
+}
+
+void kmeans_move(const Tensor& X, int64_t DP, const Tensor& changed, int64_t m,
+                 const Tensor& a_new, const Tensor& a_old, Tensor S64, Tensor cnt) {
+  TORCH_CHECK(kmeans_dp(DP) == DP, "DP must be 16/32/64/128");
+  check_points(X, (int)DP);
+  check_dev(changed, "changed");
+  TORCH_CHECK(changed.scalar_type() == at::kInt && m >= 0 && m <= changed.numel(), "changed");
+  TORCH_CHECK(a_new.scalar_type() == at::kInt && a_old.scalar_type() == at::kInt &&
+                  a_new.numel() >= X.size(0) && a_old.numel() >= X.size(0), "assignments");
+  check_dev(S64, "S64");
+  TORCH_CHECK(S64.scalar_type() == at::kDouble && S64.is_contiguous(), "S64 f64");
+  TORCH_CHECK(cnt.scalar_type() == at::kLong && cnt.is_contiguous(), "cnt int64");
+  TORCH_CHECK(S64.numel() % DP == 0 && cnt.numel() >= S64.numel() / DP, "S64 [k, DP] / cnt [k]");
+  DeviceGuard guard(X.device());
+  DALGO_CHECK_HIP(dalgo_km_move(X.data_ptr(), X.scalar_type() == at::kBFloat16, X.stride(0), (int)DP,
+                                changed.data_ptr<int32_t>(), m, a_new.data_ptr<int32_t>(),
+                                a_old.data_ptr<int32_t>(), S64.data_ptr<double>(),
+                                reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>()),
+                                cur_stream()),
+                  "kmeans_move");
+}
+
 void kmeans_update(Tensor C, const Tensor& S, const Tensor& cnt, Tensor Cq, Tensor hn,
                    const std::optional<Tensor>& shift2) {
   check_f32(C, "C");
@@ -872,6 +912,9 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("kmeans_accumulate_sorted(Tensor X, Tensor assign, int k, int DP, int seg, "
         "Tensor(a!) block_counts, Tensor(b!) cluster_start, Tensor(c!) seg_start, Tensor(d!) perm, "
         "Tensor(e!) S, Tensor(f!) cnt) -> ()");
+  m.def("kmeans_diff(Tensor a_new, Tensor a_old, Tensor(a!) changed, Tensor(b!) n_changed) -> ()");
+  m.def("kmeans_move(Tensor X, int DP, Tensor changed, int m, Tensor a_new, Tensor a_old, "
+        "Tensor(a!) S64, Tensor(b!) cnt) -> ()");
   m.def("kmeans_update(Tensor(a!) C, Tensor S, Tensor cnt, Tensor(b!) Cq, Tensor(c!) hn, "
         "Tensor(d!)? shift2) -> ()");
   m.def("rmat_edges(int seed, int scale, int e_off, float a, float b, float c, bool scramble, "
@@ -934,5 +977,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("kmeans_assign", &kmeans_assign);
   m.impl("kmeans_accumulate", &kmeans_accumulate);
   m.impl("kmeans_update", &kmeans_update);
+  m.impl("kmeans_diff", &kmeans_diff);
+  m.impl("kmeans_move", &kmeans_move);
   m.impl("kmeans_accumulate_sorted", &kmeans_accumulate_sorted);   // dispatches on its output counter
 }

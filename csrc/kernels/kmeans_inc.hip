@@ -1,0 +1,128 @@
+// K3 incremental form: per-cluster sums maintained across Lloyd iterations by
+// moving only the points whose assignment changed.
+//
+// Reference: machine_learning/k-means.py:62-63 recomputes (sum, count) per cluster
+// from every point each iteration (reduceByKey). The sums are linear in the
+// assignment, so with the previous iteration's local sums S (f64, exact for any
+// realistic n) and its assignment a_old,
+//     S[c] = S_old[c] + sum_{a_new(x)=c, a_old(x)!=c} x - sum_{a_old(x)=c, a_new(x)!=c} x
+// is the same (sum, count) table the full pass would produce (up to f64 rounding
+// order). On clustered data the changed share drops below 1 % after the first
+// iteration (0.86 % -> 0.06 % on the 1024-blob benchmark data), so the
+// 25.6 GB re-read of X in the full K3 pass becomes a pass over the two
+// assignment vectors (0.8 GB) plus ~1-2 KB of f64 atomics per moved point.
+// The caller falls back to the full pass when the changed share is large.
+//
+//   km_diff    : compare a_new / a_old, wave-aggregated append of the changed
+//                row ids (one atomic per wave)
+//   km_move    : one wave per changed row: the row's DP features (bf16 / f32, one
+//                256-B or 512-B coalesced read) are added to S[a_new] and
+//                subtracted from S[a_old] with f64 atomics shaped as contiguous
+//                512-B wave instructions; lane 0 moves the counts.
+#include "dalgo/common.h"
+
+namespace dalgo {
+namespace {
+
+constexpr int kDiffThreads = 256;
+
+__global__ void __launch_bounds__(kDiffThreads)
+km_diff_kernel(const int32_t* __restrict__ a_new, const int32_t* __restrict__ a_old, int64_t n,
+               int32_t* __restrict__ changed, unsigned long long* __restrict__ n_changed,
+               int64_t cap) {
+  for (int64_t base = (int64_t)blockIdx.x * kDiffThreads; base < n;
+       base += (int64_t)gridDim.x * kDiffThreads) {
+    const int64_t i = base + threadIdx.x;
+    const bool ch = i < n && a_new[i] != a_old[i];
+    const uint64_t mask = __ballot(ch);
+    if (mask == 0) continue;
+    const int lane = __lane_id();
+    const int leader = __ffsll((long long)mask) - 1;
+    unsigned long long b = 0;
+    if (lane == leader) b = atomicAdd(n_changed, (unsigned long long)__popcll(mask));
+    b = __shfl(b, leader);
+    if (ch) {
+      const uint64_t below = lane == 0 ? 0ull : (mask & (~0ull >> (64 - lane)));
+      const int64_t pos = (int64_t)b + __popcll(below);
+      if (pos < cap) changed[pos] = (int32_t)i;
+    }
+  }
+}
+
+template <typename T, int DP>
+__global__ void __launch_bounds__(256)
+km_move_kernel(const T* __restrict__ X, int64_t ldx, const int32_t* __restrict__ changed,
+               int64_t m, const int32_t* __restrict__ a_new, const int32_t* __restrict__ a_old,
+               double* __restrict__ S, unsigned long long* __restrict__ cnt) {
+  constexpr int PER = (DP + 63) / 64;     // features per lane
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t w = wave; w < m; w += nwaves) {
+    const int64_t row = changed[w];
+    const int cn = a_new[row], co = a_old[row];
+    const T* xr = X + row * ldx;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int j = q * 64 + lane;        // one wave instruction = 64 consecutive f64
+      if (j < DP) {
+        float v;
+        if constexpr (sizeof(T) == 2) v = bf16_to_f32(reinterpret_cast<const uint16_t*>(xr)[j]);
+        else v = reinterpret_cast<const float*>(xr)[j];
+        if (v != 0.f) {
+          atomicAdd(&S[(int64_t)cn * DP + j], (double)v);
+          atomicAdd(&S[(int64_t)co * DP + j], -(double)v);
+        }
+      }
+    }
+    if (lane == 0) {
+      atomicAdd(&cnt[cn], 1ull);
+      atomicAdd(&cnt[co], ~0ull);   // -1 (two's complement)
+    }
+  }
+}
+
+template <typename T, int DP>
+hipError_t launch_move(const void* X, int64_t ldx, const int32_t* changed, int64_t m,
+                       const int32_t* a_new, const int32_t* a_old, double* S,
+                       unsigned long long* cnt, hipStream_t st) {
+  int64_t g = (m + 3) / 4;                 // 4 waves per 256-thread block
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL((km_move_kernel<T, DP>), dim3((unsigned)g), dim3(256), 0, st,
+                     reinterpret_cast<const T*>(X), ldx, changed, m, a_new, a_old, S, cnt);
+  return hipGetLastError();
+}
+
+}  // namespace
+}  // namespace dalgo
+
+extern "C" {
+
+hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, int32_t* changed,
+                         unsigned long long* n_changed, int64_t cap, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  int64_t g = (n + dalgo::kDiffThreads - 1) / dalgo::kDiffThreads;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(dalgo::km_diff_kernel, dim3((unsigned)g), dim3(dalgo::kDiffThreads), 0, st,
+                     a_new, a_old, n, changed, n_changed, cap);
+  return hipGetLastError();
+}
+
+hipError_t dalgo_km_move(const void* X, int is_bf16, int64_t ldx, int DP, const int32_t* changed,
+                         int64_t m, const int32_t* a_new, const int32_t* a_old, double* S,
+                         unsigned long long* cnt, hipStream_t st) {
+  if (m <= 0) return hipSuccess;
+  using namespace dalgo;
+#define DALGO_KM_MOVE(DPV)                                                                   \
+  if (DP == DPV)                                                                             \
+    return is_bf16 ? launch_move<uint16_t, DPV>(X, ldx, changed, m, a_new, a_old, S, cnt, st) \
+                   : launch_move<float, DPV>(X, ldx, changed, m, a_new, a_old, S, cnt, st);
+  DALGO_KM_MOVE(16)
+  DALGO_KM_MOVE(32)
+  DALGO_KM_MOVE(64)
+  DALGO_KM_MOVE(128)
+#undef DALGO_KM_MOVE
+  return hipErrorInvalidValue;
+}
+
+}  // extern "C"

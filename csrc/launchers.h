@@ -96,6 +96,13 @@ hipError_t dalgo_pr_update(const float* acc, const int32_t* pres, const int32_t*
                            float* c, float* dangling_out, hipStream_t st);
 
 // ---- K9 transitive closure (closure.hip)
+// ---- K3 incremental form (kmeans_inc.hip)
+hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, int32_t* changed,
+                         unsigned long long* n_changed, int64_t cap, hipStream_t st);
+hipError_t dalgo_km_move(const void* X, int is_bf16, int64_t ldx, int DP, const int32_t* changed,
+                         int64_t m, const int32_t* a_new, const int32_t* a_old, double* S,
+                         unsigned long long* cnt, hipStream_t st);
+
 // ---- K9 sparse closure round on a device hash set (tc_sparse.hip)
 hipError_t dalgo_tcs_degree(const uint64_t* keys, int64_t d0, int64_t nd, const int64_t* in_ptr,
                             int64_t* deg, hipStream_t st);

@@ -7,7 +7,11 @@ but never used; here ``tol`` optionally stops when the max squared centre shift
 drops below it (off by default = reference behaviour).
 
 SPMD version per iteration, every rank on its HBM-resident row shard:
-  K2 assign (MFMA distance GEMM + argmin)  ->  K3 per-cluster sums/counts  ->
+  K2 assign (MFMA distance GEMM + argmin)  ->  K3 per-cluster sums/counts (full pass,
+  or -- GPU, from the second iteration on, while at most DALGO_KM_INC_MAX (2 %) of
+  the rank's points changed cluster -- the incremental form: only the moved points
+  are subtracted from their old and added to their new cluster's f64 local sums,
+  csrc/kernels/kmeans_inc.hip)  ->
   ONE all_reduce of the fused f32 bucket [sums k x DP || counts as 2 x k exact f32
   words]  ->  fused update.
 The reduceByKey shuffle + driver collect become one RCCL all-reduce whose size is
@@ -17,6 +21,7 @@ of the low words stays below 2^24, so the f32 reduction is exact.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -77,6 +82,11 @@ class KMeans:
         self.history = KMeansHistory()
         self.t = 0
         self.timer = None   # dalgo.utils.obs.PhaseTimer (None = off)
+        # incremental K3 state (GPU): f64 local sums / counts of the last iteration and
+        # its assignment (self.assign); None until a full pass has produced them
+        self.inc_max = float(os.environ.get("DALGO_KM_INC_MAX", "0.02"))
+        self._S64 = None
+        self.changed_history: list = []
 
     def _ph(self, name: str):
         return self.timer.phase(name) if self.timer is not None else NULL_PHASE
@@ -97,10 +107,29 @@ class KMeans:
         self.S.zero_()
         self.cnt.zero_()
         self.shift2.zero_()
+        inc = self._S64 is not None and self.inc_max > 0
+        a_out = self._a_new if inc else self.assign
         with self._ph("assign"):
-            K.assign(self.X, self.cen, out=self.assign, sse=self.sse)
-        with self._ph("accumulate"):
-            K.accumulate(self.X, self.assign, self.cfg.k, self.DP, self.S, self.cnt)
+            K.assign(self.X, self.cen, out=a_out, sse=self.sse)
+        moved = None
+        if inc:
+            with self._ph("diff"):
+                moved = K.changed_rows(a_out, self.assign, self._changed, self._n_changed)
+            self.changed_history.append(moved)
+            if moved > self.inc_max * self.X.shape[0]:
+                inc = False
+        if inc:
+            with self._ph("accumulate_incremental"):
+                K.move_rows(self.X, self.DP, self._changed, moved, a_out, self.assign,
+                            self._S64, self._cnt64)
+                self.S.copy_(self._S64)
+                self.cnt.copy_(self._cnt64)
+        else:
+            with self._ph("accumulate"):
+                K.accumulate(self.X, a_out, self.cfg.k, self.DP, self.S, self.cnt)
+            self._keep_local_sums()
+        if a_out is not self.assign:
+            self.assign, self._a_new = a_out, self.assign
         W = comm.world_size()
         if W > 1:
             with self._ph("allreduce"):
@@ -114,6 +143,20 @@ class KMeans:
         with self._ph("update"):
             K.update(self.cen, self.S, self.cnt, self.shift2)
         self.t += 1
+
+    def _keep_local_sums(self):
+        """After a full K3 pass: remember the local sums for the incremental form."""
+        if not (self.X.is_cuda and self.inc_max > 0):
+            return
+        if self._S64 is None:
+            n = self.X.shape[0]
+            self._S64 = torch.empty(self.S.shape, dtype=torch.float64, device=self.dev)
+            self._cnt64 = torch.empty_like(self.cnt)
+            self._a_new = torch.empty_like(self.assign)
+            self._changed = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)
+            self._n_changed = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self._S64.copy_(self.S)
+        self._cnt64.copy_(self.cnt)
 
     def fit(self, n_iterations: int | None = None, track: bool = True):
         n = self.cfg.n_iterations if n_iterations is None else n_iterations
@@ -141,6 +184,7 @@ class KMeans:
                 "shift": list(self.history.shift)}
 
     def load_state_dict(self, sd: dict):
+        self._S64 = None          # the next iteration runs the full K3 pass
         self.t = int(sd["t"])
         self.cen.C.copy_(sd["centers"].to(self.dev))
         K.refresh(self.cen)

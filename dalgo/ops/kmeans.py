@@ -194,6 +194,21 @@ def accumulate(X: torch.Tensor, a: torch.Tensor, k: int, DP: int, S: torch.Tenso
     return S, cnt
 
 
+def changed_rows(a_new: torch.Tensor, a_old: torch.Tensor, changed: torch.Tensor,
+                 n_changed: torch.Tensor) -> int:
+    """Row ids whose cluster changed -> changed[:m]; returns m (one host sync)."""
+    n_changed.zero_()
+    _ext.ops().kmeans_diff(a_new, a_old, changed, n_changed)
+    return int(n_changed.item())
+
+
+def move_rows(X: torch.Tensor, DP: int, changed: torch.Tensor, m: int, a_new: torch.Tensor,
+              a_old: torch.Tensor, S64: torch.Tensor, cnt: torch.Tensor):
+    """Incremental K3: S64[a_new[r]] += x_r, S64[a_old[r]] -= x_r (f64), counts likewise,
+    for the m changed rows r."""
+    _ext.ops().kmeans_move(X, int(DP), changed, int(m), a_new, a_old, S64, cnt)
+
+
 def update(cen: Centers, S: torch.Tensor, cnt: torch.Tensor, shift2: torch.Tensor | None = None):
     """c = S/n (non-empty), stale otherwise (k-means.py:70-71); refreshes Cq / hn."""
     if cen.C.is_cuda:

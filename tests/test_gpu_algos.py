@@ -540,3 +540,26 @@ def test_sparse_closure_gpu_resume(cuda):
     b = SparseClosure(src, dst, n=n, device=cuda)
     b.load_state_dict(a.state_dict())
     assert b.run().counts == ref
+
+
+@pytest.mark.parametrize("d,dtype", [(64, torch.bfloat16), (128, torch.bfloat16), (30, torch.float32)])
+def test_kmeans_incremental_accumulate_exact(cuda, d, dtype):
+    """Incremental K3 (moved rows only, f64 local sums): after every iteration the counts
+    equal a full K3 pass over the same assignment exactly and the sums to f32 rounding."""
+    from dalgo.data.synthetic import blobs
+    from dalgo.models.kmeans import KMeans, KMeansConfig
+    from dalgo.ops import kmeans as K
+    n, k = 150_000, 96
+    X = blobs(n, d, k, device=cuda, dtype=dtype, seed=5)
+    km = KMeans(KMeansConfig(k=k, n_iterations=6, seed=2), X, 0, n)
+    km.inc_max = 1.0                     # always incremental after the first pass
+    S_ref = torch.zeros_like(km.S)
+    c_ref = torch.zeros_like(km.cnt)
+    for it in range(6):
+        km.step()
+        S_ref.zero_()
+        c_ref.zero_()
+        K.accumulate(km.X, km.assign, k, km.DP, S_ref, c_ref)
+        assert torch.equal(km.cnt, c_ref), it
+        assert torch.allclose(km.S, S_ref, rtol=1e-5, atol=1e-2), it
+    assert len(km.changed_history) == 5 and km.changed_history[0] > 0
