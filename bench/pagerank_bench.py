@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--semantics", default="reference")
     ap.add_argument("--no-reorder", action="store_true", help="keep scrambled R-MAT vertex ids")
-    ap.add_argument("--spmv", default="pull", choices=["pull", "blocked"])
+    ap.add_argument("--spmv", default="pull", choices=["pull", "xcd", "blocked"])
     ap.add_argument("--bin-width", type=int, default=16384)
     ap.add_argument("--chunk", type=int, default=1 << 18)
     ap.add_argument("--tile", type=int, default=1 << 16)

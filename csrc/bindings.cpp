@@ -603,6 +603,47 @@ void pb_spmv(const Tensor& psrc, const Tensor& ppos, const Tensor& c, Tensor val
                   "pb_spmv");
 }
 
+// XCD-partitioned K4: 8 source-line parts (dalgo.ops.graph.build_xcd), per-part sums
+void pr_spmv_xcd(const Tensor& src, const Tensor& dstl, const Tensor& part_base, int64_t e_max,
+                 const Tensor& c, Tensor acc_all) {
+  check_i32(src, "src");
+  check_i32(dstl, "dstl");
+  TORCH_CHECK(src.numel() == dstl.numel(), "pr_spmv_xcd: edge arrays");
+  check_dev(part_base, "part_base");
+  TORCH_CHECK(part_base.scalar_type() == at::kLong && part_base.numel() == 9, "part_base int64[9]");
+  check_f32(c, "c");
+  check_f32(acc_all, "acc_all");
+  TORCH_CHECK(acc_all.dim() == 2 && acc_all.size(0) == 8 && acc_all.is_contiguous(), "acc_all [8, n]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(dstl.data_ptr()) % 16 == 0, "edge arrays 16-B aligned");
+  DeviceGuard guard(src.device());
+  DALGO_CHECK_HIP(dalgo_pr_spmv_xcd(src.data_ptr<int32_t>(), dstl.data_ptr<int32_t>(),
+                                    part_base.data_ptr<int64_t>(), e_max, c.data_ptr<float>(),
+                                    acc_all.data_ptr<float>(), acc_all.size(1), cur_stream()),
+                  "pr_spmv_xcd");
+}
+
+void pr_update_xcd(Tensor acc_all, const Tensor& outdeg, double q, double invN, int64_t mode,
+                   const std::optional<Tensor>& dangling_in, Tensor r, Tensor c,
+                   const std::optional<Tensor>& dangling_out) {
+  check_f32(acc_all, "acc_all");
+  TORCH_CHECK(acc_all.dim() == 2 && acc_all.size(0) == 8 && acc_all.is_contiguous(), "acc_all [8, n]");
+  check_i32(outdeg, "outdeg");
+  check_f32(r, "r");
+  check_f32(c, "c");
+  const int64_t n = r.numel();
+  TORCH_CHECK(acc_all.size(1) >= n && outdeg.numel() >= n && c.numel() >= n, "pr_update_xcd sizes");
+  const float* di = nullptr;
+  float* dout = nullptr;
+  if (dangling_in.has_value()) { check_f32(*dangling_in, "dangling_in"); di = dangling_in->data_ptr<float>(); }
+  if (dangling_out.has_value()) { check_f32(*dangling_out, "dangling_out"); dout = dangling_out->data_ptr<float>(); }
+  DeviceGuard guard(acc_all.device());
+  DALGO_CHECK_HIP(dalgo_pr_update_xcd(acc_all.data_ptr<float>(), acc_all.size(1),
+                                      outdeg.data_ptr<int32_t>(), n, (float)q, (float)invN, (int)mode,
+                                      di, r.data_ptr<float>(), c.data_ptr<float>(), dout, cur_stream()),
+                  "pr_update_xcd");
+}
+
 void pr_update(const Tensor& acc, const Tensor& pres, const Tensor& outdeg, double q, double invN,
                int64_t mode, const std::optional<Tensor>& dangling_in, Tensor r, Tensor c,
                const std::optional<Tensor>& dangling_out) {
@@ -924,6 +965,10 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(d!) slab, Tensor split_bin, Tensor split_first, Tensor split_count) -> ()");
   m.def("pr_spmv(Tensor src, Tensor dstl, Tensor c, Tensor(a!) acc, Tensor(b!) pres, "
         "bool accumulate=False) -> ()");
+  m.def("pr_spmv_xcd(Tensor src, Tensor dstl, Tensor part_base, int e_max, Tensor c, "
+        "Tensor(a!) acc_all) -> ()");
+  m.def("pr_update_xcd(Tensor(a!) acc_all, Tensor outdeg, float q, float invN, int mode, "
+        "Tensor? dangling_in, Tensor(b!) r, Tensor(c!) c, Tensor(d!)? dangling_out) -> ()");
   m.def("pr_update(Tensor acc, Tensor pres, Tensor outdeg, float q, float invN, int mode, "
         "Tensor? dangling_in, Tensor(a!) r, Tensor(b!) c, Tensor(c!)? dangling_out) -> ()");
   m.def("xgmi_buffer_bytes(int slot) -> int", &xgmi_buffer_bytes);
@@ -974,6 +1019,8 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("pr_spmv", &pr_spmv);
   m.impl("pb_spmv", &pb_spmv);
   m.impl("pr_update", &pr_update);
+  m.impl("pr_spmv_xcd", &pr_spmv_xcd);
+  m.impl("pr_update_xcd", &pr_update_xcd);
   m.impl("kmeans_assign", &kmeans_assign);
   m.impl("kmeans_accumulate", &kmeans_accumulate);
   m.impl("kmeans_update", &kmeans_update);

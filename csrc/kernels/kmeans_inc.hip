@@ -13,8 +13,8 @@
 // assignment vectors (0.8 GB) plus ~1-2 KB of f64 atomics per moved point.
 // The caller falls back to the full pass when the changed share is large.
 //
-//   km_diff    : compare a_new / a_old, wave-aggregated append of the changed
-//                row ids (one atomic per wave)
+//   km_diff    : compare a_new / a_old, append the changed row ids through a
+//                per-block LDS buffer (one global atomic per block flush)
 //   km_move    : one wave per changed row: the row's DP features (bf16 / f32, one
 //                256-B or 512-B coalesced read) are added to S[a_new] and
 //                subtracted from S[a_old] with f64 atomics shaped as contiguous
@@ -25,28 +25,55 @@ namespace dalgo {
 namespace {
 
 constexpr int kDiffThreads = 256;
+constexpr int kDiffBuf = 4096;      // changed row ids buffered per block in LDS
 
+// One block per contiguous row range. Changed rows are appended to an LDS buffer with
+// LDS atomics (one per wave and step) and flushed to the global list with ONE global
+// atomic per flush -- a global counter hit by every wave serialises (~88 atomics/us on
+// one word: 5 ms for 1.3M changed rows at 100M points, measured).
 __global__ void __launch_bounds__(kDiffThreads)
 km_diff_kernel(const int32_t* __restrict__ a_new, const int32_t* __restrict__ a_old, int64_t n,
                int32_t* __restrict__ changed, unsigned long long* __restrict__ n_changed,
                int64_t cap) {
-  for (int64_t base = (int64_t)blockIdx.x * kDiffThreads; base < n;
-       base += (int64_t)gridDim.x * kDiffThreads) {
+  __shared__ int32_t s_buf[kDiffBuf];
+  __shared__ int s_cnt;
+  __shared__ unsigned long long s_base;
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * per;
+  const int64_t hi = lo + per < n ? lo + per : n;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  auto flush = [&]() {
+    const int m = s_cnt;                       // read after a barrier: stable
+    if (m == 0) return;
+    if (threadIdx.x == 0) s_base = atomicAdd(n_changed, (unsigned long long)m);
+    __syncthreads();
+    const int64_t b = (int64_t)s_base;
+    for (int j = threadIdx.x; j < m; j += kDiffThreads)
+      if (b + j < cap) changed[b + j] = s_buf[j];
+    __syncthreads();
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+  };
+  for (int64_t base = lo; base < hi; base += kDiffThreads) {
     const int64_t i = base + threadIdx.x;
-    const bool ch = i < n && a_new[i] != a_old[i];
+    const bool ch = i < hi && a_new[i] != a_old[i];
     const uint64_t mask = __ballot(ch);
-    if (mask == 0) continue;
-    const int lane = __lane_id();
-    const int leader = __ffsll((long long)mask) - 1;
-    unsigned long long b = 0;
-    if (lane == leader) b = atomicAdd(n_changed, (unsigned long long)__popcll(mask));
-    b = __shfl(b, leader);
-    if (ch) {
-      const uint64_t below = lane == 0 ? 0ull : (mask & (~0ull >> (64 - lane)));
-      const int64_t pos = (int64_t)b + __popcll(below);
-      if (pos < cap) changed[pos] = (int32_t)i;
+    if (mask != 0) {
+      const int lane = __lane_id();
+      const int leader = __ffsll((long long)mask) - 1;
+      int b = 0;
+      if (lane == leader) b = atomicAdd(&s_cnt, __popcll(mask));
+      b = __shfl(b, leader);
+      if (ch) {
+        const uint64_t below = lane == 0 ? 0ull : (mask & (~0ull >> (64 - lane)));
+        s_buf[b + __popcll(below)] = (int32_t)i;
+      }
     }
+    __syncthreads();
+    if (s_cnt > kDiffBuf - kDiffThreads) flush();   // room for one more step
   }
+  flush();
 }
 
 template <typename T, int DP>
@@ -102,7 +129,7 @@ hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, 
                          unsigned long long* n_changed, int64_t cap, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   int64_t g = (n + dalgo::kDiffThreads - 1) / dalgo::kDiffThreads;
-  if (g > 16384) g = 16384;
+  if (g > 2048) g = 2048;
   hipLaunchKernelGGL(dalgo::km_diff_kernel, dim3((unsigned)g), dim3(dalgo::kDiffThreads), 0, st,
                      a_new, a_old, n, changed, n_changed, cap);
   return hipGetLastError();

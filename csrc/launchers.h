@@ -91,6 +91,12 @@ hipError_t dalgo_pb_spmv(const int32_t* psrc, const int32_t* ppos, int64_t E4, c
                          int bin_width, int64_t n_local, float* acc, int32_t* pres, float* slab,
                          const int32_t* split_bin, const int32_t* split_first,
                          const int32_t* split_count, int nsplit, hipStream_t st);
+hipError_t dalgo_pr_spmv_xcd(const int32_t* src, const int32_t* dstl, const int64_t* part_base,
+                             int64_t e_max_part, const float* c, float* acc_all, int64_t n_stride,
+                             hipStream_t st);
+hipError_t dalgo_pr_update_xcd(float* acc_all, int64_t n_stride, const int32_t* outdeg, int64_t n,
+                               float q, float invN, int mode, const float* dangling_in, float* r,
+                               float* c, float* dangling_out, hipStream_t st);
 hipError_t dalgo_pr_update(const float* acc, const int32_t* pres, const int32_t* outdeg, int64_t n,
                            float q, float invN, int mode, const float* dangling_in, float* r,
                            float* c, float* dangling_out, hipStream_t st);

@@ -34,7 +34,8 @@ class PageRankConfig:
     q: float = 0.15              # teleport probability (pagerank.py:19)
     n_iterations: int = 10       # pagerank.py:18
     semantics: str = "reference"  # "reference" | "standard"
-    spmv: str = ""               # "pull" | "blocked" ("" = DALGO_PR_SPMV env, default pull)
+    spmv: str = ""               # "pull" | "xcd" | "blocked" ("" = DALGO_PR_SPMV env,
+                                 # default pull)
     bin_width: int = 16384       # blocked: destination vertices per LDS bin
     chunk: int = 1 << 18         # blocked: max edge slots per workgroup
     tile: int = 1 << 16          # blocked: phase-1 edges per slot-sorted tile
@@ -98,6 +99,12 @@ class PageRank:
                                             torch.zeros_like(od))
             self.dang.fill_(float(((self.outdeg == 0).float() * self.invN).sum().item()))
             comm.all_reduce_sum(self.dang)
+        # XCD-partitioned pull SpMV (K4x): the sources of the graph the SpMV reads
+        # (c_full index space) split into 8 line parts, one per XCD
+        self.xl = None
+        if self.spmv == "xcd" and dev.type == "cuda":
+            gsp = self.g_local if self.exchange == "ghost" else self.g
+            self.xl = Gops.build_xcd(gsp)
         self.t = 0
 
     def _build_ghosts(self):
@@ -156,6 +163,9 @@ class PageRank:
             comm.all_gather_into(self.c_full, self.c_slice)
 
     def _spmv(self):
+        if self.xl is not None:
+            Gops.pr_spmv_xcd(self.xl, self.c_full)
+            return
         self.acc.zero_()
         self.pres.zero_()
         if self.layout is not None:
@@ -169,9 +179,14 @@ class PageRank:
         nl = self.g.n_local
         if self.mode == 1:
             self.dang_next.zero_()
-        Gops.pr_update(self.acc, self.pres, self.outdeg, self.cfg.q, self.invN, self.mode, self.r,
-                       self.c_slice[:nl], dangling_in=self.dang if self.mode == 1 else None,
-                       dangling_out=self.dang_next if self.mode == 1 else None)
+        if self.xl is not None:
+            Gops.pr_update_xcd(self.xl, self.outdeg, self.cfg.q, self.invN, self.mode, self.r,
+                               self.c_slice[:nl], dangling_in=self.dang if self.mode == 1 else None,
+                               dangling_out=self.dang_next if self.mode == 1 else None)
+        else:
+            Gops.pr_update(self.acc, self.pres, self.outdeg, self.cfg.q, self.invN, self.mode, self.r,
+                           self.c_slice[:nl], dangling_in=self.dang if self.mode == 1 else None,
+                           dangling_out=self.dang_next if self.mode == 1 else None)
         if self.mode == 1:
             comm.all_reduce_sum(self.dang_next)
             self.dang, self.dang_next = self.dang_next, self.dang
@@ -184,7 +199,7 @@ class PageRank:
         profiles/round2/README.md), so by default (DALGO_PR_OVERLAP=auto) it is only used
         while the own-source pass is long enough to hide the exchange: at least a quarter
         of the edges (W <= 4 with the dealt relabeling). 1 / 0 force it on / off."""
-        if self.exchange != "ghost":
+        if self.exchange != "ghost" or self.xl is not None:
             return False
         env = os.environ.get("DALGO_PR_OVERLAP", "auto")
         return env == "1" or (env == "auto" and self.own_share >= 0.25)

@@ -545,7 +545,9 @@ def test_sparse_closure_gpu_resume(cuda):
 @pytest.mark.parametrize("d,dtype", [(64, torch.bfloat16), (128, torch.bfloat16), (30, torch.float32)])
 def test_kmeans_incremental_accumulate_exact(cuda, d, dtype):
     """Incremental K3 (moved rows only, f64 local sums): after every iteration the counts
-    equal a full K3 pass over the same assignment exactly and the sums to f32 rounding."""
+    equal a full K3 pass over the same assignment exactly, and the sums equal the first
+    (full, f32) pass plus the exact f64 change of the per-cluster sums since then: the
+    moves add no error of their own."""
     from dalgo.data.synthetic import blobs
     from dalgo.models.kmeans import KMeans, KMeansConfig
     from dalgo.ops import kmeans as K
@@ -553,13 +555,51 @@ def test_kmeans_incremental_accumulate_exact(cuda, d, dtype):
     X = blobs(n, d, k, device=cuda, dtype=dtype, seed=5)
     km = KMeans(KMeansConfig(k=k, n_iterations=6, seed=2), X, 0, n)
     km.inc_max = 1.0                     # always incremental after the first pass
-    S_ref = torch.zeros_like(km.S)
+
+    def exact(a):
+        S = torch.zeros(k, km.DP, dtype=torch.float64, device=cuda)
+        S[:, :d].index_add_(0, a.long(), km.X.double())
+        return S
+
     c_ref = torch.zeros_like(km.cnt)
+    S_ref = torch.zeros_like(km.S)
     for it in range(6):
         km.step()
-        S_ref.zero_()
+        if it == 0:
+            S0, E0 = km.S.double().clone(), exact(km.assign)
         c_ref.zero_()
+        S_ref.zero_()
         K.accumulate(km.X, km.assign, k, km.DP, S_ref, c_ref)
         assert torch.equal(km.cnt, c_ref), it
-        assert torch.allclose(km.S, S_ref, rtol=1e-5, atol=1e-2), it
+        expect = S0 + (exact(km.assign) - E0)
+        assert torch.allclose(km.S.double(), expect, rtol=1e-6, atol=1e-2), it
     assert len(km.changed_history) == 5 and km.changed_history[0] > 0
+
+
+@pytest.mark.parametrize("sem", ["reference", "standard"])
+@pytest.mark.parametrize("scale,edges", [(12, 100_000), (17, 3_000_000)])
+def test_pagerank_xcd_spmv_matches_cpu(cuda, sem, scale, edges):
+    """K4x (8 source-line parts, one per XCD, per-part sums with -0.0 presence) == the f64
+    CPU reference ranks, and == the pull SpMV's present-vertex set."""
+    from dalgo.models.pagerank import PageRank, PageRankConfig
+    s, d = G.rmat_edges(edges, scale, seed=8)
+    nv = 1 << scale
+    rc = PageRank(PageRankConfig(semantics=sem), G.build_shard(s, d, nv, 0, 1)).fit().collect()
+    px = PageRank(PageRankConfig(semantics=sem, spmv="xcd"),
+                  G.build_shard(s.to(cuda), d.to(cuda), nv, 0, 1))
+    assert px.xl is not None and sum(px.xl.counts) == px.g.n_edges
+    # the snake line deal balances the parts
+    assert max(px.xl.counts) <= 1.25 * (sum(px.xl.counts) / 8) + 256
+    rx = px.fit().collect()
+    assert set(rc) == set(rx)
+    assert max(abs(rc[v] - rx[v]) for v in rc) < 1e-6
+
+
+def test_pagerank_xcd_toy(cuda):
+    from dalgo.models.pagerank import PageRank, PageRankConfig
+    src = torch.tensor([1, 1, 2, 3], dtype=torch.int32, device=cuda)
+    dst = torch.tensor([2, 3, 3, 1], dtype=torch.int32, device=cuda)
+    r = PageRank(PageRankConfig(spmv="xcd"), G.build_shard(src, dst, 4, 0, 1)).fit().collect()
+    assert r[1] == pytest.approx(0.38891305880091237, abs=1e-6)
+    assert r[2] == pytest.approx(0.214416470596171, abs=1e-6)
+    assert r[3] == pytest.approx(0.3966704706029163, abs=1e-6)
