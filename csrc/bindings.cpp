@@ -553,7 +553,8 @@ void pr_spmv(const Tensor& src, const Tensor& dstl, const Tensor& c, Tensor acc,
   TORCH_CHECK(pres.numel() >= acc.numel(), "pres size");
   DeviceGuard guard(src.device());
   DALGO_CHECK_HIP(dalgo_pr_spmv(src.data_ptr<int32_t>(), dstl.data_ptr<int32_t>(), src.numel(),
-                                c.data_ptr<float>(), acc.data_ptr<float>(), pres.data_ptr<int32_t>(),
+                                c.data_ptr<float>(), c.numel(), acc.data_ptr<float>(),
+                                pres.data_ptr<int32_t>(),
                                 accumulate ? 1 : 0, cur_stream()),
                   "pr_spmv");
 }

@@ -91,12 +91,24 @@ __device__ __forceinline__ void flush_run(float* acc, int32_t* pres, int key, fl
   }
 }
 
-template <int NW, bool NT, bool ACC>
+// HOT > 0: the contributions of sources [0, HOT) -- the hottest ones after the degree
+// relabeling -- are staged in LDS once per block and read with ds_read instead of a
+// global gather. The gather is bound by the vector-memory address path, not by bytes:
+// splitting the sources over the XCDs' L2s (K4x) cut the fabric reads 3x (62 -> 21 GB,
+// L2 hit 54 -> 82 %) at unchanged time and unchanged TA_BUSY (86 %), so the way to go
+// faster is to take gathers off that path (profiles/round3/pmc_pagerank.md).
+template <int NW, bool NT, bool ACC, int HOT = 0>
 __global__ void __launch_bounds__(NW * 64)
 pr_spmv_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dstl, int64_t E,
-               const float* __restrict__ c, float* __restrict__ acc, int32_t* __restrict__ pres) {
+               const float* __restrict__ c, float* __restrict__ acc, int32_t* __restrict__ pres,
+               int64_t n_c) {
   // dstl: destination as LOCAL row index. E is padded to a multiple of 4 with
   // (src = -1, dst = -1) edges. Windows of 256 edges, 4 consecutive per lane.
+  __shared__ float s_hot[HOT > 0 ? HOT : 1];
+  if constexpr (HOT > 0) {
+    for (int i = threadIdx.x; i < HOT; i += NW * 64) s_hot[i] = i < n_c ? c[i] : 0.f;
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63;
   const int64_t nwin = (E + 255) / 256;
   const int64_t wave = (int64_t)blockIdx.x * NW + (threadIdx.x >> 6);
@@ -112,7 +124,12 @@ pr_spmv_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dstl
     const int dv[4] = {d4.x, d4.y, d4.z, d4.w};
     float cv[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) cv[j] = (sv[j] >= 0) ? c[sv[j]] : -1.f;
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (HOT > 0)
+        cv[j] = (sv[j] < 0) ? -1.f : (sv[j] < HOT ? s_hot[sv[j]] : c[sv[j]]);
+      else
+        cv[j] = (sv[j] >= 0) ? c[sv[j]] : -1.f;
+    }
     // keys of the edges just outside the window (row continuation tests)
     int dprev = -2, dnext = -2;
     if (lane == 0 && wi > 0) dprev = dstl[wi * 256 - 1];
@@ -512,7 +529,7 @@ hipError_t dalgo_rmat(uint64_t seed, int scale, int64_t e_off, int64_t n, float 
 }
 
 hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, const float* c,
-                         float* acc, int32_t* pres, int accumulate, hipStream_t st) {
+                         int64_t n_c, float* acc, int32_t* pres, int accumulate, hipStream_t st) {
   if (E % 4 != 0) return hipErrorInvalidValue;
   constexpr int NW = 4;
   const int64_t nwin = cdiv(E, 256);
@@ -520,18 +537,36 @@ hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, con
   if (grid == 0) return hipSuccess;
   // edge stream read once per iteration: nt loads (DALGO_NT=0 restores the default policy)
   const bool nt = env_int("DALGO_NT", 1) != 0;
+  // hot-source LDS table: DALGO_PR_HOT entries (0 = off); 16-wave blocks, 2 per CU
+  const int hot = env_int("DALGO_PR_HOT", 0);
+  if (nt && !accumulate && hot > 0) {
+    constexpr int NWH = 16;
+    const int gh = (int)std::min<int64_t>(cdiv(nwin, NWH), 2 * 256);
+#define DALGO_PR_HOT_LAUNCH(H)                                                                   \
+    if (hot == H) {                                                                              \
+      hipLaunchKernelGGL((pr_spmv_kernel<NWH, true, false, H>), dim3(gh), dim3(NWH * 64), 0, st, \
+                         src, dstl, E, c, acc, pres, n_c);                                       \
+      DALGO_LAUNCH_CHECK();                                                                      \
+      return hipSuccess;                                                                         \
+    }
+    DALGO_PR_HOT_LAUNCH(8192)
+    DALGO_PR_HOT_LAUNCH(16384)
+    DALGO_PR_HOT_LAUNCH(32768)
+#undef DALGO_PR_HOT_LAUNCH
+    return hipErrorInvalidValue;
+  }
   if (nt && accumulate)
     hipLaunchKernelGGL((pr_spmv_kernel<NW, true, true>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
-                       E, c, acc, pres);
+                       E, c, acc, pres, n_c);
   else if (nt)
     hipLaunchKernelGGL((pr_spmv_kernel<NW, true, false>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
-                       E, c, acc, pres);
+                       E, c, acc, pres, n_c);
   else if (accumulate)
     hipLaunchKernelGGL((pr_spmv_kernel<NW, false, true>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
-                       E, c, acc, pres);
+                       E, c, acc, pres, n_c);
   else
     hipLaunchKernelGGL((pr_spmv_kernel<NW, false, false>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
-                       E, c, acc, pres);
+                       E, c, acc, pres, n_c);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

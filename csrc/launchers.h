@@ -84,6 +84,7 @@ hipError_t dalgo_kmeans_update(float* C, const float* S, const unsigned long lon
 hipError_t dalgo_rmat(uint64_t seed, int scale, int64_t e_off, int64_t n, float a, float b, float c,
                       int do_scramble, int32_t* src, int32_t* dst, hipStream_t st);
 hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, const float* c,
+                         int64_t n_c,
                          float* acc, int32_t* pres, int accumulate, hipStream_t st);
 hipError_t dalgo_pb_spmv(const int32_t* psrc, const int32_t* ppos, int64_t E4, const float* c,
                          float* val, const uint16_t* dloc, const int64_t* chunk_lo4,

@@ -603,3 +603,17 @@ def test_pagerank_xcd_toy(cuda):
     assert r[1] == pytest.approx(0.38891305880091237, abs=1e-6)
     assert r[2] == pytest.approx(0.214416470596171, abs=1e-6)
     assert r[3] == pytest.approx(0.3966704706029163, abs=1e-6)
+
+
+@pytest.mark.parametrize("hot", [8192, 16384, 32768])
+def test_pr_spmv_hot_lds_table(cuda, monkeypatch, hot):
+    """K4 with the hot-source LDS table (sources < HOT read from LDS) == plain K4."""
+    from dalgo.models.pagerank import PageRank, PageRankConfig
+    s, d = G.rmat_edges(2_000_000, 16, seed=3)
+    nv = 1 << 16
+    sh = G.build_shard(s.to(cuda), d.to(cuda), nv, 0, 1)
+    ref = PageRank(PageRankConfig(), sh).fit().collect()
+    monkeypatch.setenv("DALGO_PR_HOT", str(hot))
+    got = PageRank(PageRankConfig(), sh).fit().collect()
+    assert set(ref) == set(got)
+    assert max(abs(ref[v] - got[v]) for v in ref) < 1e-7
