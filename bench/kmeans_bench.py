@@ -49,7 +49,7 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
     km.sse.zero_(); km.S.zero_(); km.cnt.zero_(); km.shift2.zero_()
     ev[0].record()
-    K.assign(km.X, km.cen, out=km.assign, sse=km.sse)
+    K.assign(km.X, km.cen, out=km.assign, sse=km.sse, stats=km.pstats)
     ev[1].record()
     K.accumulate(km.X, km.assign, a.k, km.DP, km.S, km.cnt)
     ev[2].record()

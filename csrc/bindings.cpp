@@ -407,6 +407,54 @@ void kmeans_assign(const Tensor& X, const Tensor& Cq, const Tensor& hn, Tensor a
                   "kmeans_assign");
 }
 
+// centre-stationary K2 (bf16, DP 64/128, kpad 256/512/1024): xh = 0.5|x|^2 per point,
+// M >= max(xh) (both fixed for a point set; computed once by the caller)
+void kmeans_assign_cs(const Tensor& X, const Tensor& Cq, const Tensor& hn,
+                      const std::optional<Tensor>& xh,
+                      double M, Tensor assign, const std::optional<Tensor>& mind,
+                      const std::optional<Tensor>& sse) {
+  TORCH_CHECK(Cq.dim() == 2 && Cq.is_contiguous() && Cq.scalar_type() == at::kBFloat16, "Cq bf16 [kpad, DP]");
+  const int DP = (int)Cq.size(1);
+  TORCH_CHECK(DP == 64 || DP == 128, "kmeans_assign_cs: DP 64 or 128");
+  check_points(X, DP);
+  TORCH_CHECK(X.scalar_type() == at::kBFloat16, "kmeans_assign_cs: bf16 points");
+  check_dev(Cq, "Cq");
+  const int64_t kpad = Cq.size(0);
+  TORCH_CHECK(kpad == 256 || kpad == 512 || kpad == 1024, "kmeans_assign_cs: kpad 256/512/1024");
+  check_f32(hn, "hn");
+  TORCH_CHECK(hn.numel() >= kpad, "hn");
+  const float* xhp = nullptr;
+  if (xh.has_value()) {
+    check_f32(*xh, "xh");
+    TORCH_CHECK(xh->numel() >= X.size(0), "xh [n]");
+    xhp = xh->data_ptr<float>();
+  }
+  check_dev(assign, "assign");
+  TORCH_CHECK(assign.scalar_type() == at::kInt && assign.numel() >= X.size(0), "assign int32[n]");
+  float* md = nullptr;
+  if (mind.has_value()) {
+    check_f32(*mind, "mind");
+    TORCH_CHECK(mind->numel() >= X.size(0), "mind");
+    TORCH_CHECK(xhp != nullptr, "kmeans_assign_cs: per-point distances need xh");
+    md = mind->data_ptr<float>();
+  }
+  double* ss = nullptr;
+  int sse_mask = 0;
+  if (sse.has_value()) {
+    check_dev(*sse, "sse");
+    TORCH_CHECK(sse->scalar_type() == at::kDouble && sse->numel() >= 1 && sse->is_contiguous(),
+                "sse f64[>=1]");
+    ss = sse->data_ptr<double>();
+    while (sse_mask < 1023 && 2 * (sse_mask + 1) <= sse->numel()) sse_mask = 2 * sse_mask + 1;
+  }
+  DeviceGuard guard(X.device());
+  DALGO_CHECK_HIP(dalgo_kmeans_assign_cs(X.data_ptr(), X.size(0), X.stride(0), DP, Cq.data_ptr(),
+                                         (int)kpad, hn.data_ptr<float>(), xhp,
+                                         (float)M, assign.data_ptr<int>(), md, ss, sse_mask,
+                                         cur_stream()),
+                  "kmeans_assign_cs");
+}
+
 void kmeans_accumulate(const Tensor& X, const Tensor& assign, int64_t k, int64_t DP, Tensor S,
                        Tensor cnt) {
   TORCH_CHECK(kmeans_dp(DP) == DP, "DP must be 16/32/64/128");
@@ -954,6 +1002,8 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("kmeans_accumulate_sorted(Tensor X, Tensor assign, int k, int DP, int seg, "
         "Tensor(a!) block_counts, Tensor(b!) cluster_start, Tensor(c!) seg_start, Tensor(d!) perm, "
         "Tensor(e!) S, Tensor(f!) cnt) -> ()");
+  m.def("kmeans_assign_cs(Tensor X, Tensor Cq, Tensor hn, Tensor? xh, float M, Tensor(a!) assign, "
+        "Tensor(b!)? mind, Tensor(c!)? sse) -> ()");
   m.def("kmeans_diff(Tensor a_new, Tensor a_old, Tensor(a!) changed, Tensor(b!) n_changed) -> ()");
   m.def("kmeans_move(Tensor X, int DP, Tensor changed, int m, Tensor a_new, Tensor a_old, "
         "Tensor(a!) S64, Tensor(b!) cnt) -> ()");
@@ -1026,6 +1076,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("kmeans_accumulate", &kmeans_accumulate);
   m.impl("kmeans_update", &kmeans_update);
   m.impl("kmeans_diff", &kmeans_diff);
+  m.impl("kmeans_assign_cs", &kmeans_assign_cs);
   m.impl("kmeans_move", &kmeans_move);
   m.impl("kmeans_accumulate_sorted", &kmeans_accumulate_sorted);   // dispatches on its output counter
 }

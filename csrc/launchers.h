@@ -103,6 +103,11 @@ hipError_t dalgo_pr_update(const float* acc, const int32_t* pres, const int32_t*
                            float* c, float* dangling_out, hipStream_t st);
 
 // ---- K9 transitive closure (closure.hip)
+// ---- K2 centre-stationary form (kmeans_cs.hip)
+hipError_t dalgo_kmeans_assign_cs(const void* X, int64_t n, int64_t ldx, int DP, const void* Cq,
+                                  int kpad, const float* hn, const float* xh, float M, int* assign,
+                                  float* mind, double* sse, int sse_mask, hipStream_t st);
+
 // ---- K3 incremental form (kmeans_inc.hip)
 hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, int32_t* changed,
                          unsigned long long* n_changed, int64_t cap, hipStream_t st);

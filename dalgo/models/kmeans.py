@@ -69,7 +69,11 @@ class KMeans:
         k = cfg.k
         if init_centers is None:
             init_centers = self._sample_init()
-        self.cen = K.make_centers(init_centers.float(), self.X.dtype, self.dev)
+        # centre-stationary K2 (kmeans_cs.hip) when it applies: centres padded to
+        # 256 / 512 / 1024, fixed point statistics computed once
+        kp = K.cs_kpad(k, self.d, self.X.dtype, self.dev)
+        self.pstats = K.point_stats(self.X) if kp is not None else None
+        self.cen = K.make_centers(init_centers.float(), self.X.dtype, self.dev, kpad=kp)
         self.assign = torch.zeros(self.X.shape[0], dtype=torch.int32, device=self.dev)
         # [S (k x DP) || count lo (k) || count hi (k)]: one all-reduce per iteration
         self.bucket = torch.zeros(k * self.DP + 2 * k, dtype=torch.float32, device=self.dev)
@@ -110,7 +114,7 @@ class KMeans:
         inc = self._S64 is not None and self.inc_max > 0
         a_out = self._a_new if inc else self.assign
         with self._ph("assign"):
-            K.assign(self.X, self.cen, out=a_out, sse=self.sse)
+            K.assign(self.X, self.cen, out=a_out, sse=self.sse, stats=self.pstats)
         moved = None
         if inc:
             with self._ph("diff"):
@@ -173,7 +177,9 @@ class KMeans:
         return self.history
 
     def predict(self, X: torch.Tensor) -> torch.Tensor:
-        return K.assign(K.prepare_points(X), self.cen)
+        Xp = K.prepare_points(X)
+        st = K.point_stats(Xp) if self.pstats is not None else None
+        return K.assign(Xp, self.cen, stats=st)
 
     @property
     def centers(self) -> torch.Tensor:

@@ -52,10 +52,12 @@ class Centers:
         return self.Cq.shape[1]
 
 
-def make_centers(C0: torch.Tensor, dtype: torch.dtype, device) -> Centers:
+def make_centers(C0: torch.Tensor, dtype: torch.dtype, device, kpad: int | None = None) -> Centers:
     k, d = C0.shape
     DP = kmeans_dp(d)
-    kpad = ((k + 127) // 128) * 128     # multiple of every chunk width of the assign kernel
+    if kpad is None:
+        kpad = ((k + 127) // 128) * 128     # multiple of every chunk width of the assign kernel
+    assert kpad >= k and kpad % 128 == 0
     C = C0.to(device=device, dtype=torch.float32).contiguous()
     Cq = torch.zeros((kpad, DP), dtype=dtype, device=device)
     hn = torch.zeros(kpad, dtype=torch.float32, device=device)
@@ -95,6 +97,46 @@ def assign_variant(X: torch.Tensor, variant: int | None = None) -> int:
     return v
 
 
+# ------------------------------------------------------------------ centre-stationary K2
+CS_VARIANT = 60
+CS_KPADS = (256, 512, 1024)
+
+
+def cs_kpad(k: int, d: int, dtype: torch.dtype, device) -> int | None:
+    """Centre padding for the centre-stationary K2 (kmeans_cs.hip), or None if it does
+    not apply (bf16 points on the GPU, d in (32, 128], k <= 1024, variant default or 60)."""
+    if torch.device(device).type != "cuda" or dtype != torch.bfloat16:
+        return None
+    if kmeans_dp(d) not in (64, 128) or k > 1024 or ASSIGN_VARIANT not in (-1, CS_VARIANT):
+        return None
+    for kp in CS_KPADS:
+        if k <= kp:
+            return kp
+    return None
+
+
+@dataclass
+class PointStats:
+    """Fixed per point set (the points never change between Lloyd iterations)."""
+    M: float                  # >= max 0.5|x|^2 (slack against MFMA rounding)
+    x2sum: float              # sum |x|^2 (f64): SSE = kernel sum + x2sum
+    xh: torch.Tensor | None   # 0.5|x|^2 per point (only for per-point distances)
+
+
+def point_stats(X: torch.Tensor, keep_xh: bool = False, chunk: int = 1 << 22) -> PointStats:
+    n = X.shape[0]
+    mx, tot = 0.0, 0.0
+    xh = torch.empty(n, dtype=torch.float32, device=X.device) if keep_xh else None
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        q = 0.5 * (X[s:e].float() ** 2).sum(dim=1)
+        mx = max(mx, float(q.max().item())) if e > s else mx
+        tot += 2.0 * float(q.double().sum().item())
+        if xh is not None:
+            xh[s:e] = q
+    return PointStats(mx * 1.0001 + 1e-6, tot, xh)
+
+
 def _sse_slots(device) -> torch.Tensor:
     """Zeroed [256] f64 slots for the assign kernels' per-block SSE partials."""
     key = ("sse", str(device))
@@ -119,11 +161,21 @@ def _dist_scratch(n: int, device) -> torch.Tensor:
 
 def assign(X: torch.Tensor, cen: Centers, out: torch.Tensor | None = None,
            mind: torch.Tensor | None = None, sse: torch.Tensor | None = None,
-           variant: int | None = None):
-    """Nearest-centre ids (int32, ties -> lowest id), squared distances, SSE."""
+           variant: int | None = None, stats: PointStats | None = None):
+    """Nearest-centre ids (int32, ties -> lowest id), squared distances, SSE.
+
+    ``stats`` (from :func:`point_stats`) enables the centre-stationary K2 when the
+    centres are padded to 256 / 512 / 1024 (see :func:`cs_kpad`)."""
     n = X.shape[0]
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=X.device)
+    if (X.is_cuda and stats is not None and cen.Cq.shape[0] in CS_KPADS
+            and variant in (None, CS_VARIANT) and (mind is None or stats.xh is not None)):
+        slots = _sse_slots(X.device) if sse is not None else None
+        _ext.ops().kmeans_assign_cs(X, cen.Cq, cen.hn, stats.xh, float(stats.M), out, mind, slots)
+        if sse is not None:
+            sse += slots.sum() + stats.x2sum
+        return out
     if X.is_cuda:
         v = assign_variant(X, variant)
         md = mind

@@ -617,3 +617,58 @@ def test_pr_spmv_hot_lds_table(cuda, monkeypatch, hot):
     got = PageRank(PageRankConfig(), sh).fit().collect()
     assert set(ref) == set(got)
     assert max(abs(ref[v] - got[v]) for v in ref) < 1e-7
+
+
+@pytest.mark.parametrize("d,k,n", [(128, 1024, 20000), (100, 1000, 7001), (64, 512, 513),
+                                   (50, 300, 4099), (128, 200, 65), (64, 1024, 100_003)])
+def test_kmeans_assign_centre_stationary(cuda, d, k, n):
+    """K2 centre-stationary form (centres resident in VGPRs, points streamed once through
+    LDS by DMA, cross-wave argmin): assignments, per-point distances and SSE == the CPU
+    reference on the rounded operands (rare f32 near-ties allowed)."""
+    torch.manual_seed(d * k)
+    X = (torch.randn(n, d) * 3).to(torch.bfloat16)
+    C0 = torch.randn(k, d) * 3
+    Xc = K.prepare_points(X)
+    cen_c = K.make_centers(C0, torch.bfloat16, "cpu")
+    sse_c = torch.zeros(1, dtype=torch.float64)
+    a_ref = K.assign(Xc, cen_c, sse=sse_c)
+    Xd = K.prepare_points(X.to(cuda))
+    kp = K.cs_kpad(k, d, torch.bfloat16, cuda)
+    assert kp in K.CS_KPADS
+    cen_d = K.make_centers(C0, torch.bfloat16, cuda, kpad=kp)
+    st = K.point_stats(Xd, keep_xh=True)
+    mind = torch.empty(n, device=cuda)
+    sse = torch.zeros(1, dtype=torch.float64, device=cuda)
+    a = K.assign(Xd, cen_d, mind=mind, sse=sse, stats=st).cpu()
+    agree = (a == a_ref).float().mean().item()
+    assert agree > 0.999, agree
+    Xf = Xc.double()
+    Cr = cen_c.Cq[:k, :d].double()
+    dist = torch.cdist(Xf, Cr) ** 2
+    dd = dist.gather(1, a.long()[:, None]) - dist.gather(1, a_ref.long()[:, None])
+    assert dd.abs().max().item() < 1e-3 * (1 + dist.max().item())
+    best = dist.gather(1, a.long()[:, None])[:, 0]
+    assert torch.allclose(mind.cpu().double(), best, rtol=1e-3, atol=5e-2)
+    assert float(sse.item()) == pytest.approx(float(sse_c.item()), rel=1e-4)
+    # without per-point distances (the model's path: no xh vector)
+    st2 = K.point_stats(Xd)
+    a2 = K.assign(Xd, cen_d, stats=st2).cpu()
+    assert torch.equal(a2, a)
+
+
+def test_kmeans_model_centre_stationary_vs_pipelined(cuda, monkeypatch):
+    """KMeans on blobs: the centre-stationary K2 (default for bf16, k <= 1024) and the
+    pipelined variant 52 give the same centres and SSE trajectory."""
+    from dalgo.data.synthetic import blobs
+    from dalgo.models.kmeans import KMeans, KMeansConfig
+    n, d, k = 200_000, 128, 1000
+    X = blobs(n, d, k, device=cuda, dtype=torch.bfloat16, seed=4)
+    a = KMeans(KMeansConfig(k=k, n_iterations=4, seed=3), X, 0, n)
+    assert a.pstats is not None and a.cen.Cq.shape[0] == 1024
+    a.fit()
+    monkeypatch.setattr(K, "ASSIGN_VARIANT", 52)
+    b = KMeans(KMeansConfig(k=k, n_iterations=4, seed=3), X, 0, n)
+    assert b.pstats is None
+    b.fit()
+    assert np.allclose(a.history.sse, b.history.sse, rtol=1e-5)
+    assert torch.allclose(a.centers, b.centers, atol=1e-3)
