@@ -102,12 +102,16 @@ CS_VARIANT = 60
 CS_KPADS = (256, 512, 1024)
 
 
-def cs_kpad(k: int, d: int, dtype: torch.dtype, device) -> int | None:
-    """Centre padding for the centre-stationary K2 (kmeans_cs.hip), or None if it does
-    not apply (bf16 points on the GPU, d in (32, 128], k <= 1024, variant default or 60)."""
-    if torch.device(device).type != "cuda" or dtype != torch.bfloat16:
+def cs_kpad(k: int, d: int, dtype: torch.dtype, device, variant: int | None = None) -> int | None:
+    """Centre padding for the centre-stationary K2 (kmeans_cs.hip, DALGO_KM_VARIANT=60),
+    or None if it is not selected / does not apply (bf16 points on the GPU, d in (32, 128],
+    k <= 1024). Opt-in: measured 23.4 ms vs 22.8 ms for the default pipelined variant 52
+    at 100M x 128, k = 1024 (MFMA busy 57.7 % vs 68.1 %, profiles/round3/README.md): with
+    two waves per SIMD the 128 resident centres per wave leave no VGPRs to prefetch."""
+    v = ASSIGN_VARIANT if variant is None else variant
+    if torch.device(device).type != "cuda" or dtype != torch.bfloat16 or v != CS_VARIANT:
         return None
-    if kmeans_dp(d) not in (64, 128) or k > 1024 or ASSIGN_VARIANT not in (-1, CS_VARIANT):
+    if kmeans_dp(d) not in (64, 128) or k > 1024:
         return None
     for kp in CS_KPADS:
         if k <= kp:
