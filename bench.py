@@ -108,12 +108,37 @@ def calibrate_launch(model, rt, a) -> dict:
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=rt.device)
         comm.all_reduce_max(el)
         res[name] = float(el.item()) / a.cal_steps * 1e3
-    comm.check_device_errors("launch calibration")
+    try:
+        comm.check_device_errors("launch calibration")
+    except comm.DeviceCollectiveError:
+        fallback_plain(model, rt, "launch calibration")
+        model.load_state_dict(snap)
+        rt.synchronize()
+        return {"failed": True, **res}
     best = min(res, key=res.get)
     model._ok1, model._okp = cands[best]
     model.load_state_dict(snap)
     rt.synchronize()
     return res
+
+
+def fallback_plain(model, rt, why: str) -> None:
+    """A device-side wait (K11 peer flag, persistent step release) timed out on some rank
+    (collective check raised everywhere): switch EVERY rank to the plain per-step form
+    over the process group -- no kernel waits on another GPU any more -- and clear the
+    error words. The caller restores the model and measures again."""
+    from dalgo.parallel import comm, xgmi
+    if rt.is_main:
+        print(f"[bench] device-side wait failed during {why}: falling back to per-step "
+              f"launches over {rt.backend}", file=sys.stderr, flush=True)
+    rt.synchronize()
+    xgmi.disable()
+    if hasattr(model, "bucket"):
+        model.bucket.xg = None
+    model._ok1, model._okp = False, False
+    model._okg = None
+    comm.reset_device_errors()
+    rt.barrier()
 
 
 def _free_port() -> int:
@@ -204,21 +229,39 @@ def main(argv=None):
     model.run_steps(a.warmup)
     rt.synchronize()
     cal = calibrate_launch(model, rt, a) if a.launch == "auto" else {}
-    rt.barrier()
-    rt.synchronize()
-    model.count_acc = count
-    t_start = time.perf_counter()
-    model.run_steps(a.steps)
-    rt.synchronize()
-    rt.barrier()
-    rt.synchronize()
-    elapsed = time.perf_counter() - t_start
-    samples = model.global_sample_count()
-    model.count_acc = None
-    xg = getattr(getattr(model, "bucket", None), "xg", None)
+    def timed():
+        rt.barrier()
+        rt.synchronize()
+        count.zero_()
+        model.count_acc = count
+        t_start = time.perf_counter()
+        model.run_steps(a.steps)
+        rt.synchronize()
+        rt.barrier()
+        rt.synchronize()
+        el_ = time.perf_counter() - t_start
+        n_ = model.global_sample_count()
+        model.count_acc = None
+        return el_, n_
+
+    snap = model.state_dict()
+    elapsed, samples = timed()
+    if os.environ.get("DALGO_TEST_FORCE_DEVICE_ERROR") == str(rt.rank):
+        comm._forced_error = 1      # test hook: as if a wait of the timed region timed out
+    fell_back = False
     # collective: MAX of every rank's device error words (K11 peer waits, persistent
-    # step releases) first, then raise on EVERY rank (non-zero exit everywhere)
-    comm.check_device_errors("bench")
+    # step releases); if any wait timed out the timed steps are invalid: every rank
+    # falls back to the plain per-step form and the warmup + timed region run again
+    try:
+        comm.check_device_errors("bench")
+    except comm.DeviceCollectiveError:
+        fallback_plain(model, rt, "the timed region")
+        model.load_state_dict(snap)
+        model.run_steps(a.warmup)
+        elapsed, samples = timed()
+        comm.check_device_errors("bench (fallback)")
+        fell_back = True
+    xg = getattr(getattr(model, "bucket", None), "xg", None)
     launch = "persistent" if model._persistent() else (
         "hipgraph-replay" if model._graph_ok() else (
             "one-kernel" if model._one_kernel() else "per-step"))
@@ -292,6 +335,7 @@ def main(argv=None):
             except Exception:
                 out["rccl_version"] = None
         out["small_allreduce_race"] = xgmi.last_race
+        out["device_wait_fallback"] = fell_back
         out["allreduce_us_per_step"] = ar_us
         if witness is not None:
             out["heldout_accuracy"] = acc

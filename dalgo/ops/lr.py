@@ -130,6 +130,11 @@ def persistent_error() -> int:
     return e
 
 
+def reset_persistent_error():
+    for ws in _ws_cache.values():
+        ws.perr.zero_()
+
+
 def check_persistent():
     """Local (this rank only) form of the persistent-launch check; multi-rank callers
     use the collective :func:`dalgo.parallel.comm.check_device_errors`."""

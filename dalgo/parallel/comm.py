@@ -82,8 +82,14 @@ def error_seen() -> bool:
     return _error_seen
 
 
+# test hook: a device error word this rank reports once (exercises the recovery paths
+# on hosts without device-side waits; set via DALGO_TEST_FORCE_DEVICE_ERROR in bench.py)
+_forced_error = 0
+
+
 def _local_error_word() -> int:
-    e = 0
+    global _forced_error
+    e, _forced_error = _forced_error, 0
     from dalgo.parallel import xgmi
     for inst in list(xgmi._shared.values()):
         if inst is not None:
@@ -111,6 +117,20 @@ def check_device_errors(where: str = "") -> None:
         at = f" (at {where})" if where else ""
         raise DeviceCollectiveError(
             f"a device-side collective wait timed out on some rank{at}: results are invalid")
+
+
+def reset_device_errors() -> None:
+    """Clear this rank's device error words and the raised flag (call on every rank,
+    after :func:`check_device_errors` raised everywhere and the caller has switched the
+    run to paths without device-side waits, e.g. :func:`dalgo.parallel.xgmi.disable`)."""
+    global _error_seen
+    from dalgo.parallel import xgmi
+    for inst in list(xgmi._shared.values()):
+        if inst is not None:
+            inst.err.zero_()
+    from dalgo.ops import lr as lr_ops
+    lr_ops.reset_persistent_error()
+    _error_seen = False
 
 
 def all_reduce_max(t: torch.Tensor):

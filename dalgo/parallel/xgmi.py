@@ -255,6 +255,16 @@ def shared(device: torch.device) -> XgmiAllReduce | None:
     return inst
 
 
+def disable() -> None:
+    """Collective: stop using K11 for the rest of the run (every later small all-reduce
+    goes through the process group); the exchange buffers are released."""
+    for k, inst in list(_shared.items()):
+        if inst is not None:
+            inst.err.zero_()
+            inst.close()
+        _shared[k] = None
+
+
 def close_shared():
     """Release the shared instances (collective; called by runtime.shutdown)."""
     for k, inst in list(_shared.items()):

@@ -259,3 +259,15 @@ def test_metrics_jsonl_phases_two_ranks(tmp_path):
     assert len(recs) == 5 and set(recs[0]["phase_ms"]) >= {"assign", "accumulate", "allreduce",
                                                            "update"}
     assert recs[-1]["bytes_allreduced"] == 5 * 4 * (4 * 16 + 2 * 4)
+
+
+def test_bench_recovers_from_device_wait_failure():
+    """A device-side wait failure reported by one rank after the timed region: every rank
+    falls back to the plain per-step form, re-runs warmup + timed steps and the bench
+    still reports a valid (witness-checked) number, flagged in the JSON."""
+    out = _run(["bench.py", "--gpus", "2", "--device", "cpu", "--backend", "gloo", "--rows", "20000",
+                "--dim", "64", "--steps", "3", "--warmup", "1", "--dtype", "f32", "--n-test", "5000"],
+               env_extra={"DALGO_TEST_FORCE_DEVICE_ERROR": "1"}, timeout=600)
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+    assert d["device_wait_fallback"] is True and d["n_gpus"] == 2
+    assert d["correctness_witness"]["passed"]
