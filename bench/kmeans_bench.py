@@ -39,38 +39,29 @@ def main():
     torch.cuda.synchronize()
     gen = time.time() - t0
     km = KMeans(KMeansConfig(k=a.k, n_iterations=a.steps, seed=1), X, lo, a.rows)
-    for _ in range(a.warmup):
-        km.step()
-    torch.cuda.synchronize()
-    # one full-pass iteration with per-phase events (assign / full K3 / all-reduce /
-    # update) on a scratch copy of the state, so the timed loop continues from warmup
-    snap = km.cen.C.clone()
-    # phase breakdown on one iteration
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
-    km.sse.zero_(); km.S.zero_(); km.cnt.zero_(); km.shift2.zero_()
-    ev[0].record()
-    K.assign(km.X, km.cen, out=km.assign, sse=km.sse, stats=km.pstats)
-    ev[1].record()
-    K.accumulate(km.X, km.assign, a.k, km.DP, km.S, km.cnt)
-    ev[2].record()
-    km._keep_local_sums()   # local sums of this assignment for the incremental form
-    comm.all_reduce_sum(km.bucket)
-    ev[3].record()
-    K.update(km.cen, km.S, km.cnt, km.shift2)
-    ev[4].record()
-    torch.cuda.synchronize()
-    phases = {n: ev[i].elapsed_time(ev[i + 1]) for i, n in enumerate(["assign", "accumulate", "allreduce", "update"])}
-    km.cen.C.copy_(snap)
-    K.refresh(km.cen)   # the next step re-assigns with the same centres: 0 moved rows
-    rt.barrier(); torch.cuda.synchronize()
     from dalgo.utils.obs import PhaseTimer
+    # warmup: the first iteration is the full pass (full K2 + K3, bounds built); its
+    # phases are reported separately
+    km.timer = PhaseTimer(rt.device)
+    first = None
+    for i in range(a.warmup):
+        km.step()
+        if i == 0:
+            first = km.timer.summary()
+            km.timer = PhaseTimer(rt.device)
+    torch.cuda.synchronize()
+    rt.barrier(); torch.cuda.synchronize()
     km.timer = PhaseTimer(rt.device)     # HIP events only (no host sync in the loop)
     km.changed_history.clear()
+    km.active_history.clear()
     t = time.perf_counter()
     for _ in range(a.steps):
         km.step()
     torch.cuda.synchronize(); rt.barrier(); torch.cuda.synchronize()
     timed_phases = {k: v / a.steps for k, v in km.timer.summary().items()}
+    phases = first or {}
+    sse_last = km.sse.clone()
+    comm.all_reduce_sum(sse_last)
     el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=rt.device)
     comm.all_reduce_max(el)
     ms = float(el.item()) / a.steps * 1e3
@@ -78,9 +69,12 @@ def main():
     if rt.is_main:
         print(json.dumps({
             "metric": "k-means points/sec (whole node)", "value": a.rows / (ms / 1e3), "unit": "points/s",
-            "n_gpus": W, "ms_per_iter": ms, "assign_tflops_per_gpu": flops / W / (phases["assign"] / 1e3) / 1e12,
-            "phases_ms_rank0": phases, "timed_phases_ms_per_iter_rank0": timed_phases,
+            "n_gpus": W, "ms_per_iter": ms, "full_assign_tflops_per_gpu": flops / W / (phases["assign"] / 1e3) / 1e12 if phases.get("assign") else None,
+            "first_iteration_phases_ms_rank0": phases,
+            "timed_phases_ms_per_iter_rank0": timed_phases,
             "moved_rows_per_iter_rank0": list(km.changed_history),
+            "reassigned_rows_per_iter_rank0": list(km.active_history),
+            "bound_filter": km.bounds, "sse_last_iteration": float(sse_last.item()),
             "accumulate_mode": "incremental below %.1f %% moved rows" % (100 * km.inc_max)
             if km.inc_max > 0 else "full", "config": {"rows": a.rows, "dim": a.dim, "k": a.k, "dtype": a.dtype},
             "datagen_s": gen}), flush=True)

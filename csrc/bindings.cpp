@@ -522,7 +522,8 @@ void kmeans_diff(const Tensor& a_new, const Tensor& a_old, Tensor changed, Tenso
 }
 
 void kmeans_move(const Tensor& X, int64_t DP, const Tensor& changed, int64_t m,
-                 const Tensor& a_new, const Tensor& a_old, Tensor S64, Tensor cnt) {
+                 const Tensor& a_new, const Tensor& a_old, Tensor S64, Tensor cnt,
+                 const std::optional<Tensor>& xh, const std::optional<Tensor>& Q) {
   TORCH_CHECK(kmeans_dp(DP) == DP, "DP must be 16/32/64/128");
   check_points(X, (int)DP);
   check_dev(changed, "changed");
@@ -533,13 +534,101 @@ void kmeans_move(const Tensor& X, int64_t DP, const Tensor& changed, int64_t m,
   TORCH_CHECK(S64.scalar_type() == at::kDouble && S64.is_contiguous(), "S64 f64");
   TORCH_CHECK(cnt.scalar_type() == at::kLong && cnt.is_contiguous(), "cnt int64");
   TORCH_CHECK(S64.numel() % DP == 0 && cnt.numel() >= S64.numel() / DP, "S64 [k, DP] / cnt [k]");
+  const float* xp = nullptr;
+  double* qp = nullptr;
+  TORCH_CHECK(xh.has_value() == Q.has_value(), "kmeans_move: xh and Q together");
+  if (Q.has_value()) {
+    check_f32(*xh, "xh");
+    TORCH_CHECK(xh->numel() >= X.size(0), "xh [n]");
+    check_dev(*Q, "Q");
+    TORCH_CHECK(Q->scalar_type() == at::kDouble && Q->numel() >= cnt.numel() && Q->is_contiguous(),
+                "Q f64 [k]");
+    xp = xh->data_ptr<float>();
+    qp = Q->data_ptr<double>();
+  }
   DeviceGuard guard(X.device());
   DALGO_CHECK_HIP(dalgo_km_move(X.data_ptr(), X.scalar_type() == at::kBFloat16, X.stride(0), (int)DP,
                                 changed.data_ptr<int32_t>(), m, a_new.data_ptr<int32_t>(),
                                 a_old.data_ptr<int32_t>(), S64.data_ptr<double>(),
                                 reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>()),
-                                cur_stream()),
+                                xp, qp, cur_stream()),
                   "kmeans_move");
+}
+
+// bound-filtered Lloyd: active rows (u + delta[a] >= s[a]) -> idx, their assignment -> a_prev
+void kmeans_filter(const Tensor& assign, Tensor u, const Tensor& delta, const Tensor& s,
+                   Tensor a_prev, Tensor idx, Tensor n_active) {
+  const int64_t n = assign.numel();
+  check_i32(assign, "assign");
+  check_f32(u, "u");
+  check_f32(delta, "delta");
+  check_f32(s, "s");
+  check_i32(a_prev, "a_prev");
+  check_i32(idx, "idx");
+  TORCH_CHECK(u.numel() >= n && a_prev.numel() >= n && idx.numel() >= n, "kmeans_filter sizes");
+  TORCH_CHECK(delta.numel() == s.numel(), "delta / s [k]");
+  TORCH_CHECK(n_active.scalar_type() == at::kLong && n_active.numel() >= 1, "n_active int64[1]");
+  DeviceGuard guard(assign.device());
+  DALGO_CHECK_HIP(dalgo_km_filter(assign.data_ptr<int32_t>(), u.data_ptr<float>(), delta.data_ptr<float>(),
+                                  s.data_ptr<float>(), n, a_prev.data_ptr<int32_t>(), idx.data_ptr<int32_t>(),
+                                  reinterpret_cast<unsigned long long*>(n_active.data_ptr<int64_t>()),
+                                  idx.numel(), cur_stream()),
+                  "kmeans_filter");
+}
+
+void kmeans_post(const Tensor& idx, int64_t m, const Tensor& assign, const Tensor& a_prev,
+                 const Tensor& mind, double tol, Tensor u, Tensor changed, Tensor n_changed) {
+  check_i32(idx, "idx");
+  check_i32(assign, "assign");
+  check_i32(a_prev, "a_prev");
+  check_f32(mind, "mind");
+  check_f32(u, "u");
+  check_i32(changed, "changed");
+  TORCH_CHECK(m >= 0 && m <= idx.numel(), "kmeans_post: m");
+  TORCH_CHECK(n_changed.scalar_type() == at::kLong && n_changed.numel() >= 1, "n_changed int64[1]");
+  DeviceGuard guard(idx.device());
+  DALGO_CHECK_HIP(dalgo_km_post(idx.data_ptr<int32_t>(), m, assign.data_ptr<int32_t>(),
+                                a_prev.data_ptr<int32_t>(), mind.data_ptr<float>(), (float)tol,
+                                u.data_ptr<float>(), changed.data_ptr<int32_t>(),
+                                reinterpret_cast<unsigned long long*>(n_changed.data_ptr<int64_t>()),
+                                changed.numel(), cur_stream()),
+                  "kmeans_post");
+}
+
+void kmeans_qsum(const Tensor& assign, const Tensor& xh, int64_t k, Tensor Q) {
+  check_i32(assign, "assign");
+  check_f32(xh, "xh");
+  check_dev(Q, "Q");
+  TORCH_CHECK(Q.scalar_type() == at::kDouble && Q.numel() >= k && Q.is_contiguous(), "Q f64 [k]");
+  TORCH_CHECK(xh.numel() >= assign.numel() && k <= 2048, "kmeans_qsum sizes");
+  DeviceGuard guard(assign.device());
+  DALGO_CHECK_HIP(dalgo_km_qsum(assign.data_ptr<int32_t>(), xh.data_ptr<float>(), assign.numel(),
+                                (int)k, Q.data_ptr<double>(), cur_stream()),
+                  "kmeans_qsum");
+}
+
+// K2 (variant 52) over the rows idx[0, m) only
+void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn, const Tensor& idx,
+                       int64_t m, Tensor assign, Tensor mind) {
+  TORCH_CHECK(Cq.dim() == 2 && Cq.is_contiguous() && Cq.scalar_type() == at::kBFloat16, "Cq bf16");
+  const int DP = (int)Cq.size(1);
+  TORCH_CHECK(DP == 64 || DP == 128, "kmeans_assign_idx: DP 64 or 128");
+  check_points(X, DP);
+  TORCH_CHECK(X.scalar_type() == at::kBFloat16, "kmeans_assign_idx: bf16 points");
+  const int64_t kpad = Cq.size(0);
+  TORCH_CHECK(kpad % 128 == 0, "kmeans_assign_idx: kpad % 128");
+  check_f32(hn, "hn");
+  check_i32(idx, "idx");
+  TORCH_CHECK(m >= 0 && m <= idx.numel(), "kmeans_assign_idx: m");
+  check_i32(assign, "assign");
+  check_f32(mind, "mind");
+  TORCH_CHECK(assign.numel() >= X.size(0) && mind.numel() >= X.size(0), "assign / mind [n]");
+  DeviceGuard guard(X.device());
+  DALGO_CHECK_HIP(dalgo_kmeans_assign_idx(X.data_ptr(), m, X.stride(0), DP, Cq.data_ptr(),
+                                          hn.data_ptr<float>(), (int)kpad, idx.data_ptr<int32_t>(),
+                                          assign.data_ptr<int>(), mind.data_ptr<float>(), nullptr, 0,
+                                          cur_stream()),
+                  "kmeans_assign_idx");
 }
 
 void kmeans_update(Tensor C, const Tensor& S, const Tensor& cnt, Tensor Cq, Tensor hn,
@@ -1006,7 +1095,14 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(b!)? mind, Tensor(c!)? sse) -> ()");
   m.def("kmeans_diff(Tensor a_new, Tensor a_old, Tensor(a!) changed, Tensor(b!) n_changed) -> ()");
   m.def("kmeans_move(Tensor X, int DP, Tensor changed, int m, Tensor a_new, Tensor a_old, "
-        "Tensor(a!) S64, Tensor(b!) cnt) -> ()");
+        "Tensor(a!) S64, Tensor(b!) cnt, Tensor? xh=None, Tensor(c!)? Q=None) -> ()");
+  m.def("kmeans_filter(Tensor assign, Tensor(a!) u, Tensor delta, Tensor s, Tensor(b!) a_prev, "
+        "Tensor(c!) idx, Tensor(d!) n_active) -> ()");
+  m.def("kmeans_post(Tensor idx, int m, Tensor assign, Tensor a_prev, Tensor mind, float tol, "
+        "Tensor(a!) u, Tensor(b!) changed, Tensor(c!) n_changed) -> ()");
+  m.def("kmeans_qsum(Tensor assign, Tensor xh, int k, Tensor(a!) Q) -> ()");
+  m.def("kmeans_assign_idx(Tensor X, Tensor Cq, Tensor hn, Tensor idx, int m, Tensor(a!) assign, "
+        "Tensor(b!) mind) -> ()");
   m.def("kmeans_update(Tensor(a!) C, Tensor S, Tensor cnt, Tensor(b!) Cq, Tensor(c!) hn, "
         "Tensor(d!)? shift2) -> ()");
   m.def("rmat_edges(int seed, int scale, int e_off, float a, float b, float c, bool scramble, "
@@ -1078,5 +1174,9 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("kmeans_diff", &kmeans_diff);
   m.impl("kmeans_assign_cs", &kmeans_assign_cs);
   m.impl("kmeans_move", &kmeans_move);
+  m.impl("kmeans_filter", &kmeans_filter);
+  m.impl("kmeans_post", &kmeans_post);
+  m.impl("kmeans_qsum", &kmeans_qsum);
+  m.impl("kmeans_assign_idx", &kmeans_assign_idx);
   m.impl("kmeans_accumulate_sorted", &kmeans_accumulate_sorted);   // dispatches on its output counter
 }

@@ -484,7 +484,10 @@ __global__ void __launch_bounds__(NW * 64, MINB)
 kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
                           const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int kpad,
                           int* __restrict__ assign, float* __restrict__ mind,
-                          double* __restrict__ sse, int sse_mask) {
+                          double* __restrict__ sse, int sse_mask,
+                          const int32_t* __restrict__ idx) {
+  // idx (optional): the block's point j is row idx[j] of X (and of assign / mind), j < n
+  // -- the bound-filtered form of Lloyd only re-assigns the points the filter keeps
   constexpr int KS = DP / 16;                  // 32x32x16 k-steps per centre row
   constexpr int NJ = DP * 2 / 16;              // 16-B pieces per row (= 2 KS)
   constexpr int SWZ = (NJ >= 16 ? 16 : NJ) - 1;
@@ -510,7 +513,8 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   for (int t = 0; t < PT; ++t) {
     const int64_t p = pbase + t * 32 + cl;
     const bool ok = p < n;
-    const uint16_t* src = X + (ok ? p : 0) * ldx + h * 8;
+    const int64_t row = ok ? (idx ? (int64_t)idx[p] : p) : 0;
+    const uint16_t* src = X + row * ldx + h * 8;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const uint4 v = *reinterpret_cast<const uint4*>(src + 16 * s);
@@ -733,8 +737,9 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     if (h == 0 && p < n) {
       // acc = 0.5|x-c|^2 + M - 0.5|x|^2
       const float dist = fmaxf(2.f * (bv - M) + x2[t], 0.f);
-      assign[p] = bi;
-      if (mind) mind[p] = dist;
+      const int64_t row = idx ? (int64_t)idx[p] : p;
+      assign[row] = bi;
+      if (mind) mind[row] = dist;
       my_sse += (double)dist;
     }
   }
@@ -1156,7 +1161,8 @@ static hipError_t launch_assign_res(const void* X, int64_t n, int64_t ldx, const
 template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, int SWP = 0, int DIAG = 0>
 static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                      const float* hn, int kpad, int* assign, float* mind,
-                                     double* sse, int sse_mask, hipStream_t st) {
+                                     double* sse, int sse_mask, hipStream_t st,
+                                     const int32_t* idx = nullptr) {
   constexpr int CH = 32 * NSUB;
   constexpr size_t kStatic = NBUF * (size_t)CH * DP * 2;
   if (kpad % CH) return hipErrorInvalidValue;
@@ -1174,7 +1180,7 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
     attr_set = dyn;
   }
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(NW * 64), dyn, st, (const uint16_t*)X, n, ldx,
-                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse, sse_mask);
+                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse, sse_mask, idx);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -1388,6 +1394,21 @@ hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ld
   if (kpad % 32 != 0) return hipErrorInvalidValue;
   return is_bf16 ? launch_assign<uint16_t>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st)
                  : launch_assign<float>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st);
+}
+
+// K2 (variant 52) over the rows idx[0, m) of X only (bound-filtered Lloyd iteration)
+hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP, const void* Cq,
+                                   const float* hn, int kpad, const int32_t* idx, int* assign,
+                                   float* mind, double* sse, int sse_mask, hipStream_t st) {
+  if (m <= 0) return hipSuccess;
+  if (kpad % 128 != 0) return hipErrorInvalidValue;
+  if (DP == 128)
+    return launch_assign_pipe<128, 4, 3, 4, 2, 2, true, 2>(X, m, ldx, Cq, hn, kpad, assign, mind, sse,
+                                                           sse_mask, st, idx);
+  if (DP == 64)
+    return launch_assign_pipe<64, 4, 3, 4, 2, 2, true, 2>(X, m, ldx, Cq, hn, kpad, assign, mind, sse,
+                                                          sse_mask, st, idx);
+  return hipErrorInvalidValue;
 }
 
 hipError_t dalgo_kmeans_accumulate(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,

@@ -80,7 +80,8 @@ template <typename T, int DP>
 __global__ void __launch_bounds__(256)
 km_move_kernel(const T* __restrict__ X, int64_t ldx, const int32_t* __restrict__ changed,
                int64_t m, const int32_t* __restrict__ a_new, const int32_t* __restrict__ a_old,
-               double* __restrict__ S, unsigned long long* __restrict__ cnt) {
+               double* __restrict__ S, unsigned long long* __restrict__ cnt,
+               const float* __restrict__ xh, double* __restrict__ Q) {
   constexpr int PER = (DP + 63) / 64;     // features per lane
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -105,6 +106,11 @@ km_move_kernel(const T* __restrict__ X, int64_t ldx, const int32_t* __restrict__
     if (lane == 0) {
       atomicAdd(&cnt[cn], 1ull);
       atomicAdd(&cnt[co], ~0ull);   // -1 (two's complement)
+      if (Q != nullptr) {           // per-cluster sum of |x|^2 (SSE identity)
+        const double q = 2.0 * (double)xh[row];
+        atomicAdd(&Q[cn], q);
+        atomicAdd(&Q[co], -q);
+      }
     }
   }
 }
@@ -112,12 +118,145 @@ km_move_kernel(const T* __restrict__ X, int64_t ldx, const int32_t* __restrict__
 template <typename T, int DP>
 hipError_t launch_move(const void* X, int64_t ldx, const int32_t* changed, int64_t m,
                        const int32_t* a_new, const int32_t* a_old, double* S,
-                       unsigned long long* cnt, hipStream_t st) {
+                       unsigned long long* cnt, const float* xh, double* Q, hipStream_t st) {
   int64_t g = (m + 3) / 4;                 // 4 waves per 256-thread block
   if (g > 8192) g = 8192;
   hipLaunchKernelGGL((km_move_kernel<T, DP>), dim3((unsigned)g), dim3(256), 0, st,
-                     reinterpret_cast<const T*>(X), ldx, changed, m, a_new, a_old, S, cnt);
+                     reinterpret_cast<const T*>(X), ldx, changed, m, a_new, a_old, S, cnt, xh, Q);
   return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Bound-filtered Lloyd (Hamerly's centre-separation test, exact): u[i] >= |x_i - c_a|
+// for the centres of the last assignment; the centre of x_i moved by delta[a] since, so
+// u + delta[a] bounds the distance to the new centre; if that is below s[a] = half the
+// distance from c_a to its nearest other centre, c_a is still strictly the closest
+// (triangle inequality) and x_i is skipped (u := u + delta[a]); otherwise its row id is
+// appended to the active list and its assignment saved in a_prev.
+__global__ void __launch_bounds__(kDiffThreads)
+km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u,
+                 const float* __restrict__ delta, const float* __restrict__ s, int64_t n,
+                 int32_t* __restrict__ a_prev, int32_t* __restrict__ idx,
+                 unsigned long long* __restrict__ n_active, int64_t cap) {
+  __shared__ int32_t s_buf[kDiffBuf];
+  __shared__ int s_cnt;
+  __shared__ unsigned long long s_base;
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * per;
+  const int64_t hi = lo + per < n ? lo + per : n;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  auto flush = [&]() {
+    const int m = s_cnt;
+    if (m == 0) return;
+    if (threadIdx.x == 0) s_base = atomicAdd(n_active, (unsigned long long)m);
+    __syncthreads();
+    const int64_t b = (int64_t)s_base;
+    for (int j = threadIdx.x; j < m; j += kDiffThreads)
+      if (b + j < cap) idx[b + j] = s_buf[j];
+    __syncthreads();
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+  };
+  for (int64_t base = lo; base < hi; base += kDiffThreads) {
+    const int64_t i = base + threadIdx.x;
+    bool act = false;
+    if (i < hi) {
+      const int a = assign[i];
+      const float ub = u[i] + delta[a];
+      if (ub < s[a]) {
+        u[i] = ub;
+      } else {
+        act = true;
+        a_prev[i] = a;
+      }
+    }
+    const uint64_t mask = __ballot(act);
+    if (mask != 0) {
+      const int lane = __lane_id();
+      const int leader = __ffsll((long long)mask) - 1;
+      int b = 0;
+      if (lane == leader) b = atomicAdd(&s_cnt, __popcll(mask));
+      b = __shfl(b, leader);
+      if (act) {
+        const uint64_t below = lane == 0 ? 0ull : (mask & (~0ull >> (64 - lane)));
+        s_buf[b + __popcll(below)] = (int32_t)i;
+      }
+    }
+    __syncthreads();
+    if (s_cnt > kDiffBuf - kDiffThreads) flush();
+  }
+  flush();
+}
+
+// After K2 re-assigned the active rows: u = sqrt(dist + tol) (an upper bound of the
+// distance to the assigned centre, tol covering the kernel's key truncation) and the
+// rows whose cluster changed appended to `changed` (LDS-buffered, as km_diff).
+__global__ void __launch_bounds__(kDiffThreads)
+km_post_kernel(const int32_t* __restrict__ idx, int64_t m, const int32_t* __restrict__ assign,
+               const int32_t* __restrict__ a_prev, const float* __restrict__ mind, float tol,
+               float* __restrict__ u, int32_t* __restrict__ changed,
+               unsigned long long* __restrict__ n_changed, int64_t cap) {
+  __shared__ int32_t s_buf[kDiffBuf];
+  __shared__ int s_cnt;
+  __shared__ unsigned long long s_base;
+  const int64_t per = (m + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * per;
+  const int64_t hi = lo + per < m ? lo + per : m;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  auto flush = [&]() {
+    const int c = s_cnt;
+    if (c == 0) return;
+    if (threadIdx.x == 0) s_base = atomicAdd(n_changed, (unsigned long long)c);
+    __syncthreads();
+    const int64_t b = (int64_t)s_base;
+    for (int j = threadIdx.x; j < c; j += kDiffThreads)
+      if (b + j < cap) changed[b + j] = s_buf[j];
+    __syncthreads();
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+  };
+  for (int64_t base = lo; base < hi; base += kDiffThreads) {
+    const int64_t j = base + threadIdx.x;
+    bool ch = false;
+    int32_t row = 0;
+    if (j < hi) {
+      row = idx[j];
+      u[row] = sqrtf(fmaxf(mind[row], 0.f) + tol);
+      ch = assign[row] != a_prev[row];
+    }
+    const uint64_t mask = __ballot(ch);
+    if (mask != 0) {
+      const int lane = __lane_id();
+      const int leader = __ffsll((long long)mask) - 1;
+      int b = 0;
+      if (lane == leader) b = atomicAdd(&s_cnt, __popcll(mask));
+      b = __shfl(b, leader);
+      if (ch) {
+        const uint64_t below = lane == 0 ? 0ull : (mask & (~0ull >> (64 - lane)));
+        s_buf[b + __popcll(below)] = row;
+      }
+    }
+    __syncthreads();
+    if (s_cnt > kDiffBuf - kDiffThreads) flush();
+  }
+  flush();
+}
+
+// Q[c] = sum over rows assigned to c of |x|^2 = 2 xh (f64; LDS histogram per block,
+// k <= 2048, then one global add per cluster and block)
+__global__ void __launch_bounds__(256)
+km_qsum_kernel(const int32_t* __restrict__ assign, const float* __restrict__ xh, int64_t n, int k,
+               double* __restrict__ Q) {
+  __shared__ double s_q[2048];
+  for (int c = threadIdx.x; c < k; c += 256) s_q[c] = 0.0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    atomicAdd(&s_q[assign[i]], 2.0 * (double)xh[i]);
+  __syncthreads();
+  for (int c = threadIdx.x; c < k; c += 256)
+    if (s_q[c] != 0.0) atomicAdd(&Q[c], s_q[c]);
 }
 
 }  // namespace
@@ -137,19 +276,51 @@ hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, 
 
 hipError_t dalgo_km_move(const void* X, int is_bf16, int64_t ldx, int DP, const int32_t* changed,
                          int64_t m, const int32_t* a_new, const int32_t* a_old, double* S,
-                         unsigned long long* cnt, hipStream_t st) {
+                         unsigned long long* cnt, const float* xh, double* Q, hipStream_t st) {
   if (m <= 0) return hipSuccess;
   using namespace dalgo;
 #define DALGO_KM_MOVE(DPV)                                                                   \
   if (DP == DPV)                                                                             \
-    return is_bf16 ? launch_move<uint16_t, DPV>(X, ldx, changed, m, a_new, a_old, S, cnt, st) \
-                   : launch_move<float, DPV>(X, ldx, changed, m, a_new, a_old, S, cnt, st);
+    return is_bf16 ? launch_move<uint16_t, DPV>(X, ldx, changed, m, a_new, a_old, S, cnt, xh, Q, st) \
+                   : launch_move<float, DPV>(X, ldx, changed, m, a_new, a_old, S, cnt, xh, Q, st);
   DALGO_KM_MOVE(16)
   DALGO_KM_MOVE(32)
   DALGO_KM_MOVE(64)
   DALGO_KM_MOVE(128)
 #undef DALGO_KM_MOVE
   return hipErrorInvalidValue;
+}
+
+hipError_t dalgo_km_filter(const int32_t* assign, float* u, const float* delta, const float* s,
+                           int64_t n, int32_t* a_prev, int32_t* idx, unsigned long long* n_active,
+                           int64_t cap, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  int64_t g = (n + dalgo::kDiffThreads - 1) / dalgo::kDiffThreads;
+  if (g > 2048) g = 2048;
+  hipLaunchKernelGGL(dalgo::km_filter_kernel, dim3((unsigned)g), dim3(dalgo::kDiffThreads), 0, st,
+                     assign, u, delta, s, n, a_prev, idx, n_active, cap);
+  return hipGetLastError();
+}
+
+hipError_t dalgo_km_post(const int32_t* idx, int64_t m, const int32_t* assign, const int32_t* a_prev,
+                         const float* mind, float tol, float* u, int32_t* changed,
+                         unsigned long long* n_changed, int64_t cap, hipStream_t st) {
+  if (m <= 0) return hipSuccess;
+  int64_t g = (m + dalgo::kDiffThreads - 1) / dalgo::kDiffThreads;
+  if (g > 2048) g = 2048;
+  hipLaunchKernelGGL(dalgo::km_post_kernel, dim3((unsigned)g), dim3(dalgo::kDiffThreads), 0, st,
+                     idx, m, assign, a_prev, mind, tol, u, changed, n_changed, cap);
+  return hipGetLastError();
+}
+
+hipError_t dalgo_km_qsum(const int32_t* assign, const float* xh, int64_t n, int k, double* Q,
+                         hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (k > 2048) return hipErrorInvalidValue;
+  int64_t g = (n + 255) / 256;
+  if (g > 512) g = 512;
+  hipLaunchKernelGGL(dalgo::km_qsum_kernel, dim3((unsigned)g), dim3(256), 0, st, assign, xh, n, k, Q);
+  return hipGetLastError();
 }
 
 }  // extern "C"

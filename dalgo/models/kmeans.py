@@ -91,6 +91,15 @@ class KMeans:
         self.inc_max = float(os.environ.get("DALGO_KM_INC_MAX", "0.02"))
         self._S64 = None
         self.changed_history: list = []
+        # bound-filtered Lloyd (GPU, bf16, pipelined K2; DALGO_KM_BOUNDS=0 turns it off):
+        # exact -- a point is skipped only when the triangle inequality proves its centre
+        # is still the strictly closest one (see _step_bounds)
+        self.bounds = (self.dev.type == "cuda" and self.X.dtype == torch.bfloat16
+                       and self.DP in (64, 128) and self.pstats is None
+                       and K.assign_variant(self.X) == 52 and self.inc_max > 0
+                       and os.environ.get("DALGO_KM_BOUNDS", "1") != "0")
+        self._u = None
+        self.active_history: list = []
 
     def _ph(self, name: str):
         return self.timer.phase(name) if self.timer is not None else NULL_PHASE
@@ -106,11 +115,86 @@ class KMeans:
         comm.all_reduce_sum(C)
         return C
 
+    def _bounds_state(self):
+        n, k = self.X.shape[0], self.cfg.k
+        st = K.point_stats(self.X, keep_xh=True)
+        self._xh = st.xh
+        self._tol = 2.0 * st.M * 2.0 ** -14          # slack of a kernel distance
+        self._u = torch.empty(n, dtype=torch.float32, device=self.dev)
+        self._mind = torch.empty(n, dtype=torch.float32, device=self.dev)
+        self._a_prev = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)
+        self._idx = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)
+        self._changed = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)
+        self._n_active = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self._n_changed = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self._Q = torch.zeros(k, dtype=torch.float64, device=self.dev)
+        self._S64 = torch.empty(self.S.shape, dtype=torch.float64, device=self.dev)
+        self._cnt64 = torch.empty_like(self.cnt)
+        self._cq_prev = torch.empty((k, self.DP), dtype=self.cen.Cq.dtype, device=self.dev)
+
+    def _step_bounds(self):
+        """One Lloyd iteration with Hamerly's centre-separation filter (exact).
+
+        u[x] is an upper bound of |x - c_a| for the centres of the previous assignment;
+        the centre moved by delta[a] since, so if u + delta[a] < s[a] (half the distance
+        from c_a to its nearest other centre) c_a is still strictly the closest centre and
+        x keeps it without computing any distance. The other points go through K2 (row
+        indirection, variant 52) and the moved ones through the incremental K3. The SSE
+        comes from the identity sum_c (Q_c - 2 c.S_c + n_c |c|^2) with Q_c the per-cluster
+        sum of |x|^2, maintained with the sums."""
+        n, k, d = self.X.shape[0], self.cfg.k, self.d
+        if self._u is None:
+            if not hasattr(self, "_xh") or self._S64 is None:
+                self._bounds_state()
+            with self._ph("assign"):
+                K.assign(self.X, self.cen, out=self.assign, mind=self._mind)
+            with self._ph("accumulate"):
+                K.accumulate(self.X, self.assign, k, self.DP, self.S, self.cnt)
+                self._S64.copy_(self.S)
+                self._cnt64.copy_(self.cnt)
+                K.cluster_sq_sums(self.assign, self._xh, k, self._Q)
+            torch.sqrt(self._mind.clamp_min(0) + self._tol, out=self._u)
+            self.active_history.append(n)
+        else:
+            delta, s = K.centre_bounds(self.cen.Cq, self._cq_prev, k)
+            with self._ph("filter"):
+                m = K.filter_rows(self.assign, self._u, delta, s, self._a_prev, self._idx,
+                                  self._n_active)
+            self.active_history.append(m)
+            with self._ph("assign"):
+                K.assign_rows(self.X, self.cen, self._idx, m, self.assign, self._mind)
+            with self._ph("post"):
+                moved = K.post_rows(self._idx, m, self.assign, self._a_prev, self._mind,
+                                    self._tol, self._u, self._changed, self._n_changed)
+            self.changed_history.append(moved)
+            if moved <= self.inc_max * n:
+                with self._ph("accumulate_incremental"):
+                    K.move_rows(self.X, self.DP, self._changed, moved, self.assign, self._a_prev,
+                                self._S64, self._cnt64, self._xh, self._Q)
+                    self.S.copy_(self._S64)
+                    self.cnt.copy_(self._cnt64)
+            else:
+                with self._ph("accumulate"):
+                    K.accumulate(self.X, self.assign, k, self.DP, self.S, self.cnt)
+                    self._S64.copy_(self.S)
+                    self._cnt64.copy_(self.cnt)
+                    K.cluster_sq_sums(self.assign, self._xh, k, self._Q)
+        # local SSE on the (rounded) centres of this assignment
+        Cd = self.cen.Cq[:k, :d].double()
+        Sd = self._S64[:, :d]
+        sse = self._Q - 2.0 * (Cd * Sd).sum(dim=1) + self._cnt64.double() * (Cd * Cd).sum(dim=1)
+        self.sse.copy_(sse.sum().clamp_min(0).reshape(1))
+        self._cq_prev.copy_(self.cen.Cq[:k])
+
     def step(self):
         self.sse.zero_()
         self.S.zero_()
         self.cnt.zero_()
         self.shift2.zero_()
+        if self.bounds:
+            self._step_bounds()
+            self._reduce_and_update()
+            return
         inc = self._S64 is not None and self.inc_max > 0
         a_out = self._a_new if inc else self.assign
         with self._ph("assign"):
@@ -134,6 +218,9 @@ class KMeans:
             self._keep_local_sums()
         if a_out is not self.assign:
             self.assign, self._a_new = a_out, self.assign
+        self._reduce_and_update()
+
+    def _reduce_and_update(self):
         W = comm.world_size()
         if W > 1:
             with self._ph("allreduce"):
@@ -191,6 +278,7 @@ class KMeans:
 
     def load_state_dict(self, sd: dict):
         self._S64 = None          # the next iteration runs the full K3 pass
+        self._u = None            # ... and the full assignment (bounds rebuilt)
         self.t = int(sd["t"])
         self.cen.C.copy_(sd["centers"].to(self.dev))
         K.refresh(self.cen)

@@ -259,10 +259,57 @@ def changed_rows(a_new: torch.Tensor, a_old: torch.Tensor, changed: torch.Tensor
 
 
 def move_rows(X: torch.Tensor, DP: int, changed: torch.Tensor, m: int, a_new: torch.Tensor,
-              a_old: torch.Tensor, S64: torch.Tensor, cnt: torch.Tensor):
-    """Incremental K3: S64[a_new[r]] += x_r, S64[a_old[r]] -= x_r (f64), counts likewise,
-    for the m changed rows r."""
-    _ext.ops().kmeans_move(X, int(DP), changed, int(m), a_new, a_old, S64, cnt)
+              a_old: torch.Tensor, S64: torch.Tensor, cnt: torch.Tensor,
+              xh: torch.Tensor | None = None, Q: torch.Tensor | None = None):
+    """Incremental K3: S64[a_new[r]] += x_r, S64[a_old[r]] -= x_r (f64), counts likewise
+    (and Q, the per-cluster sum of |x|^2 = 2 xh, when given), for the m changed rows r."""
+    _ext.ops().kmeans_move(X, int(DP), changed, int(m), a_new, a_old, S64, cnt, xh, Q)
+
+
+# ------------------------------------------------------------------ bound-filtered Lloyd
+def centre_bounds(Cq_now: torch.Tensor, Cq_prev: torch.Tensor, k: int):
+    """(delta, s) for the bound filter, on the ROUNDED centres the assign kernel uses:
+    delta[c] = |c_now - c_prev| rounded up, s[c] = half the distance from c to its
+    nearest other centre rounded down (f64 then f32 with a relative margin)."""
+    a = Cq_now[:k].double()
+    b = Cq_prev[:k].double()
+    delta = (a - b).norm(dim=1) * (1 + 1e-6) + 1e-6
+    dd = torch.cdist(a, a)
+    dd.fill_diagonal_(float("inf"))
+    s = 0.5 * dd.min(dim=1).values * (1 - 1e-6)
+    if k == 1:
+        s = torch.full_like(s, float("inf"))
+    return delta.float(), s.float()
+
+
+def filter_rows(assign: torch.Tensor, u: torch.Tensor, delta: torch.Tensor, s: torch.Tensor,
+                a_prev: torch.Tensor, idx: torch.Tensor, n_active: torch.Tensor) -> int:
+    """Rows that may change cluster -> idx[:m] (their cluster -> a_prev); returns m."""
+    n_active.zero_()
+    _ext.ops().kmeans_filter(assign, u, delta, s, a_prev, idx, n_active)
+    return int(n_active.item())
+
+
+def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor, m: int, assign: torch.Tensor,
+                mind: torch.Tensor):
+    """K2 over the rows idx[:m] only (assign / mind written at those rows)."""
+    _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, mind)
+
+
+def post_rows(idx: torch.Tensor, m: int, assign: torch.Tensor, a_prev: torch.Tensor,
+              mind: torch.Tensor, tol: float, u: torch.Tensor, changed: torch.Tensor,
+              n_changed: torch.Tensor) -> int:
+    """u = sqrt(dist + tol) for the re-assigned rows; rows whose cluster changed ->
+    changed[:c]; returns c."""
+    n_changed.zero_()
+    _ext.ops().kmeans_post(idx, int(m), assign, a_prev, mind, float(tol), u, changed, n_changed)
+    return int(n_changed.item())
+
+
+def cluster_sq_sums(assign: torch.Tensor, xh: torch.Tensor, k: int, Q: torch.Tensor):
+    """Q[c] = sum of |x|^2 over the rows assigned to c (f64)."""
+    Q.zero_()
+    _ext.ops().kmeans_qsum(assign, xh, int(k), Q)
 
 
 def update(cen: Centers, S: torch.Tensor, cnt: torch.Tensor, shift2: torch.Tensor | None = None):

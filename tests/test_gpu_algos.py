@@ -677,3 +677,72 @@ def test_kmeans_model_centre_stationary_vs_pipelined(cuda, monkeypatch):
     assert np.allclose(a.history.sse, b.history.sse, rtol=1e-4)
     same = (a.centers - b.centers).abs().amax(dim=1) < 1e-2
     assert same.float().mean().item() > 0.9   # boundary clusters drift (chaotic near-ties)
+
+
+def test_kmeans_assign_rows_indirect(cuda):
+    """K2 with row indirection (only the listed rows) == the full K2 on those rows, and
+    leaves every other row's assignment untouched."""
+    torch.manual_seed(5)
+    n, d, k = 50_000, 128, 1000
+    X = K.prepare_points((torch.randn(n, d) * 3).to(torch.bfloat16).to(cuda))
+    cen = K.make_centers(torch.randn(k, d) * 3, torch.bfloat16, cuda)
+    full = K.assign(X, cen)
+    rows = torch.randperm(n, device=cuda)[: n // 3].to(torch.int32)
+    a = torch.full((n,), -7, dtype=torch.int32, device=cuda)
+    mind = torch.zeros(n, device=cuda)
+    K.assign_rows(X, cen, rows, rows.numel(), a, mind)
+    sel = torch.zeros(n, dtype=torch.bool, device=cuda)
+    sel[rows.long()] = True
+    assert torch.equal(a[sel], full[sel])
+    assert bool((a[~sel] == -7).all()) and bool((mind[sel] > 0).all())
+
+
+def test_kmeans_filter_and_post_match_torch(cuda):
+    from dalgo.ops import kmeans as K
+    torch.manual_seed(6)
+    n, k = 100_003, 50
+    assign = torch.randint(0, k, (n,), dtype=torch.int32, device=cuda)
+    u = torch.rand(n, device=cuda) * 10
+    delta = torch.rand(k, device=cuda)
+    s = torch.rand(k, device=cuda) * 12
+    u0 = u.clone()
+    a_prev = torch.full((n,), -1, dtype=torch.int32, device=cuda)
+    idx = torch.empty(n, dtype=torch.int32, device=cuda)
+    cnt = torch.zeros(1, dtype=torch.int64, device=cuda)
+    m = K.filter_rows(assign, u, delta, s, a_prev, idx, cnt)
+    ub = u0 + delta[assign.long()]
+    act = ~(ub < s[assign.long()])
+    assert m == int(act.sum())
+    assert torch.equal(torch.sort(idx[:m]).values.long(), torch.nonzero(act)[:, 0])
+    assert torch.allclose(u[~act], ub[~act]) and torch.equal(u[act], u0[act])
+    assert torch.equal(a_prev[act], assign[act])
+    # post: half of the active rows change cluster
+    new = assign.clone()
+    ch = act & (torch.arange(n, device=cuda) % 2 == 0)
+    new[ch] = (new[ch] + 1) % k
+    mind = torch.rand(n, device=cuda) * 4
+    changed = torch.empty(n, dtype=torch.int32, device=cuda)
+    c = K.post_rows(idx, m, new, a_prev, mind, 0.5, u, changed, cnt)
+    assert c == int(ch.sum())
+    assert torch.equal(torch.sort(changed[:c]).values.long(), torch.nonzero(ch)[:, 0])
+    assert torch.allclose(u[act], torch.sqrt(mind[act] + 0.5))
+
+
+def test_kmeans_bound_filter_exact(cuda):
+    """Bound-filtered Lloyd (default for bf16 on the GPU) == plain Lloyd: same SSE
+    trajectory (SSE via the Q identity vs the kernel's per-point sum), same counts; and
+    the filter actually skips most points once the centres settle."""
+    from dalgo.data.synthetic import blobs
+    from dalgo.models.kmeans import KMeans, KMeansConfig
+    n, d, k = 300_000, 128, 1000
+    X = blobs(n, d, k, device=cuda, dtype=torch.bfloat16, seed=11)
+    a = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5), X, 0, n)
+    assert a.bounds
+    a.fit()
+    b = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5), X, 0, n)
+    b.bounds = False
+    b.fit()
+    assert np.allclose(a.history.sse, b.history.sse, rtol=2e-4), (a.history.sse, b.history.sse)
+    same = (a.centers - b.centers).abs().amax(dim=1) < 1e-2
+    assert same.float().mean().item() > 0.9
+    assert a.active_history[0] == n and min(a.active_history[1:]) < 0.7 * n
