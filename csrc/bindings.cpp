@@ -556,11 +556,14 @@ void kmeans_move(const Tensor& X, int64_t DP, const Tensor& changed, int64_t m,
 }
 
 // bound-filtered Lloyd: active rows (u + delta[a] >= s[a]) -> idx, their assignment -> a_prev
-void kmeans_filter(const Tensor& assign, Tensor u, const Tensor& delta, const Tensor& s,
-                   Tensor a_prev, Tensor idx, Tensor n_active) {
+void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta, const Tensor& s,
+                   const Tensor& maxd, Tensor a_prev, Tensor idx, Tensor n_active) {
   const int64_t n = assign.numel();
   check_i32(assign, "assign");
   check_f32(u, "u");
+  check_f32(l, "l");
+  check_f32(maxd, "maxd");
+  TORCH_CHECK(l.numel() >= n && maxd.numel() >= 1, "kmeans_filter: l [n], maxd [1]");
   check_f32(delta, "delta");
   check_f32(s, "s");
   check_i32(a_prev, "a_prev");
@@ -569,15 +572,19 @@ void kmeans_filter(const Tensor& assign, Tensor u, const Tensor& delta, const Te
   TORCH_CHECK(delta.numel() == s.numel(), "delta / s [k]");
   TORCH_CHECK(n_active.scalar_type() == at::kLong && n_active.numel() >= 1, "n_active int64[1]");
   DeviceGuard guard(assign.device());
-  DALGO_CHECK_HIP(dalgo_km_filter(assign.data_ptr<int32_t>(), u.data_ptr<float>(), delta.data_ptr<float>(),
-                                  s.data_ptr<float>(), n, a_prev.data_ptr<int32_t>(), idx.data_ptr<int32_t>(),
+  DALGO_CHECK_HIP(dalgo_km_filter(assign.data_ptr<int32_t>(), u.data_ptr<float>(), l.data_ptr<float>(),
+                                  delta.data_ptr<float>(), s.data_ptr<float>(), maxd.data_ptr<float>(), n,
+                                  a_prev.data_ptr<int32_t>(), idx.data_ptr<int32_t>(),
                                   reinterpret_cast<unsigned long long*>(n_active.data_ptr<int64_t>()),
                                   idx.numel(), cur_stream()),
                   "kmeans_filter");
 }
 
 void kmeans_post(const Tensor& idx, int64_t m, const Tensor& assign, const Tensor& a_prev,
-                 const Tensor& mind, double tol, Tensor u, Tensor changed, Tensor n_changed) {
+                 const Tensor& mind, const Tensor& mind2, double tol, Tensor u, Tensor l,
+                 Tensor changed, Tensor n_changed) {
+  check_f32(mind2, "mind2");
+  check_f32(l, "l");
   check_i32(idx, "idx");
   check_i32(assign, "assign");
   check_i32(a_prev, "a_prev");
@@ -588,8 +595,9 @@ void kmeans_post(const Tensor& idx, int64_t m, const Tensor& assign, const Tenso
   TORCH_CHECK(n_changed.scalar_type() == at::kLong && n_changed.numel() >= 1, "n_changed int64[1]");
   DeviceGuard guard(idx.device());
   DALGO_CHECK_HIP(dalgo_km_post(idx.data_ptr<int32_t>(), m, assign.data_ptr<int32_t>(),
-                                a_prev.data_ptr<int32_t>(), mind.data_ptr<float>(), (float)tol,
-                                u.data_ptr<float>(), changed.data_ptr<int32_t>(),
+                                a_prev.data_ptr<int32_t>(), mind.data_ptr<float>(),
+                                mind2.data_ptr<float>(), (float)tol, u.data_ptr<float>(),
+                                l.data_ptr<float>(), changed.data_ptr<int32_t>(),
                                 reinterpret_cast<unsigned long long*>(n_changed.data_ptr<int64_t>()),
                                 changed.numel(), cur_stream()),
                   "kmeans_post");
@@ -608,8 +616,9 @@ void kmeans_qsum(const Tensor& assign, const Tensor& xh, int64_t k, Tensor Q) {
 }
 
 // K2 (variant 52) over the rows idx[0, m) only
-void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn, const Tensor& idx,
-                       int64_t m, Tensor assign, Tensor mind) {
+void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
+                       const std::optional<Tensor>& idx, int64_t m, Tensor assign, Tensor mind,
+                       const std::optional<Tensor>& mind2) {
   TORCH_CHECK(Cq.dim() == 2 && Cq.is_contiguous() && Cq.scalar_type() == at::kBFloat16, "Cq bf16");
   const int DP = (int)Cq.size(1);
   TORCH_CHECK(DP == 64 || DP == 128, "kmeans_assign_idx: DP 64 or 128");
@@ -618,16 +627,28 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn, cons
   const int64_t kpad = Cq.size(0);
   TORCH_CHECK(kpad % 128 == 0, "kmeans_assign_idx: kpad % 128");
   check_f32(hn, "hn");
-  check_i32(idx, "idx");
-  TORCH_CHECK(m >= 0 && m <= idx.numel(), "kmeans_assign_idx: m");
+  const int32_t* ip = nullptr;
+  if (idx.has_value()) {
+    check_i32(*idx, "idx");
+    TORCH_CHECK(m >= 0 && m <= idx->numel(), "kmeans_assign_idx: m");
+    ip = idx->data_ptr<int32_t>();
+  } else {
+    TORCH_CHECK(m >= 0 && m <= X.size(0), "kmeans_assign_idx: m <= n");
+  }
   check_i32(assign, "assign");
   check_f32(mind, "mind");
   TORCH_CHECK(assign.numel() >= X.size(0) && mind.numel() >= X.size(0), "assign / mind [n]");
+  float* m2 = nullptr;
+  if (mind2.has_value()) {
+    check_f32(*mind2, "mind2");
+    TORCH_CHECK(mind2->numel() >= X.size(0), "mind2 [n]");
+    m2 = mind2->data_ptr<float>();
+  }
   DeviceGuard guard(X.device());
   DALGO_CHECK_HIP(dalgo_kmeans_assign_idx(X.data_ptr(), m, X.stride(0), DP, Cq.data_ptr(),
-                                          hn.data_ptr<float>(), (int)kpad, idx.data_ptr<int32_t>(),
-                                          assign.data_ptr<int>(), mind.data_ptr<float>(), nullptr, 0,
-                                          cur_stream()),
+                                          hn.data_ptr<float>(), (int)kpad, ip,
+                                          assign.data_ptr<int>(), mind.data_ptr<float>(), m2,
+                                          nullptr, 0, cur_stream()),
                   "kmeans_assign_idx");
 }
 
@@ -1096,13 +1117,13 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("kmeans_diff(Tensor a_new, Tensor a_old, Tensor(a!) changed, Tensor(b!) n_changed) -> ()");
   m.def("kmeans_move(Tensor X, int DP, Tensor changed, int m, Tensor a_new, Tensor a_old, "
         "Tensor(a!) S64, Tensor(b!) cnt, Tensor? xh=None, Tensor(c!)? Q=None) -> ()");
-  m.def("kmeans_filter(Tensor assign, Tensor(a!) u, Tensor delta, Tensor s, Tensor(b!) a_prev, "
-        "Tensor(c!) idx, Tensor(d!) n_active) -> ()");
-  m.def("kmeans_post(Tensor idx, int m, Tensor assign, Tensor a_prev, Tensor mind, float tol, "
-        "Tensor(a!) u, Tensor(b!) changed, Tensor(c!) n_changed) -> ()");
+  m.def("kmeans_filter(Tensor assign, Tensor(a!) u, Tensor(e!) l, Tensor delta, Tensor s, Tensor maxd, "
+        "Tensor(b!) a_prev, Tensor(c!) idx, Tensor(d!) n_active) -> ()");
+  m.def("kmeans_post(Tensor idx, int m, Tensor assign, Tensor a_prev, Tensor mind, Tensor mind2, "
+        "float tol, Tensor(a!) u, Tensor(d!) l, Tensor(b!) changed, Tensor(c!) n_changed) -> ()");
   m.def("kmeans_qsum(Tensor assign, Tensor xh, int k, Tensor(a!) Q) -> ()");
-  m.def("kmeans_assign_idx(Tensor X, Tensor Cq, Tensor hn, Tensor idx, int m, Tensor(a!) assign, "
-        "Tensor(b!) mind) -> ()");
+  m.def("kmeans_assign_idx(Tensor X, Tensor Cq, Tensor hn, Tensor? idx, int m, Tensor(a!) assign, "
+        "Tensor(b!) mind, Tensor(c!)? mind2=None) -> ()");
   m.def("kmeans_update(Tensor(a!) C, Tensor S, Tensor cnt, Tensor(b!) Cq, Tensor(c!) hn, "
         "Tensor(d!)? shift2) -> ()");
   m.def("rmat_edges(int seed, int scale, int e_off, float a, float b, float c, bool scramble, "

@@ -479,13 +479,16 @@ typedef __attribute__((address_space(3))) void km_lds_void;
 // DIAG (diagnostics only, wrong assignments): 1 = argmin VALU replaced by one min per
 // tile, 2 = MFMAs removed (accumulator = C input, A fragments folded by XOR), 3 = 2
 // without the C-init LDS reads, 4 = 3 without the A-fragment LDS reads
-template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, int SWP = 0, int DIAG = 0>
+// TOP2 (bound-filtered Lloyd): also keep each point's second-smallest key and write the
+// second-best distance (a lower bound: keys are truncated downwards) to mind2.
+template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, int SWP = 0, int DIAG = 0,
+          bool TOP2 = false>
 __global__ void __launch_bounds__(NW * 64, MINB)
 kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
                           const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int kpad,
                           int* __restrict__ assign, float* __restrict__ mind,
                           double* __restrict__ sse, int sse_mask,
-                          const int32_t* __restrict__ idx) {
+                          const int32_t* __restrict__ idx, float* __restrict__ mind2) {
   // idx (optional): the block's point j is row idx[j] of X (and of assign / mind), j < n
   // -- the bound-filtered form of Lloyd only re-assigns the points the filter keeps
   constexpr int KS = DP / 16;                  // 32x32x16 k-steps per centre row
@@ -572,9 +575,9 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     }
   };
 
-  int bkey[PT], bsub[PT];
+  int bkey[PT], bsub[PT], bkey2[PT];
 #pragma unroll
-  for (int t = 0; t < PT; ++t) { bkey[t] = 0x7fffffff; bsub[t] = 0; }
+  for (int t = 0; t < PT; ++t) { bkey[t] = 0x7fffffff; bsub[t] = 0; bkey2[t] = 0x7fffffff; }
   int kmask;   // key mask in a VGPR so each pack is ONE v_and_or_b32 (VGPR mask, inline r)
   asm volatile("v_mov_b32 %0, 0xffffffe0" : "=v"(kmask));
 
@@ -621,11 +624,24 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       return;
     }
     int m = 0x7fffffff;
+    if constexpr (TOP2) {
+      int m2 = 0x7fffffff;
 #pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      const int k0 = (__float_as_int(acc[r]) & kmask) | r;
-      const int k1 = (__float_as_int(acc[r + 1]) & kmask) | (r + 1);
-      m = min(min(m, k0), k1);   // one v_min3_i32 per pair
+      for (int r = 0; r < 16; ++r) {
+        const int kk = (__float_as_int(acc[r]) & kmask) | r;
+        // second smallest of {m, m2, kk} (m <= m2): the median
+        asm volatile("v_med3_i32 %0, %1, %2, %3" : "=v"(m2) : "v"(m), "v"(m2), "v"(kk));
+        m = min(m, kk);
+      }
+      // merge with the running pair (bkey <= bkey2): second smallest of the four
+      bkey2[t] = min(max(bkey[t], m), min(bkey2[t], m2));
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const int k0 = (__float_as_int(acc[r]) & kmask) | r;
+        const int k1 = (__float_as_int(acc[r + 1]) & kmask) | (r + 1);
+        m = min(min(m, k0), k1);   // one v_min3_i32 per pair
+      }
     }
     // strict: an equal key of a later sub-tile (higher ids) never displaces
     const bool take = m < bkey[t];
@@ -733,6 +749,14 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     float bv = v;
     int bi = mi;
     if (pv < bv || (pv == bv && pi < bi)) { bv = pv; bi = pi; }
+    float bv2 = 0.f;
+    if constexpr (TOP2) {
+      // second best over both halves: second smallest of {v, v2, pv, pv2}
+      const float v2 = __int_as_float(bkey2[t] & ~31);
+      auto s2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v2), __float_as_uint(v2), false, false);
+      const float pv2 = __uint_as_float(h ? s2[0] : s2[1]);
+      bv2 = fminf(fmaxf(v, pv), fminf(v2, pv2));
+    }
     const int64_t p = pbase + t * 32 + cl;
     if (h == 0 && p < n) {
       // acc = 0.5|x-c|^2 + M - 0.5|x|^2
@@ -740,6 +764,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       const int64_t row = idx ? (int64_t)idx[p] : p;
       assign[row] = bi;
       if (mind) mind[row] = dist;
+      if constexpr (TOP2) mind2[row] = fmaxf(2.f * (bv2 - M) + x2[t], 0.f);
       my_sse += (double)dist;
     }
   }
@@ -1158,11 +1183,12 @@ static hipError_t launch_assign_res(const void* X, int64_t n, int64_t ldx, const
 }
 
 // pipelined K2 (bf16, DP >= 64): grid = one PT-tile group per wave, MINB blocks per CU
-template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, int SWP = 0, int DIAG = 0>
+template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, int SWP = 0, int DIAG = 0,
+          bool TOP2 = false>
 static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                      const float* hn, int kpad, int* assign, float* mind,
                                      double* sse, int sse_mask, hipStream_t st,
-                                     const int32_t* idx = nullptr) {
+                                     const int32_t* idx = nullptr, float* mind2 = nullptr) {
   constexpr int CH = 32 * NSUB;
   constexpr size_t kStatic = NBUF * (size_t)CH * DP * 2;
   if (kpad % CH) return hipErrorInvalidValue;
@@ -1171,7 +1197,7 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
   const int64_t grid = cdiv(n, (int64_t)NW * PT * 32);
   if (grid == 0) return hipSuccess;
   if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
-  auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF, SWP, DIAG>;
+  auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF, SWP, DIAG, TOP2>;
   static size_t attr_set = 0;   // largest dynamic size this instantiation was enabled for
   if (dyn > attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1180,7 +1206,7 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
     attr_set = dyn;
   }
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(NW * 64), dyn, st, (const uint16_t*)X, n, ldx,
-                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse, sse_mask, idx);
+                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse, sse_mask, idx, mind2);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -1397,11 +1423,23 @@ hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ld
 }
 
 // K2 (variant 52) over the rows idx[0, m) of X only (bound-filtered Lloyd iteration)
+// idx may be null (all m rows); mind2 non-null selects the top-2 form (second-best
+// distance per row, a lower bound for the bound filter)
 hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP, const void* Cq,
                                    const float* hn, int kpad, const int32_t* idx, int* assign,
-                                   float* mind, double* sse, int sse_mask, hipStream_t st) {
+                                   float* mind, float* mind2, double* sse, int sse_mask,
+                                   hipStream_t st) {
   if (m <= 0) return hipSuccess;
   if (kpad % 128 != 0) return hipErrorInvalidValue;
+  if (mind2 != nullptr) {
+    if (DP == 128)
+      return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, 2, 0, true>(X, m, ldx, Cq, hn, kpad, assign,
+                                                                      mind, sse, sse_mask, st, idx, mind2);
+    if (DP == 64)
+      return launch_assign_pipe<64, 4, 2, 4, 2, 2, false, 2, 0, true>(X, m, ldx, Cq, hn, kpad, assign,
+                                                                     mind, sse, sse_mask, st, idx, mind2);
+    return hipErrorInvalidValue;
+  }
   if (DP == 128)
     return launch_assign_pipe<128, 4, 3, 4, 2, 2, true, 2>(X, m, ldx, Cq, hn, kpad, assign, mind, sse,
                                                            sse_mask, st, idx);

@@ -127,15 +127,18 @@ hipError_t launch_move(const void* X, int64_t ldx, const int32_t* changed, int64
 }
 
 // ---------------------------------------------------------------------------
-// Bound-filtered Lloyd (Hamerly's centre-separation test, exact): u[i] >= |x_i - c_a|
-// for the centres of the last assignment; the centre of x_i moved by delta[a] since, so
-// u + delta[a] bounds the distance to the new centre; if that is below s[a] = half the
-// distance from c_a to its nearest other centre, c_a is still strictly the closest
-// (triangle inequality) and x_i is skipped (u := u + delta[a]); otherwise its row id is
-// appended to the active list and its assignment saved in a_prev.
+// Bound-filtered Lloyd (Hamerly, exact): u[i] >= |x_i - c_a| and l[i] <= min over the
+// other centres of |x_i - c| for the centres of the last assignment. The centre of x_i
+// moved by delta[a] since and no centre moved more than maxd, so u + delta[a] bounds
+// the distance to its centre from above and l - maxd every other distance from below;
+// if u + delta[a] < max(s[a], l - maxd) (s[a] = half the distance from c_a to its
+// nearest other centre) c_a is still strictly the closest centre (triangle inequality)
+// and x_i is skipped (u, l updated); otherwise its row id is appended to the active
+// list and its assignment saved in a_prev.
 __global__ void __launch_bounds__(kDiffThreads)
-km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u,
-                 const float* __restrict__ delta, const float* __restrict__ s, int64_t n,
+km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, float* __restrict__ l,
+                 const float* __restrict__ delta, const float* __restrict__ s,
+                 const float* __restrict__ maxd, int64_t n,
                  int32_t* __restrict__ a_prev, int32_t* __restrict__ idx,
                  unsigned long long* __restrict__ n_active, int64_t cap) {
   __shared__ int32_t s_buf[kDiffBuf];
@@ -146,6 +149,7 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u,
   const int64_t hi = lo + per < n ? lo + per : n;
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
+  const float md = maxd[0];
   auto flush = [&]() {
     const int m = s_cnt;
     if (m == 0) return;
@@ -164,8 +168,10 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u,
     if (i < hi) {
       const int a = assign[i];
       const float ub = u[i] + delta[a];
-      if (ub < s[a]) {
+      const float lb = l[i] - md;
+      if (ub < fmaxf(s[a], lb)) {
         u[i] = ub;
+        l[i] = lb;
       } else {
         act = true;
         a_prev[i] = a;
@@ -194,8 +200,9 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u,
 // rows whose cluster changed appended to `changed` (LDS-buffered, as km_diff).
 __global__ void __launch_bounds__(kDiffThreads)
 km_post_kernel(const int32_t* __restrict__ idx, int64_t m, const int32_t* __restrict__ assign,
-               const int32_t* __restrict__ a_prev, const float* __restrict__ mind, float tol,
-               float* __restrict__ u, int32_t* __restrict__ changed,
+               const int32_t* __restrict__ a_prev, const float* __restrict__ mind,
+               const float* __restrict__ mind2, float tol, float* __restrict__ u,
+               float* __restrict__ l, int32_t* __restrict__ changed,
                unsigned long long* __restrict__ n_changed, int64_t cap) {
   __shared__ int32_t s_buf[kDiffBuf];
   __shared__ int s_cnt;
@@ -224,6 +231,7 @@ km_post_kernel(const int32_t* __restrict__ idx, int64_t m, const int32_t* __rest
     if (j < hi) {
       row = idx[j];
       u[row] = sqrtf(fmaxf(mind[row], 0.f) + tol);
+      l[row] = sqrtf(fmaxf(mind2[row] - tol, 0.f));
       ch = assign[row] != a_prev[row];
     }
     const uint64_t mask = __ballot(ch);
@@ -291,25 +299,26 @@ hipError_t dalgo_km_move(const void* X, int is_bf16, int64_t ldx, int DP, const 
   return hipErrorInvalidValue;
 }
 
-hipError_t dalgo_km_filter(const int32_t* assign, float* u, const float* delta, const float* s,
-                           int64_t n, int32_t* a_prev, int32_t* idx, unsigned long long* n_active,
-                           int64_t cap, hipStream_t st) {
+hipError_t dalgo_km_filter(const int32_t* assign, float* u, float* l, const float* delta,
+                           const float* s, const float* maxd, int64_t n, int32_t* a_prev,
+                           int32_t* idx, unsigned long long* n_active, int64_t cap, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   int64_t g = (n + dalgo::kDiffThreads - 1) / dalgo::kDiffThreads;
   if (g > 2048) g = 2048;
   hipLaunchKernelGGL(dalgo::km_filter_kernel, dim3((unsigned)g), dim3(dalgo::kDiffThreads), 0, st,
-                     assign, u, delta, s, n, a_prev, idx, n_active, cap);
+                     assign, u, l, delta, s, maxd, n, a_prev, idx, n_active, cap);
   return hipGetLastError();
 }
 
 hipError_t dalgo_km_post(const int32_t* idx, int64_t m, const int32_t* assign, const int32_t* a_prev,
-                         const float* mind, float tol, float* u, int32_t* changed,
-                         unsigned long long* n_changed, int64_t cap, hipStream_t st) {
+                         const float* mind, const float* mind2, float tol, float* u, float* l,
+                         int32_t* changed, unsigned long long* n_changed, int64_t cap,
+                         hipStream_t st) {
   if (m <= 0) return hipSuccess;
   int64_t g = (m + dalgo::kDiffThreads - 1) / dalgo::kDiffThreads;
   if (g > 2048) g = 2048;
   hipLaunchKernelGGL(dalgo::km_post_kernel, dim3((unsigned)g), dim3(dalgo::kDiffThreads), 0, st,
-                     idx, m, assign, a_prev, mind, tol, u, changed, n_changed, cap);
+                     idx, m, assign, a_prev, mind, mind2, tol, u, l, changed, n_changed, cap);
   return hipGetLastError();
 }
 

@@ -114,17 +114,19 @@ hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, 
 hipError_t dalgo_km_move(const void* X, int is_bf16, int64_t ldx, int DP, const int32_t* changed,
                          int64_t m, const int32_t* a_new, const int32_t* a_old, double* S,
                          unsigned long long* cnt, const float* xh, double* Q, hipStream_t st);
-hipError_t dalgo_km_filter(const int32_t* assign, float* u, const float* delta, const float* s,
-                           int64_t n, int32_t* a_prev, int32_t* idx, unsigned long long* n_active,
-                           int64_t cap, hipStream_t st);
+hipError_t dalgo_km_filter(const int32_t* assign, float* u, float* l, const float* delta,
+                           const float* s, const float* maxd, int64_t n, int32_t* a_prev,
+                           int32_t* idx, unsigned long long* n_active, int64_t cap, hipStream_t st);
 hipError_t dalgo_km_post(const int32_t* idx, int64_t m, const int32_t* assign, const int32_t* a_prev,
-                         const float* mind, float tol, float* u, int32_t* changed,
-                         unsigned long long* n_changed, int64_t cap, hipStream_t st);
+                         const float* mind, const float* mind2, float tol, float* u, float* l,
+                         int32_t* changed, unsigned long long* n_changed, int64_t cap,
+                         hipStream_t st);
 hipError_t dalgo_km_qsum(const int32_t* assign, const float* xh, int64_t n, int k, double* Q,
                          hipStream_t st);
 hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP, const void* Cq,
                                    const float* hn, int kpad, const int32_t* idx, int* assign,
-                                   float* mind, double* sse, int sse_mask, hipStream_t st);
+                                   float* mind, float* mind2, double* sse, int sse_mask,
+                                   hipStream_t st);
 
 // ---- K9 sparse closure round on a device hash set (tc_sparse.hip)
 hipError_t dalgo_tcs_degree(const uint64_t* keys, int64_t d0, int64_t nd, const int64_t* in_ptr,

@@ -121,7 +121,9 @@ class KMeans:
         self._xh = st.xh
         self._tol = 2.0 * st.M * 2.0 ** -14          # slack of a kernel distance
         self._u = torch.empty(n, dtype=torch.float32, device=self.dev)
+        self._l = torch.empty(n, dtype=torch.float32, device=self.dev)
         self._mind = torch.empty(n, dtype=torch.float32, device=self.dev)
+        self._mind2 = torch.empty(n, dtype=torch.float32, device=self.dev)
         self._a_prev = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)
         self._idx = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)
         self._changed = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)
@@ -131,41 +133,50 @@ class KMeans:
         self._S64 = torch.empty(self.S.shape, dtype=torch.float64, device=self.dev)
         self._cnt64 = torch.empty_like(self.cnt)
         self._cq_prev = torch.empty((k, self.DP), dtype=self.cen.Cq.dtype, device=self.dev)
+        # first use of the f64 cdist / reductions loads their library kernels (~0.2 s):
+        # pay it here, in the full first pass, not in the first filtered iteration
+        K.centre_bounds(self.cen.Cq, self.cen.Cq, k)
 
     def _step_bounds(self):
-        """One Lloyd iteration with Hamerly's centre-separation filter (exact).
+        """One Lloyd iteration with Hamerly's bounds (exact).
 
-        u[x] is an upper bound of |x - c_a| for the centres of the previous assignment;
-        the centre moved by delta[a] since, so if u + delta[a] < s[a] (half the distance
-        from c_a to its nearest other centre) c_a is still strictly the closest centre and
-        x keeps it without computing any distance. The other points go through K2 (row
-        indirection, variant 52) and the moved ones through the incremental K3. The SSE
-        comes from the identity sum_c (Q_c - 2 c.S_c + n_c |c|^2) with Q_c the per-cluster
-        sum of |x|^2, maintained with the sums."""
+        u[x] >= |x - c_a| and l[x] <= |x - c| for every other centre c, both for the
+        centres of the previous assignment (K2 writes the best and the second-best
+        distance). Centre a moved by delta[a] since and no centre by more than maxd, so
+        if u + delta[a] < max(s[a], l - maxd) (s[a] = half the distance from c_a to its
+        nearest other centre) c_a is still strictly the closest centre and x keeps it
+        without computing any distance (Hamerly, "Making k-means even faster", 2010).
+        The other points go through K2 (row indirection, variant 52, top-2 epilogue) and
+        the moved ones through the incremental K3. The SSE comes from the identity
+        sum_c (Q_c - 2 c.S_c + n_c |c|^2) with Q_c the per-cluster sum of |x|^2,
+        maintained with the sums."""
         n, k, d = self.X.shape[0], self.cfg.k, self.d
         if self._u is None:
             if not hasattr(self, "_xh") or self._S64 is None:
                 self._bounds_state()
             with self._ph("assign"):
-                K.assign(self.X, self.cen, out=self.assign, mind=self._mind)
+                K.assign_rows(self.X, self.cen, None, n, self.assign, self._mind, self._mind2)
             with self._ph("accumulate"):
                 K.accumulate(self.X, self.assign, k, self.DP, self.S, self.cnt)
                 self._S64.copy_(self.S)
                 self._cnt64.copy_(self.cnt)
                 K.cluster_sq_sums(self.assign, self._xh, k, self._Q)
             torch.sqrt(self._mind.clamp_min(0) + self._tol, out=self._u)
+            torch.sqrt((self._mind2 - self._tol).clamp_min(0), out=self._l)
             self.active_history.append(n)
         else:
             delta, s = K.centre_bounds(self.cen.Cq, self._cq_prev, k)
+            maxd = delta.max().reshape(1)
             with self._ph("filter"):
-                m = K.filter_rows(self.assign, self._u, delta, s, self._a_prev, self._idx,
-                                  self._n_active)
+                m = K.filter_rows(self.assign, self._u, self._l, delta, s, maxd, self._a_prev,
+                                  self._idx, self._n_active)
             self.active_history.append(m)
             with self._ph("assign"):
-                K.assign_rows(self.X, self.cen, self._idx, m, self.assign, self._mind)
+                K.assign_rows(self.X, self.cen, self._idx, m, self.assign, self._mind, self._mind2)
             with self._ph("post"):
                 moved = K.post_rows(self._idx, m, self.assign, self._a_prev, self._mind,
-                                    self._tol, self._u, self._changed, self._n_changed)
+                                    self._mind2, self._tol, self._u, self._l, self._changed,
+                                    self._n_changed)
             self.changed_history.append(moved)
             if moved <= self.inc_max * n:
                 with self._ph("accumulate_incremental"):

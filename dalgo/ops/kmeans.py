@@ -282,27 +282,30 @@ def centre_bounds(Cq_now: torch.Tensor, Cq_prev: torch.Tensor, k: int):
     return delta.float(), s.float()
 
 
-def filter_rows(assign: torch.Tensor, u: torch.Tensor, delta: torch.Tensor, s: torch.Tensor,
-                a_prev: torch.Tensor, idx: torch.Tensor, n_active: torch.Tensor) -> int:
+def filter_rows(assign: torch.Tensor, u: torch.Tensor, l: torch.Tensor, delta: torch.Tensor,
+                s: torch.Tensor, maxd: torch.Tensor, a_prev: torch.Tensor, idx: torch.Tensor,
+                n_active: torch.Tensor) -> int:
     """Rows that may change cluster -> idx[:m] (their cluster -> a_prev); returns m."""
     n_active.zero_()
-    _ext.ops().kmeans_filter(assign, u, delta, s, a_prev, idx, n_active)
+    _ext.ops().kmeans_filter(assign, u, l, delta, s, maxd, a_prev, idx, n_active)
     return int(n_active.item())
 
 
-def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor, m: int, assign: torch.Tensor,
-                mind: torch.Tensor):
-    """K2 over the rows idx[:m] only (assign / mind written at those rows)."""
-    _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, mind)
+def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
+                assign: torch.Tensor, mind: torch.Tensor, mind2: torch.Tensor | None = None):
+    """K2 (variant 52) over the rows idx[:m] (all rows when idx is None); assign / mind
+    (and the second-best distance mind2, a lower bound, when given) written at those rows."""
+    _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, mind, mind2)
 
 
 def post_rows(idx: torch.Tensor, m: int, assign: torch.Tensor, a_prev: torch.Tensor,
-              mind: torch.Tensor, tol: float, u: torch.Tensor, changed: torch.Tensor,
-              n_changed: torch.Tensor) -> int:
-    """u = sqrt(dist + tol) for the re-assigned rows; rows whose cluster changed ->
-    changed[:c]; returns c."""
+              mind: torch.Tensor, mind2: torch.Tensor, tol: float, u: torch.Tensor,
+              l: torch.Tensor, changed: torch.Tensor, n_changed: torch.Tensor) -> int:
+    """u = sqrt(dist + tol), l = sqrt(dist2 - tol) for the re-assigned rows; rows whose
+    cluster changed -> changed[:c]; returns c."""
     n_changed.zero_()
-    _ext.ops().kmeans_post(idx, int(m), assign, a_prev, mind, float(tol), u, changed, n_changed)
+    _ext.ops().kmeans_post(idx, int(m), assign, a_prev, mind, mind2, float(tol), u, l, changed,
+                           n_changed)
     return int(n_changed.item())
 
 

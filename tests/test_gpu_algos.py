@@ -703,29 +703,56 @@ def test_kmeans_filter_and_post_match_torch(cuda):
     n, k = 100_003, 50
     assign = torch.randint(0, k, (n,), dtype=torch.int32, device=cuda)
     u = torch.rand(n, device=cuda) * 10
+    l = torch.rand(n, device=cuda) * 20
     delta = torch.rand(k, device=cuda)
     s = torch.rand(k, device=cuda) * 12
-    u0 = u.clone()
+    maxd = delta.max().reshape(1)
+    u0, l0 = u.clone(), l.clone()
     a_prev = torch.full((n,), -1, dtype=torch.int32, device=cuda)
     idx = torch.empty(n, dtype=torch.int32, device=cuda)
     cnt = torch.zeros(1, dtype=torch.int64, device=cuda)
-    m = K.filter_rows(assign, u, delta, s, a_prev, idx, cnt)
+    m = K.filter_rows(assign, u, l, delta, s, maxd, a_prev, idx, cnt)
     ub = u0 + delta[assign.long()]
-    act = ~(ub < s[assign.long()])
+    lb = l0 - maxd
+    act = ~(ub < torch.maximum(s[assign.long()], lb))
     assert m == int(act.sum())
     assert torch.equal(torch.sort(idx[:m]).values.long(), torch.nonzero(act)[:, 0])
     assert torch.allclose(u[~act], ub[~act]) and torch.equal(u[act], u0[act])
+    assert torch.allclose(l[~act], lb[~act]) and torch.equal(l[act], l0[act])
     assert torch.equal(a_prev[act], assign[act])
     # post: half of the active rows change cluster
     new = assign.clone()
     ch = act & (torch.arange(n, device=cuda) % 2 == 0)
     new[ch] = (new[ch] + 1) % k
     mind = torch.rand(n, device=cuda) * 4
+    mind2 = mind + torch.rand(n, device=cuda) * 4
     changed = torch.empty(n, dtype=torch.int32, device=cuda)
-    c = K.post_rows(idx, m, new, a_prev, mind, 0.5, u, changed, cnt)
+    c = K.post_rows(idx, m, new, a_prev, mind, mind2, 0.5, u, l, changed, cnt)
     assert c == int(ch.sum())
     assert torch.equal(torch.sort(changed[:c]).values.long(), torch.nonzero(ch)[:, 0])
     assert torch.allclose(u[act], torch.sqrt(mind[act] + 0.5))
+    assert torch.allclose(l[act], torch.sqrt((mind2[act] - 0.5).clamp_min(0)))
+
+
+def test_kmeans_assign_top2_second_best(cuda):
+    """Top-2 K2: the second-best distance is a lower bound of (and within rounding of) the
+    true second-smallest distance to the rounded centres; the best is unchanged."""
+    torch.manual_seed(8)
+    n, d, k = 40_000, 128, 1000
+    X = K.prepare_points((torch.randn(n, d) * 3).to(torch.bfloat16).to(cuda))
+    cen = K.make_centers(torch.randn(k, d) * 3, torch.bfloat16, cuda)
+    full = K.assign(X, cen)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    mind = torch.empty(n, device=cuda)
+    mind2 = torch.empty(n, device=cuda)
+    K.assign_rows(X, cen, None, n, a, mind, mind2)
+    assert (a == full).float().mean().item() > 0.999
+    dist = torch.cdist(X[:, :d].double(), cen.Cq[:k, :d].double()) ** 2
+    two = torch.topk(dist, 2, dim=1, largest=False).values
+    tol = 1e-3 * (1 + float(dist.max()))
+    assert bool((mind2.double() <= two[:, 1] + tol).all())
+    assert float((two[:, 1] - mind2.double()).abs().max()) < tol
+    assert bool((mind2 >= mind - tol).all())
 
 
 def test_kmeans_bound_filter_exact(cuda):
@@ -745,4 +772,4 @@ def test_kmeans_bound_filter_exact(cuda):
     assert np.allclose(a.history.sse, b.history.sse, rtol=2e-4), (a.history.sse, b.history.sse)
     same = (a.centers - b.centers).abs().amax(dim=1) < 1e-2
     assert same.float().mean().item() > 0.9
-    assert a.active_history[0] == n and min(a.active_history[1:]) < 0.7 * n
+    assert a.active_history[0] == n and min(a.active_history[1:]) < 0.3 * n
