@@ -53,6 +53,9 @@ def test_bench_two_ranks_gloo_on_one_gpu(cuda):
     ("optimization/bmuf.py", ["--synthetic", "50000,128", "--n-iterations", "5", "--quiet"], "Final acc:"),
     ("optimization/easgd.py", ["--synthetic", "50000,128", "--n-iterations", "5", "--quiet"], "Final acc:"),
     ("machine_learning/k-means.py", ["--synthetic", "20000,16", "--k", "8"], "Final centers:"),
+    # bf16 d = 64: the Hamerly-bounded, incremental path on every rank
+    ("machine_learning/k-means.py", ["--synthetic", "60000,64", "--k", "64", "--n-iterations", "6"],
+     "Final centers:"),
     ("graph_computation/pagerank.py", ["--rmat-scale", "12", "--top", "3"], "has rank:"),
     ("matrix_computation/matrix_decomposition.py", [], "iterations: 4, rmse:"),
     ("randomized_algorithm/monte_carlo.py", ["--num-samples", "1000000"], "Pi is roughly"),
