@@ -97,7 +97,10 @@ __device__ __forceinline__ void flush_run(float* acc, int32_t* pres, int key, fl
 // splitting the sources over the XCDs' L2s (K4x) cut the fabric reads 3x (62 -> 21 GB,
 // L2 hit 54 -> 82 %) at unchanged time and unchanged TA_BUSY (86 %), so the way to go
 // faster is to take gathers off that path (profiles/round3/pmc_pagerank.md).
-template <int NW, bool NT, bool ACC, int HOT = 0>
+// PIPE: the next window's edge stream (src, dst) is loaded before this window's gathers,
+// so a wave keeps one stream load in flight under its gathers instead of two dependent
+// round trips per window.
+template <int NW, bool NT, bool ACC, int HOT = 0, bool PIPE = false>
 __global__ void __launch_bounds__(NW * 64)
 pr_spmv_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dstl, int64_t E,
                const float* __restrict__ c, float* __restrict__ acc, int32_t* __restrict__ pres,
@@ -113,10 +116,28 @@ pr_spmv_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dstl
   const int64_t nwin = (E + 255) / 256;
   const int64_t wave = (int64_t)blockIdx.x * NW + (threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * NW;
+  int4 s4n = make_int4(-1, -1, -1, -1), d4n = make_int4(-1, -1, -1, -1);
+  if constexpr (PIPE) {
+    const int64_t e0 = wave * 256 + 4 * lane;
+    if (wave < nwin && e0 < E) {
+      s4n = ld_int4<NT>(src + e0);
+      d4n = ld_int4<NT>(dstl + e0);
+    }
+  }
   for (int64_t wi = wave; wi < nwin; wi += nwaves) {
     const int64_t e0 = wi * 256 + 4 * lane;
     int4 s4 = make_int4(-1, -1, -1, -1), d4 = make_int4(-1, -1, -1, -1);
-    if (e0 < E) {
+    if constexpr (PIPE) {
+      s4 = s4n;
+      d4 = d4n;
+      const int64_t e1 = (wi + nwaves) * 256 + 4 * lane;
+      s4n = make_int4(-1, -1, -1, -1);
+      d4n = make_int4(-1, -1, -1, -1);
+      if (wi + nwaves < nwin && e1 < E) {
+        s4n = ld_int4<NT>(src + e1);
+        d4n = ld_int4<NT>(dstl + e1);
+      }
+    } else if (e0 < E) {
       s4 = ld_int4<NT>(src + e0);
       d4 = ld_int4<NT>(dstl + e0);
     }
@@ -554,6 +575,12 @@ hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, con
     DALGO_PR_HOT_LAUNCH(32768)
 #undef DALGO_PR_HOT_LAUNCH
     return hipErrorInvalidValue;
+  }
+  if (nt && !accumulate && env_int("DALGO_PR_PIPE", 0) != 0) {   // measured slower (10.65 vs 10.33 ms)
+    hipLaunchKernelGGL((pr_spmv_kernel<NW, true, false, 0, true>), dim3(grid), dim3(NW * 64), 0, st,
+                       src, dstl, E, c, acc, pres, n_c);
+    DALGO_LAUNCH_CHECK();
+    return hipSuccess;
   }
   if (nt && accumulate)
     hipLaunchKernelGGL((pr_spmv_kernel<NW, true, true>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
