@@ -1432,6 +1432,14 @@ hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP
   if (m <= 0) return hipSuccess;
   if (kpad % 128 != 0) return hipErrorInvalidValue;
   if (mind2 != nullptr) {
+    // top-2 forms that fit 256 VGPRs without spilling (A/B: DALGO_KM_TOP2_CFG)
+    static const int cfg = env_int("DALGO_KM_TOP2_CFG", 0);
+    if (DP == 128 && cfg == 1)
+      return launch_assign_pipe<128, 4, 3, 4, 2, 2, false, 0, 0, true>(X, m, ldx, Cq, hn, kpad, assign,
+                                                                      mind, sse, sse_mask, st, idx, mind2);
+    if (DP == 128 && cfg == 2)
+      return launch_assign_pipe<128, 4, 2, 4, 2, 2, true, 0, 0, true>(X, m, ldx, Cq, hn, kpad, assign,
+                                                                     mind, sse, sse_mask, st, idx, mind2);
     if (DP == 128)
       return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, 2, 0, true>(X, m, ldx, Cq, hn, kpad, assign,
                                                                       mind, sse, sse_mask, st, idx, mind2);

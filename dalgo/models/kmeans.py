@@ -97,6 +97,7 @@ class KMeans:
         self.bounds = (self.dev.type == "cuda" and self.X.dtype == torch.bfloat16
                        and self.DP in (64, 128) and self.pstats is None
                        and K.assign_variant(self.X) == 52 and self.inc_max > 0
+                       and k <= 2048   # per-cluster |x|^2 sums: one LDS histogram
                        and os.environ.get("DALGO_KM_BOUNDS", "1") != "0")
         self._u = None
         self.active_history: list = []
