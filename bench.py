@@ -141,37 +141,10 @@ def fallback_plain(model, rt, why: str) -> None:
     rt.barrier()
 
 
-def _free_port() -> int:
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def self_launch(a, argv) -> int | None:
-    """``--gpus N`` without a launcher: run N ranks as a torchrun CHILD process.
-
-    Returns the child's exit code, or None when this process is already a rank (or
-    N == 1). Nothing here initialises the GPU (``torch.cuda.device_count()`` does not
-    on this ROCm build), and the child is a new process, never an exec."""
-    if a.gpus <= 1 or "RANK" in os.environ or "WORLD_SIZE" in os.environ:
-        return None
-    backend = a.backend or ("nccl" if a.device == "cuda" else "gloo")
-    if a.device == "cuda":
-        ndev = torch.cuda.device_count()
-        if backend == "nccl" and a.gpus > ndev:
-            print(f"[bench] --gpus {a.gpus} but only {ndev} GPU(s) are visible: RCCL needs one "
-                  f"GPU per rank; refusing to report a {a.gpus}-GPU number", file=sys.stderr)
-            return 2
-    import subprocess
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
-           "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.run(cmd, env=env).returncode
+    """``--gpus N`` without a launcher: N ranks as a torchrun child (dalgo.parallel.launch)."""
+    from dalgo.parallel.launch import self_launch as _sl
+    return _sl(a.gpus, __file__, argv, device=a.device, backend=a.backend, tag="bench")
 
 
 def allreduce_probe(model, rt, iters: int = 100) -> float | None:
@@ -197,10 +170,10 @@ def allreduce_probe(model, rt, iters: int = 100) -> float | None:
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else list(argv)
     a = parse(argv)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     rc = self_launch(a, argv)
     if rc is not None:
         sys.exit(rc)
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from dalgo.data.datasets import synthetic_logistic
     from dalgo.models.localsgd import ParallelSGD, SGDConfig
     from dalgo.parallel import comm, runtime
@@ -208,9 +181,8 @@ def main(argv=None):
 
     rt = runtime.init(backend=a.backend, device=a.device, app_name="bench-ssgd")
     W = rt.world_size
-    if a.gpus != W:
-        raise SystemExit(f"[bench] --gpus {a.gpus} but WORLD_SIZE={W}: launch N ranks "
-                         f"(or let bench.py start them) so N GPUs are measured")
+    from dalgo.parallel.launch import check_world
+    check_world(a.gpus, W, "bench")
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     n_workers = W
     layout = make_layout(a.rows, n_workers, W, rt.rank, spark_compatible=False)

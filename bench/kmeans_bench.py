@@ -24,19 +24,29 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
-    a = ap.parse_args()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
+                    help="ranks (one per GPU); started here as a torchrun child when > 1")
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--backend", default=None, choices=["nccl", "gloo"])
+    argv = sys.argv[1:]
+    a = ap.parse_args(argv)
+    from dalgo.parallel.launch import check_world, self_launch
+    rc = self_launch(a.gpus, __file__, argv, device=a.device, backend=a.backend, tag="kmeans_bench")
+    if rc is not None:
+        sys.exit(rc)
     from dalgo.data.synthetic import blobs
     from dalgo.models.kmeans import KMeans, KMeansConfig
     from dalgo.ops import kmeans as K
     from dalgo.parallel import comm, runtime
     from dalgo.parallel.sharding import even_slices
-    rt = runtime.init(device="cuda")
+    rt = runtime.init(backend=a.backend, device=a.device, app_name="kmeans-bench")
     W = rt.world_size
+    check_world(a.gpus, W, "kmeans_bench")
     lo, hi = even_slices(a.rows, W)[rt.rank]
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     t0 = time.time()
     X = blobs(a.rows, a.dim, a.k, row_range=(lo, hi), device=rt.device, dtype=dtype, seed=7)
-    torch.cuda.synchronize()
+    rt.synchronize()
     gen = time.time() - t0
     km = KMeans(KMeansConfig(k=a.k, n_iterations=a.steps, seed=1), X, lo, a.rows)
     from dalgo.utils.obs import PhaseTimer
@@ -49,19 +59,44 @@ def main():
         if i == 0:
             first = km.timer.summary()
             km.timer = PhaseTimer(rt.device)
-    torch.cuda.synchronize()
-    rt.barrier(); torch.cuda.synchronize()
+    rt.synchronize()
+    rt.barrier(); rt.synchronize()
     km.timer = PhaseTimer(rt.device)     # HIP events only (no host sync in the loop)
     km.changed_history.clear()
     km.active_history.clear()
     t = time.perf_counter()
     for _ in range(a.steps):
         km.step()
-    torch.cuda.synchronize(); rt.barrier(); torch.cuda.synchronize()
+    rt.synchronize(); rt.barrier(); rt.synchronize()
     timed_phases = {k: v / a.steps for k, v in km.timer.summary().items()}
     phases = first or {}
     sse_last = km.sse.clone()
     comm.all_reduce_sum(sse_last)
+    # correctness witness (untimed): the last assignment vs a brute-force K2 pass over all
+    # points with the same (rounded) centres, and the incrementally maintained local sums /
+    # counts vs a full K3 pass over that assignment
+    witness = None
+    if km.bounds and km._u is not None:
+        d = km.d
+        cen_last = K.make_centers(km._cq_prev[:, :d].float(), km.X.dtype, rt.device,
+                                  kpad=km.cen.Cq.shape[0])
+        sse_bf = torch.zeros(1, dtype=torch.float32, device=rt.device)
+        a_full = K.assign(km.X, cen_last, sse=sse_bf)
+        if isinstance(a_full, tuple):
+            a_full = a_full[0]
+        agree = float((a_full == km.assign).float().mean().item())
+        S_ref = torch.zeros_like(km.S)
+        c_ref = torch.zeros_like(km.cnt)
+        K.accumulate(km.X, km.assign, a.k, km.DP, S_ref, c_ref)
+        err = float(((S_ref.double() - km._S64).abs().max() /
+                     (1.0 + S_ref.double().abs().max())).item())
+        witness = {"assignment_agreement_vs_brute_force": agree,
+                   "counts_equal": bool(torch.equal(c_ref, km._cnt64)),
+                   "sums_max_rel_err": err,
+                   "local_sse_identity_vs_kernel_rel": float(
+                       ((km.sse.double() - sse_bf.double()).abs() /
+                        sse_bf.double().abs().clamp_min(1e-30)).item()),
+                   "passed": bool(agree > 0.9999 and torch.equal(c_ref, km._cnt64) and err < 1e-4)}
     el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=rt.device)
     comm.all_reduce_max(el)
     ms = float(el.item()) / a.steps * 1e3
@@ -75,8 +110,9 @@ def main():
             "moved_rows_per_iter_rank0": list(km.changed_history),
             "reassigned_rows_per_iter_rank0": list(km.active_history),
             "bound_filter": km.bounds, "sse_last_iteration": float(sse_last.item()),
+            "correctness_witness": witness,
             "accumulate_mode": "incremental below %.1f %% moved rows" % (100 * km.inc_max)
-            if km.inc_max > 0 else "full", "config": {"rows": a.rows, "dim": a.dim, "k": a.k, "dtype": a.dtype},
+            if km.inc_max > 0 and km.X.is_cuda else "full", "config": {"rows": a.rows, "dim": a.dim, "k": a.k, "dtype": a.dtype},
             "datagen_s": gen}), flush=True)
     runtime.shutdown()
 

@@ -28,40 +28,48 @@ def main():
     ap.add_argument("--bin-width", type=int, default=16384)
     ap.add_argument("--chunk", type=int, default=1 << 18)
     ap.add_argument("--tile", type=int, default=1 << 16)
-    a = ap.parse_args()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
+                    help="ranks (one per GPU); started here as a torchrun child when > 1")
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--backend", default=None, choices=["nccl", "gloo"])
+    argv = sys.argv[1:]
+    a = ap.parse_args(argv)
+    from dalgo.parallel.launch import check_world, self_launch
+    rc = self_launch(a.gpus, __file__, argv, device=a.device, backend=a.backend, tag="pagerank_bench")
+    if rc is not None:
+        sys.exit(rc)
     from dalgo.apps.pagerank_app import rmat_shard
     from dalgo.models.pagerank import PageRank, PageRankConfig
     from dalgo.ops import graph as G
     from dalgo.parallel import comm, runtime
-    rt = runtime.init(device="cuda")
+    rt = runtime.init(backend=a.backend, device=a.device, app_name="pagerank-bench")
     W = rt.world_size
+    check_world(a.gpus, W, "pagerank_bench")
     t0 = time.time()
     shard, n_gen = rmat_shard(a.scale, a.edge_factor, rt.rank, W, rt.device, reorder=not a.no_reorder)
-    torch.cuda.synchronize()
+    rt.synchronize()
     build_s = time.time() - t0
     E = comm.all_reduce_count(shard.n_edges, device=rt.device)
     pr = PageRank(PageRankConfig(semantics=a.semantics, spmv=a.spmv, bin_width=a.bin_width,
                                  chunk=a.chunk, tile=a.tile), shard, W)
     for _ in range(a.warmup):
         pr.step()
-    torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    ev[0].record()
-    pr._exchange()
-    ev[1].record()
-    pr._spmv()
-    ev[2].record()
-    pr._update()
-    ev[3].record()
-    torch.cuda.synchronize()
-    phases = {n: ev[i].elapsed_time(ev[i + 1]) for i, n in enumerate(["exchange", "spmv", "update"])}
+    rt.synchronize()
+    rt.synchronize()
+    from dalgo.utils.obs import PhaseTimer
+    tm = PhaseTimer(rt.device)
+    for name, fn in (("exchange", pr._exchange), ("spmv", pr._spmv), ("update", pr._update)):
+        with tm.phase(name):
+            fn()
+    rt.synchronize()
+    phases = tm.summary()
     xf = torch.tensor([pr.exchange_floats()], dtype=torch.int64, device=rt.device)
     comm.all_reduce_sum(xf)
-    rt.barrier(); torch.cuda.synchronize()
+    rt.barrier(); rt.synchronize()
     t = time.perf_counter()
     for _ in range(a.steps):
         pr.step()
-    torch.cuda.synchronize(); rt.barrier(); torch.cuda.synchronize()
+    rt.synchronize(); rt.barrier(); rt.synchronize()
     el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=rt.device)
     comm.all_reduce_max(el)
     ms = float(el.item()) / a.steps * 1e3

@@ -186,6 +186,21 @@ def test_bench_self_launches_n_ranks():
     assert d["correctness_witness"]["passed"] and d["correctness_witness"]["trained_steps"] == 1500
 
 
+@pytest.mark.parametrize("script,args,metric", [
+    ("bench/kmeans_bench.py", ["--rows", "20000", "--dim", "16", "--k", "8", "--dtype", "f32"],
+     "k-means points/sec (whole node)"),
+    ("bench/pagerank_bench.py", ["--scale", "10"], "PageRank edges/sec (whole node)"),
+])
+def test_secondary_benches_self_launch(script, args, metric):
+    """The k-means and PageRank benches start N ranks themselves like bench.py."""
+    out = _run([script, "--gpus", "2", "--device", "cpu", "--backend", "gloo", "--steps", "2"]
+               + args, timeout=600)
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["metric"] == metric and d["n_gpus"] == 2 and d["value"] > 0
+
+
 def test_bench_refuses_mismatched_world():
     """--gpus N under a launcher with WORLD_SIZE != N fails loudly (no silent 1-GPU number)."""
     env = dict(os.environ, PYTHONPATH=ROOT, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
