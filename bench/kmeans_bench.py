@@ -68,6 +68,8 @@ def main():
     for _ in range(a.steps):
         km.step()
     rt.synchronize(); rt.barrier(); rt.synchronize()
+    el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=rt.device)
+    comm.all_reduce_max(el)
     timed_phases = {k: v / a.steps for k, v in km.timer.summary().items()}
     phases = first or {}
     sse_last = km.sse.clone()
@@ -84,21 +86,29 @@ def main():
         a_full = K.assign(km.X, cen_last, sse=sse_bf)
         if isinstance(a_full, tuple):
             a_full = a_full[0]
-        agree = float((a_full == km.assign).float().mean().item())
+        diff = (a_full != km.assign).nonzero().flatten()
+        agree = 1.0 - diff.numel() / max(1, km.X.shape[0])
+        # every disagreement must be a near-tie: both centres within the kernel's
+        # distance slack of each other (exact f64 distances on the rounded centres)
+        Xd = km.X[diff, :d].double()
+        Cd = km._cq_prev[:, :d].double()
+        gap = ((Xd - Cd[km.assign[diff].long()]).pow(2).sum(1) -
+               (Xd - Cd[a_full[diff].long()]).pow(2).sum(1)).abs()
+        max_gap = float(gap.max().item()) if diff.numel() else 0.0
         S_ref = torch.zeros_like(km.S)
         c_ref = torch.zeros_like(km.cnt)
         K.accumulate(km.X, km.assign, a.k, km.DP, S_ref, c_ref)
         err = float(((S_ref.double() - km._S64).abs().max() /
                      (1.0 + S_ref.double().abs().max())).item())
         witness = {"assignment_agreement_vs_brute_force": agree,
+                   "disagreements": int(diff.numel()),
+                   "max_disagreement_gap": max_gap, "distance_slack": 2.0 * km._tol,
                    "counts_equal": bool(torch.equal(c_ref, km._cnt64)),
                    "sums_max_rel_err": err,
                    "local_sse_identity_vs_kernel_rel": float(
                        ((km.sse.double() - sse_bf.double()).abs() /
                         sse_bf.double().abs().clamp_min(1e-30)).item()),
-                   "passed": bool(agree > 0.9999 and torch.equal(c_ref, km._cnt64) and err < 1e-4)}
-    el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=rt.device)
-    comm.all_reduce_max(el)
+                   "passed": bool(agree > 0.999 and max_gap <= 2.0 * km._tol and torch.equal(c_ref, km._cnt64) and err < 1e-4)}
     ms = float(el.item()) / a.steps * 1e3
     flops = 2.0 * a.rows * a.k * a.dim
     if rt.is_main:
