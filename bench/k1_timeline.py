@@ -34,6 +34,9 @@ def main():
         i = args.index("--frac")
         frac = float(args[i + 1])
         args = args[:i] + args[i + 2:]
+    use_list = "--list" in args
+    if use_list:
+        args = [x for x in args if x != "--list"]
     if "--fine" in args:
         i = args.index("--fine")
         fines = [int(x) for x in args[i + 1:]]
@@ -45,6 +48,7 @@ def main():
     G = torch.zeros(1, 1025, device=dev)
     C = torch.zeros(1, device=dev)
     buf = torch.zeros(1 << 20, dtype=torch.int64, device=dev)
+    L.LR_BALANCED = use_list      # balanced slices of the compacted selection vs the walk
     for rows, fine in [(r, f) for r in rows_list for f in fines]:
         var = L.LR_VARIANT | (fine << 16)
         X, y = Xall[:rows], yall[:rows]
@@ -62,6 +66,8 @@ def main():
                       variant=var)
             ops.lr_set_trace(None)
             torch.cuda.synchronize()
+            if use_list:
+                gx = [v for v in L._sel_cache.values() if v.n == rows][0].gx
             t = buf[: gx * NW * 8].view(gx, NW, 8).cpu().double()
             t0 = t[:, :, 0].min().item()
             us = lambda v: (v - t0) / 100.0   # noqa: E731
@@ -104,7 +110,7 @@ def main():
                 "cus": len(set(t[:, :, 5].flatten().tolist())),
             })
         med = {k: round(sorted(r[k] for r in res)[len(res) // 2], 2) for k in res[0]}
-        print(json.dumps({"rows": rows, "frac": frac, "fine": fine, "blocks": gx, **med}), flush=True)
+        print(json.dumps({"rows": rows, "frac": frac, "fine": fine, "list": use_list, "blocks": gx, **med}), flush=True)
 
 
 if __name__ == "__main__":

@@ -85,8 +85,32 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
              const std::optional<Tensor>& pool, int64_t pool_parity, int64_t nsteps,
              const std::optional<Tensor>& epoch, int64_t epoch_base,
              const std::optional<Tensor>& perr, double spin_s,
-             const std::optional<Tensor>& step_dev, int64_t step_mul) {
+             const std::optional<Tensor>& step_dev, int64_t step_mul,
+             const std::optional<Tensor>& sel_list, const std::optional<Tensor>& sel_total,
+             int64_t sel_k, const std::optional<Tensor>& sel_claim) {
   check_lr_inputs(X, y, W, seg, D, has_bias);
+  DalgoLrSel sel{};
+  const DalgoLrSel* selp = nullptr;
+  if (sel_list.has_value()) {
+    TORCH_CHECK(sel_total.has_value() && sel_claim.has_value() && sel_k > 0 && sel_k < (1ll << 30),
+                "balanced slices: sel_total, sel_claim and sel_k > 0");
+    check_dev(*sel_list, "sel_list");
+    check_dev(*sel_total, "sel_total");
+    check_dev(*sel_claim, "sel_claim");
+    TORCH_CHECK(sel_list->scalar_type() == at::kInt && sel_list->is_contiguous() &&
+                sel_total->scalar_type() == at::kLong && sel_claim->scalar_type() == at::kInt,
+                "balanced slices: int32 list, int64 total, int32 claim");
+    TORCH_CHECK(W.size(0) == 1, "balanced slices: one segment");
+    // block b reads entries [b * sel_k, b * sel_k + sel_k) whatever the total, and the
+    // total is at most the shard's row count
+    TORCH_CHECK(sel_list->numel() >= std::max<int64_t>(gx * sel_k, X.size(0)),
+                "balanced slices: list shorter than max(gx * sel_k, rows)");
+    sel.list = sel_list->data_ptr<int>();
+    sel.total = sel_total->data_ptr<int64_t>();
+    sel.k = (int)sel_k;
+    sel.claim = reinterpret_cast<unsigned*>(sel_claim->data_ptr<int>());
+    selp = &sel;
+  }
   const int64_t* stepp = nullptr;
   if (step_dev.has_value()) {
     check_dev(*step_dev, "step_dev");
@@ -191,7 +215,7 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
                     reinterpret_cast<unsigned*>(cnt2.data_ptr<int>()), G.data_ptr<float>(),
                     C.data_ptr<float>(), (int)S, (int)variant, wprev, (int)upd_mode, (int)upd_reg,
                     (float)upd_eta, (float)upd_lam, (float)upd_reg_alpha, cacc, tailp, poolp,
-                    (int)(pool_parity & 1), stepp, step_mul, cur_stream()),
+                    (int)(pool_parity & 1), stepp, step_mul, selp, cur_stream()),
       "lr_grad");
 }
 
@@ -327,6 +351,43 @@ void hbm_gather_rows(const Tensor& X, const Tensor& idx, Tensor out, int64_t gri
 }
 
 // diagnostics: per-wave K1 timeline (u64, 8 per wave) for the following lr_grad launches
+void lr_select(int64_t seed, int64_t step, double frac, int64_t row_offset, int64_t n, int64_t ch,
+               Tensor list, Tensor count) {
+  check_dev(list, "list");
+  check_dev(count, "count");
+  TORCH_CHECK(list.scalar_type() == at::kInt && count.scalar_type() == at::kInt, "int32 list/count");
+  TORCH_CHECK(ch > 0 && ch % 4 == 0 && ch < (1ll << 31), "chunk rows: positive multiple of 4");
+  const int64_t nch = (n + ch - 1) / ch;
+  TORCH_CHECK(list.numel() >= nch * ch && count.numel() >= nch, "list / count too small");
+  DeviceGuard guard(list.device());
+  DALGO_CHECK_HIP(dalgo_lr_select((uint64_t)seed, (uint64_t)step, frac_threshold(frac), row_offset, n,
+                                  (int)ch, (int)std::max<int64_t>(nch, 1), list.data_ptr<int>(),
+                                  count.data_ptr<int>(), cur_stream()),
+                  "lr_select");
+}
+
+
+void lr_select_compact(const Tensor& chunks, const Tensor& counts, int64_t ch, Tensor list,
+                       Tensor total, Tensor claim) {
+  check_dev(chunks, "chunks");
+  check_dev(counts, "counts");
+  check_dev(list, "list");
+  check_dev(total, "total");
+  check_dev(claim, "claim");
+  TORCH_CHECK(chunks.scalar_type() == at::kInt && counts.scalar_type() == at::kInt &&
+              list.scalar_type() == at::kInt && total.scalar_type() == at::kLong &&
+              claim.scalar_type() == at::kInt, "lr_select_compact: int32 / int64 total");
+  const int64_t nch = counts.numel();
+  TORCH_CHECK(ch > 0 && chunks.numel() >= nch * ch && list.numel() >= chunks.numel() && nch > 0,
+              "lr_select_compact: shapes");
+  DeviceGuard guard(list.device());
+  DALGO_CHECK_HIP(dalgo_lr_select_compact(chunks.data_ptr<int>(), counts.data_ptr<int>(), (int)ch,
+                                          (int)nch, list.data_ptr<int>(), total.data_ptr<int64_t>(),
+                                          reinterpret_cast<unsigned*>(claim.data_ptr<int>()),
+                                          cur_stream()),
+                  "lr_select_compact");
+}
+
 void lr_set_trace(const c10::optional<Tensor>& buf) {
   if (buf.has_value()) {
     check_dev(*buf, "trace");
@@ -1096,7 +1157,8 @@ TORCH_LIBRARY(dalgo, m) {
         "float tail_eta=0., float tail_lam=0., float tail_reg_alpha=0., "
         "Tensor(j!)? tail_count_acc=None, Tensor(k!)? pool=None, int pool_parity=0, int nsteps=1, "
         "Tensor(l!)? epoch=None, int epoch_base=0, Tensor(m!)? perr=None, float spin_s=2., "
-        "Tensor? step_dev=None, int step_mul=1) -> ()");
+        "Tensor? step_dev=None, int step_mul=1, Tensor? sel_list=None, Tensor? sel_total=None, "
+        "int sel_k=0, Tensor(n!)? sel_claim=None) -> ()");
   m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
         "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=3) -> ()");
   m.def("sync_update(Tensor(a!) W, Tensor(d!)? G, Tensor(e!)? C, Tensor? center, Tensor? S, "
@@ -1162,11 +1224,17 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("lr_set_trace(Tensor? buf) -> ()", &lr_set_trace);
   m.def("hbm_gather_rows(Tensor X, Tensor idx, Tensor(a!) out, int grid=2048) -> ()");
   m.def("mc_pi(int seed, int stream, int offset, int n, Tensor(a!) count) -> ()");
+  m.def("lr_select(int seed, int step, float frac, int row_offset, int n, int ch, Tensor(a!) list, "
+        "Tensor(b!) count) -> ()");
+  m.def("lr_select_compact(Tensor chunks, Tensor counts, int ch, Tensor(a!) list, Tensor(b!) total, "
+        "Tensor(c!) claim) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("lr_grad", &lr_grad);
   m.impl("lr_eval", &lr_eval);
+  m.impl("lr_select", &lr_select);
+  m.impl("lr_select_compact", &lr_select_compact);
   m.impl("sync_update", &sync_update);
   m.impl("rows_sum", &rows_sum);
   m.impl("rows_broadcast", &rows_broadcast);

@@ -100,6 +100,14 @@ struct LrParams {
   uint32_t epoch_base;
   unsigned* perr;
   uint64_t spin_ticks;
+  // balanced slices (LIST instantiation): the step's selected local rows, compacted in
+  // ascending order (sel_list, *sel_total entries). Block b takes entries
+  // [b * sel_k, (b + 1) * sel_k) and every wave claims U of them at a time from LDS;
+  // entries past gx * sel_k are claimed in U-entry units from *sel_claim (zero on entry)
+  const int* sel_list;
+  const int64_t* sel_total;
+  int sel_k;
+  unsigned* sel_claim;
 };
 
 __device__ __forceinline__ void wt_store(float* a, float v) {
@@ -231,7 +239,7 @@ constexpr int64_t kPExh = (1ll << 40) - 1;   // "pool exhausted" marker
 // step (profiles/round2/README.md). The launcher falls back to the full build when a
 // launch needs any of them.
 template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, bool PERSIST, int AUX = 0,
-          bool LEAN = false>
+          bool LEAN = false, bool LIST = false>
 __global__ void __launch_bounds__(NW * 64)
 lr_rows_kernel(const LrParams p) {
   // the persistent form (fused tail, atomic epilogue, no pool / prologue: host checks)
@@ -241,9 +249,10 @@ lr_rows_kernel(const LrParams p) {
   constexpr int COLS = NC * 64 * VEC;  // columns covered per lane-set
   constexpr int RED_FLOATS = NW * (COLS + 4);
   constexpr int RING_INTS = NW * kRing;
+  constexpr int ARENA = (RED_FLOATS > RING_INTS) ? RED_FLOATS : RING_INTS;
   // one LDS arena: per-wave selection rings during the sweep, then the
   // cross-wave reduction buffer
-  __shared__ __attribute__((aligned(16))) float s_arena[(RED_FLOATS > RING_INTS) ? RED_FLOATS : RING_INTS];
+  __shared__ __attribute__((aligned(16))) float s_arena[ARENA];
   __shared__ int s_flag;
   __shared__ int s_next;   // next unclaimed work unit of this block (dynamic balancing)
   __shared__ int s_ok;     // persistent mode: the epoch wait succeeded
@@ -402,6 +411,20 @@ lr_rows_kernel(const LrParams p) {
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (threadIdx.x < kPSlots) s_punit[threadIdx.x] = 0ull;
   if (threadIdx.x == 0) { s_pnext = 0; s_pclaim = 0; }
+  // LIST: this block's slice of the compacted selection, staged in the (ring-free) arena.
+  // The entry loads do not wait for the total (the list buffer holds gx * sel_k entries
+  // whatever the total): entries past it are loaded but never used.
+  int* const sl = reinterpret_cast<int*>(s_arena);
+  int slen = 0;
+  int64_t sel_tot = 0;
+  if constexpr (LIST) {
+    const int64_t s0 = (int64_t)bx * p.sel_k;
+    const int nst_ = min(p.sel_k, ARENA);
+    for (int i = threadIdx.x; i < nst_; i += NW * 64) sl[i] = p.sel_list[s0 + i];
+    sel_tot = *p.sel_total;
+    slen = (int)max((int64_t)0, min((int64_t)p.sel_k, sel_tot - s0));
+    if (threadIdx.x == 0) s_next = 0;
+  }
   __syncthreads();
   const unsigned long long t_bar = tr ? (unsigned long long)__builtin_amdgcn_s_memrealtime() : 0ull;
   const int64_t psl = seg_lo + (int64_t)gx * p.rows_per_block;   // pool start (local row)
@@ -508,6 +531,7 @@ lr_rows_kernel(const LrParams p) {
 
   // ---- K7: Bernoulli selection of the next work unit, compacted into the ring
   auto refill = [&]() {
+    if constexpr (LIST) return;
     while ((tail - head) < (uint32_t)(2 * U) && more) {
       const int64_t r0 = gnext + 4 * lane;
       u32x4 h{0u, 0u, 0u, 0u};
@@ -555,18 +579,55 @@ lr_rows_kernel(const LrParams p) {
     __builtin_amdgcn_wave_barrier();
   };
 
+  bool sel_pool_done = false;
   auto take_and_load = [&](Batch<NC, U>& b) {
+    int64_t r[U];
+    if constexpr (LIST) {
+      int j0 = 0;
+      if (lane == 0) j0 = atomicAdd(&s_next, U);
+      j0 = __builtin_amdgcn_readfirstlane(j0);
+      if (j0 < slen) {
+        b.n = min(U, slen - j0);
+        const int last = b.n - 1;
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+          const int j = j0 + min(k, last);
+          r[k] = __builtin_amdgcn_readfirstlane(j < ARENA ? sl[j] : p.sel_list[(int64_t)bx * p.sel_k + j]);
+          r[k] = min(max(r[k], seg_lo), seg_hi - 1);   // a bad list cannot leave the shard
+        }
+      } else {
+        // entries past gx * sel_k: claimed from the launch-wide counter
+        const int64_t pbase = (int64_t)gx * p.sel_k;
+        b.n = 0;
+        if (!sel_pool_done && sel_tot > pbase) {
+          unsigned e = 0;
+          if (lane == 0) e = atomicAdd(p.sel_claim, (unsigned)U);
+          const int64_t e0 = pbase + (int64_t)__builtin_amdgcn_readfirstlane(e);
+          b.n = (int)max((int64_t)0, min((int64_t)U, sel_tot - e0));
+          if (b.n < U) sel_pool_done = true;
+          const int last = max(b.n - 1, 0);
+#pragma unroll
+          for (int k = 0; k < U; ++k)
+            r[k] = b.n ? min(max((int64_t)__builtin_amdgcn_readfirstlane(p.sel_list[e0 + min(k, last)]),
+                                 seg_lo), seg_hi - 1)
+                       : seg_lo;
+        }
+        if (b.n == 0) { sel_pool_done = true; return; }
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) b.v[k] = (k < b.n) ? 1.f : 0.f;
+    } else {
     const uint32_t avail = tail - head;
     b.n = (int)min(avail, (uint32_t)U);
     if (b.n == 0) return;
     const uint32_t last = b.n - 1;
-    int64_t r[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       r[k] = lo + __builtin_amdgcn_readfirstlane(ring[(head + min((uint32_t)k, last)) & (kRing - 1)]);
       b.v[k] = (k < b.n) ? 1.f : 0.f;
     }
     head += b.n;
+    }
     // one buffer descriptor per row (wave-uniform SGPRs, base = row start,
     // num_records = row bytes): lanes past the row read 0 via the range check
 #pragma unroll
@@ -831,11 +892,89 @@ lr_rows_kernel(const LrParams p) {
   }  // step loop
 }
 
+// K7 standalone: the compacted Bernoulli selection of one step, per chunk. Chunk c holds
+// local rows [c * ch, min(n, (c + 1) * ch)); its selected rows (ascending, the same
+// draw as K1's in-register sampling: philox(seed, step, global_row >> 2)[global_row & 3]
+// < thr) go to list[c * ch ...] and their number to count[c].
+__global__ void __launch_bounds__(256) lr_select_kernel(uint64_t seed, uint64_t step, uint32_t thr,
+                                                        int64_t row_offset, int64_t n, int ch,
+                                                        int* list, int* count) {
+  __shared__ int s_w[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t lo = (int64_t)blockIdx.x * ch, hi = min(n, lo + ch);
+  const int64_t g_lo = row_offset + lo, g_hi = row_offset + hi;
+  const int64_t q_lo = g_lo >> 2, q_hi = (g_hi + 3) >> 2;
+  int base = 0;
+  for (int64_t q0 = q_lo; q0 < q_hi; q0 += 256) {
+    const int64_t q = q0 + threadIdx.x;
+    unsigned m = 0;
+    if (q < q_hi) {
+      const u32x4 h = philox_block(seed, step, (uint64_t)q);
+      const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t gr = 4 * q + j;
+        if (gr >= g_lo && gr < g_hi && hv[j] < thr) m |= 1u << j;
+      }
+    }
+    const int cnt = __popc(m);
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += v;
+    }
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    int woff = 0, btot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int v = s_w[w];
+      woff += (w < wid) ? v : 0;
+      btot += v;
+    }
+    int pos = base + woff + incl - cnt;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((m >> j) & 1u) list[lo + pos++] = (int)(4 * q + j - row_offset);
+    base += btot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) count[blockIdx.x] = base;
+}
+
+// K7 second pass: chunk c's list moves to its place in the step's compacted list (the
+// exclusive prefix of the chunk counts, summed by the block itself: chunks are few);
+// block 0 writes the total and zeroes the overflow claim counter of the K1 launch.
+__global__ void __launch_bounds__(256) lr_select_compact_kernel(const int* chunks, const int* counts,
+                                                                int ch, int* list, int64_t* total,
+                                                                unsigned* claim) {
+  __shared__ int s_w[4];
+  const int c = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lim = (c == 0) ? (int)gridDim.x : c;   // block 0 sums every chunk (the total)
+  int v = 0;
+  for (int i = threadIdx.x; i < lim; i += 256) v += counts[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (lane == 0) s_w[wid] = v;
+  __syncthreads();
+  const int pre = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+  if (c == 0) {
+    if (threadIdx.x == 0) { *total = pre; *claim = 0u; }
+    for (int i = threadIdx.x; i < counts[0]; i += 256) list[i] = chunks[i];
+    return;
+  }
+  const int n = counts[c];
+  const int* src = chunks + (int64_t)c * ch;
+  for (int i = threadIdx.x; i < n; i += 256) list[pre + i] = src[i];
+}
+
 }  // namespace dalgo
 
 using namespace dalgo;
 
-template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, int AUX = 0, bool LEAN = false>
+template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, int AUX = 0, bool LEAN = false,
+          bool LIST = false>
 static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st) {
   dim3 grid(gx, nseg), block(NW * 64);
   if (p.nsteps > 1) {
@@ -848,7 +987,7 @@ static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st)
     }
     return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL((lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, false, AUX, LEAN>), grid, block, 0, st, p);
+  hipLaunchKernelGGL((lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, false, AUX, LEAN, LIST>), grid, block, 0, st, p);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -886,8 +1025,11 @@ static hipError_t launch_variant(const LrParams& p, int gx, int nseg, int varian
       // X-row cache policy (aux bits of the buffer load: 2 = nt, 1 = sc0, 16 = sc1)
       case 8:
         if constexpr (!EVAL) {
-          if (p.pool == nullptr && p.atomic_out && p.Wprev == nullptr && !p.probe_no_epilogue)
+          if (p.pool == nullptr && p.atomic_out && p.Wprev == nullptr && !p.probe_no_epilogue) {
+            if (p.sel_list != nullptr)
+              return launch_lr<T, NC, EVAL, 8, true, 4, 2, true, true>(p, gx, nseg, st);
             return launch_lr<T, NC, EVAL, 8, true, 4, 2, true>(p, gx, nseg, st);
+          }
         }
         return launch_lr<T, NC, EVAL, 8, true, 4, 2, false>(p, gx, nseg, st);
       case 12: return launch_lr<T, NC, EVAL, 8, true, 4, 2, false>(p, gx, nseg, st);   // 8, full build
@@ -941,7 +1083,7 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
                          const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
                          float upd_reg_alpha, double* count_acc, const DalgoLrTail* tail,
                          unsigned* pool, int pool_parity, const int64_t* step_dev,
-                         int64_t step_mul, hipStream_t st) {
+                         int64_t step_mul, const DalgoLrSel* sel, hipStream_t st) {
   LrParams p{};
   p.step_dev = step_dev;
   p.step_mul = step_mul;
@@ -985,9 +1127,36 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
   p.unit_shift = ((variant >> 24) & 0xf) ? ((variant >> 24) & 0xf) : 6;
   if (p.unit_shift < 2 || p.unit_shift > 8) return hipErrorInvalidValue;
   p.trace = g_lr_trace;
+  if (sel != nullptr) {
+    // only the lean variant-8 build has the LIST form (launch_variant)
+    if (nseg != 1 || full || step_dev != nullptr || p.nsteps > 1 || sel->k <= 0 ||
+        sel->list == nullptr || sel->total == nullptr || sel->claim == nullptr ||
+        (variant & 0xff) != 8 || pool != nullptr || Wprev != nullptr || !((variant >> 8) & 1) ||
+        ((variant >> 9) & 1))
+      return hipErrorInvalidValue;
+    p.sel_list = sel->list; p.sel_total = sel->total; p.sel_k = sel->k; p.sel_claim = sel->claim;
+  }
   p.pool = pool;
   p.pool_parity = pool_parity & 1;
   return dispatch_lr<false>(p, is_bf16, gx, nseg, variant & 0xff, st);
+}
+
+hipError_t dalgo_lr_select(uint64_t seed, uint64_t step, uint32_t thr, int64_t row_offset,
+                           int64_t n, int ch, int nchunks, int* list, int* count, hipStream_t st) {
+  if (ch <= 0 || nchunks <= 0 || (int64_t)ch * nchunks < n) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(lr_select_kernel, dim3(nchunks), dim3(256), 0, st, seed, step, thr, row_offset,
+                     n, ch, list, count);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t dalgo_lr_select_compact(const int* chunks, const int* counts, int ch, int nchunks,
+                                   int* list, int64_t* total, unsigned* claim, hipStream_t st) {
+  if (ch <= 0 || nchunks <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(lr_select_compact_kernel, dim3(nchunks), dim3(256), 0, st, chunks, counts, ch,
+                     list, total, claim);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
 }
 
 hipError_t dalgo_lr_eval(const void* X, const float* y, const float* W, const int64_t* seg,

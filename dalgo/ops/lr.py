@@ -45,6 +45,14 @@ LR_POOL_FRAC = float(os.environ.get("DALGO_LR_POOL", "0"))
 #                     (1.25M: 59.3/60.2 vs 59.6/59.0 us; 10M: 361.3 vs 361.4/362.9 us,
 #                     profiles/final/README.md), so the profiled 256 stays the default
 LR_RPB_ALIGN = max(4, int(os.environ.get("DALGO_LR_RPB_ALIGN", "256")) // 4 * 4)
+#   BALANCED        = sampled one-model launches take balanced slices of the step's
+#                     compacted selection (K7 on a side stream, one step ahead) instead of
+#                     walking static row ranges with in-register Bernoulli draws. Opt-in:
+#                     K1 itself is 2.7 us faster at 1.25M rows (46.1 vs 48.8 us, slices of
+#                     equal length), but the side-stream K7 does not overlap K1 on this
+#                     stack and the per-step event hand-offs cost more than that
+#                     (profiles/round3/README.md, "K1 balanced slices")
+LR_BALANCED = os.environ.get("DALGO_LR_LIST", "0") == "1"
 #   DETERMINISTIC   = combine per-block partials with the fixed-order two-level
 #                     hand-off (bitwise repeatable) instead of float atomics
 DETERMINISTIC = os.environ.get("DALGO_DETERMINISTIC", "0") == "1"
@@ -118,6 +126,106 @@ def _workspace(device, nseg, gx, S) -> _Workspace:
         )
         _ws_cache[key] = ws
     return ws
+
+
+class _Selection:
+    """Compacted per-step Bernoulli selections for balanced K1 slices (K7 off the K1 path).
+
+    The minibatch of step t is a pure function of (seed, t, global row), so it can be
+    drawn before step t's gradient: after each K1 launch the selection of step t + 1 is
+    built on a side stream (lr_select: per-chunk lists, lr_select_compact: one ascending
+    list + its length) and overlaps K1(t); K1(t + 1) waits for it with a stream event and
+    gives every block ``k`` consecutive entries. Two parity buffers; a buffer is rebuilt
+    only after the K1 that read it has finished (event). A step that was not prefetched
+    (first step, a jump after a restore) is built in order on the current stream.
+    ``k`` covers the mean plus two standard deviations of the binomial total, so the
+    overflow claimed at run time is rare and the last blocks are the short ones."""
+
+    def __init__(self, device, n: int, gx: int, frac: float, seed: int, row_offset: int):
+        self.n, self.gx, self.frac, self.seed, self.row_offset = n, gx, frac, seed, row_offset
+        self.ch = ((n + gx - 1) // gx + 3) // 4 * 4
+        self.nch = (n + self.ch - 1) // self.ch
+        mean = n * frac
+        sd = math.sqrt(max(n * frac * (1.0 - frac), 0.0))
+        self.k = max(1, int(math.ceil((mean + 2.0 * sd) / gx)))
+        size = max(gx * self.k, self.nch * self.ch, n) + 64
+        i32 = dict(dtype=torch.int32, device=device)
+        self.chunks = [torch.empty(self.nch * self.ch, **i32) for _ in range(2)]
+        self.counts = [torch.empty(self.nch, **i32) for _ in range(2)]
+        self.list = [torch.zeros(size, **i32) for _ in range(2)]
+        self.total = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(2)]
+        self.claim = [torch.zeros(1, **i32) for _ in range(2)]
+        self.ready = [None, None]      # step whose selection the buffer holds (enqueued)
+        self.used = [False, False]     # read by a K1 since it was built (claim is dirty)
+        self.ev_gen = [torch.cuda.Event(), torch.cuda.Event()]
+        self.ev_use = [torch.cuda.Event(), torch.cuda.Event()]
+        self.side = torch.cuda.Stream(device)
+        # the buffers were initialised on the current stream: side-stream builds follow it
+        self.side.wait_stream(torch.cuda.current_stream(device))
+
+    def _build(self, step: int, par: int, stream):
+        ops = _ext.ops()
+        with torch.cuda.stream(stream):
+            ops.lr_select(int(self.seed), int(step), float(self.frac), int(self.row_offset), self.n,
+                          self.ch, self.chunks[par], self.counts[par])
+            ops.lr_select_compact(self.chunks[par], self.counts[par], self.ch, self.list[par],
+                                  self.total[par], self.claim[par])
+            self.ev_gen[par].record(stream)
+        self.ready[par] = step
+        self.used[par] = False
+
+    def args(self, step: int) -> dict:
+        """Launch arguments of K1(step); call right before the launch."""
+        cur = torch.cuda.current_stream()
+        par = step & 1
+        if self.ready[par] != step:
+            if self.ready[par] is not None:
+                cur.wait_event(self.ev_gen[par])   # a side-stream build still writing it
+            self._build(step, par, cur)
+        else:
+            cur.wait_event(self.ev_gen[par])
+            if self.used[par]:
+                self.claim[par].zero_()            # the same step again: re-arm the claims
+        return dict(sel_list=self.list[par], sel_total=self.total[par], sel_k=self.k,
+                    sel_claim=self.claim[par])
+
+    def launched(self, step: int):
+        """After K1(step) is enqueued: prefetch step + 1 on the side stream."""
+        cur = torch.cuda.current_stream()
+        par = step & 1
+        self.ev_use[par].record(cur)
+        self.used[par] = True
+        nxt, q = step + 1, (step + 1) & 1
+        if self.ready[q] == nxt:
+            return
+        if self.used[q]:
+            self.side.wait_event(self.ev_use[q])    # the K1 that read buffer q is done
+        if self.ready[q] is not None:
+            self.side.wait_event(self.ev_gen[q])
+        self._build(nxt, q, self.side)
+
+
+_sel_cache: dict = {}
+
+
+def _selection(X, n, frac, seed, row_offset, det, w_prev, step_dev, var, nseg, pf, nsteps):
+    """The balanced-slice pipeline of this launch, or None when it does not apply."""
+    if not (LR_BALANCED and X.is_cuda and nseg == 1 and 0.0 < frac < 1.0 and not det
+            and w_prev is None and step_dev is None and pf == 0 and (var & 0xff) == 8
+            and nsteps <= 1 and n >= 1 and X.stride(0) * X.element_size() <= 2048):
+        return None
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    sel_rows = n * frac
+    gx = _TARGET_BLOCKS if sel_rows >= 32 * _TARGET_BLOCKS else max(1, int(math.ceil(sel_rows / 32)))
+    key = (str(X.device), n, gx, float(frac), int(seed), int(row_offset))
+    s = _sel_cache.get(key)
+    if s is None:
+        if len(_sel_cache) >= 8:
+            torch.cuda.synchronize(X.device)   # no launch may still use a dropped buffer
+            _sel_cache.clear()
+        s = _sel_cache[key] = _Selection(X.device, n, gx, float(frac), int(seed), int(row_offset))
+    return s
 
 
 def persistent_error() -> int:
@@ -216,6 +324,14 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
             var |= (LR_FINE_GROUPS & 0xff) << 16
         if not (var >> 24):
             var |= (LR_UNIT_SHIFT & 0xf) << 24
+        nsteps_ = int(tail.get("nsteps", 1)) if tail is not None else 1
+        selp = _selection(X, int(max_seg_rows), float(frac), seed, row_offset, det, w_prev,
+                          step_dev, var, nseg, pf, nsteps_)
+        sel = {}
+        if selp is not None:
+            gx = selp.gx
+            ws = _workspace(X.device, nseg, gx, S)
+            sel = selp.args(int(step))
         if tail is not None:
             if det or w_prev is not None or nseg != 1:
                 raise ValueError("fused tail needs the atomic epilogue, one model, no prologue update")
@@ -245,7 +361,9 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
                                tail_reg=int(tail.get("reg", 0)), tail_eta=float(tail.get("eta", 0.0)),
                                tail_lam=float(tail.get("lam", 0.0)),
                                tail_reg_alpha=float(tail.get("reg_alpha", 0.0)),
-                               tail_count_acc=tail.get("count_acc"), **kw, **pool)
+                               tail_count_acc=tail.get("count_acc"), **kw, **pool, **sel)
+            if selp is not None:
+                selp.launched(int(step))
             return G, C
         if not det and w_prev is None:
             if not g_is_zero:
@@ -257,7 +375,9 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
                            ws.cnt1, ws.cnt2, G, C, var,
                            w_prev, int(u.get("mode", 0)), int(u.get("reg", 0)),
                            float(u.get("eta", 0.0)), float(u.get("lam", 0.0)),
-                           float(u.get("reg_alpha", 0.0)), count_acc, **pool)
+                           float(u.get("reg_alpha", 0.0)), count_acc, **pool, **sel)
+        if selp is not None:
+            selp.launched(int(step))
         return G, C
     if w_prev is not None:
         from dalgo.ops import update as U

@@ -246,3 +246,74 @@ def test_lr_grad_persistent_steps(cuda, mode, reg, n):
     rel = ((w - w_ref).abs().max() / w_ref.abs().max()).item()
     assert rel < 1e-4, rel
 
+
+
+def _one_seg(n, D, dtype, cuda, seed=0):
+    X, y = _data(n, D, dtype, seed)
+    W = torch.randn(1, D + 1, generator=torch.Generator().manual_seed(3)) * 0.1
+    seg = torch.tensor([0, n], dtype=torch.int64)
+    return X, y, W, seg
+
+
+@pytest.mark.parametrize("dtype,D", [(torch.bfloat16, 1024), (torch.float32, 256), (torch.bfloat16, 30)])
+@pytest.mark.parametrize("row_offset", [0, 12345])
+def test_lr_grad_balanced_slices_match_reference(cuda, monkeypatch, dtype, D, row_offset):
+    """K1 LIST build (K7 selection one step ahead on a side stream) draws the same
+    minibatch as the CPU Philox reference, over consecutive steps, a repeated step
+    and a jump (the not-prefetched path)."""
+    monkeypatch.setattr(L, "LR_BALANCED", True)
+    L._sel_cache.clear()
+    n = 60_000
+    X, y, W, seg = _one_seg(n, D, dtype, cuda)
+    Xd, yd, Wd, sd = pad_features(X.to(cuda)), y.to(cuda), W.to(cuda), seg.to(cuda)
+    for step in [0, 1, 2, 2, 3, 9, 10]:
+        kw = dict(D=D, has_bias=True, eps=0.0, seed=42, step=step, frac=0.1, row_offset=row_offset)
+        G_ref, C_ref = L.lr_grad(pad_features(X).float(), y, W.double(), seg, **kw)
+        Gd, Cd = L.lr_grad(Xd, yd, Wd, sd, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(Cd.cpu().double(), C_ref), (step, Cd, C_ref)
+        err = (Gd.cpu().double() - G_ref).abs().max().item()
+        assert err / (G_ref.abs().max().item() + 1e-6) < 2e-5, (step, err)
+    assert len(L._sel_cache) == 1
+
+
+def test_lr_grad_balanced_slices_overflow_claims(cuda, monkeypatch):
+    """Per-block slices shorter than the step's selection: the entries past gx * k are
+    claimed at run time from the launch's counter (and re-armed for a repeated step)."""
+    monkeypatch.setattr(L, "LR_BALANCED", True)
+    L._sel_cache.clear()
+    n, D = 200_000, 256
+    X, y, W, seg = _one_seg(n, D, torch.bfloat16, cuda, seed=5)
+    Xd, yd, Wd, sd = pad_features(X.to(cuda)), y.to(cuda), W.to(cuda), seg.to(cuda)
+    kw = dict(D=D, has_bias=True, seed=7, frac=0.1)
+    L.lr_grad(Xd, yd, Wd, sd, step=0, **kw)
+    (selp,) = L._sel_cache.values()
+    selp.k = max(1, selp.k // 2)     # half of every block's share goes through the claims
+    for step in [1, 1, 2]:
+        G_ref, C_ref = L.lr_grad(pad_features(X).float(), y, W.double(), seg, step=step, **kw)
+        Gd, Cd = L.lr_grad(Xd, yd, Wd, sd, step=step, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(Cd.cpu().double(), C_ref), (step, Cd, C_ref)
+        err = (Gd.cpu().double() - G_ref).abs().max().item()
+        assert err / (G_ref.abs().max().item() + 1e-6) < 2e-5, (step, err)
+
+
+def test_lr_grad_balanced_slices_fused_tail(cuda, monkeypatch):
+    """One-kernel SSGD step (fused tail) on balanced slices equals the walk form."""
+    n, D = 100_000, 1024
+    X, y, W, seg = _one_seg(n, D, torch.bfloat16, cuda, seed=2)
+    Xd, yd, sd = pad_features(X.to(cuda)), y.to(cuda), seg.to(cuda)
+    out = {}
+    for bal in (False, True):
+        monkeypatch.setattr(L, "LR_BALANCED", bal)
+        L._sel_cache.clear()
+        Wd = W.to(cuda).clone()
+        G = torch.zeros_like(Wd)
+        C = torch.zeros(1, device=cuda)
+        for step in range(6):
+            L.lr_grad(Xd, yd, Wd, sd, D=D, seed=42, step=step, frac=0.1, G=G, C=C,
+                      tail=dict(mode=0, reg=0, eta=0.1), g_is_zero=True)
+        torch.cuda.synchronize()
+        out[bal] = Wd.cpu()
+    assert torch.allclose(out[False], out[True], rtol=1e-5, atol=1e-6), \
+        (out[False] - out[True]).abs().max()
