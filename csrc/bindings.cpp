@@ -616,6 +616,56 @@ void kmeans_move(const Tensor& X, int64_t DP, const Tensor& changed, int64_t m,
                   "kmeans_move");
 }
 
+// sort-based incremental K3 (workspace from the caller, see dalgo_kmeans_move_sorted)
+void kmeans_move_sorted(const Tensor& X, int64_t DP, const Tensor& changed, int64_t m,
+                        const Tensor& a_new, const Tensor& a_old, Tensor S64, Tensor cnt,
+                        const std::optional<Tensor>& xh, const std::optional<Tensor>& Q, int64_t seg,
+                        Tensor block_counts, Tensor cluster_start, Tensor seg_start, Tensor perm,
+                        Tensor ec, Tensor er) {
+  TORCH_CHECK(kmeans_dp(DP) == DP, "DP must be 16/32/64/128");
+  check_points(X, (int)DP);
+  check_dev(changed, "changed");
+  TORCH_CHECK(changed.scalar_type() == at::kInt && m >= 0 && m <= changed.numel(), "changed");
+  TORCH_CHECK(a_new.scalar_type() == at::kInt && a_old.scalar_type() == at::kInt &&
+                  a_new.numel() >= X.size(0) && a_old.numel() >= X.size(0), "assignments");
+  check_dev(S64, "S64");
+  TORCH_CHECK(S64.scalar_type() == at::kDouble && S64.is_contiguous(), "S64 f64");
+  TORCH_CHECK(cnt.scalar_type() == at::kLong && cnt.is_contiguous(), "cnt int64");
+  const int64_t k = S64.numel() / DP;
+  TORCH_CHECK(S64.numel() % DP == 0 && cnt.numel() >= k, "S64 [k, DP] / cnt [k]");
+  TORCH_CHECK(xh.has_value() == Q.has_value(), "kmeans_move_sorted: xh and Q together");
+  const float* xp = nullptr;
+  double* qp = nullptr;
+  if (Q.has_value()) {
+    check_f32(*xh, "xh");
+    TORCH_CHECK(xh->numel() >= X.size(0), "xh [n]");
+    check_dev(*Q, "Q");
+    TORCH_CHECK(Q->scalar_type() == at::kDouble && Q->numel() >= k && Q->is_contiguous(), "Q f64 [k]");
+    xp = xh->data_ptr<float>();
+    qp = Q->data_ptr<double>();
+  }
+  for (const Tensor* t : {&block_counts, &perm, &ec, &er}) {
+    check_dev(*t, "workspace");
+    TORCH_CHECK(t->scalar_type() == at::kInt && t->is_contiguous(), "int32 workspace");
+  }
+  check_dev(cluster_start, "cluster_start");
+  check_dev(seg_start, "seg_start");
+  TORCH_CHECK(cluster_start.scalar_type() == at::kLong && seg_start.scalar_type() == at::kLong &&
+                  cluster_start.numel() >= k + 1 && seg_start.numel() >= k + 1, "starts int64 [k+1]");
+  TORCH_CHECK(perm.numel() >= 2 * m && ec.numel() >= 2 * m && er.numel() >= 2 * m, "[2m] workspace");
+  const int64_t B = block_counts.numel() / std::max<int64_t>(k, 1);
+  TORCH_CHECK(B >= 1 && seg >= 1, "block_counts [B * k], seg >= 1");
+  DeviceGuard guard(X.device());
+  DALGO_CHECK_HIP(dalgo_kmeans_move_sorted(
+                      X.data_ptr(), X.scalar_type() == at::kBFloat16, X.stride(0), (int)DP,
+                      changed.data_ptr<int32_t>(), m, a_new.data_ptr<int32_t>(), a_old.data_ptr<int32_t>(),
+                      (int)k, (int)std::min<int64_t>(B, 1 << 20), (int)seg, ec.data_ptr<int>(), er.data_ptr<int>(),
+                      block_counts.data_ptr<int>(), cluster_start.data_ptr<int64_t>(),
+                      seg_start.data_ptr<int64_t>(), perm.data_ptr<int>(), S64.data_ptr<double>(),
+                      reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>()), xp, qp, cur_stream()),
+                  "kmeans_move_sorted");
+}
+
 // bound-filtered Lloyd: active rows (u + delta[a] >= s[a]) -> idx, their assignment -> a_prev
 void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta, const Tensor& s,
                    const Tensor& maxd, Tensor a_prev, Tensor idx, Tensor n_active) {
@@ -1177,6 +1227,10 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("kmeans_assign_cs(Tensor X, Tensor Cq, Tensor hn, Tensor? xh, float M, Tensor(a!) assign, "
         "Tensor(b!)? mind, Tensor(c!)? sse) -> ()");
   m.def("kmeans_diff(Tensor a_new, Tensor a_old, Tensor(a!) changed, Tensor(b!) n_changed) -> ()");
+  m.def("kmeans_move_sorted(Tensor X, int DP, Tensor changed, int m, Tensor a_new, Tensor a_old, "
+        "Tensor(a!) S64, Tensor(b!) cnt, Tensor? xh, Tensor(c!)? Q, int seg, Tensor(d!) block_counts, "
+        "Tensor(e!) cluster_start, Tensor(f!) seg_start, Tensor(g!) perm, Tensor(h!) ec, "
+        "Tensor(i!) er) -> ()");
   m.def("kmeans_move(Tensor X, int DP, Tensor changed, int m, Tensor a_new, Tensor a_old, "
         "Tensor(a!) S64, Tensor(b!) cnt, Tensor? xh=None, Tensor(c!)? Q=None) -> ()");
   m.def("kmeans_filter(Tensor assign, Tensor(a!) u, Tensor(e!) l, Tensor delta, Tensor s, Tensor maxd, "
@@ -1263,6 +1317,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("kmeans_diff", &kmeans_diff);
   m.impl("kmeans_assign_cs", &kmeans_assign_cs);
   m.impl("kmeans_move", &kmeans_move);
+  m.impl("kmeans_move_sorted", &kmeans_move_sorted);
   m.impl("kmeans_filter", &kmeans_filter);
   m.impl("kmeans_post", &kmeans_post);
   m.impl("kmeans_qsum", &kmeans_qsum);

@@ -1126,6 +1126,101 @@ kmeans_segsum_kernel(const T* __restrict__ X, int64_t ldx, const int* __restrict
   }
 }
 
+// Incremental K3, sort-based (moved rows only). Entry e < m adds row changed[e] to its
+// new cluster, entry m + e subtracts it from its old one. The entries are counting-sorted
+// by cluster with the K3 kernels above, then every wave sums a run of <= SEG entries of
+// one cluster in f64 registers (signed) and adds it once to S64 / cnt / Q: ~(2m/SEG + k)
+// d-vector atomics instead of 2 per moved row and feature (km_move, kmeans_inc.hip).
+__global__ void __launch_bounds__(256)
+km_dexpand_kernel(const int32_t* __restrict__ changed, int64_t m, const int32_t* __restrict__ a_new,
+                  const int32_t* __restrict__ a_old, int* __restrict__ ec, int* __restrict__ er) {
+  const int64_t n2 = 2 * m;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n2;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const bool add = e < m;
+    const int row = changed[add ? e : e - m];
+    ec[e] = add ? a_new[row] : a_old[row];
+    er[e] = add ? row : ~row;          // negative: subtract
+  }
+}
+
+template <typename T, int DP, int NW>
+__global__ void __launch_bounds__(NW * 64)
+km_dsegsum_kernel(const T* __restrict__ X, int64_t ldx, const int* __restrict__ perm,
+                  const int* __restrict__ er, const int64_t* __restrict__ cluster_start,
+                  const int64_t* __restrict__ seg_start, int k, int seg, double* __restrict__ S,
+                  unsigned long long* __restrict__ cnt, const float* __restrict__ xh,
+                  double* __restrict__ Q) {
+  constexpr int EPL = DP >= 64 ? DP / 64 : 1;
+  constexpr int kNone = (int)0x80000000;
+  const int lane = threadIdx.x & 63;
+  const int64_t nseg = seg_start[k];
+  const bool lane_on = (DP >= 64) || (lane < DP);
+  for (int64_t sid = (int64_t)blockIdx.x * NW + (threadIdx.x >> 6); sid < nseg;
+       sid += (int64_t)gridDim.x * NW) {
+    int lo = 0, hi = k - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (seg_start[mid] <= sid) lo = mid; else hi = mid - 1;
+    }
+    const int c = lo;
+    const int64_t r0 = cluster_start[c] + (sid - seg_start[c]) * (int64_t)seg;
+    const int64_t r1 = min(cluster_start[c + 1], r0 + seg);
+    double acc[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) acc[e] = 0.0;
+    int csum = 0;
+    double qsum = 0.0;
+    int code = (r0 + lane < r1) ? er[perm[r0 + lane]] : kNone;
+    for (int64_t i = r0; i < r1; i += 64) {
+      const int nxt = (i + 64 + lane < r1) ? er[perm[i + 64 + lane]] : kNone;
+      if (code != kNone) {
+        const int row = code < 0 ? ~code : code;
+        csum += code < 0 ? -1 : 1;
+        if (Q != nullptr) qsum += (code < 0 ? -2.0 : 2.0) * (double)xh[row];
+      }
+#pragma unroll
+      for (int u0 = 0; u0 < 64; u0 += 16) {
+        float v[16][EPL];
+        float sg[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int cu = __builtin_amdgcn_readlane(code, u0 + u);
+          const int row = cu == kNone ? 0 : (cu < 0 ? ~cu : cu);
+          sg[u] = cu == kNone ? 0.f : (cu < 0 ? -1.f : 1.f);
+          const T* rp = X + (int64_t)row * ldx + lane * EPL;
+#pragma unroll
+          for (int e = 0; e < EPL; ++e) {
+            float x = 0.f;
+            if constexpr (sizeof(T) == 2) x = bf16_to_f32(reinterpret_cast<const uint16_t*>(rp)[e]);
+            else x = reinterpret_cast<const float*>(rp)[e];
+            v[u][e] = lane_on ? x : 0.f;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+#pragma unroll
+          for (int e = 0; e < EPL; ++e) acc[e] += (double)(sg[u] * v[u][e]);
+      }
+      code = nxt;
+    }
+    if (lane_on) {
+#pragma unroll
+      for (int e = 0; e < EPL; ++e)
+        if (acc[e] != 0.0) atomicAdd(&S[(int64_t)c * DP + lane * EPL + e], acc[e]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      csum += __shfl_xor(csum, o, 64);
+      qsum += __shfl_xor(qsum, o, 64);
+    }
+    if (lane == 0) {
+      if (csum != 0) atomicAdd(&cnt[c], (unsigned long long)(long long)csum);
+      if (Q != nullptr && qsum != 0.0) atomicAdd(&Q[c], qsum);
+    }
+  }
+}
+
 }  // namespace dalgo
 
 using namespace dalgo;
@@ -1412,6 +1507,50 @@ hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n,
   const int64_t max_segs = cdiv(n, seg) + k;
   return is_bf16 ? launch_segsum<uint16_t>(DP, X, ldx, perm, cluster_start, seg_start, k, seg, max_segs, S, st)
                  : launch_segsum<float>(DP, X, ldx, perm, cluster_start, seg_start, k, seg, max_segs, S, st);
+}
+
+// Sort-based incremental K3 over the m moved rows (2m signed entries). Workspace:
+// ec / er / perm int32[2m], block_counts int32[B*k], cluster_start / seg_start int64[k+1].
+hipError_t dalgo_kmeans_move_sorted(const void* X, int is_bf16, int64_t ldx, int DP,
+                                    const int32_t* changed, int64_t m, const int32_t* a_new,
+                                    const int32_t* a_old, int k, int B, int seg, int* ec, int* er,
+                                    int* block_counts, int64_t* cluster_start, int64_t* seg_start,
+                                    int* perm, double* S, unsigned long long* cnt, const float* xh,
+                                    double* Q, hipStream_t st) {
+  if (m <= 0) return hipSuccess;
+  const int64_t n2 = 2 * m;
+  if (k < 1 || k > kScKmax || B < 1 || seg < 1 || n2 >= (int64_t)0x7fffffff) return hipErrorInvalidValue;
+  const int g = (int)std::min<int64_t>(cdiv(n2, 256), 4096);
+  hipLaunchKernelGGL(km_dexpand_kernel, dim3(g), dim3(256), 0, st, changed, m, a_new, a_old, ec, er);
+  DALGO_LAUNCH_CHECK();
+  const int64_t rpc = cdiv(n2, B);
+  const size_t lds_k = (size_t)k * sizeof(int);
+  hipLaunchKernelGGL(kmeans_hist_kernel, dim3(B), dim3(256), lds_k, st, (const int*)ec, n2, rpc, k,
+                     block_counts);
+  DALGO_LAUNCH_CHECK();
+  hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), 2 * lds_k, st, block_counts, B, k, seg,
+                     cluster_start, seg_start, (unsigned long long*)nullptr);
+  DALGO_LAUNCH_CHECK();
+  hipLaunchKernelGGL(kmeans_scatter_chunked_kernel, dim3(B), dim3(kScNT), 0, st, (const int*)ec, n2,
+                     rpc, k, (const int*)block_counts, (const int64_t*)cluster_start, perm);
+  DALGO_LAUNCH_CHECK();
+  constexpr int NW = 4;
+  const int64_t max_segs = cdiv(n2, seg) + k;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(max_segs, NW), 256 * 16));
+#define DALGO_DSEG(TT, D)                                                                        \
+  hipLaunchKernelGGL((km_dsegsum_kernel<TT, D, NW>), dim3(grid), dim3(NW * 64), 0, st,           \
+                     (const TT*)X, ldx, (const int*)perm, (const int*)er, (const int64_t*)cluster_start, \
+                     (const int64_t*)seg_start, k, seg, S, cnt, xh, Q)
+  switch (DP) {
+    case 16: if (is_bf16) DALGO_DSEG(uint16_t, 16); else DALGO_DSEG(float, 16); break;
+    case 32: if (is_bf16) DALGO_DSEG(uint16_t, 32); else DALGO_DSEG(float, 32); break;
+    case 64: if (is_bf16) DALGO_DSEG(uint16_t, 64); else DALGO_DSEG(float, 64); break;
+    case 128: if (is_bf16) DALGO_DSEG(uint16_t, 128); else DALGO_DSEG(float, 128); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef DALGO_DSEG
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
 }
 
 hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,

@@ -86,6 +86,12 @@ hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ld
 hipError_t dalgo_kmeans_accumulate(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
                                    const int* assign, int k, float* S, unsigned long long* cnt,
                                    hipStream_t st);
+hipError_t dalgo_kmeans_move_sorted(const void* X, int is_bf16, int64_t ldx, int DP,
+                                    const int32_t* changed, int64_t m, const int32_t* a_new,
+                                    const int32_t* a_old, int k, int B, int seg, int* ec, int* er,
+                                    int* block_counts, int64_t* cluster_start, int64_t* seg_start,
+                                    int* perm, double* S, unsigned long long* cnt, const float* xh,
+                                    double* Q, hipStream_t st);
 hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
                                           const int* assign, int k, int B, int seg, int* block_counts,
                                           int64_t* cluster_start, int64_t* seg_start, int* perm,

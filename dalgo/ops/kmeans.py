@@ -8,6 +8,7 @@ with DP = d rounded up to 16/32/64/128 and kpad = k rounded up to 32.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -258,11 +259,44 @@ def changed_rows(a_new: torch.Tensor, a_old: torch.Tensor, changed: torch.Tensor
     return int(n_changed.item())
 
 
+# moved rows from which the incremental K3 counting-sorts its signed entries by cluster
+# (below: one wave per row with f64 atomics per feature, cheaper for few rows)
+MOVE_SORTED_MIN = int(os.environ.get("DALGO_KM_MOVE_SORTED_MIN", "16384"))
+_mws: dict = {}
+
+
+def _move_ws(device, m: int, k: int):
+    cap = 1 << max(16, (2 * m - 1).bit_length())
+    key = (str(device), k)
+    ws = _mws.get(key)
+    if ws is None or ws["cap"] < cap:
+        bmax = max(1, min(4096, (cap + CHUNK_ROWS - 1) // CHUNK_ROWS))
+        i32 = dict(dtype=torch.int32, device=device)
+        ws = dict(cap=cap, perm=torch.empty(cap, **i32), ec=torch.empty(cap, **i32),
+                  er=torch.empty(cap, **i32), block_counts=torch.empty(bmax * k, **i32),
+                  cluster_start=torch.empty(k + 1, dtype=torch.int64, device=device),
+                  seg_start=torch.empty(k + 1, dtype=torch.int64, device=device))
+        _mws[key] = ws
+    return ws
+
+
 def move_rows(X: torch.Tensor, DP: int, changed: torch.Tensor, m: int, a_new: torch.Tensor,
               a_old: torch.Tensor, S64: torch.Tensor, cnt: torch.Tensor,
               xh: torch.Tensor | None = None, Q: torch.Tensor | None = None):
     """Incremental K3: S64[a_new[r]] += x_r, S64[a_old[r]] -= x_r (f64), counts likewise
-    (and Q, the per-cluster sum of |x|^2 = 2 xh, when given), for the m changed rows r."""
+    (and Q, the per-cluster sum of |x|^2 = 2 xh, when given), for the m changed rows r.
+
+    From MOVE_SORTED_MIN rows on, the 2m signed entries are counting-sorted by cluster
+    (the K3 hist / scan / scatter kernels) and every wave adds a run of <= SEG_ROWS of them
+    in f64 registers: ~(2m / SEG_ROWS + k) d-vector atomics instead of 2 * d per row."""
+    k = S64.numel() // int(DP)
+    if m >= MOVE_SORTED_MIN and k <= 2048:
+        ws = _move_ws(X.device, int(m), k)
+        B = max(1, min(4096, (2 * int(m) + CHUNK_ROWS - 1) // CHUNK_ROWS))
+        _ext.ops().kmeans_move_sorted(X, int(DP), changed, int(m), a_new, a_old, S64, cnt, xh, Q,
+                                      SEG_ROWS, ws["block_counts"][: B * k], ws["cluster_start"],
+                                      ws["seg_start"], ws["perm"], ws["ec"], ws["er"])
+        return
     _ext.ops().kmeans_move(X, int(DP), changed, int(m), a_new, a_old, S64, cnt, xh, Q)
 
 

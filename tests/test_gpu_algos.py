@@ -576,6 +576,39 @@ def test_kmeans_incremental_accumulate_exact(cuda, d, dtype):
     assert len(km.changed_history) == 5 and km.changed_history[0] > 0
 
 
+@pytest.mark.parametrize("d,dtype,k,m", [(128, torch.bfloat16, 1024, 300_000),
+                                         (64, torch.bfloat16, 96, 40_000),
+                                         (30, torch.float32, 2048, 20_000)])
+def test_kmeans_move_sorted_equals_atomic(cuda, monkeypatch, d, dtype, k, m):
+    """Sort-based incremental K3 (signed entries counting-sorted by cluster, f64 run sums)
+    == the per-row f64-atomic form: sums, counts and the |x|^2 sums Q."""
+    from dalgo.ops import kmeans as K
+    n = 500_000
+    g = torch.Generator().manual_seed(3)
+    X = K.prepare_points((torch.randn(n, d, generator=g) * 3).to(dtype).to(cuda))
+    DP = K.kmeans_dp(d)
+    a_old = torch.randint(0, k, (n,), generator=g, dtype=torch.int32).to(cuda)
+    a_new = a_old.clone()
+    rows = torch.randperm(n, generator=g)[:m].to(cuda)
+    a_new[rows] = torch.randint(0, k, (m,), generator=g, dtype=torch.int32).to(cuda)
+    changed = torch.sort(rows.to(torch.int32)).values
+    xh = (torch.rand(n, generator=g) * 10).to(cuda)
+    out = []
+    for thr in (1 << 40, 1):
+        monkeypatch.setattr(K, "MOVE_SORTED_MIN", thr)
+        S = torch.zeros(k, DP, dtype=torch.float64, device=cuda)
+        c = torch.zeros(k, dtype=torch.int64, device=cuda)
+        Q = torch.zeros(k, dtype=torch.float64, device=cuda)
+        K.move_rows(X, DP, changed, m, a_new, a_old, S, c, xh, Q)
+        torch.cuda.synchronize()
+        out.append((S, c, Q))
+    (S0, c0, Q0), (S1, c1, Q1) = out
+    assert torch.equal(c0, c1)
+    assert int(c1.sum().item()) == 0
+    assert torch.allclose(S0, S1, rtol=1e-12, atol=1e-9), (S0 - S1).abs().max()
+    assert torch.allclose(Q0, Q1, rtol=1e-12, atol=1e-6), (Q0 - Q1).abs().max()
+
+
 @pytest.mark.parametrize("sem", ["reference", "standard"])
 @pytest.mark.parametrize("scale,edges", [(12, 100_000), (17, 3_000_000)])
 def test_pagerank_xcd_spmv_matches_cpu(cuda, sem, scale, edges):
