@@ -11,14 +11,18 @@
 // iteration (0.86 % -> 0.06 % on the 1024-blob benchmark data), so the
 // 25.6 GB re-read of X in the full K3 pass becomes a pass over the two
 // assignment vectors (0.8 GB) plus ~1-2 KB of f64 atomics per moved point.
-// The caller falls back to the full pass when the changed share is large.
+// The caller falls back to the full pass when the changed share is large (25 %).
 //
 //   km_diff    : compare a_new / a_old, append the changed row ids through a
 //                per-block LDS buffer (one global atomic per block flush)
 //   km_move    : one wave per changed row: the row's DP features (bf16 / f32, one
 //                256-B or 512-B coalesced read) are added to S[a_new] and
 //                subtracted from S[a_old] with f64 atomics shaped as contiguous
-//                512-B wave instructions; lane 0 moves the counts.
+//                512-B wave instructions; lane 0 moves the counts. Used below 16k
+//                moved rows: at 100M points its 2 * DP device-scope f64 atomics per
+//                row cost ~3 ms per million moved rows, so larger moves go through
+//                the counting-sorted form in kmeans.hip (km_dexpand / km_dsegsum:
+//                ~0.1 ms per million signed entries).
 #include "dalgo/common.h"
 
 namespace dalgo {
