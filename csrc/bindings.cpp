@@ -828,49 +828,69 @@ void pr_spmv(const Tensor& src, const Tensor& dstl, const Tensor& c, Tensor acc,
                   "pr_spmv");
 }
 
-// Propagation-blocked SpMV. The layout invariants (slot < val.numel(), src < c.numel(),
-// dloc < bin_width, chunk bounds inside val) are established and asserted once when
-// dalgo.ops.graph.build_blocked() creates the layout; here shapes/dtypes are checked.
-void pb_spmv(const Tensor& psrc, const Tensor& ppos, const Tensor& c, Tensor val, const Tensor& dloc,
-             const Tensor& chunk_lo4, const Tensor& chunk_bin, const Tensor& chunk_slab,
-             int64_t bin_width, Tensor acc, Tensor pres, Tensor slab, const Tensor& split_bin,
-             const Tensor& split_first, const Tensor& split_count) {
-  check_i32(psrc, "psrc");
-  check_i32(ppos, "ppos");
-  TORCH_CHECK(psrc.numel() == ppos.numel() && psrc.numel() % 4 == 0, "pb: src/pos equal, % 4");
+// K4b two-level propagation-blocked SpMV. The layout invariants (tile / entry / run
+// offsets inside the arrays, chunk source ranges inside c, dloc < bin_width) are
+// established and asserted once by dalgo.ops.graph.build_blocked(); here the shapes,
+// dtypes and the bounds a kernel could overrun are checked.
+void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
+             const Tensor& tile_run, const Tensor& chunk_tile, const Tensor& chunk_slo,
+             const Tensor& chunk_ns, const Tensor& chunk_run, const Tensor& run_delta,
+             const Tensor& c, Tensor val, const Tensor& dloc, const Tensor& wi_bin,
+             const Tensor& wi_lo, const Tensor& wi_slab, int64_t bin_width, int64_t fixed_bits,
+             Tensor acc, Tensor pres, Tensor slab, const Tensor& split_bin, const Tensor& split_first,
+             const Tensor& split_count) {
+  check_dev(srcl, "srcl");
+  TORCH_CHECK(srcl.scalar_type() == at::kShort && srcl.is_contiguous() && srcl.numel() % 16 == 0,
+              "pb: srcl int16, len % 16 == 0");
+  check_dev(tile_e, "tile_e");
+  TORCH_CHECK(tile_e.scalar_type() == at::kLong && tile_e.is_contiguous(), "tile_e int64");
+  for (const Tensor* t : {&tile_ent, &tile_run, &chunk_tile, &chunk_slo, &chunk_ns, &chunk_run,
+                          &run_delta})
+    check_i32(*t, "pb index arrays");
+  const int64_t nch = chunk_slo.numel();
+  const int64_t nt = tile_ent.numel();
+  TORCH_CHECK(chunk_ns.numel() == nch && chunk_tile.numel() == nch + 1 && chunk_run.numel() == nch + 1 &&
+                  tile_e.numel() == nt + 1 && tile_run.numel() == nt,
+              "pb: chunk / tile arrays");
   check_f32(c, "c");
   check_f32(val, "val");
   check_dev(dloc, "dloc");
   TORCH_CHECK(dloc.scalar_type() == at::kShort && dloc.is_contiguous() && dloc.numel() == val.numel() &&
-                  val.numel() % 4 == 0, "pb: dloc int16[len(val)], len % 4 == 0");
-  check_dev(chunk_lo4, "chunk_lo4");
-  TORCH_CHECK(chunk_lo4.scalar_type() == at::kLong && chunk_lo4.is_contiguous(), "chunk_lo4 int64");
-  check_i32(chunk_bin, "chunk_bin");
-  check_i32(chunk_slab, "chunk_slab");
-  const int64_t nch = chunk_bin.numel();
-  TORCH_CHECK(chunk_slab.numel() == nch && chunk_lo4.numel() == nch + 1, "pb: chunk arrays");
+                  val.numel() % 4 == 0,
+              "pb: dloc int16[len(val)], len % 4 == 0");
+  check_i32(wi_bin, "wi_bin");
+  check_i32(wi_slab, "wi_slab");
+  check_dev(wi_lo, "wi_lo");
+  TORCH_CHECK(wi_lo.scalar_type() == at::kLong && wi_lo.is_contiguous(), "wi_lo int64");
+  const int64_t nwi = wi_bin.numel();
+  TORCH_CHECK(wi_lo.numel() == nwi + 1 && wi_slab.numel() == nwi, "pb: work items");
   check_f32(acc, "acc");
   check_i32(pres, "pres");
   TORCH_CHECK(pres.numel() >= acc.numel(), "pres size");
-  check_f32(slab, "slab");
+  check_dev(slab, "slab");
+  TORCH_CHECK(slab.scalar_type() == at::kLong && slab.is_contiguous(), "pb: slab int64 (u64 fixed point)");
   check_i32(split_bin, "split_bin");
   check_i32(split_first, "split_first");
   check_i32(split_count, "split_count");
   const int64_t nsp = split_bin.numel();
   TORCH_CHECK(split_first.numel() == nsp && split_count.numel() == nsp, "pb: split arrays");
-  for (const Tensor* t : {&psrc, &ppos, static_cast<const Tensor*>(&val), &dloc})
+  for (const Tensor* t : {&srcl, static_cast<const Tensor*>(&val), &dloc})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "pb arrays 16-B aligned");
-  DeviceGuard guard(psrc.device());
-  DALGO_CHECK_HIP(dalgo_pb_spmv(psrc.data_ptr<int32_t>(), ppos.data_ptr<int32_t>(), psrc.numel(),
-                                c.data_ptr<float>(), val.data_ptr<float>(),
-                                reinterpret_cast<const uint16_t*>(dloc.data_ptr<int16_t>()),
-                                chunk_lo4.data_ptr<int64_t>(), chunk_bin.data_ptr<int32_t>(),
-                                chunk_slab.data_ptr<int32_t>(), (int)nch, (int)bin_width,
-                                acc.numel(), acc.data_ptr<float>(), pres.data_ptr<int32_t>(),
-                                slab.data_ptr<float>(), split_bin.data_ptr<int32_t>(),
-                                split_first.data_ptr<int32_t>(), split_count.data_ptr<int32_t>(),
-                                (int)nsp, cur_stream()),
-                  "pb_spmv");
+  DeviceGuard guard(srcl.device());
+  DALGO_CHECK_HIP(
+      dalgo_pb_spmv(reinterpret_cast<const uint16_t*>(srcl.data_ptr<int16_t>()),
+                    tile_e.data_ptr<int64_t>(), tile_ent.data_ptr<int32_t>(), tile_run.data_ptr<int32_t>(),
+                    chunk_tile.data_ptr<int32_t>(), chunk_slo.data_ptr<int32_t>(),
+                    chunk_ns.data_ptr<int32_t>(), chunk_run.data_ptr<int32_t>(),
+                    run_delta.data_ptr<int32_t>(), (int)nch, 8192, c.data_ptr<float>(),
+                    val.data_ptr<float>(), reinterpret_cast<const uint16_t*>(dloc.data_ptr<int16_t>()),
+                    wi_bin.data_ptr<int32_t>(), wi_lo.data_ptr<int64_t>(), wi_slab.data_ptr<int32_t>(),
+                    (int)nwi, (int)bin_width, (int)fixed_bits, acc.numel(), acc.data_ptr<float>(),
+                    pres.data_ptr<int32_t>(), reinterpret_cast<uint64_t*>(slab.data_ptr<int64_t>()),
+                    split_bin.data_ptr<int32_t>(),
+                    split_first.data_ptr<int32_t>(), split_count.data_ptr<int32_t>(), (int)nsp,
+                    cur_stream()),
+      "pb_spmv");
 }
 
 // XCD-partitioned K4: 8 source-line parts (dalgo.ops.graph.build_xcd), per-part sums
@@ -1244,9 +1264,11 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(d!)? shift2) -> ()");
   m.def("rmat_edges(int seed, int scale, int e_off, float a, float b, float c, bool scramble, "
         "Tensor(a!) src, Tensor(b!) dst) -> ()");
-  m.def("pb_spmv(Tensor psrc, Tensor ppos, Tensor c, Tensor(a!) val, Tensor dloc, Tensor chunk_lo4, "
-        "Tensor chunk_bin, Tensor chunk_slab, int bin_width, Tensor(b!) acc, Tensor(c!) pres, "
-        "Tensor(d!) slab, Tensor split_bin, Tensor split_first, Tensor split_count) -> ()");
+  m.def("pb_spmv(Tensor srcl, Tensor tile_e, Tensor tile_ent, Tensor tile_run, Tensor chunk_tile, "
+        "Tensor chunk_slo, Tensor chunk_ns, Tensor chunk_run, Tensor run_delta, Tensor c, "
+        "Tensor(a!) val, Tensor dloc, Tensor wi_bin, Tensor wi_lo, Tensor wi_slab, int bin_width, "
+        "int fixed_bits, Tensor(b!) acc, Tensor(c!) pres, Tensor(d!) slab, Tensor split_bin, Tensor split_first, "
+        "Tensor split_count) -> ()");
   m.def("pr_spmv(Tensor src, Tensor dstl, Tensor c, Tensor(a!) acc, Tensor(b!) pres, "
         "bool accumulate=False) -> ()");
   m.def("pr_spmv_xcd(Tensor src, Tensor dstl, Tensor part_base, int e_max, Tensor c, "

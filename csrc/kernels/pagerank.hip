@@ -404,131 +404,6 @@ pr_update_kernel(const float* __restrict__ acc, const int32_t* __restrict__ pres
   }
 }
 
-// ---------------------------------------------------------------------------
-// Propagation-blocked SpMV (same result as pr_spmv, no random gathers of c):
-//   phase 1 (pb_scatter): stream the edges in SOURCE order; c[src] is then read
-//     nearly sequentially, and each value is written to the edge's slot in a
-//     destination-binned array. Within a bin the slots are in source order too,
-//     so the ~B active write fronts advance sequentially and coalesce in L2.
-//   phase 2 (pb_accumulate): one workgroup per chunk of a bin; the bin's
-//     destination range (BW vertices) is accumulated in LDS (ds_add_f32), then
-//     stored (single-chunk bin) or atomically added (bins split across chunks).
-// Per edge: 8 B (src, slot) + 4 B value write + 4 B value read + 2 B local dst,
-// all streamed; vs. one 64-B line fetch per random gather in the pull form.
-// Padding slots hold -1 (never written by phase 1) and are skipped.
-// Edge ranges are split per XCD (blocks are dispatched round-robin over the 8
-// XCDs): XCD k sweeps its own contiguous source range, so each bin's slots for
-// that range (contiguous, slots are in source order) are only ever written
-// through one L2, and the XCD's CUs advance together (grid-stride inside the
-// range) so the ~#bins active write lines stay resident until complete.
-__global__ void __launch_bounds__(256)
-pb_scatter_kernel(const int4* __restrict__ src4, const int4* __restrict__ pos4, int64_t n4,
-                  const float* __restrict__ c, float* __restrict__ val) {
-  constexpr int U = 4;
-  const int xcd = blockIdx.x % kXcds;
-  const int64_t bpx = gridDim.x / kXcds;                  // blocks per XCD
-  const int64_t per = (n4 + kXcds - 1) / kXcds;
-  const int64_t lo = xcd * per, hi = min(n4, lo + per);
-  const int64_t stride = bpx * blockDim.x;
-  for (int64_t i0 = lo + (blockIdx.x / kXcds) * blockDim.x + threadIdx.x; i0 < hi; i0 += U * stride) {
-    int4 sv[U], pv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = min(i0 + u * stride, hi - 1);
-      sv[u] = src4[i];
-      pv[u] = pos4[i];
-      if (i0 + u * stride >= hi) sv[u] = make_int4(-1, -1, -1, -1);
-    }
-    float cv[U][4];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      cv[u][0] = c[max(sv[u].x, 0)];
-      cv[u][1] = c[max(sv[u].y, 0)];
-      cv[u][2] = c[max(sv[u].z, 0)];
-      cv[u][3] = c[max(sv[u].w, 0)];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (sv[u].x >= 0) val[pv[u].x] = cv[u][0];
-      if (sv[u].y >= 0) val[pv[u].y] = cv[u][1];
-      if (sv[u].z >= 0) val[pv[u].z] = cv[u][2];
-      if (sv[u].w >= 0) val[pv[u].w] = cv[u][3];
-    }
-  }
-}
-
-// Presence without a second LDS array: the accumulator starts at -0.0f; adding
-// any contribution v >= +0 yields a value with the sign bit clear (-0 + +0 = +0),
-// so "received >= 1 record" == !signbit(acc) and each edge costs one ds_add_f32.
-template <int BW>
-__global__ void __launch_bounds__(1024)
-pb_accumulate_kernel(const float4* __restrict__ val4, const uint2* __restrict__ dloc4,
-                     const int64_t* __restrict__ chunk_lo4, const int32_t* __restrict__ chunk_bin,
-                     const int32_t* __restrict__ chunk_slab, int64_t n_local,
-                     float* __restrict__ acc, int32_t* __restrict__ pres,
-                     float* __restrict__ slab) {
-  constexpr int U = 4;
-  __shared__ float s_acc[BW];
-  const int ch = blockIdx.x;
-  for (int i = threadIdx.x; i < BW; i += blockDim.x) s_acc[i] = -0.0f;
-  __syncthreads();
-  const int64_t lo = chunk_lo4[ch], hi = chunk_lo4[ch + 1];   // in units of 4 slots
-  for (int64_t j0 = lo + threadIdx.x; j0 < hi; j0 += U * blockDim.x) {
-    float4 v[U];
-    uint2 d[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {           // all loads first: U x 24 B in flight per lane
-      const int64_t j = min(j0 + u * (int64_t)blockDim.x, hi - 1);
-      v[u] = val4[j];
-      d[u] = dloc4[j];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (j0 + u * (int64_t)blockDim.x >= hi) continue;
-      const float f[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-      const uint32_t k[4] = {d[u].x & 0xffffu, d[u].x >> 16, d[u].y & 0xffffu, d[u].y >> 16};
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (f[e] >= 0.f) atomicAdd(&s_acc[k[e]], f[e]);
-    }
-  }
-  __syncthreads();
-  const int64_t base = (int64_t)chunk_bin[ch] * BW;
-  const int nb = (int)min((int64_t)BW, n_local - base);
-  const int sl = chunk_slab[ch];
-  if (sl < 0) {                       // the bin's only chunk: final values
-    for (int i = threadIdx.x; i < nb; i += blockDim.x) {
-      const float a = s_acc[i];
-      const bool hit = !signbit(a);
-      acc[base + i] = hit ? a : 0.f;
-      pres[base + i] = hit ? 1 : 0;
-    }
-  } else {                            // partial of a split bin -> its slab (combined in order)
-    float* dst = slab + (int64_t)sl * BW;
-    for (int i = threadIdx.x; i < BW; i += blockDim.x) dst[i] = s_acc[i];
-  }
-}
-
-// Split bins: sum the chunk partials in chunk order (deterministic; no atomics on
-// the hot destinations, whose bins are exactly the ones split into many chunks).
-template <int BW>
-__global__ void __launch_bounds__(256)
-pb_combine_kernel(const float* __restrict__ slab, const int32_t* __restrict__ split_bin,
-                  const int32_t* __restrict__ split_first, const int32_t* __restrict__ split_count,
-                  int64_t n_local, float* __restrict__ acc, int32_t* __restrict__ pres) {
-  const int sb = blockIdx.y;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t base = (int64_t)split_bin[sb] * BW;
-  if (i >= BW || base + i >= n_local) return;
-  const float* p = slab + (int64_t)split_first[sb] * BW + i;
-  const int cnt = split_count[sb];
-  float s = -0.0f;
-  for (int k = 0; k < cnt; ++k) s += p[(int64_t)k * BW];
-  const bool hit = !signbit(s);
-  acc[base + i] = hit ? s : 0.f;
-  pres[base + i] = hit ? 1 : 0;
-}
-
 }  // namespace dalgo
 
 using namespace dalgo;
@@ -594,39 +469,6 @@ hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, con
   else
     hipLaunchKernelGGL((pr_spmv_kernel<NW, false, false>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
                        E, c, acc, pres, n_c);
-  DALGO_LAUNCH_CHECK();
-  return hipSuccess;
-}
-
-hipError_t dalgo_pb_spmv(const int32_t* psrc, const int32_t* ppos, int64_t E4, const float* c,
-                         float* val, const uint16_t* dloc, const int64_t* chunk_lo4,
-                         const int32_t* chunk_bin, const int32_t* chunk_slab, int nchunks,
-                         int bin_width, int64_t n_local, float* acc, int32_t* pres, float* slab,
-                         const int32_t* split_bin, const int32_t* split_first,
-                         const int32_t* split_count, int nsplit, hipStream_t st) {
-  if (E4 % 4 != 0 || (bin_width != 8192 && bin_width != 16384)) return hipErrorInvalidValue;
-  const int g1 = (int)std::min<int64_t>(round_up(cdiv(E4 / 4, 256 * 4), kXcds), 256 * 16);
-  if (E4 > 0) {
-    hipLaunchKernelGGL(pb_scatter_kernel, dim3(g1), dim3(256), 0, st, (const int4*)psrc,
-                       (const int4*)ppos, E4 / 4, c, val);
-    DALGO_LAUNCH_CHECK();
-  }
-  if (nchunks == 0) return hipSuccess;
-  if (bin_width == 16384) {
-    hipLaunchKernelGGL(pb_accumulate_kernel<16384>, dim3(nchunks), dim3(1024), 0, st,
-                       (const float4*)val, (const uint2*)dloc, chunk_lo4, chunk_bin, chunk_slab,
-                       n_local, acc, pres, slab);
-    if (nsplit > 0)
-      hipLaunchKernelGGL(pb_combine_kernel<16384>, dim3(16384 / 256, nsplit), dim3(256), 0, st,
-                         slab, split_bin, split_first, split_count, n_local, acc, pres);
-  } else {
-    hipLaunchKernelGGL(pb_accumulate_kernel<8192>, dim3(nchunks), dim3(1024), 0, st,
-                       (const float4*)val, (const uint2*)dloc, chunk_lo4, chunk_bin, chunk_slab,
-                       n_local, acc, pres, slab);
-    if (nsplit > 0)
-      hipLaunchKernelGGL(pb_combine_kernel<8192>, dim3(8192 / 256, nsplit), dim3(256), 0, st,
-                         slab, split_bin, split_first, split_count, n_local, acc, pres);
-  }
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

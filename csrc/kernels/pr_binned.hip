@@ -1,0 +1,321 @@
+// K4b: PageRank SpMV by two-level propagation blocking (no random global gathers).
+//
+// Reference: graph_computation/pagerank.py:52-57 — flatMap(computeContribs) emits one
+// (dst, c[src]) record per edge, reduceByKey(add) sums them per destination. The pull
+// K4 (pagerank.hip) does that sum as a gather of c[src] per edge; at R-MAT scale 26 it
+// is bound by the per-lane random gathers (TA 86 % busy, profiles/round3/pmc_pagerank.md).
+// Here the records are produced and reduced without a single random global access:
+//
+//   layout (built once, dalgo.ops.graph.build_blocked):
+//     chunks  : contiguous SOURCE ranges of <= S vertices (one LDS table of c each);
+//     edges   : sorted by (chunk, dst, src); per edge a u16 = local source (13 bits)
+//               | 0x4000 on the end edge of a run's first entry | 0x8000 on an entry's
+//               end edge;
+//     entries : distinct (chunk, dst) pairs = the chunk's records with equal destination
+//               pre-combined (an R-MAT hot destination appears once per chunk, not once
+//               per edge); stored BIN-MAJOR: all entries of destination bin b (BW
+//               destinations) contiguous, chunk order inside the bin;
+//     runs    : the entries of one (chunk, bin); an entry's bin-major position is its
+//               chunk-major index + the run's delta (one int per non-empty run).
+//   phase 1 (pb_gather): one workgroup per chunk stages c[chunk sources] and the chunk's
+//     run deltas in LDS; its waves stream the chunk's edges (2 B each, coalesced), read c
+//     from LDS, reduce the (dst-sorted) records to one value per entry with a segmented
+//     DPP scan and store each entry value at its bin-major slot (runs: contiguous).
+//   phase 2 (pb_accum): one workgroup per contiguous bin-major entry range (a bin, or a
+//     piece of a hot bin) streams (value, u16 destination offset) pairs and adds them
+//     into a BW-float LDS accumulator (ds_add_f32; inside a run every destination is
+//     distinct, so lanes do not collide on an address); it writes the bin's sums (or a
+//     partial slab that pb_combine sums in order).
+//
+// Per edge 2 B, per entry 4 B written + 6 B read, all streamed: ~7-10 B per edge at
+// scale 26 instead of the pull form's ~58 B of fabric traffic per edge.
+//
+// "reference" semantics: c < 0 marks an absent source; its record does not exist. The
+// accumulators start at -0.0f and absent records add -0.0f, so a destination received
+// >= 1 record iff the sign bit of its sum is clear (-0 + +0 = +0).
+#include "dalgo/common.h"
+#include "launchers.h"   // the extern "C" entry point is checked against its declaration
+#include <algorithm>
+
+namespace dalgo {
+
+namespace {
+
+// DPP moves (gfx9 family): lanes whose source is outside the pattern keep `old`
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ float dpp_mov_f(float old, float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL,
+                                                    ROWS, 0xf, false));
+}
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ int dpp_mov_i(int old, int v) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWS, 0xf, false);
+}
+
+// one step of the inclusive segmented scan of (a: open-segment sum, h: segment closed)
+// plus two plain int scans (entry count, run-start count)
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ void scan_step(float& a, int& h, int& c0, int& c1) {
+  const float a_up = dpp_mov_f<CTRL, ROWS>(-0.0f, a);
+  const int h_up = dpp_mov_i<CTRL, ROWS>(0, h);
+  const int c0_up = dpp_mov_i<CTRL, ROWS>(0, c0);
+  const int c1_up = dpp_mov_i<CTRL, ROWS>(0, c1);
+  if (!h) a = a_up + a;
+  h |= h_up;
+  c0 += c0_up;
+  c1 += c1_up;
+}
+
+}  // namespace
+
+// S: max sources per chunk (LDS table); R: run deltas staged in LDS (more: read from
+// global); NW waves per block; EPL edges per lane per step.
+template <int S, int R, int NW>
+__global__ void __launch_bounds__(NW * 64)
+pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ tile_e,
+                 const int32_t* __restrict__ tile_ent, const int32_t* __restrict__ tile_run,
+                 const int32_t* __restrict__ chunk_tile, const int32_t* __restrict__ chunk_slo,
+                 const int32_t* __restrict__ chunk_ns, const int32_t* __restrict__ chunk_run,
+                 const int32_t* __restrict__ run_delta, const float* __restrict__ c,
+                 float* __restrict__ val) {
+  static_assert(S <= 16384, "local source index must leave bits 14, 15 for the markers");
+  constexpr int EPL = 8;
+  __shared__ float s_c[S];
+  __shared__ int32_t s_d[R];
+  // per-wave staging of one step's entry values: the lane that reduces an entry is not
+  // the lane that stores it; stores go out as 64 consecutive entries per instruction
+  __shared__ float s_v[NW][64 * EPL];
+  __shared__ int32_t s_p[NW][64 * EPL];
+  const int ch = blockIdx.x;
+  const int slo = chunk_slo[ch], ns = chunk_ns[ch];
+  const int r0 = chunk_run[ch], nr = chunk_run[ch + 1] - r0;
+  for (int i = threadIdx.x; i < ns; i += NW * 64) {
+    const float v = c[slo + i];
+    s_c[i] = v >= 0.f ? v : -0.0f;            // absent source: no record
+  }
+  const bool lds_runs = nr <= R;
+  if (lds_runs)
+    for (int i = threadIdx.x; i < nr; i += NW * 64) s_d[i] = run_delta[r0 + i];
+  __syncthreads();
+  const int32_t* gd = run_delta + r0;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  float* sv = s_v[wave];
+  int32_t* sp = s_p[wave];
+  const int t_end = chunk_tile[ch + 1];
+  for (int t = chunk_tile[ch] + wave; t < t_end; t += NW) {
+    const int64_t e_lo = tile_e[t], e_hi = tile_e[t + 1];
+    int64_t ent = tile_ent[t];                // chunk-major index of the next entry
+    int run = tile_run[t];                    // run starts (in this chunk) before it
+    float carry = -0.0f;                      // open entry continuing from the last step
+    int64_t e0 = e_lo & ~(int64_t)(EPL - 1);
+    int4 wn = make_int4(0, 0, 0, 0);          // the next step's edges, loaded one step ahead
+    if (e0 + EPL * lane < e_hi) wn = ld_int4<true>(reinterpret_cast<const int32_t*>(srcl + e0 + EPL * lane));
+    for (; e0 < e_hi; e0 += 64 * EPL) {
+      const int64_t idx = e0 + EPL * lane;
+      const uint32_t ww[4] = {(uint32_t)wn.x, (uint32_t)wn.y, (uint32_t)wn.z, (uint32_t)wn.w};
+      wn = make_int4(0, 0, 0, 0);
+      if (idx + 64 * EPL < e_hi)
+        wn = ld_int4<true>(reinterpret_cast<const int32_t*>(srcl + idx + 64 * EPL));
+      float part = -0.0f, outv[EPL];
+      int nf = 0, nm = 0, fl = 0, ml = 0;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        uint32_t h = (ww[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+        const bool in = idx + k >= e_lo && idx + k < e_hi;
+        if (!in) h = 0;
+        const float v = in ? s_c[h & (S - 1)] : -0.0f;
+        part += v;
+        outv[k] = part;
+        if (h & 0x8000u) {
+          part = -0.0f;
+          ++nf;
+          fl |= 1 << k;
+          if (h & 0x4000u) {
+            ++nm;
+            ml |= 1 << k;
+          }
+        }
+      }
+      // inclusive scans over the 64 lanes (DPP: rows of 16, then row broadcasts)
+      float a = part;
+      int hh = nf > 0, cnt = nf, cm = nm;
+      scan_step<0x111>(a, hh, cnt, cm);          // row_shr:1
+      scan_step<0x112>(a, hh, cnt, cm);          // row_shr:2
+      scan_step<0x114>(a, hh, cnt, cm);          // row_shr:4
+      scan_step<0x118>(a, hh, cnt, cm);          // row_shr:8
+      scan_step<0x142, 0xa>(a, hh, cnt, cm);     // row_bcast:15 -> rows 1, 3
+      scan_step<0x143, 0xc>(a, hh, cnt, cm);     // row_bcast:31 -> rows 2, 3
+      // exclusive segment sum for this lane (wave_shr:1), joined with the step carry
+      const float a_ex = dpp_mov_f<0x138>(-0.0f, a);
+      const int h_ex = dpp_mov_i<0x138>(0, hh);
+      const float carry_in = h_ex ? a_ex : carry + a_ex;
+      int j = cnt - nf;                          // this lane's first entry of the step
+      int r_i = run + cm - nm - 1;
+      bool first = true;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        if (fl & (1 << k)) {
+          if (ml & (1 << k)) ++r_i;
+          const int dlt = lds_runs ? s_d[r_i] : gd[r_i];
+          sv[j] = first ? carry_in + outv[k] : outv[k];
+          sp[j] = (int32_t)(ent + j + dlt);
+          first = false;
+          ++j;
+        }
+      }
+      const float a63 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a), 63));
+      const int h63 = __builtin_amdgcn_readlane(hh, 63);
+      const int n_step = __builtin_amdgcn_readlane(cnt, 63);
+      carry = h63 ? a63 : carry + a63;
+      ent += n_step;
+      run += __builtin_amdgcn_readlane(cm, 63);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int q = lane; q < n_step; q += 64) val[sp[q]] = sv[q];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+}
+
+// f32 record value -> fixed point q = v * 2^K (truncated), >= 1 for any present record so
+// that "received >= 1 record" == (sum != 0). Exact integer sums: the result does not
+// depend on the order of the adds (bitwise deterministic) and is rounded to f32 once.
+__device__ __forceinline__ uint64_t to_fixed(float v, int K) {
+  const uint32_t bits = __float_as_uint(v);
+  const int e = (int)((bits >> 23) & 0xffu);
+  const uint64_t m = (bits & 0x7fffffu) | (e ? 0x800000u : 0u);
+  const int sh = max(e, 1) - 150 + K;          // v = m * 2^(max(e,1) - 150)
+  uint64_t q = sh >= 0 ? (m << min(sh, 63)) : (sh > -64 ? (m >> -sh) : 0ull);
+  return q ? q : 1ull;
+}
+
+__device__ __forceinline__ float from_fixed(uint64_t q, int K) {
+  return (float)ldexp((double)q, -K);
+}
+
+// BW destinations per LDS bin (u64 fixed-point accumulators: f32 LDS atomics run at
+// ~0.33 lane-ops per CU-clock on gfx950, u32/u64 integer ones ~28x faster,
+// profiles/round3/pb/README.md); NW waves; a work item is a contiguous bin-major entry range
+template <int BW, int NW>
+__global__ void __launch_bounds__(NW * 64)
+pb_accum_kernel(const float* __restrict__ val, const uint16_t* __restrict__ dloc,
+                const int32_t* __restrict__ wi_bin, const int64_t* __restrict__ wi_lo,
+                const int32_t* __restrict__ wi_slab, int64_t n_local, int K,
+                float* __restrict__ acc, int32_t* __restrict__ pres, uint64_t* __restrict__ slab) {
+  constexpr int U = 4;
+  __shared__ unsigned long long s_acc[BW];
+  const int w = blockIdx.x;
+  const int b = wi_bin[w];
+  const int64_t lo = wi_lo[w], hi = wi_lo[w + 1];
+  for (int i = threadIdx.x; i < BW; i += NW * 64) s_acc[i] = 0ull;
+  __syncthreads();
+  const int64_t g_lo = lo >> 2, g_hi = (hi + 3) >> 2;     // groups of 4 entries
+  for (int64_t g0 = g_lo + threadIdx.x; g0 < g_hi; g0 += (int64_t)U * NW * 64) {
+    float4 v[U];
+    uint2 k[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t g = g0 + (int64_t)u * NW * 64;
+      v[u] = make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
+      k[u] = make_uint2(0u, 0u);
+      if (g < g_hi) {
+        const int4 vi = ld_int4<true>(reinterpret_cast<const int32_t*>(val) + 4 * g);
+        v[u] = make_float4(__int_as_float(vi.x), __int_as_float(vi.y), __int_as_float(vi.z),
+                           __int_as_float(vi.w));
+        k[u] = *(reinterpret_cast<const uint2*>(dloc) + g);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = (g0 + (int64_t)u * NW * 64) * 4;
+      const float f[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+      const uint32_t kk[4] = {k[u].x & 0xffffu, k[u].x >> 16, k[u].y & 0xffffu, k[u].y >> 16};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (e + j >= lo && e + j < hi && !signbit(f[j]))
+          atomicAdd(&s_acc[kk[j]], (unsigned long long)to_fixed(f[j], K));
+    }
+  }
+  __syncthreads();
+  const int64_t base = (int64_t)b * BW;
+  const int nb = (int)min((int64_t)BW, n_local - base);
+  const int sl = wi_slab[w];
+  if (sl < 0) {                         // the bin's only work item: final values
+    for (int i = threadIdx.x; i < nb; i += NW * 64) {
+      const uint64_t q = s_acc[i];
+      acc[base + i] = from_fixed(q, K);
+      pres[base + i] = q != 0;
+    }
+  } else {                              // partial of a split bin -> its slab
+    uint64_t* dst = slab + (int64_t)sl * BW;
+    for (int i = threadIdx.x; i < BW; i += NW * 64) dst[i] = s_acc[i];
+  }
+}
+
+// Split bins: sum the partial slabs (exact integer sums).
+template <int BW>
+__global__ void __launch_bounds__(256)
+pb_combine_kernel(const uint64_t* __restrict__ slab, const int32_t* __restrict__ split_bin,
+                  const int32_t* __restrict__ split_first, const int32_t* __restrict__ split_count,
+                  int64_t n_local, int K, float* __restrict__ acc, int32_t* __restrict__ pres) {
+  const int sb = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t base = (int64_t)split_bin[sb] * BW;
+  if (i >= BW || base + i >= n_local) return;
+  const uint64_t* p = slab + (int64_t)split_first[sb] * BW + i;
+  const int cnt = split_count[sb];
+  uint64_t q = 0;
+  for (int k = 0; k < cnt; ++k) q += p[(int64_t)k * BW];
+  acc[base + i] = from_fixed(q, K);
+  pres[base + i] = q != 0;
+}
+
+}  // namespace dalgo
+
+using namespace dalgo;
+
+extern "C" {
+
+hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int32_t* tile_ent,
+                         const int32_t* tile_run, const int32_t* chunk_tile,
+                         const int32_t* chunk_slo, const int32_t* chunk_ns,
+                         const int32_t* chunk_run, const int32_t* run_delta, int nch, int src_span,
+                         const float* c, float* val, const uint16_t* dloc, const int32_t* wi_bin,
+                         const int64_t* wi_lo, const int32_t* wi_slab, int nwi, int bin_width,
+                         int fixed_bits, int64_t n_local, float* acc, int32_t* pres, uint64_t* slab,
+                         const int32_t* split_bin, const int32_t* split_first,
+                         const int32_t* split_count, int nsplit, hipStream_t st) {
+  if (src_span != 8192 || (bin_width != 8192 && bin_width != 16384) || fixed_bits < 1 ||
+      fixed_bits > 126)
+    return hipErrorInvalidValue;
+  if (nch > 0) {
+    hipLaunchKernelGGL((pb_gather_kernel<8192, 2048, 8>), dim3(nch), dim3(8 * 64), 0, st, srcl,
+                       tile_e, tile_ent, tile_run, chunk_tile, chunk_slo, chunk_ns, chunk_run,
+                       run_delta, c, val);
+    DALGO_LAUNCH_CHECK();
+  }
+  if (nwi == 0) return hipSuccess;
+  if (bin_width == 16384) {
+    hipLaunchKernelGGL((pb_accum_kernel<16384, 16>), dim3(nwi), dim3(16 * 64), 0, st, val, dloc,
+                       wi_bin, wi_lo, wi_slab, n_local, fixed_bits, acc, pres, slab);
+    DALGO_LAUNCH_CHECK();
+    if (nsplit > 0)
+      hipLaunchKernelGGL(pb_combine_kernel<16384>, dim3(16384 / 256, nsplit), dim3(256), 0, st,
+                         slab, split_bin, split_first, split_count, n_local, fixed_bits, acc, pres);
+  } else {
+    hipLaunchKernelGGL((pb_accum_kernel<8192, 16>), dim3(nwi), dim3(16 * 64), 0, st, val, dloc,
+                       wi_bin, wi_lo, wi_slab, n_local, fixed_bits, acc, pres, slab);
+    DALGO_LAUNCH_CHECK();
+    if (nsplit > 0)
+      hipLaunchKernelGGL(pb_combine_kernel<8192>, dim3(8192 / 256, nsplit), dim3(256), 0, st,
+                         slab, split_bin, split_first, split_count, n_local, fixed_bits, acc, pres);
+  }
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+}  // extern "C"

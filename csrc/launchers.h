@@ -106,10 +106,14 @@ hipError_t dalgo_rmat(uint64_t seed, int scale, int64_t e_off, int64_t n, float 
 hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, const float* c,
                          int64_t n_c,
                          float* acc, int32_t* pres, int accumulate, hipStream_t st);
-hipError_t dalgo_pb_spmv(const int32_t* psrc, const int32_t* ppos, int64_t E4, const float* c,
-                         float* val, const uint16_t* dloc, const int64_t* chunk_lo4,
-                         const int32_t* chunk_bin, const int32_t* chunk_slab, int nchunks,
-                         int bin_width, int64_t n_local, float* acc, int32_t* pres, float* slab,
+// ---- K4b two-level propagation-blocked SpMV (pr_binned.hip)
+hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int32_t* tile_ent,
+                         const int32_t* tile_run, const int32_t* chunk_tile,
+                         const int32_t* chunk_slo, const int32_t* chunk_ns,
+                         const int32_t* chunk_run, const int32_t* run_delta, int nch, int src_span,
+                         const float* c, float* val, const uint16_t* dloc, const int32_t* wi_bin,
+                         const int64_t* wi_lo, const int32_t* wi_slab, int nwi, int bin_width,
+                         int fixed_bits, int64_t n_local, float* acc, int32_t* pres, uint64_t* slab,
                          const int32_t* split_bin, const int32_t* split_first,
                          const int32_t* split_count, int nsplit, hipStream_t st);
 hipError_t dalgo_pr_spmv_xcd(const int32_t* src, const int32_t* dstl, const int64_t* part_base,

@@ -36,9 +36,9 @@ class PageRankConfig:
     semantics: str = "reference"  # "reference" | "standard"
     spmv: str = ""               # "pull" | "xcd" | "blocked" ("" = DALGO_PR_SPMV env,
                                  # default pull)
-    bin_width: int = 16384       # blocked: destination vertices per LDS bin
-    chunk: int = 1 << 18         # blocked: max edge slots per workgroup
-    tile: int = 1 << 16          # blocked: phase-1 edges per slot-sorted tile
+    bin_width: int = 16384       # blocked: destination vertices per LDS bin (8192 | 16384)
+    chunk: int = 1 << 17         # blocked: ~edges per source chunk (<= 8192 sources)
+    tile: int = 4096             # blocked: ~edges per phase-1 wave tile
     exchange: str = ""           # "ghost" | "allgather" ("" = DALGO_PR_EXCHANGE env, default
                                  # ghost on several ranks with the pull SpMV)
 
@@ -60,8 +60,6 @@ class PageRank:
         self.outdeg = od_full[shard.v_lo: shard.v_hi].contiguous()
         self.mode = 0 if cfg.semantics == "reference" else 1
         self.spmv = cfg.spmv or os.environ.get("DALGO_PR_SPMV", "pull")
-        self.layout = (Gops.build_blocked(shard, cfg.bin_width, cfg.chunk, cfg.tile)
-                       if self.spmv == "blocked" else None)
         if self.mode == 0:
             self.N = int((od_full > 0).sum().item())
         else:
@@ -75,7 +73,7 @@ class PageRank:
         self.pres = torch.zeros(nl, dtype=torch.int32, device=dev)
         self.r = torch.zeros(nl, dtype=fdt, device=dev)
         ex = cfg.exchange or os.environ.get("DALGO_PR_EXCHANGE", "ghost")
-        self.exchange = ex if (world > 1 and self.layout is None) else "allgather"
+        self.exchange = ex if world > 1 else "allgather"
         if self.exchange == "ghost":
             self._build_ghosts()
             # own slice first, then the ghosts: c_slice is a view, so the update kernel's
@@ -85,6 +83,11 @@ class PageRank:
         else:
             self.c_slice = torch.zeros(sl, dtype=fdt, device=dev)   # padded slice
             self.c_full = torch.zeros(sl * world, dtype=fdt, device=dev)
+        # K4b: built over the edge list the SpMV reads (c_full index space)
+        self.layout = None
+        if self.spmv == "blocked":
+            gsp = self.g_local if self.exchange == "ghost" else self.g
+            self.layout = Gops.build_blocked(gsp, cfg.bin_width, cfg.chunk, cfg.tile)
         self.dang = torch.zeros(1, dtype=fdt, device=dev)
         self.dang_next = torch.zeros(1, dtype=fdt, device=dev)
         od = self.outdeg.to(fdt)
@@ -169,7 +172,8 @@ class PageRank:
         self.acc.zero_()
         self.pres.zero_()
         if self.layout is not None:
-            Gops.pb_spmv(self.layout, self.c_full, self.acc, self.pres)
+            # c = r / outdeg <= 1 for both semantics: no host-side max needed
+            Gops.pb_spmv(self.layout, self.c_full, self.acc, self.pres, c_max=1.0)
         elif self.exchange == "ghost":
             Gops.pr_spmv(self.g_local, self.c_full, self.acc, self.pres)
         else:
@@ -199,7 +203,7 @@ class PageRank:
         profiles/round2/README.md), so by default (DALGO_PR_OVERLAP=auto) it is only used
         while the own-source pass is long enough to hide the exchange: at least a quarter
         of the edges (W <= 4 with the dealt relabeling). 1 / 0 force it on / off."""
-        if self.exchange != "ghost" or self.xl is not None:
+        if self.exchange != "ghost" or self.xl is not None or self.layout is not None:
             return False
         env = os.environ.get("DALGO_PR_OVERLAP", "auto")
         return env == "1" or (env == "auto" and self.own_share >= 0.25)

@@ -132,122 +132,253 @@ def local_outdeg(shard: GraphShard) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ propagation blocking
+SRC_SPAN = 8192          # sources per chunk: the LDS table of pb_gather (csrc/kernels/pr_binned.hip)
+
+
 @dataclass
 class BlockedLayout:
-    """Edge layout of the propagation-blocked SpMV (pb_spmv): see csrc/kernels/pagerank.hip.
+    """Two-level propagation-blocked SpMV layout (K4b, csrc/kernels/pr_binned.hip).
 
-    psrc/ppos: phase-1 edge list (global src id, slot in the binned array) in
-    tile order: tiles of ``tile`` consecutive edges in SOURCE order, each tile
-    re-sorted by slot, so the c[src] reads of a tile stay inside a narrow source
-    range while its writes form contiguous runs per bin (coalesced stores).
-    val/dloc: the destination-binned array (value written per iteration, static
-    destination offset inside the bin; slots of a bin are in source order).
-    chunks: contiguous slot ranges of one bin; a bin longer than ``chunk`` slots
-    is split, its chunks write partial slabs that pb_combine sums in order."""
-    psrc: torch.Tensor
-    ppos: torch.Tensor
+    chunks: contiguous source ranges [slo, slo + ns), ns <= SRC_SPAN, with about
+    ``chunk_edges`` edges each. srcl: the edges sorted by (chunk, dst, src), one u16 per
+    edge = source offset in its chunk | 0x4000 on the end edge of a run's first entry |
+    0x8000 on the end edge of an entry. An entry is one distinct (chunk, dst) pair; a run
+    the entries of one (chunk, bin of ``bin_width`` destinations). Entries are stored
+    bin-major (val, dloc = destination offset in the bin): entry e (chunk-major index)
+    lives at e + run_delta[run of e]. tiles: ~``tile`` edges starting on an entry
+    boundary (one wave each); tile_run = the chunk's run starts before the tile.
+    work items: contiguous bin-major entry ranges [wi_lo[i], wi_lo[i + 1]) of one bin; a
+    bin split into several items writes partial slabs that pb_combine sums in order."""
+    srcl: torch.Tensor
+    tile_e: torch.Tensor
+    tile_ent: torch.Tensor
+    tile_run: torch.Tensor
+    chunk_tile: torch.Tensor
+    chunk_slo: torch.Tensor
+    chunk_ns: torch.Tensor
+    chunk_run: torch.Tensor
+    run_delta: torch.Tensor
     val: torch.Tensor
     dloc: torch.Tensor
-    chunk_lo4: torch.Tensor
-    chunk_bin: torch.Tensor
-    chunk_slab: torch.Tensor
+    wi_bin: torch.Tensor
+    wi_lo: torch.Tensor
+    wi_slab: torch.Tensor
     slab: torch.Tensor
     split_bin: torch.Tensor
     split_first: torch.Tensor
     split_count: torch.Tensor
     bin_width: int
     n_local: int
+    n_chunks: int
+    n_entries: int
+    n_src: int              # c index space the layout reads: c_full.numel() >= n_src
+    max_indeg: int          # largest in-degree (fixed-point range of the accumulators)
 
 
-def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk: int = 1 << 18,
-                  tile: int = 1 << 16) -> BlockedLayout:
-    """One-time construction from a (dst, src)-sorted shard (device sorts)."""
+def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 1 << 17,
+                  tile: int = 4096, items: int = 2048, min_piece: int = 1 << 14) -> BlockedLayout:
+    """One-time construction (device sorts) from any shard (src in the c index space)."""
     if bin_width not in (8192, 16384):
-        raise ValueError("bin_width must be 8192 or 16384 (LDS accumulator sizes of the kernel)")
+        raise ValueError("bin_width must be 8192 or 16384 (u64 LDS accumulator sizes of the kernel)")
     dev = shard.src.device
     E = shard.n_edges
+    nl = shard.n_local
+    S = SRC_SPAN
+    i32 = lambda x: x.to(torch.int32).contiguous()
+    i64 = lambda x: x.to(torch.int64).contiguous()
+    it = lambda x: torch.tensor(x, dtype=torch.int32, device=dev)
+    nbins = max(1, (nl + bin_width - 1) // bin_width)
+    if E == 0:
+        z = torch.zeros(1, dtype=torch.int32, device=dev)
+        return BlockedLayout(torch.zeros(16, dtype=torch.int16, device=dev),
+                             torch.zeros(1, dtype=torch.int64, device=dev), z[:0], z[:0], z.clone(),
+                             z[:0], z[:0], z.clone(), z[:0], torch.zeros(4, device=dev),
+                             torch.zeros(4, dtype=torch.int16, device=dev), z[:0],
+                             torch.zeros(1, dtype=torch.int64, device=dev), z[:0],
+                             torch.zeros(1, dtype=torch.int64, device=dev), z[:0], z[:0], z[:0],
+                             bin_width, nl, 0, 0, 0, 0)
     s = shard.src[:E].to(torch.int64)
     d = shard.dstl[:E].to(torch.int64)
-    nl = shard.n_local
-    nbins = max(1, (nl + bin_width - 1) // bin_width)
-    b = d // bin_width
-    # slots: bins in order, inside a bin edges in source order, each bin padded to 4
-    order2 = torch.argsort(b * (shard.n_vertices + 1) + s, stable=True)
-    inv2 = torch.empty_like(order2)
-    inv2[order2] = torch.arange(E, device=dev)
-    del order2
-    cnt = torch.bincount(b, minlength=nbins)
-    start_u = torch.cumsum(cnt, 0) - cnt
-    cntp = (cnt + 3) // 4 * 4
-    start_p = torch.cumsum(cntp, 0) - cntp
-    Ep = max(int(cntp.sum().item()) if E else 0, 4)
-    pos = start_p[b] + (inv2 - start_u[b])
-    del inv2
-    val = torch.full((Ep,), -1.0, dtype=torch.float32, device=dev)
-    dloc = torch.zeros(Ep, dtype=torch.int16, device=dev)
-    dl = d - b * bin_width
-    dloc[pos] = dl.to(torch.int32).to(torch.int16)        # < 16384: fits int16 as is
-    # phase-1 order: source order, then slot order inside each tile
-    order1 = torch.argsort(s, stable=True)
-    pos1 = pos[order1]
-    t_id = torch.arange(E, device=dev) // max(1, tile)
-    order_t = torch.argsort(t_id * Ep + pos1)
-    E4 = (E + 3) // 4 * 4
-    psrc = torch.full((max(E4, 4),), -1, dtype=torch.int32, device=dev)
-    ppos = torch.zeros(max(E4, 4), dtype=torch.int32, device=dev)
-    psrc[:E] = s[order1][order_t].to(torch.int32)
-    ppos[:E] = pos1[order_t].to(torch.int32)
-    del order1, pos1, t_id, order_t
-    # chunks (host): split each non-empty bin into <= chunk-slot pieces (multiples of 4)
-    cntp_h = cntp.cpu().tolist()
-    start_h = start_p.cpu().tolist()
-    chunk = max(4, chunk // 4 * 4)
-    lo4, bins, slab_of, sp_bin, sp_first, sp_cnt = [], [], [], [], [], []
+    n_src = int(s.max().item()) + 1
+    max_indeg = int(torch.bincount(d, minlength=nl).max().item())
+    assert int(s.min().item()) >= 0 and int(d.min().item()) >= 0 and int(d.max().item()) < nl
+    # chunks: source blocks of S ids, cut further every ~chunk_edges edges (on source
+    # boundaries); only sources with edges define chunks
+    outd = torch.bincount(s, minlength=n_src)
+    cs = torch.cumsum(outd, 0) - outd
+    key = (torch.arange(n_src, device=dev) // S) * (E // chunk_edges + 2) + cs // chunk_edges
+    has = torch.nonzero(outd > 0).flatten()
+    kh = key[has]
+    new = torch.ones_like(kh, dtype=torch.bool)
+    new[1:] = kh[1:] != kh[:-1]
+    cid = torch.cumsum(new.to(torch.int64), 0) - 1
+    nch = int(cid[-1].item()) + 1
+    slo = has[new]
+    last = torch.ones_like(new)
+    last[:-1] = new[1:]
+    ns = has[last] - slo + 1
+    assert int(ns.max().item()) <= S
+    cid_src = torch.full((n_src,), -1, dtype=torch.int64, device=dev)
+    cid_src[has] = cid
+    del outd, cs, key, has, kh, new, last, cid
+    ec = cid_src[s]
+    del cid_src
+    assert nch * nl * S < (1 << 62)
+    k = (ec * nl + d) * S + (s - slo[ec])
+    del ec, s, d
+    k = torch.sort(k).values
+    ek = k // S                                       # entry key = chunk * nl + dst
+    sl = k - ek * S
+    del k
+    end = torch.ones(E, dtype=torch.bool, device=dev)
+    end[:-1] = ek[1:] != ek[:-1]
+    ent_key = ek[end]
+    del ek
+    nent = int(ent_key.numel())
+    assert nent < (1 << 31) - 8
+    end_edge = torch.nonzero(end).flatten()          # end edge of each entry
+    e_start = torch.zeros(nent, dtype=torch.int64, device=dev)
+    e_start[1:] = end_edge[:-1] + 1
+    ent_dst = ent_key % nl
+    ent_chunk = ent_key // nl
+    ent_bin = ent_dst // bin_width
+    # runs: (chunk, bin) groups of consecutive entries (chunk-major order)
+    rk = ent_chunk * nbins + ent_bin
+    rstart = torch.ones(nent, dtype=torch.bool, device=dev)
+    rstart[1:] = rk[1:] != rk[:-1]
+    run_first = torch.nonzero(rstart).flatten()      # chunk-major entry index of each run
+    run_of_ent = torch.cumsum(rstart.to(torch.int64), 0) - 1
+    run_chunk = ent_chunk[run_first]
+    run_bin = ent_bin[run_first]
+    run_len = torch.diff(torch.cat([run_first, torch.tensor([nent], device=dev)]))
+    # bin-major position of each run: bins in order, chunks in order inside a bin
+    border = torch.argsort(run_bin * (nch + 1) + run_chunk)
+    bm_start = torch.empty_like(run_first)
+    bm_start[border] = torch.cumsum(run_len[border], 0) - run_len[border]
+    run_delta = bm_start - run_first
+    chunk_run = torch.searchsorted(run_chunk, torch.arange(nch + 1, device=dev))
+    bin_cnt = torch.bincount(ent_bin, minlength=nbins)
+
+    bin_lo = torch.cumsum(bin_cnt, 0) - bin_cnt
+    # per-edge u16: local source | run-start marker | entry end
+    E16 = (E + 15) // 16 * 16                         # phase 1 reads 16 edges per lane
+    hbits = sl | (end.to(torch.int64) << 15)
+    hbits[end_edge[run_first]] |= 1 << 14
+    srcl = torch.zeros(E16, dtype=torch.int32, device=dev)
+    srcl[:E] = hbits.to(torch.int32)
+    srcl = srcl.to(torch.int16)                       # two's complement: bits 14, 15 kept
+    del sl, hbits, end, rk, rstart
+    # bin-major destination offsets
+    pos = torch.arange(nent, device=dev) + run_delta[run_of_ent]
+    n4 = (nent + 3) // 4 * 4
+    dloc = torch.zeros(n4, dtype=torch.int32, device=dev)
+    dloc[pos] = (ent_dst % bin_width).to(torch.int32)
+    dloc = dloc.to(torch.int16)                       # < 32768: exact as int16
+    del pos, ent_dst, ent_bin, ent_key
+    # tiles: ~tile edges, starting on an entry boundary, never crossing a chunk
+    ce_lo = e_start[torch.searchsorted(ent_chunk, torch.arange(nch, device=dev))]
+    tk = ent_chunk * (E // tile + 2) + (e_start - ce_lo[ent_chunk]) // tile
+    tnew = torch.ones(nent, dtype=torch.bool, device=dev)
+    tnew[1:] = tk[1:] != tk[:-1]
+    tile_ent = torch.nonzero(tnew).flatten()
+    tile_e = torch.cat([e_start[tile_ent], torch.tensor([E], dtype=torch.int64, device=dev)])
+    tile_chunk = ent_chunk[tile_ent]
+    chunk_tile = torch.searchsorted(tile_chunk, torch.arange(nch + 1, device=dev))
+    tile_run = torch.searchsorted(run_first, tile_ent) - chunk_run[tile_chunk]
+    del tk, tnew, e_start, ce_lo, ent_chunk
+    # the bounds the kernels rely on (checked once, here)
+    assert int(tile_e[-1]) <= srcl.numel() and int((slo + ns).max()) <= n_src
+    assert run_first.numel() == int(chunk_run[-1])
+    # work items: each bin's contiguous entry range, hot bins cut into ~cap pieces
+    cap = max(int(nent // max(items, 1)), min_piece)
+    cnt_h = bin_cnt.cpu().tolist()
+    lo_h = bin_lo.cpu().tolist()
+    wb, wl, slab_h, sp_bin, sp_first, sp_cnt = [], [], [], [], [], []
     nslab = 0
-    for bi, (st, n) in enumerate(zip(start_h, cntp_h)):
-        if n == 0:
+    for b, (n_b, l_b) in enumerate(zip(cnt_h, lo_h)):
+        if n_b == 0:
             continue
-        pieces = list(range(st, st + n, chunk))
-        if len(pieces) > 1:
-            sp_bin.append(bi)
-            sp_first.append(nslab)
-            sp_cnt.append(len(pieces))
-        for p0 in pieces:
-            lo4.append(p0 // 4)
-            bins.append(bi)
-            if len(pieces) > 1:
-                slab_of.append(nslab)
-                nslab += 1
+        pieces = max(1, -(-n_b // cap))
+        step = -(-n_b // pieces)
+        cuts = list(range(l_b, l_b + n_b, step))
+        if pieces > 1:
+            sp_bin.append(b); sp_first.append(nslab); sp_cnt.append(len(cuts))
+        for p0 in cuts:
+            wb.append(b)
+            wl.append(p0)
+            if pieces > 1:
+                slab_h.append(nslab); nslab += 1
             else:
-                slab_of.append(-1)
-    lo4.append(Ep // 4 if E else 0)
-    # the invariants the kernels rely on (checked once, here)
-    assert E == 0 or (int(pos.max()) < Ep and int(dl.max()) < bin_width and int(dl.min()) >= 0)
-    assert E == 0 or (int(s.min()) >= 0 and int(s.max()) < shard.n_vertices)
-    i32 = lambda x: torch.tensor(x, dtype=torch.int32, device=dev)
-    return BlockedLayout(psrc, ppos, val, dloc,
-                         torch.tensor(lo4, dtype=torch.int64, device=dev), i32(bins), i32(slab_of),
-                         torch.zeros(max(nslab, 1) * bin_width, dtype=torch.float32, device=dev),
-                         i32(sp_bin), i32(sp_first), i32(sp_cnt), bin_width, nl)
+                slab_h.append(-1)
+    wl.append(nent)
+    return BlockedLayout(srcl, i64(tile_e), i32(tile_ent), i32(tile_run), i32(chunk_tile), i32(slo),
+                         i32(ns), i32(chunk_run), i32(run_delta),
+                         torch.zeros(max(n4, 4), dtype=torch.float32, device=dev), dloc,
+                         it(wb), torch.tensor(wl, dtype=torch.int64, device=dev), it(slab_h),
+                         torch.zeros(max(nslab, 1) * bin_width, dtype=torch.int64, device=dev),
+                         it(sp_bin), it(sp_first), it(sp_cnt), bin_width, nl, nch, nent, n_src,
+                         max_indeg)
 
 
-def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: torch.Tensor):
-    """Same result as :func:`pr_spmv` (acc/pres zeroed by the caller)."""
+def pb_fixed_bits(lay: BlockedLayout, c_max: float) -> int:
+    """Fraction bits K of the u64 fixed-point accumulators: any destination's sum
+    (<= max_indeg * c_max) stays below 2^(63 - K)... with one bit of headroom."""
+    import math
+    bound = max(float(c_max), 1e-30) * max(lay.max_indeg, 1)
+    return int(min(100, max(1, 62 - math.ceil(math.log2(bound)))))
+
+
+def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: torch.Tensor,
+            c_max: float | None = None):
+    """Same result as :func:`pr_spmv` (acc/pres zeroed by the caller). The GPU sums are exact
+    u64 fixed-point sums (order independent) rounded to f32 once. ``c_max``: an upper bound
+    of the non-negative c values (PageRank: 1.0); None = measured (one host sync)."""
+    if c_full.numel() < lay.n_src or acc.numel() != lay.n_local:
+        raise ValueError("pb_spmv: c_full / acc do not match the layout")
     if c_full.is_cuda:
-        _ext.ops().pb_spmv(lay.psrc, lay.ppos, c_full, lay.val, lay.dloc, lay.chunk_lo4,
-                           lay.chunk_bin, lay.chunk_slab, lay.bin_width, acc, pres, lay.slab,
-                           lay.split_bin, lay.split_first, lay.split_count)
+        if c_max is None:
+            c_max = float(c_full.max().item()) if c_full.numel() else 1.0
+        _ext.ops().pb_spmv(lay.srcl, lay.tile_e, lay.tile_ent, lay.tile_run, lay.chunk_tile,
+                           lay.chunk_slo, lay.chunk_ns, lay.chunk_run, lay.run_delta, c_full,
+                           lay.val, lay.dloc, lay.wi_bin, lay.wi_lo, lay.wi_slab, lay.bin_width,
+                           pb_fixed_bits(lay, c_max), acc, pres, lay.slab, lay.split_bin,
+                           lay.split_first, lay.split_count)
         return
-    # CPU reference of the two phases
-    m = lay.psrc >= 0
-    lay.val[lay.ppos[m].long()] = c_full[lay.psrc[m].long()]
-    lo = lay.chunk_lo4.tolist()
-    for k, bi in enumerate(lay.chunk_bin.tolist()):
-        v = lay.val[lo[k] * 4: lo[k + 1] * 4]
-        dd = lay.dloc[lo[k] * 4: lo[k + 1] * 4].long() + bi * lay.bin_width
-        keep = v >= 0
-        acc.index_add_(0, dd[keep], v[keep])
-        pres[dd[keep]] = 1
+    # CPU reference of the two phases, decoding the same per-edge bits as the kernels
+    if lay.n_chunks == 0:
+        return
+    E = int(lay.tile_e[-1])
+    h = (lay.srcl[:E].to(torch.int32) & 0xFFFF).long()
+    nt = lay.tile_e.numel() - 1
+    tile_of_e = torch.repeat_interleave(torch.arange(nt), (lay.tile_e[1:] - lay.tile_e[:-1]))
+    chunk_of_tile = torch.repeat_interleave(torch.arange(lay.n_chunks),
+                                            (lay.chunk_tile[1:] - lay.chunk_tile[:-1]).long())
+    ch = chunk_of_tile[tile_of_e]
+    cv = c_full[lay.chunk_slo.long()[ch] + (h & (SRC_SPAN - 1))]
+    end = (h >> 15) & 1
+    ent = torch.cumsum(end, 0) - end                  # chunk-major entry of each edge
+    v = torch.zeros(lay.n_entries, dtype=c_full.dtype)
+    v.index_add_(0, ent, cv.clamp_min(0))
+    hit = torch.zeros(lay.n_entries, dtype=torch.int64)
+    hit.index_add_(0, ent, (cv >= 0).long())
+    # run of each entry: run-start markers on the entries' end edges, counted per chunk
+    ee = torch.nonzero(end).flatten()
+    mark = (h[ee] >> 14) & 1
+    ent_ch = ch[ee]
+    ordinal = torch.cumsum(mark, 0) - 1               # global run index (chunk-major)
+    assert bool((ordinal >= lay.chunk_run.long()[ent_ch]).all())
+    pos = torch.arange(lay.n_entries) + lay.run_delta.long()[ordinal]
+    vb = torch.zeros(lay.n_entries, dtype=c_full.dtype)
+    hb = torch.zeros(lay.n_entries, dtype=torch.int64)
+    vb[pos] = v
+    hb[pos] = hit
+    dl = (lay.dloc[:lay.n_entries].to(torch.int32) & 0xFFFF).long()
+    b_of = torch.repeat_interleave(lay.wi_bin.long(), lay.wi_lo[1:] - lay.wi_lo[:-1])
+    dd = b_of * lay.bin_width + dl
+    acc.index_add_(0, dd, vb.to(acc.dtype))
+    ph = torch.zeros_like(pres)
+    ph.index_add_(0, dd, (hb > 0).to(pres.dtype))
+    pres.copy_((ph > 0).to(pres.dtype))
 
 
 # ------------------------------------------------------------------ K4 kernels

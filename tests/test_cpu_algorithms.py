@@ -142,6 +142,39 @@ def test_pagerank_cpu_spmv_matches_dense():
     assert torch.allclose(acc, ref)
 
 
+def test_pagerank_blocked_layout_cpu():
+    """K4b layout invariants and its CPU two-phase reference == pull SpMV (f64)."""
+    from dalgo.ops import graph as G
+    s, d = G.rmat_edges(60000, 13, seed=5)
+    n = 1 << 13
+    for W, r in ((1, 0), (2, 1)):
+        sh = G.build_shard(s, d, n, r, W)
+        lay = G.build_blocked(sh, 16384, chunk_edges=1000, tile=300, min_piece=64)
+        E = sh.n_edges
+        assert lay.n_chunks > 1 and lay.n_entries < E
+        assert int(lay.chunk_ns.max()) <= G.SRC_SPAN
+        h = lay.srcl[:E].to(torch.int32) & 0xFFFF
+        end = (h >> 15) != 0
+        assert bool(end[-1]) and int(end.sum()) == lay.n_entries
+        # every tile starts on an entry boundary
+        te = lay.tile_e[:-1]
+        assert bool(((te == 0) | end[(te - 1).clamp_min(0)]).all())
+        assert bool((lay.wi_lo[1:] > lay.wi_lo[:-1]).all()) and int(lay.wi_lo[-1]) == lay.n_entries
+        # bin-major slots: a permutation of the entries
+        mark = (h[end] >> 14) & 1
+        pos = torch.arange(lay.n_entries) + lay.run_delta.long()[torch.cumsum(mark.long(), 0) - 1]
+        assert torch.equal(torch.sort(pos).values, torch.arange(lay.n_entries))
+        c = torch.rand(n, dtype=torch.float64)
+        c[::7] = -1.0
+        a1 = torch.zeros(sh.n_local, dtype=torch.float64)
+        p1 = torch.zeros(sh.n_local, dtype=torch.int32)
+        a2, p2 = torch.zeros_like(a1), torch.zeros_like(p1)
+        G.pr_spmv(sh, c, a1, p1)
+        G.pb_spmv(lay, c, a2, p2)
+        assert torch.equal(p1, p2)
+        assert torch.allclose(a1, a2)
+
+
 def test_transitive_closure_toy_trajectory():
     from dalgo.models.transitive_closure import DenseClosure, SparseClosure, compact_ids
     src = torch.tensor([1, 1, 2, 3])

@@ -50,6 +50,9 @@ def _others(rt):
         # the all_gather exchange (the default on several ranks is the ghost exchange)
         out["pr_ag_" + sem] = PageRank(PageRankConfig(semantics=sem, exchange="allgather"), sh,
                                        W).fit().collect()
+        # K4b propagation-blocked SpMV over the ghost index space
+        out["pr_pb_" + sem] = PageRank(PageRankConfig(semantics=sem, spmv="blocked", chunk=256,
+                                                      tile=64), sh, W).fit().collect()
     # transitive closure
     g = torch.Generator().manual_seed(4)
     ts = torch.randint(0, 60, (100,), generator=g)
@@ -85,7 +88,8 @@ def test_other_algorithms_two_ranks_equal_one():
         assert np.allclose(two[0][k], one[k], atol=1e-4), k
         assert np.allclose(two[1][k], one[k], atol=1e-4), k
     assert np.allclose(two[0]["kmeans_sse"], one["kmeans_sse"], rtol=1e-6)
-    for sem in ("pr_reference", "pr_standard", "pr_ag_reference", "pr_ag_standard"):
+    for sem in ("pr_reference", "pr_standard", "pr_ag_reference", "pr_ag_standard",
+                "pr_pb_reference", "pr_pb_standard"):
         a, b = one[sem], two[0][sem]
         assert set(a) == set(b)
         assert max(abs(a[v] - b[v]) for v in a) < 1e-12

@@ -261,27 +261,54 @@ def test_pagerank_toy_gpu(cuda):
     assert r[3] == pytest.approx(0.3966704706029163, abs=1e-6)
 
 
-@pytest.mark.parametrize("bw,chunk", [(8192, 1 << 18), (16384, 4096)])
-def test_pb_spmv_matches_pull(cuda, bw, chunk):
-    """Propagation-blocked SpMV == pull SpMV (acc to f32 rounding, pres exact), incl. split bins."""
+@pytest.mark.parametrize("bw,chunk,tile,min_piece", [(16384, 1 << 17, 4096, 1 << 14),
+                                                     (8192, 4096, 100, 64)])
+def test_pb_spmv_matches_pull(cuda, bw, chunk, tile, min_piece):
+    """K4b two-level propagation-blocked SpMV == pull SpMV (acc to f32 summation order, pres
+    exact): many chunks and tiles, entries pre-combined per chunk, split bins (slabs), absent
+    sources, 1 and 3 destination slices."""
     from dalgo.ops import graph as G
     g = torch.Generator().manual_seed(5)
     n, E = 100_000, 2_000_000
-    # skewed destinations so some bins need several chunks
-    src = torch.randint(0, n, (E,), generator=g, dtype=torch.int32)
+    # skewed sources and destinations: hot destinations repeat inside a chunk
+    src = (torch.rand(E, generator=g) ** 2 * n).to(torch.int32)
     dst = (torch.rand(E, generator=g) ** 3 * n).to(torch.int32)
     for W, r in ((1, 0), (3, 1)):
         sh = G.build_shard(src.to(cuda), dst.to(cuda), n, r, W)
-        lay = G.build_blocked(sh, bw, chunk)
+        lay = G.build_blocked(sh, bw, chunk, tile, min_piece=min_piece)
+        assert lay.n_entries < sh.n_edges            # hot destinations pre-combined
+        if min_piece < 1000:
+            assert lay.split_bin.numel() > 0         # slab path exercised
         c = (torch.rand(n, generator=g) * 2 - 0.5).to(cuda)   # negatives = absent vertices
         a1 = torch.zeros(sh.n_local, device=cuda)
         p1 = torch.zeros(sh.n_local, dtype=torch.int32, device=cuda)
         a2, p2 = torch.zeros_like(a1), torch.zeros_like(p1)
         G.pr_spmv(sh, c, a1, p1)
-        G.pb_spmv(lay, c, a2, p2)
+        for _ in range(2):                           # val / slabs are reused across calls
+            a2.zero_(); p2.zero_()
+            G.pb_spmv(lay, c, a2, p2)
         torch.cuda.synchronize()
         assert torch.equal(p1, p2)
         assert torch.allclose(a1, a2, rtol=1e-5, atol=1e-4)
+        # f64 reference
+        cc = c.double().cpu()
+        s64 = sh.src[:sh.n_edges].long().cpu()
+        d64 = sh.dstl[:sh.n_edges].long().cpu()
+        ref = torch.zeros(sh.n_local, dtype=torch.float64).index_add_(0, d64, cc[s64].clamp_min(0))
+        # exact u64 fixed-point sums rounded once: f32 rounding of the exact sum
+        assert torch.allclose(a2.double().cpu(), ref, rtol=2e-7, atol=1e-12)
+
+
+def test_pagerank_blocked_scale_matches_pull(cuda):
+    """Whole PageRank runs (reference + standard semantics) on an R-MAT graph: blocked == pull."""
+    from dalgo.apps.pagerank_app import rmat_shard
+    from dalgo.models.pagerank import PageRank, PageRankConfig
+    shard, _ = rmat_shard(16, 16, 0, 1, torch.device(cuda))
+    for sem in ("reference", "standard"):
+        rp = PageRank(PageRankConfig(semantics=sem, spmv="pull"), shard).fit()
+        rb = PageRank(PageRankConfig(semantics=sem, spmv="blocked", chunk=1 << 12), shard).fit()
+        assert torch.equal(rp.r >= 0, rb.r >= 0)
+        assert torch.allclose(rp.r, rb.r, rtol=1e-4, atol=1e-9)
 
 
 def test_pagerank_blocked_toy_and_standard(cuda):
