@@ -24,10 +24,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--semantics", default="reference")
     ap.add_argument("--no-reorder", action="store_true", help="keep scrambled R-MAT vertex ids")
-    ap.add_argument("--spmv", default="pull", choices=["pull", "xcd", "blocked"])
+    ap.add_argument("--spmv", default="blocked", choices=["pull", "xcd", "blocked"])
     ap.add_argument("--bin-width", type=int, default=16384)
-    ap.add_argument("--chunk", type=int, default=1 << 17)
-    ap.add_argument("--tile", type=int, default=4096)
+    ap.add_argument("--chunk", type=int, default=1 << 20)
+    ap.add_argument("--tile", type=int, default=16384)
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
                     help="ranks (one per GPU); started here as a torchrun child when > 1")
     ap.add_argument("--device", default="cuda")
@@ -80,6 +80,11 @@ def main():
             "vertices": 1 << a.scale, "degree_reordered": not a.no_reorder, "spmv": pr.spmv, "phases_ms_rank0": phases, "graph_build_s": build_s,
             "spmv_GBps_stream": shard.n_edges * 8 / (phases["spmv"] / 1e3) / 1e9,
             "exchange": pr.exchange, "exchange_MB_per_iter_all_ranks": int(xf.item()) * 4 / 1e6,
+            "blocked_layout_rank0": None if pr.layout is None else {
+                "chunks": pr.layout.n_chunks, "entries": pr.layout.n_entries,
+                "entries_per_edge": pr.layout.n_entries / max(shard.n_edges, 1),
+                "work_items": int(pr.layout.wi_bin.numel()), "split_bins": int(pr.layout.split_bin.numel()),
+                "bin_width": pr.layout.bin_width},
             "allgather_MB_per_iter_all_ranks": (W - 1) * W * shard.slice_size * 4 / 1e6}), flush=True)
     runtime.shutdown()
 

@@ -836,7 +836,8 @@ void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
              const Tensor& tile_run, const Tensor& chunk_tile, const Tensor& chunk_slo,
              const Tensor& chunk_ns, const Tensor& chunk_run, const Tensor& run_delta,
              const Tensor& c, Tensor val, const Tensor& dloc, const Tensor& wi_bin,
-             const Tensor& wi_lo, const Tensor& wi_slab, int64_t bin_width, int64_t fixed_bits,
+             const Tensor& wi_lo, const Tensor& wi_slab, int64_t bin_width, int64_t max_runs,
+             int64_t fixed_bits,
              Tensor acc, Tensor pres, Tensor slab, const Tensor& split_bin, const Tensor& split_first,
              const Tensor& split_count) {
   check_dev(srcl, "srcl");
@@ -882,8 +883,8 @@ void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
                     tile_e.data_ptr<int64_t>(), tile_ent.data_ptr<int32_t>(), tile_run.data_ptr<int32_t>(),
                     chunk_tile.data_ptr<int32_t>(), chunk_slo.data_ptr<int32_t>(),
                     chunk_ns.data_ptr<int32_t>(), chunk_run.data_ptr<int32_t>(),
-                    run_delta.data_ptr<int32_t>(), (int)nch, 8192, c.data_ptr<float>(),
-                    val.data_ptr<float>(), reinterpret_cast<const uint16_t*>(dloc.data_ptr<int16_t>()),
+                    run_delta.data_ptr<int32_t>(), (int)nch, (int)max_runs, 8192, c.data_ptr<float>(),
+                    val.data_ptr<float>(), val.numel(), reinterpret_cast<const uint16_t*>(dloc.data_ptr<int16_t>()),
                     wi_bin.data_ptr<int32_t>(), wi_lo.data_ptr<int64_t>(), wi_slab.data_ptr<int32_t>(),
                     (int)nwi, (int)bin_width, (int)fixed_bits, acc.numel(), acc.data_ptr<float>(),
                     pres.data_ptr<int32_t>(), reinterpret_cast<uint64_t*>(slab.data_ptr<int64_t>()),
@@ -1267,7 +1268,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("pb_spmv(Tensor srcl, Tensor tile_e, Tensor tile_ent, Tensor tile_run, Tensor chunk_tile, "
         "Tensor chunk_slo, Tensor chunk_ns, Tensor chunk_run, Tensor run_delta, Tensor c, "
         "Tensor(a!) val, Tensor dloc, Tensor wi_bin, Tensor wi_lo, Tensor wi_slab, int bin_width, "
-        "int fixed_bits, Tensor(b!) acc, Tensor(c!) pres, Tensor(d!) slab, Tensor split_bin, Tensor split_first, "
+        "int max_runs, int fixed_bits, Tensor(b!) acc, Tensor(c!) pres, Tensor(d!) slab, Tensor split_bin, Tensor split_first, "
         "Tensor split_count) -> ()");
   m.def("pr_spmv(Tensor src, Tensor dstl, Tensor c, Tensor(a!) acc, Tensor(b!) pres, "
         "bool accumulate=False) -> ()");

@@ -68,20 +68,24 @@ __device__ __forceinline__ void scan_step(float& a, int& h, int& c0, int& c1) {
 
 }  // namespace
 
-// S: max sources per chunk (LDS table); R: run deltas staged in LDS (more: read from
-// global); NW waves per block; EPL edges per lane per step.
-template <int S, int R, int NW>
+// S: max sources per chunk (LDS table); R: run deltas staged in LDS (GRUNS: a chunk with
+// more runs reads them from global memory); NW waves per block; EPL edges per lane per
+// step. The step body is branch-free up to the entry stores (loads from clamped
+// addresses, selects instead of guarded reads), so the compiler's wait counts stay exact
+// and the prefetched loads stay in flight.
+template <int S, int R, int NW, bool GRUNS, int PROBE = 0>
 __global__ void __launch_bounds__(NW * 64)
 pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ tile_e,
                  const int32_t* __restrict__ tile_ent, const int32_t* __restrict__ tile_run,
                  const int32_t* __restrict__ chunk_tile, const int32_t* __restrict__ chunk_slo,
                  const int32_t* __restrict__ chunk_ns, const int32_t* __restrict__ chunk_run,
                  const int32_t* __restrict__ run_delta, const float* __restrict__ c,
-                 float* __restrict__ val) {
+                 float* __restrict__ val, int64_t dummy) {
   static_assert(S <= 16384, "local source index must leave bits 14, 15 for the markers");
   constexpr int EPL = 8;
+  constexpr int D = 4;                        // steps of edges loaded ahead
   __shared__ float s_c[S];
-  __shared__ int32_t s_d[R];
+  __shared__ int32_t s_d[GRUNS ? 1 : R];
   // per-wave staging of one step's entry values: the lane that reduces an entry is not
   // the lane that stores it; stores go out as 64 consecutive entries per instruction
   __shared__ float s_v[NW][64 * EPL];
@@ -93,11 +97,10 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
     const float v = c[slo + i];
     s_c[i] = v >= 0.f ? v : -0.0f;            // absent source: no record
   }
-  const bool lds_runs = nr <= R;
-  if (lds_runs)
+  if constexpr (!GRUNS)
     for (int i = threadIdx.x; i < nr; i += NW * 64) s_d[i] = run_delta[r0 + i];
   __syncthreads();
-  const int32_t* gd = run_delta + r0;
+  const int32_t* dsrc = GRUNS ? run_delta + r0 : s_d;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   float* sv = s_v[wave];
@@ -108,34 +111,46 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
     int64_t ent = tile_ent[t];                // chunk-major index of the next entry
     int run = tile_run[t];                    // run starts (in this chunk) before it
     float carry = -0.0f;                      // open entry continuing from the last step
-    int64_t e0 = e_lo & ~(int64_t)(EPL - 1);
-    int4 wn = make_int4(0, 0, 0, 0);          // the next step's edges, loaded one step ahead
-    if (e0 + EPL * lane < e_hi) wn = ld_int4<true>(reinterpret_cast<const int32_t*>(srcl + e0 + EPL * lane));
-    for (; e0 < e_hi; e0 += 64 * EPL) {
+    const int64_t e_first = e_lo & ~(int64_t)(EPL - 1);
+    auto load = [&](int64_t ix) {             // out-of-tile lanes re-read the first group
+      return ld_int4<true>(reinterpret_cast<const int32_t*>(srcl + (ix < e_hi ? ix : e_first)));
+    };
+    // ring of D steps in flight, unrolled by D so that no register copy of a pending load
+    // (which would wait for it) is needed
+    int4 wq[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) wq[q] = load(e_first + (int64_t)q * 64 * EPL + EPL * lane);
+    for (int64_t e00 = e_first; e00 < e_hi; e00 += (int64_t)D * 64 * EPL) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      const int64_t e0 = e00 + (int64_t)q * 64 * EPL;
+      if (e0 >= e_hi) break;
       const int64_t idx = e0 + EPL * lane;
-      const uint32_t ww[4] = {(uint32_t)wn.x, (uint32_t)wn.y, (uint32_t)wn.z, (uint32_t)wn.w};
-      wn = make_int4(0, 0, 0, 0);
-      if (idx + 64 * EPL < e_hi)
-        wn = ld_int4<true>(reinterpret_cast<const int32_t*>(srcl + idx + 64 * EPL));
-      float part = -0.0f, outv[EPL];
-      int nf = 0, nm = 0, fl = 0, ml = 0;
+      const int4 wc = wq[q];
+      wq[q] = load(idx + (int64_t)D * 64 * EPL);
+      const uint32_t ww[4] = {(uint32_t)wc.x, (uint32_t)wc.y, (uint32_t)wc.z, (uint32_t)wc.w};
+      uint32_t hk[EPL];
+      float cv[EPL];
 #pragma unroll
       for (int k = 0; k < EPL; ++k) {
-        uint32_t h = (ww[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+        const uint32_t h = (ww[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+        hk[k] = (idx + k >= e_lo && idx + k < e_hi) ? h : 0u;
+        if constexpr (PROBE == 2) cv[k] = 1.0f;          // timing probe: no LDS reads
+        else cv[k] = s_c[hk[k] & (S - 1)];
+      }
+      float part = -0.0f, outv[EPL];
+      int nf = 0, nm = 0;
+      int rk[EPL];                                       // markers so far (inclusive)
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
         const bool in = idx + k >= e_lo && idx + k < e_hi;
-        if (!in) h = 0;
-        const float v = in ? s_c[h & (S - 1)] : -0.0f;
-        part += v;
+        part += in ? cv[k] : -0.0f;
         outv[k] = part;
-        if (h & 0x8000u) {
-          part = -0.0f;
-          ++nf;
-          fl |= 1 << k;
-          if (h & 0x4000u) {
-            ++nm;
-            ml |= 1 << k;
-          }
-        }
+        const bool f = hk[k] & 0x8000u;
+        nm += (f && (hk[k] & 0x4000u)) ? 1 : 0;
+        rk[k] = nm;
+        if (f) part = -0.0f;
+        nf += f ? 1 : 0;
       }
       // inclusive scans over the 64 lanes (DPP: rows of 16, then row broadcasts)
       float a = part;
@@ -150,16 +165,17 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
       const float a_ex = dpp_mov_f<0x138>(-0.0f, a);
       const int h_ex = dpp_mov_i<0x138>(0, hh);
       const float carry_in = h_ex ? a_ex : carry + a_ex;
+      const int rbase = run + cm - nm - 1;       // run of this lane's first entries
+      int dl[EPL];
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) dl[k] = dsrc[max(rbase + rk[k], 0)];
       int j = cnt - nf;                          // this lane's first entry of the step
-      int r_i = run + cm - nm - 1;
       bool first = true;
 #pragma unroll
       for (int k = 0; k < EPL; ++k) {
-        if (fl & (1 << k)) {
-          if (ml & (1 << k)) ++r_i;
-          const int dlt = lds_runs ? s_d[r_i] : gd[r_i];
+        if (hk[k] & 0x8000u) {
           sv[j] = first ? carry_in + outv[k] : outv[k];
-          sp[j] = (int32_t)(ent + j + dlt);
+          sp[j] = (int32_t)(ent + j + dl[k]);
           first = false;
           ++j;
         }
@@ -173,10 +189,21 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      for (int q = lane; q < n_step; q += 64) val[sp[q]] = sv[q];
+      // EPL unconditional stores per lane (lanes past n_step write the dummy slot): a fixed
+      // store count keeps the compiler's vmcnt bookkeeping exact, so the D prefetched
+      // loads are not drained at every step
+      if constexpr (PROBE != 1) {                       // PROBE 1: timing without stores
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+          const int qi = lane + 64 * q;
+          const bool ok = qi < n_step;
+          val[ok ? sp[qi] : dummy] = ok ? sv[qi] : 0.f;
+        }
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     }
   }
 }
@@ -283,8 +310,8 @@ extern "C" {
 hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int32_t* tile_ent,
                          const int32_t* tile_run, const int32_t* chunk_tile,
                          const int32_t* chunk_slo, const int32_t* chunk_ns,
-                         const int32_t* chunk_run, const int32_t* run_delta, int nch, int src_span,
-                         const float* c, float* val, const uint16_t* dloc, const int32_t* wi_bin,
+                         const int32_t* chunk_run, const int32_t* run_delta, int nch,
+                         int max_runs, int src_span, const float* c, float* val, int64_t n_val, const uint16_t* dloc, const int32_t* wi_bin,
                          const int64_t* wi_lo, const int32_t* wi_slab, int nwi, int bin_width,
                          int fixed_bits, int64_t n_local, float* acc, int32_t* pres, uint64_t* slab,
                          const int32_t* split_bin, const int32_t* split_first,
@@ -293,9 +320,18 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
       fixed_bits > 126)
     return hipErrorInvalidValue;
   if (nch > 0) {
-    hipLaunchKernelGGL((pb_gather_kernel<8192, 2048, 8>), dim3(nch), dim3(8 * 64), 0, st, srcl,
-                       tile_e, tile_ent, tile_run, chunk_tile, chunk_slo, chunk_ns, chunk_run,
-                       run_delta, c, val);
+    // max_runs: the largest number of non-empty runs of one chunk (LDS table up to 4096)
+    // DALGO_PB_PROBE (timing only, wrong results): 1 = no entry stores, 2 = no c reads
+    const int probe = env_int("DALGO_PB_PROBE", 0);
+#define DALGO_PB_GATHER(GR, PR)                                                                  \
+    hipLaunchKernelGGL((pb_gather_kernel<8192, 4096, 8, GR, PR>), dim3(nch), dim3(8 * 64), 0, st, \
+                       srcl, tile_e, tile_ent, tile_run, chunk_tile, chunk_slo, chunk_ns,        \
+                       chunk_run, run_delta, c, val, n_val - 1)
+    if (max_runs > 4096) DALGO_PB_GATHER(true, 0);
+    else if (probe == 1) DALGO_PB_GATHER(false, 1);
+    else if (probe == 2) DALGO_PB_GATHER(false, 2);
+    else DALGO_PB_GATHER(false, 0);
+#undef DALGO_PB_GATHER
     DALGO_LAUNCH_CHECK();
   }
   if (nwi == 0) return hipSuccess;

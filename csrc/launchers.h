@@ -110,8 +110,8 @@ hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, con
 hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int32_t* tile_ent,
                          const int32_t* tile_run, const int32_t* chunk_tile,
                          const int32_t* chunk_slo, const int32_t* chunk_ns,
-                         const int32_t* chunk_run, const int32_t* run_delta, int nch, int src_span,
-                         const float* c, float* val, const uint16_t* dloc, const int32_t* wi_bin,
+                         const int32_t* chunk_run, const int32_t* run_delta, int nch,
+                         int max_runs, int src_span, const float* c, float* val, int64_t n_val, const uint16_t* dloc, const int32_t* wi_bin,
                          const int64_t* wi_lo, const int32_t* wi_slab, int nwi, int bin_width,
                          int fixed_bits, int64_t n_local, float* acc, int32_t* pres, uint64_t* slab,
                          const int32_t* split_bin, const int32_t* split_first,

@@ -173,10 +173,11 @@ class BlockedLayout:
     n_entries: int
     n_src: int              # c index space the layout reads: c_full.numel() >= n_src
     max_indeg: int          # largest in-degree (fixed-point range of the accumulators)
+    max_runs: int           # most non-empty runs in one chunk (phase 1 stages <= 4096 in LDS)
 
 
-def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 1 << 17,
-                  tile: int = 4096, items: int = 2048, min_piece: int = 1 << 14) -> BlockedLayout:
+def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 1 << 20,
+                  tile: int = 16384, items: int = 2048, min_piece: int = 1 << 14) -> BlockedLayout:
     """One-time construction (device sorts) from any shard (src in the c index space)."""
     if bin_width not in (8192, 16384):
         raise ValueError("bin_width must be 8192 or 16384 (u64 LDS accumulator sizes of the kernel)")
@@ -196,7 +197,7 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
                              torch.zeros(4, dtype=torch.int16, device=dev), z[:0],
                              torch.zeros(1, dtype=torch.int64, device=dev), z[:0],
                              torch.zeros(1, dtype=torch.int64, device=dev), z[:0], z[:0], z[:0],
-                             bin_width, nl, 0, 0, 0, 0)
+                             bin_width, nl, 0, 0, 0, 0, 0)
     s = shard.src[:E].to(torch.int64)
     d = shard.dstl[:E].to(torch.int64)
     n_src = int(s.max().item()) + 1
@@ -270,7 +271,7 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
     del sl, hbits, end, rk, rstart
     # bin-major destination offsets
     pos = torch.arange(nent, device=dev) + run_delta[run_of_ent]
-    n4 = (nent + 3) // 4 * 4
+    n4 = (nent + 3) // 4 * 4 + 4                      # + padding: phase 1's dummy store slot
     dloc = torch.zeros(n4, dtype=torch.int32, device=dev)
     dloc[pos] = (ent_dst % bin_width).to(torch.int32)
     dloc = dloc.to(torch.int16)                       # < 32768: exact as int16
@@ -313,11 +314,11 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
     wl.append(nent)
     return BlockedLayout(srcl, i64(tile_e), i32(tile_ent), i32(tile_run), i32(chunk_tile), i32(slo),
                          i32(ns), i32(chunk_run), i32(run_delta),
-                         torch.zeros(max(n4, 4), dtype=torch.float32, device=dev), dloc,
+                         torch.zeros(n4, dtype=torch.float32, device=dev), dloc,
                          it(wb), torch.tensor(wl, dtype=torch.int64, device=dev), it(slab_h),
                          torch.zeros(max(nslab, 1) * bin_width, dtype=torch.int64, device=dev),
                          it(sp_bin), it(sp_first), it(sp_cnt), bin_width, nl, nch, nent, n_src,
-                         max_indeg)
+                         max_indeg, int((chunk_run[1:] - chunk_run[:-1]).max().item()))
 
 
 def pb_fixed_bits(lay: BlockedLayout, c_max: float) -> int:
@@ -341,7 +342,7 @@ def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: t
         _ext.ops().pb_spmv(lay.srcl, lay.tile_e, lay.tile_ent, lay.tile_run, lay.chunk_tile,
                            lay.chunk_slo, lay.chunk_ns, lay.chunk_run, lay.run_delta, c_full,
                            lay.val, lay.dloc, lay.wi_bin, lay.wi_lo, lay.wi_slab, lay.bin_width,
-                           pb_fixed_bits(lay, c_max), acc, pres, lay.slab, lay.split_bin,
+                           lay.max_runs, pb_fixed_bits(lay, c_max), acc, pres, lay.slab, lay.split_bin,
                            lay.split_first, lay.split_count)
         return
     # CPU reference of the two phases, decoding the same per-edge bits as the kernels
