@@ -839,8 +839,28 @@ void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
              const Tensor& wi_lo, const Tensor& wi_slab, int64_t bin_width, int64_t max_runs,
              int64_t fixed_bits,
              Tensor acc, Tensor pres, Tensor slab, const Tensor& split_bin, const Tensor& split_first,
-             const Tensor& split_count) {
+             const Tensor& split_count, const std::optional<Tensor>& outdeg, double q, double invN,
+             int64_t mode, const std::optional<Tensor>& dangling_in, const std::optional<Tensor>& r,
+             const std::optional<Tensor>& c_out, const std::optional<Tensor>& dangling_out) {
   check_dev(srcl, "srcl");
+  // fused PageRank update: all of outdeg / r / c_out or none
+  const bool fused = r.has_value();
+  TORCH_CHECK(fused == outdeg.has_value() && fused == c_out.has_value(), "pb: fused update args");
+  const int32_t* od = nullptr;
+  float *rp = nullptr, *cp = nullptr, *dout = nullptr;
+  const float* di = nullptr;
+  if (fused) {
+    check_i32(*outdeg, "outdeg");
+    check_f32(*r, "r");
+    check_f32(*c_out, "c_out");
+    TORCH_CHECK(outdeg->numel() >= acc.numel() && r->numel() >= acc.numel() && c_out->numel() >= acc.numel(),
+                "pb: update sizes");
+    od = outdeg->data_ptr<int32_t>();
+    rp = r->data_ptr<float>();
+    cp = c_out->data_ptr<float>();
+    if (dangling_in.has_value()) { check_f32(*dangling_in, "dangling_in"); di = dangling_in->data_ptr<float>(); }
+    if (dangling_out.has_value()) { check_f32(*dangling_out, "dangling_out"); dout = dangling_out->data_ptr<float>(); }
+  }
   TORCH_CHECK(srcl.scalar_type() == at::kShort && srcl.is_contiguous() && srcl.numel() % 16 == 0,
               "pb: srcl int16, len % 16 == 0");
   check_dev(tile_e, "tile_e");
@@ -889,8 +909,8 @@ void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
                     (int)nwi, (int)bin_width, (int)fixed_bits, acc.numel(), acc.data_ptr<float>(),
                     pres.data_ptr<int32_t>(), reinterpret_cast<uint64_t*>(slab.data_ptr<int64_t>()),
                     split_bin.data_ptr<int32_t>(),
-                    split_first.data_ptr<int32_t>(), split_count.data_ptr<int32_t>(), (int)nsp,
-                    cur_stream()),
+                    split_first.data_ptr<int32_t>(), split_count.data_ptr<int32_t>(), (int)nsp, od,
+                    (float)q, (float)invN, (int)mode, di, rp, cp, dout, cur_stream()),
       "pb_spmv");
 }
 
@@ -1268,8 +1288,10 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("pb_spmv(Tensor srcl, Tensor tile_e, Tensor tile_ent, Tensor tile_run, Tensor chunk_tile, "
         "Tensor chunk_slo, Tensor chunk_ns, Tensor chunk_run, Tensor run_delta, Tensor c, "
         "Tensor(a!) val, Tensor dloc, Tensor wi_bin, Tensor wi_lo, Tensor wi_slab, int bin_width, "
-        "int max_runs, int fixed_bits, Tensor(b!) acc, Tensor(c!) pres, Tensor(d!) slab, Tensor split_bin, Tensor split_first, "
-        "Tensor split_count) -> ()");
+        "int max_runs, int fixed_bits, Tensor(b!) acc, Tensor(c!) pres, Tensor(d!) slab, "
+        "Tensor split_bin, Tensor split_first, Tensor split_count, Tensor? outdeg=None, "
+        "float q=0., float invN=0., int mode=0, Tensor? dangling_in=None, Tensor(e!)? r=None, "
+        "Tensor(f!)? c_out=None, Tensor(g!)? dangling_out=None) -> ()");
   m.def("pr_spmv(Tensor src, Tensor dstl, Tensor c, Tensor(a!) acc, Tensor(b!) pres, "
         "bool accumulate=False) -> ()");
   m.def("pr_spmv_xcd(Tensor src, Tensor dstl, Tensor part_base, int e_max, Tensor c, "

@@ -224,15 +224,61 @@ __device__ __forceinline__ float from_fixed(uint64_t q, int K) {
   return (float)ldexp((double)q, -K);
 }
 
+// Where a destination's sum goes: acc/pres (the SpMV alone), or -- when r != nullptr --
+// straight through the PageRank rank / contribution update (same f32 arithmetic as
+// pr_update_kernel, pagerank.hip), which saves the acc/pres round trip and a launch.
+struct PbOut {
+  float* acc;
+  int32_t* pres;
+  const int32_t* outdeg;
+  float* r;
+  float* c;
+  const float* dang_in;
+  float* dang_out;
+  float q, invN;
+  int mode;
+};
+
+// returns this destination's dangling mass (standard semantics, fused update)
+__device__ __forceinline__ float pb_finish(const PbOut& o, int64_t v, uint64_t qs, int K) {
+  const float a = from_fixed(qs, K);
+  if (o.r == nullptr) {
+    o.acc[v] = a;
+    o.pres[v] = qs != 0;
+    return 0.f;
+  }
+  const int od = o.outdeg[v];
+  if (o.mode == 0) {
+    const bool p = qs != 0;
+    const float rv = p ? o.q * o.invN + (1.f - o.q) * a : -1.f;
+    o.r[v] = rv;
+    o.c[v] = (p && od > 0) ? rv / (float)od : -1.f;
+    return 0.f;
+  }
+  const float dang = o.dang_in ? o.dang_in[0] : 0.f;
+  const float rv = o.q * o.invN + (1.f - o.q) * (a + dang * o.invN);
+  o.r[v] = rv;
+  o.c[v] = od > 0 ? rv / (float)od : 0.f;
+  return od == 0 ? rv : 0.f;
+}
+
+__device__ __forceinline__ void pb_dangling(const PbOut& o, float dl) {
+  if (o.r != nullptr && o.mode == 1 && o.dang_out) {
+    dl = wave_sum(dl);
+    if ((threadIdx.x & 63) == 0 && dl != 0.f) atomicAdd(o.dang_out, dl);
+  }
+}
+
 // BW destinations per LDS bin (u64 fixed-point accumulators: f32 LDS atomics run at
 // ~0.33 lane-ops per CU-clock on gfx950, u32/u64 integer ones ~28x faster,
-// profiles/round3/pb/README.md); NW waves; a work item is a contiguous bin-major entry range
+// profiles/round3/pb/README.md); NW waves; a work item is a contiguous bin-major entry
+// range (possibly empty: every bin has >= 1 work item, so no output needs pre-zeroing)
 template <int BW, int NW>
 __global__ void __launch_bounds__(NW * 64)
 pb_accum_kernel(const float* __restrict__ val, const uint16_t* __restrict__ dloc,
                 const int32_t* __restrict__ wi_bin, const int64_t* __restrict__ wi_lo,
-                const int32_t* __restrict__ wi_slab, int64_t n_local, int K,
-                float* __restrict__ acc, int32_t* __restrict__ pres, uint64_t* __restrict__ slab) {
+                const int32_t* __restrict__ wi_slab, int64_t n_local, int K, PbOut o,
+                uint64_t* __restrict__ slab) {
   constexpr int U = 4;
   __shared__ unsigned long long s_acc[BW];
   const int w = blockIdx.x;
@@ -272,11 +318,9 @@ pb_accum_kernel(const float* __restrict__ val, const uint16_t* __restrict__ dloc
   const int nb = (int)min((int64_t)BW, n_local - base);
   const int sl = wi_slab[w];
   if (sl < 0) {                         // the bin's only work item: final values
-    for (int i = threadIdx.x; i < nb; i += NW * 64) {
-      const uint64_t q = s_acc[i];
-      acc[base + i] = from_fixed(q, K);
-      pres[base + i] = q != 0;
-    }
+    float dl = 0.f;
+    for (int i = threadIdx.x; i < nb; i += NW * 64) dl += pb_finish(o, base + i, s_acc[i], K);
+    pb_dangling(o, dl);
   } else {                              // partial of a split bin -> its slab
     uint64_t* dst = slab + (int64_t)sl * BW;
     for (int i = threadIdx.x; i < BW; i += NW * 64) dst[i] = s_acc[i];
@@ -288,17 +332,19 @@ template <int BW>
 __global__ void __launch_bounds__(256)
 pb_combine_kernel(const uint64_t* __restrict__ slab, const int32_t* __restrict__ split_bin,
                   const int32_t* __restrict__ split_first, const int32_t* __restrict__ split_count,
-                  int64_t n_local, int K, float* __restrict__ acc, int32_t* __restrict__ pres) {
+                  int64_t n_local, int K, PbOut o) {
   const int sb = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t base = (int64_t)split_bin[sb] * BW;
-  if (i >= BW || base + i >= n_local) return;
-  const uint64_t* p = slab + (int64_t)split_first[sb] * BW + i;
-  const int cnt = split_count[sb];
-  uint64_t q = 0;
-  for (int k = 0; k < cnt; ++k) q += p[(int64_t)k * BW];
-  acc[base + i] = from_fixed(q, K);
-  pres[base + i] = q != 0;
+  float dl = 0.f;
+  if (i < BW && base + i < n_local) {
+    const uint64_t* p = slab + (int64_t)split_first[sb] * BW + i;
+    const int cnt = split_count[sb];
+    uint64_t q = 0;
+    for (int k = 0; k < cnt; ++k) q += p[(int64_t)k * BW];
+    dl = pb_finish(o, base + i, q, K);
+  }
+  pb_dangling(o, dl);
 }
 
 }  // namespace dalgo
@@ -315,7 +361,9 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
                          const int64_t* wi_lo, const int32_t* wi_slab, int nwi, int bin_width,
                          int fixed_bits, int64_t n_local, float* acc, int32_t* pres, uint64_t* slab,
                          const int32_t* split_bin, const int32_t* split_first,
-                         const int32_t* split_count, int nsplit, hipStream_t st) {
+                         const int32_t* split_count, int nsplit, const int32_t* outdeg, float q,
+                         float invN, int mode, const float* dang_in, float* r, float* cn,
+                         float* dang_out, hipStream_t st) {
   if (src_span != 8192 || (bin_width != 8192 && bin_width != 16384) || fixed_bits < 1 ||
       fixed_bits > 126)
     return hipErrorInvalidValue;
@@ -335,20 +383,21 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
     DALGO_LAUNCH_CHECK();
   }
   if (nwi == 0) return hipSuccess;
+  const PbOut o{acc, pres, outdeg, r, cn, dang_in, dang_out, q, invN, mode};
   if (bin_width == 16384) {
     hipLaunchKernelGGL((pb_accum_kernel<16384, 16>), dim3(nwi), dim3(16 * 64), 0, st, val, dloc,
-                       wi_bin, wi_lo, wi_slab, n_local, fixed_bits, acc, pres, slab);
+                       wi_bin, wi_lo, wi_slab, n_local, fixed_bits, o, slab);
     DALGO_LAUNCH_CHECK();
     if (nsplit > 0)
       hipLaunchKernelGGL(pb_combine_kernel<16384>, dim3(16384 / 256, nsplit), dim3(256), 0, st,
-                         slab, split_bin, split_first, split_count, n_local, fixed_bits, acc, pres);
+                         slab, split_bin, split_first, split_count, n_local, fixed_bits, o);
   } else {
     hipLaunchKernelGGL((pb_accum_kernel<8192, 16>), dim3(nwi), dim3(16 * 64), 0, st, val, dloc,
-                       wi_bin, wi_lo, wi_slab, n_local, fixed_bits, acc, pres, slab);
+                       wi_bin, wi_lo, wi_slab, n_local, fixed_bits, o, slab);
     DALGO_LAUNCH_CHECK();
     if (nsplit > 0)
       hipLaunchKernelGGL(pb_combine_kernel<8192>, dim3(8192 / 256, nsplit), dim3(256), 0, st,
-                         slab, split_bin, split_first, split_count, n_local, fixed_bits, acc, pres);
+                         slab, split_bin, split_first, split_count, n_local, fixed_bits, o);
   }
   DALGO_LAUNCH_CHECK();
   return hipSuccess;

@@ -107,15 +107,19 @@ hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, con
                          int64_t n_c,
                          float* acc, int32_t* pres, int accumulate, hipStream_t st);
 // ---- K4b two-level propagation-blocked SpMV (pr_binned.hip)
+// r == nullptr: write acc / pres; otherwise fuse the PageRank update (pr_update semantics)
 hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int32_t* tile_ent,
                          const int32_t* tile_run, const int32_t* chunk_tile,
                          const int32_t* chunk_slo, const int32_t* chunk_ns,
                          const int32_t* chunk_run, const int32_t* run_delta, int nch,
-                         int max_runs, int src_span, const float* c, float* val, int64_t n_val, const uint16_t* dloc, const int32_t* wi_bin,
-                         const int64_t* wi_lo, const int32_t* wi_slab, int nwi, int bin_width,
-                         int fixed_bits, int64_t n_local, float* acc, int32_t* pres, uint64_t* slab,
+                         int max_runs, int src_span, const float* c, float* val, int64_t n_val,
+                         const uint16_t* dloc, const int32_t* wi_bin, const int64_t* wi_lo,
+                         const int32_t* wi_slab, int nwi, int bin_width, int fixed_bits,
+                         int64_t n_local, float* acc, int32_t* pres, uint64_t* slab,
                          const int32_t* split_bin, const int32_t* split_first,
-                         const int32_t* split_count, int nsplit, hipStream_t st);
+                         const int32_t* split_count, int nsplit, const int32_t* outdeg, float q,
+                         float invN, int mode, const float* dang_in, float* r, float* cn,
+                         float* dang_out, hipStream_t st);
 hipError_t dalgo_pr_spmv_xcd(const int32_t* src, const int32_t* dstl, const int64_t* part_base,
                              int64_t e_max_part, const float* c, float* acc_all, int64_t n_stride,
                              hipStream_t st);

@@ -86,9 +86,13 @@ class PageRank:
             self.c_slice = self.c_full[:sl]
         else:
             self.c_slice = torch.zeros(sl, dtype=fdt, device=dev)   # padded slice
-            self.c_full = torch.zeros(sl * world, dtype=fdt, device=dev)
+            # one rank: the slice IS the full vector (no exchange copy)
+            self.c_full = (self.c_slice if world == 1
+                           else torch.zeros(sl * world, dtype=fdt, device=dev))
         # K4b: built over the edge list the SpMV reads (c_full index space)
         self.layout = None
+        # DALGO_PR_FUSE=0: K4b writes acc / pres and the separate update kernel runs
+        self.fuse_update = os.environ.get("DALGO_PR_FUSE", "1") != "0"
         if self.spmv == "blocked":
             gsp = self.g_local if self.exchange == "ghost" else self.g
             self.layout = Gops.build_blocked(gsp, cfg.bin_width, cfg.chunk, cfg.tile)
@@ -166,25 +170,43 @@ class PageRank:
             torch.index_select(self.c_slice, 0, self.send_idx, out=self.send_buf)
             comm.all_to_all_single(self.c_full[self.g.slice_size:], self.send_buf,
                                    out_split=self.recv_split, in_split=self.send_split)
-        else:
+        elif self.world > 1:
             comm.all_gather_into(self.c_full, self.c_slice)
 
     def _spmv(self):
         if self.xl is not None:
             Gops.pr_spmv_xcd(self.xl, self.c_full)
             return
+        if self.layout is not None:
+            # K4b writes every destination and, with the update fused into its epilogue
+            # (ranks + next contributions), needs no separate update launch. c = r / outdeg
+            # <= 1 for both semantics: no host-side max needed.
+            nl = self.g.n_local
+            upd = None
+            if self.fuse_update:
+                if self.mode == 1:
+                    self.dang_next.zero_()
+                upd = dict(outdeg=self.outdeg, q=self.cfg.q, invN=self.invN, mode=self.mode,
+                           r=self.r, c=self.c_slice[:nl],
+                           dangling_in=self.dang if self.mode == 1 else None,
+                           dangling_out=self.dang_next if self.mode == 1 else None)
+            Gops.pb_spmv(self.layout, self.c_full, self.acc, self.pres, c_max=1.0, update=upd)
+            return
         self.acc.zero_()
         self.pres.zero_()
-        if self.layout is not None:
-            # c = r / outdeg <= 1 for both semantics: no host-side max needed
-            Gops.pb_spmv(self.layout, self.c_full, self.acc, self.pres, c_max=1.0)
-        elif self.exchange == "ghost":
+        if self.exchange == "ghost":
             Gops.pr_spmv(self.g_local, self.c_full, self.acc, self.pres)
         else:
             Gops.pr_spmv(self.g, self.c_full, self.acc, self.pres)
 
     def _update(self):
         nl = self.g.n_local
+        if self.layout is not None and self.fuse_update:
+            # the ranks / contributions were written by the K4b epilogue
+            if self.mode == 1:
+                comm.all_reduce_sum(self.dang_next)
+                self.dang, self.dang_next = self.dang_next, self.dang
+            return
         if self.mode == 1:
             self.dang_next.zero_()
         if self.xl is not None:

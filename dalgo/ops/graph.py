@@ -297,7 +297,8 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
     wb, wl, slab_h, sp_bin, sp_first, sp_cnt = [], [], [], [], [], []
     nslab = 0
     for b, (n_b, l_b) in enumerate(zip(cnt_h, lo_h)):
-        if n_b == 0:
+        if n_b == 0:                                  # empty bin: one empty item (writes zeros)
+            wb.append(b); wl.append(l_b); slab_h.append(-1)
             continue
         pieces = max(1, -(-n_b // cap))
         step = -(-n_b // pieces)
@@ -330,21 +331,28 @@ def pb_fixed_bits(lay: BlockedLayout, c_max: float) -> int:
 
 
 def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: torch.Tensor,
-            c_max: float | None = None):
-    """Same result as :func:`pr_spmv` (acc/pres zeroed by the caller). The GPU sums are exact
-    u64 fixed-point sums (order independent) rounded to f32 once. ``c_max``: an upper bound
-    of the non-negative c values (PageRank: 1.0); None = measured (one host sync)."""
+            c_max: float | None = None, update: dict | None = None):
+    """Same result as :func:`pr_spmv` (every acc / pres entry is written: no pre-zeroing).
+    The GPU sums are exact u64 fixed-point sums (order independent) rounded to f32 once.
+    ``c_max``: an upper bound of the non-negative c values (PageRank: 1.0); None = measured
+    (one host sync). ``update``: dict(outdeg, q, invN, mode, r, c, dangling_in, dangling_out)
+    fuses :func:`pr_update` into the epilogue (acc / pres are then not written)."""
     if c_full.numel() < lay.n_src or acc.numel() != lay.n_local:
         raise ValueError("pb_spmv: c_full / acc do not match the layout")
     if c_full.is_cuda:
         if c_max is None:
             c_max = float(c_full.max().item()) if c_full.numel() else 1.0
+        u = update or {}
         _ext.ops().pb_spmv(lay.srcl, lay.tile_e, lay.tile_ent, lay.tile_run, lay.chunk_tile,
                            lay.chunk_slo, lay.chunk_ns, lay.chunk_run, lay.run_delta, c_full,
                            lay.val, lay.dloc, lay.wi_bin, lay.wi_lo, lay.wi_slab, lay.bin_width,
                            lay.max_runs, pb_fixed_bits(lay, c_max), acc, pres, lay.slab, lay.split_bin,
-                           lay.split_first, lay.split_count)
+                           lay.split_first, lay.split_count, u.get("outdeg"), float(u.get("q", 0.0)),
+                           float(u.get("invN", 0.0)), int(u.get("mode", 0)), u.get("dangling_in"),
+                           u.get("r"), u.get("c"), u.get("dangling_out"))
         return
+    acc.zero_()
+    pres.zero_()
     # CPU reference of the two phases, decoding the same per-edge bits as the kernels
     if lay.n_chunks == 0:
         return
@@ -380,6 +388,9 @@ def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: t
     ph = torch.zeros_like(pres)
     ph.index_add_(0, dd, (hb > 0).to(pres.dtype))
     pres.copy_((ph > 0).to(pres.dtype))
+    if update is not None:
+        pr_update(acc, pres, update["outdeg"], update["q"], update["invN"], update["mode"],
+                  update["r"], update["c"], update.get("dangling_in"), update.get("dangling_out"))
 
 
 # ------------------------------------------------------------------ K4 kernels
