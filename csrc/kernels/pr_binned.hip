@@ -39,6 +39,8 @@
 
 namespace dalgo {
 
+constexpr int kPbDummy = 65536;   // padding floats after the entries (phase-1 dummy stores)
+
 namespace {
 
 // DPP moves (gfx9 family): lanes whose source is outside the pattern keep `old`
@@ -80,7 +82,7 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
                  const int32_t* __restrict__ chunk_tile, const int32_t* __restrict__ chunk_slo,
                  const int32_t* __restrict__ chunk_ns, const int32_t* __restrict__ chunk_run,
                  const int32_t* __restrict__ run_delta, const float* __restrict__ c,
-                 float* __restrict__ val, int64_t dummy) {
+                 float* __restrict__ val, int64_t dummy_base) {
   static_assert(S <= 16384, "local source index must leave bits 14, 15 for the markers");
   constexpr int EPL = 8;
   constexpr int D = 4;                        // steps of edges loaded ahead
@@ -105,6 +107,8 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
   const int wave = threadIdx.x >> 6;
   float* sv = s_v[wave];
   int32_t* sp = s_p[wave];
+  // dummy_base: kPbDummy floats past the entries, 64 per wave slot
+  const int64_t dummy = dummy_base + (int64_t)(((blockIdx.x * NW + wave) % (kPbDummy / 64)) * 64 + lane);
   const int t_end = chunk_tile[ch + 1];
   for (int t = chunk_tile[ch] + wave; t < t_end; t += NW) {
     const int64_t e_lo = tile_e[t], e_hi = tile_e[t + 1];
@@ -189,15 +193,16 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // EPL unconditional stores per lane (lanes past n_step write the dummy slot): a fixed
-      // store count keeps the compiler's vmcnt bookkeeping exact, so the D prefetched
-      // loads are not drained at every step
+      // EPL unconditional stores per lane (lanes past n_step write this wave's own dummy
+      // line group, so no single address is hammered by every wave): a fixed store count
+      // keeps the compiler's vmcnt bookkeeping exact, so the D prefetched loads are not
+      // drained at every step
       if constexpr (PROBE != 1) {                       // PROBE 1: timing without stores
 #pragma unroll
         for (int q = 0; q < EPL; ++q) {
           const int qi = lane + 64 * q;
           const bool ok = qi < n_step;
-          val[ok ? sp[qi] : dummy] = ok ? sv[qi] : 0.f;
+          val[ok ? (int64_t)sp[qi] : dummy] = ok ? sv[qi] : 0.f;
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -365,7 +370,7 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
                          float invN, int mode, const float* dang_in, float* r, float* cn,
                          float* dang_out, hipStream_t st) {
   if (src_span != 8192 || (bin_width != 8192 && bin_width != 16384) || fixed_bits < 1 ||
-      fixed_bits > 126)
+      fixed_bits > 126 || n_val < kPbDummy)
     return hipErrorInvalidValue;
   if (nch > 0) {
     // max_runs: the largest number of non-empty runs of one chunk (LDS table up to 4096)
@@ -374,7 +379,7 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
 #define DALGO_PB_GATHER(GR, PR)                                                                  \
     hipLaunchKernelGGL((pb_gather_kernel<8192, 4096, 8, GR, PR>), dim3(nch), dim3(8 * 64), 0, st, \
                        srcl, tile_e, tile_ent, tile_run, chunk_tile, chunk_slo, chunk_ns,        \
-                       chunk_run, run_delta, c, val, n_val - 1)
+                       chunk_run, run_delta, c, val, n_val - kPbDummy)
     if (max_runs > 4096) DALGO_PB_GATHER(true, 0);
     else if (probe == 1) DALGO_PB_GATHER(false, 1);
     else if (probe == 2) DALGO_PB_GATHER(false, 2);

@@ -133,6 +133,7 @@ def local_outdeg(shard: GraphShard) -> torch.Tensor:
 
 # ------------------------------------------------------------------ propagation blocking
 SRC_SPAN = 8192          # sources per chunk: the LDS table of pb_gather (csrc/kernels/pr_binned.hip)
+PB_DUMMY = 65536         # val / dloc padding after the entries (kPbDummy in pr_binned.hip)
 
 
 @dataclass
@@ -189,13 +190,17 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
     i64 = lambda x: x.to(torch.int64).contiguous()
     it = lambda x: torch.tensor(x, dtype=torch.int32, device=dev)
     nbins = max(1, (nl + bin_width - 1) // bin_width)
-    if E == 0:
+    if E == 0:        # no chunks; one empty work item per bin still writes every output
         z = torch.zeros(1, dtype=torch.int32, device=dev)
+        nb0 = (nl + bin_width - 1) // bin_width
         return BlockedLayout(torch.zeros(16, dtype=torch.int16, device=dev),
                              torch.zeros(1, dtype=torch.int64, device=dev), z[:0], z[:0], z.clone(),
-                             z[:0], z[:0], z.clone(), z[:0], torch.zeros(4, device=dev),
-                             torch.zeros(4, dtype=torch.int16, device=dev), z[:0],
-                             torch.zeros(1, dtype=torch.int64, device=dev), z[:0],
+                             z[:0], z[:0], z.clone(), z[:0],
+                             torch.zeros(PB_DUMMY, device=dev),
+                             torch.zeros(PB_DUMMY, dtype=torch.int16, device=dev),
+                             torch.arange(nb0, dtype=torch.int32, device=dev),
+                             torch.zeros(nb0 + 1, dtype=torch.int64, device=dev),
+                             torch.full((nb0,), -1, dtype=torch.int32, device=dev),
                              torch.zeros(1, dtype=torch.int64, device=dev), z[:0], z[:0], z[:0],
                              bin_width, nl, 0, 0, 0, 0, 0)
     s = shard.src[:E].to(torch.int64)
@@ -271,7 +276,7 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
     del sl, hbits, end, rk, rstart
     # bin-major destination offsets
     pos = torch.arange(nent, device=dev) + run_delta[run_of_ent]
-    n4 = (nent + 3) // 4 * 4 + 4                      # + padding: phase 1's dummy store slot
+    n4 = (nent + 3) // 4 * 4 + PB_DUMMY                # + phase 1's per-wave dummy store slots
     dloc = torch.zeros(n4, dtype=torch.int32, device=dev)
     dloc[pos] = (ent_dst % bin_width).to(torch.int32)
     dloc = dloc.to(torch.int16)                       # < 32768: exact as int16
@@ -354,8 +359,14 @@ def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: t
     acc.zero_()
     pres.zero_()
     # CPU reference of the two phases, decoding the same per-edge bits as the kernels
-    if lay.n_chunks == 0:
-        return
+    if lay.n_chunks > 0:
+        _pb_cpu(lay, c_full, acc, pres)
+    if update is not None:
+        pr_update(acc, pres, update["outdeg"], update["q"], update["invN"], update["mode"],
+                  update["r"], update["c"], update.get("dangling_in"), update.get("dangling_out"))
+
+
+def _pb_cpu(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: torch.Tensor):
     E = int(lay.tile_e[-1])
     h = (lay.srcl[:E].to(torch.int32) & 0xFFFF).long()
     nt = lay.tile_e.numel() - 1
@@ -388,9 +399,6 @@ def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: t
     ph = torch.zeros_like(pres)
     ph.index_add_(0, dd, (hb > 0).to(pres.dtype))
     pres.copy_((ph > 0).to(pres.dtype))
-    if update is not None:
-        pr_update(acc, pres, update["outdeg"], update["q"], update["invN"], update["mode"],
-                  update["r"], update["c"], update.get("dangling_in"), update.get("dangling_out"))
 
 
 # ------------------------------------------------------------------ K4 kernels

@@ -299,6 +299,21 @@ def test_pb_spmv_matches_pull(cuda, bw, chunk, tile, min_piece):
         assert torch.allclose(a2.double().cpu(), ref, rtol=2e-7, atol=1e-12)
 
 
+def test_pb_spmv_empty_shard_writes_zeros(cuda):
+    """A rank whose slice has no in-edges: every output is still written (no pre-zeroing)."""
+    from dalgo.ops import graph as G
+    src = torch.tensor([0, 1], dtype=torch.int32, device=cuda)
+    dst = torch.tensor([1, 0], dtype=torch.int32, device=cuda)
+    sh = G.build_shard(src, dst, 40000, 1, 2)
+    assert sh.n_edges == 0
+    lay = G.build_blocked(sh)
+    acc = torch.full((sh.n_local,), 5.0, device=cuda)
+    pres = torch.ones(sh.n_local, dtype=torch.int32, device=cuda)
+    G.pb_spmv(lay, torch.rand(40000, device=cuda), acc, pres)
+    torch.cuda.synchronize()
+    assert float(acc.abs().max()) == 0.0 and int(pres.max()) == 0
+
+
 def test_pagerank_blocked_scale_matches_pull(cuda):
     """Whole PageRank runs (reference + standard semantics) on an R-MAT graph: blocked == pull."""
     from dalgo.apps.pagerank_app import rmat_shard
