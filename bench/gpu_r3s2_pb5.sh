@@ -1,0 +1,8 @@
+set -o pipefail
+O=gpurun_out/r3s2pb5
+mkdir -p $O
+export PYTHONPATH=$PWD TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_algos.py -k "pb_spmv or blocked or pagerank" -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_pb.log 2>&1 || exit 1
+for i in 1 2; do
+  timeout -k 10 300 python bench/pagerank_bench.py > $O/pagerank_$i.log 2>&1 || exit 1
+done
