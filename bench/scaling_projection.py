@@ -9,7 +9,7 @@ scaling curve can be read as (per-rank compute) + (collective):
   ssgd     K1 + K8 per step on rows/W of the 10M x 1024 bf16 set    + one 4 KB all-reduce
   kmeans   assign + accumulate + update on 100M/W points (k = 1024)  + [k x 128 f32 + k] all-reduce
   pagerank rank 0's destination slice of the R-MAT scale-26 graph (dealt relabeling,
-           ghost-relabeled edge list): SpMV + update                 + ghost all_to_all (floats)
+           ghost-relabeled edge list): SpMV + update (K4b and pull)  + ghost all_to_all (floats)
 
 No collective runs here (one process); the compute-only throughput W x share / time is an
 upper bound that the measured SCALE run is compared against.
@@ -141,7 +141,17 @@ def pagerank(worlds, scale=26, edge_factor=16):
             G.pr_update(acc, pres, od, 0.15, 1.0 / n, 0, r, c[:sl])
         dt_split = timed(it_split, 5) if W > 1 else dt
         del g_own, g_gh
-        out[f"W{W}"] = {"edges_rank0": Ei, "iter_ms_rank0": dt * 1e3,
+        # K4b (default SpMV) over the same ghost-relabeled edge list, update fused
+        lay = G.build_blocked(g)
+        upd = dict(outdeg=od, q=0.15, invN=1.0 / n, mode=0, r=r, c=c[:sl])
+
+        def it_pb():
+            G.pb_spmv(lay, c, acc, pres, c_max=1.0, update=upd)
+        dt_pb = timed(it_pb, 5)
+        del lay
+        out[f"W{W}"] = {"edges_rank0": Ei, "iter_ms_rank0_k4b": dt_pb * 1e3,
+                        "compute_only_edges_per_s_whole_job_k4b": E / dt_pb,
+                        "iter_ms_rank0": dt * 1e3,
                         "iter_ms_rank0_split": dt_split * 1e3,
                         "ghost_edge_share_rank0": float((~own).float().mean().item()),
                         "compute_only_edges_per_s_whole_job": E / dt,

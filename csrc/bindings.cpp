@@ -833,7 +833,8 @@ void pr_spmv(const Tensor& src, const Tensor& dstl, const Tensor& c, Tensor acc,
 // established and asserted once by dalgo.ops.graph.build_blocked(); here the shapes,
 // dtypes and the bounds a kernel could overrun are checked.
 void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
-             const Tensor& tile_run, const Tensor& chunk_tile, const Tensor& chunk_slo,
+             const Tensor& tile_run, const Tensor& wu_tile, const Tensor& wu_chunk,
+             const Tensor& chunk_slo,
              const Tensor& chunk_ns, const Tensor& chunk_run, const Tensor& run_delta,
              const Tensor& c, Tensor val, const Tensor& dloc, const Tensor& wi_bin,
              const Tensor& wi_lo, const Tensor& wi_slab, int64_t bin_width, int64_t max_runs,
@@ -865,12 +866,13 @@ void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
               "pb: srcl int16, len % 16 == 0");
   check_dev(tile_e, "tile_e");
   TORCH_CHECK(tile_e.scalar_type() == at::kLong && tile_e.is_contiguous(), "tile_e int64");
-  for (const Tensor* t : {&tile_ent, &tile_run, &chunk_tile, &chunk_slo, &chunk_ns, &chunk_run,
+  for (const Tensor* t : {&tile_ent, &tile_run, &wu_tile, &wu_chunk, &chunk_slo, &chunk_ns, &chunk_run,
                           &run_delta})
     check_i32(*t, "pb index arrays");
   const int64_t nch = chunk_slo.numel();
   const int64_t nt = tile_ent.numel();
-  TORCH_CHECK(chunk_ns.numel() == nch && chunk_tile.numel() == nch + 1 && chunk_run.numel() == nch + 1 &&
+  const int64_t nwu = wu_chunk.numel();
+  TORCH_CHECK(chunk_ns.numel() == nch && wu_tile.numel() == nwu + 1 && chunk_run.numel() == nch + 1 &&
                   tile_e.numel() == nt + 1 && tile_run.numel() == nt,
               "pb: chunk / tile arrays");
   check_f32(c, "c");
@@ -901,7 +903,8 @@ void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
   DALGO_CHECK_HIP(
       dalgo_pb_spmv(reinterpret_cast<const uint16_t*>(srcl.data_ptr<int16_t>()),
                     tile_e.data_ptr<int64_t>(), tile_ent.data_ptr<int32_t>(), tile_run.data_ptr<int32_t>(),
-                    chunk_tile.data_ptr<int32_t>(), chunk_slo.data_ptr<int32_t>(),
+                    wu_tile.data_ptr<int32_t>(), wu_chunk.data_ptr<int32_t>(), (int)nwu,
+                    chunk_slo.data_ptr<int32_t>(),
                     chunk_ns.data_ptr<int32_t>(), chunk_run.data_ptr<int32_t>(),
                     run_delta.data_ptr<int32_t>(), (int)nch, (int)max_runs, 8192, c.data_ptr<float>(),
                     val.data_ptr<float>(), val.numel(), reinterpret_cast<const uint16_t*>(dloc.data_ptr<int16_t>()),
@@ -1285,7 +1288,8 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(d!)? shift2) -> ()");
   m.def("rmat_edges(int seed, int scale, int e_off, float a, float b, float c, bool scramble, "
         "Tensor(a!) src, Tensor(b!) dst) -> ()");
-  m.def("pb_spmv(Tensor srcl, Tensor tile_e, Tensor tile_ent, Tensor tile_run, Tensor chunk_tile, "
+  m.def("pb_spmv(Tensor srcl, Tensor tile_e, Tensor tile_ent, Tensor tile_run, Tensor wu_tile, "
+        "Tensor wu_chunk, "
         "Tensor chunk_slo, Tensor chunk_ns, Tensor chunk_run, Tensor run_delta, Tensor c, "
         "Tensor(a!) val, Tensor dloc, Tensor wi_bin, Tensor wi_lo, Tensor wi_slab, int bin_width, "
         "int max_runs, int fixed_bits, Tensor(b!) acc, Tensor(c!) pres, Tensor(d!) slab, "

@@ -79,7 +79,8 @@ template <int S, int R, int NW, bool GRUNS, int PROBE = 0>
 __global__ void __launch_bounds__(NW * 64)
 pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ tile_e,
                  const int32_t* __restrict__ tile_ent, const int32_t* __restrict__ tile_run,
-                 const int32_t* __restrict__ chunk_tile, const int32_t* __restrict__ chunk_slo,
+                 const int32_t* __restrict__ wu_tile, const int32_t* __restrict__ wu_chunk,
+                 const int32_t* __restrict__ chunk_slo,
                  const int32_t* __restrict__ chunk_ns, const int32_t* __restrict__ chunk_run,
                  const int32_t* __restrict__ run_delta, const float* __restrict__ c,
                  float* __restrict__ val, int64_t dummy_base) {
@@ -92,7 +93,11 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
   // the lane that stores it; stores go out as 64 consecutive entries per instruction
   __shared__ float s_v[NW][64 * EPL];
   __shared__ int32_t s_p[NW][64 * EPL];
-  const int ch = blockIdx.x;
+  // one workgroup per work unit: a range of one chunk's tiles (a large chunk is split
+  // over several workgroups, each staging the chunk's c range, so a hot chunk does not
+  // become the kernel's tail)
+  const int wu = blockIdx.x;
+  const int ch = wu_chunk[wu];
   const int slo = chunk_slo[ch], ns = chunk_ns[ch];
   const int r0 = chunk_run[ch], nr = chunk_run[ch + 1] - r0;
   for (int i = threadIdx.x; i < ns; i += NW * 64) {
@@ -109,8 +114,8 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
   int32_t* sp = s_p[wave];
   // dummy_base: kPbDummy floats past the entries, 64 per wave slot
   const int64_t dummy = dummy_base + (int64_t)(((blockIdx.x * NW + wave) % (kPbDummy / 64)) * 64 + lane);
-  const int t_end = chunk_tile[ch + 1];
-  for (int t = chunk_tile[ch] + wave; t < t_end; t += NW) {
+  const int t_end = wu_tile[wu + 1];
+  for (int t = wu_tile[wu] + wave; t < t_end; t += NW) {
     const int64_t e_lo = tile_e[t], e_hi = tile_e[t + 1];
     int64_t ent = tile_ent[t];                // chunk-major index of the next entry
     int run = tile_run[t];                    // run starts (in this chunk) before it
@@ -359,7 +364,8 @@ using namespace dalgo;
 extern "C" {
 
 hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int32_t* tile_ent,
-                         const int32_t* tile_run, const int32_t* chunk_tile,
+                         const int32_t* tile_run, const int32_t* wu_tile, const int32_t* wu_chunk,
+                         int nwu,
                          const int32_t* chunk_slo, const int32_t* chunk_ns,
                          const int32_t* chunk_run, const int32_t* run_delta, int nch,
                          int max_runs, int src_span, const float* c, float* val, int64_t n_val, const uint16_t* dloc, const int32_t* wi_bin,
@@ -372,13 +378,13 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
   if (src_span != 8192 || (bin_width != 8192 && bin_width != 16384) || fixed_bits < 1 ||
       fixed_bits > 126 || n_val < kPbDummy)
     return hipErrorInvalidValue;
-  if (nch > 0) {
+  if (nch > 0 && nwu > 0) {
     // max_runs: the largest number of non-empty runs of one chunk (LDS table up to 4096)
     // DALGO_PB_PROBE (timing only, wrong results): 1 = no entry stores, 2 = no c reads
     const int probe = env_int("DALGO_PB_PROBE", 0);
 #define DALGO_PB_GATHER(GR, PR)                                                                  \
-    hipLaunchKernelGGL((pb_gather_kernel<8192, 4096, 8, GR, PR>), dim3(nch), dim3(8 * 64), 0, st, \
-                       srcl, tile_e, tile_ent, tile_run, chunk_tile, chunk_slo, chunk_ns,        \
+    hipLaunchKernelGGL((pb_gather_kernel<8192, 4096, 8, GR, PR>), dim3(nwu), dim3(8 * 64), 0, st, \
+                       srcl, tile_e, tile_ent, tile_run, wu_tile, wu_chunk, chunk_slo, chunk_ns, \
                        chunk_run, run_delta, c, val, n_val - kPbDummy)
     if (max_runs > 4096) DALGO_PB_GATHER(true, 0);
     else if (probe == 1) DALGO_PB_GATHER(false, 1);

@@ -155,6 +155,8 @@ class BlockedLayout:
     tile_ent: torch.Tensor
     tile_run: torch.Tensor
     chunk_tile: torch.Tensor
+    wu_tile: torch.Tensor   # work units (one phase-1 workgroup each): tile ranges of one chunk
+    wu_chunk: torch.Tensor
     chunk_slo: torch.Tensor
     chunk_ns: torch.Tensor
     chunk_run: torch.Tensor
@@ -195,7 +197,7 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
         nb0 = (nl + bin_width - 1) // bin_width
         return BlockedLayout(torch.zeros(16, dtype=torch.int16, device=dev),
                              torch.zeros(1, dtype=torch.int64, device=dev), z[:0], z[:0], z.clone(),
-                             z[:0], z[:0], z.clone(), z[:0],
+                             z.clone(), z[:0], z[:0], z[:0], z.clone(), z[:0],
                              torch.zeros(PB_DUMMY, device=dev),
                              torch.zeros(PB_DUMMY, dtype=torch.int16, device=dev),
                              torch.arange(nb0, dtype=torch.int32, device=dev),
@@ -281,17 +283,32 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
     dloc[pos] = (ent_dst % bin_width).to(torch.int32)
     dloc = dloc.to(torch.int16)                       # < 32768: exact as int16
     del pos, ent_dst, ent_bin, ent_key
-    # tiles: ~tile edges, starting on an entry boundary, never crossing a chunk
+    # work units: a chunk is processed by ceil(E_chunk / wu_e) workgroups (wu_e ~ E / 4096:
+    # ~8 rounds of the resident workgroups, so the hot chunks are no kernel tail on small
+    # shards); tiles start on an entry boundary, never cross a work unit and are
+    # min(tile, ~E_unit / 16) edges (>= 1024) so that the 8 waves of a unit all get work
     ce_lo = e_start[torch.searchsorted(ent_chunk, torch.arange(nch, device=dev))]
-    tk = ent_chunk * (E // tile + 2) + (e_start - ce_lo[ent_chunk]) // tile
+    ce_n = torch.diff(torch.cat([ce_lo, torch.tensor([E], dtype=torch.int64, device=dev)]))
+    wu_e = max(1 << 15, E // 4096)
+    tlen = torch.clamp((torch.clamp(ce_n, max=wu_e) + 15) // 16, min=min(1024, tile), max=tile)
+    e_off = e_start - ce_lo[ent_chunk]
+    M = wu_e // min(1024, tile) + 2                   # > tiles per work unit
+    tk = ent_chunk * ((E // wu_e + 1) * M + 1) + (e_off // wu_e) * M + (e_off % wu_e) // tlen[ent_chunk]
     tnew = torch.ones(nent, dtype=torch.bool, device=dev)
     tnew[1:] = tk[1:] != tk[:-1]
     tile_ent = torch.nonzero(tnew).flatten()
     tile_e = torch.cat([e_start[tile_ent], torch.tensor([E], dtype=torch.int64, device=dev)])
     tile_chunk = ent_chunk[tile_ent]
     chunk_tile = torch.searchsorted(tile_chunk, torch.arange(nch + 1, device=dev))
+    wk = tile_chunk * (E + 2) + e_off[tile_ent] // wu_e
+    wnew = torch.ones_like(wk, dtype=torch.bool)
+    wnew[1:] = wk[1:] != wk[:-1]
+    wu_first = torch.nonzero(wnew).flatten()
+    wu_tile = torch.cat([wu_first, torch.tensor([tile_ent.numel()], dtype=torch.int64, device=dev)])
+    wu_chunk = tile_chunk[wu_first]
+    del wk, wnew, wu_first
     tile_run = torch.searchsorted(run_first, tile_ent) - chunk_run[tile_chunk]
-    del tk, tnew, e_start, ce_lo, ent_chunk
+    del tk, tnew, e_start, ce_lo, ce_n, tlen, e_off, ent_chunk
     # the bounds the kernels rely on (checked once, here)
     assert int(tile_e[-1]) <= srcl.numel() and int((slo + ns).max()) <= n_src
     assert run_first.numel() == int(chunk_run[-1])
@@ -318,7 +335,8 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
             else:
                 slab_h.append(-1)
     wl.append(nent)
-    return BlockedLayout(srcl, i64(tile_e), i32(tile_ent), i32(tile_run), i32(chunk_tile), i32(slo),
+    return BlockedLayout(srcl, i64(tile_e), i32(tile_ent), i32(tile_run), i32(chunk_tile),
+                         i32(wu_tile), i32(wu_chunk), i32(slo),
                          i32(ns), i32(chunk_run), i32(run_delta),
                          torch.zeros(n4, dtype=torch.float32, device=dev), dloc,
                          it(wb), torch.tensor(wl, dtype=torch.int64, device=dev), it(slab_h),
@@ -348,7 +366,7 @@ def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: t
         if c_max is None:
             c_max = float(c_full.max().item()) if c_full.numel() else 1.0
         u = update or {}
-        _ext.ops().pb_spmv(lay.srcl, lay.tile_e, lay.tile_ent, lay.tile_run, lay.chunk_tile,
+        _ext.ops().pb_spmv(lay.srcl, lay.tile_e, lay.tile_ent, lay.tile_run, lay.wu_tile, lay.wu_chunk,
                            lay.chunk_slo, lay.chunk_ns, lay.chunk_run, lay.run_delta, c_full,
                            lay.val, lay.dloc, lay.wi_bin, lay.wi_lo, lay.wi_slab, lay.bin_width,
                            lay.max_runs, pb_fixed_bits(lay, c_max), acc, pres, lay.slab, lay.split_bin,

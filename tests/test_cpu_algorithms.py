@@ -160,6 +160,11 @@ def test_pagerank_blocked_layout_cpu():
         te = lay.tile_e[:-1]
         assert bool(((te == 0) | end[(te - 1).clamp_min(0)]).all())
         assert bool((lay.wi_lo[1:] > lay.wi_lo[:-1]).all()) and int(lay.wi_lo[-1]) == lay.n_entries
+        # work units: consecutive tile ranges that partition the tiles, each inside one chunk
+        wt, ct = lay.wu_tile.long(), lay.chunk_tile.long()
+        wc = lay.wu_chunk.long()
+        assert int(wt[0]) == 0 and int(wt[-1]) == lay.tile_ent.numel()
+        assert bool((ct[wc] <= wt[:-1]).all()) and bool((wt[1:] <= ct[wc + 1]).all())
         # bin-major slots: a permutation of the entries
         mark = (h[end] >> 14) & 1
         pos = torch.arange(lay.n_entries) + lay.run_delta.long()[torch.cumsum(mark.long(), 0) - 1]
