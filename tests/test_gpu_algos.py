@@ -314,6 +314,28 @@ def test_pb_spmv_empty_shard_writes_zeros(cuda):
     assert float(acc.abs().max()) == 0.0 and int(pres.max()) == 0
 
 
+def test_pb_spmv_many_runs_global_delta_path(cuda):
+    """A chunk whose edges reach more than 4096 destination bins: phase 1 reads its run
+    deltas from global memory instead of the LDS table (the large-slice form)."""
+    from dalgo.ops import graph as G
+    g = torch.Generator().manual_seed(11)
+    n, E = 5000 * 8192, 200_000
+    src = torch.randint(0, 8192, (E,), generator=g, dtype=torch.int32)   # one source chunk
+    dst = torch.randint(0, n, (E,), generator=g, dtype=torch.int32)
+    sh = G.build_shard(src.to(cuda), dst.to(cuda), n, 0, 1)
+    lay = G.build_blocked(sh, 8192)
+    assert lay.max_runs > 4096
+    c = torch.rand(n, device=cuda)
+    a1 = torch.zeros(sh.n_local, device=cuda)
+    p1 = torch.zeros(sh.n_local, dtype=torch.int32, device=cuda)
+    a2, p2 = torch.zeros_like(a1), torch.zeros_like(p1)
+    G.pr_spmv(sh, c, a1, p1)
+    G.pb_spmv(lay, c, a2, p2)
+    torch.cuda.synchronize()
+    assert torch.equal(p1, p2)
+    assert torch.allclose(a1, a2, rtol=1e-6, atol=1e-7)
+
+
 def test_pagerank_blocked_scale_matches_pull(cuda):
     """Whole PageRank runs (reference + standard semantics) on an R-MAT graph: blocked == pull."""
     from dalgo.apps.pagerank_app import rmat_shard
