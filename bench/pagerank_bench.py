@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--no-reorder", action="store_true", help="keep scrambled R-MAT vertex ids")
     ap.add_argument("--spmv", default="blocked", choices=["pull", "xcd", "blocked"])
     ap.add_argument("--bin-width", type=int, default=16384)
-    ap.add_argument("--chunk", type=int, default=1 << 20)
+    ap.add_argument("--chunk", type=int, default=1 << 40)
     ap.add_argument("--tile", type=int, default=16384)
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
                     help="ranks (one per GPU); started here as a torchrun child when > 1")

@@ -146,7 +146,7 @@ def pagerank(worlds, scale=26, edge_factor=16):
         upd = dict(outdeg=od, q=0.15, invN=1.0 / n, mode=0, r=r, c=c[:sl])
 
         def it_pb():
-            G.pb_spmv(lay, c, acc, pres, c_max=1.0, update=upd)
+            G.pb_spmv(lay, c, acc, pres, update=upd)
         dt_pb = timed(it_pb, 5)
         del lay
         out[f"W{W}"] = {"edges_rank0": Ei, "iter_ms_rank0_k4b": dt_pb * 1e3,

@@ -838,7 +838,7 @@ void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
              const Tensor& chunk_ns, const Tensor& chunk_run, const Tensor& run_delta,
              const Tensor& c, Tensor val, const Tensor& dloc, const Tensor& wi_bin,
              const Tensor& wi_lo, const Tensor& wi_slab, int64_t bin_width, int64_t max_runs,
-             int64_t fixed_bits,
+             Tensor bound,
              Tensor acc, Tensor pres, Tensor slab, const Tensor& split_bin, const Tensor& split_first,
              const Tensor& split_count, const std::optional<Tensor>& outdeg, double q, double invN,
              int64_t mode, const std::optional<Tensor>& dangling_in, const std::optional<Tensor>& r,
@@ -890,6 +890,8 @@ void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
   check_f32(acc, "acc");
   check_i32(pres, "pres");
   TORCH_CHECK(pres.numel() >= acc.numel(), "pres size");
+  check_dev(bound, "bound");
+  TORCH_CHECK(bound.scalar_type() == at::kDouble && bound.numel() >= 1, "pb: bound f64[1]");
   check_dev(slab, "slab");
   TORCH_CHECK(slab.scalar_type() == at::kLong && slab.is_contiguous(), "pb: slab int64 (u64 fixed point)");
   check_i32(split_bin, "split_bin");
@@ -909,7 +911,7 @@ void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
                     run_delta.data_ptr<int32_t>(), (int)nch, (int)max_runs, 8192, c.data_ptr<float>(),
                     val.data_ptr<float>(), val.numel(), reinterpret_cast<const uint16_t*>(dloc.data_ptr<int16_t>()),
                     wi_bin.data_ptr<int32_t>(), wi_lo.data_ptr<int64_t>(), wi_slab.data_ptr<int32_t>(),
-                    (int)nwi, (int)bin_width, (int)fixed_bits, acc.numel(), acc.data_ptr<float>(),
+                    (int)nwi, (int)bin_width, bound.data_ptr<double>(), acc.numel(), acc.data_ptr<float>(),
                     pres.data_ptr<int32_t>(), reinterpret_cast<uint64_t*>(slab.data_ptr<int64_t>()),
                     split_bin.data_ptr<int32_t>(),
                     split_first.data_ptr<int32_t>(), split_count.data_ptr<int32_t>(), (int)nsp, od,
@@ -1292,7 +1294,7 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor wu_chunk, "
         "Tensor chunk_slo, Tensor chunk_ns, Tensor chunk_run, Tensor run_delta, Tensor c, "
         "Tensor(a!) val, Tensor dloc, Tensor wi_bin, Tensor wi_lo, Tensor wi_slab, int bin_width, "
-        "int max_runs, int fixed_bits, Tensor(b!) acc, Tensor(c!) pres, Tensor(d!) slab, "
+        "int max_runs, Tensor(h!) bound, Tensor(b!) acc, Tensor(c!) pres, Tensor(d!) slab, "
         "Tensor split_bin, Tensor split_first, Tensor split_count, Tensor? outdeg=None, "
         "float q=0., float invN=0., int mode=0, Tensor? dangling_in=None, Tensor(e!)? r=None, "
         "Tensor(f!)? c_out=None, Tensor(g!)? dangling_out=None) -> ()");

@@ -83,7 +83,7 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
                  const int32_t* __restrict__ chunk_slo,
                  const int32_t* __restrict__ chunk_ns, const int32_t* __restrict__ chunk_run,
                  const int32_t* __restrict__ run_delta, const float* __restrict__ c,
-                 float* __restrict__ val, int64_t dummy_base) {
+                 float* __restrict__ val, int64_t dummy_base, double* __restrict__ bound) {
   static_assert(S <= 16384, "local source index must leave bits 14, 15 for the markers");
   constexpr int EPL = 8;
   constexpr int D = 4;                        // steps of edges loaded ahead
@@ -100,9 +100,28 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
   const int ch = wu_chunk[wu];
   const int slo = chunk_slo[ch], ns = chunk_ns[ch];
   const int r0 = chunk_run[ch], nr = chunk_run[ch + 1] - r0;
+  float csum = 0.f;
   for (int i = threadIdx.x; i < ns; i += NW * 64) {
     const float v = c[slo + i];
     s_c[i] = v >= 0.f ? v : -0.0f;            // absent source: no record
+    csum += v >= 0.f ? v : 0.f;
+  }
+  // fixed-point range of phase 2: every destination sum is <= the sum of all present c
+  // the layout reads (one record per (source, destination) after dedup); the chunk's
+  // first work unit adds its source range
+  // (the partials go to wave 0's staging buffer, which only wave 0 -- the one reading
+  // them -- writes afterwards: a separate array would push the block past 80 KB of LDS,
+  // i.e. from 2 to 1 resident workgroup per CU)
+  if (wu == 0 || wu_chunk[wu - 1] != ch) {
+    csum = wave_sum(csum);
+    if ((threadIdx.x & 63) == 0) s_v[0][threadIdx.x >> 6] = csum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int w = 0; w < NW; ++w) t += (double)s_v[0][w];
+      // rounding slack: the f32 partial sums may be up to ~1e-6 relative low
+      atomicAdd(bound, t * (1.0 + 1e-5));
+    }
   }
   if constexpr (!GRUNS)
     for (int i = threadIdx.x; i < nr; i += NW * 64) s_d[i] = run_delta[r0 + i];
@@ -234,6 +253,14 @@ __device__ __forceinline__ float from_fixed(uint64_t q, int K) {
   return (float)ldexp((double)q, -K);
 }
 
+// fraction bits for a sum bound B: B * 2^K <= 2^62 (u64 headroom for the per-record
+// +1 units); derived on the device from phase 1's bound, so no host sync
+__device__ __forceinline__ int pb_fixed_bits(const double* bound) {
+  const double B = *bound;
+  if (!(B > 0.0)) return 100;
+  return min(100, max(1, 61 - ilogb(B)));
+}
+
 // Where a destination's sum goes: acc/pres (the SpMV alone), or -- when r != nullptr --
 // straight through the PageRank rank / contribution update (same f32 arithmetic as
 // pr_update_kernel, pagerank.hip), which saves the acc/pres round trip and a launch.
@@ -287,8 +314,9 @@ template <int BW, int NW>
 __global__ void __launch_bounds__(NW * 64)
 pb_accum_kernel(const float* __restrict__ val, const uint16_t* __restrict__ dloc,
                 const int32_t* __restrict__ wi_bin, const int64_t* __restrict__ wi_lo,
-                const int32_t* __restrict__ wi_slab, int64_t n_local, int K, PbOut o,
-                uint64_t* __restrict__ slab) {
+                const int32_t* __restrict__ wi_slab, int64_t n_local, const double* bound,
+                PbOut o, uint64_t* __restrict__ slab) {
+  const int K = pb_fixed_bits(bound);
   constexpr int U = 4;
   __shared__ unsigned long long s_acc[BW];
   const int w = blockIdx.x;
@@ -342,7 +370,8 @@ template <int BW>
 __global__ void __launch_bounds__(256)
 pb_combine_kernel(const uint64_t* __restrict__ slab, const int32_t* __restrict__ split_bin,
                   const int32_t* __restrict__ split_first, const int32_t* __restrict__ split_count,
-                  int64_t n_local, int K, PbOut o) {
+                  int64_t n_local, const double* bound, PbOut o) {
+  const int K = pb_fixed_bits(bound);
   const int sb = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t base = (int64_t)split_bin[sb] * BW;
@@ -370,14 +399,17 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
                          const int32_t* chunk_run, const int32_t* run_delta, int nch,
                          int max_runs, int src_span, const float* c, float* val, int64_t n_val, const uint16_t* dloc, const int32_t* wi_bin,
                          const int64_t* wi_lo, const int32_t* wi_slab, int nwi, int bin_width,
-                         int fixed_bits, int64_t n_local, float* acc, int32_t* pres, uint64_t* slab,
+                         double* bound, int64_t n_local, float* acc, int32_t* pres, uint64_t* slab,
                          const int32_t* split_bin, const int32_t* split_first,
                          const int32_t* split_count, int nsplit, const int32_t* outdeg, float q,
                          float invN, int mode, const float* dang_in, float* r, float* cn,
                          float* dang_out, hipStream_t st) {
-  if (src_span != 8192 || (bin_width != 8192 && bin_width != 16384) || fixed_bits < 1 ||
-      fixed_bits > 126 || n_val < kPbDummy)
+  if (src_span != 8192 || (bin_width != 8192 && bin_width != 16384) || n_val < kPbDummy)
     return hipErrorInvalidValue;
+  {
+    const hipError_t e = hipMemsetAsync(bound, 0, sizeof(double), st);
+    if (e != hipSuccess) return e;
+  }
   if (nch > 0 && nwu > 0) {
     // max_runs: the largest number of non-empty runs of one chunk (LDS table up to 4096)
     // DALGO_PB_PROBE (timing only, wrong results): 1 = no entry stores, 2 = no c reads
@@ -385,7 +417,7 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
 #define DALGO_PB_GATHER(GR, PR)                                                                  \
     hipLaunchKernelGGL((pb_gather_kernel<8192, 4096, 8, GR, PR>), dim3(nwu), dim3(8 * 64), 0, st, \
                        srcl, tile_e, tile_ent, tile_run, wu_tile, wu_chunk, chunk_slo, chunk_ns, \
-                       chunk_run, run_delta, c, val, n_val - kPbDummy)
+                       chunk_run, run_delta, c, val, n_val - kPbDummy, bound)
     if (max_runs > 4096) DALGO_PB_GATHER(true, 0);
     else if (probe == 1) DALGO_PB_GATHER(false, 1);
     else if (probe == 2) DALGO_PB_GATHER(false, 2);
@@ -397,18 +429,18 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
   const PbOut o{acc, pres, outdeg, r, cn, dang_in, dang_out, q, invN, mode};
   if (bin_width == 16384) {
     hipLaunchKernelGGL((pb_accum_kernel<16384, 16>), dim3(nwi), dim3(16 * 64), 0, st, val, dloc,
-                       wi_bin, wi_lo, wi_slab, n_local, fixed_bits, o, slab);
+                       wi_bin, wi_lo, wi_slab, n_local, bound, o, slab);
     DALGO_LAUNCH_CHECK();
     if (nsplit > 0)
       hipLaunchKernelGGL(pb_combine_kernel<16384>, dim3(16384 / 256, nsplit), dim3(256), 0, st,
-                         slab, split_bin, split_first, split_count, n_local, fixed_bits, o);
+                         slab, split_bin, split_first, split_count, n_local, bound, o);
   } else {
     hipLaunchKernelGGL((pb_accum_kernel<8192, 16>), dim3(nwi), dim3(16 * 64), 0, st, val, dloc,
-                       wi_bin, wi_lo, wi_slab, n_local, fixed_bits, o, slab);
+                       wi_bin, wi_lo, wi_slab, n_local, bound, o, slab);
     DALGO_LAUNCH_CHECK();
     if (nsplit > 0)
       hipLaunchKernelGGL(pb_combine_kernel<8192>, dim3(8192 / 256, nsplit), dim3(256), 0, st,
-                         slab, split_bin, split_first, split_count, n_local, fixed_bits, o);
+                         slab, split_bin, split_first, split_count, n_local, bound, o);
   }
   DALGO_LAUNCH_CHECK();
   return hipSuccess;

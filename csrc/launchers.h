@@ -115,7 +115,7 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
                          const int32_t* chunk_run, const int32_t* run_delta, int nch,
                          int max_runs, int src_span, const float* c, float* val, int64_t n_val,
                          const uint16_t* dloc, const int32_t* wi_bin, const int64_t* wi_lo,
-                         const int32_t* wi_slab, int nwi, int bin_width, int fixed_bits,
+                         const int32_t* wi_slab, int nwi, int bin_width, double* bound,
                          int64_t n_local, float* acc, int32_t* pres, uint64_t* slab,
                          const int32_t* split_bin, const int32_t* split_first,
                          const int32_t* split_count, int nsplit, const int32_t* outdeg, float q,

@@ -40,7 +40,8 @@ class PageRankConfig:
     spmv: str = ""               # "blocked" | "pull" | "xcd" ("" = DALGO_PR_SPMV env,
                                  # default blocked on GPUs (K4b), pull on the CPU)
     bin_width: int = 16384       # blocked: destination vertices per LDS bin (8192 | 16384)
-    chunk: int = 1 << 20         # blocked: ~edges per source chunk (<= 8192 sources)
+    chunk: int = 1 << 40         # blocked: ~edges per source chunk (<= 8192 sources; default:
+                                 # no edge cut, the work units balance phase 1)
     tile: int = 16384            # blocked: ~edges per phase-1 wave tile
     exchange: str = ""           # "ghost" | "allgather" ("" = DALGO_PR_EXCHANGE env, default
                                  # ghost on several ranks with the pull SpMV)
@@ -179,8 +180,7 @@ class PageRank:
             return
         if self.layout is not None:
             # K4b writes every destination and, with the update fused into its epilogue
-            # (ranks + next contributions), needs no separate update launch. c = r / outdeg
-            # <= 1 for both semantics: no host-side max needed.
+            # (ranks + next contributions), needs no separate update launch
             nl = self.g.n_local
             upd = None
             if self.fuse_update:
@@ -190,7 +190,7 @@ class PageRank:
                            r=self.r, c=self.c_slice[:nl],
                            dangling_in=self.dang if self.mode == 1 else None,
                            dangling_out=self.dang_next if self.mode == 1 else None)
-            Gops.pb_spmv(self.layout, self.c_full, self.acc, self.pres, c_max=1.0, update=upd)
+            Gops.pb_spmv(self.layout, self.c_full, self.acc, self.pres, update=upd)
             return
         self.acc.zero_()
         self.pres.zero_()

@@ -177,11 +177,16 @@ class BlockedLayout:
     n_src: int              # c index space the layout reads: c_full.numel() >= n_src
     max_indeg: int          # largest in-degree (fixed-point range of the accumulators)
     max_runs: int           # most non-empty runs in one chunk (phase 1 stages <= 4096 in LDS)
+    bound: torch.Tensor = None   # f64[1] device scratch: this call's destination-sum bound
 
 
-def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 1 << 20,
+def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 1 << 40,
                   tile: int = 16384, items: int = 2048, min_piece: int = 1 << 14) -> BlockedLayout:
-    """One-time construction (device sorts) from any shard (src in the c index space)."""
+    """One-time construction (device sorts) from any shard (src in the c index space).
+
+    chunk_edges: cut a source chunk after ~this many edges. The default (no cut: chunks are
+    the SRC_SPAN source blocks) combines the most records per entry (0.44 entries per edge
+    at R-MAT scale 26 vs 0.68 at 1M-edge chunks); load balance comes from the work units."""
     if bin_width not in (8192, 16384):
         raise ValueError("bin_width must be 8192 or 16384 (u64 LDS accumulator sizes of the kernel)")
     dev = shard.src.device
@@ -204,7 +209,8 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
                              torch.zeros(nb0 + 1, dtype=torch.int64, device=dev),
                              torch.full((nb0,), -1, dtype=torch.int32, device=dev),
                              torch.zeros(1, dtype=torch.int64, device=dev), z[:0], z[:0], z[:0],
-                             bin_width, nl, 0, 0, 0, 0, 0)
+                             bin_width, nl, 0, 0, 0, 0, 0,
+                             torch.zeros(1, dtype=torch.float64, device=dev))
     s = shard.src[:E].to(torch.int64)
     d = shard.dstl[:E].to(torch.int64)
     n_src = int(s.max().item()) + 1
@@ -342,34 +348,26 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
                          it(wb), torch.tensor(wl, dtype=torch.int64, device=dev), it(slab_h),
                          torch.zeros(max(nslab, 1) * bin_width, dtype=torch.int64, device=dev),
                          it(sp_bin), it(sp_first), it(sp_cnt), bin_width, nl, nch, nent, n_src,
-                         max_indeg, int((chunk_run[1:] - chunk_run[:-1]).max().item()))
-
-
-def pb_fixed_bits(lay: BlockedLayout, c_max: float) -> int:
-    """Fraction bits K of the u64 fixed-point accumulators: any destination's sum
-    (<= max_indeg * c_max) stays below 2^(63 - K)... with one bit of headroom."""
-    import math
-    bound = max(float(c_max), 1e-30) * max(lay.max_indeg, 1)
-    return int(min(100, max(1, 62 - math.ceil(math.log2(bound)))))
+                         max_indeg, int((chunk_run[1:] - chunk_run[:-1]).max().item()),
+                         torch.zeros(1, dtype=torch.float64, device=dev))
 
 
 def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: torch.Tensor,
-            c_max: float | None = None, update: dict | None = None):
+            update: dict | None = None):
     """Same result as :func:`pr_spmv` (every acc / pres entry is written: no pre-zeroing).
-    The GPU sums are exact u64 fixed-point sums (order independent) rounded to f32 once.
-    ``c_max``: an upper bound of the non-negative c values (PageRank: 1.0); None = measured
-    (one host sync). ``update``: dict(outdeg, q, invN, mode, r, c, dangling_in, dangling_out)
-    fuses :func:`pr_update` into the epilogue (acc / pres are then not written)."""
+    The GPU sums are exact u64 fixed-point sums (order independent) rounded to f32 once;
+    their scale 2^K comes from this call's data (phase 1 sums the present c values it
+    stages: no destination sum can exceed that), computed on the device (no host sync).
+    ``update``: dict(outdeg, q, invN, mode, r, c, dangling_in, dangling_out) fuses
+    :func:`pr_update` into the epilogue (acc / pres are then not written)."""
     if c_full.numel() < lay.n_src or acc.numel() != lay.n_local:
         raise ValueError("pb_spmv: c_full / acc do not match the layout")
     if c_full.is_cuda:
-        if c_max is None:
-            c_max = float(c_full.max().item()) if c_full.numel() else 1.0
         u = update or {}
         _ext.ops().pb_spmv(lay.srcl, lay.tile_e, lay.tile_ent, lay.tile_run, lay.wu_tile, lay.wu_chunk,
                            lay.chunk_slo, lay.chunk_ns, lay.chunk_run, lay.run_delta, c_full,
                            lay.val, lay.dloc, lay.wi_bin, lay.wi_lo, lay.wi_slab, lay.bin_width,
-                           lay.max_runs, pb_fixed_bits(lay, c_max), acc, pres, lay.slab, lay.split_bin,
+                           lay.max_runs, lay.bound, acc, pres, lay.slab, lay.split_bin,
                            lay.split_first, lay.split_count, u.get("outdeg"), float(u.get("q", 0.0)),
                            float(u.get("invN", 0.0)), int(u.get("mode", 0)), u.get("dangling_in"),
                            u.get("r"), u.get("c"), u.get("dangling_out"))
