@@ -31,8 +31,8 @@ class MonteCarloConfig:
 
 def estimate_pi(cfg: MonteCarloConfig, rank: int = 0, world: int = 1, device="cpu"):
     n = cfg.n_points
-    # even split with even offsets (a Philox block serves 2 points)
-    per = ((n // world) // 2) * 2
+    # even split with offsets on Philox-block boundaries (a block serves 3 points)
+    per = ((n // world) // 3) * 3
     lo = rank * per
     hi = n if rank == world - 1 else lo + per
     cnt = drandom.mc_pi_count(hi - lo, seed=cfg.seed, stream=cfg.stream, offset=lo, device=device)

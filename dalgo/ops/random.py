@@ -62,21 +62,28 @@ def mc_pi_count(n: int, *, seed: int = 0, stream: int = 0, offset: int = 0,
         cnt = torch.zeros(1, dtype=torch.int64, device=device)
         _ext.ops().mc_pi(int(seed), int(stream), int(offset), int(n), cnt)
         return cnt
+    # CPU mirror of K6: point i = slot i % 3 of Philox block i / 3 (21-bit coordinates)
+    if offset % 3:
+        raise ValueError("offset must be a multiple of 3 (point triples share a Philox block)")
     total = 0
-    chunk = 1 << 22
+    chunk = 3 << 21
     for s in range(0, n, chunk):
         m = min(chunk, n - s)
         i = np.arange(offset + s, offset + s + m, dtype=np.uint64)
-        blk = i >> np.uint64(1)
+        blk = i // np.uint64(3)
+        slot = (i % np.uint64(3)).astype(np.int64)
         c0 = (blk & np.uint64(0xFFFFFFFF)).astype(np.uint32)
         c1 = (blk >> np.uint64(32)).astype(np.uint32)
         c2 = np.full(i.shape, stream & 0xFFFFFFFF, dtype=np.uint32)
         c3 = np.full(i.shape, (stream >> 32) & 0xFFFFFFFF, dtype=np.uint32)
         x, y, z, w = philox.philox4x32_10(c0, c1, c2, c3, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-        odd = (i & np.uint64(1)).astype(bool)
-        u = np.where(odd, z, x)
-        v = np.where(odd, w, y)
-        fx = np.float32(2.0) * ((u >> np.uint32(8)).astype(np.float32) * np.float32(1 / 16777216.0)) - np.float32(1.0)
-        fy = np.float32(2.0) * ((v >> np.uint32(8)).astype(np.float32) * np.float32(1 / 16777216.0)) - np.float32(1.0)
+        sh, lo11, lo10 = np.uint32(11), np.uint32(0x7FF), np.uint32(0x3FF)
+        u2 = (x & lo11) | ((y & lo10) << sh)
+        v2 = (z & lo11) | ((w & lo10) << sh)
+        u = np.where(slot == 0, x >> sh, np.where(slot == 1, z >> sh, u2))
+        v = np.where(slot == 0, y >> sh, np.where(slot == 1, w >> sh, v2))
+        scale = np.float32(2.0 / 2097152.0)
+        fx = (u.astype(np.float32) + np.float32(0.5)) * scale - np.float32(1.0)
+        fy = (v.astype(np.float32) + np.float32(0.5)) * scale - np.float32(1.0)
         total += int(np.count_nonzero(fx * fx + fy * fy <= np.float32(1.0)))
     return torch.tensor([total], dtype=torch.int64)
