@@ -842,8 +842,10 @@ void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
              Tensor acc, Tensor pres, Tensor slab, const Tensor& split_bin, const Tensor& split_first,
              const Tensor& split_count, const std::optional<Tensor>& outdeg, double q, double invN,
              int64_t mode, const std::optional<Tensor>& dangling_in, const std::optional<Tensor>& r,
-             const std::optional<Tensor>& c_out, const std::optional<Tensor>& dangling_out) {
+             const std::optional<Tensor>& c_out, const std::optional<Tensor>& dangling_out,
+             int64_t wu_lo, int64_t wu_hi, int64_t phases) {
   check_dev(srcl, "srcl");
+  TORCH_CHECK(wu_lo >= 0 && wu_hi >= wu_lo && phases >= 1 && phases <= 3, "pb: work-unit range / phases");
   // fused PageRank update: all of outdeg / r / c_out or none
   const bool fused = r.has_value();
   TORCH_CHECK(fused == outdeg.has_value() && fused == c_out.has_value(), "pb: fused update args");
@@ -906,6 +908,7 @@ void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
       dalgo_pb_spmv(reinterpret_cast<const uint16_t*>(srcl.data_ptr<int16_t>()),
                     tile_e.data_ptr<int64_t>(), tile_ent.data_ptr<int32_t>(), tile_run.data_ptr<int32_t>(),
                     wu_tile.data_ptr<int32_t>(), wu_chunk.data_ptr<int32_t>(), (int)nwu,
+                    (int)std::min<int64_t>(wu_lo, nwu), (int)std::min<int64_t>(wu_hi, nwu), (int)phases,
                     chunk_slo.data_ptr<int32_t>(),
                     chunk_ns.data_ptr<int32_t>(), chunk_run.data_ptr<int32_t>(),
                     run_delta.data_ptr<int32_t>(), (int)nch, (int)max_runs, 8192, c.data_ptr<float>(),
@@ -1297,7 +1300,8 @@ TORCH_LIBRARY(dalgo, m) {
         "int max_runs, Tensor(h!) bound, Tensor(b!) acc, Tensor(c!) pres, Tensor(d!) slab, "
         "Tensor split_bin, Tensor split_first, Tensor split_count, Tensor? outdeg=None, "
         "float q=0., float invN=0., int mode=0, Tensor? dangling_in=None, Tensor(e!)? r=None, "
-        "Tensor(f!)? c_out=None, Tensor(g!)? dangling_out=None) -> ()");
+        "Tensor(f!)? c_out=None, Tensor(g!)? dangling_out=None, int wu_lo=0, "
+        "int wu_hi=2147483647, int phases=3) -> ()");
   m.def("pr_spmv(Tensor src, Tensor dstl, Tensor c, Tensor(a!) acc, Tensor(b!) pres, "
         "bool accumulate=False) -> ()");
   m.def("pr_spmv_xcd(Tensor src, Tensor dstl, Tensor part_base, int e_max, Tensor c, "

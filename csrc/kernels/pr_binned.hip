@@ -83,7 +83,8 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
                  const int32_t* __restrict__ chunk_slo,
                  const int32_t* __restrict__ chunk_ns, const int32_t* __restrict__ chunk_run,
                  const int32_t* __restrict__ run_delta, const float* __restrict__ c,
-                 float* __restrict__ val, int64_t dummy_base, double* __restrict__ bound) {
+                 float* __restrict__ val, int64_t dummy_base, double* __restrict__ bound,
+                 int wu0) {
   static_assert(S <= 16384, "local source index must leave bits 14, 15 for the markers");
   constexpr int EPL = 8;
   constexpr int D = 4;                        // steps of edges loaded ahead
@@ -96,7 +97,7 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
   // one workgroup per work unit: a range of one chunk's tiles (a large chunk is split
   // over several workgroups, each staging the chunk's c range, so a hot chunk does not
   // become the kernel's tail)
-  const int wu = blockIdx.x;
+  const int wu = wu0 + blockIdx.x;
   const int ch = wu_chunk[wu];
   const int slo = chunk_slo[ch], ns = chunk_ns[ch];
   const int r0 = chunk_run[ch], nr = chunk_run[ch + 1] - r0;
@@ -394,7 +395,7 @@ extern "C" {
 
 hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int32_t* tile_ent,
                          const int32_t* tile_run, const int32_t* wu_tile, const int32_t* wu_chunk,
-                         int nwu,
+                         int nwu, int wu_lo, int wu_hi, int phases,
                          const int32_t* chunk_slo, const int32_t* chunk_ns,
                          const int32_t* chunk_run, const int32_t* run_delta, int nch,
                          int max_runs, int src_span, const float* c, float* val, int64_t n_val, const uint16_t* dloc, const int32_t* wi_bin,
@@ -406,18 +407,22 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
                          float* dang_out, hipStream_t st) {
   if (src_span != 8192 || (bin_width != 8192 && bin_width != 16384) || n_val < kPbDummy)
     return hipErrorInvalidValue;
-  {
+  // phases: bit 0 = phase 1 over work units [wu_lo, wu_hi) (several calls may cover the
+  // units, the first one starting at 0 -- e.g. own-slice sources before the ghost
+  // exchange has landed), bit 1 = phase 2 (+ fused update)
+  wu_hi = std::min(wu_hi, nwu);
+  if ((phases & 1) && wu_lo == 0) {
     const hipError_t e = hipMemsetAsync(bound, 0, sizeof(double), st);
     if (e != hipSuccess) return e;
   }
-  if (nch > 0 && nwu > 0) {
+  if ((phases & 1) && nch > 0 && wu_hi > wu_lo) {
     // max_runs: the largest number of non-empty runs of one chunk (LDS table up to 4096)
     // DALGO_PB_PROBE (timing only, wrong results): 1 = no entry stores, 2 = no c reads
     const int probe = env_int("DALGO_PB_PROBE", 0);
 #define DALGO_PB_GATHER(GR, PR)                                                                  \
-    hipLaunchKernelGGL((pb_gather_kernel<8192, 4096, 8, GR, PR>), dim3(nwu), dim3(8 * 64), 0, st, \
+    hipLaunchKernelGGL((pb_gather_kernel<8192, 4096, 8, GR, PR>), dim3(wu_hi - wu_lo), dim3(8 * 64), 0, st, \
                        srcl, tile_e, tile_ent, tile_run, wu_tile, wu_chunk, chunk_slo, chunk_ns, \
-                       chunk_run, run_delta, c, val, n_val - kPbDummy, bound)
+                       chunk_run, run_delta, c, val, n_val - kPbDummy, bound, wu_lo)
     if (max_runs > 4096) DALGO_PB_GATHER(true, 0);
     else if (probe == 1) DALGO_PB_GATHER(false, 1);
     else if (probe == 2) DALGO_PB_GATHER(false, 2);
@@ -425,7 +430,7 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
 #undef DALGO_PB_GATHER
     DALGO_LAUNCH_CHECK();
   }
-  if (nwi == 0) return hipSuccess;
+  if (!(phases & 2) || nwi == 0) return hipSuccess;
   const PbOut o{acc, pres, outdeg, r, cn, dang_in, dang_out, q, invN, mode};
   if (bin_width == 16384) {
     hipLaunchKernelGGL((pb_accum_kernel<16384, 16>), dim3(nwi), dim3(16 * 64), 0, st, val, dloc,

@@ -110,7 +110,7 @@ hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, con
 // r == nullptr: write acc / pres; otherwise fuse the PageRank update (pr_update semantics)
 hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int32_t* tile_ent,
                          const int32_t* tile_run, const int32_t* wu_tile, const int32_t* wu_chunk,
-                         int nwu,
+                         int nwu, int wu_lo, int wu_hi, int phases,
                          const int32_t* chunk_slo, const int32_t* chunk_ns,
                          const int32_t* chunk_run, const int32_t* run_delta, int nch,
                          int max_runs, int src_span, const float* c, float* val, int64_t n_val,

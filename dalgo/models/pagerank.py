@@ -96,7 +96,8 @@ class PageRank:
         self.fuse_update = os.environ.get("DALGO_PR_FUSE", "1") != "0"
         if self.spmv == "blocked":
             gsp = self.g_local if self.exchange == "ghost" else self.g
-            self.layout = Gops.build_blocked(gsp, cfg.bin_width, cfg.chunk, cfg.tile)
+            self.layout = Gops.build_blocked(gsp, cfg.bin_width, cfg.chunk, cfg.tile,
+                                             src_split=sl if self.exchange == "ghost" else None)
         self.dang = torch.zeros(1, dtype=fdt, device=dev)
         self.dang_next = torch.zeros(1, dtype=fdt, device=dev)
         od = self.outdeg.to(fdt)
@@ -181,16 +182,8 @@ class PageRank:
         if self.layout is not None:
             # K4b writes every destination and, with the update fused into its epilogue
             # (ranks + next contributions), needs no separate update launch
-            nl = self.g.n_local
-            upd = None
-            if self.fuse_update:
-                if self.mode == 1:
-                    self.dang_next.zero_()
-                upd = dict(outdeg=self.outdeg, q=self.cfg.q, invN=self.invN, mode=self.mode,
-                           r=self.r, c=self.c_slice[:nl],
-                           dangling_in=self.dang if self.mode == 1 else None,
-                           dangling_out=self.dang_next if self.mode == 1 else None)
-            Gops.pb_spmv(self.layout, self.c_full, self.acc, self.pres, update=upd)
+            Gops.pb_spmv(self.layout, self.c_full, self.acc, self.pres,
+                         update=self._pb_update_args())
             return
         self.acc.zero_()
         self.pres.zero_()
@@ -198,6 +191,17 @@ class PageRank:
             Gops.pr_spmv(self.g_local, self.c_full, self.acc, self.pres)
         else:
             Gops.pr_spmv(self.g, self.c_full, self.acc, self.pres)
+
+    def _pb_update_args(self):
+        nl = self.g.n_local
+        if not self.fuse_update:
+            return None
+        if self.mode == 1:
+            self.dang_next.zero_()
+        return dict(outdeg=self.outdeg, q=self.cfg.q, invN=self.invN, mode=self.mode,
+                    r=self.r, c=self.c_slice[:nl],
+                    dangling_in=self.dang if self.mode == 1 else None,
+                    dangling_out=self.dang_next if self.mode == 1 else None)
 
     def _update(self):
         nl = self.g.n_local
@@ -221,6 +225,17 @@ class PageRank:
             comm.all_reduce_sum(self.dang_next)
             self.dang, self.dang_next = self.dang_next, self.dang
 
+    def _overlap_pb(self) -> bool:
+        """K4b with the ghost exchange: phase 1 over the own-slice source chunks runs while
+        the all_to_all of the ghost contributions is in flight, phase 1 over the ghost
+        chunks after it (DALGO_PR_OVERLAP: auto = when the own-slice units are at least a
+        quarter of all units, 1 / 0 force it on / off)."""
+        if self.layout is None or self.exchange != "ghost":
+            return False
+        env = os.environ.get("DALGO_PR_OVERLAP", "auto")
+        nwu = int(self.layout.wu_chunk.numel())
+        return env == "1" or (env == "auto" and nwu > 0 and self.layout.n_wu_below >= 0.25 * nwu)
+
     def _overlap(self) -> bool:
         """Ghost exchange under the SpMV over own-slice sources: the all_to_all writes only
         the ghost part of c_full, the first pass reads only the own part, the second adds
@@ -238,7 +253,26 @@ class PageRank:
         return self.timer.phase(name) if self.timer is not None else NULL_PHASE
 
     def step(self):
-        if self._overlap():
+        if self._overlap_pb():
+            lay = self.layout
+            if self.send_buf is None:
+                self.send_buf = torch.empty(self.send_idx.numel(), dtype=self.fdt, device=self.dev)
+            with self._ph("exchange_issue"):
+                torch.index_select(self.c_slice, 0, self.send_idx, out=self.send_buf)
+                work = comm.all_to_all_single(self.c_full[self.g.slice_size:], self.send_buf,
+                                              out_split=self.recv_split,
+                                              in_split=self.send_split, async_op=True)
+            with self._ph("spmv_own"):
+                Gops.pb_spmv(lay, self.c_full, self.acc, self.pres, wu_range=(0, lay.n_wu_below),
+                             phases=1)
+            with self._ph("exchange_wait"):
+                work.wait()
+            with self._ph("spmv_ghost"):
+                Gops.pb_spmv(lay, self.c_full, self.acc, self.pres,
+                             wu_range=(lay.n_wu_below, 1 << 31), phases=1)
+                Gops.pb_spmv(lay, self.c_full, self.acc, self.pres,
+                             update=self._pb_update_args(), phases=2)
+        elif self._overlap():
             if self.send_buf is None:
                 self.send_buf = torch.empty(self.send_idx.numel(), dtype=self.fdt, device=self.dev)
             with self._ph("exchange_issue"):

@@ -178,15 +178,20 @@ class BlockedLayout:
     max_indeg: int          # largest in-degree (fixed-point range of the accumulators)
     max_runs: int           # most non-empty runs in one chunk (phase 1 stages <= 4096 in LDS)
     bound: torch.Tensor = None   # f64[1] device scratch: this call's destination-sum bound
+    n_wu_below: int = 0          # work units whose sources are < src_split (build_blocked)
 
 
 def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 1 << 40,
-                  tile: int = 16384, items: int = 2048, min_piece: int = 1 << 14) -> BlockedLayout:
+                  tile: int = 16384, items: int = 2048, min_piece: int = 1 << 14,
+                  src_split: int | None = None) -> BlockedLayout:
     """One-time construction (device sorts) from any shard (src in the c index space).
 
     chunk_edges: cut a source chunk after ~this many edges. The default (no cut: chunks are
     the SRC_SPAN source blocks) combines the most records per entry (0.44 entries per edge
-    at R-MAT scale 26 vs 0.68 at 1M-edge chunks); load balance comes from the work units."""
+    at R-MAT scale 26 vs 0.68 at 1M-edge chunks); load balance comes from the work units.
+    src_split: no chunk straddles this source index, and ``n_wu_below`` counts the work
+    units of the sources below it (the own slice of the ghost index space: their phase 1
+    can run while the ghost contributions are still being exchanged)."""
     if bin_width not in (8192, 16384):
         raise ValueError("bin_width must be 8192 or 16384 (u64 LDS accumulator sizes of the kernel)")
     dev = shard.src.device
@@ -220,7 +225,14 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
     # boundaries); only sources with edges define chunks
     outd = torch.bincount(s, minlength=n_src)
     cs = torch.cumsum(outd, 0) - outd
-    key = (torch.arange(n_src, device=dev) // S) * (E // chunk_edges + 2) + cs // chunk_edges
+    ids = torch.arange(n_src, device=dev)
+    if src_split is not None:     # source blocks restart at the split: no straddling chunk
+        sp = int(src_split)
+        blk = torch.where(ids < sp, ids // S, (sp + S - 1) // S + (ids - sp) // S)
+    else:
+        blk = ids // S
+    key = blk * (E // chunk_edges + 2) + cs // chunk_edges
+    del ids, blk
     has = torch.nonzero(outd > 0).flatten()
     kh = key[has]
     new = torch.ones_like(kh, dtype=torch.bool)
@@ -349,17 +361,20 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
                          torch.zeros(max(nslab, 1) * bin_width, dtype=torch.int64, device=dev),
                          it(sp_bin), it(sp_first), it(sp_cnt), bin_width, nl, nch, nent, n_src,
                          max_indeg, int((chunk_run[1:] - chunk_run[:-1]).max().item()),
-                         torch.zeros(1, dtype=torch.float64, device=dev))
+                         torch.zeros(1, dtype=torch.float64, device=dev),
+                         int((slo[wu_chunk] < src_split).sum().item()) if src_split is not None else 0)
 
 
 def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: torch.Tensor,
-            update: dict | None = None):
+            update: dict | None = None, wu_range: tuple | None = None, phases: int = 3):
     """Same result as :func:`pr_spmv` (every acc / pres entry is written: no pre-zeroing).
     The GPU sums are exact u64 fixed-point sums (order independent) rounded to f32 once;
     their scale 2^K comes from this call's data (phase 1 sums the present c values it
     stages: no destination sum can exceed that), computed on the device (no host sync).
     ``update``: dict(outdeg, q, invN, mode, r, c, dangling_in, dangling_out) fuses
-    :func:`pr_update` into the epilogue (acc / pres are then not written)."""
+    :func:`pr_update` into the epilogue (acc / pres are then not written).
+    ``phases``: 1 = phase 1 over the work units ``wu_range`` only (the calls of one
+    product must cover all units, the first starting at 0), 2 = phase 2 only, 3 = both."""
     if c_full.numel() < lay.n_src or acc.numel() != lay.n_local:
         raise ValueError("pb_spmv: c_full / acc do not match the layout")
     if c_full.is_cuda:
@@ -370,7 +385,11 @@ def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: t
                            lay.max_runs, lay.bound, acc, pres, lay.slab, lay.split_bin,
                            lay.split_first, lay.split_count, u.get("outdeg"), float(u.get("q", 0.0)),
                            float(u.get("invN", 0.0)), int(u.get("mode", 0)), u.get("dangling_in"),
-                           u.get("r"), u.get("c"), u.get("dangling_out"))
+                           u.get("r"), u.get("c"), u.get("dangling_out"),
+                           int(wu_range[0]) if wu_range else 0,
+                           int(wu_range[1]) if wu_range else 2147483647, int(phases))
+        return
+    if not (phases & 2):          # CPU reference: everything happens in the phase-2 call
         return
     acc.zero_()
     pres.zero_()

@@ -336,6 +336,34 @@ def test_pb_spmv_fixed_point_scale_follows_data(cuda):
     assert torch.allclose(acc.double().cpu(), ref, rtol=3e-7, atol=1e-20)
 
 
+def test_pb_spmv_split_phases_bitwise_equal(cuda):
+    """Phase 1 split at the own-slice / ghost source boundary (the overlapped exchange's
+    call sequence) gives bitwise the same result as one call: the u64 fixed-point sums do
+    not depend on the order of the adds."""
+    from dalgo.ops import graph as G
+    g = torch.Generator().manual_seed(3)
+    n, E, split = 200_000, 3_000_000, 70_000
+    src = (torch.rand(E, generator=g) ** 2 * n).to(torch.int32)
+    dst = torch.randint(0, 100_000, (E,), generator=g, dtype=torch.int32)
+    sh = G.build_shard(src.to(cuda), dst.to(cuda), 100_000, 0, 1)
+    lay = G.build_blocked(sh, src_split=split)
+    nb = lay.n_wu_below
+    assert 0 < nb < lay.wu_chunk.numel()
+    slo = lay.chunk_slo.long()
+    wc = lay.wu_chunk.long()
+    assert bool((slo[wc[:nb]] < split).all()) and bool((slo[wc[nb:]] >= split).all())
+    c = torch.rand(n, generator=g).to(cuda)
+    a1 = torch.zeros(sh.n_local, device=cuda)
+    p1 = torch.zeros(sh.n_local, dtype=torch.int32, device=cuda)
+    a2, p2 = torch.zeros_like(a1), torch.zeros_like(p1)
+    G.pb_spmv(lay, c, a1, p1)
+    G.pb_spmv(lay, c, a2, p2, wu_range=(0, nb), phases=1)
+    G.pb_spmv(lay, c, a2, p2, wu_range=(nb, 1 << 31), phases=1)
+    G.pb_spmv(lay, c, a2, p2, phases=2)
+    torch.cuda.synchronize()
+    assert torch.equal(a1, a2) and torch.equal(p1, p2)
+
+
 def test_pb_spmv_many_runs_global_delta_path(cuda):
     """A chunk whose edges reach more than 4096 destination bins: phase 1 reads its run
     deltas from global memory instead of the LDS table (the large-slice form)."""
