@@ -7,32 +7,38 @@
 // Here the records are produced and reduced without a single random global access:
 //
 //   layout (built once, dalgo.ops.graph.build_blocked):
-//     chunks  : contiguous SOURCE ranges of <= S vertices (one LDS table of c each);
+//     chunks  : contiguous SOURCE ranges of <= S vertices (one LDS table of c each; on
+//               several ranks never straddling the own-slice / ghost boundary);
 //     edges   : sorted by (chunk, dst, src); per edge a u16 = local source (13 bits)
 //               | 0x4000 on the end edge of a run's first entry | 0x8000 on an entry's
 //               end edge;
 //     entries : distinct (chunk, dst) pairs = the chunk's records with equal destination
 //               pre-combined (an R-MAT hot destination appears once per chunk, not once
-//               per edge); stored BIN-MAJOR: all entries of destination bin b (BW
-//               destinations) contiguous, chunk order inside the bin;
+//               per edge: 0.44 entries per edge at scale 26); stored BIN-MAJOR: all
+//               entries of destination bin b (BW destinations) contiguous, chunk order
+//               inside the bin;
 //     runs    : the entries of one (chunk, bin); an entry's bin-major position is its
-//               chunk-major index + the run's delta (one int per non-empty run).
-//   phase 1 (pb_gather): one workgroup per chunk stages c[chunk sources] and the chunk's
-//     run deltas in LDS; its waves stream the chunk's edges (2 B each, coalesced), read c
-//     from LDS, reduce the (dst-sorted) records to one value per entry with a segmented
-//     DPP scan and store each entry value at its bin-major slot (runs: contiguous).
+//               chunk-major index + the run's delta (one int per non-empty run);
+//     work units: ranges of one chunk's wave tiles (a hot chunk spans several).
+//   phase 1 (pb_gather): one workgroup per work unit stages c[chunk sources] and the
+//     chunk's run deltas in LDS; its waves stream the edges (2 B each, a 4-step load
+//     ring), read c from LDS, reduce the (dst-sorted) records to one value per entry with
+//     a segmented DPP scan and store the entry values through a per-wave LDS transpose
+//     (64 consecutive entries per store instruction). The chunk's first unit also adds
+//     the chunk's present c to a bound of every destination sum.
 //   phase 2 (pb_accum): one workgroup per contiguous bin-major entry range (a bin, or a
 //     piece of a hot bin) streams (value, u16 destination offset) pairs and adds them
-//     into a BW-float LDS accumulator (ds_add_f32; inside a run every destination is
-//     distinct, so lanes do not collide on an address); it writes the bin's sums (or a
-//     partial slab that pb_combine sums in order).
+//     into BW u64 fixed-point LDS accumulators (ds_add_u64: gfx950 runs ds_add_f32 ~28x
+//     slower; integer sums are exact and order independent); the scale 2^K comes from
+//     phase 1's bound; it writes the bin's sums -- or runs the PageRank update on them --
+//     or a partial slab that pb_combine sums.
 //
-// Per edge 2 B, per entry 4 B written + 6 B read, all streamed: ~7-10 B per edge at
+// Per edge 2 B, per entry 4 B written + 6 B read, all streamed: ~6 B per edge at
 // scale 26 instead of the pull form's ~58 B of fabric traffic per edge.
 //
-// "reference" semantics: c < 0 marks an absent source; its record does not exist. The
-// accumulators start at -0.0f and absent records add -0.0f, so a destination received
-// >= 1 record iff the sign bit of its sum is clear (-0 + +0 = +0).
+// "reference" semantics: c < 0 marks an absent source; its record does not exist. Every
+// present record adds >= 1 fixed-point unit, so a destination received >= 1 record iff
+// its sum is non-zero.
 #include "dalgo/common.h"
 #include "launchers.h"   // the extern "C" entry point is checked against its declaration
 #include <algorithm>
