@@ -15,7 +15,7 @@ for set in "${SETS[@]}"; do
   i=$((i+1))
   timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $set --kernel-include-regex "pb_" \
     -d $O/p$i -o run --output-format csv -- python3 bench/pagerank_bench.py \
-    --spmv blocked --chunk 524288 --steps 2 --warmup 1 > $O/p$i.log 2>&1
+    --spmv blocked --steps 2 --warmup 1 > $O/p$i.log 2>&1
   rc=$?
   echo "pmc pb pass $i rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi
