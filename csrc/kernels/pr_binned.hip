@@ -317,14 +317,14 @@ __device__ __forceinline__ void pb_dangling(const PbOut& o, float dl) {
 // ~0.33 lane-ops per CU-clock on gfx950, u32/u64 integer ones ~28x faster,
 // profiles/round3/pb/README.md); NW waves; a work item is a contiguous bin-major entry
 // range (possibly empty: every bin has >= 1 work item, so no output needs pre-zeroing)
-template <int BW, int NW>
+template <int BW, int NW, int U = 4>
 __global__ void __launch_bounds__(NW * 64)
 pb_accum_kernel(const float* __restrict__ val, const uint16_t* __restrict__ dloc,
                 const int32_t* __restrict__ wi_bin, const int64_t* __restrict__ wi_lo,
                 const int32_t* __restrict__ wi_slab, int64_t n_local, const double* bound,
                 PbOut o, uint64_t* __restrict__ slab) {
   const int K = pb_fixed_bits(bound);
-  constexpr int U = 4;
+  // U: groups of 4 entries in flight per thread
   __shared__ unsigned long long s_acc[BW];
   const int w = blockIdx.x;
   const int b = wi_bin[w];
@@ -439,8 +439,13 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
   if (!(phases & 2) || nwi == 0) return hipSuccess;
   const PbOut o{acc, pres, outdeg, r, cn, dang_in, dang_out, q, invN, mode};
   if (bin_width == 16384) {
-    hipLaunchKernelGGL((pb_accum_kernel<16384, 16>), dim3(nwi), dim3(16 * 64), 0, st, val, dloc,
-                       wi_bin, wi_lo, wi_slab, n_local, bound, o, slab);
+    // DALGO_PB_U8=1: 8 groups of 4 entries in flight per thread (A/B knob)
+    if (env_int("DALGO_PB_U8", 0))
+      hipLaunchKernelGGL((pb_accum_kernel<16384, 16, 8>), dim3(nwi), dim3(16 * 64), 0, st, val, dloc,
+                         wi_bin, wi_lo, wi_slab, n_local, bound, o, slab);
+    else
+      hipLaunchKernelGGL((pb_accum_kernel<16384, 16>), dim3(nwi), dim3(16 * 64), 0, st, val, dloc,
+                         wi_bin, wi_lo, wi_slab, n_local, bound, o, slab);
     DALGO_LAUNCH_CHECK();
     if (nsplit > 0)
       hipLaunchKernelGGL(pb_combine_kernel<16384>, dim3(16384 / 256, nsplit), dim3(256), 0, st,
