@@ -64,6 +64,14 @@ def parse(argv=None):
                          "steps) after the warmup, untimed, and keep the fastest; env: the "
                          "DALGO_ONE_KERNEL / DALGO_PERSISTENT settings")
     ap.add_argument("--cal-steps", type=int, default=20, help="steps per candidate (auto)")
+    ap.add_argument("--cal-budget-s", type=float, default=20.0,
+                    help="wall-clock budget of the launch calibration (auto): no further "
+                         "candidate form is raced once it is spent")
+    ap.add_argument("--pg-timeout-s", type=float, default=120.0,
+                    help="process-group timeout: an RCCL collective stuck longer aborts the rank")
+    ap.add_argument("--deadline-s", type=float, default=420.0,
+                    help="wall-clock deadline per rank: past it the rank prints its stacks and "
+                         "exits 124 (a hang becomes a fast, rank-tagged failure); 0 = off")
     return ap.parse_args(argv)
 
 
@@ -92,10 +100,21 @@ def calibrate_launch(model, rt, a) -> dict:
     # the calibration trains extra steps: restore the model afterwards so the timed region
     # and the held-out witness see exactly warmup + steps training steps
     snap = model.state_dict()
+    # per-step first (no kernel waits on another GPU); the forms whose kernels spin on a
+    # peer (one-kernel / persistent release across ranks) only while every earlier form
+    # came back clean (collective device-error check after each) and the calibration
+    # stays inside its wall-clock budget (decided on the MAX-over-ranks clock, so every
+    # rank stops at the same candidate). On several ranks they also need the K11 exchange,
+    # which exists only if its collective self-test AND the start-up race passed.
     cands = {"per-step": (False, False), "one-kernel": (True, False), "persistent": (False, True)}
     res = {}
+    spent = 0.0
     for name, (one, pers) in cands.items():
+        if name != "per-step" and spent > a.cal_budget_s:
+            res["stopped"] = f"budget {a.cal_budget_s:.0f} s spent before {name}"
+            break
         model._ok1, model._okp = one, pers
+        t_all = time.perf_counter()
         model.run_steps(2)            # first launch of this form (code objects, workspaces)
         rt.synchronize()
         rt.barrier()
@@ -105,17 +124,20 @@ def calibrate_launch(model, rt, a) -> dict:
         rt.synchronize()
         rt.barrier()
         rt.synchronize()
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=rt.device)
+        el = torch.tensor([time.perf_counter() - t0, time.perf_counter() - t_all],
+                          dtype=torch.float64, device=rt.device)
         comm.all_reduce_max(el)
-        res[name] = float(el.item()) / a.cal_steps * 1e3
-    try:
-        comm.check_device_errors("launch calibration")
-    except comm.DeviceCollectiveError:
-        fallback_plain(model, rt, "launch calibration")
-        model.load_state_dict(snap)
-        rt.synchronize()
-        return {"failed": True, **res}
-    best = min(res, key=res.get)
+        res[name] = float(el[0].item()) / a.cal_steps * 1e3
+        spent += float(el[1].item())
+        try:
+            comm.check_device_errors(f"launch calibration ({name})")
+        except comm.DeviceCollectiveError:
+            fallback_plain(model, rt, f"launch calibration ({name})")
+            model.load_state_dict(snap)
+            rt.synchronize()
+            return {"failed": name, **res}
+    timed = {k: v for k, v in res.items() if k in cands}
+    best = min(timed, key=timed.get)
     model._ok1, model._okp = cands[best]
     model.load_state_dict(snap)
     rt.synchronize()
@@ -126,7 +148,12 @@ def fallback_plain(model, rt, why: str) -> None:
     """A device-side wait (K11 peer flag, persistent step release) timed out on some rank
     (collective check raised everywhere): switch EVERY rank to the plain per-step form
     over the process group -- no kernel waits on another GPU any more -- and clear the
-    error words. The caller restores the model and measures again."""
+    error words. The caller restores the model and measures again.
+
+    A launch that stopped early can leave partial gradient / count sums in the
+    ``[g || count]`` bucket: it is cleared here, and the next gradient launch is told
+    the bucket is NOT known to be zero (it clears it itself), so no stale partial sum
+    reaches an update or the sample count."""
     from dalgo.parallel import comm, xgmi
     if rt.is_main:
         print(f"[bench] device-side wait failed during {why}: falling back to per-step "
@@ -135,9 +162,12 @@ def fallback_plain(model, rt, why: str) -> None:
     xgmi.disable()
     if hasattr(model, "bucket"):
         model.bucket.xg = None
+        model.bucket.buffer.zero_()
+    model._g_zero = False
     model._ok1, model._okp = False, False
     model._okg = None
     comm.reset_device_errors()
+    rt.synchronize()
     rt.barrier()
 
 
@@ -179,7 +209,9 @@ def main(argv=None):
     from dalgo.parallel import comm, runtime
     from dalgo.parallel.sharding import make_layout
 
-    rt = runtime.init(backend=a.backend, device=a.device, app_name="bench-ssgd")
+    runtime.arm_watchdog(a.deadline_s, tag="bench")
+    rt = runtime.init(backend=a.backend, device=a.device, app_name="bench-ssgd",
+                      timeout_s=a.pg_timeout_s)
     W = rt.world_size
     from dalgo.parallel.launch import check_world
     check_world(a.gpus, W, "bench")
@@ -198,6 +230,7 @@ def main(argv=None):
 
     # model.run_steps(k): k full training steps, either k step() calls or (SSGD / GD with
     # DALGO_PERSISTENT=1) one persistent K1 launch running all k steps
+    snap = model.state_dict()        # the untrained model: a fallback re-measures from here
     model.run_steps(a.warmup)
     rt.synchronize()
     cal = calibrate_launch(model, rt, a) if a.launch == "auto" else {}
@@ -216,10 +249,13 @@ def main(argv=None):
         model.count_acc = None
         return el_, n_
 
-    snap = model.state_dict()
     elapsed, samples = timed()
     if os.environ.get("DALGO_TEST_FORCE_DEVICE_ERROR") == str(rt.rank):
-        comm._forced_error = 1      # test hook: as if a wait of the timed region timed out
+        # test hook: as if a wait of the timed region timed out, and as a launch that
+        # stopped early would, leave partial sums in the gradient bucket
+        comm._forced_error = 1
+        if hasattr(model, "bucket"):
+            model.bucket.buffer.fill_(1e3)
     fell_back = False
     # collective: MAX of every rank's device error words (K11 peer waits, persistent
     # step releases); if any wait timed out the timed steps are invalid: every rank
@@ -243,8 +279,6 @@ def main(argv=None):
     el = torch.tensor([elapsed], dtype=torch.float64, device=rt.device)
     comm.all_reduce_max(el)
     elapsed = float(el.item())
-    if cfg.algo not in ("ssgd", "gd"):
-        samples = a.rows * a.frac * a.steps * (cfg.n_local if cfg.algo in ("ma", "bmuf") else 1)
     value = samples / elapsed
     ar_us = allreduce_probe(model, rt) if cfg.algo in ("ssgd", "gd") else None
     acc = None
@@ -289,6 +323,7 @@ def main(argv=None):
                        "seq_len": None, "features": a.dim, "rows": a.rows,
                        "minibatch_fraction": a.frac, "parallelism": f"dp{W}",
                        "allreduce": allreduce, "launch": launch},
+            "samples_counted": int(round(samples)),
             "per_gpu_samples_per_s": value / W,
             "effective_hbm_GBps_per_gpu": value / W * a.dim * (2 if dtype == torch.bfloat16 else 4) / 1e9,
             "datagen_s": gen_s,
@@ -314,6 +349,7 @@ def main(argv=None):
             out["correctness_witness"] = witness
         print(json.dumps(out), flush=True)
     runtime.shutdown()
+    runtime.arm_watchdog(0)
     if witness is not None and not witness["passed"]:
         raise SystemExit(f"[bench] correctness witness failed: held-out accuracy {acc:.4f} < "
                          f"{witness['threshold']:.4f}")

@@ -54,10 +54,15 @@ __device__ __forceinline__ void xg_push_publish_wait(const XgLink& L, uint32_t e
     float* dst = xg_slot(L.bufs[r], ph, L.rank, L.slot);
     for (int i = tid; i < n; i += blockDim.x) dst[i] = get(i);
   }
+  // Ordering (HIP memory model, not a gfx9 side effect): every thread's slot stores are
+  // made visible at system scope by its own fence; the barrier then orders them before
+  // the flag-storing thread, whose flag store is itself a SYSTEM-scope RELEASE (fence
+  // cumulativity covers the other threads' stores it synchronised with through the
+  // barrier). The peer's ACQUIRE load of the flag below pairs with it.
   __threadfence_system();
   __syncthreads();
   if (tid < L.world)
-    __hip_atomic_store(&xg_flags(L.bufs[tid])[ph * kXgMaxRanks + L.rank], epoch, __ATOMIC_RELAXED,
+    __hip_atomic_store(&xg_flags(L.bufs[tid])[ph * kXgMaxRanks + L.rank], epoch, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid < L.world) {
     uint32_t* f = &xg_flags(L.bufs[L.rank])[ph * kXgMaxRanks + tid];

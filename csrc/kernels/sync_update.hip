@@ -35,7 +35,8 @@ struct UpdParams {
   const float* center; // [ld]        EASGD centre variable (local elastic)
   const float* S;      // [ld]        all-reduced sum of models (sync modes)
   float* Dl;           // [ld]        BMUF block-momentum buffer
-  double* count_acc;   // optional: += C[0] (throughput accounting without a host sync)
+  double* count_acc;   // optional: += sum of C[row] over the rows (throughput accounting
+                       //    without a host sync; the local modes add every local model's count)
   int n, ld, nrow;
   int mode, reg;
   float eta, lam, alpha, reg_alpha, mu, zeta, beta, inv_p;
@@ -57,7 +58,10 @@ __device__ __forceinline__ float reg_grad(float w, int reg, float a) {
 
 __global__ void __launch_bounds__(1024) sync_update_kernel(UpdParams p) {
   const int row = blockIdx.y;
-  if (p.count_acc && row == 0 && blockIdx.x == 0 && threadIdx.x == 0) p.count_acc[0] += (double)p.C[0];
+  if (p.count_acc && blockIdx.x == 0 && threadIdx.x == 0) {
+    if (p.nrow == 1) p.count_acc[0] += (double)p.C[0];
+    else atomicAdd(p.count_acc, (double)p.C[row]);
+  }
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < p.n; j += gridDim.x * blockDim.x) {
     const int64_t o = (int64_t)row * p.ld + j;
     float w = p.W[o];

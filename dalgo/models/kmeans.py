@@ -288,7 +288,7 @@ class KMeans:
         return self.cen.C
 
     def state_dict(self) -> dict:
-        return {"t": self.t, "centers": self.cen.C.detach().cpu(), "sse": list(self.history.sse),
+        return {"t": self.t, "centers": self.cen.C.detach().to("cpu", copy=True), "sse": list(self.history.sse),
                 "shift": list(self.history.shift)}
 
     def load_state_dict(self, sd: dict):

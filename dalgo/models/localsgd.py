@@ -253,12 +253,15 @@ class ParallelSGD:
             self._pending = False
 
     def global_sample_count(self) -> float:
-        """Total minibatch rows accumulated in count_acc, summed over ranks."""
+        """Total minibatch rows accumulated in count_acc, summed over ranks (exact, counted
+        on the device). SSGD / GD count the all-reduced minibatch once per step; MA / BMUF
+        / EASGD count every local model's minibatch at every local step (the gradient rows
+        actually processed: ma.py:98-102 re-reads the same sample n_local times)."""
         if self.count_acc is None:
             return 0.0
         cnt = self.count_acc.clone()
-        if self.fused:
-            comm.all_reduce_sum(cnt)   # the fused kernel accumulates LOCAL counts
+        if self.fused or self.cfg.algo in ("ma", "bmuf", "easgd"):
+            comm.all_reduce_sum(cnt)   # these kernels accumulate LOCAL counts
         return float(cnt.item())
 
     # ------------------------------------------------------- hipGraph replay
@@ -408,7 +411,7 @@ class ParallelSGD:
                         self._grad(self.W, stream)
                 with self._ph("local_update"):
                     U.sync_update(self.W, U.LOCAL_MEAN, G=self.G, C=self.C, eta=c.eta,
-                                  zero_grad=self._zg)
+                                  count_acc=self.count_acc, zero_grad=self._zg)
                 self._g_zero = True
             with self._ph("allreduce"):
                 U.rows_sum(self.W, self.S)
@@ -428,7 +431,8 @@ class ParallelSGD:
             self._finish_center()
             with self._ph("local_update"):
                 U.sync_update(self.W, U.LOCAL_ELASTIC, G=self.G, C=self.C, center=self.w,
-                              eta=c.eta, alpha=c.alpha, zero_grad=self._zg)
+                              eta=c.eta, alpha=c.alpha, count_acc=self.count_acc,
+                              zero_grad=self._zg)
             self._g_zero = True
             U.rows_sum(self.W, self.S)
             self._count_ar()
@@ -470,13 +474,16 @@ class ParallelSGD:
         with self._ph("update"):
             U.sync_update(self.w, U.ELASTIC_CENTER, S=self.S, beta=c.beta, inv_p=self.inv_p)
 
-    def _maybe_check_errors(self):
-        """Collective device-error check every DALGO_ERRCHECK_EVERY evaluations (default
-        100; also at end of fit, checkpoints and shutdown) instead of every evaluation:
-        each check is an extra collective plus host syncs on a ~50 us step."""
+    def _maybe_check_errors(self, reported: bool):
+        """Collective device-error check before an evaluation.
+
+        ``reported``: the result is about to leave the process (printed, handed to a
+        callback / metrics sink): always checked first, so no number computed after a
+        timed-out device wait is ever shown as valid. Silent evaluations (history only,
+        which fit() returns after its own end-of-fit check) are checked every 100th time:
+        each check is a collective plus host syncs on a ~50 us step."""
         self._n_evals = getattr(self, "_n_evals", 0) + 1
-        every = int(os.environ.get("DALGO_ERRCHECK_EVERY", "100"))
-        if every > 0 and self._n_evals % every == 0:
+        if reported or self._n_evals % 100 == 0:
             comm.check_device_errors("evaluation")
 
     def evaluate(self):
@@ -503,7 +510,7 @@ class ParallelSGD:
                 self.run_steps(k)
                 done += k
                 if ev and self.t % ev == 0:
-                    self._maybe_check_errors()
+                    self._maybe_check_errors(callback is not None)
                     acc, loss = self.evaluate()
                     self.history.accs.append(acc)
                     self.history.losses.append(loss)
@@ -517,7 +524,7 @@ class ParallelSGD:
                 self.rt.log("On iteration %d" % (self.t + 1))
             self.step()
             if self.cfg.eval_every and (self.t % self.cfg.eval_every == 0):
-                self._maybe_check_errors()
+                self._maybe_check_errors(verbose or callback is not None)
                 acc, loss = self.evaluate()
                 self.history.accs.append(acc)
                 self.history.losses.append(loss)
@@ -534,13 +541,15 @@ class ParallelSGD:
     def state_dict(self) -> dict:
         self._flush()
         self._finish_center()
-        sd = {"t": self.t, "w": self.w.detach().cpu(), "cfg": asdict(self.cfg),
+        # copy=True: on a CPU model .cpu() would alias the live tensors (a snapshot that
+        # later training overwrites)
+        sd = {"t": self.t, "w": self.w.detach().to("cpu", copy=True), "cfg": asdict(self.cfg),
               "accs": list(self.history.accs)}
         if hasattr(self, "W"):
-            sd["locals"] = self.W.detach().cpu()
+            sd["locals"] = self.W.detach().to("cpu", copy=True)
             sd["worker_lo"] = self.layout.worker_lo
         if hasattr(self, "Dl"):
-            sd["delta"] = self.Dl.detach().cpu()
+            sd["delta"] = self.Dl.detach().to("cpu", copy=True)
         return sd
 
     def load_state_dict(self, sd: dict):

@@ -238,6 +238,11 @@ def persistent_error() -> int:
     return e
 
 
+def persistent_used() -> bool:
+    """True once a persistent launch has armed its step-release workspace."""
+    return any(ws.epochs for ws in _ws_cache.values())
+
+
 def reset_persistent_error():
     for ws in _ws_cache.values():
         ws.perr.zero_()

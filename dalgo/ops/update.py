@@ -44,7 +44,7 @@ def sync_update(W: torch.Tensor, mode: int, *, n: int | None = None, G=None, C=N
         return W
     # ---- CPU reference (same math, W's dtype)
     if count_acc is not None:
-        count_acc += float(C.reshape(-1)[0])
+        count_acc += float(C.reshape(-1).double().sum())
     w = W2[:, :n]
     if mode == SSGD:
         c = C.reshape(-1, 1).to(w.dtype)

@@ -99,13 +99,31 @@ def _local_error_word() -> int:
     return e
 
 
+def device_waits_possible() -> bool:
+    """Could any device error word be set? Only K11 exchanges and persistent launches
+    wait on the device (both decided identically on every rank), plus the test hook
+    (an environment variable, identical on every rank). Without them the error check
+    skips its collective."""
+    import os
+    from dalgo.parallel import xgmi
+    if any(inst is not None for inst in xgmi._shared.values()):
+        return True
+    from dalgo.ops import lr as lr_ops
+    if lr_ops.persistent_used():
+        return True
+    return "DALGO_TEST_FORCE_DEVICE_ERROR" in os.environ
+
+
 def check_device_errors(where: str = "") -> None:
     """Collective (EVERY rank must call it at the same point): MAX over ranks of the
     device error words (K11 bounded peer-flag waits, persistent-launch step releases).
     Raises :class:`DeviceCollectiveError` on every rank if any rank's word is set, so
     no rank is left blocked in a later collective. The reduction goes through the
-    process group (never K11, whose failure it reports)."""
+    process group (never K11, whose failure it reports). A no-op (no collective, no
+    host sync) while no device-side wait exists on any rank."""
     global _error_seen
+    if not device_waits_possible():
+        return
     e = _local_error_word()
     if _active():
         dev = runtime.get().device if dist.get_backend() == "nccl" else torch.device("cpu")

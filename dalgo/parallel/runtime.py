@@ -107,6 +107,9 @@ def init(backend: str | None = None, *, device: str | None = None, app_name: str
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
+        # an RCCL collective that exceeds the process-group timeout aborts the
+        # communicator and raises on the rank (non-zero exit) instead of hanging
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         kw = dict(backend=backend, rank=rank, world_size=world,
                   timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
@@ -150,6 +153,37 @@ def spin_waits_allowed() -> bool:
 
 def get() -> Runtime:
     return _RT if _RT is not None else init()
+
+
+_watchdog = None
+
+
+def arm_watchdog(seconds: float, tag: str = "dalgo") -> None:
+    """Wall-clock deadline for this rank: if the process is still running after
+    ``seconds``, print a rank-tagged message plus every thread's Python stack to stderr
+    and exit with status 124. Turns a hang nothing else bounds (an RCCL call stuck below
+    the process-group timeout, a device wait spinning on a peer that never arrives) into
+    a fast, diagnosable failure. A second call re-arms; ``seconds <= 0`` disarms."""
+    global _watchdog
+    import threading
+    if _watchdog is not None:
+        _watchdog.cancel()
+        _watchdog = None
+    if seconds <= 0:
+        return
+
+    def fire():
+        import faulthandler
+        r = os.environ.get("RANK", "0")
+        print(f"[{tag}] rank {r}: wall-clock deadline of {seconds:.0f} s exceeded; "
+              f"stacks follow, exiting 124", file=sys.stderr, flush=True)
+        faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+        sys.stderr.flush()
+        os._exit(124)
+
+    _watchdog = threading.Timer(float(seconds), fire)
+    _watchdog.daemon = True
+    _watchdog.start()
 
 
 def shutdown():

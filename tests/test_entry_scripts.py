@@ -286,3 +286,31 @@ def test_bench_recovers_from_device_wait_failure():
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
     assert d["device_wait_fallback"] is True and d["n_gpus"] == 2
     assert d["correctness_witness"]["passed"]
+    # the hook also left partial sums (1e3) in the gradient bucket, as a launch that
+    # stopped early would: the fallback must clear them, so the re-measured run equals a
+    # clean run exactly (same sample count, same trained model)
+    clean = _run(["bench.py", "--gpus", "2", "--device", "cpu", "--backend", "gloo", "--rows",
+                  "20000", "--dim", "64", "--steps", "3", "--warmup", "1", "--dtype", "f32",
+                  "--n-test", "5000"], timeout=600)
+    c = json.loads([l for l in clean.splitlines() if l.startswith("{")][0])
+    assert c["device_wait_fallback"] is False
+    assert d["config"]["global_batch"] == c["config"]["global_batch"]
+    assert d["correctness_witness"]["heldout_logloss"] == c["correctness_witness"]["heldout_logloss"]
+
+
+def test_bench_local_sgd_counts_exact():
+    """MA / BMUF / EASGD report the device-counted sample total (every local model's
+    minibatch at every local step), not an estimate from rows * frac: it equals the exact
+    Bernoulli selection of the timed steps (same Philox stream as the kernels)."""
+    import numpy as np
+    from dalgo.utils.philox import bernoulli_mask
+    rows, warm, steps = 4000, 1, 3
+    for algo, n_local in (("bmuf", 5), ("easgd", 1)):
+        out = _run(["bench.py", "--device", "cpu", "--rows", str(rows), "--dim", "16", "--steps",
+                    str(steps), "--warmup", str(warm), "--dtype", "f32", "--n-test", "1000",
+                    "--algo", algo, "--no-eval"], timeout=600)
+        d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+        idx = np.arange(rows, dtype=np.uint64)
+        exp = n_local * sum(int(bernoulli_mask(42, t, idx, 0.1).sum())
+                            for t in range(warm, warm + steps))
+        assert d["samples_counted"] == exp, (algo, d["samples_counted"], exp)
