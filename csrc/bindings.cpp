@@ -430,8 +430,7 @@ void check_points(const Tensor& X, int DP) {
 }
 
 void kmeans_assign(const Tensor& X, const Tensor& Cq, const Tensor& hn, Tensor assign,
-                   const std::optional<Tensor>& mind, const std::optional<Tensor>& sse,
-                   int64_t variant) {
+                   const std::optional<Tensor>& mind, const std::optional<Tensor>& sse) {
   TORCH_CHECK(Cq.dim() == 2, "Cq [kpad, DP]");
   const int DP = (int)Cq.size(1);
   TORCH_CHECK(kmeans_dp(DP) == DP, "Cq columns must be 16/32/64/128");
@@ -463,76 +462,8 @@ void kmeans_assign(const Tensor& X, const Tensor& Cq, const Tensor& hn, Tensor a
   DeviceGuard guard(X.device());
   DALGO_CHECK_HIP(dalgo_kmeans_assign(X.data_ptr(), X.scalar_type() == at::kBFloat16, X.size(0),
                                       X.stride(0), DP, Cq.data_ptr(), hn.data_ptr<float>(),
-                                      (int)kpad, assign.data_ptr<int>(), md, ss, sse_mask, (int)variant,
-                                      cur_stream()),
+                                      (int)kpad, assign.data_ptr<int>(), md, ss, sse_mask, cur_stream()),
                   "kmeans_assign");
-}
-
-// centre-stationary K2 (bf16, DP 64/128, kpad 256/512/1024): xh = 0.5|x|^2 per point,
-// M >= max(xh) (both fixed for a point set; computed once by the caller)
-void kmeans_assign_cs(const Tensor& X, const Tensor& Cq, const Tensor& hn,
-                      const std::optional<Tensor>& xh,
-                      double M, Tensor assign, const std::optional<Tensor>& mind,
-                      const std::optional<Tensor>& sse) {
-  TORCH_CHECK(Cq.dim() == 2 && Cq.is_contiguous() && Cq.scalar_type() == at::kBFloat16, "Cq bf16 [kpad, DP]");
-  const int DP = (int)Cq.size(1);
-  TORCH_CHECK(DP == 64 || DP == 128, "kmeans_assign_cs: DP 64 or 128");
-  check_points(X, DP);
-  TORCH_CHECK(X.scalar_type() == at::kBFloat16, "kmeans_assign_cs: bf16 points");
-  check_dev(Cq, "Cq");
-  const int64_t kpad = Cq.size(0);
-  TORCH_CHECK(kpad == 256 || kpad == 512 || kpad == 1024, "kmeans_assign_cs: kpad 256/512/1024");
-  check_f32(hn, "hn");
-  TORCH_CHECK(hn.numel() >= kpad, "hn");
-  const float* xhp = nullptr;
-  if (xh.has_value()) {
-    check_f32(*xh, "xh");
-    TORCH_CHECK(xh->numel() >= X.size(0), "xh [n]");
-    xhp = xh->data_ptr<float>();
-  }
-  check_dev(assign, "assign");
-  TORCH_CHECK(assign.scalar_type() == at::kInt && assign.numel() >= X.size(0), "assign int32[n]");
-  float* md = nullptr;
-  if (mind.has_value()) {
-    check_f32(*mind, "mind");
-    TORCH_CHECK(mind->numel() >= X.size(0), "mind");
-    TORCH_CHECK(xhp != nullptr, "kmeans_assign_cs: per-point distances need xh");
-    md = mind->data_ptr<float>();
-  }
-  double* ss = nullptr;
-  int sse_mask = 0;
-  if (sse.has_value()) {
-    check_dev(*sse, "sse");
-    TORCH_CHECK(sse->scalar_type() == at::kDouble && sse->numel() >= 1 && sse->is_contiguous(),
-                "sse f64[>=1]");
-    ss = sse->data_ptr<double>();
-    while (sse_mask < 1023 && 2 * (sse_mask + 1) <= sse->numel()) sse_mask = 2 * sse_mask + 1;
-  }
-  DeviceGuard guard(X.device());
-  DALGO_CHECK_HIP(dalgo_kmeans_assign_cs(X.data_ptr(), X.size(0), X.stride(0), DP, Cq.data_ptr(),
-                                         (int)kpad, hn.data_ptr<float>(), xhp,
-                                         (float)M, assign.data_ptr<int>(), md, ss, sse_mask,
-                                         cur_stream()),
-                  "kmeans_assign_cs");
-}
-
-void kmeans_accumulate(const Tensor& X, const Tensor& assign, int64_t k, int64_t DP, Tensor S,
-                       Tensor cnt) {
-  TORCH_CHECK(kmeans_dp(DP) == DP, "DP must be 16/32/64/128");
-  check_points(X, (int)DP);
-  check_dev(assign, "assign");
-  TORCH_CHECK(assign.scalar_type() == at::kInt && assign.numel() >= X.size(0), "assign");
-  check_f32(S, "S");
-  TORCH_CHECK(S.numel() >= k * DP, "S [k, DP]");
-  check_dev(cnt, "cnt");
-  TORCH_CHECK(cnt.scalar_type() == at::kLong && cnt.numel() >= k, "cnt int64[k]");
-  DeviceGuard guard(X.device());
-  DALGO_CHECK_HIP(dalgo_kmeans_accumulate(X.data_ptr(), X.scalar_type() == at::kBFloat16,
-                                          X.size(0), X.stride(0), (int)DP,
-                                          assign.data_ptr<int>(), (int)k, S.data_ptr<float>(),
-                                          reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>()),
-                                          cur_stream()),
-                  "kmeans_accumulate");
 }
 
 void kmeans_accumulate_sorted(const Tensor& X, const Tensor& assign, int64_t k, int64_t DP,
@@ -582,46 +513,12 @@ void kmeans_diff(const Tensor& a_new, const Tensor& a_old, Tensor changed, Tenso
                   "kmeans_diff");
 }
 
-void kmeans_move(const Tensor& X, int64_t DP, const Tensor& changed, int64_t m,
-                 const Tensor& a_new, const Tensor& a_old, Tensor S64, Tensor cnt,
-                 const std::optional<Tensor>& xh, const std::optional<Tensor>& Q) {
-  TORCH_CHECK(kmeans_dp(DP) == DP, "DP must be 16/32/64/128");
-  check_points(X, (int)DP);
-  check_dev(changed, "changed");
-  TORCH_CHECK(changed.scalar_type() == at::kInt && m >= 0 && m <= changed.numel(), "changed");
-  TORCH_CHECK(a_new.scalar_type() == at::kInt && a_old.scalar_type() == at::kInt &&
-                  a_new.numel() >= X.size(0) && a_old.numel() >= X.size(0), "assignments");
-  check_dev(S64, "S64");
-  TORCH_CHECK(S64.scalar_type() == at::kDouble && S64.is_contiguous(), "S64 f64");
-  TORCH_CHECK(cnt.scalar_type() == at::kLong && cnt.is_contiguous(), "cnt int64");
-  TORCH_CHECK(S64.numel() % DP == 0 && cnt.numel() >= S64.numel() / DP, "S64 [k, DP] / cnt [k]");
-  const float* xp = nullptr;
-  double* qp = nullptr;
-  TORCH_CHECK(xh.has_value() == Q.has_value(), "kmeans_move: xh and Q together");
-  if (Q.has_value()) {
-    check_f32(*xh, "xh");
-    TORCH_CHECK(xh->numel() >= X.size(0), "xh [n]");
-    check_dev(*Q, "Q");
-    TORCH_CHECK(Q->scalar_type() == at::kDouble && Q->numel() >= cnt.numel() && Q->is_contiguous(),
-                "Q f64 [k]");
-    xp = xh->data_ptr<float>();
-    qp = Q->data_ptr<double>();
-  }
-  DeviceGuard guard(X.device());
-  DALGO_CHECK_HIP(dalgo_km_move(X.data_ptr(), X.scalar_type() == at::kBFloat16, X.stride(0), (int)DP,
-                                changed.data_ptr<int32_t>(), m, a_new.data_ptr<int32_t>(),
-                                a_old.data_ptr<int32_t>(), S64.data_ptr<double>(),
-                                reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>()),
-                                xp, qp, cur_stream()),
-                  "kmeans_move");
-}
-
 // sort-based incremental K3 (workspace from the caller, see dalgo_kmeans_move_sorted)
 void kmeans_move_sorted(const Tensor& X, int64_t DP, const Tensor& changed, int64_t m,
                         const Tensor& a_new, const Tensor& a_old, Tensor S64, Tensor cnt,
                         const std::optional<Tensor>& xh, const std::optional<Tensor>& Q, int64_t seg,
                         Tensor block_counts, Tensor cluster_start, Tensor seg_start, Tensor perm,
-                        Tensor ec, Tensor er) {
+                        Tensor ec, Tensor er, const std::optional<Tensor>& m_dev, int64_t chunk) {
   TORCH_CHECK(kmeans_dp(DP) == DP, "DP must be 16/32/64/128");
   check_points(X, (int)DP);
   check_dev(changed, "changed");
@@ -654,7 +551,14 @@ void kmeans_move_sorted(const Tensor& X, int64_t DP, const Tensor& changed, int6
                   cluster_start.numel() >= k + 1 && seg_start.numel() >= k + 1, "starts int64 [k+1]");
   TORCH_CHECK(perm.numel() >= 2 * m && ec.numel() >= 2 * m && er.numel() >= 2 * m, "[2m] workspace");
   const int64_t B = block_counts.numel() / std::max<int64_t>(k, 1);
-  TORCH_CHECK(B >= 1 && seg >= 1, "block_counts [B * k], seg >= 1");
+  TORCH_CHECK(B >= 1 && seg >= 1 && chunk >= 1, "block_counts [B * k], seg >= 1, chunk >= 1");
+  const unsigned long long* mdp = nullptr;
+  if (m_dev.has_value()) {   // device-resident count (<= m, the workspace capacity)
+    check_dev(*m_dev, "m_dev");
+    TORCH_CHECK(m_dev->scalar_type() == at::kLong && m_dev->numel() >= 1, "m_dev int64[1]");
+    mdp = reinterpret_cast<const unsigned long long*>(m_dev->data_ptr<int64_t>());
+    TORCH_CHECK(m <= X.size(0), "m_dev capacity: m <= n");
+  }
   DeviceGuard guard(X.device());
   DALGO_CHECK_HIP(dalgo_kmeans_move_sorted(
                       X.data_ptr(), X.scalar_type() == at::kBFloat16, X.stride(0), (int)DP,
@@ -662,19 +566,19 @@ void kmeans_move_sorted(const Tensor& X, int64_t DP, const Tensor& changed, int6
                       (int)k, (int)std::min<int64_t>(B, 1 << 20), (int)seg, ec.data_ptr<int>(), er.data_ptr<int>(),
                       block_counts.data_ptr<int>(), cluster_start.data_ptr<int64_t>(),
                       seg_start.data_ptr<int64_t>(), perm.data_ptr<int>(), S64.data_ptr<double>(),
-                      reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>()), xp, qp, cur_stream()),
+                      reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>()), xp, qp, mdp, chunk,
+                      cur_stream()),
                   "kmeans_move_sorted");
 }
 
 // bound-filtered Lloyd: active rows (u + delta[a] >= s[a]) -> idx, their assignment -> a_prev
 void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta, const Tensor& s,
-                   const Tensor& maxd, Tensor a_prev, Tensor idx, Tensor n_active) {
+                   Tensor a_prev, Tensor idx, Tensor n_active) {
   const int64_t n = assign.numel();
   check_i32(assign, "assign");
   check_f32(u, "u");
   check_f32(l, "l");
-  check_f32(maxd, "maxd");
-  TORCH_CHECK(l.numel() >= n && maxd.numel() >= 1, "kmeans_filter: l [n], maxd [1]");
+  TORCH_CHECK(l.numel() >= n, "kmeans_filter: l [n]");
   check_f32(delta, "delta");
   check_f32(s, "s");
   check_i32(a_prev, "a_prev");
@@ -684,7 +588,7 @@ void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta
   TORCH_CHECK(n_active.scalar_type() == at::kLong && n_active.numel() >= 1, "n_active int64[1]");
   DeviceGuard guard(assign.device());
   DALGO_CHECK_HIP(dalgo_km_filter(assign.data_ptr<int32_t>(), u.data_ptr<float>(), l.data_ptr<float>(),
-                                  delta.data_ptr<float>(), s.data_ptr<float>(), maxd.data_ptr<float>(), n,
+                                  delta.data_ptr<float>(), s.data_ptr<float>(), (int)delta.numel(), n,
                                   a_prev.data_ptr<int32_t>(), idx.data_ptr<int32_t>(),
                                   reinterpret_cast<unsigned long long*>(n_active.data_ptr<int64_t>()),
                                   idx.numel(), cur_stream()),
@@ -693,7 +597,8 @@ void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta
 
 void kmeans_post(const Tensor& idx, int64_t m, const Tensor& assign, const Tensor& a_prev,
                  const Tensor& mind, const Tensor& mind2, double tol, Tensor u, Tensor l,
-                 Tensor changed, Tensor n_changed) {
+                 Tensor changed, Tensor n_changed, const std::optional<Tensor>& m_dev,
+                 const std::optional<Tensor>& tol_dev) {
   check_f32(mind2, "mind2");
   check_f32(l, "l");
   check_i32(idx, "idx");
@@ -704,14 +609,43 @@ void kmeans_post(const Tensor& idx, int64_t m, const Tensor& assign, const Tenso
   check_i32(changed, "changed");
   TORCH_CHECK(m >= 0 && m <= idx.numel(), "kmeans_post: m");
   TORCH_CHECK(n_changed.scalar_type() == at::kLong && n_changed.numel() >= 1, "n_changed int64[1]");
+  const unsigned long long* mdp = nullptr;
+  if (m_dev.has_value()) {
+    check_dev(*m_dev, "m_dev");
+    TORCH_CHECK(m_dev->scalar_type() == at::kLong && m_dev->numel() >= 1, "m_dev int64[1]");
+    mdp = reinterpret_cast<const unsigned long long*>(m_dev->data_ptr<int64_t>());
+  }
+  const float* tp = nullptr;
+  if (tol_dev.has_value()) { check_f32(*tol_dev, "tol_dev"); tp = tol_dev->data_ptr<float>(); }
   DeviceGuard guard(idx.device());
   DALGO_CHECK_HIP(dalgo_km_post(idx.data_ptr<int32_t>(), m, assign.data_ptr<int32_t>(),
                                 a_prev.data_ptr<int32_t>(), mind.data_ptr<float>(),
                                 mind2.data_ptr<float>(), (float)tol, u.data_ptr<float>(),
                                 l.data_ptr<float>(), changed.data_ptr<int32_t>(),
                                 reinterpret_cast<unsigned long long*>(n_changed.data_ptr<int64_t>()),
-                                changed.numel(), cur_stream()),
+                                changed.numel(), mdp, tp, cur_stream()),
                   "kmeans_post");
+}
+
+// bound-filter geometry of new vs previous (rounded) centres: delta [k], s [k] (f32)
+void kmeans_centre_bounds(const Tensor& cnow, const Tensor& cprev, int64_t k, int64_t d,
+                          Tensor delta, Tensor s) {
+  check_dev(cnow, "cnow");
+  check_dev(cprev, "cprev");
+  TORCH_CHECK(cnow.dim() == 2 && cprev.dim() == 2 && cnow.is_contiguous() && cprev.is_contiguous() &&
+                  cnow.size(1) == cprev.size(1) && cnow.scalar_type() == cprev.scalar_type() &&
+                  cnow.size(0) >= k && cprev.size(0) >= k, "centres [>=k, DP], same dtype");
+  TORCH_CHECK(cnow.scalar_type() == at::kBFloat16 || cnow.scalar_type() == at::kFloat, "centres bf16/f32");
+  TORCH_CHECK(d >= 1 && d <= 128 && d <= cnow.size(1), "d <= 128");
+  check_f32(delta, "delta");
+  check_f32(s, "s");
+  TORCH_CHECK(delta.numel() >= k && s.numel() >= k, "delta / s [k]");
+  DeviceGuard guard(cnow.device());
+  DALGO_CHECK_HIP(dalgo_km_centre_bounds(cnow.data_ptr(), cprev.data_ptr(),
+                                         cnow.scalar_type() == at::kBFloat16, (int)k, (int)d,
+                                         (int)cnow.size(1), delta.data_ptr<float>(), s.data_ptr<float>(),
+                                         cur_stream()),
+                  "kmeans_centre_bounds");
 }
 
 void kmeans_qsum(const Tensor& assign, const Tensor& xh, int64_t k, Tensor Q) {
@@ -729,7 +663,8 @@ void kmeans_qsum(const Tensor& assign, const Tensor& xh, int64_t k, Tensor Q) {
 // K2 (variant 52) over the rows idx[0, m) only
 void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
                        const std::optional<Tensor>& idx, int64_t m, Tensor assign, Tensor mind,
-                       const std::optional<Tensor>& mind2) {
+                       const std::optional<Tensor>& mind2, const std::optional<Tensor>& m_dev,
+                       const std::optional<Tensor>& xh, const std::optional<Tensor>& xmax) {
   TORCH_CHECK(Cq.dim() == 2 && Cq.is_contiguous() && Cq.scalar_type() == at::kBFloat16, "Cq bf16");
   const int DP = (int)Cq.size(1);
   TORCH_CHECK(DP == 64 || DP == 128, "kmeans_assign_idx: DP 64 or 128");
@@ -755,11 +690,30 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
     TORCH_CHECK(mind2->numel() >= X.size(0), "mind2 [n]");
     m2 = mind2->data_ptr<float>();
   }
+  const unsigned long long* mdp = nullptr;
+  if (m_dev.has_value()) {   // rows = *m_dev (device), m = its upper bound
+    check_dev(*m_dev, "m_dev");
+    TORCH_CHECK(m_dev->scalar_type() == at::kLong && m_dev->numel() >= 1, "m_dev int64[1]");
+    TORCH_CHECK(m2 != nullptr, "kmeans_assign_idx: the device-count form is top-2");
+    mdp = reinterpret_cast<const unsigned long long*>(m_dev->data_ptr<int64_t>());
+  }
+  float* xhp = nullptr;
+  if (xh.has_value()) {
+    check_f32(*xh, "xh");
+    TORCH_CHECK(xh->numel() >= X.size(0), "xh [n]");
+    xhp = xh->data_ptr<float>();
+  }
+  unsigned* xmp = nullptr;
+  if (xmax.has_value()) {
+    check_dev(*xmax, "xmax");
+    TORCH_CHECK(xmax->scalar_type() == at::kInt && xmax->numel() >= 1, "xmax int32[1] (float bits)");
+    xmp = reinterpret_cast<unsigned*>(xmax->data_ptr<int32_t>());
+  }
   DeviceGuard guard(X.device());
   DALGO_CHECK_HIP(dalgo_kmeans_assign_idx(X.data_ptr(), m, X.stride(0), DP, Cq.data_ptr(),
                                           hn.data_ptr<float>(), (int)kpad, ip,
                                           assign.data_ptr<int>(), mind.data_ptr<float>(), m2,
-                                          nullptr, 0, cur_stream()),
+                                          nullptr, 0, mdp, xhp, xmp, cur_stream()),
                   "kmeans_assign_idx");
 }
 
@@ -1268,27 +1222,26 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("philox_fill(Tensor(a!) out, int D, int row_offset, int seed, int stream, int dist, "
         "float a, float b) -> ()");
   m.def("kmeans_assign(Tensor X, Tensor Cq, Tensor hn, Tensor(a!) assign, Tensor(b!)? mind, "
-        "Tensor(c!)? sse, int variant=5) -> ()");
-  m.def("kmeans_accumulate(Tensor X, Tensor assign, int k, int DP, Tensor(a!) S, Tensor(b!) cnt) -> ()");
+        "Tensor(c!)? sse) -> ()");
   m.def("kmeans_accumulate_sorted(Tensor X, Tensor assign, int k, int DP, int seg, "
         "Tensor(a!) block_counts, Tensor(b!) cluster_start, Tensor(c!) seg_start, Tensor(d!) perm, "
         "Tensor(e!) S, Tensor(f!) cnt) -> ()");
-  m.def("kmeans_assign_cs(Tensor X, Tensor Cq, Tensor hn, Tensor? xh, float M, Tensor(a!) assign, "
-        "Tensor(b!)? mind, Tensor(c!)? sse) -> ()");
   m.def("kmeans_diff(Tensor a_new, Tensor a_old, Tensor(a!) changed, Tensor(b!) n_changed) -> ()");
   m.def("kmeans_move_sorted(Tensor X, int DP, Tensor changed, int m, Tensor a_new, Tensor a_old, "
         "Tensor(a!) S64, Tensor(b!) cnt, Tensor? xh, Tensor(c!)? Q, int seg, Tensor(d!) block_counts, "
         "Tensor(e!) cluster_start, Tensor(f!) seg_start, Tensor(g!) perm, Tensor(h!) ec, "
-        "Tensor(i!) er) -> ()");
-  m.def("kmeans_move(Tensor X, int DP, Tensor changed, int m, Tensor a_new, Tensor a_old, "
-        "Tensor(a!) S64, Tensor(b!) cnt, Tensor? xh=None, Tensor(c!)? Q=None) -> ()");
-  m.def("kmeans_filter(Tensor assign, Tensor(a!) u, Tensor(e!) l, Tensor delta, Tensor s, Tensor maxd, "
+        "Tensor(i!) er, Tensor? m_dev=None, int chunk=65536) -> ()");
+  m.def("kmeans_filter(Tensor assign, Tensor(a!) u, Tensor(e!) l, Tensor delta, Tensor s, "
         "Tensor(b!) a_prev, Tensor(c!) idx, Tensor(d!) n_active) -> ()");
   m.def("kmeans_post(Tensor idx, int m, Tensor assign, Tensor a_prev, Tensor mind, Tensor mind2, "
-        "float tol, Tensor(a!) u, Tensor(d!) l, Tensor(b!) changed, Tensor(c!) n_changed) -> ()");
+        "float tol, Tensor(a!) u, Tensor(d!) l, Tensor(b!) changed, Tensor(c!) n_changed, "
+        "Tensor? m_dev=None, Tensor? tol_dev=None) -> ()");
+  m.def("kmeans_centre_bounds(Tensor cnow, Tensor cprev, int k, int d, Tensor(a!) delta, "
+        "Tensor(b!) s) -> ()");
   m.def("kmeans_qsum(Tensor assign, Tensor xh, int k, Tensor(a!) Q) -> ()");
   m.def("kmeans_assign_idx(Tensor X, Tensor Cq, Tensor hn, Tensor? idx, int m, Tensor(a!) assign, "
-        "Tensor(b!) mind, Tensor(c!)? mind2=None) -> ()");
+        "Tensor(b!) mind, Tensor(c!)? mind2=None, Tensor? m_dev=None, Tensor(d!)? xh=None, "
+        "Tensor(e!)? xmax=None) -> ()");
   m.def("kmeans_update(Tensor(a!) C, Tensor S, Tensor cnt, Tensor(b!) Cq, Tensor(c!) hn, "
         "Tensor(d!)? shift2) -> ()");
   m.def("rmat_edges(int seed, int scale, int e_off, float a, float b, float c, bool scramble, "
@@ -1367,14 +1320,12 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("pr_spmv_xcd", &pr_spmv_xcd);
   m.impl("pr_update_xcd", &pr_update_xcd);
   m.impl("kmeans_assign", &kmeans_assign);
-  m.impl("kmeans_accumulate", &kmeans_accumulate);
   m.impl("kmeans_update", &kmeans_update);
   m.impl("kmeans_diff", &kmeans_diff);
-  m.impl("kmeans_assign_cs", &kmeans_assign_cs);
-  m.impl("kmeans_move", &kmeans_move);
   m.impl("kmeans_move_sorted", &kmeans_move_sorted);
   m.impl("kmeans_filter", &kmeans_filter);
   m.impl("kmeans_post", &kmeans_post);
+  m.impl("kmeans_centre_bounds", &kmeans_centre_bounds);
   m.impl("kmeans_qsum", &kmeans_qsum);
   m.impl("kmeans_assign_idx", &kmeans_assign_idx);
   m.impl("kmeans_accumulate_sorted", &kmeans_accumulate_sorted);   // dispatches on its output counter

@@ -238,208 +238,6 @@ kmeans_assign_kernel(const T* __restrict__ X, int64_t n, int64_t ldx, const T* _
 }
 
 // ---------------------------------------------------------------------------
-// K2 "resident" form (bf16, default): one block per CU keeps up to 512 centres in
-// LDS for the whole launch — no per-chunk staging, no barriers in the main loop —
-// and its waves stream point tiles straight from HBM into VGPRs (the next tile
-// group is prefetched under the MFMAs). k > 512 runs as several launches (passes)
-// that carry the running (distance, id) per point in the output buffers.
-//
-// Distances, not scores: every centre row gets one extra 16-wide k-step
-// [h_hi, h_mid, h_lo, 1, 1, 1, 0...] (h = 0.5|c|^2 split into three bf16) and every
-// point [1, 1, 1, g_hi, g_mid, g_lo, 0...] (g = 0.5|x|^2), with the point itself
-// negated, so the MFMA (C = inline 0) produces 0.5|x - c|^2 >= 0 directly (f32
-// accumulate, the splits carry ~24 bits). Non-negative floats order like their
-// int bits, so the argmin is an integer min over keys (bits & ~0xff) | (sub << 4 | r):
-// one v_and_or + half a v_min3 per distance instead of compare + two selects.
-// Equal (truncated) distances resolve to the lower key = lower centre id, matching
-// the reference's strict '<' (k-means.py:25); the truncation is 2^-15 relative.
-template <int DP> struct ResGeom {
-  static constexpr int KS = DP / 16;       // data k-steps
-  static constexpr int KE = KS + 1;        // + the norm k-step
-  static constexpr int NJ = 2 * KE;        // 16-B pieces per LDS row
-  static constexpr int CB = 512;           // centres per pass (16 sub-tiles: 4-bit sub id)
-};
-
-__device__ __forceinline__ uint32_t bf16_pack2(float lo, float hi) {
-  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
-}
-// v ~= hi + mid + lo with each part a bf16 (about 24 significant bits in total)
-__device__ __forceinline__ void split3(float v, float& hi, float& mid, float& lo) {
-  hi = bf16_to_f32(f32_to_bf16(v));
-  const float r = v - hi;
-  mid = bf16_to_f32(f32_to_bf16(r));
-  lo = r - mid;
-}
-
-template <int DP, int NW, int PT>
-__global__ void __launch_bounds__(NW * 64, 1)
-kmeans_assign_res_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
-                         const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int c0,
-                         int ncen, int first, int last, int* __restrict__ assign,
-                         float* __restrict__ dist, double* __restrict__ sse, int sse_mask) {
-  using G = ResGeom<DP>;
-  constexpr int KS = G::KS, KE = G::KE, NJ = G::NJ;
-  constexpr int NT = NW * 64;
-  __shared__ uint4 s_c[G::CB * NJ];
-  __shared__ double s_sse[NW];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, cl = lane & 31;
-
-  // ---- stage this pass's centres (+ norm step) once; piece j of row c lives at
-  // j ^ ((c >> 4) & 1): conflict-free ds_read_b128 for the 32-row A reads
-  for (int i = tid; i < ncen * 2 * KS; i += NT) {
-    const int c = i / (2 * KS), j = i % (2 * KS);
-    s_c[c * NJ + (j ^ ((c >> 4) & 1))] =
-        *reinterpret_cast<const uint4*>(Cq + (int64_t)(c0 + c) * DP + j * 8);
-  }
-  for (int c = tid; c < ncen; c += NT) {
-    float a, b, d;
-    split3(hn[c0 + c], a, b, d);
-    const uint32_t one = 0x3f80u;
-    s_c[c * NJ + ((2 * KS) ^ ((c >> 4) & 1))] =
-        make_uint4(bf16_pack2(a, b), (uint32_t)f32_to_bf16(d) | (one << 16), one | (one << 16), 0u);
-    s_c[c * NJ + ((2 * KS + 1) ^ ((c >> 4) & 1))] = make_uint4(0u, 0u, 0u, 0u);
-  }
-  __syncthreads();
-
-  const int nsub = ncen / 32;
-  const int64_t ngrp = cdiv(n, (int64_t)PT * 32);
-  const int64_t GW = (int64_t)gridDim.x * NW;
-  double my_sse = 0.0;
-
-  // B fragments of a tile group: negated point pieces + the norm step. Rows past n
-  // re-read row n-1 (unconditional loads keep hipcc from branching around each one;
-  // those lanes' results are never written).
-  uint4 B[PT][KE];
-  auto load_raw = [&](uint4 (&R)[PT][KS], int64_t grp) {
-#pragma unroll
-    for (int t = 0; t < PT; ++t) {
-      const int64_t p = min(grp * (PT * 32) + t * 32 + cl, n - 1);
-      const uint16_t* src = X + p * ldx + h * 8;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) R[t][s] = *reinterpret_cast<const uint4*>(src + 16 * s);
-    }
-  };
-  auto finish = [&](const uint4 (&R)[PT][KS]) {
-#pragma unroll
-    for (int t = 0; t < PT; ++t) {
-      float g = 0.f;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const uint4 v = R[t][s];
-        g = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, v.x), __builtin_bit_cast(bf16x2, v.x), g, false);
-        g = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, v.y), __builtin_bit_cast(bf16x2, v.y), g, false);
-        g = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, v.z), __builtin_bit_cast(bf16x2, v.z), g, false);
-        g = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, v.w), __builtin_bit_cast(bf16x2, v.w), g, false);
-        B[t][s] = make_uint4(v.x ^ 0x80008000u, v.y ^ 0x80008000u, v.z ^ 0x80008000u, v.w ^ 0x80008000u);
-      }
-      auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(g), __float_as_uint(g), false, false);
-      g = 0.5f * (__uint_as_float(sw[0]) + __uint_as_float(sw[1]));
-      float a, b, d;
-      split3(g, a, b, d);
-      const uint32_t one = 0x3f80u;
-      B[t][KS] = h ? make_uint4(0u, 0u, 0u, 0u)
-                   : make_uint4(one | (one << 16), one | ((uint32_t)f32_to_bf16(a) << 16), bf16_pack2(b, d), 0u);
-    }
-  };
-
-  int64_t grp = (int64_t)blockIdx.x * NW + wid;
-  {
-    uint4 R[PT][KS];
-    load_raw(R, grp);
-    finish(R);
-  }
-  // piece (2s + h) ^ swz == 2s + (h ^ swz): one lane base, immediate offsets per k-step
-  const uint4* arow = &s_c[cl * NJ + (h ^ ((cl >> 4) & 1))];
-  // key mask held in a VGPR so the pack is ONE v_and_or_b32 (VGPR mask, SGPR key)
-  int kmask;
-  asm volatile("v_mov_b32 %0, 0xffffff00" : "=v"(kmask));
-  for (; grp < ngrp; grp += GW) {
-    uint4 Rn[PT][KS];
-    const bool more = grp + GW < ngrp;
-    if (more) load_raw(Rn, grp + GW);   // lands under this group's MFMAs
-
-    int key[PT];
-#pragma unroll
-    for (int t = 0; t < PT; ++t) key[t] = 0x7fffffff;
-    for (int sub = 0; sub < nsub; ++sub) {
-      uint4 a[KE];
-#pragma unroll
-      for (int s = 0; s < KE; ++s) a[s] = arow[sub * 32 * NJ + 2 * s];
-      f32x16 acc[PT];
-#pragma unroll
-      for (int t = 0; t < PT; ++t) {
-        const f32x16 z = {};
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[0]),
-                                                          __builtin_bit_cast(bf16x8, B[t][0]), z, 0, 0, 0);
-      }
-#pragma unroll
-      for (int s = 1; s < KE; ++s)
-#pragma unroll
-        for (int t = 0; t < PT; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[s]),
-                                                            __builtin_bit_cast(bf16x8, B[t][s]), acc[t], 0, 0, 0);
-      const int sk = sub << 4;
-#pragma unroll
-      for (int t = 0; t < PT; ++t) {
-        int m = key[t];
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const int k0 = (__float_as_int(acc[t][r]) & kmask) | __builtin_amdgcn_readfirstlane(sk | r);
-          const int k1 = (__float_as_int(acc[t][r + 1]) & kmask) | __builtin_amdgcn_readfirstlane(sk | (r + 1));
-          m = min(min(m, k0), k1);   // one v_min3_i32 per pair
-        }
-        key[t] = m;
-      }
-    }
-
-    // ---- decode, combine the lane halves (same point, disjoint centre rows),
-    // merge with the previous passes, write
-#pragma unroll
-    for (int t = 0; t < PT; ++t) {
-      const int kk = key[t];
-      const float v = __int_as_float(kk & ~0xff);
-      const int r = kk & 15;
-      const int ci = c0 + ((kk >> 4) & 15) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      auto sv = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-      auto si = __builtin_amdgcn_permlane32_swap((uint32_t)ci, (uint32_t)ci, false, false);
-      const float pv = __uint_as_float(h ? sv[0] : sv[1]);
-      const int pi = (int)(h ? si[0] : si[1]);
-      float bv = v;
-      int bi = ci;
-      if (pv < bv || (pv == bv && pi < bi)) { bv = pv; bi = pi; }
-      const int64_t p = grp * (PT * 32) + t * 32 + cl;
-      if (h == 0 && p < n) {
-        if (!first) {
-          const float ov = dist[p];
-          if (!(bv < ov)) { bv = ov; bi = assign[p]; }
-        }
-        assign[p] = bi;
-        if (last) {
-          const float dd = fmaxf(2.f * bv, 0.f);
-          dist[p] = dd;
-          my_sse += (double)dd;
-        } else {
-          dist[p] = bv;
-        }
-      }
-    }
-    if (more) finish(Rn);
-  }
-
-  if (sse && last) {
-    double s = my_sse;
-    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
-    if (lane == 0) s_sse[wid] = s;
-    __syncthreads();
-    if (tid == 0) {
-      double tot = 0.0;
-      for (int w = 0; w < NW; ++w) tot += s_sse[w];
-      atomicAdd(sse + (blockIdx.x & sse_mask), tot);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // K2 "pipelined" form (bf16): distance keys + LDS-DMA centre chunks, built so the
 // MFMA pipe is not starved by LDS waits, barriers or a long VALU epilogue:
 //  * centre chunks (32*NSUB rows) go global -> LDS by LDS-DMA (global_load_lds_dwordx4,
@@ -472,23 +270,32 @@ typedef __attribute__((address_space(3))) void km_lds_void;
 
 // SWP (software-pipelined argmin): the MFMA chains of sub-tile s run in the same basic
 // block as the argmin VALU of sub-tile s-1 (its accumulators stay live one sub-tile
-// longer, +16 VGPRs per point tile), so the key/min work of the LAST sub-tile of a chunk
-// no longer runs MFMA-less after the chunk's final MFMA (s_nop hazard pad + ~50 VALU +
-// DMA issue + barrier + LDS fragment latency per chunk in the plain form): it fills the
-// issue gaps of the next chunk's first MFMAs instead.
-// DIAG (diagnostics only, wrong assignments): 1 = argmin VALU replaced by one min per
-// tile, 2 = MFMAs removed (accumulator = C input, A fragments folded by XOR), 3 = 2
-// without the C-init LDS reads, 4 = 3 without the A-fragment LDS reads
+// longer), so the key/min work of the LAST sub-tile of a chunk no longer runs MFMA-less
+// after the chunk's final MFMA (s_nop hazard pad + ~50 VALU + DMA issue + barrier + LDS
+// fragment latency per chunk in the plain form): it fills the issue gaps of the next
+// chunk's first MFMAs instead. Only the last point tile's reduction is deferred (16
+// accumulator VGPRs instead of 16 * PT); the earlier tiles' reductions overlap the later
+// tiles' MFMA chains.
 // TOP2 (bound-filtered Lloyd): also keep each point's second-smallest key and write the
 // second-best distance (a lower bound: keys are truncated downwards) to mind2.
-template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, int SWP = 0, int DIAG = 0,
-          bool TOP2 = false>
+//
+// Work distribution: the grid walks "block tiles" of NW * PT * 32 points, block b taking
+// tiles b, b + gridDim.x, ... (one tile per block when the launcher sizes the grid to the
+// tile count). The number of rows may live on the device (`mcount`, the bound filter's
+// active count): the launcher then sizes a resident grid (blocks per CU x CUs) for the
+// worst case and no host sync is needed to launch.
+// Optional outputs of a full pass (the first bound-filtered iteration): xh[row] = 0.5|x|^2
+// and *xmax = max over the rows of 0.5|x|^2 (float bits, non-negative: integer max).
+template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, bool TOP2 = false,
+          bool LOOP = false>
 __global__ void __launch_bounds__(NW * 64, MINB)
 kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
                           const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int kpad,
                           int* __restrict__ assign, float* __restrict__ mind,
                           double* __restrict__ sse, int sse_mask,
-                          const int32_t* __restrict__ idx, float* __restrict__ mind2) {
+                          const int32_t* __restrict__ idx, float* __restrict__ mind2,
+                          const unsigned long long* __restrict__ mcount, float* __restrict__ xh,
+                          unsigned* __restrict__ xmax) {
   // idx (optional): the block's point j is row idx[j] of X (and of assign / mind), j < n
   // -- the bound-filtered form of Lloyd only re-assigns the points the filter keeps
   constexpr int KS = DP / 16;                  // 32x32x16 k-steps per centre row
@@ -498,6 +305,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   constexpr int NT = NW * 64;
   constexpr int CHP = CH * NJ;                 // 16-B pieces per chunk
   constexpr int GPT = CHP / NT;                // LDS-DMA instructions per thread per chunk
+  constexpr int TILE = NW * PT * 32;           // points per block tile
   static_assert(CHP % NT == 0, "chunk must be a whole number of block-wide DMA rounds");
   static_assert(NBUF >= 2 && NBUF <= 4, "double, triple or quadruple buffered chunks");
   __shared__ __attribute__((aligned(16))) uint4 s_c[NBUF * CHP];
@@ -506,8 +314,44 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   __shared__ double s_sse[NW];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, cl = lane & 31;
-  const int64_t pbase = ((int64_t)blockIdx.x * NW + wid) * (PT * 32);
   const int nchunk = kpad / CH;
+  if (mcount != nullptr) n = min(n, (int64_t)*mcount);
+  const int64_t ntile = (n + TILE - 1) / TILE;
+
+  // per-thread DMA sources: slot q = g*NT + tid of the chunk image
+  int src_off[GPT];
+#pragma unroll
+  for (int g = 0; g < GPT; ++g) {
+    const int q = g * NT + tid, row = q / NJ, jj = q % NJ;
+    src_off[g] = row * DP + (jj ^ (row & SWZ)) * 8;
+  }
+  // Issued as inline asm: with the builtin, hipcc cannot tell the DMA target from the
+  // chunk being read and drains vmcnt(0) before every ds_read (the chunk in flight
+  // would then never overlap compute). The counted waits below are the only waits.
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(km_lds_void*)s_c;
+  auto issue = [&](int ch) {
+    const uint16_t* base = Cq + (int64_t)ch * CH * DP;
+    const uint32_t dst = lds0 + (uint32_t)(((ch % NBUF) * CHP) * 16);
+#pragma unroll
+    for (int g = 0; g < GPT; ++g) {
+      const uint32_t m0v = __builtin_amdgcn_readfirstlane(dst + (uint32_t)((g * NT + wid * 64) * 16));
+      const uint16_t* src = base + src_off[g];
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                   :: "s"(m0v), "v"(src) : "memory");
+    }
+  };
+  int kmask;   // key mask in a VGPR so each pack is ONE v_and_or_b32 (VGPR mask, inline r)
+  asm volatile("v_mov_b32 %0, 0xffffffe0" : "=v"(kmask));
+  // lane's A-row base inside a chunk image: row = sub*32 + cl, piece (2s + h) ^ (cl & SWZ)
+  const int arow = cl * NJ;
+  const int asw = cl & SWZ;
+  double my_sse = 0.0;
+  float my_xmax = 0.f;
+
+  // one block tile (a lambda so the single-tile launch compiles to straight-line code:
+  // the loop form costs registers the 3-tile plain form does not have)
+  auto tile = [&](const int64_t bt) {
+  const int64_t pbase = (bt * NW + wid) * (PT * 32);
 
   // ---- points (B operand, negated), resident for the whole sweep; rows past n are zero
   uint4 bf[PT][KS];
@@ -543,6 +387,11 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     mx = fmaxf(mx, 0.5f * x2[t]);
   }
   for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+  my_xmax = fmaxf(my_xmax, mx);
+  // the previous tile's waves are past every read of s_m / s_hn / the chunk buffers
+  // (each crossed this tile's chunk barriers' predecessor: the last chunk barrier of the
+  // previous tile precedes all of its reads), so the block barrier below orders the
+  // rewrite after them
   if (lane == 0) s_m[wid] = mx;
   __syncthreads();
   float M = s_m[0];
@@ -552,77 +401,29 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   M = M * 1.0001f + 1e-6f;
   for (int c = tid; c < kpad; c += NT) s_hn[c] = hn[c] + M;
 
-  // per-thread DMA sources: slot q = g*NT + tid of the chunk image
-  int src_off[GPT];
-#pragma unroll
-  for (int g = 0; g < GPT; ++g) {
-    const int q = g * NT + tid, row = q / NJ, jj = q % NJ;
-    src_off[g] = row * DP + (jj ^ (row & SWZ)) * 8;
-  }
-  // Issued as inline asm: with the builtin, hipcc cannot tell the DMA target from the
-  // chunk being read and drains vmcnt(0) before every ds_read (the chunk in flight
-  // would then never overlap compute). The counted waits below are the only waits.
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(km_lds_void*)s_c;
-  auto issue = [&](int ch) {
-    const uint16_t* base = Cq + (int64_t)ch * CH * DP;
-    const uint32_t dst = lds0 + (uint32_t)(((ch % NBUF) * CHP) * 16);
-#pragma unroll
-    for (int g = 0; g < GPT; ++g) {
-      const uint32_t m0v = __builtin_amdgcn_readfirstlane(dst + (uint32_t)((g * NT + wid * 64) * 16));
-      const uint16_t* src = base + src_off[g];
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-                   :: "s"(m0v), "v"(src) : "memory");
-    }
-  };
-
   int bkey[PT], bsub[PT], bkey2[PT];
 #pragma unroll
   for (int t = 0; t < PT; ++t) { bkey[t] = 0x7fffffff; bsub[t] = 0; bkey2[t] = 0x7fffffff; }
-  int kmask;   // key mask in a VGPR so each pack is ONE v_and_or_b32 (VGPR mask, inline r)
-  asm volatile("v_mov_b32 %0, 0xffffffe0" : "=v"(kmask));
 
-  // lane's A-row base inside a chunk image: row = sub*32 + cl, piece (2s + h) ^ (cl & SWZ)
-  const int arow = cl * NJ;
-  const int asw = cl & SWZ;
   auto load_frag = [&](const uint4* img, int sub, int cb, uint4 (&a)[KS], f32x16& hc) {
-    if constexpr (DIAG == 4) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) a[s] = make_uint4(cb + s, sub, 0u, 0u);
-    } else {
+    for (int s = 0; s < KS; ++s) a[s] = img[sub * 32 * NJ + arow + ((2 * s + h) ^ asw)];
 #pragma unroll
-      for (int s = 0; s < KS; ++s) a[s] = img[sub * 32 * NJ + arow + ((2 * s + h) ^ asw)];
-    }
-    if constexpr (DIAG >= 3) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) hc[r] = (float)(cb + r);
-    } else {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 v = *reinterpret_cast<const float4*>(&s_hn[cb + 8 * g + 4 * h]);
-        hc[4 * g + 0] = v.x; hc[4 * g + 1] = v.y; hc[4 * g + 2] = v.z; hc[4 * g + 3] = v.w;
-      }
+    for (int g = 0; g < 4; ++g) {
+      const float4 v = *reinterpret_cast<const float4*>(&s_hn[cb + 8 * g + 4 * h]);
+      hc[4 * g + 0] = v.x; hc[4 * g + 1] = v.y; hc[4 * g + 2] = v.z; hc[4 * g + 3] = v.w;
     }
   };
 
-  // SWP: accumulators of the previous sub-tile, reduced one sub-tile late. Initial keys
-  // are NaN bits (0x7fffffe0 | r after masking): larger than any finite distance key,
-  // so the dummy first reduction is displaced by the first real one.
-  // SWP = 2 defers only the last point tile's reduction (16 accumulator VGPRs instead
-  // of 16 * PT); the earlier tiles' reductions overlap the later tiles' MFMA chains.
-  constexpr int T0 = SWP == 2 ? PT - 1 : 0;   // first deferred tile
-  f32x16 pacc[PT];
+  // accumulators of the last point tile, reduced one sub-tile late. Initial keys are NaN
+  // bits (0x7fffffe0 | r after masking): larger than any finite distance key, so the
+  // dummy first reduction is displaced by the first real one.
+  constexpr int T0 = PT - 1;                   // the deferred tile
+  f32x16 pacc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) pacc[r] = __int_as_float(0x7fffffff);
   int pcb = 0;
-  if constexpr (SWP != 0) {
-#pragma unroll
-    for (int t = T0; t < PT; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) pacc[t][r] = __int_as_float(0x7fffffff);
-  }
   auto reduce_tile = [&](const f32x16& acc, int t, int cb) {
-    if constexpr (DIAG == 1) {
-      bkey[t] = min(bkey[t], __float_as_int(acc[0]));
-      return;
-    }
     int m = 0x7fffffff;
     if constexpr (TOP2) {
       int m2 = 0x7fffffff;
@@ -682,41 +483,28 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       uint4 an[KS];
       f32x16 hn_next;
       if (PF && sub + 1 < NSUB) load_frag(img, sub + 1, cb + 32, an, hn_next);
-      f32x16 cacc[PT];
+      f32x16 cacc;
 #pragma unroll
       for (int t = 0; t < PT; ++t) {
-        f32x16 acc;
-        if constexpr (DIAG >= 2) {
-          uint32_t f = bf[t][0].x;
+        f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            __builtin_bit_cast(bf16x8, a[0]), __builtin_bit_cast(bf16x8, bf[t][0]), hc, 0, 0, 0);
 #pragma unroll
-          for (int s = 0; s < KS; ++s) f ^= a[s].x ^ a[s].w;
-          acc = hc;
-          acc[0] = __int_as_float(__float_as_int(acc[0]) ^ (int)f);
-        } else {
+        for (int s = 1; s < KS; ++s)
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              __builtin_bit_cast(bf16x8, a[0]), __builtin_bit_cast(bf16x8, bf[t][0]), hc, 0, 0, 0);
-#pragma unroll
-          for (int s = 1; s < KS; ++s)
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                __builtin_bit_cast(bf16x8, a[s]), __builtin_bit_cast(bf16x8, bf[t][s]), acc, 0, 0, 0);
-        }
-        if (SWP != 0 && t >= T0) cacc[t] = acc;
+              __builtin_bit_cast(bf16x8, a[s]), __builtin_bit_cast(bf16x8, bf[t][s]), acc, 0, 0, 0);
+        if (t == T0) cacc = acc;
         else reduce_tile(acc, t, cb);
       }
-      if constexpr (SWP != 0) {
-        // argmin of the previous sub-tile: independent of the MFMAs above, same block
+      // argmin of the previous sub-tile's last tile: independent of the MFMAs above
+      reduce_tile(pacc, T0, pcb);
+      pacc = cacc;
+      pcb = cb;
+      // pin the interleave: one MFMA, then a few argmin VALU ops, for every MFMA of
+      // this sub-tile (hipcc otherwise clusters the MFMAs and sinks the VALU after them)
 #pragma unroll
-        for (int t = T0; t < PT; ++t) reduce_tile(pacc[t], t, pcb);
-#pragma unroll
-        for (int t = T0; t < PT; ++t) pacc[t] = cacc[t];
-        pcb = cb;
-        // pin the interleave: one MFMA, then a few argmin VALU ops, for every MFMA of
-        // this sub-tile (hipcc otherwise clusters the MFMAs and sinks the VALU after them)
-#pragma unroll
-        for (int i = 0; i < PT * KS; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // VALU
-        }
+      for (int i = 0; i < PT * KS; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // VALU
       }
       if (sub + 1 < NSUB) {
         if constexpr (PF) {
@@ -730,13 +518,9 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     }
     if (NBUF >= 3 && ch + NBUF - 1 < nchunk) issue(ch + NBUF - 1);
   }
-  if constexpr (SWP != 0) {
-#pragma unroll
-    for (int t = T0; t < PT; ++t) reduce_tile(pacc[t], t, pcb);
-  }
+  reduce_tile(pacc, T0, pcb);
 
   // ---- decode, combine the two lane halves (same point, disjoint centre rows)
-  double my_sse = 0.0;
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     const int r = bkey[t] & 31;
@@ -765,9 +549,18 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       assign[row] = bi;
       if (mind) mind[row] = dist;
       if constexpr (TOP2) mind2[row] = fmaxf(2.f * (bv2 - M) + x2[t], 0.f);
+      if (xh) xh[row] = 0.5f * x2[t];
       my_sse += (double)dist;
     }
   }
+  };   // tile
+  if constexpr (LOOP) {
+    for (int64_t bt = blockIdx.x; bt < ntile; bt += gridDim.x) tile(bt);
+  } else {
+    if ((int64_t)blockIdx.x < ntile) tile(blockIdx.x);
+  }
+
+  if (xmax && lane == 0) atomicMax(xmax, __float_as_uint(my_xmax));
   if (sse) {
     double s = my_sse;
     for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
@@ -778,83 +571,6 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       for (int w = 0; w < NW; ++w) tot += s_sse[w];
       atomicAdd(sse + (blockIdx.x & sse_mask), tot);
     }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// K3: range-partitioned LDS accumulation. grid = (row chunks, cluster ranges).
-template <typename T, int DP, int CR, int NW>
-__global__ void __launch_bounds__(NW * 64)
-kmeans_accumulate_kernel(const T* __restrict__ X, int64_t n, int64_t ldx, const int* __restrict__ assign,
-                         int k, int64_t rows_per_chunk, float* __restrict__ S,
-                         unsigned long long* __restrict__ cnt) {
-  // lane l owns EPL contiguous columns [l*EPL, l*EPL+EPL) of a row (DP >= 64),
-  // or column l (DP < 64, lanes >= DP idle)
-  constexpr int EPL = DP >= 64 ? DP / 64 : 1;
-  __shared__ float s_tab[CR * DP];
-  __shared__ unsigned s_cnt[CR];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int c0 = blockIdx.y * CR;
-  for (int i = tid; i < CR * DP; i += NW * 64) s_tab[i] = 0.f;
-  for (int i = tid; i < CR; i += NW * 64) s_cnt[i] = 0u;
-  __syncthreads();
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
-  const int64_t r1 = min(n, r0 + rows_per_chunk);
-  const bool lane_on = (DP >= 64) || (lane < DP);
-  for (int64_t base = r0 + (int64_t)wid * 64; base < r1; base += (int64_t)NW * 64) {
-    const int64_t r = base + lane;
-    const int a = (r < r1) ? assign[r] : -1;
-    const bool mine = (a >= c0) && (a < c0 + CR);
-    uint64_t m = __ballot(mine);
-    while (m) {
-      // up to 4 rows per round so their loads overlap
-      int sel[4], cnum[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (m) {
-          const int b = __builtin_ctzll(m);
-          m &= m - 1;
-          sel[u] = b;
-          cnum[u] = __builtin_amdgcn_readlane(a, b) - c0;
-        } else {
-          sel[u] = sel[0];
-          cnum[u] = -1;
-        }
-      }
-      float v[4][EPL];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const T* row = X + (base + sel[u]) * ldx + lane * EPL;
-#pragma unroll
-        for (int e = 0; e < EPL; ++e) {
-          float x = 0.f;
-          if (lane_on) {
-            if constexpr (sizeof(T) == 2) x = bf16_to_f32(reinterpret_cast<const uint16_t*>(row)[e]);
-            else x = reinterpret_cast<const float*>(row)[e];
-          }
-          v[u][e] = x;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (cnum[u] >= 0) {
-          if (lane_on) {
-#pragma unroll
-            for (int e = 0; e < EPL; ++e) atomicAdd(&s_tab[cnum[u] * DP + lane * EPL + e], v[u][e]);
-          }
-          if (lane == 0) atomicAdd(&s_cnt[cnum[u]], 1u);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < CR * DP; i += NW * 64) {
-    const int c = c0 + i / DP;
-    const float val = s_tab[i];
-    if (c < k && val != 0.f) atomicAdd(&S[(int64_t)c * DP + (i % DP)], val);
-  }
-  for (int i = tid; i < CR; i += NW * 64) {
-    if (c0 + i < k && s_cnt[i] != 0u) atomicAdd(&cnt[c0 + i], (unsigned long long)s_cnt[i]);
   }
 }
 
@@ -907,9 +623,27 @@ kmeans_update_kernel(float* __restrict__ C, const float* __restrict__ S,
 //   scan    : per cluster, exclusive offsets over chunks; cluster starts; segments
 //   scatter : LDS cursors -> perm[pos] = row
 //   segsum  : per segment register accumulation -> atomicAdd into S[c]
+// Device-resident entry count (the incremental pass: 2 signed entries per moved row,
+// counted on the device by the bound filter / diff): every kernel of the sort derives the
+// same geometry from it -- n = mul * *ndev entries over B = clamp(ceil(n / chunk), 1,
+// bmax) chunks of rpc rows -- so the launches need no host sync; blocks past B exit.
+struct SortGeom { int64_t n, rpc; int B; };
+__device__ __forceinline__ SortGeom sort_geom(int64_t n, int64_t rpc, int B,
+                                              const unsigned long long* ndev, int mul,
+                                              int64_t chunk) {
+  if (ndev == nullptr) return {n, rpc, B};
+  const int64_t nn = (int64_t)mul * (int64_t)*ndev;
+  const int64_t b = min((int64_t)B, max((int64_t)1, (nn + chunk - 1) / chunk));
+  return {nn, max((int64_t)1, (nn + b - 1) / b), (int)b};
+}
+
 __global__ void __launch_bounds__(256)
-kmeans_hist_kernel(const int* __restrict__ assign, int64_t n, int64_t rpc, int k,
-                   int* __restrict__ block_counts) {
+kmeans_hist_kernel(const int* __restrict__ assign, int64_t n_, int64_t rpc_, int k,
+                   int* __restrict__ block_counts, const unsigned long long* __restrict__ ndev,
+                   int mul, int64_t chunk) {
+  const SortGeom g = sort_geom(n_, rpc_, gridDim.x, ndev, mul, chunk);
+  if ((int)blockIdx.x >= g.B) return;
+  const int64_t n = g.n, rpc = g.rpc;
   extern __shared__ int hist[];
   for (int c = threadIdx.x; c < k; c += blockDim.x) hist[c] = 0;
   __syncthreads();
@@ -920,9 +654,11 @@ kmeans_hist_kernel(const int* __restrict__ assign, int64_t n, int64_t rpc, int k
 }
 
 __global__ void __launch_bounds__(1024)
-kmeans_scan_kernel(int* __restrict__ block_counts, int B, int k, int seg,
+kmeans_scan_kernel(int* __restrict__ block_counts, int B_, int k, int seg,
                    int64_t* __restrict__ cluster_start, int64_t* __restrict__ seg_start,
-                   unsigned long long* __restrict__ cnt_out) {
+                   unsigned long long* __restrict__ cnt_out,
+                   const unsigned long long* __restrict__ ndev, int mul, int64_t chunk) {
+  const int B = sort_geom(0, 1, B_, ndev, mul, chunk).B;
   // [2k] int32 (n < 2^31 is checked by the launcher): counts, then segment counts;
   // 8 B per cluster keeps k = 16384 inside the 160 KB LDS (128 KB dynamic)
   extern __shared__ int tot[];
@@ -981,6 +717,7 @@ __global__ void __launch_bounds__(256)
 kmeans_scatter_kernel(const int* __restrict__ assign, int64_t n, int64_t rpc, int k,
                       const int* __restrict__ block_offsets, const int64_t* __restrict__ cluster_start,
                       int* __restrict__ perm) {
+  // (k > kScKmax only; host-known counts)
   extern __shared__ int cursor[];
   for (int c = threadIdx.x; c < k; c += blockDim.x)
     cursor[c] = (int)(cluster_start[c] + block_offsets[(int64_t)blockIdx.x * k + c]);
@@ -1000,9 +737,13 @@ kmeans_scatter_kernel(const int* __restrict__ assign, int64_t n, int64_t rpc, in
 // rows per run) instead of 64 unrelated 4-byte locations per store instruction.
 constexpr int kScCh = 32768, kScKmax = 2048, kScNT = 1024, kScPer = kScCh / kScNT;
 __global__ void __launch_bounds__(kScNT)
-kmeans_scatter_chunked_kernel(const int* __restrict__ assign, int64_t n, int64_t rpc, int k,
+kmeans_scatter_chunked_kernel(const int* __restrict__ assign, int64_t n_, int64_t rpc_, int k,
                               const int* __restrict__ block_offsets,
-                              const int64_t* __restrict__ cluster_start, int* __restrict__ perm) {
+                              const int64_t* __restrict__ cluster_start, int* __restrict__ perm,
+                              const unsigned long long* __restrict__ ndev, int mul, int64_t chunk) {
+  const SortGeom g = sort_geom(n_, rpc_, gridDim.x, ndev, mul, chunk);
+  if ((int)blockIdx.x >= g.B) return;
+  const int64_t n = g.n, rpc = g.rpc;
   __shared__ int stage[kScCh];
   __shared__ int cursor[kScKmax], lcnt[kScKmax], lstart[kScKmax];
   __shared__ int s_wsum[kScNT / 64];
@@ -1133,7 +874,9 @@ kmeans_segsum_kernel(const T* __restrict__ X, int64_t ldx, const int* __restrict
 // d-vector atomics instead of 2 per moved row and feature (km_move, kmeans_inc.hip).
 __global__ void __launch_bounds__(256)
 km_dexpand_kernel(const int32_t* __restrict__ changed, int64_t m, const int32_t* __restrict__ a_new,
-                  const int32_t* __restrict__ a_old, int* __restrict__ ec, int* __restrict__ er) {
+                  const int32_t* __restrict__ a_old, int* __restrict__ ec, int* __restrict__ er,
+                  const unsigned long long* __restrict__ mdev) {
+  if (mdev != nullptr) m = min(m, (int64_t)*mdev);
   const int64_t n2 = 2 * m;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n2;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -1254,45 +997,28 @@ static int device_cus() {
   return cached[dev];
 }
 
-// resident-centre K2 (bf16): one persistent block per CU, ceil(kpad / 512) passes;
-// `dist` is required (it carries the running distance between passes)
-template <int DP, int NW, int PT>
-static hipError_t launch_assign_res(const void* X, int64_t n, int64_t ldx, const void* Cq,
-                                    const float* hn, int kpad, int* assign, float* dist, double* sse, int sse_mask,
-                                    hipStream_t st) {
-  using G = ResGeom<DP>;
-  if (dist == nullptr || kpad % 32) return hipErrorInvalidValue;
-  if (n == 0) return hipSuccess;
-  const int64_t ngrp = cdiv(n, (int64_t)PT * 32);
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(device_cus(), cdiv(ngrp, NW)));
-  const int npass = (int)cdiv(kpad, G::CB);
-  for (int ps = 0; ps < npass; ++ps) {
-    const int c0 = ps * G::CB;
-    const int ncen = std::min(G::CB, kpad - c0);
-    hipLaunchKernelGGL((kmeans_assign_res_kernel<DP, NW, PT>), dim3(grid), dim3(NW * 64), 0, st,
-                       (const uint16_t*)X, n, ldx, (const uint16_t*)Cq, hn, c0, ncen, ps == 0 ? 1 : 0,
-                       ps == npass - 1 ? 1 : 0, assign, dist, sse, sse_mask);
-    DALGO_LAUNCH_CHECK();
-  }
-  return hipSuccess;
-}
-
-// pipelined K2 (bf16, DP >= 64): grid = one PT-tile group per wave, MINB blocks per CU
-template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, int SWP = 0, int DIAG = 0,
-          bool TOP2 = false>
+// pipelined K2 (bf16, DP >= 64). Host-known row count: one block tile per block.
+// Device-resident count (mcount, n = its upper bound): a resident grid (MINB blocks per
+// CU) walks the tiles, so the launch needs no host sync.
+template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, bool TOP2 = false,
+          bool LOOP = false>
 static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                      const float* hn, int kpad, int* assign, float* mind,
                                      double* sse, int sse_mask, hipStream_t st,
-                                     const int32_t* idx = nullptr, float* mind2 = nullptr) {
+                                     const int32_t* idx = nullptr, float* mind2 = nullptr,
+                                     const unsigned long long* mcount = nullptr,
+                                     float* xh = nullptr, unsigned* xmax = nullptr) {
   constexpr int CH = 32 * NSUB;
   constexpr size_t kStatic = NBUF * (size_t)CH * DP * 2;
   if (kpad % CH) return hipErrorInvalidValue;
   const size_t dyn = (size_t)kpad * sizeof(float);
   if (kStatic + dyn + 1024 > 160 * 1024) return hipErrorInvalidValue;
-  const int64_t grid = cdiv(n, (int64_t)NW * PT * 32);
+  int64_t grid = cdiv(n, (int64_t)NW * PT * 32);
   if (grid == 0) return hipSuccess;
+  if (mcount != nullptr && !LOOP) return hipErrorInvalidValue;
+  if (LOOP) grid = std::min<int64_t>(grid, (int64_t)device_cus() * MINB);
   if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
-  auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF, SWP, DIAG, TOP2>;
+  auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF, TOP2, LOOP>;
   static size_t attr_set = 0;   // largest dynamic size this instantiation was enabled for
   if (dyn > attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1301,142 +1027,45 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
     attr_set = dyn;
   }
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(NW * 64), dyn, st, (const uint16_t*)X, n, ldx,
-                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse, sse_mask, idx, mind2);
+                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse, sse_mask, idx, mind2, mcount,
+                     xh, xmax);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
 
-// variant: 0 = 8 waves x 32-centre chunks, 1 = 4 waves x 32, 2 = 4 waves x 128,
-//          3 = 8 waves x 128, 4 = 4 waves x 64, 5 = variant 0 capped at 128 VGPRs
-//          (4 waves/SIMD: two 8-wave blocks per CU), 6 = 4 waves x 4 point tiles (128
-//          points per wave), 7 = 8 waves x 4 point tiles, 8 = 4 waves capped at 128
-//          VGPRs (four blocks per CU), 9 = variant 5 with 64-centre chunks,
-//          10 = 16 waves (1024 points per block) capped at 128 VGPRs,
-//          11 / 12 / 13 = resident-centre form (bf16; f32 uses 5): 8 waves x 2 point
-//          tiles, 4 waves x 4 tiles, 8 waves x 1 tile,
-//          14..17 = pipelined distance-key form (bf16, DP >= 64; otherwise 5), 4 waves x
-//          64-centre chunks: 14 = 2 tiles/wave, 2 blocks/CU, triple-buffered, A prefetch;
-//          15 = 3 blocks/CU, no prefetch; 16 = 1 tile/wave, 4 blocks/CU, double-buffered;
-//          17 = 2 tiles, 3 blocks/CU, double-buffered;
-//          18 = 14 with the software-pipelined argmin (SWP), 19 = 18 without A prefetch,
-//          20 = 8-wave blocks (1 per CU, 512 points per chunk), 21 = 20 with 128-centre
-//          chunks, 22 = 20 with SWP, 23 = 14 quadruple-buffered (chunk ch+3 in flight
-//          while ch is consumed), 24 = 23 with SWP, 25 = 128-centre chunks double-
-//          buffered (64 MFMAs per barrier), 26 = 25 with SWP, 27 = 25 without A prefetch,
-//          28 / 29 = 8-wave blocks, 256- / 128-centre chunks double-buffered, SWP;
-//          30 = 28 without SWP, 48 / 49 / 50 = 3 point tiles per wave (96 points: each A
-//          fragment read from LDS feeds 3 MFMAs) without prefetch / with A prefetch / with
-//          SWP, 51 / 52 = 3 tiles with SWP = 2 (only the last tile's reduction deferred)
-//          without / with A prefetch (52: bf16 default), 53 = 26 with SWP = 2, 54 = 4
-//          tiles with SWP = 2 (spills), 40 / 41 / 42 / 43 = diagnostics of 26 (no argmin VALU /
-//          no MFMA / no MFMA + no C-init reads / no MFMA + no LDS fragment reads; wrong
-//          results). Measured and removed (profiles/round2/README.md): a
-//          persistent form looping blocks over point groups with next-group L2 prefetch
-//          (2-4 % slower than 26), s_setprio on alternate blocks (within 1 %), a form
-//          with the centres resident in VGPRs and the points streamed through LDS
-//          (4.79-5.30 vs 4.42-4.56 ms: the extra norm k-step costs more than the saved
-//          LDS reads), one 4-wave block per CU with the whole 512-entry register file per
-//          wave and 4-8 point tiles per wave (5.0-5.5 vs 4.14 ms for 52 at 20M: one wave
-//          per SIMD leaves the barrier / LDS / DMA waits exposed)
+// K2 dispatch. bf16 with DP >= 64: the pipelined distance-key form (4-wave blocks, two
+// per CU, 3 point tiles per wave, 128-centre chunks double-buffered by LDS-DMA, next
+// fragments prefetched, last tile's argmin software-pipelined): 1.20-1.25 PF/s at
+// 20M-100M x 128 x 1024. f32, and bf16 with DP < 64: the generic form (8-wave blocks,
+// 32-centre chunks staged through VGPRs, 128-VGPR cap, 4 blocks per CU).
+// Measured and removed (numbers in profiles/round2/README.md, profiles/round3/README.md):
+// 26 other tilings of the pipelined form (1 / 2 / 4 point tiles, 8-wave blocks, 64- and
+// 256-centre chunks, triple / quadruple buffering, with and without prefetch or the
+// software-pipelined argmin), a resident-centre form (centres in LDS for the whole
+// launch, points streamed), a centre-stationary form (centres in VGPRs, points through
+// an LDS-DMA ring: 23.4 vs 22.8 ms at 100M), a persistent form looping over point groups
+// with next-group L2 prefetch (2-4 % slower), s_setprio on alternate blocks (within 1 %)
+// and one 4-wave block per CU with 4-8 point tiles (5.0-5.5 vs 4.14 ms at 20M).
 template <typename T, int DP>
 static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const void* Cq,
-                                   const float* hn, int kpad, int* assign, float* mind, double* sse, int sse_mask,
-                                   int variant, hipStream_t st) {
-  switch (variant) {
-    case 0: return launch_assign_v<T, DP, 8, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-    case 1: return launch_assign_v<T, DP, 4, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-    case 2: return launch_assign_v<T, DP, 4, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-    case 3: return launch_assign_v<T, DP, 8, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-    case 4: return launch_assign_v<T, DP, 4, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-    case 5: return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-    case 6: return launch_assign_v<T, DP, 4, 1, 4, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-    case 7: return launch_assign_v<T, DP, 8, 1, 4, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-    case 8: return launch_assign_v<T, DP, 4, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-    case 9: return launch_assign_v<T, DP, 8, 2, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-    case 10: return launch_assign_v<T, DP, 16, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-    case 11: case 12: case 13:
-      if constexpr (sizeof(T) == 2) {
-        if (variant == 11) return launch_assign_res<DP, 8, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 12) return launch_assign_res<DP, 4, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        return launch_assign_res<DP, 8, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-      }
-      return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-    case 14: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23: case 24: case 25: case 26: case 27: case 28: case 29: case 30: case 40: case 41: case 42: case 43: case 48: case 49: case 50: case 51: case 52: case 53: case 54:
-      if constexpr (sizeof(T) == 2 && DP >= 64) {
-        // one 8-wave block per CU: every centre chunk feeds 512 points (half the L2 -> LDS
-        // centre traffic of two independent 4-wave blocks)
-        if (variant == 20) return launch_assign_pipe<DP, 8, 2, 2, 1, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 21) return launch_assign_pipe<DP, 8, 2, 4, 1, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 22) return launch_assign_pipe<DP, 8, 2, 2, 1, 3, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 23) return launch_assign_pipe<DP, 4, 2, 2, 2, 4, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 24) return launch_assign_pipe<DP, 4, 2, 2, 2, 4, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 25) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 26) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 27) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 28) return launch_assign_pipe<DP, 8, 2, 8, 1, 2, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 29) return launch_assign_pipe<DP, 8, 2, 4, 1, 2, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 30) return launch_assign_pipe<DP, 8, 2, 8, 1, 2, true, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 48) return launch_assign_pipe<DP, 4, 3, 4, 2, 2, false, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 49) return launch_assign_pipe<DP, 4, 3, 4, 2, 2, true, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 50) return launch_assign_pipe<DP, 4, 3, 4, 2, 2, false, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 51) return launch_assign_pipe<DP, 4, 3, 4, 2, 2, false, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 52) return launch_assign_pipe<DP, 4, 3, 4, 2, 2, true, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 53) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 54) return launch_assign_pipe<DP, 4, 4, 4, 2, 2, false, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 40) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, true, 1>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 41) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, true, 2>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 42) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, true, 3>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 43) return launch_assign_pipe<DP, 4, 2, 4, 2, 2, true, true, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 18) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, true, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 19) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, false, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 14) return launch_assign_pipe<DP, 4, 2, 2, 2, 3, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 15) return launch_assign_pipe<DP, 4, 2, 2, 3, 3, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        if (variant == 16) return launch_assign_pipe<DP, 4, 1, 2, 4, 2, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-        return launch_assign_pipe<DP, 4, 2, 2, 3, 2, false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-      }
-      return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
-    default: return hipErrorInvalidValue;
-  }
+                                   const float* hn, int kpad, int* assign, float* mind, double* sse,
+                                   int sse_mask, hipStream_t st) {
+  if constexpr (sizeof(T) == 2 && DP >= 64)
+    if (kpad % 128 == 0)
+      return launch_assign_pipe<DP, 4, 3, 4, 2, 2, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse,
+                                                         sse_mask, st);
+  return launch_assign_v<T, DP, 8, 1, 2, 4>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
 }
 
 template <typename T>
 static hipError_t launch_assign(int DP, const void* X, int64_t n, int64_t ldx, const void* Cq,
                                 const float* hn, int kpad, int* assign, float* mind, double* sse, int sse_mask,
-                                int variant, hipStream_t st) {
+                                hipStream_t st) {
   switch (DP) {
-    case 16: return launch_assign_dp<T, 16>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st);
-    case 32: return launch_assign_dp<T, 32>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st);
-    case 64: return launch_assign_dp<T, 64>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st);
-    case 128: return launch_assign_dp<T, 128>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-template <typename T, int DP>
-static hipError_t launch_acc_dp(const void* X, int64_t n, int64_t ldx, const int* assign, int k,
-                                float* S, unsigned long long* cnt, hipStream_t st) {
-  constexpr int NW = 8;
-  constexpr int CR = (DP >= 128) ? 64 : (8192 / DP);   // LDS table <= 32 KB
-  const int q = (int)cdiv(k, CR);
-  // ~2048 blocks in total, at least 2048 rows per chunk
-  int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n, 2048), std::max<int64_t>(1, 2048 / q)));
-  const int64_t rpc = round_up(cdiv(n, chunks), 64);
-  chunks = cdiv(n, rpc);
-  if (chunks == 0) return hipSuccess;
-  hipLaunchKernelGGL((kmeans_accumulate_kernel<T, DP, CR, NW>), dim3((unsigned)chunks, q),
-                     dim3(NW * 64), 0, st, (const T*)X, n, ldx, assign, k, rpc, S, cnt);
-  DALGO_LAUNCH_CHECK();
-  return hipSuccess;
-}
-
-template <typename T>
-static hipError_t launch_acc(int DP, const void* X, int64_t n, int64_t ldx, const int* assign,
-                             int k, float* S, unsigned long long* cnt, hipStream_t st) {
-  switch (DP) {
-    case 16: return launch_acc_dp<T, 16>(X, n, ldx, assign, k, S, cnt, st);
-    case 32: return launch_acc_dp<T, 32>(X, n, ldx, assign, k, S, cnt, st);
-    case 64: return launch_acc_dp<T, 64>(X, n, ldx, assign, k, S, cnt, st);
-    case 128: return launch_acc_dp<T, 128>(X, n, ldx, assign, k, S, cnt, st);
+    case 16: return launch_assign_dp<T, 16>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 32: return launch_assign_dp<T, 32>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 64: return launch_assign_dp<T, 64>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
+    case 128: return launch_assign_dp<T, 128>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1447,12 +1076,8 @@ static hipError_t launch_segsum_dp(const void* X, int64_t ldx, const int* perm, 
                                    hipStream_t st) {
   constexpr int NW = 4;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(max_segs, NW), 256 * 16));
-  if (env_int("DALGO_NT", 1))
-    hipLaunchKernelGGL((kmeans_segsum_kernel<T, DP, NW, true>), dim3(grid), dim3(NW * 64), 0, st,
-                       (const T*)X, ldx, perm, cs, ss, k, seg, S);
-  else
-    hipLaunchKernelGGL((kmeans_segsum_kernel<T, DP, NW, false>), dim3(grid), dim3(NW * 64), 0, st,
-                       (const T*)X, ldx, perm, cs, ss, k, seg, S);
+  hipLaunchKernelGGL((kmeans_segsum_kernel<T, DP, NW, true>), dim3(grid), dim3(NW * 64), 0, st,
+                     (const T*)X, ldx, perm, cs, ss, k, seg, S);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -1481,7 +1106,8 @@ hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n,
   if (k < 1 || k > 16384 || B < 1 || seg < 1 || n >= (int64_t)0x7fffffff) return hipErrorInvalidValue;
   const int64_t rpc = cdiv(std::max<int64_t>(n, 1), B);
   const size_t lds_k = (size_t)k * sizeof(int);
-  hipLaunchKernelGGL(kmeans_hist_kernel, dim3(B), dim3(256), lds_k, st, assign, n, rpc, k, block_counts);
+  hipLaunchKernelGGL(kmeans_hist_kernel, dim3(B), dim3(256), lds_k, st, assign, n, rpc, k, block_counts,
+                     (const unsigned long long*)nullptr, 1, (int64_t)1);
   DALGO_LAUNCH_CHECK();
   const size_t scan_lds = 2 * (size_t)k * sizeof(int);
   if (scan_lds > 64 * 1024) {
@@ -1494,12 +1120,13 @@ hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n,
     }
   }
   hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), scan_lds, st,
-                     block_counts, B, k, seg, cluster_start, seg_start, cnt);
+                     block_counts, B, k, seg, cluster_start, seg_start, cnt,
+                     (const unsigned long long*)nullptr, 1, (int64_t)1);
   DALGO_LAUNCH_CHECK();
-  const char* sc_env = getenv("DALGO_KM_SCATTER");            // "0": per-row LDS-cursor scatter
-  if (k <= kScKmax && !(sc_env && sc_env[0] == '0'))
+  if (k <= kScKmax)   // per-row LDS-cursor scatter only where the chunked form's LDS ends
     hipLaunchKernelGGL(kmeans_scatter_chunked_kernel, dim3(B), dim3(kScNT), 0, st, assign, n, rpc, k,
-                       (const int*)block_counts, (const int64_t*)cluster_start, perm);
+                       (const int*)block_counts, (const int64_t*)cluster_start, perm,
+                       (const unsigned long long*)nullptr, 1, (int64_t)1);
   else
     hipLaunchKernelGGL(kmeans_scatter_kernel, dim3(B), dim3(256), lds_k, st, assign, n, rpc, k,
                        (const int*)block_counts, (const int64_t*)cluster_start, perm);
@@ -1509,30 +1136,35 @@ hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n,
                  : launch_segsum<float>(DP, X, ldx, perm, cluster_start, seg_start, k, seg, max_segs, S, st);
 }
 
-// Sort-based incremental K3 over the m moved rows (2m signed entries). Workspace:
-// ec / er / perm int32[2m], block_counts int32[B*k], cluster_start / seg_start int64[k+1].
+// Sort-based incremental K3 over the moved rows (2 signed entries each). m = the host's
+// upper bound of the moved rows; mdev (optional) = the device-resident count (<= m).
+// Workspace: ec / er / perm int32[2m], block_counts int32[B*k], cluster_start /
+// seg_start int64[k+1]; B = the chunk count for 2m entries (chunks of `chunk` entries).
 hipError_t dalgo_kmeans_move_sorted(const void* X, int is_bf16, int64_t ldx, int DP,
                                     const int32_t* changed, int64_t m, const int32_t* a_new,
                                     const int32_t* a_old, int k, int B, int seg, int* ec, int* er,
                                     int* block_counts, int64_t* cluster_start, int64_t* seg_start,
                                     int* perm, double* S, unsigned long long* cnt, const float* xh,
-                                    double* Q, hipStream_t st) {
+                                    double* Q, const unsigned long long* mdev, int64_t chunk,
+                                    hipStream_t st) {
   if (m <= 0) return hipSuccess;
   const int64_t n2 = 2 * m;
-  if (k < 1 || k > kScKmax || B < 1 || seg < 1 || n2 >= (int64_t)0x7fffffff) return hipErrorInvalidValue;
+  if (k < 1 || k > kScKmax || B < 1 || seg < 1 || chunk < 1 || n2 >= (int64_t)0x7fffffff)
+    return hipErrorInvalidValue;
   const int g = (int)std::min<int64_t>(cdiv(n2, 256), 4096);
-  hipLaunchKernelGGL(km_dexpand_kernel, dim3(g), dim3(256), 0, st, changed, m, a_new, a_old, ec, er);
+  hipLaunchKernelGGL(km_dexpand_kernel, dim3(g), dim3(256), 0, st, changed, m, a_new, a_old, ec, er, mdev);
   DALGO_LAUNCH_CHECK();
   const int64_t rpc = cdiv(n2, B);
   const size_t lds_k = (size_t)k * sizeof(int);
   hipLaunchKernelGGL(kmeans_hist_kernel, dim3(B), dim3(256), lds_k, st, (const int*)ec, n2, rpc, k,
-                     block_counts);
+                     block_counts, mdev, 2, chunk);
   DALGO_LAUNCH_CHECK();
   hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), 2 * lds_k, st, block_counts, B, k, seg,
-                     cluster_start, seg_start, (unsigned long long*)nullptr);
+                     cluster_start, seg_start, (unsigned long long*)nullptr, mdev, 2, chunk);
   DALGO_LAUNCH_CHECK();
   hipLaunchKernelGGL(kmeans_scatter_chunked_kernel, dim3(B), dim3(kScNT), 0, st, (const int*)ec, n2,
-                     rpc, k, (const int*)block_counts, (const int64_t*)cluster_start, perm);
+                     rpc, k, (const int*)block_counts, (const int64_t*)cluster_start, perm, mdev, 2,
+                     chunk);
   DALGO_LAUNCH_CHECK();
   constexpr int NW = 4;
   const int64_t max_segs = cdiv(n2, seg) + k;
@@ -1555,52 +1187,48 @@ hipError_t dalgo_kmeans_move_sorted(const void* X, int is_bf16, int64_t ldx, int
 
 hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
                                const void* Cq, const float* hn, int kpad, int* assign, float* mind,
-                               double* sse, int sse_mask, int variant, hipStream_t st) {
+                               double* sse, int sse_mask, hipStream_t st) {
   if (kpad % 32 != 0) return hipErrorInvalidValue;
-  return is_bf16 ? launch_assign<uint16_t>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st)
-                 : launch_assign<float>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, variant, st);
+  return is_bf16 ? launch_assign<uint16_t>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st)
+                 : launch_assign<float>(DP, X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st);
 }
 
-// K2 (variant 52) over the rows idx[0, m) of X only (bound-filtered Lloyd iteration)
-// idx may be null (all m rows); mind2 non-null selects the top-2 form (second-best
-// distance per row, a lower bound for the bound filter)
+// K2 (pipelined form) over the rows idx[0, m) of X only (bound-filtered Lloyd iteration).
+// idx may be null (rows 0 .. m); mind2 non-null selects the top-2 form (second-best
+// distance per row, a lower bound for the bound filter); mcount non-null: the row count
+// is *mcount (device), m its upper bound; xh / xmax: 0.5|x|^2 per row and its maximum.
 hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP, const void* Cq,
                                    const float* hn, int kpad, const int32_t* idx, int* assign,
                                    float* mind, float* mind2, double* sse, int sse_mask,
+                                   const unsigned long long* mcount, float* xh, unsigned* xmax,
                                    hipStream_t st) {
   if (m <= 0) return hipSuccess;
   if (kpad % 128 != 0) return hipErrorInvalidValue;
   if (mind2 != nullptr) {
-    // top-2 forms that fit 256 VGPRs without spilling (A/B: DALGO_KM_TOP2_CFG)
-    static const int cfg = env_int("DALGO_KM_TOP2_CFG", 0);
-    if (DP == 128 && cfg == 1)
-      return launch_assign_pipe<128, 4, 3, 4, 2, 2, false, 0, 0, true>(X, m, ldx, Cq, hn, kpad, assign,
-                                                                      mind, sse, sse_mask, st, idx, mind2);
-    if (DP == 128 && cfg == 2)
-      return launch_assign_pipe<128, 4, 2, 4, 2, 2, true, 0, 0, true>(X, m, ldx, Cq, hn, kpad, assign,
-                                                                     mind, sse, sse_mask, st, idx, mind2);
+    // top-2: 2 point tiles per wave (3 would spill past 256 VGPRs); a device-resident row
+    // count takes the resident-grid tile loop
+    if (DP == 128 && mcount)
+      return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true, true>(
+          X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st, idx, mind2, mcount, xh, xmax);
     if (DP == 128)
-      return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, 2, 0, true>(X, m, ldx, Cq, hn, kpad, assign,
-                                                                      mind, sse, sse_mask, st, idx, mind2);
+      return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true>(
+          X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st, idx, mind2, nullptr, xh, xmax);
+    if (DP == 64 && mcount)
+      return launch_assign_pipe<64, 4, 2, 4, 2, 2, false, true, true>(
+          X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st, idx, mind2, mcount, xh, xmax);
     if (DP == 64)
-      return launch_assign_pipe<64, 4, 2, 4, 2, 2, false, 2, 0, true>(X, m, ldx, Cq, hn, kpad, assign,
-                                                                     mind, sse, sse_mask, st, idx, mind2);
+      return launch_assign_pipe<64, 4, 2, 4, 2, 2, false, true>(
+          X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st, idx, mind2, nullptr, xh, xmax);
     return hipErrorInvalidValue;
   }
+  if (mcount) return hipErrorInvalidValue;   // the device-count form is top-2 only
   if (DP == 128)
-    return launch_assign_pipe<128, 4, 3, 4, 2, 2, true, 2>(X, m, ldx, Cq, hn, kpad, assign, mind, sse,
-                                                           sse_mask, st, idx);
+    return launch_assign_pipe<128, 4, 3, 4, 2, 2, true>(X, m, ldx, Cq, hn, kpad, assign, mind, sse,
+                                                        sse_mask, st, idx, nullptr, nullptr, xh, xmax);
   if (DP == 64)
-    return launch_assign_pipe<64, 4, 3, 4, 2, 2, true, 2>(X, m, ldx, Cq, hn, kpad, assign, mind, sse,
-                                                          sse_mask, st, idx);
+    return launch_assign_pipe<64, 4, 3, 4, 2, 2, true>(X, m, ldx, Cq, hn, kpad, assign, mind, sse,
+                                                       sse_mask, st, idx, nullptr, nullptr, xh, xmax);
   return hipErrorInvalidValue;
-}
-
-hipError_t dalgo_kmeans_accumulate(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
-                                   const int* assign, int k, float* S, unsigned long long* cnt,
-                                   hipStream_t st) {
-  return is_bf16 ? launch_acc<uint16_t>(DP, X, n, ldx, assign, k, S, cnt, st)
-                 : launch_acc<float>(DP, X, n, ldx, assign, k, S, cnt, st);
 }
 
 hipError_t dalgo_kmeans_update(float* C, const float* S, const unsigned long long* cnt, int k,

@@ -15,14 +15,12 @@
 //
 //   km_diff    : compare a_new / a_old, append the changed row ids through a
 //                per-block LDS buffer (one global atomic per block flush)
-//   km_move    : one wave per changed row: the row's DP features (bf16 / f32, one
-//                256-B or 512-B coalesced read) are added to S[a_new] and
-//                subtracted from S[a_old] with f64 atomics shaped as contiguous
-//                512-B wave instructions; lane 0 moves the counts. Used below 16k
-//                moved rows: at 100M points its 2 * DP device-scope f64 atomics per
-//                row cost ~3 ms per million moved rows, so larger moves go through
-//                the counting-sorted form in kmeans.hip (km_dexpand / km_dsegsum:
-//                ~0.1 ms per million signed entries).
+//   the moved rows then go through the counting-sorted form in kmeans.hip (km_dexpand
+//                / km_dsegsum: ~0.1 ms per million signed entries; a per-row f64-atomic
+//                form, ~3 ms per million moved rows at 100M points, was removed)
+//   km_filter / km_post / km_centre_bounds: the bound-filtered (Hamerly) iteration.
+// Every count (changed rows, active rows) stays on the device: the launches that
+// consume it read it there, so an iteration needs no host sync.
 #include "dalgo/common.h"
 
 namespace dalgo {
@@ -31,6 +29,11 @@ namespace {
 constexpr int kDiffThreads = 256;
 constexpr int kDiffBuf = 4096;      // changed row ids buffered per block in LDS
 constexpr int kEpt = 8;             // rows per thread and step (filter / post)
+
+// one ulp outward after a round-to-nearest result: >= / <= the exact value (the RN error
+// is at most half an ulp), so bounds built from them stay valid bounds
+__device__ __forceinline__ float up1(float x) { return nextafterf(x, __builtin_inff()); }
+__device__ __forceinline__ float dn1(float x) { return nextafterf(x, -__builtin_inff()); }
 
 // One block per contiguous row range. Changed rows are appended to an LDS buffer with
 // LDS atomics (one per wave and step) and flushed to the global list with ONE global
@@ -81,56 +84,6 @@ km_diff_kernel(const int32_t* __restrict__ a_new, const int32_t* __restrict__ a_
   flush();
 }
 
-template <typename T, int DP>
-__global__ void __launch_bounds__(256)
-km_move_kernel(const T* __restrict__ X, int64_t ldx, const int32_t* __restrict__ changed,
-               int64_t m, const int32_t* __restrict__ a_new, const int32_t* __restrict__ a_old,
-               double* __restrict__ S, unsigned long long* __restrict__ cnt,
-               const float* __restrict__ xh, double* __restrict__ Q) {
-  constexpr int PER = (DP + 63) / 64;     // features per lane
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t w = wave; w < m; w += nwaves) {
-    const int64_t row = changed[w];
-    const int cn = a_new[row], co = a_old[row];
-    const T* xr = X + row * ldx;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int j = q * 64 + lane;        // one wave instruction = 64 consecutive f64
-      if (j < DP) {
-        float v;
-        if constexpr (sizeof(T) == 2) v = bf16_to_f32(reinterpret_cast<const uint16_t*>(xr)[j]);
-        else v = reinterpret_cast<const float*>(xr)[j];
-        if (v != 0.f) {
-          atomicAdd(&S[(int64_t)cn * DP + j], (double)v);
-          atomicAdd(&S[(int64_t)co * DP + j], -(double)v);
-        }
-      }
-    }
-    if (lane == 0) {
-      atomicAdd(&cnt[cn], 1ull);
-      atomicAdd(&cnt[co], ~0ull);   // -1 (two's complement)
-      if (Q != nullptr) {           // per-cluster sum of |x|^2 (SSE identity)
-        const double q = 2.0 * (double)xh[row];
-        atomicAdd(&Q[cn], q);
-        atomicAdd(&Q[co], -q);
-      }
-    }
-  }
-}
-
-template <typename T, int DP>
-hipError_t launch_move(const void* X, int64_t ldx, const int32_t* changed, int64_t m,
-                       const int32_t* a_new, const int32_t* a_old, double* S,
-                       unsigned long long* cnt, const float* xh, double* Q, hipStream_t st) {
-  int64_t g = (m + 3) / 4;                 // 4 waves per 256-thread block
-  if (g > 8192) g = 8192;
-  hipLaunchKernelGGL((km_move_kernel<T, DP>), dim3((unsigned)g), dim3(256), 0, st,
-                     reinterpret_cast<const T*>(X), ldx, changed, m, a_new, a_old, S, cnt, xh, Q);
-  return hipGetLastError();
-}
-
 // ---------------------------------------------------------------------------
 // Bound-filtered Lloyd (Hamerly, exact): u[i] >= |x_i - c_a| and l[i] <= min over the
 // other centres of |x_i - c| for the centres of the last assignment. The centre of x_i
@@ -140,21 +93,29 @@ hipError_t launch_move(const void* X, int64_t ldx, const int32_t* changed, int64
 // nearest other centre) c_a is still strictly the closest centre (triangle inequality)
 // and x_i is skipped (u, l updated); otherwise its row id is appended to the active
 // list and its assignment saved in a_prev.
+// maxd = max over the k centre shifts, reduced by every block from delta (k floats from
+// L2: cheaper than a separate reduction launch).
 __global__ void __launch_bounds__(kDiffThreads)
 km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, float* __restrict__ l,
-                 const float* __restrict__ delta, const float* __restrict__ s,
-                 const float* __restrict__ maxd, int64_t n,
+                 const float* __restrict__ delta, const float* __restrict__ s, int k, int64_t n,
                  int32_t* __restrict__ a_prev, int32_t* __restrict__ idx,
                  unsigned long long* __restrict__ n_active, int64_t cap) {
   __shared__ int32_t s_buf[kDiffBuf];
   __shared__ int s_cnt;
   __shared__ unsigned long long s_base;
+  __shared__ float s_md[kDiffThreads / 64];
   const int64_t per = (n + gridDim.x - 1) / gridDim.x;
   const int64_t lo = (int64_t)blockIdx.x * per;
   const int64_t hi = lo + per < n ? lo + per : n;
+  float mdl = 0.f;
+  for (int c = threadIdx.x; c < k; c += kDiffThreads) mdl = fmaxf(mdl, delta[c]);
+  for (int off = 32; off >= 1; off >>= 1) mdl = fmaxf(mdl, __shfl_xor(mdl, off));
+  if ((threadIdx.x & 63) == 0) s_md[threadIdx.x >> 6] = mdl;
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
-  const float md = maxd[0];
+  float md = s_md[0];
+#pragma unroll
+  for (int w = 1; w < kDiffThreads / 64; ++w) md = fmaxf(md, s_md[w]);
   auto flush = [&]() {
     const int m = s_cnt;
     if (m == 0) return;
@@ -180,11 +141,14 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, floa
       uu[e] = in ? u[i] : 0.f;
       ll[e] = in ? l[i] : 0.f;
     }
-    float ub[kEpt], bound[kEpt];
+    // bounds rounded outward (u up, l down): a skipped point's bounds stay valid over any
+    // number of consecutive skipped iterations, independent of the f32 rounding of u / l
+    float ub[kEpt], lb[kEpt], bound[kEpt];
 #pragma unroll
     for (int e = 0; e < kEpt; ++e) {
-      ub[e] = uu[e] + delta[a[e]];
-      bound[e] = fmaxf(s[a[e]], ll[e] - md);
+      ub[e] = up1(uu[e] + delta[a[e]]);
+      lb[e] = dn1(ll[e] - md);
+      bound[e] = fmaxf(s[a[e]], lb[e]);
     }
 #pragma unroll
     for (int e = 0; e < kEpt; ++e) {
@@ -193,7 +157,7 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, floa
       const bool act = in && !(ub[e] < bound[e]);
       if (in && !act) {
         u[i] = ub[e];
-        l[i] = ll[e] - md;
+        l[i] = lb[e];
       } else if (act) {
         a_prev[i] = a[e];
       }
@@ -219,15 +183,20 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, floa
 // After K2 re-assigned the active rows: u = sqrt(dist + tol) (an upper bound of the
 // distance to the assigned centre, tol covering the kernel's key truncation) and the
 // rows whose cluster changed appended to `changed` (LDS-buffered, as km_diff).
+// m: the active rows (host), or their upper bound when mdev (the device-resident count
+// written by km_filter) is given; tol: host value, or *tolp when tolp is given.
 __global__ void __launch_bounds__(kDiffThreads)
 km_post_kernel(const int32_t* __restrict__ idx, int64_t m, const int32_t* __restrict__ assign,
                const int32_t* __restrict__ a_prev, const float* __restrict__ mind,
                const float* __restrict__ mind2, float tol, float* __restrict__ u,
                float* __restrict__ l, int32_t* __restrict__ changed,
-               unsigned long long* __restrict__ n_changed, int64_t cap) {
+               unsigned long long* __restrict__ n_changed, int64_t cap,
+               const unsigned long long* __restrict__ mdev, const float* __restrict__ tolp) {
   __shared__ int32_t s_buf[kDiffBuf];
   __shared__ int s_cnt;
   __shared__ unsigned long long s_base;
+  if (mdev != nullptr) m = min(m, (int64_t)*mdev);
+  if (tolp != nullptr) tol = *tolp;
   const int64_t per = (m + gridDim.x - 1) / gridDim.x;
   const int64_t lo = (int64_t)blockIdx.x * per;
   const int64_t hi = lo + per < m ? lo + per : m;
@@ -266,8 +235,8 @@ km_post_kernel(const int32_t* __restrict__ idx, int64_t m, const int32_t* __rest
     for (int e = 0; e < kEpt; ++e) {
       bool ch = false;
       if (row[e] >= 0) {
-        u[row[e]] = sqrtf(fmaxf(d1[e], 0.f) + tol);
-        l[row[e]] = sqrtf(fmaxf(d2[e] - tol, 0.f));
+        u[row[e]] = up1(sqrtf(up1(fmaxf(d1[e], 0.f) + tol)));
+        l[row[e]] = fmaxf(dn1(sqrtf(fmaxf(dn1(d2[e] - tol), 0.f))), 0.f);
         ch = an[e] != ap[e];
       }
       const uint64_t mask = __ballot(ch);
@@ -304,6 +273,55 @@ km_qsum_kernel(const int32_t* __restrict__ assign, const float* __restrict__ xh,
     if (s_q[c] != 0.0) atomicAdd(&Q[c], s_q[c]);
 }
 
+// Bound-filter geometry of the new centres (f64 on the ROUNDED centres the assign kernel
+// uses, one block per centre): delta[c] = |c_now - c_prev| rounded up (relative 1e-6 +
+// absolute 1e-6 margin, then f32 round-up), s[c] = half the distance to the nearest
+// other centre rounded down (relative 1e-6 margin, f32 round-down); k == 1: s = inf.
+// Replaces a torch cdist + norm + min chain (8 launches and a library first use).
+template <typename T>
+__global__ void __launch_bounds__(256)
+km_centre_bounds_kernel(const T* __restrict__ cnow, const T* __restrict__ cprev, int k, int d,
+                        int DP, float* __restrict__ delta, float* __restrict__ sout) {
+  __shared__ double s_c[128];
+  __shared__ double s_red[2][4];
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  auto val = [](const T* p) -> double {
+    if constexpr (sizeof(T) == 2) return (double)bf16_to_f32(*reinterpret_cast<const uint16_t*>(p));
+    else return (double)*p;
+  };
+  double dd = 0.0;
+  for (int j = tid; j < d; j += 256) {
+    const double a = val(cnow + (int64_t)c * DP + j);
+    s_c[j] = a;
+    const double b = a - val(cprev + (int64_t)c * DP + j);
+    dd += b * b;
+  }
+  __syncthreads();
+  double best = __builtin_inf();
+  for (int o = tid; o < k; o += 256) {
+    if (o == c) continue;
+    const T* row = cnow + (int64_t)o * DP;
+    double acc = 0.0;
+    for (int j = 0; j < d; ++j) {
+      const double t = s_c[j] - val(row + j);
+      acc = fma(t, t, acc);
+    }
+    best = fmin(best, acc);
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    dd += __shfl_xor(dd, off);
+    best = fmin(best, __shfl_xor(best, off));
+  }
+  if (lane == 0) { s_red[0][wid] = dd; s_red[1][wid] = best; }
+  __syncthreads();
+  if (tid == 0) {
+    double a = 0.0, b = __builtin_inf();
+    for (int w = 0; w < 4; ++w) { a += s_red[0][w]; b = fmin(b, s_red[1][w]); }
+    delta[c] = up1((float)(sqrt(a) * (1.0 + 1e-6) + 1e-6));
+    sout[c] = k == 1 ? __builtin_inff() : dn1((float)(0.5 * sqrt(b) * (1.0 - 1e-6)));
+  }
+}
+
 }  // namespace
 }  // namespace dalgo
 
@@ -319,43 +337,40 @@ hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, 
   return hipGetLastError();
 }
 
-hipError_t dalgo_km_move(const void* X, int is_bf16, int64_t ldx, int DP, const int32_t* changed,
-                         int64_t m, const int32_t* a_new, const int32_t* a_old, double* S,
-                         unsigned long long* cnt, const float* xh, double* Q, hipStream_t st) {
-  if (m <= 0) return hipSuccess;
-  using namespace dalgo;
-#define DALGO_KM_MOVE(DPV)                                                                   \
-  if (DP == DPV)                                                                             \
-    return is_bf16 ? launch_move<uint16_t, DPV>(X, ldx, changed, m, a_new, a_old, S, cnt, xh, Q, st) \
-                   : launch_move<float, DPV>(X, ldx, changed, m, a_new, a_old, S, cnt, xh, Q, st);
-  DALGO_KM_MOVE(16)
-  DALGO_KM_MOVE(32)
-  DALGO_KM_MOVE(64)
-  DALGO_KM_MOVE(128)
-#undef DALGO_KM_MOVE
-  return hipErrorInvalidValue;
-}
-
 hipError_t dalgo_km_filter(const int32_t* assign, float* u, float* l, const float* delta,
-                           const float* s, const float* maxd, int64_t n, int32_t* a_prev,
-                           int32_t* idx, unsigned long long* n_active, int64_t cap, hipStream_t st) {
+                           const float* s, int k, int64_t n, int32_t* a_prev, int32_t* idx,
+                           unsigned long long* n_active, int64_t cap, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   int64_t g = (n + dalgo::kDiffThreads - 1) / dalgo::kDiffThreads;
   if (g > 2048) g = 2048;
   hipLaunchKernelGGL(dalgo::km_filter_kernel, dim3((unsigned)g), dim3(dalgo::kDiffThreads), 0, st,
-                     assign, u, l, delta, s, maxd, n, a_prev, idx, n_active, cap);
+                     assign, u, l, delta, s, k, n, a_prev, idx, n_active, cap);
+  return hipGetLastError();
+}
+
+hipError_t dalgo_km_centre_bounds(const void* cnow, const void* cprev, int is_bf16, int k, int d,
+                                  int DP, float* delta, float* s, hipStream_t st) {
+  if (k <= 0) return hipSuccess;
+  if (d > 128 || d > DP) return hipErrorInvalidValue;
+  if (is_bf16)
+    hipLaunchKernelGGL(dalgo::km_centre_bounds_kernel<uint16_t>, dim3(k), dim3(256), 0, st,
+                       (const uint16_t*)cnow, (const uint16_t*)cprev, k, d, DP, delta, s);
+  else
+    hipLaunchKernelGGL(dalgo::km_centre_bounds_kernel<float>, dim3(k), dim3(256), 0, st,
+                       (const float*)cnow, (const float*)cprev, k, d, DP, delta, s);
   return hipGetLastError();
 }
 
 hipError_t dalgo_km_post(const int32_t* idx, int64_t m, const int32_t* assign, const int32_t* a_prev,
                          const float* mind, const float* mind2, float tol, float* u, float* l,
                          int32_t* changed, unsigned long long* n_changed, int64_t cap,
-                         hipStream_t st) {
+                         const unsigned long long* mdev, const float* tolp, hipStream_t st) {
   if (m <= 0) return hipSuccess;
   int64_t g = (m + dalgo::kDiffThreads - 1) / dalgo::kDiffThreads;
   if (g > 2048) g = 2048;
   hipLaunchKernelGGL(dalgo::km_post_kernel, dim3((unsigned)g), dim3(dalgo::kDiffThreads), 0, st,
-                     idx, m, assign, a_prev, mind, mind2, tol, u, l, changed, n_changed, cap);
+                     idx, m, assign, a_prev, mind, mind2, tol, u, l, changed, n_changed, cap, mdev,
+                     tolp);
   return hipGetLastError();
 }
 

@@ -82,16 +82,14 @@ hipError_t dalgo_mc_pi(uint64_t seed, uint64_t stream, uint64_t offset, uint64_t
 // ---- K2/K3 k-means (kmeans.hip)
 hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
                                const void* Cq, const float* hn, int kpad, int* assign, float* mind,
-                               double* sse, int sse_mask, int variant, hipStream_t st);
-hipError_t dalgo_kmeans_accumulate(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
-                                   const int* assign, int k, float* S, unsigned long long* cnt,
-                                   hipStream_t st);
+                               double* sse, int sse_mask, hipStream_t st);
 hipError_t dalgo_kmeans_move_sorted(const void* X, int is_bf16, int64_t ldx, int DP,
                                     const int32_t* changed, int64_t m, const int32_t* a_new,
                                     const int32_t* a_old, int k, int B, int seg, int* ec, int* er,
                                     int* block_counts, int64_t* cluster_start, int64_t* seg_start,
                                     int* perm, double* S, unsigned long long* cnt, const float* xh,
-                                    double* Q, hipStream_t st);
+                                    double* Q, const unsigned long long* mdev, int64_t chunk,
+                                    hipStream_t st);
 hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
                                           const int* assign, int k, int B, int seg, int* block_counts,
                                           int64_t* cluster_start, int64_t* seg_start, int* perm,
@@ -132,29 +130,24 @@ hipError_t dalgo_pr_update(const float* acc, const int32_t* pres, const int32_t*
                            float* c, float* dangling_out, hipStream_t st);
 
 // ---- K9 transitive closure (closure.hip)
-// ---- K2 centre-stationary form (kmeans_cs.hip)
-hipError_t dalgo_kmeans_assign_cs(const void* X, int64_t n, int64_t ldx, int DP, const void* Cq,
-                                  int kpad, const float* hn, const float* xh, float M, int* assign,
-                                  float* mind, double* sse, int sse_mask, hipStream_t st);
-
 // ---- K3 incremental form (kmeans_inc.hip)
 hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, int32_t* changed,
                          unsigned long long* n_changed, int64_t cap, hipStream_t st);
-hipError_t dalgo_km_move(const void* X, int is_bf16, int64_t ldx, int DP, const int32_t* changed,
-                         int64_t m, const int32_t* a_new, const int32_t* a_old, double* S,
-                         unsigned long long* cnt, const float* xh, double* Q, hipStream_t st);
 hipError_t dalgo_km_filter(const int32_t* assign, float* u, float* l, const float* delta,
-                           const float* s, const float* maxd, int64_t n, int32_t* a_prev,
-                           int32_t* idx, unsigned long long* n_active, int64_t cap, hipStream_t st);
+                           const float* s, int k, int64_t n, int32_t* a_prev, int32_t* idx,
+                           unsigned long long* n_active, int64_t cap, hipStream_t st);
 hipError_t dalgo_km_post(const int32_t* idx, int64_t m, const int32_t* assign, const int32_t* a_prev,
                          const float* mind, const float* mind2, float tol, float* u, float* l,
                          int32_t* changed, unsigned long long* n_changed, int64_t cap,
-                         hipStream_t st);
+                         const unsigned long long* mdev, const float* tolp, hipStream_t st);
+hipError_t dalgo_km_centre_bounds(const void* cnow, const void* cprev, int is_bf16, int k, int d,
+                                  int DP, float* delta, float* s, hipStream_t st);
 hipError_t dalgo_km_qsum(const int32_t* assign, const float* xh, int64_t n, int k, double* Q,
                          hipStream_t st);
 hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP, const void* Cq,
                                    const float* hn, int kpad, const int32_t* idx, int* assign,
                                    float* mind, float* mind2, double* sse, int sse_mask,
+                                   const unsigned long long* mcount, float* xh, unsigned* xmax,
                                    hipStream_t st);
 
 // ---- K9 sparse closure round on a device hash set (tc_sparse.hip)

@@ -7,14 +7,17 @@ but never used; here ``tol`` optionally stops when the max squared centre shift
 drops below it (off by default = reference behaviour).
 
 SPMD version per iteration, every rank on its HBM-resident row shard:
-  K2 assign (MFMA distance GEMM + argmin)  ->  K3 per-cluster sums/counts (full pass,
-  or -- GPU, from the second iteration on, while at most DALGO_KM_INC_MAX (25 %) of
-  the rank's points changed cluster -- the incremental form: only the moved points
-  are subtracted from their old and added to their new cluster's f64 local sums, their
-  signed entries counting-sorted by cluster and summed in runs (kmeans.hip
-  km_dsegsum_kernel; per-row f64 atomics below 16k moved rows, kmeans_inc.hip))  ->
-  ONE all_reduce of the fused f32 bucket [sums k x DP || counts as 2 x k exact f32
-  words]  ->  fused update.
+  K2 assign (MFMA distance GEMM + argmin)  ->  K3 per-cluster sums/counts  ->  ONE
+  all_reduce of the fused f32 bucket [sums k x DP || counts as 2 x k exact f32 words]
+  ->  fused update.
+On the GPU the first iteration is a full pass and every later one is incremental:
+the sums are linear in the assignment, so only the points whose cluster changed are
+subtracted from their old and added to their new cluster's f64 local sums (counting-
+sorted signed entries, csrc/kernels/kmeans.hip km_dsegsum). With bf16 points (d in
+(32, 128], k <= 2048) the iterations after the first are also bound-filtered (Hamerly,
+exact): only the points the triangle inequality cannot prove unchanged go through K2.
+Every count (active, moved rows) stays on the device -- the kernels that consume it
+read it there -- so an iteration issues its launches without a host sync.
 The reduceByKey shuffle + driver collect become one RCCL all-reduce whose size is
 independent of N (520 KB at k=1024, d=128). Counts travel as (cnt mod 2^b,
 cnt >> b) f32 pairs with b = 24 - ceil(log2 W) (21 at 8 ranks): every partial sum
@@ -22,7 +25,6 @@ of the low words stays below 2^24, so the f32 reduction is exact.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -41,6 +43,7 @@ class KMeansConfig:
     init: str = "sample"       # "sample": k distinct random rows (takeSample) | "given"
     seed: int = 42             # takeSample(False, k, 42)
     tol: float | None = None   # convergeDist-style early stop (reference ignores it)
+    bound_filter: bool = True  # GPU bf16: Hamerly-filtered iterations after the first (exact)
 
 
 @dataclass
@@ -70,12 +73,9 @@ class KMeans:
         k = cfg.k
         if init_centers is None:
             init_centers = self._sample_init()
-        # centre-stationary K2 (kmeans_cs.hip) when it applies: centres padded to
-        # 256 / 512 / 1024, fixed point statistics computed once
-        kp = K.cs_kpad(k, self.d, self.X.dtype, self.dev)
-        self.pstats = K.point_stats(self.X) if kp is not None else None
-        self.cen = K.make_centers(init_centers.float(), self.X.dtype, self.dev, kpad=kp)
-        self.assign = torch.zeros(self.X.shape[0], dtype=torch.int32, device=self.dev)
+        self.cen = K.make_centers(init_centers.float(), self.X.dtype, self.dev)
+        n = self.X.shape[0]
+        self.assign = torch.zeros(n, dtype=torch.int32, device=self.dev)
         # [S (k x DP) || count lo (k) || count hi (k)]: one all-reduce per iteration
         self.bucket = torch.zeros(k * self.DP + 2 * k, dtype=torch.float32, device=self.dev)
         self.S = self.bucket[: k * self.DP].view(k, self.DP)
@@ -87,23 +87,50 @@ class KMeans:
         self.history = KMeansHistory()
         self.t = 0
         self.timer = None   # dalgo.utils.obs.PhaseTimer (None = off)
-        # incremental K3 state (GPU): f64 local sums / counts of the last iteration and
-        # its assignment (self.assign); None until a full pass has produced them
-        # the sorted incremental pass costs ~0.1 ms per million signed entries (2 per moved
-        # row) against ~5.5 ms for the full K3 + |x|^2 sums at 100M rows: break-even ~25 %
-        self.inc_max = float(os.environ.get("DALGO_KM_INC_MAX", "0.25"))
-        self._S64 = None
-        self.changed_history: list = []
-        # bound-filtered Lloyd (GPU, bf16, pipelined K2; DALGO_KM_BOUNDS=0 turns it off):
-        # exact -- a point is skipped only when the triangle inequality proves its centre
-        # is still the strictly closest one (see _step_bounds)
-        self.bounds = (self.dev.type == "cuda" and self.X.dtype == torch.bfloat16
-                       and self.DP in (64, 128) and self.pstats is None
-                       and K.assign_variant(self.X) == 52 and self.inc_max > 0
-                       and k <= 2048   # per-cluster |x|^2 sums: one LDS histogram
-                       and os.environ.get("DALGO_KM_BOUNDS", "1") != "0")
-        self._u = None
-        self.active_history: list = []
+        # incremental K3 (GPU, k within the sorted-move kernels' LDS): f64 local sums /
+        # counts of the last iteration; the move workspace is sized for every local row
+        # moving, so the moved count never has to reach the host
+        self.incremental = self.dev.type == "cuda" and k <= 2048
+        # bound-filtered Lloyd (GPU, bf16, pipelined K2): exact -- a point is skipped only
+        # when the triangle inequality proves its centre is still the strictly closest
+        self.bounds = (self.incremental and cfg.bound_filter and self.X.dtype == torch.bfloat16
+                       and self.DP in (64, 128))
+        self._first = True                       # next iteration is the full pass
+        self._hist_n = 0
+        if self.incremental:
+            i32 = dict(dtype=torch.int32, device=self.dev)
+            self._S64 = torch.zeros(self.S.shape, dtype=torch.float64, device=self.dev)
+            self._cnt64 = torch.zeros_like(self.cnt)
+            self._changed = torch.empty(max(n, 1), **i32)
+            self._n_changed = torch.zeros(1, dtype=torch.int64, device=self.dev)
+            self._mws = K.MoveWorkspace(self.dev, n, k)
+            # per-iteration device counters (read by the properties below, after the run)
+            self._hist = torch.zeros((64, 2), dtype=torch.int64, device=self.dev)
+            if self.bounds:
+                self._alloc_bounds()
+            else:
+                self._a_new = torch.empty(n, **i32)
+
+    def _alloc_bounds(self):
+        n, k = self.X.shape[0], self.cfg.k
+        f32 = dict(dtype=torch.float32, device=self.dev)
+        i32 = dict(dtype=torch.int32, device=self.dev)
+        self._xh = torch.empty(max(n, 1), **f32)     # 0.5 |x|^2 (written by the full pass)
+        self._xmax = torch.zeros(1, **i32)            # max 0.5 |x|^2 (float bits)
+        self._tol = torch.zeros(1, **f32)             # slack of a kernel distance (device)
+        self._u = torch.empty(max(n, 1), **f32)
+        self._l = torch.empty(max(n, 1), **f32)
+        self._mind = torch.empty(max(n, 1), **f32)
+        self._mind2 = torch.empty(max(n, 1), **f32)
+        self._a_prev = torch.empty(max(n, 1), **i32)
+        self._idx = torch.empty(max(n, 1), **i32)
+        self._n_active = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self._Q = torch.zeros(k, dtype=torch.float64, device=self.dev)
+        self._cq_prev = torch.empty((k, self.DP), dtype=self.cen.Cq.dtype, device=self.dev)
+        self._delta = torch.empty(k, **f32)
+        self._s = torch.empty(k, **f32)
+        self._pinf = torch.full((1,), float("inf"), **f32)   # nextafter directions
+        self._zero = torch.zeros(1, **f32)
 
     def _ph(self, name: str):
         return self.timer.phase(name) if self.timer is not None else NULL_PHASE
@@ -119,28 +146,33 @@ class KMeans:
         comm.all_reduce_sum(C)
         return C
 
-    def _bounds_state(self):
-        n, k = self.X.shape[0], self.cfg.k
-        st = K.point_stats(self.X, keep_xh=True)
-        self._xh = st.xh
-        self._tol = 2.0 * st.M * 2.0 ** -14          # slack of a kernel distance
-        self._u = torch.empty(n, dtype=torch.float32, device=self.dev)
-        self._l = torch.empty(n, dtype=torch.float32, device=self.dev)
-        self._mind = torch.empty(n, dtype=torch.float32, device=self.dev)
-        self._mind2 = torch.empty(n, dtype=torch.float32, device=self.dev)
-        self._a_prev = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)
-        self._idx = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)
-        self._changed = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)
-        self._n_active = torch.zeros(1, dtype=torch.int64, device=self.dev)
-        self._n_changed = torch.zeros(1, dtype=torch.int64, device=self.dev)
-        self._Q = torch.zeros(k, dtype=torch.float64, device=self.dev)
-        self._S64 = torch.empty(self.S.shape, dtype=torch.float64, device=self.dev)
-        self._cnt64 = torch.empty_like(self.cnt)
-        self._cq_prev = torch.empty((k, self.DP), dtype=self.cen.Cq.dtype, device=self.dev)
-        # first use of the f64 cdist / reductions loads their library kernels (~0.2 s):
-        # pay it here, in the full first pass, not in the first filtered iteration
-        K.centre_bounds(self.cen.Cq, self.cen.Cq, k)
+    # ------------------------------------------------------------- iteration counters
+    def _record(self, col: int, src: torch.Tensor | int):
+        if self._hist_n >= self._hist.shape[0]:
+            self._hist = torch.cat([self._hist, torch.zeros_like(self._hist)])
+        if isinstance(src, int):
+            self._hist[self._hist_n, col].fill_(src)
+        else:
+            self._hist[self._hist_n, col].copy_(src[0])
 
+    @property
+    def active_history(self) -> list:
+        """Rows re-assigned by K2 per iteration (bound filter; every row on a full pass)."""
+        if not self.bounds:
+            return []
+        return [int(v) for v in self._hist[: self._hist_n, 0].tolist()]
+
+    @property
+    def changed_history(self) -> list:
+        """Rows whose cluster changed per incremental iteration."""
+        if not self.incremental:
+            return []
+        return [int(v) for v in self._hist[: self._hist_n, 1].tolist()][1:]
+
+    def clear_history(self):
+        self._hist_n = 0
+
+    # ------------------------------------------------------------------- iterations
     def _step_bounds(self):
         """One Lloyd iteration with Hamerly's bounds (exact).
 
@@ -150,56 +182,87 @@ class KMeans:
         if u + delta[a] < max(s[a], l - maxd) (s[a] = half the distance from c_a to its
         nearest other centre) c_a is still strictly the closest centre and x keeps it
         without computing any distance (Hamerly, "Making k-means even faster", 2010).
-        The other points go through K2 (row indirection, variant 52, top-2 epilogue) and
-        the moved ones through the incremental K3. The SSE comes from the identity
+        The other points go through K2 (row indirection, top-2 epilogue) and the moved
+        ones through the incremental K3. The SSE comes from the identity
         sum_c (Q_c - 2 c.S_c + n_c |c|^2) with Q_c the per-cluster sum of |x|^2,
-        maintained with the sums."""
+        maintained with the sums. No host sync: the active / moved counts stay on the
+        device."""
         n, k, d = self.X.shape[0], self.cfg.k, self.d
-        if self._u is None:
-            if not hasattr(self, "_xh") or self._S64 is None:
-                self._bounds_state()
+        if self._first:
+            self._xmax.zero_()
             with self._ph("assign"):
-                K.assign_rows(self.X, self.cen, None, n, self.assign, self._mind, self._mind2)
+                # full pass: also 0.5|x|^2 per row and its maximum (the distance slack)
+                K.assign_rows(self.X, self.cen, None, n, self.assign, self._mind, self._mind2,
+                              xh=self._xh, xmax=self._xmax)
             with self._ph("accumulate"):
                 K.accumulate(self.X, self.assign, k, self.DP, self.S, self.cnt)
                 self._S64.copy_(self.S)
                 self._cnt64.copy_(self.cnt)
                 K.cluster_sq_sums(self.assign, self._xh, k, self._Q)
-            torch.sqrt(self._mind.clamp_min(0) + self._tol, out=self._u)
-            torch.sqrt((self._mind2 - self._tol).clamp_min(0), out=self._l)
-            self.active_history.append(n)
+            # tol = 2 M 2^-14, M >= max 0.5|x|^2 (slack of a truncated kernel distance)
+            M = self._xmax.view(torch.float32) * 1.0001 + 1e-6
+            torch.mul(M, 2.0 * 2.0 ** -14, out=self._tol)
+            up, dn = self._pinf, self._zero
+            torch.nextafter(torch.sqrt(torch.nextafter(self._mind[:n].clamp_min(0) + self._tol, up)),
+                            up, out=self._u[:n])
+            torch.nextafter(torch.sqrt((self._mind2[:n] - self._tol).clamp_min(0)), dn,
+                            out=self._l[:n])
+            self._l[:n].clamp_min_(0)
+            self._record(0, n)
+            self._record(1, 0)
+            self._first = False
         else:
-            delta, s = K.centre_bounds(self.cen.Cq, self._cq_prev, k)
-            maxd = delta.max().reshape(1)
+            K.centre_bounds(self.cen.Cq, self._cq_prev, k, d, self._delta, self._s)
             with self._ph("filter"):
-                m = K.filter_rows(self.assign, self._u, self._l, delta, s, maxd, self._a_prev,
-                                  self._idx, self._n_active)
-            self.active_history.append(m)
+                K.filter_rows(self.assign, self._u, self._l, self._delta, self._s, self._a_prev,
+                              self._idx, self._n_active)
             with self._ph("assign"):
-                K.assign_rows(self.X, self.cen, self._idx, m, self.assign, self._mind, self._mind2)
+                K.assign_rows(self.X, self.cen, self._idx, n, self.assign, self._mind, self._mind2,
+                              m_dev=self._n_active)
             with self._ph("post"):
-                moved = K.post_rows(self._idx, m, self.assign, self._a_prev, self._mind,
-                                    self._mind2, self._tol, self._u, self._l, self._changed,
-                                    self._n_changed)
-            self.changed_history.append(moved)
-            if moved <= self.inc_max * n:
-                with self._ph("accumulate_incremental"):
-                    K.move_rows(self.X, self.DP, self._changed, moved, self.assign, self._a_prev,
-                                self._S64, self._cnt64, self._xh, self._Q)
-                    self.S.copy_(self._S64)
-                    self.cnt.copy_(self._cnt64)
-            else:
-                with self._ph("accumulate"):
-                    K.accumulate(self.X, self.assign, k, self.DP, self.S, self.cnt)
-                    self._S64.copy_(self.S)
-                    self._cnt64.copy_(self.cnt)
-                    K.cluster_sq_sums(self.assign, self._xh, k, self._Q)
+                K.post_rows(self._idx, n, self.assign, self._a_prev, self._mind, self._mind2, 0.0,
+                            self._u, self._l, self._changed, self._n_changed,
+                            m_dev=self._n_active, tol_dev=self._tol)
+            with self._ph("accumulate_incremental"):
+                K.move_rows(self.X, self.DP, self._changed, self._n_changed, self.assign,
+                            self._a_prev, self._S64, self._cnt64, self._mws, self._xh, self._Q)
+                self.S.copy_(self._S64)
+                self.cnt.copy_(self._cnt64)
+            self._record(0, self._n_active)
+            self._record(1, self._n_changed)
+        self._hist_n += 1
         # local SSE on the (rounded) centres of this assignment
         Cd = self.cen.Cq[:k, :d].double()
         Sd = self._S64[:, :d]
         sse = self._Q - 2.0 * (Cd * Sd).sum(dim=1) + self._cnt64.double() * (Cd * Cd).sum(dim=1)
         self.sse.copy_(sse.sum().clamp_min(0).reshape(1))
         self._cq_prev.copy_(self.cen.Cq[:k])
+
+    def _step_incremental(self):
+        """Full K2 pass, incremental K3 (GPU without the bound filter)."""
+        k = self.cfg.k
+        if self._first:
+            with self._ph("assign"):
+                K.assign(self.X, self.cen, out=self.assign, sse=self.sse)
+            with self._ph("accumulate"):
+                K.accumulate(self.X, self.assign, k, self.DP, self.S, self.cnt)
+                self._S64.copy_(self.S)
+                self._cnt64.copy_(self.cnt)
+            self._record(1, 0)
+            self._first = False
+        else:
+            with self._ph("assign"):
+                K.assign(self.X, self.cen, out=self._a_new, sse=self.sse)
+            with self._ph("diff"):
+                K.changed_rows(self._a_new, self.assign, self._changed, self._n_changed)
+            with self._ph("accumulate_incremental"):
+                K.move_rows(self.X, self.DP, self._changed, self._n_changed, self._a_new,
+                            self.assign, self._S64, self._cnt64, self._mws)
+                self.S.copy_(self._S64)
+                self.cnt.copy_(self._cnt64)
+            self.assign, self._a_new = self._a_new, self.assign
+            self._record(1, self._n_changed)
+        self._hist_n += 1
 
     def step(self):
         self.sse.zero_()
@@ -208,31 +271,13 @@ class KMeans:
         self.shift2.zero_()
         if self.bounds:
             self._step_bounds()
-            self._reduce_and_update()
-            return
-        inc = self._S64 is not None and self.inc_max > 0
-        a_out = self._a_new if inc else self.assign
-        with self._ph("assign"):
-            K.assign(self.X, self.cen, out=a_out, sse=self.sse, stats=self.pstats)
-        moved = None
-        if inc:
-            with self._ph("diff"):
-                moved = K.changed_rows(a_out, self.assign, self._changed, self._n_changed)
-            self.changed_history.append(moved)
-            if moved > self.inc_max * self.X.shape[0]:
-                inc = False
-        if inc:
-            with self._ph("accumulate_incremental"):
-                K.move_rows(self.X, self.DP, self._changed, moved, a_out, self.assign,
-                            self._S64, self._cnt64)
-                self.S.copy_(self._S64)
-                self.cnt.copy_(self._cnt64)
+        elif self.incremental:
+            self._step_incremental()
         else:
+            with self._ph("assign"):
+                K.assign(self.X, self.cen, out=self.assign, sse=self.sse)
             with self._ph("accumulate"):
-                K.accumulate(self.X, a_out, self.cfg.k, self.DP, self.S, self.cnt)
-            self._keep_local_sums()
-        if a_out is not self.assign:
-            self.assign, self._a_new = a_out, self.assign
+                K.accumulate(self.X, self.assign, self.cfg.k, self.DP, self.S, self.cnt)
         self._reduce_and_update()
 
     def _reduce_and_update(self):
@@ -250,20 +295,6 @@ class KMeans:
             K.update(self.cen, self.S, self.cnt, self.shift2)
         self.t += 1
 
-    def _keep_local_sums(self):
-        """After a full K3 pass: remember the local sums for the incremental form."""
-        if not (self.X.is_cuda and self.inc_max > 0):
-            return
-        if self._S64 is None:
-            n = self.X.shape[0]
-            self._S64 = torch.empty(self.S.shape, dtype=torch.float64, device=self.dev)
-            self._cnt64 = torch.empty_like(self.cnt)
-            self._a_new = torch.empty_like(self.assign)
-            self._changed = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)
-            self._n_changed = torch.zeros(1, dtype=torch.int64, device=self.dev)
-        self._S64.copy_(self.S)
-        self._cnt64.copy_(self.cnt)
-
     def fit(self, n_iterations: int | None = None, track: bool = True):
         n = self.cfg.n_iterations if n_iterations is None else n_iterations
         for _ in range(n):
@@ -279,9 +310,7 @@ class KMeans:
         return self.history
 
     def predict(self, X: torch.Tensor) -> torch.Tensor:
-        Xp = K.prepare_points(X)
-        st = K.point_stats(Xp) if self.pstats is not None else None
-        return K.assign(Xp, self.cen, stats=st)
+        return K.assign(K.prepare_points(X), self.cen)
 
     @property
     def centers(self) -> torch.Tensor:
@@ -292,8 +321,7 @@ class KMeans:
                 "shift": list(self.history.shift)}
 
     def load_state_dict(self, sd: dict):
-        self._S64 = None          # the next iteration runs the full K3 pass
-        self._u = None            # ... and the full assignment (bounds rebuilt)
+        self._first = True        # the next iteration is the full pass (sums, bounds rebuilt)
         self.t = int(sd["t"])
         self.cen.C.copy_(sd["centers"].to(self.dev))
         K.refresh(self.cen)

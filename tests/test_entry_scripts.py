@@ -187,14 +187,13 @@ def test_bench_self_launches_n_ranks():
 
 
 @pytest.mark.parametrize("script,args,metric", [
-    ("bench/kmeans_bench.py", ["--rows", "20000", "--dim", "16", "--k", "8", "--dtype", "f32"],
-     "k-means points/sec (whole node)"),
-    ("bench/pagerank_bench.py", ["--scale", "10"], "PageRank edges/sec (whole node)"),
+    ("bench/kmeans_bench.py", ["--rows", "20000", "--dim", "16", "--k", "8", "--dtype", "f32",
+                               "--iters", "2"], "k-means points/sec (whole node)"),
+    ("bench/pagerank_bench.py", ["--scale", "10", "--steps", "2"], "PageRank edges/sec (whole node)"),
 ])
 def test_secondary_benches_self_launch(script, args, metric):
     """The k-means and PageRank benches start N ranks themselves like bench.py."""
-    out = _run([script, "--gpus", "2", "--device", "cpu", "--backend", "gloo", "--steps", "2"]
-               + args, timeout=600)
+    out = _run([script, "--gpus", "2", "--device", "cpu", "--backend", "gloo"] + args, timeout=600)
     lines = [l for l in out.splitlines() if l.startswith("{")]
     assert len(lines) == 1
     d = json.loads(lines[0])

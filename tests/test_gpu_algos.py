@@ -13,72 +13,28 @@ pytestmark = pytest.mark.gpu
 
 
 # ------------------------------------------------------------------ k-means
+# bf16 with DP 64 / 128 takes the pipelined MFMA form (ragged tile groups, one and many
+# 128-centre chunks); f32 and small d the generic form
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("d,k,n", [(2, 2, 6), (16, 40, 3000), (50, 33, 4099), (128, 1024, 20000)])
+@pytest.mark.parametrize("d,k,n", [(2, 2, 6), (16, 40, 3000), (50, 33, 4099), (64, 128, 513),
+                                   (100, 1500, 9000), (128, 600, 70001), (128, 1024, 20000)])
 def test_kmeans_assign_matches_reference(cuda, dtype, d, k, n):
-    _check_assign(cuda, dtype, d, k, n, None)
+    _check_assign(cuda, dtype, d, k, n)
 
 
-# resident-centre K2 (bf16): one and several 512-centre passes, DP = 16/32/64/128,
-# a ragged last tile group, and point counts below one tile group
-@pytest.mark.parametrize("variant", [11, 12, 13])
-@pytest.mark.parametrize("d,k,n", [(2, 2, 6), (16, 40, 3000), (30, 77, 1025), (50, 33, 4099),
-                                   (128, 1024, 20000), (128, 600, 70001), (100, 1500, 9000)])
-def test_kmeans_assign_resident(cuda, variant, d, k, n):
-    _check_assign(cuda, torch.bfloat16, d, k, n, variant)
-
-
-# pipelined K2 (bf16, LDS-DMA triple-buffered centre chunks): DP = 64 / 128 (smaller DP
-# falls back to variant 5), ragged tile groups, one and many chunks
-@pytest.mark.parametrize("variant", [14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 29,
-                                     48, 49, 50, 51, 52, 53, 54])
-@pytest.mark.parametrize("d,k,n", [(2, 2, 6), (50, 33, 4099), (100, 1500, 9000),
-                                   (128, 1024, 20000), (128, 600, 70001), (64, 128, 513)])
-def test_kmeans_assign_pipelined(cuda, variant, d, k, n):
-    _check_assign(cuda, torch.bfloat16, d, k, n, variant)
-
-
-# 256-centre chunks (8-wave blocks): the padded centre count must be a multiple of 256
-@pytest.mark.parametrize("variant", [28, 30])
-@pytest.mark.parametrize("d,k,n", [(128, 1024, 20000), (100, 250, 7001), (64, 512, 513)])
-def test_kmeans_assign_pipelined_wide_chunks(cuda, variant, d, k, n):
-    _check_assign(cuda, torch.bfloat16, d, k, n, variant)
-
-
-def test_kmeans_pipelined_ties(cuda):
+@pytest.mark.parametrize("d", [8, 128])
+def test_kmeans_assign_ties(cuda, d):
     """Exact ties resolve to the lowest id across sub-tiles, chunks and lane halves."""
-    X = torch.zeros(300, 128)
-    C0 = torch.zeros(1100, 128) + 50.0
+    X = torch.zeros(300, d)
+    C0 = torch.zeros(1100, d) + 50.0
     for c in (3, 7, 12, 515, 1030):
         C0[c] = 0.0
-        C0[c, c % 128] = 1.0
-    for v in (14, 15, 16, 17, 18, 20, 22, 23, 24, 25, 26, 27, 29, 50, 51, 52, 53, 54):
-        a = K.assign(K.prepare_points(X.to(cuda).bfloat16()), K.make_centers(C0, torch.bfloat16, cuda),
-                     variant=v).cpu()
-        assert a.tolist() == [3] * 300, v
+        C0[c, c % d] = 1.0
+    a = K.assign(K.prepare_points(X.to(cuda).bfloat16()), K.make_centers(C0, torch.bfloat16, cuda)).cpu()
+    assert a.tolist() == [3] * 300
 
 
-def test_kmeans_resident_ties_and_passes(cuda):
-    """Exact ties resolve to the lowest id inside a pass, across lane halves and across passes."""
-    X = torch.zeros(70, 8)
-    C0 = torch.zeros(1100, 8) + 50.0
-    for c in (3, 7, 12, 515, 1030):      # equidistant from 0: same pass, other half, later passes
-        C0[c] = 0.0
-        C0[c, c % 8] = 1.0
-    for v in (11, 12, 13):
-        a = K.assign(K.prepare_points(X.to(cuda).bfloat16()), K.make_centers(C0, torch.bfloat16, cuda),
-                     variant=v).cpu()
-        assert a.tolist() == [3] * 70, v
-    C0[3, 3] = 2.0                       # now the later passes hold the nearest (ids 7 and 12 stay tied)
-    C0[7, 7] = 2.0
-    C0[12, 4] = 2.0
-    for v in (11, 12, 13):
-        a = K.assign(K.prepare_points(X.to(cuda).bfloat16()), K.make_centers(C0, torch.bfloat16, cuda),
-                     variant=v).cpu()
-        assert a.tolist() == [515] * 70, v
-
-
-def _check_assign(cuda, dtype, d, k, n, variant):
+def _check_assign(cuda, dtype, d, k, n):
     g = torch.Generator().manual_seed(d + k)
     X = (torch.randn(n, d, generator=g) * 3).to(dtype)
     C0 = torch.randn(k, d, generator=g) * 3
@@ -89,7 +45,7 @@ def _check_assign(cuda, dtype, d, k, n, variant):
     cen_d = K.make_centers(C0, dtype, cuda)
     mind = torch.empty(n, device=cuda)
     sse = torch.zeros(1, dtype=torch.float64, device=cuda)
-    a = K.assign(Xd, cen_d, mind=mind, sse=sse, variant=variant).cpu()
+    a = K.assign(Xd, cen_d, mind=mind, sse=sse).cpu()
     # scores computed in f32 on the GPU vs f64 on the CPU: allow rare near-ties
     agree = (a == a_ref).float().mean().item()
     assert agree > 0.999, agree
@@ -101,6 +57,7 @@ def _check_assign(cuda, dtype, d, k, n, variant):
     assert dd.abs().max().item() < 1e-3 * (1 + dist.max().item())
     assert torch.allclose(mind.cpu().double(), dist.gather(1, a.long()[:, None])[:, 0],
                           rtol=1e-3, atol=1e-2)
+    assert float(sse.item()) == pytest.approx(float(mind.double().sum().item()), rel=1e-6)
 
 
 def test_kmeans_ties_lowest_index(cuda):
@@ -112,17 +69,13 @@ def test_kmeans_ties_lowest_index(cuda):
 
 @pytest.mark.parametrize("k,skew", [(1024, "uniform"), (1500, "uniform"), (2048, "uniform"),
                                     (2048, "one-cluster"), (1500, "two-clusters"),
-                                    (3000, "uniform"), (12000, "uniform"), (16384, "uniform")])
-@pytest.mark.parametrize("scatter", ["chunked", "cursor"])
-def test_kmeans_sorted_scatter_variants(cuda, monkeypatch, k, skew, scatter):
-    """K3 sorted accumulate with the coalesced chunked scatter (k <= 2048, default) and the
-    per-row LDS-cursor scatter (DALGO_KM_SCATTER=0, and k > 2048): several blocks, full and
-    partial 32K-row chunks; exact counts, f64-checked sums. k = 1500 / 2048 run the
-    two-clusters-per-thread scan of the chunked scatter (kScKmax boundary); "one-cluster"
-    puts every row of a 32K chunk in one cluster (15-bit local rank at its limit);
-    k = 12000 / 16384 need the > 64 KB dynamic-LDS scan."""
-    if scatter == "cursor":
-        monkeypatch.setenv("DALGO_KM_SCATTER", "0")
+                                    (3000, "uniform"), (16384, "uniform")])
+def test_kmeans_sorted_accumulate(cuda, k, skew):
+    """K3 sorted accumulate: the coalesced chunked scatter (k <= 2048) and the per-row
+    LDS-cursor scatter (k > 2048): several blocks, full and partial 32K-row chunks; exact
+    counts, f64-checked sums. k = 1500 / 2048 run the two-clusters-per-thread scan of the
+    chunked scatter (kScKmax boundary); "one-cluster" puts every row of a 32K chunk in one
+    cluster (15-bit local rank at its limit); k = 16384 needs the > 64 KB dynamic-LDS scan."""
     n, d = 300_001, 64
     g = torch.Generator().manual_seed(3)
     X = torch.randn(n, d, generator=g).to(torch.bfloat16)
@@ -135,16 +88,15 @@ def test_kmeans_sorted_scatter_variants(cuda, monkeypatch, k, skew, scatter):
     DP = K.kmeans_dp(d)
     S = torch.zeros(k, DP, device=cuda)
     cnt = torch.zeros(k, dtype=torch.int64, device=cuda)
-    K.accumulate(K.prepare_points(X.to(cuda)), a.to(cuda), k, DP, S, cnt, method="sorted")
+    K.accumulate(K.prepare_points(X.to(cuda)), a.to(cuda), k, DP, S, cnt)
     Sr = torch.zeros(k, DP, dtype=torch.float64)
     Sr[:, :d].index_add_(0, a.long(), X.double())
     assert torch.equal(cnt.cpu(), torch.bincount(a.long(), minlength=k))
     assert torch.allclose(S.cpu().double(), Sr, atol=1e-2, rtol=1e-4)
 
 
-@pytest.mark.parametrize("method", ["sorted", "table"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_kmeans_accumulate_update(cuda, dtype, method):
+def test_kmeans_accumulate_update(cuda, dtype):
     n, d, k = 50_000, 100, 70
     g = torch.Generator().manual_seed(1)
     X = torch.randn(n, d, generator=g).to(dtype)
@@ -152,7 +104,7 @@ def test_kmeans_accumulate_update(cuda, dtype, method):
     DP = K.kmeans_dp(d)
     S = torch.zeros(k, DP, device=cuda)
     cnt = torch.zeros(k, dtype=torch.int64, device=cuda)
-    K.accumulate(K.prepare_points(X.to(cuda)), a.to(cuda), k, DP, S, cnt, method=method)
+    K.accumulate(K.prepare_points(X.to(cuda)), a.to(cuda), k, DP, S, cnt)
     Sr = torch.zeros(k, DP, dtype=torch.float64)
     Sr[:, :d].index_add_(0, a.long(), X.double())
     cr = torch.bincount(a.long(), minlength=k)
@@ -667,8 +619,8 @@ def test_kmeans_incremental_accumulate_exact(cuda, d, dtype):
     from dalgo.ops import kmeans as K
     n, k = 150_000, 96
     X = blobs(n, d, k, device=cuda, dtype=dtype, seed=5)
-    km = KMeans(KMeansConfig(k=k, n_iterations=6, seed=2), X, 0, n)
-    km.inc_max = 1.0                     # always incremental after the first pass
+    km = KMeans(KMeansConfig(k=k, n_iterations=6, seed=2, bound_filter=False), X, 0, n)
+    assert km.incremental and not km.bounds
 
     def exact(a):
         S = torch.zeros(k, km.DP, dtype=torch.float64, device=cuda)
@@ -692,11 +644,12 @@ def test_kmeans_incremental_accumulate_exact(cuda, d, dtype):
 
 @pytest.mark.parametrize("d,dtype,k,m", [(128, torch.bfloat16, 1024, 300_000),
                                          (64, torch.bfloat16, 96, 40_000),
-                                         (30, torch.float32, 2048, 20_000)])
-def test_kmeans_move_sorted_equals_atomic(cuda, monkeypatch, d, dtype, k, m):
-    """Sort-based incremental K3 (signed entries counting-sorted by cluster, f64 run sums)
-    == the per-row f64-atomic form: sums, counts and the |x|^2 sums Q."""
-    from dalgo.ops import kmeans as K
+                                         (30, torch.float32, 2048, 20_000),
+                                         (128, torch.bfloat16, 1024, 3),
+                                         (64, torch.bfloat16, 512, 0)])
+def test_kmeans_move_sorted_exact(cuda, d, dtype, k, m):
+    """Sort-based incremental K3 with the moved-row count on the DEVICE (workspace sized for
+    every row): sums / counts / |x|^2 sums Q == the f64 signed moves computed by torch."""
     n = 500_000
     g = torch.Generator().manual_seed(3)
     X = K.prepare_points((torch.randn(n, d, generator=g) * 3).to(dtype).to(cuda))
@@ -705,22 +658,27 @@ def test_kmeans_move_sorted_equals_atomic(cuda, monkeypatch, d, dtype, k, m):
     a_new = a_old.clone()
     rows = torch.randperm(n, generator=g)[:m].to(cuda)
     a_new[rows] = torch.randint(0, k, (m,), generator=g, dtype=torch.int32).to(cuda)
-    changed = torch.sort(rows.to(torch.int32)).values
+    changed = torch.zeros(n, dtype=torch.int32, device=cuda)
+    changed[:m] = torch.sort(rows.to(torch.int32)).values
+    m_dev = torch.tensor([m], dtype=torch.int64, device=cuda)
     xh = (torch.rand(n, generator=g) * 10).to(cuda)
-    out = []
-    for thr in (1 << 40, 1):
-        monkeypatch.setattr(K, "MOVE_SORTED_MIN", thr)
-        S = torch.zeros(k, DP, dtype=torch.float64, device=cuda)
-        c = torch.zeros(k, dtype=torch.int64, device=cuda)
-        Q = torch.zeros(k, dtype=torch.float64, device=cuda)
-        K.move_rows(X, DP, changed, m, a_new, a_old, S, c, xh, Q)
-        torch.cuda.synchronize()
-        out.append((S, c, Q))
-    (S0, c0, Q0), (S1, c1, Q1) = out
-    assert torch.equal(c0, c1)
-    assert int(c1.sum().item()) == 0
-    assert torch.allclose(S0, S1, rtol=1e-12, atol=1e-9), (S0 - S1).abs().max()
-    assert torch.allclose(Q0, Q1, rtol=1e-12, atol=1e-6), (Q0 - Q1).abs().max()
+    ws = K.MoveWorkspace(cuda, n, k)
+    S = torch.zeros(k, DP, dtype=torch.float64, device=cuda)
+    c = torch.zeros(k, dtype=torch.int64, device=cuda)
+    Q = torch.zeros(k, dtype=torch.float64, device=cuda)
+    K.move_rows(X, DP, changed, m_dev, a_new, a_old, S, c, ws, xh, Q)
+    r = rows.long()
+    xr = X[r].double()
+    Se = torch.zeros(k, DP, dtype=torch.float64, device=cuda)
+    Se[:, :d].index_add_(0, a_new[r].long(), xr)
+    Se[:, :d].index_add_(0, a_old[r].long(), -xr)
+    ce = torch.bincount(a_new[r].long(), minlength=k) - torch.bincount(a_old[r].long(), minlength=k)
+    Qe = torch.zeros(k, dtype=torch.float64, device=cuda)
+    Qe.index_add_(0, a_new[r].long(), 2.0 * xh[r].double())
+    Qe.index_add_(0, a_old[r].long(), -2.0 * xh[r].double())
+    assert torch.equal(c, ce)
+    assert torch.allclose(S, Se, rtol=1e-12, atol=1e-9), (S - Se).abs().max()
+    assert torch.allclose(Q, Qe, rtol=1e-12, atol=1e-6), (Q - Qe).abs().max()
 
 
 @pytest.mark.parametrize("sem", ["reference", "standard"])
@@ -766,66 +724,6 @@ def test_pr_spmv_hot_lds_table(cuda, monkeypatch, hot):
     assert max(abs(ref[v] - got[v]) for v in ref) < 1e-7
 
 
-@pytest.mark.parametrize("d,k,n", [(128, 1024, 20000), (100, 1000, 7001), (64, 512, 513),
-                                   (50, 300, 4099), (128, 200, 65), (64, 1024, 100_003)])
-def test_kmeans_assign_centre_stationary(cuda, d, k, n):
-    """K2 centre-stationary form (centres resident in VGPRs, points streamed once through
-    LDS by DMA, cross-wave argmin): assignments, per-point distances and SSE == the CPU
-    reference on the rounded operands (rare f32 near-ties allowed)."""
-    torch.manual_seed(d * k)
-    X = (torch.randn(n, d) * 3).to(torch.bfloat16)
-    C0 = torch.randn(k, d) * 3
-    Xc = K.prepare_points(X)
-    cen_c = K.make_centers(C0, torch.bfloat16, "cpu")
-    sse_c = torch.zeros(1, dtype=torch.float64)
-    a_ref = K.assign(Xc, cen_c, sse=sse_c)
-    Xd = K.prepare_points(X.to(cuda))
-    kp = K.cs_kpad(k, d, torch.bfloat16, cuda, variant=K.CS_VARIANT)
-    assert kp in K.CS_KPADS
-    cen_d = K.make_centers(C0, torch.bfloat16, cuda, kpad=kp)
-    st = K.point_stats(Xd, keep_xh=True)
-    mind = torch.empty(n, device=cuda)
-    sse = torch.zeros(1, dtype=torch.float64, device=cuda)
-    a = K.assign(Xd, cen_d, mind=mind, sse=sse, stats=st).cpu()
-    agree = (a == a_ref).float().mean().item()
-    assert agree > 0.999, agree
-    Xf = Xc.double()
-    Cr = cen_c.Cq[:k, :d].double()
-    dist = torch.cdist(Xf, Cr) ** 2
-    dd = dist.gather(1, a.long()[:, None]) - dist.gather(1, a_ref.long()[:, None])
-    assert dd.abs().max().item() < 1e-3 * (1 + dist.max().item())
-    best = dist.gather(1, a.long()[:, None])[:, 0]
-    assert torch.allclose(mind.cpu().double(), best, rtol=1e-3, atol=5e-2)
-    assert float(sse.item()) == pytest.approx(float(sse_c.item()), rel=1e-4)
-    # without per-point distances (the model's path: no xh vector)
-    st2 = K.point_stats(Xd)
-    a2 = K.assign(Xd, cen_d, stats=st2).cpu()
-    assert torch.equal(a2, a)
-
-
-def test_kmeans_model_centre_stationary_vs_pipelined(cuda, monkeypatch):
-    """KMeans on blobs: the centre-stationary K2 (DALGO_KM_VARIANT=60) and the pipelined
-    variant 52 give the same SSE trajectory."""
-    from dalgo.data.synthetic import blobs
-    from dalgo.models.kmeans import KMeans, KMeansConfig
-    n, d, k = 200_000, 128, 1000
-    X = blobs(n, d, k, device=cuda, dtype=torch.bfloat16, seed=4)
-    monkeypatch.setattr(K, "ASSIGN_VARIANT", K.CS_VARIANT)
-    a = KMeans(KMeansConfig(k=k, n_iterations=4, seed=3), X, 0, n)
-    assert a.pstats is not None and a.cen.Cq.shape[0] == 1024
-    a.fit()
-    monkeypatch.setattr(K, "ASSIGN_VARIANT", 52)
-    b = KMeans(KMeansConfig(k=k, n_iterations=4, seed=3), X, 0, n)
-    assert b.pstats is None
-    b.fit()
-    # the two kernels truncate the distance keys at different offsets (global vs block
-    # max of 0.5|x|^2), so bf16 near-ties may go either way: SSE to 1e-4, and all but a
-    # handful of centres identical to f32 rounding
-    assert np.allclose(a.history.sse, b.history.sse, rtol=1e-4)
-    same = (a.centers - b.centers).abs().amax(dim=1) < 1e-2
-    assert same.float().mean().item() > 0.9   # boundary clusters drift (chaotic near-ties)
-
-
 def test_kmeans_assign_rows_indirect(cuda):
     """K2 with row indirection (only the listed rows) == the full K2 on those rows, and
     leaves every other row's assignment untouched."""
@@ -845,7 +743,8 @@ def test_kmeans_assign_rows_indirect(cuda):
 
 
 def test_kmeans_filter_and_post_match_torch(cuda):
-    from dalgo.ops import kmeans as K
+    """Bound filter (maxd reduced in-kernel from delta, bounds rounded outward) and the
+    post pass with the active count and tol on the DEVICE == torch."""
     torch.manual_seed(6)
     n, k = 100_003, 50
     assign = torch.randint(0, k, (n,), dtype=torch.int32, device=cuda)
@@ -853,32 +752,91 @@ def test_kmeans_filter_and_post_match_torch(cuda):
     l = torch.rand(n, device=cuda) * 20
     delta = torch.rand(k, device=cuda)
     s = torch.rand(k, device=cuda) * 12
-    maxd = delta.max().reshape(1)
+    maxd = delta.max()
     u0, l0 = u.clone(), l.clone()
     a_prev = torch.full((n,), -1, dtype=torch.int32, device=cuda)
     idx = torch.empty(n, dtype=torch.int32, device=cuda)
     cnt = torch.zeros(1, dtype=torch.int64, device=cuda)
-    m = K.filter_rows(assign, u, l, delta, s, maxd, a_prev, idx, cnt)
+    K.filter_rows(assign, u, l, delta, s, a_prev, idx, cnt)
+    m = int(cnt.item())
     ub = u0 + delta[assign.long()]
     lb = l0 - maxd
     act = ~(ub < torch.maximum(s[assign.long()], lb))
+    # outward rounding can only add active rows at exact float ties: none in random data
     assert m == int(act.sum())
     assert torch.equal(torch.sort(idx[:m]).values.long(), torch.nonzero(act)[:, 0])
-    assert torch.allclose(u[~act], ub[~act]) and torch.equal(u[act], u0[act])
-    assert torch.allclose(l[~act], lb[~act]) and torch.equal(l[act], l0[act])
+    assert bool((u[~act] >= ub[~act]).all()) and torch.allclose(u[~act], ub[~act])
+    assert bool((l[~act] <= lb[~act]).all()) and torch.allclose(l[~act], lb[~act])
+    assert torch.equal(u[act], u0[act]) and torch.equal(l[act], l0[act])
     assert torch.equal(a_prev[act], assign[act])
-    # post: half of the active rows change cluster
+    # post: half of the active rows change cluster; m and tol read on the device
     new = assign.clone()
     ch = act & (torch.arange(n, device=cuda) % 2 == 0)
     new[ch] = (new[ch] + 1) % k
     mind = torch.rand(n, device=cuda) * 4
     mind2 = mind + torch.rand(n, device=cuda) * 4
     changed = torch.empty(n, dtype=torch.int32, device=cuda)
-    c = K.post_rows(idx, m, new, a_prev, mind, mind2, 0.5, u, l, changed, cnt)
+    nch = torch.zeros(1, dtype=torch.int64, device=cuda)
+    tol = torch.full((1,), 0.5, device=cuda)
+    K.post_rows(idx, n, new, a_prev, mind, mind2, 0.0, u, l, changed, nch, m_dev=cnt, tol_dev=tol)
+    c = int(nch.item())
     assert c == int(ch.sum())
     assert torch.equal(torch.sort(changed[:c]).values.long(), torch.nonzero(ch)[:, 0])
-    assert torch.allclose(u[act], torch.sqrt(mind[act] + 0.5))
-    assert torch.allclose(l[act], torch.sqrt((mind2[act] - 0.5).clamp_min(0)))
+    ue, le = torch.sqrt(mind[act] + 0.5), torch.sqrt((mind2[act] - 0.5).clamp_min(0))
+    assert bool((u[act] >= ue).all()) and torch.allclose(u[act], ue)
+    assert bool((l[act] <= le).all()) and torch.allclose(l[act], le)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("k,d", [(1, 8), (7, 30), (1024, 128)])
+def test_kmeans_centre_bounds_kernel(cuda, dtype, k, d):
+    """delta / s of the bound filter (one launch) == f64 torch, rounded outward."""
+    torch.manual_seed(k + d)
+    DP = K.kmeans_dp(d)
+    a = torch.zeros(K.make_centers(torch.zeros(k, d), dtype, "cpu").Cq.shape, dtype=dtype)
+    a[:k, :d] = (torch.randn(k, d) * 3).to(dtype)
+    b = a.clone()
+    b[:k, :d] = (a[:k, :d].float() + torch.randn(k, d) * 0.1).to(dtype)
+    dg, sg = K.centre_bounds(a.to(cuda), b[:k].contiguous().to(cuda), k, d)
+    dc, sc = K.centre_bounds(a, b[:k].contiguous(), k, d)
+    ad, bd = a[:k, :d].double(), b[:k, :d].double()
+    dex = (ad - bd).norm(dim=1)
+    assert bool((dg.cpu().double() >= dex).all())
+    assert torch.allclose(dg.cpu(), dc, rtol=1e-5, atol=1e-6)
+    if k == 1:
+        assert bool(torch.isinf(sg).all())
+    else:
+        dd = torch.cdist(ad, ad)
+        dd.fill_diagonal_(float("inf"))
+        assert bool((sg.cpu().double() <= 0.5 * dd.min(dim=1).values).all())
+        assert torch.allclose(sg.cpu(), sc, rtol=1e-5)
+
+
+def test_kmeans_assign_rows_device_count(cuda):
+    """Top-2 K2 with the row count on the device (resident-grid tile loop): only
+    idx[:*m_dev] is re-assigned, equal to the full pass on those rows; also the optional
+    0.5|x|^2 / max outputs of a full pass."""
+    torch.manual_seed(9)
+    n, d, k = 60_001, 128, 1000
+    X = K.prepare_points((torch.randn(n, d) * 3).to(torch.bfloat16).to(cuda))
+    cen = K.make_centers(torch.randn(k, d) * 3, torch.bfloat16, cuda)
+    full = K.assign(X, cen)
+    rows = torch.randperm(n, device=cuda).to(torch.int32)
+    m = 23_457
+    a = torch.full((n,), -7, dtype=torch.int32, device=cuda)
+    mind = torch.zeros(n, device=cuda)
+    mind2 = torch.zeros(n, device=cuda)
+    K.assign_rows(X, cen, rows, n, a, mind, mind2,
+                  m_dev=torch.tensor([m], dtype=torch.int64, device=cuda))
+    sel = torch.zeros(n, dtype=torch.bool, device=cuda)
+    sel[rows[:m].long()] = True
+    assert torch.equal(a[sel], full[sel]) and bool((a[~sel] == -7).all())
+    xh = torch.zeros(n, device=cuda)
+    xmax = torch.zeros(1, dtype=torch.int32, device=cuda)
+    K.assign_rows(X, cen, None, n, a, mind, mind2, xh=xh, xmax=xmax)
+    ref = 0.5 * X[:, :d].float().pow(2).sum(1)
+    assert torch.allclose(xh, ref, rtol=1e-5)
+    assert float(xmax.view(torch.float32).item()) == pytest.approx(float(ref.max()), rel=1e-5)
 
 
 def test_kmeans_assign_top2_second_best(cuda):
@@ -913,8 +871,8 @@ def test_kmeans_bound_filter_exact(cuda):
     a = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5), X, 0, n)
     assert a.bounds
     a.fit()
-    b = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5), X, 0, n)
-    b.bounds = False
+    b = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5, bound_filter=False), X, 0, n)
+    assert not b.bounds
     b.fit()
     assert np.allclose(a.history.sse, b.history.sse, rtol=2e-4), (a.history.sse, b.history.sse)
     same = (a.centers - b.centers).abs().amax(dim=1) < 1e-2
