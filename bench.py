@@ -87,7 +87,7 @@ def calibrate_launch(model, rt, a) -> dict:
     ms/step."""
     from dalgo.parallel import comm, runtime
     if (a.algo not in ("ssgd", "gd") or model.device.type != "cuda" or not model._zg
-            or model.fused or model._graph_ok() or a.cal_steps <= 0):
+            or model._graph_ok() or a.cal_steps <= 0):
         return {}
     if comm.world_size() > 1 and model.bucket.xg is None:
         return {}   # the fused / persistent forms need the K11 exchange on several ranks

@@ -75,42 +75,16 @@ void check_lr_inputs(const Tensor& X, const Tensor& y, const Tensor& W, const Te
 void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& seg,
              int64_t row_offset, int64_t D, bool has_bias, double eps, int64_t seed, int64_t step,
              double frac, int64_t gx, int64_t rows_per_block, Tensor slab, Tensor gslab,
-             Tensor cnt1, Tensor cnt2, Tensor G, Tensor C, int64_t variant,
-             const std::optional<Tensor>& Wprev, int64_t upd_mode, int64_t upd_reg, double upd_eta,
-             double upd_lam, double upd_reg_alpha, const std::optional<Tensor>& count_acc,
+             Tensor cnt1, Tensor cnt2, Tensor G, Tensor C, int64_t flags,
+             const std::optional<Tensor>& count_acc,
              const std::optional<Tensor>& ticket, at::OptionalIntArrayRef xg_bufs, int64_t xg_rank,
              int64_t xg_slot, int64_t xg_epoch, const std::optional<Tensor>& xg_err,
              double xg_timeout, int64_t tail_mode, int64_t tail_reg, double tail_eta,
              double tail_lam, double tail_reg_alpha, const std::optional<Tensor>& tail_count_acc,
-             const std::optional<Tensor>& pool, int64_t pool_parity, int64_t nsteps,
-             const std::optional<Tensor>& epoch, int64_t epoch_base,
+             int64_t nsteps, const std::optional<Tensor>& epoch, int64_t epoch_base,
              const std::optional<Tensor>& perr, double spin_s,
-             const std::optional<Tensor>& step_dev, int64_t step_mul,
-             const std::optional<Tensor>& sel_list, const std::optional<Tensor>& sel_total,
-             int64_t sel_k, const std::optional<Tensor>& sel_claim) {
+             const std::optional<Tensor>& step_dev, int64_t step_mul) {
   check_lr_inputs(X, y, W, seg, D, has_bias);
-  DalgoLrSel sel{};
-  const DalgoLrSel* selp = nullptr;
-  if (sel_list.has_value()) {
-    TORCH_CHECK(sel_total.has_value() && sel_claim.has_value() && sel_k > 0 && sel_k < (1ll << 30),
-                "balanced slices: sel_total, sel_claim and sel_k > 0");
-    check_dev(*sel_list, "sel_list");
-    check_dev(*sel_total, "sel_total");
-    check_dev(*sel_claim, "sel_claim");
-    TORCH_CHECK(sel_list->scalar_type() == at::kInt && sel_list->is_contiguous() &&
-                sel_total->scalar_type() == at::kLong && sel_claim->scalar_type() == at::kInt,
-                "balanced slices: int32 list, int64 total, int32 claim");
-    TORCH_CHECK(W.size(0) == 1, "balanced slices: one segment");
-    // block b reads entries [b * sel_k, b * sel_k + sel_k) whatever the total, and the
-    // total is at most the shard's row count
-    TORCH_CHECK(sel_list->numel() >= std::max<int64_t>(gx * sel_k, X.size(0)),
-                "balanced slices: list shorter than max(gx * sel_k, rows)");
-    sel.list = sel_list->data_ptr<int>();
-    sel.total = sel_total->data_ptr<int64_t>();
-    sel.k = (int)sel_k;
-    sel.claim = reinterpret_cast<unsigned*>(sel_claim->data_ptr<int>());
-    selp = &sel;
-  }
   const int64_t* stepp = nullptr;
   if (step_dev.has_value()) {
     check_dev(*step_dev, "step_dev");
@@ -119,21 +93,13 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
     TORCH_CHECK(step_mul >= 0, "step_mul >= 0");
     stepp = step_dev->data_ptr<int64_t>();
   }
-  unsigned* poolp = nullptr;
-  if (pool.has_value()) {
-    check_dev(*pool, "pool");
-    TORCH_CHECK(pool->scalar_type() == at::kInt && pool->is_contiguous() &&
-                pool->numel() >= 2 * 64 * W.size(0), "pool: int32 [2 * 64 * n_seg] claim heads");
-    poolp = reinterpret_cast<unsigned*>(pool->data_ptr<int>());
-  }
   DalgoLrTail tail{};
   const DalgoLrTail* tailp = nullptr;
   TORCH_CHECK(nsteps <= 1 || ticket.has_value(), "persistent launch needs the fused tail");
   if (ticket.has_value()) {
     check_dev(*ticket, "ticket");
     TORCH_CHECK(ticket->scalar_type() == at::kInt && ticket->numel() >= 1, "ticket int32[1]");
-    TORCH_CHECK(W.size(0) == 1 && !Wprev.has_value() && (variant & 256),
-                "fused tail: one model, atomic epilogue, no prologue update");
+    TORCH_CHECK(W.size(0) == 1 && (flags & 256), "fused tail: one model, atomic epilogue");
     TORCH_CHECK(tail_mode == 0 || tail_mode == 1, "fused tail mode: 0 SSGD, 1 GD");
     tail.ticket = reinterpret_cast<unsigned*>(ticket->data_ptr<int>());
     tail.world = 1;
@@ -160,8 +126,7 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
       tail.count_acc = tail_count_acc->data_ptr<double>();
     }
     if (nsteps > 1) {
-      TORCH_CHECK(epoch.has_value() && perr.has_value() && !pool.has_value(),
-                  "persistent launch: epoch + perr counters, no work pool");
+      TORCH_CHECK(epoch.has_value() && perr.has_value(), "persistent launch: epoch + perr counters");
       check_dev(*epoch, "epoch");
       check_dev(*perr, "perr");
       TORCH_CHECK(epoch->scalar_type() == at::kInt && perr->scalar_type() == at::kInt,
@@ -175,14 +140,6 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
       tail.spin_s = spin_s;
     }
     tailp = &tail;
-  }
-  const float* wprev = nullptr;
-  if (Wprev.has_value()) {
-    check_f32(*Wprev, "Wprev");
-    TORCH_CHECK(W.size(0) == 1 && Wprev->numel() >= W.size(1), "fused update: one model, Wprev [1, ldw]");
-    TORCH_CHECK(Wprev->data_ptr() != W.data_ptr(), "fused update: Wprev and W must differ (ping-pong)");
-    TORCH_CHECK(upd_mode == 0 || upd_mode == 1, "fused update mode: 0 SSGD, 1 GD");
-    wprev = Wprev->data_ptr<float>();
   }
   double* cacc = nullptr;
   if (count_acc.has_value()) {
@@ -213,15 +170,14 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
                     (int)rows_per_block, slab.data_ptr<float>(), gslab.data_ptr<float>(),
                     reinterpret_cast<unsigned*>(cnt1.data_ptr<int>()),
                     reinterpret_cast<unsigned*>(cnt2.data_ptr<int>()), G.data_ptr<float>(),
-                    C.data_ptr<float>(), (int)S, (int)variant, wprev, (int)upd_mode, (int)upd_reg,
-                    (float)upd_eta, (float)upd_lam, (float)upd_reg_alpha, cacc, tailp, poolp,
-                    (int)(pool_parity & 1), stepp, step_mul, selp, cur_stream()),
+                    C.data_ptr<float>(), (int)S, (int)flags, cacc, tailp, stepp, step_mul,
+                    cur_stream()),
       "lr_grad");
 }
 
 void lr_eval(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& seg, int64_t D,
              bool has_bias, double eps, int64_t gx, int64_t rows_per_block, Tensor correct,
-             Tensor loss, int64_t variant) {
+             Tensor loss) {
   check_lr_inputs(X, y, W, seg, D, has_bias);
   const int64_t nseg = W.size(0);
   TORCH_CHECK(rows_per_block > 0 && rows_per_block % 4 == 0, "rows_per_block % 4");
@@ -235,7 +191,7 @@ void lr_eval(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
                     X.scalar_type() == at::kBFloat16 ? 1 : 0, (int)gx, (int)nseg,
                     (int)rows_per_block,
                     reinterpret_cast<unsigned long long*>(correct.data_ptr<int64_t>()),
-                    loss.data_ptr<float>(), (int)variant, cur_stream()),
+                    loss.data_ptr<float>(), cur_stream()),
       "lr_eval");
 }
 
@@ -351,42 +307,6 @@ void hbm_gather_rows(const Tensor& X, const Tensor& idx, Tensor out, int64_t gri
 }
 
 // diagnostics: per-wave K1 timeline (u64, 8 per wave) for the following lr_grad launches
-void lr_select(int64_t seed, int64_t step, double frac, int64_t row_offset, int64_t n, int64_t ch,
-               Tensor list, Tensor count) {
-  check_dev(list, "list");
-  check_dev(count, "count");
-  TORCH_CHECK(list.scalar_type() == at::kInt && count.scalar_type() == at::kInt, "int32 list/count");
-  TORCH_CHECK(ch > 0 && ch % 4 == 0 && ch < (1ll << 31), "chunk rows: positive multiple of 4");
-  const int64_t nch = (n + ch - 1) / ch;
-  TORCH_CHECK(list.numel() >= nch * ch && count.numel() >= nch, "list / count too small");
-  DeviceGuard guard(list.device());
-  DALGO_CHECK_HIP(dalgo_lr_select((uint64_t)seed, (uint64_t)step, frac_threshold(frac), row_offset, n,
-                                  (int)ch, (int)std::max<int64_t>(nch, 1), list.data_ptr<int>(),
-                                  count.data_ptr<int>(), cur_stream()),
-                  "lr_select");
-}
-
-
-void lr_select_compact(const Tensor& chunks, const Tensor& counts, int64_t ch, Tensor list,
-                       Tensor total, Tensor claim) {
-  check_dev(chunks, "chunks");
-  check_dev(counts, "counts");
-  check_dev(list, "list");
-  check_dev(total, "total");
-  check_dev(claim, "claim");
-  TORCH_CHECK(chunks.scalar_type() == at::kInt && counts.scalar_type() == at::kInt &&
-              list.scalar_type() == at::kInt && total.scalar_type() == at::kLong &&
-              claim.scalar_type() == at::kInt, "lr_select_compact: int32 / int64 total");
-  const int64_t nch = counts.numel();
-  TORCH_CHECK(ch > 0 && chunks.numel() >= nch * ch && list.numel() >= chunks.numel() && nch > 0,
-              "lr_select_compact: shapes");
-  DeviceGuard guard(list.device());
-  DALGO_CHECK_HIP(dalgo_lr_select_compact(chunks.data_ptr<int>(), counts.data_ptr<int>(), (int)ch,
-                                          (int)nch, list.data_ptr<int>(), total.data_ptr<int64_t>(),
-                                          reinterpret_cast<unsigned*>(claim.data_ptr<int>()),
-                                          cur_stream()),
-                  "lr_select_compact");
-}
 
 void lr_set_trace(const c10::optional<Tensor>& buf) {
   if (buf.has_value()) {
@@ -1203,17 +1123,15 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("lr_grad(Tensor X, Tensor y, Tensor(z!) W, Tensor seg, int row_offset, int D, bool has_bias, "
         "float eps, int seed, int step, float frac, int gx, int rows_per_block, Tensor(a!) slab, "
         "Tensor(b!) gslab, Tensor(c!) cnt1, Tensor(d!) cnt2, Tensor(e!) G, Tensor(f!) C, "
-        "int variant=3, Tensor? Wprev=None, int upd_mode=0, int upd_reg=0, float upd_eta=0., "
-        "float upd_lam=0., float upd_reg_alpha=0., Tensor(g!)? count_acc=None, "
+        "int flags=0, Tensor(g!)? count_acc=None, "
         "Tensor(h!)? ticket=None, int[]? xg_bufs=None, int xg_rank=0, int xg_slot=0, int xg_epoch=0, "
         "Tensor(i!)? xg_err=None, float xg_timeout=0., int tail_mode=0, int tail_reg=0, "
         "float tail_eta=0., float tail_lam=0., float tail_reg_alpha=0., "
-        "Tensor(j!)? tail_count_acc=None, Tensor(k!)? pool=None, int pool_parity=0, int nsteps=1, "
+        "Tensor(j!)? tail_count_acc=None, int nsteps=1, "
         "Tensor(l!)? epoch=None, int epoch_base=0, Tensor(m!)? perr=None, float spin_s=2., "
-        "Tensor? step_dev=None, int step_mul=1, Tensor? sel_list=None, Tensor? sel_total=None, "
-        "int sel_k=0, Tensor(n!)? sel_claim=None) -> ()");
+        "Tensor? step_dev=None, int step_mul=1) -> ()");
   m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
-        "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss, int variant=3) -> ()");
+        "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss) -> ()");
   m.def("sync_update(Tensor(a!) W, Tensor(d!)? G, Tensor(e!)? C, Tensor? center, Tensor? S, "
         "Tensor(b!)? Dl, Tensor(c!)? count_acc, int n, int mode, int reg, float eta, float lam, float alpha, "
         "float reg_alpha, float mu, float zeta, float beta, float inv_p, bool zero_grad=False) -> ()");
@@ -1286,17 +1204,11 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("lr_set_trace(Tensor? buf) -> ()", &lr_set_trace);
   m.def("hbm_gather_rows(Tensor X, Tensor idx, Tensor(a!) out, int grid=2048) -> ()");
   m.def("mc_pi(int seed, int stream, int offset, int n, Tensor(a!) count) -> ()");
-  m.def("lr_select(int seed, int step, float frac, int row_offset, int n, int ch, Tensor(a!) list, "
-        "Tensor(b!) count) -> ()");
-  m.def("lr_select_compact(Tensor chunks, Tensor counts, int ch, Tensor(a!) list, Tensor(b!) total, "
-        "Tensor(c!) claim) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("lr_grad", &lr_grad);
   m.impl("lr_eval", &lr_eval);
-  m.impl("lr_select", &lr_select);
-  m.impl("lr_select_compact", &lr_select_compact);
   m.impl("sync_update", &sync_update);
   m.impl("rows_sum", &rows_sum);
   m.impl("rows_broadcast", &rows_broadcast);

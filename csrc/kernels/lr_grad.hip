@@ -56,25 +56,9 @@ struct LrParams {
   // eval outputs
   unsigned long long* correct;  // [n_seg] (eval mode)
   float* loss;                  // [n_seg] sum of log-loss (eval mode)
-  // fused K8 update of the PREVIOUS step (SSGD / full-batch GD, one segment):
-  // w = upd(Wprev, Gprev, Cprev) is computed by every block for its own register
-  // fragment and written to W by block 0, so a training step is one kernel +
-  // one all-reduce (the separate update launch disappears).
-  const float* Wprev;   // nullptr: no fused update, use W as is
-  const float* Gprev;   // all-reduced gradient sum of the previous step (== G buffer)
-  const float* Cprev;
-  int upd_mode;         // 0 = SSGD (mean + reg), 1 = GD (sum)
-  int upd_reg;          // 0 none, 1 l2, 2 l1, 3 elastic net
-  float upd_eta, upd_lam, upd_reg_alpha;
   double* count_acc;    // optional: += local selected-row count of THIS step
   int atomic_out;       // 1: blocks add their partials to G/C with float atomics
                         //    (G/C zeroed by the caller; summation order not fixed)
-  int probe_no_epilogue;  // diagnostics only (variant bit 9): skip the block reduction
-  // cross-block work pool: rows past gx * rows_per_block of each segment are claimed
-  // in 128-row units from 8 shard heads (pool[(parity * n_seg + seg) * 8 + shard]);
-  // nullptr: the static block ranges cover everything
-  unsigned* pool;
-  int pool_parity;        // this launch uses set `parity` and re-arms the other one
   int fine_q;             // work claims switch from 256-row groups to 64-row quarters once
                           // fewer than fine_q quarters of the block are unclaimed (0 = never)
   int unit_shift;         // sampling: work units of 2^unit_shift rows (2..8; fine claims take one)
@@ -100,14 +84,6 @@ struct LrParams {
   uint32_t epoch_base;
   unsigned* perr;
   uint64_t spin_ticks;
-  // balanced slices (LIST instantiation): the step's selected local rows, compacted in
-  // ascending order (sel_list, *sel_total entries). Block b takes entries
-  // [b * sel_k, (b + 1) * sel_k) and every wave claims U of them at a time from LDS;
-  // entries past gx * sel_k are claimed in U-entry units from *sel_claim (zero on entry)
-  const int* sel_list;
-  const int64_t* sel_total;
-  int sel_k;
-  unsigned* sel_claim;
 };
 
 __device__ __forceinline__ void wt_store(float* a, float v) {
@@ -150,17 +126,6 @@ __device__ __forceinline__ void lr_tail(const LrParams& p, uint32_t xg_epoch) {
       __hip_atomic_fetch_add(p.tail_count_acc, (double)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-}
-
-__device__ __forceinline__ float fused_update(float w, float g, float c, const LrParams& p) {
-  if (p.upd_mode == 1) return w - p.upd_eta * g;
-  const float gm = c > 0.f ? g / c : 0.f;
-  float r = 0.f;
-  if (p.upd_reg == 1) r = w;
-  else if (p.upd_reg == 2) r = (w > 0.f) ? 1.f : (w < 0.f ? -1.f : 0.f);
-  else if (p.upd_reg == 3) r = p.upd_reg_alpha * ((w > 0.f) ? 1.f : (w < 0.f ? -1.f : 0.f)) +
-                               (1.f - p.upd_reg_alpha) * w;
-  return w - p.upd_eta * (gm + p.upd_lam * r);
 }
 
 constexpr int kGroup = 16;   // blocks per first-level reduction group
@@ -225,25 +190,21 @@ constexpr int kRing = 512;   // per-wave ring of selected local row indices
 
 // EVAL=false: gradient; EVAL=true: accuracy + log-loss over every row.
 // PIPE: software-pipelined (two register sets) vs. single-buffered sweep.
-// cross-block pool geometry (K1): 512-row units claimed per block, handed to the
-// block's waves as 64-row sub-units; unit claims run kPAhead sub-units ahead of use
-constexpr int kPU = 512, kPSub = 64, kPSubs = kPU / kPSub, kPAhead = 4, kPSlots = 8;
-constexpr int kPHeads = 64;                  // claim heads (shards) per segment; one per lane
-constexpr int64_t kPExh = (1ll << 40) - 1;   // "pool exhausted" marker
-
-// LEAN compiles out every path the default sampled launch never takes: the cross-block
-// pool, the fixed-order (deterministic) epilogue and claim map, the fused-update prologue
-// and the no-epilogue probe. Each launch starts from a cold instruction cache, and those
-// inlined paths sat between the executed instructions of the start-up path and the
-// refill loop: variant 8 without the pool alone measured 56.5 -> 53.5 us per 1.25M-row
-// step (profiles/round2/README.md). The launcher falls back to the full build when a
-// launch needs any of them.
+// LEAN compiles out the fixed-order (deterministic) epilogue and claim map, which the
+// default (atomic-epilogue) launch never takes. Each launch starts from a cold
+// instruction cache, and inlined paths that sit between the executed instructions of the
+// start-up path and the refill loop cost time: variant 8 without a cross-block work pool
+// measured 56.5 -> 53.5 us per 1.25M-row step (profiles/round2/README.md). The launcher
+// picks the full build only for deterministic launches.
+// Measured and removed (profiles/round2, profiles/round3): a cross-block work pool, a
+// fused previous-step update prologue (1.5-8 % slower than the separate 2-us update),
+// balanced slices of a precomputed compacted selection (2.7 us faster in K1, more lost
+// in the side-stream hand-off) and 11 other launch shapes.
 template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, bool PERSIST, int AUX = 0,
-          bool LEAN = false, bool LIST = false>
+          bool LEAN = false>
 __global__ void __launch_bounds__(NW * 64)
 lr_rows_kernel(const LrParams p) {
-  // the persistent form (fused tail, atomic epilogue, no pool / prologue: host checks)
-  // never takes those paths either
+  // the persistent form (fused tail, atomic epilogue: host checks) is lean as well
   constexpr bool kLean = LEAN || PERSIST;
   constexpr int VEC = VecTraits<T>::VEC;
   constexpr int COLS = NC * 64 * VEC;  // columns covered per lane-set
@@ -256,10 +217,6 @@ lr_rows_kernel(const LrParams p) {
   __shared__ int s_flag;
   __shared__ int s_next;   // next unclaimed work unit of this block (dynamic balancing)
   __shared__ int s_ok;     // persistent mode: the epoch wait succeeded
-  // block-level pool claims: next 64-row pool sub-unit to hand out, next pool unit to
-  // claim (block-local order), and the claimed units ((u + 1) << 40 | first global row)
-  __shared__ int s_pnext, s_pclaim;
-  __shared__ unsigned long long s_punit[kPSlots];
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -300,10 +257,9 @@ lr_rows_kernel(const LrParams p) {
   for (int it = 0; it < nst; ++it) {
   // the kernel argument block is never written (a modified copy would live in scratch)
   const uint64_t step_cur = step_base + (uint64_t)it;
-  // model fragment in registers (optionally applying the previous step's update).
-  // Fetched AFTER the first row batch is issued (see the sweep): the W / Wprev reads
-  // then overlap the first rows' HBM latency instead of preceding them, and the
-  // work-claim barrier below does not wait for them.
+  // model fragment in registers. Fetched AFTER the first row batch is issued (see the
+  // sweep): the W reads then overlap the first rows' HBM latency instead of preceding
+  // them, and the work-claim barrier below does not wait for them.
   float wr[NC][VEC];
   float wb = 0.f;
   // persistent mode: W was written by another CU in this launch -> agent-scope loads
@@ -314,7 +270,7 @@ lr_rows_kernel(const LrParams p) {
       return *a;
   };
   auto load_w = [&]() {
-    if (kLean || p.Wprev == nullptr) {
+    {
       const float* w = p.W + (int64_t)seg * p.ldw;
       // 16-B aligned model row (SSGD: one model): each lane's VEC contiguous weights
       // with VEC / 4 vector loads instead of VEC bounds-checked scalar ones (fewer
@@ -345,27 +301,6 @@ lr_rows_kernel(const LrParams p) {
           }
       }
       wb = p.has_bias ? ldw_(w + p.D) : 0.f;
-    } else {
-      const float cprev = p.Cprev[0];
-      float* wout = const_cast<float*>(p.W);
-      const bool writer = (bx == 0 && wid == 0);
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          int col = (c * 64 + lane) * VEC + e;
-          float v = 0.f;
-          if (col < p.D) {
-            v = fused_update(p.Wprev[col], p.Gprev[col], cprev, p);
-            if (writer) wout[col] = v;
-          }
-          wr[c][e] = v;
-        }
-      wb = 0.f;
-      if (p.has_bias) {
-        wb = fused_update(p.Wprev[p.D], p.Gprev[p.D], cprev, p);
-        if (writer && lane == 0) wout[p.D] = wb;
-      }
     }
   };
 
@@ -399,43 +334,8 @@ lr_rows_kernel(const LrParams p) {
   const bool small = nq < upg * NW + fine_u;
   const int w0 = small ? 1 : upg;
   if (threadIdx.x == 0) s_next = w0 * NW;   // units 0..w0 * NW - 1 are pre-assigned
-  // cross-block pool (segment rows past the static block ranges): 512-row units, claimed
-  // per BLOCK from 64 shard heads (shard s holds units s, s + 64, ...; the heads are only
-  // touched by agent-scope atomics, performed at memory side, and a block first tries its
-  // own shard, so few blocks share a head) and handed to the block's waves in 64-row
-  // sub-units through LDS. Block (0, 0) re-arms the other parity set, which the previous
-  // launch used and the next one will.
-  if (!kLean && p.pool != nullptr && bx == 0 && seg == 0)
-    for (int i = threadIdx.x; i < kPHeads * (int)gridDim.y; i += NW * 64)
-      __hip_atomic_store(p.pool + (int64_t)(p.pool_parity ^ 1) * gridDim.y * kPHeads + i, 0u,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (threadIdx.x < kPSlots) s_punit[threadIdx.x] = 0ull;
-  if (threadIdx.x == 0) { s_pnext = 0; s_pclaim = 0; }
-  // LIST: this block's slice of the compacted selection, staged in the (ring-free) arena.
-  // The entry loads do not wait for the total (the list buffer holds gx * sel_k entries
-  // whatever the total): entries past it are loaded but never used.
-  int* const sl = reinterpret_cast<int*>(s_arena);
-  int slen = 0;
-  int64_t sel_tot = 0;
-  if constexpr (LIST) {
-    const int64_t s0 = (int64_t)bx * p.sel_k;
-    const int nst_ = min(p.sel_k, ARENA);
-    for (int i = threadIdx.x; i < nst_; i += NW * 64) sl[i] = p.sel_list[s0 + i];
-    sel_tot = *p.sel_total;
-    slen = (int)max((int64_t)0, min((int64_t)p.sel_k, sel_tot - s0));
-    if (threadIdx.x == 0) s_next = 0;
-  }
   __syncthreads();
   const unsigned long long t_bar = tr ? (unsigned long long)__builtin_amdgcn_s_memrealtime() : 0ull;
-  const int64_t psl = seg_lo + (int64_t)gx * p.rows_per_block;   // pool start (local row)
-  const bool has_pool = !kLean && p.pool != nullptr && psl < seg_hi;
-  unsigned* const heads =
-      has_pool ? p.pool + ((int64_t)p.pool_parity * gridDim.y + seg) * kPHeads : nullptr;
-  const int64_t psg = p.row_offset + psl, psa = psg & ~(int64_t)3, sghi = p.row_offset + seg_hi;
-  const int nj = has_pool ? (int)((sghi - psa + kPU - 1) / kPU) : 0;
-  auto shard_size = [&](int s) { return nj > s ? (nj - s + kPHeads - 1) / kPHeads : 0; };
-  int pshard = bx & (kPHeads - 1);
-  bool in_pool = false, pool_done = false, pool_err = false;
 
   int64_t gnext = gstart + ((int64_t)(wid * w0) << qs);
   int64_t ulo = glo;                       // current work unit: rows [max(gnext, ulo), uhi)
@@ -443,95 +343,8 @@ lr_rows_kernel(const LrParams p) {
   bool more = gnext < ghi;
   int sclaim = w0 * (NW + wid);            // next unit of this wave in the fixed map
 
-  // claim one pool unit for the block (blocking for this wave only) and publish it
-  auto claim_unit = [&](int u) {
-    int64_t start = kPExh;
-    int k = 0;
-    if (lane == 0) k = (int)atomicAdd(&heads[pshard], 1u);
-    k = __builtin_amdgcn_readfirstlane(k);
-    for (int tries = 0;; ++tries) {
-      if (k < shard_size(pshard)) {
-        start = psa + (int64_t)(pshard + kPHeads * k) * kPU;
-        break;
-      }
-      // this shard is exhausted: read every head (plain agent-scope loads, one per lane:
-      // no read-modify-write traffic on the shared heads) and move to a shard with
-      // unclaimed units, the first one at or after a per-block rotation
-      const unsigned hv = __hip_atomic_load(&heads[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t m = __ballot((int)hv < shard_size(lane));
-      if (m == 0ull) break;                        // every unit has been claimed
-      if (tries > (1 << 16)) { pool_err = true; break; }   // never expected
-      const int rot = (bx * 7 + u) & (kPHeads - 1);
-      const uint64_t mr = (m >> rot) | (rot ? m << (64 - rot) : 0ull);
-      pshard = (rot + (int)__builtin_ctzll(mr)) & (kPHeads - 1);
-      int kk = 0;
-      if (lane == 0) kk = (int)atomicAdd(&heads[pshard], 1u);
-      k = __builtin_amdgcn_readfirstlane(kk);
-    }
-    if (lane == 0)
-      __hip_atomic_store(&s_punit[u % kPSlots], ((unsigned long long)(u + 1) << 40) | (unsigned long long)start,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
-  // published tag of pool unit u's slot (u + 1 once unit u is published)
-  auto slot_tag = [&](int u) -> int {
-    const unsigned long long raw =
-        __hip_atomic_load(&s_punit[u % kPSlots], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return __builtin_amdgcn_readfirstlane((int)(uint32_t)(raw >> 40));
-  };
-  // claim pool units up to u, one at a time and in order: unit c is only claimed once
-  // unit c - 1 is published, so "exhausted" at unit c implies it for every later unit
-  // (a wave that sees it may stop). Returns early while another wave's claim is in flight.
-  auto ensure_claimed = [&](int u) {
-    while (true) {
-      const int c = __builtin_amdgcn_readfirstlane(
-          __hip_atomic_load(&s_pclaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-      if (c > u) return;
-      if (c > 0 && slot_tag(c - 1) != c) return;     // unit c - 1 not published yet
-      int won = 0;
-      if (lane == 0) won = atomicCAS(&s_pclaim, c, c + 1) == c;
-      if (__builtin_amdgcn_readfirstlane(won)) claim_unit(c);
-    }
-  };
-  // next 64-row pool sub-unit of the block (claims run kPAhead sub-units ahead)
-  auto pool_draw = [&]() {
-    while (true) {
-      if (!has_pool || pool_done) { more = false; return; }
-      int j = 0;
-      if (lane == 0) j = atomicAdd(&s_pnext, 1);
-      j = __builtin_amdgcn_readfirstlane(j);
-      const int u = j / kPSubs, sub = j % kPSubs;
-      ensure_claimed((j + kPAhead) / kPSubs);
-      unsigned long long v = 0ull;
-      for (int spin = 0;; ++spin) {
-        const unsigned long long raw =
-            __hip_atomic_load(&s_punit[u % kPSlots], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        // (readfirstlane returns int: widen through uint32_t, never sign-extend)
-        v = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(raw >> 32)) << 32) |
-            (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)raw);
-        const unsigned long long tag = v >> 40;
-        if (tag == (unsigned long long)(u + 1)) break;
-        if (tag > (unsigned long long)(u + 1) || spin > (1 << 20)) {   // never expected
-          pool_err = true;
-          v = kPExh;
-          break;
-        }
-        ensure_claimed(u);   // the claim of unit u may be waiting for this wave
-        __builtin_amdgcn_s_sleep(1);
-      }
-      const int64_t start = (int64_t)(v & ((1ull << 40) - 1));
-      if (start == kPExh) { pool_done = true; more = false; return; }
-      gnext = start + (int64_t)sub * kPSub;
-      ulo = psg;
-      uhi = min(sghi, gnext + kPSub);
-      if (gnext < uhi) { more = true; return; }
-      // an empty sub-unit past the segment end: draw again
-    }
-  };
-  if (!more) { in_pool = true; pool_draw(); }
-
   // ---- K7: Bernoulli selection of the next work unit, compacted into the ring
   auto refill = [&]() {
-    if constexpr (LIST) return;
     while ((tail - head) < (uint32_t)(2 * U) && more) {
       const int64_t r0 = gnext + 4 * lane;
       u32x4 h{0u, 0u, 0u, 0u};
@@ -549,7 +362,7 @@ lr_rows_kernel(const LrParams p) {
       }
       // claim the next unit dynamically: waves that drew few selected rows
       // take more units, so the block's waves finish together
-      if (!in_pool) {
+      {
         int gi = 0, w = w0;
         if (!kLean && !p.atomic_out) {
           // fixed-order epilogue: a fixed group -> wave map (wave w takes groups
@@ -567,56 +380,17 @@ lr_rows_kernel(const LrParams p) {
         if (gi < nq) {
           gnext = gstart + ((int64_t)gi << qs);
           uhi = min(ghi, gnext + ((int64_t)w << qs));
-          // the block's last static unit: have the first pool unit claimed now, so
-          // it is back before it is needed
-          if (has_pool && gi + w >= nq) ensure_claimed(0);
         } else {
-          in_pool = true;
+          more = false;
         }
       }
-      if (in_pool) pool_draw();
     }
     __builtin_amdgcn_wave_barrier();
   };
 
-  bool sel_pool_done = false;
   auto take_and_load = [&](Batch<NC, U>& b) {
     int64_t r[U];
-    if constexpr (LIST) {
-      int j0 = 0;
-      if (lane == 0) j0 = atomicAdd(&s_next, U);
-      j0 = __builtin_amdgcn_readfirstlane(j0);
-      if (j0 < slen) {
-        b.n = min(U, slen - j0);
-        const int last = b.n - 1;
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-          const int j = j0 + min(k, last);
-          r[k] = __builtin_amdgcn_readfirstlane(j < ARENA ? sl[j] : p.sel_list[(int64_t)bx * p.sel_k + j]);
-          r[k] = min(max(r[k], seg_lo), seg_hi - 1);   // a bad list cannot leave the shard
-        }
-      } else {
-        // entries past gx * sel_k: claimed from the launch-wide counter
-        const int64_t pbase = (int64_t)gx * p.sel_k;
-        b.n = 0;
-        if (!sel_pool_done && sel_tot > pbase) {
-          unsigned e = 0;
-          if (lane == 0) e = atomicAdd(p.sel_claim, (unsigned)U);
-          const int64_t e0 = pbase + (int64_t)__builtin_amdgcn_readfirstlane(e);
-          b.n = (int)max((int64_t)0, min((int64_t)U, sel_tot - e0));
-          if (b.n < U) sel_pool_done = true;
-          const int last = max(b.n - 1, 0);
-#pragma unroll
-          for (int k = 0; k < U; ++k)
-            r[k] = b.n ? min(max((int64_t)__builtin_amdgcn_readfirstlane(p.sel_list[e0 + min(k, last)]),
-                                 seg_lo), seg_hi - 1)
-                       : seg_lo;
-        }
-        if (b.n == 0) { sel_pool_done = true; return; }
-      }
-#pragma unroll
-      for (int k = 0; k < U; ++k) b.v[k] = (k < b.n) ? 1.f : 0.f;
-    } else {
+    {
     const uint32_t avail = tail - head;
     b.n = (int)min(avail, (uint32_t)U);
     if (b.n == 0) return;
@@ -748,7 +522,6 @@ lr_rows_kernel(const LrParams p) {
       compute(A);
     }
   }
-  if (pool_err) cntf = __builtin_nanf("");   // a pool hand-off failed: poison the count
   if (tr && lane == 0) {
     tr[0] = t_start;
     tr[1] = t_first;
@@ -759,10 +532,6 @@ lr_rows_kernel(const LrParams p) {
     tr[7] = t_refill;
   }
   __syncthreads();   // rings are dead: the arena becomes the reduction buffer
-  if (!kLean && p.probe_no_epilogue) {
-    if (threadIdx.x == 0 && cntf < 0.f) p.C[0] = cntf + gb;   // keep the sweep live
-    continue;
-  }
 
   if constexpr (EVAL) {
     __shared__ float s_ev[NW][2];
@@ -892,89 +661,11 @@ lr_rows_kernel(const LrParams p) {
   }  // step loop
 }
 
-// K7 standalone: the compacted Bernoulli selection of one step, per chunk. Chunk c holds
-// local rows [c * ch, min(n, (c + 1) * ch)); its selected rows (ascending, the same
-// draw as K1's in-register sampling: philox(seed, step, global_row >> 2)[global_row & 3]
-// < thr) go to list[c * ch ...] and their number to count[c].
-__global__ void __launch_bounds__(256) lr_select_kernel(uint64_t seed, uint64_t step, uint32_t thr,
-                                                        int64_t row_offset, int64_t n, int ch,
-                                                        int* list, int* count) {
-  __shared__ int s_w[4];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t lo = (int64_t)blockIdx.x * ch, hi = min(n, lo + ch);
-  const int64_t g_lo = row_offset + lo, g_hi = row_offset + hi;
-  const int64_t q_lo = g_lo >> 2, q_hi = (g_hi + 3) >> 2;
-  int base = 0;
-  for (int64_t q0 = q_lo; q0 < q_hi; q0 += 256) {
-    const int64_t q = q0 + threadIdx.x;
-    unsigned m = 0;
-    if (q < q_hi) {
-      const u32x4 h = philox_block(seed, step, (uint64_t)q);
-      const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t gr = 4 * q + j;
-        if (gr >= g_lo && gr < g_hi && hv[j] < thr) m |= 1u << j;
-      }
-    }
-    const int cnt = __popc(m);
-    int incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int v = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += v;
-    }
-    if (lane == 63) s_w[wid] = incl;
-    __syncthreads();
-    int woff = 0, btot = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const int v = s_w[w];
-      woff += (w < wid) ? v : 0;
-      btot += v;
-    }
-    int pos = base + woff + incl - cnt;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if ((m >> j) & 1u) list[lo + pos++] = (int)(4 * q + j - row_offset);
-    base += btot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) count[blockIdx.x] = base;
-}
-
-// K7 second pass: chunk c's list moves to its place in the step's compacted list (the
-// exclusive prefix of the chunk counts, summed by the block itself: chunks are few);
-// block 0 writes the total and zeroes the overflow claim counter of the K1 launch.
-__global__ void __launch_bounds__(256) lr_select_compact_kernel(const int* chunks, const int* counts,
-                                                                int ch, int* list, int64_t* total,
-                                                                unsigned* claim) {
-  __shared__ int s_w[4];
-  const int c = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int lim = (c == 0) ? (int)gridDim.x : c;   // block 0 sums every chunk (the total)
-  int v = 0;
-  for (int i = threadIdx.x; i < lim; i += 256) v += counts[i];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if (lane == 0) s_w[wid] = v;
-  __syncthreads();
-  const int pre = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-  if (c == 0) {
-    if (threadIdx.x == 0) { *total = pre; *claim = 0u; }
-    for (int i = threadIdx.x; i < counts[0]; i += 256) list[i] = chunks[i];
-    return;
-  }
-  const int n = counts[c];
-  const int* src = chunks + (int64_t)c * ch;
-  for (int i = threadIdx.x; i < n; i += 256) list[pre + i] = src[i];
-}
-
 }  // namespace dalgo
 
 using namespace dalgo;
 
-template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, int AUX = 0, bool LEAN = false,
-          bool LIST = false>
+template <typename T, int NC, bool EVAL, int NW, bool PIPE, int U, int AUX = 0, bool LEAN = false>
 static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st) {
   dim3 grid(gx, nseg), block(NW * 64);
   if (p.nsteps > 1) {
@@ -982,83 +673,47 @@ static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st)
       // persistent mode: every block must be resident (blocks wait on each other);
       // the cooperative launch refuses a grid that cannot be
       void* args[] = {const_cast<LrParams*>(&p)};
-      return hipLaunchCooperativeKernel((const void*)lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, true>,
+      return hipLaunchCooperativeKernel((const void*)lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, true, AUX>,
                                         grid, block, args, 0, st);
     }
     return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL((lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, false, AUX, LEAN, LIST>), grid, block, 0, st, p);
+  hipLaunchKernelGGL((lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, false, AUX, LEAN>), grid, block, 0, st, p);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
 
-// variants (launch shape x sweep structure), A/B-tested in bench/lr_kernel_sweep.py:
-//   0: 4 waves, single set, 4-row batches   1: 4 waves, pipelined (2 sets)
-//   2: 8 waves, single set                  3: 8 waves, pipelined
-//   4: 4 waves, 8-row batches               5: 8 waves, 8-row batches
-//   6: 12 waves, pipelined (3 waves/SIMD)   7: 16 waves, single set (4 waves/SIMD)
-//   8: = 3 with nt row loads   9: = 5 with nt   10: = 3 with sc0|nt   11: = 3 with sc0|sc1
-//   (8 runs a LEAN build when the launch needs no pool, deterministic epilogue, fused
-//   update prologue or probe, else the full build; 12 = 8 always in the full build)
+// Launch shape (A/B-tested in bench/lr_kernel_sweep.py, profiles/round1-2): 8 waves per
+// block, 4-row batches, non-temporal row loads (buffer-load aux bit 2); two register sets
+// (row loads of batch i+1 in flight while batch i is computed) while the model fragment
+// fits (<= 2 column chunks per lane), one set at 4 chunks. The atomic epilogue runs the
+// LEAN build, the deterministic fixed-order epilogue the full one.
 template <typename T, int NC, bool EVAL>
-static hipError_t launch_variant(const LrParams& p, int gx, int nseg, int variant, hipStream_t st) {
-  if constexpr (NC >= 4) {   // register budget: one 4-row set at 4 chunks/lane
-    if constexpr (!EVAL) {
-      if (variant == 8 && p.pool == nullptr && p.atomic_out && p.Wprev == nullptr &&
-          !p.probe_no_epilogue)
-        return launch_lr<T, NC, EVAL, 8, false, 4, 2, true>(p, gx, nseg, st);
-    }
-    if (variant == 8 || variant == 9) return launch_lr<T, NC, EVAL, 8, false, 4, 2>(p, gx, nseg, st);
-    return (variant == 2 || variant == 3 || variant == 5)
-               ? launch_lr<T, NC, EVAL, 8, false, 4>(p, gx, nseg, st)
-               : launch_lr<T, NC, EVAL, 4, false, 4>(p, gx, nseg, st);
-  } else {
-    switch (variant) {
-      case 0: return launch_lr<T, NC, EVAL, 4, false, 4>(p, gx, nseg, st);
-      case 1: return launch_lr<T, NC, EVAL, 4, true, 4>(p, gx, nseg, st);
-      case 2: return launch_lr<T, NC, EVAL, 8, false, 4>(p, gx, nseg, st);
-      case 3: return launch_lr<T, NC, EVAL, 8, true, 4>(p, gx, nseg, st);
-      case 4: return launch_lr<T, NC, EVAL, 4, false, 8>(p, gx, nseg, st);
-      case 5: return launch_lr<T, NC, EVAL, 8, false, 8>(p, gx, nseg, st);
-      case 6: return launch_lr<T, NC, EVAL, 12, true, 4>(p, gx, nseg, st);
-      case 7: return launch_lr<T, NC, EVAL, 16, false, 4>(p, gx, nseg, st);
-      // X-row cache policy (aux bits of the buffer load: 2 = nt, 1 = sc0, 16 = sc1)
-      case 8:
-        if constexpr (!EVAL) {
-          if (p.pool == nullptr && p.atomic_out && p.Wprev == nullptr && !p.probe_no_epilogue) {
-            if (p.sel_list != nullptr)
-              return launch_lr<T, NC, EVAL, 8, true, 4, 2, true, true>(p, gx, nseg, st);
-            return launch_lr<T, NC, EVAL, 8, true, 4, 2, true>(p, gx, nseg, st);
-          }
-        }
-        return launch_lr<T, NC, EVAL, 8, true, 4, 2, false>(p, gx, nseg, st);
-      case 12: return launch_lr<T, NC, EVAL, 8, true, 4, 2, false>(p, gx, nseg, st);   // 8, full build
-      case 9: return launch_lr<T, NC, EVAL, 8, false, 8, 2>(p, gx, nseg, st);
-      case 10: return launch_lr<T, NC, EVAL, 8, true, 4, 3>(p, gx, nseg, st);
-      case 11: return launch_lr<T, NC, EVAL, 8, true, 4, 17>(p, gx, nseg, st);
-      default: return hipErrorInvalidValue;
-    }
+static hipError_t launch_shape(const LrParams& p, int gx, int nseg, hipStream_t st) {
+  constexpr bool kPipe = NC < 4;   // register budget: one 4-row set at 4 chunks/lane
+  if constexpr (!EVAL) {
+    if (p.atomic_out) return launch_lr<T, NC, EVAL, 8, kPipe, 4, 2, true>(p, gx, nseg, st);
   }
+  return launch_lr<T, NC, EVAL, 8, kPipe, 4, 2, false>(p, gx, nseg, st);
 }
 
 template <bool EVAL>
-static hipError_t dispatch_lr(const LrParams& p, int is_bf16, int gx, int nseg, int variant,
-                              hipStream_t st) {
+static hipError_t dispatch_lr(const LrParams& p, int is_bf16, int gx, int nseg, hipStream_t st) {
   const int vec = is_bf16 ? 8 : 4;
   const int64_t nchunks = p.ld / vec;
   const int nc = (int)cdiv(nchunks, 64);
   if (is_bf16) {
     switch (nc) {
-      case 1: return launch_variant<uint16_t, 1, EVAL>(p, gx, nseg, variant, st);
-      case 2: return launch_variant<uint16_t, 2, EVAL>(p, gx, nseg, variant, st);
-      case 3: case 4: return launch_variant<uint16_t, 4, EVAL>(p, gx, nseg, variant, st);
+      case 1: return launch_shape<uint16_t, 1, EVAL>(p, gx, nseg, st);
+      case 2: return launch_shape<uint16_t, 2, EVAL>(p, gx, nseg, st);
+      case 3: case 4: return launch_shape<uint16_t, 4, EVAL>(p, gx, nseg, st);
       default: return hipErrorInvalidValue;
     }
   } else {
     switch (nc) {
-      case 1: return launch_variant<float, 1, EVAL>(p, gx, nseg, variant, st);
-      case 2: return launch_variant<float, 2, EVAL>(p, gx, nseg, variant, st);
-      case 3: case 4: return launch_variant<float, 4, EVAL>(p, gx, nseg, variant, st);
+      case 1: return launch_shape<float, 1, EVAL>(p, gx, nseg, st);
+      case 2: return launch_shape<float, 2, EVAL>(p, gx, nseg, st);
+      case 3: case 4: return launch_shape<float, 4, EVAL>(p, gx, nseg, st);
       default: return hipErrorInvalidValue;
     }
   }
@@ -1075,20 +730,20 @@ void dalgo_lr_set_trace(void* buf) { g_lr_trace = static_cast<unsigned long long
 // Maximum supported row stride: 4 chunks/lane -> 2048 bf16 or 1024 f32 columns.
 int dalgo_lr_max_cols(int is_bf16) { return is_bf16 ? 2048 : 1024; }
 
+// flags: bit 8 = atomic epilogue; bits 16..23 = fine-claim threshold (64-row quarters of
+// the block's groups); bits 24..27 = log2 rows per sampled work unit (0 = 6)
 hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const int64_t* seg,
                          int64_t ld, int64_t row_offset, int D, int ldw, int has_bias, float eps,
                          uint64_t seed, uint64_t step, uint32_t thr, int full, int is_bf16,
                          int gx, int nseg, int rows_per_block, float* slab, float* gslab,
-                         unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int variant,
-                         const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
-                         float upd_reg_alpha, double* count_acc, const DalgoLrTail* tail,
-                         unsigned* pool, int pool_parity, const int64_t* step_dev,
-                         int64_t step_mul, const DalgoLrSel* sel, hipStream_t st) {
+                         unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int flags,
+                         double* count_acc, const DalgoLrTail* tail, const int64_t* step_dev,
+                         int64_t step_mul, hipStream_t st) {
   LrParams p{};
   p.step_dev = step_dev;
   p.step_mul = step_mul;
   if (tail != nullptr) {
-    if (nseg != 1 || !((variant >> 8) & 1) || Wprev != nullptr || tail->ticket == nullptr ||
+    if (nseg != 1 || !((flags >> 8) & 1) || tail->ticket == nullptr ||
         tail->world < 1 || tail->world > kXgMaxRanks || tail->rank < 0 || tail->rank >= tail->world ||
         (tail->world > 1 && (tail->epoch == 0 || tail->slot < ldw + 1)))
       return hipErrorInvalidValue;
@@ -1103,9 +758,7 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
     p.tu = XgUpdate{tail->mode, tail->reg, tail->eta, tail->lam, tail->reg_alpha};
     p.tail_count_acc = tail->count_acc;
     if (tail->nsteps > 1) {
-      if (tail->epoch_ctr == nullptr || tail->perr == nullptr || pool != nullptr ||
-          ((variant >> 9) & 1))
-        return hipErrorInvalidValue;
+      if (tail->epoch_ctr == nullptr || tail->perr == nullptr) return hipErrorInvalidValue;
       p.nsteps = tail->nsteps;
       p.epoch = tail->epoch_ctr;
       p.epoch_base = tail->epoch_base;
@@ -1113,61 +766,28 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
       p.spin_ticks = (uint64_t)(tail->spin_s * 1e8);
     }
   }
-  p.Wprev = Wprev; p.Gprev = G; p.Cprev = C; p.upd_mode = upd_mode; p.upd_reg = upd_reg;
-  p.upd_eta = upd_eta; p.upd_lam = upd_lam; p.upd_reg_alpha = upd_reg_alpha;
   p.count_acc = count_acc;
   p.X = X; p.y = y; p.W = W; p.seg = seg; p.ld = ld; p.row_offset = row_offset; p.D = D;
   p.ldw = ldw; p.has_bias = has_bias; p.eps = eps; p.seed = seed; p.step = step; p.thr = thr;
   p.full = full; p.rows_per_block = rows_per_block; p.slab = slab; p.gslab = gslab;
   p.cnt1 = cnt1; p.cnt2 = cnt2; p.G = G; p.C = C; p.S = S;
-  p.atomic_out = (variant >> 8) & 1;   // bit 8 of the variant selects the atomic epilogue
-  p.probe_no_epilogue = (variant >> 9) & 1;
-  p.fine_q = 4 * ((variant >> 16) & 0xff);   // bits 16..23: fine-claim threshold in groups
-  // bits 24..27: log2 rows per work unit when sampling (0 = 6: 64-row units)
-  p.unit_shift = ((variant >> 24) & 0xf) ? ((variant >> 24) & 0xf) : 6;
+  p.atomic_out = (flags >> 8) & 1;
+  p.fine_q = 4 * ((flags >> 16) & 0xff);
+  p.unit_shift = ((flags >> 24) & 0xf) ? ((flags >> 24) & 0xf) : 6;
   if (p.unit_shift < 2 || p.unit_shift > 8) return hipErrorInvalidValue;
   p.trace = g_lr_trace;
-  if (sel != nullptr) {
-    // only the lean variant-8 build has the LIST form (launch_variant)
-    if (nseg != 1 || full || step_dev != nullptr || p.nsteps > 1 || sel->k <= 0 ||
-        sel->list == nullptr || sel->total == nullptr || sel->claim == nullptr ||
-        (variant & 0xff) != 8 || pool != nullptr || Wprev != nullptr || !((variant >> 8) & 1) ||
-        ((variant >> 9) & 1))
-      return hipErrorInvalidValue;
-    p.sel_list = sel->list; p.sel_total = sel->total; p.sel_k = sel->k; p.sel_claim = sel->claim;
-  }
-  p.pool = pool;
-  p.pool_parity = pool_parity & 1;
-  return dispatch_lr<false>(p, is_bf16, gx, nseg, variant & 0xff, st);
-}
-
-hipError_t dalgo_lr_select(uint64_t seed, uint64_t step, uint32_t thr, int64_t row_offset,
-                           int64_t n, int ch, int nchunks, int* list, int* count, hipStream_t st) {
-  if (ch <= 0 || nchunks <= 0 || (int64_t)ch * nchunks < n) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(lr_select_kernel, dim3(nchunks), dim3(256), 0, st, seed, step, thr, row_offset,
-                     n, ch, list, count);
-  DALGO_LAUNCH_CHECK();
-  return hipSuccess;
-}
-
-hipError_t dalgo_lr_select_compact(const int* chunks, const int* counts, int ch, int nchunks,
-                                   int* list, int64_t* total, unsigned* claim, hipStream_t st) {
-  if (ch <= 0 || nchunks <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(lr_select_compact_kernel, dim3(nchunks), dim3(256), 0, st, chunks, counts, ch,
-                     list, total, claim);
-  DALGO_LAUNCH_CHECK();
-  return hipSuccess;
+  return dispatch_lr<false>(p, is_bf16, gx, nseg, st);
 }
 
 hipError_t dalgo_lr_eval(const void* X, const float* y, const float* W, const int64_t* seg,
                          int64_t ld, int D, int ldw, int has_bias, float eps, int is_bf16, int gx,
                          int nseg, int rows_per_block, unsigned long long* correct, float* loss,
-                         int variant, hipStream_t st) {
+                         hipStream_t st) {
   LrParams p{};
   p.X = X; p.y = y; p.W = W; p.seg = seg; p.ld = ld; p.row_offset = 0; p.D = D; p.ldw = ldw;
   p.has_bias = has_bias; p.eps = eps; p.full = 1; p.rows_per_block = rows_per_block;
   p.correct = correct; p.loss = loss;
-  return dispatch_lr<true>(p, is_bf16, gx, nseg, variant, st);
+  return dispatch_lr<true>(p, is_bf16, gx, nseg, st);
 }
 
 }  // extern "C"

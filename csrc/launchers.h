@@ -25,38 +25,22 @@ struct DalgoLrTail {
   double spin_s;
 };
 
-// Balanced slices of a sampled one-segment launch (K1 LIST build, lr_grad.hip): the
-// step's compacted selected local rows (list[0 .. *total)), sel_k per block, the rest
-// claimed from *claim (zero on entry)
-struct DalgoLrSel {
-  const int* list;
-  const int64_t* total;
-  int k;
-  unsigned* claim;
-};
-
 extern "C" {
 
 // ---- K1/K7/K10 logistic regression (lr_grad.hip)
 int dalgo_lr_max_cols(int is_bf16);
 void dalgo_lr_set_trace(void* buf);
-hipError_t dalgo_lr_select(uint64_t seed, uint64_t step, uint32_t thr, int64_t row_offset,
-                           int64_t n, int ch, int nchunks, int* list, int* count, hipStream_t st);
-hipError_t dalgo_lr_select_compact(const int* chunks, const int* counts, int ch, int nchunks,
-                                   int* list, int64_t* total, unsigned* claim, hipStream_t st);
 hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const int64_t* seg,
                          int64_t ld, int64_t row_offset, int D, int ldw, int has_bias, float eps,
                          uint64_t seed, uint64_t step, uint32_t thr, int full, int is_bf16,
                          int gx, int nseg, int rows_per_block, float* slab, float* gslab,
-                         unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int variant,
-                         const float* Wprev, int upd_mode, int upd_reg, float upd_eta, float upd_lam,
-                         float upd_reg_alpha, double* count_acc, const DalgoLrTail* tail,
-                         unsigned* pool, int pool_parity, const int64_t* step_dev,
-                         int64_t step_mul, const DalgoLrSel* sel, hipStream_t st);
+                         unsigned* cnt1, unsigned* cnt2, float* G, float* C, int S, int flags,
+                         double* count_acc, const DalgoLrTail* tail, const int64_t* step_dev,
+                         int64_t step_mul, hipStream_t st);
 hipError_t dalgo_lr_eval(const void* X, const float* y, const float* W, const int64_t* seg,
                          int64_t ld, int D, int ldw, int has_bias, float eps, int is_bf16, int gx,
                          int nseg, int rows_per_block, unsigned long long* correct, float* loss,
-                         int variant, hipStream_t st);
+                         hipStream_t st);
 
 // ---- K8 sync/update rules (sync_update.hip)
 hipError_t dalgo_sync_update(float* W, float* G, float* C, const float* center,

@@ -149,21 +149,10 @@ class ParallelSGD:
         # optional f64 device accumulator of minibatch sizes (bench accounting);
         # read it through global_sample_count()
         self.count_acc: torch.Tensor | None = None
-        # Optional (DALGO_FUSED_UPDATE=1): fuse the K8 update into the next step's
-        # gradient kernel (ping-pong model buffers); self._pending = G/C hold an
-        # update not yet applied to self.w (applied lazily by _flush()). Measured on
-        # MI355X it is ~1.5% (10M rows) to ~8% (1.25M rows) SLOWER than the separate
-        # 2-us update launch, which overlaps the previous kernel's tail, while the
-        # fused prologue lengthens every block's start-up path — so it is off by default.
-        self.fused = (dev.type == "cuda" and algo in ("ssgd", "gd")
-                      and os.environ.get("DALGO_FUSED_UPDATE", "0") == "1")
-        self._pending = False
         # G/C are zero (fresh, or left zeroed by the last gradient-consuming K8), so the
         # next atomic-epilogue K1 can accumulate into them without a memset launch
         self._g_zero = True
         self._zg = not lr_ops.DETERMINISTIC   # deterministic K1 overwrites G: no need to clear
-        if self.fused:
-            self.w_next = torch.empty_like(self.w)
         # hipGraph replay state (see _graph_ok): None = follow DALGO_GRAPH
         self.graph: bool | None = None
         self._graphs: dict = {}
@@ -213,7 +202,7 @@ class ParallelSGD:
         epilogue, one rank or K11 peers. K steps run as ONE cooperative K1 grid whose tail
         block releases each step's model (csrc/kernels/lr_grad.hip, nsteps)."""
         if getattr(self, "_okp", None) is None:
-            self._okp = (self.device.type == "cuda" and self._zg and not self.fused
+            self._okp = (self.device.type == "cuda" and self._zg
                          and self.cfg.algo in ("ssgd", "gd")
                          and os.environ.get("DALGO_PERSISTENT", "0") == "1"
                          and (comm.world_size() == 1 or self.bucket.xg is not None))
@@ -241,17 +230,6 @@ class ParallelSGD:
         self._g_zero = True
         self.t += k
 
-    def _flush(self):
-        """Apply a pending fused update to self.w (end of training / before reads)."""
-        if self._pending:
-            c = self.cfg
-            if c.algo == "ssgd":
-                U.sync_update(self.w, U.SSGD, G=self.G, C=self.C, reg=c.reg, eta=c.eta,
-                              lam=c.lam, reg_alpha=c.reg_alpha)
-            else:
-                U.sync_update(self.w, U.GD_SUM, G=self.G, C=self.C, eta=c.eta)
-            self._pending = False
-
     def global_sample_count(self) -> float:
         """Total minibatch rows accumulated in count_acc, summed over ranks (exact, counted
         on the device). SSGD / GD count the all-reduced minibatch once per step; MA / BMUF
@@ -260,7 +238,7 @@ class ParallelSGD:
         if self.count_acc is None:
             return 0.0
         cnt = self.count_acc.clone()
-        if self.fused or self.cfg.algo in ("ma", "bmuf", "easgd"):
+        if self.cfg.algo in ("ma", "bmuf", "easgd"):
             comm.all_reduce_sum(cnt)   # these kernels accumulate LOCAL counts
         return float(cnt.item())
 
@@ -271,7 +249,7 @@ class ParallelSGD:
         sums, the model all-reduce) is recorded once; the sampling stream comes from a
         device step counter (K1 ``step_dev``) that the graph itself advances, so a replay
         is one host call per step instead of 2 (SSGD) to 14 (MA/BMUF, 5 local steps)
-        launches. Needs GPU tensors, no persistent / fused-update / one-kernel mode, and
+        launches. Needs GPU tensors, no persistent / one-kernel mode, and
         no host-sequenced K11 epochs: one rank, or RCCL with DALGO_XGMI=0 (RCCL
         collectives are graph-capturable)."""
         if getattr(self, "_okg", None) is None:
@@ -289,7 +267,7 @@ class ParallelSGD:
                 env == "1" or (env == "auto" and auto))
             ok_comm = ws == 1 or (torch.distributed.get_backend() == "nccl"
                                   and os.environ.get("DALGO_XGMI", "auto") == "0")
-            self._okg = bool(want and self.device.type == "cuda" and not self.fused
+            self._okg = bool(want and self.device.type == "cuda"
                              and not self._persistent() and not self._one_kernel() and ok_comm
                              and getattr(getattr(self, "bucket", None), "xg", None) is None)
         return self._okg
@@ -344,23 +322,7 @@ class ParallelSGD:
         sd = dict(step_dev=step_dev) if step_dev is not None else {}
         if step_dev is not None:
             t = 0
-        if self.fused:
-            if self._pending:
-                lr_ops.lr_grad(self.data.X_train, self.data.y_train, self.w_next, self.seg, D=self.D,
-                               has_bias=True, eps=c.eps, seed=c.sample_seed, step=t, frac=c.frac,
-                               row_offset=self.data.row_offset, G=self.G, C=self.C,
-                               max_seg_rows=self.max_seg, w_prev=self.w, update=self._upd,
-                               count_acc=self.count_acc)
-                self.w, self.w_next = self.w_next, self.w
-            else:
-                lr_ops.lr_grad(self.data.X_train, self.data.y_train, self.w, self.seg, D=self.D,
-                               has_bias=True, eps=c.eps, seed=c.sample_seed, step=t, frac=c.frac,
-                               row_offset=self.data.row_offset, G=self.G, C=self.C,
-                               max_seg_rows=self.max_seg, count_acc=self.count_acc)
-            self.bucket.all_reduce()
-            self._count_ar()
-            self._pending = True
-        elif c.algo in ("ssgd", "gd") and self._one_kernel():
+        if c.algo in ("ssgd", "gd") and self._one_kernel():
             # the whole step in ONE launch: gradient, (xGMI exchange,) update
             self._count_ar()
             with self._ph("step_one_kernel"):
@@ -487,7 +449,6 @@ class ParallelSGD:
             comm.check_device_errors("evaluation")
 
     def evaluate(self):
-        self._flush()
         self._finish_center()
         d = self.data
         if d.X_test.shape[0] == 0:
@@ -539,7 +500,6 @@ class ParallelSGD:
 
     # --------------------------------------------------------- checkpointing
     def state_dict(self) -> dict:
-        self._flush()
         self._finish_center()
         # copy=True: on a CPU model .cpu() would alias the live tensors (a snapshot that
         # later training overwrites)
@@ -553,7 +513,6 @@ class ParallelSGD:
         return sd
 
     def load_state_dict(self, sd: dict):
-        self._pending = False
         self.t = int(sd["t"])
         self.w.copy_(sd["w"].to(self.w.dtype))
         if "locals" in sd and hasattr(self, "W"):
@@ -563,6 +522,5 @@ class ParallelSGD:
         self.history.accs = list(sd.get("accs", []))
 
     def weights(self) -> torch.Tensor:
-        self._flush()
         self._finish_center()
         return self.w.view(-1)

@@ -37,23 +37,24 @@ def test_lr_grad_matches_reference(cuda, dtype, D, frac):
     assert err / scale < 2e-5, (err, scale)
 
 
-@pytest.mark.parametrize("variant", list(range(12)))
+@pytest.mark.parametrize("fine", [0, 8])
 @pytest.mark.parametrize("D", [256, 1024, 2048])
-def test_lr_grad_every_variant(cuda, variant, D):
-    """Every launch-shape / cache-policy variant of K1 selects the same rows and sums
-    the same gradient (variants 8-11 differ only in the X-row load policy bits)."""
+def test_lr_grad_shapes_and_claims(cuda, fine, D):
+    """Both register layouts of the launch shape (two row sets below 4 column chunks per
+    lane, one set at 2048 columns) and both in-block claim modes (whole 256-row groups
+    only / fine 64-row quarters at the end) select the same rows and sum the same
+    gradient as the CPU reference, over several segments."""
     n = 40_000
     X, y = _data(n, D, torch.bfloat16, seed=21)
     seg = torch.tensor([0, 13_331, n], dtype=torch.int64)
     W = torch.randn(2, D + 1, generator=torch.Generator().manual_seed(3)) * 0.05
     kw = dict(D=D, frac=0.1, step=5, seed=7)
     G_ref, C_ref = L.lr_grad(X, y, W.double(), seg, **kw)
-    Gd, Cd = L.lr_grad(X.to(cuda), y.to(cuda), W.to(cuda), seg.to(cuda),
-                       variant=variant | (L.LR_FINE_GROUPS << 16), **kw)
+    Gd, Cd = L.lr_grad(X.to(cuda), y.to(cuda), W.to(cuda), seg.to(cuda), fine_groups=fine, **kw)
     torch.cuda.synchronize()
-    assert torch.equal(Cd.cpu().double(), C_ref), (variant, Cd, C_ref)
+    assert torch.equal(Cd.cpu().double(), C_ref), (fine, Cd, C_ref)
     rel = (Gd.cpu().double() - G_ref).abs().max() / G_ref.abs().max()
-    assert rel < 1e-4, (variant, rel)
+    assert rel < 1e-4, (fine, rel)
 
 
 def test_lr_grad_single_segment_deterministic(cuda):
@@ -81,35 +82,14 @@ def test_lr_grad_single_segment_deterministic(cuda):
     assert rel < 1e-4
 
 
-@pytest.mark.parametrize("pool_frac", [0.1, 0.3])
-@pytest.mark.parametrize("fine", [0, 8])
-def test_lr_grad_work_pool(cuda, pool_frac, fine):
-    """Cross-block work pool + fine in-block claims select and sum exactly the same rows
-    (several launches: the two claim-head parity sets alternate and re-arm each other)."""
-    n, D = 300_000, 1024
-    X, y = _data(n, D, torch.bfloat16, seed=5)
-    Xd, yd = X.to(cuda), y.to(cuda)
-    seg = torch.tensor([0, 70_001, 190_000, n], dtype=torch.int64)
-    W = torch.randn(3, D + 1, generator=torch.Generator().manual_seed(4)) * 0.05
-    for step in range(4):
-        kw = dict(D=D, frac=0.1, step=step, seed=11)
-        G_ref, C_ref = L.lr_grad(X, y, W.double(), seg, **kw)
-        Gd, Cd = L.lr_grad(Xd, yd, W.to(cuda), seg.to(cuda), pool_frac=pool_frac,
-                           variant=L.LR_VARIANT | (fine << 16), **kw)
-        torch.cuda.synchronize()
-        assert torch.equal(Cd.cpu().double(), C_ref), (step, Cd, C_ref)
-        rel = (Gd.cpu().double() - G_ref).abs().max() / G_ref.abs().max()
-        assert rel < 1e-4, (step, rel)
-
-
 @pytest.mark.parametrize("align", [4, 260])
-@pytest.mark.parametrize("mode", ["atomic", "deterministic", "pool"])
+@pytest.mark.parametrize("mode", ["atomic", "deterministic"])
 def test_lr_grad_static_range_alignment(cuda, monkeypatch, align, mode):
-    """K1 with block ranges that are not multiples of 256 rows (LR_RPB_ALIGN 4 / 260):
+    """K1 with block ranges that are not multiples of 256 rows (RPB_ALIGN 4 / 260):
     partial 256-row groups at every block end, Philox quads straddling block
-    boundaries, a row_offset that is not a multiple of 4, and the deterministic,
-    atomic and pool epilogues; exact counts and G vs the f64 CPU reference."""
-    monkeypatch.setattr(L, "LR_RPB_ALIGN", align)
+    boundaries, a row_offset that is not a multiple of 4, and the deterministic and
+    atomic epilogues; exact counts and G vs the f64 CPU reference."""
+    monkeypatch.setattr(L, "RPB_ALIGN", align)
     n, D = 300_001, 256
     X, y = _data(n, D, torch.bfloat16, seed=8)
     Xd, yd = X.to(cuda), y.to(cuda)
@@ -118,9 +98,8 @@ def test_lr_grad_static_range_alignment(cuda, monkeypatch, align, mode):
     for step in range(3):
         kw = dict(D=D, frac=0.1, step=step, seed=13, row_offset=6)
         G_ref, C_ref = L.lr_grad(X, y, W.double(), seg, **kw)
-        extra = dict(deterministic=(mode == "deterministic"),
-                     pool_frac=0.2 if mode == "pool" else 0.0)
-        Gd, Cd = L.lr_grad(Xd, yd, W.to(cuda), seg.to(cuda), **extra, **kw)
+        Gd, Cd = L.lr_grad(Xd, yd, W.to(cuda), seg.to(cuda), deterministic=(mode == "deterministic"),
+                           **kw)
         torch.cuda.synchronize()
         assert torch.equal(Cd.cpu().double(), C_ref), (step, Cd, C_ref)
         rel = (Gd.cpu().double() - G_ref).abs().max() / G_ref.abs().max()
@@ -245,75 +224,3 @@ def test_lr_grad_persistent_steps(cuda, mode, reg, n):
     assert bool((G == 0).all()) and bool((C == 0).all())
     rel = ((w - w_ref).abs().max() / w_ref.abs().max()).item()
     assert rel < 1e-4, rel
-
-
-
-def _one_seg(n, D, dtype, cuda, seed=0):
-    X, y = _data(n, D, dtype, seed)
-    W = torch.randn(1, D + 1, generator=torch.Generator().manual_seed(3)) * 0.1
-    seg = torch.tensor([0, n], dtype=torch.int64)
-    return X, y, W, seg
-
-
-@pytest.mark.parametrize("dtype,D", [(torch.bfloat16, 1024), (torch.float32, 256), (torch.bfloat16, 30)])
-@pytest.mark.parametrize("row_offset", [0, 12345])
-def test_lr_grad_balanced_slices_match_reference(cuda, monkeypatch, dtype, D, row_offset):
-    """K1 LIST build (K7 selection one step ahead on a side stream) draws the same
-    minibatch as the CPU Philox reference, over consecutive steps, a repeated step
-    and a jump (the not-prefetched path)."""
-    monkeypatch.setattr(L, "LR_BALANCED", True)
-    L._sel_cache.clear()
-    n = 60_000
-    X, y, W, seg = _one_seg(n, D, dtype, cuda)
-    Xd, yd, Wd, sd = pad_features(X.to(cuda)), y.to(cuda), W.to(cuda), seg.to(cuda)
-    for step in [0, 1, 2, 2, 3, 9, 10]:
-        kw = dict(D=D, has_bias=True, eps=0.0, seed=42, step=step, frac=0.1, row_offset=row_offset)
-        G_ref, C_ref = L.lr_grad(pad_features(X).float(), y, W.double(), seg, **kw)
-        Gd, Cd = L.lr_grad(Xd, yd, Wd, sd, **kw)
-        torch.cuda.synchronize()
-        assert torch.equal(Cd.cpu().double(), C_ref), (step, Cd, C_ref)
-        err = (Gd.cpu().double() - G_ref).abs().max().item()
-        assert err / (G_ref.abs().max().item() + 1e-6) < 2e-5, (step, err)
-    assert len(L._sel_cache) == 1
-
-
-def test_lr_grad_balanced_slices_overflow_claims(cuda, monkeypatch):
-    """Per-block slices shorter than the step's selection: the entries past gx * k are
-    claimed at run time from the launch's counter (and re-armed for a repeated step)."""
-    monkeypatch.setattr(L, "LR_BALANCED", True)
-    L._sel_cache.clear()
-    n, D = 200_000, 256
-    X, y, W, seg = _one_seg(n, D, torch.bfloat16, cuda, seed=5)
-    Xd, yd, Wd, sd = pad_features(X.to(cuda)), y.to(cuda), W.to(cuda), seg.to(cuda)
-    kw = dict(D=D, has_bias=True, seed=7, frac=0.1)
-    L.lr_grad(Xd, yd, Wd, sd, step=0, **kw)
-    (selp,) = L._sel_cache.values()
-    selp.k = max(1, selp.k // 2)     # half of every block's share goes through the claims
-    for step in [1, 1, 2]:
-        G_ref, C_ref = L.lr_grad(pad_features(X).float(), y, W.double(), seg, step=step, **kw)
-        Gd, Cd = L.lr_grad(Xd, yd, Wd, sd, step=step, **kw)
-        torch.cuda.synchronize()
-        assert torch.equal(Cd.cpu().double(), C_ref), (step, Cd, C_ref)
-        err = (Gd.cpu().double() - G_ref).abs().max().item()
-        assert err / (G_ref.abs().max().item() + 1e-6) < 2e-5, (step, err)
-
-
-def test_lr_grad_balanced_slices_fused_tail(cuda, monkeypatch):
-    """One-kernel SSGD step (fused tail) on balanced slices equals the walk form."""
-    n, D = 100_000, 1024
-    X, y, W, seg = _one_seg(n, D, torch.bfloat16, cuda, seed=2)
-    Xd, yd, sd = pad_features(X.to(cuda)), y.to(cuda), seg.to(cuda)
-    out = {}
-    for bal in (False, True):
-        monkeypatch.setattr(L, "LR_BALANCED", bal)
-        L._sel_cache.clear()
-        Wd = W.to(cuda).clone()
-        G = torch.zeros_like(Wd)
-        C = torch.zeros(1, device=cuda)
-        for step in range(6):
-            L.lr_grad(Xd, yd, Wd, sd, D=D, seed=42, step=step, frac=0.1, G=G, C=C,
-                      tail=dict(mode=0, reg=0, eta=0.1), g_is_zero=True)
-        torch.cuda.synchronize()
-        out[bal] = Wd.cpu()
-    assert torch.allclose(out[False], out[True], rtol=1e-5, atol=1e-6), \
-        (out[False] - out[True]).abs().max()
