@@ -3,7 +3,11 @@
 
 Graph500 R-MAT (a,b,c = 0.57,0.19,0.19), scale 26, edge factor 16 = 1.07B edges,
 vertex ids scrambled, deduplicated (distinct()). Destination-partitioned over the
-ranks. Reports edges/s (whole job, edges per iteration / iteration time).
+ranks. Reports edges/s (whole job, edges per iteration / iteration time). The phase
+split comes from HIP events on one warm-up step. A correctness witness runs after the
+timed region (untimed): one iteration of the benchmarked SpMV (K4b by default: fixed-point
+blocked, update fused) against the pull K4 SpMV from the same state; the ranks must agree
+to f32 rounding, else the bench exits non-zero.
 """
 import argparse
 import json
@@ -24,7 +28,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--semantics", default="reference")
     ap.add_argument("--no-reorder", action="store_true", help="keep scrambled R-MAT vertex ids")
-    ap.add_argument("--spmv", default="blocked", choices=["pull", "xcd", "blocked"])
+    ap.add_argument("--spmv", default="blocked", choices=["pull", "blocked"])
+    ap.add_argument("--no-witness", action="store_true")
+    ap.add_argument("--deadline-s", type=float, default=420.0)
     ap.add_argument("--bin-width", type=int, default=16384)
     ap.add_argument("--chunk", type=int, default=1 << 40)
     ap.add_argument("--tile", type=int, default=16384)
@@ -42,7 +48,8 @@ def main():
     from dalgo.models.pagerank import PageRank, PageRankConfig
     from dalgo.ops import graph as G
     from dalgo.parallel import comm, runtime
-    rt = runtime.init(backend=a.backend, device=a.device, app_name="pagerank-bench")
+    runtime.arm_watchdog(a.deadline_s, tag="pagerank_bench")
+    rt = runtime.init(backend=a.backend, device=a.device, app_name="pagerank-bench", timeout_s=120)
     W = rt.world_size
     check_world(a.gpus, W, "pagerank_bench")
     t0 = time.time()
@@ -52,17 +59,18 @@ def main():
     E = comm.all_reduce_count(shard.n_edges, device=rt.device)
     pr = PageRank(PageRankConfig(semantics=a.semantics, spmv=a.spmv, bin_width=a.bin_width,
                                  chunk=a.chunk, tile=a.tile), shard, W)
-    for _ in range(a.warmup):
-        pr.step()
-    rt.synchronize()
-    rt.synchronize()
     from dalgo.utils.obs import PhaseTimer
-    tm = PhaseTimer(rt.device)
-    for name, fn in (("exchange", pr._exchange), ("spmv", pr._spmv), ("update", pr._update)):
-        with tm.phase(name):
-            fn()
+    phases = {}
+    for i in range(max(a.warmup, 1)):
+        if i == 0:
+            pr.timer = PhaseTimer(rt.device)   # HIP events inside step(): the phase split
+        pr.step()
+        if i == 0:
+            rt.synchronize()
+            phases = pr.timer.summary()
+            pr.timer = None
     rt.synchronize()
-    phases = tm.summary()
+    done = pr.t
     xf = torch.tensor([pr.exchange_floats()], dtype=torch.int64, device=rt.device)
     comm.all_reduce_sum(xf)
     rt.barrier(); rt.synchronize()
@@ -73,12 +81,33 @@ def main():
     el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=rt.device)
     comm.all_reduce_max(el)
     ms = float(el.item()) / a.steps * 1e3
+    witness = None
+    if not a.no_witness:
+        # one more iteration of the benchmarked SpMV vs the pull SpMV from the same state
+        ref = PageRank(PageRankConfig(semantics=a.semantics, spmv="pull", exchange=pr.exchange),
+                       shard, W)
+        ref.load_state_dict(pr.state_dict())
+        pr.step()
+        ref.step()
+        rt.synchronize()
+        r1, r0 = pr.r.double(), ref.r.double()
+        both = (r1 >= 0) & (r0 >= 0)
+        err = torch.tensor([float(((r1 - r0).abs() * both).max().item()),
+                            float((r1 >= 0).ne(r0 >= 0).sum().item())], dtype=torch.float64,
+                           device=rt.device)
+        comm.all_reduce_max(err)
+        scale = torch.tensor([float(r0.abs().max().item())], dtype=torch.float64, device=rt.device)
+        comm.all_reduce_max(scale)
+        rel = float(err[0].item()) / max(float(scale.item()), 1e-30)
+        witness = {"vs": "pull K4 SpMV, same state", "max_rel_err": rel,
+                   "presence_mismatches": int(err[1].item()), "iteration": pr.t,
+                   "passed": bool(rel < 1e-5 and int(err[1].item()) == 0)}
     if rt.is_main:
         print(json.dumps({
             "metric": "PageRank edges/sec (whole node)", "value": E / (ms / 1e3), "unit": "edges/s",
             "n_gpus": W, "ms_per_iter": ms, "edges_dedup": E, "edges_generated": n_gen,
             "vertices": 1 << a.scale, "degree_reordered": not a.no_reorder, "spmv": pr.spmv, "phases_ms_rank0": phases, "graph_build_s": build_s,
-            "spmv_GBps_stream": shard.n_edges * 8 / (phases["spmv"] / 1e3) / 1e9,
+            "timed_steps": a.steps, "steps_before_timing": done, "correctness_witness": witness,
             "exchange": pr.exchange, "exchange_MB_per_iter_all_ranks": int(xf.item()) * 4 / 1e6,
             "blocked_layout_rank0": None if pr.layout is None else {
                 "chunks": pr.layout.n_chunks, "entries": pr.layout.n_entries,
@@ -87,6 +116,9 @@ def main():
                 "bin_width": pr.layout.bin_width},
             "allgather_MB_per_iter_all_ranks": (W - 1) * W * shard.slice_size * 4 / 1e6}), flush=True)
     runtime.shutdown()
+    runtime.arm_watchdog(0)
+    if witness is not None and not witness["passed"]:
+        raise SystemExit(f"[pagerank_bench] correctness witness failed: {witness}")
 
 
 if __name__ == "__main__":

@@ -515,36 +515,22 @@ void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta
                   "kmeans_filter");
 }
 
-void kmeans_post(const Tensor& idx, int64_t m, const Tensor& assign, const Tensor& a_prev,
-                 const Tensor& mind, const Tensor& mind2, double tol, Tensor u, Tensor l,
-                 Tensor changed, Tensor n_changed, const std::optional<Tensor>& m_dev,
-                 const std::optional<Tensor>& tol_dev) {
-  check_f32(mind2, "mind2");
-  check_f32(l, "l");
-  check_i32(idx, "idx");
-  check_i32(assign, "assign");
-  check_i32(a_prev, "a_prev");
-  check_f32(mind, "mind");
-  check_f32(u, "u");
-  check_i32(changed, "changed");
-  TORCH_CHECK(m >= 0 && m <= idx.numel(), "kmeans_post: m");
-  TORCH_CHECK(n_changed.scalar_type() == at::kLong && n_changed.numel() >= 1, "n_changed int64[1]");
-  const unsigned long long* mdp = nullptr;
-  if (m_dev.has_value()) {
-    check_dev(*m_dev, "m_dev");
-    TORCH_CHECK(m_dev->scalar_type() == at::kLong && m_dev->numel() >= 1, "m_dev int64[1]");
-    mdp = reinterpret_cast<const unsigned long long*>(m_dev->data_ptr<int64_t>());
+// bounds after the full first pass (u, l from the K2 distances; tol from the K2 max)
+void kmeans_bounds_init(const Tensor& mind, const Tensor& mind2, const Tensor& xmax, int64_t n,
+                        Tensor u, Tensor l, Tensor tol) {
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&mind, &mind2, &u, &l}) {
+    check_f32(*t, "bounds");
+    TORCH_CHECK(t->numel() >= n, "bounds [n]");
   }
-  const float* tp = nullptr;
-  if (tol_dev.has_value()) { check_f32(*tol_dev, "tol_dev"); tp = tol_dev->data_ptr<float>(); }
-  DeviceGuard guard(idx.device());
-  DALGO_CHECK_HIP(dalgo_km_post(idx.data_ptr<int32_t>(), m, assign.data_ptr<int32_t>(),
-                                a_prev.data_ptr<int32_t>(), mind.data_ptr<float>(),
-                                mind2.data_ptr<float>(), (float)tol, u.data_ptr<float>(),
-                                l.data_ptr<float>(), changed.data_ptr<int32_t>(),
-                                reinterpret_cast<unsigned long long*>(n_changed.data_ptr<int64_t>()),
-                                changed.numel(), mdp, tp, cur_stream()),
-                  "kmeans_post");
+  check_f32(tol, "tol");
+  check_dev(xmax, "xmax");
+  TORCH_CHECK(xmax.scalar_type() == at::kInt && xmax.numel() >= 1, "xmax int32[1]");
+  DeviceGuard guard(mind.device());
+  DALGO_CHECK_HIP(dalgo_km_bounds_init(mind.data_ptr<float>(), mind2.data_ptr<float>(),
+                                       reinterpret_cast<const unsigned*>(xmax.data_ptr<int32_t>()), n,
+                                       u.data_ptr<float>(), l.data_ptr<float>(), tol.data_ptr<float>(),
+                                       cur_stream()),
+                  "kmeans_bounds_init");
 }
 
 // bound-filter geometry of new vs previous (rounded) centres: delta [k], s [k] (f32)
@@ -582,9 +568,13 @@ void kmeans_qsum(const Tensor& assign, const Tensor& xh, int64_t k, Tensor Q) {
 
 // K2 (variant 52) over the rows idx[0, m) only
 void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
-                       const std::optional<Tensor>& idx, int64_t m, Tensor assign, Tensor mind,
-                       const std::optional<Tensor>& mind2, const std::optional<Tensor>& m_dev,
-                       const std::optional<Tensor>& xh, const std::optional<Tensor>& xmax) {
+                       const std::optional<Tensor>& idx, int64_t m, Tensor assign,
+                       const std::optional<Tensor>& mind, const std::optional<Tensor>& mind2,
+                       const std::optional<Tensor>& xh, const std::optional<Tensor>& xmax,
+                       const std::optional<Tensor>& m_dev, const std::optional<Tensor>& a_prev,
+                       const std::optional<Tensor>& tol, const std::optional<Tensor>& u,
+                       const std::optional<Tensor>& l, const std::optional<Tensor>& changed,
+                       const std::optional<Tensor>& n_changed) {
   TORCH_CHECK(Cq.dim() == 2 && Cq.is_contiguous() && Cq.scalar_type() == at::kBFloat16, "Cq bf16");
   const int DP = (int)Cq.size(1);
   TORCH_CHECK(DP == 64 || DP == 128, "kmeans_assign_idx: DP 64 or 128");
@@ -602,38 +592,53 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
     TORCH_CHECK(m >= 0 && m <= X.size(0), "kmeans_assign_idx: m <= n");
   }
   check_i32(assign, "assign");
-  check_f32(mind, "mind");
-  TORCH_CHECK(assign.numel() >= X.size(0) && mind.numel() >= X.size(0), "assign / mind [n]");
-  float* m2 = nullptr;
-  if (mind2.has_value()) {
-    check_f32(*mind2, "mind2");
-    TORCH_CHECK(mind2->numel() >= X.size(0), "mind2 [n]");
-    m2 = mind2->data_ptr<float>();
-  }
-  const unsigned long long* mdp = nullptr;
-  if (m_dev.has_value()) {   // rows = *m_dev (device), m = its upper bound
-    check_dev(*m_dev, "m_dev");
-    TORCH_CHECK(m_dev->scalar_type() == at::kLong && m_dev->numel() >= 1, "m_dev int64[1]");
-    TORCH_CHECK(m2 != nullptr, "kmeans_assign_idx: the device-count form is top-2");
-    mdp = reinterpret_cast<const unsigned long long*>(m_dev->data_ptr<int64_t>());
-  }
-  float* xhp = nullptr;
-  if (xh.has_value()) {
-    check_f32(*xh, "xh");
-    TORCH_CHECK(xh->numel() >= X.size(0), "xh [n]");
-    xhp = xh->data_ptr<float>();
-  }
+  TORCH_CHECK(assign.numel() >= X.size(0), "assign [n]");
+  auto f32n = [&](const std::optional<Tensor>& t, const char* nm) -> float* {
+    if (!t.has_value()) return nullptr;
+    check_f32(*t, nm);
+    TORCH_CHECK(t->numel() >= X.size(0), nm, " [n]");
+    return t->data_ptr<float>();
+  };
+  float* md = f32n(mind, "mind");
+  float* m2 = f32n(mind2, "mind2");
+  float* xhp = f32n(xh, "xh");
   unsigned* xmp = nullptr;
   if (xmax.has_value()) {
     check_dev(*xmax, "xmax");
     TORCH_CHECK(xmax->scalar_type() == at::kInt && xmax->numel() >= 1, "xmax int32[1] (float bits)");
     xmp = reinterpret_cast<unsigned*>(xmax->data_ptr<int32_t>());
   }
+  DalgoKmPost post{};
+  const DalgoKmPost* pp = nullptr;
+  if (m_dev.has_value()) {   // filtered iteration: rows = *m_dev (device), m = its upper bound
+    TORCH_CHECK(a_prev.has_value() && tol.has_value() && u.has_value() && l.has_value() &&
+                    changed.has_value() && n_changed.has_value(),
+                "kmeans_assign_idx: the device-count form needs a_prev, tol, u, l, changed, n_changed");
+    check_dev(*m_dev, "m_dev");
+    TORCH_CHECK(m_dev->scalar_type() == at::kLong && m_dev->numel() >= 1, "m_dev int64[1]");
+    check_i32(*a_prev, "a_prev");
+    check_i32(*changed, "changed");
+    TORCH_CHECK(a_prev->numel() >= X.size(0), "a_prev [n]");
+    check_f32(*tol, "tol");
+    TORCH_CHECK(n_changed->scalar_type() == at::kLong && n_changed->numel() >= 1, "n_changed int64[1]");
+    check_dev(*n_changed, "n_changed");
+    post.mcount = reinterpret_cast<const unsigned long long*>(m_dev->data_ptr<int64_t>());
+    post.a_prev = a_prev->data_ptr<int32_t>();
+    post.tol = tol->data_ptr<float>();
+    post.u = f32n(u, "u");
+    post.l = f32n(l, "l");
+    post.changed = changed->data_ptr<int32_t>();
+    post.n_changed = reinterpret_cast<unsigned long long*>(n_changed->data_ptr<int64_t>());
+    post.cap = changed->numel();
+    pp = &post;
+  } else {
+    TORCH_CHECK(md != nullptr, "kmeans_assign_idx: mind");
+  }
   DeviceGuard guard(X.device());
   DALGO_CHECK_HIP(dalgo_kmeans_assign_idx(X.data_ptr(), m, X.stride(0), DP, Cq.data_ptr(),
                                           hn.data_ptr<float>(), (int)kpad, ip,
-                                          assign.data_ptr<int>(), mind.data_ptr<float>(), m2,
-                                          nullptr, 0, mdp, xhp, xmp, cur_stream()),
+                                          assign.data_ptr<int>(), md, m2, nullptr, 0, xhp, xmp, pp,
+                                          cur_stream()),
                   "kmeans_assign_idx");
 }
 
@@ -794,47 +799,6 @@ void pb_spmv(const Tensor& srcl, const Tensor& tile_e, const Tensor& tile_ent,
                     split_first.data_ptr<int32_t>(), split_count.data_ptr<int32_t>(), (int)nsp, od,
                     (float)q, (float)invN, (int)mode, di, rp, cp, dout, cur_stream()),
       "pb_spmv");
-}
-
-// XCD-partitioned K4: 8 source-line parts (dalgo.ops.graph.build_xcd), per-part sums
-void pr_spmv_xcd(const Tensor& src, const Tensor& dstl, const Tensor& part_base, int64_t e_max,
-                 const Tensor& c, Tensor acc_all) {
-  check_i32(src, "src");
-  check_i32(dstl, "dstl");
-  TORCH_CHECK(src.numel() == dstl.numel(), "pr_spmv_xcd: edge arrays");
-  check_dev(part_base, "part_base");
-  TORCH_CHECK(part_base.scalar_type() == at::kLong && part_base.numel() == 9, "part_base int64[9]");
-  check_f32(c, "c");
-  check_f32(acc_all, "acc_all");
-  TORCH_CHECK(acc_all.dim() == 2 && acc_all.size(0) == 8 && acc_all.is_contiguous(), "acc_all [8, n]");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 &&
-                  reinterpret_cast<uintptr_t>(dstl.data_ptr()) % 16 == 0, "edge arrays 16-B aligned");
-  DeviceGuard guard(src.device());
-  DALGO_CHECK_HIP(dalgo_pr_spmv_xcd(src.data_ptr<int32_t>(), dstl.data_ptr<int32_t>(),
-                                    part_base.data_ptr<int64_t>(), e_max, c.data_ptr<float>(),
-                                    acc_all.data_ptr<float>(), acc_all.size(1), cur_stream()),
-                  "pr_spmv_xcd");
-}
-
-void pr_update_xcd(Tensor acc_all, const Tensor& outdeg, double q, double invN, int64_t mode,
-                   const std::optional<Tensor>& dangling_in, Tensor r, Tensor c,
-                   const std::optional<Tensor>& dangling_out) {
-  check_f32(acc_all, "acc_all");
-  TORCH_CHECK(acc_all.dim() == 2 && acc_all.size(0) == 8 && acc_all.is_contiguous(), "acc_all [8, n]");
-  check_i32(outdeg, "outdeg");
-  check_f32(r, "r");
-  check_f32(c, "c");
-  const int64_t n = r.numel();
-  TORCH_CHECK(acc_all.size(1) >= n && outdeg.numel() >= n && c.numel() >= n, "pr_update_xcd sizes");
-  const float* di = nullptr;
-  float* dout = nullptr;
-  if (dangling_in.has_value()) { check_f32(*dangling_in, "dangling_in"); di = dangling_in->data_ptr<float>(); }
-  if (dangling_out.has_value()) { check_f32(*dangling_out, "dangling_out"); dout = dangling_out->data_ptr<float>(); }
-  DeviceGuard guard(acc_all.device());
-  DALGO_CHECK_HIP(dalgo_pr_update_xcd(acc_all.data_ptr<float>(), acc_all.size(1),
-                                      outdeg.data_ptr<int32_t>(), n, (float)q, (float)invN, (int)mode,
-                                      di, r.data_ptr<float>(), c.data_ptr<float>(), dout, cur_stream()),
-                  "pr_update_xcd");
 }
 
 void pr_update(const Tensor& acc, const Tensor& pres, const Tensor& outdeg, double q, double invN,
@@ -1151,15 +1115,15 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(i!) er, Tensor? m_dev=None, int chunk=65536) -> ()");
   m.def("kmeans_filter(Tensor assign, Tensor(a!) u, Tensor(e!) l, Tensor delta, Tensor s, "
         "Tensor(b!) a_prev, Tensor(c!) idx, Tensor(d!) n_active) -> ()");
-  m.def("kmeans_post(Tensor idx, int m, Tensor assign, Tensor a_prev, Tensor mind, Tensor mind2, "
-        "float tol, Tensor(a!) u, Tensor(d!) l, Tensor(b!) changed, Tensor(c!) n_changed, "
-        "Tensor? m_dev=None, Tensor? tol_dev=None) -> ()");
   m.def("kmeans_centre_bounds(Tensor cnow, Tensor cprev, int k, int d, Tensor(a!) delta, "
         "Tensor(b!) s) -> ()");
   m.def("kmeans_qsum(Tensor assign, Tensor xh, int k, Tensor(a!) Q) -> ()");
   m.def("kmeans_assign_idx(Tensor X, Tensor Cq, Tensor hn, Tensor? idx, int m, Tensor(a!) assign, "
-        "Tensor(b!) mind, Tensor(c!)? mind2=None, Tensor? m_dev=None, Tensor(d!)? xh=None, "
-        "Tensor(e!)? xmax=None) -> ()");
+        "Tensor(b!)? mind=None, Tensor(c!)? mind2=None, Tensor(d!)? xh=None, Tensor(e!)? xmax=None, "
+        "Tensor? m_dev=None, Tensor? a_prev=None, Tensor? tol=None, Tensor(f!)? u=None, "
+        "Tensor(g!)? l=None, Tensor(h!)? changed=None, Tensor(i!)? n_changed=None) -> ()");
+  m.def("kmeans_bounds_init(Tensor mind, Tensor mind2, Tensor xmax, int n, Tensor(a!) u, "
+        "Tensor(b!) l, Tensor(c!) tol) -> ()");
   m.def("kmeans_update(Tensor(a!) C, Tensor S, Tensor cnt, Tensor(b!) Cq, Tensor(c!) hn, "
         "Tensor(d!)? shift2) -> ()");
   m.def("rmat_edges(int seed, int scale, int e_off, float a, float b, float c, bool scramble, "
@@ -1175,10 +1139,6 @@ TORCH_LIBRARY(dalgo, m) {
         "int wu_hi=2147483647, int phases=3) -> ()");
   m.def("pr_spmv(Tensor src, Tensor dstl, Tensor c, Tensor(a!) acc, Tensor(b!) pres, "
         "bool accumulate=False) -> ()");
-  m.def("pr_spmv_xcd(Tensor src, Tensor dstl, Tensor part_base, int e_max, Tensor c, "
-        "Tensor(a!) acc_all) -> ()");
-  m.def("pr_update_xcd(Tensor(a!) acc_all, Tensor outdeg, float q, float invN, int mode, "
-        "Tensor? dangling_in, Tensor(b!) r, Tensor(c!) c, Tensor(d!)? dangling_out) -> ()");
   m.def("pr_update(Tensor acc, Tensor pres, Tensor outdeg, float q, float invN, int mode, "
         "Tensor? dangling_in, Tensor(a!) r, Tensor(b!) c, Tensor(c!)? dangling_out) -> ()");
   m.def("xgmi_buffer_bytes(int slot) -> int", &xgmi_buffer_bytes);
@@ -1229,15 +1189,13 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("pr_spmv", &pr_spmv);
   m.impl("pb_spmv", &pb_spmv);
   m.impl("pr_update", &pr_update);
-  m.impl("pr_spmv_xcd", &pr_spmv_xcd);
-  m.impl("pr_update_xcd", &pr_update_xcd);
   m.impl("kmeans_assign", &kmeans_assign);
   m.impl("kmeans_update", &kmeans_update);
   m.impl("kmeans_diff", &kmeans_diff);
   m.impl("kmeans_move_sorted", &kmeans_move_sorted);
   m.impl("kmeans_filter", &kmeans_filter);
-  m.impl("kmeans_post", &kmeans_post);
   m.impl("kmeans_centre_bounds", &kmeans_centre_bounds);
+  m.impl("kmeans_bounds_init", &kmeans_bounds_init);
   m.impl("kmeans_qsum", &kmeans_qsum);
   m.impl("kmeans_assign_idx", &kmeans_assign_idx);
   m.impl("kmeans_accumulate_sorted", &kmeans_accumulate_sorted);   // dispatches on its output counter

@@ -25,6 +25,7 @@
 //   0.5|c~|^2 of the ROUNDED copy (consistent scores) and the squared shift.
 #include <cstdlib>
 #include "dalgo/common.h"
+#include "launchers.h"
 #include <algorithm>
 
 namespace dalgo {
@@ -286,6 +287,27 @@ typedef __attribute__((address_space(3))) void km_lds_void;
 // worst case and no host sync is needed to launch.
 // Optional outputs of a full pass (the first bound-filtered iteration): xh[row] = 0.5|x|^2
 // and *xmax = max over the rows of 0.5|x|^2 (float bits, non-negative: integer max).
+// LOOP (the filtered iterations) also fuses the bound update that followed K2: instead
+// of mind / mind2 it writes u = sqrt(dist + tol) rounded up and l = sqrt(dist2 - tol)
+// rounded down (tol on the device), and appends the rows whose cluster differs from
+// a_prev[row] to `changed` through a per-block LDS buffer (one global atomic per flush).
+struct KmAux {
+  const unsigned long long* mcount;   // device row count (LOOP)
+  float* xh;                          // full pass: 0.5|x|^2 per row
+  unsigned* xmax;                     // full pass: max 0.5|x|^2 (float bits)
+  const int* a_prev;                  // LOOP: cluster before this iteration
+  const float* tol;                   // LOOP: slack of a kernel distance
+  float* u;                           // LOOP: upper bound of the distance to the centre
+  float* l;                           // LOOP: lower bound of every other distance
+  int* changed;                       // LOOP: rows whose cluster changed ...
+  unsigned long long* n_changed;      //       ... and their number
+  long long cap;                      //       capacity of `changed`
+};
+constexpr int kChgBuf = 1024;         // changed rows buffered per block (LDS)
+
+__device__ __forceinline__ float km_up1(float x) { return nextafterf(x, __builtin_inff()); }
+__device__ __forceinline__ float km_dn1(float x) { return nextafterf(x, -__builtin_inff()); }
+
 template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, bool TOP2 = false,
           bool LOOP = false>
 __global__ void __launch_bounds__(NW * 64, MINB)
@@ -294,8 +316,8 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
                           int* __restrict__ assign, float* __restrict__ mind,
                           double* __restrict__ sse, int sse_mask,
                           const int32_t* __restrict__ idx, float* __restrict__ mind2,
-                          const unsigned long long* __restrict__ mcount, float* __restrict__ xh,
-                          unsigned* __restrict__ xmax) {
+                          const KmAux aux) {
+  static_assert(!LOOP || TOP2, "the fused bound update needs the second-best distance");
   // idx (optional): the block's point j is row idx[j] of X (and of assign / mind), j < n
   // -- the bound-filtered form of Lloyd only re-assigns the points the filter keeps
   constexpr int KS = DP / 16;                  // 32x32x16 k-steps per centre row
@@ -313,9 +335,33 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   __shared__ float s_m[NW];
   __shared__ double s_sse[NW];
 
+  __shared__ int s_chg[LOOP ? kChgBuf : 1];
+  __shared__ int s_nchg;
+  __shared__ unsigned long long s_chg_base;
+
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, cl = lane & 31;
   const int nchunk = kpad / CH;
-  if (mcount != nullptr) n = min(n, (int64_t)*mcount);
+  if (aux.mcount != nullptr) n = min(n, (int64_t)*aux.mcount);
+  float tol = 0.f;
+  if constexpr (LOOP) {
+    tol = *aux.tol;
+    if (tid == 0) s_nchg = 0;
+  }
+  // LOOP: move the buffered changed rows to the global list (block-uniform call)
+  auto flush_changed = [&]() {
+    __syncthreads();
+    const int c = s_nchg;
+    if (c > 0) {
+      if (tid == 0) s_chg_base = atomicAdd(aux.n_changed, (unsigned long long)c);
+      __syncthreads();
+      const long long b = (long long)s_chg_base;
+      for (int j = tid; j < c; j += NT)
+        if (b + j < aux.cap) aux.changed[b + j] = s_chg[j];
+      __syncthreads();
+      if (tid == 0) s_nchg = 0;
+    }
+    __syncthreads();
+  };
   const int64_t ntile = (n + TILE - 1) / TILE;
 
   // per-thread DMA sources: slot q = g*NT + tid of the chunk image
@@ -394,6 +440,10 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // rewrite after them
   if (lane == 0) s_m[wid] = mx;
   __syncthreads();
+  if constexpr (LOOP) {
+    // every wave is past the previous tile's appends: room for this tile's (<= TILE)?
+    if (s_nchg > kChgBuf - TILE) flush_changed();
+  }
   float M = s_m[0];
 #pragma unroll
   for (int w = 1; w < NW; ++w) M = fmaxf(M, s_m[w]);
@@ -426,13 +476,21 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   auto reduce_tile = [&](const f32x16& acc, int t, int cb) {
     int m = 0x7fffffff;
     if constexpr (TOP2) {
+      // running pair (m <= m2) fed two keys at a time: with (x, y) new,
+      //   m' = min3(m, x, y),  m2' = min(m2, med3(m, x, y))
+      // (the second smallest of {m, m2, x, y}: if m2 is it, the median of {m, x, y}
+      // -- the second of a set missing it -- is >= m2; otherwise both of the two
+      // smallest are in {m, x, y} and their second is the median): 1.5 VALU per key
+      // instead of 2 (med3 + min per key)
       int m2 = 0x7fffffff;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kk = (__float_as_int(acc[r]) & kmask) | r;
-        // second smallest of {m, m2, kk} (m <= m2): the median
-        asm volatile("v_med3_i32 %0, %1, %2, %3" : "=v"(m2) : "v"(m), "v"(m2), "v"(kk));
-        m = min(m, kk);
+      for (int r = 0; r < 16; r += 2) {
+        const int k0 = (__float_as_int(acc[r]) & kmask) | r;
+        const int k1 = (__float_as_int(acc[r + 1]) & kmask) | (r + 1);
+        int md;
+        asm volatile("v_med3_i32 %0, %1, %2, %3" : "=v"(md) : "v"(m), "v"(k0), "v"(k1));
+        m2 = min(m2, md);
+        m = min(min(m, k0), k1);   // v_min3_i32
       }
       // merge with the running pair (bkey <= bkey2): second smallest of the four
       bkey2[t] = min(max(bkey[t], m), min(bkey2[t], m2));
@@ -542,25 +600,44 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       bv2 = fminf(fmaxf(v, pv), fminf(v2, pv2));
     }
     const int64_t p = pbase + t * 32 + cl;
+    bool chg = false;
+    int64_t row = 0;
     if (h == 0 && p < n) {
       // acc = 0.5|x-c|^2 + M - 0.5|x|^2
       const float dist = fmaxf(2.f * (bv - M) + x2[t], 0.f);
-      const int64_t row = idx ? (int64_t)idx[p] : p;
+      row = idx ? (int64_t)idx[p] : p;
       assign[row] = bi;
-      if (mind) mind[row] = dist;
-      if constexpr (TOP2) mind2[row] = fmaxf(2.f * (bv2 - M) + x2[t], 0.f);
-      if (xh) xh[row] = 0.5f * x2[t];
+      if constexpr (LOOP) {
+        const float dist2 = fmaxf(2.f * (bv2 - M) + x2[t], 0.f);
+        aux.u[row] = km_up1(sqrtf(km_up1(dist + tol)));
+        aux.l[row] = fmaxf(km_dn1(sqrtf(fmaxf(km_dn1(dist2 - tol), 0.f))), 0.f);
+        chg = bi != aux.a_prev[row];
+      } else {
+        if (mind) mind[row] = dist;
+        if constexpr (TOP2) mind2[row] = fmaxf(2.f * (bv2 - M) + x2[t], 0.f);
+        if (aux.xh) aux.xh[row] = 0.5f * x2[t];
+      }
       my_sse += (double)dist;
+    }
+    if constexpr (LOOP) {
+      const uint64_t cm = __ballot(chg);
+      if (cm != 0ull) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&s_nchg, __popcll(cm));
+        base = __shfl(base, 0);
+        if (chg) s_chg[base + __popcll(cm & ((1ull << lane) - 1ull))] = (int)row;
+      }
     }
   }
   };   // tile
   if constexpr (LOOP) {
     for (int64_t bt = blockIdx.x; bt < ntile; bt += gridDim.x) tile(bt);
+    flush_changed();
   } else {
     if ((int64_t)blockIdx.x < ntile) tile(blockIdx.x);
   }
 
-  if (xmax && lane == 0) atomicMax(xmax, __float_as_uint(my_xmax));
+  if (aux.xmax && lane == 0) atomicMax(aux.xmax, __float_as_uint(my_xmax));
   if (sse) {
     double s = my_sse;
     for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
@@ -1006,8 +1083,7 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
                                      const float* hn, int kpad, int* assign, float* mind,
                                      double* sse, int sse_mask, hipStream_t st,
                                      const int32_t* idx = nullptr, float* mind2 = nullptr,
-                                     const unsigned long long* mcount = nullptr,
-                                     float* xh = nullptr, unsigned* xmax = nullptr) {
+                                     const KmAux& aux = KmAux{}) {
   constexpr int CH = 32 * NSUB;
   constexpr size_t kStatic = NBUF * (size_t)CH * DP * 2;
   if (kpad % CH) return hipErrorInvalidValue;
@@ -1015,7 +1091,10 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
   if (kStatic + dyn + 1024 > 160 * 1024) return hipErrorInvalidValue;
   int64_t grid = cdiv(n, (int64_t)NW * PT * 32);
   if (grid == 0) return hipSuccess;
-  if (mcount != nullptr && !LOOP) return hipErrorInvalidValue;
+  if ((aux.mcount != nullptr) != LOOP) return hipErrorInvalidValue;
+  if (LOOP && (aux.tol == nullptr || aux.u == nullptr || aux.l == nullptr || aux.a_prev == nullptr ||
+               aux.changed == nullptr || aux.n_changed == nullptr))
+    return hipErrorInvalidValue;
   if (LOOP) grid = std::min<int64_t>(grid, (int64_t)device_cus() * MINB);
   if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
   auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF, TOP2, LOOP>;
@@ -1027,8 +1106,7 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
     attr_set = dyn;
   }
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(NW * 64), dyn, st, (const uint16_t*)X, n, ldx,
-                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse, sse_mask, idx, mind2, mcount,
-                     xh, xmax);
+                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse, sse_mask, idx, mind2, aux);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -1195,39 +1273,47 @@ hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ld
 
 // K2 (pipelined form) over the rows idx[0, m) of X only (bound-filtered Lloyd iteration).
 // idx may be null (rows 0 .. m); mind2 non-null selects the top-2 form (second-best
-// distance per row, a lower bound for the bound filter); mcount non-null: the row count
-// is *mcount (device), m its upper bound; xh / xmax: 0.5|x|^2 per row and its maximum.
+// distance per row, a lower bound for the bound filter); xh / xmax: 0.5|x|^2 per row and
+// its maximum (full pass). post != null: the filtered-iteration form -- the row count is
+// *post->mcount (device; m its upper bound), a resident grid walks the tiles and the
+// bound update (u, l, changed rows vs a_prev) is fused into the epilogue.
 hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP, const void* Cq,
                                    const float* hn, int kpad, const int32_t* idx, int* assign,
-                                   float* mind, float* mind2, double* sse, int sse_mask,
-                                   const unsigned long long* mcount, float* xh, unsigned* xmax,
-                                   hipStream_t st) {
+                                   float* mind, float* mind2, double* sse, int sse_mask, float* xh,
+                                   unsigned* xmax, const DalgoKmPost* post, hipStream_t st) {
   if (m <= 0) return hipSuccess;
   if (kpad % 128 != 0) return hipErrorInvalidValue;
-  if (mind2 != nullptr) {
-    // top-2: 2 point tiles per wave (3 would spill past 256 VGPRs); a device-resident row
-    // count takes the resident-grid tile loop
-    if (DP == 128 && mcount)
-      return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true, true>(
-          X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st, idx, mind2, mcount, xh, xmax);
+  KmAux aux{};
+  aux.xh = xh;
+  aux.xmax = xmax;
+  if (post != nullptr) {
+    aux.mcount = post->mcount; aux.a_prev = post->a_prev; aux.tol = post->tol; aux.u = post->u;
+    aux.l = post->l; aux.changed = post->changed; aux.n_changed = post->n_changed;
+    aux.cap = post->cap;
+    // top-2: 2 point tiles per wave (3 would spill past 256 VGPRs in the tile loop)
     if (DP == 128)
-      return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true>(
-          X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st, idx, mind2, nullptr, xh, xmax);
-    if (DP == 64 && mcount)
-      return launch_assign_pipe<64, 4, 2, 4, 2, 2, false, true, true>(
-          X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st, idx, mind2, mcount, xh, xmax);
+      return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true, true>(
+          X, m, ldx, Cq, hn, kpad, assign, nullptr, sse, sse_mask, st, idx, nullptr, aux);
     if (DP == 64)
-      return launch_assign_pipe<64, 4, 2, 4, 2, 2, false, true>(
-          X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st, idx, mind2, nullptr, xh, xmax);
+      return launch_assign_pipe<64, 4, 2, 4, 2, 2, false, true, true>(
+          X, m, ldx, Cq, hn, kpad, assign, nullptr, sse, sse_mask, st, idx, nullptr, aux);
     return hipErrorInvalidValue;
   }
-  if (mcount) return hipErrorInvalidValue;   // the device-count form is top-2 only
+  if (mind2 != nullptr) {
+    if (DP == 128)
+      return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true>(
+          X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st, idx, mind2, aux);
+    if (DP == 64)
+      return launch_assign_pipe<64, 4, 2, 4, 2, 2, false, true>(
+          X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st, idx, mind2, aux);
+    return hipErrorInvalidValue;
+  }
   if (DP == 128)
     return launch_assign_pipe<128, 4, 3, 4, 2, 2, true>(X, m, ldx, Cq, hn, kpad, assign, mind, sse,
-                                                        sse_mask, st, idx, nullptr, nullptr, xh, xmax);
+                                                        sse_mask, st, idx, nullptr, aux);
   if (DP == 64)
     return launch_assign_pipe<64, 4, 3, 4, 2, 2, true>(X, m, ldx, Cq, hn, kpad, assign, mind, sse,
-                                                       sse_mask, st, idx, nullptr, nullptr, xh, xmax);
+                                                       sse_mask, st, idx, nullptr, aux);
   return hipErrorInvalidValue;
 }
 

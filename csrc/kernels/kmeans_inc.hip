@@ -18,7 +18,8 @@
 //   the moved rows then go through the counting-sorted form in kmeans.hip (km_dexpand
 //                / km_dsegsum: ~0.1 ms per million signed entries; a per-row f64-atomic
 //                form, ~3 ms per million moved rows at 100M points, was removed)
-//   km_filter / km_post / km_centre_bounds: the bound-filtered (Hamerly) iteration.
+//   km_filter / km_bounds_init / km_centre_bounds: the bound-filtered (Hamerly) iteration
+//                (the post-K2 bound update is fused into the K2 epilogue, kmeans.hip).
 // Every count (changed rows, active rows) stays on the device: the launches that
 // consume it read it there, so an iteration needs no host sync.
 #include "dalgo/common.h"
@@ -180,84 +181,6 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, floa
   flush();
 }
 
-// After K2 re-assigned the active rows: u = sqrt(dist + tol) (an upper bound of the
-// distance to the assigned centre, tol covering the kernel's key truncation) and the
-// rows whose cluster changed appended to `changed` (LDS-buffered, as km_diff).
-// m: the active rows (host), or their upper bound when mdev (the device-resident count
-// written by km_filter) is given; tol: host value, or *tolp when tolp is given.
-__global__ void __launch_bounds__(kDiffThreads)
-km_post_kernel(const int32_t* __restrict__ idx, int64_t m, const int32_t* __restrict__ assign,
-               const int32_t* __restrict__ a_prev, const float* __restrict__ mind,
-               const float* __restrict__ mind2, float tol, float* __restrict__ u,
-               float* __restrict__ l, int32_t* __restrict__ changed,
-               unsigned long long* __restrict__ n_changed, int64_t cap,
-               const unsigned long long* __restrict__ mdev, const float* __restrict__ tolp) {
-  __shared__ int32_t s_buf[kDiffBuf];
-  __shared__ int s_cnt;
-  __shared__ unsigned long long s_base;
-  if (mdev != nullptr) m = min(m, (int64_t)*mdev);
-  if (tolp != nullptr) tol = *tolp;
-  const int64_t per = (m + gridDim.x - 1) / gridDim.x;
-  const int64_t lo = (int64_t)blockIdx.x * per;
-  const int64_t hi = lo + per < m ? lo + per : m;
-  if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
-  auto flush = [&]() {
-    const int c = s_cnt;
-    if (c == 0) return;
-    if (threadIdx.x == 0) s_base = atomicAdd(n_changed, (unsigned long long)c);
-    __syncthreads();
-    const int64_t b = (int64_t)s_base;
-    for (int j = threadIdx.x; j < c; j += kDiffThreads)
-      if (b + j < cap) changed[b + j] = s_buf[j];
-    __syncthreads();
-    if (threadIdx.x == 0) s_cnt = 0;
-    __syncthreads();
-  };
-  for (int64_t base = lo; base < hi; base += (int64_t)kDiffThreads * kEpt) {
-    int32_t row[kEpt];
-#pragma unroll
-    for (int e = 0; e < kEpt; ++e) {
-      const int64_t j = base + threadIdx.x + (int64_t)kDiffThreads * e;
-      row[e] = j < hi ? idx[j] : -1;
-    }
-    float d1[kEpt], d2[kEpt];
-    int an[kEpt], ap[kEpt];
-#pragma unroll
-    for (int e = 0; e < kEpt; ++e) {
-      const int r = max(row[e], 0);
-      d1[e] = mind[r];
-      d2[e] = mind2[r];
-      an[e] = assign[r];
-      ap[e] = a_prev[r];
-    }
-#pragma unroll
-    for (int e = 0; e < kEpt; ++e) {
-      bool ch = false;
-      if (row[e] >= 0) {
-        u[row[e]] = up1(sqrtf(up1(fmaxf(d1[e], 0.f) + tol)));
-        l[row[e]] = fmaxf(dn1(sqrtf(fmaxf(dn1(d2[e] - tol), 0.f))), 0.f);
-        ch = an[e] != ap[e];
-      }
-      const uint64_t mask = __ballot(ch);
-      if (mask != 0) {
-        const int lane = __lane_id();
-        const int leader = __ffsll((long long)mask) - 1;
-        int b = 0;
-        if (lane == leader) b = atomicAdd(&s_cnt, __popcll(mask));
-        b = __shfl(b, leader);
-        if (ch) {
-          const uint64_t below = lane == 0 ? 0ull : (mask & (~0ull >> (64 - lane)));
-          s_buf[b + __popcll(below)] = row[e];
-        }
-      }
-    }
-    __syncthreads();
-    if (s_cnt > kDiffBuf - kDiffThreads * kEpt) flush();
-  }
-  flush();
-}
-
 // Q[c] = sum over rows assigned to c of |x|^2 = 2 xh (f64; LDS histogram per block,
 // k <= 2048, then one global add per cluster and block)
 __global__ void __launch_bounds__(256)
@@ -322,6 +245,22 @@ km_centre_bounds_kernel(const T* __restrict__ cnow, const T* __restrict__ cprev,
   }
 }
 
+// Bounds after the full first pass: tol = 2 M 2^-14 with M = max 0.5|x|^2 * 1.0001 + 1e-6
+// (slack of a truncated kernel distance; xmax = the float bits K2 max-reduced),
+// u = sqrt(dist + tol) rounded up, l = sqrt(dist2 - tol) rounded down. One pass.
+__global__ void __launch_bounds__(256)
+km_bounds_init_kernel(const float* __restrict__ mind, const float* __restrict__ mind2,
+                      const unsigned* __restrict__ xmax, int64_t n, float* __restrict__ u,
+                      float* __restrict__ l, float* __restrict__ tol_out) {
+  const float M = __uint_as_float(*xmax) * 1.0001f + 1e-6f;
+  const float tol = up1(2.f * M * 6.103515625e-05f);   // 2^-14
+  if (blockIdx.x == 0 && threadIdx.x == 0) *tol_out = tol;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    u[i] = up1(sqrtf(up1(fmaxf(mind[i], 0.f) + tol)));
+    l[i] = fmaxf(dn1(sqrtf(fmaxf(dn1(mind2[i] - tol), 0.f))), 0.f);
+  }
+}
+
 }  // namespace
 }  // namespace dalgo
 
@@ -348,6 +287,16 @@ hipError_t dalgo_km_filter(const int32_t* assign, float* u, float* l, const floa
   return hipGetLastError();
 }
 
+hipError_t dalgo_km_bounds_init(const float* mind, const float* mind2, const unsigned* xmax,
+                                int64_t n, float* u, float* l, float* tol, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  int64_t g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(dalgo::km_bounds_init_kernel, dim3((unsigned)g), dim3(256), 0, st, mind, mind2,
+                     xmax, n, u, l, tol);
+  return hipGetLastError();
+}
+
 hipError_t dalgo_km_centre_bounds(const void* cnow, const void* cprev, int is_bf16, int k, int d,
                                   int DP, float* delta, float* s, hipStream_t st) {
   if (k <= 0) return hipSuccess;
@@ -358,19 +307,6 @@ hipError_t dalgo_km_centre_bounds(const void* cnow, const void* cprev, int is_bf
   else
     hipLaunchKernelGGL(dalgo::km_centre_bounds_kernel<float>, dim3(k), dim3(256), 0, st,
                        (const float*)cnow, (const float*)cprev, k, d, DP, delta, s);
-  return hipGetLastError();
-}
-
-hipError_t dalgo_km_post(const int32_t* idx, int64_t m, const int32_t* assign, const int32_t* a_prev,
-                         const float* mind, const float* mind2, float tol, float* u, float* l,
-                         int32_t* changed, unsigned long long* n_changed, int64_t cap,
-                         const unsigned long long* mdev, const float* tolp, hipStream_t st) {
-  if (m <= 0) return hipSuccess;
-  int64_t g = (m + dalgo::kDiffThreads - 1) / dalgo::kDiffThreads;
-  if (g > 2048) g = 2048;
-  hipLaunchKernelGGL(dalgo::km_post_kernel, dim3((unsigned)g), dim3(dalgo::kDiffThreads), 0, st,
-                     idx, m, assign, a_prev, mind, mind2, tol, u, l, changed, n_changed, cap, mdev,
-                     tolp);
   return hipGetLastError();
 }
 

@@ -28,8 +28,6 @@
 
 namespace dalgo {
 
-constexpr int kXcds = 8;   // MI355X: 8 XCDs, blocks dealt round-robin over them
-
 // ---------------------------------------------------------------------------
 // R-MAT edge generator: edge e of stream (seed, 7): 2 Philox calls -> 8 x 32-bit
 // words; each byte picks one quadrant level (8-bit probabilities).
@@ -91,53 +89,26 @@ __device__ __forceinline__ void flush_run(float* acc, int32_t* pres, int key, fl
   }
 }
 
-// HOT > 0: the contributions of sources [0, HOT) -- the hottest ones after the degree
-// relabeling -- are staged in LDS once per block and read with ds_read instead of a
-// global gather. The gather is bound by the vector-memory address path, not by bytes:
-// splitting the sources over the XCDs' L2s (K4x) cut the fabric reads 3x (62 -> 21 GB,
-// L2 hit 54 -> 82 %) at unchanged time and unchanged TA_BUSY (86 %), so the way to go
-// faster is to take gathers off that path (profiles/round3/pmc_pagerank.md).
-// PIPE: the next window's edge stream (src, dst) is loaded before this window's gathers,
-// so a wave keeps one stream load in flight under its gathers instead of two dependent
-// round trips per window.
-template <int NW, bool NT, bool ACC, int HOT = 0, bool PIPE = false>
+// The gather c[src] bounds this kernel on the vector-memory address path, not on bytes:
+// measured and removed (profiles/round3/pmc_pagerank.md, profiles/round3/logs): an
+// XCD-partitioned form with the edges split by source line over the 8 L2s (fabric reads
+// 62 -> 21 GB, time unchanged), a hot-source LDS table and a software-pipelined edge
+// stream (both within 3 % or slower). The blocked form (pr_binned.hip) removes the
+// random gather altogether and is the default.
+template <int NW, bool NT, bool ACC>
 __global__ void __launch_bounds__(NW * 64)
 pr_spmv_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dstl, int64_t E,
-               const float* __restrict__ c, float* __restrict__ acc, int32_t* __restrict__ pres,
-               int64_t n_c) {
+               const float* __restrict__ c, float* __restrict__ acc, int32_t* __restrict__ pres) {
   // dstl: destination as LOCAL row index. E is padded to a multiple of 4 with
   // (src = -1, dst = -1) edges. Windows of 256 edges, 4 consecutive per lane.
-  __shared__ float s_hot[HOT > 0 ? HOT : 1];
-  if constexpr (HOT > 0) {
-    for (int i = threadIdx.x; i < HOT; i += NW * 64) s_hot[i] = i < n_c ? c[i] : 0.f;
-    __syncthreads();
-  }
   const int lane = threadIdx.x & 63;
   const int64_t nwin = (E + 255) / 256;
   const int64_t wave = (int64_t)blockIdx.x * NW + (threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * NW;
-  int4 s4n = make_int4(-1, -1, -1, -1), d4n = make_int4(-1, -1, -1, -1);
-  if constexpr (PIPE) {
-    const int64_t e0 = wave * 256 + 4 * lane;
-    if (wave < nwin && e0 < E) {
-      s4n = ld_int4<NT>(src + e0);
-      d4n = ld_int4<NT>(dstl + e0);
-    }
-  }
   for (int64_t wi = wave; wi < nwin; wi += nwaves) {
     const int64_t e0 = wi * 256 + 4 * lane;
     int4 s4 = make_int4(-1, -1, -1, -1), d4 = make_int4(-1, -1, -1, -1);
-    if constexpr (PIPE) {
-      s4 = s4n;
-      d4 = d4n;
-      const int64_t e1 = (wi + nwaves) * 256 + 4 * lane;
-      s4n = make_int4(-1, -1, -1, -1);
-      d4n = make_int4(-1, -1, -1, -1);
-      if (wi + nwaves < nwin && e1 < E) {
-        s4n = ld_int4<NT>(src + e1);
-        d4n = ld_int4<NT>(dstl + e1);
-      }
-    } else if (e0 < E) {
+    if (e0 < E) {
       s4 = ld_int4<NT>(src + e0);
       d4 = ld_int4<NT>(dstl + e0);
     }
@@ -145,12 +116,7 @@ pr_spmv_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dstl
     const int dv[4] = {d4.x, d4.y, d4.z, d4.w};
     float cv[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if constexpr (HOT > 0)
-        cv[j] = (sv[j] < 0) ? -1.f : (sv[j] < HOT ? s_hot[sv[j]] : c[sv[j]]);
-      else
-        cv[j] = (sv[j] >= 0) ? c[sv[j]] : -1.f;
-    }
+    for (int j = 0; j < 4; ++j) cv[j] = (sv[j] >= 0) ? c[sv[j]] : -1.f;
     // keys of the edges just outside the window (row continuation tests)
     int dprev = -2, dnext = -2;
     if (lane == 0 && wi > 0) dprev = dstl[wi * 256 - 1];
@@ -220,155 +186,6 @@ pr_spmv_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dstl
   }
 }
 
-// ---------------------------------------------------------------------------
-// XCD-partitioned pull SpMV (K4x). The gather c[src] is what bounds K4: at R-MAT scale
-// 26 the L2 hit rate is 54 % and the fabric reads are 62 GB per iteration (7.3x the
-// 8.5 GB edge stream), ~6 TB/s (profiles/round3/pmc_pagerank.md). Each XCD has its own
-// 4 MiB L2, and every XCD gathers from the whole 256 MB contribution vector, so all
-// eight L2s hold the SAME hottest ~1M sources. Here the edges are split by the 128-B
-// line of their source, part(src) = (src >> 5) & 7, into 8 lists (each sorted by
-// (dst, src), padded to whole 256-edge windows) and part x is swept by the blocks with
-// blockIdx % 8 == x, which the dispatcher deals to one XCD: that L2 then only ever
-// holds lines of part x, so the eight L2s together cache the hottest ~8M sources
-// instead of ~1M (analytic R-MAT share of edge sources: top 1M 73 %, top 8M 95 %).
-// Placement is a speed property only: any block->XCD mapping gives the same result.
-// A destination row is now split over up to 8 parts, so each part accumulates into its
-// own array acc_x (n_stride floats per part). Presence is the sign of -0.0: acc_x starts
-// at -0.0f, a row (or row piece) with >= 1 record stores / adds a sum of c >= +0, which
-// clears the sign; pr_update_xcd sums the parts in part order (deterministic) and resets
-// them to -0.0f for the next iteration.
-template <int NW, bool NT>
-__global__ void __launch_bounds__(NW * 64)
-pr_spmv_xcd_kernel(const int32_t* __restrict__ src_all, const int32_t* __restrict__ dst_all,
-                   const int64_t* __restrict__ part_base, const float* __restrict__ c,
-                   float* __restrict__ acc_all, int64_t n_stride) {
-  const int x = blockIdx.x % kXcds;
-  const int64_t base = part_base[x];
-  const int64_t E = part_base[x + 1] - base;
-  const int32_t* src = src_all + base;
-  const int32_t* dstl = dst_all + base;
-  float* acc = acc_all + (int64_t)x * n_stride;
-  const int lane = threadIdx.x & 63;
-  const int64_t nwin = (E + 255) / 256;
-  const int64_t wave = (int64_t)(blockIdx.x / kXcds) * NW + (threadIdx.x >> 6);
-  const int64_t nwaves = (int64_t)(gridDim.x / kXcds) * NW;
-  auto flush = [&](int key, float v, int f, bool partial) {
-    if (key < 0) return;
-    if (partial) {
-      if (f) atomicAdd(&acc[key], v);        // -0.0 + (>= +0) = +0: presence
-    } else {
-      acc[key] = f ? v : -0.0f;
-    }
-  };
-  for (int64_t wi = wave; wi < nwin; wi += nwaves) {
-    const int64_t e0 = wi * 256 + 4 * lane;
-    int4 s4 = make_int4(-1, -1, -1, -1), d4 = make_int4(-1, -1, -1, -1);
-    if (e0 < E) {
-      s4 = ld_int4<NT>(src + e0);
-      d4 = ld_int4<NT>(dstl + e0);
-    }
-    const int sv[4] = {s4.x, s4.y, s4.z, s4.w};
-    const int dv[4] = {d4.x, d4.y, d4.z, d4.w};
-    float cv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cv[j] = (sv[j] >= 0) ? c[sv[j]] : -1.f;
-    int dprev = -2, dnext = -2;
-    if (lane == 0 && wi > 0) dprev = dstl[wi * 256 - 1];
-    if (lane == 63 && wi * 256 + 256 < E) dnext = dstl[wi * 256 + 256];
-    dprev = __builtin_amdgcn_readlane(dprev, 0);
-    dnext = __builtin_amdgcn_readlane(dnext, 63);
-    const int wk_first = __builtin_amdgcn_readlane(dv[0], 0);
-    const int wk_last = __builtin_amdgcn_readlane(dv[3], 63);
-    auto partial_key = [&](int key) {
-      return (key == wk_first && key == dprev) || (key == wk_last && key == dnext);
-    };
-    const int k0 = dv[0];
-    int key = k0;
-    float run = 0.f;
-    int runf = 0;
-    float head = 0.f;
-    int headf = 0;
-    bool single = true;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (dv[j] != key) {
-        if (single) { head = run; headf = runf; single = false; }
-        else flush(key, run, runf, false);
-        key = dv[j];
-        run = 0.f;
-        runf = 0;
-      }
-      const float v = cv[j];
-      run += (v > 0.f) ? v : 0.f;
-      runf |= (v >= 0.f) ? 1 : 0;
-    }
-    const int kt = key;
-    const int kt_left = __shfl_up(kt, 1);
-    int flag = (!single || lane == 0 || kt_left != k0) ? 1 : 0;
-    float sv_ = run;
-    int sf_ = runf;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const float v2 = __shfl_up(sv_, off);
-      const int f2 = __shfl_up(sf_, off);
-      const int g2 = __shfl_up(flag, off);
-      if (lane >= off && !flag) {
-        sv_ += v2;
-        sf_ |= f2;
-        flag |= g2;
-      }
-    }
-    const float S_left = __shfl_up(sv_, 1);
-    const int F_left = __shfl_up(sf_, 1);
-    const bool cont_left = (lane > 0) && (kt_left == k0);
-    const int k0_right = __shfl_down(k0, 1);
-    const bool cont_right = (lane < 63) && (k0_right == kt);
-    if (!single) {
-      const float hv = head + (cont_left ? S_left : 0.f);
-      const int hf = headf | (cont_left ? F_left : 0);
-      flush(k0, hv, hf, partial_key(k0));
-    }
-    if (!cont_right) flush(kt, sv_, sf_, partial_key(kt));
-  }
-}
-
-// pr_update over the 8 part accumulators (sign of -0.0 = no record from that part);
-// resets every part to -0.0f for the next iteration.
-__global__ void __launch_bounds__(256)
-pr_update_xcd_kernel(float* __restrict__ acc_all, int64_t n_stride,
-                     const int32_t* __restrict__ outdeg, int64_t n, float q, float invN, int mode,
-                     const float* __restrict__ dangling_in, float* __restrict__ r,
-                     float* __restrict__ c, float* __restrict__ dangling_out) {
-  float dl = 0.f;
-  const float dang = (mode == 1 && dangling_in) ? dangling_in[0] : 0.f;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
-       v += (int64_t)gridDim.x * blockDim.x) {
-    float a = 0.f;
-    bool p = false;
-#pragma unroll
-    for (int x = 0; x < kXcds; ++x) {
-      float* ap = acc_all + (int64_t)x * n_stride + v;
-      const float ax = *ap;
-      if (!signbit(ax)) { a += ax; p = true; }
-      *ap = -0.0f;
-    }
-    const int od = outdeg[v];
-    if (mode == 0) {
-      const float rv = p ? q * invN + (1.f - q) * a : -1.f;
-      r[v] = rv;
-      c[v] = (p && od > 0) ? rv / (float)od : -1.f;
-    } else {
-      const float rv = q * invN + (1.f - q) * (a + dang * invN);
-      r[v] = rv;
-      c[v] = od > 0 ? rv / (float)od : 0.f;
-      if (od == 0) dl += rv;
-    }
-  }
-  if (mode == 1 && dangling_out) {
-    dl = wave_sum(dl);
-    if ((threadIdx.x & 63) == 0 && dl != 0.f) atomicAdd(dangling_out, dl);
-  }
-}
 
 // ---------------------------------------------------------------------------
 // fused epilogue: ranks, next contributions, dangling mass
@@ -431,73 +248,13 @@ hipError_t dalgo_pr_spmv(const int32_t* src, const int32_t* dstl, int64_t E, con
   const int64_t nwin = cdiv(E, 256);
   const int grid = (int)std::min<int64_t>(cdiv(nwin, NW), 256 * 16);
   if (grid == 0) return hipSuccess;
-  // edge stream read once per iteration: nt loads (DALGO_NT=0 restores the default policy)
-  const bool nt = env_int("DALGO_NT", 1) != 0;
-  // hot-source LDS table: DALGO_PR_HOT entries (0 = off); 16-wave blocks, 2 per CU
-  const int hot = env_int("DALGO_PR_HOT", 0);
-  if (nt && !accumulate && hot > 0) {
-    constexpr int NWH = 16;
-    const int gh = (int)std::min<int64_t>(cdiv(nwin, NWH), 2 * 256);
-#define DALGO_PR_HOT_LAUNCH(H)                                                                   \
-    if (hot == H) {                                                                              \
-      hipLaunchKernelGGL((pr_spmv_kernel<NWH, true, false, H>), dim3(gh), dim3(NWH * 64), 0, st, \
-                         src, dstl, E, c, acc, pres, n_c);                                       \
-      DALGO_LAUNCH_CHECK();                                                                      \
-      return hipSuccess;                                                                         \
-    }
-    DALGO_PR_HOT_LAUNCH(8192)
-    DALGO_PR_HOT_LAUNCH(16384)
-    DALGO_PR_HOT_LAUNCH(32768)
-#undef DALGO_PR_HOT_LAUNCH
-    return hipErrorInvalidValue;
-  }
-  if (nt && !accumulate && env_int("DALGO_PR_PIPE", 0) != 0) {   // measured slower (10.65 vs 10.33 ms)
-    hipLaunchKernelGGL((pr_spmv_kernel<NW, true, false, 0, true>), dim3(grid), dim3(NW * 64), 0, st,
-                       src, dstl, E, c, acc, pres, n_c);
-    DALGO_LAUNCH_CHECK();
-    return hipSuccess;
-  }
-  if (nt && accumulate)
+  // edge stream read once per iteration: non-temporal loads
+  if (accumulate)
     hipLaunchKernelGGL((pr_spmv_kernel<NW, true, true>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
-                       E, c, acc, pres, n_c);
-  else if (nt)
+                       E, c, acc, pres);
+  else
     hipLaunchKernelGGL((pr_spmv_kernel<NW, true, false>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
-                       E, c, acc, pres, n_c);
-  else if (accumulate)
-    hipLaunchKernelGGL((pr_spmv_kernel<NW, false, true>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
-                       E, c, acc, pres, n_c);
-  else
-    hipLaunchKernelGGL((pr_spmv_kernel<NW, false, false>), dim3(grid), dim3(NW * 64), 0, st, src, dstl,
-                       E, c, acc, pres, n_c);
-  DALGO_LAUNCH_CHECK();
-  return hipSuccess;
-}
-
-hipError_t dalgo_pr_spmv_xcd(const int32_t* src, const int32_t* dstl, const int64_t* part_base,
-                             int64_t e_max_part, const float* c, float* acc_all, int64_t n_stride,
-                             hipStream_t st) {
-  constexpr int NW = 4;
-  const int64_t nwin = cdiv(e_max_part, 256);
-  const int per_part = (int)std::min<int64_t>(cdiv(nwin, NW), 512);
-  if (per_part == 0) return hipSuccess;
-  const bool nt = env_int("DALGO_NT", 1) != 0;
-  if (nt)
-    hipLaunchKernelGGL((pr_spmv_xcd_kernel<NW, true>), dim3(per_part * kXcds), dim3(NW * 64), 0, st,
-                       src, dstl, part_base, c, acc_all, n_stride);
-  else
-    hipLaunchKernelGGL((pr_spmv_xcd_kernel<NW, false>), dim3(per_part * kXcds), dim3(NW * 64), 0, st,
-                       src, dstl, part_base, c, acc_all, n_stride);
-  DALGO_LAUNCH_CHECK();
-  return hipSuccess;
-}
-
-hipError_t dalgo_pr_update_xcd(float* acc_all, int64_t n_stride, const int32_t* outdeg, int64_t n,
-                               float q, float invN, int mode, const float* dangling_in, float* r,
-                               float* c, float* dangling_out, hipStream_t st) {
-  const int grid = (int)std::min<int64_t>(cdiv(n, 256), 256 * 8);
-  if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL(pr_update_xcd_kernel, dim3(grid), dim3(256), 0, st, acc_all, n_stride, outdeg,
-                     n, q, invN, mode, dangling_in, r, c, dangling_out);
+                       E, c, acc, pres);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -81,7 +81,7 @@ __device__ __forceinline__ void scan_step(float& a, int& h, int& c0, int& c1) {
 // step. The step body is branch-free up to the entry stores (loads from clamped
 // addresses, selects instead of guarded reads), so the compiler's wait counts stay exact
 // and the prefetched loads stay in flight.
-template <int S, int R, int NW, bool GRUNS, int PROBE = 0>
+template <int S, int R, int NW, bool GRUNS>
 __global__ void __launch_bounds__(NW * 64)
 pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ tile_e,
                  const int32_t* __restrict__ tile_ent, const int32_t* __restrict__ tile_run,
@@ -170,8 +170,7 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
       for (int k = 0; k < EPL; ++k) {
         const uint32_t h = (ww[k >> 1] >> (16 * (k & 1))) & 0xffffu;
         hk[k] = (idx + k >= e_lo && idx + k < e_hi) ? h : 0u;
-        if constexpr (PROBE == 2) cv[k] = 1.0f;          // timing probe: no LDS reads
-        else cv[k] = s_c[hk[k] & (S - 1)];
+        cv[k] = s_c[hk[k] & (S - 1)];
       }
       float part = -0.0f, outv[EPL];
       int nf = 0, nm = 0;
@@ -228,13 +227,11 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
       // line group, so no single address is hammered by every wave): a fixed store count
       // keeps the compiler's vmcnt bookkeeping exact, so the D prefetched loads are not
       // drained at every step
-      if constexpr (PROBE != 1) {                       // PROBE 1: timing without stores
 #pragma unroll
-        for (int q = 0; q < EPL; ++q) {
-          const int qi = lane + 64 * q;
-          const bool ok = qi < n_step;
-          val[ok ? (int64_t)sp[qi] : dummy] = ok ? sv[qi] : 0.f;
-        }
+      for (int q = 0; q < EPL; ++q) {
+        const int qi = lane + 64 * q;
+        const bool ok = qi < n_step;
+        val[ok ? (int64_t)sp[qi] : dummy] = ok ? sv[qi] : 0.f;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -423,29 +420,22 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
   }
   if ((phases & 1) && nch > 0 && wu_hi > wu_lo) {
     // max_runs: the largest number of non-empty runs of one chunk (LDS table up to 4096)
-    // DALGO_PB_PROBE (timing only, wrong results): 1 = no entry stores, 2 = no c reads
-    const int probe = env_int("DALGO_PB_PROBE", 0);
-#define DALGO_PB_GATHER(GR, PR)                                                                  \
-    hipLaunchKernelGGL((pb_gather_kernel<8192, 4096, 8, GR, PR>), dim3(wu_hi - wu_lo), dim3(8 * 64), 0, st, \
+#define DALGO_PB_GATHER(GR)                                                                      \
+    hipLaunchKernelGGL((pb_gather_kernel<8192, 4096, 8, GR>), dim3(wu_hi - wu_lo), dim3(8 * 64), 0, st, \
                        srcl, tile_e, tile_ent, tile_run, wu_tile, wu_chunk, chunk_slo, chunk_ns, \
                        chunk_run, run_delta, c, val, n_val - kPbDummy, bound, wu_lo)
-    if (max_runs > 4096) DALGO_PB_GATHER(true, 0);
-    else if (probe == 1) DALGO_PB_GATHER(false, 1);
-    else if (probe == 2) DALGO_PB_GATHER(false, 2);
-    else DALGO_PB_GATHER(false, 0);
+    if (max_runs > 4096) DALGO_PB_GATHER(true);
+    else DALGO_PB_GATHER(false);
 #undef DALGO_PB_GATHER
     DALGO_LAUNCH_CHECK();
   }
   if (!(phases & 2) || nwi == 0) return hipSuccess;
   const PbOut o{acc, pres, outdeg, r, cn, dang_in, dang_out, q, invN, mode};
   if (bin_width == 16384) {
-    // DALGO_PB_U8=1: 8 groups of 4 entries in flight per thread (A/B knob)
-    if (env_int("DALGO_PB_U8", 0))
-      hipLaunchKernelGGL((pb_accum_kernel<16384, 16, 8>), dim3(nwi), dim3(16 * 64), 0, st, val, dloc,
-                         wi_bin, wi_lo, wi_slab, n_local, bound, o, slab);
-    else
-      hipLaunchKernelGGL((pb_accum_kernel<16384, 16>), dim3(nwi), dim3(16 * 64), 0, st, val, dloc,
-                         wi_bin, wi_lo, wi_slab, n_local, bound, o, slab);
+    // 4 groups of 4 entries in flight per thread (8 groups measured slower,
+    // profiles/round3/pb/)
+    hipLaunchKernelGGL((pb_accum_kernel<16384, 16>), dim3(nwi), dim3(16 * 64), 0, st, val, dloc,
+                       wi_bin, wi_lo, wi_slab, n_local, bound, o, slab);
     DALGO_LAUNCH_CHECK();
     if (nsplit > 0)
       hipLaunchKernelGGL(pb_combine_kernel<16384>, dim3(16384 / 256, nsplit), dim3(256), 0, st,

@@ -25,6 +25,19 @@ struct DalgoLrTail {
   double spin_s;
 };
 
+// Filtered k-means iteration (kmeans.hip dalgo_kmeans_assign_idx): the K2 epilogue
+// updates the Hamerly bounds and collects the rows whose cluster changed
+struct DalgoKmPost {
+  const unsigned long long* mcount;   // active rows (device, written by km_filter)
+  const int* a_prev;                  // their cluster before this iteration
+  const float* tol;                   // distance slack (device)
+  float* u;
+  float* l;
+  int* changed;
+  unsigned long long* n_changed;      // zeroed by the caller
+  long long cap;
+};
+
 extern "C" {
 
 // ---- K1/K7/K10 logistic regression (lr_grad.hip)
@@ -103,12 +116,6 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
                          const int32_t* split_count, int nsplit, const int32_t* outdeg, float q,
                          float invN, int mode, const float* dang_in, float* r, float* cn,
                          float* dang_out, hipStream_t st);
-hipError_t dalgo_pr_spmv_xcd(const int32_t* src, const int32_t* dstl, const int64_t* part_base,
-                             int64_t e_max_part, const float* c, float* acc_all, int64_t n_stride,
-                             hipStream_t st);
-hipError_t dalgo_pr_update_xcd(float* acc_all, int64_t n_stride, const int32_t* outdeg, int64_t n,
-                               float q, float invN, int mode, const float* dangling_in, float* r,
-                               float* c, float* dangling_out, hipStream_t st);
 hipError_t dalgo_pr_update(const float* acc, const int32_t* pres, const int32_t* outdeg, int64_t n,
                            float q, float invN, int mode, const float* dangling_in, float* r,
                            float* c, float* dangling_out, hipStream_t st);
@@ -120,19 +127,16 @@ hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, 
 hipError_t dalgo_km_filter(const int32_t* assign, float* u, float* l, const float* delta,
                            const float* s, int k, int64_t n, int32_t* a_prev, int32_t* idx,
                            unsigned long long* n_active, int64_t cap, hipStream_t st);
-hipError_t dalgo_km_post(const int32_t* idx, int64_t m, const int32_t* assign, const int32_t* a_prev,
-                         const float* mind, const float* mind2, float tol, float* u, float* l,
-                         int32_t* changed, unsigned long long* n_changed, int64_t cap,
-                         const unsigned long long* mdev, const float* tolp, hipStream_t st);
 hipError_t dalgo_km_centre_bounds(const void* cnow, const void* cprev, int is_bf16, int k, int d,
                                   int DP, float* delta, float* s, hipStream_t st);
 hipError_t dalgo_km_qsum(const int32_t* assign, const float* xh, int64_t n, int k, double* Q,
                          hipStream_t st);
 hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP, const void* Cq,
                                    const float* hn, int kpad, const int32_t* idx, int* assign,
-                                   float* mind, float* mind2, double* sse, int sse_mask,
-                                   const unsigned long long* mcount, float* xh, unsigned* xmax,
-                                   hipStream_t st);
+                                   float* mind, float* mind2, double* sse, int sse_mask, float* xh,
+                                   unsigned* xmax, const DalgoKmPost* post, hipStream_t st);
+hipError_t dalgo_km_bounds_init(const float* mind, const float* mind2, const unsigned* xmax,
+                                int64_t n, float* u, float* l, float* tol, hipStream_t st);
 
 // ---- K9 sparse closure round on a device hash set (tc_sparse.hip)
 hipError_t dalgo_tcs_degree(const uint64_t* keys, int64_t d0, int64_t nd, const int64_t* in_ptr,

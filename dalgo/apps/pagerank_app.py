@@ -108,6 +108,11 @@ def main(argv=None):
     ap.add_argument("--rmat-scale", type=int, default=None, help="synthetic Graph500 R-MAT graph")
     ap.add_argument("--edge-factor", type=int, default=16)
     ap.add_argument("--top", type=int, default=20, help="print only the top ranks of large graphs")
+    ap.add_argument("--spmv", choices=["blocked", "pull"], default=None,
+                    help="SpMV form (default: blocked K4b on GPUs, pull on the CPU)")
+    ap.add_argument("--exchange", choices=["ghost", "allgather"], default="ghost")
+    ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
+                    help="ghost exchange under the own-source SpMV")
     add_ckpt_args(ap)
     a = ap.parse_args(argv)
     rt = init_from_args(a, "PageRank")
@@ -123,7 +128,8 @@ def main(argv=None):
         s, d, ids = compact_ids(src.long(), dst.long())
         shard = G.build_shard(s.to(torch.int32).to(rt.device), d.to(torch.int32).to(rt.device),
                               len(ids), rt.rank, rt.world_size)
-    pr = PageRank(PageRankConfig(q=a.q, n_iterations=a.n_iterations, semantics=a.semantics),
+    pr = PageRank(PageRankConfig(q=a.q, n_iterations=a.n_iterations, semantics=a.semantics,
+                                 spmv=a.spmv or "", exchange=a.exchange, overlap=a.overlap),
                   shard, rt.world_size)
     if a.resume and a.ckpt_dir:
         sd = checkpoint.load(a.ckpt_dir, "pagerank_state", rt.rank, per_rank=True)

@@ -129,8 +129,8 @@ class KMeans:
         self._cq_prev = torch.empty((k, self.DP), dtype=self.cen.Cq.dtype, device=self.dev)
         self._delta = torch.empty(k, **f32)
         self._s = torch.empty(k, **f32)
-        self._pinf = torch.full((1,), float("inf"), **f32)   # nextafter directions
-        self._zero = torch.zeros(1, **f32)
+        self._post_args = dict(m_dev=self._n_active, a_prev=self._a_prev, tol=self._tol, u=self._u,
+                               l=self._l, changed=self._changed, n_changed=self._n_changed)
 
     def _ph(self, name: str):
         return self.timer.phase(name) if self.timer is not None else NULL_PHASE
@@ -182,8 +182,9 @@ class KMeans:
         if u + delta[a] < max(s[a], l - maxd) (s[a] = half the distance from c_a to its
         nearest other centre) c_a is still strictly the closest centre and x keeps it
         without computing any distance (Hamerly, "Making k-means even faster", 2010).
-        The other points go through K2 (row indirection, top-2 epilogue) and the moved
-        ones through the incremental K3. The SSE comes from the identity
+        The other points go through K2 (row indirection, top-2 epilogue that also
+        updates their bounds and collects the moved rows) and the moved ones through the
+        incremental K3. The SSE comes from the identity
         sum_c (Q_c - 2 c.S_c + n_c |c|^2) with Q_c the per-cluster sum of |x|^2,
         maintained with the sums. No host sync: the active / moved counts stay on the
         device."""
@@ -199,15 +200,8 @@ class KMeans:
                 self._S64.copy_(self.S)
                 self._cnt64.copy_(self.cnt)
                 K.cluster_sq_sums(self.assign, self._xh, k, self._Q)
-            # tol = 2 M 2^-14, M >= max 0.5|x|^2 (slack of a truncated kernel distance)
-            M = self._xmax.view(torch.float32) * 1.0001 + 1e-6
-            torch.mul(M, 2.0 * 2.0 ** -14, out=self._tol)
-            up, dn = self._pinf, self._zero
-            torch.nextafter(torch.sqrt(torch.nextafter(self._mind[:n].clamp_min(0) + self._tol, up)),
-                            up, out=self._u[:n])
-            torch.nextafter(torch.sqrt((self._mind2[:n] - self._tol).clamp_min(0)), dn,
-                            out=self._l[:n])
-            self._l[:n].clamp_min_(0)
+            # u / l from the K2 distances, tol = 2 M 2^-14 from the K2 max of 0.5|x|^2
+            K.bounds_init(self._mind, self._mind2, self._xmax, n, self._u, self._l, self._tol)
             self._record(0, n)
             self._record(1, 0)
             self._first = False
@@ -216,13 +210,12 @@ class KMeans:
             with self._ph("filter"):
                 K.filter_rows(self.assign, self._u, self._l, self._delta, self._s, self._a_prev,
                               self._idx, self._n_active)
+            self._n_changed.zero_()
             with self._ph("assign"):
-                K.assign_rows(self.X, self.cen, self._idx, n, self.assign, self._mind, self._mind2,
-                              m_dev=self._n_active)
-            with self._ph("post"):
-                K.post_rows(self._idx, n, self.assign, self._a_prev, self._mind, self._mind2, 0.0,
-                            self._u, self._l, self._changed, self._n_changed,
-                            m_dev=self._n_active, tol_dev=self._tol)
+                # K2 over the active rows; its epilogue updates u / l and collects the
+                # rows whose cluster changed
+                K.assign_rows(self.X, self.cen, self._idx, n, self.assign,
+                              post=self._post_args)
             with self._ph("accumulate_incremental"):
                 K.move_rows(self.X, self.DP, self._changed, self._n_changed, self.assign,
                             self._a_prev, self._S64, self._cnt64, self._mws, self._xh, self._Q)

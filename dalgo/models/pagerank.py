@@ -22,7 +22,6 @@ vertices and dangling mass redistributed.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 
 import torch
@@ -37,14 +36,15 @@ class PageRankConfig:
     q: float = 0.15              # teleport probability (pagerank.py:19)
     n_iterations: int = 10       # pagerank.py:18
     semantics: str = "reference"  # "reference" | "standard"
-    spmv: str = ""               # "blocked" | "pull" | "xcd" ("" = DALGO_PR_SPMV env,
-                                 # default blocked on GPUs (K4b), pull on the CPU)
+    spmv: str = ""               # "blocked" | "pull" ("" = blocked (K4b) on GPUs, pull on
+                                 # the CPU)
     bin_width: int = 16384       # blocked: destination vertices per LDS bin (8192 | 16384)
     chunk: int = 1 << 40         # blocked: ~edges per source chunk (<= 8192 sources; default:
                                  # no edge cut, the work units balance phase 1)
     tile: int = 16384            # blocked: ~edges per phase-1 wave tile
-    exchange: str = ""           # "ghost" | "allgather" ("" = DALGO_PR_EXCHANGE env, default
-                                 # ghost on several ranks with the pull SpMV)
+    exchange: str = "ghost"      # "ghost" | "allgather" (several ranks)
+    overlap: str = "auto"        # ghost exchange under the own-source SpMV: "auto" | "on" | "off"
+    fuse_update: bool = True     # K4b: rank / contribution update in the SpMV epilogue
 
 
 class PageRank:
@@ -63,8 +63,9 @@ class PageRank:
         comm.all_reduce_sum(od_full)
         self.outdeg = od_full[shard.v_lo: shard.v_hi].contiguous()
         self.mode = 0 if cfg.semantics == "reference" else 1
-        self.spmv = cfg.spmv or os.environ.get("DALGO_PR_SPMV",
-                                               "blocked" if dev.type == "cuda" else "pull")
+        self.spmv = cfg.spmv or ("blocked" if dev.type == "cuda" else "pull")
+        if self.spmv not in ("blocked", "pull"):
+            raise ValueError(f"spmv must be 'blocked' or 'pull' (got {self.spmv!r})")
         if self.mode == 0:
             self.N = int((od_full > 0).sum().item())
         else:
@@ -77,8 +78,7 @@ class PageRank:
         self.acc = torch.zeros(nl, dtype=fdt, device=dev)
         self.pres = torch.zeros(nl, dtype=torch.int32, device=dev)
         self.r = torch.zeros(nl, dtype=fdt, device=dev)
-        ex = cfg.exchange or os.environ.get("DALGO_PR_EXCHANGE", "ghost")
-        self.exchange = ex if world > 1 else "allgather"
+        self.exchange = cfg.exchange if world > 1 else "allgather"
         if self.exchange == "ghost":
             self._build_ghosts()
             # own slice first, then the ghosts: c_slice is a view, so the update kernel's
@@ -92,8 +92,8 @@ class PageRank:
                            else torch.zeros(sl * world, dtype=fdt, device=dev))
         # K4b: built over the edge list the SpMV reads (c_full index space)
         self.layout = None
-        # DALGO_PR_FUSE=0: K4b writes acc / pres and the separate update kernel runs
-        self.fuse_update = os.environ.get("DALGO_PR_FUSE", "1") != "0"
+        # fuse_update=False: K4b writes acc / pres and the separate update kernel runs
+        self.fuse_update = cfg.fuse_update
         if self.spmv == "blocked":
             gsp = self.g_local if self.exchange == "ghost" else self.g
             self.layout = Gops.build_blocked(gsp, cfg.bin_width, cfg.chunk, cfg.tile,
@@ -112,12 +112,6 @@ class PageRank:
                                             torch.zeros_like(od))
             self.dang.fill_(float(((self.outdeg == 0).float() * self.invN).sum().item()))
             comm.all_reduce_sum(self.dang)
-        # XCD-partitioned pull SpMV (K4x): the sources of the graph the SpMV reads
-        # (c_full index space) split into 8 line parts, one per XCD
-        self.xl = None
-        if self.spmv == "xcd" and dev.type == "cuda":
-            gsp = self.g_local if self.exchange == "ghost" else self.g
-            self.xl = Gops.build_xcd(gsp)
         self.t = 0
 
     def _build_ghosts(self):
@@ -176,9 +170,6 @@ class PageRank:
             comm.all_gather_into(self.c_full, self.c_slice)
 
     def _spmv(self):
-        if self.xl is not None:
-            Gops.pr_spmv_xcd(self.xl, self.c_full)
-            return
         if self.layout is not None:
             # K4b writes every destination and, with the update fused into its epilogue
             # (ranks + next contributions), needs no separate update launch
@@ -213,14 +204,9 @@ class PageRank:
             return
         if self.mode == 1:
             self.dang_next.zero_()
-        if self.xl is not None:
-            Gops.pr_update_xcd(self.xl, self.outdeg, self.cfg.q, self.invN, self.mode, self.r,
-                               self.c_slice[:nl], dangling_in=self.dang if self.mode == 1 else None,
-                               dangling_out=self.dang_next if self.mode == 1 else None)
-        else:
-            Gops.pr_update(self.acc, self.pres, self.outdeg, self.cfg.q, self.invN, self.mode, self.r,
-                           self.c_slice[:nl], dangling_in=self.dang if self.mode == 1 else None,
-                           dangling_out=self.dang_next if self.mode == 1 else None)
+        Gops.pr_update(self.acc, self.pres, self.outdeg, self.cfg.q, self.invN, self.mode, self.r,
+                       self.c_slice[:nl], dangling_in=self.dang if self.mode == 1 else None,
+                       dangling_out=self.dang_next if self.mode == 1 else None)
         if self.mode == 1:
             comm.all_reduce_sum(self.dang_next)
             self.dang, self.dang_next = self.dang_next, self.dang
@@ -228,26 +214,26 @@ class PageRank:
     def _overlap_pb(self) -> bool:
         """K4b with the ghost exchange: phase 1 over the own-slice source chunks runs while
         the all_to_all of the ghost contributions is in flight, phase 1 over the ghost
-        chunks after it (DALGO_PR_OVERLAP: auto = when the own-slice units are at least a
-        quarter of all units, 1 / 0 force it on / off)."""
+        chunks after it (cfg.overlap: auto = when the own-slice units are at least a
+        quarter of all units; on / off force it)."""
         if self.layout is None or self.exchange != "ghost":
             return False
-        env = os.environ.get("DALGO_PR_OVERLAP", "auto")
+        ov = self.cfg.overlap
         nwu = int(self.layout.wu_chunk.numel())
-        return env == "1" or (env == "auto" and nwu > 0 and self.layout.n_wu_below >= 0.25 * nwu)
+        return ov == "on" or (ov == "auto" and nwu > 0 and self.layout.n_wu_below >= 0.25 * nwu)
 
     def _overlap(self) -> bool:
         """Ghost exchange under the SpMV over own-slice sources: the all_to_all writes only
         the ghost part of c_full, the first pass reads only the own part, the second adds
         the ghost-source edges into the same rows. Splitting the SpMV costs ~10 % at the
         rank-0 share of R-MAT scale 26 (1.41 -> 1.54 ms at W = 8, 5.42 -> 5.80 ms at W = 2,
-        profiles/round2/README.md), so by default (DALGO_PR_OVERLAP=auto) it is only used
+        profiles/round2/README.md), so by default (cfg.overlap = "auto") it is only used
         while the own-source pass is long enough to hide the exchange: at least a quarter
-        of the edges (W <= 4 with the dealt relabeling). 1 / 0 force it on / off."""
-        if self.exchange != "ghost" or self.xl is not None or self.layout is not None:
+        of the edges (W <= 4 with the dealt relabeling). "on" / "off" force it."""
+        if self.exchange != "ghost" or self.layout is not None:
             return False
-        env = os.environ.get("DALGO_PR_OVERLAP", "auto")
-        return env == "1" or (env == "auto" and self.own_share >= 0.25)
+        ov = self.cfg.overlap
+        return ov == "on" or (ov == "auto" and self.own_share >= 0.25)
 
     def _ph(self, name: str):
         return self.timer.phase(name) if self.timer is not None else NULL_PHASE

@@ -457,73 +457,6 @@ def pr_spmv(shard: GraphShard, c_full: torch.Tensor, acc: torch.Tensor, pres: to
     pres.copy_((hit > 0).to(pres.dtype))
 
 
-# ------------------------------------------------------------------ XCD-partitioned K4
-XCD_PARTS = 8
-
-
-@dataclass
-class XcdLayout:
-    """Edges split into 8 source-line parts for pr_spmv_xcd (csrc/kernels/pagerank.hip):
-    part p holds the edges whose source's 128-B contribution line was assigned to p,
-    each part sorted by (dst, src) and padded to whole 256-edge windows; part p is swept
-    by the blocks with blockIdx % 8 == p (one XCD), so each XCD's L2 caches only its
-    own lines. Lines are dealt to parts by descending edge count in snake order
-    (0..7, 7..0, ...), which balances the parts' edge counts."""
-    src: torch.Tensor        # int32 [E_pad]
-    dstl: torch.Tensor       # int32 [E_pad]
-    base: torch.Tensor       # int64 [9] part offsets (device)
-    counts: list             # real edges per part
-    e_max: int               # largest padded part
-    n_local: int
-    acc: torch.Tensor        # f32 [8, n_local]: per-part sums, -0.0 = no record
-
-
-def build_xcd(shard: GraphShard) -> XcdLayout:
-    E = shard.n_edges
-    dev = shard.src.device
-    s = shard.src[:E]
-    d = shard.dstl[:E]
-    line = (s >> 5).to(torch.int64)
-    n_lines = int(line.max().item()) + 1 if E else 1
-    cnt = torch.bincount(line, minlength=n_lines)
-    order = torch.argsort(cnt, descending=True, stable=True)
-    rank = torch.empty_like(order)
-    rank[order] = torch.arange(n_lines, device=dev)
-    r = rank % (2 * XCD_PARTS)
-    part_of_line = torch.where(r < XCD_PARTS, r, 2 * XCD_PARTS - 1 - r)
-    part = part_of_line[line]
-    perm = torch.argsort(part, stable=True)          # keeps the (dst, src) order per part
-    counts = torch.bincount(part, minlength=XCD_PARTS).tolist()
-    padded = [((c + 255) // 256) * 256 for c in counts]
-    tot = sum(padded)
-    src = torch.full((max(tot, 4),), -1, dtype=torch.int32, device=dev)
-    dstl = torch.full((max(tot, 4),), -1, dtype=torch.int32, device=dev)
-    base, off, o2 = [0], 0, 0
-    ps, pd = s[perm], d[perm]
-    for c, p in zip(counts, padded):
-        src[off: off + c] = ps[o2: o2 + c]
-        dstl[off: off + c] = pd[o2: o2 + c]
-        off += p
-        o2 += c
-        base.append(off)
-    nl = shard.n_local
-    acc = torch.full((XCD_PARTS, max(nl, 1)), -0.0, dtype=torch.float32, device=dev)
-    return XcdLayout(src, dstl, torch.tensor(base, dtype=torch.int64, device=dev), counts,
-                     max(padded), nl, acc)
-
-
-def pr_spmv_xcd(xl: XcdLayout, c_full: torch.Tensor):
-    """Per-part partial sums of the pull SpMV into xl.acc (see XcdLayout)."""
-    _ext.ops().pr_spmv_xcd(xl.src, xl.dstl, xl.base, int(xl.e_max), c_full, xl.acc)
-
-
-def pr_update_xcd(xl: XcdLayout, outdeg_local, q, invN, mode, r, c, dangling_in=None,
-                  dangling_out=None):
-    """pr_update over the part sums (summed in part order; parts reset to -0.0)."""
-    _ext.ops().pr_update_xcd(xl.acc, outdeg_local, float(q), float(invN), int(mode), dangling_in,
-                             r, c, dangling_out)
-
-
 def pr_update(acc, pres, outdeg_local, q, invN, mode, r, c, dangling_in=None, dangling_out=None):
     if acc.is_cuda:
         _ext.ops().pr_update(acc, pres, outdeg_local, float(q), float(invN), int(mode),

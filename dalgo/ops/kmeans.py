@@ -233,27 +233,31 @@ def filter_rows(assign: torch.Tensor, u: torch.Tensor, l: torch.Tensor, delta: t
 
 
 def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
-                assign: torch.Tensor, mind: torch.Tensor, mind2: torch.Tensor | None = None,
-                m_dev: torch.Tensor | None = None, xh: torch.Tensor | None = None,
-                xmax: torch.Tensor | None = None):
-    """K2 (pipelined form) over the rows idx[:m] (all rows when idx is None); assign /
-    mind (and the second-best distance mind2, a lower bound, when given) written at those
-    rows. m_dev: the row count lives on the device (m = its upper bound; top-2 form).
-    xh / xmax: also write 0.5|x|^2 per row and atomically max it into xmax (float bits)."""
-    _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, mind, mind2, m_dev, xh,
-                                 xmax)
+                assign: torch.Tensor, mind: torch.Tensor | None = None,
+                mind2: torch.Tensor | None = None, xh: torch.Tensor | None = None,
+                xmax: torch.Tensor | None = None, post: dict | None = None):
+    """K2 (pipelined form) over the rows idx[:m] (all rows when idx is None).
+
+    Full pass: assign / mind (and the second-best distance mind2, a lower bound, when
+    given) written at those rows; xh / xmax: also 0.5|x|^2 per row and its maximum
+    (float bits). ``post`` = dict(m_dev, a_prev, tol, u, l, changed, n_changed): the
+    filtered-iteration form -- the row count is m_dev (device; m its upper bound) and
+    the epilogue writes the Hamerly bounds u / l (rounded outward, tol on the device)
+    and appends the rows whose cluster differs from a_prev to changed (count in
+    n_changed, which the caller zeroes): no host sync, no separate bound pass."""
+    if post is None:
+        _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, mind, mind2, xh, xmax)
+        return
+    _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, None, None, None, None,
+                                 post["m_dev"], post["a_prev"], post["tol"], post["u"], post["l"],
+                                 post["changed"], post["n_changed"])
 
 
-def post_rows(idx: torch.Tensor, m: int, assign: torch.Tensor, a_prev: torch.Tensor,
-              mind: torch.Tensor, mind2: torch.Tensor, tol: float, u: torch.Tensor,
-              l: torch.Tensor, changed: torch.Tensor, n_changed: torch.Tensor,
-              m_dev: torch.Tensor | None = None, tol_dev: torch.Tensor | None = None) -> None:
-    """u = sqrt(dist + tol), l = sqrt(dist2 - tol) (rounded outward) for the re-assigned
-    rows idx[:m] (m_dev: the device count, m its upper bound; tol_dev: tol on the device);
-    rows whose cluster changed -> changed[:c], c -> n_changed (device; no sync)."""
-    n_changed.zero_()
-    _ext.ops().kmeans_post(idx, int(m), assign, a_prev, mind, mind2, float(tol), u, l, changed,
-                           n_changed, m_dev, tol_dev)
+def bounds_init(mind: torch.Tensor, mind2: torch.Tensor, xmax: torch.Tensor, n: int,
+                u: torch.Tensor, l: torch.Tensor, tol: torch.Tensor):
+    """After the full first pass: tol = 2 M 2^-14 (M from the K2 max of 0.5|x|^2), u =
+    sqrt(dist + tol) rounded up, l = sqrt(dist2 - tol) rounded down (one launch)."""
+    _ext.ops().kmeans_bounds_init(mind, mind2, xmax, int(n), u, l, tol)
 
 
 def cluster_sq_sums(assign: torch.Tensor, xh: torch.Tensor, k: int, Q: torch.Tensor):

@@ -248,7 +248,7 @@ def test_pagerank_rmat_world_size_invariant():
     # sequential exchange + single SpMV pass gives the same ranks
     seq = _top_ranks(_run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
                            "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
-                          + ["--backend", "gloo"], env_extra={"DALGO_PR_OVERLAP": "0"}, timeout=400))
+                          + ["--backend", "gloo", "--overlap", "off"], timeout=400))
     assert set(seq) == set(three) and max(abs(seq[v] - three[v]) for v in seq) < 1e-12
 
 

@@ -681,49 +681,6 @@ def test_kmeans_move_sorted_exact(cuda, d, dtype, k, m):
     assert torch.allclose(Q, Qe, rtol=1e-12, atol=1e-6), (Q - Qe).abs().max()
 
 
-@pytest.mark.parametrize("sem", ["reference", "standard"])
-@pytest.mark.parametrize("scale,edges", [(12, 100_000), (17, 3_000_000)])
-def test_pagerank_xcd_spmv_matches_cpu(cuda, sem, scale, edges):
-    """K4x (8 source-line parts, one per XCD, per-part sums with -0.0 presence) == the f64
-    CPU reference ranks, and == the pull SpMV's present-vertex set."""
-    from dalgo.models.pagerank import PageRank, PageRankConfig
-    s, d = G.rmat_edges(edges, scale, seed=8)
-    nv = 1 << scale
-    rc = PageRank(PageRankConfig(semantics=sem), G.build_shard(s, d, nv, 0, 1)).fit().collect()
-    px = PageRank(PageRankConfig(semantics=sem, spmv="xcd"),
-                  G.build_shard(s.to(cuda), d.to(cuda), nv, 0, 1))
-    assert px.xl is not None and sum(px.xl.counts) == px.g.n_edges
-    # the snake line deal balances the parts
-    assert max(px.xl.counts) <= 1.25 * (sum(px.xl.counts) / 8) + 256
-    rx = px.fit().collect()
-    assert set(rc) == set(rx)
-    assert max(abs(rc[v] - rx[v]) for v in rc) < 1e-6
-
-
-def test_pagerank_xcd_toy(cuda):
-    from dalgo.models.pagerank import PageRank, PageRankConfig
-    src = torch.tensor([1, 1, 2, 3], dtype=torch.int32, device=cuda)
-    dst = torch.tensor([2, 3, 3, 1], dtype=torch.int32, device=cuda)
-    r = PageRank(PageRankConfig(spmv="xcd"), G.build_shard(src, dst, 4, 0, 1)).fit().collect()
-    assert r[1] == pytest.approx(0.38891305880091237, abs=1e-6)
-    assert r[2] == pytest.approx(0.214416470596171, abs=1e-6)
-    assert r[3] == pytest.approx(0.3966704706029163, abs=1e-6)
-
-
-@pytest.mark.parametrize("hot", [8192, 16384, 32768])
-def test_pr_spmv_hot_lds_table(cuda, monkeypatch, hot):
-    """K4 with the hot-source LDS table (sources < HOT read from LDS) == plain K4."""
-    from dalgo.models.pagerank import PageRank, PageRankConfig
-    s, d = G.rmat_edges(2_000_000, 16, seed=3)
-    nv = 1 << 16
-    sh = G.build_shard(s.to(cuda), d.to(cuda), nv, 0, 1)
-    ref = PageRank(PageRankConfig(), sh).fit().collect()
-    monkeypatch.setenv("DALGO_PR_HOT", str(hot))
-    got = PageRank(PageRankConfig(), sh).fit().collect()
-    assert set(ref) == set(got)
-    assert max(abs(ref[v] - got[v]) for v in ref) < 1e-7
-
-
 def test_kmeans_assign_rows_indirect(cuda):
     """K2 with row indirection (only the listed rows) == the full K2 on those rows, and
     leaves every other row's assignment untouched."""
@@ -742,9 +699,9 @@ def test_kmeans_assign_rows_indirect(cuda):
     assert bool((a[~sel] == -7).all()) and bool((mind[sel] > 0).all())
 
 
-def test_kmeans_filter_and_post_match_torch(cuda):
-    """Bound filter (maxd reduced in-kernel from delta, bounds rounded outward) and the
-    post pass with the active count and tol on the DEVICE == torch."""
+def test_kmeans_filter_matches_torch(cuda):
+    """Bound filter (maxd reduced in-kernel from delta, bounds rounded outward) == torch;
+    the active count stays on the device."""
     torch.manual_seed(6)
     n, k = 100_003, 50
     assign = torch.randint(0, k, (n,), dtype=torch.int32, device=cuda)
@@ -769,22 +726,6 @@ def test_kmeans_filter_and_post_match_torch(cuda):
     assert bool((l[~act] <= lb[~act]).all()) and torch.allclose(l[~act], lb[~act])
     assert torch.equal(u[act], u0[act]) and torch.equal(l[act], l0[act])
     assert torch.equal(a_prev[act], assign[act])
-    # post: half of the active rows change cluster; m and tol read on the device
-    new = assign.clone()
-    ch = act & (torch.arange(n, device=cuda) % 2 == 0)
-    new[ch] = (new[ch] + 1) % k
-    mind = torch.rand(n, device=cuda) * 4
-    mind2 = mind + torch.rand(n, device=cuda) * 4
-    changed = torch.empty(n, dtype=torch.int32, device=cuda)
-    nch = torch.zeros(1, dtype=torch.int64, device=cuda)
-    tol = torch.full((1,), 0.5, device=cuda)
-    K.post_rows(idx, n, new, a_prev, mind, mind2, 0.0, u, l, changed, nch, m_dev=cnt, tol_dev=tol)
-    c = int(nch.item())
-    assert c == int(ch.sum())
-    assert torch.equal(torch.sort(changed[:c]).values.long(), torch.nonzero(ch)[:, 0])
-    ue, le = torch.sqrt(mind[act] + 0.5), torch.sqrt((mind2[act] - 0.5).clamp_min(0))
-    assert bool((u[act] >= ue).all()) and torch.allclose(u[act], ue)
-    assert bool((l[act] <= le).all()) and torch.allclose(l[act], le)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
@@ -812,31 +753,63 @@ def test_kmeans_centre_bounds_kernel(cuda, dtype, k, d):
         assert torch.allclose(sg.cpu(), sc, rtol=1e-5)
 
 
-def test_kmeans_assign_rows_device_count(cuda):
-    """Top-2 K2 with the row count on the device (resident-grid tile loop): only
-    idx[:*m_dev] is re-assigned, equal to the full pass on those rows; also the optional
-    0.5|x|^2 / max outputs of a full pass."""
+def test_kmeans_assign_rows_fused_post(cuda):
+    """Filtered-iteration K2 (row count on the device, resident-grid tile loop, fused
+    bound update): only idx[:*m_dev] is re-assigned, equal to the full pass on those
+    rows; u / l bracket the exact distances (rounded outward, tol on the device); the
+    changed rows (vs a_prev) are collected exactly. Also the full pass's optional
+    0.5|x|^2 / max outputs and the bounds-init kernel."""
     torch.manual_seed(9)
     n, d, k = 60_001, 128, 1000
     X = K.prepare_points((torch.randn(n, d) * 3).to(torch.bfloat16).to(cuda))
     cen = K.make_centers(torch.randn(k, d) * 3, torch.bfloat16, cuda)
     full = K.assign(X, cen)
-    rows = torch.randperm(n, device=cuda).to(torch.int32)
-    m = 23_457
-    a = torch.full((n,), -7, dtype=torch.int32, device=cuda)
+    # full pass: top-2 distances, xh, xmax, then the bounds init
+    a0 = torch.empty(n, dtype=torch.int32, device=cuda)
     mind = torch.zeros(n, device=cuda)
     mind2 = torch.zeros(n, device=cuda)
-    K.assign_rows(X, cen, rows, n, a, mind, mind2,
-                  m_dev=torch.tensor([m], dtype=torch.int64, device=cuda))
-    sel = torch.zeros(n, dtype=torch.bool, device=cuda)
-    sel[rows[:m].long()] = True
-    assert torch.equal(a[sel], full[sel]) and bool((a[~sel] == -7).all())
     xh = torch.zeros(n, device=cuda)
     xmax = torch.zeros(1, dtype=torch.int32, device=cuda)
-    K.assign_rows(X, cen, None, n, a, mind, mind2, xh=xh, xmax=xmax)
+    K.assign_rows(X, cen, None, n, a0, mind, mind2, xh=xh, xmax=xmax)
     ref = 0.5 * X[:, :d].float().pow(2).sum(1)
     assert torch.allclose(xh, ref, rtol=1e-5)
     assert float(xmax.view(torch.float32).item()) == pytest.approx(float(ref.max()), rel=1e-5)
+    u0 = torch.empty(n, device=cuda)
+    l0 = torch.empty(n, device=cuda)
+    tol = torch.zeros(1, device=cuda)
+    K.bounds_init(mind, mind2, xmax, n, u0, l0, tol)
+    t = float(tol.item())
+    assert t == pytest.approx(2 * (float(ref.max()) * 1.0001 + 1e-6) * 2 ** -14, rel=1e-5)
+    assert bool((u0 >= torch.sqrt(mind + t)).all()) and bool((l0 <= torch.sqrt((mind2 - t).clamp_min(0))).all())
+    # filtered form over a random subset, a_prev = a perturbed copy of the truth
+    rows = torch.randperm(n, device=cuda).to(torch.int32)
+    m = 23_457
+    a_prev = full.clone()
+    flip = torch.zeros(n, dtype=torch.bool, device=cuda)
+    flip[rows[: m // 3].long()] = True          # a third of the active rows "moved"
+    a_prev[flip] = (a_prev[flip] + 1) % k
+    a = torch.full((n,), -7, dtype=torch.int32, device=cuda)
+    u = torch.full((n,), -1.0, device=cuda)
+    l = torch.full((n,), -1.0, device=cuda)
+    changed = torch.empty(n, dtype=torch.int32, device=cuda)
+    nch = torch.zeros(1, dtype=torch.int64, device=cuda)
+    K.assign_rows(X, cen, rows, n, a, post=dict(
+        m_dev=torch.tensor([m], dtype=torch.int64, device=cuda), a_prev=a_prev, tol=tol, u=u, l=l,
+        changed=changed, n_changed=nch))
+    sel = torch.zeros(n, dtype=torch.bool, device=cuda)
+    sel[rows[:m].long()] = True
+    assert torch.equal(a[sel], full[sel]) and bool((a[~sel] == -7).all())
+    assert bool((u[~sel] == -1).all()) and bool((l[~sel] == -1).all())
+    dist = torch.cdist(X[:, :d].double(), cen.Cq[:k, :d].double())
+    two = torch.topk(dist, 2, dim=1, largest=False).values
+    slack = 2 * t
+    assert bool((u[sel].double() >= two[sel, 0] - 1e-3).all())
+    assert bool((u[sel].double() <= torch.sqrt(two[sel, 0] ** 2 + slack) + 1e-3).all())
+    assert bool((l[sel].double() <= two[sel, 1] + 1e-3).all())
+    c = int(nch.item())
+    exp = torch.nonzero(sel & (full != a_prev))[:, 0]
+    assert c == exp.numel()
+    assert torch.equal(torch.sort(changed[:c]).values.long(), exp)
 
 
 def test_kmeans_assign_top2_second_best(cuda):
