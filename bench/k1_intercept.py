@@ -31,12 +31,10 @@ def run(a):
         seg = torch.tensor([0, rows], dtype=torch.int64, device=dev)
         for blocks in a.blocks:
           for fine in a.fine:
-           for pf in a.pool:
             marker.add_(1.0)          # separator kernel in the trace
             for i in range(REPS):
                 L.lr_grad(X, y, W, seg, D=1024, frac=0.1, step=i, G=G, C=C,
-                          target_blocks=blocks, g_is_zero=True, pool_frac=pf,
-                          variant=L.LR_VARIANT | (fine << 16))
+                          target_blocks=blocks, g_is_zero=True, fine_groups=fine)
             torch.cuda.synchronize()
     print(json.dumps({"done": True, "rows": ROWS, "blocks": a.blocks}))
 
@@ -57,7 +55,7 @@ def parse(d, blocks, fines, pools=(0.0,)):
         elif "OnSelf_add" in n:
             cur = []
             groups.append(cur)
-    cfgs = [(r, b, f, pf) for r in ROWS for b in blocks for f in fines for pf in pools]
+    cfgs = [(r, b, f, 0.0) for r in ROWS for b in blocks for f in fines]
     out = []
     for (rows, b, f, pf), g in zip(cfgs, groups):
         g = sorted(g[5:]) if len(g) > 10 else sorted(g)
@@ -75,11 +73,10 @@ if __name__ == "__main__":
     ap.add_argument("--blocks", type=int, nargs="+", default=[256])
     ap.add_argument("--fine", type=int, nargs="+", default=[0])
     ap.add_argument("--rows", type=int, nargs="+", default=None)
-    ap.add_argument("--pool", type=float, nargs="+", default=[0.0])
     a = ap.parse_args()
     if a.rows:
         ROWS = tuple(a.rows)
     if a.parse:
-        parse(a.parse, a.blocks, a.fine, a.pool)
+        parse(a.parse, a.blocks, a.fine)
     else:
         run(a)

@@ -48,9 +48,7 @@ def main():
     G = torch.zeros(1, 1025, device=dev)
     C = torch.zeros(1, device=dev)
     buf = torch.zeros(1 << 20, dtype=torch.int64, device=dev)
-    L.LR_BALANCED = use_list      # balanced slices of the compacted selection vs the walk
     for rows, fine in [(r, f) for r in rows_list for f in fines]:
-        var = L.LR_VARIANT | (fine << 16)
         X, y = Xall[:rows], yall[:rows]
         seg = torch.tensor([0, rows], dtype=torch.int64, device=dev)
         gx, _ = L._grid(rows, 1)
@@ -58,16 +56,14 @@ def main():
         for rep in range(6):
             for i in range(5):
                 L.lr_grad(X, y, W, seg, D=1024, frac=frac, step=100 * rep + i, G=G, C=C, g_is_zero=True,
-                          variant=var)
+                          fine_groups=fine)
             buf.zero_()
             torch.cuda.synchronize()
             ops.lr_set_trace(buf)
             L.lr_grad(X, y, W, seg, D=1024, frac=frac, step=100 * rep + 50, G=G, C=C, g_is_zero=True,
-                      variant=var)
+                      fine_groups=fine)
             ops.lr_set_trace(None)
             torch.cuda.synchronize()
-            if use_list:
-                gx = [v for v in L._sel_cache.values() if v.n == rows][0].gx
             t = buf[: gx * NW * 8].view(gx, NW, 8).cpu().double()
             t0 = t[:, :, 0].min().item()
             us = lambda v: (v - t0) / 100.0   # noqa: E731

@@ -12,7 +12,7 @@ for set in "${SETS[@]}"; do
   i=$((i+1))
   timeout -k 10 120 rocprofv3 --kernel-trace --pmc $set --kernel-include-regex "scatter|hist|scan|segsum" \
     -d gpurun_out/pmc_k3_$i -o run --output-format csv -- \
-    python3 bench/kmeans_bench.py --rows 20000000 --steps 2 --warmup 1 \
+    python3 bench/kmeans_bench.py --rows 20000000 --iters 3 --no-witness \
     > gpurun_out/pmc_k3_$i.log 2>&1 || { echo "pmc pass $i failed (rc=$?)"; exit 1; }
 done
 echo pmc_k3 done

@@ -287,24 +287,6 @@ void mc_pi(int64_t seed, int64_t stream, int64_t offset, int64_t n, Tensor count
                   "mc_pi");
 }
 
-void hbm_gather_rows(const Tensor& X, const Tensor& idx, Tensor out, int64_t grid) {
-  check_dev(X, "X");
-  check_dev(idx, "idx");
-  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1 && X.stride(0) * X.element_size() >= 2048,
-              "X: 2-D with >= 2 KB rows");
-  TORCH_CHECK(idx.scalar_type() == at::kInt && idx.is_contiguous(), "idx int32");
-  if (idx.numel() > 0) {
-    const int64_t mx = idx.max().item<int>(), mn = idx.min().item<int>();
-    TORCH_CHECK(mn >= 0 && mx < X.size(0), "idx out of range");
-  }
-  TORCH_CHECK(out.scalar_type() == at::kInt && out.numel() >= 1, "out int32[1]");
-  DeviceGuard guard(X.device());
-  DALGO_CHECK_HIP(dalgo_hbm_gather_rows(X.data_ptr(), X.stride(0) * X.element_size(),
-                                        idx.data_ptr<int>(), idx.numel(),
-                                        reinterpret_cast<uint32_t*>(out.data_ptr<int>()), (int)grid,
-                                        cur_stream()),
-                  "hbm_gather_rows");
-}
 
 // diagnostics: per-wave K1 timeline (u64, 8 per wave) for the following lr_grad launches
 
@@ -318,17 +300,6 @@ void lr_set_trace(const c10::optional<Tensor>& buf) {
   }
 }
 
-void hbm_read(const Tensor& src, Tensor out, int64_t unroll) {
-  check_dev(src, "src");
-  check_dev(out, "out");
-  TORCH_CHECK(src.is_contiguous() && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0, "src");
-  TORCH_CHECK(out.scalar_type() == at::kInt && out.numel() >= 1, "out int32[grid]");
-  DeviceGuard guard(src.device());
-  DALGO_CHECK_HIP(dalgo_hbm_read(src.data_ptr(), src.numel() * src.element_size(),
-                                 reinterpret_cast<uint32_t*>(out.data_ptr<int>()), (int)out.numel(),
-                                 (int)unroll, cur_stream()),
-                  "hbm_read");
-}
 
 // ---------------------------------------------------------------------------
 // k-means
@@ -1160,9 +1131,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("als_solve(Tensor R, Tensor F, Tensor Ginv, Tensor(a!) out) -> ()");
   m.def("als_gram(Tensor F, Tensor(a!) G) -> ()");
   m.def("als_residual(Tensor R, Tensor U, Tensor V, Tensor(a!) out) -> ()");
-  m.def("hbm_read(Tensor src, Tensor(a!) out, int unroll=8) -> ()");
   m.def("lr_set_trace(Tensor? buf) -> ()", &lr_set_trace);
-  m.def("hbm_gather_rows(Tensor X, Tensor idx, Tensor(a!) out, int grid=2048) -> ()");
   m.def("mc_pi(int seed, int stream, int offset, int n, Tensor(a!) count) -> ()");
 }
 
@@ -1174,8 +1143,6 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("rows_broadcast", &rows_broadcast);
   m.impl("philox_fill", &philox_fill);
   m.impl("mc_pi", &mc_pi);
-  m.impl("hbm_read", &hbm_read);
-  m.impl("hbm_gather_rows", &hbm_gather_rows);
   m.impl("spd_inverse", &spd_inverse);
   m.impl("als_solve", &als_solve);
   m.impl("als_gram", &als_gram);

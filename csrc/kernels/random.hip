@@ -128,169 +128,6 @@ mc_pi_kernel(uint64_t seed, uint64_t stream, uint64_t offset, uint64_t n,
   }
 }
 
-// HBM read-roofline probe (diagnostics): every 16 B of [p, p+n16*16) read once with
-// dwordx4 loads, UNROLL loads in flight per lane, xor-folded into one word per
-// block so the loads cannot be dead-code eliminated.
-template <int UNROLL>
-__global__ void __launch_bounds__(256)
-hbm_read_kernel(const uint4* __restrict__ p, int64_t n16, uint32_t* __restrict__ out) {
-  uint32_t acc = 0;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + (UNROLL - 1) * stride < n16; i += UNROLL * stride) {
-    uint4 v[UNROLL];
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) v[u] = p[i + u * stride];
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-  }
-  for (; i < n16; i += stride) { uint4 v = p[i]; acc ^= v.x ^ v.y ^ v.z ^ v.w; }
-  acc = wave_sum_u32(acc);
-  if (threadIdx.x == 0) out[blockIdx.x] = acc;
-}
-
-// Probe variant: block b streams its own contiguous region [b*n/G, (b+1)*n/G)
-// (the access shape of a row-sharded sweep), UNROLL x 16 B in flight per lane.
-template <int UNROLL>
-__global__ void __launch_bounds__(256)
-hbm_read_blocked_kernel(const uint4* __restrict__ p, int64_t n16, uint32_t* __restrict__ out) {
-  const int64_t per = (n16 + gridDim.x - 1) / gridDim.x;
-  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(n16, lo + per);
-  uint32_t acc = 0;
-  int64_t i = lo + threadIdx.x;
-  for (; i + (UNROLL - 1) * 256 < hi; i += UNROLL * 256) {
-    uint4 v[UNROLL];
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) v[u] = p[i + u * 256];
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-  }
-  for (; i < hi; i += 256) { uint4 v = p[i]; acc ^= v.x ^ v.y ^ v.z ^ v.w; }
-  acc = wave_sum_u32(acc);
-  if (threadIdx.x == 0) out[blockIdx.x] = acc;
-}
-
-// Probe: the access shape of the SGD minibatch (a sorted list of selected 2-KB rows,
-// ~10 % of the matrix): each wave streams whole rows, 4 rows (8 KB) in flight per
-// wave; the ceiling any K1 design can reach for this pattern.
-__global__ void __launch_bounds__(256)
-hbm_gather_rows_kernel(const uint4* __restrict__ X, int64_t ld16, const int* __restrict__ idx,
-                       int64_t nidx, uint32_t* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-  int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  uint32_t acc = 0;
-  for (; w < nidx; w += 4 * nw) {
-    uint4 v[4][2];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t k = min(w + u * nw, nidx - 1);
-      const uint4* row = X + (int64_t)idx[k] * ld16;
-      v[u][0] = row[lane];
-      v[u][1] = row[64 + lane];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      acc ^= v[u][0].x ^ v[u][0].w ^ v[u][1].y ^ v[u][1].z;
-  }
-  acc = wave_sum_u32(acc);
-  if ((threadIdx.x & 63) == 0) atomicXor(out, acc);
-}
-
-// Probe variants of the same access shape: NT = nt loads into registers, and LDS-DMA
-// (global_load_lds_dwordx4, nt or default policy) into a per-wave ring of DEPTH rows
-// (2 KB each), each row read back from LDS once — the load path a K1 built on LDS-DMA
-// would use. Each wave streams a contiguous slice of idx; the slice's row ids are
-// staged in LDS first, so no ordinary VMEM load interleaves with the counted DMA waits.
-template <bool NT>
-__global__ void __launch_bounds__(256)
-hbm_gather_rows_nt_kernel(const uint4* __restrict__ X, int64_t ld16, const int* __restrict__ idx,
-                          int64_t nidx, uint32_t* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-  int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  uint32_t acc = 0;
-  typedef int v4i __attribute__((ext_vector_type(4)));
-  for (; w < nidx; w += 4 * nw) {
-    v4i v[4][2];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t k = min(w + u * nw, nidx - 1);
-      const v4i* row = reinterpret_cast<const v4i*>(X + (int64_t)idx[k] * ld16);
-      if constexpr (NT) {
-        v[u][0] = __builtin_nontemporal_load(row + lane);
-        v[u][1] = __builtin_nontemporal_load(row + 64 + lane);
-      } else {
-        v[u][0] = row[lane];
-        v[u][1] = row[64 + lane];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc ^= v[u][0].x ^ v[u][0].w ^ v[u][1].y ^ v[u][1].z;
-  }
-  acc = wave_sum_u32(acc);
-  if ((threadIdx.x & 63) == 0) atomicXor(out, acc);
-}
-
-typedef __attribute__((address_space(3))) void probe_lds_void;
-template <int DEPTH, bool NT>
-__global__ void __launch_bounds__(512)
-hbm_gather_rows_lds_kernel(const uint4* __restrict__ X, int64_t ld16, const int* __restrict__ idx,
-                           int64_t nidx, uint32_t* __restrict__ out) {
-  constexpr int NW = 8, IDXB = 512;
-  __shared__ __attribute__((aligned(16))) uint4 s_ring[NW * DEPTH * 128];
-  __shared__ int s_idx[NW * IDXB];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t nwv = (int64_t)gridDim.x * NW;
-  const int64_t gw = (int64_t)blockIdx.x * NW + wid;
-  const int64_t per = (nidx + nwv - 1) / nwv;
-  const int64_t lo = min(nidx, gw * per), hi = min(nidx, lo + per);
-  uint32_t acc = 0;
-  uint4* ring = s_ring + wid * DEPTH * 128;
-  int* sidx = s_idx + wid * IDXB;
-  const uint32_t rbase = (uint32_t)(uintptr_t)(probe_lds_void*)ring;
-  for (int64_t b0 = lo; b0 < hi; b0 += IDXB) {
-    const int nb = (int)min((int64_t)IDXB, hi - b0);
-    for (int j = lane; j < nb; j += 64) sidx[j] = idx[b0 + j];
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    auto issue = [&](int i) {
-      const int k = min(i, nb - 1);
-      const int r = __builtin_amdgcn_readfirstlane(sidx[k]);
-      const uint4* row = X + (int64_t)r * ld16;
-      const uint32_t m0a = __builtin_amdgcn_readfirstlane(rbase + (uint32_t)((i % DEPTH) * 2048));
-      const uint4* s0 = row + lane;
-      const uint4* s1 = row + 64 + lane;
-      if constexpr (NT) {
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt"
-                     :: "s"(m0a), "v"(s0) : "memory");
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt"
-                     :: "s"(m0a + 1024u), "v"(s1) : "memory");
-      } else {
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-                     :: "s"(m0a), "v"(s0) : "memory");
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-                     :: "s"(m0a + 1024u), "v"(s1) : "memory");
-      }
-    };
-    // DEPTH rows always in flight (the tail re-reads the last row: constant counts)
-    for (int i = 0; i < DEPTH; ++i) issue(i);
-    for (int i = 0; i < nb; ++i) {
-      // row i landed: everything but the newest 2 * (DEPTH - 1) DMA instructions
-      if constexpr (DEPTH == 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else if constexpr (DEPTH == 6) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
-      const uint4* sl = ring + (i % DEPTH) * 128;
-      const uint4 a = sl[lane], b = sl[64 + lane];
-      acc ^= a.x ^ a.w ^ b.y ^ b.z;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // slot read before it is refilled
-      issue(i + DEPTH);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  acc = wave_sum_u32(acc);
-  if (lane == 0) atomicXor(out, acc);
-}
-
 }  // namespace dalgo
 
 using namespace dalgo;
@@ -320,50 +157,6 @@ hipError_t dalgo_mc_pi(uint64_t seed, uint64_t stream, uint64_t offset, uint64_t
   const int grid = (int)std::min<uint64_t>((nblk + 255) / 256, 256 * 8);
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL(mc_pi_kernel, dim3(grid), dim3(256), 0, st, seed, stream, offset, n, count);
-  DALGO_LAUNCH_CHECK();
-  return hipSuccess;
-}
-
-hipError_t dalgo_hbm_gather_rows(const void* X, int64_t ld_bytes, const int* idx, int64_t nidx,
-                                 uint32_t* out, int grid, hipStream_t st) {
-  if (ld_bytes % 16 || ld_bytes < 2048) return hipErrorInvalidValue;
-  // grid >> 20 selects the probe form: 0 registers, 1 registers + nt, 2/3 LDS-DMA depth 4
-  // (default / nt), 4/5 depth 6, 6/7 depth 8 (LDS forms: 512-thread blocks, 2 KB rows)
-  const int mode = grid >> 20;
-  grid &= (1 << 20) - 1;
-  const uint4* X4 = (const uint4*)X;
-  const int64_t ld16 = ld_bytes / 16;
-  if (mode >= 2 && ld_bytes != 2048) return hipErrorInvalidValue;
-  switch (mode) {
-    case 0: hipLaunchKernelGGL(hbm_gather_rows_kernel, dim3(grid), dim3(256), 0, st, X4, ld16, idx, nidx, out); break;
-    case 1: hipLaunchKernelGGL(hbm_gather_rows_nt_kernel<true>, dim3(grid), dim3(256), 0, st, X4, ld16, idx, nidx, out); break;
-    case 2: hipLaunchKernelGGL((hbm_gather_rows_lds_kernel<4, false>), dim3(grid), dim3(512), 0, st, X4, ld16, idx, nidx, out); break;
-    case 3: hipLaunchKernelGGL((hbm_gather_rows_lds_kernel<4, true>), dim3(grid), dim3(512), 0, st, X4, ld16, idx, nidx, out); break;
-    case 4: hipLaunchKernelGGL((hbm_gather_rows_lds_kernel<6, false>), dim3(grid), dim3(512), 0, st, X4, ld16, idx, nidx, out); break;
-    case 5: hipLaunchKernelGGL((hbm_gather_rows_lds_kernel<6, true>), dim3(grid), dim3(512), 0, st, X4, ld16, idx, nidx, out); break;
-    case 6: hipLaunchKernelGGL((hbm_gather_rows_lds_kernel<8, false>), dim3(grid), dim3(512), 0, st, X4, ld16, idx, nidx, out); break;
-    case 7: hipLaunchKernelGGL((hbm_gather_rows_lds_kernel<8, true>), dim3(grid), dim3(512), 0, st, X4, ld16, idx, nidx, out); break;
-    default: return hipErrorInvalidValue;
-  }
-  DALGO_LAUNCH_CHECK();
-  return hipSuccess;
-}
-
-hipError_t dalgo_hbm_read(const void* p, int64_t nbytes, uint32_t* out, int grid, int unroll,
-                          hipStream_t st) {
-  const int64_t n16 = nbytes / 16;
-  if (unroll < 0) {   // blocked-region variant
-    if (unroll <= -8)
-      hipLaunchKernelGGL(hbm_read_blocked_kernel<8>, dim3(grid), dim3(256), 0, st, (const uint4*)p, n16, out);
-    else
-      hipLaunchKernelGGL(hbm_read_blocked_kernel<4>, dim3(grid), dim3(256), 0, st, (const uint4*)p, n16, out);
-    DALGO_LAUNCH_CHECK();
-    return hipSuccess;
-  }
-  if (unroll >= 8)
-    hipLaunchKernelGGL(hbm_read_kernel<8>, dim3(grid), dim3(256), 0, st, (const uint4*)p, n16, out);
-  else
-    hipLaunchKernelGGL(hbm_read_kernel<4>, dim3(grid), dim3(256), 0, st, (const uint4*)p, n16, out);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -69,10 +69,6 @@ hipError_t dalgo_rows_broadcast(float* W, int nrow, int ld, int n, const float* 
 hipError_t dalgo_philox_fill(void* out, int is_bf16, int64_t nrows, int64_t D, int64_t ld,
                              int64_t row_offset, uint64_t seed, uint64_t stream, int dist, float a,
                              float b, hipStream_t st);
-hipError_t dalgo_hbm_gather_rows(const void* X, int64_t ld_bytes, const int* idx, int64_t nidx,
-                                 uint32_t* out, int grid, hipStream_t st);
-hipError_t dalgo_hbm_read(const void* p, int64_t nbytes, uint32_t* out, int grid, int unroll,
-                          hipStream_t st);
 hipError_t dalgo_mc_pi(uint64_t seed, uint64_t stream, uint64_t offset, uint64_t n,
                        unsigned long long* count, hipStream_t st);
 
