@@ -78,7 +78,7 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
              Tensor cnt1, Tensor cnt2, Tensor G, Tensor C, int64_t flags,
              const std::optional<Tensor>& count_acc,
              const std::optional<Tensor>& ticket, at::OptionalIntArrayRef xg_bufs, int64_t xg_rank,
-             int64_t xg_slot, int64_t xg_epoch, const std::optional<Tensor>& xg_err,
+             int64_t xg_slot, const std::optional<Tensor>& xg_epoch, const std::optional<Tensor>& xg_err,
              double xg_timeout, int64_t tail_mode, int64_t tail_reg, double tail_eta,
              double tail_lam, double tail_reg_alpha, const std::optional<Tensor>& tail_count_acc,
              int64_t nsteps, const std::optional<Tensor>& epoch, int64_t epoch_base,
@@ -106,7 +106,9 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
     if (xg_bufs.has_value() && xg_bufs->size() > 1) {
       TORCH_CHECK(xg_bufs->size() <= 8 && xg_rank >= 0 && xg_rank < (int64_t)xg_bufs->size(),
                   "fused tail: 2..8 ranks");
-      TORCH_CHECK(xg_epoch > 0 && xg_epoch <= 0xffffffffLL, "fused tail: epoch in [1, 2^32)");
+      TORCH_CHECK(xg_epoch.has_value() && xg_epoch->scalar_type() == at::kInt && xg_epoch->numel() >= 1,
+                  "fused tail: device epoch int32[1]");
+      check_dev(*xg_epoch, "xg_epoch");
       TORCH_CHECK(xg_slot >= W.size(1) + 1, "fused tail: bucket larger than the slot");
       TORCH_CHECK(xg_err.has_value() && xg_err->scalar_type() == at::kInt, "fused tail: err int32");
       check_dev(*xg_err, "xg_err");
@@ -114,7 +116,7 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
       for (int r = 0; r < tail.world; ++r) tail.bufs[r] = reinterpret_cast<void*>((*xg_bufs)[r]);
       tail.rank = (int)xg_rank;
       tail.slot = (int)xg_slot;
-      tail.epoch = (uint32_t)xg_epoch;
+      tail.epoch_dev = reinterpret_cast<uint32_t*>(xg_epoch->data_ptr<int32_t>());
       tail.err = reinterpret_cast<unsigned*>(xg_err->data_ptr<int>());
       tail.timeout_s = xg_timeout;
     }
@@ -829,7 +831,7 @@ void xgmi_close(int64_t ptr) {
   DALGO_CHECK_HIP(dalgo_xgmi_close(reinterpret_cast<void*>(ptr)), "xgmi_close");
 }
 
-void xgmi_allreduce(Tensor x, at::IntArrayRef bufs, int64_t rank, int64_t slot, int64_t epoch,
+void xgmi_allreduce(Tensor x, at::IntArrayRef bufs, int64_t rank, int64_t slot, Tensor epoch,
                     Tensor err, double timeout_s, const std::optional<Tensor>& W, int64_t upd_mode,
                     int64_t upd_reg, double eta, double lam, double reg_alpha, int64_t count_index,
                     const std::optional<Tensor>& count_acc) {
@@ -837,7 +839,8 @@ void xgmi_allreduce(Tensor x, at::IntArrayRef bufs, int64_t rank, int64_t slot, 
   TORCH_CHECK(x.numel() <= slot, "xgmi_allreduce: vector larger than the slot");
   TORCH_CHECK(bufs.size() >= 1 && bufs.size() <= 8 && rank >= 0 && rank < (int64_t)bufs.size(),
               "xgmi_allreduce: 1..8 ranks");
-  TORCH_CHECK(epoch > 0 && epoch <= 0xffffffffLL, "xgmi_allreduce: epoch in [1, 2^32)");
+  check_dev(epoch, "epoch");
+  TORCH_CHECK(epoch.scalar_type() == at::kInt && epoch.numel() >= 1, "epoch: device int32[1]");
   check_dev(err, "err");
   TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() >= 1, "err int32[1]");
   void* b[8] = {};
@@ -859,7 +862,8 @@ void xgmi_allreduce(Tensor x, at::IntArrayRef bufs, int64_t rank, int64_t slot, 
   }
   DeviceGuard guard(x.device());
   DALGO_CHECK_HIP(dalgo_xgmi_allreduce(x.data_ptr<float>(), x.data_ptr<float>(), (int)x.numel(),
-                                       (int)rank, (int)bufs.size(), b, (int)slot, (uint32_t)epoch,
+                                       (int)rank, (int)bufs.size(), b, (int)slot,
+                                       reinterpret_cast<uint32_t*>(epoch.data_ptr<int32_t>()),
                                        reinterpret_cast<unsigned*>(err.data_ptr<int>()), timeout_s,
                                        w, nw, (int)count_index, (int)upd_mode, (int)upd_reg,
                                        (float)eta, (float)lam, (float)reg_alpha, cacc, cur_stream()),
@@ -1059,7 +1063,7 @@ TORCH_LIBRARY(dalgo, m) {
         "float eps, int seed, int step, float frac, int gx, int rows_per_block, Tensor(a!) slab, "
         "Tensor(b!) gslab, Tensor(c!) cnt1, Tensor(d!) cnt2, Tensor(e!) G, Tensor(f!) C, "
         "int flags=0, Tensor(g!)? count_acc=None, "
-        "Tensor(h!)? ticket=None, int[]? xg_bufs=None, int xg_rank=0, int xg_slot=0, int xg_epoch=0, "
+        "Tensor(h!)? ticket=None, int[]? xg_bufs=None, int xg_rank=0, int xg_slot=0, Tensor(k!)? xg_epoch=None, "
         "Tensor(i!)? xg_err=None, float xg_timeout=0., int tail_mode=0, int tail_reg=0, "
         "float tail_eta=0., float tail_lam=0., float tail_reg_alpha=0., "
         "Tensor(j!)? tail_count_acc=None, int nsteps=1, "
@@ -1118,7 +1122,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("xgmi_get_handle(int ptr) -> Tensor", &xgmi_get_handle);
   m.def("xgmi_open(Tensor handle, int device) -> int", &xgmi_open);
   m.def("xgmi_close(int ptr) -> ()", &xgmi_close);
-  m.def("xgmi_allreduce(Tensor(a!) x, int[] bufs, int rank, int slot, int epoch, Tensor(b!) err, "
+  m.def("xgmi_allreduce(Tensor(a!) x, int[] bufs, int rank, int slot, Tensor(e!) epoch, Tensor(b!) err, "
         "float timeout_s, Tensor(c!)? W=None, int upd_mode=0, int upd_reg=0, float eta=0., "
         "float lam=0., float reg_alpha=0., int count_index=-1, Tensor(d!)? count_acc=None) -> ()");
   m.def("tc_step(Tensor A, Tensor Told, Tensor(a!) Tnew, Tensor(b!) count, int variant=0) -> ()");

@@ -13,10 +13,22 @@ constexpr int kXgHeaderBytes = 256;   // flags[2][8] u32, padded
 struct XgLink {
   uint8_t* bufs[kXgMaxRanks];   // exchange buffer of every rank (own one included)
   int rank, world, slot;        // slot = floats per (phase, source) slot
-  uint32_t epoch;               // >= 1, +1 per exchange, identical on all ranks
+  // Device-resident exchange epoch: the last epoch this rank used (0 before the first
+  // exchange; identical on all ranks). A launch with k exchanges reads it once, uses
+  // base + 1 .. base + k and stores base + k when its last exchange is done. No launch
+  // argument changes from step to step, so the launches can be captured in a hipGraph
+  // and replayed (the epochs advance on the device). 2^32 - 1 exchanges per run.
+  uint32_t* epoch_dev;
   unsigned* err;                // set to 1 if a wait timed out
   long long timeout_ticks;      // s_memrealtime ticks (100 MHz)
 };
+
+__device__ __forceinline__ uint32_t xg_epoch_base(const XgLink& L) {
+  return __hip_atomic_load(L.epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void xg_epoch_store(const XgLink& L, uint32_t e) {
+  __hip_atomic_store(L.epoch_dev, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // SSGD (mode 0: mean + regulariser) / full-batch GD (mode 1: sum) update rule
 struct XgUpdate {
@@ -43,7 +55,7 @@ __device__ __forceinline__ float xg_update(float w, float g, float c, const XgUp
 // Block-wide: push get(i), i < n, into slot [phase][rank] of every rank's buffer,
 // publish one flag per destination and wait (bounded) until all W sources of this
 // epoch have landed in the local buffer. Every thread of the block must call it.
-// `epoch` is passed separately (a persistent launch walks L.epoch, L.epoch + 1, ...
+// `epoch` is passed separately (a persistent launch walks base + 1, base + 2, ...
 // without copying the link, whose pointer array would otherwise land in scratch).
 template <class Get>
 __device__ __forceinline__ void xg_push_publish_wait(const XgLink& L, uint32_t epoch, int n, Get get) {

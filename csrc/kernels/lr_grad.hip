@@ -107,7 +107,7 @@ __device__ __forceinline__ void lr_tail(const LrParams& p, uint32_t xg_epoch) {
   };
   float c;
   if (p.xg.world > 1) {
-    // persistent mode: one exchange epoch per step (xg_epoch = p.xg.epoch + step index)
+    // persistent mode: one exchange epoch per step (xg_epoch = device base + step + 1)
     xg_push_publish_wait(p.xg, xg_epoch, n + 1, get);
     c = xg_sum(p.xg, xg_epoch, n);
     for (int i = threadIdx.x; i < n; i += blockDim.x)
@@ -585,7 +585,12 @@ lr_rows_kernel(const LrParams p) {
       }
       __syncthreads();
       if (s_flag) {
-        lr_tail(p, p.xg.epoch + (uint32_t)it);
+        // exchange epoch of step it: device base (unchanged until this launch's last
+        // exchange is done) + it + 1; the last step's tail stores the new base
+        const uint32_t xbase = p.xg.world > 1 ? xg_epoch_base(p.xg) : 0u;
+        lr_tail(p, xbase + (uint32_t)it + 1u);
+        if (p.xg.world > 1 && it == nst - 1 && threadIdx.x == 0)
+          xg_epoch_store(p.xg, xbase + (uint32_t)nst);
         if (PERSIST && nst > 1) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // W / G / C / ticket written through
           __syncthreads();
@@ -745,7 +750,7 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
   if (tail != nullptr) {
     if (nseg != 1 || !((flags >> 8) & 1) || tail->ticket == nullptr ||
         tail->world < 1 || tail->world > kXgMaxRanks || tail->rank < 0 || tail->rank >= tail->world ||
-        (tail->world > 1 && (tail->epoch == 0 || tail->slot < ldw + 1)))
+        (tail->world > 1 && (tail->epoch_dev == nullptr || tail->slot < ldw + 1)))
       return hipErrorInvalidValue;
     p.ticket = tail->ticket;
     for (int r = 0; r < tail->world; ++r) {
@@ -753,7 +758,7 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
       p.xg.bufs[r] = static_cast<uint8_t*>(tail->bufs[r]);
     }
     p.xg.rank = tail->rank; p.xg.world = tail->world; p.xg.slot = tail->slot;
-    p.xg.epoch = tail->epoch; p.xg.err = tail->err;
+    p.xg.epoch_dev = tail->epoch_dev; p.xg.err = tail->err;
     p.xg.timeout_ticks = (long long)(tail->timeout_s * 1e8);
     p.tu = XgUpdate{tail->mode, tail->reg, tail->eta, tail->lam, tail->reg_alpha};
     p.tail_count_acc = tail->count_acc;

@@ -8,8 +8,8 @@
 //
 //   1. every rank PUSHES its vector into slot [phase][rank] of every rank's
 //      exchange buffer (remote stores travel the direct link; all 7 links busy),
-//   2. system-scope fence, then one flag word per destination: flags[phase][rank]
-//      = epoch,
+//   2. system-scope fence, then one flag word per destination (a system-scope release):
+//      flags[phase][rank] = epoch (device-resident counter, see dalgo/xgmi.h),
 //   3. wait for the W flags of this epoch in the LOCAL buffer, then sum the W slots
 //      in rank order — every rank adds the same numbers in the same order, so the
 //      result is bitwise identical on all ranks (replicated-model invariant).
@@ -42,15 +42,19 @@ struct XgParams {
 
 __global__ void __launch_bounds__(1024) xgmi_allreduce_kernel(XgParams p) {
   const int tid = threadIdx.x;
-  xg_push_publish_wait(p.L, p.L.epoch, p.n, [&](int i) { return p.in[i]; });
+  // one exchange: epoch = device base + 1 (read by every thread before any store below:
+  // the wait inside xg_push_publish_wait ends with a block barrier)
+  const uint32_t e = xg_epoch_base(p.L) + 1u;
+  xg_push_publish_wait(p.L, e, p.n, [&](int i) { return p.in[i]; });
   if (p.W == nullptr) {
-    for (int i = tid; i < p.n; i += blockDim.x) p.out[i] = xg_sum(p.L, p.L.epoch, i);
-    return;
+    for (int i = tid; i < p.n; i += blockDim.x) p.out[i] = xg_sum(p.L, e, i);
+  } else {
+    const float c = xg_sum(p.L, e, p.cidx);             // the global minibatch size
+    for (int i = tid; i < p.nw; i += blockDim.x) p.W[i] = xg_update(p.W[i], xg_sum(p.L, e, i), c, p.u);
+    for (int i = tid; i < p.n; i += blockDim.x) p.out[i] = 0.f;
+    if (tid == 0 && p.count_acc) p.count_acc[0] += (double)c;
   }
-  const float c = xg_sum(p.L, p.L.epoch, p.cidx);             // the global minibatch size
-  for (int i = tid; i < p.nw; i += blockDim.x) p.W[i] = xg_update(p.W[i], xg_sum(p.L, p.L.epoch, i), c, p.u);
-  for (int i = tid; i < p.n; i += blockDim.x) p.out[i] = 0.f;
-  if (tid == 0 && p.count_acc) p.count_acc[0] += (double)c;
+  if (tid == 0) xg_epoch_store(p.L, e);
 }
 
 }  // namespace dalgo
@@ -85,20 +89,20 @@ hipError_t dalgo_xgmi_open(const void* handle, void** ptr) {
 hipError_t dalgo_xgmi_close(void* ptr) { return hipIpcCloseMemHandle(ptr); }
 
 hipError_t dalgo_xgmi_allreduce(const float* in, float* out, int n, int rank, int world,
-                                void* const* bufs, int slot, uint32_t epoch, unsigned* err,
+                                void* const* bufs, int slot, uint32_t* epoch_dev, unsigned* err,
                                 double timeout_s, float* W, int nw, int cidx, int upd_mode,
                                 int upd_reg, float eta, float lam, float reg_alpha,
                                 double* count_acc, hipStream_t st) {
   if (W != nullptr && (cidx < 0 || cidx >= n || nw > cidx)) return hipErrorInvalidValue;
   if (world < 1 || world > kXgMaxRanks || rank < 0 || rank >= world || n < 0 || n > slot ||
-      epoch == 0)
+      epoch_dev == nullptr)
     return hipErrorInvalidValue;
   XgParams p{};
   for (int r = 0; r < world; ++r) {
     if (bufs[r] == nullptr) return hipErrorInvalidValue;
     p.L.bufs[r] = static_cast<uint8_t*>(bufs[r]);
   }
-  p.L.rank = rank; p.L.world = world; p.L.slot = slot; p.L.epoch = epoch; p.L.err = err;
+  p.L.rank = rank; p.L.world = world; p.L.slot = slot; p.L.epoch_dev = epoch_dev; p.L.err = err;
   p.L.timeout_ticks = (long long)(timeout_s * 1e8);
   p.in = in; p.out = out; p.n = n;
   p.W = W; p.nw = nw; p.cidx = cidx;

@@ -10,7 +10,7 @@ struct DalgoLrTail {
   unsigned* ticket;             // device counter, zero
   void* bufs[8];                // K11 exchange buffers (world > 1)
   int world, rank, slot;
-  uint32_t epoch;
+  uint32_t* epoch_dev;          // device-resident exchange epoch (dalgo/xgmi.h)
   unsigned* err;
   double timeout_s;
   int mode, reg;                // 0 SSGD (mean + reg), 1 GD (sum)
@@ -174,7 +174,7 @@ hipError_t dalgo_xgmi_get_handle(void* ptr, void* handle);
 hipError_t dalgo_xgmi_open(const void* handle, void** ptr);
 hipError_t dalgo_xgmi_close(void* ptr);
 hipError_t dalgo_xgmi_allreduce(const float* in, float* out, int n, int rank, int world,
-                                void* const* bufs, int slot, uint32_t epoch, unsigned* err,
+                                void* const* bufs, int slot, uint32_t* epoch_dev, unsigned* err,
                                 double timeout_s, float* W, int nw, int cidx, int upd_mode,
                                 int upd_reg, float eta, float lam, float reg_alpha,
                                 double* count_acc, hipStream_t st);

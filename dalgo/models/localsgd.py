@@ -249,9 +249,9 @@ class ParallelSGD:
         sums, the model all-reduce) is recorded once; the sampling stream comes from a
         device step counter (K1 ``step_dev``) that the graph itself advances, so a replay
         is one host call per step instead of 2 (SSGD) to 14 (MA/BMUF, 5 local steps)
-        launches. Needs GPU tensors, no persistent / one-kernel mode, and
-        no host-sequenced K11 epochs: one rank, or RCCL with DALGO_XGMI=0 (RCCL
-        collectives are graph-capturable)."""
+        launches. Needs GPU tensors, no persistent / one-kernel mode, and capturable
+        collectives: one rank, RCCL, or the K11 xGMI exchange (its epoch lives on the
+        device and is advanced by the kernel itself, csrc/include/dalgo/xgmi.h)."""
         if getattr(self, "_okg", None) is None:
             ws = comm.world_size()
             env = os.environ.get("DALGO_GRAPH", "auto")
@@ -265,11 +265,14 @@ class ParallelSGD:
             auto = self.cfg.algo in ("ma", "bmuf", "easgd") and ws == 1 and small
             want = self.graph if self.graph is not None else (
                 env == "1" or (env == "auto" and auto))
-            ok_comm = ws == 1 or (torch.distributed.get_backend() == "nccl"
-                                  and os.environ.get("DALGO_XGMI", "auto") == "0")
+            # capturable collectives: RCCL, or every collective of the step through K11
+            if self.cfg.algo in ("ssgd", "gd"):
+                k11 = getattr(getattr(self, "bucket", None), "xg", None) is not None and self._zg
+            else:
+                k11 = self.device.type == "cuda" and comm.uses_xgmi(self.S)
+            ok_comm = ws == 1 or k11 or torch.distributed.get_backend() == "nccl"
             self._okg = bool(want and self.device.type == "cuda"
-                             and not self._persistent() and not self._one_kernel() and ok_comm
-                             and getattr(getattr(self, "bucket", None), "xg", None) is None)
+                             and not self._persistent() and not self._one_kernel() and ok_comm)
         return self._okg
 
     def _graph_step(self):
@@ -291,6 +294,8 @@ class ParallelSGD:
             g = torch.cuda.CUDAGraph()
             timer, self.timer = self.timer, None     # no timing events inside a capture
             ar = self.bytes_allreduced
+            xg = comm.xgmi_instance()
+            ex = xg.exchanges if xg is not None else 0
             try:
                 with torch.cuda.graph(g):
                     self._step_impl(0, self._t_dev)
@@ -299,12 +304,16 @@ class ParallelSGD:
                 self.timer = timer
             self._ar_per_replay = self.bytes_allreduced - ar
             self.bytes_allreduced = ar
+            # K11 exchanges recorded in the graph (host epoch-space guard, per replay)
+            self._ex_per_replay = (xg.exchanges - ex) if xg is not None else 0
             self._graphs[key] = g
         if self._t_dev_val != self.t:
             self._t_dev.fill_(self.t)
         with self._ph("step_graph"):
             g.replay()
         self.bytes_allreduced += getattr(self, "_ar_per_replay", 0)
+        if getattr(self, "_ex_per_replay", 0):
+            comm.xgmi_instance().count(self._ex_per_replay)
         self.t += 1
         self._t_dev_val = self.t
 

@@ -9,9 +9,14 @@ independent, so ranks need no communication except the int64 count all-reduce):
   * dense  — P^T as a 0/1 uint8 matrix, one fused int8-MFMA boolean-GEMM round
              per iteration (K9, csrc/kernels/closure.hip). Best up to ~100k
              vertices (n^2 bytes per matrix).
-  * sparse — semi-naive set iteration on packed int64 (x<<32|z) keys with
-             sort/unique on device: only last round's NEW paths are joined
-             (same fixpoint and per-round counts as the reference's naive join).
+  * sparse — semi-naive set iteration on packed int64 (x<<32|z) keys: only last
+             round's NEW paths are joined (same fixpoint and per-round counts as the
+             reference's naive join). On the GPU every rank keeps its paths as an
+             append-only key array plus a device hash set (K9 sparse,
+             csrc/kernels/tc_sparse.hip): one kernel expands the frontier through the
+             in-edge CSR and inserts each candidate with a 64-bit CAS, so dedup, the
+             test against all earlier paths and the merge are one pass with no sort.
+             The CPU reference path uses torch sort / unique / isin.
 """
 from __future__ import annotations
 

@@ -190,8 +190,9 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
             nsteps = int(tail.get("nsteps", 1))
             kw = {}
             if xg is not None:
+                xg.count(nsteps)
                 kw = dict(xg_bufs=xg.bufs, xg_rank=xg.rank, xg_slot=xg.slot,
-                          xg_epoch=xg.next_epoch(nsteps), xg_err=xg.err, xg_timeout=xg.timeout_s)
+                          xg_epoch=xg.epoch_dev, xg_err=xg.err, xg_timeout=xg.timeout_s)
             if nsteps > 1:
                 # persistent launch: steps step .. step + nsteps - 1, one cooperative grid
                 if ws.epochs + nsteps >= 1 << 31:

@@ -47,6 +47,15 @@ def _xgmi_for(t: torch.Tensor):
     return xgmi.shared(t.device)   # collective on first use; None if disabled / failed
 
 
+def xgmi_instance():
+    """The live K11 exchange of this process (None if none was set up)."""
+    from dalgo.parallel import xgmi
+    for inst in xgmi._shared.values():
+        if inst is not None:
+            return inst
+    return None
+
+
 def uses_xgmi(t: torch.Tensor) -> bool:
     """Would a synchronous all_reduce_sum of ``t`` take the K11 one-shot path?"""
     return _active() and _xgmi_for(t) is not None

@@ -101,23 +101,22 @@ class XgmiAllReduce:
             self._release()
             raise RuntimeError(f"xGMI IPC mapping failed on some rank ({err!r})")
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.epoch = 0
+        # device-resident exchange epoch (csrc/include/dalgo/xgmi.h): the kernels read and
+        # advance it themselves, so a step with an exchange can be captured in a hipGraph
+        # and replayed; the host only counts the exchanges it enqueued (epoch-space guard)
+        self.epoch_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.exchanges = 0
 
-    def next_epoch(self, count: int = 1) -> int:
-        """Claim the next `count` exchange epochs (for kernels that run the exchange
-        themselves; a persistent multi-step launch uses first, first + 1, ...)."""
-        first = self.epoch + 1
-        self.epoch += int(count)
-        if self.epoch >= 1 << 32:
+    def count(self, k: int = 1):
+        """Account for k exchanges enqueued (eager calls, kernel tails, graph replays)."""
+        self.exchanges += int(k)
+        if self.exchanges >= (1 << 32) - 1:
             raise RuntimeError("xGMI all-reduce epoch space exhausted")
-        return first
 
     def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
         """In-place SUM over ranks of a contiguous f32 GPU vector (numel <= slot)."""
-        self.epoch += 1
-        if self.epoch >= 1 << 32:
-            raise RuntimeError("xGMI all-reduce epoch space exhausted")
-        self._ops.xgmi_allreduce(x, self.bufs, self.rank, self.slot, self.epoch, self.err,
+        self.count()
+        self._ops.xgmi_allreduce(x, self.bufs, self.rank, self.slot, self.epoch_dev, self.err,
                                  self.timeout_s)
         return x
 
@@ -127,10 +126,8 @@ class XgmiAllReduce:
         """All-reduce the ``[g || count]`` bucket ``x`` and apply the SSGD (mode 0) or
         full-batch GD (mode 1) update to ``W`` in the same launch (fused K8); ``x`` is
         left ZEROED, ready for the next atomic-epilogue gradient kernel."""
-        self.epoch += 1
-        if self.epoch >= 1 << 32:
-            raise RuntimeError("xGMI all-reduce epoch space exhausted")
-        self._ops.xgmi_allreduce(x, self.bufs, self.rank, self.slot, self.epoch, self.err,
+        self.count()
+        self._ops.xgmi_allreduce(x, self.bufs, self.rank, self.slot, self.epoch_dev, self.err,
                                  self.timeout_s, W, int(mode), int(reg), float(eta), float(lam),
                                  float(reg_alpha), int(count_index), count_acc)
         return x

@@ -41,7 +41,7 @@ def main():
     bad = sum(int(not torch.equal(o.cpu(), e)) for o, e in zip(outs, refs))
     assert bad == 0, f"rank {r}: {bad} mismatching results"
     if r == 0:
-        print(f"XGMI_OK world={W} epochs={xg.epoch}", flush=True)
+        print(f"XGMI_OK world={W} exchanges={xg.exchanges}", flush=True)
     runtime.shutdown()
 
 

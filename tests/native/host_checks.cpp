@@ -39,13 +39,14 @@ int main() {
   CHECK(dalgo_tc_step(nullptr, 120, nullptr, nullptr, 128, 128, 128, 0, &cnt, nullptr) ==
         hipErrorInvalidValue);                                 // lda not a multiple of 16
   void* bufs[9] = {};
-  CHECK(dalgo_xgmi_allreduce(nullptr, nullptr, 10, 0, 9, bufs, 16, 1, nullptr, 1.0, nullptr, 0, 0, 0, 0, 0.f, 0.f, 0.f, nullptr, nullptr) ==
+  uint32_t* ep = reinterpret_cast<uint32_t*>(&cnt);             // never dereferenced: rejected first
+  CHECK(dalgo_xgmi_allreduce(nullptr, nullptr, 10, 0, 9, bufs, 16, ep, nullptr, 1.0, nullptr, 0, 0, 0, 0, 0.f, 0.f, 0.f, nullptr, nullptr) ==
         hipErrorInvalidValue);                                 // > 8 ranks
-  CHECK(dalgo_xgmi_allreduce(nullptr, nullptr, 10, 0, 2, bufs, 16, 0, nullptr, 1.0, nullptr, 0, 0, 0, 0, 0.f, 0.f, 0.f, nullptr, nullptr) ==
-        hipErrorInvalidValue);                                 // epoch 0 is reserved
-  CHECK(dalgo_xgmi_allreduce(nullptr, nullptr, 32, 0, 2, bufs, 16, 1, nullptr, 1.0, nullptr, 0, 0, 0, 0, 0.f, 0.f, 0.f, nullptr, nullptr) ==
+  CHECK(dalgo_xgmi_allreduce(nullptr, nullptr, 10, 0, 2, bufs, 16, nullptr, nullptr, 1.0, nullptr, 0, 0, 0, 0, 0.f, 0.f, 0.f, nullptr, nullptr) ==
+        hipErrorInvalidValue);                                 // no device epoch counter
+  CHECK(dalgo_xgmi_allreduce(nullptr, nullptr, 32, 0, 2, bufs, 16, ep, nullptr, 1.0, nullptr, 0, 0, 0, 0, 0.f, 0.f, 0.f, nullptr, nullptr) ==
         hipErrorInvalidValue);                                 // vector larger than the slot
-  CHECK(dalgo_xgmi_allreduce(nullptr, nullptr, 8, 0, 2, bufs, 16, 1, nullptr, 1.0, nullptr, 0, 0, 0, 0, 0.f, 0.f, 0.f, nullptr, nullptr) ==
+  CHECK(dalgo_xgmi_allreduce(nullptr, nullptr, 8, 0, 2, bufs, 16, ep, nullptr, 1.0, nullptr, 0, 0, 0, 0, 0.f, 0.f, 0.f, nullptr, nullptr) ==
         hipErrorInvalidValue);                                 // unmapped peer buffer
   CHECK(dalgo_xgmi_buffer_bytes(4096) == 256 + 2 * 8 * 4096 * sizeof(float));
   CHECK(dalgo_lr_max_cols(1) == 2048 && dalgo_lr_max_cols(0) == 1024);

@@ -109,7 +109,7 @@ def _final_w(out):
 
 
 @pytest.mark.gpu_shared
-@pytest.mark.parametrize("one_kernel", ["1", "0", "persistent"])
+@pytest.mark.parametrize("one_kernel", ["1", "0", "persistent", "graph"])
 @pytest.mark.parametrize("algo", ["ssgd", "logistic_regression"])
 def test_fused_xgmi_update_matches_process_group(cuda, algo, one_kernel):
     """SSGD / full-batch GD: one-launch step (K1 tail: xGMI exchange + update), a
@@ -120,9 +120,14 @@ def test_fused_xgmi_update_matches_process_group(cuda, algo, one_kernel):
     args = [script, "--device", "cuda", "--backend", "gloo", "--no-plot", "--quiet",
             "--synthetic", "40000,64", "--n-iterations", "30", "--dtype", "f32",
             "--eval-every", "10"]   # persistent mode: 10-step launches between evaluations
-    env_key = "DALGO_PERSISTENT" if one_kernel == "persistent" else "DALGO_ONE_KERNEL"
-    fused = _torchrun(args, env_extra=dict(SPIN, DALGO_XGMI="1", **{
-        env_key: "1" if one_kernel == "persistent" else one_kernel}))
+    if one_kernel == "graph":
+        # K1 + K11 (device-resident epoch) captured once, replayed every step
+        mode = {"DALGO_GRAPH": "1", "DALGO_ONE_KERNEL": "0"}
+    elif one_kernel == "persistent":
+        mode = {"DALGO_PERSISTENT": "1"}
+    else:
+        mode = {"DALGO_ONE_KERNEL": one_kernel}
+    fused = _torchrun(args, env_extra=dict(SPIN, DALGO_XGMI="1", **mode))
     plain = _torchrun(args, env_extra={"DALGO_XGMI": "0"})
     wf, wp = _final_w(fused), _final_w(plain)
     assert wf.shape == wp.shape and np.allclose(wf, wp, rtol=1e-4, atol=1e-5), (wf[:5], wp[:5])
@@ -130,14 +135,14 @@ def test_fused_xgmi_update_matches_process_group(cuda, algo, one_kernel):
 
 @pytest.mark.gpu_shared
 def test_bench_launch_calibration_two_ranks(cuda):
-    """bench.py --launch auto with the K11 exchange: the per-step, one-kernel and
-    persistent forms are each timed on both ranks and one is kept (same on every rank)."""
+    """bench.py --launch auto with the K11 exchange: the per-step, hipGraph-replay,
+    one-kernel and persistent forms are each timed on both ranks and one is kept (same on every rank)."""
     out = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--rows", "200000",
                      "--steps", "5", "--warmup", "2", "--cal-steps", "4"],
                     env_extra=dict(SPIN, DALGO_XGMI="1"))
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
     cal = d["launch_calibration_ms_per_step"]
-    assert set(cal) == {"per-step", "one-kernel", "persistent"}
+    assert set(cal) == {"per-step", "graph", "one-kernel", "persistent"}
     assert d["config"]["launch"] == min(cal, key=cal.get)
     assert d["config"]["allreduce"] == "xgmi-oneshot (K11)" and d["value"] > 0
 
