@@ -46,6 +46,8 @@
 namespace dalgo {
 
 constexpr int kPbDummy = 65536;   // padding floats after the entries (phase-1 dummy stores)
+// fraction bits of the phase-1 sum bound (u64 fixed point: sums of present c up to 2^43)
+constexpr int kPbBoundFrac = 20;
 
 namespace {
 
@@ -89,8 +91,8 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
                  const int32_t* __restrict__ chunk_slo,
                  const int32_t* __restrict__ chunk_ns, const int32_t* __restrict__ chunk_run,
                  const int32_t* __restrict__ run_delta, const float* __restrict__ c,
-                 float* __restrict__ val, int64_t dummy_base, double* __restrict__ bound,
-                 int wu0) {
+                 float* __restrict__ val, int64_t dummy_base,
+                 unsigned long long* __restrict__ bound, int wu0) {
   static_assert(S <= 16384, "local source index must leave bits 14, 15 for the markers");
   constexpr int EPL = 8;
   constexpr int D = 4;                        // steps of edges loaded ahead
@@ -126,8 +128,10 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
     if (threadIdx.x == 0) {
       double t = 0.0;
       for (int w = 0; w < NW; ++w) t += (double)s_v[0][w];
-      // rounding slack: the f32 partial sums may be up to ~1e-6 relative low
-      atomicAdd(bound, t * (1.0 + 1e-5));
+      // rounding slack: the f32 partial sums may be up to ~1e-6 relative low. The bound
+      // is summed as u64 fixed point (2^-kPbBoundFrac units, rounded up): integer adds
+      // commute, so K below does not depend on the order the work units ran in
+      atomicAdd(bound, (unsigned long long)ceil(ldexp(t * (1.0 + 1e-5), kPbBoundFrac)));
     }
   }
   if constexpr (!GRUNS)
@@ -259,8 +263,8 @@ __device__ __forceinline__ float from_fixed(uint64_t q, int K) {
 
 // fraction bits for a sum bound B: B * 2^K <= 2^62 (u64 headroom for the per-record
 // +1 units); derived on the device from phase 1's bound, so no host sync
-__device__ __forceinline__ int pb_fixed_bits(const double* bound) {
-  const double B = *bound;
+__device__ __forceinline__ int pb_fixed_bits(const unsigned long long* bound) {
+  const double B = ldexp((double)*bound, -kPbBoundFrac);
   if (!(B > 0.0)) return 100;
   return min(100, max(1, 61 - ilogb(B)));
 }
@@ -318,7 +322,8 @@ template <int BW, int NW, int U = 4>
 __global__ void __launch_bounds__(NW * 64)
 pb_accum_kernel(const float* __restrict__ val, const uint16_t* __restrict__ dloc,
                 const int32_t* __restrict__ wi_bin, const int64_t* __restrict__ wi_lo,
-                const int32_t* __restrict__ wi_slab, int64_t n_local, const double* bound,
+                const int32_t* __restrict__ wi_slab, int64_t n_local,
+                const unsigned long long* bound,
                 PbOut o, uint64_t* __restrict__ slab) {
   const int K = pb_fixed_bits(bound);
   // U: groups of 4 entries in flight per thread
@@ -374,7 +379,7 @@ template <int BW>
 __global__ void __launch_bounds__(256)
 pb_combine_kernel(const uint64_t* __restrict__ slab, const int32_t* __restrict__ split_bin,
                   const int32_t* __restrict__ split_first, const int32_t* __restrict__ split_count,
-                  int64_t n_local, const double* bound, PbOut o) {
+                  int64_t n_local, const unsigned long long* bound, PbOut o) {
   const int K = pb_fixed_bits(bound);
   const int sb = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -403,7 +408,7 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
                          const int32_t* chunk_run, const int32_t* run_delta, int nch,
                          int max_runs, int src_span, const float* c, float* val, int64_t n_val, const uint16_t* dloc, const int32_t* wi_bin,
                          const int64_t* wi_lo, const int32_t* wi_slab, int nwi, int bin_width,
-                         double* bound, int64_t n_local, float* acc, int32_t* pres, uint64_t* slab,
+                         double* bound_word, int64_t n_local, float* acc, int32_t* pres, uint64_t* slab,
                          const int32_t* split_bin, const int32_t* split_first,
                          const int32_t* split_count, int nsplit, const int32_t* outdeg, float q,
                          float invN, int mode, const float* dang_in, float* r, float* cn,
@@ -414,8 +419,10 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
   // units, the first one starting at 0 -- e.g. own-slice sources before the ghost
   // exchange has landed), bit 1 = phase 2 (+ fused update)
   wu_hi = std::min(wu_hi, nwu);
+  // the 8-byte bound word holds a u64 fixed-point sum (see pb_gather_kernel)
+  unsigned long long* bound = reinterpret_cast<unsigned long long*>(bound_word);
   if ((phases & 1) && wu_lo == 0) {
-    const hipError_t e = hipMemsetAsync(bound, 0, sizeof(double), st);
+    const hipError_t e = hipMemsetAsync(bound, 0, sizeof(*bound), st);
     if (e != hipSuccess) return e;
   }
   if ((phases & 1) && nch > 0 && wu_hi > wu_lo) {
