@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--backend", default=None, choices=["nccl", "gloo"])
     ap.add_argument("--no-witness", action="store_true")
+    ap.add_argument("--no-candidates", action="store_true",
+                    help="filtered iterations without the candidate-pruned K2 tiles")
     ap.add_argument("--no-bound-filter", action="store_true",
                     help="plain (full K2 every iteration) Lloyd with the incremental K3")
     ap.add_argument("--deadline-s", type=float, default=420.0)
@@ -134,7 +136,8 @@ def main():
     t = time.perf_counter()
     marks = [ev()]
     km = KMeans(KMeansConfig(k=a.k, n_iterations=a.iters, seed=1,
-                             bound_filter=not a.no_bound_filter), X, lo, a.rows)
+                             bound_filter=not a.no_bound_filter,
+                             candidates=not a.no_candidates), X, lo, a.rows)
     marks.append(ev())
     for _ in range(a.iters):
         km.step()
@@ -165,7 +168,8 @@ def main():
             "steady_ms_per_iter_rank0": sum(steady) / len(steady) if steady else None,
             "full_pass_tflops_per_gpu": (flops / W / (iter_ms[0] / 1e3) / 1e12) if iter_ms else None,
             "reassigned_rows_per_iter_rank0": active, "moved_rows_per_iter_rank0": moved,
-            "bound_filter": km.bounds, "incremental_k3": km.incremental,
+            "bound_filter": km.bounds, "candidate_pruning": getattr(km, "_cand", None) is not None,
+            "incremental_k3": km.incremental,
             "sse_last_iteration": float(sse_last.item()),
             "correctness_witness": witness,
             "config": {"rows": a.rows, "dim": a.dim, "k": a.k, "dtype": a.dtype,

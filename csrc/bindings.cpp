@@ -466,7 +466,7 @@ void kmeans_move_sorted(const Tensor& X, int64_t DP, const Tensor& changed, int6
 
 // bound-filtered Lloyd: active rows (u + delta[a] >= s[a]) -> idx, their assignment -> a_prev
 void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta, const Tensor& s,
-                   Tensor a_prev, Tensor idx, Tensor n_active) {
+                   Tensor a_prev, Tensor idx, Tensor n_active, const std::optional<Tensor>& acl) {
   const int64_t n = assign.numel();
   check_i32(assign, "assign");
   check_f32(u, "u");
@@ -479,12 +479,18 @@ void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta
   TORCH_CHECK(u.numel() >= n && a_prev.numel() >= n && idx.numel() >= n, "kmeans_filter sizes");
   TORCH_CHECK(delta.numel() == s.numel(), "delta / s [k]");
   TORCH_CHECK(n_active.scalar_type() == at::kLong && n_active.numel() >= 1, "n_active int64[1]");
+  int32_t* aclp = nullptr;
+  if (acl.has_value()) {
+    check_i32(*acl, "acl");
+    TORCH_CHECK(acl->numel() >= idx.numel(), "kmeans_filter: acl [cap]");
+    aclp = acl->data_ptr<int32_t>();
+  }
   DeviceGuard guard(assign.device());
   DALGO_CHECK_HIP(dalgo_km_filter(assign.data_ptr<int32_t>(), u.data_ptr<float>(), l.data_ptr<float>(),
                                   delta.data_ptr<float>(), s.data_ptr<float>(), (int)delta.numel(), n,
                                   a_prev.data_ptr<int32_t>(), idx.data_ptr<int32_t>(),
                                   reinterpret_cast<unsigned long long*>(n_active.data_ptr<int64_t>()),
-                                  idx.numel(), cur_stream()),
+                                  idx.numel(), aclp, cur_stream()),
                   "kmeans_filter");
 }
 
@@ -547,7 +553,7 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
                        const std::optional<Tensor>& m_dev, const std::optional<Tensor>& a_prev,
                        const std::optional<Tensor>& tol, const std::optional<Tensor>& u,
                        const std::optional<Tensor>& l, const std::optional<Tensor>& changed,
-                       const std::optional<Tensor>& n_changed) {
+                       const std::optional<Tensor>& n_changed, at::TensorList cand) {
   TORCH_CHECK(Cq.dim() == 2 && Cq.is_contiguous() && Cq.scalar_type() == at::kBFloat16, "Cq bf16");
   const int DP = (int)Cq.size(1);
   TORCH_CHECK(DP == 64 || DP == 128, "kmeans_assign_idx: DP 64 or 128");
@@ -607,12 +613,105 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
   } else {
     TORCH_CHECK(md != nullptr, "kmeans_assign_idx: mind");
   }
+  // candidate-pruned form: [tile_cl, tile_lo, cstart, n_tiles, cnb, hnb, nb, nd]
+  DalgoKmCand cd{};
+  const DalgoKmCand* cp = nullptr;
+  if (!cand.empty()) {
+    TORCH_CHECK(cand.size() == 8 && pp != nullptr && ip != nullptr,
+                "kmeans_assign_idx: cand = 8 tensors, with the device-count form and idx");
+    for (const Tensor& t : cand) check_dev(t, "cand");
+    const int64_t k = cand[2].numel() - 1;
+    TORCH_CHECK(cand[0].scalar_type() == at::kInt && cand[1].scalar_type() == at::kLong &&
+                    cand[2].scalar_type() == at::kLong && cand[3].scalar_type() == at::kLong &&
+                    cand[4].scalar_type() == at::kBFloat16 && cand[5].scalar_type() == at::kFloat &&
+                    cand[6].scalar_type() == at::kInt && cand[7].scalar_type() == at::kFloat,
+                "kmeans_assign_idx: cand dtypes");
+    TORCH_CHECK(k >= 1 && k <= kpad && cand[4].numel() >= k * kpad * DP && cand[5].numel() >= k * kpad &&
+                    cand[6].numel() >= k * kpad && cand[7].numel() >= k * kpad &&
+                    cand[0].numel() == cand[1].numel(),
+                "kmeans_assign_idx: cand sizes");
+    cd.tile_cl = cand[0].data_ptr<int32_t>();
+    cd.tile_lo = cand[1].data_ptr<int64_t>();
+    cd.cstart = cand[2].data_ptr<int64_t>();
+    cd.n_tiles = reinterpret_cast<const unsigned long long*>(cand[3].data_ptr<int64_t>());
+    cd.cnb = cand[4].data_ptr();
+    cd.hnb = cand[5].data_ptr<float>();
+    cd.nb = cand[6].data_ptr<int32_t>();
+    cd.nd = cand[7].data_ptr<float>();
+    cp = &cd;
+  }
   DeviceGuard guard(X.device());
   DALGO_CHECK_HIP(dalgo_kmeans_assign_idx(X.data_ptr(), m, X.stride(0), DP, Cq.data_ptr(),
                                           hn.data_ptr<float>(), (int)kpad, ip,
                                           assign.data_ptr<int>(), md, m2, nullptr, 0, xhp, xmp, pp,
-                                          cur_stream()),
+                                          cp, cur_stream()),
                   "kmeans_assign_idx");
+}
+
+// candidate-pruned K2 preparation: active rows sorted by cluster + tile table
+void kmeans_sort_active(const Tensor& acl, const Tensor& idx, const Tensor& n_active, int64_t k,
+                        int64_t chunk, Tensor block_counts, Tensor cstart, Tensor seg_start,
+                        Tensor rows_sorted, int64_t tile, Tensor tile_cl, Tensor tile_lo,
+                        Tensor n_tiles) {
+  check_i32(acl, "acl");
+  check_i32(idx, "idx");
+  check_i32(rows_sorted, "rows_sorted");
+  check_i32(block_counts, "block_counts");
+  check_i32(tile_cl, "tile_cl");
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&n_active, &cstart, &seg_start, &tile_lo, &n_tiles}) {
+    check_dev(*t, "sort_active");
+    TORCH_CHECK(t->scalar_type() == at::kLong && t->is_contiguous(), "sort_active: int64 tensors");
+  }
+  const int64_t cap = idx.numel();
+  TORCH_CHECK(acl.numel() >= cap && rows_sorted.numel() >= cap && k >= 1 && k <= 2048 &&
+                  cstart.numel() >= k + 1 && seg_start.numel() >= k + 1 && tile >= 1 && chunk >= 1,
+              "kmeans_sort_active sizes");
+  const int64_t B = std::max<int64_t>(1, std::min<int64_t>((cap + chunk - 1) / chunk,
+                                                           block_counts.numel() / k));
+  TORCH_CHECK(B * chunk >= cap, "kmeans_sort_active: block_counts too small for cap / chunk");
+  TORCH_CHECK(tile_cl.numel() == tile_lo.numel() && tile_cl.numel() >= (cap + tile - 1) / tile + k,
+              "kmeans_sort_active: tile table [cap / tile + k]");
+  DeviceGuard guard(idx.device());
+  DALGO_CHECK_HIP(dalgo_kmeans_sort_active(
+                      acl.data_ptr<int32_t>(), idx.data_ptr<int32_t>(), cap,
+                      reinterpret_cast<const unsigned long long*>(n_active.data_ptr<int64_t>()), (int)k,
+                      (int)B, chunk, block_counts.data_ptr<int>(), cstart.data_ptr<int64_t>(),
+                      seg_start.data_ptr<int64_t>(), rows_sorted.data_ptr<int32_t>(), (int)tile,
+                      tile_cl.data_ptr<int32_t>(), tile_lo.data_ptr<int64_t>(),
+                      reinterpret_cast<unsigned long long*>(n_tiles.data_ptr<int64_t>()),
+                      tile_cl.numel(), cur_stream()),
+                  "kmeans_sort_active");
+}
+
+// centre geometry of the candidate-pruned iteration: delta, s and the neighbour lists
+void kmeans_centre_nbrs(const Tensor& cq, const Tensor& cprev, const Tensor& hn, int64_t k,
+                        int64_t d, Tensor delta, Tensor s, Tensor nd, Tensor nb, Tensor hnb,
+                        Tensor cnb) {
+  check_dev(cq, "cq");
+  check_dev(cprev, "cprev");
+  TORCH_CHECK(cq.dim() == 2 && cq.is_contiguous() && cq.scalar_type() == at::kBFloat16 &&
+                  cprev.is_contiguous() && cprev.scalar_type() == at::kBFloat16 &&
+                  cprev.size(1) == cq.size(1) && cprev.size(0) >= k,
+              "kmeans_centre_nbrs: bf16 centres [kpad, DP]");
+  const int64_t kpad = cq.size(0), DP = cq.size(1);
+  TORCH_CHECK(k >= 1 && k <= kpad && kpad <= 2048 && d >= 1 && d <= 128 && d <= DP, "kmeans_centre_nbrs: k, d");
+  check_f32(hn, "hn");
+  check_f32(delta, "delta");
+  check_f32(s, "s");
+  check_f32(nd, "nd");
+  check_f32(hnb, "hnb");
+  check_i32(nb, "nb");
+  check_dev(cnb, "cnb");
+  TORCH_CHECK(hn.numel() >= kpad && delta.numel() >= k && s.numel() >= k && nd.numel() >= k * kpad &&
+                  nb.numel() >= k * kpad && hnb.numel() >= k * kpad &&
+                  cnb.scalar_type() == at::kBFloat16 && cnb.is_contiguous() && cnb.numel() >= k * kpad * DP,
+              "kmeans_centre_nbrs sizes");
+  DeviceGuard guard(cq.device());
+  DALGO_CHECK_HIP(dalgo_km_centre_nbrs(cq.data_ptr(), cprev.data_ptr(), hn.data_ptr<float>(), (int)k,
+                                       (int)kpad, (int)d, (int)DP, delta.data_ptr<float>(),
+                                       s.data_ptr<float>(), nd.data_ptr<float>(), nb.data_ptr<int32_t>(),
+                                       hnb.data_ptr<float>(), cnb.data_ptr(), cur_stream()),
+                  "kmeans_centre_nbrs");
 }
 
 void kmeans_update(Tensor C, const Tensor& S, const Tensor& cnt, Tensor Cq, Tensor hn,
@@ -1089,14 +1188,20 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(e!) cluster_start, Tensor(f!) seg_start, Tensor(g!) perm, Tensor(h!) ec, "
         "Tensor(i!) er, Tensor? m_dev=None, int chunk=65536) -> ()");
   m.def("kmeans_filter(Tensor assign, Tensor(a!) u, Tensor(e!) l, Tensor delta, Tensor s, "
-        "Tensor(b!) a_prev, Tensor(c!) idx, Tensor(d!) n_active) -> ()");
+        "Tensor(b!) a_prev, Tensor(c!) idx, Tensor(d!) n_active, Tensor(f!)? acl=None) -> ()");
+  m.def("kmeans_sort_active(Tensor acl, Tensor idx, Tensor n_active, int k, int chunk, "
+        "Tensor(a!) block_counts, Tensor(b!) cstart, Tensor(c!) seg_start, Tensor(d!) rows_sorted, "
+        "int tile, Tensor(e!) tile_cl, Tensor(f!) tile_lo, Tensor(g!) n_tiles) -> ()");
+  m.def("kmeans_centre_nbrs(Tensor cq, Tensor cprev, Tensor hn, int k, int d, Tensor(a!) delta, "
+        "Tensor(b!) s, Tensor(c!) nd, Tensor(d!) nb, Tensor(e!) hnb, Tensor(f!) cnb) -> ()");
   m.def("kmeans_centre_bounds(Tensor cnow, Tensor cprev, int k, int d, Tensor(a!) delta, "
         "Tensor(b!) s) -> ()");
   m.def("kmeans_qsum(Tensor assign, Tensor xh, int k, Tensor(a!) Q) -> ()");
   m.def("kmeans_assign_idx(Tensor X, Tensor Cq, Tensor hn, Tensor? idx, int m, Tensor(a!) assign, "
         "Tensor(b!)? mind=None, Tensor(c!)? mind2=None, Tensor(d!)? xh=None, Tensor(e!)? xmax=None, "
         "Tensor? m_dev=None, Tensor? a_prev=None, Tensor? tol=None, Tensor(f!)? u=None, "
-        "Tensor(g!)? l=None, Tensor(h!)? changed=None, Tensor(i!)? n_changed=None) -> ()");
+        "Tensor(g!)? l=None, Tensor(h!)? changed=None, Tensor(i!)? n_changed=None, "
+        "Tensor[] cand=[]) -> ()");
   m.def("kmeans_bounds_init(Tensor mind, Tensor mind2, Tensor xmax, int n, Tensor(a!) u, "
         "Tensor(b!) l, Tensor(c!) tol) -> ()");
   m.def("kmeans_update(Tensor(a!) C, Tensor S, Tensor cnt, Tensor(b!) Cq, Tensor(c!) hn, "
@@ -1165,6 +1270,8 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("kmeans_diff", &kmeans_diff);
   m.impl("kmeans_move_sorted", &kmeans_move_sorted);
   m.impl("kmeans_filter", &kmeans_filter);
+  m.impl("kmeans_sort_active", &kmeans_sort_active);
+  m.impl("kmeans_centre_nbrs", &kmeans_centre_nbrs);
   m.impl("kmeans_centre_bounds", &kmeans_centre_bounds);
   m.impl("kmeans_bounds_init", &kmeans_bounds_init);
   m.impl("kmeans_qsum", &kmeans_qsum);

@@ -302,6 +302,16 @@ struct KmAux {
   int* changed;                       // LOOP: rows whose cluster changed ...
   unsigned long long* n_changed;      //       ... and their number
   long long cap;                      //       capacity of `changed`
+  // CAND (candidate-pruned LOOP): the active rows sorted by cluster (idx), tiles that never
+  // straddle two clusters, and each centre's neighbour lists (km_centre_nbrs_kernel)
+  const int32_t* tile_cl;             // cluster of tile t
+  const int64_t* tile_lo;             // its first position in idx
+  const int64_t* cstart;              // [k + 1]: cluster runs in idx
+  const unsigned long long* n_tiles;  // device tile count
+  const uint16_t* cnb;                // [k][kpad][DP]: centres in neighbour order of centre a
+  const float* hnb;                   // [k][kpad]: their 0.5|c|^2
+  const int32_t* nb;                  // [k][kpad]: their ids
+  const float* nd;                    // [k][kpad]: |c - c_a| rounded down, ascending
 };
 constexpr int kChgBuf = 1024;         // changed rows buffered per block (LDS)
 
@@ -309,7 +319,7 @@ __device__ __forceinline__ float km_up1(float x) { return nextafterf(x, __builti
 __device__ __forceinline__ float km_dn1(float x) { return nextafterf(x, -__builtin_inff()); }
 
 template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, bool TOP2 = false,
-          bool LOOP = false>
+          bool LOOP = false, bool CAND = false>
 __global__ void __launch_bounds__(NW * 64, MINB)
 kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
                           const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int kpad,
@@ -318,6 +328,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
                           const int32_t* __restrict__ idx, float* __restrict__ mind2,
                           const KmAux aux) {
   static_assert(!LOOP || TOP2, "the fused bound update needs the second-best distance");
+  static_assert(!CAND || LOOP, "candidate pruning is a form of the filtered iteration");
   // idx (optional): the block's point j is row idx[j] of X (and of assign / mind), j < n
   // -- the bound-filtered form of Lloyd only re-assigns the points the filter keeps
   constexpr int KS = DP / 16;                  // 32x32x16 k-steps per centre row
@@ -333,6 +344,8 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   __shared__ __attribute__((aligned(16))) uint4 s_c[NBUF * CHP];
   extern __shared__ __attribute__((aligned(16))) float s_hn[];   // [kpad]: 0.5|c|^2 + M
   __shared__ float s_m[NW];
+  __shared__ float s_r[NW];
+  __shared__ int s_nc[NW];
   __shared__ double s_sse[NW];
 
   __shared__ int s_chg[LOOP ? kChgBuf : 1];
@@ -362,7 +375,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     }
     __syncthreads();
   };
-  const int64_t ntile = (n + TILE - 1) / TILE;
+  const int64_t ntile = CAND ? (int64_t)*aux.n_tiles : (n + TILE - 1) / TILE;
 
   // per-thread DMA sources: slot q = g*NT + tid of the chunk image
   int src_off[GPT];
@@ -375,8 +388,9 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // chunk being read and drains vmcnt(0) before every ds_read (the chunk in flight
   // would then never overlap compute). The counted waits below are the only waits.
   const uint32_t lds0 = (uint32_t)(uintptr_t)(km_lds_void*)s_c;
+  const uint16_t* cbase = Cq;   // CAND: the tile cluster's neighbour-ordered centres
   auto issue = [&](int ch) {
-    const uint16_t* base = Cq + (int64_t)ch * CH * DP;
+    const uint16_t* base = cbase + (int64_t)ch * CH * DP;
     const uint32_t dst = lds0 + (uint32_t)(((ch % NBUF) * CHP) * 16);
 #pragma unroll
     for (int g = 0; g < GPT; ++g) {
@@ -397,15 +411,29 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // one block tile (a lambda so the single-tile launch compiles to straight-line code:
   // the loop form costs registers the 3-tile plain form does not have)
   auto tile = [&](const int64_t bt) {
-  const int64_t pbase = (bt * NW + wid) * (PT * 32);
+  // CAND: tile bt = up to TILE positions of one cluster's run in idx
+  int acl = 0;
+  int64_t pbase, pend = n;
+  const float* hbase = hn;
+  if constexpr (CAND) {
+    acl = aux.tile_cl[bt];
+    const int64_t lo = aux.tile_lo[bt];
+    pend = min(aux.cstart[acl + 1], lo + TILE);
+    pbase = lo + (int64_t)wid * (PT * 32);
+    cbase = aux.cnb + (int64_t)acl * kpad * DP;
+    hbase = aux.hnb + (int64_t)acl * kpad;
+  } else {
+    pbase = (bt * NW + wid) * (PT * 32);
+  }
 
   // ---- points (B operand, negated), resident for the whole sweep; rows past n are zero
   uint4 bf[PT][KS];
   float x2[PT];                                // |x|^2 of the lane's point (both halves)
+  float ub[CAND ? PT : 1];                     // CAND: filter's bound on |x - c_acl|
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     const int64_t p = pbase + t * 32 + cl;
-    const bool ok = p < n;
+    const bool ok = p < pend;
     const int64_t row = ok ? (idx ? (int64_t)idx[p] : p) : 0;
     const uint16_t* src = X + row * ldx + h * 8;
 #pragma unroll
@@ -413,6 +441,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       const uint4 v = *reinterpret_cast<const uint4*>(src + 16 * s);
       bf[t][s] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
     }
+    if constexpr (CAND) ub[t] = ok ? aux.u[row] : 0.f;
   }
   // all ordinary loads retired before the DMA stream starts, and the fragments pinned
   // here, so the compiler's own waits never drain a chunk in flight (vmcnt(0) in-loop)
@@ -434,12 +463,40 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   }
   for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
   my_xmax = fmaxf(my_xmax, mx);
+  float um = 0.f;
+  if constexpr (CAND) {
+#pragma unroll
+    for (int t = 0; t < PT; ++t) um = fmaxf(um, ub[t]);
+    for (int off = 32; off >= 1; off >>= 1) um = fmaxf(um, __shfl_xor(um, off));
+  }
   // the previous tile's waves are past every read of s_m / s_hn / the chunk buffers
   // (each crossed this tile's chunk barriers' predecessor: the last chunk barrier of the
   // previous tile precedes all of its reads), so the block barrier below orders the
   // rewrite after them
-  if (lane == 0) s_m[wid] = mx;
+  if (lane == 0) { s_m[wid] = mx; if constexpr (CAND) s_r[wid] = um; }
   __syncthreads();
+  // CAND: only centres c with |c - c_acl| <= R can be the nearest of a tile point
+  // (|x - c| >= |c - c_acl| - |x - c_acl| > |x - c_acl| for |c - c_acl| > 2 u >= 2|x - c_acl|),
+  // R = 2 max u + sqrt(tol) (slack of the kernel distances); nd is ascending, so they are
+  // a prefix of the neighbour list: nsub_t 32-centre sub-tiles of it
+  int nsub_t = nchunk * NSUB, nch_t = nchunk;
+  if constexpr (CAND) {
+    float R = s_r[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) R = fmaxf(R, s_r[w]);
+    R = km_up1(km_up1(2.f * R) + km_up1(sqrtf(tol)));
+    const float* ndr = aux.nd + (int64_t)acl * kpad;
+    int c = 0;
+    for (int j = tid; j < kpad; j += NT) c += ndr[j] <= R ? 1 : 0;
+    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
+    if (lane == 0) s_nc[wid] = c;
+    __syncthreads();
+    int nc = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) nc += s_nc[w];
+    nsub_t = max(1, (nc + 31) / 32);
+    nch_t = (nsub_t + NSUB - 1) / NSUB;
+  }
   if constexpr (LOOP) {
     // every wave is past the previous tile's appends: room for this tile's (<= TILE)?
     if (s_nchg > kChgBuf - TILE) flush_changed();
@@ -449,7 +506,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   for (int w = 1; w < NW; ++w) M = fmaxf(M, s_m[w]);
   // slack so that rounding of the MFMA sum cannot push a near-zero distance negative
   M = M * 1.0001f + 1e-6f;
-  for (int c = tid; c < kpad; c += NT) s_hn[c] = hn[c] + M;
+  for (int c = tid; c < nsub_t * 32; c += NT) s_hn[c] = hbase[c] + M;
 
   int bkey[PT], bsub[PT], bkey2[PT];
 #pragma unroll
@@ -509,11 +566,11 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   };
 
   issue(0);
-  if (NBUF >= 3 && nchunk > 1) issue(1);
-  if (NBUF >= 4 && nchunk > 2) issue(2);
-  for (int ch = 0; ch < nchunk; ++ch) {
+  if (NBUF >= 3 && nch_t > 1) issue(1);
+  if (NBUF >= 4 && nch_t > 2) issue(2);
+  for (int ch = 0; ch < nch_t; ++ch) {
     // chunk ch landed; chunks ch+1 .. ch+NBUF-2 stay in flight
-    const int ahead = NBUF >= 3 ? min(NBUF - 2, nchunk - 1 - ch) : 0;
+    const int ahead = NBUF >= 3 ? min(NBUF - 2, nch_t - 1 - ch) : 0;
     if constexpr (NBUF >= 4) {
       if (ahead >= 2) km_wait_vmcnt<2 * GPT>();
       else if (ahead == 1) km_wait_vmcnt<GPT>();
@@ -530,7 +587,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     // double: chunk ch+1 right away)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (NBUF == 2 && ch + 1 < nchunk) issue(ch + 1);
+    if (NBUF == 2 && ch + 1 < nch_t) issue(ch + 1);
     const uint4* img = s_c + (ch % NBUF) * CHP;
     uint4 a[KS];
     f32x16 hc;
@@ -538,6 +595,13 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
 #pragma unroll
     for (int sub = 0; sub < NSUB; ++sub) {
       const int cb = ch * CH + sub * 32;
+      if (CAND && ch * NSUB + sub >= nsub_t) {
+        // past the candidates (block-uniform): retire the deferred tile, feed dummies
+        reduce_tile(pacc, T0, pcb);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pacc[r] = __int_as_float(0x7fffffff);
+        continue;
+      }
       uint4 an[KS];
       f32x16 hn_next;
       if (PF && sub + 1 < NSUB) load_frag(img, sub + 1, cb + 32, an, hn_next);
@@ -574,16 +638,21 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
         }
       }
     }
-    if (NBUF >= 3 && ch + NBUF - 1 < nchunk) issue(ch + NBUF - 1);
+    if (NBUF >= 3 && ch + NBUF - 1 < nch_t) issue(ch + NBUF - 1);
   }
   reduce_tile(pacc, T0, pcb);
+  // CAND: every centre past the processed prefix is >= nd_first - |x - c_acl| from x
+  float nd_first = __builtin_inff();
+  if constexpr (CAND)
+    if (nsub_t * 32 < kpad) nd_first = aux.nd[(int64_t)acl * kpad + nsub_t * 32];
 
   // ---- decode, combine the two lane halves (same point, disjoint centre rows)
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     const int r = bkey[t] & 31;
     const float v = __int_as_float(bkey[t] & ~31);
-    const int mi = bsub[t] + (r & 3) + 8 * (r >> 2) + 4 * h;
+    int mi = bsub[t] + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if constexpr (CAND) mi = aux.nb[(int64_t)acl * kpad + mi];   // list position -> id
     auto sv = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     auto si = __builtin_amdgcn_permlane32_swap((uint32_t)mi, (uint32_t)mi, false, false);
     const float pv = __uint_as_float(h ? sv[0] : sv[1]);
@@ -602,7 +671,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     const int64_t p = pbase + t * 32 + cl;
     bool chg = false;
     int64_t row = 0;
-    if (h == 0 && p < n) {
+    if (h == 0 && p < pend) {
       // acc = 0.5|x-c|^2 + M - 0.5|x|^2
       const float dist = fmaxf(2.f * (bv - M) + x2[t], 0.f);
       row = idx ? (int64_t)idx[p] : p;
@@ -610,7 +679,9 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       if constexpr (LOOP) {
         const float dist2 = fmaxf(2.f * (bv2 - M) + x2[t], 0.f);
         aux.u[row] = km_up1(sqrtf(km_up1(dist + tol)));
-        aux.l[row] = fmaxf(km_dn1(sqrtf(fmaxf(km_dn1(dist2 - tol), 0.f))), 0.f);
+        float lo2 = km_dn1(sqrtf(fmaxf(km_dn1(dist2 - tol), 0.f)));
+        if constexpr (CAND) lo2 = fminf(lo2, km_dn1(nd_first - ub[t]));
+        aux.l[row] = fmaxf(lo2, 0.f);
         chg = bi != aux.a_prev[row];
       } else {
         if (mind) mind[row] = dist;
@@ -817,7 +888,9 @@ __global__ void __launch_bounds__(kScNT)
 kmeans_scatter_chunked_kernel(const int* __restrict__ assign, int64_t n_, int64_t rpc_, int k,
                               const int* __restrict__ block_offsets,
                               const int64_t* __restrict__ cluster_start, int* __restrict__ perm,
-                              const unsigned long long* __restrict__ ndev, int mul, int64_t chunk) {
+                              const unsigned long long* __restrict__ ndev, int mul, int64_t chunk,
+                              const int* __restrict__ vals = nullptr) {
+  // vals (optional): store vals[entry] instead of the entry index
   const SortGeom g = sort_geom(n_, rpc_, gridDim.x, ndev, mul, chunk);
   if ((int)blockIdx.x >= g.B) return;
   const int64_t n = g.n, rpc = g.rpc;
@@ -870,7 +943,8 @@ kmeans_scatter_chunked_kernel(const int* __restrict__ assign, int64_t n_, int64_
     for (int i = tid; i < m; i += kScNT) {
       const int v = stage[i];
       const int c = v >> 15;
-      perm[cursor[c] + (i - lstart[c])] = (int)(q0 + (v & 0x7fff));
+      const int64_t e = q0 + (v & 0x7fff);
+      perm[cursor[c] + (i - lstart[c])] = vals ? vals[e] : (int)e;
     }
     __syncthreads();
     for (int c = tid; c < k; c += kScNT) cursor[c] += lcnt[c];
@@ -962,6 +1036,39 @@ km_dexpand_kernel(const int32_t* __restrict__ changed, int64_t m, const int32_t*
     ec[e] = add ? a_new[row] : a_old[row];
     er[e] = add ? row : ~row;          // negative: subtract
   }
+}
+
+// Candidate-pruned K2 tiles: cluster c's run [cs[c], cs[c+1]) of the cluster-sorted active
+// rows is cut into ceil(run / tile) tiles; tile t -> (cluster, first position). One block
+// (k <= 2048): per-thread clusters, block exclusive scan of their tile counts.
+__global__ void __launch_bounds__(1024)
+km_tiles_kernel(const int64_t* __restrict__ cs, int k, int tile, int32_t* __restrict__ tile_cl,
+                int64_t* __restrict__ tile_lo, unsigned long long* __restrict__ n_tiles,
+                int64_t max_tiles) {
+  __shared__ int64_t s_part[1024 / 64];
+  const int per = (k + blockDim.x - 1) / blockDim.x;
+  const int c0 = threadIdx.x * per, c1 = min(k, c0 + per);
+  int64_t a = 0;
+  for (int c = c0; c < c1; ++c) a += (cs[c + 1] - cs[c] + tile - 1) / tile;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t ia = a;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t t = __shfl_up(ia, off);
+    if (lane >= off) ia += t;
+  }
+  if (lane == 63) s_part[wid] = ia;
+  __syncthreads();
+  int64_t t0 = ia - a;
+  for (int w = 0; w < wid; ++w) t0 += s_part[w];
+  for (int c = c0; c < c1; ++c) {
+    for (int64_t lo = cs[c]; lo < cs[c + 1]; lo += tile, ++t0) {
+      if (t0 < max_tiles) {
+        tile_cl[t0] = c;
+        tile_lo[t0] = lo;
+      }
+    }
+  }
+  if (c1 == k && c0 < k) *n_tiles = (unsigned long long)min(t0, max_tiles);
 }
 
 template <typename T, int DP, int NW>
@@ -1078,7 +1185,7 @@ static int device_cus() {
 // Device-resident count (mcount, n = its upper bound): a resident grid (MINB blocks per
 // CU) walks the tiles, so the launch needs no host sync.
 template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, bool TOP2 = false,
-          bool LOOP = false>
+          bool LOOP = false, bool CAND = false>
 static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                      const float* hn, int kpad, int* assign, float* mind,
                                      double* sse, int sse_mask, hipStream_t st,
@@ -1095,9 +1202,15 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
   if (LOOP && (aux.tol == nullptr || aux.u == nullptr || aux.l == nullptr || aux.a_prev == nullptr ||
                aux.changed == nullptr || aux.n_changed == nullptr))
     return hipErrorInvalidValue;
-  if (LOOP) grid = std::min<int64_t>(grid, (int64_t)device_cus() * MINB);
+  if (CAND && (aux.tile_cl == nullptr || aux.tile_lo == nullptr || aux.cstart == nullptr ||
+               aux.n_tiles == nullptr || aux.cnb == nullptr || aux.hnb == nullptr ||
+               aux.nb == nullptr || aux.nd == nullptr || idx == nullptr))
+    return hipErrorInvalidValue;
+  // CAND: up to n / TILE + k tiles (device count) -> always the resident grid
+  if (CAND) grid = (int64_t)device_cus() * MINB;
+  else if (LOOP) grid = std::min<int64_t>(grid, (int64_t)device_cus() * MINB);
   if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
-  auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF, TOP2, LOOP>;
+  auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF, TOP2, LOOP, CAND>;
   static size_t attr_set = 0;   // largest dynamic size this instantiation was enabled for
   if (dyn > attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1280,16 +1393,31 @@ hipError_t dalgo_kmeans_assign(const void* X, int is_bf16, int64_t n, int64_t ld
 hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP, const void* Cq,
                                    const float* hn, int kpad, const int32_t* idx, int* assign,
                                    float* mind, float* mind2, double* sse, int sse_mask, float* xh,
-                                   unsigned* xmax, const DalgoKmPost* post, hipStream_t st) {
+                                   unsigned* xmax, const DalgoKmPost* post, const DalgoKmCand* cand,
+                                   hipStream_t st) {
   if (m <= 0) return hipSuccess;
   if (kpad % 128 != 0) return hipErrorInvalidValue;
   KmAux aux{};
   aux.xh = xh;
   aux.xmax = xmax;
+  if (cand != nullptr && post == nullptr) return hipErrorInvalidValue;
   if (post != nullptr) {
     aux.mcount = post->mcount; aux.a_prev = post->a_prev; aux.tol = post->tol; aux.u = post->u;
     aux.l = post->l; aux.changed = post->changed; aux.n_changed = post->n_changed;
     aux.cap = post->cap;
+    if (cand != nullptr) {
+      // idx = the active rows sorted by cluster (dalgo_kmeans_sort_active)
+      aux.tile_cl = cand->tile_cl; aux.tile_lo = cand->tile_lo; aux.cstart = cand->cstart;
+      aux.n_tiles = cand->n_tiles; aux.cnb = (const uint16_t*)cand->cnb; aux.hnb = cand->hnb;
+      aux.nb = cand->nb; aux.nd = cand->nd;
+      if (DP == 128)
+        return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true, true, true>(
+            X, m, ldx, Cq, hn, kpad, assign, nullptr, sse, sse_mask, st, idx, nullptr, aux);
+      if (DP == 64)
+        return launch_assign_pipe<64, 4, 2, 4, 2, 2, false, true, true, true>(
+            X, m, ldx, Cq, hn, kpad, assign, nullptr, sse, sse_mask, st, idx, nullptr, aux);
+      return hipErrorInvalidValue;
+    }
     // top-2: 2 point tiles per wave (3 would spill past 256 VGPRs in the tile loop)
     if (DP == 128)
       return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true, true>(
@@ -1328,6 +1456,39 @@ hipError_t dalgo_kmeans_update(float* C, const float* S, const unsigned long lon
   else
     hipLaunchKernelGGL(kmeans_update_kernel<float>, dim3(grid), dim3(256), 0, st, C, S, cnt, k, d,
                        DP, (float*)Cq, hn, kpad, shift2);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+// Candidate-pruned K2 preparation: the active rows idx[0, *n_active) (cluster acl[e] each)
+// counting-sorted by cluster into rows_sorted, their cluster runs cstart[0..k], and the
+// tile table (tile -> cluster, first position; tiles of `tile` rows never straddle two
+// clusters). cap = the capacity of idx; B = the chunk bound of the sort (entries per chunk
+// `chunk`). No host sync: every launch derives its geometry from the device count.
+hipError_t dalgo_kmeans_sort_active(const int32_t* acl, const int32_t* idx, int64_t cap,
+                                    const unsigned long long* n_active, int k, int B, int64_t chunk,
+                                    int* block_counts, int64_t* cstart, int64_t* seg_start,
+                                    int32_t* rows_sorted, int tile, int32_t* tile_cl,
+                                    int64_t* tile_lo, unsigned long long* n_tiles,
+                                    int64_t max_tiles, hipStream_t st) {
+  if (cap <= 0) return hipSuccess;
+  if (k < 1 || k > kScKmax || B < 1 || chunk < 1 || tile < 1 || cap >= (int64_t)0x7fffffff ||
+      n_active == nullptr)
+    return hipErrorInvalidValue;
+  const int64_t rpc = cdiv(cap, B);
+  const size_t lds_k = (size_t)k * sizeof(int);
+  hipLaunchKernelGGL(kmeans_hist_kernel, dim3(B), dim3(256), lds_k, st, (const int*)acl, cap, rpc, k,
+                     block_counts, n_active, 1, chunk);
+  DALGO_LAUNCH_CHECK();
+  hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), 2 * lds_k, st, block_counts, B, k,
+                     1 << 20, cstart, seg_start, (unsigned long long*)nullptr, n_active, 1, chunk);
+  DALGO_LAUNCH_CHECK();
+  hipLaunchKernelGGL(kmeans_scatter_chunked_kernel, dim3(B), dim3(kScNT), 0, st, (const int*)acl, cap,
+                     rpc, k, (const int*)block_counts, (const int64_t*)cstart, (int*)rows_sorted,
+                     n_active, 1, chunk, (const int*)idx);
+  DALGO_LAUNCH_CHECK();
+  hipLaunchKernelGGL(km_tiles_kernel, dim3(1), dim3(1024), 0, st, (const int64_t*)cstart, k, tile,
+                     tile_cl, tile_lo, n_tiles, max_tiles);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -100,8 +100,12 @@ __global__ void __launch_bounds__(kDiffThreads)
 km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, float* __restrict__ l,
                  const float* __restrict__ delta, const float* __restrict__ s, int k, int64_t n,
                  int32_t* __restrict__ a_prev, int32_t* __restrict__ idx,
-                 unsigned long long* __restrict__ n_active, int64_t cap) {
+                 unsigned long long* __restrict__ n_active, int64_t cap,
+                 int32_t* __restrict__ acl) {
+  // acl (optional): cluster of every appended row, in list order (the candidate-pruned
+  // K2 sorts the active rows by it)
   __shared__ int32_t s_buf[kDiffBuf];
+  __shared__ int32_t s_cl[kDiffBuf];
   __shared__ int s_cnt;
   __shared__ unsigned long long s_base;
   __shared__ float s_md[kDiffThreads / 64];
@@ -124,7 +128,10 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, floa
     __syncthreads();
     const int64_t b = (int64_t)s_base;
     for (int j = threadIdx.x; j < m; j += kDiffThreads)
-      if (b + j < cap) idx[b + j] = s_buf[j];
+      if (b + j < cap) {
+        idx[b + j] = s_buf[j];
+        if (acl) acl[b + j] = s_cl[j];
+      }
     __syncthreads();
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
@@ -161,6 +168,7 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, floa
         l[i] = lb[e];
       } else if (act) {
         a_prev[i] = a[e];
+        u[i] = ub[e];      // the candidate-pruned K2 reads it (and rewrites it)
       }
       const uint64_t mask = __ballot(act);
       if (mask != 0) {
@@ -172,6 +180,7 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, floa
         if (act) {
           const uint64_t below = lane == 0 ? 0ull : (mask & (~0ull >> (64 - lane)));
           s_buf[b + __popcll(below)] = (int32_t)i;
+          s_cl[b + __popcll(below)] = a[e];
         }
       }
     }
@@ -245,6 +254,101 @@ km_centre_bounds_kernel(const T* __restrict__ cnow, const T* __restrict__ cprev,
   }
 }
 
+// Candidate lists of the pruned K2 (one block per centre a, kpad <= 2048, d <= 128, f64 on
+// the ROUNDED centres the assign kernel uses): nd[a][j] = the j-th smallest |c - c_a|
+// rounded down (relative 1e-6 margin, f32 round-down; +inf for the padding centres),
+// nb[a][.] = the same centres with each aligned group of 32 re-ordered by id (a group of
+// the list is one 32-centre sub-tile of K2, so any processed prefix of whole sub-tiles is
+// the same set as the distance order's), hnb / cnb = their 0.5|c|^2 and rows (the K2
+// chunk stream of a tile of cluster a is then contiguous). Also delta[a] and s[a] as
+// km_centre_bounds_kernel (one launch per iteration instead of two).
+__global__ void __launch_bounds__(256)
+km_centre_nbrs_kernel(const uint16_t* __restrict__ cq, const uint16_t* __restrict__ cprev,
+                      const float* __restrict__ hn, int k, int kpad, int d, int DP,
+                      float* __restrict__ delta, float* __restrict__ sout, float* __restrict__ nd,
+                      int32_t* __restrict__ nb, float* __restrict__ hnb, uint16_t* __restrict__ cnb) {
+  __shared__ double s_c[128];
+  __shared__ float s_d[2048];
+  __shared__ int32_t s_i[2048];
+  __shared__ int32_t s_g[2048];
+  __shared__ double s_red[2][4];
+  const int a = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  double dd = 0.0;
+  for (int j = tid; j < d; j += 256) {
+    const double v = (double)bf16_to_f32(cq[(int64_t)a * DP + j]);
+    s_c[j] = v;
+    const double b = v - (double)bf16_to_f32(cprev[(int64_t)a * DP + j]);
+    dd += b * b;
+  }
+  __syncthreads();
+  int P = 32;
+  while (P < kpad) P <<= 1;
+  double best = __builtin_inf();
+  for (int o = tid; o < P; o += 256) {
+    float dv = __builtin_inff();
+    if (o < k) {
+      const uint16_t* row = cq + (int64_t)o * DP;
+      double acc = 0.0;
+      for (int j = 0; j < d; ++j) {
+        const double t = s_c[j] - (double)bf16_to_f32(row[j]);
+        acc = fma(t, t, acc);
+      }
+      if (o != a) best = fmin(best, acc);
+      dv = o == a ? 0.f : dn1((float)(sqrt(acc) * (1.0 - 1e-6)));
+    }
+    s_d[o] = dv;
+    s_i[o] = o;
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    dd += __shfl_xor(dd, off);
+    best = fmin(best, __shfl_xor(best, off));
+  }
+  if (lane == 0) { s_red[0][wid] = dd; s_red[1][wid] = best; }
+  __syncthreads();
+  if (tid == 0) {
+    double x = 0.0, y = __builtin_inf();
+    for (int w = 0; w < 4; ++w) { x += s_red[0][w]; y = fmin(y, s_red[1][w]); }
+    delta[a] = up1((float)(sqrt(x) * (1.0 + 1e-6) + 1e-6));
+    sout[a] = k == 1 ? __builtin_inff() : dn1((float)(0.5 * sqrt(y) * (1.0 - 1e-6)));
+  }
+  // bitonic sort of (distance, id) ascending (ties by id: deterministic)
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int i = tid; i < P / 2; i += 256) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const float d0 = s_d[lo], d1 = s_d[hi];
+        const int i0 = s_i[lo], i1 = s_i[hi];
+        const bool gt = d0 > d1 || (d0 == d1 && i0 > i1);
+        if (gt == up) { s_d[lo] = d1; s_d[hi] = d0; s_i[lo] = i1; s_i[hi] = i0; }
+      }
+    }
+  }
+  __syncthreads();
+  // regroup: position of entry j inside its aligned group of 32 = its id rank there
+  const int64_t base = (int64_t)a * kpad;
+  for (int j = tid; j < kpad; j += 256) {
+    const int g0 = j & ~31, id = s_i[j];
+    int rank = 0;
+    for (int q = 0; q < 32; ++q) rank += s_i[g0 + q] < id ? 1 : 0;
+    s_g[g0 + rank] = id;
+    nd[base + j] = s_d[j];
+  }
+  __syncthreads();
+  for (int j = tid; j < kpad; j += 256) {
+    nb[base + j] = s_g[j];
+    hnb[base + j] = hn[s_g[j]];
+  }
+  const int pieces = DP / 8;                     // 16-B pieces per bf16 row
+  for (int q = tid; q < kpad * pieces; q += 256) {
+    const int j = q / pieces, pc = q - j * pieces;
+    const uint4 v = *reinterpret_cast<const uint4*>(cq + (int64_t)s_g[j] * DP + pc * 8);
+    *reinterpret_cast<uint4*>(cnb + (base + j) * DP + pc * 8) = v;
+  }
+}
+
 // Bounds after the full first pass: tol = 2 M 2^-14 with M = max 0.5|x|^2 * 1.0001 + 1e-6
 // (slack of a truncated kernel distance; xmax = the float bits K2 max-reduced),
 // u = sqrt(dist + tol) rounded up, l = sqrt(dist2 - tol) rounded down. One pass.
@@ -278,12 +382,13 @@ hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, 
 
 hipError_t dalgo_km_filter(const int32_t* assign, float* u, float* l, const float* delta,
                            const float* s, int k, int64_t n, int32_t* a_prev, int32_t* idx,
-                           unsigned long long* n_active, int64_t cap, hipStream_t st) {
+                           unsigned long long* n_active, int64_t cap, int32_t* acl,
+                           hipStream_t st) {
   if (n <= 0) return hipSuccess;
   int64_t g = (n + dalgo::kDiffThreads - 1) / dalgo::kDiffThreads;
   if (g > 2048) g = 2048;
   hipLaunchKernelGGL(dalgo::km_filter_kernel, dim3((unsigned)g), dim3(dalgo::kDiffThreads), 0, st,
-                     assign, u, l, delta, s, k, n, a_prev, idx, n_active, cap);
+                     assign, u, l, delta, s, k, n, a_prev, idx, n_active, cap, acl);
   return hipGetLastError();
 }
 
@@ -307,6 +412,18 @@ hipError_t dalgo_km_centre_bounds(const void* cnow, const void* cprev, int is_bf
   else
     hipLaunchKernelGGL(dalgo::km_centre_bounds_kernel<float>, dim3(k), dim3(256), 0, st,
                        (const float*)cnow, (const float*)cprev, k, d, DP, delta, s);
+  return hipGetLastError();
+}
+
+hipError_t dalgo_km_centre_nbrs(const void* cq, const void* cprev, const float* hn, int k, int kpad,
+                                int d, int DP, float* delta, float* s, float* nd, int32_t* nb,
+                                float* hnb, void* cnb, hipStream_t st) {
+  if (k <= 0) return hipSuccess;
+  if (d > 128 || d > DP || kpad > 2048 || kpad < k || kpad % 32 != 0 || DP % 8 != 0)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dalgo::km_centre_nbrs_kernel, dim3(k), dim3(256), 0, st,
+                     (const uint16_t*)cq, (const uint16_t*)cprev, hn, k, kpad, d, DP, delta, s, nd,
+                     nb, hnb, (uint16_t*)cnb);
   return hipGetLastError();
 }
 

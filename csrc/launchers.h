@@ -38,6 +38,18 @@ struct DalgoKmPost {
   long long cap;
 };
 
+// candidate-pruned K2 (dalgo_kmeans_sort_active + dalgo_km_centre_nbrs outputs)
+struct DalgoKmCand {
+  const int32_t* tile_cl;
+  const int64_t* tile_lo;
+  const int64_t* cstart;
+  const unsigned long long* n_tiles;
+  const void* cnb;                    // bf16 [k][kpad][DP]
+  const float* hnb;
+  const int32_t* nb;
+  const float* nd;
+};
+
 extern "C" {
 
 // ---- K1/K7/K10 logistic regression (lr_grad.hip)
@@ -122,7 +134,8 @@ hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, 
                          unsigned long long* n_changed, int64_t cap, hipStream_t st);
 hipError_t dalgo_km_filter(const int32_t* assign, float* u, float* l, const float* delta,
                            const float* s, int k, int64_t n, int32_t* a_prev, int32_t* idx,
-                           unsigned long long* n_active, int64_t cap, hipStream_t st);
+                           unsigned long long* n_active, int64_t cap, int32_t* acl,
+                           hipStream_t st);
 hipError_t dalgo_km_centre_bounds(const void* cnow, const void* cprev, int is_bf16, int k, int d,
                                   int DP, float* delta, float* s, hipStream_t st);
 hipError_t dalgo_km_qsum(const int32_t* assign, const float* xh, int64_t n, int k, double* Q,
@@ -130,7 +143,17 @@ hipError_t dalgo_km_qsum(const int32_t* assign, const float* xh, int64_t n, int 
 hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP, const void* Cq,
                                    const float* hn, int kpad, const int32_t* idx, int* assign,
                                    float* mind, float* mind2, double* sse, int sse_mask, float* xh,
-                                   unsigned* xmax, const DalgoKmPost* post, hipStream_t st);
+                                   unsigned* xmax, const DalgoKmPost* post,
+                                   const DalgoKmCand* cand, hipStream_t st);
+hipError_t dalgo_kmeans_sort_active(const int32_t* acl, const int32_t* idx, int64_t cap,
+                                    const unsigned long long* n_active, int k, int B, int64_t chunk,
+                                    int* block_counts, int64_t* cstart, int64_t* seg_start,
+                                    int32_t* rows_sorted, int tile, int32_t* tile_cl,
+                                    int64_t* tile_lo, unsigned long long* n_tiles,
+                                    int64_t max_tiles, hipStream_t st);
+hipError_t dalgo_km_centre_nbrs(const void* cq, const void* cprev, const float* hn, int k, int kpad,
+                                int d, int DP, float* delta, float* s, float* nd, int32_t* nb,
+                                float* hnb, void* cnb, hipStream_t st);
 hipError_t dalgo_km_bounds_init(const float* mind, const float* mind2, const unsigned* xmax,
                                 int64_t n, float* u, float* l, float* tol, hipStream_t st);
 

@@ -44,6 +44,8 @@ class KMeansConfig:
     seed: int = 42             # takeSample(False, k, 42)
     tol: float | None = None   # convergeDist-style early stop (reference ignores it)
     bound_filter: bool = True  # GPU bf16: Hamerly-filtered iterations after the first (exact)
+    candidates: bool = True    # ... whose K2 tiles (one cluster each) stream only the centres
+                               # near their cluster's centre (exact; k <= 2048)
 
 
 @dataclass
@@ -131,6 +133,10 @@ class KMeans:
         self._s = torch.empty(k, **f32)
         self._post_args = dict(m_dev=self._n_active, a_prev=self._a_prev, tol=self._tol, u=self._u,
                                l=self._l, changed=self._changed, n_changed=self._n_changed)
+        # candidate pruning (Exponion-style at tile granularity): the active rows sorted by
+        # cluster, every tile's centre stream cut to a prefix of its centre's neighbour list
+        self._cand = (K.CandWorkspace(self.dev, n, k, self.cen.Cq.shape[0], self.DP)
+                      if self.cfg.candidates and self.cen.Cq.shape[0] <= 2048 else None)
 
     def _ph(self, name: str):
         return self.timer.phase(name) if self.timer is not None else NULL_PHASE
@@ -206,16 +212,23 @@ class KMeans:
             self._record(1, 0)
             self._first = False
         else:
-            K.centre_bounds(self.cen.Cq, self._cq_prev, k, d, self._delta, self._s)
+            cw = self._cand
+            with self._ph("centres"):
+                if cw is not None:
+                    K.centre_nbrs(self.cen, self._cq_prev, self._delta, self._s, cw)
+                else:
+                    K.centre_bounds(self.cen.Cq, self._cq_prev, k, d, self._delta, self._s)
             with self._ph("filter"):
                 K.filter_rows(self.assign, self._u, self._l, self._delta, self._s, self._a_prev,
-                              self._idx, self._n_active)
+                              self._idx, self._n_active, cw.acl if cw is not None else None)
+                if cw is not None:
+                    K.sort_active(self._idx, self._n_active, cw)
             self._n_changed.zero_()
             with self._ph("assign"):
                 # K2 over the active rows; its epilogue updates u / l and collects the
                 # rows whose cluster changed
-                K.assign_rows(self.X, self.cen, self._idx, n, self.assign,
-                              post=self._post_args)
+                K.assign_rows(self.X, self.cen, cw.rows if cw is not None else self._idx, n,
+                              self.assign, post=self._post_args, cand=cw)
             with self._ph("accumulate_incremental"):
                 K.move_rows(self.X, self.DP, self._changed, self._n_changed, self.assign,
                             self._a_prev, self._S64, self._cnt64, self._mws, self._xh, self._Q)

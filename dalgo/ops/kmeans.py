@@ -225,17 +225,72 @@ def centre_bounds(Cq_now: torch.Tensor, Cq_prev: torch.Tensor, k: int, d: int,
 
 def filter_rows(assign: torch.Tensor, u: torch.Tensor, l: torch.Tensor, delta: torch.Tensor,
                 s: torch.Tensor, a_prev: torch.Tensor, idx: torch.Tensor,
-                n_active: torch.Tensor) -> None:
-    """Rows that may change cluster -> idx[:m] (their cluster -> a_prev), m -> n_active
+                n_active: torch.Tensor, acl: torch.Tensor | None = None) -> None:
+    """Rows that may change cluster -> idx[:m] (their cluster -> a_prev, and -> acl[:m] in
+    list order when given; u of the kept rows becomes u + delta[a]), m -> n_active
     (device; no sync). The largest centre shift is reduced from delta in the kernel."""
     n_active.zero_()
-    _ext.ops().kmeans_filter(assign, u, l, delta, s, a_prev, idx, n_active)
+    _ext.ops().kmeans_filter(assign, u, l, delta, s, a_prev, idx, n_active, acl)
+
+
+# ------------------------------------------------- candidate-pruned K2 (filtered iterations)
+CAND_TILE = 256          # rows per K2 block tile (4 waves x 2 point tiles x 32)
+
+
+class CandWorkspace:
+    """Buffers of the candidate-pruned filtered iteration for n rows, k clusters (kpad
+    padded) and DP columns: per-centre neighbour lists (nd / nb / hnb and the
+    neighbour-ordered centre rows cnb, k * kpad * DP bf16: 256 MB at k = 1024, DP = 128),
+    the cluster-sorted active rows and the tile table."""
+
+    def __init__(self, device, n: int, k: int, kpad: int, DP: int):
+        i32 = dict(dtype=torch.int32, device=device)
+        i64 = dict(dtype=torch.int64, device=device)
+        f32 = dict(dtype=torch.float32, device=device)
+        n = max(1, int(n))
+        self.k, self.kpad = int(k), int(kpad)
+        self.nd = torch.empty(k * kpad, **f32)
+        self.nb = torch.empty(k * kpad, **i32)
+        self.hnb = torch.empty(k * kpad, **f32)
+        self.cnb = torch.empty(k * kpad * DP, dtype=torch.bfloat16, device=device)
+        self.acl = torch.empty(n, **i32)
+        self.rows = torch.empty(n, **i32)
+        bmax = max(1, (n + CHUNK_ROWS - 1) // CHUNK_ROWS)
+        self.block_counts = torch.empty(bmax * k, **i32)
+        self.cstart = torch.empty(k + 1, **i64)
+        self.seg_start = torch.empty(k + 1, **i64)
+        tiles = (n + CAND_TILE - 1) // CAND_TILE + k
+        self.tile_cl = torch.empty(tiles, **i32)
+        self.tile_lo = torch.empty(tiles, **i64)
+        self.n_tiles = torch.zeros(1, **i64)
+
+    def cand(self):
+        return [self.tile_cl, self.tile_lo, self.cstart, self.n_tiles, self.cnb, self.hnb,
+                self.nb, self.nd]
+
+
+def centre_nbrs(cen: Centers, Cq_prev: torch.Tensor, delta: torch.Tensor, s: torch.Tensor,
+                ws: CandWorkspace):
+    """delta / s as centre_bounds, plus every centre's neighbour lists for the pruned K2
+    (one launch, kmeans_inc.hip km_centre_nbrs_kernel)."""
+    _ext.ops().kmeans_centre_nbrs(cen.Cq, Cq_prev, cen.hn, ws.k, cen.d, delta, s, ws.nd, ws.nb,
+                                  ws.hnb, ws.cnb)
+
+
+def sort_active(idx: torch.Tensor, n_active: torch.Tensor, ws: CandWorkspace):
+    """The active rows idx[:*n_active] (clusters in ws.acl) sorted by cluster -> ws.rows,
+    cluster runs -> ws.cstart, tiles of CAND_TILE rows of one cluster -> ws.tile_cl /
+    tile_lo / n_tiles (4 launches, device counts only)."""
+    _ext.ops().kmeans_sort_active(ws.acl, idx, n_active, ws.k, CHUNK_ROWS, ws.block_counts,
+                                  ws.cstart, ws.seg_start, ws.rows, CAND_TILE, ws.tile_cl,
+                                  ws.tile_lo, ws.n_tiles)
 
 
 def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
                 assign: torch.Tensor, mind: torch.Tensor | None = None,
                 mind2: torch.Tensor | None = None, xh: torch.Tensor | None = None,
-                xmax: torch.Tensor | None = None, post: dict | None = None):
+                xmax: torch.Tensor | None = None, post: dict | None = None,
+                cand: CandWorkspace | None = None):
     """K2 (pipelined form) over the rows idx[:m] (all rows when idx is None).
 
     Full pass: assign / mind (and the second-best distance mind2, a lower bound, when
@@ -244,13 +299,18 @@ def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
     filtered-iteration form -- the row count is m_dev (device; m its upper bound) and
     the epilogue writes the Hamerly bounds u / l (rounded outward, tol on the device)
     and appends the rows whose cluster differs from a_prev to changed (count in
-    n_changed, which the caller zeroes): no host sync, no separate bound pass."""
+    n_changed, which the caller zeroes): no host sync, no separate bound pass.
+    ``cand`` (with post; idx = cand.rows, the active rows sorted by cluster): the
+    candidate-pruned form -- a tile of cluster a only streams the centres within
+    2 max(u) + slack of c_a (a prefix of a's neighbour list), and the pruned centres
+    enter the new lower bound as nd_first - u."""
     if post is None:
         _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, mind, mind2, xh, xmax)
         return
     _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, None, None, None, None,
                                  post["m_dev"], post["a_prev"], post["tol"], post["u"], post["l"],
-                                 post["changed"], post["n_changed"])
+                                 post["changed"], post["n_changed"],
+                                 cand.cand() if cand is not None else [])
 
 
 def bounds_init(mind: torch.Tensor, mind2: torch.Tensor, xmax: torch.Tensor, n: int,

@@ -851,3 +851,158 @@ def test_kmeans_bound_filter_exact(cuda):
     same = (a.centers - b.centers).abs().amax(dim=1) < 1e-2
     assert same.float().mean().item() > 0.9
     assert a.active_history[0] == n and min(a.active_history[1:]) < 0.3 * n
+
+
+@pytest.mark.parametrize("k,d", [(1, 8), (37, 30), (1024, 128)])
+def test_kmeans_centre_nbrs_kernel(cuda, k, d):
+    """Neighbour lists of the candidate-pruned K2: nd ascending lower bounds of the centre
+    distances, nb = the same order with each aligned 32-group re-ordered by id, hnb / cnb
+    gathered through nb; delta / s equal the plain centre-bounds kernel's."""
+    torch.manual_seed(k + d)
+    cen = K.make_centers(torch.randn(k, d) * 3, torch.bfloat16, cuda)
+    kpad, DP = cen.Cq.shape
+    prev = cen.Cq[:k].clone()
+    prev[:, :d] = (prev[:, :d].float() + 0.1 * torch.randn(k, d, device=cuda)).to(torch.bfloat16)
+    ws = K.CandWorkspace(cuda, 1000, k, kpad, DP)
+    delta = torch.empty(k, device=cuda)
+    s = torch.empty(k, device=cuda)
+    K.centre_nbrs(cen, prev, delta, s, ws)
+    d0, s0 = K.centre_bounds(cen.Cq, prev, k, d)
+    assert torch.equal(delta, d0) and torch.equal(s, s0)
+    C = cen.Cq[:k, :d].double()
+    D = torch.cdist(C, C)
+    nd = ws.nd.view(k, kpad)
+    nb = ws.nb.view(k, kpad).long()
+    assert bool((nd[:, 1:] >= nd[:, :-1]).all())
+    assert bool(torch.isinf(nd[:, k:]).all())
+    sd = torch.sort(D, dim=1).values
+    assert bool((nd[:, :k].double() <= sd + 1e-9).all())
+    assert torch.allclose(nd[:, :k].double(), sd, rtol=1e-5, atol=1e-5)
+    for g in range(0, kpad, 32):
+        grp = nb[:, g:g + 32]
+        assert bool((grp[:, 1:] > grp[:, :-1]).all())            # ids ascending per group
+    # each group holds the centres of those distance ranks
+    got = torch.where(nb < k, D.gather(1, nb.clamp(max=k - 1)),
+                      torch.full(nb.shape, float("inf"), dtype=torch.float64, device=cuda))
+    for g in range(0, kpad, 32):
+        hi = torch.sort(got[:, g:g + 32], dim=1).values
+        ref = torch.cat([sd, torch.full((k, kpad - k), float("inf"), device=cuda, dtype=torch.float64)], 1)[:, g:g + 32]
+        assert torch.allclose(hi, ref, rtol=1e-5, atol=1e-5)
+    assert torch.equal(ws.hnb.view(k, kpad), cen.hn[nb])
+    assert torch.equal(ws.cnb.view(k, kpad, DP), cen.Cq[nb])
+
+
+def test_kmeans_sort_active(cuda):
+    """Active rows counting-sorted by cluster with a device count, cluster runs and the
+    tile table (tiles never straddle clusters)."""
+    torch.manual_seed(4)
+    n, k, m = 300_001, 97, 123_457
+    ws = K.CandWorkspace(cuda, n, k, 128, 64)
+    idx = torch.randperm(n, device=cuda).to(torch.int32)
+    ws.acl.copy_(torch.randint(0, k, (n,), device=cuda, dtype=torch.int32))
+    cnt = torch.tensor([m], dtype=torch.int64, device=cuda)
+    K.sort_active(idx, cnt, ws)
+    acl, rows = ws.acl[:m].long(), ws.rows[:m].long()
+    cl_of_row = torch.full((n,), -1, dtype=torch.long, device=cuda)
+    cl_of_row[idx[:m].long()] = acl
+    assert torch.equal(torch.sort(rows).values, torch.sort(idx[:m].long()).values)
+    cs = ws.cstart
+    assert torch.equal(cs, torch.cat([torch.zeros(1, dtype=torch.long, device=cuda),
+                                      torch.cumsum(torch.bincount(acl, minlength=k), 0)]))
+    rc = cl_of_row[rows]
+    assert bool((rc[1:] >= rc[:-1]).all())
+    T = int(ws.n_tiles.item())
+    ref = sum((int(cs[c + 1] - cs[c]) + K.CAND_TILE - 1) // K.CAND_TILE for c in range(k))
+    assert T == ref
+    tc, tl = ws.tile_cl[:T].long(), ws.tile_lo[:T]
+    assert bool((tl >= cs[tc]).all()) and bool((tl < cs[tc + 1]).all())
+    assert bool(((tl - cs[tc]) % K.CAND_TILE == 0).all())
+
+
+def test_kmeans_assign_rows_candidates(cuda):
+    """Candidate-pruned filtered K2 (tiles of one cluster stream only the centres within
+    2 max(u) + slack of their centre): same assignment as the full pass on the active
+    rows (mismatches only at kernel-rounding near-ties), the pruned centres bound l from
+    below, the changed rows are collected exactly."""
+    torch.manual_seed(12)
+    from dalgo.data.synthetic import blobs
+    n, d, k = 120_000, 128, 512
+    X = K.prepare_points(blobs(n, d, k, device=cuda, dtype=torch.bfloat16, seed=4))
+    g = torch.Generator(device="cpu").manual_seed(2)
+    C0 = X[torch.randperm(n, generator=g)[:k].to(cuda), :d].float()
+    cen = K.make_centers(C0 + 0.5 * torch.randn_like(C0), torch.bfloat16, cuda)
+    full = K.assign(X, cen)
+    a0 = torch.empty(n, dtype=torch.int32, device=cuda)
+    mind = torch.zeros(n, device=cuda)
+    mind2 = torch.zeros(n, device=cuda)
+    xmax = torch.zeros(1, dtype=torch.int32, device=cuda)
+    K.assign_rows(X, cen, None, n, a0, mind, mind2, xh=torch.zeros(n, device=cuda), xmax=xmax)
+    u0 = torch.empty(n, device=cuda)
+    l0 = torch.empty(n, device=cuda)
+    tol = torch.zeros(1, device=cuda)
+    K.bounds_init(mind, mind2, xmax, n, u0, l0, tol)
+    kpad, DP = cen.Cq.shape
+    ws = K.CandWorkspace(cuda, n, k, kpad, DP)
+    K.centre_nbrs(cen, cen.Cq[:k].clone(), torch.empty(k, device=cuda), torch.empty(k, device=cuda), ws)
+    # active rows: a random subset; a_prev = the truth with a third of them perturbed, u =
+    # a valid upper bound of the distance to c_{a_prev}
+    m = 50_001
+    rows = torch.randperm(n, device=cuda)[:m].to(torch.int32)
+    a_prev = full.clone()
+    flip = torch.zeros(n, dtype=torch.bool, device=cuda)
+    flip[rows[: m // 3].long()] = True
+    a_prev[flip] = (a_prev[flip] + 1) % k
+    dprev = (X[:, :d].float() - cen.Cq[a_prev.long(), :d].float()).norm(dim=1)
+    u = dprev * 1.001 + 1e-3
+    l = torch.full((n,), -1.0, device=cuda)
+    ws.acl[:m].copy_(a_prev[rows.long()])
+    cnt = torch.tensor([m], dtype=torch.int64, device=cuda)
+    K.sort_active(rows, cnt, ws)
+    a = torch.full((n,), -7, dtype=torch.int32, device=cuda)
+    changed = torch.empty(n, dtype=torch.int32, device=cuda)
+    nch = torch.zeros(1, dtype=torch.int64, device=cuda)
+    K.assign_rows(X, cen, ws.rows, n, a, post=dict(
+        m_dev=cnt, a_prev=a_prev, tol=tol, u=u, l=l, changed=changed, n_changed=nch), cand=ws)
+    sel = torch.zeros(n, dtype=torch.bool, device=cuda)
+    sel[rows.long()] = True
+    assert bool((a[~sel] == -7).all())
+    dist = torch.cdist(X[:, :d].double(), cen.Cq[:k, :d].double())
+    bad = sel & (a != full)
+    if bool(bad.any()):
+        db = dist[bad].gather(1, a[bad].long()[:, None])[:, 0]
+        df = dist[bad].gather(1, full[bad].long()[:, None])[:, 0]
+        assert float(((db - df).abs() / df).max()) < 1e-4
+    assert int(bad.sum()) <= 5
+    two = torch.topk(dist, 2, dim=1, largest=False).values
+    t = float(tol.item())
+    assert bool((u[sel].double() >= two[sel, 0] - 1e-3).all())
+    assert bool((u[sel].double() <= torch.sqrt(two[sel, 0] ** 2 + 2 * t) + 1e-3).all())
+    assert bool((l[sel].double() <= two[sel, 1] + 1e-3).all())
+    assert bool((l[sel] >= 0).all())
+    c = int(nch.item())
+    exp = torch.nonzero(sel & (a != a_prev))[:, 0]
+    assert c == exp.numel()
+    assert torch.equal(torch.sort(changed[:c]).values.long(), exp)
+
+
+def test_kmeans_candidates_match_plain(cuda):
+    """Filtered Lloyd with candidate-pruned tiles == without == plain Lloyd (SSE
+    trajectory, centres), and the pruned run re-assigns the same rows."""
+    from dalgo.data.synthetic import blobs
+    from dalgo.models.kmeans import KMeans, KMeansConfig
+    n, d, k = 300_000, 128, 1000
+    X = blobs(n, d, k, device=cuda, dtype=torch.bfloat16, seed=11)
+    runs = {}
+    for name, kw in [("cand", {}), ("bounds", dict(candidates=False)),
+                     ("plain", dict(bound_filter=False))]:
+        km = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5, **kw), X, 0, n)
+        km.fit()
+        runs[name] = km
+    assert runs["cand"]._cand is not None and runs["bounds"]._cand is None
+    for other in ("bounds", "plain"):
+        assert np.allclose(runs["cand"].history.sse, runs[other].history.sse, rtol=2e-4)
+        same = (runs["cand"].centers - runs[other].centers).abs().amax(dim=1) < 1e-2
+        assert same.float().mean().item() > 0.9
+    # the pruned centres enter l as nd_first - u (looser): never fewer active rows
+    ha, hb = runs["cand"].active_history, runs["bounds"].active_history
+    assert ha[0] == n and len(ha) == len(hb)
