@@ -548,12 +548,13 @@ void kmeans_qsum(const Tensor& assign, const Tensor& xh, int64_t k, Tensor Q) {
 // K2 (variant 52) over the rows idx[0, m) only
 void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
                        const std::optional<Tensor>& idx, int64_t m, Tensor assign,
+                       at::TensorList cand,
                        const std::optional<Tensor>& mind, const std::optional<Tensor>& mind2,
                        const std::optional<Tensor>& xh, const std::optional<Tensor>& xmax,
                        const std::optional<Tensor>& m_dev, const std::optional<Tensor>& a_prev,
                        const std::optional<Tensor>& tol, const std::optional<Tensor>& u,
                        const std::optional<Tensor>& l, const std::optional<Tensor>& changed,
-                       const std::optional<Tensor>& n_changed, at::TensorList cand) {
+                       const std::optional<Tensor>& n_changed) {
   TORCH_CHECK(Cq.dim() == 2 && Cq.is_contiguous() && Cq.scalar_type() == at::kBFloat16, "Cq bf16");
   const int DP = (int)Cq.size(1);
   TORCH_CHECK(DP == 64 || DP == 128, "kmeans_assign_idx: DP 64 or 128");
@@ -1198,10 +1199,10 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(b!) s) -> ()");
   m.def("kmeans_qsum(Tensor assign, Tensor xh, int k, Tensor(a!) Q) -> ()");
   m.def("kmeans_assign_idx(Tensor X, Tensor Cq, Tensor hn, Tensor? idx, int m, Tensor(a!) assign, "
+        "Tensor[] cand, "
         "Tensor(b!)? mind=None, Tensor(c!)? mind2=None, Tensor(d!)? xh=None, Tensor(e!)? xmax=None, "
         "Tensor? m_dev=None, Tensor? a_prev=None, Tensor? tol=None, Tensor(f!)? u=None, "
-        "Tensor(g!)? l=None, Tensor(h!)? changed=None, Tensor(i!)? n_changed=None, "
-        "Tensor[] cand=[]) -> ()");
+        "Tensor(g!)? l=None, Tensor(h!)? changed=None, Tensor(i!)? n_changed=None) -> ()");
   m.def("kmeans_bounds_init(Tensor mind, Tensor mind2, Tensor xmax, int n, Tensor(a!) u, "
         "Tensor(b!) l, Tensor(c!) tol) -> ()");
   m.def("kmeans_update(Tensor(a!) C, Tensor S, Tensor cnt, Tensor(b!) Cq, Tensor(c!) hn, "

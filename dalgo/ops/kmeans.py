@@ -305,12 +305,13 @@ def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
     2 max(u) + slack of c_a (a prefix of a's neighbour list), and the pruned centres
     enter the new lower bound as nd_first - u."""
     if post is None:
-        _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, mind, mind2, xh, xmax)
+        _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, [], mind, mind2, xh,
+                                     xmax)
         return
-    _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, None, None, None, None,
+    _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign,
+                                 cand.cand() if cand is not None else [], None, None, None, None,
                                  post["m_dev"], post["a_prev"], post["tol"], post["u"], post["l"],
-                                 post["changed"], post["n_changed"],
-                                 cand.cand() if cand is not None else [])
+                                 post["changed"], post["n_changed"])
 
 
 def bounds_init(mind: torch.Tensor, mind2: torch.Tensor, xmax: torch.Tensor, n: int,

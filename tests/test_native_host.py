@@ -9,6 +9,7 @@ launchers' argument validation, which must reject bad shapes before any HIP call
 """
 import os
 import shutil
+from pathlib import Path
 import subprocess
 
 import numpy as np
@@ -57,3 +58,21 @@ def test_native_host_checks_asan(host_binary):
         # block b of stream t = indices 4b..4b+3 of the NumPy mirror
         exp = philox.draw_u32(s, t, np.uint64(4 * b) + np.arange(4, dtype=np.uint64))
         assert tuple(int(x) for x in exp) == g, (s, t, b)
+
+
+def test_extension_loads_and_registers_ops():
+    """The built extension loads in a fresh process on the CPU host (HIP runtime present,
+    no GPU needed) and every operator schema parses: a schema error aborts the process
+    at load time, which only a GPU box would otherwise reveal."""
+    import subprocess
+    import sys
+    from dalgo.ops import _ext
+    lib = _ext.lib_path() if hasattr(_ext, "lib_path") else _ext._LIB
+    if not Path(lib).exists():
+        pytest.skip("extension not built")
+    code = ("import torch; torch.ops.load_library(%r); "
+            "print(len([s for s in torch._C._jit_get_all_schemas() if s.name.startswith('dalgo::')]))"
+            % str(lib))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert int(r.stdout.strip().splitlines()[-1]) >= 30
