@@ -701,7 +701,7 @@ def test_kmeans_assign_rows_indirect(cuda):
 
 def test_kmeans_filter_matches_torch(cuda):
     """Bound filter (maxd reduced in-kernel from delta, bounds rounded outward) == torch;
-    the active count stays on the device."""
+    the active count stays on the device; with acl, the kept rows' clusters in list order."""
     torch.manual_seed(6)
     n, k = 100_003, 50
     assign = torch.randint(0, k, (n,), dtype=torch.int32, device=cuda)
@@ -714,8 +714,10 @@ def test_kmeans_filter_matches_torch(cuda):
     a_prev = torch.full((n,), -1, dtype=torch.int32, device=cuda)
     idx = torch.empty(n, dtype=torch.int32, device=cuda)
     cnt = torch.zeros(1, dtype=torch.int64, device=cuda)
-    K.filter_rows(assign, u, l, delta, s, a_prev, idx, cnt)
+    acl = torch.full((n,), -1, dtype=torch.int32, device=cuda)
+    K.filter_rows(assign, u, l, delta, s, a_prev, idx, cnt, acl)
     m = int(cnt.item())
+    assert torch.equal(acl[:m], assign[idx[:m].long()])
     ub = u0 + delta[assign.long()]
     lb = l0 - maxd
     act = ~(ub < torch.maximum(s[assign.long()], lb))
@@ -724,7 +726,9 @@ def test_kmeans_filter_matches_torch(cuda):
     assert torch.equal(torch.sort(idx[:m]).values.long(), torch.nonzero(act)[:, 0])
     assert bool((u[~act] >= ub[~act]).all()) and torch.allclose(u[~act], ub[~act])
     assert bool((l[~act] <= lb[~act]).all()) and torch.allclose(l[~act], lb[~act])
-    assert torch.equal(u[act], u0[act]) and torch.equal(l[act], l0[act])
+    # kept rows: u becomes the shifted bound (the candidate-pruned K2 reads it), l unchanged
+    assert bool((u[act] >= ub[act]).all()) and torch.allclose(u[act], ub[act])
+    assert torch.equal(l[act], l0[act])
     assert torch.equal(a_prev[act], assign[act])
 
 
