@@ -345,7 +345,6 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   extern __shared__ __attribute__((aligned(16))) float s_hn[];   // [kpad]: 0.5|c|^2 + M
   __shared__ float s_m[NW];
   __shared__ float s_r[NW];
-  __shared__ int s_nc[NW];
   __shared__ double s_sse[NW];
 
   __shared__ int s_chg[LOOP ? kChgBuf : 1];
@@ -429,7 +428,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // ---- points (B operand, negated), resident for the whole sweep; rows past n are zero
   uint4 bf[PT][KS];
   float x2[PT];                                // |x|^2 of the lane's point (both halves)
-  float ub[CAND ? PT : 1];                     // CAND: filter's bound on |x - c_acl|
+  float ua[CAND ? PT : 1];                     // CAND: bound on |x - c_acl| (from chunk 0)
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     const int64_t p = pbase + t * 32 + cl;
@@ -441,61 +440,81 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       const uint4 v = *reinterpret_cast<const uint4*>(src + 16 * s);
       bf[t][s] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
     }
-    if constexpr (CAND) ub[t] = ok ? aux.u[row] : 0.f;
   }
   // all ordinary loads retired before the DMA stream starts, and the fragments pinned
   // here, so the compiler's own waits never drain a chunk in flight (vmcnt(0) in-loop)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float mx = 0.f;
+  // CAND: the lane's half of c_acl (same k layout as the point fragments), for the exact
+  // distance of every tile point to its cluster's centre (v_dot2 on the bf16 pairs)
+  uint4 ca[CAND ? KS : 1];
+  if constexpr (CAND) {
+    const uint16_t* src = Cq + (int64_t)acl * DP + h * 8;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) ca[s] = *reinterpret_cast<const uint4*>(src + 16 * s);
+  }
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     float q = 0.f;
+    float dt = 0.f;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       asm volatile("" : "+v"(bf[t][s].x), "+v"(bf[t][s].y), "+v"(bf[t][s].z), "+v"(bf[t][s].w));
       q += sq_sum(bf[t][s], uint16_t{});
+      if constexpr (CAND) {
+        const uint32_t xw[4] = {bf[t][s].x, bf[t][s].y, bf[t][s].z, bf[t][s].w};
+        const uint32_t cw[4] = {ca[s].x, ca[s].y, ca[s].z, ca[s].w};
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+          dt = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, xw[w]),
+                                               __builtin_bit_cast(bf16x2, cw[w]), dt, false);
+      }
       bf[t][s] = make_uint4(bf[t][s].x ^ 0x80008000u, bf[t][s].y ^ 0x80008000u,
                             bf[t][s].z ^ 0x80008000u, bf[t][s].w ^ 0x80008000u);
     }
     auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(q), __float_as_uint(q), false, false);
     x2[t] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
     mx = fmaxf(mx, 0.5f * x2[t]);
+    if constexpr (CAND) {
+      auto sd = __builtin_amdgcn_permlane32_swap(__float_as_uint(dt), __float_as_uint(dt), false, false);
+      const float dot = __uint_as_float(sd[0]) + __uint_as_float(sd[1]);
+      // |x - c|^2 = |x|^2 - 2 x.c + 2 hn (f32 error far below tol: the K2 slack)
+      const float dist = fmaxf(x2[t] - 2.f * dot + 2.f * hn[acl], 0.f);
+      ua[t] = km_up1(sqrtf(km_up1(dist + tol)));
+    }
   }
   for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
   my_xmax = fmaxf(my_xmax, mx);
-  float um = 0.f;
-  if constexpr (CAND) {
-#pragma unroll
-    for (int t = 0; t < PT; ++t) um = fmaxf(um, ub[t]);
-    for (int off = 32; off >= 1; off >>= 1) um = fmaxf(um, __shfl_xor(um, off));
-  }
   // the previous tile's waves are past every read of s_m / s_hn / the chunk buffers
   // (each crossed this tile's chunk barriers' predecessor: the last chunk barrier of the
   // previous tile precedes all of its reads), so the block barrier below orders the
   // rewrite after them
+  float um = 0.f;
+  if constexpr (CAND) {
+#pragma unroll
+    for (int t = 0; t < PT; ++t)
+      if (pbase + t * 32 + cl < pend) um = fmaxf(um, ua[t]);
+    for (int off = 32; off >= 1; off >>= 1) um = fmaxf(um, __shfl_xor(um, off));
+  }
   if (lane == 0) { s_m[wid] = mx; if constexpr (CAND) s_r[wid] = um; }
   __syncthreads();
-  // CAND: only centres c with |c - c_acl| <= R can be the nearest of a tile point
-  // (|x - c| >= |c - c_acl| - |x - c_acl| > |x - c_acl| for |c - c_acl| > 2 u >= 2|x - c_acl|),
-  // R = 2 max u + sqrt(tol) (slack of the kernel distances); nd is ascending, so they are
-  // a prefix of the neighbour list: nsub_t 32-centre sub-tiles of it
-  int nsub_t = nchunk * NSUB, nch_t = nchunk;
+  // CAND: the tile's centre stream is cluster acl's neighbour list. ua >= |x - c_acl| for
+  // every tile point, so only centres c with |c - c_acl| <= R = 2 max ua can be the
+  // nearest of one (|x - c| >= |c - c_acl| - |x - c_acl| > |x - c_acl| otherwise); nd is
+  // ascending, so they are a prefix of the list: nch_t whole chunks of it. Every wave
+  // finds the count by a two-level search of nd (all agree: no barrier)
+  int nch_t = nchunk;
   if constexpr (CAND) {
     float R = s_r[0];
 #pragma unroll
     for (int w = 1; w < NW; ++w) R = fmaxf(R, s_r[w]);
-    R = km_up1(km_up1(2.f * R) + km_up1(sqrtf(tol)));
+    R = km_up1(2.f * R);
     const float* ndr = aux.nd + (int64_t)acl * kpad;
-    int c = 0;
-    for (int j = tid; j < kpad; j += NT) c += ndr[j] <= R ? 1 : 0;
-    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
-    if (lane == 0) s_nc[wid] = c;
-    __syncthreads();
-    int nc = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) nc += s_nc[w];
-    nsub_t = max(1, (nc + 31) / 32);
-    nch_t = (nsub_t + NSUB - 1) / NSUB;
+    const int S = kpad / 64;                      // kpad % 128 == 0: S >= 2
+    const int cc = __popcll(__ballot(ndr[lane * S] <= R));   // >= 1 (nd[0] = 0)
+    const int j = (cc - 1) * S + lane;
+    const int nc = (cc - 1) * S + __popcll(__ballot(lane < S && j < kpad && ndr[j] <= R));
+    nch_t = max(1, (nc + CH - 1) / CH);
   }
   if constexpr (LOOP) {
     // every wave is past the previous tile's appends: room for this tile's (<= TILE)?
@@ -506,7 +525,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   for (int w = 1; w < NW; ++w) M = fmaxf(M, s_m[w]);
   // slack so that rounding of the MFMA sum cannot push a near-zero distance negative
   M = M * 1.0001f + 1e-6f;
-  for (int c = tid; c < nsub_t * 32; c += NT) s_hn[c] = hbase[c] + M;
+  for (int c = tid; c < nch_t * CH; c += NT) s_hn[c] = hbase[c] + M;
 
   int bkey[PT], bsub[PT], bkey2[PT];
 #pragma unroll
@@ -595,13 +614,6 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
 #pragma unroll
     for (int sub = 0; sub < NSUB; ++sub) {
       const int cb = ch * CH + sub * 32;
-      if (CAND && ch * NSUB + sub >= nsub_t) {
-        // past the candidates (block-uniform): retire the deferred tile, feed dummies
-        reduce_tile(pacc, T0, pcb);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) pacc[r] = __int_as_float(0x7fffffff);
-        continue;
-      }
       uint4 an[KS];
       f32x16 hn_next;
       if (PF && sub + 1 < NSUB) load_frag(img, sub + 1, cb + 32, an, hn_next);
@@ -644,7 +656,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // CAND: every centre past the processed prefix is >= nd_first - |x - c_acl| from x
   float nd_first = __builtin_inff();
   if constexpr (CAND)
-    if (nsub_t * 32 < kpad) nd_first = aux.nd[(int64_t)acl * kpad + nsub_t * 32];
+    if (nch_t * CH < kpad) nd_first = aux.nd[(int64_t)acl * kpad + nch_t * CH];
 
   // ---- decode, combine the two lane halves (same point, disjoint centre rows)
 #pragma unroll
@@ -680,7 +692,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
         const float dist2 = fmaxf(2.f * (bv2 - M) + x2[t], 0.f);
         aux.u[row] = km_up1(sqrtf(km_up1(dist + tol)));
         float lo2 = km_dn1(sqrtf(fmaxf(km_dn1(dist2 - tol), 0.f)));
-        if constexpr (CAND) lo2 = fminf(lo2, km_dn1(nd_first - ub[t]));
+        if constexpr (CAND) lo2 = fminf(lo2, km_dn1(nd_first - ua[t]));
         aux.l[row] = fmaxf(lo2, 0.f);
         chg = bi != aux.a_prev[row];
       } else {

@@ -168,7 +168,6 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, floa
         l[i] = lb[e];
       } else if (act) {
         a_prev[i] = a[e];
-        u[i] = ub[e];      // the candidate-pruned K2 reads it (and rewrites it)
       }
       const uint64_t mask = __ballot(act);
       if (mask != 0) {

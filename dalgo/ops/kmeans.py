@@ -227,8 +227,8 @@ def filter_rows(assign: torch.Tensor, u: torch.Tensor, l: torch.Tensor, delta: t
                 s: torch.Tensor, a_prev: torch.Tensor, idx: torch.Tensor,
                 n_active: torch.Tensor, acl: torch.Tensor | None = None) -> None:
     """Rows that may change cluster -> idx[:m] (their cluster -> a_prev, and -> acl[:m] in
-    list order when given; u of the kept rows becomes u + delta[a]), m -> n_active
-    (device; no sync). The largest centre shift is reduced from delta in the kernel."""
+    list order when given), m -> n_active (device; no sync). The largest centre shift is
+    reduced from delta in the kernel."""
     n_active.zero_()
     _ext.ops().kmeans_filter(assign, u, l, delta, s, a_prev, idx, n_active, acl)
 
@@ -301,9 +301,10 @@ def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
     and appends the rows whose cluster differs from a_prev to changed (count in
     n_changed, which the caller zeroes): no host sync, no separate bound pass.
     ``cand`` (with post; idx = cand.rows, the active rows sorted by cluster): the
-    candidate-pruned form -- a tile of cluster a only streams the centres within
-    2 max(u) + slack of c_a (a prefix of a's neighbour list), and the pruned centres
-    enter the new lower bound as nd_first - u."""
+    candidate-pruned form -- a tile of cluster a streams only the chunks of a's
+    neighbour list within 2 max(ua) of c_a (ua = the tile's distances to c_a, computed in
+    the tile prologue and rounded up); the pruned centres enter the new lower bound as
+    nd_first - ua."""
     if post is None:
         _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, [], mind, mind2, xh,
                                      xmax)

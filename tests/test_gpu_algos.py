@@ -726,9 +726,7 @@ def test_kmeans_filter_matches_torch(cuda):
     assert torch.equal(torch.sort(idx[:m]).values.long(), torch.nonzero(act)[:, 0])
     assert bool((u[~act] >= ub[~act]).all()) and torch.allclose(u[~act], ub[~act])
     assert bool((l[~act] <= lb[~act]).all()) and torch.allclose(l[~act], lb[~act])
-    # kept rows: u becomes the shifted bound (the candidate-pruned K2 reads it), l unchanged
-    assert bool((u[act] >= ub[act]).all()) and torch.allclose(u[act], ub[act])
-    assert torch.equal(l[act], l0[act])
+    assert torch.equal(u[act], u0[act]) and torch.equal(l[act], l0[act])
     assert torch.equal(a_prev[act], assign[act])
 
 
