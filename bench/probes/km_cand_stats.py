@@ -18,15 +18,36 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=20_000_000)
 ap.add_argument("--k", type=int, default=1024)
 ap.add_argument("--iters", type=int, default=5)
+ap.add_argument("--no-candidates", action="store_true")
 a = ap.parse_args()
 dev = torch.device("cuda")
 X = blobs(a.rows, 128, a.k, device=dev, dtype=torch.bfloat16, seed=7)
-km = KMeans(KMeansConfig(k=a.k, n_iterations=a.iters, seed=42), X, 0, a.rows)
+km = KMeans(KMeansConfig(k=a.k, n_iterations=a.iters, seed=42, candidates=not a.no_candidates),
+            X, 0, a.rows)
 orig = K.assign_rows
 stats = []
 
 
+def lower_bound_quality(X_, cen, idx, post):
+    """l written by K2 over the active rows vs the exact second-best distance."""
+    n_act = int(post["m_dev"].item())
+    r = idx[:n_act].long()
+    k = cen.k
+    ratios = []
+    for s0 in range(0, n_act, 1 << 18):
+        rr = r[s0:s0 + (1 << 18)]
+        D = torch.cdist(X_[rr, :128].float(), cen.Cq[:k, :128].float())
+        two = torch.topk(D, 2, dim=1, largest=False).values
+        ratios.append(post["l"][rr] / two[:, 1].clamp_min(1e-6))
+    q = torch.cat(ratios)
+    return dict(l_over_second_best_mean=float(q.mean()), l_lt_90pct=float((q < 0.9).float().mean()))
+
+
 def probe(X_, cen, idx, m, assign, *args, post=None, cand=None, **kw):
+    if post is not None and cand is None:
+        out = orig(X_, cen, idx, m, assign, *args, post=post, cand=cand, **kw)
+        stats.append(dict(active=int(post["m_dev"].item()), **lower_bound_quality(X_, cen, idx, post)))
+        return out
     if cand is not None:
         torch.cuda.synchronize()
         n_act = int(post["m_dev"].item())
@@ -60,7 +81,10 @@ def probe(X_, cen, idx, m, assign, *args, post=None, cand=None, **kw):
                           nchunks_p10_50_90_99=[float(v) for v in qs],
                           R_median=float(R.median()), u_median=float(u.median()),
                           tile_fill=n_act / (T * K.CAND_TILE)))
-    return orig(X_, cen, idx, m, assign, *args, post=post, cand=cand, **kw)
+    out = orig(X_, cen, idx, m, assign, *args, post=post, cand=cand, **kw)
+    if cand is not None:
+        stats[-1].update(lower_bound_quality(X_, cen, idx, post))
+    return out
 
 
 K.assign_rows = probe

@@ -441,18 +441,27 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       bf[t][s] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
     }
   }
+  uint4 ca[CAND ? KS : 1];
+  // CAND: everything the tile's set-up reads is loaded here, under the point loads (one
+  // memory latency per tile instead of a chain): c_acl, the first distance of every
+  // chunk of acl's list (lane j: nd[acl][j * CH]) and the list's 0.5|c|^2
+  constexpr int KH = CAND ? 2048 / NT : 1;
+  float thrv = __builtin_inff();
+  float hv[KH];
+  if constexpr (CAND) {
+    const uint16_t* src = Cq + (int64_t)acl * DP + h * 8;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) ca[s] = *reinterpret_cast<const uint4*>(src + 16 * s);
+    if (lane < nchunk) thrv = aux.nd[(int64_t)acl * kpad + lane * CH];
+#pragma unroll
+    for (int j = 0; j < KH; ++j) hv[j] = tid + j * NT < kpad ? hbase[tid + j * NT] : 0.f;
+  }
   // all ordinary loads retired before the DMA stream starts, and the fragments pinned
   // here, so the compiler's own waits never drain a chunk in flight (vmcnt(0) in-loop)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float mx = 0.f;
   // CAND: the lane's half of c_acl (same k layout as the point fragments), for the exact
   // distance of every tile point to its cluster's centre (v_dot2 on the bf16 pairs)
-  uint4 ca[CAND ? KS : 1];
-  if constexpr (CAND) {
-    const uint16_t* src = Cq + (int64_t)acl * DP + h * 8;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) ca[s] = *reinterpret_cast<const uint4*>(src + 16 * s);
-  }
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     float q = 0.f;
@@ -504,17 +513,17 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // ascending, so they are a prefix of the list: nch_t whole chunks of it. Every wave
   // finds the count by a two-level search of nd (all agree: no barrier)
   int nch_t = nchunk;
+  float nd_first = __builtin_inff();   // CAND: smallest distance of a pruned centre
   if constexpr (CAND) {
     float R = s_r[0];
 #pragma unroll
     for (int w = 1; w < NW; ++w) R = fmaxf(R, s_r[w]);
     R = km_up1(2.f * R);
-    const float* ndr = aux.nd + (int64_t)acl * kpad;
-    const int S = kpad / 64;                      // kpad % 128 == 0: S >= 2
-    const int cc = __popcll(__ballot(ndr[lane * S] <= R));   // >= 1 (nd[0] = 0)
-    const int j = (cc - 1) * S + lane;
-    const int nc = (cc - 1) * S + __popcll(__ballot(lane < S && j < kpad && ndr[j] <= R));
-    nch_t = max(1, (nc + CH - 1) / CH);
+    // chunk j >= 1 is needed iff its first (smallest) distance is <= R; chunk 0 always
+    nch_t = 1 + __popcll(__ballot(lane >= 1 && lane < nchunk && thrv <= R));
+    const float nf = __shfl(thrv, nch_t < 64 ? nch_t : 0);
+    if (nch_t < nchunk) nd_first = nf;
+    issue(0);                           // under the set-up below (buffer 0 free: barrier)
   }
   if constexpr (LOOP) {
     // every wave is past the previous tile's appends: room for this tile's (<= TILE)?
@@ -525,7 +534,13 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   for (int w = 1; w < NW; ++w) M = fmaxf(M, s_m[w]);
   // slack so that rounding of the MFMA sum cannot push a near-zero distance negative
   M = M * 1.0001f + 1e-6f;
-  for (int c = tid; c < nch_t * CH; c += NT) s_hn[c] = hbase[c] + M;
+  if constexpr (CAND) {
+#pragma unroll
+    for (int j = 0; j < KH; ++j)
+      if (tid + j * NT < nch_t * CH) s_hn[tid + j * NT] = hv[j] + M;
+  } else {
+    for (int c = tid; c < kpad; c += NT) s_hn[c] = hbase[c] + M;
+  }
 
   int bkey[PT], bsub[PT], bkey2[PT];
 #pragma unroll
@@ -584,7 +599,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     bsub[t] = take ? cb : bsub[t];
   };
 
-  issue(0);
+  if constexpr (!CAND) issue(0);
   if (NBUF >= 3 && nch_t > 1) issue(1);
   if (NBUF >= 4 && nch_t > 2) issue(2);
   for (int ch = 0; ch < nch_t; ++ch) {
@@ -653,10 +668,6 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     if (NBUF >= 3 && ch + NBUF - 1 < nch_t) issue(ch + NBUF - 1);
   }
   reduce_tile(pacc, T0, pcb);
-  // CAND: every centre past the processed prefix is >= nd_first - |x - c_acl| from x
-  float nd_first = __builtin_inff();
-  if constexpr (CAND)
-    if (nch_t * CH < kpad) nd_first = aux.nd[(int64_t)acl * kpad + nch_t * CH];
 
   // ---- decode, combine the two lane halves (same point, disjoint centre rows)
 #pragma unroll
@@ -692,6 +703,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
         const float dist2 = fmaxf(2.f * (bv2 - M) + x2[t], 0.f);
         aux.u[row] = km_up1(sqrtf(km_up1(dist + tol)));
         float lo2 = km_dn1(sqrtf(fmaxf(km_dn1(dist2 - tol), 0.f)));
+        // CAND: every pruned centre is >= nd_first - |x - c_acl| from x
         if constexpr (CAND) lo2 = fminf(lo2, km_dn1(nd_first - ua[t]));
         aux.l[row] = fmaxf(lo2, 0.f);
         chg = bi != aux.a_prev[row];
