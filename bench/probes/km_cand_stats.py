@@ -69,7 +69,7 @@ def probe(X_, cen, idx, m, assign, *args, post=None, cand=None, **kw):
             u[s0:s0 + (1 << 22)] = (xd.pow(2).sum(1) + tol).sqrt()
         umax = torch.zeros(T, device=dev).scatter_reduce(0, tid, u, "amax", include_self=True)
         R = 2 * umax
-        tcl = cand.tile_cl[:T].long()
+        tcl = cand.tiles.view(-1, 4)[:T, 0].long()
         nd = cand.nd.view(-1, kpad)[tcl]
         nc = torch.searchsorted(nd, R[:, None], right=True)[:, 0]
         nsub = (nc + 127) // 128

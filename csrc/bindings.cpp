@@ -614,31 +614,26 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
   } else {
     TORCH_CHECK(md != nullptr, "kmeans_assign_idx: mind");
   }
-  // candidate-pruned form: [tile_cl, tile_lo, cstart, n_tiles, cnb, hnb, nb, nd]
+  // candidate-pruned form: [tiles int32 [T, 4], n_tiles, hnb, nb, nd]
   DalgoKmCand cd{};
   const DalgoKmCand* cp = nullptr;
   if (!cand.empty()) {
-    TORCH_CHECK(cand.size() == 8 && pp != nullptr && ip != nullptr,
-                "kmeans_assign_idx: cand = 8 tensors, with the device-count form and idx");
+    TORCH_CHECK(cand.size() == 5 && pp != nullptr && ip != nullptr,
+                "kmeans_assign_idx: cand = 5 tensors, with the device-count form and idx");
     for (const Tensor& t : cand) check_dev(t, "cand");
-    const int64_t k = cand[2].numel() - 1;
     TORCH_CHECK(cand[0].scalar_type() == at::kInt && cand[1].scalar_type() == at::kLong &&
-                    cand[2].scalar_type() == at::kLong && cand[3].scalar_type() == at::kLong &&
-                    cand[4].scalar_type() == at::kBFloat16 && cand[5].scalar_type() == at::kFloat &&
-                    cand[6].scalar_type() == at::kInt && cand[7].scalar_type() == at::kFloat,
+                    cand[2].scalar_type() == at::kFloat && cand[3].scalar_type() == at::kInt &&
+                    cand[4].scalar_type() == at::kFloat,
                 "kmeans_assign_idx: cand dtypes");
-    TORCH_CHECK(k >= 1 && k <= kpad && cand[4].numel() >= k * kpad * DP && cand[5].numel() >= k * kpad &&
-                    cand[6].numel() >= k * kpad && cand[7].numel() >= k * kpad &&
-                    cand[0].numel() == cand[1].numel(),
-                "kmeans_assign_idx: cand sizes");
-    cd.tile_cl = cand[0].data_ptr<int32_t>();
-    cd.tile_lo = cand[1].data_ptr<int64_t>();
-    cd.cstart = cand[2].data_ptr<int64_t>();
-    cd.n_tiles = reinterpret_cast<const unsigned long long*>(cand[3].data_ptr<int64_t>());
-    cd.cnb = cand[4].data_ptr();
-    cd.hnb = cand[5].data_ptr<float>();
-    cd.nb = cand[6].data_ptr<int32_t>();
-    cd.nd = cand[7].data_ptr<float>();
+    const int64_t k = cand[2].numel() / kpad;
+    TORCH_CHECK(kpad <= 1024 && k >= 1 && k <= kpad && cand[3].numel() >= k * kpad &&
+                    cand[4].numel() >= k * kpad && cand[0].numel() % 4 == 0,
+                "kmeans_assign_idx: cand sizes (kpad <= 1024)");
+    cd.tiles = cand[0].data_ptr<int32_t>();
+    cd.n_tiles = reinterpret_cast<const unsigned long long*>(cand[1].data_ptr<int64_t>());
+    cd.hnb = cand[2].data_ptr<float>();
+    cd.nb = cand[3].data_ptr<int32_t>();
+    cd.nd = cand[4].data_ptr<float>();
     cp = &cd;
   }
   DeviceGuard guard(X.device());
@@ -652,14 +647,13 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
 // candidate-pruned K2 preparation: active rows sorted by cluster + tile table
 void kmeans_sort_active(const Tensor& acl, const Tensor& idx, const Tensor& n_active, int64_t k,
                         int64_t chunk, Tensor block_counts, Tensor cstart, Tensor seg_start,
-                        Tensor rows_sorted, int64_t tile, Tensor tile_cl, Tensor tile_lo,
-                        Tensor n_tiles) {
+                        Tensor rows_sorted, int64_t tile, Tensor tiles, Tensor n_tiles) {
   check_i32(acl, "acl");
   check_i32(idx, "idx");
   check_i32(rows_sorted, "rows_sorted");
   check_i32(block_counts, "block_counts");
-  check_i32(tile_cl, "tile_cl");
-  for (const Tensor* t : std::initializer_list<const Tensor*>{&n_active, &cstart, &seg_start, &tile_lo, &n_tiles}) {
+  check_i32(tiles, "tiles");
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&n_active, &cstart, &seg_start, &n_tiles}) {
     check_dev(*t, "sort_active");
     TORCH_CHECK(t->scalar_type() == at::kLong && t->is_contiguous(), "sort_active: int64 tensors");
   }
@@ -670,24 +664,23 @@ void kmeans_sort_active(const Tensor& acl, const Tensor& idx, const Tensor& n_ac
   const int64_t B = std::max<int64_t>(1, std::min<int64_t>((cap + chunk - 1) / chunk,
                                                            block_counts.numel() / k));
   TORCH_CHECK(B * chunk >= cap, "kmeans_sort_active: block_counts too small for cap / chunk");
-  TORCH_CHECK(tile_cl.numel() == tile_lo.numel() && tile_cl.numel() >= (cap + tile - 1) / tile + k,
-              "kmeans_sort_active: tile table [cap / tile + k]");
+  TORCH_CHECK(tiles.numel() % 4 == 0 && tiles.numel() / 4 >= (cap + tile - 1) / tile + k,
+              "kmeans_sort_active: tile table [cap / tile + k, 4]");
   DeviceGuard guard(idx.device());
   DALGO_CHECK_HIP(dalgo_kmeans_sort_active(
                       acl.data_ptr<int32_t>(), idx.data_ptr<int32_t>(), cap,
                       reinterpret_cast<const unsigned long long*>(n_active.data_ptr<int64_t>()), (int)k,
                       (int)B, chunk, block_counts.data_ptr<int>(), cstart.data_ptr<int64_t>(),
                       seg_start.data_ptr<int64_t>(), rows_sorted.data_ptr<int32_t>(), (int)tile,
-                      tile_cl.data_ptr<int32_t>(), tile_lo.data_ptr<int64_t>(),
+                      tiles.data_ptr<int32_t>(),
                       reinterpret_cast<unsigned long long*>(n_tiles.data_ptr<int64_t>()),
-                      tile_cl.numel(), cur_stream()),
+                      tiles.numel() / 4, cur_stream()),
                   "kmeans_sort_active");
 }
 
 // centre geometry of the candidate-pruned iteration: delta, s and the neighbour lists
 void kmeans_centre_nbrs(const Tensor& cq, const Tensor& cprev, const Tensor& hn, int64_t k,
-                        int64_t d, Tensor delta, Tensor s, Tensor nd, Tensor nb, Tensor hnb,
-                        Tensor cnb) {
+                        int64_t d, Tensor delta, Tensor s, Tensor nd, Tensor nb, Tensor hnb) {
   check_dev(cq, "cq");
   check_dev(cprev, "cprev");
   TORCH_CHECK(cq.dim() == 2 && cq.is_contiguous() && cq.scalar_type() == at::kBFloat16 &&
@@ -702,16 +695,14 @@ void kmeans_centre_nbrs(const Tensor& cq, const Tensor& cprev, const Tensor& hn,
   check_f32(nd, "nd");
   check_f32(hnb, "hnb");
   check_i32(nb, "nb");
-  check_dev(cnb, "cnb");
   TORCH_CHECK(hn.numel() >= kpad && delta.numel() >= k && s.numel() >= k && nd.numel() >= k * kpad &&
-                  nb.numel() >= k * kpad && hnb.numel() >= k * kpad &&
-                  cnb.scalar_type() == at::kBFloat16 && cnb.is_contiguous() && cnb.numel() >= k * kpad * DP,
+                  nb.numel() >= k * kpad && hnb.numel() >= k * kpad,
               "kmeans_centre_nbrs sizes");
   DeviceGuard guard(cq.device());
   DALGO_CHECK_HIP(dalgo_km_centre_nbrs(cq.data_ptr(), cprev.data_ptr(), hn.data_ptr<float>(), (int)k,
                                        (int)kpad, (int)d, (int)DP, delta.data_ptr<float>(),
                                        s.data_ptr<float>(), nd.data_ptr<float>(), nb.data_ptr<int32_t>(),
-                                       hnb.data_ptr<float>(), cnb.data_ptr(), cur_stream()),
+                                       hnb.data_ptr<float>(), cur_stream()),
                   "kmeans_centre_nbrs");
 }
 
@@ -1192,9 +1183,9 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(b!) a_prev, Tensor(c!) idx, Tensor(d!) n_active, Tensor(f!)? acl=None) -> ()");
   m.def("kmeans_sort_active(Tensor acl, Tensor idx, Tensor n_active, int k, int chunk, "
         "Tensor(a!) block_counts, Tensor(b!) cstart, Tensor(c!) seg_start, Tensor(d!) rows_sorted, "
-        "int tile, Tensor(e!) tile_cl, Tensor(f!) tile_lo, Tensor(g!) n_tiles) -> ()");
+        "int tile, Tensor(e!) tiles, Tensor(g!) n_tiles) -> ()");
   m.def("kmeans_centre_nbrs(Tensor cq, Tensor cprev, Tensor hn, int k, int d, Tensor(a!) delta, "
-        "Tensor(b!) s, Tensor(c!) nd, Tensor(d!) nb, Tensor(e!) hnb, Tensor(f!) cnb) -> ()");
+        "Tensor(b!) s, Tensor(c!) nd, Tensor(d!) nb, Tensor(e!) hnb) -> ()");
   m.def("kmeans_centre_bounds(Tensor cnow, Tensor cprev, int k, int d, Tensor(a!) delta, "
         "Tensor(b!) s) -> ()");
   m.def("kmeans_qsum(Tensor assign, Tensor xh, int k, Tensor(a!) Q) -> ()");

@@ -304,12 +304,9 @@ struct KmAux {
   long long cap;                      //       capacity of `changed`
   // CAND (candidate-pruned LOOP): the active rows sorted by cluster (idx), tiles that never
   // straddle two clusters, and each centre's neighbour lists (km_centre_nbrs_kernel)
-  const int32_t* tile_cl;             // cluster of tile t
-  const int64_t* tile_lo;             // its first position in idx
-  const int64_t* cstart;              // [k + 1]: cluster runs in idx
+  const int4* tiles;                  // tile t: (cluster, first, end position in idx, -)
   const unsigned long long* n_tiles;  // device tile count
-  const uint16_t* cnb;                // [k][kpad][DP]: centres in neighbour order of centre a
-  const float* hnb;                   // [k][kpad]: their 0.5|c|^2
+  const float* hnb;                   // [k][kpad]: 0.5|c|^2 in neighbour order of centre a
   const int32_t* nb;                  // [k][kpad]: their ids
   const float* nd;                    // [k][kpad]: |c - c_a| rounded down, ascending
 };
@@ -340,6 +337,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   constexpr int GPT = CHP / NT;                // LDS-DMA instructions per thread per chunk
   constexpr int TILE = NW * PT * 32;           // points per block tile
   static_assert(CHP % NT == 0, "chunk must be a whole number of block-wide DMA rounds");
+  static_assert((NT / NJ) % (SWZ + 1) == 0, "DMA swizzle must repeat every block-wide round");
   static_assert(NBUF >= 2 && NBUF <= 4, "double, triple or quadruple buffered chunks");
   __shared__ __attribute__((aligned(16))) uint4 s_c[NBUF * CHP];
   extern __shared__ __attribute__((aligned(16))) float s_hn[];   // [kpad]: 0.5|c|^2 + M
@@ -348,6 +346,10 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   __shared__ double s_sse[NW];
 
   __shared__ int s_chg[LOOP ? kChgBuf : 1];
+  // CAND: the tile cluster's neighbour list (ids, k <= 1024), double-buffered by tile parity
+  // so a tile can stage its list before the barrier that ends the previous tile's reads
+  __shared__ uint16_t s_nb[CAND ? 2 : 1][CAND ? 1024 : 1];
+  int par = 0;
   __shared__ int s_nchg;
   __shared__ unsigned long long s_chg_base;
 
@@ -387,16 +389,26 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // chunk being read and drains vmcnt(0) before every ds_read (the chunk in flight
   // would then never overlap compute). The counted waits below are the only waits.
   const uint32_t lds0 = (uint32_t)(uintptr_t)(km_lds_void*)s_c;
-  const uint16_t* cbase = Cq;   // CAND: the tile cluster's neighbour-ordered centres
   auto issue = [&](int ch) {
-    const uint16_t* base = cbase + (int64_t)ch * CH * DP;
+    const uint16_t* base = Cq + (int64_t)ch * CH * DP;
     const uint32_t dst = lds0 + (uint32_t)(((ch % NBUF) * CHP) * 16);
 #pragma unroll
     for (int g = 0; g < GPT; ++g) {
       const uint32_t m0v = __builtin_amdgcn_readfirstlane(dst + (uint32_t)((g * NT + wid * 64) * 16));
-      const uint16_t* src = base + src_off[g];
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-                   :: "s"(m0v), "v"(src) : "memory");
+      if constexpr (CAND) {
+        // gather: chunk row r of the tile's stream is centre s_nb[par][ch * CH + r] of Cq
+        // (L2-resident); src_off[g] = r * DP + piece offset. SGPR base + 32-bit offset
+        // (NT / NJ is a multiple of SWZ + 1: the swizzled piece is the same for every g)
+        const int rr = tid / NJ, r = g * (NT / NJ) + rr;
+        const uint32_t pz = (uint32_t)(((tid % NJ) ^ (rr & SWZ)) * 8);
+        const uint32_t off = ((uint32_t)s_nb[par][ch * CH + r] * DP + pz) * 2u;
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+                     :: "s"(m0v), "v"(off), "s"(Cq) : "memory");
+      } else {
+        const uint16_t* src = base + src_off[g];
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                     :: "s"(m0v), "v"(src) : "memory");
+      }
     }
   };
   int kmask;   // key mask in a VGPR so each pack is ONE v_and_or_b32 (VGPR mask, inline r)
@@ -415,12 +427,12 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   int64_t pbase, pend = n;
   const float* hbase = hn;
   if constexpr (CAND) {
-    acl = aux.tile_cl[bt];
-    const int64_t lo = aux.tile_lo[bt];
-    pend = min(aux.cstart[acl + 1], lo + TILE);
-    pbase = lo + (int64_t)wid * (PT * 32);
-    cbase = aux.cnb + (int64_t)acl * kpad * DP;
+    const int4 tr = aux.tiles[bt];
+    acl = tr.x;
+    pend = tr.z;
+    pbase = (int64_t)tr.y + (int64_t)wid * (PT * 32);
     hbase = aux.hnb + (int64_t)acl * kpad;
+    par ^= 1;
   } else {
     pbase = (bt * NW + wid) * (PT * 32);
   }
@@ -445,16 +457,21 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // CAND: everything the tile's set-up reads is loaded here, under the point loads (one
   // memory latency per tile instead of a chain): c_acl, the first distance of every
   // chunk of acl's list (lane j: nd[acl][j * CH]) and the list's 0.5|c|^2
-  constexpr int KH = CAND ? 2048 / NT : 1;
+  constexpr int KH = CAND ? 1024 / NT : 1;
   float thrv = __builtin_inff();
   float hv[KH];
+  int nbv[KH];
   if constexpr (CAND) {
     const uint16_t* src = Cq + (int64_t)acl * DP + h * 8;
 #pragma unroll
     for (int s = 0; s < KS; ++s) ca[s] = *reinterpret_cast<const uint4*>(src + 16 * s);
     if (lane < nchunk) thrv = aux.nd[(int64_t)acl * kpad + lane * CH];
 #pragma unroll
-    for (int j = 0; j < KH; ++j) hv[j] = tid + j * NT < kpad ? hbase[tid + j * NT] : 0.f;
+    for (int j = 0; j < KH; ++j) {
+      const bool in = tid + j * NT < kpad;
+      hv[j] = in ? hbase[tid + j * NT] : 0.f;
+      nbv[j] = in ? aux.nb[(int64_t)acl * kpad + tid + j * NT] : 0;
+    }
   }
   // all ordinary loads retired before the DMA stream starts, and the fragments pinned
   // here, so the compiler's own waits never drain a chunk in flight (vmcnt(0) in-loop)
@@ -506,6 +523,11 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     for (int off = 32; off >= 1; off >>= 1) um = fmaxf(um, __shfl_xor(um, off));
   }
   if (lane == 0) { s_m[wid] = mx; if constexpr (CAND) s_r[wid] = um; }
+  if constexpr (CAND) {
+#pragma unroll
+    for (int j = 0; j < KH; ++j)
+      if (tid + j * NT < kpad) s_nb[par][tid + j * NT] = (uint16_t)nbv[j];
+  }
   __syncthreads();
   // CAND: the tile's centre stream is cluster acl's neighbour list. ua >= |x - c_acl| for
   // every tile point, so only centres c with |c - c_acl| <= R = 2 max ua can be the
@@ -675,7 +697,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     const int r = bkey[t] & 31;
     const float v = __int_as_float(bkey[t] & ~31);
     int mi = bsub[t] + (r & 3) + 8 * (r >> 2) + 4 * h;
-    if constexpr (CAND) mi = aux.nb[(int64_t)acl * kpad + mi];   // list position -> id
+    if constexpr (CAND) mi = s_nb[par][mi];   // list position -> id
     auto sv = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     auto si = __builtin_amdgcn_permlane32_swap((uint32_t)mi, (uint32_t)mi, false, false);
     const float pv = __uint_as_float(h ? sv[0] : sv[1]);
@@ -706,7 +728,8 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
         // CAND: every pruned centre is >= nd_first - |x - c_acl| from x
         if constexpr (CAND) lo2 = fminf(lo2, km_dn1(nd_first - ua[t]));
         aux.l[row] = fmaxf(lo2, 0.f);
-        chg = bi != aux.a_prev[row];
+        // CAND: the tile's rows were sorted by their previous cluster, acl
+        chg = bi != (CAND ? acl : aux.a_prev[row]);
       } else {
         if (mind) mind[row] = dist;
         if constexpr (TOP2) mind2[row] = fmaxf(2.f * (bv2 - M) + x2[t], 0.f);
@@ -1066,9 +1089,8 @@ km_dexpand_kernel(const int32_t* __restrict__ changed, int64_t m, const int32_t*
 // rows is cut into ceil(run / tile) tiles; tile t -> (cluster, first position). One block
 // (k <= 2048): per-thread clusters, block exclusive scan of their tile counts.
 __global__ void __launch_bounds__(1024)
-km_tiles_kernel(const int64_t* __restrict__ cs, int k, int tile, int32_t* __restrict__ tile_cl,
-                int64_t* __restrict__ tile_lo, unsigned long long* __restrict__ n_tiles,
-                int64_t max_tiles) {
+km_tiles_kernel(const int64_t* __restrict__ cs, int k, int tile, int4* __restrict__ tiles,
+                unsigned long long* __restrict__ n_tiles, int64_t max_tiles) {
   __shared__ int64_t s_part[1024 / 64];
   const int per = (k + blockDim.x - 1) / blockDim.x;
   const int c0 = threadIdx.x * per, c1 = min(k, c0 + per);
@@ -1086,10 +1108,8 @@ km_tiles_kernel(const int64_t* __restrict__ cs, int k, int tile, int32_t* __rest
   for (int w = 0; w < wid; ++w) t0 += s_part[w];
   for (int c = c0; c < c1; ++c) {
     for (int64_t lo = cs[c]; lo < cs[c + 1]; lo += tile, ++t0) {
-      if (t0 < max_tiles) {
-        tile_cl[t0] = c;
-        tile_lo[t0] = lo;
-      }
+      if (t0 < max_tiles)
+        tiles[t0] = make_int4(c, (int)lo, (int)min(cs[c + 1], lo + tile), 0);
     }
   }
   if (c1 == k && c0 < k) *n_tiles = (unsigned long long)min(t0, max_tiles);
@@ -1226,8 +1246,7 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
   if (LOOP && (aux.tol == nullptr || aux.u == nullptr || aux.l == nullptr || aux.a_prev == nullptr ||
                aux.changed == nullptr || aux.n_changed == nullptr))
     return hipErrorInvalidValue;
-  if (CAND && (aux.tile_cl == nullptr || aux.tile_lo == nullptr || aux.cstart == nullptr ||
-               aux.n_tiles == nullptr || aux.cnb == nullptr || aux.hnb == nullptr ||
+  if (CAND && (kpad > 1024 || aux.tiles == nullptr || aux.n_tiles == nullptr || aux.hnb == nullptr ||
                aux.nb == nullptr || aux.nd == nullptr || idx == nullptr))
     return hipErrorInvalidValue;
   // CAND: up to n / TILE + k tiles (device count) -> always the resident grid
@@ -1431,8 +1450,8 @@ hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP
     aux.cap = post->cap;
     if (cand != nullptr) {
       // idx = the active rows sorted by cluster (dalgo_kmeans_sort_active)
-      aux.tile_cl = cand->tile_cl; aux.tile_lo = cand->tile_lo; aux.cstart = cand->cstart;
-      aux.n_tiles = cand->n_tiles; aux.cnb = (const uint16_t*)cand->cnb; aux.hnb = cand->hnb;
+      aux.tiles = reinterpret_cast<const int4*>(cand->tiles);
+      aux.n_tiles = cand->n_tiles; aux.hnb = cand->hnb;
       aux.nb = cand->nb; aux.nd = cand->nd;
       if (DP == 128)
         return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true, true, true>(
@@ -1492,8 +1511,8 @@ hipError_t dalgo_kmeans_update(float* C, const float* S, const unsigned long lon
 hipError_t dalgo_kmeans_sort_active(const int32_t* acl, const int32_t* idx, int64_t cap,
                                     const unsigned long long* n_active, int k, int B, int64_t chunk,
                                     int* block_counts, int64_t* cstart, int64_t* seg_start,
-                                    int32_t* rows_sorted, int tile, int32_t* tile_cl,
-                                    int64_t* tile_lo, unsigned long long* n_tiles,
+                                    int32_t* rows_sorted, int tile, int32_t* tiles,
+                                    unsigned long long* n_tiles,
                                     int64_t max_tiles, hipStream_t st) {
   if (cap <= 0) return hipSuccess;
   if (k < 1 || k > kScKmax || B < 1 || chunk < 1 || tile < 1 || cap >= (int64_t)0x7fffffff ||
@@ -1512,7 +1531,7 @@ hipError_t dalgo_kmeans_sort_active(const int32_t* acl, const int32_t* idx, int6
                      n_active, 1, chunk, (const int*)idx);
   DALGO_LAUNCH_CHECK();
   hipLaunchKernelGGL(km_tiles_kernel, dim3(1), dim3(1024), 0, st, (const int64_t*)cstart, k, tile,
-                     tile_cl, tile_lo, n_tiles, max_tiles);
+                     reinterpret_cast<int4*>(tiles), n_tiles, max_tiles);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -258,14 +258,13 @@ km_centre_bounds_kernel(const T* __restrict__ cnow, const T* __restrict__ cprev,
 // rounded down (relative 1e-6 margin, f32 round-down; +inf for the padding centres),
 // nb[a][.] = the same centres with each aligned group of 32 re-ordered by id (a group of
 // the list is one 32-centre sub-tile of K2, so any processed prefix of whole sub-tiles is
-// the same set as the distance order's), hnb / cnb = their 0.5|c|^2 and rows (the K2
-// chunk stream of a tile of cluster a is then contiguous). Also delta[a] and s[a] as
+// the same set as the distance order's), hnb = their 0.5|c|^2. Also delta[a] and s[a] as
 // km_centre_bounds_kernel (one launch per iteration instead of two).
 __global__ void __launch_bounds__(256)
 km_centre_nbrs_kernel(const uint16_t* __restrict__ cq, const uint16_t* __restrict__ cprev,
                       const float* __restrict__ hn, int k, int kpad, int d, int DP,
                       float* __restrict__ delta, float* __restrict__ sout, float* __restrict__ nd,
-                      int32_t* __restrict__ nb, float* __restrict__ hnb, uint16_t* __restrict__ cnb) {
+                      int32_t* __restrict__ nb, float* __restrict__ hnb) {
   __shared__ double s_c[128];
   __shared__ float s_d[2048];
   __shared__ int32_t s_i[2048];
@@ -340,12 +339,6 @@ km_centre_nbrs_kernel(const uint16_t* __restrict__ cq, const uint16_t* __restric
     nb[base + j] = s_g[j];
     hnb[base + j] = hn[s_g[j]];
   }
-  const int pieces = DP / 8;                     // 16-B pieces per bf16 row
-  for (int q = tid; q < kpad * pieces; q += 256) {
-    const int j = q / pieces, pc = q - j * pieces;
-    const uint4 v = *reinterpret_cast<const uint4*>(cq + (int64_t)s_g[j] * DP + pc * 8);
-    *reinterpret_cast<uint4*>(cnb + (base + j) * DP + pc * 8) = v;
-  }
 }
 
 // Bounds after the full first pass: tol = 2 M 2^-14 with M = max 0.5|x|^2 * 1.0001 + 1e-6
@@ -416,13 +409,13 @@ hipError_t dalgo_km_centre_bounds(const void* cnow, const void* cprev, int is_bf
 
 hipError_t dalgo_km_centre_nbrs(const void* cq, const void* cprev, const float* hn, int k, int kpad,
                                 int d, int DP, float* delta, float* s, float* nd, int32_t* nb,
-                                float* hnb, void* cnb, hipStream_t st) {
+                                float* hnb, hipStream_t st) {
   if (k <= 0) return hipSuccess;
   if (d > 128 || d > DP || kpad > 2048 || kpad < k || kpad % 32 != 0 || DP % 8 != 0)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(dalgo::km_centre_nbrs_kernel, dim3(k), dim3(256), 0, st,
                      (const uint16_t*)cq, (const uint16_t*)cprev, hn, k, kpad, d, DP, delta, s, nd,
-                     nb, hnb, (uint16_t*)cnb);
+                     nb, hnb);
   return hipGetLastError();
 }
 

@@ -40,11 +40,8 @@ struct DalgoKmPost {
 
 // candidate-pruned K2 (dalgo_kmeans_sort_active + dalgo_km_centre_nbrs outputs)
 struct DalgoKmCand {
-  const int32_t* tile_cl;
-  const int64_t* tile_lo;
-  const int64_t* cstart;
+  const int32_t* tiles;               // [T][4]: cluster, first, end position, -
   const unsigned long long* n_tiles;
-  const void* cnb;                    // bf16 [k][kpad][DP]
   const float* hnb;
   const int32_t* nb;
   const float* nd;
@@ -148,12 +145,12 @@ hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP
 hipError_t dalgo_kmeans_sort_active(const int32_t* acl, const int32_t* idx, int64_t cap,
                                     const unsigned long long* n_active, int k, int B, int64_t chunk,
                                     int* block_counts, int64_t* cstart, int64_t* seg_start,
-                                    int32_t* rows_sorted, int tile, int32_t* tile_cl,
-                                    int64_t* tile_lo, unsigned long long* n_tiles,
+                                    int32_t* rows_sorted, int tile, int32_t* tiles,
+                                    unsigned long long* n_tiles,
                                     int64_t max_tiles, hipStream_t st);
 hipError_t dalgo_km_centre_nbrs(const void* cq, const void* cprev, const float* hn, int k, int kpad,
                                 int d, int DP, float* delta, float* s, float* nd, int32_t* nb,
-                                float* hnb, void* cnb, hipStream_t st);
+                                float* hnb, hipStream_t st);
 hipError_t dalgo_km_bounds_init(const float* mind, const float* mind2, const unsigned* xmax,
                                 int64_t n, float* u, float* l, float* tol, hipStream_t st);
 

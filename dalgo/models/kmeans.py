@@ -45,7 +45,7 @@ class KMeansConfig:
     tol: float | None = None   # convergeDist-style early stop (reference ignores it)
     bound_filter: bool = True  # GPU bf16: Hamerly-filtered iterations after the first (exact)
     candidates: bool = True    # ... whose K2 tiles (one cluster each) stream only the centres
-                               # near their cluster's centre (exact; k <= 2048)
+                               # near their cluster's centre (exact; k <= 1024)
 
 
 @dataclass
@@ -136,7 +136,7 @@ class KMeans:
         # candidate pruning (Exponion-style at tile granularity): the active rows sorted by
         # cluster, every tile's centre stream cut to a prefix of its centre's neighbour list
         self._cand = (K.CandWorkspace(self.dev, n, k, self.cen.Cq.shape[0], self.DP)
-                      if self.cfg.candidates and self.cen.Cq.shape[0] <= 2048 else None)
+                      if self.cfg.candidates and self.cen.Cq.shape[0] <= 1024 else None)
 
     def _ph(self, name: str):
         return self.timer.phase(name) if self.timer is not None else NULL_PHASE

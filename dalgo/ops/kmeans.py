@@ -239,9 +239,8 @@ CAND_TILE = 256          # rows per K2 block tile (4 waves x 2 point tiles x 32)
 
 class CandWorkspace:
     """Buffers of the candidate-pruned filtered iteration for n rows, k clusters (kpad
-    padded) and DP columns: per-centre neighbour lists (nd / nb / hnb and the
-    neighbour-ordered centre rows cnb, k * kpad * DP bf16: 256 MB at k = 1024, DP = 128),
-    the cluster-sorted active rows and the tile table."""
+    padded, <= 1024): per-centre neighbour lists (nd / nb / hnb, k * kpad each), the
+    cluster-sorted active rows and the tile table."""
 
     def __init__(self, device, n: int, k: int, kpad: int, DP: int):
         i32 = dict(dtype=torch.int32, device=device)
@@ -252,7 +251,6 @@ class CandWorkspace:
         self.nd = torch.empty(k * kpad, **f32)
         self.nb = torch.empty(k * kpad, **i32)
         self.hnb = torch.empty(k * kpad, **f32)
-        self.cnb = torch.empty(k * kpad * DP, dtype=torch.bfloat16, device=device)
         self.acl = torch.empty(n, **i32)
         self.rows = torch.empty(n, **i32)
         bmax = max(1, (n + CHUNK_ROWS - 1) // CHUNK_ROWS)
@@ -260,13 +258,11 @@ class CandWorkspace:
         self.cstart = torch.empty(k + 1, **i64)
         self.seg_start = torch.empty(k + 1, **i64)
         tiles = (n + CAND_TILE - 1) // CAND_TILE + k
-        self.tile_cl = torch.empty(tiles, **i32)
-        self.tile_lo = torch.empty(tiles, **i64)
+        self.tiles = torch.empty(tiles * 4, **i32)      # (cluster, first, end, -) per tile
         self.n_tiles = torch.zeros(1, **i64)
 
     def cand(self):
-        return [self.tile_cl, self.tile_lo, self.cstart, self.n_tiles, self.cnb, self.hnb,
-                self.nb, self.nd]
+        return [self.tiles, self.n_tiles, self.hnb, self.nb, self.nd]
 
 
 def centre_nbrs(cen: Centers, Cq_prev: torch.Tensor, delta: torch.Tensor, s: torch.Tensor,
@@ -274,16 +270,16 @@ def centre_nbrs(cen: Centers, Cq_prev: torch.Tensor, delta: torch.Tensor, s: tor
     """delta / s as centre_bounds, plus every centre's neighbour lists for the pruned K2
     (one launch, kmeans_inc.hip km_centre_nbrs_kernel)."""
     _ext.ops().kmeans_centre_nbrs(cen.Cq, Cq_prev, cen.hn, ws.k, cen.d, delta, s, ws.nd, ws.nb,
-                                  ws.hnb, ws.cnb)
+                                  ws.hnb)
 
 
 def sort_active(idx: torch.Tensor, n_active: torch.Tensor, ws: CandWorkspace):
     """The active rows idx[:*n_active] (clusters in ws.acl) sorted by cluster -> ws.rows,
-    cluster runs -> ws.cstart, tiles of CAND_TILE rows of one cluster -> ws.tile_cl /
-    tile_lo / n_tiles (4 launches, device counts only)."""
+    cluster runs -> ws.cstart, tiles of CAND_TILE rows of one cluster -> ws.tiles /
+    n_tiles (4 launches, device counts only)."""
     _ext.ops().kmeans_sort_active(ws.acl, idx, n_active, ws.k, CHUNK_ROWS, ws.block_counts,
-                                  ws.cstart, ws.seg_start, ws.rows, CAND_TILE, ws.tile_cl,
-                                  ws.tile_lo, ws.n_tiles)
+                                  ws.cstart, ws.seg_start, ws.rows, CAND_TILE, ws.tiles,
+                                  ws.n_tiles)
 
 
 def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,

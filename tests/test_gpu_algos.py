@@ -858,7 +858,7 @@ def test_kmeans_bound_filter_exact(cuda):
 @pytest.mark.parametrize("k,d", [(1, 8), (37, 30), (1024, 128)])
 def test_kmeans_centre_nbrs_kernel(cuda, k, d):
     """Neighbour lists of the candidate-pruned K2: nd ascending lower bounds of the centre
-    distances, nb = the same order with each aligned 32-group re-ordered by id, hnb / cnb
+    distances, nb = the same order with each aligned 32-group re-ordered by id, hnb
     gathered through nb; delta / s equal the plain centre-bounds kernel's."""
     torch.manual_seed(k + d)
     cen = K.make_centers(torch.randn(k, d) * 3, torch.bfloat16, cuda)
@@ -891,7 +891,6 @@ def test_kmeans_centre_nbrs_kernel(cuda, k, d):
         ref = torch.cat([sd, torch.full((k, kpad - k), float("inf"), device=cuda, dtype=torch.float64)], 1)[:, g:g + 32]
         assert torch.allclose(hi, ref, rtol=1e-5, atol=1e-5)
     assert torch.equal(ws.hnb.view(k, kpad), cen.hn[nb])
-    assert torch.equal(ws.cnb.view(k, kpad, DP), cen.Cq[nb])
 
 
 def test_kmeans_sort_active(cuda):
@@ -916,9 +915,12 @@ def test_kmeans_sort_active(cuda):
     T = int(ws.n_tiles.item())
     ref = sum((int(cs[c + 1] - cs[c]) + K.CAND_TILE - 1) // K.CAND_TILE for c in range(k))
     assert T == ref
-    tc, tl = ws.tile_cl[:T].long(), ws.tile_lo[:T]
+    tr = ws.tiles.view(-1, 4)[:T].long()
+    tc, tl, th = tr[:, 0], tr[:, 1], tr[:, 2]
     assert bool((tl >= cs[tc]).all()) and bool((tl < cs[tc + 1]).all())
     assert bool(((tl - cs[tc]) % K.CAND_TILE == 0).all())
+    assert torch.equal(th, torch.minimum(cs[tc + 1], tl + K.CAND_TILE))
+    assert int((th - tl).sum()) == m
 
 
 def test_kmeans_assign_rows_candidates(cuda):
