@@ -343,6 +343,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   extern __shared__ __attribute__((aligned(16))) float s_hn[];   // [kpad]: 0.5|c|^2 + M
   __shared__ float s_m[NW];
   __shared__ float s_r[NW];
+  __shared__ int s_ext[NW];
   __shared__ double s_sse[NW];
 
   __shared__ int s_chg[LOOP ? kChgBuf : 1];
@@ -543,8 +544,6 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     R = km_up1(2.f * R);
     // chunk j >= 1 is needed iff its first (smallest) distance is <= R; chunk 0 always
     nch_t = 1 + __popcll(__ballot(lane >= 1 && lane < nchunk && thrv <= R));
-    const float nf = __shfl(thrv, nch_t < 64 ? nch_t : 0);
-    if (nch_t < nchunk) nd_first = nf;
     issue(0);                           // under the set-up below (buffer 0 free: barrier)
   }
   if constexpr (LOOP) {
@@ -688,8 +687,43 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       }
     }
     if (NBUF >= 3 && ch + NBUF - 1 < nch_t) issue(ch + NBUF - 1);
+    if constexpr (CAND) {
+      if (ch == nch_t - 1 && nch_t < nchunk) {
+        // The pruned centres bound l from below by nd_first - ua only. Where that is below
+        // a point's second-best distance so far, its l (and the next iteration's filter)
+        // would be loose: then the tile streams one more chunk (block-uniform decision)
+        reduce_tile(pacc, T0, pcb);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pacc[r] = __int_as_float(0x7fffffff);
+        const float nf = __shfl(thrv, nch_t);
+        bool need = false;
+#pragma unroll
+        for (int t = 0; t < PT; ++t) {
+          const float v = __int_as_float(bkey[t] & ~31), v2 = __int_as_float(bkey2[t] & ~31);
+          auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+          auto s2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v2), __float_as_uint(v2), false, false);
+          const float pv = __uint_as_float(h ? s1[0] : s1[1]);
+          const float pv2 = __uint_as_float(h ? s2[0] : s2[1]);
+          const float sec = fminf(fmaxf(v, pv), fminf(v2, pv2));
+          const float d2 = 2.f * (sec - M) + x2[t];
+          const float lp = nf - ua[t];
+          need |= pbase + t * 32 + cl < pend && (lp < 0.f || lp * lp < d2);
+        }
+        if (lane == 0) s_ext[wid] = __ballot(need) != 0ull;
+        __syncthreads();
+        int ext = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) ext |= s_ext[w];
+        if (ext) {
+          ++nch_t;
+          if (NBUF == 2) issue(ch + 1);   // buffer (ch + 1) % 2: chunk ch - 1 retired
+        }
+      }
+    }
   }
   reduce_tile(pacc, T0, pcb);
+  if constexpr (CAND)
+    if (nch_t < nchunk) nd_first = __shfl(thrv, nch_t);
 
   // ---- decode, combine the two lane halves (same point, disjoint centre rows)
 #pragma unroll
@@ -1092,6 +1126,7 @@ __global__ void __launch_bounds__(1024)
 km_tiles_kernel(const int64_t* __restrict__ cs, int k, int tile, int4* __restrict__ tiles,
                 unsigned long long* __restrict__ n_tiles, int64_t max_tiles) {
   __shared__ int64_t s_part[1024 / 64];
+  __shared__ int s_toff[2049];                     // first tile of cluster c (k <= 2048)
   const int per = (k + blockDim.x - 1) / blockDim.x;
   const int c0 = threadIdx.x * per, c1 = min(k, c0 + per);
   int64_t a = 0;
@@ -1107,12 +1142,25 @@ km_tiles_kernel(const int64_t* __restrict__ cs, int k, int tile, int4* __restric
   int64_t t0 = ia - a;
   for (int w = 0; w < wid; ++w) t0 += s_part[w];
   for (int c = c0; c < c1; ++c) {
-    for (int64_t lo = cs[c]; lo < cs[c + 1]; lo += tile, ++t0) {
-      if (t0 < max_tiles)
-        tiles[t0] = make_int4(c, (int)lo, (int)min(cs[c + 1], lo + tile), 0);
-    }
+    s_toff[c] = (int)t0;
+    t0 += (cs[c + 1] - cs[c] + tile - 1) / tile;
   }
-  if (c1 == k && c0 < k) *n_tiles = (unsigned long long)min(t0, max_tiles);
+  if (c1 == k && c0 < k) {
+    s_toff[k] = (int)t0;
+    *n_tiles = (unsigned long long)min(t0, max_tiles);
+  }
+  __syncthreads();
+  // tile t (consecutive threads, coalesced records): its cluster by binary search in LDS
+  const int total = (int)min((int64_t)s_toff[k], max_tiles);
+  for (int t = threadIdx.x; t < total; t += blockDim.x) {
+    int lo = 0, hi = k - 1;                        // last c with s_toff[c] <= t
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_toff[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    const int64_t first = cs[lo] + (int64_t)(t - s_toff[lo]) * tile;
+    tiles[t] = make_int4(lo, (int)first, (int)min(cs[lo + 1], first + tile), 0);
+  }
 }
 
 template <typename T, int DP, int NW>
