@@ -558,7 +558,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   if constexpr (CAND) {
 #pragma unroll
     for (int j = 0; j < KH; ++j)
-      if (tid + j * NT < nch_t * CH) s_hn[tid + j * NT] = hv[j] + M;
+      if (tid + j * NT < kpad) s_hn[tid + j * NT] = hv[j] + M;   // extensions read past nch_t
   } else {
     for (int c = tid; c < kpad; c += NT) s_hn[c] = hbase[c] + M;
   }
