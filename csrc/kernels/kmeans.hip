@@ -642,7 +642,9 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     // double: chunk ch+1 right away)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (NBUF == 2 && ch + 1 < nch_t) issue(ch + 1);
+    // CAND: the next chunk is prefetched even past the planned prefix (a tile may extend;
+    // an unused prefetch only costs L2 reads, and drains before the next tile's DMA)
+    if (NBUF == 2 && ch + 1 < (CAND ? nchunk : nch_t)) issue(ch + 1);
     const uint4* img = s_c + (ch % NBUF) * CHP;
     uint4 a[KS];
     f32x16 hc;
@@ -714,10 +716,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
         int ext = 0;
 #pragma unroll
         for (int w = 0; w < NW; ++w) ext |= s_ext[w];
-        if (ext) {
-          ++nch_t;
-          if (NBUF == 2) issue(ch + 1);   // buffer (ch + 1) % 2: chunk ch - 1 retired
-        }
+        if (ext) ++nch_t;                 // its chunk is already in flight
       }
     }
   }
@@ -1125,12 +1124,17 @@ km_dexpand_kernel(const int32_t* __restrict__ changed, int64_t m, const int32_t*
 __global__ void __launch_bounds__(1024)
 km_tiles_kernel(const int64_t* __restrict__ cs, int k, int tile, int4* __restrict__ tiles,
                 unsigned long long* __restrict__ n_tiles, int64_t max_tiles) {
+  // every block scans the (k <= 2048) tile counts itself, then writes its share of the
+  // records: tile t's cluster by binary search in LDS (coalesced record stores)
   __shared__ int64_t s_part[1024 / 64];
-  __shared__ int s_toff[2049];                     // first tile of cluster c (k <= 2048)
+  __shared__ int s_toff[2049];                     // first tile of cluster c
+  __shared__ int s_cs[2049];                       // cluster runs (positions < 2^31)
   const int per = (k + blockDim.x - 1) / blockDim.x;
   const int c0 = threadIdx.x * per, c1 = min(k, c0 + per);
+  for (int c = threadIdx.x; c <= k; c += blockDim.x) s_cs[c] = (int)cs[c];
+  __syncthreads();
   int64_t a = 0;
-  for (int c = c0; c < c1; ++c) a += (cs[c + 1] - cs[c] + tile - 1) / tile;
+  for (int c = c0; c < c1; ++c) a += (s_cs[c + 1] - s_cs[c] + tile - 1) / tile;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int64_t ia = a;
   for (int off = 1; off < 64; off <<= 1) {
@@ -1143,23 +1147,22 @@ km_tiles_kernel(const int64_t* __restrict__ cs, int k, int tile, int4* __restric
   for (int w = 0; w < wid; ++w) t0 += s_part[w];
   for (int c = c0; c < c1; ++c) {
     s_toff[c] = (int)t0;
-    t0 += (cs[c + 1] - cs[c] + tile - 1) / tile;
+    t0 += (s_cs[c + 1] - s_cs[c] + tile - 1) / tile;
   }
   if (c1 == k && c0 < k) {
     s_toff[k] = (int)t0;
-    *n_tiles = (unsigned long long)min(t0, max_tiles);
+    if (blockIdx.x == 0) *n_tiles = (unsigned long long)min(t0, max_tiles);
   }
   __syncthreads();
-  // tile t (consecutive threads, coalesced records): its cluster by binary search in LDS
   const int total = (int)min((int64_t)s_toff[k], max_tiles);
-  for (int t = threadIdx.x; t < total; t += blockDim.x) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
     int lo = 0, hi = k - 1;                        // last c with s_toff[c] <= t
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
       if (s_toff[mid] <= t) lo = mid; else hi = mid - 1;
     }
-    const int64_t first = cs[lo] + (int64_t)(t - s_toff[lo]) * tile;
-    tiles[t] = make_int4(lo, (int)first, (int)min(cs[lo + 1], first + tile), 0);
+    const int first = s_cs[lo] + (t - s_toff[lo]) * tile;
+    tiles[t] = make_int4(lo, first, min(s_cs[lo + 1], first + tile), 0);
   }
 }
 
@@ -1578,7 +1581,7 @@ hipError_t dalgo_kmeans_sort_active(const int32_t* acl, const int32_t* idx, int6
                      rpc, k, (const int*)block_counts, (const int64_t*)cstart, (int*)rows_sorted,
                      n_active, 1, chunk, (const int*)idx);
   DALGO_LAUNCH_CHECK();
-  hipLaunchKernelGGL(km_tiles_kernel, dim3(1), dim3(1024), 0, st, (const int64_t*)cstart, k, tile,
+  hipLaunchKernelGGL(km_tiles_kernel, dim3(64), dim3(1024), 0, st, (const int64_t*)cstart, k, tile,
                      reinterpret_cast<int4*>(tiles), n_tiles, max_tiles);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;

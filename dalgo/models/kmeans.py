@@ -198,8 +198,13 @@ class KMeans:
         if self._first:
             self._xmax.zero_()
             with self._ph("assign"):
-                # full pass: also 0.5|x|^2 per row and its maximum (the distance slack)
-                K.assign_rows(self.X, self.cen, None, n, self.assign, self._mind, self._mind2,
+                # full pass: also 0.5|x|^2 per row and its maximum (the distance slack).
+                # With candidate pruning the plain (top-1) pass: its l = the best distance
+                # (a valid lower bound of the second best) costs the next filter little --
+                # the first centre shifts are large, so l - maxd rarely decides there -- and
+                # the pruned iterations rebuild tight bounds
+                K.assign_rows(self.X, self.cen, None, n, self.assign, self._mind,
+                              None if self._cand is not None else self._mind2,
                               xh=self._xh, xmax=self._xmax)
             with self._ph("accumulate"):
                 K.accumulate(self.X, self.assign, k, self.DP, self.S, self.cnt)
@@ -207,7 +212,8 @@ class KMeans:
                 self._cnt64.copy_(self.cnt)
                 K.cluster_sq_sums(self.assign, self._xh, k, self._Q)
             # u / l from the K2 distances, tol = 2 M 2^-14 from the K2 max of 0.5|x|^2
-            K.bounds_init(self._mind, self._mind2, self._xmax, n, self._u, self._l, self._tol)
+            K.bounds_init(self._mind, self._mind if self._cand is not None else self._mind2,
+                          self._xmax, n, self._u, self._l, self._tol)
             self._record(0, n)
             self._record(1, 0)
             self._first = False
