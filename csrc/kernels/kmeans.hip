@@ -420,6 +420,22 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   double my_sse = 0.0;
   float my_xmax = 0.f;
 
+  // CAND: the next tile's record and row ids are loaded during the current tile (after
+  // its chunk-0 DMA), so a tile starts with its point loads instead of a chain of three
+  int4 trn = make_int4(0, 0, 0, 0);
+  int idxn[CAND ? PT : 1];
+  auto prefetch_tile = [&](int64_t bt) {
+    if constexpr (CAND) {
+      trn = bt < ntile ? aux.tiles[bt] : make_int4(0, 0, 0, 0);
+      // always PT loads per lane (clamped): the chunk-0 wait counts them
+      const int64_t hi = trn.z > trn.y ? (int64_t)trn.z - 1 : 0;
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        const int64_t p = min((int64_t)trn.y + wid * (PT * 32) + t * 32 + cl, hi);
+        idxn[t] = idx[p];
+      }
+    }
+  };
   // one block tile (a lambda so the single-tile launch compiles to straight-line code:
   // the loop form costs registers the 3-tile plain form does not have)
   auto tile = [&](const int64_t bt) {
@@ -428,7 +444,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   int64_t pbase, pend = n;
   const float* hbase = hn;
   if constexpr (CAND) {
-    const int4 tr = aux.tiles[bt];
+    const int4 tr = trn;
     acl = tr.x;
     pend = tr.z;
     pbase = (int64_t)tr.y + (int64_t)wid * (PT * 32);
@@ -446,7 +462,9 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   for (int t = 0; t < PT; ++t) {
     const int64_t p = pbase + t * 32 + cl;
     const bool ok = p < pend;
-    const int64_t row = ok ? (idx ? (int64_t)idx[p] : p) : 0;
+    int64_t row;
+    if constexpr (CAND) row = ok ? (int64_t)idxn[t] : 0;
+    else row = ok ? (idx ? (int64_t)idx[p] : p) : 0;
     const uint16_t* src = X + row * ldx + h * 8;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
@@ -545,6 +563,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     // chunk j >= 1 is needed iff its first (smallest) distance is <= R; chunk 0 always
     nch_t = 1 + __popcll(__ballot(lane >= 1 && lane < nchunk && thrv <= R));
     issue(0);                           // under the set-up below (buffer 0 free: barrier)
+    prefetch_tile(bt + gridDim.x);      // PT loads after the DMA: chunk 0 waits vmcnt(PT)
   }
   if constexpr (LOOP) {
     // every wave is past the previous tile's appends: room for this tile's (<= TILE)?
@@ -634,7 +653,12 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       if (ahead >= 1) km_wait_vmcnt<GPT>();
       else km_wait_vmcnt<0>();
     } else {
-      km_wait_vmcnt<0>();
+      if constexpr (CAND) {
+        if (ch == 0) km_wait_vmcnt<PT>();   // the next tile's row ids stay in flight
+        else km_wait_vmcnt<0>();
+      } else {
+        km_wait_vmcnt<0>();
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // s_hn stores (first chunk)
     // publishes chunk ch to every wave AND retires everyone's reads of chunk ch-1,
@@ -785,6 +809,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   }
   };   // tile
   if constexpr (LOOP) {
+    prefetch_tile(blockIdx.x);
     for (int64_t bt = blockIdx.x; bt < ntile; bt += gridDim.x) tile(bt);
     flush_changed();
   } else {
