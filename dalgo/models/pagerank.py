@@ -43,7 +43,7 @@ class PageRankConfig:
                                  # no edge cut, the work units balance phase 1)
     tile: int = 16384            # blocked: ~edges per phase-1 wave tile
     exchange: str = "ghost"      # "ghost" | "allgather" (several ranks)
-    overlap: str = "auto"        # ghost exchange under the own-source SpMV: "auto" | "on" | "off"
+    overlap: str = "auto"        # ghost exchange under the SpMV: "auto" | "on" | "peer" | "off"
     fuse_update: bool = True     # K4b: rank / contribution update in the SpMV epilogue
 
 
@@ -96,8 +96,14 @@ class PageRank:
         self.fuse_update = cfg.fuse_update
         if self.spmv == "blocked":
             gsp = self.g_local if self.exchange == "ghost" else self.g
+            # ghost index space: no chunk straddles the own slice's end or a peer's block,
+            # so each peer's ghost chunks are one work-unit range (per-peer overlap)
+            splits = None
+            if self.exchange == "ghost":
+                splits = [sl] + [sl + o for o in self.ghost_off[1:-1]]
             self.layout = Gops.build_blocked(gsp, cfg.bin_width, cfg.chunk, cfg.tile,
-                                             src_split=sl if self.exchange == "ghost" else None)
+                                             src_split=sl if self.exchange == "ghost" else None,
+                                             src_splits=splits)
         self.dang = torch.zeros(1, dtype=fdt, device=dev)
         self.dang_next = torch.zeros(1, dtype=fdt, device=dev)
         od = self.outdeg.to(fdt)
@@ -153,6 +159,10 @@ class PageRank:
         comm.all_to_all_single(send_counts, recv_counts)
         self.recv_split = [int(x) for x in recv_counts.tolist()]
         self.send_split = [int(x) for x in send_counts.tolist()]
+        # ghost block of peer p: [ghost_off[p], ghost_off[p + 1]) past the own slice
+        self.ghost_off = [0]
+        for c_ in self.recv_split:
+            self.ghost_off.append(self.ghost_off[-1] + c_)
         req = torch.empty(sum(self.send_split), dtype=torch.int64, device=src.device)
         comm.all_to_all_single(req, ghosts, out_split=self.send_split, in_split=self.recv_split)
         self.send_idx = (req - g.v_lo).contiguous()
@@ -211,16 +221,25 @@ class PageRank:
             comm.all_reduce_sum(self.dang_next)
             self.dang, self.dang_next = self.dang_next, self.dang
 
-    def _overlap_pb(self) -> bool:
-        """K4b with the ghost exchange: phase 1 over the own-slice source chunks runs while
-        the all_to_all of the ghost contributions is in flight, phase 1 over the ghost
-        chunks after it (cfg.overlap: auto = when the own-slice units are at least a
-        quarter of all units; on / off force it)."""
+    def _overlap_pb(self) -> str:
+        """K4b with the ghost exchange: "whole" = phase 1 over the own-slice source chunks
+        runs while the all_to_all of the ghost contributions is in flight, phase 1 over the
+        ghost chunks after it; "peer" = the exchange is W - 1 grouped send/recv shifts and
+        each peer's ghost chunks run as soon as that peer's shift lands (the own share
+        alone is too short to hide a whole all_to_all at W >= 8); "" = no overlap.
+        cfg.overlap: auto = whole while the own-slice units are >= 1/4 of all units, else
+        peer; on = whole; peer; off."""
         if self.layout is None or self.exchange != "ghost":
-            return False
+            return ""
         ov = self.cfg.overlap
+        if ov in ("on", "peer"):
+            return "whole" if ov == "on" else "peer"
+        if ov != "auto":
+            return ""
         nwu = int(self.layout.wu_chunk.numel())
-        return ov == "on" or (ov == "auto" and nwu > 0 and self.layout.n_wu_below >= 0.25 * nwu)
+        if nwu == 0:
+            return ""
+        return "whole" if self.layout.n_wu_below >= 0.25 * nwu else "peer"
 
     def _overlap(self) -> bool:
         """Ghost exchange under the SpMV over own-slice sources: the all_to_all writes only
@@ -238,8 +257,42 @@ class PageRank:
     def _ph(self, name: str):
         return self.timer.phase(name) if self.timer is not None else NULL_PHASE
 
+    def _step_peer(self):
+        """K4b with the per-peer overlapped exchange (see _overlap_pb)."""
+        lay = self.layout
+        sl = self.g.slice_size
+        if self.send_buf is None:
+            self.send_buf = torch.empty(self.send_idx.numel(), dtype=self.fdt, device=self.dev)
+        with self._ph("exchange_issue"):
+            torch.index_select(self.c_slice, 0, self.send_idx, out=self.send_buf)
+            shifts = comm.exchange_by_shift(self.c_full[sl:], self.send_buf, self.recv_split,
+                                            self.send_split)
+        # work-unit range of every source block: own slice, then peer p's ghosts
+        bounds = (0,) + tuple(lay.wu_bounds) + (1 << 31,)
+        blk_of_peer = {}
+        bi = 1                                   # block 0 = own slice
+        for p in range(self.world):
+            if self.ghost_off[p + 1] > self.ghost_off[p]:
+                blk_of_peer[p] = bi
+                bi += 1
+        with self._ph("spmv_own"):
+            Gops.pb_spmv(lay, self.c_full, self.acc, self.pres, wu_range=(0, bounds[1]),
+                         phases=1)
+        with self._ph("spmv_ghost"):
+            for peer, h in shifts:
+                h.wait()
+                b = blk_of_peer.get(peer)
+                if b is not None:
+                    Gops.pb_spmv(lay, self.c_full, self.acc, self.pres,
+                                 wu_range=(bounds[b], bounds[b + 1]), phases=1)
+            Gops.pb_spmv(lay, self.c_full, self.acc, self.pres,
+                         update=self._pb_update_args(), phases=2)
+
     def step(self):
-        if self._overlap_pb():
+        ovp = self._overlap_pb()
+        if ovp == "peer":
+            self._step_peer()
+        elif ovp == "whole":
             lay = self.layout
             if self.send_buf is None:
                 self.send_buf = torch.empty(self.send_idx.numel(), dtype=self.fdt, device=self.dev)

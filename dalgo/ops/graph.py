@@ -179,11 +179,12 @@ class BlockedLayout:
     max_runs: int           # most non-empty runs in one chunk (phase 1 stages <= 4096 in LDS)
     bound: torch.Tensor = None   # f64[1] device scratch: this call's destination-sum bound
     n_wu_below: int = 0          # work units whose sources are < src_split (build_blocked)
+    wu_bounds: tuple = ()        # work units whose sources are < each of src_splits
 
 
 def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 1 << 40,
                   tile: int = 16384, items: int = 2048, min_piece: int = 1 << 14,
-                  src_split: int | None = None) -> BlockedLayout:
+                  src_split: int | None = None, src_splits=None) -> BlockedLayout:
     """One-time construction (device sorts) from any shard (src in the c index space).
 
     chunk_edges: cut a source chunk after ~this many edges. The default (no cut: chunks are
@@ -191,7 +192,12 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
     at R-MAT scale 26 vs 0.68 at 1M-edge chunks); load balance comes from the work units.
     src_split: no chunk straddles this source index, and ``n_wu_below`` counts the work
     units of the sources below it (the own slice of the ghost index space: their phase 1
-    can run while the ghost contributions are still being exchanged)."""
+    can run while the ghost contributions are still being exchanged).
+    src_splits: ascending source indices no chunk straddles (the own slice's end and the
+    start of every peer's ghost block); ``wu_bounds[i]`` counts the work units of the
+    sources below src_splits[i], so each peer's ghost chunks are one unit range."""
+    splits = sorted({int(x) for x in (src_splits or [])} |
+                    ({int(src_split)} if src_split is not None else set()))
     if bin_width not in (8192, 16384):
         raise ValueError("bin_width must be 8192 or 16384 (u64 LDS accumulator sizes of the kernel)")
     dev = shard.src.device
@@ -226,9 +232,14 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
     outd = torch.bincount(s, minlength=n_src)
     cs = torch.cumsum(outd, 0) - outd
     ids = torch.arange(n_src, device=dev)
-    if src_split is not None:     # source blocks restart at the split: no straddling chunk
-        sp = int(src_split)
-        blk = torch.where(ids < sp, ids // S, (sp + S - 1) // S + (ids - sp) // S)
+    if splits:                    # source blocks restart at every split: no straddling chunk
+        bnd = torch.tensor([0] + splits, dtype=torch.int64, device=dev)
+        seg = torch.searchsorted(bnd, ids, right=True) - 1
+        seg_len = torch.diff(torch.cat([bnd, torch.tensor([max(n_src, splits[-1])], device=dev)]))
+        nblk = (seg_len + S - 1) // S
+        base = torch.cumsum(nblk, 0) - nblk
+        blk = base[seg] + (ids - bnd[seg]) // S
+        del bnd, seg, seg_len, nblk, base
     else:
         blk = ids // S
     key = blk * (E // chunk_edges + 2) + cs // chunk_edges
@@ -362,7 +373,8 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
                          it(sp_bin), it(sp_first), it(sp_cnt), bin_width, nl, nch, nent, n_src,
                          max_indeg, int((chunk_run[1:] - chunk_run[:-1]).max().item()),
                          torch.zeros(1, dtype=torch.float64, device=dev),
-                         int((slo[wu_chunk] < src_split).sum().item()) if src_split is not None else 0)
+                         int((slo[wu_chunk] < src_split).sum().item()) if src_split is not None else 0,
+                         tuple(int((slo[wu_chunk] < b).sum().item()) for b in splits))
 
 
 def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: torch.Tensor,

@@ -244,6 +244,46 @@ def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, out_split: list[int]
     return work if async_op else out
 
 
+class _Group:
+    """Handles of one shift of :func:`exchange_by_shift` (wait() waits all of them)."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+
+
+def exchange_by_shift(out: torch.Tensor, inp: torch.Tensor, out_split: list[int],
+                      in_split: list[int]) -> list:
+    """The personalised exchange of :func:`all_to_all_single`, issued as W - 1 grouped
+    send/recv shifts (shift k: to rank + k, from rank - k; the same order on every rank,
+    so the pairs always match) that all start now. Returns [(source rank, handle)] in
+    shift order: a caller can consume each peer's rows as soon as they land (handle.wait()
+    orders the current stream after that shift only) instead of after the whole exchange.
+    Empty directions post nothing (both sides agree: the splits are each other's)."""
+    W, r = world_size(), rank()
+    if W == 1 or (inp.is_cuda and dist.get_backend() == "gloo"):
+        all_to_all_single(out, inp, out_split, in_split)
+        return [((r - k) % W, _Done()) for k in range(1, W)]
+    so = [0] * (W + 1)
+    ro = [0] * (W + 1)
+    for p in range(W):
+        so[p + 1] = so[p] + int(in_split[p])
+        ro[p + 1] = ro[p] + int(out_split[p])
+    res = []
+    for k in range(1, W):
+        dst, src = (r + k) % W, (r - k) % W
+        ops = []
+        if in_split[dst] > 0:
+            ops.append(dist.P2POp(dist.isend, inp[so[dst]:so[dst + 1]], dst))
+        if out_split[src] > 0:
+            ops.append(dist.P2POp(dist.irecv, out[ro[src]:ro[src + 1]], src))
+        res.append((src, _Group(dist.batch_isend_irecv(ops) if ops else [])))
+    return res
+
+
 def gather_to_rank0(local: torch.Tensor, counts: list[int]) -> torch.Tensor | None:
     """``collect()``: rows of every rank concatenated on rank 0 (None elsewhere)."""
     full = all_gather_varlen(local, counts)

@@ -100,6 +100,36 @@ def test_other_algorithms_two_ranks_equal_one():
     assert abs(one["mc"][0] - math.pi) < 0.02
 
 
+def _pr_peer(rt):
+    """K4b with the ghost exchange run as W - 1 per-peer shifts (each peer's ghost chunks
+    consumed as its shift lands) vs the whole all_to_all and vs no overlap."""
+    from dalgo.models.pagerank import PageRank, PageRankConfig
+    from dalgo.ops import graph as G
+    W, r = rt.world_size, rt.rank
+    s, d = G.rmat_edges(6000, 10, seed=5)
+    out = {}
+    for sem in ("reference", "standard"):
+        sh = G.build_shard(s, d, 1024, r, W)
+        for ov in ("peer", "on", "off"):
+            pr = PageRank(PageRankConfig(semantics=sem, spmv="blocked", chunk=256, tile=64,
+                                         overlap=ov), sh, W)
+            out[(sem, ov, "mode")] = pr._overlap_pb()
+            out[(sem, ov)] = pr.fit().collect()
+    return out
+
+
+def test_pagerank_per_peer_overlap_three_ranks():
+    one = run_world(_pr_peer, world=1)[0]
+    three = run_world(_pr_peer, world=3)
+    for sem in ("reference", "standard"):
+        assert three[0][(sem, "peer", "mode")] == "peer"
+        ref = one[(sem, "off")]
+        for ov in ("peer", "on", "off"):
+            got = three[0][(sem, ov)]
+            assert set(got) == set(ref)
+            assert max(abs(got[v] - ref[v]) for v in ref) < 1e-12, (sem, ov)
+
+
 def _error_check_body(rt):
     """Rank 1 alone carries a set K11 error word; both ranks must raise."""
     import torch
