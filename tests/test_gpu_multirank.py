@@ -40,16 +40,7 @@ def _torchrun(args, n=2, timeout=600, env_extra=None):
     return r.stdout
 
 
-def test_bench_two_ranks_gloo_on_one_gpu(cuda):
-    out = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--rows", "200000",
-                     "--steps", "5", "--warmup", "2"])
-    lines = [l for l in out.splitlines() if l.startswith("{")]
-    assert len(lines) == 1
-    d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0
-
-
-@pytest.mark.parametrize("script,extra,needle", [
+SCRIPTS = [
     ("optimization/bmuf.py", ["--synthetic", "50000,128", "--n-iterations", "5", "--quiet"], "Final acc:"),
     ("optimization/easgd.py", ["--synthetic", "50000,128", "--n-iterations", "5", "--quiet"], "Final acc:"),
     ("machine_learning/k-means.py", ["--synthetic", "20000,16", "--k", "8"], "Final centers:"),
@@ -59,21 +50,33 @@ def test_bench_two_ranks_gloo_on_one_gpu(cuda):
     ("graph_computation/pagerank.py", ["--rmat-scale", "12", "--top", "3"], "has rank:"),
     ("matrix_computation/matrix_decomposition.py", [], "iterations: 4, rmse:"),
     ("randomized_algorithm/monte_carlo.py", ["--num-samples", "1000000"], "Pi is roughly"),
-])
-def test_scripts_two_ranks_gloo_on_one_gpu(cuda, script, extra, needle):
-    out = _torchrun([script, "--device", "cuda", "--backend", "gloo", "--no-plot"] + extra)
-    assert needle in out
+]
+
+
+def test_scripts_two_ranks_gloo_on_one_gpu(cuda):
+    """Every entry script with 2 gloo ranks on cuda:0, all in ONE torchrun job
+    (tests/helpers/run_scripts.py: one process group, scripts run in-process in turn)."""
+    jobs = [[p, ["--device", "cuda", "--backend", "gloo", "--no-plot"] + extra]
+            for p, extra, _ in SCRIPTS]
+    out = _torchrun(["tests/helpers/run_scripts.py", json.dumps(jobs)])
+    for i, (path, _, needle) in enumerate(SCRIPTS):
+        part = out.split(f"==BEGIN {i}==")[1].split(f"==END {i}==")[0]
+        assert needle in part, (path, part[-2000:])
 
 
 SPIN = {"DALGO_ALLOW_SHARED_SPIN": "1"}
 
 
-def test_shared_gpu_disables_cross_process_waits(cuda):
-    """Two ranks on one GPU: every rank sees shared_device, K11 is never built (so no
-    persistent / one-kernel form either) and the bench reports the process group."""
+def test_bench_two_ranks_shared_gpu(cuda):
+    """bench.py with two gloo ranks on one GPU: one JSON line with the dp2 contract; every
+    rank sees shared_device, K11 is never built even when forced (so no persistent /
+    one-kernel form either) and the bench reports the process group."""
     out = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--rows", "200000",
                      "--steps", "5", "--warmup", "2"], env_extra={"DALGO_XGMI": "1"})
-    d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0
     assert d["shared_device"] is True and d["distinct_devices"] == 1
     assert d["config"]["allreduce"] == "gloo" and d["config"]["launch"] == "per-step"
     assert d["correctness_witness"]["passed"]
