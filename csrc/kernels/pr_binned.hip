@@ -170,10 +170,16 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
       const uint32_t ww[4] = {(uint32_t)wc.x, (uint32_t)wc.y, (uint32_t)wc.z, (uint32_t)wc.w};
       uint32_t hk[EPL];
       float cv[EPL];
+      // the lane's edges idx + k inside [e_lo, e_hi): k in [klo, klo + span), one 32-bit
+      // compare per edge instead of two 64-bit ones
+      const int klo = (int)min(max(e_lo - idx, (int64_t)0), (int64_t)EPL);
+      const int span = max((int)min(max(e_hi - idx, (int64_t)0), (int64_t)EPL) - klo, 0);
+      bool inr[EPL];
 #pragma unroll
       for (int k = 0; k < EPL; ++k) {
+        inr[k] = (uint32_t)(k - klo) < (uint32_t)span;
         const uint32_t h = (ww[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-        hk[k] = (idx + k >= e_lo && idx + k < e_hi) ? h : 0u;
+        hk[k] = inr[k] ? h : 0u;
         cv[k] = s_c[hk[k] & (S - 1)];
       }
       float part = -0.0f, outv[EPL];
@@ -181,7 +187,7 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
       int rk[EPL];                                       // markers so far (inclusive)
 #pragma unroll
       for (int k = 0; k < EPL; ++k) {
-        const bool in = idx + k >= e_lo && idx + k < e_hi;
+        const bool in = inr[k];
         part += in ? cv[k] : -0.0f;
         outv[k] = part;
         const bool f = hk[k] & 0x8000u;
@@ -204,9 +210,20 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
       const int h_ex = dpp_mov_i<0x138>(0, hh);
       const float carry_in = h_ex ? a_ex : carry + a_ex;
       const int rbase = run + cm - nm - 1;       // run of this lane's first entries
+      // run deltas of the lane's entries: its 8 edges touch at most nm + 1 runs and nearly
+      // always <= 2 (a run is one (chunk, 16K-destination bin) group: hundreds of edges),
+      // so two reads and a select, with all 8 reads only in a step where some lane spans
+      // three runs (wave-uniform branch; LDS reads: no vmcnt bookkeeping involved)
       int dl[EPL];
+      if (__ballot(nm >= 2) == 0ull) {
+        const int d0 = dsrc[max(rbase, 0)];
+        const int d1 = dsrc[max(min(rbase + 1, nr - 1), 0)];
 #pragma unroll
-      for (int k = 0; k < EPL; ++k) dl[k] = dsrc[max(rbase + rk[k], 0)];
+        for (int k = 0; k < EPL; ++k) dl[k] = rk[k] == 0 ? d0 : d1;
+      } else {
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) dl[k] = dsrc[max(rbase + rk[k], 0)];
+      }
       int j = cnt - nf;                          // this lane's first entry of the step
       bool first = true;
 #pragma unroll
@@ -231,11 +248,19 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
       // line group, so no single address is hammered by every wave): a fixed store count
       // keeps the compiler's vmcnt bookkeeping exact, so the D prefetched loads are not
       // drained at every step
+      // staged values read unconditionally (every slot is in range), all before the first
+      // store: one LDS round trip per step instead of one per store
+      int32_t pq[EPL];
+      float vq[EPL];
 #pragma unroll
       for (int q = 0; q < EPL; ++q) {
-        const int qi = lane + 64 * q;
-        const bool ok = qi < n_step;
-        val[ok ? (int64_t)sp[qi] : dummy] = ok ? sv[qi] : 0.f;
+        pq[q] = sp[lane + 64 * q];
+        vq[q] = sv[lane + 64 * q];
+      }
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) {
+        const bool ok = lane + 64 * q < n_step;
+        val[ok ? (int64_t)pq[q] : dummy] = ok ? vq[q] : 0.f;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
