@@ -119,8 +119,31 @@ def calibrate_launch(model, rt, a) -> dict:
         model._ok1, model._okp = one, pers
         model.graph, model._okg = graph, None
         t_all = time.perf_counter()
-        model.run_steps(2)            # first launch of this form (code objects, workspaces)
-        rt.synchronize()
+        # first launch of this form (code objects, workspaces; graph: warm step + capture).
+        # A form that raises on any rank is dropped on every rank (MAX of a failure flag)
+        bad = torch.zeros(1, dtype=torch.float64, device=rt.device)
+        try:
+            model.run_steps(2)
+            rt.synchronize()
+        except Exception as e:   # noqa: BLE001 -- reported, then decided collectively
+            print(f"[bench] rank {rt.rank}: launch form {name} failed: {e!r}", file=sys.stderr,
+                  flush=True)
+            bad.fill_(1.0)
+        comm.all_reduce_max(bad)
+        if float(bad.item()) > 0:
+            res[name] = None              # dropped on every rank
+            model.graph, model._okg = False, None
+            model._graphs.clear()
+            model._ok1, model._okp = False, False
+            try:
+                comm.check_device_errors(f"launch calibration ({name})")
+            except comm.DeviceCollectiveError:
+                fallback_plain(model, rt, f"launch calibration ({name})")
+                model.load_state_dict(snap)
+                rt.synchronize()
+                return {"failed": name, **res}
+            model.load_state_dict(snap)
+            continue
         rt.barrier()
         rt.synchronize()
         t0 = time.perf_counter()
@@ -140,7 +163,7 @@ def calibrate_launch(model, rt, a) -> dict:
             model.load_state_dict(snap)
             rt.synchronize()
             return {"failed": name, **res}
-    timed = {k: v for k, v in res.items() if k in cands}
+    timed = {k: v for k, v in res.items() if k in cands and v is not None}
     best = min(timed, key=timed.get)
     model._ok1, model._okp, graph = cands[best]
     model.graph, model._okg = graph, None

@@ -297,7 +297,9 @@ class ParallelSGD:
             xg = comm.xgmi_instance()
             ex = xg.exchanges if xg is not None else 0
             try:
-                with torch.cuda.graph(g):
+                # thread_local: the process group's watchdog thread keeps querying its own
+                # streams during the capture, which a global-mode capture would reject
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     self._step_impl(0, self._t_dev)
                     self._t_dev.add_(1)
             finally:
