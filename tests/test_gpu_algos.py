@@ -923,14 +923,15 @@ def test_kmeans_sort_active(cuda):
     assert int((th - tl).sum()) == m
 
 
-def test_kmeans_assign_rows_candidates(cuda):
+@pytest.mark.parametrize("d", [64, 128])
+def test_kmeans_assign_rows_candidates(cuda, d):
     """Candidate-pruned filtered K2 (tiles of one cluster stream only the centres within
     2 max(u) + slack of their centre): same assignment as the full pass on the active
     rows (mismatches only at kernel-rounding near-ties), the pruned centres bound l from
     below, the changed rows are collected exactly."""
     torch.manual_seed(12)
     from dalgo.data.synthetic import blobs
-    n, d, k = 120_000, 128, 512
+    n, k = 120_000, 512
     X = K.prepare_points(blobs(n, d, k, device=cuda, dtype=torch.bfloat16, seed=4))
     g = torch.Generator(device="cpu").manual_seed(2)
     C0 = X[torch.randperm(n, generator=g)[:k].to(cuda), :d].float()
