@@ -411,8 +411,19 @@ void kmeans_move_sorted(const Tensor& X, int64_t DP, const Tensor& changed, int6
                         const Tensor& a_new, const Tensor& a_old, Tensor S64, Tensor cnt,
                         const std::optional<Tensor>& xh, const std::optional<Tensor>& Q, int64_t seg,
                         Tensor block_counts, Tensor cluster_start, Tensor seg_start, Tensor perm,
-                        Tensor ec, Tensor er, const std::optional<Tensor>& m_dev, int64_t chunk) {
+                        Tensor ec, Tensor er, const std::optional<Tensor>& m_dev, int64_t chunk,
+                        const std::optional<Tensor>& cnew, const std::optional<Tensor>& cold) {
   TORCH_CHECK(kmeans_dp(DP) == DP, "DP must be 16/32/64/128");
+  TORCH_CHECK(cnew.has_value() == cold.has_value(), "kmeans_move_sorted: cnew and cold together");
+  const int32_t* cnp = nullptr;
+  const int32_t* cop = nullptr;
+  if (cnew.has_value()) {     // clusters aligned with `changed` (the K2 epilogue's)
+    check_i32(*cnew, "cnew");
+    check_i32(*cold, "cold");
+    TORCH_CHECK(cnew->numel() >= m && cold->numel() >= m, "cnew / cold [m]");
+    cnp = cnew->data_ptr<int32_t>();
+    cop = cold->data_ptr<int32_t>();
+  }
   check_points(X, (int)DP);
   check_dev(changed, "changed");
   TORCH_CHECK(changed.scalar_type() == at::kInt && m >= 0 && m <= changed.numel(), "changed");
@@ -460,13 +471,14 @@ void kmeans_move_sorted(const Tensor& X, int64_t DP, const Tensor& changed, int6
                       block_counts.data_ptr<int>(), cluster_start.data_ptr<int64_t>(),
                       seg_start.data_ptr<int64_t>(), perm.data_ptr<int>(), S64.data_ptr<double>(),
                       reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>()), xp, qp, mdp, chunk,
-                      cur_stream()),
+                      cnp, cop, cur_stream()),
                   "kmeans_move_sorted");
 }
 
 // bound-filtered Lloyd: active rows (u + delta[a] >= s[a]) -> idx, their assignment -> a_prev
 void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta, const Tensor& s,
-                   Tensor a_prev, Tensor idx, Tensor n_active, const std::optional<Tensor>& acl) {
+                   const std::optional<Tensor>& a_prev, Tensor idx, Tensor n_active,
+                   const std::optional<Tensor>& acl) {
   const int64_t n = assign.numel();
   check_i32(assign, "assign");
   check_f32(u, "u");
@@ -474,9 +486,14 @@ void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta
   TORCH_CHECK(l.numel() >= n, "kmeans_filter: l [n]");
   check_f32(delta, "delta");
   check_f32(s, "s");
-  check_i32(a_prev, "a_prev");
+  int32_t* app = nullptr;
+  if (a_prev.has_value()) {   // the Hamerly-only K2 reads the previous clusters per row
+    check_i32(*a_prev, "a_prev");
+    TORCH_CHECK(a_prev->numel() >= n, "kmeans_filter: a_prev [n]");
+    app = a_prev->data_ptr<int32_t>();
+  }
   check_i32(idx, "idx");
-  TORCH_CHECK(u.numel() >= n && a_prev.numel() >= n && idx.numel() >= n, "kmeans_filter sizes");
+  TORCH_CHECK(u.numel() >= n && idx.numel() >= n, "kmeans_filter sizes");
   TORCH_CHECK(delta.numel() == s.numel(), "delta / s [k]");
   TORCH_CHECK(n_active.scalar_type() == at::kLong && n_active.numel() >= 1, "n_active int64[1]");
   int32_t* aclp = nullptr;
@@ -488,7 +505,7 @@ void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta
   DeviceGuard guard(assign.device());
   DALGO_CHECK_HIP(dalgo_km_filter(assign.data_ptr<int32_t>(), u.data_ptr<float>(), l.data_ptr<float>(),
                                   delta.data_ptr<float>(), s.data_ptr<float>(), (int)delta.numel(), n,
-                                  a_prev.data_ptr<int32_t>(), idx.data_ptr<int32_t>(),
+                                  app, idx.data_ptr<int32_t>(),
                                   reinterpret_cast<unsigned long long*>(n_active.data_ptr<int64_t>()),
                                   idx.numel(), aclp, cur_stream()),
                   "kmeans_filter");
@@ -554,7 +571,8 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
                        const std::optional<Tensor>& m_dev, const std::optional<Tensor>& a_prev,
                        const std::optional<Tensor>& tol, const std::optional<Tensor>& u,
                        const std::optional<Tensor>& l, const std::optional<Tensor>& changed,
-                       const std::optional<Tensor>& n_changed) {
+                       const std::optional<Tensor>& n_changed, const std::optional<Tensor>& chg_new,
+                       const std::optional<Tensor>& chg_old) {
   TORCH_CHECK(Cq.dim() == 2 && Cq.is_contiguous() && Cq.scalar_type() == at::kBFloat16, "Cq bf16");
   const int DP = (int)Cq.size(1);
   TORCH_CHECK(DP == 64 || DP == 128, "kmeans_assign_idx: DP 64 or 128");
@@ -591,19 +609,31 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
   DalgoKmPost post{};
   const DalgoKmPost* pp = nullptr;
   if (m_dev.has_value()) {   // filtered iteration: rows = *m_dev (device), m = its upper bound
-    TORCH_CHECK(a_prev.has_value() && tol.has_value() && u.has_value() && l.has_value() &&
-                    changed.has_value() && n_changed.has_value(),
+    // a_prev: the previous clusters (the candidate form takes them from its tiles)
+    TORCH_CHECK((a_prev.has_value() || !cand.empty()) && tol.has_value() && u.has_value() &&
+                    l.has_value() && changed.has_value() && n_changed.has_value(),
                 "kmeans_assign_idx: the device-count form needs a_prev, tol, u, l, changed, n_changed");
     check_dev(*m_dev, "m_dev");
     TORCH_CHECK(m_dev->scalar_type() == at::kLong && m_dev->numel() >= 1, "m_dev int64[1]");
-    check_i32(*a_prev, "a_prev");
+    if (a_prev.has_value()) {
+      check_i32(*a_prev, "a_prev");
+      TORCH_CHECK(a_prev->numel() >= X.size(0), "a_prev [n]");
+      post.a_prev = a_prev->data_ptr<int32_t>();
+    }
     check_i32(*changed, "changed");
-    TORCH_CHECK(a_prev->numel() >= X.size(0), "a_prev [n]");
+    TORCH_CHECK(chg_new.has_value() == chg_old.has_value(), "chg_new and chg_old together");
+    if (chg_new.has_value()) {
+      check_i32(*chg_new, "chg_new");
+      check_i32(*chg_old, "chg_old");
+      TORCH_CHECK(chg_new->numel() >= changed->numel() && chg_old->numel() >= changed->numel(),
+                  "chg_new / chg_old [cap]");
+      post.chg_new = chg_new->data_ptr<int32_t>();
+      post.chg_old = chg_old->data_ptr<int32_t>();
+    }
     check_f32(*tol, "tol");
     TORCH_CHECK(n_changed->scalar_type() == at::kLong && n_changed->numel() >= 1, "n_changed int64[1]");
     check_dev(*n_changed, "n_changed");
     post.mcount = reinterpret_cast<const unsigned long long*>(m_dev->data_ptr<int64_t>());
-    post.a_prev = a_prev->data_ptr<int32_t>();
     post.tol = tol->data_ptr<float>();
     post.u = f32n(u, "u");
     post.l = f32n(l, "l");
@@ -1178,9 +1208,10 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("kmeans_move_sorted(Tensor X, int DP, Tensor changed, int m, Tensor a_new, Tensor a_old, "
         "Tensor(a!) S64, Tensor(b!) cnt, Tensor? xh, Tensor(c!)? Q, int seg, Tensor(d!) block_counts, "
         "Tensor(e!) cluster_start, Tensor(f!) seg_start, Tensor(g!) perm, Tensor(h!) ec, "
-        "Tensor(i!) er, Tensor? m_dev=None, int chunk=65536) -> ()");
+        "Tensor(i!) er, Tensor? m_dev=None, int chunk=65536, Tensor? cnew=None, "
+        "Tensor? cold=None) -> ()");
   m.def("kmeans_filter(Tensor assign, Tensor(a!) u, Tensor(e!) l, Tensor delta, Tensor s, "
-        "Tensor(b!) a_prev, Tensor(c!) idx, Tensor(d!) n_active, Tensor(f!)? acl=None) -> ()");
+        "Tensor(b!)? a_prev, Tensor(c!) idx, Tensor(d!) n_active, Tensor(f!)? acl=None) -> ()");
   m.def("kmeans_sort_active(Tensor acl, Tensor idx, Tensor n_active, int k, int chunk, "
         "Tensor(a!) block_counts, Tensor(b!) cstart, Tensor(c!) seg_start, Tensor(d!) rows_sorted, "
         "int tile, Tensor(e!) tiles, Tensor(g!) n_tiles) -> ()");
@@ -1193,7 +1224,8 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor[] cand, "
         "Tensor(b!)? mind=None, Tensor(c!)? mind2=None, Tensor(d!)? xh=None, Tensor(e!)? xmax=None, "
         "Tensor? m_dev=None, Tensor? a_prev=None, Tensor? tol=None, Tensor(f!)? u=None, "
-        "Tensor(g!)? l=None, Tensor(h!)? changed=None, Tensor(i!)? n_changed=None) -> ()");
+        "Tensor(g!)? l=None, Tensor(h!)? changed=None, Tensor(i!)? n_changed=None, "
+        "Tensor(j!)? chg_new=None, Tensor(l!)? chg_old=None) -> ()");
   m.def("kmeans_bounds_init(Tensor mind, Tensor mind2, Tensor xmax, int n, Tensor(a!) u, "
         "Tensor(b!) l, Tensor(c!) tol) -> ()");
   m.def("kmeans_update(Tensor(a!) C, Tensor S, Tensor cnt, Tensor(b!) Cq, Tensor(c!) hn, "

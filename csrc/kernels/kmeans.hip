@@ -302,6 +302,9 @@ struct KmAux {
   int* changed;                       // LOOP: rows whose cluster changed ...
   unsigned long long* n_changed;      //       ... and their number
   long long cap;                      //       capacity of `changed`
+  int* chg_new;                       // LOOP (optional): their new and previous cluster,
+  int* chg_old;                       //       aligned with `changed` (the moved-row sort
+                                      //       then reads them sequentially)
   // CAND (candidate-pruned LOOP): the active rows sorted by cluster (idx), tiles that never
   // straddle two clusters, and each centre's neighbour lists (km_centre_nbrs_kernel)
   const int4* tiles;                  // tile t: (cluster, first, end position in idx, -)
@@ -310,7 +313,7 @@ struct KmAux {
   const int32_t* nb;                  // [k][kpad]: their ids
   const float* nd;                    // [k][kpad]: |c - c_a| rounded down, ascending
 };
-constexpr int kChgBuf = 1024;         // changed rows buffered per block (LDS)
+constexpr int kChgBuf = 512;          // changed rows buffered per block (LDS)
 
 __device__ __forceinline__ float km_up1(float x) { return nextafterf(x, __builtin_inff()); }
 __device__ __forceinline__ float km_dn1(float x) { return nextafterf(x, -__builtin_inff()); }
@@ -347,6 +350,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   __shared__ double s_sse[NW];
 
   __shared__ int s_chg[LOOP ? kChgBuf : 1];
+  __shared__ uint16_t s_chgn[LOOP ? kChgBuf : 1], s_chgo[LOOP ? kChgBuf : 1];
   // CAND: the tile cluster's neighbour list (ids, k <= 1024), double-buffered by tile parity
   // so a tile can stage its list before the barrier that ends the previous tile's reads
   __shared__ uint16_t s_nb[CAND ? 2 : 1][CAND ? 1024 : 1];
@@ -373,7 +377,13 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       __syncthreads();
       const long long b = (long long)s_chg_base;
       for (int j = tid; j < c; j += NT)
-        if (b + j < aux.cap) aux.changed[b + j] = s_chg[j];
+        if (b + j < aux.cap) {
+          aux.changed[b + j] = s_chg[j];
+          if (aux.chg_new) {
+            aux.chg_new[b + j] = s_chgn[j];
+            aux.chg_old[b + j] = s_chgo[j];
+          }
+        }
       __syncthreads();
       if (tid == 0) s_nchg = 0;
     }
@@ -791,6 +801,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     const int64_t p = pbase + t * 32 + cl;
     bool chg = false;
     int64_t row = 0;
+    int old_c = 0;
     if (h == 0 && p < pend) {
       // acc = 0.5|x-c|^2 + M - 0.5|x|^2
       const float dist = fmaxf(2.f * (bv - M) + x2[t], 0.f);
@@ -804,7 +815,8 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
         if constexpr (CAND) lo2 = fminf(lo2, km_dn1(nd_first - ua[t]));
         aux.l[row] = fmaxf(lo2, 0.f);
         // CAND: the tile's rows were sorted by their previous cluster, acl
-        chg = bi != (CAND ? acl : aux.a_prev[row]);
+        old_c = CAND ? acl : aux.a_prev[row];
+        chg = bi != old_c;
       } else {
         if (mind) mind[row] = dist;
         if constexpr (TOP2) mind2[row] = fmaxf(2.f * (bv2 - M) + x2[t], 0.f);
@@ -818,7 +830,12 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
         int base = 0;
         if (lane == 0) base = atomicAdd(&s_nchg, __popcll(cm));
         base = __shfl(base, 0);
-        if (chg) s_chg[base + __popcll(cm & ((1ull << lane) - 1ull))] = (int)row;
+        if (chg) {
+          const int slot = base + __popcll(cm & ((1ull << lane) - 1ull));
+          s_chg[slot] = (int)row;
+          s_chgn[slot] = (uint16_t)bi;
+          s_chgo[slot] = (uint16_t)old_c;
+        }
       }
     }
   }
@@ -1149,14 +1166,18 @@ kmeans_segsum_kernel(const T* __restrict__ X, int64_t ldx, const int* __restrict
 __global__ void __launch_bounds__(256)
 km_dexpand_kernel(const int32_t* __restrict__ changed, int64_t m, const int32_t* __restrict__ a_new,
                   const int32_t* __restrict__ a_old, int* __restrict__ ec, int* __restrict__ er,
-                  const unsigned long long* __restrict__ mdev) {
+                  const unsigned long long* __restrict__ mdev, const int32_t* __restrict__ cnew,
+                  const int32_t* __restrict__ cold) {
+  // cnew / cold (optional): the clusters aligned with `changed` (written by the K2
+  // epilogue): sequential reads instead of two gathers per moved row
   if (mdev != nullptr) m = min(m, (int64_t)*mdev);
   const int64_t n2 = 2 * m;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n2;
        e += (int64_t)gridDim.x * blockDim.x) {
     const bool add = e < m;
     const int row = changed[add ? e : e - m];
-    ec[e] = add ? a_new[row] : a_old[row];
+    if (cnew) ec[e] = add ? cnew[e] : cold[e - m];
+    else ec[e] = add ? a_new[row] : a_old[row];
     er[e] = add ? row : ~row;          // negative: subtract
   }
 }
@@ -1337,8 +1358,10 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
   int64_t grid = cdiv(n, (int64_t)NW * PT * 32);
   if (grid == 0) return hipSuccess;
   if ((aux.mcount != nullptr) != LOOP) return hipErrorInvalidValue;
-  if (LOOP && (aux.tol == nullptr || aux.u == nullptr || aux.l == nullptr || aux.a_prev == nullptr ||
-               aux.changed == nullptr || aux.n_changed == nullptr))
+  // a_prev: the Hamerly-only form's previous clusters (the candidate form has them per tile)
+  if (LOOP && (aux.tol == nullptr || aux.u == nullptr || aux.l == nullptr ||
+               (!CAND && aux.a_prev == nullptr) || aux.changed == nullptr ||
+               aux.n_changed == nullptr))
     return hipErrorInvalidValue;
   if (CAND && (kpad > 1024 || aux.tiles == nullptr || aux.n_tiles == nullptr || aux.hnb == nullptr ||
                aux.nb == nullptr || aux.nd == nullptr || idx == nullptr))
@@ -1474,13 +1497,15 @@ hipError_t dalgo_kmeans_move_sorted(const void* X, int is_bf16, int64_t ldx, int
                                     int* block_counts, int64_t* cluster_start, int64_t* seg_start,
                                     int* perm, double* S, unsigned long long* cnt, const float* xh,
                                     double* Q, const unsigned long long* mdev, int64_t chunk,
-                                    hipStream_t st) {
+                                    const int32_t* cnew, const int32_t* cold, hipStream_t st) {
   if (m <= 0) return hipSuccess;
   const int64_t n2 = 2 * m;
   if (k < 1 || k > kScKmax || B < 1 || seg < 1 || chunk < 1 || n2 >= (int64_t)0x7fffffff)
     return hipErrorInvalidValue;
   const int g = (int)std::min<int64_t>(cdiv(n2, 256), 4096);
-  hipLaunchKernelGGL(km_dexpand_kernel, dim3(g), dim3(256), 0, st, changed, m, a_new, a_old, ec, er, mdev);
+  if ((cnew == nullptr) != (cold == nullptr)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(km_dexpand_kernel, dim3(g), dim3(256), 0, st, changed, m, a_new, a_old, ec, er, mdev,
+                     cnew, cold);
   DALGO_LAUNCH_CHECK();
   const int64_t rpc = cdiv(n2, B);
   const size_t lds_k = (size_t)k * sizeof(int);
@@ -1541,7 +1566,9 @@ hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP
   if (post != nullptr) {
     aux.mcount = post->mcount; aux.a_prev = post->a_prev; aux.tol = post->tol; aux.u = post->u;
     aux.l = post->l; aux.changed = post->changed; aux.n_changed = post->n_changed;
-    aux.cap = post->cap;
+    aux.cap = post->cap; aux.chg_new = post->chg_new; aux.chg_old = post->chg_old;
+    if ((aux.chg_new == nullptr) != (aux.chg_old == nullptr)) return hipErrorInvalidValue;
+    if (cand == nullptr && aux.a_prev == nullptr) return hipErrorInvalidValue;
     if (cand != nullptr) {
       // idx = the active rows sorted by cluster (dalgo_kmeans_sort_active)
       aux.tiles = reinterpret_cast<const int4*>(cand->tiles);

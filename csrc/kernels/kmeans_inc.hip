@@ -166,7 +166,7 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, floa
       if (in && !act) {
         u[i] = ub[e];
         l[i] = lb[e];
-      } else if (act) {
+      } else if (act && a_prev) {
         a_prev[i] = a[e];
       }
       const uint64_t mask = __ballot(act);

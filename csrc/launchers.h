@@ -36,6 +36,8 @@ struct DalgoKmPost {
   int* changed;
   unsigned long long* n_changed;      // zeroed by the caller
   long long cap;
+  int* chg_new;                       // optional: clusters of the changed rows (aligned)
+  int* chg_old;
 };
 
 // candidate-pruned K2 (dalgo_kmeans_sort_active + dalgo_km_centre_nbrs outputs)
@@ -91,7 +93,7 @@ hipError_t dalgo_kmeans_move_sorted(const void* X, int is_bf16, int64_t ldx, int
                                     int* block_counts, int64_t* cluster_start, int64_t* seg_start,
                                     int* perm, double* S, unsigned long long* cnt, const float* xh,
                                     double* Q, const unsigned long long* mdev, int64_t chunk,
-                                    hipStream_t st);
+                                    const int32_t* cnew, const int32_t* cold, hipStream_t st);
 hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n, int64_t ldx, int DP,
                                           const int* assign, int k, int B, int seg, int* block_counts,
                                           int64_t* cluster_start, int64_t* seg_start, int* perm,

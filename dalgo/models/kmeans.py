@@ -137,6 +137,13 @@ class KMeans:
         # cluster, every tile's centre stream cut to a prefix of its centre's neighbour list
         self._cand = (K.CandWorkspace(self.dev, n, k, self.cen.Cq.shape[0], self.DP)
                       if self.cfg.candidates and self.cen.Cq.shape[0] <= 1024 else None)
+        if self._cand is not None:
+            # the candidate K2 takes the previous cluster from its tile and writes the moved
+            # rows' new / previous clusters next to them: no a_prev pass, no gathers
+            self._chg_new = torch.empty(max(n, 1), **i32)
+            self._chg_old = torch.empty(max(n, 1), **i32)
+            self._post_args = dict(self._post_args, a_prev=None, chg_new=self._chg_new,
+                                   chg_old=self._chg_old)
 
     def _ph(self, name: str):
         return self.timer.phase(name) if self.timer is not None else NULL_PHASE
@@ -225,8 +232,9 @@ class KMeans:
                 else:
                     K.centre_bounds(self.cen.Cq, self._cq_prev, k, d, self._delta, self._s)
             with self._ph("filter"):
-                K.filter_rows(self.assign, self._u, self._l, self._delta, self._s, self._a_prev,
-                              self._idx, self._n_active, cw.acl if cw is not None else None)
+                K.filter_rows(self.assign, self._u, self._l, self._delta, self._s,
+                              self._a_prev if cw is None else None, self._idx, self._n_active,
+                              cw.acl if cw is not None else None)
                 if cw is not None:
                     K.sort_active(self._idx, self._n_active, cw)
             self._n_changed.zero_()
@@ -237,7 +245,8 @@ class KMeans:
                               self.assign, post=self._post_args, cand=cw)
             with self._ph("accumulate_incremental"):
                 K.move_rows(self.X, self.DP, self._changed, self._n_changed, self.assign,
-                            self._a_prev, self._S64, self._cnt64, self._mws, self._xh, self._Q)
+                            self._a_prev, self._S64, self._cnt64, self._mws, self._xh, self._Q,
+                            *((self._chg_new, self._chg_old) if cw is not None else (None, None)))
                 self.S.copy_(self._S64)
                 self.cnt.copy_(self._cnt64)
             self._record(0, self._n_active)

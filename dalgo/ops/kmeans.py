@@ -188,15 +188,17 @@ class MoveWorkspace:
 
 def move_rows(X: torch.Tensor, DP: int, changed: torch.Tensor, m_dev: torch.Tensor,
               a_new: torch.Tensor, a_old: torch.Tensor, S64: torch.Tensor, cnt: torch.Tensor,
-              ws: MoveWorkspace, xh: torch.Tensor | None = None, Q: torch.Tensor | None = None):
+              ws: MoveWorkspace, xh: torch.Tensor | None = None, Q: torch.Tensor | None = None,
+              cnew: torch.Tensor | None = None, cold: torch.Tensor | None = None):
     """Incremental K3: S64[a_new[r]] += x_r, S64[a_old[r]] -= x_r (f64), counts likewise
     (and Q, the per-cluster sum of |x|^2 = 2 xh, when given), for the rows r in
     changed[:*m_dev] (device count, <= ws.cap). The 2m signed entries are counting-sorted
     by cluster and every wave adds a run of <= SEG_ROWS of them in f64 registers:
-    ~(2m / SEG_ROWS + k) d-vector atomics."""
+    ~(2m / SEG_ROWS + k) d-vector atomics. cnew / cold: the moved rows' clusters aligned
+    with ``changed`` (the filtered K2 writes them): read in order instead of gathered."""
     _ext.ops().kmeans_move_sorted(X, int(DP), changed, ws.cap, a_new, a_old, S64, cnt, xh, Q,
                                   SEG_ROWS, ws.block_counts, ws.cluster_start, ws.seg_start,
-                                  ws.perm, ws.ec, ws.er, m_dev, CHUNK_ROWS)
+                                  ws.perm, ws.ec, ws.er, m_dev, CHUNK_ROWS, cnew, cold)
 
 
 # ------------------------------------------------------------------ bound-filtered Lloyd
@@ -224,11 +226,11 @@ def centre_bounds(Cq_now: torch.Tensor, Cq_prev: torch.Tensor, k: int, d: int,
 
 
 def filter_rows(assign: torch.Tensor, u: torch.Tensor, l: torch.Tensor, delta: torch.Tensor,
-                s: torch.Tensor, a_prev: torch.Tensor, idx: torch.Tensor,
+                s: torch.Tensor, a_prev: torch.Tensor | None, idx: torch.Tensor,
                 n_active: torch.Tensor, acl: torch.Tensor | None = None) -> None:
-    """Rows that may change cluster -> idx[:m] (their cluster -> a_prev, and -> acl[:m] in
-    list order when given), m -> n_active (device; no sync). The largest centre shift is
-    reduced from delta in the kernel."""
+    """Rows that may change cluster -> idx[:m] (their cluster -> a_prev[row] when given,
+    and -> acl[:m] in list order when given), m -> n_active (device; no sync). The
+    largest centre shift is reduced from delta in the kernel."""
     n_active.zero_()
     _ext.ops().kmeans_filter(assign, u, l, delta, s, a_prev, idx, n_active, acl)
 
@@ -307,8 +309,9 @@ def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
         return
     _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign,
                                  cand.cand() if cand is not None else [], None, None, None, None,
-                                 post["m_dev"], post["a_prev"], post["tol"], post["u"], post["l"],
-                                 post["changed"], post["n_changed"])
+                                 post["m_dev"], post.get("a_prev"), post["tol"], post["u"],
+                                 post["l"], post["changed"], post["n_changed"],
+                                 post.get("chg_new"), post.get("chg_old"))
 
 
 def bounds_init(mind: torch.Tensor, mind2: torch.Tensor, xmax: torch.Tensor, n: int,

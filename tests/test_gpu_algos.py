@@ -965,9 +965,12 @@ def test_kmeans_assign_rows_candidates(cuda, d):
     K.sort_active(rows, cnt, ws)
     a = torch.full((n,), -7, dtype=torch.int32, device=cuda)
     changed = torch.empty(n, dtype=torch.int32, device=cuda)
+    cnew = torch.full((n,), -1, dtype=torch.int32, device=cuda)
+    cold = torch.full((n,), -1, dtype=torch.int32, device=cuda)
     nch = torch.zeros(1, dtype=torch.int64, device=cuda)
     K.assign_rows(X, cen, ws.rows, n, a, post=dict(
-        m_dev=cnt, a_prev=a_prev, tol=tol, u=u, l=l, changed=changed, n_changed=nch), cand=ws)
+        m_dev=cnt, a_prev=None, tol=tol, u=u, l=l, changed=changed, n_changed=nch,
+        chg_new=cnew, chg_old=cold), cand=ws)
     sel = torch.zeros(n, dtype=torch.bool, device=cuda)
     sel[rows.long()] = True
     assert bool((a[~sel] == -7).all())
@@ -988,6 +991,9 @@ def test_kmeans_assign_rows_candidates(cuda, d):
     exp = torch.nonzero(sel & (a != a_prev))[:, 0]
     assert c == exp.numel()
     assert torch.equal(torch.sort(changed[:c]).values.long(), exp)
+    # the moved rows' clusters travel next to them (no a_prev array was given)
+    rows_c = changed[:c].long()
+    assert torch.equal(cnew[:c], a[rows_c]) and torch.equal(cold[:c], a_prev[rows_c])
 
 
 def test_kmeans_candidates_match_plain(cuda):
