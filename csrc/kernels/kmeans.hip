@@ -354,8 +354,6 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // CAND: the tile cluster's neighbour list (ids, k <= 1024), double-buffered by tile parity
   // so a tile can stage its list before the barrier that ends the previous tile's reads
   __shared__ uint16_t s_nb[CAND ? 2 : 1][CAND ? 1024 : 1];
-  // CAND: landing slots of the next tile's row prefetch (4 B per lane, never read)
-  __shared__ uint32_t s_pf[CAND ? NW * 64 : 1];
   int par = 0;
   __shared__ int s_nchg;
   __shared__ unsigned long long s_chg_base;
@@ -760,21 +758,10 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     }
   }
   reduce_tile(pacc, T0, pcb);
-  if constexpr (CAND) {
+  // (warming L2 with the next tile's rows by throw-away LDS-DMA here measured no gain:
+  // 17.92 vs 17.86 ms per iteration of the benchmark job)
+  if constexpr (CAND)
     if (nch_t < nchunk) nd_first = __shfl(thrv, nch_t);
-    // warm L2 with the next tile's point rows (its row ids arrived during this tile): one
-    // 4-B LDS-DMA per 128-B line (lane half h takes line h of its point's 256-B row) into
-    // throw-away LDS slots, so the next prologue's gathers hit L2 instead of HBM; the DMA
-    // drains at the next tile's own load wait
-    const uint32_t m0v = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(km_lds_void*)s_pf + (uint32_t)(wid * 64 * 4));
-#pragma unroll
-    for (int t = 0; t < PT; ++t) {
-      const uint16_t* src = X + (int64_t)idxn[t] * ldx + h * (DP / 2);
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off"
-                   :: "s"(m0v), "v"(src) : "memory");
-    }
-  }
 
   // ---- decode, combine the two lane halves (same point, disjoint centre rows)
 #pragma unroll
