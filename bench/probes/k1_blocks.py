@@ -14,6 +14,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=1_250_000)
 ap.add_argument("--dim", type=int, default=1024)
 ap.add_argument("--iters", type=int, default=300)
+ap.add_argument("--tbs", default="192,256,320,384,512")
+ap.add_argument("--fgs", default="0,8")
+ap.add_argument("--reps", type=int, default=1)
 a = ap.parse_args()
 dev = torch.device("cuda")
 X = torch.empty((a.rows, a.dim), dtype=torch.bfloat16, device=dev)
@@ -25,8 +28,9 @@ G = torch.zeros_like(W)
 C = torch.zeros(1, device=dev)
 cnt = torch.zeros(1, dtype=torch.float64, device=dev)
 res = {}
-for tb in (192, 256, 320, 384, 512):
-    for fg in (0, 8):
+for rep in range(a.reps):
+  for tb in [int(v) for v in a.tbs.split(",")]:
+    for fg in [int(v) for v in a.fgs.split(",")]:
         def run(t):
             L.lr_grad(X, y, W, seg, D=a.dim, seed=7, step=t, frac=0.1, G=G, C=C,
                       target_blocks=tb, fine_groups=fg, g_is_zero=True,
@@ -40,5 +44,5 @@ for tb in (192, 256, 320, 384, 512):
             run(100 + t)
         e1.record()
         torch.cuda.synchronize()
-        res[f"tb{tb}_fg{fg}"] = round(e0.elapsed_time(e1) / a.iters * 1000, 2)
+        res.setdefault(f"tb{tb}_fg{fg}", []).append(round(e0.elapsed_time(e1) / a.iters * 1000, 2))
 print(json.dumps(res))
