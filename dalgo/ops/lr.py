@@ -28,11 +28,9 @@ import os
 # Launch geometry of the row-streaming kernels (tuned on MI355X: bench/lr_kernel_sweep.py,
 # profiles/round1-3). One launch shape remains (csrc/kernels/lr_grad.hip launch_shape).
 TARGET_BLOCKS = 256        # workgroups per launch (split over segments): one per CU
-# one segment drawing >= LARGE_STEP_ROWS rows per step: 192 workgroups instead (5M / 10M
-# x 1024 bf16 at f = 0.1: 170.3 / 326.2 us vs 172.4 / 331.1 us per fused step; at 1.25M /
-# 2.5M rows 256 stays ahead: profiles/round4/r4_10/)
-LARGE_STEP_BLOCKS = 192
-LARGE_STEP_ROWS = 400_000
+# (192 for large steps measured 1.2-1.5 % faster in an isolated fused-step loop at 5M-10M
+# rows, but not in bench.py's one-kernel step, and 7 % slower in the persistent form:
+# profiles/round4/r4_10/, r4_11/ -- kept at 256)
 FINE_GROUPS = 8            # switch in-block work claims from 256-row groups to 64-row
                            # quarters once fewer than this many groups are unclaimed
 UNIT_SHIFT = 6             # sampled steps: work units of 2^6 rows (the final, fine claims
@@ -179,8 +177,6 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
                 b = seg.tolist()
                 max_seg_rows = max(b[i + 1] - b[i] for i in range(nseg))
         det = DETERMINISTIC if deterministic is None else bool(deterministic)
-        if target_blocks is None and nseg == 1 and max_seg_rows * min(frac, 1.0) >= LARGE_STEP_ROWS:
-            target_blocks = LARGE_STEP_BLOCKS
         gx, rpb = _grid(max(int(max_seg_rows), 1), nseg, target_blocks)
         S = ((D + 2 + 63) // 64) * 64
         ws = _workspace(X.device, nseg, gx, S)
