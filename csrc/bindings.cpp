@@ -572,7 +572,7 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
                        const std::optional<Tensor>& tol, const std::optional<Tensor>& u,
                        const std::optional<Tensor>& l, const std::optional<Tensor>& changed,
                        const std::optional<Tensor>& n_changed, const std::optional<Tensor>& chg_new,
-                       const std::optional<Tensor>& chg_old) {
+                       const std::optional<Tensor>& chg_old, int64_t cand_extend) {
   TORCH_CHECK(Cq.dim() == 2 && Cq.is_contiguous() && Cq.scalar_type() == at::kBFloat16, "Cq bf16");
   const int DP = (int)Cq.size(1);
   TORCH_CHECK(DP == 64 || DP == 128, "kmeans_assign_idx: DP 64 or 128");
@@ -664,6 +664,7 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
     cd.hnb = cand[2].data_ptr<float>();
     cd.nb = cand[3].data_ptr<int32_t>();
     cd.nd = cand[4].data_ptr<float>();
+    cd.extend = cand_extend != 0;
     cp = &cd;
   }
   DeviceGuard guard(X.device());
@@ -1225,7 +1226,7 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(b!)? mind=None, Tensor(c!)? mind2=None, Tensor(d!)? xh=None, Tensor(e!)? xmax=None, "
         "Tensor? m_dev=None, Tensor? a_prev=None, Tensor? tol=None, Tensor(f!)? u=None, "
         "Tensor(g!)? l=None, Tensor(h!)? changed=None, Tensor(i!)? n_changed=None, "
-        "Tensor(j!)? chg_new=None, Tensor(l!)? chg_old=None) -> ()");
+        "Tensor(j!)? chg_new=None, Tensor(l!)? chg_old=None, int cand_extend=1) -> ()");
   m.def("kmeans_bounds_init(Tensor mind, Tensor mind2, Tensor xmax, int n, Tensor(a!) u, "
         "Tensor(b!) l, Tensor(c!) tol) -> ()");
   m.def("kmeans_update(Tensor(a!) C, Tensor S, Tensor cnt, Tensor(b!) Cq, Tensor(c!) hn, "

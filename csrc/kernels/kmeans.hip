@@ -312,6 +312,7 @@ struct KmAux {
   const float* hnb;                   // [k][kpad]: 0.5|c|^2 in neighbour order of centre a
   const int32_t* nb;                  // [k][kpad]: their ids
   const float* nd;                    // [k][kpad]: |c - c_a| rounded down, ascending
+  int extend;                         // CAND: stream more chunks where l would be loose
 };
 constexpr int kChgBuf = 512;          // changed rows buffered per block (LDS)
 
@@ -722,7 +723,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     }
     if (NBUF >= 3 && ch + NBUF - 1 < nch_t) issue(ch + NBUF - 1);
     if constexpr (CAND) {
-      if (ch == nch_t - 1 && nch_t < nchunk) {
+      if (aux.extend && ch == nch_t - 1 && nch_t < nchunk) {
         // The pruned centres bound l from below by nd_first - ua only. Where that is below
         // a point's second-best distance so far, its l (and the next iteration's filter)
         // would be loose: then the tile streams one more chunk (block-uniform decision)
@@ -1560,7 +1561,7 @@ hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP
       // idx = the active rows sorted by cluster (dalgo_kmeans_sort_active)
       aux.tiles = reinterpret_cast<const int4*>(cand->tiles);
       aux.n_tiles = cand->n_tiles; aux.hnb = cand->hnb;
-      aux.nb = cand->nb; aux.nd = cand->nd;
+      aux.nb = cand->nb; aux.nd = cand->nd; aux.extend = cand->extend;
       if (DP == 128)
         return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true, true, true>(
             X, m, ldx, Cq, hn, kpad, assign, nullptr, sse, sse_mask, st, idx, nullptr, aux);

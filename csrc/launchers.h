@@ -47,6 +47,7 @@ struct DalgoKmCand {
   const float* hnb;
   const int32_t* nb;
   const float* nd;
+  int extend;                         // stream extra chunks for tight lower bounds
 };
 
 extern "C" {

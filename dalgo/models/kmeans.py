@@ -127,6 +127,7 @@ class KMeans:
         self._a_prev = torch.empty(max(n, 1), **i32)
         self._idx = torch.empty(max(n, 1), **i32)
         self._n_active = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self._just_full = False                       # last iteration was the full pass
         self._Q = torch.zeros(k, dtype=torch.float64, device=self.dev)
         self._cq_prev = torch.empty((k, self.DP), dtype=self.cen.Cq.dtype, device=self.dev)
         self._delta = torch.empty(k, **f32)
@@ -224,6 +225,7 @@ class KMeans:
             self._record(0, n)
             self._record(1, 0)
             self._first = False
+            self._just_full = True
         else:
             cw = self._cand
             with self._ph("centres"):
@@ -241,8 +243,12 @@ class KMeans:
             with self._ph("assign"):
                 # K2 over the active rows; its epilogue updates u / l and collects the
                 # rows whose cluster changed
+                # no chunk extension right after the full pass: the first centre shifts
+                # are so large that the next filter never decides on l (the same active
+                # rows either way, profiles/round4/r4_13), so tight l there is pure cost
                 K.assign_rows(self.X, self.cen, cw.rows if cw is not None else self._idx, n,
-                              self.assign, post=self._post_args, cand=cw)
+                              self.assign, post=self._post_args, cand=cw,
+                              extend=not self._just_full)
             with self._ph("accumulate_incremental"):
                 K.move_rows(self.X, self.DP, self._changed, self._n_changed, self.assign,
                             self._a_prev, self._S64, self._cnt64, self._mws, self._xh, self._Q,
@@ -251,6 +257,7 @@ class KMeans:
                 self.cnt.copy_(self._cnt64)
             self._record(0, self._n_active)
             self._record(1, self._n_changed)
+            self._just_full = False
         self._hist_n += 1
         # local SSE on the (rounded) centres of this assignment
         Cd = self.cen.Cq[:k, :d].double()

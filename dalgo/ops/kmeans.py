@@ -288,7 +288,7 @@ def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
                 assign: torch.Tensor, mind: torch.Tensor | None = None,
                 mind2: torch.Tensor | None = None, xh: torch.Tensor | None = None,
                 xmax: torch.Tensor | None = None, post: dict | None = None,
-                cand: CandWorkspace | None = None):
+                cand: CandWorkspace | None = None, extend: bool = True):
     """K2 (pipelined form) over the rows idx[:m] (all rows when idx is None).
 
     Full pass: assign / mind (and the second-best distance mind2, a lower bound, when
@@ -302,7 +302,8 @@ def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
     candidate-pruned form -- a tile of cluster a streams only the chunks of a's
     neighbour list within 2 max(ua) of c_a (ua = the tile's distances to c_a, computed in
     the tile prologue and rounded up); the pruned centres enter the new lower bound as
-    nd_first - ua."""
+    nd_first - ua. ``extend``: where that bound would be looser than a point's second
+    best, the tile streams more chunks (tight l for the next filter)."""
     if post is None:
         _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, [], mind, mind2, xh,
                                      xmax)
@@ -311,7 +312,7 @@ def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
                                  cand.cand() if cand is not None else [], None, None, None, None,
                                  post["m_dev"], post.get("a_prev"), post["tol"], post["u"],
                                  post["l"], post["changed"], post["n_changed"],
-                                 post.get("chg_new"), post.get("chg_old"))
+                                 post.get("chg_new"), post.get("chg_old"), int(bool(extend)))
 
 
 def bounds_init(mind: torch.Tensor, mind2: torch.Tensor, xmax: torch.Tensor, n: int,
