@@ -38,7 +38,7 @@ def lower_bound_quality(X_, cen, idx, post):
         rr = r[s0:s0 + (1 << 18)]
         D = torch.cdist(X_[rr, :128].float(), cen.Cq[:k, :128].float())
         two = torch.topk(D, 2, dim=1, largest=False).values
-        ratios.append(post["l"][rr] / two[:, 1].clamp_min(1e-6))
+        ratios.append(post["ul"][rr, 1] / two[:, 1].clamp_min(1e-6))
     q = torch.cat(ratios)
     return dict(l_over_second_best_mean=float(q.mean()), l_lt_90pct=float((q < 0.9).float().mean()))
 

@@ -55,9 +55,12 @@ def probe(X_, cen, idx, m, assign, *args, post=None, cand=None, **kw):
                 assign.copy_(asg)
                 post["n_changed"].zero_()
             idx_f = km._idx
+            # the Hamerly-only form reads the previous clusters (the candidate form knows
+            # them from its tile's cluster): the snapshot of assign is that
+            post_h = dict(post, a_prev=asg, chg_new=None, chg_old=None)
             runs = {
-                "hamerly_filter_order": lambda: orig(X_, cen, idx_f, m, assign, post=post),
-                "hamerly_sorted_order": lambda: orig(X_, cen, cand.rows, m, assign, post=post),
+                "hamerly_filter_order": lambda: orig(X_, cen, idx_f, m, assign, post=post_h),
+                "hamerly_sorted_order": lambda: orig(X_, cen, cand.rows, m, assign, post=post_h),
                 "candidates": lambda: orig(X_, cen, cand.rows, m, assign, post=post, cand=cand),
             }
             for name, fn in runs.items():

@@ -476,14 +476,19 @@ void kmeans_move_sorted(const Tensor& X, int64_t DP, const Tensor& changed, int6
 }
 
 // bound-filtered Lloyd: active rows (u + delta[a] >= s[a]) -> idx, their assignment -> a_prev
-void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta, const Tensor& s,
+// ul [n][2] f32: the Hamerly bounds (u, l) of a row, stored as one 8-byte pair
+static void check_ul(const Tensor& ul, int64_t n, const char* what) {
+  check_f32(ul, what);
+  TORCH_CHECK(ul.dim() == 2 && ul.size(1) == 2 && ul.is_contiguous() && ul.size(0) >= n,
+              what, ": ul must be a contiguous [n, 2] float32 tensor");
+}
+
+void kmeans_filter(const Tensor& assign, Tensor ul, const Tensor& delta, const Tensor& s,
                    const std::optional<Tensor>& a_prev, Tensor idx, Tensor n_active,
                    const std::optional<Tensor>& acl) {
   const int64_t n = assign.numel();
   check_i32(assign, "assign");
-  check_f32(u, "u");
-  check_f32(l, "l");
-  TORCH_CHECK(l.numel() >= n, "kmeans_filter: l [n]");
+  check_ul(ul, n, "kmeans_filter");
   check_f32(delta, "delta");
   check_f32(s, "s");
   int32_t* app = nullptr;
@@ -493,7 +498,7 @@ void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta
     app = a_prev->data_ptr<int32_t>();
   }
   check_i32(idx, "idx");
-  TORCH_CHECK(u.numel() >= n && idx.numel() >= n, "kmeans_filter sizes");
+  TORCH_CHECK(idx.numel() >= n, "kmeans_filter sizes");
   TORCH_CHECK(delta.numel() == s.numel(), "delta / s [k]");
   TORCH_CHECK(n_active.scalar_type() == at::kLong && n_active.numel() >= 1, "n_active int64[1]");
   int32_t* aclp = nullptr;
@@ -503,7 +508,7 @@ void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta
     aclp = acl->data_ptr<int32_t>();
   }
   DeviceGuard guard(assign.device());
-  DALGO_CHECK_HIP(dalgo_km_filter(assign.data_ptr<int32_t>(), u.data_ptr<float>(), l.data_ptr<float>(),
+  DALGO_CHECK_HIP(dalgo_km_filter(assign.data_ptr<int32_t>(), ul.data_ptr<float>(),
                                   delta.data_ptr<float>(), s.data_ptr<float>(), (int)delta.numel(), n,
                                   app, idx.data_ptr<int32_t>(),
                                   reinterpret_cast<unsigned long long*>(n_active.data_ptr<int64_t>()),
@@ -513,18 +518,19 @@ void kmeans_filter(const Tensor& assign, Tensor u, Tensor l, const Tensor& delta
 
 // bounds after the full first pass (u, l from the K2 distances; tol from the K2 max)
 void kmeans_bounds_init(const Tensor& mind, const Tensor& mind2, const Tensor& xmax, int64_t n,
-                        Tensor u, Tensor l, Tensor tol) {
-  for (const Tensor* t : std::initializer_list<const Tensor*>{&mind, &mind2, &u, &l}) {
+                        Tensor ul, Tensor tol) {
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&mind, &mind2}) {
     check_f32(*t, "bounds");
     TORCH_CHECK(t->numel() >= n, "bounds [n]");
   }
+  check_ul(ul, n, "kmeans_bounds_init");
   check_f32(tol, "tol");
   check_dev(xmax, "xmax");
   TORCH_CHECK(xmax.scalar_type() == at::kInt && xmax.numel() >= 1, "xmax int32[1]");
   DeviceGuard guard(mind.device());
   DALGO_CHECK_HIP(dalgo_km_bounds_init(mind.data_ptr<float>(), mind2.data_ptr<float>(),
                                        reinterpret_cast<const unsigned*>(xmax.data_ptr<int32_t>()), n,
-                                       u.data_ptr<float>(), l.data_ptr<float>(), tol.data_ptr<float>(),
+                                       ul.data_ptr<float>(), tol.data_ptr<float>(),
                                        cur_stream()),
                   "kmeans_bounds_init");
 }
@@ -569,8 +575,8 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
                        const std::optional<Tensor>& mind, const std::optional<Tensor>& mind2,
                        const std::optional<Tensor>& xh, const std::optional<Tensor>& xmax,
                        const std::optional<Tensor>& m_dev, const std::optional<Tensor>& a_prev,
-                       const std::optional<Tensor>& tol, const std::optional<Tensor>& u,
-                       const std::optional<Tensor>& l, const std::optional<Tensor>& changed,
+                       const std::optional<Tensor>& tol, const std::optional<Tensor>& ul,
+                       const std::optional<Tensor>& changed,
                        const std::optional<Tensor>& n_changed, const std::optional<Tensor>& chg_new,
                        const std::optional<Tensor>& chg_old, int64_t cand_extend) {
   TORCH_CHECK(Cq.dim() == 2 && Cq.is_contiguous() && Cq.scalar_type() == at::kBFloat16, "Cq bf16");
@@ -610,9 +616,9 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
   const DalgoKmPost* pp = nullptr;
   if (m_dev.has_value()) {   // filtered iteration: rows = *m_dev (device), m = its upper bound
     // a_prev: the previous clusters (the candidate form takes them from its tiles)
-    TORCH_CHECK((a_prev.has_value() || !cand.empty()) && tol.has_value() && u.has_value() &&
-                    l.has_value() && changed.has_value() && n_changed.has_value(),
-                "kmeans_assign_idx: the device-count form needs a_prev, tol, u, l, changed, n_changed");
+    TORCH_CHECK((a_prev.has_value() || !cand.empty()) && tol.has_value() && ul.has_value() &&
+                    changed.has_value() && n_changed.has_value(),
+                "kmeans_assign_idx: the device-count form needs a_prev, tol, ul, changed, n_changed");
     check_dev(*m_dev, "m_dev");
     TORCH_CHECK(m_dev->scalar_type() == at::kLong && m_dev->numel() >= 1, "m_dev int64[1]");
     if (a_prev.has_value()) {
@@ -635,8 +641,8 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
     check_dev(*n_changed, "n_changed");
     post.mcount = reinterpret_cast<const unsigned long long*>(m_dev->data_ptr<int64_t>());
     post.tol = tol->data_ptr<float>();
-    post.u = f32n(u, "u");
-    post.l = f32n(l, "l");
+    check_ul(*ul, X.size(0), "kmeans_assign_idx");
+    post.ul = ul->data_ptr<float>();
     post.changed = changed->data_ptr<int32_t>();
     post.n_changed = reinterpret_cast<unsigned long long*>(n_changed->data_ptr<int64_t>());
     post.cap = changed->numel();
@@ -1211,7 +1217,7 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(e!) cluster_start, Tensor(f!) seg_start, Tensor(g!) perm, Tensor(h!) ec, "
         "Tensor(i!) er, Tensor? m_dev=None, int chunk=65536, Tensor? cnew=None, "
         "Tensor? cold=None) -> ()");
-  m.def("kmeans_filter(Tensor assign, Tensor(a!) u, Tensor(e!) l, Tensor delta, Tensor s, "
+  m.def("kmeans_filter(Tensor assign, Tensor(a!) ul, Tensor delta, Tensor s, "
         "Tensor(b!)? a_prev, Tensor(c!) idx, Tensor(d!) n_active, Tensor(f!)? acl=None) -> ()");
   m.def("kmeans_sort_active(Tensor acl, Tensor idx, Tensor n_active, int k, int chunk, "
         "Tensor(a!) block_counts, Tensor(b!) cstart, Tensor(c!) seg_start, Tensor(d!) rows_sorted, "
@@ -1224,11 +1230,11 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("kmeans_assign_idx(Tensor X, Tensor Cq, Tensor hn, Tensor? idx, int m, Tensor(a!) assign, "
         "Tensor[] cand, "
         "Tensor(b!)? mind=None, Tensor(c!)? mind2=None, Tensor(d!)? xh=None, Tensor(e!)? xmax=None, "
-        "Tensor? m_dev=None, Tensor? a_prev=None, Tensor? tol=None, Tensor(f!)? u=None, "
-        "Tensor(g!)? l=None, Tensor(h!)? changed=None, Tensor(i!)? n_changed=None, "
+        "Tensor? m_dev=None, Tensor? a_prev=None, Tensor? tol=None, Tensor(f!)? ul=None, "
+        "Tensor(h!)? changed=None, Tensor(i!)? n_changed=None, "
         "Tensor(j!)? chg_new=None, Tensor(l!)? chg_old=None, int cand_extend=1) -> ()");
-  m.def("kmeans_bounds_init(Tensor mind, Tensor mind2, Tensor xmax, int n, Tensor(a!) u, "
-        "Tensor(b!) l, Tensor(c!) tol) -> ()");
+  m.def("kmeans_bounds_init(Tensor mind, Tensor mind2, Tensor xmax, int n, Tensor(a!) ul, "
+        "Tensor(c!) tol) -> ()");
   m.def("kmeans_update(Tensor(a!) C, Tensor S, Tensor cnt, Tensor(b!) Cq, Tensor(c!) hn, "
         "Tensor(d!)? shift2) -> ()");
   m.def("rmat_edges(int seed, int scale, int e_off, float a, float b, float c, bool scramble, "

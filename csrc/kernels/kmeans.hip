@@ -297,8 +297,8 @@ struct KmAux {
   unsigned* xmax;                     // full pass: max 0.5|x|^2 (float bits)
   const int* a_prev;                  // LOOP: cluster before this iteration
   const float* tol;                   // LOOP: slack of a kernel distance
-  float* u;                           // LOOP: upper bound of the distance to the centre
-  float* l;                           // LOOP: lower bound of every other distance
+  float2* ul;                         // LOOP: (u, l) per row: upper bound of the distance
+                                      //       to the centre, lower bound of every other
   int* changed;                       // LOOP: rows whose cluster changed ...
   unsigned long long* n_changed;      //       ... and their number
   long long cap;                      //       capacity of `changed`
@@ -794,18 +794,21 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       // acc = 0.5|x-c|^2 + M - 0.5|x|^2
       const float dist = fmaxf(2.f * (bv - M) + x2[t], 0.f);
       row = idx ? (int64_t)idx[p] : p;
-      assign[row] = bi;
       if constexpr (LOOP) {
         const float dist2 = fmaxf(2.f * (bv2 - M) + x2[t], 0.f);
-        aux.u[row] = km_up1(sqrtf(km_up1(dist + tol)));
         float lo2 = km_dn1(sqrtf(fmaxf(km_dn1(dist2 - tol), 0.f)));
         // CAND: every pruned centre is >= nd_first - |x - c_acl| from x
         if constexpr (CAND) lo2 = fminf(lo2, km_dn1(nd_first - ua[t]));
-        aux.l[row] = fmaxf(lo2, 0.f);
+        // the rows are scattered over X, so each store is a separate partial line write
+        // (the kernel's largest cost after the MFMAs): u and l go out as one 8-byte pair,
+        // and assign only where the cluster changed (assign[row] holds old_c otherwise)
+        aux.ul[row] = make_float2(km_up1(sqrtf(km_up1(dist + tol))), fmaxf(lo2, 0.f));
         // CAND: the tile's rows were sorted by their previous cluster, acl
         old_c = CAND ? acl : aux.a_prev[row];
         chg = bi != old_c;
+        if (chg) assign[row] = bi;
       } else {
+        assign[row] = bi;
         if (mind) mind[row] = dist;
         if constexpr (TOP2) mind2[row] = fmaxf(2.f * (bv2 - M) + x2[t], 0.f);
         if (aux.xh) aux.xh[row] = 0.5f * x2[t];
@@ -1347,7 +1350,7 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
   if (grid == 0) return hipSuccess;
   if ((aux.mcount != nullptr) != LOOP) return hipErrorInvalidValue;
   // a_prev: the Hamerly-only form's previous clusters (the candidate form has them per tile)
-  if (LOOP && (aux.tol == nullptr || aux.u == nullptr || aux.l == nullptr ||
+  if (LOOP && (aux.tol == nullptr || aux.ul == nullptr ||
                (!CAND && aux.a_prev == nullptr) || aux.changed == nullptr ||
                aux.n_changed == nullptr))
     return hipErrorInvalidValue;
@@ -1552,8 +1555,8 @@ hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP
   aux.xmax = xmax;
   if (cand != nullptr && post == nullptr) return hipErrorInvalidValue;
   if (post != nullptr) {
-    aux.mcount = post->mcount; aux.a_prev = post->a_prev; aux.tol = post->tol; aux.u = post->u;
-    aux.l = post->l; aux.changed = post->changed; aux.n_changed = post->n_changed;
+    aux.mcount = post->mcount; aux.a_prev = post->a_prev; aux.tol = post->tol;
+    aux.ul = reinterpret_cast<float2*>(post->ul); aux.changed = post->changed; aux.n_changed = post->n_changed;
     aux.cap = post->cap; aux.chg_new = post->chg_new; aux.chg_old = post->chg_old;
     if ((aux.chg_new == nullptr) != (aux.chg_old == nullptr)) return hipErrorInvalidValue;
     if (cand == nullptr && aux.a_prev == nullptr) return hipErrorInvalidValue;

@@ -97,7 +97,7 @@ km_diff_kernel(const int32_t* __restrict__ a_new, const int32_t* __restrict__ a_
 // maxd = max over the k centre shifts, reduced by every block from delta (k floats from
 // L2: cheaper than a separate reduction launch).
 __global__ void __launch_bounds__(kDiffThreads)
-km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, float* __restrict__ l,
+km_filter_kernel(const int32_t* __restrict__ assign, float2* __restrict__ ul,
                  const float* __restrict__ delta, const float* __restrict__ s, int k, int64_t n,
                  int32_t* __restrict__ a_prev, int32_t* __restrict__ idx,
                  unsigned long long* __restrict__ n_active, int64_t cap,
@@ -146,8 +146,9 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, floa
       const int64_t i = base + threadIdx.x + (int64_t)kDiffThreads * e;
       const bool in = i < hi;
       a[e] = in ? assign[i] : 0;
-      uu[e] = in ? u[i] : 0.f;
-      ll[e] = in ? l[i] : 0.f;
+      const float2 b = in ? ul[i] : make_float2(0.f, 0.f);
+      uu[e] = b.x;
+      ll[e] = b.y;
     }
     // bounds rounded outward (u up, l down): a skipped point's bounds stay valid over any
     // number of consecutive skipped iterations, independent of the f32 rounding of u / l
@@ -164,8 +165,7 @@ km_filter_kernel(const int32_t* __restrict__ assign, float* __restrict__ u, floa
       const bool in = i < hi;
       const bool act = in && !(ub[e] < bound[e]);
       if (in && !act) {
-        u[i] = ub[e];
-        l[i] = lb[e];
+        ul[i] = make_float2(ub[e], lb[e]);
       } else if (act && a_prev) {
         a_prev[i] = a[e];
       }
@@ -346,14 +346,14 @@ km_centre_nbrs_kernel(const uint16_t* __restrict__ cq, const uint16_t* __restric
 // u = sqrt(dist + tol) rounded up, l = sqrt(dist2 - tol) rounded down. One pass.
 __global__ void __launch_bounds__(256)
 km_bounds_init_kernel(const float* __restrict__ mind, const float* __restrict__ mind2,
-                      const unsigned* __restrict__ xmax, int64_t n, float* __restrict__ u,
-                      float* __restrict__ l, float* __restrict__ tol_out) {
+                      const unsigned* __restrict__ xmax, int64_t n, float2* __restrict__ ul,
+                      float* __restrict__ tol_out) {
   const float M = __uint_as_float(*xmax) * 1.0001f + 1e-6f;
   const float tol = up1(2.f * M * 6.103515625e-05f);   // 2^-14
   if (blockIdx.x == 0 && threadIdx.x == 0) *tol_out = tol;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    u[i] = up1(sqrtf(up1(fmaxf(mind[i], 0.f) + tol)));
-    l[i] = fmaxf(dn1(sqrtf(fmaxf(dn1(mind2[i] - tol), 0.f))), 0.f);
+    ul[i] = make_float2(up1(sqrtf(up1(fmaxf(mind[i], 0.f) + tol))),
+                        fmaxf(dn1(sqrtf(fmaxf(dn1(mind2[i] - tol), 0.f))), 0.f));
   }
 }
 
@@ -372,7 +372,7 @@ hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, 
   return hipGetLastError();
 }
 
-hipError_t dalgo_km_filter(const int32_t* assign, float* u, float* l, const float* delta,
+hipError_t dalgo_km_filter(const int32_t* assign, float* ul, const float* delta,
                            const float* s, int k, int64_t n, int32_t* a_prev, int32_t* idx,
                            unsigned long long* n_active, int64_t cap, int32_t* acl,
                            hipStream_t st) {
@@ -380,17 +380,17 @@ hipError_t dalgo_km_filter(const int32_t* assign, float* u, float* l, const floa
   int64_t g = (n + dalgo::kDiffThreads - 1) / dalgo::kDiffThreads;
   if (g > 2048) g = 2048;
   hipLaunchKernelGGL(dalgo::km_filter_kernel, dim3((unsigned)g), dim3(dalgo::kDiffThreads), 0, st,
-                     assign, u, l, delta, s, k, n, a_prev, idx, n_active, cap, acl);
+                     assign, reinterpret_cast<float2*>(ul), delta, s, k, n, a_prev, idx, n_active, cap, acl);
   return hipGetLastError();
 }
 
 hipError_t dalgo_km_bounds_init(const float* mind, const float* mind2, const unsigned* xmax,
-                                int64_t n, float* u, float* l, float* tol, hipStream_t st) {
+                                int64_t n, float* ul, float* tol, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   int64_t g = (n + 255) / 256;
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(dalgo::km_bounds_init_kernel, dim3((unsigned)g), dim3(256), 0, st, mind, mind2,
-                     xmax, n, u, l, tol);
+                     xmax, n, reinterpret_cast<float2*>(ul), tol);
   return hipGetLastError();
 }
 

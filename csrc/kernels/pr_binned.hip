@@ -42,6 +42,7 @@
 #include "dalgo/common.h"
 #include "launchers.h"   // the extern "C" entry point is checked against its declaration
 #include <algorithm>
+#include <type_traits>
 
 namespace dalgo {
 
@@ -167,101 +168,111 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
       const int64_t idx = e0 + EPL * lane;
       const int4 wc = wq[q];
       wq[q] = load(idx + (int64_t)D * 64 * EPL);
-      const uint32_t ww[4] = {(uint32_t)wc.x, (uint32_t)wc.y, (uint32_t)wc.z, (uint32_t)wc.w};
-      uint32_t hk[EPL];
-      float cv[EPL];
-      // the lane's edges idx + k inside [e_lo, e_hi): k in [klo, klo + span), one 32-bit
-      // compare per edge instead of two 64-bit ones
-      const int klo = (int)min(max(e_lo - idx, (int64_t)0), (int64_t)EPL);
-      const int span = max((int)min(max(e_hi - idx, (int64_t)0), (int64_t)EPL) - klo, 0);
-      bool inr[EPL];
-#pragma unroll
-      for (int k = 0; k < EPL; ++k) {
-        inr[k] = (uint32_t)(k - klo) < (uint32_t)span;
-        const uint32_t h = (ww[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-        hk[k] = inr[k] ? h : 0u;
-        cv[k] = s_c[hk[k] & (S - 1)];
-      }
-      float part = -0.0f, outv[EPL];
-      int nf = 0, nm = 0;
-      int rk[EPL];                                       // markers so far (inclusive)
-#pragma unroll
-      for (int k = 0; k < EPL; ++k) {
-        const bool in = inr[k];
-        part += in ? cv[k] : -0.0f;
-        outv[k] = part;
-        const bool f = hk[k] & 0x8000u;
-        nm += (f && (hk[k] & 0x4000u)) ? 1 : 0;
-        rk[k] = nm;
-        if (f) part = -0.0f;
-        nf += f ? 1 : 0;
-      }
-      // inclusive scans over the 64 lanes (DPP: rows of 16, then row broadcasts)
-      float a = part;
-      int hh = nf > 0, cnt = nf, cm = nm;
-      scan_step<0x111>(a, hh, cnt, cm);          // row_shr:1
-      scan_step<0x112>(a, hh, cnt, cm);          // row_shr:2
-      scan_step<0x114>(a, hh, cnt, cm);          // row_shr:4
-      scan_step<0x118>(a, hh, cnt, cm);          // row_shr:8
-      scan_step<0x142, 0xa>(a, hh, cnt, cm);     // row_bcast:15 -> rows 1, 3
-      scan_step<0x143, 0xc>(a, hh, cnt, cm);     // row_bcast:31 -> rows 2, 3
-      // exclusive segment sum for this lane (wave_shr:1), joined with the step carry
-      const float a_ex = dpp_mov_f<0x138>(-0.0f, a);
-      const int h_ex = dpp_mov_i<0x138>(0, hh);
-      const float carry_in = h_ex ? a_ex : carry + a_ex;
-      const int rbase = run + cm - nm - 1;       // run of this lane's first entries
-      // run deltas of the lane's entries: its 8 edges touch at most nm + 1 runs and nearly
-      // always <= 2 (a run is one (chunk, 16K-destination bin) group: hundreds of edges),
-      // so two reads and a select, with all 8 reads only in a step where some lane spans
-      // three runs (wave-uniform branch; LDS reads: no vmcnt bookkeeping involved)
-      int dl[EPL];
-      if (__ballot(nm >= 2) == 0ull) {
-        const int d0 = dsrc[max(rbase, 0)];
-        const int d1 = dsrc[max(min(rbase + 1, nr - 1), 0)];
-#pragma unroll
-        for (int k = 0; k < EPL; ++k) dl[k] = rk[k] == 0 ? d0 : d1;
-      } else {
-#pragma unroll
-        for (int k = 0; k < EPL; ++k) dl[k] = dsrc[max(rbase + rk[k], 0)];
-      }
-      int j = cnt - nf;                          // this lane's first entry of the step
-      bool first = true;
-#pragma unroll
-      for (int k = 0; k < EPL; ++k) {
-        if (hk[k] & 0x8000u) {
-          sv[j] = first ? carry_in + outv[k] : outv[k];
-          sp[j] = (int32_t)(ent + j + dl[k]);
-          first = false;
-          ++j;
+      // a step whose 512 edges all lie inside the tile (all but the first and last of a
+      // tile: wave-uniform) drops the per-edge in-range selects
+      const bool full = e0 >= e_lo && e0 + 64 * EPL <= e_hi;
+      auto step = [&](auto full_c) {
+        constexpr bool FULL = decltype(full_c)::value;
+        const uint32_t ww[4] = {(uint32_t)wc.x, (uint32_t)wc.y, (uint32_t)wc.z, (uint32_t)wc.w};
+        uint32_t hk[EPL];
+        float cv[EPL];
+        // the lane's edges idx + k inside [e_lo, e_hi): k in [klo, klo + span), one 32-bit
+        // compare per edge instead of two 64-bit ones
+        int klo = 0, span = EPL;
+        if constexpr (!FULL) {
+          klo = (int)min(max(e_lo - idx, (int64_t)0), (int64_t)EPL);
+          span = max((int)min(max(e_hi - idx, (int64_t)0), (int64_t)EPL) - klo, 0);
         }
-      }
-      const float a63 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a), 63));
-      const int h63 = __builtin_amdgcn_readlane(hh, 63);
-      const int n_step = __builtin_amdgcn_readlane(cnt, 63);
-      carry = h63 ? a63 : carry + a63;
-      ent += n_step;
-      run += __builtin_amdgcn_readlane(cm, 63);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // EPL unconditional stores per lane (lanes past n_step write this wave's own dummy
-      // line group, so no single address is hammered by every wave): a fixed store count
-      // keeps the compiler's vmcnt bookkeeping exact, so the D prefetched loads are not
-      // drained at every step
-      // staged values read unconditionally (every slot is in range), all before the first
-      // store: one LDS round trip per step instead of one per store
-      int32_t pq[EPL];
-      float vq[EPL];
+        bool inr[EPL];
 #pragma unroll
-      for (int q = 0; q < EPL; ++q) {
-        pq[q] = sp[lane + 64 * q];
-        vq[q] = sv[lane + 64 * q];
-      }
+        for (int k = 0; k < EPL; ++k) {
+          inr[k] = FULL || (uint32_t)(k - klo) < (uint32_t)span;
+          const uint32_t h = (ww[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+          hk[k] = inr[k] ? h : 0u;
+          cv[k] = s_c[hk[k] & (S - 1)];
+        }
+        float part = -0.0f, outv[EPL];
+        int nf = 0, nm = 0;
+        int rk[EPL];                                       // markers so far (inclusive)
 #pragma unroll
-      for (int q = 0; q < EPL; ++q) {
-        const bool ok = lane + 64 * q < n_step;
-        val[ok ? (int64_t)pq[q] : dummy] = ok ? vq[q] : 0.f;
-      }
+        for (int k = 0; k < EPL; ++k) {
+          const bool in = inr[k];
+          part += in ? cv[k] : -0.0f;
+          outv[k] = part;
+          const bool f = hk[k] & 0x8000u;
+          nm += (f && (hk[k] & 0x4000u)) ? 1 : 0;
+          rk[k] = nm;
+          if (f) part = -0.0f;
+          nf += f ? 1 : 0;
+        }
+        // inclusive scans over the 64 lanes (DPP: rows of 16, then row broadcasts)
+        float a = part;
+        int hh = nf > 0, cnt = nf, cm = nm;
+        scan_step<0x111>(a, hh, cnt, cm);          // row_shr:1
+        scan_step<0x112>(a, hh, cnt, cm);          // row_shr:2
+        scan_step<0x114>(a, hh, cnt, cm);          // row_shr:4
+        scan_step<0x118>(a, hh, cnt, cm);          // row_shr:8
+        scan_step<0x142, 0xa>(a, hh, cnt, cm);     // row_bcast:15 -> rows 1, 3
+        scan_step<0x143, 0xc>(a, hh, cnt, cm);     // row_bcast:31 -> rows 2, 3
+        // exclusive segment sum for this lane (wave_shr:1), joined with the step carry
+        const float a_ex = dpp_mov_f<0x138>(-0.0f, a);
+        const int h_ex = dpp_mov_i<0x138>(0, hh);
+        const float carry_in = h_ex ? a_ex : carry + a_ex;
+        const int rbase = run + cm - nm - 1;       // run of this lane's first entries
+        // run deltas of the lane's entries: its 8 edges touch at most nm + 1 runs and nearly
+        // always <= 2 (a run is one (chunk, 16K-destination bin) group: hundreds of edges),
+        // so two reads and a select, with all 8 reads only in a step where some lane spans
+        // three runs (wave-uniform branch; LDS reads: no vmcnt bookkeeping involved)
+        int dl[EPL];
+        if (__ballot(nm >= 2) == 0ull) {
+          const int d0 = dsrc[max(rbase, 0)];
+          const int d1 = dsrc[max(min(rbase + 1, nr - 1), 0)];
+#pragma unroll
+          for (int k = 0; k < EPL; ++k) dl[k] = rk[k] == 0 ? d0 : d1;
+        } else {
+#pragma unroll
+          for (int k = 0; k < EPL; ++k) dl[k] = dsrc[max(rbase + rk[k], 0)];
+        }
+        int j = cnt - nf;                          // this lane's first entry of the step
+        bool first = true;
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) {
+          if (hk[k] & 0x8000u) {
+            sv[j] = first ? carry_in + outv[k] : outv[k];
+            sp[j] = (int32_t)(ent + j + dl[k]);
+            first = false;
+            ++j;
+          }
+        }
+        const float a63 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a), 63));
+        const int h63 = __builtin_amdgcn_readlane(hh, 63);
+        const int n_step = __builtin_amdgcn_readlane(cnt, 63);
+        carry = h63 ? a63 : carry + a63;
+        ent += n_step;
+        run += __builtin_amdgcn_readlane(cm, 63);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // EPL unconditional stores per lane (lanes past n_step write this wave's own dummy
+        // line group, so no single address is hammered by every wave): a fixed store count
+        // keeps the compiler's vmcnt bookkeeping exact, so the D prefetched loads are not
+        // drained at every step
+        // staged values read unconditionally (every slot is in range), all before the first
+        // store: one LDS round trip per step instead of one per store
+        int32_t pq[EPL];
+        float vq[EPL];
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+          pq[q] = sp[lane + 64 * q];
+          vq[q] = sv[lane + 64 * q];
+        }
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+          const bool ok = lane + 64 * q < n_step;
+          val[ok ? (int64_t)pq[q] : dummy] = ok ? vq[q] : 0.f;
+        }
+      };
+      if (full) step(std::true_type{}); else step(std::false_type{});
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -31,8 +31,7 @@ struct DalgoKmPost {
   const unsigned long long* mcount;   // active rows (device, written by km_filter)
   const int* a_prev;                  // their cluster before this iteration
   const float* tol;                   // distance slack (device)
-  float* u;
-  float* l;
+  float* ul;                          // [n][2]: (u, l) per row
   int* changed;
   unsigned long long* n_changed;      // zeroed by the caller
   long long cap;
@@ -132,7 +131,7 @@ hipError_t dalgo_pr_update(const float* acc, const int32_t* pres, const int32_t*
 // ---- K3 incremental form (kmeans_inc.hip)
 hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, int32_t* changed,
                          unsigned long long* n_changed, int64_t cap, hipStream_t st);
-hipError_t dalgo_km_filter(const int32_t* assign, float* u, float* l, const float* delta,
+hipError_t dalgo_km_filter(const int32_t* assign, float* ul, const float* delta,
                            const float* s, int k, int64_t n, int32_t* a_prev, int32_t* idx,
                            unsigned long long* n_active, int64_t cap, int32_t* acl,
                            hipStream_t st);
@@ -155,7 +154,7 @@ hipError_t dalgo_km_centre_nbrs(const void* cq, const void* cprev, const float* 
                                 int d, int DP, float* delta, float* s, float* nd, int32_t* nb,
                                 float* hnb, hipStream_t st);
 hipError_t dalgo_km_bounds_init(const float* mind, const float* mind2, const unsigned* xmax,
-                                int64_t n, float* u, float* l, float* tol, hipStream_t st);
+                                int64_t n, float* ul, float* tol, hipStream_t st);
 
 // ---- K9 sparse closure round on a device hash set (tc_sparse.hip)
 hipError_t dalgo_tcs_degree(const uint64_t* keys, int64_t d0, int64_t nd, const int64_t* in_ptr,

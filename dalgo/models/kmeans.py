@@ -120,8 +120,8 @@ class KMeans:
         self._xh = torch.empty(max(n, 1), **f32)     # 0.5 |x|^2 (written by the full pass)
         self._xmax = torch.zeros(1, **i32)            # max 0.5 |x|^2 (float bits)
         self._tol = torch.zeros(1, **f32)             # slack of a kernel distance (device)
-        self._u = torch.empty(max(n, 1), **f32)
-        self._l = torch.empty(max(n, 1), **f32)
+        # Hamerly bounds (u, l) per row as one 8-byte pair: K2 writes them at scattered rows
+        self._ul = torch.empty((max(n, 1), 2), **f32)
         self._mind = torch.empty(max(n, 1), **f32)
         self._mind2 = torch.empty(max(n, 1), **f32)
         self._a_prev = torch.empty(max(n, 1), **i32)
@@ -132,8 +132,8 @@ class KMeans:
         self._cq_prev = torch.empty((k, self.DP), dtype=self.cen.Cq.dtype, device=self.dev)
         self._delta = torch.empty(k, **f32)
         self._s = torch.empty(k, **f32)
-        self._post_args = dict(m_dev=self._n_active, a_prev=self._a_prev, tol=self._tol, u=self._u,
-                               l=self._l, changed=self._changed, n_changed=self._n_changed)
+        self._post_args = dict(m_dev=self._n_active, a_prev=self._a_prev, tol=self._tol, ul=self._ul,
+                               changed=self._changed, n_changed=self._n_changed)
         # candidate pruning (Exponion-style at tile granularity): the active rows sorted by
         # cluster, every tile's centre stream cut to a prefix of its centre's neighbour list
         self._cand = (K.CandWorkspace(self.dev, n, k, self.cen.Cq.shape[0], self.DP)
@@ -221,7 +221,7 @@ class KMeans:
                 K.cluster_sq_sums(self.assign, self._xh, k, self._Q)
             # u / l from the K2 distances, tol = 2 M 2^-14 from the K2 max of 0.5|x|^2
             K.bounds_init(self._mind, self._mind if self._cand is not None else self._mind2,
-                          self._xmax, n, self._u, self._l, self._tol)
+                          self._xmax, n, self._ul, self._tol)
             self._record(0, n)
             self._record(1, 0)
             self._first = False
@@ -234,7 +234,7 @@ class KMeans:
                 else:
                     K.centre_bounds(self.cen.Cq, self._cq_prev, k, d, self._delta, self._s)
             with self._ph("filter"):
-                K.filter_rows(self.assign, self._u, self._l, self._delta, self._s,
+                K.filter_rows(self.assign, self._ul, self._delta, self._s,
                               self._a_prev if cw is None else None, self._idx, self._n_active,
                               cw.acl if cw is not None else None)
                 if cw is not None:

@@ -225,14 +225,14 @@ def centre_bounds(Cq_now: torch.Tensor, Cq_prev: torch.Tensor, k: int, d: int,
     return delta, s
 
 
-def filter_rows(assign: torch.Tensor, u: torch.Tensor, l: torch.Tensor, delta: torch.Tensor,
-                s: torch.Tensor, a_prev: torch.Tensor | None, idx: torch.Tensor,
+def filter_rows(assign: torch.Tensor, ul: torch.Tensor, delta: torch.Tensor, s: torch.Tensor, a_prev: torch.Tensor | None, idx: torch.Tensor,
                 n_active: torch.Tensor, acl: torch.Tensor | None = None) -> None:
     """Rows that may change cluster -> idx[:m] (their cluster -> a_prev[row] when given,
     and -> acl[:m] in list order when given), m -> n_active (device; no sync). The
-    largest centre shift is reduced from delta in the kernel."""
+    largest centre shift is reduced from delta in the kernel. ``ul`` [n, 2]: the Hamerly
+    bounds (u, l) per row (updated in place for the rows that are skipped)."""
     n_active.zero_()
-    _ext.ops().kmeans_filter(assign, u, l, delta, s, a_prev, idx, n_active, acl)
+    _ext.ops().kmeans_filter(assign, ul, delta, s, a_prev, idx, n_active, acl)
 
 
 # ------------------------------------------------- candidate-pruned K2 (filtered iterations)
@@ -293,11 +293,12 @@ def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
 
     Full pass: assign / mind (and the second-best distance mind2, a lower bound, when
     given) written at those rows; xh / xmax: also 0.5|x|^2 per row and its maximum
-    (float bits). ``post`` = dict(m_dev, a_prev, tol, u, l, changed, n_changed): the
+    (float bits). ``post`` = dict(m_dev, a_prev, tol, ul, changed, n_changed): the
     filtered-iteration form -- the row count is m_dev (device; m its upper bound) and
-    the epilogue writes the Hamerly bounds u / l (rounded outward, tol on the device)
-    and appends the rows whose cluster differs from a_prev to changed (count in
-    n_changed, which the caller zeroes): no host sync, no separate bound pass.
+    the epilogue writes the Hamerly bounds ul[row] = (u, l) (rounded outward, tol on the
+    device) and appends the rows whose cluster differs from a_prev to changed (count in
+    n_changed, which the caller zeroes): no host sync, no separate bound pass. In this
+    form assign must hold the previous clusters: only the changed rows are written.
     ``cand`` (with post; idx = cand.rows, the active rows sorted by cluster): the
     candidate-pruned form -- a tile of cluster a streams only the chunks of a's
     neighbour list within 2 max(ua) of c_a (ua = the tile's distances to c_a, computed in
@@ -310,16 +311,17 @@ def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
         return
     _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign,
                                  cand.cand() if cand is not None else [], None, None, None, None,
-                                 post["m_dev"], post.get("a_prev"), post["tol"], post["u"],
-                                 post["l"], post["changed"], post["n_changed"],
+                                 post["m_dev"], post.get("a_prev"), post["tol"], post["ul"],
+                                 post["changed"], post["n_changed"],
                                  post.get("chg_new"), post.get("chg_old"), int(bool(extend)))
 
 
 def bounds_init(mind: torch.Tensor, mind2: torch.Tensor, xmax: torch.Tensor, n: int,
-                u: torch.Tensor, l: torch.Tensor, tol: torch.Tensor):
-    """After the full first pass: tol = 2 M 2^-14 (M from the K2 max of 0.5|x|^2), u =
-    sqrt(dist + tol) rounded up, l = sqrt(dist2 - tol) rounded down (one launch)."""
-    _ext.ops().kmeans_bounds_init(mind, mind2, xmax, int(n), u, l, tol)
+                ul: torch.Tensor, tol: torch.Tensor):
+    """After the full first pass: tol = 2 M 2^-14 (M from the K2 max of 0.5|x|^2), ul =
+    (u, l) per row: u = sqrt(dist + tol) rounded up, l = sqrt(dist2 - tol) rounded down
+    (one launch)."""
+    _ext.ops().kmeans_bounds_init(mind, mind2, xmax, int(n), ul, tol)
 
 
 def cluster_sq_sums(assign: torch.Tensor, xh: torch.Tensor, k: int, Q: torch.Tensor):

@@ -705,8 +705,8 @@ def test_kmeans_filter_matches_torch(cuda):
     torch.manual_seed(6)
     n, k = 100_003, 50
     assign = torch.randint(0, k, (n,), dtype=torch.int32, device=cuda)
-    u = torch.rand(n, device=cuda) * 10
-    l = torch.rand(n, device=cuda) * 20
+    ul = torch.stack([torch.rand(n, device=cuda) * 10, torch.rand(n, device=cuda) * 20], 1)
+    u, l = ul[:, 0], ul[:, 1]                   # views: the kernel updates ul in place
     delta = torch.rand(k, device=cuda)
     s = torch.rand(k, device=cuda) * 12
     maxd = delta.max()
@@ -715,7 +715,7 @@ def test_kmeans_filter_matches_torch(cuda):
     idx = torch.empty(n, dtype=torch.int32, device=cuda)
     cnt = torch.zeros(1, dtype=torch.int64, device=cuda)
     acl = torch.full((n,), -1, dtype=torch.int32, device=cuda)
-    K.filter_rows(assign, u, l, delta, s, a_prev, idx, cnt, acl)
+    K.filter_rows(assign, ul, delta, s, a_prev, idx, cnt, acl)
     m = int(cnt.item())
     assert torch.equal(acl[:m], assign[idx[:m].long()])
     ub = u0 + delta[assign.long()]
@@ -776,10 +776,10 @@ def test_kmeans_assign_rows_fused_post(cuda):
     ref = 0.5 * X[:, :d].float().pow(2).sum(1)
     assert torch.allclose(xh, ref, rtol=1e-5)
     assert float(xmax.view(torch.float32).item()) == pytest.approx(float(ref.max()), rel=1e-5)
-    u0 = torch.empty(n, device=cuda)
-    l0 = torch.empty(n, device=cuda)
+    ul0 = torch.empty((n, 2), device=cuda)
+    u0, l0 = ul0[:, 0], ul0[:, 1]
     tol = torch.zeros(1, device=cuda)
-    K.bounds_init(mind, mind2, xmax, n, u0, l0, tol)
+    K.bounds_init(mind, mind2, xmax, n, ul0, tol)
     t = float(tol.item())
     assert t == pytest.approx(2 * (float(ref.max()) * 1.0001 + 1e-6) * 2 ** -14, rel=1e-5)
     assert bool((u0 >= torch.sqrt(mind + t)).all()) and bool((l0 <= torch.sqrt((mind2 - t).clamp_min(0))).all())
@@ -790,16 +790,17 @@ def test_kmeans_assign_rows_fused_post(cuda):
     flip = torch.zeros(n, dtype=torch.bool, device=cuda)
     flip[rows[: m // 3].long()] = True          # a third of the active rows "moved"
     a_prev[flip] = (a_prev[flip] + 1) % k
-    a = torch.full((n,), -7, dtype=torch.int32, device=cuda)
-    u = torch.full((n,), -1.0, device=cuda)
-    l = torch.full((n,), -1.0, device=cuda)
+    sel = torch.zeros(n, dtype=torch.bool, device=cuda)
+    sel[rows[:m].long()] = True
+    # assign holds the previous clusters of the active rows: only the changed ones are written
+    a = torch.where(sel, a_prev, torch.full_like(a_prev, -7))
+    ul = torch.full((n, 2), -1.0, device=cuda)
+    u, l = ul[:, 0], ul[:, 1]
     changed = torch.empty(n, dtype=torch.int32, device=cuda)
     nch = torch.zeros(1, dtype=torch.int64, device=cuda)
     K.assign_rows(X, cen, rows, n, a, post=dict(
-        m_dev=torch.tensor([m], dtype=torch.int64, device=cuda), a_prev=a_prev, tol=tol, u=u, l=l,
+        m_dev=torch.tensor([m], dtype=torch.int64, device=cuda), a_prev=a_prev, tol=tol, ul=ul,
         changed=changed, n_changed=nch))
-    sel = torch.zeros(n, dtype=torch.bool, device=cuda)
-    sel[rows[:m].long()] = True
     assert torch.equal(a[sel], full[sel]) and bool((a[~sel] == -7).all())
     assert bool((u[~sel] == -1).all()) and bool((l[~sel] == -1).all())
     dist = torch.cdist(X[:, :d].double(), cen.Cq[:k, :d].double())
@@ -942,10 +943,8 @@ def test_kmeans_assign_rows_candidates(cuda, d):
     mind2 = torch.zeros(n, device=cuda)
     xmax = torch.zeros(1, dtype=torch.int32, device=cuda)
     K.assign_rows(X, cen, None, n, a0, mind, mind2, xh=torch.zeros(n, device=cuda), xmax=xmax)
-    u0 = torch.empty(n, device=cuda)
-    l0 = torch.empty(n, device=cuda)
     tol = torch.zeros(1, device=cuda)
-    K.bounds_init(mind, mind2, xmax, n, u0, l0, tol)
+    K.bounds_init(mind, mind2, xmax, n, torch.empty((n, 2), device=cuda), tol)
     kpad, DP = cen.Cq.shape
     ws = K.CandWorkspace(cuda, n, k, kpad, DP)
     K.centre_nbrs(cen, cen.Cq[:k].clone(), torch.empty(k, device=cuda), torch.empty(k, device=cuda), ws)
@@ -958,21 +957,22 @@ def test_kmeans_assign_rows_candidates(cuda, d):
     flip[rows[: m // 3].long()] = True
     a_prev[flip] = (a_prev[flip] + 1) % k
     dprev = (X[:, :d].float() - cen.Cq[a_prev.long(), :d].float()).norm(dim=1)
-    u = dprev * 1.001 + 1e-3
-    l = torch.full((n,), -1.0, device=cuda)
+    ul = torch.stack([dprev * 1.001 + 1e-3, torch.full((n,), -1.0, device=cuda)], 1)
+    u, l = ul[:, 0], ul[:, 1]
     ws.acl[:m].copy_(a_prev[rows.long()])
     cnt = torch.tensor([m], dtype=torch.int64, device=cuda)
     K.sort_active(rows, cnt, ws)
-    a = torch.full((n,), -7, dtype=torch.int32, device=cuda)
+    sel = torch.zeros(n, dtype=torch.bool, device=cuda)
+    sel[rows.long()] = True
+    # assign holds the previous clusters of the active rows: only the changed ones are written
+    a = torch.where(sel, a_prev, torch.full_like(a_prev, -7))
     changed = torch.empty(n, dtype=torch.int32, device=cuda)
     cnew = torch.full((n,), -1, dtype=torch.int32, device=cuda)
     cold = torch.full((n,), -1, dtype=torch.int32, device=cuda)
     nch = torch.zeros(1, dtype=torch.int64, device=cuda)
     K.assign_rows(X, cen, ws.rows, n, a, post=dict(
-        m_dev=cnt, a_prev=None, tol=tol, u=u, l=l, changed=changed, n_changed=nch,
+        m_dev=cnt, a_prev=None, tol=tol, ul=ul, changed=changed, n_changed=nch,
         chg_new=cnew, chg_old=cold), cand=ws)
-    sel = torch.zeros(n, dtype=torch.bool, device=cuda)
-    sel[rows.long()] = True
     assert bool((a[~sel] == -7).all())
     dist = torch.cdist(X[:, :d].double(), cen.Cq[:k, :d].double())
     bad = sel & (a != full)
