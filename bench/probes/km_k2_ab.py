@@ -73,6 +73,13 @@ def probe(X_, cen, idx, m, assign, *args, post=None, cand=None, **kw):
             cand.nd.copy_(nd0)
             restore()
             res["restore_only"] = timed(restore)
+            # a standalone scatter of one 8-byte pair per active row (torch index_copy_)
+            ul = post["ul"]
+            src = torch.randn(n_act, 2, device=ul.device)
+            rl = cand.rows[:n_act].long()
+            res["scatter_pairs_torch"] = timed(lambda: ul.index_copy_(0, rl, src))
+            rs = torch.sort(rl).values
+            res["scatter_pairs_sorted_rows"] = timed(lambda: ul.index_copy_(0, rs, src))
             res["active"] = n_act
     return orig(X_, cen, idx, m, assign, *args, post=post, cand=cand, **kw)
 

@@ -319,6 +319,19 @@ constexpr int kChgBuf = 512;          // changed rows buffered per block (LDS)
 __device__ __forceinline__ float km_up1(float x) { return nextafterf(x, __builtin_inff()); }
 __device__ __forceinline__ float km_dn1(float x) { return nextafterf(x, -__builtin_inff()); }
 
+#ifdef KM_XP_TIMING
+// timing experiment: per-tile phase clocks of the first blocks (wave 0, lane 0)
+constexpr int kDbgBlocks = 64, kDbgTiles = 64, kDbgSlots = 16;
+__device__ unsigned long long g_km_dbg[kDbgBlocks * kDbgTiles * kDbgSlots];
+#define KM_TS(slot)                                                                          \
+  if (CAND && lane == 0 && (wid == 0 || wid == NW - 1) && blockIdx.x < kDbgBlocks &&        \
+      dbg_it < kDbgTiles)                                                                    \
+    g_km_dbg[((int)blockIdx.x * kDbgTiles + dbg_it) * kDbgSlots + (slot) + (wid == 0 ? 0 : 8)] = \
+        __builtin_amdgcn_s_memtime();
+#else
+#define KM_TS(slot)
+#endif
+
 template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, bool TOP2 = false,
           bool LOOP = false, bool CAND = false>
 __global__ void __launch_bounds__(NW * 64, MINB)
@@ -355,7 +368,13 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // CAND: the tile cluster's neighbour list (ids, k <= 1024), double-buffered by tile parity
   // so a tile can stage its list before the barrier that ends the previous tile's reads
   __shared__ uint16_t s_nb[CAND ? 2 : 1][CAND ? 1024 : 1];
+  // CAND: the tile cluster's centre c_acl, one copy per wave (each wave DMAs its own: no
+  // barrier before its reads)
+  __shared__ __attribute__((aligned(16))) uint4 s_ca[CAND ? NW : 1][CAND ? NJ : 1];
   int par = 0;
+#ifdef KM_XP_TIMING
+  int dbg_it = 0;
+#endif
   __shared__ int s_nchg;
   __shared__ unsigned long long s_chg_base;
 
@@ -450,6 +469,11 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // one block tile (a lambda so the single-tile launch compiles to straight-line code:
   // the loop form costs registers the 3-tile plain form does not have)
   auto tile = [&](const int64_t bt) {
+  KM_TS(0)
+#ifdef KM_XP_TIMING
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  KM_TS(7)
+#endif
   // CAND: tile bt = up to TILE positions of one cluster's run in idx
   int acl = 0;
   int64_t pbase, pend = n;
@@ -469,21 +493,64 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   uint4 bf[PT][KS];
   float x2[PT];                                // |x|^2 of the lane's point (both halves)
   float ua[CAND ? PT : 1];                     // CAND: bound on |x - c_acl| (from chunk 0)
+  int rowk[CAND ? PT : 1];                     // CAND: the lane's rows (kept for the epilogue:
+                                               // no second, dependent idx read there)
+  if constexpr (CAND) {
+    // The tile's rows are scattered over X. Loaded straight into the fragment layout, each
+    // wave-instruction would touch 32 rows (32 B of each): the per-line cost of those
+    // gathers made the load the longest phase of a tile. Instead they are gathered into
+    // LDS (the chunk buffers, free until chunk 0 is issued after the set-up barrier) by
+    // LDS-DMA in whole-row pieces -- NJ lanes per row, 64 / NJ rows per instruction, the
+    // XOR swizzle on the source side -- and read back as B fragments below.
+    static_assert(NW * PT * 32 * NJ <= NBUF * CHP, "the point tile must fit the chunk buffers");
+    constexpr int RPI = 64 / NJ;                 // rows per wave-instruction
+    __syncthreads();                             // every wave is past the last tile's chunk reads
+    {
+      // c_acl first (the lane term opaque per tile, so its address is not a hoisted,
+      // spilled loop invariant whose reload would wait for the point DMAs)
+      int lq = lane;
+      asm volatile("" : "+v"(lq));
+      if (lq < NJ) {
+        const uint16_t* src = Cq + ((int64_t)acl * DP + lq * 8);
+        const uint32_t m0v = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(km_lds_void*)&s_ca[wid][0]);
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                     :: "s"(m0v), "v"(src) : "memory");
+      }
+    }
+    const int rsub = lane / NJ, q = lane % NJ;
+    const uint32_t wbase = lds0 + (uint32_t)(wid * PT * 32 * NJ * 16);
 #pragma unroll
-  for (int t = 0; t < PT; ++t) {
-    const int64_t p = pbase + t * 32 + cl;
-    const bool ok = p < pend;
-    int64_t row;
-    if constexpr (CAND) row = ok ? (int64_t)idxn[t] : 0;
-    else row = ok ? (idx ? (int64_t)idx[p] : p) : 0;
-    const uint16_t* src = X + row * ldx + h * 8;
+    for (int t = 0; t < PT; ++t) {
+      const int idt = idxn[t];
+      // (not unrolled: 16 precomputed 64-bit addresses would spill the fragment registers)
+#pragma unroll 1
+      for (int g = 0; g < 32 / RPI; ++g) {
+        const int rc = g * RPI + rsub;           // lane of the row's id in idxn[t]
+        const int rl = t * 32 + rc;              // the wave's row
+        const int rid = __shfl(idt, rc);
+        const bool ok = pbase + rl < pend;
+        const uint16_t* src = X + (int64_t)(ok ? rid : 0) * ldx + (q ^ (rl & SWZ)) * 8;
+        const uint32_t m0v = __builtin_amdgcn_readfirstlane(wbase + (uint32_t)(rl - rsub) * (NJ * 16));
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                     :: "s"(m0v), "v"(src) : "memory");
+      }
+    }
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const uint4 v = *reinterpret_cast<const uint4*>(src + 16 * s);
-      bf[t][s] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
+    for (int t = 0; t < PT; ++t) rowk[t] = idxn[t];
+  } else {
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      const int64_t p = pbase + t * 32 + cl;
+      const bool ok = p < pend;
+      const int64_t row = ok ? (idx ? (int64_t)idx[p] : p) : 0;
+      const uint16_t* src = X + row * ldx + h * 8;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const uint4 v = *reinterpret_cast<const uint4*>(src + 16 * s);
+        bf[t][s] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
+      }
     }
   }
-  uint4 ca[CAND ? KS : 1];
   // CAND: everything the tile's set-up reads is loaded here, under the point loads (one
   // memory latency per tile instead of a chain): c_acl, the first distance of every
   // chunk of acl's list (lane j: nd[acl][j * CH]) and the list's 0.5|c|^2
@@ -491,10 +558,9 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   float thrv = __builtin_inff();
   float hv[KH];
   int nbv[KH];
+  float hna = 0.f;                             // CAND: 0.5|c_acl|^2
   if constexpr (CAND) {
-    const uint16_t* src = Cq + (int64_t)acl * DP + h * 8;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) ca[s] = *reinterpret_cast<const uint4*>(src + 16 * s);
+    hna = hn[acl];
     if (lane < nchunk) thrv = aux.nd[(int64_t)acl * kpad + lane * CH];
 #pragma unroll
     for (int j = 0; j < KH; ++j) {
@@ -506,28 +572,57 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // all ordinary loads retired before the DMA stream starts, and the fragments pinned
   // here, so the compiler's own waits never drain a chunk in flight (vmcnt(0) in-loop)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  KM_TS(1)
+  if constexpr (CAND) {
+    // the wave's own rows (its DMA, retired above): no barrier needed before the reads.
+    // Branch-free (unconditional reads, masked), and the swizzle term made opaque per
+    // tile: hoisted out of the tile loop, the 16 read addresses were spilled, and each
+    // read waited for its own scratch reload
+    const uint4* img = s_c + wid * PT * 32 * NJ;
+    int sw = cl & SWZ;                           // (t * 32 + cl) & SWZ
+    asm volatile("" : "+v"(sw));
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      const int rl = t * 32 + cl;
+      const uint32_t m = pbase + rl < pend ? 0xffffffffu : 0u;
+      const uint4* rowp = img + rl * NJ;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const uint4 v = rowp[(2 * s + h) ^ sw];
+        bf[t][s] = make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+      }
+    }
+  }
   float mx = 0.f;
-  // CAND: the lane's half of c_acl (same k layout as the point fragments), for the exact
-  // distance of every tile point to its cluster's centre (v_dot2 on the bf16 pairs)
+  // CAND: the lane's half of c_acl (same k layout as the point fragments, from the wave's
+  // LDS copy one k-step at a time), for the exact distance of every tile point to its
+  // cluster's centre (v_dot2 on the bf16 pairs)
+  float qs[PT], dts[PT];
 #pragma unroll
-  for (int t = 0; t < PT; ++t) {
-    float q = 0.f;
-    float dt = 0.f;
+  for (int t = 0; t < PT; ++t) { qs[t] = 0.f; dts[t] = 0.f; }
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
+  for (int s = 0; s < KS; ++s) {
+    uint4 cas = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (CAND) cas = s_ca[wid][2 * s + h];
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
       asm volatile("" : "+v"(bf[t][s].x), "+v"(bf[t][s].y), "+v"(bf[t][s].z), "+v"(bf[t][s].w));
-      q += sq_sum(bf[t][s], uint16_t{});
+      qs[t] += sq_sum(bf[t][s], uint16_t{});
       if constexpr (CAND) {
         const uint32_t xw[4] = {bf[t][s].x, bf[t][s].y, bf[t][s].z, bf[t][s].w};
-        const uint32_t cw[4] = {ca[s].x, ca[s].y, ca[s].z, ca[s].w};
+        const uint32_t cw[4] = {cas.x, cas.y, cas.z, cas.w};
 #pragma unroll
         for (int w = 0; w < 4; ++w)
-          dt = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, xw[w]),
-                                               __builtin_bit_cast(bf16x2, cw[w]), dt, false);
+          dts[t] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, xw[w]),
+                                                   __builtin_bit_cast(bf16x2, cw[w]), dts[t], false);
       }
       bf[t][s] = make_uint4(bf[t][s].x ^ 0x80008000u, bf[t][s].y ^ 0x80008000u,
                             bf[t][s].z ^ 0x80008000u, bf[t][s].w ^ 0x80008000u);
     }
+  }
+#pragma unroll
+  for (int t = 0; t < PT; ++t) {
+    const float q = qs[t], dt = dts[t];
     auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(q), __float_as_uint(q), false, false);
     x2[t] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
     mx = fmaxf(mx, 0.5f * x2[t]);
@@ -535,7 +630,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       auto sd = __builtin_amdgcn_permlane32_swap(__float_as_uint(dt), __float_as_uint(dt), false, false);
       const float dot = __uint_as_float(sd[0]) + __uint_as_float(sd[1]);
       // |x - c|^2 = |x|^2 - 2 x.c + 2 hn (f32 error far below tol: the K2 slack)
-      const float dist = fmaxf(x2[t] - 2.f * dot + 2.f * hn[acl], 0.f);
+      const float dist = fmaxf(x2[t] - 2.f * dot + 2.f * hna, 0.f);
       ua[t] = km_up1(sqrtf(km_up1(dist + tol)));
     }
   }
@@ -564,6 +659,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // nearest of one (|x - c| >= |c - c_acl| - |x - c_acl| > |x - c_acl| otherwise); nd is
   // ascending, so they are a prefix of the list: nch_t whole chunks of it. Every wave
   // finds the count by a two-level search of nd (all agree: no barrier)
+  KM_TS(2)
   int nch_t = nchunk;
   float nd_first = __builtin_inff();   // CAND: smallest distance of a pruned centre
   if constexpr (CAND) {
@@ -677,6 +773,9 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     // double: chunk ch+1 right away)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+#ifdef KM_XP_TIMING
+    if (ch == 0) { KM_TS(3) }
+#endif
     if (NBUF == 2 && ch + 1 < nch_t) issue(ch + 1);
     const uint4* img = s_c + (ch % NBUF) * CHP;
     uint4 a[KS];
@@ -759,6 +858,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     }
   }
   reduce_tile(pacc, T0, pcb);
+  KM_TS(4)
   // (warming L2 with the next tile's rows by throw-away LDS-DMA here measured no gain:
   // 17.92 vs 17.86 ms per iteration of the benchmark job)
   if constexpr (CAND)
@@ -793,7 +893,8 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     if (h == 0 && p < pend) {
       // acc = 0.5|x-c|^2 + M - 0.5|x|^2
       const float dist = fmaxf(2.f * (bv - M) + x2[t], 0.f);
-      row = idx ? (int64_t)idx[p] : p;
+      if constexpr (CAND) row = rowk[t];
+      else row = idx ? (int64_t)idx[p] : p;
       if constexpr (LOOP) {
         const float dist2 = fmaxf(2.f * (bv2 - M) + x2[t], 0.f);
         float lo2 = km_dn1(sqrtf(fmaxf(km_dn1(dist2 - tol), 0.f)));
@@ -830,6 +931,12 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       }
     }
   }
+#ifdef KM_XP_TIMING
+  KM_TS(5)
+  if (CAND && tid == 0 && blockIdx.x < kDbgBlocks && dbg_it < kDbgTiles)
+    g_km_dbg[((int)blockIdx.x * kDbgTiles + dbg_it) * kDbgSlots + 6] = (unsigned long long)nch_t;
+  ++dbg_it;
+#endif
   };   // tile
   if constexpr (LOOP) {
     prefetch_tile(blockIdx.x);
@@ -1438,6 +1545,11 @@ static hipError_t launch_segsum(int DP, const void* X, int64_t ldx, const int* p
 }
 
 extern "C" {
+#ifdef KM_XP_TIMING
+hipError_t dalgo_km_dbg_read(void* host, size_t bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dalgo::g_km_dbg), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 // Sort-based K3. Workspace: block_counts int32[B*k], cluster_start/seg_start
 // int64[k+1], perm int32[n]. B = number of row chunks (any >= 1).
