@@ -3,7 +3,11 @@ preprocessor flags, linked with the other objects of the in-tree build into
 ``dalgo/_xp_<name>.so`` (load it with DALGO_EXT_LIB=...). Timing experiments only.
 
     python bench/probes/build_variant.py NAME kmeans -DKM_XP_FOO [...]
+
+BV_SRC_<stem>=path compiles that file instead of csrc/kernels/<stem>.hip (e.g. an older
+revision: git show HEAD~1:csrc/kernels/kmeans.hip > /tmp/old.hip).
 """
+import os
 import subprocess
 import sys
 from pathlib import Path
@@ -21,7 +25,7 @@ def main():
             obj = B.BUILD / f"{src.stem}.xp_{name}.o"
             B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-fPIC", "-std=c++17",
                     f"-I{B.CSRC / 'include'}", f"-I{B.CSRC}", "-munsafe-fp-atomics", *flags,
-                    "-c", src, "-o", obj], False)
+                    "-c", os.environ.get(f"BV_SRC_{src.stem}", src), "-o", obj], False)
             objs.append(obj)
         else:
             objs.append(B.BUILD / f"{src.stem}.o")

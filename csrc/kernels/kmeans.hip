@@ -450,13 +450,16 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   double my_sse = 0.0;
   float my_xmax = 0.f;
 
-  // CAND: the next tile's record and row ids are loaded during the current tile (after
-  // its chunk-0 DMA), so a tile starts with its point loads instead of a chain of three
+  // CAND: the next tile's record (with the current tile's set-up loads) and row ids (after
+  // the current tile's chunk-0 DMA) are loaded during the current tile, so a tile starts
+  // with its point loads instead of a chain of three
   int4 trn = make_int4(0, 0, 0, 0);
   int idxn[CAND ? PT : 1];
-  auto prefetch_tile = [&](int64_t bt) {
+  auto load_rec = [&](int64_t bt) {
+    if constexpr (CAND) trn = bt < ntile ? aux.tiles[bt] : make_int4(0, 0, 0, 0);
+  };
+  auto load_ids = [&]() {
     if constexpr (CAND) {
-      trn = bt < ntile ? aux.tiles[bt] : make_int4(0, 0, 0, 0);
       // always PT loads per lane (clamped): the chunk-0 wait counts them
       const int64_t hi = trn.z > trn.y ? (int64_t)trn.z - 1 : 0;
 #pragma unroll
@@ -504,6 +507,12 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     // XOR swizzle on the source side -- and read back as B fragments below.
     static_assert(NW * PT * 32 * NJ <= NBUF * CHP, "the point tile must fit the chunk buffers");
     constexpr int RPI = 64 / NJ;                 // rows per wave-instruction
+    // the row ids (prefetched during the previous tile) are consumed here, before the
+    // first DMA: the compiler does not see the DMAs (inline asm), and a wait it placed
+    // for an id inside the DMA loop would also drain the DMAs issued before it
+#pragma unroll
+    for (int t = 0; t < PT; ++t) rowk[t] = idxn[t];
+    asm volatile("" :: "v"(rowk[0]), "v"(rowk[PT - 1]));
     __syncthreads();                             // every wave is past the last tile's chunk reads
     {
       // c_acl first (the lane term opaque per tile, so its address is not a hoisted,
@@ -521,7 +530,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     const uint32_t wbase = lds0 + (uint32_t)(wid * PT * 32 * NJ * 16);
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
-      const int idt = idxn[t];
+      const int idt = rowk[t];
       // (not unrolled: 16 precomputed 64-bit addresses would spill the fragment registers)
 #pragma unroll 1
       for (int g = 0; g < 32 / RPI; ++g) {
@@ -535,8 +544,6 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
                      :: "s"(m0v), "v"(src) : "memory");
       }
     }
-#pragma unroll
-    for (int t = 0; t < PT; ++t) rowk[t] = idxn[t];
   } else {
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
@@ -568,11 +575,15 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       hv[j] = in ? hbase[tid + j * NT] : 0.f;
       nbv[j] = in ? aux.nb[(int64_t)acl * kpad + tid + j * NT] : 0;
     }
+    load_rec(bt + gridDim.x);            // the next tile's record (tr holds this one's)
   }
   // all ordinary loads retired before the DMA stream starts, and the fragments pinned
   // here, so the compiler's own waits never drain a chunk in flight (vmcnt(0) in-loop)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   KM_TS(1)
+  // the next record is consumed here (retired above), so that the compiler's own wait
+  // for it is not placed after the chunk-0 DMA, where it would drain that DMA
+  if constexpr (CAND) asm volatile("" :: "v"(trn.y), "v"(trn.z));
   if constexpr (CAND) {
     // the wave's own rows (its DMA, retired above): no barrier needed before the reads.
     // Branch-free (unconditional reads, masked), and the swizzle term made opaque per
@@ -592,6 +603,14 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
         bf[t][s] = make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
       }
     }
+#pragma unroll
+    for (int j = 0; j < KH; ++j)
+      if (tid + j * NT < kpad) s_nb[par][tid + j * NT] = (uint16_t)nbv[j];
+    // every wave has its fragments (the chunk buffers are free again) and the list is
+    // staged: chunk 0 -- always streamed -- goes out now, under the set-up below
+    __syncthreads();
+    issue(0);
+    load_ids();                          // PT loads after the DMA: chunk 0 waits vmcnt(PT)
   }
   float mx = 0.f;
   // CAND: the lane's half of c_acl (same k layout as the point fragments, from the wave's
@@ -648,11 +667,6 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     for (int off = 32; off >= 1; off >>= 1) um = fmaxf(um, __shfl_xor(um, off));
   }
   if (lane == 0) { s_m[wid] = mx; if constexpr (CAND) s_r[wid] = um; }
-  if constexpr (CAND) {
-#pragma unroll
-    for (int j = 0; j < KH; ++j)
-      if (tid + j * NT < kpad) s_nb[par][tid + j * NT] = (uint16_t)nbv[j];
-  }
   __syncthreads();
   // CAND: the tile's centre stream is cluster acl's neighbour list. ua >= |x - c_acl| for
   // every tile point, so only centres c with |c - c_acl| <= R = 2 max ua can be the
@@ -669,8 +683,6 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     R = km_up1(2.f * R);
     // chunk j >= 1 is needed iff its first (smallest) distance is <= R; chunk 0 always
     nch_t = 1 + __popcll(__ballot(lane >= 1 && lane < nchunk && thrv <= R));
-    issue(0);                           // under the set-up below (buffer 0 free: barrier)
-    prefetch_tile(bt + gridDim.x);      // PT loads after the DMA: chunk 0 waits vmcnt(PT)
   }
   if constexpr (LOOP) {
     // every wave is past the previous tile's appends: room for this tile's (<= TILE)?
@@ -939,7 +951,8 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
 #endif
   };   // tile
   if constexpr (LOOP) {
-    prefetch_tile(blockIdx.x);
+    load_rec(blockIdx.x);
+    load_ids();
     for (int64_t bt = blockIdx.x; bt < ntile; bt += gridDim.x) tile(bt);
     flush_changed();
   } else {
