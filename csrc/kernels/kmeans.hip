@@ -496,6 +496,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   uint4 bf[PT][KS];
   float x2[PT];                                // |x|^2 of the lane's point (both halves)
   float ua[CAND ? PT : 1];                     // CAND: bound on |x - c_acl| (from chunk 0)
+  uint32_t pmask[CAND ? 1 : PT];               // !CAND: ~0 for the lane's rows inside the tile
   int rowk[CAND ? PT : 1];                     // CAND: the lane's rows (kept for the epilogue:
                                                // no second, dependent idx read there)
   if constexpr (CAND) {
@@ -545,17 +546,24 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
       }
     }
   } else {
+    // unconditional loads (rows past the end read row 0), masked after the prologue wait
+    // below: with a select, hipcc sank every load into its own branch and waited for it
+    // there (24 serialized memory latencies per tile)
+    // (the row ids first: a wait for one of them between two rows' loads would also
+    // wait for the loads before it)
+    int64_t rowv[CAND ? 1 : PT];
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
       const int64_t p = pbase + t * 32 + cl;
       const bool ok = p < pend;
-      const int64_t row = ok ? (idx ? (int64_t)idx[p] : p) : 0;
-      const uint16_t* src = X + row * ldx + h * 8;
+      pmask[t] = ok ? 0xffffffffu : 0u;
+      rowv[t] = ok ? (idx ? (int64_t)idx[min(p, pend - 1)] : p) : 0;
+    }
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const uint4 v = *reinterpret_cast<const uint4*>(src + 16 * s);
-        bf[t][s] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
-      }
+    for (int t = 0; t < PT; ++t) {
+      const uint16_t* src = X + rowv[t] * ldx + h * 8;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) bf[t][s] = *reinterpret_cast<const uint4*>(src + 16 * s);
     }
   }
   // CAND: everything the tile's set-up reads is loaded here, under the point loads (one
@@ -584,6 +592,14 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // the next record is consumed here (retired above), so that the compiler's own wait
   // for it is not placed after the chunk-0 DMA, where it would drain that DMA
   if constexpr (CAND) asm volatile("" :: "v"(trn.y), "v"(trn.z));
+  if constexpr (!CAND) {
+#pragma unroll
+    for (int t = 0; t < PT; ++t)
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        bf[t][s] = make_uint4(bf[t][s].x & pmask[t], bf[t][s].y & pmask[t], bf[t][s].z & pmask[t],
+                              bf[t][s].w & pmask[t]);
+  }
   if constexpr (CAND) {
     // the wave's own rows (its DMA, retired above): no barrier needed before the reads.
     // Branch-free (unconditional reads, masked), and the swizzle term made opaque per
