@@ -320,15 +320,16 @@ struct PbOut {
   int mode;
 };
 
-// returns this destination's dangling mass (standard semantics, fused update)
-__device__ __forceinline__ float pb_finish(const PbOut& o, int64_t v, uint64_t qs, int K) {
+// returns this destination's dangling mass (standard semantics, fused update); od =
+// outdeg[v] and dang = *dang_in (or 0) are loaded by the caller, in batches
+__device__ __forceinline__ float pb_finish(const PbOut& o, int64_t v, uint64_t qs, int K, int od,
+                                           float dang) {
   const float a = from_fixed(qs, K);
   if (o.r == nullptr) {
     o.acc[v] = a;
     o.pres[v] = qs != 0;
     return 0.f;
   }
-  const int od = o.outdeg[v];
   if (o.mode == 0) {
     const bool p = qs != 0;
     const float rv = p ? o.q * o.invN + (1.f - o.q) * a : -1.f;
@@ -336,7 +337,6 @@ __device__ __forceinline__ float pb_finish(const PbOut& o, int64_t v, uint64_t q
     o.c[v] = (p && od > 0) ? rv / (float)od : -1.f;
     return 0.f;
   }
-  const float dang = o.dang_in ? o.dang_in[0] : 0.f;
   const float rv = o.q * o.invN + (1.f - o.q) * (a + dang * o.invN);
   o.r[v] = rv;
   o.c[v] = od > 0 ? rv / (float)od : 0.f;
@@ -370,30 +370,46 @@ pb_accum_kernel(const float* __restrict__ val, const uint16_t* __restrict__ dloc
   for (int i = threadIdx.x; i < BW; i += NW * 64) s_acc[i] = 0ull;
   __syncthreads();
   const int64_t g_lo = lo >> 2, g_hi = (hi + 3) >> 2;     // groups of 4 entries
-  for (int64_t g0 = g_lo + threadIdx.x; g0 < g_hi; g0 += (int64_t)U * NW * 64) {
-    float4 v[U];
-    uint2 k[U];
+  // software pipelined: batch b + 1's loads are in flight while batch b is added (two
+  // register sets, loop unrolled by 2 so that no copy of a pending load is needed); loads
+  // past the range read the last group again (clamped, unconditional: a load under a
+  // branch gets its own wait)
+  constexpr int64_t STEP = (int64_t)U * NW * 64;
+  auto load_batch = [&](int64_t gb, int4 (&v)[U], uint2 (&k)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t g = g0 + (int64_t)u * NW * 64;
-      v[u] = make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
-      k[u] = make_uint2(0u, 0u);
-      if (g < g_hi) {
-        const int4 vi = ld_int4<true>(reinterpret_cast<const int32_t*>(val) + 4 * g);
-        v[u] = make_float4(__int_as_float(vi.x), __int_as_float(vi.y), __int_as_float(vi.z),
-                           __int_as_float(vi.w));
-        k[u] = *(reinterpret_cast<const uint2*>(dloc) + g);
-      }
+      const int64_t g = min(gb + (int64_t)u * NW * 64, g_hi - 1);
+      v[u] = ld_int4<true>(reinterpret_cast<const int32_t*>(val) + 4 * g);
+      k[u] = *(reinterpret_cast<const uint2*>(dloc) + g);
     }
+  };
+  auto add_batch = [&](int64_t gb, const int4 (&v)[U], const uint2 (&k)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t e = (g0 + (int64_t)u * NW * 64) * 4;
-      const float f[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+      const int64_t e = (gb + (int64_t)u * NW * 64) * 4;
+      const float f[4] = {__int_as_float(v[u].x), __int_as_float(v[u].y), __int_as_float(v[u].z),
+                          __int_as_float(v[u].w)};
       const uint32_t kk[4] = {k[u].x & 0xffffu, k[u].x >> 16, k[u].y & 0xffffu, k[u].y >> 16};
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (e + j >= lo && e + j < hi && !signbit(f[j]))
           atomicAdd(&s_acc[kk[j]], (unsigned long long)to_fixed(f[j], K));
+    }
+  };
+  int64_t g0 = g_lo + threadIdx.x;
+  if (g0 < g_hi) {
+    int4 va[U], vb[U];
+    uint2 ka[U], kb[U];
+    load_batch(g0, va, ka);
+    for (;; g0 += 2 * STEP) {
+      const bool more = g0 + STEP < g_hi;
+      if (more) load_batch(g0 + STEP, vb, kb);
+      add_batch(g0, va, ka);
+      if (!more) break;
+      const bool more2 = g0 + 2 * STEP < g_hi;
+      if (more2) load_batch(g0 + 2 * STEP, va, ka);
+      add_batch(g0 + STEP, vb, kb);
+      if (!more2) break;
     }
   }
   __syncthreads();
@@ -401,8 +417,25 @@ pb_accum_kernel(const float* __restrict__ val, const uint16_t* __restrict__ dloc
   const int nb = (int)min((int64_t)BW, n_local - base);
   const int sl = wi_slab[w];
   if (sl < 0) {                         // the bin's only work item: final values
+    // out-degrees loaded in one batch (clamped, unconditional): one memory latency per
+    // work item instead of one per destination a thread finishes
+    constexpr int PER = BW / (NW * 64);
+    int od[PER];
+    const float dang = (o.r != nullptr && o.mode == 1 && o.dang_in) ? o.dang_in[0] : 0.f;
+    if (o.r != nullptr) {
+#pragma unroll
+      for (int j = 0; j < PER; ++j)
+        od[j] = o.outdeg[base + min((int)threadIdx.x + j * NW * 64, nb - 1)];
+    } else {
+#pragma unroll
+      for (int j = 0; j < PER; ++j) od[j] = 0;
+    }
     float dl = 0.f;
-    for (int i = threadIdx.x; i < nb; i += NW * 64) dl += pb_finish(o, base + i, s_acc[i], K);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = threadIdx.x + j * NW * 64;
+      if (i < nb) dl += pb_finish(o, base + i, s_acc[i], K, od[j], dang);
+    }
     pb_dangling(o, dl);
   } else {                              // partial of a split bin -> its slab
     uint64_t* dst = slab + (int64_t)sl * BW;
@@ -426,7 +459,9 @@ pb_combine_kernel(const uint64_t* __restrict__ slab, const int32_t* __restrict__
     const int cnt = split_count[sb];
     uint64_t q = 0;
     for (int k = 0; k < cnt; ++k) q += p[(int64_t)k * BW];
-    dl = pb_finish(o, base + i, q, K);
+    const int od = o.r != nullptr ? o.outdeg[base + i] : 0;
+    const float dang = (o.r != nullptr && o.mode == 1 && o.dang_in) ? o.dang_in[0] : 0.f;
+    dl = pb_finish(o, base + i, q, K, od, dang);
   }
   pb_dangling(o, dl);
 }
