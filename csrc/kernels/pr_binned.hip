@@ -58,6 +58,26 @@ __device__ __forceinline__ float dpp_mov_f(float old, float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL,
                                                     ROWS, 0xf, false));
 }
+typedef int pb_v4i __attribute__((ext_vector_type(4)));
+
+// Phase 1's edge ring and entry stores are issued as inline asm with hand-counted waits:
+// the compiler's own vmcnt bookkeeping treats a mix of pending loads and stores as out of
+// order and waited vmcnt(0..2) at every step; it sees no vector memory op in the step
+// loop now, so it places no wait there. The stores use the SGPR-base form with a 32-bit
+// byte offset (one select per store instead of a 64-bit address).
+__device__ __forceinline__ pb_v4i pb_ld16(const void* p) {
+  pb_v4i r;
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+__device__ __forceinline__ void pb_st4(float* base, uint32_t off_bytes, float v) {
+  asm volatile("global_store_dword %0, %1, %2" :: "v"(off_bytes), "v"(v), "s"(base) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void pb_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+}
+
 template <int CTRL, int ROWS = 0xf>
 __device__ __forceinline__ int dpp_mov_i(int old, int v) {
   return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWS, 0xf, false);
@@ -144,7 +164,9 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
   float* sv = s_v[wave];
   int32_t* sp = s_p[wave];
   // dummy_base: kPbDummy floats past the entries, 64 per wave slot
-  const int64_t dummy = dummy_base + (int64_t)(((blockIdx.x * NW + wave) % (kPbDummy / 64)) * 64 + lane);
+  // (positions < 2^30, checked by the launcher: 32-bit byte offsets)
+  const uint32_t dummy4 =
+      ((uint32_t)dummy_base + (uint32_t)(((blockIdx.x * NW + wave) % (kPbDummy / 64)) * 64 + lane)) * 4u;
   const int t_end = wu_tile[wu + 1];
   for (int t = wu_tile[wu] + wave; t < t_end; t += NW) {
     const int64_t e_lo = tile_e[t], e_hi = tile_e[t + 1];
@@ -153,21 +175,36 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
     float carry = -0.0f;                      // open entry continuing from the last step
     const int64_t e_first = e_lo & ~(int64_t)(EPL - 1);
     auto load = [&](int64_t ix) {             // out-of-tile lanes re-read the first group
-      return ld_int4<true>(reinterpret_cast<const int32_t*>(srcl + (ix < e_hi ? ix : e_first)));
+      return pb_ld16(srcl + (ix < e_hi ? ix : e_first));
     };
     // ring of D steps in flight, unrolled by D so that no register copy of a pending load
     // (which would wait for it) is needed
-    int4 wq[D];
+    // the tile's scalars are consumed here, before the ring's first loads: a wait the
+    // compiler placed at their first use inside the step loop would run every step
+    {
+      int ent_lo = (int)ent;
+      asm volatile("" :: "v"(ent_lo), "v"(run), "v"(e_lo), "v"(e_hi));
+    }
+    pb_v4i wq[D];
 #pragma unroll
     for (int q = 0; q < D; ++q) wq[q] = load(e_first + (int64_t)q * 64 * EPL + EPL * lane);
+    // vector memory ops per step: EPL stores, then the ring refill. Slot q's data was
+    // loaded D steps back; younger than it: (D - 1) (EPL + 1) ops in steady state, and in
+    // the first D steps at least the D - 1 other initial loads
+    static_assert((D - 1) * (EPL + 1) <= 63, "vmcnt field");
+    bool first = true;
     for (int64_t e00 = e_first; e00 < e_hi; e00 += (int64_t)D * 64 * EPL) {
 #pragma unroll
     for (int q = 0; q < D; ++q) {
       const int64_t e0 = e00 + (int64_t)q * 64 * EPL;
       if (e0 >= e_hi) break;
       const int64_t idx = e0 + EPL * lane;
-      const int4 wc = wq[q];
-      wq[q] = load(idx + (int64_t)D * 64 * EPL);
+      if (first) pb_wait_vm<D - 1>();
+      else pb_wait_vm<(D - 1) * (EPL + 1)>();
+      // the slot is routed through an (ordered) asm after the wait: no read of it can be
+      // scheduled before the wait
+      asm volatile("" : "+v"(wq[q]));
+      const int4 wc = make_int4(wq[q].x, wq[q].y, wq[q].z, wq[q].w);
       // a step whose 512 edges all lie inside the tile (all but the first and last of a
       // tile: wave-uniform) drops the per-edge in-range selects
       const bool full = e0 >= e_lo && e0 + 64 * EPL <= e_hi;
@@ -269,15 +306,24 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
 #pragma unroll
         for (int q = 0; q < EPL; ++q) {
           const bool ok = lane + 64 * q < n_step;
-          val[ok ? (int64_t)pq[q] : dummy] = ok ? vq[q] : 0.f;
+          pb_st4(val, ok ? (uint32_t)pq[q] * 4u : dummy4, ok ? vq[q] : 0.f);
         }
       };
       if (full) step(std::true_type{}); else step(std::false_type{});
+      // the ring slot is refilled after the step's last read of it: the old and the new
+      // value never live together, so they share registers (no copy of a pending load)
+      wq[q] = load(idx + (int64_t)D * 64 * EPL);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    first = false;
     }
+    // the ring refills past the tile's end are still landing in the slot registers: drain
+    // them while the slots are still held (operands of the wait), before any later code
+    // can reuse those registers
+    static_assert(D == 4, "drain operands");
+    asm volatile("s_waitcnt vmcnt(0)" :: "v"(wq[0]), "v"(wq[1]), "v"(wq[2]), "v"(wq[3]) : "memory");
   }
 }
 
@@ -484,7 +530,8 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
                          const int32_t* split_count, int nsplit, const int32_t* outdeg, float q,
                          float invN, int mode, const float* dang_in, float* r, float* cn,
                          float* dang_out, hipStream_t st) {
-  if (src_span != 8192 || (bin_width != 8192 && bin_width != 16384) || n_val < kPbDummy)
+  if (src_span != 8192 || (bin_width != 8192 && bin_width != 16384) || n_val < kPbDummy ||
+      n_val >= ((int64_t)1 << 30))
     return hipErrorInvalidValue;
   // phases: bit 0 = phase 1 over work units [wu_lo, wu_hi) (several calls may cover the
   // units, the first one starting at 0 -- e.g. own-slice sources before the ghost
