@@ -170,7 +170,7 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
   const int t_end = wu_tile[wu + 1];
   for (int t = wu_tile[wu] + wave; t < t_end; t += NW) {
     const int64_t e_lo = tile_e[t], e_hi = tile_e[t + 1];
-    int64_t ent = tile_ent[t];                // chunk-major index of the next entry
+    int32_t ent = tile_ent[t];                // chunk-major index of the next entry (< 2^30)
     int run = tile_run[t];                    // run starts (in this chunk) before it
     float carry = -0.0f;                      // open entry continuing from the last step
     const int64_t e_first = e_lo & ~(int64_t)(EPL - 1);
@@ -276,7 +276,7 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
         for (int k = 0; k < EPL; ++k) {
           if (hk[k] & 0x8000u) {
             sv[j] = first ? carry_in + outv[k] : outv[k];
-            sp[j] = (int32_t)(ent + j + dl[k]);
+            sp[j] = ent + j + dl[k];
             first = false;
             ++j;
           }
