@@ -32,6 +32,7 @@ namespace dalgo {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 template <typename T> struct KTraits;
@@ -1511,6 +1512,225 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
   return hipSuccess;
 }
 
+// ---------------------------------------------------------------------------
+// K2 full pass on 16x16x32 MFMAs (bf16, DP = 128, no row indirection): the same distance
+// keys as the pipelined form, tiled for v_mfma_f32_16x16x32_bf16, which sustains ~12 %
+// more FLOP/s than the 32x32x16 form next to an argmin VALU load (profiles/round4/r4_36:
+// a power / clock effect). A wave holds PG groups of 16 points (B operand, negated; lane
+// l: point l % 16, dims 32 s + 8 (l / 16) .. +8 of k-step s); a 128-centre chunk (the
+// same swizzled LDS-DMA image as the 32x32 form) is 8 sub-tiles of 16 centres (A: lane
+// l reads centre l % 16, piece 4 s + l / 16). The accumulator starts at 0.5|c|^2 + M, so
+// acc = 0.5|x - c|^2 + M - 0.5|x|^2 >= 0 and its float bits order like the distances;
+// lane l holds centres 4 (l / 16) + r of the sub-tile for point l % 16: key = bits & ~31
+// | (sub * 4 + r) keeps the lowest id among equal keys of a chunk, chunks compare on the
+// value bits only (strict), and the four lane groups of a point are merged at the end.
+template <int NW, int PG, int MINB>
+__global__ void __launch_bounds__(NW * 64, MINB)
+kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
+                       const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int kpad,
+                       int* __restrict__ assign, float* __restrict__ mind,
+                       double* __restrict__ sse, int sse_mask, float* __restrict__ xh,
+                       unsigned* __restrict__ xmax) {
+  constexpr int DP = 128, KS = DP / 32;        // 16x16x32 k-steps per centre row
+  constexpr int NJ = DP * 2 / 16;              // 16-B pieces per row
+  constexpr int SWZ = 15;
+  constexpr int CH = 128, NSUB = CH / 16;
+  constexpr int NT = NW * 64;
+  constexpr int CHP = CH * NJ;
+  constexpr int GPT = CHP / NT;
+  constexpr int NBUF = 2;
+  constexpr int TILE = NW * PG * 16;
+  static_assert(CHP % NT == 0 && (NT / NJ) % (SWZ + 1) == 0, "DMA layout");
+  __shared__ __attribute__((aligned(16))) uint4 s_c[NBUF * CHP];
+  extern __shared__ __attribute__((aligned(16))) float s_hn16[];   // [kpad]: 0.5|c|^2 + M
+  __shared__ float s_m[NW];
+  __shared__ double s_sse[NW];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lg = lane >> 4, pl = lane & 15;
+  const int nchunk = kpad / CH;
+  const int64_t pbase = ((int64_t)blockIdx.x * NW + wid) * (PG * 16);
+
+  // ---- points: unconditional loads (rows past n read row 0), masked after the wait
+  uint4 bf[PG][KS];
+  uint32_t pm[PG];
+#pragma unroll
+  for (int g = 0; g < PG; ++g) {
+    const int64_t p = pbase + g * 16 + pl;
+    pm[g] = p < n ? 0xffffffffu : 0u;
+    const uint16_t* src = X + (p < n ? p : 0) * ldx + 8 * lg;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) bf[g][s] = *reinterpret_cast<const uint4*>(src + 32 * s);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float x2[PG];
+  float mx = 0.f;
+#pragma unroll
+  for (int g = 0; g < PG; ++g) {
+    float q = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf[g][s] = make_uint4(bf[g][s].x & pm[g], bf[g][s].y & pm[g], bf[g][s].z & pm[g], bf[g][s].w & pm[g]);
+      q += sq_sum(bf[g][s], uint16_t{});
+      bf[g][s] = make_uint4(bf[g][s].x ^ 0x80008000u, bf[g][s].y ^ 0x80008000u,
+                            bf[g][s].z ^ 0x80008000u, bf[g][s].w ^ 0x80008000u);
+    }
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    x2[g] = q;
+    mx = fmaxf(mx, 0.5f * q);
+  }
+  for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+  if (lane == 0) s_m[wid] = mx;
+
+  // ---- chunk DMA (the 32x32 form's image: slot (row, jj) holds piece jj ^ (row & SWZ))
+  int src_off[GPT];
+#pragma unroll
+  for (int g = 0; g < GPT; ++g) {
+    const int qq = g * NT + tid, row = qq / NJ, jj = qq % NJ;
+    src_off[g] = row * DP + (jj ^ (row & SWZ)) * 8;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(km_lds_void*)s_c;
+  auto issue = [&](int ch) {
+    const uint16_t* base = Cq + (int64_t)ch * CH * DP;
+    const uint32_t dst = lds0 + (uint32_t)(((ch % NBUF) * CHP) * 16);
+#pragma unroll
+    for (int g = 0; g < GPT; ++g) {
+      const uint32_t m0v = __builtin_amdgcn_readfirstlane(dst + (uint32_t)((g * NT + wid * 64) * 16));
+      const uint16_t* src = base + src_off[g];
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                   :: "s"(m0v), "v"(src) : "memory");
+    }
+  };
+  __syncthreads();
+  float M = s_m[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) M = fmaxf(M, s_m[w]);
+  M = M * 1.0001f + 1e-6f;
+  for (int c = tid; c < kpad; c += NT) s_hn16[c] = hn[c] + M;
+  issue(0);
+
+  int bkey[PG], bch[PG];
+#pragma unroll
+  for (int g = 0; g < PG; ++g) { bkey[g] = 0x7fffffff; bch[g] = 0; }
+  const int kmask = ~31;
+  for (int ch = 0; ch < nchunk; ++ch) {
+    km_wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();              // chunk ch landed; chunk ch - 1 retired
+    asm volatile("" ::: "memory");
+    if (ch + 1 < nchunk) issue(ch + 1);
+    const uint4* img = s_c + (ch % NBUF) * CHP;
+    int cm[PG];
+#pragma unroll
+    for (int g = 0; g < PG; ++g) cm[g] = 0x7fffffff;
+    // the next sub-tile's fragments are read under the current one's MFMAs; the PG
+    // accumulators advance k-step by k-step (independent chains in flight)
+    auto load_frag = [&](int sub, uint4 (&a)[KS], float4& h4) {
+      const int row = sub * 16 + pl;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a[s] = img[row * NJ + ((4 * s + lg) ^ (row & SWZ))];
+      h4 = *reinterpret_cast<const float4*>(&s_hn16[ch * CH + sub * 16 + 4 * lg]);
+    };
+    uint4 a[KS];
+    float4 h4;
+    load_frag(0, a, h4);
+#pragma unroll
+    for (int sub = 0; sub < NSUB; ++sub) {
+      uint4 an[KS];
+      float4 hn4;
+      if (sub + 1 < NSUB) load_frag(sub + 1, an, hn4);
+      f32x4 acc[PG];
+#pragma unroll
+      for (int g = 0; g < PG; ++g) acc[g] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int g = 0; g < PG; ++g)
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[s]),
+                                                          __builtin_bit_cast(bf16x8, bf[g][s]), acc[g], 0, 0, 0);
+#pragma unroll
+      for (int g = 0; g < PG; ++g) {
+        const int k0 = (__float_as_int(acc[g][0]) & kmask) | (sub * 4 + 0);
+        const int k1 = (__float_as_int(acc[g][1]) & kmask) | (sub * 4 + 1);
+        const int k2 = (__float_as_int(acc[g][2]) & kmask) | (sub * 4 + 2);
+        const int k3 = (__float_as_int(acc[g][3]) & kmask) | (sub * 4 + 3);
+        cm[g] = min(min(cm[g], min(k0, k1)), min(k2, k3));
+      }
+      if (sub + 1 < NSUB) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) a[s] = an[s];
+        h4 = hn4;
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < PG; ++g) {
+      // across chunks on the value bits only (strict: the earlier chunk keeps a tie)
+      const bool take = (cm[g] & kmask) < (bkey[g] & kmask);
+      bkey[g] = take ? cm[g] : bkey[g];
+      bch[g] = take ? ch : bch[g];
+    }
+  }
+
+  // ---- merge the 4 lane groups of each point, write the outputs
+  double my_sse = 0.0;
+#pragma unroll
+  for (int g = 0; g < PG; ++g) {
+    float v = __int_as_float(bkey[g] & kmask);
+    const int ix = bkey[g] & 31;
+    int id = bch[g] * CH + (ix >> 2) * 16 + 4 * lg + (ix & 3);
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+      const float pv = __shfl_xor(v, o, 64);
+      const int pi = __shfl_xor(id, o, 64);
+      if (pv < v || (pv == v && pi < id)) { v = pv; id = pi; }
+    }
+    const int64_t p = pbase + g * 16 + pl;
+    if (lg == 0 && p < n) {
+      const float dist = fmaxf(2.f * (v - M) + x2[g], 0.f);
+      assign[p] = id;
+      if (mind) mind[p] = dist;
+      if (xh) xh[p] = 0.5f * x2[g];
+      my_sse += (double)dist;
+    }
+  }
+  if (xmax && lane == 0) atomicMax(xmax, __float_as_uint(mx));
+  if (sse) {
+    double s = my_sse;
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) s_sse[wid] = s;
+    __syncthreads();
+    if (tid == 0) {
+      double tot = 0.0;
+      for (int w = 0; w < NW; ++w) tot += s_sse[w];
+      atomicAdd(sse + (blockIdx.x & sse_mask), tot);
+    }
+  }
+}
+
+static hipError_t launch_assign16(const void* X, int64_t n, int64_t ldx, const void* Cq,
+                                  const float* hn, int kpad, int* assign, float* mind, double* sse,
+                                  int sse_mask, float* xh, unsigned* xmax, hipStream_t st) {
+  constexpr int NW = 4, PG = 6, MINB = 2;
+  if (kpad % 128) return hipErrorInvalidValue;
+  const size_t dyn = (size_t)kpad * sizeof(float);
+  if (2 * 128 * 128 * 2 + dyn + 1024 > 80 * 1024) return hipErrorInvalidValue;   // 2 blocks per CU
+  const int64_t grid = cdiv(n, (int64_t)NW * PG * 16);
+  if (grid == 0) return hipSuccess;
+  if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
+  auto kfn = kmeans_assign16_kernel<NW, PG, MINB>;
+  static size_t attr_set = 0;
+  if (dyn > attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)dyn);
+    if (e != hipSuccess) return e;
+    attr_set = dyn;
+  }
+  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(NW * 64), dyn, st, (const uint16_t*)X, n, ldx,
+                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse, sse_mask, xh, xmax);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
 // K2 dispatch. bf16 with DP >= 64: the pipelined distance-key form (4-wave blocks, two
 // per CU, 3 point tiles per wave, 128-centre chunks double-buffered by LDS-DMA, next
 // fragments prefetched, last tile's argmin software-pipelined): 1.20-1.25 PF/s at
@@ -1528,6 +1748,11 @@ template <typename T, int DP>
 static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                    const float* hn, int kpad, int* assign, float* mind, double* sse,
                                    int sse_mask, hipStream_t st) {
+#ifndef KM_XP_NO16
+  if constexpr (sizeof(T) == 2 && DP == 128)
+    if (kpad % 128 == 0)
+      return launch_assign16(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, nullptr, nullptr, st);
+#endif
   if constexpr (sizeof(T) == 2 && DP >= 64)
     if (kpad % 128 == 0)
       return launch_assign_pipe<DP, 4, 3, 4, 2, 2, true>(X, n, ldx, Cq, hn, kpad, assign, mind, sse,
@@ -1732,6 +1957,10 @@ hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP
           X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, st, idx, mind2, aux);
     return hipErrorInvalidValue;
   }
+#ifndef KM_XP_NO16
+  if (DP == 128 && idx == nullptr)
+    return launch_assign16(X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, aux.xh, aux.xmax, st);
+#endif
   if (DP == 128)
     return launch_assign_pipe<128, 4, 3, 4, 2, 2, true>(X, m, ldx, Cq, hn, kpad, assign, mind, sse,
                                                         sse_mask, st, idx, nullptr, aux);
