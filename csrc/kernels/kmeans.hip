@@ -1731,7 +1731,8 @@ static hipError_t launch_assign16(const void* X, int64_t n, int64_t ldx, const v
   return hipSuccess;
 }
 
-// K2 dispatch. bf16 with DP >= 64: the pipelined distance-key form (4-wave blocks, two
+// K2 dispatch. bf16 with DP = 128: the 16x16x32 form above (kmeans_assign16_kernel).
+// bf16 with DP = 64 (and the indexed forms): the pipelined distance-key form (4-wave blocks, two
 // per CU, 3 point tiles per wave, 128-centre chunks double-buffered by LDS-DMA, next
 // fragments prefetched, last tile's argmin software-pipelined): 1.20-1.25 PF/s at
 // 20M-100M x 128 x 1024. f32, and bf16 with DP < 64: the generic form (8-wave blocks,
