@@ -1064,7 +1064,16 @@ kmeans_hist_kernel(const int* __restrict__ assign, int64_t n_, int64_t rpc_, int
   for (int c = threadIdx.x; c < k; c += blockDim.x) hist[c] = 0;
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * rpc, r1 = min(n, r0 + rpc);
-  for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) atomicAdd(&hist[assign[r]], 1);
+  // kHB loads in flight per thread (clamped, unconditional) before their LDS atomics
+  constexpr int kHB = 8;
+  for (int64_t q = r0 + threadIdx.x; q < r1; q += (int64_t)kHB * blockDim.x) {
+    int c[kHB];
+#pragma unroll
+    for (int b = 0; b < kHB; ++b) c[b] = assign[min(q + (int64_t)b * blockDim.x, r1 - 1)];
+#pragma unroll
+    for (int b = 0; b < kHB; ++b)
+      if (q + (int64_t)b * blockDim.x < r1) atomicAdd(&hist[c[b]], 1);
+  }
   __syncthreads();
   for (int c = threadIdx.x; c < k; c += blockDim.x) block_counts[(int64_t)blockIdx.x * k + c] = hist[c];
 }
@@ -1146,12 +1155,15 @@ kmeans_scatter_kernel(const int* __restrict__ assign, int64_t n, int64_t rpc, in
 }
 
 // Coalesced scatter (default for k <= kScKmax): the block's rows are handled in
-// chunks of kScCh; each chunk is counting-sorted by cluster in LDS first (local
+// chunks of CH rows; each chunk is counting-sorted by cluster in LDS first (local
 // ranks by LDS atomics, block scan of the local counts, one packed (cluster, row
 // offset) word per slot), then slot i is written to cursor[c] + (i - lstart[c]):
-// consecutive lanes store consecutive perm entries of one cluster run (~kScCh/k
+// consecutive lanes store consecutive perm entries of one cluster run (~CH/k
 // rows per run) instead of 64 unrelated 4-byte locations per store instruction.
-constexpr int kScCh = 32768, kScKmax = 2048, kScNT = 1024, kScPer = kScCh / kScNT;
+// CH / KMAX: chunk rows / cluster bound; <16384, 1024> (76 KB LDS) runs 2 blocks per CU
+// where k <= 1024, so one block's scan and barriers overlap the other's memory phases.
+constexpr int kScKmax = 2048, kScNT = 1024;
+template <int CH, int KMAX>
 __global__ void __launch_bounds__(kScNT)
 kmeans_scatter_chunked_kernel(const int* __restrict__ assign, int64_t n_, int64_t rpc_, int k,
                               const int* __restrict__ block_offsets,
@@ -1162,16 +1174,17 @@ kmeans_scatter_chunked_kernel(const int* __restrict__ assign, int64_t n_, int64_
   const SortGeom g = sort_geom(n_, rpc_, gridDim.x, ndev, mul, chunk);
   if ((int)blockIdx.x >= g.B) return;
   const int64_t n = g.n, rpc = g.rpc;
-  __shared__ int stage[kScCh];
-  __shared__ int cursor[kScKmax], lcnt[kScKmax], lstart[kScKmax];
+  constexpr int kScPer = CH / kScNT;
+  __shared__ int stage[CH];
+  __shared__ int cursor[KMAX], lcnt[KMAX], lstart[KMAX];
   __shared__ int s_wsum[kScNT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int c = tid; c < k; c += kScNT)
     cursor[c] = (int)(cluster_start[c] + block_offsets[(int64_t)blockIdx.x * k + c]);
   const int64_t r0 = (int64_t)blockIdx.x * rpc, r1 = min(n, r0 + rpc);
   const int per = (k + kScNT - 1) / kScNT;        // scan entries per thread
-  for (int64_t q0 = r0; q0 < r1; q0 += kScCh) {
-    const int m = (int)min((int64_t)kScCh, r1 - q0);
+  for (int64_t q0 = r0; q0 < r1; q0 += CH) {
+    const int m = (int)min((int64_t)CH, r1 - q0);
     for (int c = tid; c < k; c += kScNT) lcnt[c] = 0;
     __syncthreads();
     int packed[kScPer];                            // (cluster << 15) | local rank
@@ -1208,6 +1221,8 @@ kmeans_scatter_chunked_kernel(const int* __restrict__ assign, int64_t n_, int64_
       }
     }
     __syncthreads();
+    // (batching the vals[e] gathers 16 deep measured no faster, profiles/round4/r4_42:
+    // the chunk's vals window is L2-resident after its first touches)
     for (int i = tid; i < m; i += kScNT) {
       const int v = stage[i];
       const int c = v >> 15;
@@ -1218,6 +1233,17 @@ kmeans_scatter_chunked_kernel(const int* __restrict__ assign, int64_t n_, int64_
     for (int c = tid; c < k; c += kScNT) cursor[c] += lcnt[c];
     __syncthreads();
   }
+}
+
+template <typename... A>
+static void launch_scatter_chunked(int k, int B, hipStream_t st, A... a) {
+#ifndef KM_XP_SC1
+  if (k <= 1024) {
+    hipLaunchKernelGGL((kmeans_scatter_chunked_kernel<16384, 1024>), dim3(B), dim3(kScNT), 0, st, a...);
+    return;
+  }
+#endif
+  hipLaunchKernelGGL((kmeans_scatter_chunked_kernel<32768, kScKmax>), dim3(B), dim3(kScNT), 0, st, a...);
 }
 
 template <typename T, int DP, int NW, bool NT>
@@ -1833,7 +1859,7 @@ hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n,
                      (const unsigned long long*)nullptr, 1, (int64_t)1);
   DALGO_LAUNCH_CHECK();
   if (k <= kScKmax)   // per-row LDS-cursor scatter only where the chunked form's LDS ends
-    hipLaunchKernelGGL(kmeans_scatter_chunked_kernel, dim3(B), dim3(kScNT), 0, st, assign, n, rpc, k,
+    launch_scatter_chunked(k, B, st, assign, n, rpc, k,
                        (const int*)block_counts, (const int64_t*)cluster_start, perm,
                        (const unsigned long long*)nullptr, 1, (int64_t)1);
   else
@@ -1873,7 +1899,7 @@ hipError_t dalgo_kmeans_move_sorted(const void* X, int is_bf16, int64_t ldx, int
   hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), 2 * lds_k, st, block_counts, B, k, seg,
                      cluster_start, seg_start, (unsigned long long*)nullptr, mdev, 2, chunk);
   DALGO_LAUNCH_CHECK();
-  hipLaunchKernelGGL(kmeans_scatter_chunked_kernel, dim3(B), dim3(kScNT), 0, st, (const int*)ec, n2,
+  launch_scatter_chunked(k, B, st, (const int*)ec, n2,
                      rpc, k, (const int*)block_counts, (const int64_t*)cluster_start, perm, mdev, 2,
                      chunk);
   DALGO_LAUNCH_CHECK();
@@ -2009,7 +2035,7 @@ hipError_t dalgo_kmeans_sort_active(const int32_t* acl, const int32_t* idx, int6
   hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), 2 * lds_k, st, block_counts, B, k,
                      1 << 20, cstart, seg_start, (unsigned long long*)nullptr, n_active, 1, chunk);
   DALGO_LAUNCH_CHECK();
-  hipLaunchKernelGGL(kmeans_scatter_chunked_kernel, dim3(B), dim3(kScNT), 0, st, (const int*)acl, cap,
+  launch_scatter_chunked(k, B, st, (const int*)acl, cap,
                      rpc, k, (const int*)block_counts, (const int64_t*)cstart, (int*)rows_sorted,
                      n_active, 1, chunk, (const int*)idx);
   DALGO_LAUNCH_CHECK();
