@@ -1078,37 +1078,62 @@ kmeans_hist_kernel(const int* __restrict__ assign, int64_t n_, int64_t rpc_, int
   for (int c = threadIdx.x; c < k; c += blockDim.x) block_counts[(int64_t)blockIdx.x * k + c] = hist[c];
 }
 
-__global__ void __launch_bounds__(1024)
-kmeans_scan_kernel(int* __restrict__ block_counts, int B_, int k, int seg,
-                   int64_t* __restrict__ cluster_start, int64_t* __restrict__ seg_start,
-                   unsigned long long* __restrict__ cnt_out,
-                   const unsigned long long* __restrict__ ndev, int mul, int64_t chunk) {
+// Column pass of the sort scan: block_counts[b][c] -> exclusive prefix over b, column
+// totals -> colsum[c] (the cluster_start array, overwritten by kmeans_scan_kernel).
+// 64 columns per block, 16 row ranges per column: 16x the memory parallelism of one
+// block walking every column (that walk was load-latency bound: ~96 us at B=1100, k=1024).
+constexpr int kCsCols = 64, kCsParts = 16, kCsBat = 16;
+__global__ void __launch_bounds__(kCsCols * kCsParts)
+kmeans_colscan_kernel(int* __restrict__ block_counts, int B_, int k, int64_t* __restrict__ colsum,
+                      unsigned long long* __restrict__ cnt_out,
+                      const unsigned long long* __restrict__ ndev, int mul, int64_t chunk) {
   const int B = sort_geom(0, 1, B_, ndev, mul, chunk).B;
+  __shared__ int s_sum[kCsParts][kCsCols];
+  const int col = threadIdx.x % kCsCols, p = threadIdx.x / kCsCols;
+  const int c = blockIdx.x * kCsCols + col;
+  const bool okc = c < k;
+  const int cc = okc ? c : k - 1;
+  const int rp = (B + kCsParts - 1) / kCsParts;
+  const int b0 = min(B, p * rp), b1 = min(B, b0 + rp);
+  int sum = 0;
+  for (int b = b0; b < b1; b += kCsBat) {
+    int v[kCsBat];
+#pragma unroll
+    for (int j = 0; j < kCsBat; ++j) v[j] = block_counts[(int64_t)min(b + j, b1 - 1) * k + cc];
+#pragma unroll
+    for (int j = 0; j < kCsBat; ++j) sum += b + j < b1 ? v[j] : 0;
+  }
+  s_sum[p][col] = sum;
+  __syncthreads();
+  int run = 0;
+  for (int q = 0; q < p; ++q) run += s_sum[q][col];
+  for (int b = b0; b < b1; b += kCsBat) {
+    int v[kCsBat];
+#pragma unroll
+    for (int j = 0; j < kCsBat; ++j) v[j] = block_counts[(int64_t)min(b + j, b1 - 1) * k + cc];
+#pragma unroll
+    for (int j = 0; j < kCsBat; ++j)
+      if (okc && b + j < b1) { block_counts[(int64_t)(b + j) * k + c] = run; run += v[j]; }
+  }
+  if (okc && p == kCsParts - 1) {
+    colsum[c] = run;
+    if (cnt_out) cnt_out[c] += (unsigned long long)run;
+  }
+}
+
+// Cross-cluster scan: colsum[c] (kmeans_colscan_kernel's totals, in cluster_start) ->
+// cluster_start / seg_start exclusive prefixes.
+__global__ void __launch_bounds__(1024)
+kmeans_scan_kernel(int k, int seg, int64_t* __restrict__ cluster_start,
+                   int64_t* __restrict__ seg_start) {
   // [2k] int32 (n < 2^31 is checked by the launcher): counts, then segment counts;
   // 8 B per cluster keeps k = 16384 inside the 160 KB LDS (128 KB dynamic)
   extern __shared__ int tot[];
   __shared__ int64_t s_part[2][1024 / 64];
   for (int c = threadIdx.x; c < k; c += blockDim.x) {
-    // the column walk is load-latency bound: issue kBat loads before the stores
-    // that depend on them (one HBM round trip per kBat blocks, not per block)
-    constexpr int kBat = 32;
-    int run = 0;
-    int b = 0;
-    for (; b + kBat <= B; b += kBat) {
-      int v[kBat];
-#pragma unroll
-      for (int j = 0; j < kBat; ++j) v[j] = __builtin_nontemporal_load(&block_counts[(int64_t)(b + j) * k + c]);
-#pragma unroll
-      for (int j = 0; j < kBat; ++j) { block_counts[(int64_t)(b + j) * k + c] = run; run += v[j]; }
-    }
-    for (; b < B; ++b) {
-      const int v = block_counts[(int64_t)b * k + c];
-      block_counts[(int64_t)b * k + c] = run;
-      run += v;
-    }
+    const int run = (int)cluster_start[c];
     tot[c] = run;
     tot[k + c] = (run + seg - 1) / seg;
-    if (cnt_out) cnt_out[c] += (unsigned long long)run;
   }
   __syncthreads();
   // exclusive scans of tot[0..k) and tot[k..2k) by a single thread per chunk of k/1024
@@ -1233,6 +1258,16 @@ kmeans_scatter_chunked_kernel(const int* __restrict__ assign, int64_t n_, int64_
     for (int c = tid; c < k; c += kScNT) cursor[c] += lcnt[c];
     __syncthreads();
   }
+}
+
+// the sort scan: column pass (multi-block) then the cross-cluster pass (one block)
+static void launch_sort_scan(int* block_counts, int B, int k, int seg, int64_t* cluster_start,
+                             int64_t* seg_start, unsigned long long* cnt,
+                             const unsigned long long* ndev, int mul, int64_t chunk, size_t lds,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(kmeans_colscan_kernel, dim3((k + kCsCols - 1) / kCsCols), dim3(kCsCols * kCsParts),
+                     0, st, block_counts, B, k, cluster_start, cnt, ndev, mul, chunk);
+  hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), lds, st, k, seg, cluster_start, seg_start);
 }
 
 template <typename... A>
@@ -1854,9 +1889,7 @@ hipError_t dalgo_kmeans_accumulate_sorted(const void* X, int is_bf16, int64_t n,
       scan_attr = scan_lds;
     }
   }
-  hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), scan_lds, st,
-                     block_counts, B, k, seg, cluster_start, seg_start, cnt,
-                     (const unsigned long long*)nullptr, 1, (int64_t)1);
+  launch_sort_scan(block_counts, B, k, seg, cluster_start, seg_start, cnt, nullptr, 1, 1, scan_lds, st);
   DALGO_LAUNCH_CHECK();
   if (k <= kScKmax)   // per-row LDS-cursor scatter only where the chunked form's LDS ends
     launch_scatter_chunked(k, B, st, assign, n, rpc, k,
@@ -1896,8 +1929,8 @@ hipError_t dalgo_kmeans_move_sorted(const void* X, int is_bf16, int64_t ldx, int
   hipLaunchKernelGGL(kmeans_hist_kernel, dim3(B), dim3(256), lds_k, st, (const int*)ec, n2, rpc, k,
                      block_counts, mdev, 2, chunk);
   DALGO_LAUNCH_CHECK();
-  hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), 2 * lds_k, st, block_counts, B, k, seg,
-                     cluster_start, seg_start, (unsigned long long*)nullptr, mdev, 2, chunk);
+  launch_sort_scan(block_counts, B, k, seg, cluster_start, seg_start, nullptr, mdev, 2, chunk, 2 * lds_k,
+                   st);
   DALGO_LAUNCH_CHECK();
   launch_scatter_chunked(k, B, st, (const int*)ec, n2,
                      rpc, k, (const int*)block_counts, (const int64_t*)cluster_start, perm, mdev, 2,
@@ -2032,8 +2065,8 @@ hipError_t dalgo_kmeans_sort_active(const int32_t* acl, const int32_t* idx, int6
   hipLaunchKernelGGL(kmeans_hist_kernel, dim3(B), dim3(256), lds_k, st, (const int*)acl, cap, rpc, k,
                      block_counts, n_active, 1, chunk);
   DALGO_LAUNCH_CHECK();
-  hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), 2 * lds_k, st, block_counts, B, k,
-                     1 << 20, cstart, seg_start, (unsigned long long*)nullptr, n_active, 1, chunk);
+  launch_sort_scan(block_counts, B, k, 1 << 20, cstart, seg_start, nullptr, n_active, 1, chunk, 2 * lds_k,
+                   st);
   DALGO_LAUNCH_CHECK();
   launch_scatter_chunked(k, B, st, (const int*)acl, cap,
                      rpc, k, (const int*)block_counts, (const int64_t*)cstart, (int*)rows_sorted,
