@@ -69,7 +69,19 @@ def parse(argv=None):
                          "candidate form is raced once it is spent")
     ap.add_argument("--pg-timeout-s", type=float, default=120.0,
                     help="process-group timeout: an RCCL collective stuck longer aborts the rank")
-    ap.add_argument("--deadline-s", type=float, default=420.0,
+    ap.add_argument("--secondary", default="auto", choices=["auto", "on", "off"],
+                    help="after the headline, the BMUF / EASGD, k-means and PageRank jobs "
+                         "(BASELINE configs #3-#5) under a 'secondary' key of the same JSON "
+                         "line; auto = on for one GPU")
+    ap.add_argument("--secondary-budget-s", type=float, default=240.0,
+                    help="no further secondary config starts once this much wall clock is spent")
+    ap.add_argument("--secondary-steps", type=int, default=20)
+    ap.add_argument("--secondary-warmup", type=int, default=5)
+    ap.add_argument("--km-rows", type=int, default=100_000_000)
+    ap.add_argument("--km-hard-noise", type=float, default=4.0,
+                    help="blob noise of the overlapping-cluster k-means run")
+    ap.add_argument("--pr-scale", type=int, default=26)
+    ap.add_argument("--deadline-s", type=float, default=540.0,
                     help="wall-clock deadline per rank: past it the rank prints its stacks and "
                          "exits 124 (a hang becomes a fast, rank-tagged failure); 0 = off")
     return ap.parse_args(argv)
@@ -135,6 +147,11 @@ def calibrate_launch(model, rt, a) -> dict:
             model.graph, model._okg = False, None
             model._graphs.clear()
             model._ok1, model._okp = False, False
+            # a form that raised after K1 ran can leave partial sums in [g || count]:
+            # clear it, and tell the next gradient launch the bucket is not known zero
+            if hasattr(model, "bucket"):
+                model.bucket.buffer.zero_()
+            model._g_zero = False
             try:
                 comm.check_device_errors(f"launch calibration ({name})")
             except comm.DeviceCollectiveError:
@@ -164,6 +181,11 @@ def calibrate_launch(model, rt, a) -> dict:
             rt.synchronize()
             return {"failed": name, **res}
     timed = {k: v for k, v in res.items() if k in cands and v is not None}
+    if not timed:   # every form raised: keep the plain per-step form
+        fallback_plain(model, rt, "launch calibration (no form ran)")
+        model.load_state_dict(snap)
+        rt.synchronize()
+        return {"failed": "all", **res}
     best = min(timed, key=timed.get)
     model._ok1, model._okp, graph = cands[best]
     model.graph, model._okg = graph, None
@@ -226,50 +248,32 @@ def allreduce_probe(model, rt, iters: int = 100) -> float | None:
     return float(el.item()) / iters * 1e6
 
 
-def main(argv=None):
-    argv = sys.argv[1:] if argv is None else list(argv)
-    a = parse(argv)
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    rc = self_launch(a, argv)
-    if rc is not None:
-        sys.exit(rc)
-    from dalgo.data.datasets import synthetic_logistic
+def run_lr(a, rt, data, layout, algo: str, steps: int, warmup: int, witness_steps: int,
+           calibrate: bool) -> dict:
+    """One LR-family configuration on the shared data: warmup, optional launch-form
+    calibration, EXACTLY ``steps`` timed training steps (barrier + synchronize on both
+    sides, MAX over ranks; sampled rows counted on the device), then the held-out witness
+    (untimed: training continues to ``witness_steps`` total steps)."""
     from dalgo.models.localsgd import ParallelSGD, SGDConfig
-    from dalgo.parallel import comm, runtime
-    from dalgo.parallel.sharding import make_layout
-
-    runtime.arm_watchdog(a.deadline_s, tag="bench")
-    rt = runtime.init(backend=a.backend, device=a.device, app_name="bench-ssgd",
-                      timeout_s=a.pg_timeout_s)
+    from dalgo.parallel import comm
     W = rt.world_size
-    from dalgo.parallel.launch import check_world
-    check_world(a.gpus, W, "bench")
-    dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
-    n_workers = W
-    layout = make_layout(a.rows, n_workers, W, rt.rank, spark_compatible=False)
-    t0 = time.time()
-    data = synthetic_logistic(a.rows, a.dim, row_range=(layout.row_lo, layout.row_hi),
-                              n_test=a.n_test if a.eval else 0, device=rt.device, dtype=dtype)
-    rt.synchronize()
-    gen_s = time.time() - t0
-    cfg = SGDConfig(algo=a.algo, n_workers=n_workers, frac=a.frac, eval_every=0,
-                    n_iterations=a.steps)
+    cfg = SGDConfig(algo=algo, n_workers=W, frac=a.frac, eval_every=0, n_iterations=steps)
     model = ParallelSGD(cfg, data, layout, rt)
     count = torch.zeros(1, dtype=torch.float64, device=rt.device)
-
     # model.run_steps(k): k full training steps, either k step() calls or (SSGD / GD with
     # DALGO_PERSISTENT=1) one persistent K1 launch running all k steps
     snap = model.state_dict()        # the untrained model: a fallback re-measures from here
-    model.run_steps(a.warmup)
+    model.run_steps(warmup)
     rt.synchronize()
-    cal = calibrate_launch(model, rt, a) if a.launch == "auto" else {}
+    cal = calibrate_launch(model, rt, a) if calibrate else {}
+
     def timed():
         rt.barrier()
         rt.synchronize()
         count.zero_()
         model.count_acc = count
         t_start = time.perf_counter()
-        model.run_steps(a.steps)
+        model.run_steps(steps)
         rt.synchronize()
         rt.barrier()
         rt.synchronize()
@@ -279,7 +283,7 @@ def main(argv=None):
         return el_, n_
 
     elapsed, samples = timed()
-    if os.environ.get("DALGO_TEST_FORCE_DEVICE_ERROR") == str(rt.rank):
+    if os.environ.get("DALGO_TEST_FORCE_DEVICE_ERROR") == str(rt.rank) and calibrate:
         # test hook: as if a wait of the timed region timed out, and as a launch that
         # stopped early would, leave partial sums in the gradient bucket
         comm._forced_error = 1
@@ -294,7 +298,7 @@ def main(argv=None):
     except comm.DeviceCollectiveError:
         fallback_plain(model, rt, "the timed region")
         model.load_state_dict(snap)
-        model.run_steps(a.warmup)
+        model.run_steps(warmup)
         elapsed, samples = timed()
         comm.check_device_errors("bench (fallback)")
         fell_back = True
@@ -304,23 +308,25 @@ def main(argv=None):
             "one-kernel" if model._one_kernel() else "per-step"))
     allreduce = "xgmi-oneshot (K11)" if xg is not None else (
         f"{rt.backend}" if W > 1 else "none (1 rank)")
-
     el = torch.tensor([elapsed], dtype=torch.float64, device=rt.device)
     comm.all_reduce_max(el)
     elapsed = float(el.item())
-    value = samples / elapsed
-    ar_us = allreduce_probe(model, rt) if cfg.algo in ("ssgd", "gd") else None
-    acc = None
-    witness = None
+    out = {"value": samples / elapsed, "ms_per_step": elapsed / steps * 1e3, "steps": steps,
+           "warmup": warmup, "samples_counted": int(round(samples)),
+           "global_batch": int(round(samples / steps)), "launch": launch, "allreduce": allreduce,
+           "device_wait_fallback": fell_back}
+    if cal:
+        out["launch_calibration_ms_per_step"] = cal
+    out["allreduce_us_per_step"] = allreduce_probe(model, rt) if algo in ("ssgd", "gd") else None
     if a.eval:
-        # correctness witness (untimed): train on to the reference's 1500 iterations
-        # (ssgd.py:18, 93) and score the held-out split. The planted model's own accuracy
+        # correctness witness (untimed): train on to witness_steps (the reference's
+        # n_iterations) and score the held-out split. The planted model's own accuracy
         # on that split is the Bayes ceiling; a random w scores ~0.5. Passing needs at
         # least half the way from chance to the ceiling, which a broken gradient kernel
         # cannot reach (measured in f64 on 200k x 1024: 0.49 @100, 0.81 @1000, 0.83 @1500,
         # ceiling 0.83)
-        done = a.warmup + a.steps
-        extra = max(0, a.witness_steps - done)
+        done = warmup + steps
+        extra = max(0, witness_steps - done)
         model.run_steps(extra)
         rt.synchronize()
         comm.check_device_errors("witness training")
@@ -331,9 +337,114 @@ def main(argv=None):
         zs = d.X_test.float() @ ws[:a.dim] + ws[a.dim]
         bayes = float(((zs > 0).float() == d.y_test).float().mean().item())
         thr = 0.5 + 0.5 * (bayes - 0.5)
-        witness = {"heldout_accuracy": acc, "heldout_logloss": loss, "n_test": a.n_test,
-                   "trained_steps": done + extra, "planted_model_accuracy": bayes,
-                   "threshold": thr, "passed": bool(acc >= thr)}
+        out["correctness_witness"] = {
+            "heldout_accuracy": acc, "heldout_logloss": loss, "n_test": a.n_test,
+            "trained_steps": done + extra, "planted_model_accuracy": bayes,
+            "threshold": thr, "passed": bool(acc >= thr)}
+    del model
+    return out
+
+
+# what the secondary witnesses train to: the reference's iteration counts (ssgd.py:18,
+# easgd.py:20), except MA / BMUF at 1500 rounds instead of 300 (ma.py:20, bmuf.py:20):
+# BMUF's random initial block-momentum buffer (bmuf.py:95) adds sum_t 0.9^t Delta_0 =
+# 10 Delta_0, Delta_0 ~ U[-1, 1), to every weight; at D = 1024 that takes more than 300
+# rounds to train away (held-out 0.56 at 300 rounds, 0.83 at 1500 on one MI355X)
+REF_ITERS = {"ssgd": 1500, "gd": 1500, "ma": 1500, "bmuf": 1500, "easgd": 1500}
+
+
+def run_secondary(a, rt, data, layout) -> dict:
+    """BASELINE configs #3-#5 after the headline, inside a wall-clock budget: BMUF and
+    EASGD on the headline's data (exact sampled-row counts, held-out witness at the
+    reference's iteration counts), then -- with the LR data freed -- the k-means job
+    (100M x 128, k = 1024; also on overlapping clusters) and the PageRank job (R-MAT scale
+    26). A config whose start would come after the budget is recorded as skipped; a
+    config that raises is recorded with its error (and fails the run)."""
+    from dalgo.apps import jobs
+    t0 = time.perf_counter()
+    res = {}
+
+    def budget_left():
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=rt.device)
+        from dalgo.parallel import comm
+        comm.all_reduce_max(el)
+        return a.secondary_budget_s - float(el.item())
+
+    def attempt(name, fn):
+        if budget_left() <= 0:
+            res[name] = {"skipped": f"secondary budget {a.secondary_budget_s:.0f} s spent"}
+            return
+        ts = time.perf_counter()
+        try:
+            r = fn()
+        except Exception as e:   # noqa: BLE001 -- recorded; the run then exits non-zero
+            import traceback
+            traceback.print_exc()
+            r = {"error": repr(e)}
+        r["wall_s"] = time.perf_counter() - ts
+        res[name] = r
+        if rt.device.type == "cuda":
+            torch.cuda.empty_cache()
+
+    for algo in ("bmuf", "easgd"):
+        attempt(algo, lambda algo=algo: dict(
+            run_lr(a, rt, data, layout, algo, a.secondary_steps, a.secondary_warmup,
+                   REF_ITERS[algo], calibrate=False),
+            metric=f"samples/sec (whole node) {algo.upper()} logistic regression",
+            unit="samples/s", config={"model": f"{algo.upper()} logistic regression",
+                                      "rows": a.rows, "features": a.dim,
+                                      "minibatch_fraction": a.frac,
+                                      "parallelism": f"dp{rt.world_size}"}))
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    attempt("kmeans", lambda: jobs.kmeans_job(rt, a.km_rows, 128, 1024, 5, dtype=dt))
+    attempt("kmeans_overlapping", lambda: jobs.kmeans_job(rt, a.km_rows, 128, 1024, 5, dtype=dt,
+                                                          noise=a.km_hard_noise, warm=False))
+    attempt("pagerank", lambda: jobs.pagerank_job(rt, a.pr_scale, 16, 10))
+    return res
+
+
+def secondary_failed(sec: dict) -> list:
+    bad = []
+    for k, v in sec.items():
+        if "error" in v:
+            bad.append(f"{k}: {v['error']}")
+        w = v.get("correctness_witness")
+        if w is not None and not w.get("passed", False):
+            bad.append(f"{k}: witness failed")
+    return bad
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    a = parse(argv)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    rc = self_launch(a, argv)
+    if rc is not None:
+        sys.exit(rc)
+    from dalgo.data.datasets import synthetic_logistic
+    from dalgo.parallel import runtime
+    from dalgo.parallel.sharding import make_layout
+
+    runtime.arm_watchdog(a.deadline_s, tag="bench")
+    rt = runtime.init(backend=a.backend, device=a.device, app_name="bench-ssgd",
+                      timeout_s=a.pg_timeout_s)
+    W = rt.world_size
+    from dalgo.parallel.launch import check_world
+    check_world(a.gpus, W, "bench")
+    dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    layout = make_layout(a.rows, W, W, rt.rank, spark_compatible=False)
+    t0 = time.time()
+    data = synthetic_logistic(a.rows, a.dim, row_range=(layout.row_lo, layout.row_hi),
+                              n_test=a.n_test if a.eval else 0, device=rt.device, dtype=dtype)
+    rt.synchronize()
+    gen_s = time.time() - t0
+    head = run_lr(a, rt, data, layout, a.algo, a.steps, a.warmup, a.witness_steps,
+                  calibrate=a.launch == "auto")
+    sec_on = a.secondary == "on" or (a.secondary == "auto" and W == 1
+                                     and rt.device.type == "cuda")
+    sec = run_secondary(a, rt, data, layout) if sec_on else None
+    value = head["value"]
+    witness = head.get("correctness_witness")
     if rt.is_main:
         out = {
             "metric": BASELINE_METRIC,
@@ -342,23 +453,23 @@ def main(argv=None):
             "n_gpus": W,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": elapsed / a.steps * 1e3,
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": a.dtype,
             "data": f"synthetic (on-device Philox planted logistic model, {a.rows}x{a.dim}, random-init w)",
-            "config": {"model": f"{a.algo.upper()} logistic regression", "global_batch": int(round(samples / a.steps)),
+            "config": {"model": f"{a.algo.upper()} logistic regression", "global_batch": head["global_batch"],
                        "seq_len": None, "features": a.dim, "rows": a.rows,
                        "minibatch_fraction": a.frac, "parallelism": f"dp{W}",
-                       "allreduce": allreduce, "launch": launch},
-            "samples_counted": int(round(samples)),
+                       "allreduce": head["allreduce"], "launch": head["launch"]},
+            "samples_counted": head["samples_counted"],
             "per_gpu_samples_per_s": value / W,
             "effective_hbm_GBps_per_gpu": value / W * a.dim * (2 if dtype == torch.bfloat16 else 4) / 1e9,
             "datagen_s": gen_s,
         }
-        if cal:
-            out["launch_calibration_ms_per_step"] = cal
+        if "launch_calibration_ms_per_step" in head:
+            out["launch_calibration_ms_per_step"] = head["launch_calibration_ms_per_step"]
         from dalgo.parallel import xgmi
         out["world_size"] = W
         out["device_ids"] = list(rt.device_ids)
@@ -371,17 +482,22 @@ def main(argv=None):
             except Exception:
                 out["rccl_version"] = None
         out["small_allreduce_race"] = xgmi.last_race
-        out["device_wait_fallback"] = fell_back
-        out["allreduce_us_per_step"] = ar_us
+        out["device_wait_fallback"] = head["device_wait_fallback"]
+        out["allreduce_us_per_step"] = head["allreduce_us_per_step"]
         if witness is not None:
-            out["heldout_accuracy"] = acc
+            out["heldout_accuracy"] = witness["heldout_accuracy"]
             out["correctness_witness"] = witness
+        if sec is not None:
+            out["secondary"] = sec
         print(json.dumps(out), flush=True)
     runtime.shutdown()
     runtime.arm_watchdog(0)
     if witness is not None and not witness["passed"]:
-        raise SystemExit(f"[bench] correctness witness failed: held-out accuracy {acc:.4f} < "
-                         f"{witness['threshold']:.4f}")
+        raise SystemExit(f"[bench] correctness witness failed: held-out accuracy "
+                         f"{witness['heldout_accuracy']:.4f} < {witness['threshold']:.4f}")
+    bad = secondary_failed(sec or {})
+    if bad:
+        raise SystemExit("[bench] secondary config failed: " + "; ".join(bad))
 
 
 if __name__ == "__main__":

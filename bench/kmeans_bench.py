@@ -22,53 +22,10 @@ import argparse
 import json
 import os
 import sys
-import time
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-
-
-def witness_check(km, rt):
-    """One more (untimed) iteration, checked against brute force and a full K3 pass."""
-    from dalgo.ops import kmeans as K
-    k, d = km.cfg.k, km.d
-    cq = km.cen.Cq.clone()                     # the centres the next assignment uses
-    km.step()
-    rt.synchronize()
-    cen_used = K.make_centers(cq[:k, :d].float(), km.X.dtype, rt.device, kpad=cq.shape[0])
-    a_full = K.assign(km.X, cen_used)
-    diff = (a_full != km.assign).nonzero().flatten()
-    agree = 1.0 - diff.numel() / max(1, km.X.shape[0])
-    Xd = km.X[diff, :d].double()
-    Cd = cq[:k, :d].double()
-    gap = ((Xd - Cd[km.assign[diff].long()]).pow(2).sum(1) -
-           (Xd - Cd[a_full[diff].long()]).pow(2).sum(1)).abs()
-    max_gap = float(gap.max().item()) if diff.numel() else 0.0
-    # slack of a kernel distance: keys truncate 5 mantissa bits of 0.5|x-c|^2 + M
-    xmax = 0.0
-    for s0 in range(0, km.X.shape[0], 1 << 22):   # chunked: no 100M x 128 f32 temporary
-        xmax = max(xmax, float((km.X[s0:s0 + (1 << 22), :d].float().pow(2).sum(1).max() * 0.5).item()))
-    slack = 2.0 * (xmax * 1.0001 + 1e-6) * 2.0 ** -14 * 2.0
-    S_ref = torch.zeros_like(km.S)
-    c_ref = torch.zeros_like(km.cnt)
-    K.accumulate(km.X, km.assign, k, km.DP, S_ref, c_ref)
-    if km.incremental:
-        S_m, c_m = km._S64, km._cnt64           # this rank's maintained local sums
-    else:
-        from dalgo.parallel import comm         # the full path keeps only the global sums
-        comm.all_reduce_sum(S_ref)
-        comm.all_reduce_sum(c_ref)
-        S_m, c_m = km.S.double(), km.cnt
-    err = float(((S_ref.double() - S_m.double()).abs().max() /
-                 (1.0 + S_ref.double().abs().max())).item())
-    counts_equal = bool(torch.equal(c_ref, c_m))
-    return {"iteration": km.t, "path": "bounds" if km.bounds else (
-                "incremental" if km.incremental else "full"),
-            "assignment_agreement_vs_brute_force": agree, "disagreements": int(diff.numel()),
-            "max_disagreement_gap": max_gap, "distance_slack": slack,
-            "counts_equal": counts_equal, "sums_max_rel_err": err,
-            "passed": bool(agree > 0.999 and max_gap <= slack and counts_equal and err < 1e-4)}
 
 
 def main():
@@ -88,6 +45,9 @@ def main():
                     help="filtered iterations without the candidate-pruned K2 tiles")
     ap.add_argument("--no-bound-filter", action="store_true",
                     help="plain (full K2 every iteration) Lloyd with the incremental K3")
+    ap.add_argument("--noise", type=float, default=1.0,
+                    help="blob noise (1 = well separated; 4 = overlapping clusters, the hard case "
+                         "for the bound filters)")
     ap.add_argument("--deadline-s", type=float, default=420.0)
     argv = sys.argv[1:]
     a = ap.parse_args(argv)
@@ -95,92 +55,22 @@ def main():
     rc = self_launch(a.gpus, __file__, argv, device=a.device, backend=a.backend, tag="kmeans_bench")
     if rc is not None:
         sys.exit(rc)
-    from dalgo.data.synthetic import blobs
-    from dalgo.models.kmeans import KMeans, KMeansConfig
-    from dalgo.parallel import comm, runtime
-    from dalgo.parallel.sharding import even_slices
+    from dalgo.apps.jobs import kmeans_job
+    from dalgo.parallel import runtime
     runtime.arm_watchdog(a.deadline_s, tag="kmeans_bench")
     rt = runtime.init(backend=a.backend, device=a.device, app_name="kmeans-bench", timeout_s=120)
-    W = rt.world_size
-    check_world(a.gpus, W, "kmeans_bench")
-    lo, hi = even_slices(a.rows, W)[rt.rank]
+    check_world(a.gpus, rt.world_size, "kmeans_bench")
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
-    cuda = rt.device.type == "cuda"
-
-    # process warm-up (separate, small model; discarded)
-    wn = min(1_000_000, a.rows)
-    wlo, whi = even_slices(wn, W)[rt.rank]
-    Xw = blobs(wn, a.dim, a.k, row_range=(wlo, whi), device=rt.device, dtype=dtype, seed=3)
-    kw = KMeans(KMeansConfig(k=min(a.k, wn), n_iterations=2, seed=5), Xw, wlo, wn)
-    kw.step()
-    kw.step()
-    del kw, Xw
-
-    t0 = time.time()
-    X = blobs(a.rows, a.dim, a.k, row_range=(lo, hi), device=rt.device, dtype=dtype, seed=7)
-    rt.synchronize()
-    gen = time.time() - t0
-
-    def ev():
-        if not cuda:
-            return time.perf_counter()
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        return e
-
-    def span(e0, e1):
-        return (e1 - e0) * 1e3 if not cuda else e0.elapsed_time(e1)
-
-    rt.barrier()
-    rt.synchronize()
-    t = time.perf_counter()
-    marks = [ev()]
-    km = KMeans(KMeansConfig(k=a.k, n_iterations=a.iters, seed=1,
-                             bound_filter=not a.no_bound_filter,
-                             candidates=not a.no_candidates), X, lo, a.rows)
-    marks.append(ev())
-    for _ in range(a.iters):
-        km.step()
-        marks.append(ev())
-    rt.synchronize()
-    rt.barrier()
-    rt.synchronize()
-    el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=rt.device)
-    comm.all_reduce_max(el)
-    job_ms = float(el.item()) * 1e3
-    init_ms = span(marks[0], marks[1])
-    iter_ms = [span(marks[i], marks[i + 1]) for i in range(1, len(marks) - 1)]
-    sse_last = km.sse.clone()
-    comm.all_reduce_sum(sse_last)
-    active = km.active_history
-    moved = km.changed_history
-    witness = None if a.no_witness else witness_check(km, rt)
-    flops = 2.0 * a.rows * a.k * a.dim
+    out = kmeans_job(rt, a.rows, a.dim, a.k, a.iters, dtype=dtype, noise=a.noise,
+                     bound_filter=not a.no_bound_filter, candidates=not a.no_candidates,
+                     witness=not a.no_witness)
     if rt.is_main:
-        steady = iter_ms[1:]
-        print(json.dumps({
-            "metric": "k-means points/sec (whole node)",
-            "measured": f"reference job: init + {a.iters} Lloyd iterations, iteration 1 included",
-            "value": a.rows * a.iters / (job_ms / 1e3), "unit": "points/s", "n_gpus": W,
-            "job_ms": job_ms, "ms_per_iter": job_ms / a.iters, "iterations": a.iters,
-            "init_ms_rank0": init_ms, "iteration_ms_rank0": iter_ms,
-            "first_iteration_ms_rank0": iter_ms[0] if iter_ms else None,
-            "steady_ms_per_iter_rank0": sum(steady) / len(steady) if steady else None,
-            "full_pass_tflops_per_gpu": (flops / W / (iter_ms[0] / 1e3) / 1e12) if iter_ms else None,
-            "reassigned_rows_per_iter_rank0": active, "moved_rows_per_iter_rank0": moved,
-            "bound_filter": km.bounds, "candidate_pruning": getattr(km, "_cand", None) is not None,
-            "incremental_k3": km.incremental,
-            "sse_last_iteration": float(sse_last.item()),
-            "correctness_witness": witness,
-            "config": {"rows": a.rows, "dim": a.dim, "k": a.k, "dtype": a.dtype,
-                       "init": "takeSample-style: k distinct seeded rows (k-means.py:53)"},
-            "timing": "model construction + iterations 1..%d inside the clock (MAX over ranks); "
-                      "process warmed up on a separate 1M-row model" % a.iters,
-            "datagen_s": gen}), flush=True)
+        print(json.dumps(out), flush=True)
     runtime.shutdown()
     runtime.arm_watchdog(0)
-    if witness is not None and not witness["passed"]:
-        raise SystemExit(f"[kmeans_bench] correctness witness failed: {witness}")
+    w = out["correctness_witness"]
+    if w is not None and not w["passed"]:
+        raise SystemExit(f"[kmeans_bench] correctness witness failed: {w}")
 
 
 if __name__ == "__main__":

@@ -1670,10 +1670,70 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   for (int c = tid; c < kpad; c += NT) s_hn16[c] = hn[c] + M;
   issue(0);
 
-  int bkey[PG], bch[PG];
+  int bkey[PG], bch[PG], cm[PG];
 #pragma unroll
-  for (int g = 0; g < PG; ++g) { bkey[g] = 0x7fffffff; bch[g] = 0; }
+  for (int g = 0; g < PG; ++g) { bkey[g] = 0x7fffffff; bch[g] = 0; cm[g] = 0x7fffffff; }
   const int kmask = ~31;
+  // software pipeline over the 8 sub-tiles of a chunk: sub-tile s accumulates into set
+  // s & 1 while the argmin of sub-tile s - 1 reads the other set, so the argmin VALU runs
+  // between the MFMAs instead of after them (sched_group_barrier pins the interleave);
+  // sub-tile 7's argmin and the chunk merge run under the next chunk's sub-tile 0. The
+  // pending set starts as +huge keys, so the first chunk's merge of "chunk -1" is inert.
+  f32x4 acc[2][PG];
+#pragma unroll
+  for (int g = 0; g < PG; ++g) {
+    const float big = __int_as_float(0x7f7fffff);
+    acc[1][g] = {big, big, big, big};
+  }
+  auto load_frag = [&](const uint4* img, int ch, int sub, uint4 (&af)[KS], float4& h4) {
+    const int row = sub * 16 + pl;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) af[s] = img[row * NJ + ((4 * s + lg) ^ (row & SWZ))];
+    h4 = *reinterpret_cast<const float4*>(&s_hn16[ch * CH + sub * 16 + 4 * lg]);
+  };
+  auto mfma_sub = [&](f32x4 (&ac)[PG], const uint4 (&af)[KS], const float4& h4) {
+    const f32x4 c0 = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+    for (int g = 0; g < PG; ++g)
+      ac[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[0]),
+                                                      __builtin_bit_cast(bf16x8, bf[g][0]), c0, 0, 0, 0);
+#pragma unroll
+    for (int s = 1; s < KS; ++s)
+#pragma unroll
+      for (int g = 0; g < PG; ++g)
+        ac[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[s]),
+                                                        __builtin_bit_cast(bf16x8, bf[g][s]), ac[g], 0, 0, 0);
+  };
+  // keys = value bits & ~31 | (sub * 4 + r): the lowest id wins among equal keys of a chunk
+  auto argmin_sub = [&](const f32x4 (&ac)[PG], int sub) {
+#pragma unroll
+    for (int g = 0; g < PG; ++g) {
+      const int k0 = (__float_as_int(ac[g][0]) & kmask) | (sub * 4 + 0);
+      const int k1 = (__float_as_int(ac[g][1]) & kmask) | (sub * 4 + 1);
+      const int k2 = (__float_as_int(ac[g][2]) & kmask) | (sub * 4 + 2);
+      const int k3 = (__float_as_int(ac[g][3]) & kmask) | (sub * 4 + 3);
+      cm[g] = min(min(cm[g], k0), k1);
+      cm[g] = min(min(cm[g], k2), k3);
+    }
+  };
+  // interleave: 24 MFMAs of this sub-tile, the previous sub-tile's 36 argmin VALU ops
+  // (1.5 per MFMA: inside the 8 issue cycles a 16x16x32 MFMA leaves free) and the next
+  // sub-tile's 5 fragment reads early in the group
+  auto pin = [&]() {
+#ifndef KM_XP_NOPIN
+#pragma unroll
+    for (int i = 0; i < KS * PG; i += 2) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                 // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);                 // VALU
+      if (i < 5) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);      // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+      if (i + 1 < 5) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+#endif
+  };
+  uint4 a[KS], an[KS];
+  float4 h4, hn4;
   for (int ch = 0; ch < nchunk; ++ch) {
     km_wait_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1681,55 +1741,41 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
     asm volatile("" ::: "memory");
     if (ch + 1 < nchunk) issue(ch + 1);
     const uint4* img = s_c + (ch % NBUF) * CHP;
-    int cm[PG];
-#pragma unroll
-    for (int g = 0; g < PG; ++g) cm[g] = 0x7fffffff;
-    // the next sub-tile's fragments are read under the current one's MFMAs; the PG
-    // accumulators advance k-step by k-step (independent chains in flight)
-    auto load_frag = [&](int sub, uint4 (&a)[KS], float4& h4) {
-      const int row = sub * 16 + pl;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) a[s] = img[row * NJ + ((4 * s + lg) ^ (row & SWZ))];
-      h4 = *reinterpret_cast<const float4*>(&s_hn16[ch * CH + sub * 16 + 4 * lg]);
-    };
-    uint4 a[KS];
-    float4 h4;
-    load_frag(0, a, h4);
-#pragma unroll
-    for (int sub = 0; sub < NSUB; ++sub) {
-      uint4 an[KS];
-      float4 hn4;
-      if (sub + 1 < NSUB) load_frag(sub + 1, an, hn4);
-      f32x4 acc[PG];
-#pragma unroll
-      for (int g = 0; g < PG; ++g) acc[g] = {h4.x, h4.y, h4.z, h4.w};
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int g = 0; g < PG; ++g)
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[s]),
-                                                          __builtin_bit_cast(bf16x8, bf[g][s]), acc[g], 0, 0, 0);
-#pragma unroll
-      for (int g = 0; g < PG; ++g) {
-        const int k0 = (__float_as_int(acc[g][0]) & kmask) | (sub * 4 + 0);
-        const int k1 = (__float_as_int(acc[g][1]) & kmask) | (sub * 4 + 1);
-        const int k2 = (__float_as_int(acc[g][2]) & kmask) | (sub * 4 + 2);
-        const int k3 = (__float_as_int(acc[g][3]) & kmask) | (sub * 4 + 3);
-        cm[g] = min(min(cm[g], min(k0, k1)), min(k2, k3));
-      }
-      if (sub + 1 < NSUB) {
-#pragma unroll
-        for (int s = 0; s < KS; ++s) a[s] = an[s];
-        h4 = hn4;
-      }
-    }
+    load_frag(img, ch, 0, a, h4);
+    __builtin_amdgcn_sched_barrier(0);
+    // sub-tile 0 under the previous chunk's sub-tile 7 argmin, then the merge of that chunk
+    load_frag(img, ch, 1, an, hn4);
+    mfma_sub(acc[0], a, h4);
+    argmin_sub(acc[1], 7);
+    pin();
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int g = 0; g < PG; ++g) {
       // across chunks on the value bits only (strict: the earlier chunk keeps a tie)
       const bool take = (cm[g] & kmask) < (bkey[g] & kmask);
       bkey[g] = take ? cm[g] : bkey[g];
-      bch[g] = take ? ch : bch[g];
+      bch[g] = take ? ch - 1 : bch[g];
+      cm[g] = 0x7fffffff;
     }
+#pragma unroll
+    for (int sub = 1; sub < NSUB; ++sub) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a[s] = an[s];
+      h4 = hn4;
+      if (sub + 1 < NSUB) load_frag(img, ch, sub + 1, an, hn4);
+      mfma_sub(acc[sub & 1], a, h4);
+      argmin_sub(acc[(sub - 1) & 1], sub - 1);
+      pin();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // the last chunk's sub-tile 7 and merge
+  argmin_sub(acc[1], 7);
+#pragma unroll
+  for (int g = 0; g < PG; ++g) {
+    const bool take = (cm[g] & kmask) < (bkey[g] & kmask);
+    bkey[g] = take ? cm[g] : bkey[g];
+    bch[g] = take ? nchunk - 1 : bch[g];
   }
 
   // ---- merge the 4 lane groups of each point, write the outputs
@@ -1768,13 +1814,18 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   }
 }
 
+// the 16x16x32 form holds two 32 KB centre chunks plus 0.5|c|^2 for every centre in LDS
+// and runs two blocks per CU: it takes kpad <= 3840; larger k goes to the pipelined form
+static bool assign16_fits(int kpad) {
+  return kpad % 128 == 0 && 2 * 128 * 128 * 2 + (size_t)kpad * sizeof(float) + 1024 <= 80 * 1024;
+}
+
 static hipError_t launch_assign16(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                   const float* hn, int kpad, int* assign, float* mind, double* sse,
                                   int sse_mask, float* xh, unsigned* xmax, hipStream_t st) {
   constexpr int NW = 4, PG = 6, MINB = 2;
-  if (kpad % 128) return hipErrorInvalidValue;
+  if (!assign16_fits(kpad)) return hipErrorInvalidValue;
   const size_t dyn = (size_t)kpad * sizeof(float);
-  if (2 * 128 * 128 * 2 + dyn + 1024 > 80 * 1024) return hipErrorInvalidValue;   // 2 blocks per CU
   const int64_t grid = cdiv(n, (int64_t)NW * PG * 16);
   if (grid == 0) return hipSuccess;
   if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
@@ -1812,7 +1863,7 @@ static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const 
                                    int sse_mask, hipStream_t st) {
 #ifndef KM_XP_NO16
   if constexpr (sizeof(T) == 2 && DP == 128)
-    if (kpad % 128 == 0)
+    if (assign16_fits(kpad))
       return launch_assign16(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, nullptr, nullptr, st);
 #endif
   if constexpr (sizeof(T) == 2 && DP >= 64)
@@ -2018,7 +2069,7 @@ hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP
     return hipErrorInvalidValue;
   }
 #ifndef KM_XP_NO16
-  if (DP == 128 && idx == nullptr)
+  if (DP == 128 && idx == nullptr && assign16_fits(kpad))
     return launch_assign16(X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, aux.xh, aux.xmax, st);
 #endif
   if (DP == 128)

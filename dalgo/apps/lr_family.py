@@ -110,6 +110,7 @@ def main(algo: str, argv=None):
         if a.ckpt_dir and a.ckpt_every and m.t % a.ckpt_every == 0:
             checkpoint.save(m.state_dict(), a.ckpt_dir, ck_name, rt.rank, per_rank=True)
 
+    runtime.test_hang_point("fit")
     model.fit(remaining, verbose=not a.quiet, callback=cb)
     acc, _ = model.evaluate()
     rt.log("Final w: %s " % model.weights().double().cpu().numpy())

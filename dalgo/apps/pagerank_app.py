@@ -41,7 +41,7 @@ def degree_order(scale: int, edge_factor: int, rank: int, world: int, device, se
         if i % world != rank:
             continue
         s, _ = G.rmat_edges(min(chunk, n_edges - off), scale, seed=seed, e_off=off, device=device)
-        deg += torch.bincount(s.long(), minlength=n_vertices)
+        G.degree_count_(deg, s)
     comm.all_reduce_sum(deg)
     order = torch.argsort(-deg * n_vertices - torch.arange(n_vertices, device=device, dtype=torch.int64))
     return deal_ids(order, n_vertices, world).to(torch.int32)
@@ -71,23 +71,41 @@ def deal_ids(order: torch.Tensor, n_vertices: int, world: int) -> torch.Tensor:
     return new_id
 
 
-def rmat_shard(scale: int, edge_factor: int, rank: int, world: int, device, seed: int = 1,
-               chunk: int = 1 << 26, reorder: bool = True):
-    """Generate the global R-MAT stream in chunks, keep this rank's destinations.
-
-    reorder=True relabels vertices by descending out-degree (see degree_order);
-    PageRank values are invariant to the relabeling (map back with the returned
-    ``new_id`` if original ids are needed).
-    """
-    n_vertices = 1 << scale
-    n_edges = edge_factor * n_vertices
-    sl = G.vertex_slices(n_vertices, world)
-    v_lo, v_hi = rank * sl, min(n_vertices, (rank + 1) * sl)
-    new_id = degree_order(scale, edge_factor, rank, world, device, seed, chunk) if reorder else None
+def rmat_input(scale: int, edge_factor: int, device, seed: int = 1, chunk: int = 1 << 26):
+    """The whole R-MAT edge stream as a list of (src, dst) int32 chunks (the job's input:
+    the reference's ``parallelize(links)``, graph_computation/pagerank.py:35-38)."""
+    n_edges = edge_factor * (1 << scale)
     parts = []
     for off in range(0, n_edges, chunk):
-        m = min(chunk, n_edges - off)
-        s, d = G.rmat_edges(m, scale, seed=seed, e_off=off, device=device)
+        parts.append(G.rmat_edges(min(chunk, n_edges - off), scale, seed=seed, e_off=off,
+                                  device=device))
+    return parts, n_edges
+
+
+def degree_order_from(edges: list, scale: int, rank: int, world: int, device) -> torch.Tensor:
+    """:func:`degree_order` over a given chunk list (every rank counts chunks i % W == rank,
+    one all-reduce)."""
+    from dalgo.parallel import comm
+    n_vertices = 1 << scale
+    deg = torch.zeros(n_vertices, dtype=torch.int64, device=device)
+    for i, (s, _) in enumerate(edges):
+        if i % world == rank:
+            G.degree_count_(deg, s)
+    comm.all_reduce_sum(deg)
+    order = torch.argsort(-deg * n_vertices - torch.arange(n_vertices, device=device, dtype=torch.int64))
+    return deal_ids(order, n_vertices, world).to(torch.int32)
+
+
+def build_rmat_shard(edges: list, scale: int, rank: int, world: int, device, reorder: bool = True,
+                     seed: int = 1):
+    """This rank's shard of the given R-MAT edge chunks: optional degree relabeling, keep
+    the destinations of this rank's slice, sort + dedup (``distinct().groupByKey()``)."""
+    n_vertices = 1 << scale
+    sl = G.vertex_slices(n_vertices, world)
+    v_lo, v_hi = rank * sl, min(n_vertices, (rank + 1) * sl)
+    new_id = degree_order_from(edges, scale, rank, world, device) if reorder else None
+    parts = []
+    for s, d in edges:
         if new_id is not None:
             s = new_id[s.long()]
             d = new_id[d.long()]
@@ -96,6 +114,19 @@ def rmat_shard(scale: int, edge_factor: int, rank: int, world: int, device, seed
         del s, d
     shard = G.merge_shards(parts, v_lo, v_hi, n_vertices, sl)
     shard.new_id = new_id
+    return shard
+
+
+def rmat_shard(scale: int, edge_factor: int, rank: int, world: int, device, seed: int = 1,
+               chunk: int = 1 << 26, reorder: bool = True):
+    """Generate the global R-MAT stream, keep this rank's destinations.
+
+    reorder=True relabels vertices by descending out-degree (see degree_order);
+    PageRank values are invariant to the relabeling (map back with the returned
+    ``new_id`` if original ids are needed).
+    """
+    edges, n_edges = rmat_input(scale, edge_factor, device, seed, chunk)
+    shard = build_rmat_shard(edges, scale, rank, world, device, reorder=reorder, seed=seed)
     return shard, n_edges
 
 

@@ -14,8 +14,9 @@ On the GPU the first iteration is a full pass and every later one is incremental
 the sums are linear in the assignment, so only the points whose cluster changed are
 subtracted from their old and added to their new cluster's f64 local sums (counting-
 sorted signed entries, csrc/kernels/kmeans.hip km_dsegsum). With bf16 points (d in
-(32, 128], k <= 2048) the iterations after the first are also bound-filtered (Hamerly,
-exact): only the points the triangle inequality cannot prove unchanged go through K2.
+(32, 128], k <= 2048) the iterations after the first are also bound-filtered (Hamerly):
+only the points the triangle inequality cannot prove unchanged go through K2 (exact up
+to near-ties within the kernels' distance rounding, see KMeansConfig).
 Every count (active, moved rows) stays on the device -- the kernels that consume it
 read it there -- so an iteration issues its launches without a host sync.
 The reduceByKey shuffle + driver collect become one RCCL all-reduce whose size is
@@ -43,9 +44,18 @@ class KMeansConfig:
     init: str = "sample"       # "sample": k distinct random rows (takeSample) | "given"
     seed: int = 42             # takeSample(False, k, 42)
     tol: float | None = None   # convergeDist-style early stop (reference ignores it)
-    bound_filter: bool = True  # GPU bf16: Hamerly-filtered iterations after the first (exact)
+    bound_filter: bool = True  # GPU bf16: Hamerly-filtered iterations after the first
     candidates: bool = True    # ... whose K2 tiles (one cluster each) stream only the centres
-                               # near their cluster's centre (exact; k <= 1024)
+                               # near their cluster's centre (k <= 1024)
+    # GPU, k <= 2048: incremental K3 (only moved rows re-summed) and the bound-filter state.
+    # Costs ~24 B/row (move workspace) + ~48 B/row (bounds, candidates) of HBM on top of X
+    # (bf16 d = 128: X is 256 B/row); False = plain full-pass Lloyd, no per-row state
+    incremental: bool = True
+    # "Exact" for the filtered paths means: a row keeps its centre only when the triangle
+    # inequality proves it is still the closest, with the kernels' distance rounding
+    # (distance keys drop 5 mantissa bits of 0.5|x - c|^2 + M) folded into the bounds.
+    # Two K2 forms may still resolve a near-tie (distances equal within that slack,
+    # 2^-13 max|x|^2) differently; tests check every difference against the slack.
 
 
 @dataclass
@@ -92,8 +102,8 @@ class KMeans:
         # incremental K3 (GPU, k within the sorted-move kernels' LDS): f64 local sums /
         # counts of the last iteration; the move workspace is sized for every local row
         # moving, so the moved count never has to reach the host
-        self.incremental = self.dev.type == "cuda" and k <= 2048
-        # bound-filtered Lloyd (GPU, bf16, pipelined K2): exact -- a point is skipped only
+        self.incremental = self.dev.type == "cuda" and k <= 2048 and cfg.incremental
+        # bound-filtered Lloyd (GPU, bf16, pipelined K2): a point is skipped only
         # when the triangle inequality proves its centre is still the strictly closest
         self.bounds = (self.incremental and cfg.bound_filter and self.X.dtype == torch.bfloat16
                        and self.DP in (64, 128))
@@ -106,8 +116,9 @@ class KMeans:
             self._changed = torch.empty(max(n, 1), **i32)
             self._n_changed = torch.zeros(1, dtype=torch.int64, device=self.dev)
             self._mws = K.MoveWorkspace(self.dev, n, k)
-            # per-iteration device counters (read by the properties below, after the run)
-            self._hist = torch.zeros((64, 2), dtype=torch.int64, device=self.dev)
+            # per-iteration device counters (read by the properties below, after the run):
+            # [active rows, moved rows, 1 if the iteration was a full pass]
+            self._hist = torch.zeros((64, 3), dtype=torch.int64, device=self.dev)
             if self.bounds:
                 self._alloc_bounds()
             else:
@@ -178,17 +189,19 @@ class KMeans:
 
     @property
     def changed_history(self) -> list:
-        """Rows whose cluster changed per incremental iteration."""
+        """Rows whose cluster changed per incremental iteration (full passes, which
+        have no previous assignment to compare with, are left out)."""
         if not self.incremental:
             return []
-        return [int(v) for v in self._hist[: self._hist_n, 1].tolist()][1:]
+        h = self._hist[: self._hist_n].tolist()
+        return [int(r[1]) for r in h if not r[2]]
 
     def clear_history(self):
         self._hist_n = 0
 
     # ------------------------------------------------------------------- iterations
     def _step_bounds(self):
-        """One Lloyd iteration with Hamerly's bounds (exact).
+        """One Lloyd iteration with Hamerly's bounds (exact up to near-ties).
 
         u[x] >= |x - c_a| and l[x] <= |x - c| for every other centre c, both for the
         centres of the previous assignment (K2 writes the best and the second-best
@@ -224,6 +237,7 @@ class KMeans:
                           self._xmax, n, self._ul, self._tol)
             self._record(0, n)
             self._record(1, 0)
+            self._record(2, 1)
             self._first = False
             self._just_full = True
         else:
@@ -257,6 +271,7 @@ class KMeans:
                 self.cnt.copy_(self._cnt64)
             self._record(0, self._n_active)
             self._record(1, self._n_changed)
+            self._record(2, 0)
             self._just_full = False
         self._hist_n += 1
         # local SSE on the (rounded) centres of this assignment
@@ -277,6 +292,7 @@ class KMeans:
                 self._S64.copy_(self.S)
                 self._cnt64.copy_(self.cnt)
             self._record(1, 0)
+            self._record(2, 1)
             self._first = False
         else:
             with self._ph("assign"):
@@ -290,6 +306,7 @@ class KMeans:
                 self.cnt.copy_(self._cnt64)
             self.assign, self._a_new = self._a_new, self.assign
             self._record(1, self._n_changed)
+            self._record(2, 0)
         self._hist_n += 1
 
     def step(self):

@@ -4,8 +4,9 @@ Destination-partitioned formulation: rank r owns vertex slice r and its in-edges
 iteration ONE collective exchange of contributions c[u] = r[u]/outdeg(u), then the SpMV
 and the fused rank/contribution epilogue. The SpMV on GPUs is K4b by default
 (csrc/kernels/pr_binned.hip: two-level propagation blocking, no random global access,
-exact fixed-point sums; 2.3x the pull K4 at R-MAT scale 26); the pull K4 (segmented wave
-reduction over gathered c[src]) and its XCD-partitioned form stay selectable. The exchange is
+exact fixed-point sums; 5x the pull K4 at R-MAT scale 26: 2.1 vs 10.8 ms per iteration,
+profiles/round4/r4_29); the pull K4 (segmented wave reduction over gathered c[src]) stays
+selectable. The exchange is
 either an all_gather of the full slices (half the bytes of an all-reduce of a full
 vector) or, by default on several ranks, a ghost exchange: each rank receives only the
 c[u] of the remote sources that actually have an edge into its slice (one uneven

@@ -125,6 +125,12 @@ def merge_shards(parts: list, v_lo, v_hi, n_vertices, sl, dedup=True) -> GraphSh
     return _shard_from_keys(keys, v_lo, v_hi, n_vertices, sl)
 
 
+def degree_count_(deg: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    """deg[v] += #occurrences of v in ids (int64 deg)."""
+    deg += torch.bincount(ids.long(), minlength=deg.numel())
+    return deg
+
+
 def local_outdeg(shard: GraphShard) -> torch.Tensor:
     """Out-degree contribution of this shard's edges (sum over ranks = global out-degree)."""
     s = shard.src[: shard.n_edges].to(torch.int64)

@@ -26,6 +26,9 @@ from dalgo.parallel import runtime
 
 
 def _active() -> bool:
+    # every collective wrapper enters through here: that is the progress beat the
+    # stall watchdog (runtime.arm_stall_watchdog) listens for
+    runtime.heartbeat()
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 

@@ -74,7 +74,7 @@ def _env_int(name: str, default: int) -> int:
 
 
 def init(backend: str | None = None, *, device: str | None = None, app_name: str = "dalgo",
-         timeout_s: float = 600.0) -> Runtime:
+         timeout_s: float = 120.0) -> Runtime:
     """Initialise (idempotent) and return the process runtime.
 
     backend: "nccl" (RCCL, GPU), "gloo" (CPU) or None = auto (nccl when a GPU is
@@ -186,10 +186,68 @@ def arm_watchdog(seconds: float, tag: str = "dalgo") -> None:
     _watchdog.start()
 
 
+_beat = [0.0]
+_stall = None
+
+
+def heartbeat() -> None:
+    """Progress beat (every collective wrapper in :mod:`dalgo.parallel.comm` calls it)."""
+    import time
+    _beat[0] = time.monotonic()
+
+
+def arm_stall_watchdog(seconds: float, tag: str = "dalgo") -> None:
+    """Progress deadline for this rank: if no :func:`heartbeat` arrives for ``seconds``
+    (every collective beats, so a multi-rank job beats at least once per iteration),
+    print a rank-tagged message plus every thread's Python stack and exit 124. Unlike
+    :func:`arm_watchdog` it bounds a hang without bounding the job's length. A second
+    call re-arms; ``seconds <= 0`` disarms."""
+    global _stall
+    import threading
+    import time
+    if _stall is not None:
+        _stall.set()
+        _stall = None
+    if seconds <= 0:
+        return
+    stop = threading.Event()
+    heartbeat()
+
+    def run():
+        while not stop.wait(min(1.0, seconds / 4)):
+            idle = time.monotonic() - _beat[0]
+            if idle > seconds:
+                import faulthandler
+                r = os.environ.get("RANK", "0")
+                print(f"[{tag}] rank {r}: no progress for {idle:.0f} s (stall deadline "
+                      f"{seconds:.0f} s); stacks follow, exiting 124", file=sys.stderr, flush=True)
+                faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+                sys.stderr.flush()
+                os._exit(124)
+
+    threading.Thread(target=run, daemon=True, name="dalgo-stall-watchdog").start()
+    _stall = stop
+
+
+def test_hang_point(where: str) -> None:
+    """Fault-injection hook of the hang tests: ``DALGO_TEST_HANG=<rank>:<where>`` makes
+    that rank stop making progress here (sleeps), as a rank stuck in a kernel would."""
+    spec = os.environ.get("DALGO_TEST_HANG")
+    if not spec:
+        return
+    r, _, w = spec.partition(":")
+    if r == os.environ.get("RANK", "0") and w == where:
+        import time
+        print(f"[dalgo] rank {r}: DALGO_TEST_HANG at {where}", file=sys.stderr, flush=True)
+        while True:
+            time.sleep(3600)
+
+
 def shutdown():
     """Tear down the process group (``spark.stop()`` equivalent)."""
     global _RT
     failed = False
+    arm_stall_watchdog(0)
     if dist.is_available() and dist.is_initialized():
         from dalgo.parallel import comm
         try:

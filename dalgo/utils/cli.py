@@ -22,6 +22,13 @@ def common_parser(description: str) -> argparse.ArgumentParser:
     ap.add_argument("--metrics-out", default=None, help="JSONL metrics file (rank 0)")
     ap.add_argument("--quiet", action="store_true", help="suppress per-iteration lines")
     ap.add_argument("--no-plot", action="store_true")
+    ap.add_argument("--pg-timeout-s", type=float, default=120.0,
+                    help="process-group timeout: a collective stuck longer raises on the rank")
+    ap.add_argument("--stall-timeout-s", type=float, default=300.0,
+                    help="multi-rank runs: a rank with no collective for this long prints its "
+                         "stacks and exits 124 (0 = off)")
+    ap.add_argument("--deadline-s", type=float, default=0.0,
+                    help="wall-clock deadline of the whole run, exit 124 past it (0 = off)")
     return ap
 
 
@@ -38,7 +45,13 @@ def init_from_args(a, app_name: str) -> runtime.Runtime:
     dev = None if a.device == "auto" else a.device
     if dev is None and a.backend == "gloo":
         dev = "cpu"
-    return runtime.init(backend=a.backend, device=dev, app_name=app_name)
+    timeout = getattr(a, "pg_timeout_s", 120.0)
+    if getattr(a, "deadline_s", 0.0) > 0:
+        runtime.arm_watchdog(a.deadline_s, tag=app_name)
+    rt = runtime.init(backend=a.backend, device=dev, app_name=app_name, timeout_s=timeout)
+    if rt.distributed and getattr(a, "stall_timeout_s", 0.0) > 0:
+        runtime.arm_stall_watchdog(a.stall_timeout_s, tag=app_name)
+    return rt
 
 
 def default_dtype(rt: runtime.Runtime, want: str | None = None) -> torch.dtype:

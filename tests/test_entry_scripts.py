@@ -127,6 +127,25 @@ def test_torchrun_two_ranks_gloo():
     assert out.count("Final acc:") == 1   # rank 0 prints only
 
 
+def test_torchrun_hung_rank_fails_fast():
+    """A rank that stops making progress ends a 2-rank gloo entry-script run non-zero
+    within the deadlines (process-group timeout on the waiting rank, stall watchdog on
+    the hung one) instead of hanging until torchrun is killed."""
+    import time
+    env = dict(os.environ, PYTHONPATH=ROOT, DALGO_TEST_HANG="1:fit")
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(_port()), "optimization/ssgd.py", "--device", "cpu",
+                        "--backend", "gloo", "--n-iterations", "20", "--quiet", "--no-plot",
+                        "--pg-timeout-s", "10", "--stall-timeout-s", "15"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    el = time.time() - t0
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert el < 120, el
+    assert "DALGO_TEST_HANG at fit" in r.stderr
+
+
 def test_checkpoint_resume(tmp_path):
     ck = str(tmp_path / "ck")
     full = _run(["optimization/easgd.py", "--device", "cpu", "--n-iterations", "40", "--quiet",

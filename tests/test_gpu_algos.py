@@ -17,7 +17,8 @@ pytestmark = pytest.mark.gpu
 # 128-centre chunks); f32 and small d the generic form
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("d,k,n", [(2, 2, 6), (16, 40, 3000), (50, 33, 4099), (64, 128, 513),
-                                   (100, 1500, 9000), (128, 600, 70001), (128, 1024, 20000)])
+                                   (100, 1500, 9000), (128, 600, 70001), (128, 1024, 20000),
+                                   (128, 4096, 20000)])
 def test_kmeans_assign_matches_reference(cuda, dtype, d, k, n):
     _check_assign(cuda, dtype, d, k, n)
 
@@ -837,9 +838,10 @@ def test_kmeans_assign_top2_second_best(cuda):
 
 
 def test_kmeans_bound_filter_exact(cuda):
-    """Bound-filtered Lloyd (default for bf16 on the GPU) == plain Lloyd: same SSE
-    trajectory (SSE via the Q identity vs the kernel's per-point sum), same counts; and
-    the filter actually skips most points once the centres settle."""
+    """Bound-filtered Lloyd (default for bf16 on the GPU): every step equals brute force
+    from the same state (near-ties within the rounding slack aside) with exact counts and
+    sums; SSE trajectory (Q identity) vs plain Lloyd; the filter skips most points once
+    the centres settle."""
     from dalgo.data.synthetic import blobs
     from dalgo.models.kmeans import KMeans, KMeansConfig
     n, d, k = 300_000, 128, 1000
@@ -851,12 +853,45 @@ def test_kmeans_bound_filter_exact(cuda):
     assert not b.bounds
     b.fit()
     assert np.allclose(a.history.sse, b.history.sse, rtol=2e-4), (a.history.sse, b.history.sse)
-    # the plain Lloyd passes run on the 16x16x32 K2, the filtered ones on the 32x32x16
-    # forms: the kernels round differently, so near-tie points of a 300-point cluster may
-    # land on the other centre (SSE agrees to 2e-4; most centres to 1e-2)
-    same = (a.centers - b.centers).abs().amax(dim=1) < 1e-2
-    assert same.float().mean().item() > 0.8
     assert a.active_history[0] == n and min(a.active_history[1:]) < 0.3 * n
+    # the oracle: every filtered step, from its own centres and bounds, against the
+    # brute-force full pass over the same centres (plus exact counts and sums)
+    c = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5, candidates=False), X, 0, n)
+    for _ in range(7):
+        _kmeans_step_oracle(c)
+
+
+def _kmeans_step_oracle(km):
+    """One step of ``km`` checked against brute force from the same state: the K2
+    assignment over the centres the step used differs from the full-pass K2 only at
+    near-ties (distance gap within the kernels' rounding slack), the counts equal a K3
+    pass over the step's assignment exactly and the maintained sums equal the f64 sums."""
+    from dalgo.ops import kmeans as K
+    k, d = km.cfg.k, km.d
+    cq = km.cen.Cq.clone()
+    km.step()
+    used = K.make_centers(cq[:k, :d].float(), km.X.dtype, km.dev, kpad=cq.shape[0])
+    a_full = K.assign(km.X, used)
+    diff = (a_full != km.assign).nonzero().flatten()
+    assert diff.numel() <= max(5, km.X.shape[0] // 2000), diff.numel()
+    if diff.numel():
+        Xd = km.X[diff, :d].double()
+        Cd = cq[:k, :d].double()
+        gap = ((Xd - Cd[km.assign[diff].long()]).pow(2).sum(1) -
+               (Xd - Cd[a_full[diff].long()]).pow(2).sum(1)).abs()
+        xmax = float((km.X[:, :d].float().pow(2).sum(1).max() * 0.5).item())
+        slack = 2.0 * (xmax * 1.0001 + 1e-6) * 2.0 ** -14 * 2.0
+        assert float(gap.max()) <= slack, (float(gap.max()), slack)
+    S_ref = torch.zeros_like(km.S)
+    c_ref = torch.zeros_like(km.cnt)
+    K.accumulate(km.X, km.assign, k, km.DP, S_ref, c_ref)
+    S_m = km._S64 if km.incremental else km.S.double()
+    c_m = km._cnt64 if km.incremental else km.cnt
+    assert torch.equal(c_ref, c_m)
+    S_ex = torch.zeros(k, km.DP, dtype=torch.float64, device=km.dev)
+    S_ex[:, :d].index_add_(0, km.assign.long(), km.X[:, :d].double())
+    rel = float(((S_m.double() - S_ex).abs().max() / (1.0 + S_ex.abs().max())).item())
+    assert rel < 1e-5, rel
 
 
 @pytest.mark.parametrize("k,d", [(1, 8), (37, 30), (1024, 128)])
@@ -1000,8 +1035,9 @@ def test_kmeans_assign_rows_candidates(cuda, d):
 
 
 def test_kmeans_candidates_match_plain(cuda):
-    """Filtered Lloyd with candidate-pruned tiles == without == plain Lloyd (SSE
-    trajectory, centres), and the pruned run re-assigns the same rows."""
+    """Filtered Lloyd with candidate-pruned tiles: every step equals brute force from
+    the same state (near-ties within the rounding slack aside); the SSE trajectories of
+    the pruned, bound-only and plain runs agree."""
     from dalgo.data.synthetic import blobs
     from dalgo.models.kmeans import KMeans, KMeansConfig
     n, d, k = 300_000, 128, 1000
@@ -1013,13 +1049,12 @@ def test_kmeans_candidates_match_plain(cuda):
         km.fit()
         runs[name] = km
     assert runs["cand"]._cand is not None and runs["bounds"]._cand is None
-    # the kernels round differently (per-tile distance offset M): near-tie points may
-    # land on the other centre, which moves a 300-point cluster's mean by > 1e-2 -- the
-    # SSE trajectories agree to 2e-4 and most centres to 1e-2
     for other in ("bounds", "plain"):
         assert np.allclose(runs["cand"].history.sse, runs[other].history.sse, rtol=2e-4)
-        same = (runs["cand"].centers - runs[other].centers).abs().amax(dim=1) < 1e-2
-        assert same.float().mean().item() > 0.8
-    # the pruned centres enter l as nd_first - u (looser): never fewer active rows
     ha, hb = runs["cand"].active_history, runs["bounds"].active_history
     assert ha[0] == n and len(ha) == len(hb)
+    # the oracle: every candidate-pruned step against brute force from the same state
+    c = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5), X, 0, n)
+    assert c._cand is not None
+    for _ in range(7):
+        _kmeans_step_oracle(c)
