@@ -485,7 +485,7 @@ static void check_ul(const Tensor& ul, int64_t n, const char* what) {
 
 void kmeans_filter(const Tensor& assign, Tensor ul, const Tensor& delta, const Tensor& s,
                    const std::optional<Tensor>& a_prev, Tensor idx, Tensor n_active,
-                   const std::optional<Tensor>& acl) {
+                   const std::optional<Tensor>& acl, const std::optional<Tensor>& nd, int64_t kpad) {
   const int64_t n = assign.numel();
   check_i32(assign, "assign");
   check_ul(ul, n, "kmeans_filter");
@@ -507,12 +507,19 @@ void kmeans_filter(const Tensor& assign, Tensor ul, const Tensor& delta, const T
     TORCH_CHECK(acl->numel() >= idx.numel(), "kmeans_filter: acl [cap]");
     aclp = acl->data_ptr<int32_t>();
   }
+  const float* ndp = nullptr;
+  if (nd.has_value()) {   // near / far keys for the candidate tiles
+    check_f32(*nd, "nd");
+    TORCH_CHECK(aclp != nullptr, "kmeans_filter: nd needs acl");
+    TORCH_CHECK(kpad >= delta.numel() && nd->numel() >= delta.numel() * kpad, "kmeans_filter: nd [k][kpad]");
+    ndp = nd->data_ptr<float>();
+  }
   DeviceGuard guard(assign.device());
   DALGO_CHECK_HIP(dalgo_km_filter(assign.data_ptr<int32_t>(), ul.data_ptr<float>(),
                                   delta.data_ptr<float>(), s.data_ptr<float>(), (int)delta.numel(), n,
                                   app, idx.data_ptr<int32_t>(),
                                   reinterpret_cast<unsigned long long*>(n_active.data_ptr<int64_t>()),
-                                  idx.numel(), aclp, cur_stream()),
+                                  idx.numel(), aclp, ndp, (int)kpad, cur_stream()),
                   "kmeans_filter");
 }
 
@@ -787,6 +794,176 @@ void rmat_edges(int64_t seed, int64_t scale, int64_t e_off, double a, double b, 
                              (float)c, scramble ? 1 : 0, src.data_ptr<int32_t>(),
                              dst.data_ptr<int32_t>(), cur_stream()),
                   "rmat_edges");
+}
+
+// ---- native PageRank adjacency build (graph_build.hip)
+inline void check_t(const Tensor& t, at::ScalarType st, const char* what) {
+  check_dev(t, what);
+  TORCH_CHECK(t.scalar_type() == st && t.is_contiguous(), "dalgo: ", what, " has the wrong dtype / layout");
+}
+template <typename T>
+inline T* opt_ptr(const std::optional<Tensor>& t) {
+  return t.has_value() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+void gb_degree(const Tensor& ids, Tensor deg) {
+  check_i32(ids, "ids");
+  check_i32(deg, "deg");
+  DeviceGuard guard(ids.device());
+  DALGO_CHECK_HIP(dalgo_gb_degree(ids.data_ptr<int32_t>(), ids.numel(),
+                                  reinterpret_cast<uint32_t*>(deg.data_ptr<int32_t>()), cur_stream()),
+                  "gb_degree");
+}
+
+// phase 0: counts[block] = kept edges, remote sources marked in bitmap; phase 1: keys
+void gb_keys(const Tensor& src, const Tensor& dst, const std::optional<Tensor>& new_id, int64_t v_lo,
+             int64_t v_hi, int64_t sl, int64_t world, int64_t rank, int64_t dbits, int64_t phase,
+             const std::optional<Tensor>& bitmap, const std::optional<Tensor>& counts,
+             const std::optional<Tensor>& offsets, int64_t base_all, const std::optional<Tensor>& keys,
+             const std::optional<Tensor>& word_prefix, const std::optional<Tensor>& seg_start,
+             const std::optional<Tensor>& seg_blk0) {
+  check_i32(src, "src");
+  check_i32(dst, "dst");
+  TORCH_CHECK(src.numel() == dst.numel(), "gb_keys: src / dst size");
+  const int64_t n = src.numel();
+  const int64_t nb = dalgo_gb_key_blocks(n);
+  if (new_id) check_i32(*new_id, "new_id");
+  if (world > 1) {
+    TORCH_CHECK(bitmap.has_value(), "gb_keys: bitmap needed at world > 1");
+    check_i32(*bitmap, "bitmap");
+  }
+  if (phase == 0) {
+    TORCH_CHECK(counts.has_value() && counts->numel() >= nb, "gb_keys: counts [blocks]");
+    check_i32(*counts, "counts");
+  } else {
+    TORCH_CHECK(keys.has_value(), "gb_keys: keys");
+    check_t(*keys, at::kLong, "keys");
+    if (offsets) {
+      check_t(*offsets, at::kLong, "offsets");
+      TORCH_CHECK(offsets->numel() >= nb, "gb_keys: offsets [blocks]");
+    } else {
+      TORCH_CHECK(base_all >= 0 && base_all + n <= keys->numel(), "gb_keys: keys too short");
+    }
+    if (world > 1) {
+      TORCH_CHECK(word_prefix && seg_start && seg_blk0, "gb_keys: ghost tables needed at world > 1");
+      check_t(*word_prefix, at::kLong, "word_prefix");
+      check_t(*seg_start, at::kLong, "seg_start");
+      check_t(*seg_blk0, at::kLong, "seg_blk0");
+      TORCH_CHECK(seg_start->numel() >= world && seg_blk0->numel() >= world, "gb_keys: segment tables");
+    }
+  }
+  DalgoGbKeyArgs a{v_lo, v_hi, sl, (int)world, (int)rank, (int)dbits, opt_ptr<const int32_t>(new_id),
+                   opt_ptr<const uint32_t>(bitmap), opt_ptr<const int64_t>(word_prefix),
+                   opt_ptr<const int64_t>(seg_start), opt_ptr<const int64_t>(seg_blk0)};
+  DeviceGuard guard(src.device());
+  DALGO_CHECK_HIP(dalgo_gb_keys(src.data_ptr<int32_t>(), dst.data_ptr<int32_t>(), n, &a, (int)phase,
+                                opt_ptr<uint32_t>(bitmap), opt_ptr<int32_t>(counts),
+                                opt_ptr<const int64_t>(offsets), base_all, opt_ptr<uint64_t>(keys),
+                                cur_stream()),
+                  "gb_keys");
+}
+
+// sort keys[:n] over bits [0, end_bit) and deduplicate: returns the distinct count; the
+// distinct keys are in keys[:count] afterwards (work: a scratch tensor of n int64)
+int64_t gb_sort_unique(Tensor keys, int64_t n, int64_t end_bit, Tensor work) {
+  check_t(keys, at::kLong, "keys");
+  check_t(work, at::kLong, "work");
+  TORCH_CHECK(n >= 0 && n <= keys.numel() && n <= work.numel(), "gb_sort_unique: sizes");
+  if (n == 0) return 0;
+  DeviceGuard guard(keys.device());
+  auto* k = reinterpret_cast<uint64_t*>(keys.data_ptr<int64_t>());
+  auto* w = reinterpret_cast<uint64_t*>(work.data_ptr<int64_t>());
+  size_t b_sort = 0, b_uniq = 0;
+  DALGO_CHECK_HIP(dalgo_gb_sort(nullptr, &b_sort, k, w, n, (int)end_bit, cur_stream()), "gb_sort(size)");
+  DALGO_CHECK_HIP(dalgo_gb_unique(nullptr, &b_uniq, w, k, nullptr, n, cur_stream()), "gb_unique(size)");
+  Tensor tmp = at::empty({(int64_t)std::max(b_sort, b_uniq) + 256}, keys.options().dtype(at::kByte));
+  Tensor cnt = at::zeros({1}, keys.options());
+  size_t bs = b_sort, bu = b_uniq;
+  DALGO_CHECK_HIP(dalgo_gb_sort(tmp.data_ptr(), &bs, k, w, n, (int)end_bit, cur_stream()), "gb_sort");
+  DALGO_CHECK_HIP(dalgo_gb_unique(tmp.data_ptr(), &bu, w, k,
+                                  reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>()), n,
+                                  cur_stream()),
+                  "gb_unique");
+  return cnt.item<int64_t>();
+}
+
+void gb_decode(const Tensor& K, int64_t E, int64_t shift, int64_t dbits, const Tensor& blk_base,
+               int64_t phase, const std::optional<Tensor>& ent_counts, const std::optional<Tensor>& outdeg,
+               const std::optional<Tensor>& ent_offsets, const std::optional<Tensor>& srcl,
+               const std::optional<Tensor>& ent_end, const std::optional<Tensor>& ent_blk,
+               const std::optional<Tensor>& ent_dst) {
+  check_t(K, at::kLong, "K");
+  TORCH_CHECK(E >= 0 && E <= K.numel(), "gb_decode: E");
+  check_t(blk_base, at::kLong, "blk_base");
+  const int64_t nb = dalgo_gb_decode_blocks(E);
+  if (phase == 0) {
+    TORCH_CHECK(ent_counts && outdeg, "gb_decode: ent_counts / outdeg");
+    check_i32(*ent_counts, "ent_counts");
+    check_i32(*outdeg, "outdeg");
+    TORCH_CHECK(ent_counts->numel() >= nb, "gb_decode: ent_counts [blocks]");
+  } else {
+    TORCH_CHECK(ent_offsets && srcl && ent_end && ent_blk && ent_dst, "gb_decode: outputs");
+    check_t(*ent_offsets, at::kLong, "ent_offsets");
+    TORCH_CHECK(ent_offsets->numel() >= nb, "gb_decode: ent_offsets [blocks]");
+    check_t(*srcl, at::kShort, "srcl");
+    TORCH_CHECK(srcl->numel() >= E, "gb_decode: srcl");
+    check_t(*ent_end, at::kLong, "ent_end");
+    check_i32(*ent_blk, "ent_blk");
+    check_i32(*ent_dst, "ent_dst");
+  }
+  DeviceGuard guard(K.device());
+  DALGO_CHECK_HIP(dalgo_gb_decode(reinterpret_cast<const uint64_t*>(K.data_ptr<int64_t>()), E, (int)shift,
+                                  (int)dbits, blk_base.data_ptr<int64_t>(), (int)phase,
+                                  opt_ptr<int32_t>(ent_counts), opt_ptr<uint32_t>(outdeg),
+                                  opt_ptr<const int64_t>(ent_offsets), opt_ptr<uint16_t>(srcl),
+                                  opt_ptr<int64_t>(ent_end), opt_ptr<int32_t>(ent_blk),
+                                  opt_ptr<int32_t>(ent_dst), cur_stream()),
+                  "gb_decode");
+}
+
+void gb_entry_flags(const Tensor& ent_blk, const Tensor& ent_dst, const Tensor& ent_end, int64_t bin_shift,
+                    Tensor rs, Tensor cs, Tensor srcl) {
+  check_i32(ent_blk, "ent_blk");
+  check_i32(ent_dst, "ent_dst");
+  check_t(ent_end, at::kLong, "ent_end");
+  check_t(rs, at::kByte, "rs");
+  check_t(cs, at::kByte, "cs");
+  check_t(srcl, at::kShort, "srcl");
+  const int64_t ne = ent_blk.numel();
+  TORCH_CHECK(ent_dst.numel() == ne && ent_end.numel() == ne && rs.numel() >= ne && cs.numel() >= ne,
+              "gb_entry_flags: sizes");
+  DeviceGuard guard(ent_blk.device());
+  DALGO_CHECK_HIP(dalgo_gb_entry_flags(ent_blk.data_ptr<int32_t>(), ent_dst.data_ptr<int32_t>(),
+                                       ent_end.data_ptr<int64_t>(), ne, (int)bin_shift, rs.data_ptr<uint8_t>(),
+                                       cs.data_ptr<uint8_t>(), reinterpret_cast<uint16_t*>(srcl.data_ptr<int16_t>()),
+                                       cur_stream()),
+                  "gb_entry_flags");
+}
+
+void gb_entry_place(const Tensor& ent_dst, const Tensor& ent_end, const Tensor& run_of_ent,
+                    const Tensor& run_delta, const Tensor& run_chunk, const Tensor& cs, const Tensor& ce_lo,
+                    const Tensor& tlen, int64_t wu_e, int64_t bin_mask, Tensor dloc, Tensor ts) {
+  check_i32(ent_dst, "ent_dst");
+  check_t(ent_end, at::kLong, "ent_end");
+  check_i32(run_of_ent, "run_of_ent");
+  check_i32(run_delta, "run_delta");
+  check_i32(run_chunk, "run_chunk");
+  check_t(cs, at::kByte, "cs");
+  check_t(ce_lo, at::kLong, "ce_lo");
+  check_t(tlen, at::kLong, "tlen");
+  check_t(dloc, at::kShort, "dloc");
+  check_t(ts, at::kByte, "ts");
+  const int64_t ne = ent_dst.numel();
+  TORCH_CHECK(ent_end.numel() == ne && run_of_ent.numel() == ne && cs.numel() >= ne && ts.numel() >= ne,
+              "gb_entry_place: sizes");
+  TORCH_CHECK(run_delta.numel() == run_chunk.numel() && ce_lo.numel() == tlen.numel(), "gb_entry_place: tables");
+  DeviceGuard guard(ent_dst.device());
+  DALGO_CHECK_HIP(dalgo_gb_entry_place(ent_dst.data_ptr<int32_t>(), ent_end.data_ptr<int64_t>(), ne,
+                                       run_of_ent.data_ptr<int32_t>(), run_delta.data_ptr<int32_t>(),
+                                       run_chunk.data_ptr<int32_t>(), cs.data_ptr<uint8_t>(),
+                                       ce_lo.data_ptr<int64_t>(), tlen.data_ptr<int64_t>(), wu_e, (int)bin_mask,
+                                       dloc.data_ptr<int16_t>(), ts.data_ptr<uint8_t>(), cur_stream()),
+                  "gb_entry_place");
 }
 
 void pr_spmv(const Tensor& src, const Tensor& dstl, const Tensor& c, Tensor acc, Tensor pres,
@@ -1218,7 +1395,8 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(i!) er, Tensor? m_dev=None, int chunk=65536, Tensor? cnew=None, "
         "Tensor? cold=None) -> ()");
   m.def("kmeans_filter(Tensor assign, Tensor(a!) ul, Tensor delta, Tensor s, "
-        "Tensor(b!)? a_prev, Tensor(c!) idx, Tensor(d!) n_active, Tensor(f!)? acl=None) -> ()");
+        "Tensor(b!)? a_prev, Tensor(c!) idx, Tensor(d!) n_active, Tensor(f!)? acl=None, "
+        "Tensor? nd=None, int kpad=0) -> ()");
   m.def("kmeans_sort_active(Tensor acl, Tensor idx, Tensor n_active, int k, int chunk, "
         "Tensor(a!) block_counts, Tensor(b!) cstart, Tensor(c!) seg_start, Tensor(d!) rows_sorted, "
         "int tile, Tensor(e!) tiles, Tensor(g!) n_tiles) -> ()");
@@ -1239,6 +1417,19 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(d!)? shift2) -> ()");
   m.def("rmat_edges(int seed, int scale, int e_off, float a, float b, float c, bool scramble, "
         "Tensor(a!) src, Tensor(b!) dst) -> ()");
+  m.def("gb_degree(Tensor ids, Tensor(a!) deg) -> ()");
+  m.def("gb_keys(Tensor src, Tensor dst, Tensor? new_id, int v_lo, int v_hi, int sl, int world, int rank, "
+        "int dbits, int phase, Tensor(a!)? bitmap, Tensor(b!)? counts, Tensor? offsets, int base_all, "
+        "Tensor(c!)? keys, Tensor? word_prefix, Tensor? seg_start, Tensor? seg_blk0) -> ()");
+  m.def("gb_sort_unique(Tensor(a!) keys, int n, int end_bit, Tensor(b!) work) -> int");
+  m.def("gb_decode(Tensor K, int E, int shift, int dbits, Tensor blk_base, int phase, "
+        "Tensor(a!)? ent_counts, Tensor(b!)? outdeg, Tensor? ent_offsets, Tensor(c!)? srcl, "
+        "Tensor(d!)? ent_end, Tensor(e!)? ent_blk, Tensor(f!)? ent_dst) -> ()");
+  m.def("gb_entry_flags(Tensor ent_blk, Tensor ent_dst, Tensor ent_end, int bin_shift, Tensor(a!) rs, "
+        "Tensor(b!) cs, Tensor(c!) srcl) -> ()");
+  m.def("gb_entry_place(Tensor ent_dst, Tensor ent_end, Tensor run_of_ent, Tensor run_delta, "
+        "Tensor run_chunk, Tensor cs, Tensor ce_lo, Tensor tlen, int wu_e, int bin_mask, Tensor(a!) dloc, "
+        "Tensor(b!) ts) -> ()");
   m.def("pb_spmv(Tensor srcl, Tensor tile_e, Tensor tile_ent, Tensor tile_run, Tensor wu_tile, "
         "Tensor wu_chunk, "
         "Tensor chunk_slo, Tensor chunk_ns, Tensor chunk_run, Tensor run_delta, Tensor c, "
@@ -1293,6 +1484,12 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("tcs_insert", &tcs_insert);
   m.impl("xgmi_allreduce", &xgmi_allreduce);
   m.impl("rmat_edges", &rmat_edges);
+  m.impl("gb_degree", &gb_degree);
+  m.impl("gb_keys", &gb_keys);
+  m.impl("gb_sort_unique", &gb_sort_unique);
+  m.impl("gb_decode", &gb_decode);
+  m.impl("gb_entry_flags", &gb_entry_flags);
+  m.impl("gb_entry_place", &gb_entry_place);
   m.impl("pr_spmv", &pr_spmv);
   m.impl("pb_spmv", &pb_spmv);
   m.impl("pr_update", &pr_update);

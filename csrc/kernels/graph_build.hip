@@ -1,0 +1,374 @@
+// Native adjacency build of the PageRank job (graph_computation/pagerank.py:41,44:
+// ``links.distinct().groupByKey().cache()`` + ``count()``), gfx950.
+//
+// The K4b layout (pr_binned.hip) wants the deduplicated edges ordered by (source chunk,
+// destination, source): one 64-bit key per edge = block | local destination | source
+// offset in its 8192-source block, so ONE radix sort (rocPRIM onesweep over only the
+// key's bits) + one unique pass produce the distinct edges already in layout order. The
+// passes around it are single sweeps:
+//   degree   -- raw out-degree of the input edges (degree relabeling), u32 atomics;
+//   keys     -- relabel, keep this rank's destinations, map sources to the [own | ghost]
+//               index space and pack the key (two-phase compaction: count, write);
+//   decode   -- per distinct edge the u16 source offset + entry-end bit, the entry list
+//               (end edge, block, destination) and the deduplicated out-degree of every
+//               source (LDS-privatised histogram per 8192-source block, no global atomic
+//               per edge);
+//   entries  -- run-start bits (a run = the entries of one (block, destination bin)),
+//               chunk starts, bin-major destination offsets and tile starts.
+// Everything else (per-chunk / per-run tables, a few thousand to a few million rows) is
+// torch on the device (dalgo/ops/graph.py::build_blocked_native).
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_select.hpp>
+
+#include <cstdint>
+
+#include "dalgo/common.h"
+#include "launchers.h"
+
+namespace dalgo {
+namespace {
+
+constexpr int kSpan = 8192;          // sources per block (pr_binned.hip kPbSpan / graph.SRC_SPAN)
+constexpr int kSpanBits = 13;
+
+// ---------------------------------------------------------------------------- degree
+__global__ void __launch_bounds__(256) gb_degree_kernel(const int32_t* __restrict__ ids, int64_t n,
+                                                        uint32_t* __restrict__ deg) {
+  const int64_t stride = (int64_t)gridDim.x * 256 * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 3 < n) {
+      const int4 v = *reinterpret_cast<const int4*>(ids + i);
+      atomicAdd(deg + v.x, 1u);
+      atomicAdd(deg + v.y, 1u);
+      atomicAdd(deg + v.z, 1u);
+      atomicAdd(deg + v.w, 1u);
+    } else {
+      for (int64_t j = i; j < n; ++j) atomicAdd(deg + ids[j], 1u);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- keys
+// Local source index of a global (relabelled) source id and its block:
+//   own slice [v_lo, v_hi): li = s - v_lo, segment 0;
+//   remote (W > 1): li = sl + ghost rank of s (ghosts sorted by id = grouped by owner),
+//   segment = the owner's ghost block.
+// Blocks restart at every segment start; blk = seg_blk0[seg] + (li - seg_start[seg]) / 8192.
+struct GbKeyCtx {
+  int64_t v_lo, v_hi, sl;
+  int world, rank, dbits;
+  const int32_t* new_id;        // nullable: no relabeling
+  const uint32_t* bitmap;       // W > 1: remote sources with an edge into this slice
+  const int64_t* word_prefix;   // W > 1: exclusive popcount prefix of the bitmap words
+  const int64_t* seg_start;     // [W]: local index where segment p starts (p = owner)
+  const int64_t* seg_blk0;      // [W]: first block id of segment p
+};
+
+__device__ __forceinline__ bool gb_edge(const GbKeyCtx& c, int32_t s0, int32_t d0, int32_t& s,
+                                        int64_t& dl) {
+  s = c.new_id ? c.new_id[s0] : s0;
+  const int32_t d = c.new_id ? c.new_id[d0] : d0;
+  dl = (int64_t)d - c.v_lo;
+  return d >= c.v_lo && d < c.v_hi;
+}
+
+__device__ __forceinline__ uint64_t gb_key(const GbKeyCtx& c, int32_t s, int64_t dl) {
+  int64_t rel, blk0;
+  if (c.world == 1 || (s >= c.v_lo && s < c.v_hi)) {
+    rel = (int64_t)s - c.v_lo;
+    blk0 = 0;
+  } else {
+    const int p = (int)((int64_t)s / c.sl);
+    const int64_t w = s >> 5;
+    const uint32_t below = c.bitmap[w] & ((1u << (s & 31)) - 1u);
+    const int64_t g = c.word_prefix[w] + __popc(below);          // ghost rank of s
+    rel = c.sl + g - c.seg_start[p];
+    blk0 = c.seg_blk0[p];
+  }
+  const uint64_t blk = (uint64_t)(blk0 + (rel >> kSpanBits));
+  return (blk << (c.dbits + kSpanBits)) | ((uint64_t)dl << kSpanBits) | (uint64_t)(rel & (kSpan - 1));
+}
+
+constexpr int kKeyR = 8192;          // edges per block of the two key phases
+
+// phase 0: count the kept edges per block (and mark remote sources, W > 1)
+__global__ void __launch_bounds__(256) gb_keys_count_kernel(const int32_t* __restrict__ src,
+                                                            const int32_t* __restrict__ dst, int64_t n,
+                                                            GbKeyCtx c, uint32_t* __restrict__ bitmap,
+                                                            int32_t* __restrict__ counts) {
+  __shared__ int s_cnt;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * kKeyR;
+  const int64_t r1 = r0 + kKeyR < n ? r0 + kKeyR : n;
+  int mine = 0;
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) {
+    int32_t s;
+    int64_t dl;
+    if (gb_edge(c, src[i], dst[i], s, dl)) {
+      ++mine;
+      if (c.world > 1 && !(s >= c.v_lo && s < c.v_hi)) atomicOr(bitmap + (s >> 5), 1u << (s & 31));
+    }
+  }
+  atomicAdd(&s_cnt, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = s_cnt;
+}
+
+// phase 1: write the kept edges' keys at offsets[block] + (any order inside the block:
+// the keys are sorted afterwards)
+__global__ void __launch_bounds__(256) gb_keys_write_kernel(const int32_t* __restrict__ src,
+                                                            const int32_t* __restrict__ dst, int64_t n,
+                                                            GbKeyCtx c, const int64_t* __restrict__ offsets,
+                                                            int64_t base_all, uint64_t* __restrict__ keys) {
+  __shared__ int s_cur;
+  if (threadIdx.x == 0) s_cur = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * kKeyR;
+  const int64_t r1 = r0 + kKeyR < n ? r0 + kKeyR : n;
+  const int64_t base = offsets ? offsets[blockIdx.x] : base_all + r0;
+  const int lane = threadIdx.x & 63;
+  for (int64_t i0 = r0; i0 < r1; i0 += 256) {
+    const int64_t i = i0 + threadIdx.x;
+    int32_t s = 0;
+    int64_t dl = 0;
+    const bool keep = i < r1 && gb_edge(c, src[i], dst[i], s, dl);
+    const uint64_t m = __ballot(keep);
+    int wbase = 0;
+    if (lane == 0 && m) wbase = atomicAdd(&s_cur, __popcll(m));
+    wbase = __shfl(wbase, 0, 64);
+    if (keep) {
+      const int r = __popcll(m & ((1ull << lane) - 1ull));
+      keys[base + wbase + r] = gb_key(c, s, dl);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- decode
+constexpr int kDecR = 65536;         // distinct edges per block of the decode kernels
+constexpr int kDecT = 256;           // threads; each owns kDecR / kDecT consecutive edges
+
+__device__ __forceinline__ bool gb_end(const uint64_t* K, int64_t i, int64_t E) {
+  return i == E - 1 || (K[i + 1] >> kSpanBits) != (K[i] >> kSpanBits);
+}
+
+// entry ends per block + the deduplicated out-degree per local source (LDS histogram of
+// the block's first source block; edges of later source blocks in the range: global atomics)
+__global__ void __launch_bounds__(kDecT) gb_decode_count_kernel(const uint64_t* __restrict__ K, int64_t E,
+                                                                int shift, const int64_t* __restrict__ blk_base,
+                                                                int32_t* __restrict__ ent_counts,
+                                                                uint32_t* __restrict__ outdeg) {
+  __shared__ uint32_t hist[kSpan];
+  __shared__ int s_cnt;
+  for (int j = threadIdx.x; j < kSpan; j += kDecT) hist[j] = 0u;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * kDecR;
+  const int64_t r1 = r0 + kDecR < E ? r0 + kDecR : E;
+  const uint64_t blk0 = K[r0] >> shift;
+  int mine = 0;
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += kDecT) {
+    const uint64_t k = K[i];
+    const uint64_t blk = k >> shift;
+    const uint32_t off = (uint32_t)(k & (kSpan - 1));
+    if (blk == blk0) atomicAdd(hist + off, 1u);
+    else atomicAdd(outdeg + blk_base[blk] + off, 1u);
+    mine += gb_end(K, i, E) ? 1 : 0;
+  }
+  atomicAdd(&s_cnt, mine);
+  __syncthreads();
+  const int64_t b0 = blk_base[blk0];
+  for (int j = threadIdx.x; j < kSpan; j += kDecT)
+    if (hist[j]) atomicAdd(outdeg + b0 + j, hist[j]);
+  if (threadIdx.x == 0) ent_counts[blockIdx.x] = s_cnt;
+}
+
+// srcl (u16 source offset | 0x8000 on an entry's end edge) and the entry list in key
+// order: each thread owns a contiguous piece, one block scan places the pieces
+__global__ void __launch_bounds__(kDecT) gb_decode_write_kernel(const uint64_t* __restrict__ K, int64_t E,
+                                                                int shift, int dbits,
+                                                                const int64_t* __restrict__ ent_offsets,
+                                                                uint16_t* __restrict__ srcl,
+                                                                int64_t* __restrict__ ent_end,
+                                                                int32_t* __restrict__ ent_blk,
+                                                                int32_t* __restrict__ ent_dst) {
+  __shared__ int s_scan[kDecT];
+  constexpr int PER = kDecR / kDecT;
+  const int64_t r0 = (int64_t)blockIdx.x * kDecR + (int64_t)threadIdx.x * PER;
+  const int64_t r1 = r0 + PER < E ? r0 + PER : E;
+  int cnt = 0;
+  for (int64_t i = r0; i < r1; ++i) cnt += gb_end(K, i, E) ? 1 : 0;
+  s_scan[threadIdx.x] = cnt;
+  __syncthreads();
+  // inclusive Hillis-Steele scan over 256 counts
+  for (int off = 1; off < kDecT; off <<= 1) {
+    const int v = threadIdx.x >= off ? s_scan[threadIdx.x - off] : 0;
+    __syncthreads();
+    s_scan[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int64_t pos = ent_offsets[blockIdx.x] + s_scan[threadIdx.x] - cnt;
+  const uint64_t dmask = (1ull << dbits) - 1ull;
+  for (int64_t i = r0; i < r1; ++i) {
+    const uint64_t k = K[i];
+    const bool end = gb_end(K, i, E);
+    srcl[i] = (uint16_t)((k & (kSpan - 1)) | (end ? 0x8000u : 0u));
+    if (end) {
+      ent_end[pos] = i;
+      ent_blk[pos] = (int32_t)(k >> shift);
+      ent_dst[pos] = (int32_t)((k >> kSpanBits) & dmask);
+      ++pos;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- entries
+// run starts (new block or new destination bin), chunk starts (new block); the run-start
+// bit 0x4000 goes on the entry's end edge
+__global__ void __launch_bounds__(256) gb_entry_flags_kernel(const int32_t* __restrict__ ent_blk,
+                                                             const int32_t* __restrict__ ent_dst,
+                                                             const int64_t* __restrict__ ent_end, int64_t nent,
+                                                             int bin_shift, uint8_t* __restrict__ rs,
+                                                             uint8_t* __restrict__ cs,
+                                                             uint16_t* __restrict__ srcl) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nent; e += stride) {
+    const int32_t b = ent_blk[e];
+    const int32_t bin = ent_dst[e] >> bin_shift;
+    bool c = true, r = true;
+    if (e > 0) {
+      const int32_t pb = ent_blk[e - 1];
+      c = pb != b;
+      r = c || (ent_dst[e - 1] >> bin_shift) != bin;
+    }
+    rs[e] = r;
+    cs[e] = c;
+    if (r) srcl[ent_end[e]] |= (uint16_t)0x4000;
+  }
+}
+
+// bin-major destination offsets: entry e of run q lives at e + run_delta[q]; and tile
+// starts: within a chunk, a new work unit every wu_e edges and a new tile every tlen[chunk]
+// edges of the unit, both on entry boundaries (dalgo/ops/graph.py::build_blocked)
+__global__ void __launch_bounds__(256) gb_entry_place_kernel(const int32_t* __restrict__ ent_dst,
+                                                             const int64_t* __restrict__ ent_end, int64_t nent,
+                                                             const int32_t* __restrict__ run_of_ent,
+                                                             const int32_t* __restrict__ run_delta,
+                                                             const int32_t* __restrict__ run_chunk,
+                                                             const uint8_t* __restrict__ cs,
+                                                             const int64_t* __restrict__ ce_lo,
+                                                             const int64_t* __restrict__ tlen, int64_t wu_e,
+                                                             int bin_mask, int16_t* __restrict__ dloc,
+                                                             uint8_t* __restrict__ ts) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nent; e += stride) {
+    const int q = run_of_ent[e];
+    dloc[e + run_delta[q]] = (int16_t)(ent_dst[e] & bin_mask);
+    const int ch = run_chunk[q];
+    bool t = cs[e] != 0;
+    if (!t) {
+      const int64_t tl = tlen[ch];
+      const int64_t a = (e > 1 ? ent_end[e - 2] + 1 : 0) - ce_lo[ch];   // entry e - 1's first edge
+      const int64_t b = ent_end[e - 1] + 1 - ce_lo[ch];                 // entry e's first edge
+      t = (a / wu_e) != (b / wu_e) || ((a % wu_e) / tl) != ((b % wu_e) / tl);
+    }
+    ts[e] = t;
+  }
+}
+
+}  // namespace
+}  // namespace dalgo
+
+using namespace dalgo;
+
+extern "C" {
+
+hipError_t dalgo_gb_degree(const int32_t* ids, int64_t n, uint32_t* deg, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t g = std::min<int64_t>(cdiv(n, 256 * 4), 256 * 64);
+  hipLaunchKernelGGL(gb_degree_kernel, dim3((unsigned)g), dim3(256), 0, st, ids, n, deg);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+int64_t dalgo_gb_key_blocks(int64_t n) { return cdiv(n, (int64_t)kKeyR); }
+
+hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, const DalgoGbKeyArgs* a,
+                         int phase, uint32_t* bitmap, int32_t* counts, const int64_t* offsets,
+                         int64_t base_all, uint64_t* keys, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (a->dbits < 0 || a->dbits > 31 || a->world < 1) return hipErrorInvalidValue;
+  GbKeyCtx c{a->v_lo, a->v_hi, a->sl, a->world, a->rank, a->dbits, a->new_id, a->bitmap,
+             a->word_prefix, a->seg_start, a->seg_blk0};
+  if (c.world > 1 && (c.sl <= 0 || (phase == 1 && (!c.bitmap || !c.word_prefix || !c.seg_start || !c.seg_blk0))))
+    return hipErrorInvalidValue;
+  const int64_t g = cdiv(n, (int64_t)kKeyR);
+  if (g > 0x7fffffffLL) return hipErrorInvalidValue;
+  if (phase == 0)
+    hipLaunchKernelGGL(gb_keys_count_kernel, dim3((unsigned)g), dim3(256), 0, st, src, dst, n, c, bitmap, counts);
+  else
+    hipLaunchKernelGGL(gb_keys_write_kernel, dim3((unsigned)g), dim3(256), 0, st, src, dst, n, c, offsets,
+                       base_all, keys);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+// rocPRIM onesweep radix sort of n u64 keys over bits [0, end_bit); tmp == nullptr: query
+hipError_t dalgo_gb_sort(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
+                         int end_bit, hipStream_t st) {
+  if (n < 0 || end_bit < 1 || end_bit > 64) return hipErrorInvalidValue;
+  return rocprim::radix_sort_keys(tmp, *tmp_bytes, in, out, (size_t)n, 0u, (unsigned)end_bit, st);
+}
+
+// rocPRIM unique over sorted keys (n < 2^32); the count lands in *count (device)
+hipError_t dalgo_gb_unique(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out,
+                           unsigned long long* count, int64_t n, hipStream_t st) {
+  if (n < 0 || n >= (int64_t)0xffffffffLL) return hipErrorInvalidValue;
+  return rocprim::unique(tmp, *tmp_bytes, in, out, count, (size_t)n, rocprim::equal_to<uint64_t>(), st);
+}
+
+int64_t dalgo_gb_decode_blocks(int64_t E) { return cdiv(E, (int64_t)kDecR); }
+
+hipError_t dalgo_gb_decode(const uint64_t* K, int64_t E, int shift, int dbits, const int64_t* blk_base,
+                           int phase, int32_t* ent_counts, uint32_t* outdeg, const int64_t* ent_offsets,
+                           uint16_t* srcl, int64_t* ent_end, int32_t* ent_blk, int32_t* ent_dst,
+                           hipStream_t st) {
+  if (E <= 0) return hipSuccess;
+  if (shift < kSpanBits || shift > 63 || dbits < 0 || dbits > 31) return hipErrorInvalidValue;
+  const int64_t g = cdiv(E, (int64_t)kDecR);
+  if (phase == 0)
+    hipLaunchKernelGGL(gb_decode_count_kernel, dim3((unsigned)g), dim3(kDecT), 0, st, K, E, shift, blk_base,
+                       ent_counts, outdeg);
+  else
+    hipLaunchKernelGGL(gb_decode_write_kernel, dim3((unsigned)g), dim3(kDecT), 0, st, K, E, shift, dbits,
+                       ent_offsets, srcl, ent_end, ent_blk, ent_dst);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t dalgo_gb_entry_flags(const int32_t* ent_blk, const int32_t* ent_dst, const int64_t* ent_end,
+                                int64_t nent, int bin_shift, uint8_t* rs, uint8_t* cs, uint16_t* srcl,
+                                hipStream_t st) {
+  if (nent <= 0) return hipSuccess;
+  const int64_t g = std::min<int64_t>(cdiv(nent, 256), 256 * 64);
+  hipLaunchKernelGGL(gb_entry_flags_kernel, dim3((unsigned)g), dim3(256), 0, st, ent_blk, ent_dst, ent_end,
+                     nent, bin_shift, rs, cs, srcl);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t dalgo_gb_entry_place(const int32_t* ent_dst, const int64_t* ent_end, int64_t nent,
+                                const int32_t* run_of_ent, const int32_t* run_delta, const int32_t* run_chunk,
+                                const uint8_t* cs, const int64_t* ce_lo, const int64_t* tlen, int64_t wu_e,
+                                int bin_mask, int16_t* dloc, uint8_t* ts, hipStream_t st) {
+  if (nent <= 0) return hipSuccess;
+  if (wu_e < 1) return hipErrorInvalidValue;
+  const int64_t g = std::min<int64_t>(cdiv(nent, 256), 256 * 64);
+  hipLaunchKernelGGL(gb_entry_place_kernel, dim3((unsigned)g), dim3(256), 0, st, ent_dst, ent_end, nent,
+                     run_of_ent, run_delta, run_chunk, cs, ce_lo, tlen, wu_e, bin_mask, dloc, ts);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+}  // extern "C"

@@ -484,7 +484,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   const float* hbase = hn;
   if constexpr (CAND) {
     const int4 tr = trn;
-    acl = tr.x;
+    acl = tr.x >> 1;                           // tile key = 2 cluster + far (km_filter_kernel)
     pend = tr.z;
     pbase = (int64_t)tr.y + (int64_t)wid * (PT * 32);
     hbase = aux.hnb + (int64_t)acl * kpad;
@@ -1611,29 +1611,38 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   const int nchunk = kpad / CH;
   const int64_t pbase = ((int64_t)blockIdx.x * NW + wid) * (PG * 16);
 
-  // ---- points: unconditional loads (rows past n read row 0), masked after the wait
+  // ---- points: rows past n read row 0 and are zeroed after the wait (the last wave only)
   uint4 bf[PG][KS];
-  uint32_t pm[PG];
+  const bool full = pbase + PG * 16 <= n;
 #pragma unroll
   for (int g = 0; g < PG; ++g) {
     const int64_t p = pbase + g * 16 + pl;
-    pm[g] = p < n ? 0xffffffffu : 0u;
-    const uint16_t* src = X + (p < n ? p : 0) * ldx + 8 * lg;
+    const uint16_t* src = X + (full || p < n ? p : 0) * ldx + 8 * lg;
 #pragma unroll
     for (int s = 0; s < KS; ++s) bf[g][s] = *reinterpret_cast<const uint4*>(src + 32 * s);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!full) {
+#pragma unroll
+    for (int g = 0; g < PG; ++g)
+      if (pbase + g * 16 + pl >= n)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) bf[g][s] = make_uint4(0u, 0u, 0u, 0u);
+  }
   float x2[PG];
   float mx = 0.f;
 #pragma unroll
   for (int g = 0; g < PG; ++g) {
+    // |x|^2 by v_dot2c_f32_bf16 (two bf16 products per instruction, f32 accumulate)
     float q = 0.f;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      bf[g][s] = make_uint4(bf[g][s].x & pm[g], bf[g][s].y & pm[g], bf[g][s].z & pm[g], bf[g][s].w & pm[g]);
-      q += sq_sum(bf[g][s], uint16_t{});
-      bf[g][s] = make_uint4(bf[g][s].x ^ 0x80008000u, bf[g][s].y ^ 0x80008000u,
-                            bf[g][s].z ^ 0x80008000u, bf[g][s].w ^ 0x80008000u);
+      const uint32_t w[4] = {bf[g][s].x, bf[g][s].y, bf[g][s].z, bf[g][s].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16x2 h = __builtin_bit_cast(bf16x2, w[j]);
+        q = __builtin_amdgcn_fdot2_f32_bf16(h, h, q, false);
+      }
     }
     q += __shfl_xor(q, 16, 64);
     q += __shfl_xor(q, 32, 64);
@@ -1643,23 +1652,25 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
   if (lane == 0) s_m[wid] = mx;
 
-  // ---- chunk DMA (the 32x32 form's image: slot (row, jj) holds piece jj ^ (row & SWZ))
-  int src_off[GPT];
+  // ---- chunk DMA (the 32x32 form's image: slot (row, jj) holds piece jj ^ (row & SWZ));
+  // the global address is an SGPR base (the chunk) + a loop-invariant VGPR offset, the
+  // LDS destination an SGPR (m0): no per-chunk vector address arithmetic
+  uint32_t src_off[GPT];
 #pragma unroll
   for (int g = 0; g < GPT; ++g) {
     const int qq = g * NT + tid, row = qq / NJ, jj = qq % NJ;
-    src_off[g] = row * DP + (jj ^ (row & SWZ)) * 8;
+    src_off[g] = (uint32_t)(row * DP + (jj ^ (row & SWZ)) * 8) * 2u;
   }
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(km_lds_void*)s_c;
+  const uint32_t lds_w = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(km_lds_void*)s_c + (uint32_t)(wid * 64 * 16));
   auto issue = [&](int ch) {
     const uint16_t* base = Cq + (int64_t)ch * CH * DP;
-    const uint32_t dst = lds0 + (uint32_t)(((ch % NBUF) * CHP) * 16);
+    const uint32_t dst = lds_w + (uint32_t)(((ch % NBUF) * CHP) * 16);
 #pragma unroll
     for (int g = 0; g < GPT; ++g) {
-      const uint32_t m0v = __builtin_amdgcn_readfirstlane(dst + (uint32_t)((g * NT + wid * 64) * 16));
-      const uint16_t* src = base + src_off[g];
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-                   :: "s"(m0v), "v"(src) : "memory");
+      const uint32_t m0v = dst + (uint32_t)(g * NT * 16);
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+                   :: "s"(m0v), "v"(src_off[g]), "s"(base) : "memory");
     }
   };
   __syncthreads();
@@ -1667,7 +1678,11 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
 #pragma unroll
   for (int w = 1; w < NW; ++w) M = fmaxf(M, s_m[w]);
   M = M * 1.0001f + 1e-6f;
-  for (int c = tid; c < kpad; c += NT) s_hn16[c] = hn[c] + M;
+  // the accumulators start at -(0.5|c|^2 + M) and add c.x (B = the points as loaded):
+  // acc = -(0.5|x - c|^2 + M - 0.5|x|^2) < 0, and for negative floats the SIGNED integer
+  // order of the bits is the reverse of the value order, so the smallest key is the
+  // largest acc = the nearest centre (padding centres, -1e30, have the largest keys)
+  for (int c = tid; c < kpad; c += NT) s_hn16[c] = -(hn[c] + M);
   issue(0);
 
   int bkey[PG], bch[PG], cm[PG];
@@ -1782,7 +1797,7 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   double my_sse = 0.0;
 #pragma unroll
   for (int g = 0; g < PG; ++g) {
-    float v = __int_as_float(bkey[g] & kmask);
+    float v = -__int_as_float(bkey[g] & kmask);
     const int ix = bkey[g] & 31;
     int id = bch[g] * CH + (ix >> 2) * 16 + 4 * lg + (ix & 3);
 #pragma unroll

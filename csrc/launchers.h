@@ -134,7 +134,7 @@ hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, 
 hipError_t dalgo_km_filter(const int32_t* assign, float* ul, const float* delta,
                            const float* s, int k, int64_t n, int32_t* a_prev, int32_t* idx,
                            unsigned long long* n_active, int64_t cap, int32_t* acl,
-                           hipStream_t st);
+                           const float* nd, int kpad, hipStream_t st);
 hipError_t dalgo_km_centre_bounds(const void* cnow, const void* cprev, int is_bf16, int k, int d,
                                   int DP, float* delta, float* s, hipStream_t st);
 hipError_t dalgo_km_qsum(const int32_t* assign, const float* xh, int64_t n, int k, double* Q,
@@ -202,3 +202,37 @@ hipError_t dalgo_xgmi_allreduce(const float* in, float* out, int n, int rank, in
                                 double* count_acc, hipStream_t st);
 
 }  // extern "C"
+
+// ---- native PageRank adjacency build (graph_build.hip)
+struct DalgoGbKeyArgs {
+  int64_t v_lo, v_hi, sl;       // this rank's destination slice, slice size (owner = id / sl)
+  int world, rank, dbits;       // dbits: bits of a local destination index
+  const int32_t* new_id;        // nullable: degree relabeling old -> new id
+  const uint32_t* bitmap;       // W > 1: remote sources with an edge into this slice
+  const int64_t* word_prefix;   // W > 1: exclusive popcount prefix per bitmap word
+  const int64_t* seg_start;     // [W]: local source index where owner p's segment starts
+  const int64_t* seg_blk0;      // [W]: first block id of owner p's segment
+};
+extern "C" {
+hipError_t dalgo_gb_degree(const int32_t* ids, int64_t n, uint32_t* deg, hipStream_t st);
+int64_t dalgo_gb_key_blocks(int64_t n);
+hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, const DalgoGbKeyArgs* a,
+                         int phase, uint32_t* bitmap, int32_t* counts, const int64_t* offsets,
+                         int64_t base_all, uint64_t* keys, hipStream_t st);
+hipError_t dalgo_gb_sort(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
+                         int end_bit, hipStream_t st);
+hipError_t dalgo_gb_unique(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out,
+                           unsigned long long* count, int64_t n, hipStream_t st);
+int64_t dalgo_gb_decode_blocks(int64_t E);
+hipError_t dalgo_gb_decode(const uint64_t* K, int64_t E, int shift, int dbits, const int64_t* blk_base,
+                           int phase, int32_t* ent_counts, uint32_t* outdeg, const int64_t* ent_offsets,
+                           uint16_t* srcl, int64_t* ent_end, int32_t* ent_blk, int32_t* ent_dst,
+                           hipStream_t st);
+hipError_t dalgo_gb_entry_flags(const int32_t* ent_blk, const int32_t* ent_dst, const int64_t* ent_end,
+                                int64_t nent, int bin_shift, uint8_t* rs, uint8_t* cs, uint16_t* srcl,
+                                hipStream_t st);
+hipError_t dalgo_gb_entry_place(const int32_t* ent_dst, const int64_t* ent_end, int64_t nent,
+                                const int32_t* run_of_ent, const int32_t* run_delta, const int32_t* run_chunk,
+                                const uint8_t* cs, const int64_t* ce_lo, const int64_t* tlen, int64_t wu_e,
+                                int bin_mask, int16_t* dloc, uint8_t* ts, hipStream_t st);
+}

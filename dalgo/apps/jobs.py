@@ -177,7 +177,8 @@ def kmeans_job(rt, rows: int = 100_000_000, dim: int = 128, k: int = 1024, iters
 def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
                  spmv: str = "blocked", semantics: str = "reference", witness: bool = True,
                  reorder: bool = True, seed: int = 1, bin_width: int = 16384,
-                 chunk: int = 1 << 40, tile: int = 16384, timed_iters: int = 10) -> dict:
+                 chunk: int = 1 << 40, tile: int = 16384, timed_iters: int = 10,
+                 native_build: bool = True) -> dict:
     """BASELINE config #5 (R-MAT scale 26, edge factor 16 = 1.07B edges, Graph500
     a,b,c = 0.57,0.19,0.19, scrambled ids): the reference's PageRank job, destination-
     partitioned over the ranks. The input edge list is generated before the clock; the
@@ -185,7 +186,7 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
     plus ``iters`` iterations. After it, ``timed_iters`` more iterations are timed alone
     (per-iteration edges/s, secondary) and the witness checks one more K4b step against
     the pull K4 SpMV from the same state."""
-    from dalgo.apps.pagerank_app import build_rmat_shard, rmat_input
+    from dalgo.apps.pagerank_app import build_rmat_native, build_rmat_shard, rmat_input
     from dalgo.models.pagerank import PageRank, PageRankConfig
     from dalgo.utils.obs import PhaseTimer
     W = rt.world_size
@@ -200,7 +201,14 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
     rt.synchronize()
     t = time.perf_counter()
     ev.mark()
-    shard = build_rmat_shard(edges, scale, rt.rank, W, rt.device, reorder=reorder, seed=seed)
+    # GPU + blocked SpMV + (one rank or the ghost exchange): the native build straight into
+    # the K4b layout; otherwise the (dst, src)-sorted shard
+    native = (native_build and rt.device.type == "cuda" and spmv == "blocked" and chunk >= 1 << 40)
+    if native:
+        shard = build_rmat_native(edges, scale, rt.rank, W, rt.device, reorder=reorder,
+                                  keep_keys=witness, bin_width=bin_width, tile=tile)
+    else:
+        shard = build_rmat_shard(edges, scale, rt.rank, W, rt.device, reorder=reorder, seed=seed)
     ev.mark()
     pr = PageRank(cfg, shard, W)
     ev.mark()
@@ -233,7 +241,7 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
     if witness:
         # one more iteration of the benchmarked SpMV vs the pull SpMV from the same state
         ref = PageRank(PageRankConfig(semantics=semantics, spmv="pull", exchange=pr.exchange),
-                       shard, W)
+                       shard.to_shard() if native else shard, W)
         ref.load_state_dict(pr.state_dict())
         pr.step()
         ref.step()
@@ -264,6 +272,7 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
         "ms_per_iter": it_ms, "edges_per_s_per_iter": E / (it_ms / 1e3),
         "edges_dedup": E, "edges_generated": n_gen, "vertices": 1 << scale,
         "degree_reordered": reorder, "spmv": pr.spmv, "exchange": pr.exchange,
+        "adjacency_build": "native (graph_build.hip)" if native else "torch (dst, src) shard",
         "phases_ms_rank0": phases, "correctness_witness": wit,
         "blocked_layout_rank0": None if lay is None else {
             "chunks": lay.n_chunks, "entries": lay.n_entries,

@@ -87,12 +87,13 @@ def degree_order_from(edges: list, scale: int, rank: int, world: int, device) ->
     one all-reduce)."""
     from dalgo.parallel import comm
     n_vertices = 1 << scale
-    deg = torch.zeros(n_vertices, dtype=torch.int64, device=device)
+    deg = torch.zeros(n_vertices, dtype=torch.int32, device=device)
     for i, (s, _) in enumerate(edges):
         if i % world == rank:
             G.degree_count_(deg, s)
     comm.all_reduce_sum(deg)
-    order = torch.argsort(-deg * n_vertices - torch.arange(n_vertices, device=device, dtype=torch.int64))
+    order = torch.argsort(-deg.to(torch.int64) * n_vertices
+                          - torch.arange(n_vertices, device=device, dtype=torch.int64))
     return deal_ids(order, n_vertices, world).to(torch.int32)
 
 
@@ -115,6 +116,16 @@ def build_rmat_shard(edges: list, scale: int, rank: int, world: int, device, reo
     shard = G.merge_shards(parts, v_lo, v_hi, n_vertices, sl)
     shard.new_id = new_id
     return shard
+
+
+def build_rmat_native(edges: list, scale: int, rank: int, world: int, device, reorder: bool = True,
+                      keep_keys: bool = False, bin_width: int = 16384, tile: int = 16384):
+    """This rank's K4b-ready adjacency of the given R-MAT edge chunks, built natively
+    (dalgo.ops.graph.build_native): degree relabeling, destination filter, dedup and the
+    blocked layout without the (dst, src)-sorted intermediate shard."""
+    new_id = degree_order_from(edges, scale, rank, world, device) if reorder else None
+    return G.build_native(edges, 1 << scale, rank, world, new_id, bin_width=bin_width, tile=tile,
+                          keep_keys=keep_keys)
 
 
 def rmat_shard(scale: int, edge_factor: int, rank: int, world: int, device, seed: int = 1,

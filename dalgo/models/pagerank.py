@@ -51,22 +51,35 @@ class PageRankConfig:
 class PageRank:
     timer = None   # dalgo.utils.obs.PhaseTimer (None = off)
 
-    def __init__(self, cfg: PageRankConfig, shard: Gops.GraphShard, world: int = 1):
+    def __init__(self, cfg: PageRankConfig, shard, world: int = 1):
+        """shard: a (dst, src)-sorted :class:`GraphShard`, or a :class:`NativeGraph` from
+        ``Gops.build_native`` (blocked SpMV only: the K4b layout, out-degrees and ghost
+        list come prebuilt)."""
         self.cfg = cfg
         self.g = shard
         self.world = world
-        dev = shard.src.device
+        native = isinstance(shard, Gops.NativeGraph)
+        self.native = native
+        dev = shard.layout.srcl.device if native else shard.src.device
         self.dev = dev
         nl = shard.n_local
         sl = shard.slice_size
         # global out-degree (each rank holds the in-edges of its slice only)
-        od_full = Gops.local_outdeg(shard)
+        if native:
+            od_full = torch.zeros(shard.n_vertices, dtype=torch.int32, device=dev)
+            od_full[shard.v_lo: shard.v_hi] += shard.outdeg_loc[:nl]
+            if shard.ghosts is not None and shard.n_ghost:
+                od_full.index_add_(0, shard.ghosts, shard.outdeg_loc[sl: sl + shard.n_ghost])
+        else:
+            od_full = Gops.local_outdeg(shard)
         comm.all_reduce_sum(od_full)
         self.outdeg = od_full[shard.v_lo: shard.v_hi].contiguous()
         self.mode = 0 if cfg.semantics == "reference" else 1
         self.spmv = cfg.spmv or ("blocked" if dev.type == "cuda" else "pull")
         if self.spmv not in ("blocked", "pull"):
             raise ValueError(f"spmv must be 'blocked' or 'pull' (got {self.spmv!r})")
+        if native and self.spmv != "blocked":
+            raise ValueError("a NativeGraph carries the blocked (K4b) layout only")
         if self.mode == 0:
             self.N = int((od_full > 0).sum().item())
         else:
@@ -80,8 +93,13 @@ class PageRank:
         self.pres = torch.zeros(nl, dtype=torch.int32, device=dev)
         self.r = torch.zeros(nl, dtype=fdt, device=dev)
         self.exchange = cfg.exchange if world > 1 else "allgather"
+        if native and world > 1 and self.exchange != "ghost":
+            raise ValueError("a NativeGraph uses the ghost exchange on several ranks")
         if self.exchange == "ghost":
-            self._build_ghosts()
+            if native:
+                self._native_ghosts()
+            else:
+                self._build_ghosts()
             # own slice first, then the ghosts: c_slice is a view, so the update kernel's
             # writes are already in place for the SpMV
             self.c_full = torch.zeros(sl + self.n_ghost, dtype=fdt, device=dev)
@@ -95,7 +113,9 @@ class PageRank:
         self.layout = None
         # fuse_update=False: K4b writes acc / pres and the separate update kernel runs
         self.fuse_update = cfg.fuse_update
-        if self.spmv == "blocked":
+        if native:
+            self.layout = shard.layout
+        elif self.spmv == "blocked":
             gsp = self.g_local if self.exchange == "ghost" else self.g
             # ghost index space: no chunk straddles the own slice's end or a peer's block,
             # so each peer's ghost chunks are one work-unit range (per-peer overlap)
@@ -169,6 +189,27 @@ class PageRank:
         self.send_idx = (req - g.v_lo).contiguous()
         assert bool(((self.send_idx >= 0) & (self.send_idx < g.n_local)).all())
         self.send_buf = None
+
+    def _native_ghosts(self):
+        """The ghost exchange plan from a NativeGraph's ghost list (sorted global ids,
+        grouped by owner): who sends which own c values to whom."""
+        g, W = self.g, self.world
+        ghosts = g.ghosts if g.ghosts is not None else torch.zeros(0, dtype=torch.int64, device=self.dev)
+        self.n_ghost = int(ghosts.numel())
+        recv_counts = torch.tensor(g.recv_counts + [0] * (W - len(g.recv_counts)), dtype=torch.int64,
+                                   device=self.dev)[:W]
+        send_counts = torch.empty_like(recv_counts)
+        comm.all_to_all_single(send_counts, recv_counts)
+        self.recv_split = [int(x) for x in recv_counts.tolist()]
+        self.send_split = [int(x) for x in send_counts.tolist()]
+        self.ghost_off = [0]
+        for c_ in self.recv_split:
+            self.ghost_off.append(self.ghost_off[-1] + c_)
+        req = torch.empty(sum(self.send_split), dtype=torch.int64, device=self.dev)
+        comm.all_to_all_single(req, ghosts, out_split=self.send_split, in_split=self.recv_split)
+        self.send_idx = (req - g.v_lo).contiguous()
+        self.send_buf = None
+        self.own_share = 0.0
 
     def _exchange(self):
         if self.exchange == "ghost":

@@ -126,8 +126,12 @@ def merge_shards(parts: list, v_lo, v_hi, n_vertices, sl, dedup=True) -> GraphSh
 
 
 def degree_count_(deg: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
-    """deg[v] += #occurrences of v in ids (int64 deg)."""
-    deg += torch.bincount(ids.long(), minlength=deg.numel())
+    """deg[v] += #occurrences of v in ids. GPU (int32 deg, int32 ids): one u32 atomic per
+    id (csrc/kernels/graph_build.hip), not torch's int64 histogram."""
+    if deg.is_cuda and deg.dtype == torch.int32 and ids.dtype == torch.int32:
+        _ext.ops().gb_degree(ids.contiguous(), deg)
+        return deg
+    deg += torch.bincount(ids.long(), minlength=deg.numel()).to(deg.dtype)
     return deg
 
 
@@ -381,6 +385,280 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
                          torch.zeros(1, dtype=torch.float64, device=dev),
                          int((slo[wu_chunk] < src_split).sum().item()) if src_split is not None else 0,
                          tuple(int((slo[wu_chunk] < b).sum().item()) for b in splits))
+
+
+# ------------------------------------------------------------------ native build
+@dataclass
+class NativeGraph:
+    """A rank's PageRank adjacency built natively from raw edge chunks (build_native):
+    the K4b layout over the [own slice | ghosts] source index space, the deduplicated
+    out-degree of every local source, and the ghost list (W > 1). Stands in for the
+    (dst, src)-sorted :class:`GraphShard` of the blocked path; :meth:`to_shard` rebuilds
+    that form (pull SpMV, witnesses) from the kept keys."""
+    layout: BlockedLayout
+    n_edges: int
+    v_lo: int
+    v_hi: int
+    n_vertices: int
+    slice_size: int
+    outdeg_loc: torch.Tensor            # int32 [sl + n_ghost]: distinct out-edges per local source
+    ghosts: torch.Tensor | None         # int64 sorted global ids of the remote sources (W > 1)
+    recv_counts: list                   # ghosts per owner rank
+    keys: torch.Tensor | None = None    # distinct keys (kept for to_shard), int64 [n_edges]
+    key_shift: int = 0
+    dbits: int = 0
+    blk_base: torch.Tensor | None = None
+    new_id: torch.Tensor | None = None
+
+    @property
+    def n_local(self) -> int:
+        return self.v_hi - self.v_lo
+
+    @property
+    def n_ghost(self) -> int:
+        return 0 if self.ghosts is None else int(self.ghosts.numel())
+
+    def to_shard(self) -> GraphShard:
+        """The (dst, src)-sorted shard with GLOBAL source ids (needs the kept keys)."""
+        if self.keys is None:
+            raise ValueError("NativeGraph.to_shard needs the keys (build_native(keep_keys=True))")
+        K = self.keys[: self.n_edges]
+        blk = K >> self.key_shift
+        dl = (K >> SRC_BITS) & ((1 << self.dbits) - 1)
+        li = self.blk_base[blk] + (K & (SRC_SPAN - 1))
+        sl = self.slice_size
+        if self.ghosts is not None:
+            gs = torch.where(li < sl, li + self.v_lo,
+                             self.ghosts[(li - sl).clamp(0, max(self.n_ghost - 1, 0))])
+        else:
+            gs = li + self.v_lo
+        key = torch.sort((dl << 32) | gs).values
+        sh = _shard_from_keys(key, self.v_lo, self.v_hi, self.n_vertices, sl)
+        sh.new_id = self.new_id
+        return sh
+
+
+SRC_BITS = 13            # log2(SRC_SPAN)
+
+
+def _popcount32(x: torch.Tensor) -> torch.Tensor:
+    x = x.to(torch.int64) & 0xFFFFFFFF
+    x = x - ((x >> 1) & 0x55555555)
+    x = (x & 0x33333333) + ((x >> 2) & 0x33333333)
+    x = (x + (x >> 4)) & 0x0F0F0F0F
+    return ((x * 0x01010101) & 0xFFFFFFFF) >> 24
+
+
+def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: torch.Tensor | None = None,
+                 bin_width: int = 16384, tile: int = 16384, items: int = 2048,
+                 min_piece: int = 1 << 14, keep_keys: bool = False) -> NativeGraph:
+    """``distinct().groupByKey()`` of graph_computation/pagerank.py:41 straight into the
+    K4b layout, on the device (csrc/kernels/graph_build.hip): relabel + keep this rank's
+    destinations + pack one (block, destination, source offset) key per edge, ONE radix
+    sort over the key's bits, unique, then single passes for the per-edge source offsets,
+    the entries and their runs / tiles. Same layout as :func:`build_blocked` over the
+    (dst, src)-sorted shard (chunks = whole 8192-source blocks, no edge cut).
+
+    edges: list of (src, dst) int32 GPU chunks of GLOBAL ids (before ``new_id``)."""
+    if bin_width not in (8192, 16384):
+        raise ValueError("bin_width must be 8192 or 16384")
+    ops = _ext.ops()
+    dev = edges[0][0].device
+    N, W = n_vertices, world
+    sl = vertex_slices(N, W)
+    v_lo, v_hi = rank * sl, min(N, (rank + 1) * sl)
+    nl = v_hi - v_lo
+    dbits = max(1, (max(nl, 1) - 1).bit_length())
+    S = SRC_SPAN
+    i64 = dict(dtype=torch.int64, device=dev)
+    i32 = dict(dtype=torch.int32, device=dev)
+    nid = new_id.to(torch.int32).contiguous() if new_id is not None else None
+    # ---- phase 0: kept edges per key block (+ remote-source marks, W > 1)
+    bitmap = torch.zeros((N + 31) // 32 + 1, **i32) if W > 1 else None
+    nbs = [(int(s.numel()) + 8191) // 8192 for s, _ in edges]
+    if W > 1:
+        counts = torch.empty(sum(nbs), **i32)
+        o = 0
+        for (s, d), nb in zip(edges, nbs):
+            ops.gb_keys(s, d, nid, v_lo, v_hi, sl, W, rank, dbits, 0, bitmap, counts[o:o + nb], None, 0,
+                        None, None, None, None)
+            o += nb
+        c64 = counts.to(torch.int64)
+        offsets = torch.cumsum(c64, 0) - c64
+        total = int(c64.sum().item())
+        pc = _popcount32(bitmap)
+        word_prefix = torch.cumsum(pc, 0) - pc
+        n_ghost = int(pc.sum().item())
+        bits = (bitmap.to(torch.int64)[:, None] >> torch.arange(32, device=dev)) & 1
+        ghosts = torch.nonzero(bits.flatten()).flatten()
+        del bits
+        assert int(ghosts.numel()) == n_ghost
+        recv = torch.bincount(ghosts // sl, minlength=W)[:W]
+        recv_counts = [int(x) for x in recv.tolist()]
+    else:
+        total = sum(int(s.numel()) for s, _ in edges)
+        offsets, word_prefix, ghosts, n_ghost, recv_counts = None, None, None, 0, [0]
+    # ---- segments of the local source index space: own [0, nl), then each peer's ghosts
+    seg_start = [0] * W
+    seg_end = [0] * W
+    seg_blk0 = [0] * W
+    seg_end[rank] = nl
+    nblk = (nl + S - 1) // S
+    goff = 0
+    for p in range(W):
+        if p == rank:
+            continue
+        seg_start[p] = sl + goff
+        goff += recv_counts[p]
+        seg_end[p] = sl + goff
+        seg_blk0[p] = nblk
+        nblk += (recv_counts[p] + S - 1) // S
+    blk_base = torch.empty(max(nblk, 1), **i64)
+    blk_end = torch.empty(max(nblk, 1), **i64)
+    for p in range(W):
+        nb = ((seg_end[p] - seg_start[p]) + S - 1) // S
+        if nb:
+            b0 = seg_blk0[p]
+            base = seg_start[p] + S * torch.arange(nb, **i64)
+            blk_base[b0:b0 + nb] = base
+            blk_end[b0:b0 + nb] = seg_end[p]
+    blk_bits = max(1, (max(nblk, 1) - 1).bit_length())
+    shift = dbits + SRC_BITS
+    nbits = shift + blk_bits
+    assert nbits <= 63, "key does not fit 63 bits"
+    st = torch.tensor(seg_start, **i64)
+    sb = torch.tensor(seg_blk0, **i64)
+    # ---- phase 1: keys
+    keys = torch.empty(max(total, 1), **i64)
+    o, base_all = 0, 0
+    for (s, d), nb in zip(edges, nbs):
+        ops.gb_keys(s, d, nid, v_lo, v_hi, sl, W, rank, dbits, 1, bitmap, None,
+                    offsets[o:o + nb] if offsets is not None else None, base_all, keys,
+                    word_prefix, st, sb)
+        o += nb
+        base_all += int(s.numel())
+    del bitmap, word_prefix, offsets
+    work = torch.empty_like(keys)
+    E = int(ops.gb_sort_unique(keys, total, nbits, work)) if total else 0
+    del work
+    n_src_loc = (sl + n_ghost) if W > 1 else max(N, 1)
+    outdeg_loc = torch.zeros(n_src_loc, **i32)
+    if E == 0:
+        shard = GraphShard(torch.full((4,), -1, **i32), torch.full((4,), -1, **i32), 0, v_lo, v_hi, N, sl)
+        lay = build_blocked(shard, bin_width, 1 << 40, tile, items, min_piece)
+        return NativeGraph(lay, 0, v_lo, v_hi, N, sl, outdeg_loc, ghosts, recv_counts,
+                           keys if keep_keys else None, shift, dbits, blk_base, new_id)
+    # ---- decode: per-edge source offsets + entry-end bits, entries, distinct out-degrees
+    nbd = (E + 65535) // 65536
+    ent_counts = torch.empty(nbd, **i32)
+    ops.gb_decode(keys, E, shift, dbits, blk_base, 0, ent_counts, outdeg_loc, None, None, None, None, None)
+    ec = ent_counts.to(torch.int64)
+    ent_offsets = torch.cumsum(ec, 0) - ec
+    nent = int(ec.sum().item())
+    E16 = (E + 15) // 16 * 16
+    srcl = torch.zeros(E16, dtype=torch.int16, device=dev)
+    ent_end = torch.empty(nent, **i64)
+    ent_blk = torch.empty(nent, **i32)
+    ent_dst = torch.empty(nent, **i32)
+    ops.gb_decode(keys, E, shift, dbits, blk_base, 1, None, None, ent_offsets, srcl, ent_end, ent_blk, ent_dst)
+    del ent_counts, ec, ent_offsets
+    if not keep_keys:
+        del keys
+        keys = None
+    # ---- entries: run / chunk starts, run-start bits
+    bshift = bin_width.bit_length() - 1
+    nbins = max(1, (nl + bin_width - 1) // bin_width)
+    rs = torch.empty(nent, dtype=torch.uint8, device=dev)
+    cs = torch.empty(nent, dtype=torch.uint8, device=dev)
+    ops.gb_entry_flags(ent_blk, ent_dst, ent_end, bshift, rs, cs, srcl)
+    run_first = torch.nonzero(rs).flatten()
+    chunk_first = torch.nonzero(cs).flatten()
+    nch = int(chunk_first.numel())
+    nruns = int(run_first.numel())
+    assert nent < (1 << 31) - 8 and nruns < (1 << 31)
+    chunk_blk = ent_blk[chunk_first].to(torch.int64)
+    run_of_ent = (torch.cumsum(rs, 0, dtype=torch.int32) - 1)
+    del rs
+    run_chunk = torch.searchsorted(chunk_first, run_first, right=True) - 1
+    run_bin = (ent_dst[run_first] >> bshift).to(torch.int64)
+    run_len = torch.diff(torch.cat([run_first, torch.tensor([nent], **i64)]))
+    border = torch.argsort(run_bin * (nch + 1) + run_chunk)
+    bm_start = torch.empty_like(run_first)
+    bm_start[border] = torch.cumsum(run_len[border], 0) - run_len[border]
+    run_delta = bm_start - run_first
+    del bm_start, border
+    chunk_run = torch.searchsorted(run_chunk, torch.arange(nch + 1, **i64))
+    bin_cnt = torch.zeros(nbins, **i64).index_add_(0, run_bin, run_len)
+    bin_lo = torch.cumsum(bin_cnt, 0) - bin_cnt
+    # ---- tiles / work units: a chunk is cut every wu_e edges into work units and every
+    # tlen edges inside a unit into tiles, both on entry boundaries
+    ce_lo = torch.where(chunk_first > 0, ent_end[(chunk_first - 1).clamp_min(0)] + 1,
+                        torch.zeros_like(chunk_first))
+    ce_n = torch.diff(torch.cat([ce_lo, torch.tensor([E], **i64)]))
+    wu_e = max(1 << 15, E // 4096)
+    tlen = torch.clamp((torch.clamp(ce_n, max=wu_e) + 15) // 16, min=min(1024, tile), max=tile)
+    n4 = (nent + 3) // 4 * 4 + PB_DUMMY
+    dloc = torch.zeros(n4, dtype=torch.int16, device=dev)
+    ts = torch.empty(nent, dtype=torch.uint8, device=dev)
+    ops.gb_entry_place(ent_dst, ent_end, run_of_ent, run_delta.to(torch.int32), run_chunk.to(torch.int32), cs,
+                       ce_lo, tlen, wu_e, bin_width - 1, dloc, ts)
+    del run_of_ent, cs, ent_dst, ent_blk
+    tile_ent = torch.nonzero(ts).flatten()
+    del ts
+    e_start_t = torch.where(tile_ent > 0, ent_end[(tile_ent - 1).clamp_min(0)] + 1, torch.zeros_like(tile_ent))
+    del ent_end
+    tile_e = torch.cat([e_start_t, torch.tensor([E], **i64)])
+    tile_chunk = torch.searchsorted(chunk_first, tile_ent, right=True) - 1
+    chunk_tile = torch.searchsorted(tile_chunk, torch.arange(nch + 1, **i64))
+    wk = tile_chunk * (E + 2) + (e_start_t - ce_lo[tile_chunk]) // wu_e
+    wnew = torch.ones_like(wk, dtype=torch.bool)
+    wnew[1:] = wk[1:] != wk[:-1]
+    wu_first = torch.nonzero(wnew).flatten()
+    wu_tile = torch.cat([wu_first, torch.tensor([tile_ent.numel()], **i64)])
+    wu_chunk = tile_chunk[wu_first]
+    tile_run = torch.searchsorted(run_first, tile_ent) - chunk_run[tile_chunk]
+    slo = blk_base[chunk_blk]
+    ns = torch.clamp(blk_end[chunk_blk] - slo, max=S)
+    n_src = int((slo + ns).max().item())
+    assert int(tile_e[-1]) <= srcl.numel() and int(ns.min().item()) >= 1
+    max_runs = int((chunk_run[1:] - chunk_run[:-1]).max().item())
+    # ---- phase-2 work items (as build_blocked)
+    cap = max(int(nent // max(items, 1)), min_piece)
+    cnt_h = bin_cnt.cpu().tolist()
+    lo_h = bin_lo.cpu().tolist()
+    wb, wl, slab_h, sp_bin, sp_first, sp_cnt = [], [], [], [], [], []
+    nslab = 0
+    for b, (n_b, l_b) in enumerate(zip(cnt_h, lo_h)):
+        if n_b == 0:
+            wb.append(b); wl.append(l_b); slab_h.append(-1)
+            continue
+        pieces = max(1, -(-n_b // cap))
+        step = -(-n_b // pieces)
+        cuts = list(range(l_b, l_b + n_b, step))
+        if pieces > 1:
+            sp_bin.append(b); sp_first.append(nslab); sp_cnt.append(len(cuts))
+        for p0 in cuts:
+            wb.append(b)
+            wl.append(p0)
+            if pieces > 1:
+                slab_h.append(nslab); nslab += 1
+            else:
+                slab_h.append(-1)
+    wl.append(nent)
+    it = lambda x: torch.tensor(x, **i32)
+    c32 = lambda x: x.to(torch.int32).contiguous()
+    splits = sorted({int(x) for x in seg_start if x > 0})
+    lay = BlockedLayout(srcl, tile_e.contiguous(), c32(tile_ent), c32(tile_run), c32(chunk_tile),
+                        c32(wu_tile), c32(wu_chunk), c32(slo), c32(ns), c32(chunk_run), c32(run_delta),
+                        torch.zeros(n4, dtype=torch.float32, device=dev), dloc,
+                        it(wb), torch.tensor(wl, **i64), it(slab_h),
+                        torch.zeros(max(nslab, 1) * bin_width, **i64),
+                        it(sp_bin), it(sp_first), it(sp_cnt), bin_width, nl, nch, nent, n_src,
+                        0, max_runs, torch.zeros(1, dtype=torch.float64, device=dev),
+                        int((slo[wu_chunk] < sl).sum().item()) if W > 1 else 0,
+                        tuple(int((slo[wu_chunk] < b).sum().item()) for b in splits))
+    return NativeGraph(lay, E, v_lo, v_hi, N, sl, outdeg_loc, ghosts, recv_counts, keys, shift, dbits,
+                       blk_base, new_id)
 
 
 def pb_spmv(lay: BlockedLayout, c_full: torch.Tensor, acc: torch.Tensor, pres: torch.Tensor,

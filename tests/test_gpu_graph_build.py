@@ -1,0 +1,127 @@
+"""Native PageRank adjacency build (csrc/kernels/graph_build.hip, dalgo.ops.graph.build_native)
+against the torch path: same distinct edge set per rank, the K4b layout's SpMV equals the
+pull SpMV over the same edges, whole PageRank runs equal the torch-built model."""
+import pytest
+import torch
+
+from dalgo.apps.pagerank_app import build_rmat_native, build_rmat_shard, rmat_input
+from dalgo.models.pagerank import PageRank, PageRankConfig
+from dalgo.ops import graph as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _edge_set(shard):
+    E = shard.n_edges
+    return (shard.dstl[:E].long() << 32) | shard.src[:E].long()
+
+
+@pytest.mark.parametrize("reorder", [True, False])
+def test_degree_count_matches_bincount(cuda, reorder):
+    s, _ = G.rmat_edges(1 << 20, 16, seed=3, device=cuda)
+    deg = torch.zeros(1 << 16, dtype=torch.int32, device=cuda)
+    G.degree_count_(deg, s)
+    G.degree_count_(deg, s[: 1000])
+    ref = torch.bincount(s.long(), minlength=1 << 16) + torch.bincount(s[:1000].long(), minlength=1 << 16)
+    assert torch.equal(deg.long(), ref)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("reorder", [True, False])
+def test_native_edges_equal_torch_shard(cuda, world, reorder):
+    """Every rank's distinct edges (global ids) == the torch-built (dst, src) shard, and the
+    out-degree of every local source counts exactly its distinct out-edges."""
+    scale = 14
+    edges, _ = rmat_input(scale, 8, torch.device(cuda), seed=5, chunk=1 << 15)
+    for rank in range(world):
+        if reorder and world > 1:
+            # the relabeling needs every rank's degree share (a collective): one process
+            # emulates it with the full count
+            new_id = _full_order(edges, scale, world, cuda)
+            ng = G.build_native(edges, 1 << scale, rank, world, new_id, keep_keys=True)
+            ref = _torch_shard(edges, scale, rank, world, new_id)
+        else:
+            ng = build_rmat_native(edges, scale, rank, world, cuda, reorder=reorder, keep_keys=True)
+            ref = build_rmat_shard(edges, scale, rank, world, cuda, reorder=reorder)
+        sh = ng.to_shard()
+        assert ng.n_edges == ref.n_edges
+        assert torch.equal(_edge_set(sh), _edge_set(ref))
+        # distinct out-degree per local source
+        sl = ng.slice_size
+        src = ref.src[: ref.n_edges].long()
+        own = (src >= ng.v_lo) & (src < ng.v_hi)
+        od = torch.zeros_like(ng.outdeg_loc, dtype=torch.int64)
+        od.index_add_(0, src[own] - ng.v_lo, torch.ones_like(src[own]))
+        if ng.ghosts is not None and ng.n_ghost:
+            gi = torch.searchsorted(ng.ghosts, src[~own])
+            od.index_add_(0, sl + gi, torch.ones_like(gi))
+        assert torch.equal(od, ng.outdeg_loc.long())
+
+
+def _full_order(edges, scale, world, cuda):
+    from dalgo.apps.pagerank_app import deal_ids
+    n = 1 << scale
+    deg = torch.zeros(n, dtype=torch.int32, device=cuda)
+    for s, _ in edges:
+        G.degree_count_(deg, s)
+    order = torch.argsort(-deg.long() * n - torch.arange(n, device=cuda))
+    return deal_ids(order, n, world).to(torch.int32)
+
+
+def _torch_shard(edges, scale, rank, world, new_id):
+    n = 1 << scale
+    sl = G.vertex_slices(n, world)
+    v_lo, v_hi = rank * sl, min(n, (rank + 1) * sl)
+    parts = []
+    for s, d in edges:
+        s, d = new_id[s.long()], new_id[d.long()]
+        keep = (d >= v_lo) & (d < v_hi)
+        parts.append((s[keep], d[keep] - v_lo))
+    return G.merge_shards(parts, v_lo, v_hi, n, sl)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_native_layout_spmv_matches_pull(cuda, world):
+    """K4b over the native layout (local [own | ghost] source space) == the pull SpMV over
+    the same edges, per rank, on random contributions (some absent)."""
+    scale = 15
+    edges, _ = rmat_input(scale, 16, torch.device(cuda), seed=9, chunk=1 << 16)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    for rank in range(world):
+        ng = build_rmat_native(edges, scale, rank, world, cuda, reorder=False, keep_keys=True)
+        sl = ng.slice_size
+        nc = sl + ng.n_ghost
+        c = torch.rand(nc, generator=g).to(cuda)
+        c[torch.rand(nc, generator=g).to(cuda) < 0.2] = -1.0
+        lay = ng.layout
+        acc = torch.empty(ng.n_local, device=cuda)
+        pres = torch.empty(ng.n_local, dtype=torch.int32, device=cuda)
+        G.pb_spmv(lay, c, acc, pres)
+        # pull reference in the same local source space
+        sh = ng.to_shard()
+        gs = sh.src[: sh.n_edges].long()
+        d = sh.dstl[: sh.n_edges].long()
+        own = (gs >= ng.v_lo) & (gs < ng.v_hi)
+        li = torch.where(own, gs - ng.v_lo, torch.zeros_like(gs))
+        if ng.ghosts is not None and ng.n_ghost:
+            li = torch.where(own, li, sl + torch.searchsorted(ng.ghosts, gs))
+        cv = c[li].double()
+        ref = torch.zeros(ng.n_local, dtype=torch.float64, device=cuda)
+        ref.index_add_(0, d, cv.clamp_min(0))
+        hit = torch.zeros(ng.n_local, dtype=torch.int64, device=cuda)
+        hit.index_add_(0, d, (cv >= 0).long())
+        assert torch.equal(pres.bool(), hit > 0)
+        assert torch.allclose(acc.double(), ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("sem", ["reference", "standard"])
+def test_native_pagerank_equals_torch_build(cuda, sem):
+    scale = 16
+    edges, _ = rmat_input(scale, 16, torch.device(cuda), seed=2, chunk=1 << 18)
+    ng = build_rmat_native(edges, scale, 0, 1, cuda, reorder=True)
+    sh = build_rmat_shard(edges, scale, 0, 1, cuda, reorder=True)
+    a = PageRank(PageRankConfig(semantics=sem, spmv="blocked"), ng).fit()
+    b = PageRank(PageRankConfig(semantics=sem, spmv="pull"), sh).fit()
+    assert a.N == b.N
+    assert torch.equal(a.r >= 0, b.r >= 0)
+    assert torch.allclose(a.r, b.r, rtol=2e-5, atol=1e-12)
