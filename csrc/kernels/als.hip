@@ -427,157 +427,6 @@ als_rf16_kernel(const float* __restrict__ R, int64_t m, int64_t n, int64_t ldr,
   }
 }
 
-// 16x16x32 form with the F fragments shared through LDS: NW (8) waves of one block run the
-// same super-steps on different rows, so each super-step's F fragments (SS * NC * 2 KB,
-// the Fq16 layout) are copied global -> registers -> LDS once per block instead of once
-// per wave. That lets each wave own only RT = 2-4 row tiles (32-64 rows: the row-visit
-// shape that streams best, row_tile_probe.hip) without multiplying the F traffic.
-// Pipeline per super-step S (one raw s_barrier each):
-//   a. ds_write the F(S+1) pieces staged in registers -> LDS buffer (S+1) % 3
-//   b. lgkmcnt(0) + s_barrier: F(S), F(S+1) visible; every wave is done with S-1
-//   c. issue global loads of F(S+2) (staging registers) and R(S+2) (register ring slot)
-//   d. MFMAs of S: R from ring slot S % 3, F fragments ds_read from LDS buffer S % 3
-// Buffer (S+1) % 3 == (S-2) % 3 was last read by the MFMAs of S-2, before the barrier of
-// S-1, so step a of S never overwrites live data; the F(S+1) loads were issued before
-// R(S+1), so waiting for them in a only waits for R(S), which d needs anyway.
-template <int RT, int NC, int SS, int NW>
-__global__ void __launch_bounds__(NW * 64, 1)
-als_rf16l_kernel(const float* __restrict__ R, int64_t m, int64_t n, int64_t ldr,
-                 const uint4* __restrict__ Fq, int nrb, int nsplit, int ss_per_split,
-                 float* __restrict__ P, int kpad) {
-  typedef float f32x4 __attribute__((ext_vector_type(4)));
-  constexpr int ROWS = NW * RT * 16;
-  constexpr int W = 32 * SS;
-  constexpr int NQ = 2 * SS;
-  constexpr int FP = SS * NC * 2 * 64;                 // 16-B pieces of F per super-step
-  constexpr int PPT = (FP + NW * 64 - 1) / (NW * 64);  // pieces per thread
-  __shared__ __attribute__((aligned(16))) uint4 s_f[3][FP];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, rr = lane & 15, g = lane >> 4;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int sp = L / nrb, rb = L % nrb;
-  const int64_t nss_full = n / W;
-  const int64_t nss = (n + W - 1) / W;
-  const int64_t S0 = (int64_t)sp * ss_per_split;
-  const int64_t S1 = std::min<int64_t>(nss, S0 + ss_per_split);
-  const int64_t row0 = (int64_t)rb * ROWS + (int64_t)wid * (RT * 16);
-
-  const float* rp[RT];
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    const int64_t row = row0 + 16 * t + rr;
-    rp[t] = R + (row < m ? row : 0) * ldr + 4 * g;
-  }
-  f32x4 acc[RT][NC];
-#pragma unroll
-  for (int t = 0; t < RT; ++t)
-#pragma unroll
-    for (int c = 0; c < NC; ++c) acc[t][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  uint4 fst[PPT];
-  auto load_f = [&](int64_t S) {
-    const uint4* src = Fq + S * FP;
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const int q = i * NW * 64 + tid;
-      if (FP % (NW * 64) == 0 || q < FP) fst[i] = src[q];
-    }
-  };
-  auto store_f = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const int q = i * NW * 64 + tid;
-      if (FP % (NW * 64) == 0 || q < FP) s_f[buf][q] = fst[i];
-    }
-  };
-  auto load_r = [&](float4 (&rv)[RT][NQ], int64_t S) {
-    const int64_t c0 = S * W;
-    if (S < nss_full) {
-#pragma unroll
-      for (int t = 0; t < RT; ++t)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) rv[t][q] = ld_f4(rp[t] + c0 + 16 * q);
-    } else {   // tail super-step: element-wise guarded loads, zeros past n
-#pragma unroll
-      for (int t = 0; t < RT; ++t)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            v[e] = (c0 + 16 * q + 4 * g + e < n) ? rp[t][c0 + 16 * q + e] : 0.f;
-          rv[t][q] = make_float4(v[0], v[1], v[2], v[3]);
-        }
-    }
-  };
-  auto compute = [&](const float4 (&rv)[RT][NQ], int buf) {
-    const uint4* fb = s_f[buf] + lane;
-#pragma unroll
-    for (int u = 0; u < SS; ++u) {
-      uint4 fh[NC], fl[NC];
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        fh[c] = fb[((u * NC + c) * 2) * 64];
-        fl[c] = fb[((u * NC + c) * 2 + 1) * 64];
-      }
-#pragma unroll
-      for (int t = 0; t < RT; ++t) {
-        uint4 rh, rl;
-        split8(rv[t][2 * u], rv[t][2 * u + 1], rh, rl);
-        const bf16x8 bh = __builtin_bit_cast(bf16x8, rh), bl = __builtin_bit_cast(bf16x8, rl);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          const bf16x8 ah = __builtin_bit_cast(bf16x8, fh[c]);
-          const bf16x8 al = __builtin_bit_cast(bf16x8, fl[c]);
-          acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[t][c], 0, 0, 0);
-          acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[t][c], 0, 0, 0);
-          acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[t][c], 0, 0, 0);
-        }
-      }
-    }
-  };
-
-  float4 rv[3][RT][NQ];
-  // prologue: F(S0) -> LDS buffer 0, F(S0+1) staged, R(S0), R(S0+1) in flight
-  if (S0 < S1) {
-    load_f(S0);
-    store_f(0);
-    if (S0 + 1 < S1) load_f(S0 + 1);
-    load_r(rv[0], S0);
-    if (S0 + 1 < S1) load_r(rv[1], S0 + 1);
-  }
-  for (int64_t S = S0; S < S1; S += 3) {
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      const int64_t Sc = S + b;
-      if (Sc < S1) {
-        if (Sc + 1 < S1) store_f((b + 1) % 3);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (Sc + 2 < S1) {
-          load_f(Sc + 2);
-          load_r(rv[(b + 2) % 3], Sc + 2);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        compute(rv[b], b);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  }
-
-  float* Ps = P + (int64_t)sp * m * kpad;
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    const int64_t row = row0 + 16 * t + rr;
-    if (row >= m) continue;
-    float* dst = Ps + row * kpad + 4 * g;
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-      *reinterpret_cast<float4*>(dst + 16 * c) =
-          make_float4(acc[t][c][0], acc[t][c][1], acc[t][c][2], acc[t][c][3]);
-  }
-}
-
 // ---- residual sum of squares  sum_ij (R_ij - U_i . V_j)^2  (the ALS RMSE of
 // matrix_decomposition.py:19-21) in one pass over R, never forming U V^T: the closed form
 // ||R||^2 - 2<U, R V> + <U^T U, V^T V> cancels ~5 significant digits at 100k x 50k, where
@@ -824,35 +673,22 @@ static int als_device_cus() {
   return cached[dev];
 }
 
-// Launch configuration by factor count k and variant (DALGO_ALS_VARIANT):
-//   form 16: als_rf16_kernel, 16-row tiles, NC = factor tiles of 16 (k padded to 16/32/64/128)
-//   form 32: als_rf_kernel,   32-row tiles, NC = factor tiles of 32
+// Launch configuration by factor count k (DALGO_ALS_VARIANT = 1 selects the fallback):
+//   form 16 (default): als_rf16_kernel, 16-row tiles, NC = factor tiles of 16 (k padded
+//                      to 16/32/64/128), 8 row tiles per wave (4 at k > 64), 3 F buffers;
+//   form 32 (fallback): als_rf_kernel, 32-row tiles, NC = factor tiles of 32.
 // rt = row tiles per wave, ss = K-steps per super-step, minb = blocks per CU (4 waves each).
+// The other launch shapes measured in rounds 2-4 (8-wave LDS-shared F, 2 / 4 F buffers,
+// 2 blocks per CU) were slower and are gone (profiles/round4/README.md).
 struct AlsCfg { int form, nc, rt, ss, minb, nbuf; };
 static int als_variant() { return env_int("DALGO_ALS_VARIANT", 0); }
 static AlsCfg als_cfg(int k, int variant) {
   const int nc16 = k <= 16 ? 1 : k <= 32 ? 2 : k <= 64 ? 4 : 8;
   const int nc32 = (k + 31) / 32;
-  if (nc16 <= 4) {
-    switch (variant) {
-      case 5: return {17, nc16, 2, 2, 1, 3};
-      case 6: return {17, nc16, 4, 1, 1, 3};
-      case 7: return {17, nc16, 2, 1, 1, 3};
-      case 1: return {16, nc16, 4, 1, 2, 2};
-      case 2: return {16, nc16, 8, 1, 1, 2};
-      case 3: return {16, nc16, 4, 1, 1, 4};
-      case 4: return {32, nc32, 4, 2, 1, 2};
-      default: return {16, nc16, 8, 1, 1, 3};
-    }
-  }
-  switch (variant) {
-    case 1: return {32, nc32, 2, 2, 1, 2};
-    case 2: return {16, 8, 4, 1, 1, 2};
-    default: return {16, 8, 4, 1, 1, 3};
-  }
+  if (variant == 1) return {32, nc32, nc32 <= 2 ? 4 : 2, 2, 1, 2};
+  return {16, nc16, nc16 <= 4 ? 8 : 4, 1, 1, 3};
 }
-// form 17 = the 16x16x32 form with F shared through LDS (8-wave blocks)
-static int als_waves(const AlsCfg& c) { return c.form == 17 ? 8 : 4; }
+static int als_waves(const AlsCfg&) { return 4; }
 static int als_tile(const AlsCfg& c) { return c.form == 32 ? 32 : 16; }
 static int64_t als_rows_per_block(const AlsCfg& c) { return (int64_t)als_waves(c) * c.rt * als_tile(c); }
 static int64_t als_ks_width(const AlsCfg& c) { return c.form == 32 ? 16 : 32; }   // columns per K-step
@@ -861,12 +697,9 @@ static int als_kpad(const AlsCfg& c) { return c.nc * als_tile(c); }
 template <int FORM, int RT, int NC, int SS, int MINB, int NBUF>
 static hipError_t launch_rf(const float* R, int64_t m, int64_t n, int64_t ldr, const uint4* Fq,
                             int nsplit, int ssps, float* P, int kpad, hipStream_t st) {
-  constexpr int NW = FORM == 17 ? 8 : 4;
+  constexpr int NW = 4;
   const int nrb = (int)cdiv(m, NW * RT * (FORM == 32 ? 32 : 16));
-  if constexpr (FORM == 17) {
-    hipLaunchKernelGGL((als_rf16l_kernel<RT, NC, SS, NW>), dim3(nrb * nsplit), dim3(NW * 64), 0, st,
-                       R, m, n, ldr, Fq, nrb, nsplit, ssps, P, kpad);
-  } else if constexpr (FORM == 16) {
+  if constexpr (FORM == 16) {
     hipLaunchKernelGGL((als_rf16_kernel<RT, NC, SS, NW, MINB, NBUF>), dim3(nrb * nsplit), dim3(NW * 64), 0,
                        st, R, m, n, ldr, Fq, nrb, nsplit, ssps, P, kpad);
   } else {
@@ -880,22 +713,15 @@ static hipError_t launch_rf(const float* R, int64_t m, int64_t n, int64_t ldr, c
 static hipError_t dispatch_rf(const AlsCfg& cf, const float* R, int64_t m, int64_t n, int64_t ldr,
                               const uint4* Fq, int nsplit, int ssps, float* P, int kpad,
                               hipStream_t st) {
-#define DALGO_RF(FM_, RT_, NC_, SS_, MB_, NB_)                                                \
+#define ALS_RF_CASE(FM_, RT_, NC_, SS_, MB_, NB_)                                             \
   if (cf.form == FM_ && cf.rt == RT_ && cf.nc == NC_ && cf.ss == SS_ && cf.minb == MB_ &&        \
       cf.nbuf == NB_)                                                                            \
     return launch_rf<FM_, RT_, NC_, SS_, MB_, NB_>(R, m, n, ldr, Fq, nsplit, ssps, P, kpad, st);
-#define DALGO_RF16(NC_)                                                                          \
-  DALGO_RF(16, 8, NC_, 1, 1, 3) DALGO_RF(16, 4, NC_, 1, 2, 2) DALGO_RF(16, 8, NC_, 1, 1, 2)     \
-  DALGO_RF(16, 4, NC_, 1, 1, 4)
-  DALGO_RF16(1) DALGO_RF16(2) DALGO_RF16(4)
-#define DALGO_RF17(NC_) DALGO_RF(17, 2, NC_, 2, 1, 3) DALGO_RF(17, 4, NC_, 1, 1, 3) DALGO_RF(17, 2, NC_, 1, 1, 3)
-  DALGO_RF17(1) DALGO_RF17(2) DALGO_RF17(4)
-#undef DALGO_RF17
-  DALGO_RF(16, 4, 8, 1, 1, 3) DALGO_RF(16, 4, 8, 1, 1, 2)
-  DALGO_RF(32, 4, 1, 2, 1, 2) DALGO_RF(32, 4, 2, 2, 1, 2) DALGO_RF(32, 2, 3, 2, 1, 2)
-  DALGO_RF(32, 2, 4, 2, 1, 2)
-#undef DALGO_RF16
-#undef DALGO_RF
+  ALS_RF_CASE(16, 8, 1, 1, 1, 3) ALS_RF_CASE(16, 8, 2, 1, 1, 3) ALS_RF_CASE(16, 8, 4, 1, 1, 3)
+  ALS_RF_CASE(16, 4, 8, 1, 1, 3)
+  ALS_RF_CASE(32, 4, 1, 2, 1, 2) ALS_RF_CASE(32, 4, 2, 2, 1, 2) ALS_RF_CASE(32, 2, 3, 2, 1, 2)
+  ALS_RF_CASE(32, 2, 4, 2, 1, 2)
+#undef ALS_RF_CASE
   return hipErrorInvalidValue;
 }
 

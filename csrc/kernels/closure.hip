@@ -181,24 +181,18 @@ using namespace dalgo;
 extern "C" {
 
 // A: [npad, lda] uint8 0/1, T_old/T_new: [nz, ldt] uint8 0/1; npad, nz multiples
-// of 128, lda/ldt >= npad and multiples of 16. variant 0: 128-tiles BK = 64, 1: 128-tiles
-// BK = 128, 2: 256-tiles BK = 64, 3: 256-tiles BK = 128 (2 / 3 need npad and nz multiples
-// of 256 and fall back to 1 otherwise).
+// of 128, lda/ldt >= npad and multiples of 16. 256 x 256 tiles (8 waves, 128-B K stages)
+// when npad and nz are multiples of 256, else 128 x 128 tiles. The 64-B K-stage forms were
+// slower at every size measured (n = 16384: 1.51 / 2.14 vs 1.73 / 2.33 POP/s) and are gone.
 hipError_t dalgo_tc_step(const void* A, int64_t lda, const void* Told, void* Tnew, int64_t ldt,
                          int npad, int nz, int variant, unsigned long long* count, hipStream_t st) {
+  (void)variant;
   if (npad % 128 || nz % 128 || lda % 16 || ldt % 16) return hipErrorInvalidValue;
   if (npad == 0 || nz == 0) return hipSuccess;
-  if ((variant == 2 || variant == 3) && npad % 256 == 0 && nz % 256 == 0) {
-    const int gx = npad / 256, gz = nz / 256;
-    if (variant == 3) launch_tc_step<128, 256>(A, lda, Told, Tnew, ldt, npad, gx, gz, count, st);
-    else launch_tc_step<64, 256>(A, lda, Told, Tnew, ldt, npad, gx, gz, count, st);
-    DALGO_LAUNCH_CHECK();
-    return hipSuccess;
-  }
-  const int gx = npad / 128, gz = nz / 128;
-  if (variant == 1 || variant == 2 || variant == 3)
-    launch_tc_step<128, 128>(A, lda, Told, Tnew, ldt, npad, gx, gz, count, st);
-  else launch_tc_step<64, 128>(A, lda, Told, Tnew, ldt, npad, gx, gz, count, st);
+  if (npad % 256 == 0 && nz % 256 == 0)
+    launch_tc_step<128, 256>(A, lda, Told, Tnew, ldt, npad, npad / 256, nz / 256, count, st);
+  else
+    launch_tc_step<128, 128>(A, lda, Told, Tnew, ldt, npad, npad / 128, nz / 128, count, st);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -2005,18 +2005,18 @@ hipError_t dalgo_kmeans_move_sorted(const void* X, int is_bf16, int64_t ldx, int
   constexpr int NW = 4;
   const int64_t max_segs = cdiv(n2, seg) + k;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(max_segs, NW), 256 * 16));
-#define DALGO_DSEG(TT, D)                                                                        \
+#define KM_DSEG_LAUNCH(TT, D)                                                                        \
   hipLaunchKernelGGL((km_dsegsum_kernel<TT, D, NW>), dim3(grid), dim3(NW * 64), 0, st,           \
                      (const TT*)X, ldx, (const int*)perm, (const int*)er, (const int64_t*)cluster_start, \
                      (const int64_t*)seg_start, k, seg, S, cnt, xh, Q)
   switch (DP) {
-    case 16: if (is_bf16) DALGO_DSEG(uint16_t, 16); else DALGO_DSEG(float, 16); break;
-    case 32: if (is_bf16) DALGO_DSEG(uint16_t, 32); else DALGO_DSEG(float, 32); break;
-    case 64: if (is_bf16) DALGO_DSEG(uint16_t, 64); else DALGO_DSEG(float, 64); break;
-    case 128: if (is_bf16) DALGO_DSEG(uint16_t, 128); else DALGO_DSEG(float, 128); break;
+    case 16: if (is_bf16) KM_DSEG_LAUNCH(uint16_t, 16); else KM_DSEG_LAUNCH(float, 16); break;
+    case 32: if (is_bf16) KM_DSEG_LAUNCH(uint16_t, 32); else KM_DSEG_LAUNCH(float, 32); break;
+    case 64: if (is_bf16) KM_DSEG_LAUNCH(uint16_t, 64); else KM_DSEG_LAUNCH(float, 64); break;
+    case 128: if (is_bf16) KM_DSEG_LAUNCH(uint16_t, 128); else KM_DSEG_LAUNCH(float, 128); break;
     default: return hipErrorInvalidValue;
   }
-#undef DALGO_DSEG
+#undef KM_DSEG_LAUNCH
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -545,13 +545,13 @@ hipError_t dalgo_pb_spmv(const uint16_t* srcl, const int64_t* tile_e, const int3
   }
   if ((phases & 1) && nch > 0 && wu_hi > wu_lo) {
     // max_runs: the largest number of non-empty runs of one chunk (LDS table up to 4096)
-#define DALGO_PB_GATHER(GR)                                                                      \
+#define PB_GATHER_LAUNCH(GR)                                                                      \
     hipLaunchKernelGGL((pb_gather_kernel<8192, 4096, 8, GR>), dim3(wu_hi - wu_lo), dim3(8 * 64), 0, st, \
                        srcl, tile_e, tile_ent, tile_run, wu_tile, wu_chunk, chunk_slo, chunk_ns, \
                        chunk_run, run_delta, c, val, n_val - kPbDummy, bound, wu_lo)
-    if (max_runs > 4096) DALGO_PB_GATHER(true);
-    else DALGO_PB_GATHER(false);
-#undef DALGO_PB_GATHER
+    if (max_runs > 4096) PB_GATHER_LAUNCH(true);
+    else PB_GATHER_LAUNCH(false);
+#undef PB_GATHER_LAUNCH
     DALGO_LAUNCH_CHECK();
   }
   if (!(phases & 2) || nwi == 0) return hipSuccess;

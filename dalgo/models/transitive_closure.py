@@ -20,7 +20,6 @@ independent, so ranks need no communication except the int64 count all-reduce):
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -44,11 +43,9 @@ def compact_ids(src: torch.Tensor, dst: torch.Tensor):
     return inv[:n], inv[n:], ids
 
 
-# K9 launch variant (csrc/kernels/closure.hip): 0 / 1 = 128 x 128 tiles with 64 / 128-B K
-# stages, 2 / 3 = 256 x 256 tiles (8 waves, half the operand bytes per MFMA) with 64 / 128-B
-# stages. n = 16384, 1 x MI355X: 1.51 / 1.73 / 2.14 / 2.33 POP/s int8 (torch._int_mm, the
+# K9 (csrc/kernels/closure.hip): 256 x 256 tiles (8 waves, 128-B K stages) when the padded
+# sizes allow, else 128 x 128. n = 16384, 1 x MI355X: 2.33 POP/s int8 (torch._int_mm, the
 # plain library GEMM of the same shape without the OR epilogue: 2.86 POP/s)
-TC_VARIANT = int(os.environ.get("DALGO_TC_VARIANT", "3"))
 
 
 def _round_up(a, b):
@@ -122,7 +119,7 @@ class DenseClosure(_Fixpoint):
     def step(self) -> int:
         if self.dev.type == "cuda":
             self.count.zero_()
-            _ext.ops().tc_step(self.A, self.T, self.T2, self.count, TC_VARIANT)
+            _ext.ops().tc_step(self.A, self.T, self.T2, self.count)
         else:
             C = self.T @ self.A.T                           # C^T[z][x] = sum_y T[z][y] A[x][y]
             self.T2.copy_(((self.T != 0) | (C > 0.5)).to(self.T.dtype))

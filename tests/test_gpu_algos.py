@@ -386,11 +386,10 @@ def test_transitive_closure_gpu(cuda):
         assert b.run().counts == ref, cls.__name__
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("n,nz", [(640, 384), (768, 512)])
-def test_tc_step_kernel_exact(cuda, variant, n, nz):
-    """One K9 step (128 / 256 tiles x both K-staging depths; 256 tiles fall back to 128 when
-    the sizes are not multiples of 256) == (T | (T A^T > 0)) computed in f32 on the CPU."""
+def test_tc_step_kernel_exact(cuda, n, nz):
+    """One K9 step (128 tiles at 640 x 384, 256 tiles at 768 x 512) == (T | (T A^T > 0))
+    computed in f32 on the CPU."""
     from dalgo.ops import _ext
     g = torch.Generator().manual_seed(3)
     A = (torch.rand(n, n, generator=g) < 0.01).to(torch.uint8)
@@ -398,7 +397,7 @@ def test_tc_step_kernel_exact(cuda, variant, n, nz):
     ref = ((T != 0) | ((T.float() @ A.float().T) > 0.5)).to(torch.uint8)
     Tn = torch.zeros_like(T, device=cuda)
     cnt = torch.zeros(1, dtype=torch.int64, device=cuda)
-    _ext.ops().tc_step(A.to(cuda), T.to(cuda), Tn, cnt, variant)
+    _ext.ops().tc_step(A.to(cuda), T.to(cuda), Tn, cnt)
     torch.cuda.synchronize()
     assert torch.equal(Tn.cpu(), ref)
     assert int(cnt.item()) == int(ref.sum())
@@ -417,7 +416,7 @@ def test_spd_inverse_gpu(cuda):
 # K5 als_solve: (R F) Ginv against f64, every launch variant (16x16x32 and 32x32x16 forms),
 # k across 1..8 factor-column tiles, n not a multiple of 16 (tail K-step), rows not a multiple of
 # the block, a strided (non-contiguous rows) R, a K-split count > 1
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("m,n,k", [(100, 500, 10), (1000, 777, 64), (3000, 4096, 33),
                                    (600, 1000, 128), (513, 100, 96), (7, 5, 1), (20000, 3001, 64)])
 def test_als_solve_gpu(cuda, monkeypatch, variant, m, n, k):
