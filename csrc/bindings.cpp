@@ -485,7 +485,7 @@ static void check_ul(const Tensor& ul, int64_t n, const char* what) {
 
 void kmeans_filter(const Tensor& assign, Tensor ul, const Tensor& delta, const Tensor& s,
                    const std::optional<Tensor>& a_prev, Tensor idx, Tensor n_active,
-                   const std::optional<Tensor>& acl, const std::optional<Tensor>& nd, int64_t kpad) {
+                   const std::optional<Tensor>& acl) {
   const int64_t n = assign.numel();
   check_i32(assign, "assign");
   check_ul(ul, n, "kmeans_filter");
@@ -507,19 +507,12 @@ void kmeans_filter(const Tensor& assign, Tensor ul, const Tensor& delta, const T
     TORCH_CHECK(acl->numel() >= idx.numel(), "kmeans_filter: acl [cap]");
     aclp = acl->data_ptr<int32_t>();
   }
-  const float* ndp = nullptr;
-  if (nd.has_value()) {   // near / far keys for the candidate tiles
-    check_f32(*nd, "nd");
-    TORCH_CHECK(aclp != nullptr, "kmeans_filter: nd needs acl");
-    TORCH_CHECK(kpad >= delta.numel() && nd->numel() >= delta.numel() * kpad, "kmeans_filter: nd [k][kpad]");
-    ndp = nd->data_ptr<float>();
-  }
   DeviceGuard guard(assign.device());
   DALGO_CHECK_HIP(dalgo_km_filter(assign.data_ptr<int32_t>(), ul.data_ptr<float>(),
                                   delta.data_ptr<float>(), s.data_ptr<float>(), (int)delta.numel(), n,
                                   app, idx.data_ptr<int32_t>(),
                                   reinterpret_cast<unsigned long long*>(n_active.data_ptr<int64_t>()),
-                                  idx.numel(), aclp, ndp, (int)kpad, cur_stream()),
+                                  idx.numel(), aclp, cur_stream()),
                   "kmeans_filter");
 }
 
@@ -825,6 +818,8 @@ void gb_keys(const Tensor& src, const Tensor& dst, const std::optional<Tensor>& 
   check_i32(src, "src");
   check_i32(dst, "dst");
   TORCH_CHECK(src.numel() == dst.numel(), "gb_keys: src / dst size");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0, "gb_keys: src / dst 16-B aligned");
   const int64_t n = src.numel();
   const int64_t nb = dalgo_gb_key_blocks(n);
   if (new_id) check_i32(*new_id, "new_id");
@@ -863,59 +858,50 @@ void gb_keys(const Tensor& src, const Tensor& dst, const std::optional<Tensor>& 
                   "gb_keys");
 }
 
-// sort keys[:n] over bits [0, end_bit) and deduplicate: returns the distinct count; the
-// distinct keys are in keys[:count] afterwards (work: a scratch tensor of n int64)
-int64_t gb_sort_unique(Tensor keys, int64_t n, int64_t end_bit, Tensor work) {
+// sort keys[:n] over bits [0, end_bit) into out[:n] (rocPRIM onesweep radix sort)
+void gb_sort(const Tensor& keys, int64_t n, int64_t end_bit, Tensor out) {
   check_t(keys, at::kLong, "keys");
-  check_t(work, at::kLong, "work");
-  TORCH_CHECK(n >= 0 && n <= keys.numel() && n <= work.numel(), "gb_sort_unique: sizes");
-  if (n == 0) return 0;
+  check_t(out, at::kLong, "out");
+  TORCH_CHECK(n >= 0 && n <= keys.numel() && n <= out.numel(), "gb_sort: sizes");
+  TORCH_CHECK(end_bit >= 1 && end_bit <= 64, "gb_sort: end_bit");
+  if (n == 0) return;
   DeviceGuard guard(keys.device());
-  auto* k = reinterpret_cast<uint64_t*>(keys.data_ptr<int64_t>());
-  auto* w = reinterpret_cast<uint64_t*>(work.data_ptr<int64_t>());
-  size_t b_sort = 0, b_uniq = 0;
-  DALGO_CHECK_HIP(dalgo_gb_sort(nullptr, &b_sort, k, w, n, (int)end_bit, cur_stream()), "gb_sort(size)");
-  DALGO_CHECK_HIP(dalgo_gb_unique(nullptr, &b_uniq, w, k, nullptr, n, cur_stream()), "gb_unique(size)");
-  Tensor tmp = at::empty({(int64_t)std::max(b_sort, b_uniq) + 256}, keys.options().dtype(at::kByte));
-  Tensor cnt = at::zeros({1}, keys.options());
-  size_t bs = b_sort, bu = b_uniq;
-  DALGO_CHECK_HIP(dalgo_gb_sort(tmp.data_ptr(), &bs, k, w, n, (int)end_bit, cur_stream()), "gb_sort");
-  DALGO_CHECK_HIP(dalgo_gb_unique(tmp.data_ptr(), &bu, w, k,
-                                  reinterpret_cast<unsigned long long*>(cnt.data_ptr<int64_t>()), n,
-                                  cur_stream()),
-                  "gb_unique");
-  return cnt.item<int64_t>();
+  auto* k = reinterpret_cast<const uint64_t*>(keys.data_ptr<int64_t>());
+  auto* o = reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>());
+  size_t bytes = 0;
+  DALGO_CHECK_HIP(dalgo_gb_sort(nullptr, &bytes, k, o, n, (int)end_bit, cur_stream()), "gb_sort(size)");
+  Tensor tmp = at::empty({(int64_t)bytes + 256}, keys.options().dtype(at::kByte));
+  DALGO_CHECK_HIP(dalgo_gb_sort(tmp.data_ptr(), &bytes, k, o, n, (int)end_bit, cur_stream()), "gb_sort");
 }
 
-void gb_decode(const Tensor& K, int64_t E, int64_t shift, int64_t dbits, const Tensor& blk_base,
-               int64_t phase, const std::optional<Tensor>& ent_counts, const std::optional<Tensor>& outdeg,
-               const std::optional<Tensor>& ent_offsets, const std::optional<Tensor>& srcl,
+void gb_decode(const Tensor& K, int64_t n, int64_t shift, int64_t dbits, const Tensor& blk_base,
+               int64_t phase, const std::optional<Tensor>& counts, const std::optional<Tensor>& outdeg,
+               const std::optional<Tensor>& offsets, const std::optional<Tensor>& srcl,
                const std::optional<Tensor>& ent_end, const std::optional<Tensor>& ent_blk,
                const std::optional<Tensor>& ent_dst) {
   check_t(K, at::kLong, "K");
-  TORCH_CHECK(E >= 0 && E <= K.numel(), "gb_decode: E");
+  TORCH_CHECK(n >= 0 && n <= K.numel(), "gb_decode: n");
   check_t(blk_base, at::kLong, "blk_base");
-  const int64_t nb = dalgo_gb_decode_blocks(E);
+  const int64_t nb = dalgo_gb_decode_blocks(n);
   if (phase == 0) {
-    TORCH_CHECK(ent_counts && outdeg, "gb_decode: ent_counts / outdeg");
-    check_i32(*ent_counts, "ent_counts");
+    TORCH_CHECK(counts && outdeg, "gb_decode: counts / outdeg");
+    check_t(*counts, at::kLong, "counts");
     check_i32(*outdeg, "outdeg");
-    TORCH_CHECK(ent_counts->numel() >= nb, "gb_decode: ent_counts [blocks]");
+    TORCH_CHECK(counts->numel() >= 2 * nb, "gb_decode: counts [2 blocks]");
   } else {
-    TORCH_CHECK(ent_offsets && srcl && ent_end && ent_blk && ent_dst, "gb_decode: outputs");
-    check_t(*ent_offsets, at::kLong, "ent_offsets");
-    TORCH_CHECK(ent_offsets->numel() >= nb, "gb_decode: ent_offsets [blocks]");
+    TORCH_CHECK(offsets && srcl && ent_end && ent_blk && ent_dst, "gb_decode: outputs");
+    check_t(*offsets, at::kLong, "offsets");
+    TORCH_CHECK(offsets->numel() >= 2 * nb, "gb_decode: offsets [2 blocks]");
     check_t(*srcl, at::kShort, "srcl");
-    TORCH_CHECK(srcl->numel() >= E, "gb_decode: srcl");
     check_t(*ent_end, at::kLong, "ent_end");
     check_i32(*ent_blk, "ent_blk");
     check_i32(*ent_dst, "ent_dst");
   }
   DeviceGuard guard(K.device());
-  DALGO_CHECK_HIP(dalgo_gb_decode(reinterpret_cast<const uint64_t*>(K.data_ptr<int64_t>()), E, (int)shift,
+  DALGO_CHECK_HIP(dalgo_gb_decode(reinterpret_cast<const uint64_t*>(K.data_ptr<int64_t>()), n, (int)shift,
                                   (int)dbits, blk_base.data_ptr<int64_t>(), (int)phase,
-                                  opt_ptr<int32_t>(ent_counts), opt_ptr<uint32_t>(outdeg),
-                                  opt_ptr<const int64_t>(ent_offsets), opt_ptr<uint16_t>(srcl),
+                                  opt_ptr<int64_t>(counts), opt_ptr<uint32_t>(outdeg),
+                                  opt_ptr<const int64_t>(offsets), opt_ptr<uint16_t>(srcl),
                                   opt_ptr<int64_t>(ent_end), opt_ptr<int32_t>(ent_blk),
                                   opt_ptr<int32_t>(ent_dst), cur_stream()),
                   "gb_decode");
@@ -1395,8 +1381,7 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(i!) er, Tensor? m_dev=None, int chunk=65536, Tensor? cnew=None, "
         "Tensor? cold=None) -> ()");
   m.def("kmeans_filter(Tensor assign, Tensor(a!) ul, Tensor delta, Tensor s, "
-        "Tensor(b!)? a_prev, Tensor(c!) idx, Tensor(d!) n_active, Tensor(f!)? acl=None, "
-        "Tensor? nd=None, int kpad=0) -> ()");
+        "Tensor(b!)? a_prev, Tensor(c!) idx, Tensor(d!) n_active, Tensor(f!)? acl=None) -> ()");
   m.def("kmeans_sort_active(Tensor acl, Tensor idx, Tensor n_active, int k, int chunk, "
         "Tensor(a!) block_counts, Tensor(b!) cstart, Tensor(c!) seg_start, Tensor(d!) rows_sorted, "
         "int tile, Tensor(e!) tiles, Tensor(g!) n_tiles) -> ()");
@@ -1421,9 +1406,9 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("gb_keys(Tensor src, Tensor dst, Tensor? new_id, int v_lo, int v_hi, int sl, int world, int rank, "
         "int dbits, int phase, Tensor(a!)? bitmap, Tensor(b!)? counts, Tensor? offsets, int base_all, "
         "Tensor(c!)? keys, Tensor? word_prefix, Tensor? seg_start, Tensor? seg_blk0) -> ()");
-  m.def("gb_sort_unique(Tensor(a!) keys, int n, int end_bit, Tensor(b!) work) -> int");
-  m.def("gb_decode(Tensor K, int E, int shift, int dbits, Tensor blk_base, int phase, "
-        "Tensor(a!)? ent_counts, Tensor(b!)? outdeg, Tensor? ent_offsets, Tensor(c!)? srcl, "
+  m.def("gb_sort(Tensor keys, int n, int end_bit, Tensor(a!) out) -> ()");
+  m.def("gb_decode(Tensor K, int n, int shift, int dbits, Tensor blk_base, int phase, "
+        "Tensor(a!)? counts, Tensor(b!)? outdeg, Tensor? offsets, Tensor(c!)? srcl, "
         "Tensor(d!)? ent_end, Tensor(e!)? ent_blk, Tensor(f!)? ent_dst) -> ()");
   m.def("gb_entry_flags(Tensor ent_blk, Tensor ent_dst, Tensor ent_end, int bin_shift, Tensor(a!) rs, "
         "Tensor(b!) cs, Tensor(c!) srcl) -> ()");
@@ -1486,7 +1471,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("rmat_edges", &rmat_edges);
   m.impl("gb_degree", &gb_degree);
   m.impl("gb_keys", &gb_keys);
-  m.impl("gb_sort_unique", &gb_sort_unique);
+  m.impl("gb_sort", &gb_sort);
   m.impl("gb_decode", &gb_decode);
   m.impl("gb_entry_flags", &gb_entry_flags);
   m.impl("gb_entry_place", &gb_entry_place);

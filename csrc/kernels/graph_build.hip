@@ -4,8 +4,8 @@
 // The K4b layout (pr_binned.hip) wants the deduplicated edges ordered by (source chunk,
 // destination, source): one 64-bit key per edge = block | local destination | source
 // offset in its 8192-source block, so ONE radix sort (rocPRIM onesweep over only the
-// key's bits) + one unique pass produce the distinct edges already in layout order. The
-// passes around it are single sweeps:
+// key's bits) puts the edges in layout order, and the decode pass skips the duplicates
+// (a distinct edge = the last copy of its key). The passes around it are single sweeps:
 //   degree   -- raw out-degree of the input edges (degree relabeling), u32 atomics;
 //   keys     -- relabel, keep this rank's destinations, map sources to the [own | ghost]
 //               index space and pack the key (two-phase compaction: count, write);
@@ -19,7 +19,6 @@
 // torch on the device (dalgo/ops/graph.py::build_blocked_native).
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_select.hpp>
 
 #include <cstdint>
 
@@ -90,7 +89,28 @@ __device__ __forceinline__ uint64_t gb_key(const GbKeyCtx& c, int32_t s, int64_t
   return (blk << (c.dbits + kSpanBits)) | ((uint64_t)dl << kSpanBits) | (uint64_t)(rel & (kSpan - 1));
 }
 
-constexpr int kKeyR = 8192;          // edges per block of the two key phases
+constexpr int kKeyR = 16384;         // edges per block of the two key phases
+constexpr int kKeyV = 4;             // edges per thread per step (int4 loads, 8 gathers in flight)
+
+__device__ __forceinline__ void gb_load4(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                         int64_t i, int64_t r1, int32_t (&s)[kKeyV], int32_t (&d)[kKeyV],
+                                         bool (&in)[kKeyV]) {
+  if (i + kKeyV <= r1) {
+    const int4 a = *reinterpret_cast<const int4*>(src + i);
+    const int4 b = *reinterpret_cast<const int4*>(dst + i);
+    s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
+    d[0] = b.x; d[1] = b.y; d[2] = b.z; d[3] = b.w;
+#pragma unroll
+    for (int v = 0; v < kKeyV; ++v) in[v] = true;
+  } else {
+#pragma unroll
+    for (int v = 0; v < kKeyV; ++v) {
+      in[v] = i + v < r1;
+      s[v] = in[v] ? src[i + v] : 0;
+      d[v] = in[v] ? dst[i + v] : 0;
+    }
+  }
+}
 
 // phase 0: count the kept edges per block (and mark remote sources, W > 1)
 __global__ void __launch_bounds__(256) gb_keys_count_kernel(const int32_t* __restrict__ src,
@@ -103,12 +123,18 @@ __global__ void __launch_bounds__(256) gb_keys_count_kernel(const int32_t* __res
   const int64_t r0 = (int64_t)blockIdx.x * kKeyR;
   const int64_t r1 = r0 + kKeyR < n ? r0 + kKeyR : n;
   int mine = 0;
-  for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) {
-    int32_t s;
-    int64_t dl;
-    if (gb_edge(c, src[i], dst[i], s, dl)) {
-      ++mine;
-      if (c.world > 1 && !(s >= c.v_lo && s < c.v_hi)) atomicOr(bitmap + (s >> 5), 1u << (s & 31));
+  for (int64_t i = r0 + (int64_t)threadIdx.x * kKeyV; i < r1; i += 256 * kKeyV) {
+    int32_t s0[kKeyV], d0[kKeyV];
+    bool in[kKeyV];
+    gb_load4(src, dst, i, r1, s0, d0, in);
+#pragma unroll
+    for (int v = 0; v < kKeyV; ++v) {
+      int32_t sv;
+      int64_t dl;
+      if (in[v] && gb_edge(c, s0[v], d0[v], sv, dl)) {
+        ++mine;
+        if (c.world > 1 && !(sv >= c.v_lo && sv < c.v_hi)) atomicOr(bitmap + (sv >> 5), 1u << (sv & 31));
+      }
     }
   }
   atomicAdd(&s_cnt, mine);
@@ -129,97 +155,152 @@ __global__ void __launch_bounds__(256) gb_keys_write_kernel(const int32_t* __res
   const int64_t r1 = r0 + kKeyR < n ? r0 + kKeyR : n;
   const int64_t base = offsets ? offsets[blockIdx.x] : base_all + r0;
   const int lane = threadIdx.x & 63;
-  for (int64_t i0 = r0; i0 < r1; i0 += 256) {
-    const int64_t i = i0 + threadIdx.x;
-    int32_t s = 0;
-    int64_t dl = 0;
-    const bool keep = i < r1 && gb_edge(c, src[i], dst[i], s, dl);
-    const uint64_t m = __ballot(keep);
-    int wbase = 0;
-    if (lane == 0 && m) wbase = atomicAdd(&s_cur, __popcll(m));
-    wbase = __shfl(wbase, 0, 64);
-    if (keep) {
-      const int r = __popcll(m & ((1ull << lane) - 1ull));
-      keys[base + wbase + r] = gb_key(c, s, dl);
+  for (int64_t i0 = r0; i0 < r1; i0 += 256 * kKeyV) {
+    const int64_t i = i0 + (int64_t)threadIdx.x * kKeyV;
+    int32_t s0[kKeyV], d0[kKeyV], sv[kKeyV];
+    int64_t dl[kKeyV];
+    bool in[kKeyV], keep[kKeyV];
+    gb_load4(src, dst, i, r1, s0, d0, in);
+    int cnt = 0;
+#pragma unroll
+    for (int v = 0; v < kKeyV; ++v) {
+      keep[v] = in[v] && gb_edge(c, s0[v], d0[v], sv[v], dl[v]);
+      cnt += keep[v] ? 1 : 0;
     }
+    // wave-inclusive scan of the counts, one LDS cursor bump per wave
+    int x = cnt;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    int wbase = 0;
+    if (lane == 63 && x) wbase = atomicAdd(&s_cur, x);
+    wbase = __shfl(wbase, 63, 64);
+    int64_t o = base + wbase + x - cnt;
+#pragma unroll
+    for (int v = 0; v < kKeyV; ++v)
+      if (keep[v]) keys[o++] = gb_key(c, sv[v], dl[v]);
   }
 }
 
 // ---------------------------------------------------------------------------- decode
-constexpr int kDecR = 65536;         // distinct edges per block of the decode kernels
-constexpr int kDecT = 256;           // threads; each owns kDecR / kDecT consecutive edges
+// Over the SORTED keys with duplicates (the dedup is folded in: no separate unique pass).
+// The last copy of every key stands for the distinct edge; an entry (block, destination)
+// ends at the last copy of its last key. Blocks of kDecR keys, each thread 4 consecutive
+// keys per step (coalesced), one block scan per step places the distinct edges and the
+// entries in key order.
+constexpr int kDecR = 65536;         // keys per block of the decode kernels
+constexpr int kDecT = 256;
+constexpr int kDecV = 4;             // keys per thread per step
 
-__device__ __forceinline__ bool gb_end(const uint64_t* K, int64_t i, int64_t E) {
-  return i == E - 1 || (K[i + 1] >> kSpanBits) != (K[i] >> kSpanBits);
+__device__ __forceinline__ void gb_flags(const uint64_t* __restrict__ K, int64_t n, int64_t i,
+                                         bool& last, bool& end, uint64_t& k) {
+  k = K[i];
+  const bool has_next = i + 1 < n;
+  const uint64_t kn = has_next ? K[i + 1] : ~0ull;
+  last = !has_next || kn != k;
+  end = last && (!has_next || (kn >> kSpanBits) != (k >> kSpanBits));
 }
 
-// entry ends per block + the deduplicated out-degree per local source (LDS histogram of
-// the block's first source block; edges of later source blocks in the range: global atomics)
-__global__ void __launch_bounds__(kDecT) gb_decode_count_kernel(const uint64_t* __restrict__ K, int64_t E,
+// per block: distinct edges, entries, and the distinct out-degree per local source (LDS
+// histogram of the block's first source block; other source blocks: global atomics)
+__global__ void __launch_bounds__(kDecT) gb_decode_count_kernel(const uint64_t* __restrict__ K, int64_t n,
                                                                 int shift, const int64_t* __restrict__ blk_base,
-                                                                int32_t* __restrict__ ent_counts,
+                                                                int64_t* __restrict__ counts,
                                                                 uint32_t* __restrict__ outdeg) {
   __shared__ uint32_t hist[kSpan];
-  __shared__ int s_cnt;
+  __shared__ int s_d, s_e;
   for (int j = threadIdx.x; j < kSpan; j += kDecT) hist[j] = 0u;
-  if (threadIdx.x == 0) s_cnt = 0;
+  if (threadIdx.x == 0) { s_d = 0; s_e = 0; }
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * kDecR;
-  const int64_t r1 = r0 + kDecR < E ? r0 + kDecR : E;
+  const int64_t r1 = r0 + kDecR < n ? r0 + kDecR : n;
   const uint64_t blk0 = K[r0] >> shift;
-  int mine = 0;
+  int md = 0, me = 0;
   for (int64_t i = r0 + threadIdx.x; i < r1; i += kDecT) {
-    const uint64_t k = K[i];
-    const uint64_t blk = k >> shift;
-    const uint32_t off = (uint32_t)(k & (kSpan - 1));
-    if (blk == blk0) atomicAdd(hist + off, 1u);
-    else atomicAdd(outdeg + blk_base[blk] + off, 1u);
-    mine += gb_end(K, i, E) ? 1 : 0;
+    bool last, end;
+    uint64_t k;
+    gb_flags(K, n, i, last, end, k);
+    if (last) {
+      ++md;
+      const uint64_t blk = k >> shift;
+      const uint32_t off = (uint32_t)(k & (kSpan - 1));
+      if (blk == blk0) atomicAdd(hist + off, 1u);
+      else atomicAdd(outdeg + blk_base[blk] + off, 1u);
+    }
+    me += end ? 1 : 0;
   }
-  atomicAdd(&s_cnt, mine);
+  atomicAdd(&s_d, md);
+  atomicAdd(&s_e, me);
   __syncthreads();
   const int64_t b0 = blk_base[blk0];
   for (int j = threadIdx.x; j < kSpan; j += kDecT)
     if (hist[j]) atomicAdd(outdeg + b0 + j, hist[j]);
-  if (threadIdx.x == 0) ent_counts[blockIdx.x] = s_cnt;
+  if (threadIdx.x == 0) {
+    counts[2 * blockIdx.x] = s_d;
+    counts[2 * blockIdx.x + 1] = s_e;
+  }
 }
 
-// srcl (u16 source offset | 0x8000 on an entry's end edge) and the entry list in key
-// order: each thread owns a contiguous piece, one block scan places the pieces
-__global__ void __launch_bounds__(kDecT) gb_decode_write_kernel(const uint64_t* __restrict__ K, int64_t E,
+// offsets[2 b] / [2 b + 1]: distinct edges / entries before block b
+__global__ void __launch_bounds__(kDecT) gb_decode_write_kernel(const uint64_t* __restrict__ K, int64_t n,
                                                                 int shift, int dbits,
-                                                                const int64_t* __restrict__ ent_offsets,
+                                                                const int64_t* __restrict__ offsets,
                                                                 uint16_t* __restrict__ srcl,
                                                                 int64_t* __restrict__ ent_end,
                                                                 int32_t* __restrict__ ent_blk,
                                                                 int32_t* __restrict__ ent_dst) {
-  __shared__ int s_scan[kDecT];
-  constexpr int PER = kDecR / kDecT;
-  const int64_t r0 = (int64_t)blockIdx.x * kDecR + (int64_t)threadIdx.x * PER;
-  const int64_t r1 = r0 + PER < E ? r0 + PER : E;
-  int cnt = 0;
-  for (int64_t i = r0; i < r1; ++i) cnt += gb_end(K, i, E) ? 1 : 0;
-  s_scan[threadIdx.x] = cnt;
-  __syncthreads();
-  // inclusive Hillis-Steele scan over 256 counts
-  for (int off = 1; off < kDecT; off <<= 1) {
-    const int v = threadIdx.x >= off ? s_scan[threadIdx.x - off] : 0;
-    __syncthreads();
-    s_scan[threadIdx.x] += v;
-    __syncthreads();
-  }
-  int64_t pos = ent_offsets[blockIdx.x] + s_scan[threadIdx.x] - cnt;
+  __shared__ int s_wd[kDecT / 64], s_we[kDecT / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * kDecR;
+  const int64_t r1 = r0 + kDecR < n ? r0 + kDecR : n;
+  int64_t dbase = offsets[2 * blockIdx.x], ebase = offsets[2 * blockIdx.x + 1];
   const uint64_t dmask = (1ull << dbits) - 1ull;
-  for (int64_t i = r0; i < r1; ++i) {
-    const uint64_t k = K[i];
-    const bool end = gb_end(K, i, E);
-    srcl[i] = (uint16_t)((k & (kSpan - 1)) | (end ? 0x8000u : 0u));
-    if (end) {
-      ent_end[pos] = i;
-      ent_blk[pos] = (int32_t)(k >> shift);
-      ent_dst[pos] = (int32_t)((k >> kSpanBits) & dmask);
-      ++pos;
+  for (int64_t i0 = r0; i0 < r1; i0 += (int64_t)kDecT * kDecV) {
+    const int64_t ib = i0 + (int64_t)threadIdx.x * kDecV;
+    bool last[kDecV], end[kDecV];
+    uint64_t k[kDecV];
+    int cd = 0, ce = 0;
+#pragma unroll
+    for (int v = 0; v < kDecV; ++v) {
+      last[v] = end[v] = false;
+      k[v] = 0;
+      if (ib + v < r1) gb_flags(K, n, ib + v, last[v], end[v], k[v]);
+      cd += last[v] ? 1 : 0;
+      ce += end[v] ? 1 : 0;
     }
+    // block-wide exclusive scan of (cd, ce), packed (each <= 1024 per step)
+    int x = cd | (ce << 16);
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) { s_wd[wid] = x & 0xffff; s_we[wid] = x >> 16; }
+    __syncthreads();
+    int pd = (x & 0xffff) - cd, pe = (x >> 16) - ce, td = 0, te = 0;
+#pragma unroll
+    for (int w = 0; w < kDecT / 64; ++w) {
+      if (w < wid) { pd += s_wd[w]; pe += s_we[w]; }
+      td += s_wd[w];
+      te += s_we[w];
+    }
+    int64_t d = dbase + pd, e = ebase + pe;
+#pragma unroll
+    for (int v = 0; v < kDecV; ++v) {
+      if (last[v]) {
+        srcl[d] = (uint16_t)((k[v] & (kSpan - 1)) | (end[v] ? 0x8000u : 0u));
+        if (end[v]) {
+          ent_end[e] = d;
+          ent_blk[e] = (int32_t)(k[v] >> shift);
+          ent_dst[e] = (int32_t)((k[v] >> kSpanBits) & dmask);
+          ++e;
+        }
+        ++d;
+      }
+    }
+    dbase += td;
+    ebase += te;
+    __syncthreads();
   }
 }
 
@@ -321,28 +402,23 @@ hipError_t dalgo_gb_sort(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint6
   return rocprim::radix_sort_keys(tmp, *tmp_bytes, in, out, (size_t)n, 0u, (unsigned)end_bit, st);
 }
 
-// rocPRIM unique over sorted keys (n < 2^32); the count lands in *count (device)
-hipError_t dalgo_gb_unique(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out,
-                           unsigned long long* count, int64_t n, hipStream_t st) {
-  if (n < 0 || n >= (int64_t)0xffffffffLL) return hipErrorInvalidValue;
-  return rocprim::unique(tmp, *tmp_bytes, in, out, count, (size_t)n, rocprim::equal_to<uint64_t>(), st);
-}
+int64_t dalgo_gb_decode_blocks(int64_t n) { return cdiv(n, (int64_t)kDecR); }
 
-int64_t dalgo_gb_decode_blocks(int64_t E) { return cdiv(E, (int64_t)kDecR); }
-
-hipError_t dalgo_gb_decode(const uint64_t* K, int64_t E, int shift, int dbits, const int64_t* blk_base,
-                           int phase, int32_t* ent_counts, uint32_t* outdeg, const int64_t* ent_offsets,
+// phase 0: counts[2 b], [2 b + 1] = distinct edges / entries of block b, outdeg += the
+// distinct out-degrees; phase 1 (offsets = exclusive scan of counts): srcl and the entries
+hipError_t dalgo_gb_decode(const uint64_t* K, int64_t n, int shift, int dbits, const int64_t* blk_base,
+                           int phase, int64_t* counts, uint32_t* outdeg, const int64_t* offsets,
                            uint16_t* srcl, int64_t* ent_end, int32_t* ent_blk, int32_t* ent_dst,
                            hipStream_t st) {
-  if (E <= 0) return hipSuccess;
+  if (n <= 0) return hipSuccess;
   if (shift < kSpanBits || shift > 63 || dbits < 0 || dbits > 31) return hipErrorInvalidValue;
-  const int64_t g = cdiv(E, (int64_t)kDecR);
+  const int64_t g = cdiv(n, (int64_t)kDecR);
   if (phase == 0)
-    hipLaunchKernelGGL(gb_decode_count_kernel, dim3((unsigned)g), dim3(kDecT), 0, st, K, E, shift, blk_base,
-                       ent_counts, outdeg);
+    hipLaunchKernelGGL(gb_decode_count_kernel, dim3((unsigned)g), dim3(kDecT), 0, st, K, n, shift, blk_base,
+                       counts, outdeg);
   else
-    hipLaunchKernelGGL(gb_decode_write_kernel, dim3((unsigned)g), dim3(kDecT), 0, st, K, E, shift, dbits,
-                       ent_offsets, srcl, ent_end, ent_blk, ent_dst);
+    hipLaunchKernelGGL(gb_decode_write_kernel, dim3((unsigned)g), dim3(kDecT), 0, st, K, n, shift, dbits,
+                       offsets, srcl, ent_end, ent_blk, ent_dst);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

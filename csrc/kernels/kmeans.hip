@@ -484,7 +484,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   const float* hbase = hn;
   if constexpr (CAND) {
     const int4 tr = trn;
-    acl = tr.x >> 1;                           // tile key = 2 cluster + far (km_filter_kernel)
+    acl = tr.x;
     pend = tr.z;
     pbase = (int64_t)tr.y + (int64_t)wid * (PT * 32);
     hbase = aux.hnb + (int64_t)acl * kpad;
@@ -1606,6 +1606,7 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   extern __shared__ __attribute__((aligned(16))) float s_hn16[];   // [kpad]: 0.5|c|^2 + M
   __shared__ float s_m[NW];
   __shared__ double s_sse[NW];
+  __shared__ float s_x2[NW][PG * 16];           // |x|^2 per point (read in the epilogue)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lg = lane >> 4, pl = lane & 15;
   const int nchunk = kpad / CH;
@@ -1629,7 +1630,6 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
 #pragma unroll
         for (int s = 0; s < KS; ++s) bf[g][s] = make_uint4(0u, 0u, 0u, 0u);
   }
-  float x2[PG];
   float mx = 0.f;
 #pragma unroll
   for (int g = 0; g < PG; ++g) {
@@ -1646,7 +1646,7 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
     }
     q += __shfl_xor(q, 16, 64);
     q += __shfl_xor(q, 32, 64);
-    x2[g] = q;
+    if (lg == 0) s_x2[wid][g * 16 + pl] = q;
     mx = fmaxf(mx, 0.5f * q);
   }
   for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
@@ -1655,24 +1655,25 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   // ---- chunk DMA (the 32x32 form's image: slot (row, jj) holds piece jj ^ (row & SWZ));
   // the global address is an SGPR base (the chunk) + a loop-invariant VGPR offset, the
   // LDS destination an SGPR (m0): no per-chunk vector address arithmetic
-  uint32_t src_off[GPT];
-#pragma unroll
-  for (int g = 0; g < GPT; ++g) {
-    const int qq = g * NT + tid, row = qq / NJ, jj = qq % NJ;
-    src_off[g] = (uint32_t)(row * DP + (jj ^ (row & SWZ)) * 8) * 2u;
-  }
+  // slot qq = g * NT + tid: row = qq / NJ, piece jj = qq % NJ = tid % NJ; NT / NJ rows per
+  // round is a multiple of SWZ + 1, so the swizzle term (row & SWZ) does not depend on g:
+  // round g is the same VGPR offset + g * (NT / NJ) rows, added to the SGPR base
+  static_assert((NT / NJ) % (SWZ + 1) == 0 && NT % NJ == 0, "DMA offset layout");
+  const uint32_t src_off = (uint32_t)((tid / NJ) * DP + ((tid % NJ) ^ ((tid / NJ) & SWZ)) * 8) * 2u;
   const uint32_t lds_w = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)(km_lds_void*)s_c + (uint32_t)(wid * 64 * 16));
-  auto issue = [&](int ch) {
+  auto issue_to = [&](int ch, int buf) {
     const uint16_t* base = Cq + (int64_t)ch * CH * DP;
-    const uint32_t dst = lds_w + (uint32_t)(((ch % NBUF) * CHP) * 16);
+    const uint32_t dst = lds_w + (uint32_t)((buf * CHP) * 16);
 #pragma unroll
     for (int g = 0; g < GPT; ++g) {
       const uint32_t m0v = dst + (uint32_t)(g * NT * 16);
+      const uint16_t* bg = base + g * (NT / NJ) * DP;
       asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
-                   :: "s"(m0v), "v"(src_off[g]), "s"(base) : "memory");
+                   :: "s"(m0v), "v"(src_off), "s"(bg) : "memory");
     }
   };
+  auto issue = [&](int ch) { issue_to(ch, ch % NBUF); };
   __syncthreads();
   float M = s_m[0];
 #pragma unroll
@@ -1702,9 +1703,9 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   }
   auto load_frag = [&](const uint4* img, int ch, int sub, uint4 (&af)[KS], float4& h4) {
     const int row = sub * 16 + pl;
+    h4 = *reinterpret_cast<const float4*>(&s_hn16[ch * CH + sub * 16 + 4 * lg]);
 #pragma unroll
     for (int s = 0; s < KS; ++s) af[s] = img[row * NJ + ((4 * s + lg) ^ (row & SWZ))];
-    h4 = *reinterpret_cast<const float4*>(&s_hn16[ch * CH + sub * 16 + 4 * lg]);
   };
   auto mfma_sub = [&](f32x4 (&ac)[PG], const uint4 (&af)[KS], const float4& h4) {
     const f32x4 c0 = {h4.x, h4.y, h4.z, h4.w};
@@ -1732,32 +1733,33 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
     }
   };
   // interleave: 24 MFMAs of this sub-tile, the previous sub-tile's 36 argmin VALU ops
-  // (1.5 per MFMA: inside the 8 issue cycles a 16x16x32 MFMA leaves free) and the next
-  // sub-tile's 5 fragment reads early in the group
+  // (1.5 per MFMA: inside the 8 issue cycles a 16x16x32 MFMA leaves free), and the next
+  // sub-tile's fragment reads each right after the MFMAs that last read the register it
+  // replaces (k-step s of all PG groups, then fragment s is dead): the next C values and
+  // fragment 0 after MFMA 6, fragment 1 after 12, 2 after 18, 3 after 24 -- the two
+  // fragment sets share registers instead of both living through the whole sub-tile
   auto pin = [&]() {
 #ifndef KM_XP_NOPIN
 #pragma unroll
     for (int i = 0; i < KS * PG; i += 2) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                 // MFMA
       __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);                 // VALU
-      if (i < 5) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);      // DS read
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-      if (i + 1 < 5) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      if (i + 2 == PG) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS read
+      else if ((i + 2) % PG == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
 #endif
   };
   uint4 a[KS], an[KS];
   float4 h4, hn4;
+  km_wait_vmcnt<0>();
+  __syncthreads();                             // chunk 0 landed, s_hn16 written
+  if (nchunk > 1) issue(1);
+  load_frag(s_c, 0, 0, a, h4);
   for (int ch = 0; ch < nchunk; ++ch) {
-    km_wait_vmcnt<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();              // chunk ch landed; chunk ch - 1 retired
-    asm volatile("" ::: "memory");
-    if (ch + 1 < nchunk) issue(ch + 1);
     const uint4* img = s_c + (ch % NBUF) * CHP;
-    load_frag(img, ch, 0, a, h4);
-    __builtin_amdgcn_sched_barrier(0);
+    const uint4* img_next = s_c + ((ch + 1) % NBUF) * CHP;
     // sub-tile 0 under the previous chunk's sub-tile 7 argmin, then the merge of that chunk
     load_frag(img, ch, 1, an, hn4);
     mfma_sub(acc[0], a, h4);
@@ -1777,13 +1779,34 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
 #pragma unroll
       for (int s = 0; s < KS; ++s) a[s] = an[s];
       h4 = hn4;
+      // (branch-free: the last chunk re-reads its own first fragments, unused)
       if (sub + 1 < NSUB) load_frag(img, ch, sub + 1, an, hn4);
+      else load_frag(ch + 1 < nchunk ? img_next : img, ch + 1 < nchunk ? ch + 1 : ch, 0, an, hn4);
       mfma_sub(acc[sub & 1], a, h4);
       argmin_sub(acc[(sub - 1) & 1], sub - 1);
       pin();
       __builtin_amdgcn_sched_barrier(0);
+      if (sub == NSUB - 2) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        km_wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();          // chunk ch + 1 landed; chunk ch retired
+        asm volatile("" ::: "memory");
+        {
+          // branch-free (a branch here splits the unrolled body and spills): past the
+          // end the last chunk is loaded again into buffer (ch + 2) % 2, which no wave reads
+          // again (chunk ch's, all of whose reads precede the barrier) or which already
+          // holds those same bytes (the last chunk's own)
+          const int c2 = ch + 2 < nchunk ? ch + 2 : nchunk - 1;
+          issue_to(c2, (ch + 2) % NBUF);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) a[s] = an[s];
+    h4 = hn4;
   }
+  km_wait_vmcnt<0>();                          // the redundant last DMAs landed
   // the last chunk's sub-tile 7 and merge
   argmin_sub(acc[1], 7);
 #pragma unroll
@@ -1808,10 +1831,11 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
     }
     const int64_t p = pbase + g * 16 + pl;
     if (lg == 0 && p < n) {
-      const float dist = fmaxf(2.f * (v - M) + x2[g], 0.f);
+      const float x2 = s_x2[wid][g * 16 + pl];
+      const float dist = fmaxf(2.f * (v - M) + x2, 0.f);
       assign[p] = id;
       if (mind) mind[p] = dist;
-      if (xh) xh[p] = 0.5f * x2[g];
+      if (xh) xh[p] = 0.5f * x2;
       my_sse += (double)dist;
     }
   }
@@ -1830,9 +1854,11 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
 }
 
 // the 16x16x32 form holds two 32 KB centre chunks plus 0.5|c|^2 for every centre in LDS
-// and runs two blocks per CU: it takes kpad <= 3840; larger k goes to the pipelined form
+// and runs two blocks per CU: it takes kpad <= 3456; larger k goes to the pipelined form
 static bool assign16_fits(int kpad) {
-  return kpad % 128 == 0 && 2 * 128 * 128 * 2 + (size_t)kpad * sizeof(float) + 1024 <= 80 * 1024;
+  // static: 2 chunk buffers (64 KB) + |x|^2 of the 384 points + small; 2 blocks per CU
+  return kpad % 128 == 0 && 2 * 128 * 128 * 2 + 4 * 6 * 16 * 4 + (size_t)kpad * sizeof(float) + 1024 <=
+                                80 * 1024;
 }
 
 static hipError_t launch_assign16(const void* X, int64_t n, int64_t ldx, const void* Cq,

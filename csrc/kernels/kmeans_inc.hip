@@ -101,13 +101,9 @@ km_filter_kernel(const int32_t* __restrict__ assign, float2* __restrict__ ul,
                  const float* __restrict__ delta, const float* __restrict__ s, int k, int64_t n,
                  int32_t* __restrict__ a_prev, int32_t* __restrict__ idx,
                  unsigned long long* __restrict__ n_active, int64_t cap,
-                 int32_t* __restrict__ acl, const float* __restrict__ nd, int kpad) {
+                 int32_t* __restrict__ acl) {
   // acl (optional): cluster of every appended row, in list order (the candidate-pruned
-  // K2 sorts the active rows by it). nd (optional, with acl): the centres' neighbour
-  // distance lists [k][kpad]; acl then holds 2 a + far, far = the row's distance bound
-  // u + delta[a] reaches half the distance to a's 129th-nearest centre: a tile of near rows
-  // (far = 0) can be pruned to its first 128-centre chunk, and tiles never mix the two
-  // (the sort runs over 2 k keys), so the far rows no longer stretch every tile's stream
+  // K2 sorts the active rows by it)
   __shared__ int32_t s_buf[kDiffBuf];
   __shared__ int32_t s_cl[kDiffBuf];
   __shared__ int s_cnt;
@@ -183,9 +179,7 @@ km_filter_kernel(const int32_t* __restrict__ assign, float2* __restrict__ ul,
         if (act) {
           const uint64_t below = lane == 0 ? 0ull : (mask & (~0ull >> (64 - lane)));
           s_buf[b + __popcll(below)] = (int32_t)i;
-          int key = a[e];
-          if (nd) key = 2 * key + (kpad > 128 && 2.f * ub[e] >= nd[(int64_t)a[e] * kpad + 128] ? 1 : 0);
-          s_cl[b + __popcll(below)] = key;
+          s_cl[b + __popcll(below)] = a[e];
         }
       }
     }
@@ -381,14 +375,12 @@ hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, 
 hipError_t dalgo_km_filter(const int32_t* assign, float* ul, const float* delta,
                            const float* s, int k, int64_t n, int32_t* a_prev, int32_t* idx,
                            unsigned long long* n_active, int64_t cap, int32_t* acl,
-                           const float* nd, int kpad, hipStream_t st) {
+                           hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  if (nd && !acl) return hipErrorInvalidValue;
   int64_t g = (n + dalgo::kDiffThreads - 1) / dalgo::kDiffThreads;
   if (g > 2048) g = 2048;
   hipLaunchKernelGGL(dalgo::km_filter_kernel, dim3((unsigned)g), dim3(dalgo::kDiffThreads), 0, st,
-                     assign, reinterpret_cast<float2*>(ul), delta, s, k, n, a_prev, idx, n_active, cap, acl,
-                     nd, kpad);
+                     assign, reinterpret_cast<float2*>(ul), delta, s, k, n, a_prev, idx, n_active, cap, acl);
   return hipGetLastError();
 }
 

@@ -134,7 +134,7 @@ hipError_t dalgo_km_diff(const int32_t* a_new, const int32_t* a_old, int64_t n, 
 hipError_t dalgo_km_filter(const int32_t* assign, float* ul, const float* delta,
                            const float* s, int k, int64_t n, int32_t* a_prev, int32_t* idx,
                            unsigned long long* n_active, int64_t cap, int32_t* acl,
-                           const float* nd, int kpad, hipStream_t st);
+                           hipStream_t st);
 hipError_t dalgo_km_centre_bounds(const void* cnow, const void* cprev, int is_bf16, int k, int d,
                                   int DP, float* delta, float* s, hipStream_t st);
 hipError_t dalgo_km_qsum(const int32_t* assign, const float* xh, int64_t n, int k, double* Q,
@@ -221,11 +221,9 @@ hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, cons
                          int64_t base_all, uint64_t* keys, hipStream_t st);
 hipError_t dalgo_gb_sort(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
                          int end_bit, hipStream_t st);
-hipError_t dalgo_gb_unique(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out,
-                           unsigned long long* count, int64_t n, hipStream_t st);
-int64_t dalgo_gb_decode_blocks(int64_t E);
-hipError_t dalgo_gb_decode(const uint64_t* K, int64_t E, int shift, int dbits, const int64_t* blk_base,
-                           int phase, int32_t* ent_counts, uint32_t* outdeg, const int64_t* ent_offsets,
+int64_t dalgo_gb_decode_blocks(int64_t n);
+hipError_t dalgo_gb_decode(const uint64_t* K, int64_t n, int shift, int dbits, const int64_t* blk_base,
+                           int phase, int64_t* counts, uint32_t* outdeg, const int64_t* offsets,
                            uint16_t* srcl, int64_t* ent_end, int32_t* ent_blk, int32_t* ent_dst,
                            hipStream_t st);
 hipError_t dalgo_gb_entry_flags(const int32_t* ent_blk, const int32_t* ent_dst, const int64_t* ent_end,

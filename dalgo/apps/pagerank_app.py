@@ -92,9 +92,25 @@ def degree_order_from(edges: list, scale: int, rank: int, world: int, device) ->
         if i % world == rank:
             G.degree_count_(deg, s)
     comm.all_reduce_sum(deg)
-    order = torch.argsort(-deg.to(torch.int64) * n_vertices
-                          - torch.arange(n_vertices, device=device, dtype=torch.int64))
-    return deal_ids(order, n_vertices, world).to(torch.int32)
+    return deal_ids(rank_by_degree(deg), n_vertices, world).to(torch.int32)
+
+
+def rank_by_degree(deg: torch.Tensor) -> torch.Tensor:
+    """Vertex ids by descending degree, ties by descending id (argsort of -deg * n - id).
+    GPU: one rocPRIM radix sort of ((max - deg) << b | (n - 1 - id)) keys over their
+    significant bits (graph_build.hip gb_sort)."""
+    n = deg.numel()
+    ids = torch.arange(n, device=deg.device, dtype=torch.int64)
+    if deg.is_cuda:
+        from dalgo.ops import _ext
+        dmax = int(deg.max().item()) if n else 0
+        dbits = max(1, dmax.bit_length())
+        ibits = max(1, (n - 1).bit_length())
+        keys = ((dmax - deg.to(torch.int64)) << ibits) | (n - 1 - ids)
+        out = torch.empty_like(keys)
+        _ext.ops().gb_sort(keys, n, dbits + ibits, out)
+        return (n - 1) - (out & ((1 << ibits) - 1))
+    return torch.argsort(-deg.to(torch.int64) * n - ids)
 
 
 def build_rmat_shard(edges: list, scale: int, rank: int, world: int, device, reorder: bool = True,

@@ -250,7 +250,7 @@ class KMeans:
             with self._ph("filter"):
                 K.filter_rows(self.assign, self._ul, self._delta, self._s,
                               self._a_prev if cw is None else None, self._idx, self._n_active,
-                              cw.acl if cw is not None else None, cand=cw)
+                              cw.acl if cw is not None else None)
                 if cw is not None:
                     K.sort_active(self._idx, self._n_active, cw)
             self._n_changed.zero_()

@@ -404,7 +404,8 @@ class NativeGraph:
     outdeg_loc: torch.Tensor            # int32 [sl + n_ghost]: distinct out-edges per local source
     ghosts: torch.Tensor | None         # int64 sorted global ids of the remote sources (W > 1)
     recv_counts: list                   # ghosts per owner rank
-    keys: torch.Tensor | None = None    # distinct keys (kept for to_shard), int64 [n_edges]
+    keys: torch.Tensor | None = None    # sorted keys with duplicates (kept for to_shard)
+    n_keys: int = 0
     key_shift: int = 0
     dbits: int = 0
     blk_base: torch.Tensor | None = None
@@ -422,7 +423,7 @@ class NativeGraph:
         """The (dst, src)-sorted shard with GLOBAL source ids (needs the kept keys)."""
         if self.keys is None:
             raise ValueError("NativeGraph.to_shard needs the keys (build_native(keep_keys=True))")
-        K = self.keys[: self.n_edges]
+        K = torch.unique_consecutive(self.keys[: self.n_keys])
         blk = K >> self.key_shift
         dl = (K >> SRC_BITS) & ((1 << self.dbits) - 1)
         li = self.blk_base[blk] + (K & (SRC_SPAN - 1))
@@ -475,7 +476,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     nid = new_id.to(torch.int32).contiguous() if new_id is not None else None
     # ---- phase 0: kept edges per key block (+ remote-source marks, W > 1)
     bitmap = torch.zeros((N + 31) // 32 + 1, **i32) if W > 1 else None
-    nbs = [(int(s.numel()) + 8191) // 8192 for s, _ in edges]
+    nbs = [(int(s.numel()) + 16383) // 16384 for s, _ in edges]     # graph_build.hip kKeyR
     if W > 1:
         counts = torch.empty(sum(nbs), **i32)
         o = 0
@@ -538,33 +539,35 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
         o += nb
         base_all += int(s.numel())
     del bitmap, word_prefix, offsets
-    work = torch.empty_like(keys)
-    E = int(ops.gb_sort_unique(keys, total, nbits, work)) if total else 0
-    del work
+    K = torch.empty_like(keys)
+    if total:
+        ops.gb_sort(keys, total, nbits, K)
+    del keys
     n_src_loc = (sl + n_ghost) if W > 1 else max(N, 1)
     outdeg_loc = torch.zeros(n_src_loc, **i32)
-    if E == 0:
+    if total == 0:
         shard = GraphShard(torch.full((4,), -1, **i32), torch.full((4,), -1, **i32), 0, v_lo, v_hi, N, sl)
         lay = build_blocked(shard, bin_width, 1 << 40, tile, items, min_piece)
         return NativeGraph(lay, 0, v_lo, v_hi, N, sl, outdeg_loc, ghosts, recv_counts,
-                           keys if keep_keys else None, shift, dbits, blk_base, new_id)
-    # ---- decode: per-edge source offsets + entry-end bits, entries, distinct out-degrees
-    nbd = (E + 65535) // 65536
-    ent_counts = torch.empty(nbd, **i32)
-    ops.gb_decode(keys, E, shift, dbits, blk_base, 0, ent_counts, outdeg_loc, None, None, None, None, None)
-    ec = ent_counts.to(torch.int64)
-    ent_offsets = torch.cumsum(ec, 0) - ec
-    nent = int(ec.sum().item())
+                           K if keep_keys else None, 0, shift, dbits, blk_base, new_id)
+    # ---- decode (dedup folded in): per distinct edge the source offset + entry-end bit,
+    # the entries, the distinct out-degrees
+    nbd = (total + 65535) // 65536                     # graph_build.hip kDecR
+    counts = torch.empty(2 * nbd, **i64)
+    ops.gb_decode(K, total, shift, dbits, blk_base, 0, counts, outdeg_loc, None, None, None, None, None)
+    offsets = torch.cumsum(counts.view(nbd, 2), 0) - counts.view(nbd, 2)
+    E, nent = (int(x) for x in counts.view(nbd, 2).sum(0).tolist())
     E16 = (E + 15) // 16 * 16
     srcl = torch.zeros(E16, dtype=torch.int16, device=dev)
     ent_end = torch.empty(nent, **i64)
     ent_blk = torch.empty(nent, **i32)
     ent_dst = torch.empty(nent, **i32)
-    ops.gb_decode(keys, E, shift, dbits, blk_base, 1, None, None, ent_offsets, srcl, ent_end, ent_blk, ent_dst)
-    del ent_counts, ec, ent_offsets
+    ops.gb_decode(K, total, shift, dbits, blk_base, 1, None, None, offsets.contiguous().view(-1), srcl,
+                  ent_end, ent_blk, ent_dst)
+    del counts, offsets
     if not keep_keys:
-        del keys
-        keys = None
+        del K
+        K = None
     # ---- entries: run / chunk starts, run-start bits
     bshift = bin_width.bit_length() - 1
     nbins = max(1, (nl + bin_width - 1) // bin_width)
@@ -657,7 +660,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
                         0, max_runs, torch.zeros(1, dtype=torch.float64, device=dev),
                         int((slo[wu_chunk] < sl).sum().item()) if W > 1 else 0,
                         tuple(int((slo[wu_chunk] < b).sum().item()) for b in splits))
-    return NativeGraph(lay, E, v_lo, v_hi, N, sl, outdeg_loc, ghosts, recv_counts, keys, shift, dbits,
+    return NativeGraph(lay, E, v_lo, v_hi, N, sl, outdeg_loc, ghosts, recv_counts, K, total, shift, dbits,
                        blk_base, new_id)
 
 

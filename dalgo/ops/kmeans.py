@@ -226,19 +226,13 @@ def centre_bounds(Cq_now: torch.Tensor, Cq_prev: torch.Tensor, k: int, d: int,
 
 
 def filter_rows(assign: torch.Tensor, ul: torch.Tensor, delta: torch.Tensor, s: torch.Tensor, a_prev: torch.Tensor | None, idx: torch.Tensor,
-                n_active: torch.Tensor, acl: torch.Tensor | None = None,
-                cand: "CandWorkspace | None" = None) -> None:
+                n_active: torch.Tensor, acl: torch.Tensor | None = None) -> None:
     """Rows that may change cluster -> idx[:m] (their cluster -> a_prev[row] when given,
     and -> acl[:m] in list order when given), m -> n_active (device; no sync). The
     largest centre shift is reduced from delta in the kernel. ``ul`` [n, 2]: the Hamerly
-    bounds (u, l) per row (updated in place for the rows that are skipped). ``cand``: acl
-    holds the candidate tiles' sort key 2 a + far (far rows may need more than the first
-    128-centre chunk of a's neighbour list; see CandWorkspace)."""
+    bounds (u, l) per row (updated in place for the rows that are skipped)."""
     n_active.zero_()
-    if cand is not None:
-        _ext.ops().kmeans_filter(assign, ul, delta, s, a_prev, idx, n_active, acl, cand.nd, cand.kpad)
-    else:
-        _ext.ops().kmeans_filter(assign, ul, delta, s, a_prev, idx, n_active, acl)
+    _ext.ops().kmeans_filter(assign, ul, delta, s, a_prev, idx, n_active, acl)
 
 
 # ------------------------------------------------- candidate-pruned K2 (filtered iterations)
@@ -248,8 +242,7 @@ CAND_TILE = 256          # rows per K2 block tile (4 waves x 2 point tiles x 32)
 class CandWorkspace:
     """Buffers of the candidate-pruned filtered iteration for n rows, k clusters (kpad
     padded, <= 1024): per-centre neighbour lists (nd / nb / hnb, k * kpad each), the
-    active rows sorted by key = 2 cluster + far (a cluster's near rows and far rows form
-    separate tiles: a near tile streams one chunk) and the tile table."""
+    cluster-sorted active rows and the tile table."""
 
     def __init__(self, device, n: int, k: int, kpad: int, DP: int):
         i32 = dict(dtype=torch.int32, device=device)
@@ -263,12 +256,12 @@ class CandWorkspace:
         self.acl = torch.empty(n, **i32)
         self.rows = torch.empty(n, **i32)
         bmax = max(1, (n + CHUNK_ROWS - 1) // CHUNK_ROWS)
-        self.nkeys = 2 * self.k                          # sort keys: 2 cluster + far
+        self.nkeys = self.k                              # sort keys: the clusters
         self.block_counts = torch.empty(bmax * self.nkeys, **i32)
         self.cstart = torch.empty(self.nkeys + 1, **i64)
         self.seg_start = torch.empty(self.nkeys + 1, **i64)
         tiles = (n + CAND_TILE - 1) // CAND_TILE + self.nkeys
-        self.tiles = torch.empty(tiles * 4, **i32)      # (key, first, end, -) per tile
+        self.tiles = torch.empty(tiles * 4, **i32)      # (cluster, first, end, -) per tile
         self.n_tiles = torch.zeros(1, **i64)
 
     def cand(self):

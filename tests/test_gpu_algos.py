@@ -730,39 +730,6 @@ def test_kmeans_filter_matches_torch(cuda):
     assert torch.equal(a_prev[act], assign[act])
 
 
-def test_kmeans_filter_near_far_keys(cuda):
-    """With the candidate workspace, the filter's list keys are 2 a + far, far = the row's
-    bound u + delta[a] reaches half the distance to a's 129th-nearest centre."""
-    torch.manual_seed(7)
-    n, k, d = 50_003, 300, 32
-    cen = K.make_centers(torch.randn(k, d) * 3, torch.bfloat16, cuda)
-    kpad, DP = cen.Cq.shape
-    ws = K.CandWorkspace(cuda, n, k, kpad, DP)
-    delta = torch.empty(k, device=cuda)
-    s = torch.empty(k, device=cuda)
-    K.centre_nbrs(cen, cen.Cq[:k].clone(), delta, s, ws)
-    delta = torch.rand(k, device=cuda)
-    s = torch.rand(k, device=cuda) * 2
-    assign = torch.randint(0, k, (n,), dtype=torch.int32, device=cuda)
-    ul = torch.stack([torch.rand(n, device=cuda) * 30, torch.rand(n, device=cuda)], 1)
-    u0 = ul[:, 0].clone()
-    idx = torch.empty(n, dtype=torch.int32, device=cuda)
-    cnt = torch.zeros(1, dtype=torch.int64, device=cuda)
-    K.filter_rows(assign, ul, delta, s, None, idx, cnt, ws.acl, cand=ws)
-    m = int(cnt.item())
-    rows = idx[:m].long()
-    a = assign[rows].long()
-    ub = u0[rows] + delta[a]
-    thr = ws.nd.view(k, kpad)[a, 128]
-    far = (2 * ub >= thr).to(torch.int32)
-    got = ws.acl[:m]
-    assert torch.equal(got >> 1, a.to(torch.int32))
-    # the kernel rounds ub up by one ulp: allow the exact-threshold rows either way
-    edge = (2 * ub - thr).abs() < 1e-4 * thr.abs().clamp_min(1)
-    assert bool(((got & 1) == far)[~edge].all())
-    assert 0 < int(far.sum()) < m
-
-
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("k,d", [(1, 8), (7, 30), (1024, 128)])
 def test_kmeans_centre_bounds_kernel(cuda, dtype, k, d):
@@ -1029,8 +996,7 @@ def test_kmeans_assign_rows_candidates(cuda, d):
     dprev = (X[:, :d].float() - cen.Cq[a_prev.long(), :d].float()).norm(dim=1)
     ul = torch.stack([dprev * 1.001 + 1e-3, torch.full((n,), -1.0, device=cuda)], 1)
     u, l = ul[:, 0], ul[:, 1]
-    # tile keys 2 a + far: half the rows as far (the kernel takes the cluster from key >> 1)
-    ws.acl[:m].copy_(2 * a_prev[rows.long()] + (torch.arange(m, device=cuda) % 2).to(torch.int32))
+    ws.acl[:m].copy_(a_prev[rows.long()])
     cnt = torch.tensor([m], dtype=torch.int64, device=cuda)
     K.sort_active(rows, cnt, ws)
     sel = torch.zeros(n, dtype=torch.bool, device=cuda)

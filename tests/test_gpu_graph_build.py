@@ -125,3 +125,12 @@ def test_native_pagerank_equals_torch_build(cuda, sem):
     assert a.N == b.N
     assert torch.equal(a.r >= 0, b.r >= 0)
     assert torch.allclose(a.r, b.r, rtol=2e-5, atol=1e-12)
+
+
+def test_rank_by_degree_matches_argsort(cuda):
+    from dalgo.apps.pagerank_app import rank_by_degree
+    g = torch.Generator().manual_seed(4)
+    deg = torch.randint(0, 50, (100_003,), generator=g, dtype=torch.int32)
+    ref = rank_by_degree(deg)
+    got = rank_by_degree(deg.to(cuda)).cpu()
+    assert torch.equal(got, ref)
