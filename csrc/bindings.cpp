@@ -858,6 +858,32 @@ void gb_keys(const Tensor& src, const Tensor& dst, const std::optional<Tensor>& 
                   "gb_keys");
 }
 
+// deg[v] = occurrences of v in ids (int32, ids < 2^end_bit): one rocPRIM radix sort of the
+// ids over end_bit bits + one pass over the run boundaries (no per-id atomics)
+void gb_degree_sorted(const Tensor& ids, int64_t end_bit, Tensor deg) {
+  check_i32(ids, "ids");
+  check_i32(deg, "deg");
+  const int64_t n = ids.numel();
+  TORCH_CHECK(end_bit >= 1 && end_bit <= 31 && deg.numel() >= ((int64_t)1 << end_bit),
+              "gb_degree_sorted: deg must cover 2^end_bit ids");
+  if (n == 0) return;
+  DeviceGuard guard(ids.device());
+  Tensor sorted = at::empty_like(ids);
+  auto* in = reinterpret_cast<const uint32_t*>(ids.data_ptr<int32_t>());
+  auto* out = reinterpret_cast<uint32_t*>(sorted.data_ptr<int32_t>());
+  size_t bytes = 0;
+  DALGO_CHECK_HIP(dalgo_gb_sort32(nullptr, &bytes, in, out, n, (int)end_bit, cur_stream()), "gb_sort32(size)");
+  {
+    Tensor tmp = at::empty({(int64_t)bytes + 256}, ids.options().dtype(at::kByte));
+    DALGO_CHECK_HIP(dalgo_gb_sort32(tmp.data_ptr(), &bytes, in, out, n, (int)end_bit, cur_stream()), "gb_sort32");
+  }
+  Tensor start = at::zeros_like(deg);
+  Tensor end = at::zeros_like(deg);
+  DALGO_CHECK_HIP(dalgo_gb_runs(out, n, start.data_ptr<int32_t>(), end.data_ptr<int32_t>(), cur_stream()),
+                  "gb_runs");
+  deg.add_(end.sub_(start));
+}
+
 // sort keys[:n] over bits [0, end_bit) into out[:n] (rocPRIM onesweep radix sort)
 void gb_sort(const Tensor& keys, int64_t n, int64_t end_bit, Tensor out) {
   check_t(keys, at::kLong, "keys");
@@ -1407,6 +1433,7 @@ TORCH_LIBRARY(dalgo, m) {
         "int dbits, int phase, Tensor(a!)? bitmap, Tensor(b!)? counts, Tensor? offsets, int base_all, "
         "Tensor(c!)? keys, Tensor? word_prefix, Tensor? seg_start, Tensor? seg_blk0) -> ()");
   m.def("gb_sort(Tensor keys, int n, int end_bit, Tensor(a!) out) -> ()");
+  m.def("gb_degree_sorted(Tensor ids, int end_bit, Tensor(a!) deg) -> ()");
   m.def("gb_decode(Tensor K, int n, int shift, int dbits, Tensor blk_base, int phase, "
         "Tensor(a!)? counts, Tensor(b!)? outdeg, Tensor? offsets, Tensor(c!)? srcl, "
         "Tensor(d!)? ent_end, Tensor(e!)? ent_blk, Tensor(f!)? ent_dst) -> ()");
@@ -1472,6 +1499,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("gb_degree", &gb_degree);
   m.impl("gb_keys", &gb_keys);
   m.impl("gb_sort", &gb_sort);
+  m.impl("gb_degree_sorted", &gb_degree_sorted);
   m.impl("gb_decode", &gb_decode);
   m.impl("gb_entry_flags", &gb_entry_flags);
   m.impl("gb_entry_place", &gb_entry_place);

@@ -48,6 +48,23 @@ __global__ void __launch_bounds__(256) gb_degree_kernel(const int32_t* __restric
   }
 }
 
+// degree by sort: over the SORTED ids, every run boundary records where the run of its id
+// starts and where the previous id's run ends (deg = end - start; absent ids stay 0 / 0)
+__global__ void __launch_bounds__(256) gb_runs_kernel(const uint32_t* __restrict__ sorted, int64_t n,
+                                                      int32_t* __restrict__ start, int32_t* __restrict__ end) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i <= n; i += stride) {
+    const uint32_t cur = i < n ? sorted[i] : 0u;
+    const uint32_t prev = i > 0 ? sorted[i - 1] : 0u;
+    if (i == n) {
+      end[prev] = (int32_t)n;
+    } else if (i == 0 || cur != prev) {
+      start[cur] = (int32_t)i;
+      if (i > 0) end[prev] = (int32_t)i;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------- keys
 // Local source index of a global (relabelled) source id and its block:
 //   own slice [v_lo, v_hi): li = s - v_lo, segment 0;
@@ -369,6 +386,21 @@ hipError_t dalgo_gb_degree(const int32_t* ids, int64_t n, uint32_t* deg, hipStre
   if (n <= 0) return hipSuccess;
   const int64_t g = std::min<int64_t>(cdiv(n, 256 * 4), 256 * 64);
   hipLaunchKernelGGL(gb_degree_kernel, dim3((unsigned)g), dim3(256), 0, st, ids, n, deg);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t dalgo_gb_sort32(void* tmp, size_t* tmp_bytes, const uint32_t* in, uint32_t* out, int64_t n,
+                           int end_bit, hipStream_t st) {
+  if (n < 0 || n >= (int64_t)0x7fffffffLL || end_bit < 1 || end_bit > 32) return hipErrorInvalidValue;
+  return rocprim::radix_sort_keys(tmp, *tmp_bytes, in, out, (size_t)n, 0u, (unsigned)end_bit, st);
+}
+
+hipError_t dalgo_gb_runs(const uint32_t* sorted, int64_t n, int32_t* start, int32_t* end, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (n >= (int64_t)0x7fffffffLL) return hipErrorInvalidValue;
+  const int64_t g = std::min<int64_t>(cdiv(n + 1, 256), 256 * 64);
+  hipLaunchKernelGGL(gb_runs_kernel, dim3((unsigned)g), dim3(256), 0, st, sorted, n, start, end);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -188,10 +188,14 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
     pb_v4i wq[D];
 #pragma unroll
     for (int q = 0; q < D; ++q) wq[q] = load(e_first + (int64_t)q * 64 * EPL + EPL * lane);
-    // vector memory ops per step: EPL stores, then the ring refill. Slot q's data was
-    // loaded D steps back; younger than it: (D - 1) (EPL + 1) ops in steady state, and in
-    // the first D steps at least the D - 1 other initial loads
-    static_assert((D - 1) * (EPL + 1) <= 63, "vmcnt field");
+    // vector memory ops per step: SF stores (more in a step with > SF * 64 entries), then
+    // the ring refill. Slot q's data was loaded D steps back; younger than it: at least
+    // (D - 1) (SF + 1) ops in steady state, and in the first D steps at least the D - 1
+    // other initial loads. vmcnt(N) waits for all but the N youngest ops, so waiting with
+    // N <= the true count of younger ops is safe (a step that stored more only makes it
+    // wait a little longer)
+    constexpr int SF = 4;                     // store instructions every step issues
+    static_assert((D - 1) * (SF + 1) <= 63, "vmcnt field");
     bool first = true;
     for (int64_t e00 = e_first; e00 < e_hi; e00 += (int64_t)D * 64 * EPL) {
 #pragma unroll
@@ -200,7 +204,7 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
       if (e0 >= e_hi) break;
       const int64_t idx = e0 + EPL * lane;
       if (first) pb_wait_vm<D - 1>();
-      else pb_wait_vm<(D - 1) * (EPL + 1)>();
+      else pb_wait_vm<(D - 1) * (SF + 1)>();
       // the slot is routed through an (ordered) asm after the wait: no read of it can be
       // scheduled before the wait
       asm volatile("" : "+v"(wq[q]));
@@ -290,23 +294,34 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // EPL unconditional stores per lane (lanes past n_step write this wave's own dummy
-        // line group, so no single address is hammered by every wave): a fixed store count
-        // keeps the compiler's vmcnt bookkeeping exact, so the D prefetched loads are not
-        // drained at every step
-        // staged values read unconditionally (every slot is in range), all before the first
-        // store: one LDS round trip per step instead of one per store
-        int32_t pq[EPL];
-        float vq[EPL];
+        // SF unconditional stores per lane (lanes past n_step write this wave's own dummy
+        // line group, so no single address is hammered by every wave): a minimum store
+        // count keeps the hand-counted vmcnt waits valid, so the D prefetched loads are not
+        // drained at every step. A step with more than SF * 64 entries (0.42 entries per
+        // edge on average: ~215 of 512) adds the missing stores in a wave-uniform branch.
+        // Staged values read before the first store: one LDS round trip per step
+        int32_t pq[SF];
+        float vq[SF];
 #pragma unroll
-        for (int q = 0; q < EPL; ++q) {
+        for (int q = 0; q < SF; ++q) {
           pq[q] = sp[lane + 64 * q];
           vq[q] = sv[lane + 64 * q];
         }
 #pragma unroll
-        for (int q = 0; q < EPL; ++q) {
+        for (int q = 0; q < SF; ++q) {
           const bool ok = lane + 64 * q < n_step;
           pb_st4(val, ok ? (uint32_t)pq[q] * 4u : dummy4, ok ? vq[q] : 0.f);
+        }
+        if (n_step > SF * 64) {
+#pragma unroll
+          for (int q = SF; q < EPL; ++q) {
+            if (64 * q < n_step) {
+              const bool ok = lane + 64 * q < n_step;
+              const int32_t p2 = sp[lane + 64 * q];
+              const float v2 = sv[lane + 64 * q];
+              pb_st4(val, ok ? (uint32_t)p2 * 4u : dummy4, ok ? v2 : 0.f);
+            }
+          }
         }
       };
       if (full) step(std::true_type{}); else step(std::false_type{});

@@ -215,6 +215,9 @@ struct DalgoGbKeyArgs {
 };
 extern "C" {
 hipError_t dalgo_gb_degree(const int32_t* ids, int64_t n, uint32_t* deg, hipStream_t st);
+hipError_t dalgo_gb_sort32(void* tmp, size_t* tmp_bytes, const uint32_t* in, uint32_t* out, int64_t n,
+                           int end_bit, hipStream_t st);
+hipError_t dalgo_gb_runs(const uint32_t* sorted, int64_t n, int32_t* start, int32_t* end, hipStream_t st);
 int64_t dalgo_gb_key_blocks(int64_t n);
 hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, const DalgoGbKeyArgs* a,
                          int phase, uint32_t* bitmap, int32_t* counts, const int64_t* offsets,

@@ -88,8 +88,14 @@ def degree_order_from(edges: list, scale: int, rank: int, world: int, device) ->
     from dalgo.parallel import comm
     n_vertices = 1 << scale
     deg = torch.zeros(n_vertices, dtype=torch.int32, device=device)
-    for i, (s, _) in enumerate(edges):
-        if i % world == rank:
+    mine = [s for i, (s, _) in enumerate(edges) if i % world == rank]
+    if mine and deg.is_cuda:
+        # one radix sort of this rank's sources + run lengths (graph_build.hip)
+        ids = torch.cat(mine) if len(mine) > 1 else mine[0]
+        G.degree_sorted_(deg, ids, scale)
+        del ids
+    else:
+        for s in mine:
             G.degree_count_(deg, s)
     comm.all_reduce_sum(deg)
     return deal_ids(rank_by_degree(deg), n_vertices, world).to(torch.int32)

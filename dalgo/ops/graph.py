@@ -135,6 +135,13 @@ def degree_count_(deg: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
     return deg
 
 
+def degree_sorted_(deg: torch.Tensor, ids: torch.Tensor, bits: int) -> torch.Tensor:
+    """deg[v] += #occurrences of v in ids (GPU int32, ids < 2^bits): a radix sort of the
+    ids and their run lengths instead of one atomic per id (graph_build.hip)."""
+    _ext.ops().gb_degree_sorted(ids.contiguous(), int(bits), deg)
+    return deg
+
+
 def local_outdeg(shard: GraphShard) -> torch.Tensor:
     """Out-degree contribution of this shard's edges (sum over ranks = global out-degree)."""
     s = shard.src[: shard.n_edges].to(torch.int64)

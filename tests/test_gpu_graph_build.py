@@ -134,3 +134,11 @@ def test_rank_by_degree_matches_argsort(cuda):
     ref = rank_by_degree(deg)
     got = rank_by_degree(deg.to(cuda)).cpu()
     assert torch.equal(got, ref)
+
+
+def test_degree_sorted_matches_bincount(cuda):
+    s, _ = G.rmat_edges(3 << 20, 18, seed=7, device=cuda)
+    deg = torch.full((1 << 18,), 5, dtype=torch.int32, device=cuda)
+    G.degree_sorted_(deg, s, 18)
+    ref = torch.bincount(s.long(), minlength=1 << 18) + 5
+    assert torch.equal(deg.long(), ref)
