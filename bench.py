@@ -21,6 +21,13 @@ the small-all-reduce path the start-up race chose with both timings, the
 per-step all-reduce time measured in isolation after the timed region, and the
 held-out accuracy of the trained model (a correctness witness: a fast but wrong
 gradient kernel cannot post a number).
+
+After the headline (untimed by it, on one GPU by default: ``--secondary``), the same JSON
+line carries BASELINE configs #3-#5 under ``secondary``: BMUF and EASGD on the headline's
+data (exact sampled-row counts, held-out witnesses), the k-means reference job at 100M x
+128, k = 1024 (also on overlapping clusters) and the PageRank reference job at R-MAT scale
+26 (adjacency build + 10 iterations), each with its witness (dalgo/apps/jobs.py). A
+failed secondary witness makes the exit code non-zero.
 """
 from __future__ import annotations
 

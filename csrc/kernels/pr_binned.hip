@@ -83,18 +83,16 @@ __device__ __forceinline__ int dpp_mov_i(int old, int v) {
   return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWS, 0xf, false);
 }
 
-// one step of the inclusive segmented scan of (a: open-segment sum, h: segment closed)
-// plus two plain int scans (entry count, run-start count)
+// one step of the inclusive segmented scan of a (open-segment sum) together with the
+// packed int scan c = entries | run starts << 16 (each <= 512 per step: no carry between
+// the fields). "A segment closed inside the window" is exactly "the window's entry count
+// is non-zero", so the segment flag needs no scan of its own
 template <int CTRL, int ROWS = 0xf>
-__device__ __forceinline__ void scan_step(float& a, int& h, int& c0, int& c1) {
+__device__ __forceinline__ void scan_step(float& a, int& c) {
   const float a_up = dpp_mov_f<CTRL, ROWS>(-0.0f, a);
-  const int h_up = dpp_mov_i<CTRL, ROWS>(0, h);
-  const int c0_up = dpp_mov_i<CTRL, ROWS>(0, c0);
-  const int c1_up = dpp_mov_i<CTRL, ROWS>(0, c1);
-  if (!h) a = a_up + a;
-  h |= h_up;
-  c0 += c0_up;
-  c1 += c1_up;
+  const int c_up = dpp_mov_i<CTRL, ROWS>(0, c);
+  if ((c & 0xffff) == 0) a = a_up + a;
+  c += c_up;
 }
 
 }  // namespace
@@ -248,17 +246,18 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
         }
         // inclusive scans over the 64 lanes (DPP: rows of 16, then row broadcasts)
         float a = part;
-        int hh = nf > 0, cnt = nf, cm = nm;
-        scan_step<0x111>(a, hh, cnt, cm);          // row_shr:1
-        scan_step<0x112>(a, hh, cnt, cm);          // row_shr:2
-        scan_step<0x114>(a, hh, cnt, cm);          // row_shr:4
-        scan_step<0x118>(a, hh, cnt, cm);          // row_shr:8
-        scan_step<0x142, 0xa>(a, hh, cnt, cm);     // row_bcast:15 -> rows 1, 3
-        scan_step<0x143, 0xc>(a, hh, cnt, cm);     // row_bcast:31 -> rows 2, 3
+        int cc = nf | (nm << 16);
+        scan_step<0x111>(a, cc);                   // row_shr:1
+        scan_step<0x112>(a, cc);                   // row_shr:2
+        scan_step<0x114>(a, cc);                   // row_shr:4
+        scan_step<0x118>(a, cc);                   // row_shr:8
+        scan_step<0x142, 0xa>(a, cc);              // row_bcast:15 -> rows 1, 3
+        scan_step<0x143, 0xc>(a, cc);              // row_bcast:31 -> rows 2, 3
+        const int cnt = cc & 0xffff, cm = cc >> 16;
         // exclusive segment sum for this lane (wave_shr:1), joined with the step carry
         const float a_ex = dpp_mov_f<0x138>(-0.0f, a);
-        const int h_ex = dpp_mov_i<0x138>(0, hh);
-        const float carry_in = h_ex ? a_ex : carry + a_ex;
+        const int c_ex = dpp_mov_i<0x138>(0, cc);
+        const float carry_in = (c_ex & 0xffff) ? a_ex : carry + a_ex;
         const int rbase = run + cm - nm - 1;       // run of this lane's first entries
         // run deltas of the lane's entries: its 8 edges touch at most nm + 1 runs and nearly
         // always <= 2 (a run is one (chunk, 16K-destination bin) group: hundreds of edges),
@@ -286,11 +285,11 @@ pb_gather_kernel(const uint16_t* __restrict__ srcl, const int64_t* __restrict__ 
           }
         }
         const float a63 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a), 63));
-        const int h63 = __builtin_amdgcn_readlane(hh, 63);
-        const int n_step = __builtin_amdgcn_readlane(cnt, 63);
-        carry = h63 ? a63 : carry + a63;
+        const int c63 = __builtin_amdgcn_readlane(cc, 63);
+        const int n_step = c63 & 0xffff;
+        carry = n_step ? a63 : carry + a63;
         ent += n_step;
-        run += __builtin_amdgcn_readlane(cm, 63);
+        run += c63 >> 16;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -205,6 +205,8 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
     # the K4b layout; otherwise the (dst, src)-sorted shard
     native = (native_build and rt.device.type == "cuda" and spmv == "blocked" and chunk >= 1 << 40)
     if native:
+        from dalgo.ops import graph as G
+        G.build_marks = []
         shard = build_rmat_native(edges, scale, rt.rank, W, rt.device, reorder=reorder,
                                   keep_keys=witness, bin_width=bin_width, tile=tile)
     else:
@@ -220,6 +222,11 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
     rt.synchronize()
     job_ms = _max_over_ranks(time.perf_counter() - t, rt.device) * 1e3
     shard_ms, model_ms, iters_ms = ev.spans()
+    build_phases = None
+    if native:
+        from dalgo.ops import graph as G
+        build_phases = G.build_phase_spans()
+        G.build_marks = None
     del edges
     E = comm.all_reduce_count(shard.n_edges, device=rt.device)
     # per-iteration rate alone (after the job), with the phase split of one step
@@ -268,6 +275,7 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
         "value": E * iters / (job_ms / 1e3), "unit": "edges/s", "n_gpus": W,
         "job_ms": job_ms, "build_ms_rank0": shard_ms + model_ms,
         "shard_build_ms_rank0": shard_ms, "model_build_ms_rank0": model_ms,
+        "build_phases_ms_rank0": build_phases,
         "iterations_ms_rank0": iters_ms,
         "ms_per_iter": it_ms, "edges_per_s_per_iter": E / (it_ms / 1e3),
         "edges_dedup": E, "edges_generated": n_gen, "vertices": 1 << scale,

@@ -98,7 +98,10 @@ def degree_order_from(edges: list, scale: int, rank: int, world: int, device) ->
         for s in mine:
             G.degree_count_(deg, s)
     comm.all_reduce_sum(deg)
-    return deal_ids(rank_by_degree(deg), n_vertices, world).to(torch.int32)
+    G._mark("degree_count")
+    order = rank_by_degree(deg)
+    G._mark("degree_rank")
+    return deal_ids(order, n_vertices, world).to(torch.int32)
 
 
 def rank_by_degree(deg: torch.Tensor) -> torch.Tensor:
@@ -145,7 +148,9 @@ def build_rmat_native(edges: list, scale: int, rank: int, world: int, device, re
     """This rank's K4b-ready adjacency of the given R-MAT edge chunks, built natively
     (dalgo.ops.graph.build_native): degree relabeling, destination filter, dedup and the
     blocked layout without the (dst, src)-sorted intermediate shard."""
+    G._mark("start")
     new_id = degree_order_from(edges, scale, rank, world, device) if reorder else None
+    G._mark("deal_ids")
     return G.build_native(edges, 1 << scale, rank, world, new_id, bin_width=bin_width, tile=tile,
                           keep_keys=keep_keys)
 

@@ -457,6 +457,26 @@ def _popcount32(x: torch.Tensor) -> torch.Tensor:
     return ((x * 0x01010101) & 0xFFFFFFFF) >> 24
 
 
+# phase marks of the native build (HIP events; None = off): build_phase_spans() turns the
+# recorded marks into {phase: ms} after a device sync (bench diagnostics)
+build_marks: list | None = None
+
+
+def _mark(name: str):
+    if build_marks is not None and torch.cuda.is_available():
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        build_marks.append((name, e))
+
+
+def build_phase_spans() -> dict:
+    out = {}
+    if build_marks:
+        for (_, a), (name, b) in zip(build_marks[:-1], build_marks[1:]):
+            out[name] = out.get(name, 0.0) + a.elapsed_time(b)
+    return out
+
+
 def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: torch.Tensor | None = None,
                  bin_width: int = 16384, tile: int = 16384, items: int = 2048,
                  min_piece: int = 1 << 14, keep_keys: bool = False) -> NativeGraph:
@@ -506,6 +526,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     else:
         total = sum(int(s.numel()) for s, _ in edges)
         offsets, word_prefix, ghosts, n_ghost, recv_counts = None, None, None, 0, [0]
+    _mark("count")
     # ---- segments of the local source index space: own [0, nl), then each peer's ghosts
     seg_start = [0] * W
     seg_end = [0] * W
@@ -536,6 +557,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     assert nbits <= 63, "key does not fit 63 bits"
     st = torch.tensor(seg_start, **i64)
     sb = torch.tensor(seg_blk0, **i64)
+    _mark("segments")
     # ---- phase 1: keys
     keys = torch.empty(max(total, 1), **i64)
     o, base_all = 0, 0
@@ -546,10 +568,12 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
         o += nb
         base_all += int(s.numel())
     del bitmap, word_prefix, offsets
+    _mark("keys")
     K = torch.empty_like(keys)
     if total:
         ops.gb_sort(keys, total, nbits, K)
     del keys
+    _mark("sort")
     n_src_loc = (sl + n_ghost) if W > 1 else max(N, 1)
     outdeg_loc = torch.zeros(n_src_loc, **i32)
     if total == 0:
@@ -575,6 +599,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     if not keep_keys:
         del K
         K = None
+    _mark("decode")
     # ---- entries: run / chunk starts, run-start bits
     bshift = bin_width.bit_length() - 1
     nbins = max(1, (nl + bin_width - 1) // bin_width)
@@ -600,6 +625,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     chunk_run = torch.searchsorted(run_chunk, torch.arange(nch + 1, **i64))
     bin_cnt = torch.zeros(nbins, **i64).index_add_(0, run_bin, run_len)
     bin_lo = torch.cumsum(bin_cnt, 0) - bin_cnt
+    _mark("entries_runs")
     # ---- tiles / work units: a chunk is cut every wu_e edges into work units and every
     # tlen edges inside a unit into tiles, both on entry boundaries
     ce_lo = torch.where(chunk_first > 0, ent_end[(chunk_first - 1).clamp_min(0)] + 1,
@@ -632,6 +658,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     n_src = int((slo + ns).max().item())
     assert int(tile_e[-1]) <= srcl.numel() and int(ns.min().item()) >= 1
     max_runs = int((chunk_run[1:] - chunk_run[:-1]).max().item())
+    _mark("tiles")
     # ---- phase-2 work items (as build_blocked)
     cap = max(int(nent // max(items, 1)), min_piece)
     cnt_h = bin_cnt.cpu().tolist()
@@ -667,6 +694,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
                         0, max_runs, torch.zeros(1, dtype=torch.float64, device=dev),
                         int((slo[wu_chunk] < sl).sum().item()) if W > 1 else 0,
                         tuple(int((slo[wu_chunk] < b).sum().item()) for b in splits))
+    _mark("work_items")
     return NativeGraph(lay, E, v_lo, v_hi, N, sl, outdeg_loc, ghosts, recv_counts, K, total, shift, dbits,
                        blk_base, new_id)
 
