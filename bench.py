@@ -390,8 +390,6 @@ def run_secondary(a, rt, data, layout) -> dict:
             r = {"error": repr(e)}
         r["wall_s"] = time.perf_counter() - ts
         res[name] = r
-        if rt.device.type == "cuda":
-            torch.cuda.empty_cache()
 
     for algo in ("bmuf", "easgd"):
         attempt(algo, lambda algo=algo: dict(

@@ -54,6 +54,10 @@ def deal_ids(order: torch.Tensor, n_vertices: int, world: int) -> torch.Tensor:
     G.vertex_slices (the last ones may be shorter); ranks past a full slice take the
     free positions in order. A bijection of [0, n_vertices)."""
     dev = order.device
+    if world == 1:                       # rank j -> position j
+        new_id = torch.empty(n_vertices, dtype=torch.int64, device=dev)
+        new_id[order] = torch.arange(n_vertices, device=dev, dtype=torch.int64)
+        return new_id
     sl = G.vertex_slices(n_vertices, world)
     j = torch.arange(n_vertices, device=dev, dtype=torch.int64)
     p = j // world
