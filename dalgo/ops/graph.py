@@ -463,7 +463,15 @@ build_marks: list | None = None
 
 
 def _mark(name: str):
+    """A phase boundary: a HIP event, or (DALGO_BUILD_SYNC=1, diagnostics) a device sync
+    and the host clock, so host-side costs land in the phase that causes them."""
     if build_marks is not None and torch.cuda.is_available():
+        import os
+        if os.environ.get("DALGO_BUILD_SYNC") == "1":
+            import time
+            torch.cuda.synchronize()
+            build_marks.append((name, time.perf_counter()))
+            return
         e = torch.cuda.Event(enable_timing=True)
         e.record()
         build_marks.append((name, e))
@@ -473,7 +481,8 @@ def build_phase_spans() -> dict:
     out = {}
     if build_marks:
         for (_, a), (name, b) in zip(build_marks[:-1], build_marks[1:]):
-            out[name] = out.get(name, 0.0) + a.elapsed_time(b)
+            dt = (b - a) * 1e3 if isinstance(a, float) else a.elapsed_time(b)
+            out[name] = out.get(name, 0.0) + dt
     return out
 
 

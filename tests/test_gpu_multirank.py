@@ -64,6 +64,18 @@ def test_scripts_two_ranks_gloo_on_one_gpu(cuda):
         assert needle in part, (path, part[-2000:])
 
 
+def test_pagerank_native_build_two_ranks(cuda):
+    """The PageRank job at 2 gloo ranks on one GPU: each rank builds its K4b layout natively
+    over the [own slice | ghosts] source space (ghost list from the bitmap pass), runs the
+    ghost exchange, and its ranks match the pull K4 over the same edges (witness)."""
+    out = _torchrun(["bench/pagerank_bench.py", "--gpus", "2", "--backend", "gloo", "--scale", "15",
+                     "--steps", "2", "--pool-gb", "1"])
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["exchange"] == "ghost"
+    assert d["adjacency_build"].startswith("native")
+    assert d["correctness_witness"]["passed"], d["correctness_witness"]
+
+
 SPIN = {"DALGO_ALLOW_SHARED_SPIN": "1"}
 
 
