@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--deadline-s", type=float, default=420.0)
     ap.add_argument("--pool-gb", type=float, default=96.0,
                     help="device memory held by the caching allocator before the clock")
+    ap.add_argument("--no-warm", action="store_true",
+                    help="skip the scale-16 process warm-up before the clock")
     ap.add_argument("--bin-width", type=int, default=16384)
     ap.add_argument("--chunk", type=int, default=1 << 40)
     ap.add_argument("--tile", type=int, default=16384)
@@ -53,7 +55,8 @@ def main():
     check_world(a.gpus, rt.world_size, "pagerank_bench")
     out = pagerank_job(rt, a.scale, a.edge_factor, a.iters, spmv=a.spmv, semantics=a.semantics,
                        witness=not a.no_witness, reorder=not a.no_reorder, bin_width=a.bin_width,
-                       chunk=a.chunk, tile=a.tile, timed_iters=a.steps, pool_gb=a.pool_gb)
+                       chunk=a.chunk, tile=a.tile, timed_iters=a.steps, pool_gb=a.pool_gb,
+                       warm=not a.no_warm)
     if rt.is_main:
         print(json.dumps(out), flush=True)
     runtime.shutdown()

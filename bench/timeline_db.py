@@ -34,7 +34,7 @@ def main():
             continue
         if (e - s) / 1e3 < a.min_us and gap < 50:
             continue
-        short = n.replace("void ", "").split("(")[0][:70]
+        short = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:70]
         print(f"| {i} | {(s - t0) / 1e6:.3f} | {gap:.1f} | {(e - s) / 1e3:.1f} | `{short}` |")
     span = (rows[-1][2] - t0) / 1e6
     print(f"\n{len(rows)} dispatches, span {span:.3f} ms, kernel busy {busy / 1e6:.3f} ms")
