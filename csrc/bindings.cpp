@@ -578,7 +578,8 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
                        const std::optional<Tensor>& tol, const std::optional<Tensor>& ul,
                        const std::optional<Tensor>& changed,
                        const std::optional<Tensor>& n_changed, const std::optional<Tensor>& chg_new,
-                       const std::optional<Tensor>& chg_old, int64_t cand_extend) {
+                       const std::optional<Tensor>& chg_old, int64_t cand_extend,
+                       const std::optional<Tensor>& acl) {
   TORCH_CHECK(Cq.dim() == 2 && Cq.is_contiguous() && Cq.scalar_type() == at::kBFloat16, "Cq bf16");
   const int DP = (int)Cq.size(1);
   TORCH_CHECK(DP == 64 || DP == 128, "kmeans_assign_idx: DP 64 or 128");
@@ -615,8 +616,9 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
   DalgoKmPost post{};
   const DalgoKmPost* pp = nullptr;
   if (m_dev.has_value()) {   // filtered iteration: rows = *m_dev (device), m = its upper bound
-    // a_prev: the previous clusters (the candidate form takes them from its tiles)
-    TORCH_CHECK((a_prev.has_value() || !cand.empty()) && tol.has_value() && ul.has_value() &&
+    // previous clusters: a_prev[row], acl[p] (the filter's list order), the candidate
+    // form's tiles, or (none given, dense form) assign itself
+    TORCH_CHECK(tol.has_value() && ul.has_value() &&
                     changed.has_value() && n_changed.has_value(),
                 "kmeans_assign_idx: the device-count form needs a_prev, tol, ul, changed, n_changed");
     check_dev(*m_dev, "m_dev");
@@ -625,6 +627,11 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
       check_i32(*a_prev, "a_prev");
       TORCH_CHECK(a_prev->numel() >= X.size(0), "a_prev [n]");
       post.a_prev = a_prev->data_ptr<int32_t>();
+    }
+    if (acl.has_value()) {
+      check_i32(*acl, "acl");
+      TORCH_CHECK(ip != nullptr && acl->numel() >= m, "kmeans_assign_idx: acl [m] with idx");
+      post.acl = acl->data_ptr<int32_t>();
     }
     check_i32(*changed, "changed");
     TORCH_CHECK(chg_new.has_value() == chg_old.has_value(), "chg_new and chg_old together");
@@ -868,20 +875,27 @@ void gb_degree_sorted(const Tensor& ids, int64_t end_bit, Tensor deg) {
               "gb_degree_sorted: deg must cover 2^end_bit ids");
   if (n == 0) return;
   DeviceGuard guard(ids.device());
-  Tensor sorted = at::empty_like(ids);
   auto* in = reinterpret_cast<const uint32_t*>(ids.data_ptr<int32_t>());
+  const int kb = dalgo_gb_bucket_bits();
+  if (end_bit <= kb + 2) {   // small id space: one atomic per id
+    DALGO_CHECK_HIP(dalgo_gb_degree(ids.data_ptr<int32_t>(), n,
+                                    reinterpret_cast<uint32_t*>(deg.data_ptr<int32_t>()), cur_stream()),
+                    "gb_degree");
+    return;
+  }
+  // partition on the high bits only, then one LDS histogram per bucket
+  Tensor sorted = at::empty_like(ids);
   auto* out = reinterpret_cast<uint32_t*>(sorted.data_ptr<int32_t>());
   size_t bytes = 0;
-  DALGO_CHECK_HIP(dalgo_gb_sort32(nullptr, &bytes, in, out, n, (int)end_bit, cur_stream()), "gb_sort32(size)");
+  DALGO_CHECK_HIP(dalgo_gb_sort32(nullptr, &bytes, in, out, n, kb, (int)end_bit, cur_stream()), "gb_sort32(size)");
   {
     Tensor tmp = at::empty({(int64_t)bytes + 256}, ids.options().dtype(at::kByte));
-    DALGO_CHECK_HIP(dalgo_gb_sort32(tmp.data_ptr(), &bytes, in, out, n, (int)end_bit, cur_stream()), "gb_sort32");
+    DALGO_CHECK_HIP(dalgo_gb_sort32(tmp.data_ptr(), &bytes, in, out, n, kb, (int)end_bit, cur_stream()), "gb_sort32");
   }
-  Tensor start = at::zeros_like(deg);
-  Tensor end = at::zeros_like(deg);
-  DALGO_CHECK_HIP(dalgo_gb_runs(out, n, start.data_ptr<int32_t>(), end.data_ptr<int32_t>(), cur_stream()),
-                  "gb_runs");
-  deg.add_(end.sub_(start));
+  Tensor starts = at::empty({((int64_t)1 << (end_bit - kb)) + 1}, ids.options().dtype(at::kLong));
+  DALGO_CHECK_HIP(dalgo_gb_bucket_degree(out, n, (int)end_bit, starts.data_ptr<int64_t>(), deg.data_ptr<int32_t>(),
+                                         cur_stream()),
+                  "gb_bucket_degree");
 }
 
 // sort keys[:n] over bits [0, end_bit) into out[:n] (rocPRIM onesweep radix sort)
@@ -976,6 +990,126 @@ void gb_entry_place(const Tensor& ent_dst, const Tensor& ent_end, const Tensor& 
                                        ce_lo.data_ptr<int64_t>(), tlen.data_ptr<int64_t>(), wu_e, (int)bin_mask,
                                        dloc.data_ptr<int16_t>(), ts.data_ptr<uint8_t>(), cur_stream()),
                   "gb_entry_place");
+}
+
+// ---- (block, bin) cell matrix of the K4b runs (graph_build.hip gb_cell_*)
+static void check_cells(const Tensor& C, int64_t nblk, int64_t nbins) {
+  check_i32(C, "C");
+  TORCH_CHECK(nblk >= 1 && nbins >= 1 && nblk * nbins <= ((int64_t)1 << 31) && C.numel() >= nblk * nbins,
+              "gb_cells: C [nblk * nbins]");
+}
+
+void gb_cell_count(const Tensor& ent_blk, const Tensor& ent_dst, int64_t bshift, int64_t nblk, int64_t nbins,
+                   Tensor C) {
+  check_i32(ent_blk, "ent_blk");
+  check_i32(ent_dst, "ent_dst");
+  check_cells(C, nblk, nbins);
+  TORCH_CHECK(ent_blk.numel() == ent_dst.numel(), "gb_cell_count: entry arrays");
+  DeviceGuard guard(C.device());
+  DALGO_CHECK_HIP(dalgo_gb_cells(0, ent_blk.data_ptr<int32_t>(), ent_dst.data_ptr<int32_t>(), ent_blk.numel(),
+                                 (int)bshift, (int)nblk, (int)nbins, C.data_ptr<int32_t>(), nullptr, nullptr, nullptr,
+                                 nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+                                 cur_stream()),
+                  "gb_cell_count");
+}
+
+void gb_cell_rows(const Tensor& C, int64_t nblk, int64_t nbins, Tensor T, Tensor R) {
+  check_cells(C, nblk, nbins);
+  check_t(T, at::kLong, "T");
+  check_t(R, at::kLong, "R");
+  TORCH_CHECK(T.numel() >= nblk && R.numel() >= nblk, "gb_cell_rows: T / R [nblk]");
+  DeviceGuard guard(C.device());
+  DALGO_CHECK_HIP(dalgo_gb_cells(1, nullptr, nullptr, 0, 0, (int)nblk, (int)nbins, C.data_ptr<int32_t>(),
+                                 T.data_ptr<int64_t>(), R.data_ptr<int64_t>(), nullptr, nullptr, nullptr, nullptr, 0,
+                                 nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, cur_stream()),
+                  "gb_cell_rows");
+}
+
+void gb_cell_scan(const Tensor& C, int64_t nblk, int64_t nbins, const Tensor& RE, const Tensor& RR, Tensor CM,
+                  Tensor RID) {
+  check_cells(C, nblk, nbins);
+  check_t(RE, at::kLong, "RE");
+  check_t(RR, at::kLong, "RR");
+  check_i32(CM, "CM");
+  check_i32(RID, "RID");
+  TORCH_CHECK(RE.numel() >= nblk && RR.numel() >= nblk && CM.numel() >= nblk * nbins && RID.numel() >= nblk * nbins,
+              "gb_cell_scan: sizes");
+  DeviceGuard guard(C.device());
+  DALGO_CHECK_HIP(dalgo_gb_cells(2, nullptr, nullptr, 0, 0, (int)nblk, (int)nbins, C.data_ptr<int32_t>(), nullptr,
+                                 nullptr, RE.data_ptr<int64_t>(), RR.data_ptr<int64_t>(), CM.data_ptr<int32_t>(),
+                                 RID.data_ptr<int32_t>(), 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+                                 cur_stream()),
+                  "gb_cell_scan");
+}
+
+void gb_cell_colsum(const Tensor& C, int64_t nblk, int64_t nbins, int64_t G, Tensor P) {
+  check_cells(C, nblk, nbins);
+  check_t(P, at::kLong, "P");
+  TORCH_CHECK(G >= 1 && P.numel() >= ((nblk + G - 1) / G) * nbins, "gb_cell_colsum: P [groups * nbins]");
+  DeviceGuard guard(C.device());
+  DALGO_CHECK_HIP(dalgo_gb_cells(3, nullptr, nullptr, 0, 0, (int)nblk, (int)nbins, C.data_ptr<int32_t>(), nullptr,
+                                 nullptr, nullptr, nullptr, nullptr, nullptr, (int)G, P.data_ptr<int64_t>(), nullptr,
+                                 nullptr, 0, nullptr, nullptr, nullptr, cur_stream()),
+                  "gb_cell_colsum");
+}
+
+void gb_cell_place(const Tensor& C, const Tensor& CM, const Tensor& RID, int64_t nblk, int64_t nbins, int64_t G,
+                   const Tensor& Poff, const Tensor& CI, Tensor run_delta, Tensor run_chunk, Tensor run_first) {
+  check_cells(C, nblk, nbins);
+  check_i32(CM, "CM");
+  check_i32(RID, "RID");
+  check_t(Poff, at::kLong, "Poff");
+  check_i32(CI, "CI");
+  check_i32(run_delta, "run_delta");
+  check_i32(run_chunk, "run_chunk");
+  check_t(run_first, at::kLong, "run_first");
+  const int64_t nruns = run_delta.numel();
+  TORCH_CHECK(G >= 1 && Poff.numel() >= ((nblk + G - 1) / G) * nbins && CI.numel() >= nblk &&
+                  CM.numel() >= nblk * nbins && RID.numel() >= nblk * nbins && run_chunk.numel() == nruns &&
+                  run_first.numel() == nruns,
+              "gb_cell_place: sizes");
+  DeviceGuard guard(C.device());
+  DALGO_CHECK_HIP(dalgo_gb_cells(4, nullptr, nullptr, 0, 0, (int)nblk, (int)nbins, C.data_ptr<int32_t>(), nullptr,
+                                 nullptr, nullptr, nullptr, CM.data_ptr<int32_t>(), RID.data_ptr<int32_t>(), (int)G,
+                                 nullptr, Poff.data_ptr<int64_t>(), CI.data_ptr<int32_t>(), nruns,
+                                 run_delta.data_ptr<int32_t>(), run_chunk.data_ptr<int32_t>(),
+                                 run_first.data_ptr<int64_t>(), cur_stream()),
+                  "gb_cell_place");
+}
+
+void gb_entry_cells(const Tensor& ent_blk, const Tensor& ent_dst, const Tensor& ent_end, int64_t bshift,
+                    int64_t nblk, int64_t nbins, const Tensor& CM, const Tensor& RID, const Tensor& run_delta,
+                    const Tensor& RE, const Tensor& CI, const Tensor& ce_lo, const Tensor& tlen, int64_t wu_e,
+                    int64_t bin_mask, Tensor dloc, Tensor ts, Tensor srcl) {
+  check_i32(ent_blk, "ent_blk");
+  check_i32(ent_dst, "ent_dst");
+  check_t(ent_end, at::kLong, "ent_end");
+  check_i32(CM, "CM");
+  check_i32(RID, "RID");
+  check_i32(run_delta, "run_delta");
+  check_t(RE, at::kLong, "RE");
+  check_i32(CI, "CI");
+  check_t(ce_lo, at::kLong, "ce_lo");
+  check_t(tlen, at::kLong, "tlen");
+  check_t(dloc, at::kShort, "dloc");
+  check_t(ts, at::kByte, "ts");
+  check_t(srcl, at::kShort, "srcl");
+  const int64_t ne = ent_blk.numel();
+  TORCH_CHECK(ent_dst.numel() == ne && ent_end.numel() == ne && ts.numel() >= ne && dloc.numel() >= ne,
+              "gb_entry_cells: entry arrays");
+  TORCH_CHECK(nblk >= 1 && nbins >= 1 && CM.numel() >= nblk * nbins && RID.numel() >= nblk * nbins &&
+                  RE.numel() >= nblk && CI.numel() >= nblk && ce_lo.numel() == tlen.numel(),
+              "gb_entry_cells: tables");
+  DeviceGuard guard(ent_blk.device());
+  DALGO_CHECK_HIP(dalgo_gb_entry_cells(ent_blk.data_ptr<int32_t>(), ent_dst.data_ptr<int32_t>(),
+                                       ent_end.data_ptr<int64_t>(), ne, (int)bshift, (int)nblk, (int)nbins,
+                                       CM.data_ptr<int32_t>(), RID.data_ptr<int32_t>(), run_delta.data_ptr<int32_t>(),
+                                       run_delta.numel(), RE.data_ptr<int64_t>(), CI.data_ptr<int32_t>(),
+                                       ce_lo.data_ptr<int64_t>(), tlen.data_ptr<int64_t>(), ce_lo.numel(), wu_e,
+                                       (int)bin_mask, dloc.data_ptr<int16_t>(), dloc.numel(), ts.data_ptr<uint8_t>(),
+                                       reinterpret_cast<uint16_t*>(srcl.data_ptr<int16_t>()), srcl.numel(),
+                                       cur_stream()),
+                  "gb_entry_cells");
 }
 
 void pr_spmv(const Tensor& src, const Tensor& dstl, const Tensor& c, Tensor acc, Tensor pres,
@@ -1421,7 +1555,7 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(b!)? mind=None, Tensor(c!)? mind2=None, Tensor(d!)? xh=None, Tensor(e!)? xmax=None, "
         "Tensor? m_dev=None, Tensor? a_prev=None, Tensor? tol=None, Tensor(f!)? ul=None, "
         "Tensor(h!)? changed=None, Tensor(i!)? n_changed=None, "
-        "Tensor(j!)? chg_new=None, Tensor(l!)? chg_old=None, int cand_extend=1) -> ()");
+        "Tensor(j!)? chg_new=None, Tensor(l!)? chg_old=None, int cand_extend=1, Tensor? acl=None) -> ()");
   m.def("kmeans_bounds_init(Tensor mind, Tensor mind2, Tensor xmax, int n, Tensor(a!) ul, "
         "Tensor(c!) tol) -> ()");
   m.def("kmeans_update(Tensor(a!) C, Tensor S, Tensor cnt, Tensor(b!) Cq, Tensor(c!) hn, "
@@ -1437,6 +1571,15 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("gb_decode(Tensor K, int n, int shift, int dbits, Tensor blk_base, int phase, "
         "Tensor(a!)? counts, Tensor(b!)? outdeg, Tensor? offsets, Tensor(c!)? srcl, "
         "Tensor(d!)? ent_end, Tensor(e!)? ent_blk, Tensor(f!)? ent_dst) -> ()");
+  m.def("gb_cell_count(Tensor ent_blk, Tensor ent_dst, int bshift, int nblk, int nbins, Tensor(a!) C) -> ()");
+  m.def("gb_cell_rows(Tensor C, int nblk, int nbins, Tensor(a!) T, Tensor(b!) R) -> ()");
+  m.def("gb_cell_scan(Tensor C, int nblk, int nbins, Tensor RE, Tensor RR, Tensor(a!) CM, Tensor(b!) RID) -> ()");
+  m.def("gb_cell_colsum(Tensor C, int nblk, int nbins, int G, Tensor(a!) P) -> ()");
+  m.def("gb_cell_place(Tensor C, Tensor CM, Tensor RID, int nblk, int nbins, int G, Tensor Poff, Tensor CI, "
+        "Tensor(a!) run_delta, Tensor(b!) run_chunk, Tensor(c!) run_first) -> ()");
+  m.def("gb_entry_cells(Tensor ent_blk, Tensor ent_dst, Tensor ent_end, int bshift, int nblk, int nbins, "
+        "Tensor CM, Tensor RID, Tensor run_delta, Tensor RE, Tensor CI, Tensor ce_lo, Tensor tlen, int wu_e, "
+        "int bin_mask, Tensor(a!) dloc, Tensor(b!) ts, Tensor(c!) srcl) -> ()");
   m.def("gb_entry_flags(Tensor ent_blk, Tensor ent_dst, Tensor ent_end, int bin_shift, Tensor(a!) rs, "
         "Tensor(b!) cs, Tensor(c!) srcl) -> ()");
   m.def("gb_entry_place(Tensor ent_dst, Tensor ent_end, Tensor run_of_ent, Tensor run_delta, "
@@ -1501,6 +1644,12 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("gb_sort", &gb_sort);
   m.impl("gb_degree_sorted", &gb_degree_sorted);
   m.impl("gb_decode", &gb_decode);
+  m.impl("gb_cell_count", &gb_cell_count);
+  m.impl("gb_cell_rows", &gb_cell_rows);
+  m.impl("gb_cell_scan", &gb_cell_scan);
+  m.impl("gb_cell_colsum", &gb_cell_colsum);
+  m.impl("gb_cell_place", &gb_cell_place);
+  m.impl("gb_entry_cells", &gb_entry_cells);
   m.impl("gb_entry_flags", &gb_entry_flags);
   m.impl("gb_entry_place", &gb_entry_place);
   m.impl("pr_spmv", &pr_spmv);

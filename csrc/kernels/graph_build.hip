@@ -6,7 +6,8 @@
 // offset in its 8192-source block, so ONE radix sort (rocPRIM onesweep over only the
 // key's bits) puts the edges in layout order, and the decode pass skips the duplicates
 // (a distinct edge = the last copy of its key). The passes around it are single sweeps:
-//   degree   -- raw out-degree of the input edges (degree relabeling), u32 atomics;
+//   degree   -- raw out-degree of the input edges (degree relabeling): ids partitioned
+//               on their high bits by a 2-pass radix sort, one LDS histogram per bucket;
 //   keys     -- relabel, keep this rank's destinations, map sources to the [own | ghost]
 //               index space and pack the key (two-phase compaction: count, write);
 //   decode   -- per distinct edge the u16 source offset + entry-end bit, the entry list
@@ -14,7 +15,9 @@
 //               source (LDS-privatised histogram per 8192-source block, no global atomic
 //               per edge);
 //   entries  -- run-start bits (a run = the entries of one (block, destination bin)),
-//               chunk starts, bin-major destination offsets and tile starts.
+//               chunk starts, bin-major destination offsets and tile starts, from the
+//               (block, bin) cell matrix: row scans give each run's first entry and index,
+//               column scans its bin-major position (gb_cell_* kernels).
 // Everything else (per-chunk / per-run tables, a few thousand to a few million rows) is
 // torch on the device (dalgo/ops/graph.py::build_blocked_native).
 #include <hip/hip_runtime.h>
@@ -48,21 +51,50 @@ __global__ void __launch_bounds__(256) gb_degree_kernel(const int32_t* __restric
   }
 }
 
-// degree by sort: over the SORTED ids, every run boundary records where the run of its id
-// starts and where the previous id's run ends (deg = end - start; absent ids stay 0 / 0)
-__global__ void __launch_bounds__(256) gb_runs_kernel(const uint32_t* __restrict__ sorted, int64_t n,
-                                                      int32_t* __restrict__ start, int32_t* __restrict__ end) {
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i <= n; i += stride) {
-    const uint32_t cur = i < n ? sorted[i] : 0u;
-    const uint32_t prev = i > 0 ? sorted[i - 1] : 0u;
-    if (i == n) {
-      end[prev] = (int32_t)n;
-    } else if (i == 0 || cur != prev) {
-      start[cur] = (int32_t)i;
-      if (i > 0) end[prev] = (int32_t)i;
-    }
+// degree by partition: the ids sorted on their HIGH bits only (2 radix passes at 2^26
+// ids), so every bucket of 2^kBktBits consecutive ids is one contiguous range; one block
+// per bucket counts it in an LDS histogram and adds it to deg (each entry owned by one
+// block: no global atomics)
+constexpr int kBktBits = 13;
+
+__global__ void __launch_bounds__(256) gb_bucket_starts_kernel(const uint32_t* __restrict__ sorted, int64_t n,
+                                                               int nb, int64_t* __restrict__ starts) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b > nb) return;
+  if (b == nb) { starts[b] = n; return; }
+  int64_t lo = 0, hi = n;   // first i with (sorted[i] >> kBktBits) >= b
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)(sorted[mid] >> kBktBits) < b) lo = mid + 1;
+    else hi = mid;
   }
+  starts[b] = lo;
+}
+
+__global__ void __launch_bounds__(256) gb_bucket_degree_kernel(const uint32_t* __restrict__ sorted,
+                                                               const int64_t* __restrict__ starts,
+                                                               int32_t* __restrict__ deg) {
+  __shared__ uint32_t hist[1 << kBktBits];
+  for (int j = threadIdx.x; j < (1 << kBktBits); j += 256) hist[j] = 0u;
+  __syncthreads();
+  const int64_t b = blockIdx.x, i0 = starts[b], i1 = starts[b + 1];
+  constexpr uint32_t mask = (1u << kBktBits) - 1u;
+  // 16-B loads from the first aligned position on
+  const int64_t a0 = min(i1, (i0 + 3) & ~(int64_t)3);
+  for (int64_t i = i0 + threadIdx.x; i < a0; i += 256) atomicAdd(&hist[sorted[i] & mask], 1u);
+  const int64_t nv = (i1 - a0) >> 2;
+  const uint4* v = reinterpret_cast<const uint4*>(sorted + a0);
+  for (int64_t q = threadIdx.x; q < nv; q += 256) {
+    const uint4 x = v[q];
+    atomicAdd(&hist[x.x & mask], 1u);
+    atomicAdd(&hist[x.y & mask], 1u);
+    atomicAdd(&hist[x.z & mask], 1u);
+    atomicAdd(&hist[x.w & mask], 1u);
+  }
+  for (int64_t i = a0 + (nv << 2) + threadIdx.x; i < i1; i += 256) atomicAdd(&hist[sorted[i] & mask], 1u);
+  __syncthreads();
+  int32_t* d = deg + (b << kBktBits);
+  for (int j = threadIdx.x; j < (1 << kBktBits); j += 256) d[j] += (int32_t)hist[j];
 }
 
 // ---------------------------------------------------------------------------- keys
@@ -375,6 +407,191 @@ __global__ void __launch_bounds__(256) gb_entry_place_kernel(const int32_t* __re
   }
 }
 
+
+// ---------------------------------------------------------------------------- cells
+// The runs of the K4b layout are the non-empty cells of the (block, destination bin)
+// matrix: entries are in chunk-major (block, destination) order, so the entries of one cell
+// are contiguous, a row-major scan of the cell counts gives every run's first entry and
+// its index, and a column-major scan gives its bin-major position -- no per-entry scans,
+// sorts or searches (nblk x nbins cells: 33.5M at R-MAT scale 26 on one rank).
+
+// C[cell] += entries of the cell; one atomic per run of equal cells inside a wave
+__global__ void __launch_bounds__(256) gb_cell_count_kernel(const int32_t* __restrict__ ent_blk,
+                                                            const int32_t* __restrict__ ent_dst, int64_t nent,
+                                                            int bshift, int nblk, int nbins,
+                                                            int32_t* __restrict__ C) {
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t e0 = (int64_t)blockIdx.x * 256; e0 < nent; e0 += stride) {
+    const int64_t e = e0 + threadIdx.x;
+    const bool in = e < nent;
+    int64_t cell = -1;
+    if (in) {
+      const int32_t b = ent_blk[e], bin = ent_dst[e] >> bshift;
+      if (b >= 0 && b < nblk && bin >= 0 && bin < nbins) cell = (int64_t)b * nbins + bin;
+    }
+    const int64_t prev = __shfl_up(cell, 1, 64);
+    const bool head = cell >= 0 && (lane == 0 || prev != cell);
+    const uint64_t hm = __ballot(head), vm = __ballot(in);
+    if (head) {
+      const uint64_t above = hm & ~((2ull << lane) - 1ull);   // heads after this lane
+      const int end = above ? __ffsll((long long)above) - 1 : 64 - __clzll((long long)vm);
+      atomicAdd(C + cell, end - lane);
+    }
+  }
+}
+
+// per row (block): entries T and non-empty cells R
+__global__ void __launch_bounds__(256) gb_cell_rows_kernel(const int32_t* __restrict__ C, int nbins,
+                                                           int64_t* __restrict__ T, int64_t* __restrict__ R) {
+  __shared__ int64_t s_t[4], s_r[4];
+  const int64_t row = blockIdx.x;
+  const int32_t* c = C + row * nbins;
+  int64_t t = 0, r = 0;
+  for (int j = threadIdx.x; j < nbins; j += 256) {
+    const int32_t v = c[j];
+    t += v;
+    r += v > 0;
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    t += __shfl_xor(t, off, 64);
+    r += __shfl_xor(r, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) { s_t[threadIdx.x >> 6] = t; s_r[threadIdx.x >> 6] = r; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T[row] = s_t[0] + s_t[1] + s_t[2] + s_t[3];
+    R[row] = s_r[0] + s_r[1] + s_r[2] + s_r[3];
+  }
+}
+
+// per row: CM[cell] = first entry of the cell (RE[row] + exclusive count prefix), RID[cell]
+// = its run index (RR[row] + exclusive non-empty prefix); 4 cells per thread per step
+__global__ void __launch_bounds__(256) gb_cell_scan_kernel(const int32_t* __restrict__ C, int nbins,
+                                                           const int64_t* __restrict__ RE,
+                                                           const int64_t* __restrict__ RR,
+                                                           int32_t* __restrict__ CM, int32_t* __restrict__ RID) {
+  __shared__ int s_c[4], s_n[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t row = blockIdx.x;
+  const int64_t base = row * nbins;
+  int64_t ce = RE[row], cr = RR[row];
+  for (int j0 = 0; j0 < nbins; j0 += 1024) {
+    const int j = j0 + threadIdx.x * 4;
+    int v[4];
+    int sc = 0, sn = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v[u] = j + u < nbins ? C[base + j + u] : 0;
+      sc += v[u];
+      sn += v[u] > 0;
+    }
+    int xc = sc, xn = sn;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int yc = __shfl_up(xc, off, 64), yn = __shfl_up(xn, off, 64);
+      if (lane >= off) { xc += yc; xn += yn; }
+    }
+    if (lane == 63) { s_c[wid] = xc; s_n[wid] = xn; }
+    __syncthreads();
+    int pc = xc - sc, pn = xn - sn, tc = 0, tn = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      if (w < wid) { pc += s_c[w]; pn += s_n[w]; }
+      tc += s_c[w];
+      tn += s_n[w];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (j + u < nbins) {
+        CM[base + j + u] = (int32_t)(ce + pc);
+        RID[base + j + u] = (int32_t)(cr + pn);
+      }
+      pc += v[u];
+      pn += v[u] > 0;
+    }
+    ce += tc;
+    cr += tn;
+    __syncthreads();
+  }
+}
+
+// P[g][bin] = entries of column bin over rows [g G, (g + 1) G)
+__global__ void __launch_bounds__(256) gb_cell_colsum_kernel(const int32_t* __restrict__ C, int nblk, int nbins,
+                                                             int G, int64_t* __restrict__ P) {
+  const int bin = blockIdx.x * 256 + threadIdx.x;
+  const int g = blockIdx.y;
+  if (bin >= nbins) return;
+  const int r1 = min(nblk, (g + 1) * G);
+  int64_t s = 0;
+  for (int r = g * G; r < r1; ++r) s += C[(int64_t)r * nbins + bin];
+  P[(int64_t)g * nbins + bin] = s;
+}
+
+// walks column bin over rows [g G, (g + 1) G) from its bin-major start Poff[g][bin]: every
+// non-empty cell (= run q) gets run_delta[q] = bin-major start - chunk-major start, its
+// chunk and its first entry
+__global__ void __launch_bounds__(256) gb_cell_place_kernel(const int32_t* __restrict__ C,
+                                                            const int32_t* __restrict__ CM,
+                                                            const int32_t* __restrict__ RID, int nblk,
+                                                            int nbins, int G, const int64_t* __restrict__ Poff,
+                                                            const int32_t* __restrict__ CI, int64_t nruns,
+                                                            int32_t* __restrict__ run_delta,
+                                                            int32_t* __restrict__ run_chunk,
+                                                            int64_t* __restrict__ run_first) {
+  const int bin = blockIdx.x * 256 + threadIdx.x;
+  const int g = blockIdx.y;
+  if (bin >= nbins) return;
+  const int r1 = min(nblk, (g + 1) * G);
+  int64_t pos = Poff[(int64_t)g * nbins + bin];
+  for (int r = g * G; r < r1; ++r) {
+    const int64_t cell = (int64_t)r * nbins + bin;
+    const int32_t c = C[cell];
+    if (c > 0) {
+      const int32_t q = RID[cell];
+      if (q >= 0 && q < nruns) {
+        const int32_t cm = CM[cell];
+        run_delta[q] = (int32_t)(pos - cm);
+        run_chunk[q] = CI[r];
+        run_first[q] = cm;
+      }
+      pos += c;
+    }
+  }
+}
+
+// per entry: bin-major destination (dloc), run-start bit on the end edge of a run's first
+// entry, tile starts (a new work unit every wu_e edges of a chunk and a new tile every
+// tlen[chunk] edges of the unit, on entry boundaries; chunk starts always)
+__global__ void __launch_bounds__(256) gb_entry_cells_kernel(
+    const int32_t* __restrict__ ent_blk, const int32_t* __restrict__ ent_dst, const int64_t* __restrict__ ent_end,
+    int64_t nent, int bshift, int nblk, int nbins, const int32_t* __restrict__ CM,
+    const int32_t* __restrict__ RID, const int32_t* __restrict__ run_delta, int64_t nruns,
+    const int64_t* __restrict__ RE, const int32_t* __restrict__ CI, const int64_t* __restrict__ ce_lo,
+    const int64_t* __restrict__ tlen, int64_t nch, int64_t wu_e, int bin_mask, int16_t* __restrict__ dloc,
+    int64_t ndloc, uint8_t* __restrict__ ts, uint16_t* __restrict__ srcl, int64_t nsrcl) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nent; e += stride) {
+    const int32_t b = ent_blk[e], d = ent_dst[e], bin = d >> bshift;
+    if (b < 0 || b >= nblk || bin < 0 || bin >= nbins) continue;
+    const int64_t cell = (int64_t)b * nbins + bin;
+    const int32_t q = RID[cell];
+    if (q < 0 || q >= nruns) continue;
+    const int64_t pos = e + run_delta[q];
+    if (pos >= 0 && pos < ndloc) dloc[pos] = (int16_t)(d & bin_mask);
+    const int64_t ee = ent_end[e];
+    if (e == CM[cell] && ee >= 0 && ee < nsrcl) srcl[ee] |= (uint16_t)0x4000;
+    const int32_t ch = CI[b];
+    bool t = e == RE[b];
+    if (!t && e > 0 && ch >= 0 && ch < nch) {
+      const int64_t tl = tlen[ch];
+      const int64_t a = (e > 1 ? ent_end[e - 2] + 1 : 0) - ce_lo[ch];   // entry e - 1's first edge
+      const int64_t bb = ent_end[e - 1] + 1 - ce_lo[ch];                // entry e's first edge
+      t = (a / wu_e) != (bb / wu_e) || ((a % wu_e) / tl) != ((bb % wu_e) / tl);
+    }
+    ts[e] = t;
+  }
+}
+
 }  // namespace
 }  // namespace dalgo
 
@@ -391,16 +608,26 @@ hipError_t dalgo_gb_degree(const int32_t* ids, int64_t n, uint32_t* deg, hipStre
 }
 
 hipError_t dalgo_gb_sort32(void* tmp, size_t* tmp_bytes, const uint32_t* in, uint32_t* out, int64_t n,
-                           int end_bit, hipStream_t st) {
-  if (n < 0 || n >= (int64_t)0x7fffffffLL || end_bit < 1 || end_bit > 32) return hipErrorInvalidValue;
-  return rocprim::radix_sort_keys(tmp, *tmp_bytes, in, out, (size_t)n, 0u, (unsigned)end_bit, st);
+                           int begin_bit, int end_bit, hipStream_t st) {
+  if (n < 0 || n >= (int64_t)0x7fffffffLL || end_bit < 1 || end_bit > 32 || begin_bit < 0 || begin_bit >= end_bit)
+    return hipErrorInvalidValue;
+  return rocprim::radix_sort_keys(tmp, *tmp_bytes, in, out, (size_t)n, (unsigned)begin_bit, (unsigned)end_bit, st);
 }
 
-hipError_t dalgo_gb_runs(const uint32_t* sorted, int64_t n, int32_t* start, int32_t* end, hipStream_t st) {
+int dalgo_gb_bucket_bits() { return kBktBits; }
+
+// ids sorted on bits [kBktBits, end_bit): deg[v] += occurrences of v (ids < 2^end_bit);
+// starts: int64[2^(end_bit - kBktBits) + 1] workspace
+hipError_t dalgo_gb_bucket_degree(const uint32_t* sorted, int64_t n, int end_bit, int64_t* starts, int32_t* deg,
+                                  hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  if (n >= (int64_t)0x7fffffffLL) return hipErrorInvalidValue;
-  const int64_t g = std::min<int64_t>(cdiv(n + 1, 256), 256 * 64);
-  hipLaunchKernelGGL(gb_runs_kernel, dim3((unsigned)g), dim3(256), 0, st, sorted, n, start, end);
+  if (end_bit <= kBktBits || end_bit > 31 || n >= (int64_t)0x7fffffffLL) return hipErrorInvalidValue;
+  const int nb = 1 << (end_bit - kBktBits);
+  hipLaunchKernelGGL(gb_bucket_starts_kernel, dim3((unsigned)cdiv(nb + 1, 256)), dim3(256), 0, st, sorted, n, nb,
+                     starts);
+  DALGO_LAUNCH_CHECK();
+  hipLaunchKernelGGL(gb_bucket_degree_kernel, dim3((unsigned)nb), dim3(256), 0, st, sorted,
+                     (const int64_t*)starts, deg);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -475,6 +702,63 @@ hipError_t dalgo_gb_entry_place(const int32_t* ent_dst, const int64_t* ent_end, 
   const int64_t g = std::min<int64_t>(cdiv(nent, 256), 256 * 64);
   hipLaunchKernelGGL(gb_entry_place_kernel, dim3((unsigned)g), dim3(256), 0, st, ent_dst, ent_end, nent,
                      run_of_ent, run_delta, run_chunk, cs, ce_lo, tlen, wu_e, bin_mask, dloc, ts);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+
+hipError_t dalgo_gb_cells(int phase, const int32_t* ent_blk, const int32_t* ent_dst, int64_t nent, int bshift,
+                          int nblk, int nbins, int32_t* C, int64_t* T, int64_t* R, const int64_t* RE,
+                          const int64_t* RR, int32_t* CM, int32_t* RID, int G, int64_t* P, const int64_t* Poff,
+                          const int32_t* CI, int64_t nruns, int32_t* run_delta, int32_t* run_chunk,
+                          int64_t* run_first, hipStream_t st) {
+  if (nblk < 1 || nbins < 1 || (int64_t)nblk * nbins > ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  const int ng = G > 0 ? (nblk + G - 1) / G : 0;
+  switch (phase) {
+    case 0: {   // counts
+      if (nent <= 0) return hipSuccess;
+      const int64_t g = std::min<int64_t>(cdiv(nent, 256), 256 * 64);
+      hipLaunchKernelGGL(gb_cell_count_kernel, dim3((unsigned)g), dim3(256), 0, st, ent_blk, ent_dst, nent, bshift,
+                         nblk, nbins, C);
+      break;
+    }
+    case 1:     // row totals
+      hipLaunchKernelGGL(gb_cell_rows_kernel, dim3((unsigned)nblk), dim3(256), 0, st, (const int32_t*)C, nbins, T, R);
+      break;
+    case 2:     // row scans
+      hipLaunchKernelGGL(gb_cell_scan_kernel, dim3((unsigned)nblk), dim3(256), 0, st, (const int32_t*)C, nbins, RE,
+                         RR, CM, RID);
+      break;
+    case 3:     // column sums per row group
+      if (G < 1) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(gb_cell_colsum_kernel, dim3((unsigned)cdiv(nbins, 256), (unsigned)ng), dim3(256), 0, st,
+                         (const int32_t*)C, nblk, nbins, G, P);
+      break;
+    case 4:     // run tables
+      if (G < 1) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(gb_cell_place_kernel, dim3((unsigned)cdiv(nbins, 256), (unsigned)ng), dim3(256), 0, st,
+                         (const int32_t*)C, (const int32_t*)CM, (const int32_t*)RID, nblk, nbins, G, Poff, CI, nruns,
+                         run_delta, run_chunk, run_first);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t dalgo_gb_entry_cells(const int32_t* ent_blk, const int32_t* ent_dst, const int64_t* ent_end, int64_t nent,
+                                int bshift, int nblk, int nbins, const int32_t* CM, const int32_t* RID,
+                                const int32_t* run_delta, int64_t nruns, const int64_t* RE, const int32_t* CI,
+                                const int64_t* ce_lo, const int64_t* tlen, int64_t nch, int64_t wu_e, int bin_mask,
+                                int16_t* dloc, int64_t ndloc, uint8_t* ts, uint16_t* srcl, int64_t nsrcl,
+                                hipStream_t st) {
+  if (nent <= 0) return hipSuccess;
+  if (wu_e < 1) return hipErrorInvalidValue;
+  const int64_t g = std::min<int64_t>(cdiv(nent, 256), 256 * 64);
+  hipLaunchKernelGGL(gb_entry_cells_kernel, dim3((unsigned)g), dim3(256), 0, st, ent_blk, ent_dst, ent_end, nent,
+                     bshift, nblk, nbins, CM, RID, run_delta, nruns, RE, CI, ce_lo, tlen, nch, wu_e, bin_mask, dloc,
+                     ndloc, ts, srcl, nsrcl);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

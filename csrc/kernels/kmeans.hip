@@ -306,6 +306,9 @@ struct KmAux {
   int* chg_new;                       // LOOP (optional): their new and previous cluster,
   int* chg_old;                       //       aligned with `changed` (the moved-row sort
                                       //       then reads them sequentially)
+  const int* acl;                     // LOOP (optional, no a_prev): previous cluster of the
+                                      //       active row at list position p (the filter's
+                                      //       output order); neither: assign[row] itself
   // CAND (candidate-pruned LOOP): the active rows sorted by cluster (idx), tiles that never
   // straddle two clusters, and each centre's neighbour lists (km_centre_nbrs_kernel)
   const int4* tiles;                  // tile t: (cluster, first, end position in idx, -)
@@ -934,7 +937,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
         // and assign only where the cluster changed (assign[row] holds old_c otherwise)
         aux.ul[row] = make_float2(km_up1(sqrtf(km_up1(dist + tol))), fmaxf(lo2, 0.f));
         // CAND: the tile's rows were sorted by their previous cluster, acl
-        old_c = CAND ? acl : aux.a_prev[row];
+        old_c = CAND ? acl : (aux.a_prev ? aux.a_prev[row] : (aux.acl ? aux.acl[p] : assign[row]));
         chg = bi != old_c;
         if (chg) assign[row] = bi;
       } else {
@@ -1574,24 +1577,29 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
 }
 
 // ---------------------------------------------------------------------------
-// K2 full pass on 16x16x32 MFMAs (bf16, DP = 128, no row indirection): the same distance
-// keys as the pipelined form, tiled for v_mfma_f32_16x16x32_bf16, which sustains ~12 %
-// more FLOP/s than the 32x32x16 form next to an argmin VALU load (profiles/round4/r4_36:
-// a power / clock effect). A wave holds PG groups of 16 points (B operand, negated; lane
-// l: point l % 16, dims 32 s + 8 (l / 16) .. +8 of k-step s); a 128-centre chunk (the
-// same swizzled LDS-DMA image as the 32x32 form) is 8 sub-tiles of 16 centres (A: lane
-// l reads centre l % 16, piece 4 s + l / 16). The accumulator starts at 0.5|c|^2 + M, so
-// acc = 0.5|x - c|^2 + M - 0.5|x|^2 >= 0 and its float bits order like the distances;
-// lane l holds centres 4 (l / 16) + r of the sub-tile for point l % 16: key = bits & ~31
-// | (sub * 4 + r) keeps the lowest id among equal keys of a chunk, chunks compare on the
-// value bits only (strict), and the four lane groups of a point are merged at the end.
-template <int NW, int PG, int MINB>
+// K2 on 16x16x32 MFMAs (bf16, DP = 128): the same distance keys as the pipelined form,
+// tiled for v_mfma_f32_16x16x32_bf16, which sustains ~12 % more FLOP/s than the 32x32x16
+// form next to an argmin VALU load (profiles/round4/r4_36: a power / clock effect). A wave
+// holds PG groups of 16 points (B operand; lane l: point l % 16, dims 32 s + 8 (l / 16)
+// .. +8 of k-step s); a 128-centre chunk (the same swizzled LDS-DMA image as the 32x32
+// form) is 8 sub-tiles of 16 centres (A: lane l reads centre l % 16, piece 4 s + l / 16).
+// The accumulator starts at -(0.5|c|^2 + M), so acc = -(0.5|x - c|^2 + M - 0.5|x|^2) < 0
+// and the signed-integer order of its bits is the distance order; lane l holds centres
+// 4 (l / 16) + r of the sub-tile for point l % 16: key = bits & ~31 | (sub * 4 + r) keeps
+// the lowest id among equal keys of a chunk, chunks compare on the value bits only
+// (strict), and the four lane groups of a point are merged at the end.
+// BND (the dense form of a bound-filtered iteration): the rows are idx[0, *aux.mcount)
+// (device count; blocks past it exit at once), every lane also keeps its second-smallest
+// key (v_med3 per key pair, merged over chunks and lane groups), and the epilogue is the
+// filtered iteration's: u / l per row, assign and the moved-row list where the cluster
+// differs from the previous one (aux.acl[p], else aux.a_prev[row], else assign[row]).
+template <int NW, int PG, int MINB, bool BND = false>
 __global__ void __launch_bounds__(NW * 64, MINB)
 kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
                        const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int kpad,
                        int* __restrict__ assign, float* __restrict__ mind,
                        double* __restrict__ sse, int sse_mask, float* __restrict__ xh,
-                       unsigned* __restrict__ xmax) {
+                       unsigned* __restrict__ xmax, const int32_t* __restrict__ idx, const KmAux aux) {
   constexpr int DP = 128, KS = DP / 32;        // 16x16x32 k-steps per centre row
   constexpr int NJ = DP * 2 / 16;              // 16-B pieces per row
   constexpr int SWZ = 15;
@@ -1607,20 +1615,51 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   __shared__ float s_m[NW];
   __shared__ double s_sse[NW];
   __shared__ float s_x2[NW][PG * 16];           // |x|^2 per point (read in the epilogue)
+  __shared__ int s_row[BND ? NW : 1][BND ? PG * 16 : 1];   // BND: row and previous cluster
+  __shared__ int s_old[BND ? NW : 1][BND ? PG * 16 : 1];   //      per point
+  // BND: the block's moved rows (row, new, previous cluster), appended to the global list
+  // with ONE atomic per block: a device-scope atomic per wave on the single counter
+  // serialised the launch (55 vs 19 ms at 14M moved rows, profiles/round5/r5_13)
+  __shared__ int s_mv[BND ? 3 : 1][BND ? TILE : 1];
+  __shared__ int s_nmv;
+  __shared__ unsigned long long s_mvbase;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lg = lane >> 4, pl = lane & 15;
   const int nchunk = kpad / CH;
   const int64_t pbase = ((int64_t)blockIdx.x * NW + wid) * (PG * 16);
+  float tol = 0.f;
+  if constexpr (BND) {
+    n = min(n, (int64_t)*aux.mcount);
+    if ((int64_t)blockIdx.x * TILE >= n) return;   // block-uniform, before any barrier
+    tol = *aux.tol;
+    if (tid == 0) s_nmv = 0;                       // published by the first barrier below
+  }
 
-  // ---- points: rows past n read row 0 and are zeroed after the wait (the last wave only)
+  // ---- points: rows past n read a valid row and are zeroed after the wait (last wave only)
   uint4 bf[PG][KS];
   const bool full = pbase + PG * 16 <= n;
+  int rowv[BND ? PG : 1], oldv[BND ? PG : 1];
+  if constexpr (BND) {
+#pragma unroll
+    for (int g = 0; g < PG; ++g) {
+      const int64_t p = pbase + g * 16 + pl;
+      rowv[g] = idx[p < n ? p : n - 1];
+    }
+  }
 #pragma unroll
   for (int g = 0; g < PG; ++g) {
     const int64_t p = pbase + g * 16 + pl;
-    const uint16_t* src = X + (full || p < n ? p : 0) * ldx + 8 * lg;
+    const int64_t row = BND ? (int64_t)rowv[g] : (full || p < n ? p : 0);
+    const uint16_t* src = X + row * ldx + 8 * lg;
 #pragma unroll
     for (int s = 0; s < KS; ++s) bf[g][s] = *reinterpret_cast<const uint4*>(src + 32 * s);
+  }
+  if constexpr (BND) {
+#pragma unroll
+    for (int g = 0; g < PG; ++g) {
+      const int64_t p = pbase + g * 16 + pl;
+      oldv[g] = aux.acl ? aux.acl[p < n ? p : n - 1] : (aux.a_prev ? aux.a_prev[rowv[g]] : assign[rowv[g]]);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (!full) {
@@ -1629,6 +1668,15 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
       if (pbase + g * 16 + pl >= n)
 #pragma unroll
         for (int s = 0; s < KS; ++s) bf[g][s] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  if constexpr (BND) {
+    if (lg == 0) {
+#pragma unroll
+      for (int g = 0; g < PG; ++g) {
+        s_row[wid][g * 16 + pl] = rowv[g];
+        s_old[wid][g * 16 + pl] = oldv[g];
+      }
+    }
   }
   float mx = 0.f;
 #pragma unroll
@@ -1687,8 +1735,13 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   issue(0);
 
   int bkey[PG], bch[PG], cm[PG];
+  int bkey2[BND ? PG : 1], cm2[BND ? PG : 1];   // BND: second-smallest keys
 #pragma unroll
   for (int g = 0; g < PG; ++g) { bkey[g] = 0x7fffffff; bch[g] = 0; cm[g] = 0x7fffffff; }
+  if constexpr (BND) {
+#pragma unroll
+    for (int g = 0; g < PG; ++g) { bkey2[g] = 0x7fffffff; cm2[g] = 0x7fffffff; }
+  }
   const int kmask = ~31;
   // software pipeline over the 8 sub-tiles of a chunk: sub-tile s accumulates into set
   // s & 1 while the argmin of sub-tile s - 1 reads the other set, so the argmin VALU runs
@@ -1720,7 +1773,14 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
         ac[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[s]),
                                                         __builtin_bit_cast(bf16x8, bf[g][s]), ac[g], 0, 0, 0);
   };
-  // keys = value bits & ~31 | (sub * 4 + r): the lowest id wins among equal keys of a chunk
+  // keys = value bits & ~31 | (sub * 4 + r): the lowest id wins among equal keys of a chunk.
+  // BND: with (x, y) new, the running pair (m <= m2) becomes m' = min3(m, x, y),
+  // m2' = min(m2, med3(m, x, y)) (see reduce_tile of the pipelined form)
+  auto med3 = [](int a, int b, int c) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+  };
   auto argmin_sub = [&](const f32x4 (&ac)[PG], int sub) {
 #pragma unroll
     for (int g = 0; g < PG; ++g) {
@@ -1728,14 +1788,29 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
       const int k1 = (__float_as_int(ac[g][1]) & kmask) | (sub * 4 + 1);
       const int k2 = (__float_as_int(ac[g][2]) & kmask) | (sub * 4 + 2);
       const int k3 = (__float_as_int(ac[g][3]) & kmask) | (sub * 4 + 3);
+      if constexpr (BND) cm2[g] = min(cm2[g], med3(cm[g], k0, k1));
       cm[g] = min(min(cm[g], k0), k1);
+      if constexpr (BND) cm2[g] = min(cm2[g], med3(cm[g], k2, k3));
       cm[g] = min(min(cm[g], k2), k3);
     }
   };
-  // interleave: 24 MFMAs of this sub-tile, the previous sub-tile's 36 argmin VALU ops
-  // (1.5 per MFMA: inside the 8 issue cycles a 16x16x32 MFMA leaves free), and the next
-  // sub-tile's fragment reads each right after the MFMAs that last read the register it
-  // replaces (k-step s of all PG groups, then fragment s is dead): the next C values and
+  // chunk merge: across chunks on the value bits only (strict: the earlier chunk keeps a
+  // tie); BND: second smallest of {bkey, bkey2, cm, cm2}
+  auto merge_chunk = [&](int chp) {
+#pragma unroll
+    for (int g = 0; g < PG; ++g) {
+      if constexpr (BND) bkey2[g] = min(max(bkey[g], cm[g]), min(bkey2[g], cm2[g]));
+      const bool take = (cm[g] & kmask) < (bkey[g] & kmask);
+      bkey[g] = take ? cm[g] : bkey[g];
+      bch[g] = take ? chp : bch[g];
+      cm[g] = 0x7fffffff;
+      if constexpr (BND) cm2[g] = 0x7fffffff;
+    }
+  };
+  // interleave: 24 MFMAs of this sub-tile, the previous sub-tile's argmin VALU ops (36,
+  // 1.5 per MFMA: inside the 8 issue cycles a 16x16x32 MFMA leaves free; BND: 60), and the
+  // next sub-tile's fragment reads each right after the MFMAs that last read the register
+  // it replaces (k-step s of all PG groups, then fragment s is dead): the next C values and
   // fragment 0 after MFMA 6, fragment 1 after 12, 2 after 18, 3 after 24 -- the two
   // fragment sets share registers instead of both living through the whole sub-tile
   auto pin = [&]() {
@@ -1743,9 +1818,9 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
 #pragma unroll
     for (int i = 0; i < KS * PG; i += 2) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                 // MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);                 // VALU
+      __builtin_amdgcn_sched_group_barrier(0x002, BND ? 3 : 2, 0);       // VALU
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, BND ? 2 : 1, 0);
       if (i + 2 == PG) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS read
       else if ((i + 2) % PG == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
@@ -1766,14 +1841,7 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
     argmin_sub(acc[1], 7);
     pin();
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int g = 0; g < PG; ++g) {
-      // across chunks on the value bits only (strict: the earlier chunk keeps a tie)
-      const bool take = (cm[g] & kmask) < (bkey[g] & kmask);
-      bkey[g] = take ? cm[g] : bkey[g];
-      bch[g] = take ? ch - 1 : bch[g];
-      cm[g] = 0x7fffffff;
-    }
+    merge_chunk(ch - 1);
 #pragma unroll
     for (int sub = 1; sub < NSUB; ++sub) {
 #pragma unroll
@@ -1809,34 +1877,85 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   km_wait_vmcnt<0>();                          // the redundant last DMAs landed
   // the last chunk's sub-tile 7 and merge
   argmin_sub(acc[1], 7);
-#pragma unroll
-  for (int g = 0; g < PG; ++g) {
-    const bool take = (cm[g] & kmask) < (bkey[g] & kmask);
-    bkey[g] = take ? cm[g] : bkey[g];
-    bch[g] = take ? nchunk - 1 : bch[g];
-  }
+  merge_chunk(nchunk - 1);
 
   // ---- merge the 4 lane groups of each point, write the outputs
   double my_sse = 0.0;
 #pragma unroll
   for (int g = 0; g < PG; ++g) {
     float v = -__int_as_float(bkey[g] & kmask);
+    float v2 = 0.f;
+    if constexpr (BND) v2 = -__int_as_float(bkey2[g] & kmask);
     const int ix = bkey[g] & 31;
     int id = bch[g] * CH + (ix >> 2) * 16 + 4 * lg + (ix & 3);
 #pragma unroll
     for (int o = 16; o <= 32; o <<= 1) {
       const float pv = __shfl_xor(v, o, 64);
       const int pi = __shfl_xor(id, o, 64);
+      if constexpr (BND) {
+        // second best over both: second smallest of {v, v2, pv, pv2}
+        const float pv2 = __shfl_xor(v2, o, 64);
+        v2 = fminf(fmaxf(v, pv), fminf(v2, pv2));
+      }
       if (pv < v || (pv == v && pi < id)) { v = pv; id = pi; }
     }
     const int64_t p = pbase + g * 16 + pl;
-    if (lg == 0 && p < n) {
-      const float x2 = s_x2[wid][g * 16 + pl];
-      const float dist = fmaxf(2.f * (v - M) + x2, 0.f);
-      assign[p] = id;
-      if (mind) mind[p] = dist;
-      if (xh) xh[p] = 0.5f * x2;
-      my_sse += (double)dist;
+    if constexpr (BND) {
+      bool chg = false;
+      int row = 0, old_c = 0;
+      if (lg == 0 && p < n) {
+        const float x2 = s_x2[wid][g * 16 + pl];
+        row = s_row[wid][g * 16 + pl];
+        old_c = s_old[wid][g * 16 + pl];
+        const float dist = fmaxf(2.f * (v - M) + x2, 0.f);
+        const float dist2 = fmaxf(2.f * (v2 - M) + x2, 0.f);
+        // u rounded up, l rounded down (the keys are truncated towards smaller distances)
+        const float lo2 = km_dn1(sqrtf(fmaxf(km_dn1(dist2 - tol), 0.f)));
+        aux.ul[row] = make_float2(km_up1(sqrtf(km_up1(dist + tol))), fmaxf(lo2, 0.f));
+        chg = id != old_c;
+        if (chg) assign[row] = id;
+        my_sse += (double)dist;
+      }
+      // moved rows -> the block's LDS list (one LDS atomic per wave and point group)
+      const uint64_t cmk = __ballot(chg);
+      if (cmk != 0ull) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&s_nmv, __popcll(cmk));
+        base = __shfl(base, 0);
+        if (chg) {
+          const int slot = base + __popcll(cmk & ((1ull << lane) - 1ull));
+          s_mv[0][slot] = row;
+          s_mv[1][slot] = id;
+          s_mv[2][slot] = old_c;
+        }
+      }
+    } else {
+      if (lg == 0 && p < n) {
+        const float x2 = s_x2[wid][g * 16 + pl];
+        const float dist = fmaxf(2.f * (v - M) + x2, 0.f);
+        assign[p] = id;
+        if (mind) mind[p] = dist;
+        if (xh) xh[p] = 0.5f * x2;
+        my_sse += (double)dist;
+      }
+    }
+  }
+  if constexpr (BND) {
+    // the block's moved rows -> the global list at one reserved range (coalesced writes)
+    __syncthreads();
+    const int c = s_nmv;
+    if (c > 0) {
+      if (tid == 0) s_mvbase = atomicAdd(aux.n_changed, (unsigned long long)c);
+      __syncthreads();
+      const long long b = (long long)s_mvbase;
+      for (int j = tid; j < c; j += NT)
+        if (b + j < aux.cap) {
+          aux.changed[b + j] = s_mv[0][j];
+          if (aux.chg_new) {
+            aux.chg_new[b + j] = s_mv[1][j];
+            aux.chg_old[b + j] = s_mv[2][j];
+          }
+        }
     }
   }
   if (xmax && lane == 0) atomicMax(xmax, __float_as_uint(mx));
@@ -1854,23 +1973,33 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
 }
 
 // the 16x16x32 form holds two 32 KB centre chunks plus 0.5|c|^2 for every centre in LDS
-// and runs two blocks per CU: it takes kpad <= 3456; larger k goes to the pipelined form
-static bool assign16_fits(int kpad) {
-  // static: 2 chunk buffers (64 KB) + |x|^2 of the 384 points + small; 2 blocks per CU
-  return kpad % 128 == 0 && 2 * 128 * 128 * 2 + 4 * 6 * 16 * 4 + (size_t)kpad * sizeof(float) + 1024 <=
-                                80 * 1024;
+// and runs two blocks per CU: it takes kpad <= 3456 (BND, with the per-point row /
+// previous-cluster tables and the moved-row list: <= 2304); larger k goes to the
+// pipelined form
+static bool assign16_fits(int kpad, bool bnd = false) {
+  // static: 2 chunk buffers (64 KB) + |x|^2 of the 384 points (+ BND: 5 x 384 ints) + small
+  return kpad % 128 == 0 &&
+         2 * 128 * 128 * 2 + (bnd ? 6 : 1) * 4 * 6 * 16 * 4 + (size_t)kpad * sizeof(float) + 1024 <=
+             80 * 1024;
 }
 
+template <bool BND>
 static hipError_t launch_assign16(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                   const float* hn, int kpad, int* assign, float* mind, double* sse,
-                                  int sse_mask, float* xh, unsigned* xmax, hipStream_t st) {
+                                  int sse_mask, float* xh, unsigned* xmax, hipStream_t st,
+                                  const int32_t* idx = nullptr, const KmAux& aux = KmAux{}) {
   constexpr int NW = 4, PG = 6, MINB = 2;
-  if (!assign16_fits(kpad)) return hipErrorInvalidValue;
+  if (!assign16_fits(kpad, BND)) return hipErrorInvalidValue;
+  if (BND && (idx == nullptr || aux.mcount == nullptr || aux.tol == nullptr || aux.ul == nullptr ||
+              aux.changed == nullptr || aux.n_changed == nullptr ||
+              (aux.chg_new == nullptr) != (aux.chg_old == nullptr)))
+    return hipErrorInvalidValue;
   const size_t dyn = (size_t)kpad * sizeof(float);
+  // BND: n = the host's upper bound of the device count (blocks past the count exit)
   const int64_t grid = cdiv(n, (int64_t)NW * PG * 16);
   if (grid == 0) return hipSuccess;
   if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
-  auto kfn = kmeans_assign16_kernel<NW, PG, MINB>;
+  auto kfn = kmeans_assign16_kernel<NW, PG, MINB, BND>;
   static size_t attr_set = 0;
   if (dyn > attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1879,7 +2008,7 @@ static hipError_t launch_assign16(const void* X, int64_t n, int64_t ldx, const v
     attr_set = dyn;
   }
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(NW * 64), dyn, st, (const uint16_t*)X, n, ldx,
-                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse, sse_mask, xh, xmax);
+                     (const uint16_t*)Cq, hn, kpad, assign, mind, sse, sse_mask, xh, xmax, idx, aux);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -1905,7 +2034,7 @@ static hipError_t launch_assign_dp(const void* X, int64_t n, int64_t ldx, const 
 #ifndef KM_XP_NO16
   if constexpr (sizeof(T) == 2 && DP == 128)
     if (assign16_fits(kpad))
-      return launch_assign16(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, nullptr, nullptr, st);
+      return launch_assign16<false>(X, n, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, nullptr, nullptr, st);
 #endif
   if constexpr (sizeof(T) == 2 && DP >= 64)
     if (kpad % 128 == 0)
@@ -2075,9 +2204,8 @@ hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP
   if (post != nullptr) {
     aux.mcount = post->mcount; aux.a_prev = post->a_prev; aux.tol = post->tol;
     aux.ul = reinterpret_cast<float2*>(post->ul); aux.changed = post->changed; aux.n_changed = post->n_changed;
-    aux.cap = post->cap; aux.chg_new = post->chg_new; aux.chg_old = post->chg_old;
+    aux.cap = post->cap; aux.chg_new = post->chg_new; aux.chg_old = post->chg_old; aux.acl = post->acl;
     if ((aux.chg_new == nullptr) != (aux.chg_old == nullptr)) return hipErrorInvalidValue;
-    if (cand == nullptr && aux.a_prev == nullptr) return hipErrorInvalidValue;
     if (cand != nullptr) {
       // idx = the active rows sorted by cluster (dalgo_kmeans_sort_active)
       aux.tiles = reinterpret_cast<const int4*>(cand->tiles);
@@ -2091,6 +2219,14 @@ hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP
             X, m, ldx, Cq, hn, kpad, assign, nullptr, sse, sse_mask, st, idx, nullptr, aux);
       return hipErrorInvalidValue;
     }
+#ifndef KM_XP_NO16
+    // the dense form of the filtered iteration: 16x16x32 MFMAs, top-2 keys, no pruning
+    if (DP == 128 && assign16_fits(kpad, true) && idx != nullptr)
+      return launch_assign16<true>(X, m, ldx, Cq, hn, kpad, assign, nullptr, sse, sse_mask, nullptr, nullptr,
+                                   st, idx, aux);
+#endif
+    if (cand == nullptr && aux.a_prev == nullptr && aux.acl == nullptr && idx == nullptr)
+      return hipErrorInvalidValue;
     // top-2: 2 point tiles per wave (3 would spill past 256 VGPRs in the tile loop)
     if (DP == 128)
       return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true, true>(
@@ -2111,7 +2247,7 @@ hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP
   }
 #ifndef KM_XP_NO16
   if (DP == 128 && idx == nullptr && assign16_fits(kpad))
-    return launch_assign16(X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, aux.xh, aux.xmax, st);
+    return launch_assign16<false>(X, m, ldx, Cq, hn, kpad, assign, mind, sse, sse_mask, aux.xh, aux.xmax, st);
 #endif
   if (DP == 128)
     return launch_assign_pipe<128, 4, 3, 4, 2, 2, true>(X, m, ldx, Cq, hn, kpad, assign, mind, sse,

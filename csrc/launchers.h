@@ -37,6 +37,7 @@ struct DalgoKmPost {
   long long cap;
   int* chg_new;                       // optional: clusters of the changed rows (aligned)
   int* chg_old;
+  const int* acl;                     // optional: previous cluster of active row p (idx order)
 };
 
 // candidate-pruned K2 (dalgo_kmeans_sort_active + dalgo_km_centre_nbrs outputs)
@@ -216,8 +217,10 @@ struct DalgoGbKeyArgs {
 extern "C" {
 hipError_t dalgo_gb_degree(const int32_t* ids, int64_t n, uint32_t* deg, hipStream_t st);
 hipError_t dalgo_gb_sort32(void* tmp, size_t* tmp_bytes, const uint32_t* in, uint32_t* out, int64_t n,
-                           int end_bit, hipStream_t st);
-hipError_t dalgo_gb_runs(const uint32_t* sorted, int64_t n, int32_t* start, int32_t* end, hipStream_t st);
+                           int begin_bit, int end_bit, hipStream_t st);
+int dalgo_gb_bucket_bits();
+hipError_t dalgo_gb_bucket_degree(const uint32_t* sorted, int64_t n, int end_bit, int64_t* starts, int32_t* deg,
+                                  hipStream_t st);
 int64_t dalgo_gb_key_blocks(int64_t n);
 hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, const DalgoGbKeyArgs* a,
                          int phase, uint32_t* bitmap, int32_t* counts, const int64_t* offsets,
@@ -231,6 +234,17 @@ hipError_t dalgo_gb_decode(const uint64_t* K, int64_t n, int shift, int dbits, c
                            hipStream_t st);
 hipError_t dalgo_gb_entry_flags(const int32_t* ent_blk, const int32_t* ent_dst, const int64_t* ent_end,
                                 int64_t nent, int bin_shift, uint8_t* rs, uint8_t* cs, uint16_t* srcl,
+                                hipStream_t st);
+hipError_t dalgo_gb_cells(int phase, const int32_t* ent_blk, const int32_t* ent_dst, int64_t nent, int bshift,
+                          int nblk, int nbins, int32_t* C, int64_t* T, int64_t* R, const int64_t* RE,
+                          const int64_t* RR, int32_t* CM, int32_t* RID, int G, int64_t* P, const int64_t* Poff,
+                          const int32_t* CI, int64_t nruns, int32_t* run_delta, int32_t* run_chunk,
+                          int64_t* run_first, hipStream_t st);
+hipError_t dalgo_gb_entry_cells(const int32_t* ent_blk, const int32_t* ent_dst, const int64_t* ent_end, int64_t nent,
+                                int bshift, int nblk, int nbins, const int32_t* CM, const int32_t* RID,
+                                const int32_t* run_delta, int64_t nruns, const int64_t* RE, const int32_t* CI,
+                                const int64_t* ce_lo, const int64_t* tlen, int64_t nch, int64_t wu_e, int bin_mask,
+                                int16_t* dloc, int64_t ndloc, uint8_t* ts, uint16_t* srcl, int64_t nsrcl,
                                 hipStream_t st);
 hipError_t dalgo_gb_entry_place(const int32_t* ent_dst, const int64_t* ent_end, int64_t nent,
                                 const int32_t* run_of_ent, const int32_t* run_delta, const int32_t* run_chunk,

@@ -118,7 +118,7 @@ def kmeans_witness(km, rt) -> dict:
 def kmeans_job(rt, rows: int = 100_000_000, dim: int = 128, k: int = 1024, iters: int = 5,
                dtype=torch.bfloat16, noise: float = 1.0, data_seed: int = 7,
                bound_filter: bool = True, candidates: bool = True, witness: bool = True,
-               warm: bool = True, pool_gb: float = 48.0) -> dict:
+               warm: bool = True, pool_gb: float = 48.0, dense: str = "auto") -> dict:
     """BASELINE config #4 (100M x 128, k = 1024): the reference's k-means job, strong
     scaling (the global point set is row-sharded over the ranks)."""
     from dalgo.data.synthetic import blobs
@@ -134,8 +134,9 @@ def kmeans_job(rt, rows: int = 100_000_000, dim: int = 128, k: int = 1024, iters
         wlo, whi = even_slices(wn, W)[rt.rank]
         Xw = blobs(wn, dim, k, row_range=(wlo, whi), device=rt.device, dtype=dtype, seed=3,
                    noise=noise)
-        kw = KMeans(KMeansConfig(k=min(k, wn), n_iterations=2, seed=5, bound_filter=bound_filter,
-                                 candidates=candidates), Xw, wlo, wn)
+        kw = KMeans(KMeansConfig(k=min(k, wn), n_iterations=3, seed=5, bound_filter=bound_filter,
+                                 candidates=candidates, dense=dense), Xw, wlo, wn)
+        kw.step()
         kw.step()
         kw.step()
         del kw, Xw
@@ -150,7 +151,7 @@ def kmeans_job(rt, rows: int = 100_000_000, dim: int = 128, k: int = 1024, iters
     t = time.perf_counter()
     ev.mark()
     km = KMeans(KMeansConfig(k=k, n_iterations=iters, seed=1, bound_filter=bound_filter,
-                             candidates=candidates), X, lo, rows)
+                             candidates=candidates, dense=dense), X, lo, rows)
     ev.mark()
     for _ in range(iters):
         km.step()
@@ -163,7 +164,7 @@ def kmeans_job(rt, rows: int = 100_000_000, dim: int = 128, k: int = 1024, iters
     init_ms, iter_ms = spans[0], spans[1:]
     sse_last = km.sse.clone()
     comm.all_reduce_sum(sse_last)
-    active, moved = km.active_history, km.changed_history
+    active, moved, dense_rows = km.active_history, km.changed_history, km.dense_history
     wit = kmeans_witness(km, rt) if witness else None
     flops = 2.0 * rows * k * dim
     steady = iter_ms[1:]
@@ -178,6 +179,8 @@ def kmeans_job(rt, rows: int = 100_000_000, dim: int = 128, k: int = 1024, iters
         "full_pass_tflops_per_gpu": (flops / W / (iter_ms[0] / 1e3) / 1e12) if iter_ms else None,
         "reassigned_rows_per_iter_rank0": active, "moved_rows_per_iter_rank0": moved,
         "bound_filter": km.bounds, "candidate_pruning": getattr(km, "_cand", None) is not None,
+        "dense_filtered_iterations": dense,
+        "dense_k2_rows_per_iter_rank0": dense_rows,
         "incremental_k3": km.incremental, "sse_last_iteration": float(sse_last.item()),
         "correctness_witness": wit,
         "config": {"rows": rows, "dim": dim, "k": k, "dtype": str(dtype).replace("torch.", ""),

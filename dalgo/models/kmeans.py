@@ -28,6 +28,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
+import math
+
 import numpy as np
 import torch
 
@@ -47,6 +49,12 @@ class KMeansConfig:
     bound_filter: bool = True  # GPU bf16: Hamerly-filtered iterations after the first
     candidates: bool = True    # ... whose K2 tiles (one cluster each) stream only the centres
                                # near their cluster's centre (k <= 1024)
+    # filtered iterations that run the dense top-2 K2 over the active rows instead of the
+    # candidate-pruned one: "auto" = the iteration right after the full pass (the first
+    # centre shifts are large, few chunks prune; no cluster sort either) and, decided on
+    # the device, every iteration with >= DENSE_FRACTION of the rows active; "always";
+    # "never"
+    dense: str = "auto"
     # GPU, k <= 2048: incremental K3 (only moved rows re-summed) and the bound-filter state.
     # Costs ~24 B/row (move workspace) + ~48 B/row (bounds, candidates) of HBM on top of X
     # (bf16 d = 128: X is 256 B/row); False = plain full-pass Lloyd, no per-row state
@@ -62,6 +70,12 @@ class KMeansConfig:
 class KMeansHistory:
     sse: list = field(default_factory=list)
     shift: list = field(default_factory=list)
+
+
+# measured crossover of the two filtered K2 forms (profiles/round5/r5_14, 100M x 128,
+# k = 1024): the dense form wins at 49-100 % active rows (overlapping blobs), the pruned
+# one at 19-32 % (separated blobs); at ~70 % they tie
+DENSE_FRACTION = 0.4
 
 
 def sample_rows(n_global: int, k: int, seed: int) -> np.ndarray:
@@ -117,8 +131,9 @@ class KMeans:
             self._n_changed = torch.zeros(1, dtype=torch.int64, device=self.dev)
             self._mws = K.MoveWorkspace(self.dev, n, k)
             # per-iteration device counters (read by the properties below, after the run):
-            # [active rows, moved rows, 1 if the iteration was a full pass]
-            self._hist = torch.zeros((64, 3), dtype=torch.int64, device=self.dev)
+            # [active rows, moved rows, 1 if the iteration was a full pass, rows of the
+            # dense filtered K2]
+            self._hist = torch.zeros((64, 4), dtype=torch.int64, device=self.dev)
             if self.bounds:
                 self._alloc_bounds()
             else:
@@ -138,6 +153,8 @@ class KMeans:
         self._a_prev = torch.empty(max(n, 1), **i32)
         self._idx = torch.empty(max(n, 1), **i32)
         self._n_active = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self._n_cand = torch.zeros(1, dtype=torch.int64, device=self.dev)    # device K2 choice
+        self._n_dense = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self._just_full = False                       # last iteration was the full pass
         self._Q = torch.zeros(k, dtype=torch.float64, device=self.dev)
         self._cq_prev = torch.empty((k, self.DP), dtype=self.cen.Cq.dtype, device=self.dev)
@@ -196,6 +213,14 @@ class KMeans:
         h = self._hist[: self._hist_n].tolist()
         return [int(r[1]) for r in h if not r[2]]
 
+    @property
+    def dense_history(self) -> list:
+        """Rows re-assigned by the dense (unpruned top-2) K2 per iteration (0: full pass or
+        the candidate-pruned K2)."""
+        if not self.bounds:
+            return []
+        return [int(v) for v in self._hist[: self._hist_n, 3].tolist()]
+
     def clear_history(self):
         self._hist_n = 0
 
@@ -238,12 +263,26 @@ class KMeans:
             self._record(0, n)
             self._record(1, 0)
             self._record(2, 1)
+            self._record(3, 0)
             self._first = False
             self._just_full = True
         else:
             cw = self._cand
+            # K2 form: "dense" (the candidate workspace's filter outputs -- active rows in
+            # row order, their clusters in acl -- no neighbour lists / cluster sort, the
+            # unpruned top-2 K2), "cand" (pruned), or "device": both launched, the active
+            # count on the device picks one (the other sees a zero row count)
+            mode = self.cfg.dense
+            if cw is None:
+                form = "bounds"
+            elif mode == "always" or (mode == "auto" and self._just_full):
+                form = "dense"
+            elif mode == "never":
+                form = "cand"
+            else:
+                form = "device"
             with self._ph("centres"):
-                if cw is not None:
+                if form in ("cand", "device"):
                     K.centre_nbrs(self.cen, self._cq_prev, self._delta, self._s, cw)
                 else:
                     K.centre_bounds(self.cen.Cq, self._cq_prev, k, d, self._delta, self._s)
@@ -251,8 +290,15 @@ class KMeans:
                 K.filter_rows(self.assign, self._ul, self._delta, self._s,
                               self._a_prev if cw is None else None, self._idx, self._n_active,
                               cw.acl if cw is not None else None)
-                if cw is not None:
-                    K.sort_active(self._idx, self._n_active, cw)
+                n_cand, n_dense = self._n_active, self._n_active
+                if form == "device":
+                    # dense iff active >= DENSE_FRACTION n (no host sync)
+                    on = self._n_active >= int(math.ceil(DENSE_FRACTION * n))
+                    torch.mul(self._n_active, on, out=self._n_dense)
+                    torch.sub(self._n_active, self._n_dense, out=self._n_cand)
+                    n_cand, n_dense = self._n_cand, self._n_dense
+                if form in ("cand", "device"):
+                    K.sort_active(self._idx, n_cand, cw)
             self._n_changed.zero_()
             with self._ph("assign"):
                 # K2 over the active rows; its epilogue updates u / l and collects the
@@ -260,9 +306,13 @@ class KMeans:
                 # no chunk extension right after the full pass: the first centre shifts
                 # are so large that the next filter never decides on l (the same active
                 # rows either way, profiles/round4/r4_13), so tight l there is pure cost
-                K.assign_rows(self.X, self.cen, cw.rows if cw is not None else self._idx, n,
-                              self.assign, post=self._post_args, cand=cw,
-                              extend=not self._just_full)
+                if form in ("cand", "device", "bounds"):
+                    K.assign_rows(self.X, self.cen, cw.rows if cw is not None else self._idx, n,
+                                  self.assign, post=dict(self._post_args, m_dev=n_cand), cand=cw,
+                                  extend=not self._just_full)
+                if form in ("dense", "device"):
+                    K.assign_rows(self.X, self.cen, self._idx, n, self.assign,
+                                  post=dict(self._post_args, m_dev=n_dense, acl=cw.acl))
             with self._ph("accumulate_incremental"):
                 K.move_rows(self.X, self.DP, self._changed, self._n_changed, self.assign,
                             self._a_prev, self._S64, self._cnt64, self._mws, self._xh, self._Q,
@@ -272,6 +322,7 @@ class KMeans:
             self._record(0, self._n_active)
             self._record(1, self._n_changed)
             self._record(2, 0)
+            self._record(3, n_dense if form in ("dense", "device") else 0)
             self._just_full = False
         self._hist_n += 1
         # local SSE on the (rounded) centres of this assignment

@@ -136,8 +136,9 @@ def degree_count_(deg: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
 
 
 def degree_sorted_(deg: torch.Tensor, ids: torch.Tensor, bits: int) -> torch.Tensor:
-    """deg[v] += #occurrences of v in ids (GPU int32, ids < 2^bits): a radix sort of the
-    ids and their run lengths instead of one atomic per id (graph_build.hip)."""
+    """deg[v] += #occurrences of v in ids (GPU int32, ids < 2^bits): the ids partitioned
+    on their high bits (2 radix passes at 2^26 ids), then one LDS histogram per bucket of
+    8192 ids, instead of one global atomic per id (graph_build.hip)."""
     _ext.ops().gb_degree_sorted(ids.contiguous(), int(bits), deg)
     return deg
 
@@ -150,6 +151,7 @@ def local_outdeg(shard: GraphShard) -> torch.Tensor:
 
 # ------------------------------------------------------------------ propagation blocking
 SRC_SPAN = 8192          # sources per chunk: the LDS table of pb_gather (csrc/kernels/pr_binned.hip)
+CELL_CAP = 1 << 30       # largest (block, bin) cell matrix of the native build (4 B x 3 per cell)
 PB_DUMMY = 65536         # val / dloc padding after the entries (kPbDummy in pr_binned.hip)
 
 
@@ -609,45 +611,90 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
         del K
         K = None
     _mark("decode")
-    # ---- entries: run / chunk starts, run-start bits
+    # ---- entries: run / chunk starts, run-start bits, bin-major places, tile starts
     bshift = bin_width.bit_length() - 1
     nbins = max(1, (nl + bin_width - 1) // bin_width)
-    rs = torch.empty(nent, dtype=torch.uint8, device=dev)
-    cs = torch.empty(nent, dtype=torch.uint8, device=dev)
-    ops.gb_entry_flags(ent_blk, ent_dst, ent_end, bshift, rs, cs, srcl)
-    run_first = torch.nonzero(rs).flatten()
-    chunk_first = torch.nonzero(cs).flatten()
-    nch = int(chunk_first.numel())
-    nruns = int(run_first.numel())
-    assert nent < (1 << 31) - 8 and nruns < (1 << 31)
-    chunk_blk = ent_blk[chunk_first].to(torch.int64)
-    run_of_ent = (torch.cumsum(rs, 0, dtype=torch.int32) - 1)
-    del rs
-    run_chunk = torch.searchsorted(chunk_first, run_first, right=True) - 1
-    run_bin = (ent_dst[run_first] >> bshift).to(torch.int64)
-    run_len = torch.diff(torch.cat([run_first, torch.tensor([nent], **i64)]))
-    border = torch.argsort(run_bin * (nch + 1) + run_chunk)
-    bm_start = torch.empty_like(run_first)
-    bm_start[border] = torch.cumsum(run_len[border], 0) - run_len[border]
-    run_delta = bm_start - run_first
-    del bm_start, border
-    chunk_run = torch.searchsorted(run_chunk, torch.arange(nch + 1, **i64))
-    bin_cnt = torch.zeros(nbins, **i64).index_add_(0, run_bin, run_len)
-    bin_lo = torch.cumsum(bin_cnt, 0) - bin_cnt
-    _mark("entries_runs")
-    # ---- tiles / work units: a chunk is cut every wu_e edges into work units and every
-    # tlen edges inside a unit into tiles, both on entry boundaries
-    ce_lo = torch.where(chunk_first > 0, ent_end[(chunk_first - 1).clamp_min(0)] + 1,
-                        torch.zeros_like(chunk_first))
-    ce_n = torch.diff(torch.cat([ce_lo, torch.tensor([E], **i64)]))
+    nblk_k = max(nblk, 1)
     wu_e = max(1 << 15, E // 4096)
-    tlen = torch.clamp((torch.clamp(ce_n, max=wu_e) + 15) // 16, min=min(1024, tile), max=tile)
     n4 = (nent + 3) // 4 * 4 + PB_DUMMY
     dloc = torch.zeros(n4, dtype=torch.int16, device=dev)
     ts = torch.empty(nent, dtype=torch.uint8, device=dev)
-    ops.gb_entry_place(ent_dst, ent_end, run_of_ent, run_delta.to(torch.int32), run_chunk.to(torch.int32), cs,
-                       ce_lo, tlen, wu_e, bin_width - 1, dloc, ts)
-    del run_of_ent, cs, ent_dst, ent_blk
+    assert nent < (1 << 31) - 8
+    if nblk_k * nbins <= CELL_CAP:
+        # runs = the non-empty cells of the (block, bin) matrix (graph_build.hip gb_cell_*)
+        ncell = nblk_k * nbins
+        C = torch.zeros(ncell, **i32)
+        ops.gb_cell_count(ent_blk, ent_dst, bshift, nblk_k, nbins, C)
+        T = torch.empty(nblk_k, **i64)
+        R = torch.empty(nblk_k, **i64)
+        ops.gb_cell_rows(C, nblk_k, nbins, T, R)
+        RE = torch.cumsum(T, 0) - T                       # first entry of every block
+        RR = torch.cumsum(R, 0) - R                       # first run of every block
+        nz = T > 0
+        CI = (torch.cumsum(nz, 0) - nz.long()).to(torch.int32)   # chunk of a non-empty block
+        nch, nruns, max_runs = (int(x) for x in torch.stack([nz.sum(), R.sum(), R.max()]).tolist())
+        CM = torch.empty(ncell, **i32)
+        RID = torch.empty(ncell, **i32)
+        ops.gb_cell_scan(C, nblk_k, nbins, RE, RR, CM, RID)
+        G = 64
+        ng = (nblk_k + G - 1) // G
+        P = torch.empty((ng, nbins), **i64)
+        ops.gb_cell_colsum(C, nblk_k, nbins, G, P)
+        bin_cnt = P.sum(0)
+        bin_lo = torch.cumsum(bin_cnt, 0) - bin_cnt
+        Poff = torch.cumsum(P, 0) - P + bin_lo
+        run_delta = torch.empty(nruns, **i32)
+        run_chunk = torch.empty(nruns, **i32)
+        run_first = torch.empty(nruns, **i64)
+        ops.gb_cell_place(C, CM, RID, nblk_k, nbins, G, Poff, CI, run_delta, run_chunk, run_first)
+        del C, P, Poff
+        chunk_blk = torch.nonzero(nz).flatten()
+        chunk_first = RE[chunk_blk]
+        chunk_run = torch.cat([RR[chunk_blk], torch.tensor([nruns], **i64)])
+        _mark("entries_runs")
+        ce_lo = torch.where(chunk_first > 0, ent_end[(chunk_first - 1).clamp_min(0)] + 1,
+                            torch.zeros_like(chunk_first))
+        ce_n = torch.diff(torch.cat([ce_lo, torch.tensor([E], **i64)]))
+        tlen = torch.clamp((torch.clamp(ce_n, max=wu_e) + 15) // 16, min=min(1024, tile), max=tile)
+        ops.gb_entry_cells(ent_blk, ent_dst, ent_end, bshift, nblk_k, nbins, CM, RID, run_delta, RE, CI,
+                           ce_lo, tlen, wu_e, bin_width - 1, dloc, ts, srcl)
+        del CM, RID, ent_dst, ent_blk, RE, RR, CI
+    else:
+        # matrix too large: per-entry flags, scans and a sort of the runs
+        rs = torch.empty(nent, dtype=torch.uint8, device=dev)
+        cs = torch.empty(nent, dtype=torch.uint8, device=dev)
+        ops.gb_entry_flags(ent_blk, ent_dst, ent_end, bshift, rs, cs, srcl)
+        run_first = torch.nonzero(rs).flatten()
+        chunk_first = torch.nonzero(cs).flatten()
+        nch = int(chunk_first.numel())
+        nruns = int(run_first.numel())
+        chunk_blk = ent_blk[chunk_first].to(torch.int64)
+        run_of_ent = (torch.cumsum(rs, 0, dtype=torch.int32) - 1)
+        del rs
+        run_chunk = torch.searchsorted(chunk_first, run_first, right=True) - 1
+        run_bin = (ent_dst[run_first] >> bshift).to(torch.int64)
+        run_len = torch.diff(torch.cat([run_first, torch.tensor([nent], **i64)]))
+        border = torch.argsort(run_bin * (nch + 1) + run_chunk)
+        bm_start = torch.empty_like(run_first)
+        bm_start[border] = torch.cumsum(run_len[border], 0) - run_len[border]
+        run_delta = (bm_start - run_first).to(torch.int32)
+        run_chunk = run_chunk.to(torch.int32)
+        del bm_start, border
+        chunk_run = torch.searchsorted(run_chunk.to(torch.int64), torch.arange(nch + 1, **i64))
+        bin_cnt = torch.zeros(nbins, **i64).index_add_(0, run_bin, run_len)
+        bin_lo = torch.cumsum(bin_cnt, 0) - bin_cnt
+        max_runs = int((chunk_run[1:] - chunk_run[:-1]).max().item())
+        _mark("entries_runs")
+        # tiles / work units: a chunk is cut every wu_e edges into work units and every
+        # tlen edges inside a unit into tiles, both on entry boundaries
+        ce_lo = torch.where(chunk_first > 0, ent_end[(chunk_first - 1).clamp_min(0)] + 1,
+                            torch.zeros_like(chunk_first))
+        ce_n = torch.diff(torch.cat([ce_lo, torch.tensor([E], **i64)]))
+        tlen = torch.clamp((torch.clamp(ce_n, max=wu_e) + 15) // 16, min=min(1024, tile), max=tile)
+        ops.gb_entry_place(ent_dst, ent_end, run_of_ent, run_delta, run_chunk, cs,
+                           ce_lo, tlen, wu_e, bin_width - 1, dloc, ts)
+        del run_of_ent, cs, ent_dst, ent_blk
+    assert nruns < (1 << 31)
     tile_ent = torch.nonzero(ts).flatten()
     del ts
     e_start_t = torch.where(tile_ent > 0, ent_end[(tile_ent - 1).clamp_min(0)] + 1, torch.zeros_like(tile_ent))
@@ -664,9 +711,8 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     tile_run = torch.searchsorted(run_first, tile_ent) - chunk_run[tile_chunk]
     slo = blk_base[chunk_blk]
     ns = torch.clamp(blk_end[chunk_blk] - slo, max=S)
-    n_src = int((slo + ns).max().item())
-    assert int(tile_e[-1]) <= srcl.numel() and int(ns.min().item()) >= 1
-    max_runs = int((chunk_run[1:] - chunk_run[:-1]).max().item())
+    n_src, ns_min, te_last = (int(x) for x in torch.stack([(slo + ns).max(), ns.min(), tile_e[-1]]).tolist())
+    assert te_last <= srcl.numel() and ns_min >= 1
     _mark("tiles")
     # ---- phase-2 work items (as build_blocked)
     cap = max(int(nent // max(items, 1)), min_piece)

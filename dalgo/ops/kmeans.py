@@ -297,9 +297,11 @@ def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
     (float bits). ``post`` = dict(m_dev, a_prev, tol, ul, changed, n_changed): the
     filtered-iteration form -- the row count is m_dev (device; m its upper bound) and
     the epilogue writes the Hamerly bounds ul[row] = (u, l) (rounded outward, tol on the
-    device) and appends the rows whose cluster differs from a_prev to changed (count in
-    n_changed, which the caller zeroes): no host sync, no separate bound pass. In this
-    form assign must hold the previous clusters: only the changed rows are written.
+    device) and appends the rows whose cluster differs from the previous one (a_prev[row],
+    else post["acl"][p] -- the filter's list order -- else assign[row]) to changed (count
+    in n_changed, which the caller zeroes): no host sync, no separate bound pass. In this
+    form assign must hold the previous clusters: only the changed rows are written. On
+    DP = 128 it runs the dense 16x16x32 top-2 K2 (kmeans_assign16_kernel, BND form).
     ``cand`` (with post; idx = cand.rows, the active rows sorted by cluster): the
     candidate-pruned form -- a tile of cluster a streams only the chunks of a's
     neighbour list within 2 max(ua) of c_a (ua = the tile's distances to c_a, computed in
@@ -314,7 +316,8 @@ def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
                                  cand.cand() if cand is not None else [], None, None, None, None,
                                  post["m_dev"], post.get("a_prev"), post["tol"], post["ul"],
                                  post["changed"], post["n_changed"],
-                                 post.get("chg_new"), post.get("chg_old"), int(bool(extend)))
+                                 post.get("chg_new"), post.get("chg_old"), int(bool(extend)),
+                                 post.get("acl"))
 
 
 def bounds_init(mind: torch.Tensor, mind2: torch.Tensor, xmax: torch.Tensor, n: int,

@@ -755,12 +755,14 @@ def test_kmeans_centre_bounds_kernel(cuda, dtype, k, d):
         assert torch.allclose(sg.cpu(), sc, rtol=1e-5)
 
 
-def test_kmeans_assign_rows_fused_post(cuda):
-    """Filtered-iteration K2 (row count on the device, resident-grid tile loop, fused
-    bound update): only idx[:*m_dev] is re-assigned, equal to the full pass on those
-    rows; u / l bracket the exact distances (rounded outward, tol on the device); the
-    changed rows (vs a_prev) are collected exactly. Also the full pass's optional
-    0.5|x|^2 / max outputs and the bounds-init kernel."""
+@pytest.mark.parametrize("prev", ["a_prev", "acl", "assign"])
+def test_kmeans_assign_rows_fused_post(cuda, prev):
+    """Filtered-iteration K2 (row count on the device, fused bound update; d = 128: the
+    dense 16x16x32 top-2 form): only idx[:*m_dev] is re-assigned, equal to the full pass
+    on those rows; u / l bracket the exact distances (rounded outward, tol on the device);
+    the changed rows (vs the previous cluster: a_prev[row], acl[p] in list order, or
+    assign[row] itself) are collected exactly, with their new / previous clusters. Also
+    the full pass's optional 0.5|x|^2 / max outputs and the bounds-init kernel."""
     torch.manual_seed(9)
     n, d, k = 60_001, 128, 1000
     X = K.prepare_points((torch.randn(n, d) * 3).to(torch.bfloat16).to(cuda))
@@ -798,9 +800,17 @@ def test_kmeans_assign_rows_fused_post(cuda):
     u, l = ul[:, 0], ul[:, 1]
     changed = torch.empty(n, dtype=torch.int32, device=cuda)
     nch = torch.zeros(1, dtype=torch.int64, device=cuda)
-    K.assign_rows(X, cen, rows, n, a, post=dict(
-        m_dev=torch.tensor([m], dtype=torch.int64, device=cuda), a_prev=a_prev, tol=tol, ul=ul,
-        changed=changed, n_changed=nch))
+    cnew = torch.full((n,), -1, dtype=torch.int32, device=cuda)
+    cold = torch.full((n,), -1, dtype=torch.int32, device=cuda)
+    post = dict(m_dev=torch.tensor([m], dtype=torch.int64, device=cuda), tol=tol, ul=ul,
+                changed=changed, n_changed=nch, chg_new=cnew, chg_old=cold)
+    if prev == "a_prev":
+        post["a_prev"] = a_prev
+    elif prev == "acl":
+        acl = torch.full((n,), -3, dtype=torch.int32, device=cuda)
+        acl[:m] = a_prev[rows[:m].long()]
+        post["acl"] = acl
+    K.assign_rows(X, cen, rows, n, a, post=post)
     assert torch.equal(a[sel], full[sel]) and bool((a[~sel] == -7).all())
     assert bool((u[~sel] == -1).all()) and bool((l[~sel] == -1).all())
     dist = torch.cdist(X[:, :d].double(), cen.Cq[:k, :d].double())
@@ -813,6 +823,8 @@ def test_kmeans_assign_rows_fused_post(cuda):
     exp = torch.nonzero(sel & (full != a_prev))[:, 0]
     assert c == exp.numel()
     assert torch.equal(torch.sort(changed[:c]).values.long(), exp)
+    rows_c = changed[:c].long()
+    assert torch.equal(cnew[:c], full[rows_c]) and torch.equal(cold[:c], a_prev[rows_c])
 
 
 def test_kmeans_assign_top2_second_best(cuda):
@@ -1043,17 +1055,19 @@ def test_kmeans_candidates_match_plain(cuda):
     X = blobs(n, d, k, device=cuda, dtype=torch.bfloat16, seed=11)
     runs = {}
     for name, kw in [("cand", {}), ("bounds", dict(candidates=False)),
-                     ("plain", dict(bound_filter=False))]:
+                     ("plain", dict(bound_filter=False)), ("dense", dict(dense="always"))]:
         km = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5, **kw), X, 0, n)
         km.fit()
         runs[name] = km
     assert runs["cand"]._cand is not None and runs["bounds"]._cand is None
-    for other in ("bounds", "plain"):
+    for other in ("bounds", "plain", "dense"):
         assert np.allclose(runs["cand"].history.sse, runs[other].history.sse, rtol=2e-4)
     ha, hb = runs["cand"].active_history, runs["bounds"].active_history
     assert ha[0] == n and len(ha) == len(hb)
-    # the oracle: every candidate-pruned step against brute force from the same state
-    c = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5), X, 0, n)
-    assert c._cand is not None
-    for _ in range(7):
-        _kmeans_step_oracle(c)
+    # the oracle: every candidate-pruned step (the dense one right after the full pass
+    # included) against brute force from the same state; then the dense form on every step
+    for kw in ({}, dict(dense="always")):
+        c = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5, **kw), X, 0, n)
+        assert c._cand is not None
+        for _ in range(7):
+            _kmeans_step_oracle(c)

@@ -142,3 +142,24 @@ def test_degree_sorted_matches_bincount(cuda):
     G.degree_sorted_(deg, s, 18)
     ref = torch.bincount(s.long(), minlength=1 << 18) + 5
     assert torch.equal(deg.long(), ref)
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_cell_matrix_layout_equals_entry_scan(cuda, world, monkeypatch):
+    """The (block, bin) cell-matrix path of the run / tile tables (gb_cell_* kernels) and
+    the per-entry flag + scan + run-sort fallback build the same K4b layout, field by
+    field, on every rank (ghost blocks included)."""
+    scale = 15
+    edges, _ = rmat_input(scale, 16, torch.device(cuda), seed=21, chunk=1 << 16)
+    fields = ("srcl", "tile_e", "tile_ent", "tile_run", "chunk_tile", "wu_tile", "wu_chunk", "chunk_slo",
+              "chunk_ns", "chunk_run", "run_delta", "dloc", "wi_bin", "wi_lo", "wi_slab", "split_bin",
+              "split_first", "split_count")
+    for rank in range(world):
+        a = build_rmat_native(edges, scale, rank, world, cuda, reorder=False, bin_width=8192, tile=2048).layout
+        monkeypatch.setattr(G, "CELL_CAP", 0)
+        b = build_rmat_native(edges, scale, rank, world, cuda, reorder=False, bin_width=8192, tile=2048).layout
+        monkeypatch.undo()
+        for f in fields:
+            assert torch.equal(getattr(a, f), getattr(b, f)), f
+        for f in ("n_chunks", "n_entries", "n_src", "max_runs", "n_local"):
+            assert getattr(a, f) == getattr(b, f), f
