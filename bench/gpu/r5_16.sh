@@ -1,0 +1,8 @@
+set -o pipefail
+# round 5, session 16: full GPU suite; PageRank job with the bucketed degree count
+O=gpurun_out/r5_16
+mkdir -p $O
+export PYTHONPATH=$PWD TMPDIR=/tmp
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_all.log 2>&1 || exit $?
+timeout -k 10 200 python3 bench/pagerank_bench.py > $O/pr.log 2>&1 || exit $?
+DALGO_BUILD_SYNC=1 timeout -k 10 200 python3 bench/pagerank_bench.py --no-witness > $O/prs.log 2>&1 || exit $?

@@ -1550,10 +1550,10 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
   int64_t grid = cdiv(n, (int64_t)NW * PT * 32);
   if (grid == 0) return hipSuccess;
   if ((aux.mcount != nullptr) != LOOP) return hipErrorInvalidValue;
-  // a_prev: the Hamerly-only form's previous clusters (the candidate form has them per tile)
-  if (LOOP && (aux.tol == nullptr || aux.ul == nullptr ||
-               (!CAND && aux.a_prev == nullptr) || aux.changed == nullptr ||
-               aux.n_changed == nullptr))
+  // previous clusters: the Hamerly-only form reads a_prev[row], acl[p] or assign[row]; the
+  // candidate form has them per tile
+  if (LOOP && (aux.tol == nullptr || aux.ul == nullptr || aux.changed == nullptr ||
+               aux.n_changed == nullptr || (!CAND && aux.acl != nullptr && idx == nullptr)))
     return hipErrorInvalidValue;
   if (CAND && (kpad > 1024 || aux.tiles == nullptr || aux.n_tiles == nullptr || aux.hnb == nullptr ||
                aux.nb == nullptr || aux.nd == nullptr || idx == nullptr))

@@ -755,16 +755,18 @@ def test_kmeans_centre_bounds_kernel(cuda, dtype, k, d):
         assert torch.allclose(sg.cpu(), sc, rtol=1e-5)
 
 
+@pytest.mark.parametrize("d", [64, 128])
 @pytest.mark.parametrize("prev", ["a_prev", "acl", "assign"])
-def test_kmeans_assign_rows_fused_post(cuda, prev):
+def test_kmeans_assign_rows_fused_post(cuda, prev, d):
     """Filtered-iteration K2 (row count on the device, fused bound update; d = 128: the
     dense 16x16x32 top-2 form): only idx[:*m_dev] is re-assigned, equal to the full pass
     on those rows; u / l bracket the exact distances (rounded outward, tol on the device);
     the changed rows (vs the previous cluster: a_prev[row], acl[p] in list order, or
     assign[row] itself) are collected exactly, with their new / previous clusters. Also
-    the full pass's optional 0.5|x|^2 / max outputs and the bounds-init kernel."""
+    the full pass's optional 0.5|x|^2 / max outputs and the bounds-init kernel. d = 64:
+    the pipelined 32x32x16 form."""
     torch.manual_seed(9)
-    n, d, k = 60_001, 128, 1000
+    n, k = 60_001, 1000
     X = K.prepare_points((torch.randn(n, d) * 3).to(torch.bfloat16).to(cuda))
     cen = K.make_centers(torch.randn(k, d) * 3, torch.bfloat16, cuda)
     full = K.assign(X, cen)
