@@ -149,6 +149,32 @@ def local_outdeg(shard: GraphShard) -> torch.Tensor:
     return torch.bincount(s, minlength=shard.n_vertices).to(torch.int32)
 
 
+def _work_items(bin_cnt: torch.Tensor, bin_lo: torch.Tensor, nent: int, items: int, min_piece: int):
+    """Phase-2 work items: each bin's contiguous bin-major entry range, a hot bin cut into
+    ~cap-entry pieces (each with its own slab, combined in order afterwards); an empty
+    bin is one empty item (it writes zeros). Vectorised over the bins (numpy, one host
+    copy). Returns (wi_bin, wi_lo + [nent], wi_slab, split_bin, split_first, split_count)
+    as int arrays and the slab count."""
+    cap = max(int(nent // max(items, 1)), min_piece)
+    both = torch.stack([bin_cnt.to(torch.int64), bin_lo.to(torch.int64)]).cpu().numpy()
+    cnt, lo = both[0], both[1]
+    pieces = np.maximum(1, -(-cnt // cap))
+    step = np.maximum(1, -(-cnt // pieces))
+    ncut = np.where(cnt == 0, 1, -(-cnt // step))             # len(range(lo, lo + cnt, step))
+    nb = cnt.shape[0]
+    first = np.cumsum(ncut) - ncut
+    wb = np.repeat(np.arange(nb, dtype=np.int64), ncut)
+    k = np.arange(int(ncut.sum()), dtype=np.int64) - np.repeat(first, ncut)
+    wl = np.repeat(lo, ncut) + k * np.repeat(np.where(cnt == 0, 0, step), ncut)
+    split = pieces > 1
+    sp_bin = np.nonzero(split)[0]
+    sp_cnt = ncut[split]
+    sp_first = np.cumsum(sp_cnt) - sp_cnt
+    in_split = np.repeat(split, ncut)
+    slab = np.where(in_split, np.cumsum(in_split) - 1, -1)
+    return (wb, np.append(wl, nent), slab, sp_bin, sp_first, sp_cnt), int(sp_cnt.sum())
+
+
 # ------------------------------------------------------------------ propagation blocking
 SRC_SPAN = 8192          # sources per chunk: the LDS table of pb_gather (csrc/kernels/pr_binned.hip)
 CELL_CAP = 1 << 30       # largest (block, bin) cell matrix of the native build (4 B x 3 per cell)
@@ -361,28 +387,7 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
     assert int(tile_e[-1]) <= srcl.numel() and int((slo + ns).max()) <= n_src
     assert run_first.numel() == int(chunk_run[-1])
     # work items: each bin's contiguous entry range, hot bins cut into ~cap pieces
-    cap = max(int(nent // max(items, 1)), min_piece)
-    cnt_h = bin_cnt.cpu().tolist()
-    lo_h = bin_lo.cpu().tolist()
-    wb, wl, slab_h, sp_bin, sp_first, sp_cnt = [], [], [], [], [], []
-    nslab = 0
-    for b, (n_b, l_b) in enumerate(zip(cnt_h, lo_h)):
-        if n_b == 0:                                  # empty bin: one empty item (writes zeros)
-            wb.append(b); wl.append(l_b); slab_h.append(-1)
-            continue
-        pieces = max(1, -(-n_b // cap))
-        step = -(-n_b // pieces)
-        cuts = list(range(l_b, l_b + n_b, step))
-        if pieces > 1:
-            sp_bin.append(b); sp_first.append(nslab); sp_cnt.append(len(cuts))
-        for p0 in cuts:
-            wb.append(b)
-            wl.append(p0)
-            if pieces > 1:
-                slab_h.append(nslab); nslab += 1
-            else:
-                slab_h.append(-1)
-    wl.append(nent)
+    (wb, wl, slab_h, sp_bin, sp_first, sp_cnt), nslab = _work_items(bin_cnt, bin_lo, nent, items, min_piece)
     return BlockedLayout(srcl, i64(tile_e), i32(tile_ent), i32(tile_run), i32(chunk_tile),
                          i32(wu_tile), i32(wu_chunk), i32(slo),
                          i32(ns), i32(chunk_run), i32(run_delta),
@@ -715,28 +720,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     assert te_last <= srcl.numel() and ns_min >= 1
     _mark("tiles")
     # ---- phase-2 work items (as build_blocked)
-    cap = max(int(nent // max(items, 1)), min_piece)
-    cnt_h = bin_cnt.cpu().tolist()
-    lo_h = bin_lo.cpu().tolist()
-    wb, wl, slab_h, sp_bin, sp_first, sp_cnt = [], [], [], [], [], []
-    nslab = 0
-    for b, (n_b, l_b) in enumerate(zip(cnt_h, lo_h)):
-        if n_b == 0:
-            wb.append(b); wl.append(l_b); slab_h.append(-1)
-            continue
-        pieces = max(1, -(-n_b // cap))
-        step = -(-n_b // pieces)
-        cuts = list(range(l_b, l_b + n_b, step))
-        if pieces > 1:
-            sp_bin.append(b); sp_first.append(nslab); sp_cnt.append(len(cuts))
-        for p0 in cuts:
-            wb.append(b)
-            wl.append(p0)
-            if pieces > 1:
-                slab_h.append(nslab); nslab += 1
-            else:
-                slab_h.append(-1)
-    wl.append(nent)
+    (wb, wl, slab_h, sp_bin, sp_first, sp_cnt), nslab = _work_items(bin_cnt, bin_lo, nent, items, min_piece)
     it = lambda x: torch.tensor(x, **i32)
     c32 = lambda x: x.to(torch.int32).contiguous()
     splits = sorted({int(x) for x in seg_start if x > 0})
