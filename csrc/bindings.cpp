@@ -860,9 +860,69 @@ void gb_keys(const Tensor& src, const Tensor& dst, const std::optional<Tensor>& 
   DeviceGuard guard(src.device());
   DALGO_CHECK_HIP(dalgo_gb_keys(src.data_ptr<int32_t>(), dst.data_ptr<int32_t>(), n, &a, (int)phase,
                                 opt_ptr<uint32_t>(bitmap), opt_ptr<int32_t>(counts),
-                                opt_ptr<const int64_t>(offsets), base_all, opt_ptr<uint64_t>(keys),
+                                opt_ptr<const int64_t>(offsets), base_all, opt_ptr<uint64_t>(keys), nullptr,
                                 cur_stream()),
                   "gb_keys");
+}
+
+// one rank: keys of the packed (src << 32 | dst) edges (every destination is kept)
+void gb_keys_packed(const Tensor& packed, const std::optional<Tensor>& new_id, int64_t n_vertices, int64_t dbits,
+                    Tensor keys) {
+  check_t(packed, at::kLong, "packed");
+  check_t(keys, at::kLong, "keys");
+  const int64_t n = packed.numel();
+  TORCH_CHECK(keys.numel() >= n, "gb_keys_packed: keys too short");
+  if (new_id) {
+    check_i32(*new_id, "new_id");
+    TORCH_CHECK(new_id->numel() >= n_vertices, "gb_keys_packed: new_id [n_vertices]");
+  }
+  DalgoGbKeyArgs a{0, n_vertices, n_vertices, 1, 0, (int)dbits, opt_ptr<const int32_t>(new_id), nullptr, nullptr,
+                   nullptr, nullptr};
+  DeviceGuard guard(packed.device());
+  DALGO_CHECK_HIP(dalgo_gb_keys(nullptr, nullptr, n, &a, 1, nullptr, nullptr, nullptr, 0, reinterpret_cast<uint64_t*>(keys.data_ptr<int64_t>()),
+                                reinterpret_cast<const uint64_t*>(packed.data_ptr<int64_t>()), cur_stream()),
+                  "gb_keys_packed");
+}
+
+// packed[i] = src[i] << 32 | dst[i]
+void gb_pack(const Tensor& src, const Tensor& dst, Tensor out) {
+  check_i32(src, "src");
+  check_i32(dst, "dst");
+  check_t(out, at::kLong, "out");
+  TORCH_CHECK(src.numel() == dst.numel() && out.numel() >= src.numel(), "gb_pack: sizes");
+  DeviceGuard guard(src.device());
+  DALGO_CHECK_HIP(dalgo_gb_pack(src.data_ptr<int32_t>(), dst.data_ptr<int32_t>(), src.numel(),
+                                reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>()), cur_stream()),
+                  "gb_pack");
+}
+
+// packed edges partitioned on the HIGH bits of their source (bits [kb, end_bit) of src,
+// 2 radix passes at 2^26) into out, and deg[src] += the raw out-degree (one LDS histogram
+// per bucket of 2^kb sources)
+void gb_degree_packed(const Tensor& packed, int64_t end_bit, Tensor deg, Tensor out) {
+  check_t(packed, at::kLong, "packed");
+  check_t(out, at::kLong, "out");
+  check_i32(deg, "deg");
+  const int64_t n = packed.numel();
+  const int kb = dalgo_gb_bucket_bits();
+  TORCH_CHECK(end_bit > kb && end_bit <= 31 && deg.numel() >= ((int64_t)1 << end_bit) && out.numel() >= n,
+              "gb_degree_packed: sizes");
+  if (n == 0) return;
+  DeviceGuard guard(packed.device());
+  auto* in = reinterpret_cast<const uint64_t*>(packed.data_ptr<int64_t>());
+  auto* o = reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>());
+  size_t bytes = 0;
+  DALGO_CHECK_HIP(dalgo_gb_sort(nullptr, &bytes, in, o, n, 32 + kb, 32 + (int)end_bit, cur_stream()),
+                  "gb_sort(size)");
+  {
+    Tensor tmp = at::empty({(int64_t)bytes + 256}, packed.options().dtype(at::kByte));
+    DALGO_CHECK_HIP(dalgo_gb_sort(tmp.data_ptr(), &bytes, in, o, n, 32 + kb, 32 + (int)end_bit, cur_stream()),
+                    "gb_sort");
+  }
+  Tensor starts = at::empty({((int64_t)1 << (end_bit - kb)) + 1}, packed.options());
+  DALGO_CHECK_HIP(dalgo_gb_bucket_degree(o, 1, n, (int)end_bit, starts.data_ptr<int64_t>(), deg.data_ptr<int32_t>(),
+                                         cur_stream()),
+                  "gb_bucket_degree");
 }
 
 // deg[v] = occurrences of v in ids (int32, ids < 2^end_bit): one rocPRIM radix sort of the
@@ -893,7 +953,7 @@ void gb_degree_sorted(const Tensor& ids, int64_t end_bit, Tensor deg) {
     DALGO_CHECK_HIP(dalgo_gb_sort32(tmp.data_ptr(), &bytes, in, out, n, kb, (int)end_bit, cur_stream()), "gb_sort32");
   }
   Tensor starts = at::empty({((int64_t)1 << (end_bit - kb)) + 1}, ids.options().dtype(at::kLong));
-  DALGO_CHECK_HIP(dalgo_gb_bucket_degree(out, n, (int)end_bit, starts.data_ptr<int64_t>(), deg.data_ptr<int32_t>(),
+  DALGO_CHECK_HIP(dalgo_gb_bucket_degree(out, 0, n, (int)end_bit, starts.data_ptr<int64_t>(), deg.data_ptr<int32_t>(),
                                          cur_stream()),
                   "gb_bucket_degree");
 }
@@ -909,9 +969,9 @@ void gb_sort(const Tensor& keys, int64_t n, int64_t end_bit, Tensor out) {
   auto* k = reinterpret_cast<const uint64_t*>(keys.data_ptr<int64_t>());
   auto* o = reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>());
   size_t bytes = 0;
-  DALGO_CHECK_HIP(dalgo_gb_sort(nullptr, &bytes, k, o, n, (int)end_bit, cur_stream()), "gb_sort(size)");
+  DALGO_CHECK_HIP(dalgo_gb_sort(nullptr, &bytes, k, o, n, 0, (int)end_bit, cur_stream()), "gb_sort(size)");
   Tensor tmp = at::empty({(int64_t)bytes + 256}, keys.options().dtype(at::kByte));
-  DALGO_CHECK_HIP(dalgo_gb_sort(tmp.data_ptr(), &bytes, k, o, n, (int)end_bit, cur_stream()), "gb_sort");
+  DALGO_CHECK_HIP(dalgo_gb_sort(tmp.data_ptr(), &bytes, k, o, n, 0, (int)end_bit, cur_stream()), "gb_sort");
 }
 
 void gb_decode(const Tensor& K, int64_t n, int64_t shift, int64_t dbits, const Tensor& blk_base,
@@ -1567,6 +1627,9 @@ TORCH_LIBRARY(dalgo, m) {
         "int dbits, int phase, Tensor(a!)? bitmap, Tensor(b!)? counts, Tensor? offsets, int base_all, "
         "Tensor(c!)? keys, Tensor? word_prefix, Tensor? seg_start, Tensor? seg_blk0) -> ()");
   m.def("gb_sort(Tensor keys, int n, int end_bit, Tensor(a!) out) -> ()");
+  m.def("gb_keys_packed(Tensor packed, Tensor? new_id, int n_vertices, int dbits, Tensor(a!) keys) -> ()");
+  m.def("gb_pack(Tensor src, Tensor dst, Tensor(a!) out) -> ()");
+  m.def("gb_degree_packed(Tensor packed, int end_bit, Tensor(a!) deg, Tensor(b!) out) -> ()");
   m.def("gb_degree_sorted(Tensor ids, int end_bit, Tensor(a!) deg) -> ()");
   m.def("gb_decode(Tensor K, int n, int shift, int dbits, Tensor blk_base, int phase, "
         "Tensor(a!)? counts, Tensor(b!)? outdeg, Tensor? offsets, Tensor(c!)? srcl, "
@@ -1642,6 +1705,9 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("gb_degree", &gb_degree);
   m.impl("gb_keys", &gb_keys);
   m.impl("gb_sort", &gb_sort);
+  m.impl("gb_keys_packed", &gb_keys_packed);
+  m.impl("gb_pack", &gb_pack);
+  m.impl("gb_degree_packed", &gb_degree_packed);
   m.impl("gb_degree_sorted", &gb_degree_sorted);
   m.impl("gb_decode", &gb_decode);
   m.impl("gb_cell_count", &gb_cell_count);

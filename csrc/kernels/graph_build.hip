@@ -8,6 +8,8 @@
 // (a distinct edge = the last copy of its key). The passes around it are single sweeps:
 //   degree   -- raw out-degree of the input edges (degree relabeling): ids partitioned
 //               on their high bits by a 2-pass radix sort, one LDS histogram per bucket;
+//               on one rank the (src, dst) pairs themselves are partitioned (packed u64),
+//               so the key pass's source relabeling reads one 32 KB table slice per bucket;
 //   keys     -- relabel, keep this rank's destinations, map sources to the [own | ghost]
 //               index space and pack the key (two-phase compaction: count, write);
 //   decode   -- per distinct edge the u16 source offset + entry-end bit, the entry list
@@ -57,21 +59,27 @@ __global__ void __launch_bounds__(256) gb_degree_kernel(const int32_t* __restric
 // block: no global atomics)
 constexpr int kBktBits = 13;
 
-__global__ void __launch_bounds__(256) gb_bucket_starts_kernel(const uint32_t* __restrict__ sorted, int64_t n,
+// the id of an element: u32 ids as they are; u64 packed edges (src << 32 | dst): src
+__device__ __forceinline__ uint32_t gb_id(uint32_t x) { return x; }
+__device__ __forceinline__ uint32_t gb_id(uint64_t x) { return (uint32_t)(x >> 32); }
+
+template <typename E>
+__global__ void __launch_bounds__(256) gb_bucket_starts_kernel(const E* __restrict__ sorted, int64_t n,
                                                                int nb, int64_t* __restrict__ starts) {
   const int b = blockIdx.x * 256 + threadIdx.x;
   if (b > nb) return;
   if (b == nb) { starts[b] = n; return; }
-  int64_t lo = 0, hi = n;   // first i with (sorted[i] >> kBktBits) >= b
+  int64_t lo = 0, hi = n;   // first i with (id(sorted[i]) >> kBktBits) >= b
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if ((int64_t)(sorted[mid] >> kBktBits) < b) lo = mid + 1;
+    if ((int64_t)(gb_id(sorted[mid]) >> kBktBits) < b) lo = mid + 1;
     else hi = mid;
   }
   starts[b] = lo;
 }
 
-__global__ void __launch_bounds__(256) gb_bucket_degree_kernel(const uint32_t* __restrict__ sorted,
+template <typename E>
+__global__ void __launch_bounds__(256) gb_bucket_degree_kernel(const E* __restrict__ sorted,
                                                                const int64_t* __restrict__ starts,
                                                                int32_t* __restrict__ deg) {
   __shared__ uint32_t hist[1 << kBktBits];
@@ -79,22 +87,34 @@ __global__ void __launch_bounds__(256) gb_bucket_degree_kernel(const uint32_t* _
   __syncthreads();
   const int64_t b = blockIdx.x, i0 = starts[b], i1 = starts[b + 1];
   constexpr uint32_t mask = (1u << kBktBits) - 1u;
-  // 16-B loads from the first aligned position on
-  const int64_t a0 = min(i1, (i0 + 3) & ~(int64_t)3);
-  for (int64_t i = i0 + threadIdx.x; i < a0; i += 256) atomicAdd(&hist[sorted[i] & mask], 1u);
-  const int64_t nv = (i1 - a0) >> 2;
-  const uint4* v = reinterpret_cast<const uint4*>(sorted + a0);
-  for (int64_t q = threadIdx.x; q < nv; q += 256) {
-    const uint4 x = v[q];
-    atomicAdd(&hist[x.x & mask], 1u);
-    atomicAdd(&hist[x.y & mask], 1u);
-    atomicAdd(&hist[x.z & mask], 1u);
-    atomicAdd(&hist[x.w & mask], 1u);
+  if constexpr (sizeof(E) == 4) {
+    // 16-B loads from the first aligned position on
+    const int64_t a0 = min(i1, (i0 + 3) & ~(int64_t)3);
+    for (int64_t i = i0 + threadIdx.x; i < a0; i += 256) atomicAdd(&hist[gb_id(sorted[i]) & mask], 1u);
+    const int64_t nv = (i1 - a0) >> 2;
+    const uint4* v = reinterpret_cast<const uint4*>(sorted + a0);
+    for (int64_t q = threadIdx.x; q < nv; q += 256) {
+      const uint4 x = v[q];
+      atomicAdd(&hist[x.x & mask], 1u);
+      atomicAdd(&hist[x.y & mask], 1u);
+      atomicAdd(&hist[x.z & mask], 1u);
+      atomicAdd(&hist[x.w & mask], 1u);
+    }
+    for (int64_t i = a0 + (nv << 2) + threadIdx.x; i < i1; i += 256) atomicAdd(&hist[gb_id(sorted[i]) & mask], 1u);
+  } else {
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) atomicAdd(&hist[gb_id(sorted[i]) & mask], 1u);
   }
-  for (int64_t i = a0 + (nv << 2) + threadIdx.x; i < i1; i += 256) atomicAdd(&hist[sorted[i] & mask], 1u);
   __syncthreads();
   int32_t* d = deg + (b << kBktBits);
   for (int j = threadIdx.x; j < (1 << kBktBits); j += 256) d[j] += (int32_t)hist[j];
+}
+
+// packed edges: out[i] = src[i] << 32 | dst[i]
+__global__ void __launch_bounds__(256) gb_pack_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                                      int64_t n, uint64_t* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+    out[i] = ((uint64_t)(uint32_t)src[i] << 32) | (uint64_t)(uint32_t)dst[i];
 }
 
 // ---------------------------------------------------------------------------- keys
@@ -115,10 +135,12 @@ struct GbKeyCtx {
 
 __device__ __forceinline__ bool gb_edge(const GbKeyCtx& c, int32_t s0, int32_t d0, int32_t& s,
                                         int64_t& dl) {
-  s = c.new_id ? c.new_id[s0] : s0;
   const int32_t d = c.new_id ? c.new_id[d0] : d0;
   dl = (int64_t)d - c.v_lo;
-  return d >= c.v_lo && d < c.v_hi;
+  const bool keep = d >= c.v_lo && d < c.v_hi;
+  // (one rank: every edge is kept; several: the source is relabelled only where kept)
+  s = c.new_id && (c.world == 1 || keep) ? c.new_id[s0] : s0;
+  return keep;
 }
 
 __device__ __forceinline__ uint64_t gb_key(const GbKeyCtx& c, int32_t s, int64_t dl) {
@@ -143,7 +165,17 @@ constexpr int kKeyV = 4;             // edges per thread per step (int4 loads, 8
 
 __device__ __forceinline__ void gb_load4(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
                                          int64_t i, int64_t r1, int32_t (&s)[kKeyV], int32_t (&d)[kKeyV],
-                                         bool (&in)[kKeyV]) {
+                                         bool (&in)[kKeyV], const uint64_t* __restrict__ packed = nullptr) {
+  if (packed != nullptr) {   // (src << 32 | dst) words
+#pragma unroll
+    for (int v = 0; v < kKeyV; ++v) {
+      in[v] = i + v < r1;
+      const uint64_t w = in[v] ? packed[i + v] : 0ull;
+      s[v] = (int32_t)(w >> 32);
+      d[v] = (int32_t)(uint32_t)w;
+    }
+    return;
+  }
   if (i + kKeyV <= r1) {
     const int4 a = *reinterpret_cast<const int4*>(src + i);
     const int4 b = *reinterpret_cast<const int4*>(dst + i);
@@ -196,7 +228,8 @@ __global__ void __launch_bounds__(256) gb_keys_count_kernel(const int32_t* __res
 __global__ void __launch_bounds__(256) gb_keys_write_kernel(const int32_t* __restrict__ src,
                                                             const int32_t* __restrict__ dst, int64_t n,
                                                             GbKeyCtx c, const int64_t* __restrict__ offsets,
-                                                            int64_t base_all, uint64_t* __restrict__ keys) {
+                                                            int64_t base_all, uint64_t* __restrict__ keys,
+                                                            const uint64_t* __restrict__ packed) {
   __shared__ int s_cur;
   if (threadIdx.x == 0) s_cur = 0;
   __syncthreads();
@@ -209,7 +242,7 @@ __global__ void __launch_bounds__(256) gb_keys_write_kernel(const int32_t* __res
     int32_t s0[kKeyV], d0[kKeyV], sv[kKeyV];
     int64_t dl[kKeyV];
     bool in[kKeyV], keep[kKeyV];
-    gb_load4(src, dst, i, r1, s0, d0, in);
+    gb_load4(src, dst, i, r1, s0, d0, in, packed);
     int cnt = 0;
 #pragma unroll
     for (int v = 0; v < kKeyV; ++v) {
@@ -618,16 +651,24 @@ int dalgo_gb_bucket_bits() { return kBktBits; }
 
 // ids sorted on bits [kBktBits, end_bit): deg[v] += occurrences of v (ids < 2^end_bit);
 // starts: int64[2^(end_bit - kBktBits) + 1] workspace
-hipError_t dalgo_gb_bucket_degree(const uint32_t* sorted, int64_t n, int end_bit, int64_t* starts, int32_t* deg,
-                                  hipStream_t st) {
+hipError_t dalgo_gb_bucket_degree(const void* sorted, int packed, int64_t n, int end_bit, int64_t* starts,
+                                  int32_t* deg, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   if (end_bit <= kBktBits || end_bit > 31 || n >= (int64_t)0x7fffffffLL) return hipErrorInvalidValue;
   const int nb = 1 << (end_bit - kBktBits);
-  hipLaunchKernelGGL(gb_bucket_starts_kernel, dim3((unsigned)cdiv(nb + 1, 256)), dim3(256), 0, st, sorted, n, nb,
-                     starts);
-  DALGO_LAUNCH_CHECK();
-  hipLaunchKernelGGL(gb_bucket_degree_kernel, dim3((unsigned)nb), dim3(256), 0, st, sorted,
-                     (const int64_t*)starts, deg);
+  if (packed) {
+    hipLaunchKernelGGL(gb_bucket_starts_kernel<uint64_t>, dim3((unsigned)cdiv(nb + 1, 256)), dim3(256), 0, st,
+                       (const uint64_t*)sorted, n, nb, starts);
+    DALGO_LAUNCH_CHECK();
+    hipLaunchKernelGGL(gb_bucket_degree_kernel<uint64_t>, dim3((unsigned)nb), dim3(256), 0, st,
+                       (const uint64_t*)sorted, (const int64_t*)starts, deg);
+  } else {
+    hipLaunchKernelGGL(gb_bucket_starts_kernel<uint32_t>, dim3((unsigned)cdiv(nb + 1, 256)), dim3(256), 0, st,
+                       (const uint32_t*)sorted, n, nb, starts);
+    DALGO_LAUNCH_CHECK();
+    hipLaunchKernelGGL(gb_bucket_degree_kernel<uint32_t>, dim3((unsigned)nb), dim3(256), 0, st,
+                       (const uint32_t*)sorted, (const int64_t*)starts, deg);
+  }
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -636,7 +677,7 @@ int64_t dalgo_gb_key_blocks(int64_t n) { return cdiv(n, (int64_t)kKeyR); }
 
 hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, const DalgoGbKeyArgs* a,
                          int phase, uint32_t* bitmap, int32_t* counts, const int64_t* offsets,
-                         int64_t base_all, uint64_t* keys, hipStream_t st) {
+                         int64_t base_all, uint64_t* keys, const uint64_t* packed, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   if (a->dbits < 0 || a->dbits > 31 || a->world < 1) return hipErrorInvalidValue;
   GbKeyCtx c{a->v_lo, a->v_hi, a->sl, a->world, a->rank, a->dbits, a->new_id, a->bitmap,
@@ -645,20 +686,29 @@ hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, cons
     return hipErrorInvalidValue;
   const int64_t g = cdiv(n, (int64_t)kKeyR);
   if (g > 0x7fffffffLL) return hipErrorInvalidValue;
+  if (packed != nullptr && (phase == 0 || c.world > 1)) return hipErrorInvalidValue;   // one rank only
   if (phase == 0)
     hipLaunchKernelGGL(gb_keys_count_kernel, dim3((unsigned)g), dim3(256), 0, st, src, dst, n, c, bitmap, counts);
   else
     hipLaunchKernelGGL(gb_keys_write_kernel, dim3((unsigned)g), dim3(256), 0, st, src, dst, n, c, offsets,
-                       base_all, keys);
+                       base_all, keys, packed);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }
 
 // rocPRIM onesweep radix sort of n u64 keys over bits [0, end_bit); tmp == nullptr: query
 hipError_t dalgo_gb_sort(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
-                         int end_bit, hipStream_t st) {
-  if (n < 0 || end_bit < 1 || end_bit > 64) return hipErrorInvalidValue;
-  return rocprim::radix_sort_keys(tmp, *tmp_bytes, in, out, (size_t)n, 0u, (unsigned)end_bit, st);
+                         int begin_bit, int end_bit, hipStream_t st) {
+  if (n < 0 || end_bit < 1 || end_bit > 64 || begin_bit < 0 || begin_bit >= end_bit) return hipErrorInvalidValue;
+  return rocprim::radix_sort_keys(tmp, *tmp_bytes, in, out, (size_t)n, (unsigned)begin_bit, (unsigned)end_bit, st);
+}
+
+hipError_t dalgo_gb_pack(const int32_t* src, const int32_t* dst, int64_t n, uint64_t* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t g = std::min<int64_t>(cdiv(n, 256), 256 * 64);
+  hipLaunchKernelGGL(gb_pack_kernel, dim3((unsigned)g), dim3(256), 0, st, src, dst, n, out);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
 }
 
 int64_t dalgo_gb_decode_blocks(int64_t n) { return cdiv(n, (int64_t)kDecR); }

@@ -219,14 +219,15 @@ hipError_t dalgo_gb_degree(const int32_t* ids, int64_t n, uint32_t* deg, hipStre
 hipError_t dalgo_gb_sort32(void* tmp, size_t* tmp_bytes, const uint32_t* in, uint32_t* out, int64_t n,
                            int begin_bit, int end_bit, hipStream_t st);
 int dalgo_gb_bucket_bits();
-hipError_t dalgo_gb_bucket_degree(const uint32_t* sorted, int64_t n, int end_bit, int64_t* starts, int32_t* deg,
-                                  hipStream_t st);
+hipError_t dalgo_gb_bucket_degree(const void* sorted, int packed, int64_t n, int end_bit, int64_t* starts,
+                                  int32_t* deg, hipStream_t st);
+hipError_t dalgo_gb_pack(const int32_t* src, const int32_t* dst, int64_t n, uint64_t* out, hipStream_t st);
 int64_t dalgo_gb_key_blocks(int64_t n);
 hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, const DalgoGbKeyArgs* a,
                          int phase, uint32_t* bitmap, int32_t* counts, const int64_t* offsets,
-                         int64_t base_all, uint64_t* keys, hipStream_t st);
+                         int64_t base_all, uint64_t* keys, const uint64_t* packed, hipStream_t st);
 hipError_t dalgo_gb_sort(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
-                         int end_bit, hipStream_t st);
+                         int begin_bit, int end_bit, hipStream_t st);
 int64_t dalgo_gb_decode_blocks(int64_t n);
 hipError_t dalgo_gb_decode(const uint64_t* K, int64_t n, int shift, int dbits, const int64_t* blk_base,
                            int phase, int64_t* counts, uint32_t* outdeg, const int64_t* offsets,

@@ -151,12 +151,24 @@ def build_rmat_native(edges: list, scale: int, rank: int, world: int, device, re
                       keep_keys: bool = False, bin_width: int = 16384, tile: int = 16384):
     """This rank's K4b-ready adjacency of the given R-MAT edge chunks, built natively
     (dalgo.ops.graph.build_native): degree relabeling, destination filter, dedup and the
-    blocked layout without the (dst, src)-sorted intermediate shard."""
+    blocked layout without the (dst, src)-sorted intermediate shard. One rank with
+    relabeling: the (src, dst) pairs are packed and partitioned on the high source bits
+    first (the degree count's own partition), so the key pass relabels the sources from a
+    32 KB slice of the table per bucket instead of at random."""
     G._mark("start")
-    new_id = degree_order_from(edges, scale, rank, world, device) if reorder else None
+    packed = None
+    if reorder and world == 1 and torch.device(device).type == "cuda" and scale > G.BUCKET_BITS:
+        packed, deg = G.partition_edges(edges, scale)
+        G._mark("degree_count")
+        order = rank_by_degree(deg)
+        G._mark("degree_rank")
+        new_id = deal_ids(order, 1 << scale, 1).to(torch.int32)
+        del deg, order
+    else:
+        new_id = degree_order_from(edges, scale, rank, world, device) if reorder else None
     G._mark("deal_ids")
     return G.build_native(edges, 1 << scale, rank, world, new_id, bin_width=bin_width, tile=tile,
-                          keep_keys=keep_keys)
+                          keep_keys=keep_keys, packed=packed)
 
 
 def rmat_shard(scale: int, edge_factor: int, rank: int, world: int, device, seed: int = 1,

@@ -135,6 +135,28 @@ def degree_count_(deg: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
     return deg
 
 
+BUCKET_BITS = 13          # ids per degree bucket: 2^13 (graph_build.hip kBktBits)
+
+
+def partition_edges(edges: list, bits: int):
+    """One rank: every (src, dst) edge packed as src << 32 | dst and partitioned on the high
+    source bits (2 radix passes at 2^26 ids), plus the raw out-degree of every source
+    (ids < 2^bits, bits > BUCKET_BITS): (packed int64 [E], deg int32 [2^bits])."""
+    ops = _ext.ops()
+    dev = edges[0][0].device
+    n = sum(int(s.numel()) for s, _ in edges)
+    packed = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    o = 0
+    for s, d in edges:
+        ops.gb_pack(s, d, packed[o:o + s.numel()])
+        o += int(s.numel())
+    out = torch.empty_like(packed)
+    deg = torch.zeros(1 << bits, dtype=torch.int32, device=dev)
+    ops.gb_degree_packed(packed[:n], int(bits), deg, out)
+    del packed
+    return out[:n], deg
+
+
 def degree_sorted_(deg: torch.Tensor, ids: torch.Tensor, bits: int) -> torch.Tensor:
     """deg[v] += #occurrences of v in ids (GPU int32, ids < 2^bits): the ids partitioned
     on their high bits (2 radix passes at 2^26 ids), then one LDS histogram per bucket of
@@ -495,7 +517,8 @@ def build_phase_spans() -> dict:
 
 def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: torch.Tensor | None = None,
                  bin_width: int = 16384, tile: int = 16384, items: int = 2048,
-                 min_piece: int = 1 << 14, keep_keys: bool = False) -> NativeGraph:
+                 min_piece: int = 1 << 14, keep_keys: bool = False,
+                 packed: torch.Tensor | None = None) -> NativeGraph:
     """``distinct().groupByKey()`` of graph_computation/pagerank.py:41 straight into the
     K4b layout, on the device (csrc/kernels/graph_build.hip): relabel + keep this rank's
     destinations + pack one (block, destination, source offset) key per edge, ONE radix
@@ -503,7 +526,9 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     the entries and their runs / tiles. Same layout as :func:`build_blocked` over the
     (dst, src)-sorted shard (chunks = whole 8192-source blocks, no edge cut).
 
-    edges: list of (src, dst) int32 GPU chunks of GLOBAL ids (before ``new_id``)."""
+    edges: list of (src, dst) int32 GPU chunks of GLOBAL ids (before ``new_id``).
+    packed (one rank): the same edges as (src << 32 | dst) int64 words in any order
+    (:func:`partition_edges`: partitioned on the source), read instead of ``edges``."""
     if bin_width not in (8192, 16384):
         raise ValueError("bin_width must be 8192 or 16384")
     ops = _ext.ops()
@@ -576,8 +601,16 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     _mark("segments")
     # ---- phase 1: keys
     keys = torch.empty(max(total, 1), **i64)
+    from_packed = packed is not None
+    if from_packed:
+        if W != 1 or packed.numel() != total:
+            raise ValueError("build_native: packed edges are the one-rank path over every edge")
+        ops.gb_keys_packed(packed, nid, N, dbits, keys)
+        del packed
     o, base_all = 0, 0
     for (s, d), nb in zip(edges, nbs):
+        if from_packed:
+            break
         ops.gb_keys(s, d, nid, v_lo, v_hi, sl, W, rank, dbits, 1, bitmap, None,
                     offsets[o:o + nb] if offsets is not None else None, base_all, keys,
                     word_prefix, st, sb)
