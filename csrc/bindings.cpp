@@ -974,6 +974,9 @@ void gb_sort(const Tensor& keys, int64_t n, int64_t end_bit, Tensor out) {
   DALGO_CHECK_HIP(dalgo_gb_sort(tmp.data_ptr(), &bytes, k, o, n, 0, (int)end_bit, cur_stream()), "gb_sort");
 }
 
+// blocks of the decode kernels over n sorted keys (size of their counts / offsets tables)
+int64_t gb_decode_blocks(int64_t n) { return dalgo_gb_decode_blocks(n); }
+
 void gb_decode(const Tensor& K, int64_t n, int64_t shift, int64_t dbits, const Tensor& blk_base,
                int64_t phase, const std::optional<Tensor>& counts, const std::optional<Tensor>& outdeg,
                const std::optional<Tensor>& offsets, const std::optional<Tensor>& srcl,
@@ -1631,6 +1634,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("gb_pack(Tensor src, Tensor dst, Tensor(a!) out) -> ()");
   m.def("gb_degree_packed(Tensor packed, int end_bit, Tensor(a!) deg, Tensor(b!) out) -> ()");
   m.def("gb_degree_sorted(Tensor ids, int end_bit, Tensor(a!) deg) -> ()");
+  m.def("gb_decode_blocks(int n) -> int", &gb_decode_blocks);   // no tensors: catch-all kernel
   m.def("gb_decode(Tensor K, int n, int shift, int dbits, Tensor blk_base, int phase, "
         "Tensor(a!)? counts, Tensor(b!)? outdeg, Tensor? offsets, Tensor(c!)? srcl, "
         "Tensor(d!)? ent_end, Tensor(e!)? ent_blk, Tensor(f!)? ent_dst) -> ()");

@@ -166,13 +166,23 @@ constexpr int kKeyV = 4;             // edges per thread per step (int4 loads, 8
 __device__ __forceinline__ void gb_load4(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
                                          int64_t i, int64_t r1, int32_t (&s)[kKeyV], int32_t (&d)[kKeyV],
                                          bool (&in)[kKeyV], const uint64_t* __restrict__ packed = nullptr) {
-  if (packed != nullptr) {   // (src << 32 | dst) words
+  if (packed != nullptr) {   // (src << 32 | dst) words: two 16-B loads per 4 edges
+    static_assert(kKeyV == 4, "packed loads assume 4 edges per step");
+    if (i + kKeyV <= r1) {
+      const uint4 a = *reinterpret_cast<const uint4*>(packed + i);
+      const uint4 b = *reinterpret_cast<const uint4*>(packed + i + 2);
+      d[0] = (int32_t)a.x; s[0] = (int32_t)a.y; d[1] = (int32_t)a.z; s[1] = (int32_t)a.w;
+      d[2] = (int32_t)b.x; s[2] = (int32_t)b.y; d[3] = (int32_t)b.z; s[3] = (int32_t)b.w;
 #pragma unroll
-    for (int v = 0; v < kKeyV; ++v) {
-      in[v] = i + v < r1;
-      const uint64_t w = in[v] ? packed[i + v] : 0ull;
-      s[v] = (int32_t)(w >> 32);
-      d[v] = (int32_t)(uint32_t)w;
+      for (int v = 0; v < kKeyV; ++v) in[v] = true;
+    } else {
+#pragma unroll
+      for (int v = 0; v < kKeyV; ++v) {
+        in[v] = i + v < r1;
+        const uint64_t w = in[v] ? packed[i + v] : 0ull;
+        s[v] = (int32_t)(w >> 32);
+        d[v] = (int32_t)(uint32_t)w;
+      }
     }
     return;
   }
@@ -271,7 +281,8 @@ __global__ void __launch_bounds__(256) gb_keys_write_kernel(const int32_t* __res
 // ends at the last copy of its last key. Blocks of kDecR keys, each thread 4 consecutive
 // keys per step (coalesced), one block scan per step places the distinct edges and the
 // entries in key order.
-constexpr int kDecR = 65536;         // keys per block of the decode kernels
+constexpr int kDecR = 65536;         // keys per block of the decode kernels (262144: 13.0 ->
+                                     // 14.3 ms at scale 26, profiles/round5/r5_21)
 constexpr int kDecT = 256;
 constexpr int kDecV = 4;             // keys per thread per step
 

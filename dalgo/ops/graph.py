@@ -632,7 +632,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
                            K if keep_keys else None, 0, shift, dbits, blk_base, new_id)
     # ---- decode (dedup folded in): per distinct edge the source offset + entry-end bit,
     # the entries, the distinct out-degrees
-    nbd = (total + 65535) // 65536                     # graph_build.hip kDecR
+    nbd = int(ops.gb_decode_blocks(total))            # graph_build.hip kDecR keys per block
     counts = torch.empty(2 * nbd, **i64)
     ops.gb_decode(K, total, shift, dbits, blk_base, 0, counts, outdeg_loc, None, None, None, None, None)
     offsets = torch.cumsum(counts.view(nbd, 2), 0) - counts.view(nbd, 2)
