@@ -1988,6 +1988,8 @@ static hipError_t launch_assign16(const void* X, int64_t n, int64_t ldx, const v
                                   const float* hn, int kpad, int* assign, float* mind, double* sse,
                                   int sse_mask, float* xh, unsigned* xmax, hipStream_t st,
                                   const int32_t* idx = nullptr, const KmAux& aux = KmAux{}) {
+  // (one 8-wave block per CU -- half the centre-chunk traffic per point -- measured 2 %
+  // slower: 20.5-20.7 vs 20.1-20.2 ms on one box, profiles/round5/r5_22)
   constexpr int NW = 4, PG = 6, MINB = 2;
   if (!assign16_fits(kpad, BND)) return hipErrorInvalidValue;
   if (BND && (idx == nullptr || aux.mcount == nullptr || aux.tol == nullptr || aux.ul == nullptr ||
