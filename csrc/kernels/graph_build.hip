@@ -295,6 +295,37 @@ __device__ __forceinline__ void gb_flags(const uint64_t* __restrict__ K, int64_t
   end = last && (!has_next || (kn >> kSpanBits) != (k >> kSpanBits));
 }
 
+// keys ib .. ib + 3 (ib % 4 == 0, < r1 each or flagged out) and their flags: two 16-B loads
+// and one 8-B load of the following key instead of eight 8-B loads
+__device__ __forceinline__ void gb_flags4(const uint64_t* __restrict__ K, int64_t n, int64_t ib, int64_t r1,
+                                          bool (&last)[kDecV], bool (&end)[kDecV], uint64_t (&k)[kDecV]) {
+  static_assert(kDecV == 4, "4 keys per thread per step");
+  if (ib + kDecV <= r1) {
+    const uint4 a = *reinterpret_cast<const uint4*>(K + ib);
+    const uint4 b = *reinterpret_cast<const uint4*>(K + ib + 2);
+    k[0] = ((uint64_t)a.y << 32) | a.x;
+    k[1] = ((uint64_t)a.w << 32) | a.z;
+    k[2] = ((uint64_t)b.y << 32) | b.x;
+    k[3] = ((uint64_t)b.w << 32) | b.z;
+    const bool has_next = ib + kDecV < n;
+    const uint64_t kn = has_next ? K[ib + kDecV] : ~0ull;
+#pragma unroll
+    for (int v = 0; v < kDecV; ++v) {
+      const uint64_t nx = v + 1 < kDecV ? k[v + 1] : kn;
+      const bool hn = v + 1 < kDecV || has_next;
+      last[v] = !hn || nx != k[v];
+      end[v] = last[v] && (!hn || (nx >> kSpanBits) != (k[v] >> kSpanBits));
+    }
+  } else {
+#pragma unroll
+    for (int v = 0; v < kDecV; ++v) {
+      last[v] = end[v] = false;
+      k[v] = 0;
+      if (ib + v < r1) gb_flags(K, n, ib + v, last[v], end[v], k[v]);
+    }
+  }
+}
+
 // per block: distinct edges, entries, and the distinct out-degree per local source (LDS
 // histogram of the block's first source block; other source blocks: global atomics)
 __global__ void __launch_bounds__(kDecT) gb_decode_count_kernel(const uint64_t* __restrict__ K, int64_t n,
@@ -310,18 +341,21 @@ __global__ void __launch_bounds__(kDecT) gb_decode_count_kernel(const uint64_t* 
   const int64_t r1 = r0 + kDecR < n ? r0 + kDecR : n;
   const uint64_t blk0 = K[r0] >> shift;
   int md = 0, me = 0;
-  for (int64_t i = r0 + threadIdx.x; i < r1; i += kDecT) {
-    bool last, end;
-    uint64_t k;
-    gb_flags(K, n, i, last, end, k);
-    if (last) {
-      ++md;
-      const uint64_t blk = k >> shift;
-      const uint32_t off = (uint32_t)(k & (kSpan - 1));
-      if (blk == blk0) atomicAdd(hist + off, 1u);
-      else atomicAdd(outdeg + blk_base[blk] + off, 1u);
+  for (int64_t ib = r0 + (int64_t)threadIdx.x * kDecV; ib < r1; ib += (int64_t)kDecT * kDecV) {
+    bool last[kDecV], end[kDecV];
+    uint64_t k[kDecV];
+    gb_flags4(K, n, ib, r1, last, end, k);
+#pragma unroll
+    for (int v = 0; v < kDecV; ++v) {
+      if (last[v]) {
+        ++md;
+        const uint64_t blk = k[v] >> shift;
+        const uint32_t off = (uint32_t)(k[v] & (kSpan - 1));
+        if (blk == blk0) atomicAdd(hist + off, 1u);
+        else atomicAdd(outdeg + blk_base[blk] + off, 1u);
+      }
+      me += end[v] ? 1 : 0;
     }
-    me += end ? 1 : 0;
   }
   atomicAdd(&s_d, md);
   atomicAdd(&s_e, me);
@@ -354,11 +388,9 @@ __global__ void __launch_bounds__(kDecT) gb_decode_write_kernel(const uint64_t* 
     bool last[kDecV], end[kDecV];
     uint64_t k[kDecV];
     int cd = 0, ce = 0;
+    gb_flags4(K, n, ib, r1, last, end, k);
 #pragma unroll
     for (int v = 0; v < kDecV; ++v) {
-      last[v] = end[v] = false;
-      k[v] = 0;
-      if (ib + v < r1) gb_flags(K, n, ib + v, last[v], end[v], k[v]);
       cd += last[v] ? 1 : 0;
       ce += end[v] ? 1 : 0;
     }

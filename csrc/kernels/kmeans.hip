@@ -1788,10 +1788,17 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
       const int k1 = (__float_as_int(ac[g][1]) & kmask) | (sub * 4 + 1);
       const int k2 = (__float_as_int(ac[g][2]) & kmask) | (sub * 4 + 2);
       const int k3 = (__float_as_int(ac[g][3]) & kmask) | (sub * 4 + 3);
-      if constexpr (BND) cm2[g] = min(cm2[g], med3(cm[g], k0, k1));
-      cm[g] = min(min(cm[g], k0), k1);
-      if constexpr (BND) cm2[g] = min(cm2[g], med3(cm[g], k2, k3));
-      cm[g] = min(min(cm[g], k2), k3);
+      if constexpr (BND) {
+        // second smallest of {cm, cm2, k0..k3}: min3(cm2, med3(cm, k0, k1), med3(cm', k2, k3))
+        const int md1 = med3(cm[g], k0, k1);
+        cm[g] = min(min(cm[g], k0), k1);
+        const int md2 = med3(cm[g], k2, k3);
+        cm[g] = min(min(cm[g], k2), k3);
+        cm2[g] = min(min(cm2[g], md1), md2);
+      } else {
+        cm[g] = min(min(cm[g], k0), k1);
+        cm[g] = min(min(cm[g], k2), k3);
+      }
     }
   };
   // chunk merge: across chunks on the value bits only (strict: the earlier chunk keeps a

@@ -733,8 +733,10 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
                            ce_lo, tlen, wu_e, bin_width - 1, dloc, ts)
         del run_of_ent, cs, ent_dst, ent_blk
     assert nruns < (1 << 31)
+    _mark("entry_place")
     tile_ent = torch.nonzero(ts).flatten()
     del ts
+    _mark("tile_select")
     e_start_t = torch.where(tile_ent > 0, ent_end[(tile_ent - 1).clamp_min(0)] + 1, torch.zeros_like(tile_ent))
     del ent_end
     tile_e = torch.cat([e_start_t, torch.tensor([E], **i64)])
@@ -754,6 +756,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     _mark("tiles")
     # ---- phase-2 work items (as build_blocked)
     (wb, wl, slab_h, sp_bin, sp_first, sp_cnt), nslab = _work_items(bin_cnt, bin_lo, nent, items, min_piece)
+    _mark("work_split")
     it = lambda x: torch.tensor(x, **i32)
     c32 = lambda x: x.to(torch.int32).contiguous()
     splits = sorted({int(x) for x in seg_start if x > 0})
