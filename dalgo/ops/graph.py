@@ -174,27 +174,32 @@ def local_outdeg(shard: GraphShard) -> torch.Tensor:
 def _work_items(bin_cnt: torch.Tensor, bin_lo: torch.Tensor, nent: int, items: int, min_piece: int):
     """Phase-2 work items: each bin's contiguous bin-major entry range, a hot bin cut into
     ~cap-entry pieces (each with its own slab, combined in order afterwards); an empty
-    bin is one empty item (it writes zeros). Vectorised over the bins (numpy, one host
-    copy). Returns (wi_bin, wi_lo + [nent], wi_slab, split_bin, split_first, split_count)
-    as int arrays and the slab count."""
+    bin is one empty item (it writes zeros). Computed where the bin counts live (torch,
+    on the device for a GPU build: only the item and slab counts come to the host -- a
+    first 64 KB device-to-host read of the counts cost 7-17 ms in a fresh process,
+    profiles/round5/r5_24, r5_25). Returns (wi_bin, wi_lo + [nent], wi_slab, split_bin,
+    split_first, split_count) as int64 tensors and the slab count."""
     cap = max(int(nent // max(items, 1)), min_piece)
-    both = torch.stack([bin_cnt.to(torch.int64), bin_lo.to(torch.int64)]).cpu().numpy()
-    cnt, lo = both[0], both[1]
-    pieces = np.maximum(1, -(-cnt // cap))
-    step = np.maximum(1, -(-cnt // pieces))
-    ncut = np.where(cnt == 0, 1, -(-cnt // step))             # len(range(lo, lo + cnt, step))
-    nb = cnt.shape[0]
-    first = np.cumsum(ncut) - ncut
-    wb = np.repeat(np.arange(nb, dtype=np.int64), ncut)
-    k = np.arange(int(ncut.sum()), dtype=np.int64) - np.repeat(first, ncut)
-    wl = np.repeat(lo, ncut) + k * np.repeat(np.where(cnt == 0, 0, step), ncut)
+    cnt, lo = bin_cnt.to(torch.int64), bin_lo.to(torch.int64)
+    dev = cnt.device
+    pieces = torch.clamp((cnt + cap - 1) // cap, min=1)
+    step = torch.clamp((cnt + pieces - 1) // pieces, min=1)
+    ncut = torch.where(cnt == 0, torch.ones_like(cnt), (cnt + step - 1) // step)   # len(range(lo, lo + cnt, step))
     split = pieces > 1
-    sp_bin = np.nonzero(split)[0]
+    total, nslab = (int(x) for x in torch.stack([ncut.sum(), torch.where(split, ncut, 0).sum()]).tolist())
+    nb = cnt.numel()
+    rep = lambda x: torch.repeat_interleave(x, ncut, output_size=total)
+    wb = rep(torch.arange(nb, device=dev, dtype=torch.int64))
+    first = torch.cumsum(ncut, 0) - ncut
+    k = torch.arange(total, device=dev, dtype=torch.int64) - rep(first)
+    wl = rep(lo) + k * rep(torch.where(cnt == 0, torch.zeros_like(step), step))
+    in_split = rep(split)
+    slab = torch.where(in_split, torch.cumsum(in_split, 0) - 1, torch.full_like(wb, -1))
+    sp_bin = torch.nonzero(split).flatten()
     sp_cnt = ncut[split]
-    sp_first = np.cumsum(sp_cnt) - sp_cnt
-    in_split = np.repeat(split, ncut)
-    slab = np.where(in_split, np.cumsum(in_split) - 1, -1)
-    return (wb, np.append(wl, nent), slab, sp_bin, sp_first, sp_cnt), int(sp_cnt.sum())
+    sp_first = torch.cumsum(sp_cnt, 0) - sp_cnt
+    wl = torch.cat([wl, torch.full((1,), nent, dtype=torch.int64, device=dev)])
+    return (wb, wl, slab, sp_bin, sp_first, sp_cnt), nslab
 
 
 # ------------------------------------------------------------------ propagation blocking
@@ -414,9 +419,9 @@ def build_blocked(shard: GraphShard, bin_width: int = 16384, chunk_edges: int = 
                          i32(wu_tile), i32(wu_chunk), i32(slo),
                          i32(ns), i32(chunk_run), i32(run_delta),
                          torch.zeros(n4, dtype=torch.float32, device=dev), dloc,
-                         it(wb), torch.tensor(wl, dtype=torch.int64, device=dev), it(slab_h),
+                         i32(wb), i64(wl), i32(slab_h),
                          torch.zeros(max(nslab, 1) * bin_width, dtype=torch.int64, device=dev),
-                         it(sp_bin), it(sp_first), it(sp_cnt), bin_width, nl, nch, nent, n_src,
+                         i32(sp_bin), i32(sp_first), i32(sp_cnt), bin_width, nl, nch, nent, n_src,
                          max_indeg, int((chunk_run[1:] - chunk_run[:-1]).max().item()),
                          torch.zeros(1, dtype=torch.float64, device=dev),
                          int((slo[wu_chunk] < src_split).sum().item()) if src_split is not None else 0,
@@ -763,9 +768,9 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     lay = BlockedLayout(srcl, tile_e.contiguous(), c32(tile_ent), c32(tile_run), c32(chunk_tile),
                         c32(wu_tile), c32(wu_chunk), c32(slo), c32(ns), c32(chunk_run), c32(run_delta),
                         torch.zeros(n4, dtype=torch.float32, device=dev), dloc,
-                        it(wb), torch.tensor(wl, **i64), it(slab_h),
+                        c32(wb), wl.to(device=dev).contiguous(), c32(slab_h),
                         torch.zeros(max(nslab, 1) * bin_width, **i64),
-                        it(sp_bin), it(sp_first), it(sp_cnt), bin_width, nl, nch, nent, n_src,
+                        c32(sp_bin), c32(sp_first), c32(sp_cnt), bin_width, nl, nch, nent, n_src,
                         0, max_runs, torch.zeros(1, dtype=torch.float64, device=dev),
                         int((slo[wu_chunk] < sl).sum().item()) if W > 1 else 0,
                         tuple(int((slo[wu_chunk] < b).sum().item()) for b in splits))
