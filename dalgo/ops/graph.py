@@ -187,13 +187,14 @@ def _work_items(bin_cnt: torch.Tensor, bin_lo: torch.Tensor, nent: int, items: i
     ncut = torch.where(cnt == 0, torch.ones_like(cnt), (cnt + step - 1) // step)   # len(range(lo, lo + cnt, step))
     split = pieces > 1
     total, nslab = (int(x) for x in torch.stack([ncut.sum(), torch.where(split, ncut, 0).sum()]).tolist())
-    nb = cnt.numel()
-    rep = lambda x: torch.repeat_interleave(x, ncut, output_size=total)
-    wb = rep(torch.arange(nb, device=dev, dtype=torch.int64))
-    first = torch.cumsum(ncut, 0) - ncut
-    k = torch.arange(total, device=dev, dtype=torch.int64) - rep(first)
-    wl = rep(lo) + k * rep(torch.where(cnt == 0, torch.zeros_like(step), step))
-    in_split = rep(split)
+    # item j belongs to bin wb[j] (a search over the inclusive item counts: torch's
+    # repeat_interleave cost ~2 ms of host time per call here, profiles/round5/r5_27)
+    ends = torch.cumsum(ncut, 0)
+    j = torch.arange(total, device=dev, dtype=torch.int64)
+    wb = torch.searchsorted(ends, j, right=True)
+    k = j - (ends - ncut)[wb]
+    wl = lo[wb] + k * torch.where(cnt == 0, torch.zeros_like(step), step)[wb]
+    in_split = split[wb]
     slab = torch.where(in_split, torch.cumsum(in_split, 0) - 1, torch.full_like(wb, -1))
     sp_bin = torch.nonzero(split).flatten()
     sp_cnt = ncut[split]
