@@ -958,20 +958,23 @@ void gb_degree_sorted(const Tensor& ids, int64_t end_bit, Tensor deg) {
                   "gb_bucket_degree");
 }
 
-// sort keys[:n] over bits [0, end_bit) into out[:n] (rocPRIM onesweep radix sort)
-void gb_sort(const Tensor& keys, int64_t n, int64_t end_bit, Tensor out) {
+// sort keys[:n] over bits [begin_bit, end_bit) into out[:n] (rocPRIM onesweep radix sort,
+// stable: keys equal on those bits keep their input order)
+void gb_sort(const Tensor& keys, int64_t n, int64_t end_bit, Tensor out, int64_t begin_bit) {
   check_t(keys, at::kLong, "keys");
   check_t(out, at::kLong, "out");
   TORCH_CHECK(n >= 0 && n <= keys.numel() && n <= out.numel(), "gb_sort: sizes");
-  TORCH_CHECK(end_bit >= 1 && end_bit <= 64, "gb_sort: end_bit");
+  TORCH_CHECK(end_bit >= 1 && end_bit <= 64 && begin_bit >= 0 && begin_bit < end_bit, "gb_sort: bits");
   if (n == 0) return;
   DeviceGuard guard(keys.device());
   auto* k = reinterpret_cast<const uint64_t*>(keys.data_ptr<int64_t>());
   auto* o = reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>());
   size_t bytes = 0;
-  DALGO_CHECK_HIP(dalgo_gb_sort(nullptr, &bytes, k, o, n, 0, (int)end_bit, cur_stream()), "gb_sort(size)");
+  DALGO_CHECK_HIP(dalgo_gb_sort(nullptr, &bytes, k, o, n, (int)begin_bit, (int)end_bit, cur_stream()),
+                  "gb_sort(size)");
   Tensor tmp = at::empty({(int64_t)bytes + 256}, keys.options().dtype(at::kByte));
-  DALGO_CHECK_HIP(dalgo_gb_sort(tmp.data_ptr(), &bytes, k, o, n, 0, (int)end_bit, cur_stream()), "gb_sort");
+  DALGO_CHECK_HIP(dalgo_gb_sort(tmp.data_ptr(), &bytes, k, o, n, (int)begin_bit, (int)end_bit, cur_stream()),
+                  "gb_sort");
 }
 
 // blocks of the decode kernels over n sorted keys (size of their counts / offsets tables)
@@ -1629,7 +1632,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("gb_keys(Tensor src, Tensor dst, Tensor? new_id, int v_lo, int v_hi, int sl, int world, int rank, "
         "int dbits, int phase, Tensor(a!)? bitmap, Tensor(b!)? counts, Tensor? offsets, int base_all, "
         "Tensor(c!)? keys, Tensor? word_prefix, Tensor? seg_start, Tensor? seg_blk0) -> ()");
-  m.def("gb_sort(Tensor keys, int n, int end_bit, Tensor(a!) out) -> ()");
+  m.def("gb_sort(Tensor keys, int n, int end_bit, Tensor(a!) out, int begin_bit=0) -> ()");
   m.def("gb_keys_packed(Tensor packed, Tensor? new_id, int n_vertices, int dbits, Tensor(a!) keys) -> ()");
   m.def("gb_pack(Tensor src, Tensor dst, Tensor(a!) out) -> ()");
   m.def("gb_degree_packed(Tensor packed, int end_bit, Tensor(a!) deg, Tensor(b!) out) -> ()");

@@ -110,19 +110,21 @@ def degree_order_from(edges: list, scale: int, rank: int, world: int, device) ->
 
 def rank_by_degree(deg: torch.Tensor) -> torch.Tensor:
     """Vertex ids by descending degree, ties by descending id (argsort of -deg * n - id).
-    GPU: one rocPRIM radix sort of ((max - deg) << b | (n - 1 - id)) keys over their
-    significant bits (graph_build.hip gb_sort)."""
+    GPU: one rocPRIM radix sort of ((max - deg) << b | id) keys laid out in descending id
+    order, over the degree bits only (stable: equal degrees keep that order; 3 passes at
+    R-MAT scale 26 instead of 6 over all bits; graph_build.hip gb_sort)."""
     n = deg.numel()
-    ids = torch.arange(n, device=deg.device, dtype=torch.int64)
     if deg.is_cuda:
         from dalgo.ops import _ext
         dmax = int(deg.max().item()) if n else 0
         dbits = max(1, dmax.bit_length())
         ibits = max(1, (n - 1).bit_length())
-        keys = ((dmax - deg.to(torch.int64)) << ibits) | (n - 1 - ids)
+        rid = torch.arange(n - 1, -1, -1, device=deg.device, dtype=torch.int64)   # descending ids
+        keys = ((dmax - deg.to(torch.int64).flip(0)) << ibits) | rid
         out = torch.empty_like(keys)
-        _ext.ops().gb_sort(keys, n, dbits + ibits, out)
-        return (n - 1) - (out & ((1 << ibits) - 1))
+        _ext.ops().gb_sort(keys, n, dbits + ibits, out, ibits)
+        return out & ((1 << ibits) - 1)
+    ids = torch.arange(n, device=deg.device, dtype=torch.int64)
     return torch.argsort(-deg.to(torch.int64) * n - ids)
 
 
