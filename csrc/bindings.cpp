@@ -1146,7 +1146,7 @@ void gb_cell_place(const Tensor& C, const Tensor& CM, const Tensor& RID, int64_t
 void gb_entry_cells(const Tensor& ent_blk, const Tensor& ent_dst, const Tensor& ent_end, int64_t bshift,
                     int64_t nblk, int64_t nbins, const Tensor& CM, const Tensor& RID, const Tensor& run_delta,
                     const Tensor& RE, const Tensor& CI, const Tensor& ce_lo, const Tensor& tlen, int64_t wu_e,
-                    int64_t bin_mask, Tensor dloc, Tensor ts, Tensor srcl) {
+                    int64_t bin_mask, Tensor dloc, Tensor tiles, Tensor n_tiles, Tensor srcl) {
   check_i32(ent_blk, "ent_blk");
   check_i32(ent_dst, "ent_dst");
   check_t(ent_end, at::kLong, "ent_end");
@@ -1158,10 +1158,11 @@ void gb_entry_cells(const Tensor& ent_blk, const Tensor& ent_dst, const Tensor& 
   check_t(ce_lo, at::kLong, "ce_lo");
   check_t(tlen, at::kLong, "tlen");
   check_t(dloc, at::kShort, "dloc");
-  check_t(ts, at::kByte, "ts");
+  check_i32(tiles, "tiles");
+  check_t(n_tiles, at::kLong, "n_tiles");
   check_t(srcl, at::kShort, "srcl");
   const int64_t ne = ent_blk.numel();
-  TORCH_CHECK(ent_dst.numel() == ne && ent_end.numel() == ne && ts.numel() >= ne && dloc.numel() >= ne,
+  TORCH_CHECK(ent_dst.numel() == ne && ent_end.numel() == ne && dloc.numel() >= ne && n_tiles.numel() >= 1,
               "gb_entry_cells: entry arrays");
   TORCH_CHECK(nblk >= 1 && nbins >= 1 && CM.numel() >= nblk * nbins && RID.numel() >= nblk * nbins &&
                   RE.numel() >= nblk && CI.numel() >= nblk && ce_lo.numel() == tlen.numel(),
@@ -1172,9 +1173,11 @@ void gb_entry_cells(const Tensor& ent_blk, const Tensor& ent_dst, const Tensor& 
                                        CM.data_ptr<int32_t>(), RID.data_ptr<int32_t>(), run_delta.data_ptr<int32_t>(),
                                        run_delta.numel(), RE.data_ptr<int64_t>(), CI.data_ptr<int32_t>(),
                                        ce_lo.data_ptr<int64_t>(), tlen.data_ptr<int64_t>(), ce_lo.numel(), wu_e,
-                                       (int)bin_mask, dloc.data_ptr<int16_t>(), dloc.numel(), ts.data_ptr<uint8_t>(),
-                                       reinterpret_cast<uint16_t*>(srcl.data_ptr<int16_t>()), srcl.numel(),
-                                       cur_stream()),
+                                       (int)bin_mask, dloc.data_ptr<int16_t>(), dloc.numel(),
+                                       tiles.data_ptr<int32_t>(),
+                                       reinterpret_cast<unsigned long long*>(n_tiles.data_ptr<int64_t>()),
+                                       tiles.numel(), reinterpret_cast<uint16_t*>(srcl.data_ptr<int16_t>()),
+                                       srcl.numel(), cur_stream()),
                   "gb_entry_cells");
 }
 
@@ -1649,7 +1652,7 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(a!) run_delta, Tensor(b!) run_chunk, Tensor(c!) run_first) -> ()");
   m.def("gb_entry_cells(Tensor ent_blk, Tensor ent_dst, Tensor ent_end, int bshift, int nblk, int nbins, "
         "Tensor CM, Tensor RID, Tensor run_delta, Tensor RE, Tensor CI, Tensor ce_lo, Tensor tlen, int wu_e, "
-        "int bin_mask, Tensor(a!) dloc, Tensor(b!) ts, Tensor(c!) srcl) -> ()");
+        "int bin_mask, Tensor(a!) dloc, Tensor(b!) tiles, Tensor(c!) n_tiles, Tensor(d!) srcl) -> ()");
   m.def("gb_entry_flags(Tensor ent_blk, Tensor ent_dst, Tensor ent_end, int bin_shift, Tensor(a!) rs, "
         "Tensor(b!) cs, Tensor(c!) srcl) -> ()");
   m.def("gb_entry_place(Tensor ent_dst, Tensor ent_end, Tensor run_of_ent, Tensor run_delta, "

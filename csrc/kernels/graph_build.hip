@@ -644,27 +644,46 @@ __global__ void __launch_bounds__(256) gb_entry_cells_kernel(
     const int32_t* __restrict__ RID, const int32_t* __restrict__ run_delta, int64_t nruns,
     const int64_t* __restrict__ RE, const int32_t* __restrict__ CI, const int64_t* __restrict__ ce_lo,
     const int64_t* __restrict__ tlen, int64_t nch, int64_t wu_e, int bin_mask, int16_t* __restrict__ dloc,
-    int64_t ndloc, uint8_t* __restrict__ ts, uint16_t* __restrict__ srcl, int64_t nsrcl) {
+    int64_t ndloc, int32_t* __restrict__ tiles, unsigned long long* __restrict__ n_tiles, int64_t tile_cap,
+    uint16_t* __restrict__ srcl, int64_t nsrcl) {
+  const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nent; e += stride) {
-    const int32_t b = ent_blk[e], d = ent_dst[e], bin = d >> bshift;
-    if (b < 0 || b >= nblk || bin < 0 || bin >= nbins) continue;
-    const int64_t cell = (int64_t)b * nbins + bin;
-    const int32_t q = RID[cell];
-    if (q < 0 || q >= nruns) continue;
-    const int64_t pos = e + run_delta[q];
-    if (pos >= 0 && pos < ndloc) dloc[pos] = (int16_t)(d & bin_mask);
-    const int64_t ee = ent_end[e];
-    if (e == CM[cell] && ee >= 0 && ee < nsrcl) srcl[ee] |= (uint16_t)0x4000;
-    const int32_t ch = CI[b];
-    bool t = e == RE[b];
-    if (!t && e > 0 && ch >= 0 && ch < nch) {
-      const int64_t tl = tlen[ch];
-      const int64_t a = (e > 1 ? ent_end[e - 2] + 1 : 0) - ce_lo[ch];   // entry e - 1's first edge
-      const int64_t bb = ent_end[e - 1] + 1 - ce_lo[ch];                // entry e's first edge
-      t = (a / wu_e) != (bb / wu_e) || ((a % wu_e) / tl) != ((bb % wu_e) / tl);
+  // (block-uniform loop: every lane reaches the ballot below)
+  for (int64_t e0 = (int64_t)blockIdx.x * 256; e0 < nent; e0 += stride) {
+    const int64_t e = e0 + threadIdx.x;
+    bool t = false;
+    if (e < nent) {
+      const int32_t b = ent_blk[e], d = ent_dst[e], bin = d >> bshift;
+      const bool okc = b >= 0 && b < nblk && bin >= 0 && bin < nbins;
+      const int64_t cell = okc ? (int64_t)b * nbins + bin : 0;
+      const int32_t q = okc ? RID[cell] : -1;
+      if (q >= 0 && q < nruns) {
+        const int64_t pos = e + run_delta[q];
+        if (pos >= 0 && pos < ndloc) dloc[pos] = (int16_t)(d & bin_mask);
+        const int64_t ee = ent_end[e];
+        if (e == CM[cell] && ee >= 0 && ee < nsrcl) srcl[ee] |= (uint16_t)0x4000;
+        const int32_t ch = CI[b];
+        t = e == RE[b];
+        if (!t && e > 0 && ch >= 0 && ch < nch) {
+          const int64_t tl = tlen[ch];
+          const int64_t a = (e > 1 ? ent_end[e - 2] + 1 : 0) - ce_lo[ch];   // entry e - 1's first edge
+          const int64_t bb = ent_end[e - 1] + 1 - ce_lo[ch];                // entry e's first edge
+          t = (a / wu_e) != (bb / wu_e) || ((a % wu_e) / tl) != ((bb % wu_e) / tl);
+        }
+      }
     }
-    ts[e] = t;
+    // tile starts -> an unordered list (one global atomic per wave that has any; sorted
+    // on the host side afterwards): no per-entry flag array, no compaction pass
+    const uint64_t m = __ballot(t);
+    if (m != 0ull) {
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(n_tiles, (unsigned long long)__popcll(m));
+      base = __shfl(base, 0);
+      if (t) {
+        const long long slot = (long long)base + __popcll(m & ((1ull << lane) - 1ull));
+        if (slot < tile_cap) tiles[slot] = (int32_t)e;
+      }
+    }
   }
 }
 
@@ -844,14 +863,14 @@ hipError_t dalgo_gb_entry_cells(const int32_t* ent_blk, const int32_t* ent_dst, 
                                 int bshift, int nblk, int nbins, const int32_t* CM, const int32_t* RID,
                                 const int32_t* run_delta, int64_t nruns, const int64_t* RE, const int32_t* CI,
                                 const int64_t* ce_lo, const int64_t* tlen, int64_t nch, int64_t wu_e, int bin_mask,
-                                int16_t* dloc, int64_t ndloc, uint8_t* ts, uint16_t* srcl, int64_t nsrcl,
-                                hipStream_t st) {
+                                int16_t* dloc, int64_t ndloc, int32_t* tiles, unsigned long long* n_tiles,
+                                int64_t tile_cap, uint16_t* srcl, int64_t nsrcl, hipStream_t st) {
   if (nent <= 0) return hipSuccess;
-  if (wu_e < 1) return hipErrorInvalidValue;
+  if (wu_e < 1 || nent >= (int64_t)0x7fffffffLL) return hipErrorInvalidValue;
   const int64_t g = std::min<int64_t>(cdiv(nent, 256), 256 * 64);
   hipLaunchKernelGGL(gb_entry_cells_kernel, dim3((unsigned)g), dim3(256), 0, st, ent_blk, ent_dst, ent_end, nent,
                      bshift, nblk, nbins, CM, RID, run_delta, nruns, RE, CI, ce_lo, tlen, nch, wu_e, bin_mask, dloc,
-                     ndloc, ts, srcl, nsrcl);
+                     ndloc, tiles, n_tiles, tile_cap, srcl, nsrcl);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -1467,12 +1467,19 @@ km_dsegsum_kernel(const T* __restrict__ X, int64_t ldx, const int* __restrict__ 
           const int row = cu == kNone ? 0 : (cu < 0 ? ~cu : cu);
           sg[u] = cu == kNone ? 0.f : (cu < 0 ? -1.f : 1.f);
           const T* rp = X + (int64_t)row * ldx + lane * EPL;
+          if constexpr (sizeof(T) == 2 && EPL == 2) {
+            // both bf16 of the lane in one dword load (4-B aligned: ldx is a multiple of 8)
+            const uint32_t w = ld_u32<true>(reinterpret_cast<const uint32_t*>(rp));   // nt: read once
+            v[u][0] = bf16lo(w);
+            v[u][1] = bf16hi(w);
+          } else {
 #pragma unroll
-          for (int e = 0; e < EPL; ++e) {
-            float x = 0.f;
-            if constexpr (sizeof(T) == 2) x = bf16_to_f32(reinterpret_cast<const uint16_t*>(rp)[e]);
-            else x = reinterpret_cast<const float*>(rp)[e];
-            v[u][e] = lane_on ? x : 0.f;
+            for (int e = 0; e < EPL; ++e) {
+              float x = 0.f;
+              if constexpr (sizeof(T) == 2) x = bf16_to_f32(reinterpret_cast<const uint16_t*>(rp)[e]);
+              else x = reinterpret_cast<const float*>(rp)[e];
+              v[u][e] = lane_on ? x : 0.f;
+            }
           }
         }
 #pragma unroll

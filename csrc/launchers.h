@@ -245,8 +245,8 @@ hipError_t dalgo_gb_entry_cells(const int32_t* ent_blk, const int32_t* ent_dst, 
                                 int bshift, int nblk, int nbins, const int32_t* CM, const int32_t* RID,
                                 const int32_t* run_delta, int64_t nruns, const int64_t* RE, const int32_t* CI,
                                 const int64_t* ce_lo, const int64_t* tlen, int64_t nch, int64_t wu_e, int bin_mask,
-                                int16_t* dloc, int64_t ndloc, uint8_t* ts, uint16_t* srcl, int64_t nsrcl,
-                                hipStream_t st);
+                                int16_t* dloc, int64_t ndloc, int32_t* tiles, unsigned long long* n_tiles,
+                                int64_t tile_cap, uint16_t* srcl, int64_t nsrcl, hipStream_t st);
 hipError_t dalgo_gb_entry_place(const int32_t* ent_dst, const int64_t* ent_end, int64_t nent,
                                 const int32_t* run_of_ent, const int32_t* run_delta, const int32_t* run_chunk,
                                 const uint8_t* cs, const int64_t* ce_lo, const int64_t* tlen, int64_t wu_e,

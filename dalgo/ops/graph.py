@@ -662,7 +662,6 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     wu_e = max(1 << 15, E // 4096)
     n4 = (nent + 3) // 4 * 4 + PB_DUMMY
     dloc = torch.zeros(n4, dtype=torch.int16, device=dev)
-    ts = torch.empty(nent, dtype=torch.uint8, device=dev)
     assert nent < (1 << 31) - 8
     if nblk_k * nbins <= CELL_CAP:
         # runs = the non-empty cells of the (block, bin) matrix (graph_build.hip gb_cell_*)
@@ -700,9 +699,24 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
                             torch.zeros_like(chunk_first))
         ce_n = torch.diff(torch.cat([ce_lo, torch.tensor([E], **i64)]))
         tlen = torch.clamp((torch.clamp(ce_n, max=wu_e) + 15) // 16, min=min(1024, tile), max=tile)
+        # tile starts: at most one per chunk start, per work-unit boundary and per tlen
+        # boundary inside a unit
+        cap_t = int((1 + (ce_n + wu_e - 1) // wu_e + (ce_n + tlen - 1) // tlen).sum().item())
+        tiles_l = torch.empty(max(cap_t, 1), **i32)
+        n_t = torch.zeros(1, **i64)
         ops.gb_entry_cells(ent_blk, ent_dst, ent_end, bshift, nblk_k, nbins, CM, RID, run_delta, RE, CI,
-                           ce_lo, tlen, wu_e, bin_width - 1, dloc, ts, srcl)
+                           ce_lo, tlen, wu_e, bin_width - 1, dloc, tiles_l, n_t, srcl)
         del CM, RID, ent_dst, ent_blk, RE, RR, CI
+        _mark("entry_place")
+        nt = int(n_t.item())
+        assert nt <= cap_t, (nt, cap_t)
+        # (the build's own u64 radix sort: torch.sort at this size took 32 ms on its first
+        # use in a process, profiles/round5/r5_31)
+        tk = tiles_l[:nt].to(torch.int64)
+        tile_ent = torch.empty_like(tk)
+        if nt:
+            ops.gb_sort(tk, nt, max(1, (nent - 1).bit_length()), tile_ent)
+        del tiles_l, tk
     else:
         # matrix too large: per-entry flags, scans and a sort of the runs
         rs = torch.empty(nent, dtype=torch.uint8, device=dev)
@@ -735,13 +749,14 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
                             torch.zeros_like(chunk_first))
         ce_n = torch.diff(torch.cat([ce_lo, torch.tensor([E], **i64)]))
         tlen = torch.clamp((torch.clamp(ce_n, max=wu_e) + 15) // 16, min=min(1024, tile), max=tile)
+        ts = torch.empty(nent, dtype=torch.uint8, device=dev)
         ops.gb_entry_place(ent_dst, ent_end, run_of_ent, run_delta, run_chunk, cs,
                            ce_lo, tlen, wu_e, bin_width - 1, dloc, ts)
         del run_of_ent, cs, ent_dst, ent_blk
+        _mark("entry_place")
+        tile_ent = torch.nonzero(ts).flatten()
+        del ts
     assert nruns < (1 << 31)
-    _mark("entry_place")
-    tile_ent = torch.nonzero(ts).flatten()
-    del ts
     _mark("tile_select")
     e_start_t = torch.where(tile_ent > 0, ent_end[(tile_ent - 1).clamp_min(0)] + 1, torch.zeros_like(tile_ent))
     del ent_end
