@@ -1073,3 +1073,32 @@ def test_kmeans_candidates_match_plain(cuda):
         assert c._cand is not None
         for _ in range(7):
             _kmeans_step_oracle(c)
+
+
+def test_kmeans_dense_choice_on_device(cuda):
+    """Filtered iterations pick the dense top-2 K2 or the pruned one on the device: right
+    after the full pass always dense, later dense iff >= DENSE_FRACTION of the rows are
+    active (dense_history = rows the dense K2 took, 0 otherwise); "never" / "always"
+    force one form; every run passes the one-step oracle."""
+    from dalgo.data.synthetic import blobs
+    from dalgo.models.kmeans import DENSE_FRACTION, KMeans, KMeansConfig
+    n, d, k = 200_000, 128, 512
+    X = blobs(n, d, k, device=cuda, dtype=torch.bfloat16, seed=13, noise=2.0)
+    for mode in ("auto", "never", "always"):
+        km = KMeans(KMeansConfig(k=k, n_iterations=6, seed=3, dense=mode), X, 0, n)
+        assert km._cand is not None
+        for _ in range(6):
+            _kmeans_step_oracle(km)
+        act, dense = km.active_history, km.dense_history
+        assert dense[0] == 0                                   # the full pass
+        for i in range(1, len(act)):
+            if mode == "never":
+                want = 0
+            elif mode == "always" or i == 1:
+                want = act[i]
+            else:
+                want = act[i] if act[i] >= DENSE_FRACTION * n else 0
+            assert dense[i] == want, (mode, i, act, dense)
+        if mode == "auto":   # this data exercises both device choices (probe: r5_34)
+            assert any(dense[i] > 0 for i in range(2, len(act))), (act, dense)
+            assert any(dense[i] == 0 for i in range(2, len(act))), (act, dense)
