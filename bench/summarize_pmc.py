@@ -12,12 +12,14 @@ CUS, SIMDS, XCDS = 256, 4, 8   # GRBM_GUI_ACTIVE is summed over the 8 XCDs
 
 def load(root):
     per = defaultdict(lambda: defaultdict(list))
-    for f in glob.glob(os.path.join(root, "pmc_*_*", "run_counter_collection.csv")):
+    files = glob.glob(os.path.join(root, "pmc_*_*", "run_counter_collection.csv"))
+    files += glob.glob(os.path.join(root, "csv", "pmc_*_*.csv"))      # flattened copies
+    for f in files:
         for r in csv.DictReader(open(f)):
             name = r.get("Kernel_Name", "")
             if "dalgo::" not in name and "kmeans_assign16" not in name:
                 continue
-            short = name.replace("void ", "").split("(")[0]
+            short = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
             per[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return per
 
