@@ -456,6 +456,10 @@ pb_accum_kernel(const float* __restrict__ val, const uint16_t* __restrict__ dloc
           atomicAdd(&s_acc[kk[j]], (unsigned long long)to_fixed(f[j], K));
     }
   };
+  // (64 consecutive entries per atomic instruction -- 4 strided entries per thread, so
+  // a dense run's destinations hit distinct LDS banks -- measured 2 % slower per
+  // iteration despite the 5.75 bank-conflict cycles per LDS instruction of this form:
+  // profiles/round5/r5_36)
   int64_t g0 = g_lo + threadIdx.x;
   if (g0 < g_hi) {
     int4 va[U], vb[U];
