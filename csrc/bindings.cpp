@@ -867,7 +867,7 @@ void gb_keys(const Tensor& src, const Tensor& dst, const std::optional<Tensor>& 
 
 // one rank: keys of the packed (src << 32 | dst) edges (every destination is kept)
 void gb_keys_packed(const Tensor& packed, const std::optional<Tensor>& new_id, int64_t n_vertices, int64_t dbits,
-                    Tensor keys) {
+                    Tensor keys, int64_t src_new) {
   check_t(packed, at::kLong, "packed");
   check_t(keys, at::kLong, "keys");
   const int64_t n = packed.numel();
@@ -877,11 +877,21 @@ void gb_keys_packed(const Tensor& packed, const std::optional<Tensor>& new_id, i
     TORCH_CHECK(new_id->numel() >= n_vertices, "gb_keys_packed: new_id [n_vertices]");
   }
   DalgoGbKeyArgs a{0, n_vertices, n_vertices, 1, 0, (int)dbits, opt_ptr<const int32_t>(new_id), nullptr, nullptr,
-                   nullptr, nullptr};
+                   nullptr, nullptr, (int)(src_new != 0)};
   DeviceGuard guard(packed.device());
   DALGO_CHECK_HIP(dalgo_gb_keys(nullptr, nullptr, n, &a, 1, nullptr, nullptr, nullptr, 0, reinterpret_cast<uint64_t*>(keys.data_ptr<int64_t>()),
                                 reinterpret_cast<const uint64_t*>(packed.data_ptr<int64_t>()), cur_stream()),
                   "gb_keys_packed");
+}
+
+// packed (src << 32 | dst) words: src := new_id[src], in place
+void gb_relabel_src(Tensor packed, const Tensor& new_id) {
+  check_t(packed, at::kLong, "packed");
+  check_i32(new_id, "new_id");
+  DeviceGuard guard(packed.device());
+  DALGO_CHECK_HIP(dalgo_gb_relabel_src(reinterpret_cast<uint64_t*>(packed.data_ptr<int64_t>()), packed.numel(),
+                                       new_id.data_ptr<int32_t>(), cur_stream()),
+                  "gb_relabel_src");
 }
 
 // packed[i] = src[i] << 32 | dst[i]
@@ -1636,7 +1646,8 @@ TORCH_LIBRARY(dalgo, m) {
         "int dbits, int phase, Tensor(a!)? bitmap, Tensor(b!)? counts, Tensor? offsets, int base_all, "
         "Tensor(c!)? keys, Tensor? word_prefix, Tensor? seg_start, Tensor? seg_blk0) -> ()");
   m.def("gb_sort(Tensor keys, int n, int end_bit, Tensor(a!) out, int begin_bit=0) -> ()");
-  m.def("gb_keys_packed(Tensor packed, Tensor? new_id, int n_vertices, int dbits, Tensor(a!) keys) -> ()");
+  m.def("gb_keys_packed(Tensor packed, Tensor? new_id, int n_vertices, int dbits, Tensor(a!) keys, int src_new=0) -> ()");
+  m.def("gb_relabel_src(Tensor(a!) packed, Tensor new_id) -> ()");
   m.def("gb_pack(Tensor src, Tensor dst, Tensor(a!) out) -> ()");
   m.def("gb_degree_packed(Tensor packed, int end_bit, Tensor(a!) deg, Tensor(b!) out) -> ()");
   m.def("gb_degree_sorted(Tensor ids, int end_bit, Tensor(a!) deg) -> ()");
@@ -1716,6 +1727,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("gb_keys", &gb_keys);
   m.impl("gb_sort", &gb_sort);
   m.impl("gb_keys_packed", &gb_keys_packed);
+  m.impl("gb_relabel_src", &gb_relabel_src);
   m.impl("gb_pack", &gb_pack);
   m.impl("gb_degree_packed", &gb_degree_packed);
   m.impl("gb_degree_sorted", &gb_degree_sorted);

@@ -109,6 +109,17 @@ __global__ void __launch_bounds__(256) gb_bucket_degree_kernel(const E* __restri
   for (int j = threadIdx.x; j < (1 << kBktBits); j += 256) d[j] += (int32_t)hist[j];
 }
 
+// packed edges partitioned on the source: the source relabelled in place (the gathers of
+// one block stay inside a few 32 KB slices of new_id)
+__global__ void __launch_bounds__(256) gb_relabel_src_kernel(uint64_t* __restrict__ packed, int64_t n,
+                                                             const int32_t* __restrict__ new_id) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const uint64_t w = packed[i];
+    packed[i] = ((uint64_t)(uint32_t)new_id[(uint32_t)(w >> 32)] << 32) | (w & 0xffffffffull);
+  }
+}
+
 // packed edges: out[i] = src[i] << 32 | dst[i]
 __global__ void __launch_bounds__(256) gb_pack_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
                                                       int64_t n, uint64_t* __restrict__ out) {
@@ -131,6 +142,7 @@ struct GbKeyCtx {
   const int64_t* word_prefix;   // W > 1: exclusive popcount prefix of the bitmap words
   const int64_t* seg_start;     // [W]: local index where segment p starts (p = owner)
   const int64_t* seg_blk0;      // [W]: first block id of segment p
+  int src_new;                  // the sources are already relabelled
 };
 
 __device__ __forceinline__ bool gb_edge(const GbKeyCtx& c, int32_t s0, int32_t d0, int32_t& s,
@@ -139,7 +151,7 @@ __device__ __forceinline__ bool gb_edge(const GbKeyCtx& c, int32_t s0, int32_t d
   dl = (int64_t)d - c.v_lo;
   const bool keep = d >= c.v_lo && d < c.v_hi;
   // (one rank: every edge is kept; several: the source is relabelled only where kept)
-  s = c.new_id && (c.world == 1 || keep) ? c.new_id[s0] : s0;
+  s = c.new_id && !c.src_new && (c.world == 1 || keep) ? c.new_id[s0] : s0;
   return keep;
 }
 
@@ -743,7 +755,7 @@ hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, cons
   if (n <= 0) return hipSuccess;
   if (a->dbits < 0 || a->dbits > 31 || a->world < 1) return hipErrorInvalidValue;
   GbKeyCtx c{a->v_lo, a->v_hi, a->sl, a->world, a->rank, a->dbits, a->new_id, a->bitmap,
-             a->word_prefix, a->seg_start, a->seg_blk0};
+             a->word_prefix, a->seg_start, a->seg_blk0, a->src_new};
   if (c.world > 1 && (c.sl <= 0 || (phase == 1 && (!c.bitmap || !c.word_prefix || !c.seg_start || !c.seg_blk0))))
     return hipErrorInvalidValue;
   const int64_t g = cdiv(n, (int64_t)kKeyR);
@@ -763,6 +775,14 @@ hipError_t dalgo_gb_sort(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint6
                          int begin_bit, int end_bit, hipStream_t st) {
   if (n < 0 || end_bit < 1 || end_bit > 64 || begin_bit < 0 || begin_bit >= end_bit) return hipErrorInvalidValue;
   return rocprim::radix_sort_keys(tmp, *tmp_bytes, in, out, (size_t)n, (unsigned)begin_bit, (unsigned)end_bit, st);
+}
+
+hipError_t dalgo_gb_relabel_src(uint64_t* packed, int64_t n, const int32_t* new_id, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t g = std::min<int64_t>(cdiv(n, 256), 256 * 64);
+  hipLaunchKernelGGL(gb_relabel_src_kernel, dim3((unsigned)g), dim3(256), 0, st, packed, n, new_id);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
 }
 
 hipError_t dalgo_gb_pack(const int32_t* src, const int32_t* dst, int64_t n, uint64_t* out, hipStream_t st) {

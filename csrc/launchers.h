@@ -213,6 +213,7 @@ struct DalgoGbKeyArgs {
   const int64_t* word_prefix;   // W > 1: exclusive popcount prefix per bitmap word
   const int64_t* seg_start;     // [W]: local source index where owner p's segment starts
   const int64_t* seg_blk0;      // [W]: first block id of owner p's segment
+  int src_new;                  // 1: the sources are already relabelled (only dst via new_id)
 };
 extern "C" {
 hipError_t dalgo_gb_degree(const int32_t* ids, int64_t n, uint32_t* deg, hipStream_t st);
@@ -221,6 +222,7 @@ hipError_t dalgo_gb_sort32(void* tmp, size_t* tmp_bytes, const uint32_t* in, uin
 int dalgo_gb_bucket_bits();
 hipError_t dalgo_gb_bucket_degree(const void* sorted, int packed, int64_t n, int end_bit, int64_t* starts,
                                   int32_t* deg, hipStream_t st);
+hipError_t dalgo_gb_relabel_src(uint64_t* packed, int64_t n, const int32_t* new_id, hipStream_t st);
 hipError_t dalgo_gb_pack(const int32_t* src, const int32_t* dst, int64_t n, uint64_t* out, hipStream_t st);
 int64_t dalgo_gb_key_blocks(int64_t n);
 hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, const DalgoGbKeyArgs* a,

@@ -155,8 +155,9 @@ def build_rmat_native(edges: list, scale: int, rank: int, world: int, device, re
     (dalgo.ops.graph.build_native): degree relabeling, destination filter, dedup and the
     blocked layout without the (dst, src)-sorted intermediate shard. One rank with
     relabeling: the (src, dst) pairs are packed and partitioned on the high source bits
-    first (the degree count's own partition), so the key pass relabels the sources from a
-    32 KB slice of the table per bucket instead of at random."""
+    first (the degree count's own partition), the sources relabelled there (32 KB slices of
+    the table per bucket), then partitioned on the high destination bits, so the key pass
+    relabels the destinations from such slices too: no random table gathers."""
     G._mark("start")
     packed = None
     if reorder and world == 1 and torch.device(device).type == "cuda" and scale > G.BUCKET_BITS:
@@ -166,11 +167,14 @@ def build_rmat_native(edges: list, scale: int, rank: int, world: int, device, re
         G._mark("degree_rank")
         new_id = deal_ids(order, 1 << scale, 1).to(torch.int32)
         del deg, order
+        G._mark("deal_ids")
+        packed = G.relabel_partition_dst(packed, new_id, scale)
+        G._mark("dst_partition")
     else:
         new_id = degree_order_from(edges, scale, rank, world, device) if reorder else None
-    G._mark("deal_ids")
+        G._mark("deal_ids")
     return G.build_native(edges, 1 << scale, rank, world, new_id, bin_width=bin_width, tile=tile,
-                          keep_keys=keep_keys, packed=packed)
+                          keep_keys=keep_keys, packed=packed, packed_src_new=packed is not None)
 
 
 def rmat_shard(scale: int, edge_factor: int, rank: int, world: int, device, seed: int = 1,

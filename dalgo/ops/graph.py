@@ -157,6 +157,22 @@ def partition_edges(edges: list, bits: int):
     return out[:n], deg
 
 
+def relabel_partition_dst(packed: torch.Tensor, new_id: torch.Tensor, bits: int) -> torch.Tensor:
+    """Source-partitioned packed edges (:func:`partition_edges`): the sources relabelled in
+    place (gathers local to each source bucket), then the edges partitioned on the top 8
+    destination bits (one radix pass), so the key pass's destination relabeling reads one
+    L2-resident slice of new_id per bucket."""
+    ops = _ext.ops()
+    n = packed.numel()
+    ops.gb_relabel_src(packed, new_id)
+    out = torch.empty_like(packed)
+    if n:
+        # one radix pass over the top 8 destination bits: 2^(bits - 8)-id buckets (1 MB of
+        # new_id at scale 26) stay L2-resident while the key pass walks them
+        ops.gb_sort(packed, n, int(bits), out, max(0, int(bits) - 8))
+    return out
+
+
 def degree_sorted_(deg: torch.Tensor, ids: torch.Tensor, bits: int) -> torch.Tensor:
     """deg[v] += #occurrences of v in ids (GPU int32, ids < 2^bits): the ids partitioned
     on their high bits (2 radix passes at 2^26 ids), then one LDS histogram per bucket of
@@ -524,7 +540,7 @@ def build_phase_spans() -> dict:
 def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: torch.Tensor | None = None,
                  bin_width: int = 16384, tile: int = 16384, items: int = 2048,
                  min_piece: int = 1 << 14, keep_keys: bool = False,
-                 packed: torch.Tensor | None = None) -> NativeGraph:
+                 packed: torch.Tensor | None = None, packed_src_new: bool = False) -> NativeGraph:
     """``distinct().groupByKey()`` of graph_computation/pagerank.py:41 straight into the
     K4b layout, on the device (csrc/kernels/graph_build.hip): relabel + keep this rank's
     destinations + pack one (block, destination, source offset) key per edge, ONE radix
@@ -534,7 +550,8 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
 
     edges: list of (src, dst) int32 GPU chunks of GLOBAL ids (before ``new_id``).
     packed (one rank): the same edges as (src << 32 | dst) int64 words in any order
-    (:func:`partition_edges`: partitioned on the source), read instead of ``edges``."""
+    (:func:`partition_edges`: partitioned on the source), read instead of ``edges``;
+    packed_src_new: their sources are already relabelled (:func:`relabel_partition_dst`)."""
     if bin_width not in (8192, 16384):
         raise ValueError("bin_width must be 8192 or 16384")
     ops = _ext.ops()
@@ -611,7 +628,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     if from_packed:
         if W != 1 or packed.numel() != total:
             raise ValueError("build_native: packed edges are the one-rank path over every edge")
-        ops.gb_keys_packed(packed, nid, N, dbits, keys)
+        ops.gb_keys_packed(packed, nid, N, dbits, keys, int(bool(packed_src_new)))
         del packed
     o, base_all = 0, 0
     for (s, d), nb in zip(edges, nbs):
