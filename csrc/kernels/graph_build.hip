@@ -296,7 +296,8 @@ __global__ void __launch_bounds__(256) gb_keys_write_kernel(const int32_t* __res
 constexpr int kDecR = 65536;         // keys per block of the decode kernels (262144: 13.0 ->
                                      // 14.3 ms at scale 26, profiles/round5/r5_21)
 constexpr int kDecT = 256;
-constexpr int kDecV = 4;             // keys per thread per step
+constexpr int kDecV = 4;             // keys per thread per step (8: decode 11.3 -> 13.1 ms,
+                                     // profiles/round5/r5_41)
 
 __device__ __forceinline__ void gb_flags(const uint64_t* __restrict__ K, int64_t n, int64_t i,
                                          bool& last, bool& end, uint64_t& k) {
