@@ -987,6 +987,22 @@ void gb_sort(const Tensor& keys, int64_t n, int64_t end_bit, Tensor out, int64_t
                   "gb_sort");
 }
 
+// keys[:n] sorted on bits [lo_bits, 64) only: each run of keys equal there sorted on its
+// low lo_bits in place (graph_build.hip gb_run_*), so the whole range ends up sorted;
+// returns the device count of the runs (> 256 keys) handed to the block kernel
+Tensor gb_run_sort(Tensor keys, int64_t n, int64_t lo_bits) {
+  check_t(keys, at::kLong, "keys");
+  TORCH_CHECK(n >= 0 && n <= keys.numel(), "gb_run_sort: sizes");
+  TORCH_CHECK(lo_bits >= 1 && lo_bits <= 13, "gb_run_sort: lo_bits");
+  if (n <= 1) return at::zeros({1}, keys.options());
+  DeviceGuard guard(keys.device());
+  Tensor ws = at::empty({dalgo_gb_run_ws(n)}, keys.options());
+  DALGO_CHECK_HIP(dalgo_gb_run_sort(reinterpret_cast<uint64_t*>(keys.data_ptr<int64_t>()), n, (int)lo_bits,
+                                    ws.data_ptr<int64_t>(), cur_stream()),
+                  "gb_run_sort");
+  return ws.slice(0, 0, 1).clone();
+}
+
 // blocks of the decode kernels over n sorted keys (size of their counts / offsets tables)
 int64_t gb_decode_blocks(int64_t n) { return dalgo_gb_decode_blocks(n); }
 
@@ -1646,6 +1662,7 @@ TORCH_LIBRARY(dalgo, m) {
         "int dbits, int phase, Tensor(a!)? bitmap, Tensor(b!)? counts, Tensor? offsets, int base_all, "
         "Tensor(c!)? keys, Tensor? word_prefix, Tensor? seg_start, Tensor? seg_blk0) -> ()");
   m.def("gb_sort(Tensor keys, int n, int end_bit, Tensor(a!) out, int begin_bit=0) -> ()");
+  m.def("gb_run_sort(Tensor(a!) keys, int n, int lo_bits) -> Tensor");
   m.def("gb_keys_packed(Tensor packed, Tensor? new_id, int n_vertices, int dbits, Tensor(a!) keys, int src_new=0) -> ()");
   m.def("gb_relabel_src(Tensor(a!) packed, Tensor new_id) -> ()");
   m.def("gb_pack(Tensor src, Tensor dst, Tensor(a!) out) -> ()");
@@ -1726,6 +1743,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("gb_degree", &gb_degree);
   m.impl("gb_keys", &gb_keys);
   m.impl("gb_sort", &gb_sort);
+  m.impl("gb_run_sort", &gb_run_sort);
   m.impl("gb_keys_packed", &gb_keys_packed);
   m.impl("gb_relabel_src", &gb_relabel_src);
   m.impl("gb_pack", &gb_pack);

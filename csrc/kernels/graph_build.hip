@@ -700,6 +700,311 @@ __global__ void __launch_bounds__(256) gb_entry_cells_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------- run sort
+// The key sort runs over the bits ABOVE the source offset only (39 of 52 bits at scale 26:
+// 5 radix passes instead of 7); the runs of keys equal above lo_bits (one entry's edges:
+// 449M runs over 1.07B keys at scale 26, 75 % of length 1, 6.6M of 17-256 keys, 140K
+// longer, profiles/round5/r5_44) are then sorted on their low lo_bits in place, which makes
+// the copies of an edge adjacent again for the decode's dedup. One block stages a tile of
+// keys plus a halo in LDS, sorts the runs starting in its tile there and writes the changed
+// keys back coalesced: a run of 2 keys by the thread at its first key, 3..kRunShort keys
+// by one thread per run from size-class lists (min/max networks of 4 / 8 / 16 in
+// registers), <= kRunMid keys by one wave (bitonic network over registers and lane
+// shuffles); a longer one is listed (one global atomic per block that has any) and
+// counting-sorted by one block of gb_run_long_kernel over an LDS histogram of the
+// 2^lo_bits offsets. No per-run global atomics: 6.6M of them on one counter took ~60 ms.
+constexpr int kRunShort = 16;
+constexpr int kRunMid = 256;
+constexpr int kRunTile = 2048;        // run starts per block of the tile kernel
+constexpr int kRunT = 256;
+
+template <int N>
+__device__ __forceinline__ void gb_net_sort(uint32_t (&v)[kRunShort]) {
+  // bitonic sorting network on v[0 .. N), ascending (N a power of two, indices static)
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint32_t a = v[i], b = v[l];
+          const bool up = (i & k) == 0;
+          v[i] = up ? min(a, b) : max(a, b);
+          v[l] = up ? max(a, b) : min(a, b);
+        }
+      }
+}
+
+// the listed runs of one size class (entry = j | L << 16, 2 < L <= N): one thread per run,
+// an N-key network over the run's low bits, the run rewritten in the staged keys
+template <int N>
+__device__ __forceinline__ void gb_class_runs(const int* list, int cnt, uint64_t* s_k, uint8_t* s_chg,
+                                              uint64_t lmask) {
+  for (int i = threadIdx.x; i < cnt; i += kRunT) {
+    const int j = list[i] & 0xffff, L = list[i] >> 16;
+    uint32_t v[kRunShort], o[kRunShort];
+#pragma unroll
+    for (int t = 0; t < N; ++t) o[t] = v[t] = t < L ? (uint32_t)(s_k[j + t] & lmask) : 0xffffffffu;
+    gb_net_sort<N>(v);
+    const uint64_t hi = s_k[j] & ~lmask;
+#pragma unroll
+    for (int t = 0; t < N; ++t)
+      if (t < L && v[t] != o[t]) {
+        s_k[j + t] = hi | v[t];
+        s_chg[j + t] = 1;
+      }
+  }
+}
+
+// ascending bitonic sort of the 64 * R values of a wave, element lane * R + r in v[r]
+template <int R>
+__device__ __forceinline__ void gb_wave_sort(uint32_t (&v)[R], int lane) {
+#pragma unroll
+  for (int k = 2; k <= 64 * R; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= R) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int i = lane * R + r;
+          const uint32_t o = __shfl_xor(v[r], j / R, 64);
+          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+          v[r] = keep_min ? min(v[r], o) : max(v[r], o);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int l = r ^ j;
+          if (l > r) {
+            const bool up = ((lane * R + r) & k) == 0;
+            const uint32_t a = v[r], b = v[l];
+            v[r] = up ? min(a, b) : max(a, b);
+            v[l] = up ? max(a, b) : min(a, b);
+          }
+        }
+      }
+    }
+  }
+}
+
+// one wave: the run at tile offset j (L = its length, 17..64 * R) sorted in the staged
+// keys; changed positions flagged for the block's write-out
+template <int R>
+__device__ __forceinline__ void gb_wave_run(uint64_t* s_k, uint8_t* s_chg, int j, int L, int lane,
+                                            uint64_t lmask) {
+  const uint64_t hi = s_k[j] & ~lmask;
+  uint32_t v[R], o[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int e = lane * R + r;
+    o[r] = v[r] = e < L ? (uint32_t)(s_k[j + e] & lmask) : 0xffffffffu;
+  }
+  gb_wave_sort<R>(v, lane);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int e = lane * R + r;
+    if (e < L && v[r] != o[r]) {
+      s_k[j + e] = hi | v[r];
+      s_chg[j + e] = 1;
+    }
+  }
+}
+
+// one wave: a run of 17..64 keys at tile offset j, lane e holding key e; its place is its
+// rank (keys below it, ties by position: stable) from L broadcasts of one register --
+// no LDS round trips, L iterations instead of the 21 shuffle stages of a 64-key network
+__device__ __forceinline__ void gb_wave_rank_run(uint64_t* s_k, uint8_t* s_chg, int j, int L, int lane,
+                                                 uint64_t lmask) {
+  const uint64_t hi = s_k[j] & ~lmask;
+  const uint32_t v = lane < L ? (uint32_t)(s_k[j + lane] & lmask) : 0xffffffffu;
+  int rank = 0;
+  for (int i = 0; i < L; ++i) {
+    const uint32_t u = __builtin_amdgcn_readlane(v, i);
+    rank += (u < v || (u == v && i < lane)) ? 1 : 0;
+  }
+  const uint32_t was = __shfl(v, rank & 63, 64);          // the key at position rank before
+  if (lane < L && was != v) {
+    s_k[j + rank] = hi | v;
+    s_chg[j + rank] = 1;
+  }
+}
+
+__global__ void __launch_bounds__(kRunT) gb_run_tile_kernel(uint64_t* __restrict__ K, int64_t n, int lo_bits,
+                                                            int64_t* __restrict__ longs,
+                                                            unsigned long long* __restrict__ nlong) {
+  constexpr int W = kRunTile + kRunMid + 2;    // keys staged: the tile, a halo, one spare
+  constexpr int kMaxMid = kRunTile / (kRunShort + 1) + 1;
+  constexpr int kMaxLong = kRunTile / (kRunMid + 1) + 1;
+  __shared__ __attribute__((aligned(16))) uint64_t s_k[W];
+  __shared__ uint8_t s_eq[W];                  // key j equal to key j - 1 above lo_bits
+  __shared__ uint8_t s_chg[W];                 // key j rewritten
+  __shared__ int s_mid[kMaxMid];
+  __shared__ int s_long[kMaxLong];
+  __shared__ int s_c4[kRunTile / 3 + 1], s_c8[kRunTile / 5 + 1], s_c16[kRunTile / 9 + 1];
+  __shared__ int s_n[3];
+  __shared__ int s_nmid, s_nlong;
+  __shared__ unsigned long long s_lbase;
+  const int64_t base = (int64_t)blockIdx.x * kRunTile;   // even: 16-B aligned pairs
+  const uint64_t lmask = (1ull << lo_bits) - 1ull;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) { s_nmid = 0; s_nlong = 0; s_n[0] = s_n[1] = s_n[2] = 0; }
+  // keys past n: ~0 (its high bits equal no key's: keys are < 2^63)
+  for (int j = 2 * threadIdx.x; j < W; j += 2 * kRunT) {
+    const int64_t p = base + j;
+    uint64_t k0 = ~0ull, k1 = ~0ull;
+    if (p + 1 < n) {
+      const uint4 v = *reinterpret_cast<const uint4*>(K + p);
+      k0 = ((uint64_t)v.y << 32) | v.x;
+      k1 = ((uint64_t)v.w << 32) | v.z;
+    } else if (p < n) {
+      k0 = K[p];
+    }
+    s_k[j] = k0;
+    s_k[j + 1] = k1;
+  }
+  const uint64_t kprev = base > 0 ? K[base - 1] : ~0ull;
+  __syncthreads();
+  for (int j = threadIdx.x; j < W; j += kRunT) {
+    const uint64_t pk = j ? s_k[j - 1] : kprev;
+    s_eq[j] = base + j < n && ((pk ^ s_k[j]) >> lo_bits) == 0;
+    s_chg[j] = 0;
+  }
+  __syncthreads();
+  // runs of 2 keys: the thread at the first key; 3 .. kRunShort: listed by size class (so
+  // each network below runs on full waves, not on the union of a wave's run sizes)
+  for (int j = threadIdx.x; j < kRunTile; j += kRunT) {
+    if (s_eq[j] || !s_eq[j + 1]) continue;               // not the first key of a >= 2 run
+    int L = 2;
+#pragma unroll
+    for (int t = 2; t <= kRunShort; ++t) L += (L == t && s_eq[j + t]) ? 1 : 0;
+    if (L == 2) {
+      const uint64_t a = s_k[j], b = s_k[j + 1];
+      if (b < a) {
+        s_k[j] = b;
+        s_k[j + 1] = a;
+        s_chg[j] = s_chg[j + 1] = 1;
+      }
+    } else if (L <= 4) {
+      s_c4[atomicAdd(&s_n[0], 1)] = j | (L << 16);
+    } else if (L <= 8) {
+      s_c8[atomicAdd(&s_n[1], 1)] = j | (L << 16);
+    } else if (L <= kRunShort) {
+      s_c16[atomicAdd(&s_n[2], 1)] = j | (L << 16);
+    } else {
+      s_mid[atomicAdd(&s_nmid, 1)] = j;
+    }
+  }
+  __syncthreads();
+  gb_class_runs<4>(s_c4, s_n[0], s_k, s_chg, lmask);
+  gb_class_runs<8>(s_c8, s_n[1], s_k, s_chg, lmask);
+  gb_class_runs<16>(s_c16, s_n[2], s_k, s_chg, lmask);
+  __syncthreads();
+  // runs of kRunShort + 1 .. kRunMid keys: one wave each
+  const int nmid = s_nmid;
+  for (int m = wid; m < nmid; m += kRunT / 64) {
+    const int j = s_mid[m];
+    // L = first e >= 1 with s_eq[j + e] == 0 (the run is a prefix); kRunMid + 1: longer
+    constexpr int R = kRunMid / 64;
+    int zl = R;
+#pragma unroll
+    for (int r = R - 1; r >= 0; --r) {
+      const int e = 1 + lane * R + r;                      // e = 1 .. kRunMid
+      if (!s_eq[j + e]) zl = r;
+    }
+    const uint64_t zb = __ballot(zl < R);
+    int L;
+    if (zb == 0) {
+      L = kRunMid + 1;
+    } else {
+      const int fl = __ffsll((long long)zb) - 1;
+      L = 1 + fl * R + __shfl(zl, fl, 64);
+    }
+    if (L > kRunMid) {
+      if (lane == 0) s_long[atomicAdd(&s_nlong, 1)] = j;
+      continue;
+    }
+    if (L <= 64) gb_wave_rank_run(s_k, s_chg, j, L, lane, lmask);
+    else gb_wave_run<R>(s_k, s_chg, j, L, lane, lmask);
+  }
+  __syncthreads();
+  // coalesced write-out of the rewritten keys (tile and halo: a run started here may reach
+  // into the next tile, whose block never rewrites it)
+  for (int j = threadIdx.x; j < W; j += kRunT)
+    if (s_chg[j]) K[base + j] = s_k[j];
+  // longer runs: appended to the global list, one atomic per block that has any
+  const int nl = s_nlong;
+  if (nl) {
+    if (threadIdx.x == 0) s_lbase = atomicAdd(nlong, (unsigned long long)nl);
+    __syncthreads();
+    if (threadIdx.x < nl) longs[s_lbase + threadIdx.x] = base + s_long[threadIdx.x];
+  }
+}
+
+// one block per listed run (block-uniform loop over the device count): histogram of the
+// low offsets, exclusive scan, the run rewritten in offset order (copies kept adjacent)
+__global__ void __launch_bounds__(kRunT) gb_run_long_kernel(uint64_t* __restrict__ K, int64_t n, int lo_bits,
+                                                            const int64_t* __restrict__ longs,
+                                                            const unsigned long long* __restrict__ nlong) {
+  __shared__ __attribute__((aligned(16))) uint32_t h[kSpan];
+  __shared__ int s_len[2][kRunT / 64];
+  __shared__ uint32_t s_ws[kRunT / 64];
+  constexpr int PER = kSpan / kRunT;                  // histogram words per thread
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nv = 1 << lo_bits;                        // <= kSpan (launcher checks)
+  const uint64_t lmask = (uint64_t)nv - 1ull;
+  const int64_t cnt = (int64_t)*nlong;
+  for (int64_t r = blockIdx.x; r < cnt; r += gridDim.x) {
+    const int64_t p = longs[r];
+    const uint64_t hi = K[p] & ~lmask;
+    for (int j = threadIdx.x; j < kSpan / 4; j += kRunT) reinterpret_cast<uint4*>(h)[j] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    // one pass over the run, 256 keys per step: histogram of the in-run offsets and the
+    // equal-prefix count from per-wave ballots (double-buffered: one barrier per step)
+    int64_t L = 0;
+    for (int buf = 0;; buf ^= 1) {
+      const int64_t q = p + L + threadIdx.x;
+      const uint64_t k = q < n ? K[q] : ~0ull;          // ~0: no key's high bits (keys < 2^63)
+      const bool in = (k & ~lmask) == hi;
+      if (in) atomicAdd(&h[(int)(k & lmask)], 1u);
+      const uint64_t b = __ballot(in);
+      if (lane == 0) s_len[buf][wid] = __popcll(b);
+      __syncthreads();
+      int step = 0;
+#pragma unroll
+      for (int w = 0; w < kRunT / 64; ++w) step += s_len[buf][w];
+      L += step;
+      if (step < kRunT) break;                         // keys equal above lo_bits are contiguous
+    }
+    // exclusive scan of h[0 .. nv): PER consecutive words per thread
+    uint32_t c[PER], s = 0;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int v = threadIdx.x * PER + u;
+      c[u] = v < nv ? h[v] : 0u;
+      s += c[u];
+    }
+    uint32_t x = s;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) s_ws[wid] = x;
+    __syncthreads();
+    uint32_t ofs = x - s;
+#pragma unroll
+    for (int w = 0; w < kRunT / 64; ++w) ofs += w < wid ? s_ws[w] : 0u;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const uint64_t key = hi | (uint64_t)(threadIdx.x * PER + u);
+      for (uint32_t m = 0; m < c[u]; ++m) K[p + ofs + m] = key;
+      ofs += c[u];
+    }
+    __syncthreads();                                   // h and s_ws reused by the next run
+  }
+}
+
 }  // namespace
 }  // namespace dalgo
 
@@ -776,6 +1081,30 @@ hipError_t dalgo_gb_sort(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint6
                          int begin_bit, int end_bit, hipStream_t st) {
   if (n < 0 || end_bit < 1 || end_bit > 64 || begin_bit < 0 || begin_bit >= end_bit) return hipErrorInvalidValue;
   return rocprim::radix_sort_keys(tmp, *tmp_bytes, in, out, (size_t)n, (unsigned)begin_bit, (unsigned)end_bit, st);
+}
+
+// keys sorted on bits [lo_bits, 64): every run of keys equal there sorted on its low
+// lo_bits in place (lo_bits <= 13). longs: int64[n / (kRunShort + 1) + 1] workspace,
+// nlong: one u64 counter (zeroed here); no host synchronisation.
+// ws: int64[dalgo_gb_run_ws(n)] workspace = [long-run count, long-run list]
+int64_t dalgo_gb_run_ws(int64_t n) { return 1 + n / (kRunMid + 1) + 1; }
+
+hipError_t dalgo_gb_run_sort(uint64_t* K, int64_t n, int lo_bits, int64_t* ws, hipStream_t st) {
+  if (n <= 1) return hipSuccess;
+  if (lo_bits < 1 || lo_bits > kSpanBits) return hipErrorInvalidValue;
+  const int64_t g = cdiv(n, (int64_t)kRunTile);
+  if (g > 0x7fffffffLL) return hipErrorInvalidValue;
+  auto* nlong = reinterpret_cast<unsigned long long*>(ws);
+  int64_t* longs = ws + 1;
+  hipError_t e = hipMemsetAsync(ws, 0, sizeof(int64_t), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(gb_run_tile_kernel, dim3((unsigned)g), dim3(kRunT), 0, st, K, n, lo_bits, longs, nlong);
+  DALGO_LAUNCH_CHECK();
+  // 4 blocks of 32 KB LDS per CU: one resident round
+  hipLaunchKernelGGL(gb_run_long_kernel, dim3(1024), dim3(kRunT), 0, st, K, n, lo_bits,
+                     (const int64_t*)longs, (const unsigned long long*)nlong);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
 }
 
 hipError_t dalgo_gb_relabel_src(uint64_t* packed, int64_t n, const int32_t* new_id, hipStream_t st) {

@@ -230,6 +230,8 @@ hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, cons
                          int64_t base_all, uint64_t* keys, const uint64_t* packed, hipStream_t st);
 hipError_t dalgo_gb_sort(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, int64_t n,
                          int begin_bit, int end_bit, hipStream_t st);
+int64_t dalgo_gb_run_ws(int64_t n);
+hipError_t dalgo_gb_run_sort(uint64_t* K, int64_t n, int lo_bits, int64_t* ws, hipStream_t st);
 int64_t dalgo_gb_decode_blocks(int64_t n);
 hipError_t dalgo_gb_decode(const uint64_t* K, int64_t n, int shift, int dbits, const int64_t* blk_base,
                            int phase, int64_t* counts, uint32_t* outdeg, const int64_t* offsets,

@@ -537,6 +537,16 @@ def build_phase_spans() -> dict:
     return out
 
 
+def sort_split_bits(nbits: int) -> int:
+    """Low key bits left to the in-place run sort (graph_build.hip gb_run_sort): the radix
+    sort covers the bits above the source offset in whole 8-bit passes, extended down into
+    the offset as far as its last pass has room (12 of 52 bits at scale 26)."""
+    if nbits <= SRC_BITS:
+        return 0
+    passes = (nbits - SRC_BITS + 7) // 8
+    return max(0, nbits - 8 * passes)
+
+
 def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: torch.Tensor | None = None,
                  bin_width: int = 16384, tile: int = 16384, items: int = 2048,
                  min_piece: int = 1 << 14, keep_keys: bool = False,
@@ -643,7 +653,12 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     _mark("keys")
     K = torch.empty_like(keys)
     if total:
-        ops.gb_sort(keys, total, nbits, K)
+        # whole radix passes over the bits above the source offset (5 instead of 7 at scale
+        # 26: bits 12..51), then each run of keys equal there sorted in place on the rest
+        lo = sort_split_bits(nbits)
+        ops.gb_sort(keys, total, nbits, K, lo)
+        if lo:
+            ops.gb_run_sort(K, total, lo)
     del keys
     _mark("sort")
     n_src_loc = (sl + n_ghost) if W > 1 else max(N, 1)
