@@ -1,42 +1,49 @@
-"""Build an A/B variant of the extension: the given kernel sources recompiled with extra
-preprocessor flags, linked with the other objects of the in-tree build into
-``dalgo/_xp_<name>.so`` (load it with DALGO_EXT_LIB=...). Timing experiments only.
+"""Build an experiment copy of the extension with one kernel source patched, relinked as
+``bench/variants/<name>.so``; a probe run with ``DALGO_EXT_LIB=bench/variants/<name>.so``
+(dalgo/ops/_ext.py) loads it while the tree keeps one code path. Patches are literal
+(old -> new) replacements that must match.
 
-    python bench/probes/build_variant.py NAME kmeans -DKM_XP_FOO [...]
-
-BV_SRC_<stem>=path compiles that file instead of csrc/kernels/<stem>.hip (e.g. an older
-revision: git show HEAD~1:csrc/kernels/kmeans.hip > /tmp/old.hip).
+    python bench/probes/build_variant.py NAME csrc/kernels/X.hip 'old' 'new' ['old' 'new' ...]
 """
-import os
 import subprocess
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
-from dalgo import _build as B   # noqa: E402
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+from dalgo import _build   # noqa: E402
 
 
-def main():
-    name, stems, flags = sys.argv[1], sys.argv[2].split(","), sys.argv[3:]
-    B.build()
-    objs = []
-    for src in B.kernel_sources():
-        if src.stem in stems:
-            obj = B.BUILD / f"{src.stem}.xp_{name}.o"
-            B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-fPIC", "-std=c++17",
-                    f"-I{B.CSRC / 'include'}", f"-I{B.CSRC}", "-munsafe-fp-atomics", *flags,
-                    "-c", os.environ.get(f"BV_SRC_{src.stem}", src), "-o", obj], False)
-            objs.append(obj)
-        else:
-            objs.append(B.BUILD / f"{src.stem}.o")
-    objs.append(B.BUILD / "bindings.o")
-    tdir, tinc, tlib = B._torch_paths()
-    out = B.ROOT / "dalgo" / f"_xp_{name}.so"
-    B._run([B._hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", out,
-            f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch",
-            f"-Wl,-rpath,{tlib}", f"-L{B.ROCM / 'lib'}", "-lamdhip64", "-Wl,--no-undefined"], False)
-    print(out)
+def main(argv):
+    name, src, pairs = argv[0], ROOT / argv[1], argv[2:]
+    if len(pairs) % 2:
+        raise SystemExit("patches come in (old, new) pairs")
+    _build.build()
+    text = src.read_text()
+    for old, new in zip(pairs[::2], pairs[1::2]):
+        if old not in text:
+            raise SystemExit(f"patch does not match: {old[:60]!r}")
+        text = text.replace(old, new, 1)
+    out = ROOT / "bench" / "variants"
+    out.mkdir(parents=True, exist_ok=True)
+    vsrc = out / f"{name}_{src.name}"
+    vsrc.write_text(text)
+    obj = out / f"{name}_{src.stem}.o"
+    hipcc = _build._hipcc()
+    common = ["-O3", "-fPIC", "-std=c++17", f"-I{_build.CSRC / 'include'}", f"-I{_build.CSRC}"]
+    subprocess.run([hipcc, f"--offload-arch={_build.ARCH}", *common, "-munsafe-fp-atomics", "-c", str(vsrc),
+                    "-o", str(obj)], check=True)
+    objs = [str(obj) if p.stem == src.stem else str(_build.BUILD / (p.stem + ".o"))
+            for p in _build.kernel_sources()] + [str(_build.BUILD / "bindings.o")]
+    _, _, tlib = _build._torch_paths()
+    subprocess.run([hipcc, f"--offload-arch={_build.ARCH}", "-shared", "-fPIC", *objs, "-o",
+                    str(out / f"{name}.so"), f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip",
+                    "-ltorch", f"-Wl,-rpath,{tlib}", f"-L{_build.ROCM / 'lib'}", "-lamdhip64",
+                    "-Wl,--no-undefined"], check=True)
+    vsrc.unlink()
+    obj.unlink()
+    print(f"[variant] {out / (name + '.so')}")
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -10,13 +10,15 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.append(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from dalgo.apps.pagerank_app import build_rmat_native, rmat_input   # noqa: E402
 from dalgo.ops import _ext                                           # noqa: E402
 from dalgo.ops import graph as G                                     # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--scale", type=int, default=26)
+ap.add_argument("--no-census", action="store_true", help="skip the run-length histogram")
+ap.add_argument("--lo-bits", type=int, default=None, help="split point (default: build_native's)")
 a = ap.parse_args()
 dev = torch.device("cuda")
 edges, _ = rmat_input(a.scale, 16, dev, seed=1)
@@ -25,20 +27,21 @@ del edges
 K = ng.keys[: ng.n_keys] if hasattr(ng, "n_keys") else ng.keys
 n = K.numel()
 nbits = ng.key_shift + max(1, (int(ng.blk_base.numel()) - 1).bit_length())   # as build_native
-lo_bits = G.sort_split_bits(nbits)
-hi = K >> lo_bits
-_, cnt = torch.unique_consecutive(hi, return_counts=True)
-del hi
-edges_b = [1, 2, 4, 8, 16, 64, 256, 1024, 8192, 1 << 40]
-hist = {}
-lo = 0
-for e in edges_b:
-    m = (cnt > lo) & (cnt <= e)
-    hist[f"{lo + 1}-{e}"] = {"runs": int(m.sum()), "keys": int(cnt[m].sum())}
-    lo = e
-print(json.dumps({"n_keys": n, "nbits": nbits, "lo_bits": lo_bits, "runs": int(cnt.numel()), "max_run": int(cnt.max()),
-                  "hist": hist}))
-del cnt
+lo_bits = G.sort_split_bits(nbits) if a.lo_bits is None else a.lo_bits
+if not a.no_census:
+    hi = K >> lo_bits
+    _, cnt = torch.unique_consecutive(hi, return_counts=True)
+    del hi
+    edges_b = [1, 2, 4, 8, 16, 64, 256, 1024, 8192, 1 << 40]
+    hist = {}
+    lo = 0
+    for e in edges_b:
+        m = (cnt > lo) & (cnt <= e)
+        hist[f"{lo + 1}-{e}"] = {"runs": int(m.sum()), "keys": int(cnt[m].sum())}
+        lo = e
+    print(json.dumps({"n_keys": n, "nbits": nbits, "lo_bits": lo_bits, "runs": int(cnt.numel()),
+                      "max_run": int(cnt.max()), "hist": hist}))
+    del cnt
 ops = _ext.ops()
 perm = K[torch.randperm(n, device=dev)]
 out = torch.empty_like(perm)

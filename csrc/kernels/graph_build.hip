@@ -831,6 +831,20 @@ __device__ __forceinline__ void gb_wave_rank_run(uint64_t* s_k, uint8_t* s_chg, 
   }
 }
 
+// consecutive set bits of the bitmap from bit q on, counted up to at least `limit` (the
+// bitmap ends with a zero word)
+__device__ __forceinline__ int gb_ones_from(const uint64_t* eqb, int q, int limit) {
+  int c = 0;
+  for (;;) {
+    const int b = q & 63;
+    const uint64_t inv = ~(eqb[q >> 6] >> b);            // ones above the 64 - b valid bits
+    const int t = inv ? __builtin_ctzll(inv) : 64;
+    c += t;
+    if (t < 64 - b || c > limit) return c;
+    q += t;
+  }
+}
+
 __global__ void __launch_bounds__(kRunT) gb_run_tile_kernel(uint64_t* __restrict__ K, int64_t n, int lo_bits,
                                                             int64_t* __restrict__ longs,
                                                             unsigned long long* __restrict__ nlong) {
@@ -838,7 +852,9 @@ __global__ void __launch_bounds__(kRunT) gb_run_tile_kernel(uint64_t* __restrict
   constexpr int kMaxMid = kRunTile / (kRunShort + 1) + 1;
   constexpr int kMaxLong = kRunTile / (kRunMid + 1) + 1;
   __shared__ __attribute__((aligned(16))) uint64_t s_k[W];
-  __shared__ uint8_t s_eq[W];                  // key j equal to key j - 1 above lo_bits
+  constexpr int kEqW = (W + kRunT - 1) / kRunT * (kRunT / 64) + 1;
+  // bit j: key j equal to key j - 1 above lo_bits (one ballot per 64 keys; a zero spare word)
+  __shared__ uint64_t s_eqb[kEqW];
   __shared__ uint8_t s_chg[W];                 // key j rewritten
   __shared__ int s_mid[kMaxMid];
   __shared__ int s_long[kMaxLong];
@@ -849,7 +865,7 @@ __global__ void __launch_bounds__(kRunT) gb_run_tile_kernel(uint64_t* __restrict
   const int64_t base = (int64_t)blockIdx.x * kRunTile;   // even: 16-B aligned pairs
   const uint64_t lmask = (1ull << lo_bits) - 1ull;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) { s_nmid = 0; s_nlong = 0; s_n[0] = s_n[1] = s_n[2] = 0; }
+  if (threadIdx.x == 0) { s_nmid = 0; s_nlong = 0; s_n[0] = s_n[1] = s_n[2] = 0; s_eqb[kEqW - 1] = 0ull; }
   // keys past n: ~0 (its high bits equal no key's: keys are < 2^63)
   for (int j = 2 * threadIdx.x; j < W; j += 2 * kRunT) {
     const int64_t p = base + j;
@@ -866,19 +882,25 @@ __global__ void __launch_bounds__(kRunT) gb_run_tile_kernel(uint64_t* __restrict
   }
   const uint64_t kprev = base > 0 ? K[base - 1] : ~0ull;
   __syncthreads();
-  for (int j = threadIdx.x; j < W; j += kRunT) {
-    const uint64_t pk = j ? s_k[j - 1] : kprev;
-    s_eq[j] = base + j < n && ((pk ^ s_k[j]) >> lo_bits) == 0;
-    s_chg[j] = 0;
+  for (int j = threadIdx.x; j < (kEqW - 1) * 64; j += kRunT) {
+    bool eq = false;
+    if (j < W) {
+      const uint64_t pk = j ? s_k[j - 1] : kprev;
+      eq = base + j < n && ((pk ^ s_k[j]) >> lo_bits) == 0;
+      s_chg[j] = 0;
+    }
+    const uint64_t b = __ballot(eq);
+    if (lane == 0) s_eqb[j >> 6] = b;
   }
   __syncthreads();
   // runs of 2 keys: the thread at the first key; 3 .. kRunShort: listed by size class (so
-  // each network below runs on full waves, not on the union of a wave's run sizes)
+  // each network below runs on full waves, not on the union of a wave's run sizes). The
+  // starts of a wave's 64 keys come from two bitmap words: ~E & (E >> 1 | next << 63).
   for (int j = threadIdx.x; j < kRunTile; j += kRunT) {
-    if (s_eq[j] || !s_eq[j + 1]) continue;               // not the first key of a >= 2 run
-    int L = 2;
-#pragma unroll
-    for (int t = 2; t <= kRunShort; ++t) L += (L == t && s_eq[j + t]) ? 1 : 0;
+    const uint64_t E = s_eqb[j >> 6], En = s_eqb[(j >> 6) + 1];
+    const uint64_t S = ~E & ((E >> 1) | (En << 63));
+    if (!((S >> lane) & 1ull)) continue;                 // not the first key of a >= 2 run
+    const int L = 1 + gb_ones_from(s_eqb, j + 1, kRunShort);
     if (L == 2) {
       const uint64_t a = s_k[j], b = s_k[j + 1];
       if (b < a) {
@@ -905,22 +927,8 @@ __global__ void __launch_bounds__(kRunT) gb_run_tile_kernel(uint64_t* __restrict
   const int nmid = s_nmid;
   for (int m = wid; m < nmid; m += kRunT / 64) {
     const int j = s_mid[m];
-    // L = first e >= 1 with s_eq[j + e] == 0 (the run is a prefix); kRunMid + 1: longer
     constexpr int R = kRunMid / 64;
-    int zl = R;
-#pragma unroll
-    for (int r = R - 1; r >= 0; --r) {
-      const int e = 1 + lane * R + r;                      // e = 1 .. kRunMid
-      if (!s_eq[j + e]) zl = r;
-    }
-    const uint64_t zb = __ballot(zl < R);
-    int L;
-    if (zb == 0) {
-      L = kRunMid + 1;
-    } else {
-      const int fl = __ffsll((long long)zb) - 1;
-      L = 1 + fl * R + __shfl(zl, fl, 64);
-    }
+    const int L = 1 + gb_ones_from(s_eqb, j + 1, kRunMid);   // kRunMid + 1: longer
     if (L > kRunMid) {
       if (lane == 0) s_long[atomicAdd(&s_nlong, 1)] = j;
       continue;
