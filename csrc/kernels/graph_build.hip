@@ -707,56 +707,15 @@ __global__ void __launch_bounds__(256) gb_entry_cells_kernel(
 // longer, profiles/round5/r5_44) are then sorted on their low lo_bits in place, which makes
 // the copies of an edge adjacent again for the decode's dedup. One block stages a tile of
 // keys plus a halo in LDS, sorts the runs starting in its tile there and writes the changed
-// keys back coalesced: a run of 2 keys by the thread at its first key, 3..kRunShort keys
-// by one thread per run from size-class lists (min/max networks of 4 / 8 / 16 in
-// registers), <= kRunMid keys by one wave (bitonic network over registers and lane
-// shuffles); a longer one is listed (one global atomic per block that has any) and
+// keys back coalesced: a run of <= kRankMax keys by per-key ranks (each key's thread counts
+// the run's keys below it), <= kRunMid keys by one wave (bitonic network over registers
+// and lane shuffles); a longer one is listed (one global atomic per block that has any) and
 // counting-sorted by one block of gb_run_long_kernel over an LDS histogram of the
 // 2^lo_bits offsets. No per-run global atomics: 6.6M of them on one counter took ~60 ms.
-constexpr int kRunShort = 16;
-constexpr int kRunMid = 256;
+constexpr int kRankMax = 64;         // runs sorted by per-key ranks
+constexpr int kRunMid = 256;          // runs sorted by one wave's network
 constexpr int kRunTile = 2048;        // run starts per block of the tile kernel
 constexpr int kRunT = 256;
-
-template <int N>
-__device__ __forceinline__ void gb_net_sort(uint32_t (&v)[kRunShort]) {
-  // bitonic sorting network on v[0 .. N), ascending (N a power of two, indices static)
-#pragma unroll
-  for (int k = 2; k <= N; k <<= 1)
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1)
-#pragma unroll
-      for (int i = 0; i < N; ++i) {
-        const int l = i ^ j;
-        if (l > i) {
-          const uint32_t a = v[i], b = v[l];
-          const bool up = (i & k) == 0;
-          v[i] = up ? min(a, b) : max(a, b);
-          v[l] = up ? max(a, b) : min(a, b);
-        }
-      }
-}
-
-// the listed runs of one size class (entry = j | L << 16, 2 < L <= N): one thread per run,
-// an N-key network over the run's low bits, the run rewritten in the staged keys
-template <int N>
-__device__ __forceinline__ void gb_class_runs(const int* list, int cnt, uint64_t* s_k, uint8_t* s_chg,
-                                              uint64_t lmask) {
-  for (int i = threadIdx.x; i < cnt; i += kRunT) {
-    const int j = list[i] & 0xffff, L = list[i] >> 16;
-    uint32_t v[kRunShort], o[kRunShort];
-#pragma unroll
-    for (int t = 0; t < N; ++t) o[t] = v[t] = t < L ? (uint32_t)(s_k[j + t] & lmask) : 0xffffffffu;
-    gb_net_sort<N>(v);
-    const uint64_t hi = s_k[j] & ~lmask;
-#pragma unroll
-    for (int t = 0; t < N; ++t)
-      if (t < L && v[t] != o[t]) {
-        s_k[j + t] = hi | v[t];
-        s_chg[j + t] = 1;
-      }
-  }
-}
 
 // ascending bitonic sort of the 64 * R values of a wave, element lane * R + r in v[r]
 template <int R>
@@ -812,25 +771,6 @@ __device__ __forceinline__ void gb_wave_run(uint64_t* s_k, uint8_t* s_chg, int j
   }
 }
 
-// one wave: a run of 17..64 keys at tile offset j, lane e holding key e; its place is its
-// rank (keys below it, ties by position: stable) from L broadcasts of one register --
-// no LDS round trips, L iterations instead of the 21 shuffle stages of a 64-key network
-__device__ __forceinline__ void gb_wave_rank_run(uint64_t* s_k, uint8_t* s_chg, int j, int L, int lane,
-                                                 uint64_t lmask) {
-  const uint64_t hi = s_k[j] & ~lmask;
-  const uint32_t v = lane < L ? (uint32_t)(s_k[j + lane] & lmask) : 0xffffffffu;
-  int rank = 0;
-  for (int i = 0; i < L; ++i) {
-    const uint32_t u = __builtin_amdgcn_readlane(v, i);
-    rank += (u < v || (u == v && i < lane)) ? 1 : 0;
-  }
-  const uint32_t was = __shfl(v, rank & 63, 64);          // the key at position rank before
-  if (lane < L && was != v) {
-    s_k[j + rank] = hi | v;
-    s_chg[j + rank] = 1;
-  }
-}
-
 // consecutive set bits of the bitmap from bit q on, counted up to at least `limit` (the
 // bitmap ends with a zero word)
 __device__ __forceinline__ int gb_ones_from(const uint64_t* eqb, int q, int limit) {
@@ -849,7 +789,7 @@ __global__ void __launch_bounds__(kRunT) gb_run_tile_kernel(uint64_t* __restrict
                                                             int64_t* __restrict__ longs,
                                                             unsigned long long* __restrict__ nlong) {
   constexpr int W = kRunTile + kRunMid + 2;    // keys staged: the tile, a halo, one spare
-  constexpr int kMaxMid = kRunTile / (kRunShort + 1) + 1;
+  constexpr int kMaxMid = kRunTile / (kRankMax + 1) + 1;
   constexpr int kMaxLong = kRunTile / (kRunMid + 1) + 1;
   __shared__ __attribute__((aligned(16))) uint64_t s_k[W];
   constexpr int kEqW = (W + kRunT - 1) / kRunT * (kRunT / 64) + 1;
@@ -858,14 +798,12 @@ __global__ void __launch_bounds__(kRunT) gb_run_tile_kernel(uint64_t* __restrict
   __shared__ uint8_t s_chg[W];                 // key j rewritten
   __shared__ int s_mid[kMaxMid];
   __shared__ int s_long[kMaxLong];
-  __shared__ int s_c4[kRunTile / 3 + 1], s_c8[kRunTile / 5 + 1], s_c16[kRunTile / 9 + 1];
-  __shared__ int s_n[3];
   __shared__ int s_nmid, s_nlong;
   __shared__ unsigned long long s_lbase;
   const int64_t base = (int64_t)blockIdx.x * kRunTile;   // even: 16-B aligned pairs
   const uint64_t lmask = (1ull << lo_bits) - 1ull;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) { s_nmid = 0; s_nlong = 0; s_n[0] = s_n[1] = s_n[2] = 0; s_eqb[kEqW - 1] = 0ull; }
+  if (threadIdx.x == 0) { s_nmid = 0; s_nlong = 0; s_eqb[kEqW - 1] = 0ull; }
   // keys past n: ~0 (its high bits equal no key's: keys are < 2^63)
   for (int j = 2 * threadIdx.x; j < W; j += 2 * kRunT) {
     const int64_t p = base + j;
@@ -893,37 +831,54 @@ __global__ void __launch_bounds__(kRunT) gb_run_tile_kernel(uint64_t* __restrict
     if (lane == 0) s_eqb[j >> 6] = b;
   }
   __syncthreads();
-  // runs of 2 keys: the thread at the first key; 3 .. kRunShort: listed by size class (so
-  // each network below runs on full waves, not on the union of a wave's run sizes). The
-  // starts of a wave's 64 keys come from two bitmap words: ~E & (E >> 1 | next << 63).
-  for (int j = threadIdx.x; j < kRunTile; j += kRunT) {
-    const uint64_t E = s_eqb[j >> 6], En = s_eqb[(j >> 6) + 1];
-    const uint64_t S = ~E & ((E >> 1) | (En << 63));
-    if (!((S >> lane) & 1ull)) continue;                 // not the first key of a >= 2 run
-    const int L = 1 + gb_ones_from(s_eqb, j + 1, kRunShort);
-    if (L == 2) {
-      const uint64_t a = s_k[j], b = s_k[j + 1];
-      if (b < a) {
-        s_k[j] = b;
-        s_k[j + 1] = a;
-        s_chg[j] = s_chg[j + 1] = 1;
-      }
-    } else if (L <= 4) {
-      s_c4[atomicAdd(&s_n[0], 1)] = j | (L << 16);
-    } else if (L <= 8) {
-      s_c8[atomicAdd(&s_n[1], 1)] = j | (L << 16);
-    } else if (L <= kRunShort) {
-      s_c16[atomicAdd(&s_n[2], 1)] = j | (L << 16);
-    } else {
-      s_mid[atomicAdd(&s_nmid, 1)] = j;
+  // runs of 2 .. kRankMax keys: every key's place is its rank in its run (keys below it,
+  // ties by position: stable), counted by the key's own thread over the run's staged low
+  // bits (lanes of one run read the same LDS words: broadcasts); the run of key q starts
+  // at the last zero bit of the bitmap at or below q. The ranks of a thread's keys are
+  // held in registers and the keys moved after a barrier. A longer run is listed by the
+  // thread at its first key for the wave tier below.
+  constexpr int NQ = (kRunTile + kRankMax + kRunT - 1) / kRunT;
+  const uint32_t* klo = reinterpret_cast<const uint32_t*>(s_k);   // low words (little endian)
+  int tgt[NQ];
+  uint64_t kv[NQ];
+#pragma unroll
+  for (int it = 0; it < NQ; ++it) {
+    const int q = it * kRunT + threadIdx.x;
+    tgt[it] = -1;
+    int w = q >> 6;
+    uint64_t z = ~s_eqb[w] & ((q & 63) == 63 ? ~0ull : ((2ull << (q & 63)) - 1ull));
+#pragma unroll
+    for (int k = 0; k < kRankMax / 64; ++k)              // a run of <= kRankMax keys: its start
+      if (!z && w > 0) z = ~s_eqb[--w];                  // is <= kRankMax / 64 words back
+    if (!z) continue;                                    // started in the previous tile, or longer
+    const int st = w * 64 + 63 - __builtin_clzll(z);
+    if (st >= kRunTile || q - st >= kRankMax) continue;  // the next block's run, or longer
+    const int L = 1 + gb_ones_from(s_eqb, st + 1, kRankMax);
+    if (L > kRankMax) {
+      if (q == st) s_mid[atomicAdd(&s_nmid, 1)] = st;
+      continue;
+    }
+    if (L == 1) continue;
+    const uint32_t v = klo[2 * q] & (uint32_t)lmask;
+    int rank = 0;
+    for (int i = 0; i < L; ++i) {
+      const uint32_t u = klo[2 * (st + i)] & (uint32_t)lmask;
+      rank += (u < v || (u == v && st + i < q)) ? 1 : 0;
+    }
+    if (st + rank != q) {
+      tgt[it] = st + rank;
+      kv[it] = s_k[q];
     }
   }
   __syncthreads();
-  gb_class_runs<4>(s_c4, s_n[0], s_k, s_chg, lmask);
-  gb_class_runs<8>(s_c8, s_n[1], s_k, s_chg, lmask);
-  gb_class_runs<16>(s_c16, s_n[2], s_k, s_chg, lmask);
+#pragma unroll
+  for (int it = 0; it < NQ; ++it)
+    if (tgt[it] >= 0) {
+      s_k[tgt[it]] = kv[it];
+      s_chg[tgt[it]] = 1;
+    }
   __syncthreads();
-  // runs of kRunShort + 1 .. kRunMid keys: one wave each
+  // runs of kRankMax + 1 .. kRunMid keys: one wave each (bitonic network); longer: listed
   const int nmid = s_nmid;
   for (int m = wid; m < nmid; m += kRunT / 64) {
     const int j = s_mid[m];
@@ -933,8 +888,7 @@ __global__ void __launch_bounds__(kRunT) gb_run_tile_kernel(uint64_t* __restrict
       if (lane == 0) s_long[atomicAdd(&s_nlong, 1)] = j;
       continue;
     }
-    if (L <= 64) gb_wave_rank_run(s_k, s_chg, j, L, lane, lmask);
-    else gb_wave_run<R>(s_k, s_chg, j, L, lane, lmask);
+    gb_wave_run<R>(s_k, s_chg, j, L, lane, lmask);
   }
   __syncthreads();
   // coalesced write-out of the rewritten keys (tile and halo: a run started here may reach
@@ -1092,9 +1046,8 @@ hipError_t dalgo_gb_sort(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint6
 }
 
 // keys sorted on bits [lo_bits, 64): every run of keys equal there sorted on its low
-// lo_bits in place (lo_bits <= 13). longs: int64[n / (kRunShort + 1) + 1] workspace,
-// nlong: one u64 counter (zeroed here); no host synchronisation.
-// ws: int64[dalgo_gb_run_ws(n)] workspace = [long-run count, long-run list]
+// lo_bits in place (lo_bits <= 13), no host synchronisation.
+// ws: int64[dalgo_gb_run_ws(n)] workspace = [long-run count (zeroed here), long-run list]
 int64_t dalgo_gb_run_ws(int64_t n) { return 1 + n / (kRunMid + 1) + 1; }
 
 hipError_t dalgo_gb_run_sort(uint64_t* K, int64_t n, int lo_bits, int64_t* ws, hipStream_t st) {

@@ -10,10 +10,12 @@ from dalgo.ops.lr import pad_features
 pytestmark = pytest.mark.gpu
 
 
-def _data(n, D, dtype, seed=0):
-    g = torch.Generator().manual_seed(seed)
-    X = (torch.rand((n, D), generator=g) * 2 - 1).to(dtype)
-    y = (torch.rand(n, generator=g) < 0.5).float()
+def _data(n, D, dtype, seed=0, device=None):
+    """Uniform(-1, 1) rows and 0/1 labels; device=...: generated there (the large cases:
+    1.25M x 1024 on the host took ~5 s of the suite)."""
+    g = torch.Generator(device=device or "cpu").manual_seed(seed)
+    X = (torch.rand((n, D), generator=g, device=device) * 2 - 1).to(dtype)
+    y = (torch.rand(n, generator=g, device=device) < 0.5).float()
     return X, y
 
 
@@ -58,7 +60,7 @@ def test_lr_grad_shapes_and_claims(cuda, fine, D):
 
 
 def test_lr_grad_single_segment_deterministic(cuda):
-    X, y = _data(200_000, 1024, torch.bfloat16, seed=3)
+    X, y = _data(200_000, 1024, torch.bfloat16, seed=3, device=cuda)
     Xd, yd = X.to(cuda), y.to(cuda)
     W = torch.randn(1, 1025, generator=torch.Generator().manual_seed(2)).to(cuda) * 0.05
     seg = torch.tensor([0, X.shape[0]], dtype=torch.int64, device=cuda)
@@ -76,7 +78,7 @@ def test_lr_grad_single_segment_deterministic(cuda):
     L.lr_grad(Xd, yd, W, seg, D=1024, frac=0.1, step=3, G=G0, C=C0, g_is_zero=True)
     assert torch.equal(C0, Ca)
     assert ((G0 - Ga).abs().max() / Ga.abs().max()).item() < 1e-5
-    G_ref, C_ref = L.lr_grad(X, y, W.cpu().double(), seg.cpu(), D=1024, frac=0.1, step=3)
+    G_ref, C_ref = L.lr_grad(X.cpu(), y.cpu(), W.cpu().double(), seg.cpu(), D=1024, frac=0.1, step=3)
     assert float(outs[0][1].item()) == float(C_ref.item())
     rel = (outs[0][0].cpu().double() - G_ref).abs().max() / G_ref.abs().max()
     assert rel < 1e-4
@@ -164,8 +166,8 @@ def test_rows_sum_broadcast(cuda):
 @pytest.mark.parametrize("mode,reg", [(0, 0), (0, 3), (1, 0)])
 def test_lr_grad_fused_tail_single_rank(cuda, mode, reg):
     """One-launch step (gradient + update in the last block) == lr_grad + K8."""
-    X, y = _data(300_000, 1024, torch.bfloat16, seed=11)
-    Xd, yd = X.to(cuda), y.to(cuda)
+    Xd, yd = _data(300_000, 1024, torch.bfloat16, seed=11, device=cuda)
+    X = Xd
     seg = torch.tensor([0, X.shape[0]], dtype=torch.int64, device=cuda)
     w0 = torch.randn(1, 1025, generator=torch.Generator().manual_seed(4)).to(cuda) * 0.05
     kw = dict(D=1024, frac=0.1, eps=0.0, seed=42)
@@ -196,8 +198,7 @@ def test_lr_grad_fused_tail_single_rank(cuda, mode, reg):
 def test_lr_grad_persistent_steps(cuda, mode, reg, n):
     """Persistent launch (K steps in one cooperative grid, epoch-released W) == K
     separate gradient + update steps; the release counter ends at base + K."""
-    X, y = _data(n, 1024, torch.bfloat16, seed=12)
-    Xd, yd = X.to(cuda), y.to(cuda)
+    Xd, yd = _data(n, 1024, torch.bfloat16, seed=12, device=cuda)
     seg = torch.tensor([0, n], dtype=torch.int64, device=cuda)
     w0 = torch.randn(1, 1025, generator=torch.Generator().manual_seed(5)).to(cuda) * 0.05
     kw = dict(D=1024, frac=0.1, eps=0.0, seed=42)
