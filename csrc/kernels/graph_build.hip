@@ -888,7 +888,7 @@ __global__ void __launch_bounds__(kRunT) gb_run_tile_kernel(uint64_t* __restrict
       if (lane == 0) s_long[atomicAdd(&s_nlong, 1)] = j;
       continue;
     }
-    gb_wave_run<R>(s_k, s_chg, j, L, lane, lmask);
+    gb_wave_run<R>(s_k, s_chg, j, L, lane, lmask);   // a 128-key network for <= 128: no gain (r5_56)
   }
   __syncthreads();
   // coalesced write-out of the rewritten keys (tile and halo: a run started here may reach

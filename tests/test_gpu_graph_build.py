@@ -29,13 +29,15 @@ def test_degree_count_matches_bincount(cuda, reorder):
 @pytest.mark.parametrize("lo_bits", [13, 5])
 def test_run_sort_completes_high_bit_sort(cuda, lo_bits):
     """gb_sort over the bits above lo_bits + gb_run_sort (each run of equal high bits sorted
-    on its low bits in place) == a full sort: runs of 1, 2-16 (thread network), 17-256 (wave
-    network), 257-70000 keys (block counting sort, copies kept), runs crossing 2048-key tiles."""
+    on its low bits in place) == a full sort: runs of 1, 2-64 (per-key ranks), 65-256 (wave
+    network), 257-70000 keys (block counting sort, copies kept), runs crossing 2048-key
+    tiles."""
     g = torch.Generator().manual_seed(11)
     parts = [torch.randint(0, 1 << 20, (300_000,), generator=g)]          # mostly runs of 1
     parts.append(torch.randint(0, 1 << 14, (200_000,), generator=g))      # runs of ~12
     for ln, hv in ((17, 1 << 21), (40, (1 << 21) + 1), (300, (1 << 21) + 2), (5000, (1 << 21) + 3),
-                   (70000, (1 << 21) + 4), (256, (1 << 21) + 5), (257, (1 << 21) + 6)):
+                   (70000, (1 << 21) + 4), (256, (1 << 21) + 5), (257, (1 << 21) + 6),
+                   (100, (1 << 21) + 7), (64, (1 << 21) + 8), (65, (1 << 21) + 9)):
         parts.append(torch.full((ln,), hv))
     hi = torch.cat(parts).to(torch.int64)
     lo = torch.randint(0, 1 << lo_bits, (hi.numel(),), generator=g)
