@@ -299,43 +299,39 @@ constexpr int kDecT = 256;
 constexpr int kDecV = 4;             // keys per thread per step (8: decode 11.3 -> 13.1 ms,
                                      // profiles/round5/r5_41)
 
-__device__ __forceinline__ void gb_flags(const uint64_t* __restrict__ K, int64_t n, int64_t i,
-                                         bool& last, bool& end, uint64_t& k) {
-  k = K[i];
-  const bool has_next = i + 1 < n;
-  const uint64_t kn = has_next ? K[i + 1] : ~0ull;
-  last = !has_next || kn != k;
-  end = last && (!has_next || (kn >> kSpanBits) != (k >> kSpanBits));
-}
+// keys ib .. ib + 3 (ib % 4 == 0) and the key after them: two 16-B loads and one 8-B load;
+// positions past n read as ~0 (no key's value: keys are < 2^63). Split from the flags so
+// the decode loops can issue the next step's loads before they work on this one.
+struct GbQuad {
+  uint64_t k[kDecV];
+  uint64_t kn;
+};
 
-// keys ib .. ib + 3 (ib % 4 == 0, < r1 each or flagged out) and their flags: two 16-B loads
-// and one 8-B load of the following key instead of eight 8-B loads
-__device__ __forceinline__ void gb_flags4(const uint64_t* __restrict__ K, int64_t n, int64_t ib, int64_t r1,
-                                          bool (&last)[kDecV], bool (&end)[kDecV], uint64_t (&k)[kDecV]) {
+__device__ __forceinline__ void gb_load4(const uint64_t* __restrict__ K, int64_t n, int64_t ib, GbQuad& q) {
   static_assert(kDecV == 4, "4 keys per thread per step");
-  if (ib + kDecV <= r1) {
+  if (ib + kDecV <= n) {
     const uint4 a = *reinterpret_cast<const uint4*>(K + ib);
     const uint4 b = *reinterpret_cast<const uint4*>(K + ib + 2);
-    k[0] = ((uint64_t)a.y << 32) | a.x;
-    k[1] = ((uint64_t)a.w << 32) | a.z;
-    k[2] = ((uint64_t)b.y << 32) | b.x;
-    k[3] = ((uint64_t)b.w << 32) | b.z;
-    const bool has_next = ib + kDecV < n;
-    const uint64_t kn = has_next ? K[ib + kDecV] : ~0ull;
-#pragma unroll
-    for (int v = 0; v < kDecV; ++v) {
-      const uint64_t nx = v + 1 < kDecV ? k[v + 1] : kn;
-      const bool hn = v + 1 < kDecV || has_next;
-      last[v] = !hn || nx != k[v];
-      end[v] = last[v] && (!hn || (nx >> kSpanBits) != (k[v] >> kSpanBits));
-    }
+    q.k[0] = ((uint64_t)a.y << 32) | a.x;
+    q.k[1] = ((uint64_t)a.w << 32) | a.z;
+    q.k[2] = ((uint64_t)b.y << 32) | b.x;
+    q.k[3] = ((uint64_t)b.w << 32) | b.z;
   } else {
 #pragma unroll
-    for (int v = 0; v < kDecV; ++v) {
-      last[v] = end[v] = false;
-      k[v] = 0;
-      if (ib + v < r1) gb_flags(K, n, ib + v, last[v], end[v], k[v]);
-    }
+    for (int v = 0; v < kDecV; ++v) q.k[v] = ib + v < n ? K[ib + v] : ~0ull;
+  }
+  q.kn = ib + kDecV < n ? K[ib + kDecV] : ~0ull;
+}
+
+// last: the key differs from the next one (the copy that stands for a distinct edge); end:
+// also the last key of its (block, destination) entry. Positions >= r1 are flagged out.
+__device__ __forceinline__ void gb_quad_flags(const GbQuad& q, int64_t ib, int64_t r1, bool (&last)[kDecV],
+                                              bool (&end)[kDecV]) {
+#pragma unroll
+  for (int v = 0; v < kDecV; ++v) {
+    const uint64_t nx = v + 1 < kDecV ? q.k[v + 1] : q.kn;
+    last[v] = ib + v < r1 && nx != q.k[v];
+    end[v] = last[v] && ((nx ^ q.k[v]) >> kSpanBits) != 0;
   }
 }
 
@@ -354,21 +350,28 @@ __global__ void __launch_bounds__(kDecT) gb_decode_count_kernel(const uint64_t* 
   const int64_t r1 = r0 + kDecR < n ? r0 + kDecR : n;
   const uint64_t blk0 = K[r0] >> shift;
   int md = 0, me = 0;
-  for (int64_t ib = r0 + (int64_t)threadIdx.x * kDecV; ib < r1; ib += (int64_t)kDecT * kDecV) {
+  constexpr int64_t kStep = (int64_t)kDecT * kDecV;
+  int64_t ib = r0 + (int64_t)threadIdx.x * kDecV;
+  GbQuad cur;
+  if (ib < r1) gb_load4(K, n, ib, cur);
+  for (; ib < r1; ib += kStep) {
+    GbQuad nxt;
+    const bool more = ib + kStep < r1;
+    if (more) gb_load4(K, n, ib + kStep, nxt);          // in flight while this step works
     bool last[kDecV], end[kDecV];
-    uint64_t k[kDecV];
-    gb_flags4(K, n, ib, r1, last, end, k);
+    gb_quad_flags(cur, ib, r1, last, end);
 #pragma unroll
     for (int v = 0; v < kDecV; ++v) {
       if (last[v]) {
         ++md;
-        const uint64_t blk = k[v] >> shift;
-        const uint32_t off = (uint32_t)(k[v] & (kSpan - 1));
+        const uint64_t blk = cur.k[v] >> shift;
+        const uint32_t off = (uint32_t)(cur.k[v] & (kSpan - 1));
         if (blk == blk0) atomicAdd(hist + off, 1u);
         else atomicAdd(outdeg + blk_base[blk] + off, 1u);
       }
       me += end[v] ? 1 : 0;
     }
+    if (more) cur = nxt;
   }
   atomicAdd(&s_d, md);
   atomicAdd(&s_e, me);
@@ -396,12 +399,18 @@ __global__ void __launch_bounds__(kDecT) gb_decode_write_kernel(const uint64_t* 
   const int64_t r1 = r0 + kDecR < n ? r0 + kDecR : n;
   int64_t dbase = offsets[2 * blockIdx.x], ebase = offsets[2 * blockIdx.x + 1];
   const uint64_t dmask = (1ull << dbits) - 1ull;
-  for (int64_t i0 = r0; i0 < r1; i0 += (int64_t)kDecT * kDecV) {
+  constexpr int64_t kStep = (int64_t)kDecT * kDecV;
+  GbQuad cur;
+  gb_load4(K, n, r0 + (int64_t)threadIdx.x * kDecV, cur);
+  for (int64_t i0 = r0; i0 < r1; i0 += kStep) {
     const int64_t ib = i0 + (int64_t)threadIdx.x * kDecV;
+    GbQuad nxt;
+    const bool more = i0 + kStep < r1;                   // block-uniform
+    if (more) gb_load4(K, n, ib + kStep, nxt);          // in flight while this step works
     bool last[kDecV], end[kDecV];
-    uint64_t k[kDecV];
+    const uint64_t (&k)[kDecV] = cur.k;
     int cd = 0, ce = 0;
-    gb_flags4(K, n, ib, r1, last, end, k);
+    gb_quad_flags(cur, ib, r1, last, end);
 #pragma unroll
     for (int v = 0; v < kDecV; ++v) {
       cd += last[v] ? 1 : 0;
@@ -438,6 +447,7 @@ __global__ void __launch_bounds__(kDecT) gb_decode_write_kernel(const uint64_t* 
     }
     dbase += td;
     ebase += te;
+    if (more) cur = nxt;
     __syncthreads();
   }
 }
