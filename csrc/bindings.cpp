@@ -885,12 +885,15 @@ void gb_keys_packed(const Tensor& packed, const std::optional<Tensor>& new_id, i
 }
 
 // packed (src << 32 | dst) words: src := new_id[src], in place
-void gb_relabel_src(Tensor packed, const Tensor& new_id) {
+// partitioned: packed is sorted on src >> 13 (gb_degree_packed's output), every src <
+// new_id.numel(): one block per 8192-source bucket with its id slice in LDS
+void gb_relabel_src(Tensor packed, const Tensor& new_id, int64_t partitioned) {
   check_t(packed, at::kLong, "packed");
   check_i32(new_id, "new_id");
   DeviceGuard guard(packed.device());
   DALGO_CHECK_HIP(dalgo_gb_relabel_src(reinterpret_cast<uint64_t*>(packed.data_ptr<int64_t>()), packed.numel(),
-                                       new_id.data_ptr<int32_t>(), cur_stream()),
+                                       new_id.data_ptr<int32_t>(), new_id.numel(), (int)partitioned,
+                                       cur_stream()),
                   "gb_relabel_src");
 }
 
@@ -1664,7 +1667,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("gb_sort(Tensor keys, int n, int end_bit, Tensor(a!) out, int begin_bit=0) -> ()");
   m.def("gb_run_sort(Tensor(a!) keys, int n, int lo_bits) -> Tensor");
   m.def("gb_keys_packed(Tensor packed, Tensor? new_id, int n_vertices, int dbits, Tensor(a!) keys, int src_new=0) -> ()");
-  m.def("gb_relabel_src(Tensor(a!) packed, Tensor new_id) -> ()");
+  m.def("gb_relabel_src(Tensor(a!) packed, Tensor new_id, int partitioned=0) -> ()");
   m.def("gb_pack(Tensor src, Tensor dst, Tensor(a!) out) -> ()");
   m.def("gb_degree_packed(Tensor packed, int end_bit, Tensor(a!) deg, Tensor(b!) out) -> ()");
   m.def("gb_degree_sorted(Tensor ids, int end_bit, Tensor(a!) deg) -> ()");

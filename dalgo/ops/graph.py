@@ -164,7 +164,7 @@ def relabel_partition_dst(packed: torch.Tensor, new_id: torch.Tensor, bits: int)
     L2-resident slice of new_id per bucket."""
     ops = _ext.ops()
     n = packed.numel()
-    ops.gb_relabel_src(packed, new_id)
+    ops.gb_relabel_src(packed, new_id, 1)           # bucketed: id slices staged in LDS
     out = torch.empty_like(packed)
     if n:
         # one radix pass over the top 8 destination bits: 2^(bits - 8)-id buckets (1 MB of
