@@ -339,6 +339,46 @@ __global__ void __launch_bounds__(256) gb_keys_write_kernel(const int32_t* __res
   }
 }
 
+// one rank, packed (src << 32 | dst) edges with relabelled sources: every edge is kept, so
+// key i is written at i (no compaction) and the key is three fields: source block, new
+// destination, source offset. 8 edges per thread per step (four 16-B loads, 8 gathers,
+// four 16-B stores); the general kernel's wave scan and per-lane stores cost 12.9 ms (r5_42)
+__global__ void __launch_bounds__(256) gb_keys_one_kernel(const uint64_t* __restrict__ packed, int64_t n,
+                                                          const int32_t* __restrict__ new_id, int dbits,
+                                                          uint64_t* __restrict__ keys) {
+  constexpr int V = 8;
+  const int64_t stride = (int64_t)gridDim.x * 256 * V;
+  const int sh = dbits + kSpanBits;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V; i < n; i += stride) {
+    if (i + V <= n) {
+      uint4 q[V / 2];
+#pragma unroll
+      for (int u = 0; u < V / 2; ++u) q[u] = reinterpret_cast<const uint4*>(packed + i)[u];
+      uint32_t d[V];
+#pragma unroll
+      for (int u = 0; u < V / 2; ++u) {
+        d[2 * u] = (uint32_t)new_id[q[u].x];
+        d[2 * u + 1] = (uint32_t)new_id[q[u].z];
+      }
+#pragma unroll
+      for (int u = 0; u < V / 2; ++u) {
+        const uint64_t k0 = ((uint64_t)(q[u].y >> kSpanBits) << sh) | ((uint64_t)d[2 * u] << kSpanBits) |
+                            (q[u].y & (kSpan - 1));
+        const uint64_t k1 = ((uint64_t)(q[u].w >> kSpanBits) << sh) | ((uint64_t)d[2 * u + 1] << kSpanBits) |
+                            (q[u].w & (kSpan - 1));
+        reinterpret_cast<uint4*>(keys + i)[u] =
+            make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+      }
+    } else {
+      for (int64_t j = i; j < n; ++j) {
+        const uint64_t w = packed[j];
+        const uint32_t s = (uint32_t)(w >> 32), d = (uint32_t)new_id[(uint32_t)w];
+        keys[j] = ((uint64_t)(s >> kSpanBits) << sh) | ((uint64_t)d << kSpanBits) | (s & (kSpan - 1));
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------- decode
 // Over the SORTED keys with duplicates (the dedup is folded in: no separate unique pass).
 // The last copy of every key stands for the distinct edge; an entry (block, destination)
@@ -1098,6 +1138,13 @@ hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, cons
   const int64_t g = cdiv(n, (int64_t)kKeyR);
   if (g > 0x7fffffffLL) return hipErrorInvalidValue;
   if (packed != nullptr && (phase == 0 || c.world > 1)) return hipErrorInvalidValue;   // one rank only
+  if (packed != nullptr && c.src_new && c.new_id && c.v_lo == 0 && c.v_hi >= c.sl) {
+    const int64_t gw = std::min<int64_t>(cdiv(n, (int64_t)256 * 8), 256 * 64);
+    hipLaunchKernelGGL(gb_keys_one_kernel, dim3((unsigned)gw), dim3(256), 0, st, packed, n, c.new_id, c.dbits,
+                       keys);
+    DALGO_LAUNCH_CHECK();
+    return hipSuccess;
+  }
   if (phase == 0)
     hipLaunchKernelGGL(gb_keys_count_kernel, dim3((unsigned)g), dim3(256), 0, st, src, dst, n, c, bitmap, counts);
   else
