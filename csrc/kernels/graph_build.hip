@@ -102,7 +102,16 @@ __global__ void __launch_bounds__(256) gb_bucket_degree_kernel(const E* __restri
     }
     for (int64_t i = a0 + (nv << 2) + threadIdx.x; i < i1; i += 256) atomicAdd(&hist[gb_id(sorted[i]) & mask], 1u);
   } else {
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) atomicAdd(&hist[gb_id(sorted[i]) & mask], 1u);
+    // 4 independent loads in flight per thread before their LDS atomics
+    constexpr int U = 4;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += 256 * U) {
+      E w[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) w[u] = i + u * 256 < i1 ? sorted[i + u * 256] : E(0);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (i + u * 256 < i1) atomicAdd(&hist[gb_id(w[u]) & mask], 1u);
+    }
   }
   __syncthreads();
   int32_t* d = deg + (b << kBktBits);
