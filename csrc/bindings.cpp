@@ -891,9 +891,11 @@ void gb_relabel_src(Tensor packed, const Tensor& new_id, int64_t partitioned) {
   check_t(packed, at::kLong, "packed");
   check_i32(new_id, "new_id");
   DeviceGuard guard(packed.device());
+  const int64_t nb = (new_id.numel() + ((int64_t)1 << dalgo_gb_bucket_bits()) - 1) >> dalgo_gb_bucket_bits();
+  Tensor starts = at::empty({partitioned ? nb + 1 : 1}, packed.options());
   DALGO_CHECK_HIP(dalgo_gb_relabel_src(reinterpret_cast<uint64_t*>(packed.data_ptr<int64_t>()), packed.numel(),
                                        new_id.data_ptr<int32_t>(), new_id.numel(), (int)partitioned,
-                                       cur_stream()),
+                                       starts.data_ptr<int64_t>(), cur_stream()),
                   "gb_relabel_src");
 }
 

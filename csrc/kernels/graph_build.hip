@@ -146,27 +146,19 @@ __global__ void __launch_bounds__(256) gb_relabel_src_kernel(uint64_t* __restric
 
 // the same over edges partitioned on src >> kBktBits (gb_degree_packed's output): one block
 // per 8192-source bucket stages its 32 KB slice of new_id in LDS and relabels the bucket's
-// edges from there (its range found by two binary searches); the global gathers of the
-// flat kernel made it 7.8 ms at scale 26 (r5_42)
-__global__ void __launch_bounds__(256) gb_relabel_bucket_kernel(uint64_t* __restrict__ packed, int64_t n,
+// edges from there; the global gathers of the flat kernel made it 7.8 ms at scale 26
+// (r5_42). The bucket ranges come from a SEPARATE launch (gb_bucket_starts_kernel): a
+// binary search inside this kernel would read words other blocks are rewriting (the r5_60
+// .. r5_64 race that changed the scale-26 edge set run to run)
+__global__ void __launch_bounds__(256) gb_relabel_bucket_kernel(uint64_t* __restrict__ packed,
+                                                                const int64_t* __restrict__ starts,
                                                                 const int32_t* __restrict__ new_id, int64_t nv) {
   __shared__ int32_t s_id[1 << kBktBits];
-  __shared__ int64_t s_rng[2];
   const int64_t b = blockIdx.x;
-  if (threadIdx.x < 2) {
-    const int64_t t = b + threadIdx.x;                   // first i with (src_i >> kBktBits) >= t
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if ((int64_t)(packed[mid] >> (32 + kBktBits)) < t) lo = mid + 1;
-      else hi = mid;
-    }
-    s_rng[threadIdx.x] = lo;
-  }
+  const int64_t r0 = starts[b], r1 = starts[b + 1];
   const int64_t v0 = b << kBktBits;
   for (int j = threadIdx.x; j < (1 << kBktBits); j += 256) s_id[j] = v0 + j < nv ? new_id[v0 + j] : 0;
   __syncthreads();
-  const int64_t r0 = s_rng[0], r1 = s_rng[1];
   constexpr int U = 4;
   for (int64_t i = r0 + threadIdx.x; i < r1; i += 256 * U) {
     uint64_t w[U];
@@ -1193,13 +1185,19 @@ hipError_t dalgo_gb_run_sort(uint64_t* K, int64_t n, int lo_bits, int64_t* ws, h
   return hipSuccess;
 }
 
+// partitioned: starts = int64[cdiv(nv, 2^kBktBits) + 1] workspace (the bucket ranges,
+// found by their own launch before any edge is rewritten)
 hipError_t dalgo_gb_relabel_src(uint64_t* packed, int64_t n, const int32_t* new_id, int64_t nv, int partitioned,
-                                hipStream_t st) {
+                                int64_t* starts, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   if (partitioned) {
     const int64_t nb = cdiv(nv, (int64_t)1 << kBktBits);
-    if (nv <= 0 || nb > 0x7fffffffLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(gb_relabel_bucket_kernel, dim3((unsigned)nb), dim3(256), 0, st, packed, n, new_id, nv);
+    if (nv <= 0 || nb > 0x7fffffffLL || starts == nullptr) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gb_bucket_starts_kernel<uint64_t>, dim3((unsigned)cdiv(nb + 1, 256)), dim3(256), 0, st,
+                       (const uint64_t*)packed, n, (int)nb, starts);
+    DALGO_LAUNCH_CHECK();
+    hipLaunchKernelGGL(gb_relabel_bucket_kernel, dim3((unsigned)nb), dim3(256), 0, st, packed,
+                       (const int64_t*)starts, new_id, nv);
     DALGO_LAUNCH_CHECK();
     return hipSuccess;
   }

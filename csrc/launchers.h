@@ -223,7 +223,7 @@ int dalgo_gb_bucket_bits();
 hipError_t dalgo_gb_bucket_degree(const void* sorted, int packed, int64_t n, int end_bit, int64_t* starts,
                                   int32_t* deg, hipStream_t st);
 hipError_t dalgo_gb_relabel_src(uint64_t* packed, int64_t n, const int32_t* new_id, int64_t nv, int partitioned,
-                                hipStream_t st);
+                                int64_t* starts, hipStream_t st);
 hipError_t dalgo_gb_pack(const int32_t* src, const int32_t* dst, int64_t n, uint64_t* out, hipStream_t st);
 int64_t dalgo_gb_key_blocks(int64_t n);
 hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, const DalgoGbKeyArgs* a,

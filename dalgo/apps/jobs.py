@@ -194,6 +194,78 @@ def kmeans_job(rt, rows: int = 100_000_000, dim: int = 128, k: int = 1024, iters
 
 
 # --------------------------------------------------------------------- PageRank
+def build_witness(edges: list, shard, pull_shard, rt) -> dict:
+    """The adjacency build checked against torch over the RAW input edges (untimed), with
+    nothing taken from the native keys: ``distinct()`` / ``count()`` of
+    graph_computation/pagerank.py:41,44.
+
+    * new_id is a bijection of [0, N);
+    * this rank's distinct edges = torch.unique of the raw (src, dst) pairs relabelled
+      through new_id and filtered to this rank's destinations: same count and the same
+      edge set as the built shard (``pull_shard``, which the K4b-vs-pull check then uses);
+    * the distinct out-degree of every local source (own slice and ghosts) = a bincount
+      over that torch edge set, and the out-degrees sum to the edge count;
+    * one rank: the distinct count of the un-relabelled input equals the built edge count
+      (a bijective relabel preserves it).
+    Every check is all-reduced (a failure on any rank fails the witness)."""
+    dev = rt.device
+    N, v_lo, v_hi, sl = shard.n_vertices, shard.v_lo, shard.v_hi, shard.slice_size
+    nid = shard.new_id.long() if getattr(shard, "new_id", None) is not None else None
+    bij = True
+    if nid is not None:
+        hit = torch.zeros(N, dtype=torch.int32, device=dev)
+        hit.index_fill_(0, nid, 1)
+        bij = bool(int(nid.min().item()) >= 0 and int(nid.max().item()) < N and int(hit.sum().item()) == N)
+        del hit
+    parts = []
+    raw_parts = []
+    for s, d in edges:
+        s64, d64 = s.long(), d.long()
+        if rt.world_size == 1:
+            raw_parts.append((s64 << 32) | d64)
+        if nid is not None:
+            s64, d64 = nid[s64], nid[d64]
+        keep = (d64 >= v_lo) & (d64 < v_hi)
+        parts.append(((d64[keep] - v_lo) << 32) | s64[keep])
+        del s64, d64, keep
+    ref = torch.unique(torch.cat(parts))
+    del parts
+    n_ref = int(ref.numel())
+    raw_distinct = None
+    if raw_parts:
+        raw_distinct = int(torch.unique(torch.cat(raw_parts)).numel())
+    del raw_parts
+    E = pull_shard.n_edges
+    got = (pull_shard.dstl[:E].long() << 32) | pull_shard.src[:E].long()
+    same_set = n_ref == E and bool(torch.equal(got, ref))
+    del got
+    # distinct out-degree per local source (the [own | ghost] index space of the native build)
+    od_ok = True
+    od = getattr(shard, "outdeg_loc", None)
+    if od is not None:
+        src = ref & 0xFFFFFFFF
+        own = (src >= v_lo) & (src < v_hi)
+        cnt = torch.zeros(od.numel(), dtype=torch.int64, device=dev)
+        cnt.index_add_(0, src[own] - v_lo, torch.ones_like(src[own]))
+        gh = getattr(shard, "ghosts", None)
+        if gh is not None and gh.numel():
+            gi = torch.searchsorted(gh, src[~own])
+            ok_g = bool((gi < gh.numel()).all().item()) and bool(torch.equal(gh[gi.clamp_max(gh.numel() - 1)], src[~own]))
+            od_ok = ok_g
+            cnt.index_add_(0, sl + gi.clamp_max(gh.numel() - 1), torch.ones_like(gi))
+        od_ok = od_ok and bool(torch.equal(cnt, od.long())) and int(od.long().sum().item()) == E
+        del src, own, cnt
+    del ref
+    ok = bij and same_set and od_ok and (raw_distinct is None or raw_distinct == E)
+    okt = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+    comm.all_reduce_max(okt)
+    return {"vs": "torch.unique over the raw input edges (relabelled through new_id)",
+            "relabel_bijective": bij, "edges_rank0": E, "torch_distinct_rank0": n_ref,
+            "edge_set_equal_rank0": same_set, "outdeg_equal_rank0": od_ok,
+            "raw_distinct_one_rank": raw_distinct,
+            "passed": bool(float(okt.item()) == 0.0)}
+
+
 def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
                  spmv: str = "blocked", semantics: str = "reference", witness: bool = True,
                  reorder: bool = True, seed: int = 1, bin_width: int = 16384,
@@ -263,7 +335,6 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
         from dalgo.ops import graph as G
         build_phases = G.build_phase_spans()
         G.build_marks = None
-    del edges
     E = comm.all_reduce_count(shard.n_edges, device=rt.device)
     # per-iteration rate alone (after the job), with the phase split of one step
     pr.timer = PhaseTimer(rt.device)
@@ -281,10 +352,16 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
     rt.synchronize()
     it_ms = _max_over_ranks(time.perf_counter() - t, rt.device) / max(timed_iters, 1) * 1e3
     wit = None
+    bwit = None
+    pull_shard = None
+    if witness:
+        pull_shard = shard.to_shard() if native else shard
+        bwit = build_witness(edges, shard, pull_shard, rt)
+    del edges
     if witness:
         # one more iteration of the benchmarked SpMV vs the pull SpMV from the same state
         ref = PageRank(PageRankConfig(semantics=semantics, spmv="pull", exchange=pr.exchange),
-                       shard.to_shard() if native else shard, W)
+                       pull_shard, W)
         ref.load_state_dict(pr.state_dict())
         pr.step()
         ref.step()
@@ -301,8 +378,9 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
         rel = float(err[0].item()) / max(float(sc.item()), 1e-30)
         wit = {"vs": "pull K4 SpMV, same state", "max_rel_err": rel,
                "presence_mismatches": int(err[1].item()), "iteration": pr.t,
-               "passed": bool(rel < 1e-5 and int(err[1].item()) == 0)}
-        del ref
+               "build": bwit,
+               "passed": bool(rel < 1e-5 and int(err[1].item()) == 0 and bwit["passed"])}
+        del ref, pull_shard
     lay = pr.layout
     out = {
         "metric": "PageRank edges/sec (whole node)",

@@ -188,3 +188,23 @@ def test_cell_matrix_layout_equals_entry_scan(cuda, world, monkeypatch):
             assert torch.equal(getattr(a, f), getattr(b, f)), f
         for f in ("n_chunks", "n_entries", "n_src", "max_runs", "n_local"):
             assert getattr(a, f) == getattr(b, f), f
+
+
+def test_native_relabel_many_buckets_equals_torch_shard(cuda):
+    """The one-rank packed path with degree relabeling at scale 20: 128 source buckets of
+    the bucketed relabel (gb_relabel_bucket_kernel, one block per bucket) -- enough blocks
+    in flight for a cross-block race on the edge words to show. Edge set, edge count and the
+    distinct out-degree of every source equal the torch build."""
+    scale = 20
+    edges, _ = rmat_input(scale, 16, torch.device(cuda), seed=13, chunk=1 << 22)
+    ng = build_rmat_native(edges, scale, 0, 1, cuda, reorder=True, keep_keys=True)
+    ref = build_rmat_shard(edges, scale, 0, 1, cuda, reorder=True)
+    assert torch.equal(ng.new_id.long(), ref.new_id.long())
+    assert ng.n_edges == ref.n_edges
+    sh = ng.to_shard()
+    assert torch.equal(_edge_set(sh), _edge_set(ref))
+    od = torch.bincount(ref.src[: ref.n_edges].long(), minlength=ng.outdeg_loc.numel())
+    assert torch.equal(od, ng.outdeg_loc.long())
+    # the relabel is a bijection and the raw distinct count is preserved by it
+    raw = torch.unique(torch.cat([(s.long() << 32) | d.long() for s, d in edges]))
+    assert int(raw.numel()) == ng.n_edges
