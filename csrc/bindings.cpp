@@ -899,6 +899,40 @@ void gb_relabel_src(Tensor packed, const Tensor& new_id, int64_t partitioned) {
                   "gb_relabel_src");
 }
 
+// sharded build shuffle: the edges relabelled through new_id (optional) and grouped by the
+// owner rank of their destination (dst' / sl) into out (packed src << 32 | dst); returns
+// the per-owner counts [world] (int64, device)
+Tensor gb_owner_partition(const Tensor& src, const Tensor& dst, const std::optional<Tensor>& new_id, int64_t sl,
+                          int64_t world, Tensor out) {
+  check_i32(src, "src");
+  check_i32(dst, "dst");
+  check_t(out, at::kLong, "out");
+  const int64_t n = src.numel();
+  TORCH_CHECK(dst.numel() == n && out.numel() >= n, "gb_owner_partition: sizes");
+  TORCH_CHECK(world >= 1 && world <= 64 && sl >= 1, "gb_owner_partition: 1..64 ranks");
+  TORCH_CHECK(src.is_contiguous() && dst.is_contiguous() && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0,
+              "gb_owner_partition: src / dst must be contiguous and 16-B aligned (int4 loads)");
+  if (new_id) check_i32(*new_id, "new_id");
+  DeviceGuard guard(src.device());
+  const int64_t nb = std::max<int64_t>(dalgo_gb_owner_blocks(n), 1);
+  Tensor counts = at::zeros({world, nb}, src.options().dtype(at::kLong));
+  if (n == 0) return counts.sum(1);
+  Tensor tmp = at::empty({n}, src.options().dtype(at::kLong));
+  auto* tp = reinterpret_cast<uint64_t*>(tmp.data_ptr<int64_t>());
+  DALGO_CHECK_HIP(dalgo_gb_owner_scatter(0, src.data_ptr<int32_t>(), dst.data_ptr<int32_t>(), n,
+                                         opt_ptr<const int32_t>(new_id), sl, (int)world, tp,
+                                         counts.data_ptr<int64_t>(), nullptr, nullptr, cur_stream()),
+                  "gb_owner_scatter(count)");
+  Tensor flat = counts.view({-1});
+  Tensor offs = flat.cumsum(0) - flat;
+  DALGO_CHECK_HIP(dalgo_gb_owner_scatter(2, nullptr, nullptr, n, nullptr, sl, (int)world, tp, nullptr,
+                                         offs.data_ptr<int64_t>(),
+                                         reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>()), cur_stream()),
+                  "gb_owner_scatter(scatter)");
+  return counts.sum(1);
+}
+
 // packed[i] = src[i] << 32 | dst[i]
 void gb_pack(const Tensor& src, const Tensor& dst, Tensor out) {
   check_i32(src, "src");
@@ -1671,6 +1705,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("gb_keys_packed(Tensor packed, Tensor? new_id, int n_vertices, int dbits, Tensor(a!) keys, int src_new=0) -> ()");
   m.def("gb_relabel_src(Tensor(a!) packed, Tensor new_id, int partitioned=0) -> ()");
   m.def("gb_pack(Tensor src, Tensor dst, Tensor(a!) out) -> ()");
+  m.def("gb_owner_partition(Tensor src, Tensor dst, Tensor? new_id, int sl, int world, Tensor(a!) out) -> Tensor");
   m.def("gb_degree_packed(Tensor packed, int end_bit, Tensor(a!) deg, Tensor(b!) out) -> ()");
   m.def("gb_degree_sorted(Tensor ids, int end_bit, Tensor(a!) deg) -> ()");
   m.def("gb_decode_blocks(int n) -> int", &gb_decode_blocks);   // no tensors: catch-all kernel
@@ -1752,6 +1787,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("gb_keys_packed", &gb_keys_packed);
   m.impl("gb_relabel_src", &gb_relabel_src);
   m.impl("gb_pack", &gb_pack);
+  m.impl("gb_owner_partition", &gb_owner_partition);
   m.impl("gb_degree_packed", &gb_degree_packed);
   m.impl("gb_degree_sorted", &gb_degree_sorted);
   m.impl("gb_decode", &gb_decode);

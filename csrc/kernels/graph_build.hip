@@ -181,6 +181,107 @@ __global__ void __launch_bounds__(256) gb_pack_kernel(const int32_t* __restrict_
     out[i] = ((uint64_t)(uint32_t)src[i] << 32) | (uint64_t)(uint32_t)dst[i];
 }
 
+// ---------------------------------------------------------------------------- owners
+// The sharded build's shuffle (graph_computation/pagerank.py:41 ``groupByKey`` over W
+// ranks): every rank relabels its E/W input edges through new_id and groups them by the
+// rank that owns the destination (owner = dst / sl) for one all_to_all. Phase 0 relabels
+// and packs (src << 32 | dst) at the edge's own position of a scratch array (the only
+// random new_id gathers) and counts the block's edges per owner; phase 2 re-reads the
+// packed words and scatters them owner-major at the scanned offsets. Per-owner counting
+// is wave-aggregated (one LDS atomic per distinct owner in a wave, <= W per step).
+constexpr int kOwnR = 16384;         // edges per block
+constexpr int kOwnMax = 64;          // largest world size
+
+__device__ __forceinline__ int gb_owner_slot(int o, bool valid, int* s_cnt, bool want_base, int lane) {
+  uint64_t act = __ballot(valid);
+  int mine = 0;
+  while (act) {
+    const int leader = __ffsll((long long)act) - 1;
+    const int ol = __shfl(o, leader);
+    const uint64_t m = __ballot(valid && o == ol);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&s_cnt[ol], __popcll(m));
+    if (want_base) {
+      base = __shfl(base, leader);
+      if (valid && o == ol) mine = base + __popcll(m & ((1ull << lane) - 1ull));
+    }
+    act &= ~m;
+  }
+  return mine;
+}
+
+__global__ void __launch_bounds__(256) gb_owner_count_kernel(const int32_t* __restrict__ src,
+                                                             const int32_t* __restrict__ dst, int64_t n,
+                                                             const int32_t* __restrict__ new_id, uint32_t sl,
+                                                             int world, uint64_t* __restrict__ tmp,
+                                                             int64_t* __restrict__ counts) {
+  __shared__ int s_cnt[kOwnMax];
+  if (threadIdx.x < kOwnMax) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 = (int64_t)blockIdx.x * kOwnR;
+  const int64_t r1 = r0 + kOwnR < n ? r0 + kOwnR : n;
+  for (int64_t i = r0 + (int64_t)threadIdx.x * 4; i < r1 + 0; i += 256 * 4) {
+    int32_t s4[4], d4[4];
+    bool in[4];
+    if (i + 4 <= r1) {
+      const int4 a = *reinterpret_cast<const int4*>(src + i);
+      const int4 b = *reinterpret_cast<const int4*>(dst + i);
+      s4[0] = a.x; s4[1] = a.y; s4[2] = a.z; s4[3] = a.w;
+      d4[0] = b.x; d4[1] = b.y; d4[2] = b.z; d4[3] = b.w;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) in[v] = true;
+    } else {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        in[v] = i + v < r1;
+        s4[v] = in[v] ? src[i + v] : 0;
+        d4[v] = in[v] ? dst[i + v] : 0;
+      }
+    }
+    if (new_id) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        s4[v] = new_id[s4[v]];
+        d4[v] = new_id[d4[v]];
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      if (in[v]) tmp[i + v] = ((uint64_t)(uint32_t)s4[v] << 32) | (uint32_t)d4[v];
+      gb_owner_slot((int)((uint32_t)d4[v] / sl), in[v], s_cnt, false, lane);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < world) counts[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s_cnt[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(256) gb_owner_scatter_kernel(const uint64_t* __restrict__ tmp, int64_t n,
+                                                               uint32_t sl, const int64_t* __restrict__ offsets,
+                                                               uint64_t* __restrict__ out) {
+  __shared__ int s_cur[kOwnMax];
+  if (threadIdx.x < kOwnMax) s_cur[threadIdx.x] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 = (int64_t)blockIdx.x * kOwnR;
+  const int64_t r1 = r0 + kOwnR < n ? r0 + kOwnR : n;
+  for (int64_t i = r0 + (int64_t)threadIdx.x * 4; i < r1; i += 256 * 4) {
+    uint64_t w[4];
+    bool in[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      in[v] = i + v < r1;
+      w[v] = in[v] ? tmp[i + v] : 0ull;
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int o = (int)((uint32_t)w[v] / sl);
+      const int pos = gb_owner_slot(o, in[v], s_cur, true, lane);
+      if (in[v]) out[offsets[(int64_t)o * gridDim.x + blockIdx.x] + pos] = w[v];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------- keys
 // Local source index of a global (relabelled) source id and its block:
 //   own slice [v_lo, v_hi): li = s - v_lo, segment 0;
@@ -1121,6 +1222,28 @@ hipError_t dalgo_gb_bucket_degree(const void* sorted, int packed, int64_t n, int
     hipLaunchKernelGGL(gb_bucket_degree_kernel<uint32_t>, dim3((unsigned)nb), dim3(256), 0, st,
                        (const uint32_t*)sorted, (const int64_t*)starts, deg);
   }
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+int64_t dalgo_gb_owner_blocks(int64_t n) { return cdiv(n, (int64_t)kOwnR); }
+
+// phase 0: tmp[i] = new_id[src[i]] << 32 | new_id[dst[i]] (new_id nullable), counts[o * nb + b] =
+// edges of block b owned by rank o = dst' / sl; phase 2 (offsets = exclusive scan of counts):
+// out[offsets[o * nb + b] + ...] = the block's words owned by o
+hipError_t dalgo_gb_owner_scatter(int phase, const int32_t* src, const int32_t* dst, int64_t n,
+                                  const int32_t* new_id, int64_t sl, int world, uint64_t* tmp,
+                                  int64_t* counts, const int64_t* offsets, uint64_t* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (world < 1 || world > kOwnMax || sl < 1 || sl > 0x7fffffffLL) return hipErrorInvalidValue;
+  const int64_t g = cdiv(n, (int64_t)kOwnR);
+  if (g > 0x7fffffffLL) return hipErrorInvalidValue;
+  if (phase == 0)
+    hipLaunchKernelGGL(gb_owner_count_kernel, dim3((unsigned)g), dim3(256), 0, st, src, dst, n, new_id,
+                       (uint32_t)sl, world, tmp, counts);
+  else
+    hipLaunchKernelGGL(gb_owner_scatter_kernel, dim3((unsigned)g), dim3(256), 0, st, (const uint64_t*)tmp, n,
+                       (uint32_t)sl, offsets, out);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

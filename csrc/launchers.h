@@ -226,6 +226,10 @@ hipError_t dalgo_gb_relabel_src(uint64_t* packed, int64_t n, const int32_t* new_
                                 int64_t* starts, hipStream_t st);
 hipError_t dalgo_gb_pack(const int32_t* src, const int32_t* dst, int64_t n, uint64_t* out, hipStream_t st);
 int64_t dalgo_gb_key_blocks(int64_t n);
+int64_t dalgo_gb_owner_blocks(int64_t n);
+hipError_t dalgo_gb_owner_scatter(int phase, const int32_t* src, const int32_t* dst, int64_t n,
+                                  const int32_t* new_id, int64_t sl, int world, uint64_t* tmp,
+                                  int64_t* counts, const int64_t* offsets, uint64_t* out, hipStream_t st);
 hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, const DalgoGbKeyArgs* a,
                          int phase, uint32_t* bitmap, int32_t* counts, const int64_t* offsets,
                          int64_t base_all, uint64_t* keys, const uint64_t* packed, hipStream_t st);

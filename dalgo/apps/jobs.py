@@ -280,18 +280,29 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
     the pull K4 SpMV from the same state. ``warm``: the same build + 2 iterations on a
     separate scale-16 graph first (discarded), as the k-means job does: the first launch of
     every library kernel loads its code object (tens of ms each on a cold process)."""
-    from dalgo.apps.pagerank_app import build_rmat_native, build_rmat_shard, rmat_input
+    from dalgo.apps.pagerank_app import (build_rmat_native, build_rmat_shard, build_rmat_sharded,
+                                         rmat_input, rmat_input_share)
     from dalgo.models.pagerank import PageRank, PageRankConfig
     from dalgo.utils.obs import PhaseTimer
     W = rt.world_size
     pool = reserve_pool(rt.device, pool_gb)
     native = (native_build and rt.device.type == "cuda" and spmv == "blocked" and chunk >= 1 << 40)
+    # several ranks: every rank holds E / W input edges and the build shuffles them to
+    # their destination owners (pagerank_app.build_rmat_sharded); one rank: the whole
+    # stream through the packed one-rank build
+    sharded = W > 1
     cfg = PageRankConfig(semantics=semantics, spmv=spmv, bin_width=bin_width, chunk=chunk,
                          tile=tile, n_iterations=iters)
     if warm:
         ws = min(16, scale)
-        we, _ = rmat_input(ws, edge_factor, rt.device, seed + 1)
-        if native:
+        if sharded:
+            we, _ = rmat_input_share(ws, edge_factor, rt.rank, W, rt.device, seed + 1)
+        else:
+            we, _ = rmat_input(ws, edge_factor, rt.device, seed + 1)
+        if sharded:
+            wsh = build_rmat_sharded(we, ws, rt.rank, W, rt.device, reorder=reorder, native=native,
+                                     keep_keys=witness, bin_width=bin_width, tile=tile)
+        elif native:
             wsh = build_rmat_native(we, ws, rt.rank, W, rt.device, reorder=reorder, keep_keys=witness,
                                     bin_width=bin_width, tile=tile)
         else:
@@ -302,7 +313,10 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
         rt.synchronize()
         del we, wsh, wpr
     t0 = time.time()
-    edges, n_gen = rmat_input(scale, edge_factor, rt.device, seed)
+    if sharded:
+        edges, n_gen = rmat_input_share(scale, edge_factor, rt.rank, W, rt.device, seed)
+    else:
+        edges, n_gen = rmat_input(scale, edge_factor, rt.device, seed)
     rt.synchronize()
     gen_s = time.time() - t0
     ev = _Events(rt.device)
@@ -315,6 +329,10 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
     if native:
         from dalgo.ops import graph as G
         G.build_marks = []
+    if sharded:
+        shard = build_rmat_sharded(edges, scale, rt.rank, W, rt.device, reorder=reorder, native=native,
+                                   keep_keys=witness, bin_width=bin_width, tile=tile)
+    elif native:
         shard = build_rmat_native(edges, scale, rt.rank, W, rt.device, reorder=reorder,
                                   keep_keys=witness, bin_width=bin_width, tile=tile)
     else:
@@ -356,6 +374,9 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
     pull_shard = None
     if witness:
         pull_shard = shard.to_shard() if native else shard
+        if sharded:   # the witness needs every input edge: the same stream, regenerated
+            del edges
+            edges, _ = rmat_input(scale, edge_factor, rt.device, seed)
         bwit = build_witness(edges, shard, pull_shard, rt)
     del edges
     if witness:
@@ -394,7 +415,9 @@ def pagerank_job(rt, scale: int = 26, edge_factor: int = 16, iters: int = 10,
         "ms_per_iter": it_ms, "edges_per_s_per_iter": E / (it_ms / 1e3),
         "edges_dedup": E, "edges_generated": n_gen, "vertices": 1 << scale,
         "degree_reordered": reorder, "spmv": pr.spmv, "exchange": pr.exchange,
-        "adjacency_build": "native (graph_build.hip)" if native else "torch (dst, src) shard",
+        "adjacency_build": ("native (graph_build.hip)" if native else "torch (dst, src) shard") + (
+            ", sharded input (E / W edges per rank, all_to_all to the destination owners)"
+            if sharded else ""),
         "phases_ms_rank0": phases, "correctness_witness": wit,
         "allocator_pool_gib": pool,
         "timing": "adjacency build + %d iterations inside the clock (MAX over ranks); input "

@@ -79,8 +79,10 @@ def rmat_input(scale: int, edge_factor: int, device, seed: int = 1, chunk: int =
     """The whole R-MAT edge stream as a list of (src, dst) int32 chunks (the job's input:
     the reference's ``parallelize(links)``, graph_computation/pagerank.py:35-38)."""
     n_edges = edge_factor * (1 << scale)
+    from dalgo.parallel import runtime
     parts = []
     for off in range(0, n_edges, chunk):
+        runtime.heartbeat()   # long generation is progress (stall watchdog)
         parts.append(G.rmat_edges(min(chunk, n_edges - off), scale, seed=seed, e_off=off,
                                   device=device))
     return parts, n_edges
@@ -175,6 +177,105 @@ def build_rmat_native(edges: list, scale: int, rank: int, world: int, device, re
         G._mark("deal_ids")
     return G.build_native(edges, 1 << scale, rank, world, new_id, bin_width=bin_width, tile=tile,
                           keep_keys=keep_keys, packed=packed, packed_src_new=packed is not None)
+
+
+def edge_range(n_edges: int, rank: int, world: int) -> tuple[int, int]:
+    """Rank's contiguous share [lo, hi) of an n_edges input stream."""
+    return n_edges * rank // world, n_edges * (rank + 1) // world
+
+
+def rmat_input_share(scale: int, edge_factor: int, rank: int, world: int, device, seed: int = 1):
+    """This rank's E/W share of the R-MAT stream as ONE (src, dst) chunk: each rank holds
+    (generates, or would load) only its part of the input, the reference's
+    ``parallelize(links, n_slices)`` (graph_computation/pagerank.py:35-38)."""
+    from dalgo.parallel import runtime
+    n_edges = edge_factor * (1 << scale)
+    lo, hi = edge_range(n_edges, rank, world)
+    runtime.heartbeat()
+    return [G.rmat_edges(hi - lo, scale, seed=seed, e_off=lo, device=device)], n_edges
+
+
+def degree_order_share(edges: list, scale: int, world: int, device) -> torch.Tensor:
+    """:func:`degree_order` when every rank holds a disjoint share of the input: each rank
+    counts the sources of ALL its chunks, one all-reduce of the degrees, the same ranking
+    and dealing on every rank."""
+    from dalgo.parallel import comm
+    n_vertices = 1 << scale
+    deg = torch.zeros(n_vertices, dtype=torch.int32, device=device)
+    if edges and deg.is_cuda and scale > G.BUCKET_BITS + 2:
+        ids = torch.cat([s for s, _ in edges]) if len(edges) > 1 else edges[0][0]
+        G.degree_sorted_(deg, ids, scale)
+        del ids
+    else:
+        for s, _ in edges:
+            G.degree_count_(deg, s)
+    comm.all_reduce_sum(deg)
+    G._mark("degree_count")
+    order = rank_by_degree(deg)
+    G._mark("degree_rank")
+    return deal_ids(order, n_vertices, world).to(torch.int32)
+
+
+def shuffle_edges(edges: list, new_id: torch.Tensor | None, n_vertices: int, world: int):
+    """``groupByKey`` over the ranks (graph_computation/pagerank.py:41): this rank's input
+    edges relabelled through new_id and sent to the owners of their destinations in ONE
+    uneven all_to_all of packed (src << 32 | dst) words (plus one of the counts). Returns
+    the (src, dst) int32 edges whose destination this rank owns, global new ids."""
+    from dalgo.parallel import comm
+    packs, counts = [], []
+    for s, d in edges:
+        p, c = G.owner_partition(s, d, new_id, n_vertices, world)
+        packs.append(p)
+        counts.append(c)
+    if len(packs) == 1:
+        packed, send = packs[0], counts[0]
+    else:   # several chunks: owner-major concatenation
+        pieces = []
+        for o in range(world):
+            for p, c in zip(packs, counts):
+                a = sum(c[:o])
+                pieces.append(p[a:a + c[o]])
+        packed = torch.cat(pieces)
+        send = [sum(c[o] for c in counts) for o in range(world)]
+    del packs
+    G._mark("owner_partition")
+    dev = packed.device
+    st = torch.tensor(send, dtype=torch.int64, device=dev)
+    rt_ = torch.empty_like(st)
+    comm.all_to_all_single(rt_, st)
+    recv = [int(x) for x in rt_.tolist()]
+    out = torch.empty(max(sum(recv), 1), dtype=torch.int64, device=dev)
+    comm.all_to_all_single(out[: sum(recv)], packed, recv, send)
+    del packed
+    G._mark("all_to_all")
+    return G.unpack_edges(out[: sum(recv)])
+
+
+def build_rmat_sharded(edges: list, scale: int, rank: int, world: int, device, reorder: bool = True,
+                       native: bool | None = None, keep_keys: bool = False, bin_width: int = 16384,
+                       tile: int = 16384):
+    """This rank's PageRank adjacency when every rank holds only E/W input edges: degree
+    relabeling from one all-reduce of the share degrees, the shuffle of the relabelled
+    edges to their destination owners (:func:`shuffle_edges`), then the build over what
+    arrived -- native K4b layout on GPUs (dalgo.ops.graph.build_native, no relabeling left
+    to do), the torch (dst, src) shard otherwise. Per rank O(E / W) work but the O(N)
+    ranking of the degree order."""
+    G._mark("start")
+    n_vertices = 1 << scale
+    new_id = degree_order_share(edges, scale, world, device) if reorder else None
+    G._mark("deal_ids")
+    s, d = shuffle_edges(edges, new_id, n_vertices, world)
+    use_native = (torch.device(device).type == "cuda") if native is None else native
+    if use_native:
+        ng = G.build_native([(s, d)], n_vertices, rank, world, None, bin_width=bin_width, tile=tile,
+                            keep_keys=keep_keys)
+        ng.new_id = new_id
+        return ng
+    sl = G.vertex_slices(n_vertices, world)
+    v_lo, v_hi = rank * sl, min(n_vertices, (rank + 1) * sl)
+    shard = G.merge_shards([(s, d - v_lo)], v_lo, v_hi, n_vertices, sl)
+    shard.new_id = new_id
+    return shard
 
 
 def rmat_shard(scale: int, edge_factor: int, rank: int, world: int, device, seed: int = 1,

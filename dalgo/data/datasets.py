@@ -75,7 +75,9 @@ def synthetic_logistic(n_rows: int, D: int, *, row_range: tuple[int, int] | None
     def make(n, off, stream_x, stream_y):
         X = _padded(n, D, dtype, device)
         y = torch.empty(n, dtype=torch.float32, device=device)
+        from dalgo.parallel import runtime
         for s in range(0, n, chunk_rows):
+            runtime.heartbeat()   # long generation is progress (stall watchdog)
             e = min(n, s + chunk_rows)
             base = X.as_strided((e - s, X.stride(0)), (X.stride(0), 1), X.storage_offset() + s * X.stride(0))
             drandom.philox_fill_(base, D=D, row_offset=off + s, seed=seed, stream=stream_x,

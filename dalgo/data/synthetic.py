@@ -19,7 +19,9 @@ def blobs(n: int, d: int, k: int, *, row_range=None, device="cpu", dtype=torch.f
     device = torch.device(device)
     C = blob_centers(k, d, seed, device, spread)
     X = torch.empty((hi - lo, d), dtype=dtype, device=device)
+    from dalgo.parallel import runtime
     for s in range(0, hi - lo, chunk):
+        runtime.heartbeat()   # long generation is progress (stall watchdog)
         e = min(hi - lo, s + chunk)
         u = torch.empty((e - s, 1), dtype=torch.float32, device=device)
         drandom.philox_fill_(u, D=1, row_offset=lo + s, seed=seed, stream=22, a=0.0, b=float(k))

@@ -173,6 +173,34 @@ def relabel_partition_dst(packed: torch.Tensor, new_id: torch.Tensor, bits: int)
     return out
 
 
+def owner_partition(src: torch.Tensor, dst: torch.Tensor, new_id: torch.Tensor | None, n_vertices: int,
+                    world: int) -> tuple[torch.Tensor, list]:
+    """The sharded build's shuffle source (graph_computation/pagerank.py:41 groupByKey over
+    W ranks): this rank's input edges relabelled through ``new_id`` and grouped by the rank
+    that owns the destination (owner = dst' // slice size), packed src << 32 | dst. Returns
+    (packed int64 [E], edges per owner). GPU: two passes of graph_build.hip (relabel + count,
+    then an owner-major scatter); CPU: torch."""
+    sl = vertex_slices(n_vertices, world)
+    if src.is_cuda:
+        out = torch.empty(src.numel(), dtype=torch.int64, device=src.device)
+        nid = new_id.to(torch.int32).contiguous() if new_id is not None else None
+        cnt = _ext.ops().gb_owner_partition(src.contiguous(), dst.contiguous(), nid, sl, world, out)
+        return out, [int(x) for x in cnt.tolist()]
+    s, d = src.long(), dst.long()
+    if new_id is not None:
+        s, d = new_id.long()[s], new_id.long()[d]
+    owner = d // sl
+    order = torch.argsort(owner, stable=True)
+    packed = ((s << 32) | d)[order]
+    cnt = torch.bincount(owner, minlength=world)[:world]
+    return packed, [int(x) for x in cnt.tolist()]
+
+
+def unpack_edges(packed: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """(src, dst) int32 of packed src << 32 | dst words."""
+    return (packed >> 32).to(torch.int32), (packed & 0xFFFFFFFF).to(torch.int32)
+
+
 def degree_sorted_(deg: torch.Tensor, ids: torch.Tensor, bits: int) -> torch.Tensor:
     """deg[v] += #occurrences of v in ids (GPU int32, ids < 2^bits): the ids partitioned
     on their high bits (2 radix passes at 2^26 ids), then one LDS histogram per bucket of

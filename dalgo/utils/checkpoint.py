@@ -20,15 +20,17 @@ def save(state: dict, ckpt_dir: str, name: str, rank: int = 0, per_rank: bool = 
     """Collective: every rank calls it (rank 0 writes unless ``per_rank``). A device
     collective that timed out on any rank raises here on every rank, so a poisoned
     state is never written."""
-    from dalgo.parallel import comm
+    from dalgo.parallel import comm, runtime
     comm.check_device_errors("checkpoint save")
     if not per_rank and rank != 0:
         return None
     os.makedirs(ckpt_dir, exist_ok=True)
     p = path_for(ckpt_dir, name, rank if per_rank else None)
     tmp = p + ".tmp"
+    runtime.heartbeat()  # a long write is progress, not a stall (runtime.arm_stall_watchdog)
     torch.save(state, tmp)
     os.replace(tmp, p)   # atomic: a crash never leaves a torn checkpoint
+    runtime.heartbeat()
     return p
 
 

@@ -23,10 +23,13 @@ def common_parser(description: str) -> argparse.ArgumentParser:
     ap.add_argument("--quiet", action="store_true", help="suppress per-iteration lines")
     ap.add_argument("--no-plot", action="store_true")
     ap.add_argument("--pg-timeout-s", type=float, default=120.0,
-                    help="process-group timeout: a collective stuck longer raises on the rank")
+                    help="process-group timeout (default 120 s): a collective stuck longer raises on "
+                         "the rank; raise it for runs where one rank does long work (I/O, data "
+                         "generation) while its peers already wait in a collective")
     ap.add_argument("--stall-timeout-s", type=float, default=300.0,
-                    help="multi-rank runs: a rank with no collective for this long prints its "
-                         "stacks and exits 124 (0 = off)")
+                    help="multi-rank runs (default 300 s): a rank with no progress beat for this "
+                         "long prints its stacks and exits 124 (0 = off). Collectives, data "
+                         "generation chunks and checkpoint writes beat")
     ap.add_argument("--deadline-s", type=float, default=0.0,
                     help="wall-clock deadline of the whole run, exit 124 past it (0 = off)")
     return ap

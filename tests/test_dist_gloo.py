@@ -318,3 +318,41 @@ def test_kmeans_fused_bucket_exact_large_counts():
     res = run_world(_kmeans_big_counts, world=3)
     extra = 3 * (1 << 25) + 12345 * 6
     assert all(r == [12 + extra, 12 + extra] for r in res), res
+
+
+def _pr_sharded(rt, scale):
+    """Sharded-input build (each rank E / W edges, shuffle to destination owners) vs the
+    full-stream build of the same rank with the same relabeling; PageRank ranks in the
+    generator's ids."""
+    from dalgo.apps.pagerank_app import (build_rmat_sharded, build_rmat_shard, rmat_input,
+                                         rmat_input_share)
+    from dalgo.models.pagerank import PageRank, PageRankConfig
+    W, r = rt.world_size, rt.rank
+    mine, n_e = rmat_input_share(scale, 8, r, W, "cpu", seed=3)
+    sh = build_rmat_sharded(mine, scale, r, W, "cpu", reorder=True)
+    full, _ = rmat_input(scale, 8, "cpu", seed=3, chunk=1 << 11)
+    ref = build_rmat_shard(full, scale, r, W, "cpu", reorder=True)
+    E = sh.n_edges
+    got = (sh.dstl[:E].long() << 32) | sh.src[:E].long()
+    exp = (ref.dstl[:ref.n_edges].long() << 32) | ref.src[:ref.n_edges].long()
+    pr = PageRank(PageRankConfig(), sh, W).fit()
+    ranks = pr.collect()
+    inv = torch.empty_like(sh.new_id, dtype=torch.int64)
+    inv[sh.new_id.long()] = torch.arange(sh.new_id.numel())
+    return {"same_new_id": bool(torch.equal(sh.new_id.long(), ref.new_id.long())),
+            "same_edges": bool(torch.equal(got, exp)), "E": E,
+            "ranks": {int(inv[v]): x for v, x in ranks.items()}}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pagerank_sharded_input_build(world):
+    scale = 11
+    res = run_world(_pr_sharded, world=world, args=(scale,))
+    one = run_world(_pr_sharded, world=1, args=(scale,))[0]
+    for r in res:
+        assert r["same_new_id"] and r["same_edges"]
+    assert sum(r["E"] for r in res) == one["E"]
+    for r in res:
+        for v, x in r["ranks"].items():
+            assert math.isclose(x, one["ranks"][v], rel_tol=1e-9, abs_tol=1e-15)
+    assert set(res[0]["ranks"]) == set(one["ranks"])

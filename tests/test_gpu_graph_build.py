@@ -208,3 +208,19 @@ def test_native_relabel_many_buckets_equals_torch_shard(cuda):
     # the relabel is a bijection and the raw distinct count is preserved by it
     raw = torch.unique(torch.cat([(s.long() << 32) | d.long() for s, d in edges]))
     assert int(raw.numel()) == ng.n_edges
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_owner_partition_matches_torch(cuda, world):
+    """gb_owner_partition (relabel + group by destination owner) == the torch path: the same
+    per-owner counts and, per owner, the same multiset of packed edges."""
+    scale = 16
+    s, d = G.rmat_edges((1 << 20) + 3, scale, seed=17, device=cuda)        # ragged length
+    new_id = torch.randperm(1 << scale, device=cuda).to(torch.int32)
+    got, cg = G.owner_partition(s, d, new_id, 1 << scale, world)
+    exp, ce = G.owner_partition(s.cpu(), d.cpu(), new_id.cpu(), 1 << scale, world)
+    assert cg == ce and sum(cg) == s.numel()
+    a = 0
+    for c in cg:
+        assert torch.equal(torch.sort(got[a:a + c].cpu()).values, torch.sort(exp[a:a + c]).values)
+        a += c

@@ -64,16 +64,36 @@ def test_scripts_two_ranks_gloo_on_one_gpu(cuda):
         assert needle in part, (path, part[-2000:])
 
 
-def test_pagerank_native_build_two_ranks(cuda):
-    """The PageRank job at 2 gloo ranks on one GPU: each rank builds its K4b layout natively
-    over the [own slice | ghosts] source space (ghost list from the bitmap pass), runs the
-    ghost exchange, and its ranks match the pull K4 over the same edges (witness)."""
-    out = _torchrun(["bench/pagerank_bench.py", "--gpus", "2", "--backend", "gloo", "--scale", "15",
-                     "--steps", "2", "--pool-gb", "1"])
+@pytest.mark.parametrize("n", [2, 3])
+def test_pagerank_native_build_ranks(cuda, n):
+    """The PageRank job at 2 and 3 gloo ranks on one GPU: every rank generates only its
+    E / W input edges, the relabelled edges go to their destination owners in one
+    all_to_all, each rank builds its K4b layout natively over the [own slice | ghosts]
+    source space, runs the ghost exchange; the build witness checks every rank's edge set
+    and out-degrees against torch over the whole raw input, and the ranks match the pull K4
+    over the same edges."""
+    out = _torchrun(["bench/pagerank_bench.py", "--gpus", str(n), "--backend", "gloo", "--scale", "15",
+                     "--steps", "2", "--pool-gb", "1"], n=n)
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
-    assert d["n_gpus"] == 2 and d["exchange"] == "ghost"
-    assert d["adjacency_build"].startswith("native")
-    assert d["correctness_witness"]["passed"], d["correctness_witness"]
+    assert d["n_gpus"] == n and d["exchange"] == "ghost"
+    assert d["adjacency_build"].startswith("native") and "sharded" in d["adjacency_build"]
+    w = d["correctness_witness"]
+    assert w["passed"] and w["build"]["passed"] and w["build"]["edge_set_equal_rank0"], w
+
+
+def test_bench_secondary_two_ranks(cuda):
+    """bench.py at 2 gloo ranks on one GPU runs BASELINE configs #3-#5 too (reduced sizes):
+    BMUF / EASGD, both k-means jobs and the sharded PageRank job, every witness passing."""
+    out = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--rows", "200000",
+                     "--steps", "5", "--warmup", "2", "--secondary-steps", "5", "--secondary-warmup", "2",
+                     "--km-rows", "2000000", "--pr-scale", "16", "--km-pool-gb", "4", "--pr-pool-gb", "4"])
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+    sec = d["secondary"]
+    assert set(sec) == {"bmuf", "easgd", "kmeans", "kmeans_overlapping", "pagerank"}, sec.keys()
+    for k, v in sec.items():
+        assert "error" not in v and "skipped" not in v, (k, v)
+        assert v["correctness_witness"]["passed"], (k, v["correctness_witness"])
+    assert sec["pagerank"]["n_gpus"] == 2 and "sharded" in sec["pagerank"]["adjacency_build"]
 
 
 SPIN = {"DALGO_ALLOW_SHARED_SPIN": "1"}
