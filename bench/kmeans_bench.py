@@ -50,6 +50,8 @@ def main():
                          "for the bound filters)")
     ap.add_argument("--dense", default="auto", choices=["auto", "always", "never"],
                     help="filtered iterations on the dense top-2 K2 (auto: right after the full pass)")
+    ap.add_argument("--no-drift", action="store_true",
+                    help="candidate lists without the centre-shift pruning")
     ap.add_argument("--deadline-s", type=float, default=420.0)
     argv = sys.argv[1:]
     a = ap.parse_args(argv)
@@ -65,7 +67,7 @@ def main():
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     out = kmeans_job(rt, a.rows, a.dim, a.k, a.iters, dtype=dtype, noise=a.noise,
                      bound_filter=not a.no_bound_filter, candidates=not a.no_candidates,
-                     witness=not a.no_witness, dense=a.dense)
+                     witness=not a.no_witness, dense=a.dense, drift=not a.no_drift)
     if rt.is_main:
         print(json.dumps(out), flush=True)
     runtime.shutdown()

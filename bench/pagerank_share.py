@@ -66,6 +66,8 @@ def main():
             ev[2].record()
             packed, send = G.owner_partition(s_own, d_own, nid, N, W)
             ev[3].record()
+            G.build_marks = []
+            G._mark("start")
             ng = G.build_native([(rs, rd)], N, r, W, None)
             ev[4].record()
             torch.cuda.synchronize()
@@ -77,7 +79,9 @@ def main():
                         "input_edges": hi - lo, "received_edges": int(rs.numel()),
                         "edges_dedup": ng.n_edges, "ghosts": ng.n_ghost,
                         "all_to_all_send_bytes": 8 * (sum(send) - send[r]),
-                        "degree_all_reduce_bytes": 4 * N}
+                        "degree_all_reduce_bytes": 4 * N,
+                        "build_phases_ms": G.build_phase_spans()}
+            G.build_marks = None
             del packed, ng, deg, nid
         res["ranks"][r] = best
         print(f"rank {r}/{W}: {best}", file=sys.stderr, flush=True)

@@ -18,6 +18,8 @@ noise = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
 top2_first = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 use_drift = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 TILE = int(sys.argv[5]) if len(sys.argv) > 5 else 256
+FRAC = float(sys.argv[6]) if len(sys.argv) > 6 else 1.0      # drift threshold = FRAC * tau_T
+DENSE2 = int(sys.argv[7]) if len(sys.argv) > 7 else 1        # iteration 2 dense (exact top-2)
 CH = 128
 k, d = 1024, 128
 torch.set_num_threads(8)
@@ -83,8 +85,10 @@ for it in range(2, 6):
             t1 = min(bnd[i + 1], t0 + TILE)
             R = 2 * float(un[t0:t1].max())
             inball = ccd[c0] <= R
-            if use_drift:
-                tau = float((l[ia[t0:t1]] - un[t0:t1]).min())
+            if DENSE2 and it == 2:
+                inball = torch.ones_like(inball)
+            if use_drift and not (DENSE2 and it == 2):
+                tau = FRAC * float((l[ia[t0:t1]] - un[t0:t1]).min())
                 keep = inball & (delta > tau)
             else:
                 keep = inball.clone()
@@ -100,7 +104,7 @@ for it in range(2, 6):
             out_ball = ~inball
             nd_first = float(ccd[c0][out_ball].min()) if out_ball.any() else float("inf")
             lb = torch.minimum(sec, nd_first - un[t0:t1])
-            if use_drift:
+            if use_drift and not (DENSE2 and it == 2):
                 dp = (~keep) & inball
                 dmp = float(delta[dp].max()) if dp.any() else 0.0
                 if dp.any():

@@ -657,12 +657,12 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
   } else {
     TORCH_CHECK(md != nullptr, "kmeans_assign_idx: mind");
   }
-  // candidate-pruned form: [tiles int32 [T, 4], n_tiles, hnb, nb, nd]
+  // candidate-pruned form: [tiles int32 [T, 4], n_tiles, hnb, nb, nd] (+ [ndb, dnb]: drift-aware)
   DalgoKmCand cd{};
   const DalgoKmCand* cp = nullptr;
   if (!cand.empty()) {
-    TORCH_CHECK(cand.size() == 5 && pp != nullptr && ip != nullptr,
-                "kmeans_assign_idx: cand = 5 tensors, with the device-count form and idx");
+    TORCH_CHECK((cand.size() == 5 || cand.size() == 7 || cand.size() == 8) && pp != nullptr && ip != nullptr,
+                "kmeans_assign_idx: cand = 5 (7, 8) tensors, with the device-count form and idx");
     for (const Tensor& t : cand) check_dev(t, "cand");
     TORCH_CHECK(cand[0].scalar_type() == at::kInt && cand[1].scalar_type() == at::kLong &&
                     cand[2].scalar_type() == at::kFloat && cand[3].scalar_type() == at::kInt &&
@@ -678,6 +678,17 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
     cd.nb = cand[3].data_ptr<int32_t>();
     cd.nd = cand[4].data_ptr<float>();
     cd.extend = cand_extend != 0;
+    if (cand.size() >= 7) {
+      TORCH_CHECK(cand[5].scalar_type() == at::kFloat && cand[6].scalar_type() == at::kFloat &&
+                      cand[5].numel() >= k * kpad && cand[6].numel() >= k * kpad,
+                  "kmeans_assign_idx: ndb / dnb f32 [k * kpad]");
+      cd.ndb = cand[5].data_ptr<float>();
+      cd.dnb = cand[6].data_ptr<float>();
+    }
+    if (cand.size() == 8) {
+      TORCH_CHECK(cand[7].scalar_type() == at::kFloat && cand[7].numel() >= 1, "kmeans_assign_idx: tau_cap f32[1]");
+      cd.tau_cap = cand[7].data_ptr<float>();
+    }
     cp = &cd;
   }
   DeviceGuard guard(X.device());
@@ -724,7 +735,8 @@ void kmeans_sort_active(const Tensor& acl, const Tensor& idx, const Tensor& n_ac
 
 // centre geometry of the candidate-pruned iteration: delta, s and the neighbour lists
 void kmeans_centre_nbrs(const Tensor& cq, const Tensor& cprev, const Tensor& hn, int64_t k,
-                        int64_t d, Tensor delta, Tensor s, Tensor nd, Tensor nb, Tensor hnb) {
+                        int64_t d, Tensor delta, Tensor s, Tensor nd, Tensor nb, Tensor hnb,
+                        const std::optional<Tensor>& ndb, const std::optional<Tensor>& dnb) {
   check_dev(cq, "cq");
   check_dev(cprev, "cprev");
   TORCH_CHECK(cq.dim() == 2 && cq.is_contiguous() && cq.scalar_type() == at::kBFloat16 &&
@@ -742,11 +754,21 @@ void kmeans_centre_nbrs(const Tensor& cq, const Tensor& cprev, const Tensor& hn,
   TORCH_CHECK(hn.numel() >= kpad && delta.numel() >= k && s.numel() >= k && nd.numel() >= k * kpad &&
                   nb.numel() >= k * kpad && hnb.numel() >= k * kpad,
               "kmeans_centre_nbrs sizes");
+  TORCH_CHECK(ndb.has_value() == dnb.has_value(), "kmeans_centre_nbrs: ndb and dnb together");
+  float* ndbp = nullptr;
+  float* dnbp = nullptr;
+  if (ndb.has_value()) {
+    check_f32(*ndb, "ndb");
+    check_f32(*dnb, "dnb");
+    TORCH_CHECK(ndb->numel() >= k * kpad && dnb->numel() >= k * kpad, "ndb / dnb [k * kpad]");
+    ndbp = ndb->data_ptr<float>();
+    dnbp = dnb->data_ptr<float>();
+  }
   DeviceGuard guard(cq.device());
   DALGO_CHECK_HIP(dalgo_km_centre_nbrs(cq.data_ptr(), cprev.data_ptr(), hn.data_ptr<float>(), (int)k,
                                        (int)kpad, (int)d, (int)DP, delta.data_ptr<float>(),
                                        s.data_ptr<float>(), nd.data_ptr<float>(), nb.data_ptr<int32_t>(),
-                                       hnb.data_ptr<float>(), cur_stream()),
+                                       hnb.data_ptr<float>(), ndbp, dnbp, cur_stream()),
                   "kmeans_centre_nbrs");
 }
 
@@ -831,8 +853,15 @@ void gb_keys(const Tensor& src, const Tensor& dst, const std::optional<Tensor>& 
   const int64_t nb = dalgo_gb_key_blocks(n);
   if (new_id) check_i32(*new_id, "new_id");
   if (world > 1) {
+    // phase 0: a byte map (uint8, one byte per vertex id) of the remote sources; phase 1:
+    // the bitmap packed from it (gb_bytes_to_bits)
     TORCH_CHECK(bitmap.has_value(), "gb_keys: bitmap needed at world > 1");
-    check_i32(*bitmap, "bitmap");
+    if (phase == 0) {
+      check_t(*bitmap, at::kByte, "marks");
+      TORCH_CHECK(bitmap->numel() >= sl * world, "gb_keys: marks [>= n_vertices] bytes");
+    } else {
+      check_i32(*bitmap, "bitmap");
+    }
   }
   if (phase == 0) {
     TORCH_CHECK(counts.has_value() && counts->numel() >= nb, "gb_keys: counts [blocks]");
@@ -931,6 +960,40 @@ Tensor gb_owner_partition(const Tensor& src, const Tensor& dst, const std::optio
                                          reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>()), cur_stream()),
                   "gb_owner_scatter(scatter)");
   return counts.sum(1);
+}
+
+// bits[w] = bit j set iff marks[32 w + j] != 0
+void gb_bytes_to_bits(const Tensor& marks, Tensor bits) {
+  check_t(marks, at::kByte, "marks");
+  check_i32(bits, "bits");
+  TORCH_CHECK(marks.numel() >= 32 * bits.numel(), "gb_bytes_to_bits: 32 bytes per word");
+  DeviceGuard guard(marks.device());
+  DALGO_CHECK_HIP(dalgo_gb_bytes_to_bits(marks.data_ptr<uint8_t>(), bits.numel(),
+                                         reinterpret_cast<uint32_t*>(bits.data_ptr<int32_t>()), cur_stream()),
+                  "gb_bytes_to_bits");
+}
+
+// ids of the set bits of a u32 bitmap, ascending, at the words' exclusive popcount prefix
+void gb_bitmap_ids(const Tensor& bitmap, const Tensor& prefix, Tensor ids) {
+  check_i32(bitmap, "bitmap");
+  check_t(prefix, at::kLong, "prefix");
+  check_t(ids, at::kLong, "ids");
+  TORCH_CHECK(prefix.numel() >= bitmap.numel(), "gb_bitmap_ids: prefix per word");
+  DeviceGuard guard(bitmap.device());
+  DALGO_CHECK_HIP(dalgo_gb_bitmap_ids(reinterpret_cast<const uint32_t*>(bitmap.data_ptr<int32_t>()), bitmap.numel(),
+                                      prefix.data_ptr<int64_t>(), ids.data_ptr<int64_t>(), cur_stream()),
+                  "gb_bitmap_ids");
+}
+
+// new_id[order[j]] = snake-dealt position of rank j over `world` full slices of size sl
+void gb_deal(const Tensor& order, int64_t world, int64_t sl, Tensor new_id) {
+  check_t(order, at::kLong, "order");
+  check_i32(new_id, "new_id");
+  TORCH_CHECK(new_id.numel() >= order.numel() && sl * world >= order.numel(), "gb_deal: sizes");
+  DeviceGuard guard(order.device());
+  DALGO_CHECK_HIP(dalgo_gb_deal(order.data_ptr<int64_t>(), order.numel(), (int)world, sl, new_id.data_ptr<int32_t>(),
+                                cur_stream()),
+                  "gb_deal");
 }
 
 // packed[i] = src[i] << 32 | dst[i]
@@ -1680,7 +1743,8 @@ TORCH_LIBRARY(dalgo, m) {
         "Tensor(a!) block_counts, Tensor(b!) cstart, Tensor(c!) seg_start, Tensor(d!) rows_sorted, "
         "int tile, Tensor(e!) tiles, Tensor(g!) n_tiles) -> ()");
   m.def("kmeans_centre_nbrs(Tensor cq, Tensor cprev, Tensor hn, int k, int d, Tensor(a!) delta, "
-        "Tensor(b!) s, Tensor(c!) nd, Tensor(d!) nb, Tensor(e!) hnb) -> ()");
+        "Tensor(b!) s, Tensor(c!) nd, Tensor(d!) nb, Tensor(e!) hnb, Tensor(f!)? ndb=None, "
+        "Tensor(g!)? dnb=None) -> ()");
   m.def("kmeans_centre_bounds(Tensor cnow, Tensor cprev, int k, int d, Tensor(a!) delta, "
         "Tensor(b!) s) -> ()");
   m.def("kmeans_qsum(Tensor assign, Tensor xh, int k, Tensor(a!) Q) -> ()");
@@ -1706,6 +1770,9 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("gb_relabel_src(Tensor(a!) packed, Tensor new_id, int partitioned=0) -> ()");
   m.def("gb_pack(Tensor src, Tensor dst, Tensor(a!) out) -> ()");
   m.def("gb_owner_partition(Tensor src, Tensor dst, Tensor? new_id, int sl, int world, Tensor(a!) out) -> Tensor");
+  m.def("gb_bitmap_ids(Tensor bitmap, Tensor prefix, Tensor(a!) ids) -> ()");
+  m.def("gb_bytes_to_bits(Tensor marks, Tensor(a!) bits) -> ()");
+  m.def("gb_deal(Tensor order, int world, int sl, Tensor(a!) new_id) -> ()");
   m.def("gb_degree_packed(Tensor packed, int end_bit, Tensor(a!) deg, Tensor(b!) out) -> ()");
   m.def("gb_degree_sorted(Tensor ids, int end_bit, Tensor(a!) deg) -> ()");
   m.def("gb_decode_blocks(int n) -> int", &gb_decode_blocks);   // no tensors: catch-all kernel
@@ -1788,6 +1855,9 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("gb_relabel_src", &gb_relabel_src);
   m.impl("gb_pack", &gb_pack);
   m.impl("gb_owner_partition", &gb_owner_partition);
+  m.impl("gb_bitmap_ids", &gb_bitmap_ids);
+  m.impl("gb_bytes_to_bits", &gb_bytes_to_bits);
+  m.impl("gb_deal", &gb_deal);
   m.impl("gb_degree_packed", &gb_degree_packed);
   m.impl("gb_degree_sorted", &gb_degree_sorted);
   m.impl("gb_decode", &gb_decode);

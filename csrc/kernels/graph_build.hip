@@ -282,6 +282,55 @@ __global__ void __launch_bounds__(256) gb_owner_scatter_kernel(const uint64_t* _
   }
 }
 
+// byte map (one byte per id, 0 / 1) -> bitmap (one bit per id): 32 bytes per word
+__global__ void __launch_bounds__(256) gb_bytes_to_bits_kernel(const uint4* __restrict__ marks, int64_t nw,
+                                                               uint32_t* __restrict__ bits) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < nw; w += stride) {
+    const uint4 a = marks[2 * w], b = marks[2 * w + 1];
+    const uint32_t q[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      // bytes (0 / 1) of q[i] -> 4 bits: bit j of the nibble = byte j != 0
+      const uint32_t v = q[i];
+      const uint32_t nib = ((v & 0xffu) ? 1u : 0u) | (((v >> 8) & 0xffu) ? 2u : 0u) |
+                           (((v >> 16) & 0xffu) ? 4u : 0u) | ((v >> 24) ? 8u : 0u);
+      m |= nib << (4 * i);
+    }
+    bits[w] = m;
+  }
+}
+
+// W > 1: the ghost list (sorted ids of the bitmap's set bits) at the words' exclusive
+// popcount prefix, one thread per word (the torch form expanded every bit to an int64:
+// ~15 ms of the W = 8 per-rank build share at scale 26)
+__global__ void __launch_bounds__(256) gb_bitmap_ids_kernel(const uint32_t* __restrict__ bm, int64_t nw,
+                                                            const int64_t* __restrict__ prefix,
+                                                            int64_t* __restrict__ ids) {
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= nw) return;
+  uint32_t b = bm[w];
+  int64_t o = prefix[w];
+  while (b) {
+    const int t = __ffs((int)b) - 1;
+    ids[o++] = w * 32 + t;
+    b &= b - 1u;
+  }
+}
+
+// deal of the ranked vertex list (pagerank_app.deal_ids, W > 1, every slice full): rank j
+// goes to slice r = j % W (snake: odd rounds W - 1 .. 0), position j / W
+__global__ void __launch_bounds__(256) gb_deal_kernel(const int64_t* __restrict__ order, int64_t n, int world,
+                                                      int64_t sl, int32_t* __restrict__ new_id) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += stride) {
+    const int64_t p = j / world, q = j - p * world;
+    const int64_t r = (p & 1) ? world - 1 - q : q;
+    new_id[order[j]] = (int32_t)(r * sl + p);
+  }
+}
+
 // ---------------------------------------------------------------------------- keys
 // Local source index of a global (relabelled) source id and its block:
 //   own slice [v_lo, v_hi): li = s - v_lo, segment 0;
@@ -369,10 +418,13 @@ __device__ __forceinline__ void gb_load4(const int32_t* __restrict__ src, const 
   }
 }
 
-// phase 0: count the kept edges per block (and mark remote sources, W > 1)
+// phase 0: count the kept edges per block (and mark remote sources, W > 1: one plain byte
+// store per remote source into a byte map -- idempotent, no read-modify-write; a u32
+// atomicOr per edge into the bitmap made this phase 18.9 ms of the W = 8 per-rank build
+// share at scale 26, profiles/round6/r6_5 -- packed into the bitmap by gb_bytes_to_bits)
 __global__ void __launch_bounds__(256) gb_keys_count_kernel(const int32_t* __restrict__ src,
                                                             const int32_t* __restrict__ dst, int64_t n,
-                                                            GbKeyCtx c, uint32_t* __restrict__ bitmap,
+                                                            GbKeyCtx c, uint8_t* __restrict__ marks,
                                                             int32_t* __restrict__ counts) {
   __shared__ int s_cnt;
   if (threadIdx.x == 0) s_cnt = 0;
@@ -390,7 +442,7 @@ __global__ void __launch_bounds__(256) gb_keys_count_kernel(const int32_t* __res
       int64_t dl;
       if (in[v] && gb_edge(c, s0[v], d0[v], sv, dl)) {
         ++mine;
-        if (c.world > 1 && !(sv >= c.v_lo && sv < c.v_hi)) atomicOr(bitmap + (sv >> 5), 1u << (sv & 31));
+        if (c.world > 1 && !(sv >= c.v_lo && sv < c.v_hi)) marks[sv] = 1;
       }
     }
   }
@@ -1226,6 +1278,35 @@ hipError_t dalgo_gb_bucket_degree(const void* sorted, int packed, int64_t n, int
   return hipSuccess;
 }
 
+// marks: >= 32 nw bytes (16-B aligned); bits: nw words
+hipError_t dalgo_gb_bytes_to_bits(const uint8_t* marks, int64_t nw, uint32_t* bits, hipStream_t st) {
+  if (nw <= 0) return hipSuccess;
+  if (reinterpret_cast<uintptr_t>(marks) % 16) return hipErrorInvalidValue;
+  const int64_t g = std::min<int64_t>(cdiv(nw, (int64_t)256), 256 * 64);
+  hipLaunchKernelGGL(gb_bytes_to_bits_kernel, dim3((unsigned)g), dim3(256), 0, st,
+                     reinterpret_cast<const uint4*>(marks), nw, bits);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t dalgo_gb_bitmap_ids(const uint32_t* bm, int64_t nw, const int64_t* prefix, int64_t* ids,
+                               hipStream_t st) {
+  if (nw <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gb_bitmap_ids_kernel, dim3((unsigned)cdiv(nw, (int64_t)256)), dim3(256), 0, st, bm, nw,
+                     prefix, ids);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t dalgo_gb_deal(const int64_t* order, int64_t n, int world, int64_t sl, int32_t* new_id, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (world < 1 || sl * world < n || sl > 0x7fffffffLL) return hipErrorInvalidValue;
+  const int64_t g = std::min<int64_t>(cdiv(n, (int64_t)256), 256 * 64);
+  hipLaunchKernelGGL(gb_deal_kernel, dim3((unsigned)g), dim3(256), 0, st, order, n, world, sl, new_id);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
 int64_t dalgo_gb_owner_blocks(int64_t n) { return cdiv(n, (int64_t)kOwnR); }
 
 // phase 0: tmp[i] = new_id[src[i]] << 32 | new_id[dst[i]] (new_id nullable), counts[o * nb + b] =
@@ -1270,7 +1351,8 @@ hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, cons
     return hipSuccess;
   }
   if (phase == 0)
-    hipLaunchKernelGGL(gb_keys_count_kernel, dim3((unsigned)g), dim3(256), 0, st, src, dst, n, c, bitmap, counts);
+    hipLaunchKernelGGL(gb_keys_count_kernel, dim3((unsigned)g), dim3(256), 0, st, src, dst, n, c,
+                       reinterpret_cast<uint8_t*>(bitmap), counts);
   else
     hipLaunchKernelGGL(gb_keys_write_kernel, dim3((unsigned)g), dim3(256), 0, st, src, dst, n, c, offsets,
                        base_all, keys, packed);

@@ -317,6 +317,13 @@ struct KmAux {
   const int32_t* nb;                  // [k][kpad]: their ids
   const float* nd;                    // [k][kpad]: |c - c_a| rounded down, ascending
   int extend;                         // CAND: stream more chunks where l would be loose
+  // CAND + DRIFT: per list entry (aligned with nb) its distance to c_a (rounded down) and
+  // its centre's shift since the last iteration (rounded up)
+  const float* ndb;
+  const float* dnb;
+  const float* tau_cap;               // DRIFT (device, nullable): largest pruning threshold
+  int drift_ball;                     // DRIFT: also drop the centres outside the ball R (their
+                                      // bound nd_first - ua is loose where ua is small)
 };
 constexpr int kChgBuf = 512;          // changed rows buffered per block (LDS)
 
@@ -337,7 +344,7 @@ __device__ unsigned long long g_km_dbg[kDbgBlocks * kDbgTiles * kDbgSlots];
 #endif
 
 template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, bool TOP2 = false,
-          bool LOOP = false, bool CAND = false>
+          bool LOOP = false, bool CAND = false, bool DRIFT = false>
 __global__ void __launch_bounds__(NW * 64, MINB)
 kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
                           const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int kpad,
@@ -347,6 +354,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
                           const KmAux aux) {
   static_assert(!LOOP || TOP2, "the fused bound update needs the second-best distance");
   static_assert(!CAND || LOOP, "candidate pruning is a form of the filtered iteration");
+  static_assert(!DRIFT || CAND, "drift pruning refines the candidate lists");
   // idx (optional): the block's point j is row idx[j] of X (and of assign / mind), j < n
   // -- the bound-filtered form of Lloyd only re-assigns the points the filter keeps
   constexpr int KS = DP / 16;                  // 32x32x16 k-steps per centre row
@@ -365,6 +373,11 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   __shared__ float s_m[NW];
   __shared__ float s_r[NW];
   __shared__ int s_ext[NW];
+  __shared__ float s_tau[DRIFT ? NW : 1];
+  __shared__ int s_kc[DRIFT ? NW : 1];
+  __shared__ float s_kd[DRIFT ? NW : 1], s_kf[DRIFT ? NW : 1];
+  // DRIFT: every tile row's l (read again by the epilogue: not held in VGPRs over the sweep)
+  __shared__ float s_lold[DRIFT ? NW * PT * 32 : 1];
   __shared__ double s_sse[NW];
 
   __shared__ int s_chg[LOOP ? kChgBuf : 1];
@@ -578,14 +591,36 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   float hv[KH];
   int nbv[KH];
   float hna = 0.f;                             // CAND: 0.5|c_acl|^2
+  // DRIFT: entry p = KH tid + j of acl's list (consecutive per thread: one scan over the
+  // threads compacts the list) -- its distance to c_acl and its centre's shift; and the
+  // lower bound l of every tile row (vs the previous centres, from the last iteration)
+  float ndv[DRIFT ? KH : 1], dnv[DRIFT ? KH : 1], lold[DRIFT ? PT : 1];
   if constexpr (CAND) {
     hna = hn[acl];
-    if (lane < nchunk) thrv = aux.nd[(int64_t)acl * kpad + lane * CH];
+    if constexpr (DRIFT) {
+      static_assert(KH == 4, "DRIFT: four consecutive list entries per thread");
+      const bool in = tid * KH < kpad;
+      const int64_t o = (int64_t)acl * kpad + tid * KH;
+      const int4 i4 = in ? *reinterpret_cast<const int4*>(aux.nb + o) : make_int4(0, 0, 0, 0);
+      const float4 h4 = in ? *reinterpret_cast<const float4*>(hbase + tid * KH) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float inf = __builtin_inff();
+      const float4 n4 = in ? *reinterpret_cast<const float4*>(aux.ndb + o) : make_float4(inf, inf, inf, inf);
+      const float4 d4 = in ? *reinterpret_cast<const float4*>(aux.dnb + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+      nbv[0] = i4.x; nbv[1] = i4.y; nbv[2] = i4.z; nbv[3] = i4.w;
+      hv[0] = h4.x; hv[1] = h4.y; hv[2] = h4.z; hv[3] = h4.w;
+      ndv[0] = n4.x; ndv[1] = n4.y; ndv[2] = n4.z; ndv[3] = n4.w;
+      dnv[0] = d4.x; dnv[1] = d4.y; dnv[2] = d4.z; dnv[3] = d4.w;
+      const float* ulf = reinterpret_cast<const float*>(aux.ul);
 #pragma unroll
-    for (int j = 0; j < KH; ++j) {
-      const bool in = tid + j * NT < kpad;
-      hv[j] = in ? hbase[tid + j * NT] : 0.f;
-      nbv[j] = in ? aux.nb[(int64_t)acl * kpad + tid + j * NT] : 0;
+      for (int t = 0; t < PT; ++t) lold[t] = ulf[2 * (int64_t)rowk[t] + 1];
+    } else {
+      if (lane < nchunk) thrv = aux.nd[(int64_t)acl * kpad + lane * CH];
+#pragma unroll
+      for (int j = 0; j < KH; ++j) {
+        const bool in = tid + j * NT < kpad;
+        hv[j] = in ? hbase[tid + j * NT] : 0.f;
+        nbv[j] = in ? aux.nb[(int64_t)acl * kpad + tid + j * NT] : 0;
+      }
     }
     load_rec(bt + gridDim.x);            // the next tile's record (tr holds this one's)
   }
@@ -623,9 +658,17 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
         bf[t][s] = make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
       }
     }
+    if constexpr (DRIFT) {
+      // chunk 0 (acl and its CH - 1 nearest, always streamed) now; the rest of the list
+      // is compacted after the tile's bounds are known
 #pragma unroll
-    for (int j = 0; j < KH; ++j)
-      if (tid + j * NT < kpad) s_nb[par][tid + j * NT] = (uint16_t)nbv[j];
+      for (int j = 0; j < KH; ++j)
+        if (tid * KH + j < CH) s_nb[par][tid * KH + j] = (uint16_t)nbv[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < KH; ++j)
+        if (tid + j * NT < kpad) s_nb[par][tid + j * NT] = (uint16_t)nbv[j];
+    }
     // every wave has its fragments (the chunk buffers are free again) and the list is
     // staged: chunk 0 -- always streamed -- goes out now, under the set-up below
     __syncthreads();
@@ -680,13 +723,27 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   // previous tile precedes all of its reads), so the block barrier below orders the
   // rewrite after them
   float um = 0.f;
+  float tv = __builtin_inff();                 // DRIFT: min over the tile rows of l - u
   if constexpr (CAND) {
 #pragma unroll
-    for (int t = 0; t < PT; ++t)
-      if (pbase + t * 32 + cl < pend) um = fmaxf(um, ua[t]);
-    for (int off = 32; off >= 1; off >>= 1) um = fmaxf(um, __shfl_xor(um, off));
+    for (int t = 0; t < PT; ++t) {
+      if (pbase + t * 32 + cl < pend) {
+        um = fmaxf(um, ua[t]);
+        if constexpr (DRIFT) tv = fminf(tv, km_dn1(lold[t] - ua[t]));
+      }
+      // (the previous tile's epilogue reads of s_lold precede this tile's first barrier)
+      if constexpr (DRIFT) if (h == 0) s_lold[(wid * PT + t) * 32 + cl] = lold[t];
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+      um = fmaxf(um, __shfl_xor(um, off));
+      if constexpr (DRIFT) tv = fminf(tv, __shfl_xor(tv, off));
+    }
   }
-  if (lane == 0) { s_m[wid] = mx; if constexpr (CAND) s_r[wid] = um; }
+  if (lane == 0) {
+    s_m[wid] = mx;
+    if constexpr (CAND) s_r[wid] = um;
+    if constexpr (DRIFT) s_tau[wid] = tv;
+  }
   __syncthreads();
   // CAND: the tile's centre stream is cluster acl's neighbour list. ua >= |x - c_acl| for
   // every tile point, so only centres c with |c - c_acl| <= R = 2 max ua can be the
@@ -696,13 +753,76 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   KM_TS(2)
   int nch_t = nchunk;
   float nd_first = __builtin_inff();   // CAND: smallest distance of a pruned centre
+  float dmp = -__builtin_inff();       // DRIFT: largest shift of a drift-pruned centre
+  int kept = 0;                        // DRIFT: list entries kept past chunk 0
+  int sp[DRIFT ? KH : 1];              // DRIFT: stream position of the thread's entries
   if constexpr (CAND) {
     float R = s_r[0];
 #pragma unroll
     for (int w = 1; w < NW; ++w) R = fmaxf(R, s_r[w]);
     R = km_up1(2.f * R);
-    // chunk j >= 1 is needed iff its first (smallest) distance is <= R; chunk 0 always
-    nch_t = 1 + __popcll(__ballot(lane >= 1 && lane < nchunk && thrv <= R));
+    if constexpr (DRIFT) {
+      // Past chunk 0 an entry c of the list is streamed iff |c - c_acl| <= R (the ball) AND
+      // its shift delta_c >= tau = min over the tile rows of (l - ua): l <= |x - c_prev| for
+      // every c other than acl (last iteration's centres), so a centre with delta_c < tau has
+      // |x - c| >= l - delta_c > ua >= |x - c_acl| for every tile row and cannot be the
+      // nearest. The kept entries are compacted (block scan) behind chunk 0; the pruned
+      // ones bound l by nd_first - ua (ball) and l - dmp (drift)
+      float tau = s_tau[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) tau = fminf(tau, s_tau[w]);
+      // a pruned centre costs the rows up to tau of their lower bound l (the next filter
+      // tests l - maxd): the threshold is capped so only the slow centres are dropped
+      if (aux.tau_cap != nullptr) tau = fminf(tau, *aux.tau_cap);
+      int c = 0;
+      float dm = -__builtin_inff(), nf = __builtin_inff();
+      bool keep[KH];
+#pragma unroll
+      for (int j = 0; j < KH; ++j) {
+        const int p = tid * KH + j;
+        const bool tail = p >= CH && p < kpad;
+        const bool ball = !aux.drift_ball || ndv[j] <= R;
+        keep[j] = tail && ball && dnv[j] >= tau;
+        c += keep[j] ? 1 : 0;
+        // every dropped centre c has |x - c| >= l - delta_c (drift bound) and, outside the
+        // ball, also >= |c - c_acl| - ua: the slow ones (delta_c < tau) enter the new l
+        // through l - dmp, the fast ones outside the ball through nd_first - ua (the first
+        // distance among them only, not among every dropped centre: tight l where ua is small)
+        if (tail && !keep[j]) {
+          if (dnv[j] < tau) dm = fmaxf(dm, dnv[j]);
+          else nf = fminf(nf, ndv[j]);
+        }
+      }
+      int x = c;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+      }
+      for (int off = 32; off >= 1; off >>= 1) {
+        dm = fmaxf(dm, __shfl_xor(dm, off));
+        nf = fminf(nf, __shfl_xor(nf, off));
+      }
+      if (lane == 63) s_kc[wid] = x;
+      if (lane == 0) { s_kd[wid] = dm; s_kf[wid] = nf; }
+      __syncthreads();
+      int pre = x - c;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        if (w < wid) pre += s_kc[w];
+        kept += s_kc[w];
+        dmp = fmaxf(dmp, s_kd[w]);
+        nd_first = fminf(nd_first, s_kf[w]);
+      }
+      nch_t = 1 + (kept + CH - 1) / CH;
+#pragma unroll
+      for (int j = 0; j < KH; ++j) {
+        sp[j] = keep[j] ? CH + pre : -1;
+        if (keep[j]) s_nb[par][CH + pre++] = (uint16_t)nbv[j];
+      }
+    } else {
+      // chunk j >= 1 is needed iff its first (smallest) distance is <= R; chunk 0 always
+      nch_t = 1 + __popcll(__ballot(lane >= 1 && lane < nchunk && thrv <= R));
+    }
   }
   if constexpr (LOOP) {
     // every wave is past the previous tile's appends: room for this tile's (<= TILE)?
@@ -713,7 +833,21 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   for (int w = 1; w < NW; ++w) M = fmaxf(M, s_m[w]);
   // slack so that rounding of the MFMA sum cannot push a near-zero distance negative
   M = M * 1.0001f + 1e-6f;
-  if constexpr (CAND) {
+  if constexpr (DRIFT) {
+    // 0.5|c|^2 + M in stream order: chunk 0 as listed, the kept entries at their compacted
+    // places (sp, from the scan), then padding up to whole chunks (acl, never the nearest:
+    // 1e30 as hn's padding centres)
+#pragma unroll
+    for (int j = 0; j < KH; ++j) {
+      const int p = tid * KH + j;
+      if (p < CH) s_hn[p] = hv[j] + M;
+      else if (sp[j] >= 0) s_hn[sp[j]] = hv[j] + M;
+    }
+    for (int q = CH + kept + tid; q < nch_t * CH; q += NT) {
+      s_hn[q] = 1e30f + M;
+      s_nb[par][q] = (uint16_t)acl;
+    }
+  } else if constexpr (CAND) {
 #pragma unroll
     for (int j = 0; j < KH; ++j)
       if (tid + j * NT < kpad) s_hn[tid + j * NT] = hv[j] + M;   // extensions read past nch_t
@@ -854,7 +988,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
     }
     if (NBUF >= 3 && ch + NBUF - 1 < nch_t) issue(ch + NBUF - 1);
     if constexpr (CAND) {
-      if (aux.extend && ch == nch_t - 1 && nch_t < nchunk) {
+      if (!DRIFT && aux.extend && ch == nch_t - 1 && nch_t < nchunk) {
         // The pruned centres bound l from below by nd_first - ua only. Where that is below
         // a point's second-best distance so far, its l (and the next iteration's filter)
         // would be loose: then the tile streams one more chunk (block-uniform decision)
@@ -893,7 +1027,7 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
   KM_TS(4)
   // (warming L2 with the next tile's rows by throw-away LDS-DMA here measured no gain:
   // 17.92 vs 17.86 ms per iteration of the benchmark job)
-  if constexpr (CAND)
+  if constexpr (CAND && !DRIFT)
     if (nch_t < nchunk) nd_first = __shfl(thrv, nch_t);
 
   // ---- decode, combine the two lane halves (same point, disjoint centre rows)
@@ -932,6 +1066,8 @@ kmeans_assign_pipe_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx
         float lo2 = km_dn1(sqrtf(fmaxf(km_dn1(dist2 - tol), 0.f)));
         // CAND: every pruned centre is >= nd_first - |x - c_acl| from x
         if constexpr (CAND) lo2 = fminf(lo2, km_dn1(nd_first - ua[t]));
+        // DRIFT: every drift-pruned centre is >= l - dmp from x (dmp = -inf: none pruned)
+        if constexpr (DRIFT) lo2 = fminf(lo2, km_dn1(s_lold[(wid * PT + t) * 32 + cl] - dmp));
         // the rows are scattered over X, so each store is a separate partial line write
         // (the kernel's largest cost after the MFMAs): u and l go out as one 8-byte pair,
         // and assign only where the cluster changed (assign[row] holds old_c otherwise)
@@ -1543,7 +1679,7 @@ static int device_cus() {
 // Device-resident count (mcount, n = its upper bound): a resident grid (MINB blocks per
 // CU) walks the tiles, so the launch needs no host sync.
 template <int DP, int NW, int PT, int NSUB, int MINB, int NBUF, bool PF, bool TOP2 = false,
-          bool LOOP = false, bool CAND = false>
+          bool LOOP = false, bool CAND = false, bool DRIFT = false>
 static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                      const float* hn, int kpad, int* assign, float* mind,
                                      double* sse, int sse_mask, hipStream_t st,
@@ -1565,11 +1701,12 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
   if (CAND && (kpad > 1024 || aux.tiles == nullptr || aux.n_tiles == nullptr || aux.hnb == nullptr ||
                aux.nb == nullptr || aux.nd == nullptr || idx == nullptr))
     return hipErrorInvalidValue;
+  if (DRIFT && (aux.ndb == nullptr || aux.dnb == nullptr || kpad % 4 != 0)) return hipErrorInvalidValue;
   // CAND: up to n / TILE + k tiles (device count) -> always the resident grid
   if (CAND) grid = (int64_t)device_cus() * MINB;
   else if (LOOP) grid = std::min<int64_t>(grid, (int64_t)device_cus() * MINB);
   if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
-  auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF, TOP2, LOOP, CAND>;
+  auto kfn = kmeans_assign_pipe_kernel<DP, NW, PT, NSUB, MINB, NBUF, PF, TOP2, LOOP, CAND, DRIFT>;
   static size_t attr_set = 0;   // largest dynamic size this instantiation was enabled for
   if (dyn > attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2227,6 +2364,17 @@ hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP
       aux.tiles = reinterpret_cast<const int4*>(cand->tiles);
       aux.n_tiles = cand->n_tiles; aux.hnb = cand->hnb;
       aux.nb = cand->nb; aux.nd = cand->nd; aux.extend = cand->extend;
+      aux.ndb = cand->ndb; aux.dnb = cand->dnb; aux.tau_cap = cand->tau_cap;
+      aux.drift_ball = cand->extend;   // (no extension chunks in the drift form)
+      if (cand->ndb != nullptr) {   // drift-aware candidate lists
+        if (DP == 128)
+          return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true, true, true, true>(
+              X, m, ldx, Cq, hn, kpad, assign, nullptr, sse, sse_mask, st, idx, nullptr, aux);
+        if (DP == 64)
+          return launch_assign_pipe<64, 4, 2, 4, 2, 2, false, true, true, true, true>(
+              X, m, ldx, Cq, hn, kpad, assign, nullptr, sse, sse_mask, st, idx, nullptr, aux);
+        return hipErrorInvalidValue;
+      }
       if (DP == 128)
         return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true, true, true>(
             X, m, ldx, Cq, hn, kpad, assign, nullptr, sse, sse_mask, st, idx, nullptr, aux);

@@ -264,11 +264,12 @@ __global__ void __launch_bounds__(256)
 km_centre_nbrs_kernel(const uint16_t* __restrict__ cq, const uint16_t* __restrict__ cprev,
                       const float* __restrict__ hn, int k, int kpad, int d, int DP,
                       float* __restrict__ delta, float* __restrict__ sout, float* __restrict__ nd,
-                      int32_t* __restrict__ nb, float* __restrict__ hnb) {
+                      int32_t* __restrict__ nb, float* __restrict__ hnb, float* __restrict__ ndb) {
   __shared__ double s_c[128];
   __shared__ float s_d[2048];
   __shared__ int32_t s_i[2048];
   __shared__ int32_t s_g[2048];
+  __shared__ float s_gd[2048];
   __shared__ double s_red[2][4];
   const int a = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   double dd = 0.0;
@@ -332,12 +333,25 @@ km_centre_nbrs_kernel(const uint16_t* __restrict__ cq, const uint16_t* __restric
     int rank = 0;
     for (int q = 0; q < 32; ++q) rank += s_i[g0 + q] < id ? 1 : 0;
     s_g[g0 + rank] = id;
+    s_gd[g0 + rank] = s_d[j];
     nd[base + j] = s_d[j];
   }
   __syncthreads();
   for (int j = tid; j < kpad; j += 256) {
     nb[base + j] = s_g[j];
     hnb[base + j] = hn[s_g[j]];
+    if (ndb) ndb[base + j] = s_gd[j];
+  }
+}
+
+// drift-aware lists: dnb[a][j] = delta[nb[a][j]] (every centre's shift, after the launch
+// that computes them; padding entries: 0)
+__global__ void __launch_bounds__(256)
+km_nbr_drift_kernel(const int32_t* __restrict__ nb, const float* __restrict__ delta, int k, int64_t total,
+                    float* __restrict__ dnb) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = nb[i];
+    dnb[i] = c < k ? delta[c] : 0.f;
   }
 }
 
@@ -409,13 +423,19 @@ hipError_t dalgo_km_centre_bounds(const void* cnow, const void* cprev, int is_bf
 
 hipError_t dalgo_km_centre_nbrs(const void* cq, const void* cprev, const float* hn, int k, int kpad,
                                 int d, int DP, float* delta, float* s, float* nd, int32_t* nb,
-                                float* hnb, hipStream_t st) {
+                                float* hnb, float* ndb, float* dnb, hipStream_t st) {
   if (k <= 0) return hipSuccess;
   if (d > 128 || d > DP || kpad > 2048 || kpad < k || kpad % 32 != 0 || DP % 8 != 0)
     return hipErrorInvalidValue;
+  if ((ndb == nullptr) != (dnb == nullptr)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(dalgo::km_centre_nbrs_kernel, dim3(k), dim3(256), 0, st,
                      (const uint16_t*)cq, (const uint16_t*)cprev, hn, k, kpad, d, DP, delta, s, nd,
-                     nb, hnb);
+                     nb, hnb, ndb);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || dnb == nullptr) return e;
+  const int64_t total = (int64_t)k * kpad;
+  hipLaunchKernelGGL(dalgo::km_nbr_drift_kernel, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 4096)),
+                     dim3(256), 0, st, nb, delta, k, total, dnb);
   return hipGetLastError();
 }
 

@@ -48,6 +48,9 @@ struct DalgoKmCand {
   const int32_t* nb;
   const float* nd;
   int extend;                         // stream extra chunks for tight lower bounds
+  const float* ndb;                   // nullable: drift-aware lists (nd aligned with nb)
+  const float* dnb;                   //           and each entry's centre shift
+  const float* tau_cap;               // nullable (device): cap of the drift threshold
 };
 
 extern "C" {
@@ -153,7 +156,7 @@ hipError_t dalgo_kmeans_sort_active(const int32_t* acl, const int32_t* idx, int6
                                     int64_t max_tiles, hipStream_t st);
 hipError_t dalgo_km_centre_nbrs(const void* cq, const void* cprev, const float* hn, int k, int kpad,
                                 int d, int DP, float* delta, float* s, float* nd, int32_t* nb,
-                                float* hnb, hipStream_t st);
+                                float* hnb, float* ndb, float* dnb, hipStream_t st);
 hipError_t dalgo_km_bounds_init(const float* mind, const float* mind2, const unsigned* xmax,
                                 int64_t n, float* ul, float* tol, hipStream_t st);
 
@@ -227,6 +230,10 @@ hipError_t dalgo_gb_relabel_src(uint64_t* packed, int64_t n, const int32_t* new_
 hipError_t dalgo_gb_pack(const int32_t* src, const int32_t* dst, int64_t n, uint64_t* out, hipStream_t st);
 int64_t dalgo_gb_key_blocks(int64_t n);
 int64_t dalgo_gb_owner_blocks(int64_t n);
+hipError_t dalgo_gb_bytes_to_bits(const uint8_t* marks, int64_t nw, uint32_t* bits, hipStream_t st);
+hipError_t dalgo_gb_bitmap_ids(const uint32_t* bm, int64_t nw, const int64_t* prefix, int64_t* ids,
+                               hipStream_t st);
+hipError_t dalgo_gb_deal(const int64_t* order, int64_t n, int world, int64_t sl, int32_t* new_id, hipStream_t st);
 hipError_t dalgo_gb_owner_scatter(int phase, const int32_t* src, const int32_t* dst, int64_t n,
                                   const int32_t* new_id, int64_t sl, int world, uint64_t* tmp,
                                   int64_t* counts, const int64_t* offsets, uint64_t* out, hipStream_t st);

@@ -118,7 +118,7 @@ def kmeans_witness(km, rt) -> dict:
 def kmeans_job(rt, rows: int = 100_000_000, dim: int = 128, k: int = 1024, iters: int = 5,
                dtype=torch.bfloat16, noise: float = 1.0, data_seed: int = 7,
                bound_filter: bool = True, candidates: bool = True, witness: bool = True,
-               warm: bool = True, pool_gb: float = 48.0, dense: str = "auto") -> dict:
+               warm: bool = True, pool_gb: float = 48.0, dense: str = "auto", drift: bool = True) -> dict:
     """BASELINE config #4 (100M x 128, k = 1024): the reference's k-means job, strong
     scaling (the global point set is row-sharded over the ranks)."""
     from dalgo.data.synthetic import blobs
@@ -135,7 +135,7 @@ def kmeans_job(rt, rows: int = 100_000_000, dim: int = 128, k: int = 1024, iters
         Xw = blobs(wn, dim, k, row_range=(wlo, whi), device=rt.device, dtype=dtype, seed=3,
                    noise=noise)
         kw = KMeans(KMeansConfig(k=min(k, wn), n_iterations=3, seed=5, bound_filter=bound_filter,
-                                 candidates=candidates, dense=dense), Xw, wlo, wn)
+                                 candidates=candidates, dense=dense, drift=drift), Xw, wlo, wn)
         kw.step()
         kw.step()
         kw.step()
@@ -151,7 +151,7 @@ def kmeans_job(rt, rows: int = 100_000_000, dim: int = 128, k: int = 1024, iters
     t = time.perf_counter()
     ev.mark()
     km = KMeans(KMeansConfig(k=k, n_iterations=iters, seed=1, bound_filter=bound_filter,
-                             candidates=candidates, dense=dense), X, lo, rows)
+                             candidates=candidates, dense=dense, drift=drift), X, lo, rows)
     ev.mark()
     for _ in range(iters):
         km.step()
@@ -179,7 +179,7 @@ def kmeans_job(rt, rows: int = 100_000_000, dim: int = 128, k: int = 1024, iters
         "full_pass_tflops_per_gpu": (flops / W / (iter_ms[0] / 1e3) / 1e12) if iter_ms else None,
         "reassigned_rows_per_iter_rank0": active, "moved_rows_per_iter_rank0": moved,
         "bound_filter": km.bounds, "candidate_pruning": getattr(km, "_cand", None) is not None,
-        "dense_filtered_iterations": dense,
+        "dense_filtered_iterations": dense, "drift_pruned_candidates": drift,
         "dense_k2_rows_per_iter_rank0": dense_rows,
         "incremental_k3": km.incremental, "sse_last_iteration": float(sse_last.item()),
         "correctness_witness": wit,

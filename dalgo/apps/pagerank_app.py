@@ -59,6 +59,12 @@ def deal_ids(order: torch.Tensor, n_vertices: int, world: int) -> torch.Tensor:
         new_id[order] = torch.arange(n_vertices, device=dev, dtype=torch.int64)
         return new_id
     sl = G.vertex_slices(n_vertices, world)
+    if dev.type == "cuda" and sl * world == n_vertices:
+        # every slice full: one scatter kernel (graph_build.hip gb_deal)
+        from dalgo.ops import _ext
+        new_id = torch.empty(n_vertices, dtype=torch.int32, device=dev)
+        _ext.ops().gb_deal(order.to(torch.int64).contiguous(), world, sl, new_id)
+        return new_id
     j = torch.arange(n_vertices, device=dev, dtype=torch.int64)
     p = j // world
     r = torch.where(p % 2 == 0, j % world, world - 1 - j % world)

@@ -55,6 +55,11 @@ class KMeansConfig:
     # the device, every iteration with >= DENSE_FRACTION of the rows active; "always";
     # "never"
     dense: str = "auto"
+    # candidate lists also pruned by the centre shifts (Elkan's per-centre drift bound at
+    # tile granularity, with the single Hamerly l per row): past the first chunk, a centre
+    # whose shift since the last iteration is below min over the tile of (l - u) cannot
+    # be the nearest of any tile row
+    drift: bool = True
     # GPU, k <= 2048: incremental K3 (only moved rows re-summed) and the bound-filter state.
     # Costs ~24 B/row (move workspace) + ~48 B/row (bounds, candidates) of HBM on top of X
     # (bf16 d = 128: X is 256 B/row); False = plain full-pass Lloyd, no per-row state
@@ -76,6 +81,20 @@ class KMeansHistory:
 # k = 1024): the dense form wins at 49-100 % active rows (overlapping blobs), the pruned
 # one at 19-32 % (separated blobs); at ~70 % they tie
 DENSE_FRACTION = 0.4
+# with drift-aware candidate lists the pruned form wins at higher active fractions: 100M x
+# 128, k = 1024 (profiles/round6/r6_8): overlapping blobs 100.0 -> 93.7 ms per job (pruned
+# at 49-75 % active instead of dense), separated blobs 73.8 -> 74.5 ms (iteration 3 at 70 %
+# active: 17.3 -> 12.5 ms, but its looser lower bounds leave 59M instead of 32M rows active
+# in iteration 4: 5.9 -> 10.8 ms)
+DENSE_FRACTION_DRIFT = 0.75
+
+
+def _dense_fraction(drift: bool) -> float:
+    import os
+    v = os.environ.get("DALGO_KM_DENSE_FRACTION")
+    if v is not None:
+        return float(v)
+    return DENSE_FRACTION_DRIFT if drift else DENSE_FRACTION
 
 
 def sample_rows(n_global: int, k: int, seed: int) -> np.ndarray:
@@ -164,7 +183,7 @@ class KMeans:
                                changed=self._changed, n_changed=self._n_changed)
         # candidate pruning (Exponion-style at tile granularity): the active rows sorted by
         # cluster, every tile's centre stream cut to a prefix of its centre's neighbour list
-        self._cand = (K.CandWorkspace(self.dev, n, k, self.cen.Cq.shape[0], self.DP)
+        self._cand = (K.CandWorkspace(self.dev, n, k, self.cen.Cq.shape[0], self.DP, drift=self.cfg.drift)
                       if self.cfg.candidates and self.cen.Cq.shape[0] <= 1024 else None)
         if self._cand is not None:
             # the candidate K2 takes the previous cluster from its tile and writes the moved
@@ -293,7 +312,7 @@ class KMeans:
                 n_cand, n_dense = self._n_active, self._n_active
                 if form == "device":
                     # dense iff active >= DENSE_FRACTION n (no host sync)
-                    on = self._n_active >= int(math.ceil(DENSE_FRACTION * n))
+                    on = self._n_active >= int(math.ceil(_dense_fraction(cw.ndb is not None) * n))
                     torch.mul(self._n_active, on, out=self._n_dense)
                     torch.sub(self._n_active, self._n_dense, out=self._n_cand)
                     n_cand, n_dense = self._n_cand, self._n_dense
@@ -307,9 +326,13 @@ class KMeans:
                 # are so large that the next filter never decides on l (the same active
                 # rows either way, profiles/round4/r4_13), so tight l there is pure cost
                 if form in ("cand", "device", "bounds"):
+                    # drift-aware lists: `extend` selects whether the Exponion ball also
+                    # drops centres (no extension chunks in that form)
+                    ext = (K.drift_ball() if cw is not None and cw.ndb is not None
+                           else not self._just_full)
                     K.assign_rows(self.X, self.cen, cw.rows if cw is not None else self._idx, n,
                                   self.assign, post=dict(self._post_args, m_dev=n_cand), cand=cw,
-                                  extend=not self._just_full)
+                                  extend=ext)
                 if form in ("dense", "device"):
                     K.assign_rows(self.X, self.cen, self._idx, n, self.assign,
                                   post=dict(self._post_args, m_dev=n_dense, acl=cw.acl))

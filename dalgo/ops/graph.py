@@ -604,27 +604,31 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     i32 = dict(dtype=torch.int32, device=dev)
     nid = new_id.to(torch.int32).contiguous() if new_id is not None else None
     # ---- phase 0: kept edges per key block (+ remote-source marks, W > 1)
-    bitmap = torch.zeros((N + 31) // 32 + 1, **i32) if W > 1 else None
+    nwords = (N + 31) // 32 + 1
+    bitmap = torch.empty(nwords, **i32) if W > 1 else None
     nbs = [(int(s.numel()) + 16383) // 16384 for s, _ in edges]     # graph_build.hip kKeyR
     if W > 1:
         counts = torch.empty(sum(nbs), **i32)
+        # remote sources: one byte per id (plain stores), packed into the bitmap after
+        marks = torch.zeros(max(32 * nwords, sl * W), dtype=torch.uint8, device=dev)
         o = 0
         for (s, d), nb in zip(edges, nbs):
-            ops.gb_keys(s, d, nid, v_lo, v_hi, sl, W, rank, dbits, 0, bitmap, counts[o:o + nb], None, 0,
+            ops.gb_keys(s, d, nid, v_lo, v_hi, sl, W, rank, dbits, 0, marks, counts[o:o + nb], None, 0,
                         None, None, None, None)
             o += nb
+        ops.gb_bytes_to_bits(marks, bitmap)
+        del marks
         c64 = counts.to(torch.int64)
         offsets = torch.cumsum(c64, 0) - c64
         total = int(c64.sum().item())
         pc = _popcount32(bitmap)
         word_prefix = torch.cumsum(pc, 0) - pc
         n_ghost = int(pc.sum().item())
-        bits = (bitmap.to(torch.int64)[:, None] >> torch.arange(32, device=dev)) & 1
-        ghosts = torch.nonzero(bits.flatten()).flatten()
-        del bits
-        assert int(ghosts.numel()) == n_ghost
-        recv = torch.bincount(ghosts // sl, minlength=W)[:W]
-        recv_counts = [int(x) for x in recv.tolist()]
+        ghosts = torch.empty(n_ghost, **i64)
+        ops.gb_bitmap_ids(bitmap, word_prefix, ghosts)     # sorted ids of the set bits
+        # ghosts per owner: the sorted list cut at the slice boundaries
+        cuts = torch.searchsorted(ghosts, torch.arange(W + 1, **i64) * sl)
+        recv_counts = [int(x) for x in torch.diff(cuts).tolist()]
     else:
         total = sum(int(s.numel()) for s, _ in edges)
         offsets, word_prefix, ghosts, n_ghost, recv_counts = None, None, None, 0, [0]

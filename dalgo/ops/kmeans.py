@@ -244,7 +244,7 @@ class CandWorkspace:
     padded, <= 1024): per-centre neighbour lists (nd / nb / hnb, k * kpad each), the
     cluster-sorted active rows and the tile table."""
 
-    def __init__(self, device, n: int, k: int, kpad: int, DP: int):
+    def __init__(self, device, n: int, k: int, kpad: int, DP: int, drift: bool = False):
         i32 = dict(dtype=torch.int32, device=device)
         i64 = dict(dtype=torch.int64, device=device)
         f32 = dict(dtype=torch.float32, device=device)
@@ -253,6 +253,12 @@ class CandWorkspace:
         self.nd = torch.empty(k * kpad, **f32)
         self.nb = torch.empty(k * kpad, **i32)
         self.hnb = torch.empty(k * kpad, **f32)
+        # drift-aware lists: every entry's distance to the list's centre (aligned with nb)
+        # and its centre's shift since the last iteration
+        self.ndb = torch.empty(k * kpad, **f32) if drift else None
+        self.dnb = torch.empty(k * kpad, **f32) if drift else None
+        # cap of the drift threshold (device): the DRIFT_QUANTILE of this iteration's shifts
+        self.tau_cap = torch.full((1,), float("inf"), **f32) if drift else None
         self.acl = torch.empty(n, **i32)
         self.rows = torch.empty(n, **i32)
         bmax = max(1, (n + CHUNK_ROWS - 1) // CHUNK_ROWS)
@@ -265,7 +271,8 @@ class CandWorkspace:
         self.n_tiles = torch.zeros(1, **i64)
 
     def cand(self):
-        return [self.tiles, self.n_tiles, self.hnb, self.nb, self.nd]
+        c = [self.tiles, self.n_tiles, self.hnb, self.nb, self.nd]
+        return c + [self.ndb, self.dnb, self.tau_cap] if self.ndb is not None else c
 
 
 def centre_nbrs(cen: Centers, Cq_prev: torch.Tensor, delta: torch.Tensor, s: torch.Tensor,
@@ -273,7 +280,36 @@ def centre_nbrs(cen: Centers, Cq_prev: torch.Tensor, delta: torch.Tensor, s: tor
     """delta / s as centre_bounds, plus every centre's neighbour lists for the pruned K2
     (one launch, kmeans_inc.hip km_centre_nbrs_kernel)."""
     _ext.ops().kmeans_centre_nbrs(cen.Cq, Cq_prev, cen.hn, ws.k, cen.d, delta, s, ws.nd, ws.nb,
-                                  ws.hnb)
+                                  ws.hnb, ws.ndb, ws.dnb)
+    if ws.tau_cap is not None:
+        # only centres slower than this quantile of the shifts are dropped: a dropped centre
+        # costs the rows its shift of lower bound, which the next filter pays
+        q = drift_quantile()
+        if q < 1.0:
+            kq = max(1, min(ws.k, int(round(q * ws.k))))
+            torch.kthvalue(delta[: ws.k], kq, out=(ws.tau_cap.view(()), torch.empty((), dtype=torch.int64,
+                                                                                     device=delta.device)))
+        else:
+            ws.tau_cap.fill_(float("inf"))
+
+
+def drift_quantile() -> float:
+    """Quantile of the centre shifts that caps the drift-pruning threshold
+    (DALGO_KM_DRIFT_Q, default DRIFT_QUANTILE; >= 1: no cap)."""
+    import os
+    return float(os.environ.get("DALGO_KM_DRIFT_Q", DRIFT_QUANTILE))
+
+
+# (profiles/round6/r6_6 - r6_8: 0.5 / 0.75 / 0.9 / none measured; 0.9 best over both data sets)
+DRIFT_QUANTILE = 0.9
+
+
+def drift_ball() -> bool:
+    """Drift-aware lists: also drop the fast centres outside the Exponion ball
+    (DALGO_KM_DRIFT_BALL, default on; off streams every fast centre: 94 -> 106 ms on
+    overlapping blobs, profiles/round6/r6_7)."""
+    import os
+    return os.environ.get("DALGO_KM_DRIFT_BALL", "1") == "1"
 
 
 def sort_active(idx: torch.Tensor, n_active: torch.Tensor, ws: CandWorkspace):
@@ -307,7 +343,12 @@ def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
     neighbour list within 2 max(ua) of c_a (ua = the tile's distances to c_a, computed in
     the tile prologue and rounded up); the pruned centres enter the new lower bound as
     nd_first - ua. ``extend``: where that bound would be looser than a point's second
-    best, the tile streams more chunks (tight l for the next filter)."""
+    best, the tile streams more chunks (tight l for the next filter). A drift-aware
+    workspace (``CandWorkspace(drift=True)``) also drops, past the first chunk, every
+    centre whose shift is below min over the tile rows of (l - ua): such a centre is
+    farther than c_a from every tile point (l bounds the distances to the previous
+    centres); the kept entries are compacted in the tile prologue, the dropped ones bound
+    the new l by l - (their largest shift), and no extension chunks are streamed."""
     if post is None:
         _ext.ops().kmeans_assign_idx(X, cen.Cq, cen.hn, idx, int(m), assign, [], mind, mind2, xh,
                                      xmax)

@@ -917,10 +917,20 @@ def test_kmeans_centre_nbrs_kernel(cuda, k, d):
     kpad, DP = cen.Cq.shape
     prev = cen.Cq[:k].clone()
     prev[:, :d] = (prev[:, :d].float() + 0.1 * torch.randn(k, d, device=cuda)).to(torch.bfloat16)
-    ws = K.CandWorkspace(cuda, 1000, k, kpad, DP)
+    ws = K.CandWorkspace(cuda, 1000, k, kpad, DP, drift=True)
     delta = torch.empty(k, device=cuda)
     s = torch.empty(k, device=cuda)
     K.centre_nbrs(cen, prev, delta, s, ws)
+    # drift-aware lists: each entry's own distance (rounded down) and its centre's shift
+    nbl = ws.nb.view(k, kpad).long()
+    Dl = torch.cdist(cen.Cq[:k, :d].double(), cen.Cq[:k, :d].double())
+    ndb = ws.ndb.view(k, kpad)
+    real = nbl < k
+    got_d = Dl.gather(1, nbl.clamp(max=k - 1))
+    assert bool((ndb[real].double() <= got_d[real] + 1e-9).all())
+    assert torch.allclose(ndb[real].double(), got_d[real], rtol=1e-5, atol=1e-5)
+    assert bool(torch.isinf(ndb[~real]).all())
+    assert torch.equal(ws.dnb.view(k, kpad)[real], delta[nbl[real]])
     d0, s0 = K.centre_bounds(cen.Cq, prev, k, d)
     assert torch.equal(delta, d0) and torch.equal(s, s0)
     C = cen.Cq[:k, :d].double()
@@ -1057,18 +1067,20 @@ def test_kmeans_candidates_match_plain(cuda):
     X = blobs(n, d, k, device=cuda, dtype=torch.bfloat16, seed=11)
     runs = {}
     for name, kw in [("cand", {}), ("bounds", dict(candidates=False)),
-                     ("plain", dict(bound_filter=False)), ("dense", dict(dense="always"))]:
+                     ("plain", dict(bound_filter=False)), ("dense", dict(dense="always")),
+                     ("cand_nodrift", dict(drift=False)), ("cand_never", dict(dense="never"))]:
         km = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5, **kw), X, 0, n)
         km.fit()
         runs[name] = km
     assert runs["cand"]._cand is not None and runs["bounds"]._cand is None
-    for other in ("bounds", "plain", "dense"):
+    assert runs["cand"]._cand.ndb is not None and runs["cand_nodrift"]._cand.ndb is None
+    for other in ("bounds", "plain", "dense", "cand_nodrift", "cand_never"):
         assert np.allclose(runs["cand"].history.sse, runs[other].history.sse, rtol=2e-4)
     ha, hb = runs["cand"].active_history, runs["bounds"].active_history
     assert ha[0] == n and len(ha) == len(hb)
     # the oracle: every candidate-pruned step (the dense one right after the full pass
     # included) against brute force from the same state; then the dense form on every step
-    for kw in ({}, dict(dense="always")):
+    for kw in ({}, dict(dense="always"), dict(dense="never"), dict(dense="never", drift=False)):
         c = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5, **kw), X, 0, n)
         assert c._cand is not None
         for _ in range(7):
@@ -1085,7 +1097,9 @@ def test_kmeans_dense_choice_on_device(cuda):
     n, d, k = 200_000, 128, 512
     X = blobs(n, d, k, device=cuda, dtype=torch.bfloat16, seed=13, noise=2.0)
     for mode in ("auto", "never", "always"):
-        km = KMeans(KMeansConfig(k=k, n_iterations=6, seed=3, dense=mode), X, 0, n)
+        # (the plain candidate lists: the device choice at DENSE_FRACTION; the drift-aware
+        # lists use the same mechanism at DENSE_FRACTION_DRIFT)
+        km = KMeans(KMeansConfig(k=k, n_iterations=6, seed=3, dense=mode, drift=False), X, 0, n)
         assert km._cand is not None
         for _ in range(6):
             _kmeans_step_oracle(km)
@@ -1102,3 +1116,67 @@ def test_kmeans_dense_choice_on_device(cuda):
         if mode == "auto":   # this data exercises both device choices (probe: r5_34)
             assert any(dense[i] > 0 for i in range(2, len(act))), (act, dense)
             assert any(dense[i] == 0 for i in range(2, len(act))), (act, dense)
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_kmeans_assign_rows_drift_candidates(cuda, d):
+    """Drift-aware candidate lists: with valid lower bounds l (below the true second-best
+    distance) and small centre shifts most of every list is dropped past the first chunk;
+    the assignment still equals the full pass on the active rows (near-ties aside), u / l
+    stay valid bounds and the changed rows are collected exactly."""
+    torch.manual_seed(13)
+    from dalgo.data.synthetic import blobs
+    n, k = 120_000, 1000
+    X = K.prepare_points(blobs(n, d, k, device=cuda, dtype=torch.bfloat16, seed=6))
+    g = torch.Generator(device="cpu").manual_seed(3)
+    C0 = X[torch.randperm(n, generator=g)[:k].to(cuda), :d].float()
+    prevc = K.make_centers(C0, torch.bfloat16, cuda)
+    cen = K.make_centers(C0 + 0.05 * torch.randn_like(C0), torch.bfloat16, cuda)
+    full = K.assign(X, cen)
+    kpad, DP = cen.Cq.shape
+    xmax = torch.zeros(1, dtype=torch.int32, device=cuda)
+    mind = torch.zeros(n, device=cuda)
+    K.assign_rows(X, cen, None, n, torch.empty(n, dtype=torch.int32, device=cuda), mind,
+                  torch.zeros(n, device=cuda), xh=torch.zeros(n, device=cuda), xmax=xmax)
+    tol = torch.zeros(1, device=cuda)
+    K.bounds_init(mind, mind, xmax, n, torch.empty((n, 2), device=cuda), tol)
+    ws = K.CandWorkspace(cuda, n, k, kpad, DP, drift=True)
+    delta = torch.empty(k, device=cuda)
+    K.centre_nbrs(cen, prevc.Cq[:k].clone(), delta, torch.empty(k, device=cuda), ws)
+    # previous assignment / bounds vs the PREVIOUS centres: a_prev = their nearest, l = a
+    # valid lower bound of the distance to every other previous centre
+    dprev = torch.cdist(X[:, :d].double(), prevc.Cq[:k, :d].double())
+    two = torch.topk(dprev, 2, dim=1, largest=False)
+    a_prev = two.indices[:, 0].to(torch.int32)
+    lold = (two.values[:, 1] * 0.999 - 1e-3).clamp_min(0).float()
+    ul = torch.stack([two.values[:, 0].float() * 1.001 + 1e-3, lold], 1).contiguous()
+    m = 60_001
+    rows = torch.randperm(n, device=cuda)[:m].to(torch.int32)
+    ws.acl[:m].copy_(a_prev[rows.long()])
+    cnt = torch.tensor([m], dtype=torch.int64, device=cuda)
+    K.sort_active(rows, cnt, ws)
+    sel = torch.zeros(n, dtype=torch.bool, device=cuda)
+    sel[rows.long()] = True
+    a = torch.where(sel, a_prev, torch.full_like(a_prev, -7))
+    changed = torch.empty(n, dtype=torch.int32, device=cuda)
+    nch = torch.zeros(1, dtype=torch.int64, device=cuda)
+    K.assign_rows(X, cen, ws.rows, n, a, post=dict(
+        m_dev=cnt, a_prev=None, tol=tol, ul=ul, changed=changed, n_changed=nch,
+        chg_new=torch.empty(n, dtype=torch.int32, device=cuda),
+        chg_old=torch.empty(n, dtype=torch.int32, device=cuda)), cand=ws)
+    assert bool((a[~sel] == -7).all())
+    dist = torch.cdist(X[:, :d].double(), cen.Cq[:k, :d].double())
+    bad = sel & (a != full)
+    if bool(bad.any()):
+        db = dist[bad].gather(1, a[bad].long()[:, None])[:, 0]
+        df = dist[bad].gather(1, full[bad].long()[:, None])[:, 0]
+        assert float(((db - df).abs() / df).max()) < 1e-4
+    assert int(bad.sum()) <= 5
+    tw = torch.topk(dist, 2, dim=1, largest=False).values
+    u, l = ul[:, 0], ul[:, 1]
+    assert bool((u[sel].double() >= tw[sel, 0] - 1e-3).all())
+    assert bool((l[sel].double() <= tw[sel, 1] + 1e-3).all())
+    c = int(nch.item())
+    exp = torch.nonzero(sel & (a != a_prev))[:, 0]
+    assert c == exp.numel()
+    assert torch.equal(torch.sort(changed[:c]).values.long(), exp)

@@ -224,3 +224,26 @@ def test_owner_partition_matches_torch(cuda, world):
     for c in cg:
         assert torch.equal(torch.sort(got[a:a + c].cpu()).values, torch.sort(exp[a:a + c]).values)
         a += c
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_deal_kernel_matches_torch(cuda, world):
+    from dalgo.apps.pagerank_app import deal_ids
+    n = 1 << 16
+    order = torch.randperm(n)
+    exp = deal_ids(order, n, world)
+    got = deal_ids(order.to(cuda), n, world)
+    assert torch.equal(got.long().cpu(), exp.long())
+
+
+def test_bitmap_ghost_ids(cuda):
+    g = torch.Generator().manual_seed(5)
+    bm = torch.randint(-(1 << 31), (1 << 31) - 1, (5000,), generator=g, dtype=torch.int64).to(torch.int32)
+    bm[::7] = 0
+    bits = (bm.long()[:, None] >> torch.arange(32)) & 1
+    exp = torch.nonzero(bits.flatten()).flatten()
+    pc = bits.sum(1)
+    prefix = (torch.cumsum(pc, 0) - pc).to(cuda)
+    out = torch.empty(exp.numel(), dtype=torch.int64, device=cuda)
+    G._ext.ops().gb_bitmap_ids(bm.to(cuda), prefix, out)
+    assert torch.equal(out.cpu(), exp)
