@@ -5,6 +5,9 @@
 // calls the extern "C" launcher of the gfx950 kernel on the caller's current HIP
 // stream, so ops compose with torch streams and hipGraph capture. Launch
 // failures surface as c10::Error with the op name.
+#include <map>
+#include <string>
+#include <cstdlib>
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
@@ -1008,6 +1011,49 @@ void gb_pack(const Tensor& src, const Tensor& dst, Tensor out) {
                   "gb_pack");
 }
 
+// ---- the adjacency build's sorts: rocPRIM's onesweep radix sort by default, the native
+// reduce-then-scan LSD sort (radix_sort.hip) with DALGO_SORT=native. Measured on one MI355X
+// (bench/probes/sort_bench.py, profiles/round6/r6_16): 1.07B u64 keys over 40 bits, native
+// 51.2 ms (count passes 1.6 ms each at 5.4 TB/s, scatter passes 7.4 ms: 128-B digit runs
+// written at scattered places) against rocPRIM 33.3 ms -- rocPRIM stays the default.
+// rs_sort_error() keeps the (always clear: nothing in the native sort waits) error word.
+static bool use_rocprim_sort() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("DALGO_SORT");
+    v = (e != nullptr && std::string(e) == "native") ? 0 : 1;
+  }
+  return v == 1;
+}
+static Tensor rs_err_word(const at::Device& dev) {
+  static std::map<int, Tensor> words;
+  auto it = words.find(dev.index());
+  if (it != words.end()) return it->second;
+  Tensor t = at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(dev));
+  words[dev.index()] = t;
+  return t;
+}
+static void native_sort(const void* in, void* out, int key_bytes, int64_t n, int begin_bit, int end_bit,
+                        const at::TensorOptions& opts, const char* what) {
+  const size_t wsb = dalgo_rs_ws_bytes(n, key_bytes, begin_bit, end_bit);
+  Tensor ws = at::empty({(int64_t)wsb}, opts.dtype(at::kByte));
+  const int np = (end_bit - begin_bit + 7) / 8;
+  Tensor tmp = np > 1 ? at::empty({n * key_bytes}, opts.dtype(at::kByte)) : Tensor();
+  Tensor errw = at::empty({1}, opts.dtype(at::kInt));
+  hipError_t e = key_bytes == 8
+      ? dalgo_rs_sort64(reinterpret_cast<const uint64_t*>(in), reinterpret_cast<uint64_t*>(out),
+                        np > 1 ? reinterpret_cast<uint64_t*>(tmp.data_ptr()) : nullptr, n, begin_bit, end_bit,
+                        ws.data_ptr(), wsb, reinterpret_cast<unsigned*>(errw.data_ptr<int>()), cur_stream())
+      : dalgo_rs_sort32(reinterpret_cast<const uint32_t*>(in), reinterpret_cast<uint32_t*>(out),
+                        np > 1 ? reinterpret_cast<uint32_t*>(tmp.data_ptr()) : nullptr, n, begin_bit, end_bit,
+                        ws.data_ptr(), wsb, reinterpret_cast<unsigned*>(errw.data_ptr<int>()), cur_stream());
+  TORCH_CHECK(e == hipSuccess, "dalgo::", what, " launch failed: ", hipGetErrorString(e));
+  Tensor acc = rs_err_word(opts.device());
+  acc.bitwise_or_(errw);
+}
+
+Tensor rs_sort_error(const Tensor& like) { return rs_err_word(like.device()); }
+
 // packed edges partitioned on the HIGH bits of their source (bits [kb, end_bit) of src,
 // 2 radix passes at 2^26) into out, and deg[src] += the raw out-degree (one LDS histogram
 // per bucket of 2^kb sources)
@@ -1023,10 +1069,12 @@ void gb_degree_packed(const Tensor& packed, int64_t end_bit, Tensor deg, Tensor 
   DeviceGuard guard(packed.device());
   auto* in = reinterpret_cast<const uint64_t*>(packed.data_ptr<int64_t>());
   auto* o = reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>());
-  size_t bytes = 0;
-  DALGO_CHECK_HIP(dalgo_gb_sort(nullptr, &bytes, in, o, n, 32 + kb, 32 + (int)end_bit, cur_stream()),
-                  "gb_sort(size)");
-  {
+  if (!use_rocprim_sort()) {
+    native_sort(in, o, 8, n, 32 + kb, 32 + (int)end_bit, packed.options(), "rs_sort64(degree partition)");
+  } else {
+    size_t bytes = 0;
+    DALGO_CHECK_HIP(dalgo_gb_sort(nullptr, &bytes, in, o, n, 32 + kb, 32 + (int)end_bit, cur_stream()),
+                    "gb_sort(size)");
     Tensor tmp = at::empty({(int64_t)bytes + 256}, packed.options().dtype(at::kByte));
     DALGO_CHECK_HIP(dalgo_gb_sort(tmp.data_ptr(), &bytes, in, o, n, 32 + kb, 32 + (int)end_bit, cur_stream()),
                     "gb_sort");
@@ -1058,9 +1106,11 @@ void gb_degree_sorted(const Tensor& ids, int64_t end_bit, Tensor deg) {
   // partition on the high bits only, then one LDS histogram per bucket
   Tensor sorted = at::empty_like(ids);
   auto* out = reinterpret_cast<uint32_t*>(sorted.data_ptr<int32_t>());
-  size_t bytes = 0;
-  DALGO_CHECK_HIP(dalgo_gb_sort32(nullptr, &bytes, in, out, n, kb, (int)end_bit, cur_stream()), "gb_sort32(size)");
-  {
+  if (!use_rocprim_sort()) {
+    native_sort(in, out, 4, n, kb, (int)end_bit, ids.options(), "rs_sort32(degree partition)");
+  } else {
+    size_t bytes = 0;
+    DALGO_CHECK_HIP(dalgo_gb_sort32(nullptr, &bytes, in, out, n, kb, (int)end_bit, cur_stream()), "gb_sort32(size)");
     Tensor tmp = at::empty({(int64_t)bytes + 256}, ids.options().dtype(at::kByte));
     DALGO_CHECK_HIP(dalgo_gb_sort32(tmp.data_ptr(), &bytes, in, out, n, kb, (int)end_bit, cur_stream()), "gb_sort32");
   }
@@ -1070,8 +1120,8 @@ void gb_degree_sorted(const Tensor& ids, int64_t end_bit, Tensor deg) {
                   "gb_bucket_degree");
 }
 
-// sort keys[:n] over bits [begin_bit, end_bit) into out[:n] (rocPRIM onesweep radix sort,
-// stable: keys equal on those bits keep their input order)
+// sort keys[:n] over bits [begin_bit, end_bit) into out[:n] (native LSD radix sort, stable:
+// keys equal on those bits keep their input order)
 void gb_sort(const Tensor& keys, int64_t n, int64_t end_bit, Tensor out, int64_t begin_bit) {
   check_t(keys, at::kLong, "keys");
   check_t(out, at::kLong, "out");
@@ -1081,6 +1131,11 @@ void gb_sort(const Tensor& keys, int64_t n, int64_t end_bit, Tensor out, int64_t
   DeviceGuard guard(keys.device());
   auto* k = reinterpret_cast<const uint64_t*>(keys.data_ptr<int64_t>());
   auto* o = reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>());
+  TORCH_CHECK(keys.data_ptr() != out.data_ptr(), "gb_sort: keys and out must differ");
+  if (!use_rocprim_sort()) {
+    native_sort(k, o, 8, n, (int)begin_bit, (int)end_bit, keys.options(), "rs_sort64");
+    return;
+  }
   size_t bytes = 0;
   DALGO_CHECK_HIP(dalgo_gb_sort(nullptr, &bytes, k, o, n, (int)begin_bit, (int)end_bit, cur_stream()),
                   "gb_sort(size)");
@@ -1772,6 +1827,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("gb_owner_partition(Tensor src, Tensor dst, Tensor? new_id, int sl, int world, Tensor(a!) out) -> Tensor");
   m.def("gb_bitmap_ids(Tensor bitmap, Tensor prefix, Tensor(a!) ids) -> ()");
   m.def("gb_bytes_to_bits(Tensor marks, Tensor(a!) bits) -> ()");
+  m.def("rs_sort_error(Tensor like) -> Tensor");
   m.def("gb_deal(Tensor order, int world, int sl, Tensor(a!) new_id) -> ()");
   m.def("gb_degree_packed(Tensor packed, int end_bit, Tensor(a!) deg, Tensor(b!) out) -> ()");
   m.def("gb_degree_sorted(Tensor ids, int end_bit, Tensor(a!) deg) -> ()");
@@ -1857,6 +1913,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("gb_owner_partition", &gb_owner_partition);
   m.impl("gb_bitmap_ids", &gb_bitmap_ids);
   m.impl("gb_bytes_to_bits", &gb_bytes_to_bits);
+  m.impl("rs_sort_error", &rs_sort_error);
   m.impl("gb_deal", &gb_deal);
   m.impl("gb_degree_packed", &gb_degree_packed);
   m.impl("gb_degree_sorted", &gb_degree_sorted);

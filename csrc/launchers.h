@@ -230,6 +230,11 @@ hipError_t dalgo_gb_relabel_src(uint64_t* packed, int64_t n, const int32_t* new_
 hipError_t dalgo_gb_pack(const int32_t* src, const int32_t* dst, int64_t n, uint64_t* out, hipStream_t st);
 int64_t dalgo_gb_key_blocks(int64_t n);
 int64_t dalgo_gb_owner_blocks(int64_t n);
+size_t dalgo_rs_ws_bytes(int64_t n, int key_bytes, int begin_bit, int end_bit);
+hipError_t dalgo_rs_sort64(const uint64_t* in, uint64_t* out, uint64_t* tmp, int64_t n, int begin_bit, int end_bit,
+                           void* ws, size_t ws_bytes, unsigned* err_out, hipStream_t st);
+hipError_t dalgo_rs_sort32(const uint32_t* in, uint32_t* out, uint32_t* tmp, int64_t n, int begin_bit, int end_bit,
+                           void* ws, size_t ws_bytes, unsigned* err_out, hipStream_t st);
 hipError_t dalgo_gb_bytes_to_bits(const uint8_t* marks, int64_t nw, uint32_t* bits, hipStream_t st);
 hipError_t dalgo_gb_bitmap_ids(const uint32_t* bm, int64_t nw, const int64_t* prefix, int64_t* ids,
                                hipStream_t st);
