@@ -28,9 +28,12 @@ using at::Tensor;
 inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 using DeviceGuard = c10::hip::HIPGuardMasqueradingAsCUDA;
 
+// a failed launch leaves its error in the runtime's last-error slot, which the next torch
+// call on the stream would report again: cleared here, reported once
 #define DALGO_CHECK_HIP(expr, name)                                                   \
   do {                                                                                \
     hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess) (void)hipGetLastError();                                    \
     TORCH_CHECK(_e == hipSuccess, "dalgo::" name " launch failed: ", hipGetErrorString(_e)); \
   } while (0)
 

@@ -27,7 +27,8 @@ import os
 
 # Launch geometry of the row-streaming kernels (tuned on MI355X: bench/lr_kernel_sweep.py,
 # profiles/round1-3). One launch shape remains (csrc/kernels/lr_grad.hip launch_shape).
-TARGET_BLOCKS = 256        # workgroups per launch (split over segments): one per CU
+TARGET_BLOCKS = int(os.environ.get("DALGO_LR_BLOCKS", "256"))   # workgroups per launch
+                           # (split over segments): one per CU
 # (192 for large steps measured 1.2-1.5 % faster in an isolated fused-step loop at 5M-10M
 # rows, but not in bench.py's one-kernel step, and 7 % slower in the persistent form:
 # profiles/round4/r4_10/, r4_11/ -- kept at 256)
@@ -35,7 +36,8 @@ FINE_GROUPS = 8            # switch in-block work claims from 256-row groups to 
                            # quarters once fewer than this many groups are unclaimed
 UNIT_SHIFT = 6             # sampled steps: work units of 2^6 rows (the final, fine claims
                            # take one unit: how closely a block's 8 waves finish together)
-RPB_ALIGN = 256            # granularity (rows) of each block's static range (4-row ranges
+RPB_ALIGN = int(os.environ.get("DALGO_LR_RPB_ALIGN", "256"))
+                           # granularity (rows) of each block's static range (4-row ranges
                            # measured equal: profiles/final/README.md)
 # DETERMINISTIC = combine per-block partials with the fixed-order two-level hand-off
 # (bitwise repeatable) instead of float atomics (race-detection mode)
