@@ -494,7 +494,32 @@ lr_rows_kernel(const LrParams p) {
   // ---- software-pipelined sweep: load(i+1) || compute(i)
   Batch<NC, U> A;
   unsigned long long t_first = 0ull, t_refill = 0ull;
-  if constexpr (PIPE) {
+  if constexpr (PIPE && PERSIST) {
+    // persistent steps: TWO row batches are issued before the wait for the previous
+    // step's model release (the selection does not depend on W), so the release chain
+    // (last block's epilogue -> tail update -> epoch -> W reads) overlaps two batches'
+    // HBM traffic instead of one; then the same one-ahead pipeline
+    Batch<NC, U> B;
+    refill();
+    if (tr) t_refill = __builtin_amdgcn_s_memrealtime();
+    take_and_load(A);
+    refill();
+    take_and_load(B);
+    if (it > 0 && !wait_epoch(it)) return;
+    load_w();
+    if (tr) t_first = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+      if (A.n == 0) break;
+      compute(A);
+      if (B.n == 0) break;
+      refill();
+      take_and_load(A);
+      compute(B);
+      if (A.n == 0) break;
+      refill();
+      take_and_load(B);
+    }
+  } else if constexpr (PIPE) {
     Batch<NC, U> B;
     refill();
     if (tr) t_refill = __builtin_amdgcn_s_memrealtime();
