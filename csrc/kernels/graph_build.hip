@@ -189,6 +189,9 @@ __global__ void __launch_bounds__(256) gb_pack_kernel(const int32_t* __restrict_
 // random new_id gathers) and counts the block's edges per owner; phase 2 re-reads the
 // packed words and scatters them owner-major at the scanned offsets. Per-owner counting
 // is wave-aggregated (one LDS atomic per distinct owner in a wave, <= W per step).
+// The phase-0 gathers dominate (5.2 of the 5.9 ms at the W = 8 share, 134M edges: ~55 G
+// random new_id reads/s, profiles/round6/r6_23); relabelling in 2-4 id-range passes first, so
+// that each pass gathers from a 1/P slice of new_id, was slower (7.6-8.1 ms, r6_24).
 constexpr int kOwnR = 16384;         // edges per block
 constexpr int kOwnMax = 64;          // largest world size
 
