@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     a = ap.parse_args()
     from dalgo.apps.jobs import reserve_pool
-    from dalgo.apps.pagerank_app import deal_ids, edge_range, rank_by_degree, rmat_input
+    from dalgo.apps.pagerank_app import degree_new_id, edge_range, rmat_input
     from dalgo.ops import graph as G
     dev = torch.device("cuda")
     reserve_pool(dev, 120.0)
@@ -38,7 +38,7 @@ def main():
     # what the degree all-reduce delivers: the whole stream's degrees
     deg_all = torch.zeros(N, dtype=torch.int32, device=dev)
     G.degree_sorted_(deg_all, torch.cat([s for s, _ in full]), a.scale)
-    new_id = deal_ids(rank_by_degree(deg_all), N, W).to(torch.int32)
+    new_id = degree_new_id(deg_all, N, W)
     sl = G.vertex_slices(N, W)
     res = {"scale": a.scale, "world": W, "edges": E, "ranks": {}}
     for r in [int(x) for x in a.ranks.split(",")]:
@@ -62,7 +62,7 @@ def main():
             deg = torch.zeros(N, dtype=torch.int32, device=dev)
             G.degree_sorted_(deg, s_own, a.scale)
             ev[1].record()
-            nid = deal_ids(rank_by_degree(deg_all), N, W).to(torch.int32)
+            nid = degree_new_id(deg_all, N, W)
             ev[2].record()
             packed, send = G.owner_partition(s_own, d_own, nid, N, W)
             ev[3].record()

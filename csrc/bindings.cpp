@@ -992,14 +992,30 @@ void gb_bitmap_ids(const Tensor& bitmap, const Tensor& prefix, Tensor ids) {
 }
 
 // new_id[order[j]] = snake-dealt position of rank j over `world` full slices of size sl
-void gb_deal(const Tensor& order, int64_t world, int64_t sl, Tensor new_id) {
+// id_bits > 0: order holds sort keys whose low id_bits bits are the vertex (gb_rank_keys)
+void gb_deal(const Tensor& order, int64_t world, int64_t sl, int64_t id_bits, Tensor new_id) {
   check_t(order, at::kLong, "order");
   check_i32(new_id, "new_id");
   TORCH_CHECK(new_id.numel() >= order.numel() && sl * world >= order.numel(), "gb_deal: sizes");
+  TORCH_CHECK(id_bits == 0 || (order.numel() - 1) >> id_bits == 0, "gb_deal: ids must fit id_bits");
   DeviceGuard guard(order.device());
-  DALGO_CHECK_HIP(dalgo_gb_deal(order.data_ptr<int64_t>(), order.numel(), (int)world, sl, new_id.data_ptr<int32_t>(),
-                                cur_stream()),
+  DALGO_CHECK_HIP(dalgo_gb_deal(order.data_ptr<int64_t>(), order.numel(), (int)world, sl, (int)id_bits,
+                                new_id.data_ptr<int32_t>(), cur_stream()),
                   "gb_deal");
+}
+
+// keys[j] = (dmax - deg[n-1-j]) << ibits | (n-1-j): the degree ranking's sort keys
+void gb_rank_keys(const Tensor& deg, int64_t dmax, int64_t ibits, Tensor keys) {
+  check_i32(deg, "deg");
+  check_t(keys, at::kLong, "keys");
+  const int64_t n = deg.numel();
+  TORCH_CHECK(keys.numel() >= n && ibits >= 1 && ibits <= 40 && ((n - 1) >> ibits) == 0 && dmax >= 0 &&
+                  ibits + (int64_t)(64 - __builtin_clzll((unsigned long long)dmax | 1ull)) <= 63,
+              "gb_rank_keys: sizes");
+  DeviceGuard guard(deg.device());
+  DALGO_CHECK_HIP(dalgo_gb_rank_keys(deg.data_ptr<int32_t>(), n, dmax, (int)ibits,
+                                     reinterpret_cast<uint64_t*>(keys.data_ptr<int64_t>()), cur_stream()),
+                  "gb_rank_keys");
 }
 
 // packed[i] = src[i] << 32 | dst[i]
@@ -1831,7 +1847,8 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("gb_bitmap_ids(Tensor bitmap, Tensor prefix, Tensor(a!) ids) -> ()");
   m.def("gb_bytes_to_bits(Tensor marks, Tensor(a!) bits) -> ()");
   m.def("rs_sort_error(Tensor like) -> Tensor");
-  m.def("gb_deal(Tensor order, int world, int sl, Tensor(a!) new_id) -> ()");
+  m.def("gb_deal(Tensor order, int world, int sl, int id_bits, Tensor(a!) new_id) -> ()");
+  m.def("gb_rank_keys(Tensor deg, int dmax, int ibits, Tensor(a!) keys) -> ()");
   m.def("gb_degree_packed(Tensor packed, int end_bit, Tensor(a!) deg, Tensor(b!) out) -> ()");
   m.def("gb_degree_sorted(Tensor ids, int end_bit, Tensor(a!) deg) -> ()");
   m.def("gb_decode_blocks(int n) -> int", &gb_decode_blocks);   // no tensors: catch-all kernel
@@ -1918,6 +1935,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("gb_bytes_to_bits", &gb_bytes_to_bits);
   m.impl("rs_sort_error", &rs_sort_error);
   m.impl("gb_deal", &gb_deal);
+  m.impl("gb_rank_keys", &gb_rank_keys);
   m.impl("gb_degree_packed", &gb_degree_packed);
   m.impl("gb_degree_sorted", &gb_degree_sorted);
   m.impl("gb_decode", &gb_decode);

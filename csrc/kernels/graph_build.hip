@@ -324,13 +324,26 @@ __global__ void __launch_bounds__(256) gb_bitmap_ids_kernel(const uint32_t* __re
 
 // deal of the ranked vertex list (pagerank_app.deal_ids, W > 1, every slice full): rank j
 // goes to slice r = j % W (snake: odd rounds W - 1 .. 0), position j / W
+// order[j] & id_mask = the j-th vertex (id_mask strips the sort key's degree bits)
 __global__ void __launch_bounds__(256) gb_deal_kernel(const int64_t* __restrict__ order, int64_t n, int world,
-                                                      int64_t sl, int32_t* __restrict__ new_id) {
+                                                      int64_t sl, int64_t id_mask, int32_t* __restrict__ new_id) {
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += stride) {
     const int64_t p = j / world, q = j - p * world;
     const int64_t r = (p & 1) ? world - 1 - q : q;
-    new_id[order[j]] = (int32_t)(r * sl + p);
+    new_id[order[j] & id_mask] = (int32_t)(r * sl + p);
+  }
+}
+
+// The degree ranking's sort keys in one pass: keys[j] = (dmax - deg[v]) << ibits | v for
+// v = n - 1 - j (descending ids, so the stable sort on the degree bits breaks ties by
+// descending id) -- was six torch elementwise kernels, ~1.1 ms at 2^26 vertices.
+__global__ void __launch_bounds__(256) gb_rank_keys_kernel(const int32_t* __restrict__ deg, int64_t n,
+                                                           int64_t dmax, int ibits, uint64_t* __restrict__ keys) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += stride) {
+    const int64_t v = n - 1 - j;
+    keys[j] = ((uint64_t)(dmax - (int64_t)deg[v]) << ibits) | (uint64_t)v;
   }
 }
 
@@ -1301,11 +1314,22 @@ hipError_t dalgo_gb_bitmap_ids(const uint32_t* bm, int64_t nw, const int64_t* pr
   return hipSuccess;
 }
 
-hipError_t dalgo_gb_deal(const int64_t* order, int64_t n, int world, int64_t sl, int32_t* new_id, hipStream_t st) {
+hipError_t dalgo_gb_deal(const int64_t* order, int64_t n, int world, int64_t sl, int id_bits, int32_t* new_id,
+                         hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  if (world < 1 || sl * world < n || sl > 0x7fffffffLL) return hipErrorInvalidValue;
+  if (world < 1 || sl * world < n || sl > 0x7fffffffLL || id_bits < 0 || id_bits > 62) return hipErrorInvalidValue;
+  const int64_t mask = id_bits ? (int64_t)((1ull << id_bits) - 1ull) : (int64_t)-1;
   const int64_t g = std::min<int64_t>(cdiv(n, (int64_t)256), 256 * 64);
-  hipLaunchKernelGGL(gb_deal_kernel, dim3((unsigned)g), dim3(256), 0, st, order, n, world, sl, new_id);
+  hipLaunchKernelGGL(gb_deal_kernel, dim3((unsigned)g), dim3(256), 0, st, order, n, world, sl, mask, new_id);
+  DALGO_LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t dalgo_gb_rank_keys(const int32_t* deg, int64_t n, int64_t dmax, int ibits, uint64_t* keys, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (ibits < 1 || ibits > 40 || (n - 1) >> ibits) return hipErrorInvalidValue;
+  const int64_t g = std::min<int64_t>(cdiv(n, (int64_t)256), 256 * 64);
+  hipLaunchKernelGGL(gb_rank_keys_kernel, dim3((unsigned)g), dim3(256), 0, st, deg, n, dmax, ibits, keys);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -238,7 +238,9 @@ hipError_t dalgo_rs_sort32(const uint32_t* in, uint32_t* out, uint32_t* tmp, int
 hipError_t dalgo_gb_bytes_to_bits(const uint8_t* marks, int64_t nw, uint32_t* bits, hipStream_t st);
 hipError_t dalgo_gb_bitmap_ids(const uint32_t* bm, int64_t nw, const int64_t* prefix, int64_t* ids,
                                hipStream_t st);
-hipError_t dalgo_gb_deal(const int64_t* order, int64_t n, int world, int64_t sl, int32_t* new_id, hipStream_t st);
+hipError_t dalgo_gb_deal(const int64_t* order, int64_t n, int world, int64_t sl, int id_bits, int32_t* new_id,
+                         hipStream_t st);
+hipError_t dalgo_gb_rank_keys(const int32_t* deg, int64_t n, int64_t dmax, int ibits, uint64_t* keys, hipStream_t st);
 hipError_t dalgo_gb_owner_scatter(int phase, const int32_t* src, const int32_t* dst, int64_t n,
                                   const int32_t* new_id, int64_t sl, int world, uint64_t* tmp,
                                   int64_t* counts, const int64_t* offsets, uint64_t* out, hipStream_t st);

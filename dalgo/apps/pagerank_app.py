@@ -63,7 +63,7 @@ def deal_ids(order: torch.Tensor, n_vertices: int, world: int) -> torch.Tensor:
         # every slice full: one scatter kernel (graph_build.hip gb_deal)
         from dalgo.ops import _ext
         new_id = torch.empty(n_vertices, dtype=torch.int32, device=dev)
-        _ext.ops().gb_deal(order.to(torch.int64).contiguous(), world, sl, new_id)
+        _ext.ops().gb_deal(order.to(torch.int64).contiguous(), world, sl, 0, new_id)
         return new_id
     j = torch.arange(n_vertices, device=dev, dtype=torch.int64)
     p = j // world
@@ -111,9 +111,32 @@ def degree_order_from(edges: list, scale: int, rank: int, world: int, device) ->
             G.degree_count_(deg, s)
     comm.all_reduce_sum(deg)
     G._mark("degree_count")
-    order = rank_by_degree(deg)
-    G._mark("degree_rank")
-    return deal_ids(order, n_vertices, world).to(torch.int32)
+    return degree_new_id(deg, n_vertices, world)
+
+
+def degree_new_id(deg: torch.Tensor, n_vertices: int, world: int) -> torch.Tensor:
+    """int32 new_id of the degree relabeling, ``deal_ids(rank_by_degree(deg), n, W)``. GPU with
+    full slices (every W dividing 2^scale, W = 1 included): the ranking keys in one kernel,
+    the sort over the degree bits, then the snake deal straight from the sorted keys (their
+    id bits masked in the scatter) -- 3 kernels and a sort instead of ~10 (graph_build.hip
+    gb_rank_keys, gb_deal)."""
+    sl = G.vertex_slices(n_vertices, world)
+    if not (deg.is_cuda and sl * world == n_vertices and deg.numel() == n_vertices and n_vertices > 1):
+        return deal_ids(rank_by_degree(deg), n_vertices, world).to(torch.int32)
+    from dalgo.ops import _ext
+    ops = _ext.ops()
+    deg = deg.to(torch.int32).contiguous()
+    dmax = int(deg.max().item())
+    dbits = max(1, dmax.bit_length())
+    ibits = max(1, (n_vertices - 1).bit_length())
+    keys = torch.empty(n_vertices, dtype=torch.int64, device=deg.device)
+    ops.gb_rank_keys(deg, dmax, ibits, keys)
+    out = torch.empty_like(keys)
+    ops.gb_sort(keys, n_vertices, dbits + ibits, out, ibits)
+    del keys
+    new_id = torch.empty(n_vertices, dtype=torch.int32, device=deg.device)
+    ops.gb_deal(out, world, sl, ibits, new_id)
+    return new_id
 
 
 def rank_by_degree(deg: torch.Tensor) -> torch.Tensor:
@@ -171,10 +194,8 @@ def build_rmat_native(edges: list, scale: int, rank: int, world: int, device, re
     if reorder and world == 1 and torch.device(device).type == "cuda" and scale > G.BUCKET_BITS:
         packed, deg = G.partition_edges(edges, scale)
         G._mark("degree_count")
-        order = rank_by_degree(deg)
-        G._mark("degree_rank")
-        new_id = deal_ids(order, 1 << scale, 1).to(torch.int32)
-        del deg, order
+        new_id = degree_new_id(deg, 1 << scale, 1)
+        del deg
         G._mark("deal_ids")
         packed = G.relabel_partition_dst(packed, new_id, scale)
         G._mark("dst_partition")
@@ -217,9 +238,7 @@ def degree_order_share(edges: list, scale: int, world: int, device) -> torch.Ten
             G.degree_count_(deg, s)
     comm.all_reduce_sum(deg)
     G._mark("degree_count")
-    order = rank_by_degree(deg)
-    G._mark("degree_rank")
-    return deal_ids(order, n_vertices, world).to(torch.int32)
+    return degree_new_id(deg, n_vertices, world)
 
 
 def shuffle_edges(edges: list, new_id: torch.Tensor | None, n_vertices: int, world: int):

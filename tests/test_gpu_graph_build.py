@@ -236,6 +236,20 @@ def test_deal_kernel_matches_torch(cuda, world):
     assert torch.equal(got.long().cpu(), exp.long())
 
 
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_degree_new_id_matches_torch(cuda, world):
+    """The fused ranking (gb_rank_keys + sort + masked gb_deal) == deal_ids(rank_by_degree)
+    on the CPU: degree ties (small degree range) broken by descending id, snake deal."""
+    from dalgo.apps.pagerank_app import deal_ids, degree_new_id, rank_by_degree
+    n = 1 << 17
+    g = torch.Generator().manual_seed(6)
+    deg = torch.randint(0, 40, (n,), generator=g, dtype=torch.int32)
+    deg[:5] = 1 << 20                     # a few hubs: degree bits past the low range
+    exp = deal_ids(rank_by_degree(deg), n, world).to(torch.int32)
+    got = degree_new_id(deg.to(cuda), n, world).cpu()
+    assert got.dtype == torch.int32 and torch.equal(got, exp)
+
+
 def test_bitmap_ghost_ids(cuda):
     g = torch.Generator().manual_seed(5)
     bm = torch.randint(-(1 << 31), (1 << 31) - 1, (5000,), generator=g, dtype=torch.int64).to(torch.int32)
