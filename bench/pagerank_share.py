@@ -3,8 +3,9 @@
 one MI355X: what rank r of W computes between the collectives of
 dalgo.apps.pagerank_app.build_rmat_sharded --
 
-  degree count of its E / W input edges | [all_reduce of the degrees] | ranking + dealing |
-  relabel + group by destination owner | [all_to_all] | native build over received edges
+  degree count of its E / W input edges (with the source partition) | [all_reduce of the
+  degrees] | ranking + dealing | relabel + group by destination owner | [all_to_all] |
+  native build over received edges
 
 The collectives are left out (their inputs / outputs are computed untimed from the whole
 stream, exactly what they would deliver) and reported as bytes per rank. Timed with HIP
@@ -26,6 +27,9 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--ranks", default="0,7")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--direct", action="store_true",
+                    help="the direct shuffle (owner partition with random new_id gathers) instead "
+                         "of build_rmat_sharded's source-bucketed path")
     a = ap.parse_args()
     from dalgo.apps.jobs import reserve_pool
     from dalgo.apps.pagerank_app import degree_new_id, edge_range, rmat_input
@@ -40,7 +44,7 @@ def main():
     G.degree_sorted_(deg_all, torch.cat([s for s, _ in full]), a.scale)
     new_id = degree_new_id(deg_all, N, W)
     sl = G.vertex_slices(N, W)
-    res = {"scale": a.scale, "world": W, "edges": E, "ranks": {}}
+    res = {"scale": a.scale, "world": W, "edges": E, "shuffle": "direct" if a.direct else "bucketed", "ranks": {}}
     for r in [int(x) for x in a.ranks.split(",")]:
         lo, hi = edge_range(E, r, W)
         s_own, d_own = G.rmat_edges(hi - lo, a.scale, seed=1, e_off=lo, device=dev)
@@ -59,12 +63,20 @@ def main():
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
             torch.cuda.synchronize()
             ev[0].record()
-            deg = torch.zeros(N, dtype=torch.int32, device=dev)
-            G.degree_sorted_(deg, s_own, a.scale)
-            ev[1].record()
-            nid = degree_new_id(deg_all, N, W)
-            ev[2].record()
-            packed, send = G.owner_partition(s_own, d_own, nid, N, W)
+            if a.direct:   # degree sort of the sources; relabel by random gathers
+                deg = torch.zeros(N, dtype=torch.int32, device=dev)
+                G.degree_sorted_(deg, s_own, a.scale)
+                ev[1].record()
+                nid = degree_new_id(deg_all, N, W)
+                ev[2].record()
+                packed, send = G.owner_partition(s_own, d_own, nid, N, W)
+            else:          # build_rmat_sharded's bucketed path
+                packed, deg = G.partition_edges([(s_own, d_own)], a.scale)
+                ev[1].record()
+                nid = degree_new_id(deg_all, N, W)
+                ev[2].record()
+                packed = G.relabel_partition_dst(packed, nid, a.scale)
+                packed, send = G.owner_partition_packed(packed, nid, N, W)
             ev[3].record()
             G.build_marks = []
             G._mark("start")
@@ -75,7 +87,7 @@ def main():
             tot = sum(t)
             if rep > 0 and (best is None or tot < best["total_ms"]):
                 best = {"total_ms": tot, "degree_count_ms": t[0], "rank_deal_ms": t[1],
-                        "owner_partition_ms": t[2], "build_received_ms": t[3],
+                        "relabel_owner_partition_ms": t[2], "build_received_ms": t[3],
                         "input_edges": hi - lo, "received_edges": int(rs.numel()),
                         "edges_dedup": ng.n_edges, "ghosts": ng.n_ghost,
                         "all_to_all_send_bytes": 8 * (sum(send) - send[r]),

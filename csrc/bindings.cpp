@@ -968,6 +968,35 @@ Tensor gb_owner_partition(const Tensor& src, const Tensor& dst, const std::optio
   return counts.sum(1);
 }
 
+// the same over edges already packed (src << 32 | dst) with RELABELLED sources, partitioned
+// on their destination bits (dalgo.ops.graph.relabel_partition_dst): the destinations are
+// relabelled in place in `packed` (new_id optional), then the owner-major scatter into out
+Tensor gb_owner_partition_packed(Tensor packed, const std::optional<Tensor>& new_id, int64_t sl, int64_t world,
+                                 Tensor out) {
+  check_t(packed, at::kLong, "packed");
+  check_t(out, at::kLong, "out");
+  const int64_t n = packed.numel();
+  TORCH_CHECK(out.numel() >= n && packed.is_contiguous() && reinterpret_cast<uintptr_t>(packed.data_ptr()) % 16 == 0,
+              "gb_owner_partition_packed: packed must be contiguous and 16-B aligned");
+  TORCH_CHECK(world >= 1 && world <= 64 && sl >= 1, "gb_owner_partition_packed: 1..64 ranks");
+  if (new_id) check_i32(*new_id, "new_id");
+  DeviceGuard guard(packed.device());
+  const int64_t nb = std::max<int64_t>(dalgo_gb_owner_blocks(n), 1);
+  Tensor counts = at::zeros({world, nb}, packed.options());
+  if (n == 0) return counts.sum(1);
+  auto* tp = reinterpret_cast<uint64_t*>(packed.data_ptr<int64_t>());
+  DALGO_CHECK_HIP(dalgo_gb_owner_scatter(0, nullptr, nullptr, n, opt_ptr<const int32_t>(new_id), sl, (int)world, tp,
+                                         counts.data_ptr<int64_t>(), nullptr, nullptr, cur_stream()),
+                  "gb_owner_scatter(count, packed)");
+  Tensor flat = counts.view({-1});
+  Tensor offs = flat.cumsum(0) - flat;
+  DALGO_CHECK_HIP(dalgo_gb_owner_scatter(2, nullptr, nullptr, n, nullptr, sl, (int)world, tp, nullptr,
+                                         offs.data_ptr<int64_t>(),
+                                         reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>()), cur_stream()),
+                  "gb_owner_scatter(scatter, packed)");
+  return counts.sum(1);
+}
+
 // bits[w] = bit j set iff marks[32 w + j] != 0
 void gb_bytes_to_bits(const Tensor& marks, Tensor bits) {
   check_t(marks, at::kByte, "marks");
@@ -1844,6 +1873,7 @@ TORCH_LIBRARY(dalgo, m) {
   m.def("gb_relabel_src(Tensor(a!) packed, Tensor new_id, int partitioned=0) -> ()");
   m.def("gb_pack(Tensor src, Tensor dst, Tensor(a!) out) -> ()");
   m.def("gb_owner_partition(Tensor src, Tensor dst, Tensor? new_id, int sl, int world, Tensor(a!) out) -> Tensor");
+  m.def("gb_owner_partition_packed(Tensor(a!) packed, Tensor? new_id, int sl, int world, Tensor(b!) out) -> Tensor");
   m.def("gb_bitmap_ids(Tensor bitmap, Tensor prefix, Tensor(a!) ids) -> ()");
   m.def("gb_bytes_to_bits(Tensor marks, Tensor(a!) bits) -> ()");
   m.def("rs_sort_error(Tensor like) -> Tensor");
@@ -1931,6 +1961,7 @@ TORCH_LIBRARY_IMPL(dalgo, CUDA, m) {
   m.impl("gb_relabel_src", &gb_relabel_src);
   m.impl("gb_pack", &gb_pack);
   m.impl("gb_owner_partition", &gb_owner_partition);
+  m.impl("gb_owner_partition_packed", &gb_owner_partition_packed);
   m.impl("gb_bitmap_ids", &gb_bitmap_ids);
   m.impl("gb_bytes_to_bits", &gb_bytes_to_bits);
   m.impl("rs_sort_error", &rs_sort_error);

@@ -26,6 +26,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "dalgo/common.h"
 #include "launchers.h"
@@ -192,7 +193,13 @@ __global__ void __launch_bounds__(256) gb_pack_kernel(const int32_t* __restrict_
 // The phase-0 gathers dominate (5.2 of the 5.9 ms at the W = 8 share, 134M edges: ~55 G
 // random new_id reads/s, profiles/round6/r6_23); relabelling in 2-4 id-range passes first, so
 // that each pass gathers from a 1/P slice of new_id, was slower (7.6-8.1 ms, r6_24).
-constexpr int kOwnR = 16384;         // edges per block
+// Blocks walk the edges grid-stride in 1024-edge steps (block b: steps b, b + G, ...), so the
+// edges in flight at any moment are one ~G * 1024-edge window: over destination-partitioned
+// input (the source-bucketed path) that window's destinations come from one or two 1 MB
+// slices of new_id, which every XCD's L2 then holds (16384-edge blocks put ~32 slices in
+// flight on every XCD). The scatter walks the same steps per block, so the (owner, block)
+// counts of the first pass place its words.
+constexpr int kOwnStep = 1024;       // edges per block step (256 threads x 4)
 constexpr int kOwnMax = 64;          // largest world size
 
 __device__ __forceinline__ int gb_owner_slot(int o, bool valid, int* s_cnt, bool want_base, int lane) {
@@ -222,12 +229,40 @@ __global__ void __launch_bounds__(256) gb_owner_count_kernel(const int32_t* __re
   if (threadIdx.x < kOwnMax) s_cnt[threadIdx.x] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int64_t r0 = (int64_t)blockIdx.x * kOwnR;
-  const int64_t r1 = r0 + kOwnR < n ? r0 + kOwnR : n;
-  for (int64_t i = r0 + (int64_t)threadIdx.x * 4; i < r1 + 0; i += 256 * 4) {
+  const int64_t r1 = n;
+  // src == nullptr: the edges are already packed in tmp with relabelled sources (the
+  // source-bucketed path, gb_relabel_src + a destination-bit partition): only the
+  // destinations are relabelled, from the L2-resident new_id slice of their bucket, in place
+  const bool packed_in = src == nullptr;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < r1; i += (int64_t)gridDim.x * kOwnStep) {
     int32_t s4[4], d4[4];
     bool in[4];
-    if (i + 4 <= r1) {
+    if (packed_in) {
+      uint64_t w[4];
+      if (i + 4 <= r1) {                       // 16-B aligned (binding checks the base)
+        const uint4 a = *reinterpret_cast<const uint4*>(tmp + i);
+        const uint4 b = *reinterpret_cast<const uint4*>(tmp + i + 2);
+        w[0] = ((uint64_t)a.y << 32) | a.x; w[1] = ((uint64_t)a.w << 32) | a.z;
+        w[2] = ((uint64_t)b.y << 32) | b.x; w[3] = ((uint64_t)b.w << 32) | b.z;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) in[v] = true;
+      } else {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          in[v] = i + v < r1;
+          w[v] = in[v] ? tmp[i + v] : 0ull;
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        s4[v] = (int32_t)(w[v] >> 32);
+        d4[v] = (int32_t)(uint32_t)w[v];
+      }
+      if (new_id) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) d4[v] = in[v] ? new_id[d4[v]] : 0;
+      }
+    } else if (i + 4 <= r1) {
       const int4 a = *reinterpret_cast<const int4*>(src + i);
       const int4 b = *reinterpret_cast<const int4*>(dst + i);
       s4[0] = a.x; s4[1] = a.y; s4[2] = a.z; s4[3] = a.w;
@@ -242,7 +277,7 @@ __global__ void __launch_bounds__(256) gb_owner_count_kernel(const int32_t* __re
         d4[v] = in[v] ? dst[i + v] : 0;
       }
     }
-    if (new_id) {
+    if (new_id && !packed_in) {
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         s4[v] = new_id[s4[v]];
@@ -251,7 +286,7 @@ __global__ void __launch_bounds__(256) gb_owner_count_kernel(const int32_t* __re
     }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      if (in[v]) tmp[i + v] = ((uint64_t)(uint32_t)s4[v] << 32) | (uint32_t)d4[v];
+      if (in[v] && (new_id || !packed_in)) tmp[i + v] = ((uint64_t)(uint32_t)s4[v] << 32) | (uint32_t)d4[v];
       gb_owner_slot((int)((uint32_t)d4[v] / sl), in[v], s_cnt, false, lane);
     }
   }
@@ -266,9 +301,8 @@ __global__ void __launch_bounds__(256) gb_owner_scatter_kernel(const uint64_t* _
   if (threadIdx.x < kOwnMax) s_cur[threadIdx.x] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int64_t r0 = (int64_t)blockIdx.x * kOwnR;
-  const int64_t r1 = r0 + kOwnR < n ? r0 + kOwnR : n;
-  for (int64_t i = r0 + (int64_t)threadIdx.x * 4; i < r1; i += 256 * 4) {
+  const int64_t r1 = n;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < r1; i += (int64_t)gridDim.x * kOwnStep) {
     uint64_t w[4];
     bool in[4];
 #pragma unroll
@@ -1334,8 +1368,20 @@ hipError_t dalgo_gb_rank_keys(const int32_t* deg, int64_t n, int64_t dmax, int i
   return hipSuccess;
 }
 
-int64_t dalgo_gb_owner_blocks(int64_t n) { return cdiv(n, (int64_t)kOwnR); }
+// DALGO_GB_OWNER_BLOCKS overrides the grid (default 2048: at the W = 8 share the bucketed
+// relabel + owner pass took 5.16 / 4.42 / 4.69 / 4.68 ms at 512 / 1024 / 2048 / 4096 blocks,
+// 5.2 ms with 16384-edge blocks, profiles/round6/r6_28)
+int64_t dalgo_gb_owner_blocks(int64_t n) {
+  static int64_t g = -1;
+  if (g < 0) {
+    const char* e = std::getenv("DALGO_GB_OWNER_BLOCKS");
+    g = e ? std::max<int64_t>(1, std::atoll(e)) : 2048;
+  }
+  return std::max<int64_t>(1, std::min<int64_t>(cdiv(n, (int64_t)kOwnStep), g));
+}
 
+// phase 0 (src == dst == nullptr: tmp holds the packed edges, sources relabelled, and only the
+// destinations go through new_id, in place):
 // phase 0: tmp[i] = new_id[src[i]] << 32 | new_id[dst[i]] (new_id nullable), counts[o * nb + b] =
 // edges of block b owned by rank o = dst' / sl; phase 2 (offsets = exclusive scan of counts):
 // out[offsets[o * nb + b] + ...] = the block's words owned by o
@@ -1344,8 +1390,7 @@ hipError_t dalgo_gb_owner_scatter(int phase, const int32_t* src, const int32_t* 
                                   int64_t* counts, const int64_t* offsets, uint64_t* out, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   if (world < 1 || world > kOwnMax || sl < 1 || sl > 0x7fffffffLL) return hipErrorInvalidValue;
-  const int64_t g = cdiv(n, (int64_t)kOwnR);
-  if (g > 0x7fffffffLL) return hipErrorInvalidValue;
+  const int64_t g = dalgo_gb_owner_blocks(n);
   if (phase == 0)
     hipLaunchKernelGGL(gb_owner_count_kernel, dim3((unsigned)g), dim3(256), 0, st, src, dst, n, new_id,
                        (uint32_t)sl, world, tmp, counts);

@@ -246,7 +246,6 @@ def shuffle_edges(edges: list, new_id: torch.Tensor | None, n_vertices: int, wor
     edges relabelled through new_id and sent to the owners of their destinations in ONE
     uneven all_to_all of packed (src << 32 | dst) words (plus one of the counts). Returns
     the (src, dst) int32 edges whose destination this rank owns, global new ids."""
-    from dalgo.parallel import comm
     packs, counts = [], []
     for s, d in edges:
         p, c = G.owner_partition(s, d, new_id, n_vertices, world)
@@ -264,6 +263,13 @@ def shuffle_edges(edges: list, new_id: torch.Tensor | None, n_vertices: int, wor
         send = [sum(c[o] for c in counts) for o in range(world)]
     del packs
     G._mark("owner_partition")
+    return exchange_owner_major(packed, send)
+
+
+def exchange_owner_major(packed: torch.Tensor, send: list):
+    """The shuffle's collective: owner-major packed words (``send[o]`` for rank o) through ONE
+    uneven all_to_all (plus one of the counts). Returns the received (src, dst) int32 edges."""
+    from dalgo.parallel import comm
     dev = packed.device
     st = torch.tensor(send, dtype=torch.int64, device=dev)
     rt_ = torch.empty_like(st)
@@ -287,9 +293,29 @@ def build_rmat_sharded(edges: list, scale: int, rank: int, world: int, device, r
     ranking of the degree order."""
     G._mark("start")
     n_vertices = 1 << scale
-    new_id = degree_order_share(edges, scale, world, device) if reorder else None
-    G._mark("deal_ids")
-    s, d = shuffle_edges(edges, new_id, n_vertices, world)
+    if reorder and torch.device(device).type == "cuda" and scale > G.BUCKET_BITS and edges:
+        # the one-rank build's partitions over this rank's share: sources partitioned on
+        # their high bits (the degree count's own pass), relabelled bucket by bucket, then
+        # grouped on the destination bits so the owner pass relabels destinations from
+        # L2-resident slices of new_id (the direct path's random gathers over the whole table
+        # were 5.2 of its 5.9 ms at the W = 8 share, profiles/round6/r6_23)
+        from dalgo.parallel import comm
+        packed, deg = G.partition_edges(edges, scale)
+        comm.all_reduce_sum(deg)
+        G._mark("degree_count")
+        new_id = degree_new_id(deg, n_vertices, world)
+        del deg
+        G._mark("deal_ids")
+        packed = G.relabel_partition_dst(packed, new_id, scale)
+        G._mark("dst_partition")
+        packed, send = G.owner_partition_packed(packed, new_id, n_vertices, world)
+        G._mark("owner_partition")
+        s, d = exchange_owner_major(packed, send)
+        del packed
+    else:
+        new_id = degree_order_share(edges, scale, world, device) if reorder else None
+        G._mark("deal_ids")
+        s, d = shuffle_edges(edges, new_id, n_vertices, world)
     use_native = (torch.device(device).type == "cuda") if native is None else native
     if use_native:
         ng = G.build_native([(s, d)], n_vertices, rank, world, None, bin_width=bin_width, tile=tile,

@@ -196,6 +196,28 @@ def owner_partition(src: torch.Tensor, dst: torch.Tensor, new_id: torch.Tensor |
     return packed, [int(x) for x in cnt.tolist()]
 
 
+def owner_partition_packed(packed: torch.Tensor, new_id: torch.Tensor | None, n_vertices: int,
+                           world: int) -> tuple[torch.Tensor, list]:
+    """:func:`owner_partition` over edges already packed with RELABELLED sources and grouped
+    on their destination bits (:func:`relabel_partition_dst`): only the destinations go
+    through ``new_id`` -- from the L2-resident slice of their bucket instead of random
+    gathers over the whole table -- then the owner-major grouping. ``packed`` is consumed
+    (overwritten on the GPU). Returns (packed int64 [E], edges per owner)."""
+    sl = vertex_slices(n_vertices, world)
+    if packed.is_cuda:
+        out = torch.empty_like(packed)
+        nid = new_id.to(torch.int32).contiguous() if new_id is not None else None
+        cnt = _ext.ops().gb_owner_partition_packed(packed.contiguous(), nid, sl, world, out)
+        return out, [int(x) for x in cnt.tolist()]
+    s, d = packed >> 32, packed & 0xFFFFFFFF
+    if new_id is not None:
+        d = new_id.long()[d]
+    owner = d // sl
+    order = torch.argsort(owner, stable=True)
+    cnt = torch.bincount(owner, minlength=world)[:world]
+    return ((s << 32) | d)[order], [int(x) for x in cnt.tolist()]
+
+
 def unpack_edges(packed: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     """(src, dst) int32 of packed src << 32 | dst words."""
     return (packed >> 32).to(torch.int32), (packed & 0xFFFFFFFF).to(torch.int32)

@@ -226,6 +226,26 @@ def test_owner_partition_matches_torch(cuda, world):
         a += c
 
 
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_bucketed_owner_partition_matches_torch(cuda, world):
+    """build_rmat_sharded's GPU shuffle source: source partition + degrees, bucketed source
+    relabel, destination-bit partition, then the owner pass relabelling destinations in
+    place (gb_owner_partition_packed) == the torch owner partition of the raw edges."""
+    scale = 17
+    s, d = G.rmat_edges((1 << 20) + 5, scale, seed=19, device=cuda)
+    new_id = torch.randperm(1 << scale, device=cuda).to(torch.int32)
+    packed, deg = G.partition_edges([(s, d)], scale)
+    assert torch.equal(deg.long().cpu(), torch.bincount(s.long().cpu(), minlength=1 << scale))
+    packed = G.relabel_partition_dst(packed, new_id, scale)
+    got, cg = G.owner_partition_packed(packed, new_id, 1 << scale, world)
+    exp, ce = G.owner_partition(s.cpu(), d.cpu(), new_id.cpu(), 1 << scale, world)
+    assert cg == ce and sum(cg) == s.numel()
+    a = 0
+    for c in cg:
+        assert torch.equal(torch.sort(got[a:a + c].cpu()).values, torch.sort(exp[a:a + c]).values)
+        a += c
+
+
 @pytest.mark.parametrize("world", [2, 8])
 def test_deal_kernel_matches_torch(cuda, world):
     from dalgo.apps.pagerank_app import deal_ids
