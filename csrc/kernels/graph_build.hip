@@ -202,6 +202,16 @@ __global__ void __launch_bounds__(256) gb_pack_kernel(const int32_t* __restrict_
 constexpr int kOwnStep = 1024;       // edges per block step (256 threads x 4)
 constexpr int kOwnMax = 64;          // largest world size
 
+// Logical block of hardware block b of g: blocks b and b + 8 share an XCD (round-robin
+// dealing, observed), so the XCD of b % 8 == x gets the consecutive logical blocks
+// [x * (g / 8) + min(x, g % 8), ...): within each g-step window an XCD walks its own
+// contiguous eighth, and its L2 holds one eighth of the window's new_id slices. A bijection
+// for any g; placement only affects speed.
+__device__ __forceinline__ int64_t gb_xcd_block(int64_t b, int64_t g) {
+  const int64_t x = b & 7, i = b >> 3, per = g >> 3, rem = g & 7;
+  return x * per + (x < rem ? x : rem) + i;
+}
+
 __device__ __forceinline__ int gb_owner_slot(int o, bool valid, int* s_cnt, bool want_base, int lane) {
   uint64_t act = __ballot(valid);
   int mine = 0;
@@ -234,7 +244,8 @@ __global__ void __launch_bounds__(256) gb_owner_count_kernel(const int32_t* __re
   // source-bucketed path, gb_relabel_src + a destination-bit partition): only the
   // destinations are relabelled, from the L2-resident new_id slice of their bucket, in place
   const bool packed_in = src == nullptr;
-  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < r1; i += (int64_t)gridDim.x * kOwnStep) {
+  const int64_t lb = gb_xcd_block(blockIdx.x, gridDim.x);
+  for (int64_t i = (lb * 256 + threadIdx.x) * 4; i < r1; i += (int64_t)gridDim.x * kOwnStep) {
     int32_t s4[4], d4[4];
     bool in[4];
     if (packed_in) {
@@ -291,7 +302,7 @@ __global__ void __launch_bounds__(256) gb_owner_count_kernel(const int32_t* __re
     }
   }
   __syncthreads();
-  if (threadIdx.x < world) counts[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s_cnt[threadIdx.x];
+  if (threadIdx.x < world) counts[(int64_t)threadIdx.x * gridDim.x + lb] = s_cnt[threadIdx.x];
 }
 
 __global__ void __launch_bounds__(256) gb_owner_scatter_kernel(const uint64_t* __restrict__ tmp, int64_t n,
@@ -302,7 +313,8 @@ __global__ void __launch_bounds__(256) gb_owner_scatter_kernel(const uint64_t* _
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int64_t r1 = n;
-  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < r1; i += (int64_t)gridDim.x * kOwnStep) {
+  const int64_t lb = gb_xcd_block(blockIdx.x, gridDim.x);
+  for (int64_t i = (lb * 256 + threadIdx.x) * 4; i < r1; i += (int64_t)gridDim.x * kOwnStep) {
     uint64_t w[4];
     bool in[4];
 #pragma unroll
@@ -314,7 +326,7 @@ __global__ void __launch_bounds__(256) gb_owner_scatter_kernel(const uint64_t* _
     for (int v = 0; v < 4; ++v) {
       const int o = (int)((uint32_t)w[v] / sl);
       const int pos = gb_owner_slot(o, in[v], s_cur, true, lane);
-      if (in[v]) out[offsets[(int64_t)o * gridDim.x + blockIdx.x] + pos] = w[v];
+      if (in[v]) out[offsets[(int64_t)o * gridDim.x + lb] + pos] = w[v];
     }
   }
 }
@@ -1368,14 +1380,15 @@ hipError_t dalgo_gb_rank_keys(const int32_t* deg, int64_t n, int64_t dmax, int i
   return hipSuccess;
 }
 
-// DALGO_GB_OWNER_BLOCKS overrides the grid (default 2048: at the W = 8 share the bucketed
+// DALGO_GB_OWNER_BLOCKS overrides the grid (default 1024: at the W = 8 share the bucketed
 // relabel + owner pass took 5.16 / 4.42 / 4.69 / 4.68 ms at 512 / 1024 / 2048 / 4096 blocks,
-// 5.2 ms with 16384-edge blocks, profiles/round6/r6_28)
+// 5.2 ms with 16384-edge blocks, profiles/round6/r6_28; with XCD-aware logical blocks 4.30 /
+// 4.47 / 4.59 at 1024 / 2048 / 4096, r6_29)
 int64_t dalgo_gb_owner_blocks(int64_t n) {
   static int64_t g = -1;
   if (g < 0) {
     const char* e = std::getenv("DALGO_GB_OWNER_BLOCKS");
-    g = e ? std::max<int64_t>(1, std::atoll(e)) : 2048;
+    g = e ? std::max<int64_t>(1, std::atoll(e)) : 1024;
   }
   return std::max<int64_t>(1, std::min<int64_t>(cdiv(n, (int64_t)kOwnStep), g));
 }
