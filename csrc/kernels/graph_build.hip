@@ -565,7 +565,8 @@ __global__ void __launch_bounds__(256) gb_keys_one_kernel(const uint64_t* __rest
   constexpr int V = 8;
   const int64_t stride = (int64_t)gridDim.x * 256 * V;
   const int sh = dbits + kSpanBits;
-  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V; i < n; i += stride) {
+  const int64_t lb = gb_xcd_block(blockIdx.x, gridDim.x);
+  for (int64_t i = (lb * 256 + threadIdx.x) * V; i < n; i += stride) {
     if (i + V <= n) {
       uint4 q[V / 2];
 #pragma unroll
@@ -1429,7 +1430,14 @@ hipError_t dalgo_gb_keys(const int32_t* src, const int32_t* dst, int64_t n, cons
   if (g > 0x7fffffffLL) return hipErrorInvalidValue;
   if (packed != nullptr && (phase == 0 || c.world > 1)) return hipErrorInvalidValue;   // one rank only
   if (packed != nullptr && c.src_new && c.new_id && c.v_lo == 0 && c.v_hi >= c.sl) {
-    const int64_t gw = std::min<int64_t>(cdiv(n, (int64_t)256 * 8), 256 * 64);
+    // DALGO_GB_KEYS_BLOCKS: grid cap (key pass at scale 26: 11.1 / 10.8 / 10.0 / 10.0 ms at
+    // 16384 / 2048 / 4096 / 8192 blocks with XCD-aware logical blocks, profiles/round6/r6_30)
+    static int64_t gmax = -1;
+    if (gmax < 0) {
+      const char* e = std::getenv("DALGO_GB_KEYS_BLOCKS");
+      gmax = e ? std::max<int64_t>(1, std::atoll(e)) : 8192;
+    }
+    const int64_t gw = std::min<int64_t>(cdiv(n, (int64_t)256 * 8), gmax);
     hipLaunchKernelGGL(gb_keys_one_kernel, dim3((unsigned)gw), dim3(256), 0, st, packed, n, c.new_id, c.dbits,
                        keys);
     DALGO_LAUNCH_CHECK();
