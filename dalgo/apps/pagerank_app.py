@@ -132,6 +132,8 @@ def degree_new_id(deg: torch.Tensor, n_vertices: int, world: int) -> torch.Tenso
     keys = torch.empty(n_vertices, dtype=torch.int64, device=deg.device)
     ops.gb_rank_keys(deg, dmax, ibits, keys)
     out = torch.empty_like(keys)
+    # (capping the degree bits at 16 -- 2 radix passes instead of 3 at scale 26 -- and
+    # re-ranking the few vertices above the cap with torch was no faster: r6_31)
     ops.gb_sort(keys, n_vertices, dbits + ibits, out, ibits)
     del keys
     new_id = torch.empty(n_vertices, dtype=torch.int32, device=deg.device)

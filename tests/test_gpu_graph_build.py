@@ -256,15 +256,18 @@ def test_deal_kernel_matches_torch(cuda, world):
     assert torch.equal(got.long().cpu(), exp.long())
 
 
-@pytest.mark.parametrize("world", [1, 2, 8])
-def test_degree_new_id_matches_torch(cuda, world):
+@pytest.mark.parametrize("world,hubs", [(1, 0), (1, 300), (2, 300), (8, 0), (8, 300)])
+def test_degree_new_id_matches_torch(cuda, world, hubs):
     """The fused ranking (gb_rank_keys + sort + masked gb_deal) == deal_ids(rank_by_degree)
-    on the CPU: degree ties (small degree range) broken by descending id, snake deal."""
+    on the CPU: degree ties (small degree range) broken by descending id, snake deal; hubs
+    with degrees past 16 bits (ties among them too)."""
     from dalgo.apps.pagerank_app import deal_ids, degree_new_id, rank_by_degree
     n = 1 << 17
     g = torch.Generator().manual_seed(6)
     deg = torch.randint(0, 40, (n,), generator=g, dtype=torch.int32)
-    deg[:5] = 1 << 20                     # a few hubs: degree bits past the low range
+    if hubs:
+        idx = torch.randperm(n, generator=g)[:hubs]
+        deg[idx] = torch.randint(1 << 16, (1 << 16) + 50, (hubs,), generator=g, dtype=torch.int32)
     exp = deal_ids(rank_by_degree(deg), n, world).to(torch.int32)
     got = degree_new_id(deg.to(cuda), n, world).cpu()
     assert got.dtype == torch.int32 and torch.equal(got, exp)
