@@ -89,7 +89,8 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
              double tail_lam, double tail_reg_alpha, const std::optional<Tensor>& tail_count_acc,
              int64_t nsteps, const std::optional<Tensor>& epoch, int64_t epoch_base,
              const std::optional<Tensor>& perr, double spin_s,
-             const std::optional<Tensor>& step_dev, int64_t step_mul) {
+             const std::optional<Tensor>& step_dev, int64_t step_mul, const std::optional<Tensor>& pool,
+             int64_t pool_lo, int64_t pool_shift) {
   check_lr_inputs(X, y, W, seg, D, has_bias);
   const int64_t* stepp = nullptr;
   if (step_dev.has_value()) {
@@ -146,6 +147,15 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
       tail.epoch_base = (uint32_t)epoch_base;
       tail.perr = reinterpret_cast<unsigned*>(perr->data_ptr<int>());
       tail.spin_s = spin_s;
+      if (pool.has_value()) {
+        check_dev(*pool, "pool");
+        TORCH_CHECK(pool->scalar_type() == at::kInt && pool->numel() >= 2, "pool: int32[2] counters");
+        TORCH_CHECK(pool_lo >= 0 && pool_lo <= X.size(0) && pool_shift >= 6 && pool_shift <= 16,
+                    "pool: 0 <= pool_lo <= rows, 6 <= pool_shift <= 16");
+        tail.pool = pool->data_ptr<int>();
+        tail.pool_lo = pool_lo;
+        tail.pool_shift = (int)pool_shift;
+      }
     }
     tailp = &tail;
   }
@@ -1819,7 +1829,7 @@ TORCH_LIBRARY(dalgo, m) {
         "float tail_eta=0., float tail_lam=0., float tail_reg_alpha=0., "
         "Tensor(j!)? tail_count_acc=None, int nsteps=1, "
         "Tensor(l!)? epoch=None, int epoch_base=0, Tensor(m!)? perr=None, float spin_s=2., "
-        "Tensor? step_dev=None, int step_mul=1) -> ()");
+        "Tensor? step_dev=None, int step_mul=1, Tensor(n!)? pool=None, int pool_lo=0, int pool_shift=6) -> ()");
   m.def("lr_eval(Tensor X, Tensor y, Tensor W, Tensor seg, int D, bool has_bias, float eps, "
         "int gx, int rows_per_block, Tensor(a!) correct, Tensor(b!) loss) -> ()");
   m.def("sync_update(Tensor(a!) W, Tensor(d!)? G, Tensor(e!)? C, Tensor? center, Tensor? S, "

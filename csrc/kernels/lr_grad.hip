@@ -84,6 +84,12 @@ struct LrParams {
   uint32_t epoch_base;
   unsigned* perr;
   uint64_t spin_ticks;
+  // persistent mode, cross-block balance: local rows [pool_lo, seg_hi) belong to no block's
+  // static range; a wave whose block has no unit left claims 2^pool_shift-row units of them
+  // from pool[step & 1] (agent-scope atomic; the step's tail block re-arms it)
+  int* pool;
+  int64_t pool_lo;
+  int pool_shift;
 };
 
 __device__ __forceinline__ void wt_store(float* a, float v) {
@@ -187,6 +193,8 @@ struct Batch {
 };
 
 constexpr int kRing = 512;   // per-wave ring of selected local row indices
+constexpr int kPoolSlots = 64;   // pool chunks one block can take per step
+constexpr int kPoolPre = 3;      // units before a chunk's end at which the next is claimed
 
 // EVAL=false: gradient; EVAL=true: accuracy + log-loss over every row.
 // PIPE: software-pipelined (two register sets) vs. single-buffered sweep.
@@ -217,6 +225,10 @@ lr_rows_kernel(const LrParams p) {
   __shared__ int s_flag;
   __shared__ int s_next;   // next unclaimed work unit of this block (dynamic balancing)
   __shared__ int s_ok;     // persistent mode: the epoch wait succeeded
+  // persistent mode with a cross-block pool: the block's claimed pool chunks (by claim
+  // order) and the next unit of them
+  __shared__ int s_chunk[PERSIST ? kPoolSlots : 1];
+  __shared__ int s_pnext;
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -227,8 +239,10 @@ lr_rows_kernel(const LrParams p) {
   const int bx = blockIdx.x;
   const int gx = gridDim.x;
   const int64_t seg_lo = p.seg[seg], seg_hi = p.seg[seg + 1];
+  const bool use_pool = PERSIST && p.pool != nullptr;
+  const int64_t static_hi = use_pool ? min(seg_hi, p.pool_lo) : seg_hi;
   const int64_t lo = seg_lo + (int64_t)bx * p.rows_per_block;
-  const int64_t hi = max(lo, min(seg_hi, lo + (int64_t)p.rows_per_block));
+  const int64_t hi = max(lo, min(static_hi, lo + (int64_t)p.rows_per_block));
   // ---- step loop (one iteration unless persistent: p.nsteps > 1)
   // (a separate instantiation: the step loop costs registers the one-step kernel keeps)
   const int nst = PERSIST && p.nsteps > 1 ? p.nsteps : 1;
@@ -334,6 +348,10 @@ lr_rows_kernel(const LrParams p) {
   const bool small = nq < upg * NW + fine_u;
   const int w0 = small ? 1 : upg;
   if (threadIdx.x == 0) s_next = w0 * NW;   // units 0..w0 * NW - 1 are pre-assigned
+  if (use_pool) {
+    if (threadIdx.x < kPoolSlots) s_chunk[threadIdx.x] = -2;
+    if (threadIdx.x == 0) s_pnext = 0;
+  }
   __syncthreads();
   const unsigned long long t_bar = tr ? (unsigned long long)__builtin_amdgcn_s_memrealtime() : 0ull;
 
@@ -380,6 +398,57 @@ lr_rows_kernel(const LrParams p) {
         if (gi < nq) {
           gnext = gstart + ((int64_t)gi << qs);
           uhi = min(ghi, gnext + ((int64_t)w << qs));
+        } else if (use_pool) {
+          // the block's own units are gone: units of pool chunks. The BLOCK claims chunks
+          // of 2^pool_shift rows (one agent-scope atomic each: a per-wave claim of single
+          // units serialised ~2000 atomics on one address, 51 -> 82 us per step, r6_35);
+          // its waves draw the chunk's 2^qs-row units from an LDS counter. The drawer of
+          // unit upc - kPoolPre of chunk m claims chunk m + 1 ahead; chunk 0 is claimed by
+          // the first drawer. Slot states: -2 pending, -1 pool exhausted, else the chunk.
+          const int upc = 1 << (p.pool_shift - qs);
+          int k = 0;
+          if (lane == 0) k = atomicAdd(&s_pnext, 1);
+          k = __builtin_amdgcn_readfirstlane(k);
+          const int m = k >> (p.pool_shift - qs), j = k & (upc - 1);
+          if (m >= kPoolSlots) {
+            more = false;
+          } else {
+            const int64_t nchunk = (seg_hi - p.pool_lo + ((int64_t)1 << p.pool_shift) - 1) >> p.pool_shift;
+            auto claim = [&](int mm) {
+              if (lane == 0) {
+                const int c = __hip_atomic_fetch_add(p.pool + (step_cur & 1), 1, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                *(volatile int*)&s_chunk[mm] = c < nchunk ? c : -1;
+              }
+            };
+            if (m == 0 && j == 0) claim(0);
+            if (j == max(0, upc - kPoolPre) && m + 1 < kPoolSlots) claim(m + 1);
+            int c = 0;
+            if (lane == 0) {
+              // bounded like the step-release wait: a slot never written would be a bug;
+              // it then ends this wave's sweep and raises the persistent error word
+              const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+              while ((c = *(volatile int*)&s_chunk[m]) == -2) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > p.spin_ticks) {
+                  __hip_atomic_store(p.perr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  c = -1;
+                  break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+              }
+            }
+            c = __builtin_amdgcn_readfirstlane(c);
+            const int64_t g0 = p.row_offset + p.pool_lo + ((int64_t)c << p.pool_shift) + ((int64_t)j << qs);
+            const int64_t gend = p.row_offset + seg_hi;
+            if (c >= 0 && g0 < gend) {
+              // (the Philox quad stays aligned: the walk starts at the unit's quad)
+              gnext = g0 & ~(int64_t)3;
+              ulo = g0;
+              uhi = min(gend, g0 + ((int64_t)1 << qs));
+            } else {
+              more = false;
+            }
+          }
         } else {
           more = false;
         }
@@ -616,6 +685,8 @@ lr_rows_kernel(const LrParams p) {
         lr_tail(p, xbase + (uint32_t)it + 1u);
         if (p.xg.world > 1 && it == nst - 1 && threadIdx.x == 0)
           xg_epoch_store(p.xg, xbase + (uint32_t)nst);
+        if (use_pool && threadIdx.x == 0)   // every block is past this step's pool claims
+          __hip_atomic_store(p.pool + (step_cur & 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (PERSIST && nst > 1) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // W / G / C / ticket written through
           __syncthreads();
@@ -794,6 +865,12 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
       p.epoch_base = tail->epoch_base;
       p.perr = tail->perr;
       p.spin_ticks = (uint64_t)(tail->spin_s * 1e8);
+      if (tail->pool != nullptr) {
+        if (tail->pool_lo < 0 || tail->pool_shift < 6 || tail->pool_shift > 16) return hipErrorInvalidValue;
+        p.pool = tail->pool;
+        p.pool_lo = tail->pool_lo;
+        p.pool_shift = tail->pool_shift;
+      }
     }
   }
   p.count_acc = count_acc;

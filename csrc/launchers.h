@@ -23,6 +23,12 @@ struct DalgoLrTail {
   uint32_t epoch_base;
   unsigned* perr;
   double spin_s;
+  // persistent launches (optional): local rows [pool_lo, end of the segment) are not in any
+  // block's static range but claimed in 2^pool_shift-row units from a device counter
+  // (int32[2], one per step parity, zero on entry; each step's tail block re-arms its own)
+  int* pool;
+  int64_t pool_lo;
+  int pool_shift;
 };
 
 // Filtered k-means iteration (kmeans.hip dalgo_kmeans_assign_idx): the K2 epilogue

@@ -39,6 +39,14 @@ UNIT_SHIFT = 6             # sampled steps: work units of 2^6 rows (the final, f
 RPB_ALIGN = int(os.environ.get("DALGO_LR_RPB_ALIGN", "256"))
                            # granularity (rows) of each block's static range (4-row ranges
                            # measured equal: profiles/final/README.md)
+# persistent launches: this fraction of the rows (the top of the range) is left out of the
+# blocks' static ranges and claimed across blocks in 2^POOL_SHIFT-row chunks (the blocks that
+# finish their own rows early take them: the last block no longer sets the step time).
+# 10M x 1024 bf16 on one MI355X: 0.3321 ms/step without, 0.3193 / 0.3168 / 0.3153 / 0.3164
+# with 5 / 10 / 15 / 20 % pooled (one-kernel form 0.3287 on the same box,
+# profiles/round6/r6_37); 1.25M rows: flat (54.3 -> 54.4 us, r6_36)
+POOL_FRAC = float(os.environ.get("DALGO_LR_POOL", "0.15"))
+POOL_SHIFT = int(os.environ.get("DALGO_LR_POOL_SHIFT", "9"))   # rows per block claim: 2^9
 # DETERMINISTIC = combine per-block partials with the fixed-order two-level hand-off
 # (bitwise repeatable) instead of float atomics (race-detection mode)
 DETERMINISTIC = os.environ.get("DALGO_DETERMINISTIC", "0") == "1"
@@ -82,6 +90,7 @@ class _Workspace:
     ticket: torch.Tensor   # fused-tail arrival counter (re-armed by the kernel)
     epoch: torch.Tensor    # persistent launches: device step-release counter ...
     perr: torch.Tensor     # ... and its wait-timeout error word
+    pool: torch.Tensor     # persistent launches: cross-block unit counters (per step parity)
     epochs: int = 0        # host mirror of `epoch` (advanced by nsteps per launch)
 
 
@@ -101,6 +110,7 @@ def _workspace(device, nseg, gx, S) -> _Workspace:
             ticket=torch.zeros(1, dtype=torch.int32, device=device),
             epoch=torch.zeros(1, dtype=torch.int32, device=device),
             perr=torch.zeros(1, dtype=torch.int32, device=device),
+            pool=torch.zeros(2, dtype=torch.int32, device=device),
         )
         _ws_cache[key] = ws
     return ws
@@ -179,7 +189,16 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
                 b = seg.tolist()
                 max_seg_rows = max(b[i + 1] - b[i] for i in range(nseg))
         det = DETERMINISTIC if deterministic is None else bool(deterministic)
-        gx, rpb = _grid(max(int(max_seg_rows), 1), nseg, target_blocks)
+        nst = int(tail.get("nsteps", 1)) if tail is not None else 1
+        pool_lo = None
+        if nst > 1 and nseg == 1 and POOL_FRAC > 0 and not det:
+            # static ranges over the rows below pool_lo (a 256-row multiple), the rest pooled
+            nr = int(max_seg_rows)
+            pool_lo = max(256, (int(nr * (1.0 - POOL_FRAC)) // 256) * 256)
+            # (a block takes at most 64 chunks per step: the pool never needs more)
+            if pool_lo >= nr or nr - pool_lo > 64 * (1 << POOL_SHIFT) * max(1, TARGET_BLOCKS // 2):
+                pool_lo = None
+        gx, rpb = _grid(max(int(max_seg_rows if pool_lo is None else pool_lo), 1), nseg, target_blocks)
         S = ((D + 2 + 63) // 64) * 64
         ws = _workspace(X.device, nseg, gx, S)
         fg = FINE_GROUPS if fine_groups is None else int(fine_groups)
@@ -205,6 +224,8 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
                     ws.epochs = 0
                 kw.update(nsteps=nsteps, epoch=ws.epoch, epoch_base=ws.epochs, perr=ws.perr,
                           spin_s=float(tail.get("spin_s", 2.0)))
+                if pool_lo is not None:
+                    kw.update(pool=ws.pool, pool_lo=pool_lo, pool_shift=POOL_SHIFT)
                 ws.epochs += nsteps
             _ext.ops().lr_grad(X, y, W, seg, int(row_offset), int(D), bool(has_bias), float(eps),
                                int(seed), int(step), float(frac), gx, rpb, ws.slab, ws.gslab,

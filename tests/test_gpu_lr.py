@@ -194,10 +194,14 @@ def test_lr_grad_fused_tail_single_rank(cuda, mode, reg):
     assert rel < 1e-5, rel
 
 
-@pytest.mark.parametrize("mode,reg,n", [(0, 0, 300_000), (0, 3, 1_250_000), (1, 0, 40_000)])
-def test_lr_grad_persistent_steps(cuda, mode, reg, n):
+@pytest.mark.parametrize("mode,reg,n,pool", [(0, 0, 300_000, 0.0), (0, 3, 1_250_000, 0.0), (1, 0, 40_000, 0.0),
+                                             (0, 0, 1_250_001, 0.15), (1, 0, 300_002, 0.3)])
+def test_lr_grad_persistent_steps(cuda, mode, reg, n, pool, monkeypatch):
     """Persistent launch (K steps in one cooperative grid, epoch-released W) == K
-    separate gradient + update steps; the release counter ends at base + K."""
+    separate gradient + update steps; the release counter ends at base + K. With a
+    cross-block pool (the top rows claimed in 64-row units by whichever block runs out
+    first) every row is still taken exactly once: the minibatch sizes match exactly."""
+    monkeypatch.setattr(L, "POOL_FRAC", pool)
     Xd, yd = _data(n, 1024, torch.bfloat16, seed=12, device=cuda)
     seg = torch.tensor([0, n], dtype=torch.int64, device=cuda)
     w0 = torch.randn(1, 1025, generator=torch.Generator().manual_seed(5)).to(cuda) * 0.05
