@@ -20,6 +20,8 @@
 //
 // Segments: rows [seg_lo[s], seg_lo[s+1]) use model s (MA/BMUF/EASGD keep one
 // local model per logical worker, ma.py:86-87); SSGD uses a single segment.
+#include <cstdlib>
+
 #include "dalgo/common.h"
 #include "dalgo/xgmi.h"
 #include "launchers.h"
@@ -772,7 +774,18 @@ static hipError_t launch_lr(const LrParams& p, int gx, int nseg, hipStream_t st)
   if (p.nsteps > 1) {
     if constexpr (!EVAL) {
       // persistent mode: every block must be resident (blocks wait on each other);
-      // the cooperative launch refuses a grid that cannot be
+      // the cooperative launch refuses a grid that cannot be. DALGO_PERSIST_COOP=0: a plain
+      // launch instead (experiment: the cooperative path's fixed cost per launch)
+      static int coop = -1;
+      if (coop < 0) {
+        const char* e = std::getenv("DALGO_PERSIST_COOP");
+        coop = (e != nullptr && e[0] == '0') ? 0 : 1;
+      }
+      if (!coop) {
+        hipLaunchKernelGGL((lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, true, AUX>), grid, block, 0, st, p);
+        DALGO_LAUNCH_CHECK();
+        return hipSuccess;
+      }
       void* args[] = {const_cast<LrParams*>(&p)};
       return hipLaunchCooperativeKernel((const void*)lr_rows_kernel<T, NC, EVAL, NW, PIPE, U, true, AUX>,
                                         grid, block, args, 0, st);
