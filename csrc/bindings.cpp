@@ -147,15 +147,18 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
       tail.epoch_base = (uint32_t)epoch_base;
       tail.perr = reinterpret_cast<unsigned*>(perr->data_ptr<int>());
       tail.spin_s = spin_s;
-      if (pool.has_value()) {
-        check_dev(*pool, "pool");
-        TORCH_CHECK(pool->scalar_type() == at::kInt && pool->numel() >= 2, "pool: int32[2] counters");
-        TORCH_CHECK(pool_lo >= 0 && pool_lo <= X.size(0) && pool_shift >= 6 && pool_shift <= 16,
-                    "pool: 0 <= pool_lo <= rows, 6 <= pool_shift <= 16");
-        tail.pool = pool->data_ptr<int>();
-        tail.pool_lo = pool_lo;
-        tail.pool_shift = (int)pool_shift;
-      }
+    }
+    if (pool.has_value()) {
+      check_dev(*pool, "pool");
+      TORCH_CHECK(pool->scalar_type() == at::kInt && pool->numel() >= 2, "pool: int32[2] counters");
+      TORCH_CHECK(pool_lo >= 0 && pool_lo <= X.size(0) && pool_shift >= 6 && pool_shift <= 16,
+                  "pool: 0 <= pool_lo <= rows, 6 <= pool_shift <= 16");
+      TORCH_CHECK(perr.has_value() && perr->scalar_type() == at::kInt, "pool: needs the perr error word");
+      check_dev(*perr, "perr");
+      tail.pool = pool->data_ptr<int>();
+      tail.pool_lo = pool_lo;
+      tail.pool_shift = (int)pool_shift;
+      tail.perr = reinterpret_cast<unsigned*>(perr->data_ptr<int>());
     }
     tailp = &tail;
   }

@@ -229,7 +229,7 @@ lr_rows_kernel(const LrParams p) {
   __shared__ int s_ok;     // persistent mode: the epoch wait succeeded
   // persistent mode with a cross-block pool: the block's claimed pool chunks (by claim
   // order) and the next unit of them
-  __shared__ int s_chunk[PERSIST ? kPoolSlots : 1];
+  __shared__ int s_chunk[kLean ? kPoolSlots : 1];
   __shared__ int s_pnext;
 
   const int lane = threadIdx.x & 63;
@@ -241,7 +241,7 @@ lr_rows_kernel(const LrParams p) {
   const int bx = blockIdx.x;
   const int gx = gridDim.x;
   const int64_t seg_lo = p.seg[seg], seg_hi = p.seg[seg + 1];
-  const bool use_pool = PERSIST && p.pool != nullptr;
+  const bool use_pool = kLean && p.pool != nullptr;   // fused-tail launches only (the tail re-arms)
   const int64_t static_hi = use_pool ? min(seg_hi, p.pool_lo) : seg_hi;
   const int64_t lo = seg_lo + (int64_t)bx * p.rows_per_block;
   const int64_t hi = max(lo, min(static_hi, lo + (int64_t)p.rows_per_block));
@@ -878,12 +878,15 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
       p.epoch_base = tail->epoch_base;
       p.perr = tail->perr;
       p.spin_ticks = (uint64_t)(tail->spin_s * 1e8);
-      if (tail->pool != nullptr) {
-        if (tail->pool_lo < 0 || tail->pool_shift < 6 || tail->pool_shift > 16) return hipErrorInvalidValue;
-        p.pool = tail->pool;
-        p.pool_lo = tail->pool_lo;
-        p.pool_shift = tail->pool_shift;
-      }
+    }
+    if (tail->pool != nullptr) {
+      if (tail->pool_lo < 0 || tail->pool_shift < 6 || tail->pool_shift > 16) return hipErrorInvalidValue;
+      p.pool = tail->pool;
+      p.pool_lo = tail->pool_lo;
+      p.pool_shift = tail->pool_shift;
+      if (p.spin_ticks == 0) p.spin_ticks = (uint64_t)(2.0 * 1e8);   // the chunk-slot wait bound
+      p.perr = tail->perr;
+      if (p.perr == nullptr) return hipErrorInvalidValue;
     }
   }
   p.count_acc = count_acc;

@@ -47,6 +47,12 @@ RPB_ALIGN = int(os.environ.get("DALGO_LR_RPB_ALIGN", "256"))
 # profiles/round6/r6_37); 1.25M rows: flat (54.3 -> 54.4 us, r6_36)
 POOL_FRAC = float(os.environ.get("DALGO_LR_POOL", "0.15"))
 POOL_SHIFT = int(os.environ.get("DALGO_LR_POOL_SHIFT", "9"))   # rows per block claim: 2^9
+# the same for one-step fused (one-kernel) launches: 10M x 1024 bf16, 20 steps, alternating
+# runs on one box: 0.3353 -> 0.3274 ms/step with 10 % pooled (profiles/round6/r6_44)
+POOL_FRAC_ONE = float(os.environ.get("DALGO_LR_POOL1", "0.1"))
+# only where the blocks' static ranges are long: at 1.25M rows (the 8-GPU per-rank share)
+# the pool cost 1-2 % (r6_36, r6_43)
+POOL_MIN_ROWS = int(os.environ.get("DALGO_LR_POOL_MIN_ROWS", str(4_000_000)))
 # DETERMINISTIC = combine per-block partials with the fixed-order two-level hand-off
 # (bitwise repeatable) instead of float atomics (race-detection mode)
 DETERMINISTIC = os.environ.get("DALGO_DETERMINISTIC", "0") == "1"
@@ -92,6 +98,7 @@ class _Workspace:
     perr: torch.Tensor     # ... and its wait-timeout error word
     pool: torch.Tensor     # persistent launches: cross-block unit counters (per step parity)
     epochs: int = 0        # host mirror of `epoch` (advanced by nsteps per launch)
+    pool_used: bool = False  # a pooled launch can raise perr too (bounded chunk-slot wait)
 
 
 _ws_cache: dict = {}
@@ -121,14 +128,14 @@ def persistent_error() -> int:
     timed out, the launch ended early and the model is not trustworthy)."""
     e = 0
     for ws in _ws_cache.values():
-        if ws.epochs:
+        if ws.epochs or ws.pool_used:
             e = max(e, int(ws.perr.item()))
     return e
 
 
 def persistent_used() -> bool:
     """True once a persistent launch has armed its step-release workspace."""
-    return any(ws.epochs for ws in _ws_cache.values())
+    return any(ws.epochs or ws.pool_used for ws in _ws_cache.values())
 
 
 def reset_persistent_error():
@@ -191,10 +198,11 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
         det = DETERMINISTIC if deterministic is None else bool(deterministic)
         nst = int(tail.get("nsteps", 1)) if tail is not None else 1
         pool_lo = None
-        if nst > 1 and nseg == 1 and POOL_FRAC > 0 and not det:
+        pf = POOL_FRAC if nst > 1 else POOL_FRAC_ONE
+        if tail is not None and nseg == 1 and pf > 0 and not det and int(max_seg_rows) >= POOL_MIN_ROWS:
             # static ranges over the rows below pool_lo (a 256-row multiple), the rest pooled
             nr = int(max_seg_rows)
-            pool_lo = max(256, (int(nr * (1.0 - POOL_FRAC)) // 256) * 256)
+            pool_lo = max(256, (int(nr * (1.0 - pf)) // 256) * 256)
             # (a block takes at most 64 chunks per step: the pool never needs more)
             if pool_lo >= nr or nr - pool_lo > 64 * (1 << POOL_SHIFT) * max(1, TARGET_BLOCKS // 2):
                 pool_lo = None
@@ -224,9 +232,10 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
                     ws.epochs = 0
                 kw.update(nsteps=nsteps, epoch=ws.epoch, epoch_base=ws.epochs, perr=ws.perr,
                           spin_s=float(tail.get("spin_s", 2.0)))
-                if pool_lo is not None:
-                    kw.update(pool=ws.pool, pool_lo=pool_lo, pool_shift=POOL_SHIFT)
                 ws.epochs += nsteps
+            if pool_lo is not None:
+                kw.update(pool=ws.pool, pool_lo=pool_lo, pool_shift=POOL_SHIFT, perr=ws.perr)
+                ws.pool_used = True
             _ext.ops().lr_grad(X, y, W, seg, int(row_offset), int(D), bool(has_bias), float(eps),
                                int(seed), int(step), float(frac), gx, rpb, ws.slab, ws.gslab,
                                ws.cnt1, ws.cnt2, G, C, flags | ATOMIC_EPILOGUE, count_acc,

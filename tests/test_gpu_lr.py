@@ -163,9 +163,12 @@ def test_rows_sum_broadcast(cuda):
     assert torch.equal(Wd.cpu(), src.expand(4, -1))
 
 
-@pytest.mark.parametrize("mode,reg", [(0, 0), (0, 3), (1, 0)])
-def test_lr_grad_fused_tail_single_rank(cuda, mode, reg):
-    """One-launch step (gradient + update in the last block) == lr_grad + K8."""
+@pytest.mark.parametrize("mode,reg,pool", [(0, 0, 0.0), (0, 3, 0.0), (1, 0, 0.0), (0, 0, 0.2)])
+def test_lr_grad_fused_tail_single_rank(cuda, mode, reg, pool, monkeypatch):
+    """One-launch step (gradient + update in the last block) == lr_grad + K8 (also with
+    the cross-block row pool: exact minibatch counts)."""
+    monkeypatch.setattr(L, "POOL_FRAC_ONE", pool)
+    monkeypatch.setattr(L, "POOL_MIN_ROWS", 0)
     Xd, yd = _data(300_000, 1024, torch.bfloat16, seed=11, device=cuda)
     X = Xd
     seg = torch.tensor([0, X.shape[0]], dtype=torch.int64, device=cuda)
@@ -202,6 +205,7 @@ def test_lr_grad_persistent_steps(cuda, mode, reg, n, pool, monkeypatch):
     cross-block pool (the top rows claimed in 64-row units by whichever block runs out
     first) every row is still taken exactly once: the minibatch sizes match exactly."""
     monkeypatch.setattr(L, "POOL_FRAC", pool)
+    monkeypatch.setattr(L, "POOL_MIN_ROWS", 0)
     Xd, yd = _data(n, 1024, torch.bfloat16, seed=12, device=cuda)
     seg = torch.tensor([0, n], dtype=torch.int64, device=cuda)
     w0 = torch.randn(1, 1025, generator=torch.Generator().manual_seed(5)).to(cuda) * 0.05
