@@ -107,7 +107,8 @@ void lr_grad(const Tensor& X, const Tensor& y, const Tensor& W, const Tensor& se
     check_dev(*ticket, "ticket");
     TORCH_CHECK(ticket->scalar_type() == at::kInt && ticket->numel() >= 1, "ticket int32[1]");
     TORCH_CHECK(W.size(0) == 1 && (flags & 256), "fused tail: one model, atomic epilogue");
-    TORCH_CHECK(tail_mode == 0 || tail_mode == 1, "fused tail mode: 0 SSGD, 1 GD");
+    TORCH_CHECK(tail_mode == 0 || tail_mode == 1 || (tail_mode == 2 && nsteps <= 1 && pool.has_value()),
+                "fused tail mode: 0 SSGD, 1 GD, 2 none (pooled gradient launch)");
     tail.ticket = reinterpret_cast<unsigned*>(ticket->data_ptr<int>());
     tail.world = 1;
     if (xg_bufs.has_value() && xg_bufs->size() > 1) {

@@ -681,12 +681,18 @@ lr_rows_kernel(const LrParams p) {
       }
       __syncthreads();
       if (s_flag) {
-        // exchange epoch of step it: device base (unchanged until this launch's last
-        // exchange is done) + it + 1; the last step's tail stores the new base
-        const uint32_t xbase = p.xg.world > 1 ? xg_epoch_base(p.xg) : 0u;
-        lr_tail(p, xbase + (uint32_t)it + 1u);
-        if (p.xg.world > 1 && it == nst - 1 && threadIdx.x == 0)
-          xg_epoch_store(p.xg, xbase + (uint32_t)nst);
+        if (p.tu.mode == 2) {
+          // no fused update (a plain gradient launch with the row pool): the last block
+          // only re-arms the ticket and the pool
+          if (threadIdx.x == 0) __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          // exchange epoch of step it: device base (unchanged until this launch's last
+          // exchange is done) + it + 1; the last step's tail stores the new base
+          const uint32_t xbase = p.xg.world > 1 ? xg_epoch_base(p.xg) : 0u;
+          lr_tail(p, xbase + (uint32_t)it + 1u);
+          if (p.xg.world > 1 && it == nst - 1 && threadIdx.x == 0)
+            xg_epoch_store(p.xg, xbase + (uint32_t)nst);
+        }
         if (use_pool && threadIdx.x == 0)   // every block is past this step's pool claims
           __hip_atomic_store(p.pool + (step_cur & 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (PERSIST && nst > 1) {
@@ -857,6 +863,8 @@ hipError_t dalgo_lr_grad(const void* X, const float* y, const float* W, const in
   p.step_dev = step_dev;
   p.step_mul = step_mul;
   if (tail != nullptr) {
+    if (tail->mode == 2 && (tail->world != 1 || tail->nsteps > 1 || tail->pool == nullptr))
+      return hipErrorInvalidValue;   // mode 2: a pooled gradient launch without the update
     if (nseg != 1 || !((flags >> 8) & 1) || tail->ticket == nullptr ||
         tail->world < 1 || tail->world > kXgMaxRanks || tail->rank < 0 || tail->rank >= tail->world ||
         (tail->world > 1 && (tail->epoch_dev == nullptr || tail->slot < ldw + 1)))

@@ -199,7 +199,7 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
         nst = int(tail.get("nsteps", 1)) if tail is not None else 1
         pool_lo = None
         pf = POOL_FRAC if nst > 1 else POOL_FRAC_ONE
-        if tail is not None and nseg == 1 and pf > 0 and not det and int(max_seg_rows) >= POOL_MIN_ROWS:
+        if nseg == 1 and pf > 0 and not det and int(max_seg_rows) >= POOL_MIN_ROWS:
             # static ranges over the rows below pool_lo (a 256-row multiple), the rest pooled
             nr = int(max_seg_rows)
             pool_lo = max(256, (int(nr * (1.0 - pf)) // 256) * 256)
@@ -250,6 +250,11 @@ def lr_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, seg: torch.Tensor
                 G.zero_()
                 C.zero_()
             flags |= ATOMIC_EPILOGUE
+        if pool_lo is not None:
+            # the row pool without a fused update: the last block re-arms ticket and pool
+            dev.update(ticket=ws.ticket, tail_mode=2, pool=ws.pool, pool_lo=pool_lo,
+                       pool_shift=POOL_SHIFT, perr=ws.perr)
+            ws.pool_used = True
         _ext.ops().lr_grad(X, y, W, seg, int(row_offset), int(D), bool(has_bias), float(eps),
                            int(seed), int(step), float(frac), gx, rpb, ws.slab, ws.gslab,
                            ws.cnt1, ws.cnt2, G, C, flags, count_acc, **dev)

@@ -233,3 +233,24 @@ def test_lr_grad_persistent_steps(cuda, mode, reg, n, pool, monkeypatch):
     assert bool((G == 0).all()) and bool((C == 0).all())
     rel = ((w - w_ref).abs().max() / w_ref.abs().max()).item()
     assert rel < 1e-4, rel
+
+
+@pytest.mark.parametrize("n", [300_001, 1_250_000])
+def test_lr_grad_row_pool_plain_launch(cuda, n, monkeypatch):
+    """A plain gradient launch with the cross-block row pool (the last block only re-arms
+    the ticket and the pool counter) == the same launch without it: the same selected-row
+    count (exact) and gradient sum over several steps."""
+    Xd, yd = _data(n, 1024, torch.bfloat16, seed=13, device=cuda)
+    seg = torch.tensor([0, n], dtype=torch.int64, device=cuda)
+    w = torch.randn(1, 1025, generator=torch.Generator().manual_seed(6)).to(cuda) * 0.05
+    kw = dict(D=1024, frac=0.1, eps=0.0, seed=42)
+    for t in range(4):
+        monkeypatch.setattr(L, "POOL_FRAC_ONE", 0.0)
+        G0, C0 = L.lr_grad(Xd, yd, w, seg, step=t, **kw)
+        monkeypatch.setattr(L, "POOL_FRAC_ONE", 0.2)
+        monkeypatch.setattr(L, "POOL_MIN_ROWS", 0)
+        G1, C1 = L.lr_grad(Xd, yd, w, seg, step=t, **kw)
+        torch.cuda.synchronize()
+        assert float(C1.item()) == float(C0.item())
+        assert torch.allclose(G1, G0, rtol=1e-4, atol=1e-3)
+    L.check_persistent()
