@@ -727,8 +727,11 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     nbd = int(ops.gb_decode_blocks(total))            # graph_build.hip kDecR keys per block
     counts = torch.empty(2 * nbd, **i64)
     ops.gb_decode(K, total, shift, dbits, blk_base, 0, counts, outdeg_loc, None, None, None, None, None)
-    offsets = torch.cumsum(counts.view(nbd, 2), 0) - counts.view(nbd, 2)
-    E, nent = (int(x) for x in counts.view(nbd, 2).sum(0).tolist())
+    # (scanned as two rows: torch's scan down the 2-column [nbd, 2] view ran 2.6 ms at scale
+    # 26 -- one thread per column -- profiles/round6/r6_48)
+    ct = counts.view(nbd, 2).t().contiguous()
+    offsets = (torch.cumsum(ct, 1) - ct).t()
+    E, nent = (int(x) for x in ct.sum(1).tolist())
     E16 = (E + 15) // 16 * 16
     srcl = torch.zeros(E16, dtype=torch.int16, device=dev)
     ent_end = torch.empty(nent, **i64)
