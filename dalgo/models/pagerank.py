@@ -65,7 +65,9 @@ class PageRank:
         nl = shard.n_local
         sl = shard.slice_size
         # global out-degree (each rank holds the in-edges of its slice only)
-        if native:
+        if native and world == 1 and shard.v_lo == 0 and shard.v_hi == shard.n_vertices and not shard.n_ghost:
+            od_full = shard.outdeg_loc[:nl]        # one rank: the local out-degrees are global
+        elif native:
             od_full = torch.zeros(shard.n_vertices, dtype=torch.int32, device=dev)
             od_full[shard.v_lo: shard.v_hi] += shard.outdeg_loc[:nl]
             if shard.ghosts is not None and shard.n_ghost:
@@ -129,9 +131,11 @@ class PageRank:
         self.dang_next = torch.zeros(1, dtype=fdt, device=dev)
         od = self.outdeg.to(fdt)
         if self.mode == 0:
+            # (scalar where: one kernel each -- the full_like / clamp forms were ~1 ms of
+            # small kernels in the scale-26 job, profiles/round6/r6_48)
             p = self.outdeg > 0
-            self.r.copy_(torch.where(p, torch.full_like(od, self.invN), torch.full_like(od, -1.0)))
-            self.c_slice[:nl] = torch.where(p, self.invN / od.clamp_min(1), torch.full_like(od, -1.0))
+            self.r.copy_(torch.where(p, self.invN, -1.0))
+            self.c_slice[:nl] = torch.where(p, self.invN / od, -1.0)
             self.c_slice[nl:] = -1.0
         else:
             self.r.fill_(self.invN)

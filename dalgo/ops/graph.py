@@ -733,7 +733,8 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     offsets = (torch.cumsum(ct, 1) - ct).t()
     E, nent = (int(x) for x in ct.sum(1).tolist())
     E16 = (E + 15) // 16 * 16
-    srcl = torch.zeros(E16, dtype=torch.int16, device=dev)
+    srcl = torch.empty(E16, dtype=torch.int16, device=dev)   # the decode writes [0, E)
+    srcl[E:].zero_()
     ent_end = torch.empty(nent, **i64)
     ent_blk = torch.empty(nent, **i32)
     ent_dst = torch.empty(nent, **i32)
