@@ -697,7 +697,9 @@ void kmeans_assign_idx(const Tensor& X, const Tensor& Cq, const Tensor& hn,
     cd.hnb = cand[2].data_ptr<float>();
     cd.nb = cand[3].data_ptr<int32_t>();
     cd.nd = cand[4].data_ptr<float>();
-    cd.extend = cand_extend != 0;
+    cd.extend = (cand_extend & 1) != 0;
+    cd.tile16 = (cand_extend & 2) != 0;   // bit 1: tiles of <= 384 rows, 16x16x32 form
+    cd.max_tiles = cand[0].numel() / 4;
     if (cand.size() >= 7) {
       TORCH_CHECK(cand[5].scalar_type() == at::kFloat && cand[6].scalar_type() == at::kFloat &&
                       cand[5].numel() >= k * kpad && cand[6].numel() >= k * kpad,

@@ -1737,7 +1737,20 @@ static hipError_t launch_assign_pipe(const void* X, int64_t n, int64_t ldx, cons
 // key (v_med3 per key pair, merged over chunks and lane groups), and the epilogue is the
 // filtered iteration's: u / l per row, assign and the moved-row list where the cluster
 // differs from the previous one (aux.acl[p], else aux.a_prev[row], else assign[row]).
-template <int NW, int PG, int MINB, bool BND = false>
+// CND (the candidate-pruned form on the same tiling, BND implied): block b is tile b of the
+// cluster-sorted active rows (<= TILE rows of one cluster acl; blocks past the device tile
+// count exit), the centre stream is acl's neighbour list (gathered by LDS-DMA through the
+// staged ids, 0.5|c|^2 from hnb in list order), and only its first nc chunks are streamed:
+// the chunks whose first distance to c_acl is <= R = 2 max over the tile of ua, ua >= |x -
+// c_acl| (exact v_dot2 distance in the prologue, rounded up) -- a centre farther than R
+// from c_acl is farther than c_acl from every tile point. The pruned centres bound the new
+// l by nd_first - ua; the previous cluster of every row is acl.
+// CND + DRIFT (drift-aware lists, as the pipelined form's DRIFT): past chunk 0 a list entry
+// is streamed iff it is inside the ball AND its centre moved by >= tau = min over the tile
+// rows of (l - ua) (capped): a slower centre is farther than c_acl from every tile row. The
+// kept entries are compacted behind chunk 0 (block scan); the dropped ones bound the new l
+// by l - (largest dropped shift) and nd_first - ua.
+template <int NW, int PG, int MINB, bool BND = false, bool CND = false, bool DRIFT = false>
 __global__ void __launch_bounds__(NW * 64, MINB)
 kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
                        const uint16_t* __restrict__ Cq, const float* __restrict__ hn, int kpad,
@@ -1754,25 +1767,47 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   constexpr int NBUF = 2;
   constexpr int TILE = NW * PG * 16;
   static_assert(CHP % NT == 0 && (NT / NJ) % (SWZ + 1) == 0, "DMA layout");
+  static_assert(!CND || BND, "the candidate form is a form of the filtered iteration");
+  static_assert(!DRIFT || CND, "drift pruning refines the candidate lists");
+  constexpr int KH = DRIFT ? 1024 / (NW * 64) : 1;   // list entries per thread (consecutive)
   __shared__ __attribute__((aligned(16))) uint4 s_c[NBUF * CHP];
   extern __shared__ __attribute__((aligned(16))) float s_hn16[];   // [kpad]: 0.5|c|^2 + M
   __shared__ float s_m[NW];
   __shared__ double s_sse[NW];
   __shared__ float s_x2[NW][PG * 16];           // |x|^2 per point (read in the epilogue)
   __shared__ int s_row[BND ? NW : 1][BND ? PG * 16 : 1];   // BND: row and previous cluster
-  __shared__ int s_old[BND ? NW : 1][BND ? PG * 16 : 1];   //      per point
+  __shared__ int s_old[BND && !CND ? NW : 1][BND && !CND ? PG * 16 : 1];   //      per point
+  __shared__ uint16_t s_nbl[CND ? 1024 : 1];   // CND: the tile cluster's neighbour list
+  __shared__ float s_ur[CND ? NW : 1];         // CND: per-wave max of ua
+  // CND / DRIFT: every point's ua and last l, read again by the epilogue (LDS rather than
+  // 12 VGPRs held over the chunk loop: the register file is full there)
+  __shared__ float s_ua[CND ? NW : 1][CND ? PG * 16 : 1];
+  __shared__ float s_lold[DRIFT ? NW : 1][DRIFT ? PG * 16 : 1];
+  __shared__ float s_tau[DRIFT ? NW : 1];      // DRIFT: per-wave min of l - ua
+  __shared__ int s_kc[DRIFT ? NW : 1];         // DRIFT: kept entries per wave
+  __shared__ float s_kd[DRIFT ? NW : 1], s_kf[DRIFT ? NW : 1];
   // BND: the block's moved rows (row, new, previous cluster), appended to the global list
   // with ONE atomic per block: a device-scope atomic per wave on the single counter
   // serialised the launch (55 vs 19 ms at 14M moved rows, profiles/round5/r5_13)
-  __shared__ int s_mv[BND ? 3 : 1][BND ? TILE : 1];
+  __shared__ int s_mv[BND ? TILE : 1];
+  __shared__ uint16_t s_mvn[BND ? TILE : 1], s_mvo[BND ? TILE : 1];   // clusters < 2^16
   __shared__ int s_nmv;
   __shared__ unsigned long long s_mvbase;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lg = lane >> 4, pl = lane & 15;
   const int nchunk = kpad / CH;
-  const int64_t pbase = ((int64_t)blockIdx.x * NW + wid) * (PG * 16);
+  int64_t pbase = ((int64_t)blockIdx.x * NW + wid) * (PG * 16);
   float tol = 0.f;
-  if constexpr (BND) {
+  int acl = 0;
+  if constexpr (CND) {
+    if ((int64_t)blockIdx.x >= (int64_t)*aux.n_tiles) return;   // block-uniform
+    const int4 tr = aux.tiles[blockIdx.x];
+    acl = tr.x;
+    n = tr.z;
+    pbase = (int64_t)tr.y + (int64_t)wid * (PG * 16);
+    tol = *aux.tol;
+    if (tid == 0) s_nmv = 0;
+  } else if constexpr (BND) {
     n = min(n, (int64_t)*aux.mcount);
     if ((int64_t)blockIdx.x * TILE >= n) return;   // block-uniform, before any barrier
     tol = *aux.tol;
@@ -1798,11 +1833,44 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
 #pragma unroll
     for (int s = 0; s < KS; ++s) bf[g][s] = *reinterpret_cast<const uint4*>(src + 32 * s);
   }
-  if constexpr (BND) {
+  if constexpr (BND && !CND) {
 #pragma unroll
     for (int g = 0; g < PG; ++g) {
       const int64_t p = pbase + g * 16 + pl;
       oldv[g] = aux.acl ? aux.acl[p < n ? p : n - 1] : (aux.a_prev ? aux.a_prev[rowv[g]] : assign[rowv[g]]);
+    }
+  }
+  // CND: c_acl in the points' k layout (lane: dims 32 s + 8 lg .. + 8), the list's first
+  // distance of every chunk (lane j: chunk j), the list itself (ids -> LDS)
+  uint4 ca[CND ? KS : 1];
+  float thrv = __builtin_inff(), hna = 0.f;
+  // DRIFT: entries p = KH tid + j of acl's list (ids, 0.5|c|^2, distance to c_acl, shift)
+  // and every point's l from the last iteration
+  int nbv[KH];
+  float hv[KH], ndv[KH], dnv[KH], lold[DRIFT ? PG : 1];
+  if constexpr (CND) {
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) ca[s2] = *reinterpret_cast<const uint4*>(Cq + (int64_t)acl * DP + 32 * s2 + 8 * lg);
+    if (lane < nchunk) thrv = aux.nd[(int64_t)acl * kpad + lane * CH];
+    hna = hn[acl];
+    if constexpr (DRIFT) {
+      static_assert(KH == 4, "DRIFT: four consecutive list entries per thread");
+      const bool in = tid * KH < kpad;
+      const int64_t o = (int64_t)acl * kpad + tid * KH;
+      const float inf = __builtin_inff();
+      const int4 i4 = in ? *reinterpret_cast<const int4*>(aux.nb + o) : make_int4(0, 0, 0, 0);
+      const float4 h4v = in ? *reinterpret_cast<const float4*>(aux.hnb + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 n4 = in ? *reinterpret_cast<const float4*>(aux.ndb + o) : make_float4(inf, inf, inf, inf);
+      const float4 d4 = in ? *reinterpret_cast<const float4*>(aux.dnb + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+      nbv[0] = i4.x; nbv[1] = i4.y; nbv[2] = i4.z; nbv[3] = i4.w;
+      hv[0] = h4v.x; hv[1] = h4v.y; hv[2] = h4v.z; hv[3] = h4v.w;
+      ndv[0] = n4.x; ndv[1] = n4.y; ndv[2] = n4.z; ndv[3] = n4.w;
+      dnv[0] = d4.x; dnv[1] = d4.y; dnv[2] = d4.z; dnv[3] = d4.w;
+      const float* ulf = reinterpret_cast<const float*>(aux.ul);
+#pragma unroll
+      for (int g = 0; g < PG; ++g) lold[g] = ulf[2 * (int64_t)rowv[g] + 1];
+    } else {
+      for (int i = tid; i < kpad; i += NT) s_nbl[i] = (uint16_t)aux.nb[(int64_t)acl * kpad + i];
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1818,15 +1886,18 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
 #pragma unroll
       for (int g = 0; g < PG; ++g) {
         s_row[wid][g * 16 + pl] = rowv[g];
-        s_old[wid][g * 16 + pl] = oldv[g];
+        if constexpr (!CND) s_old[wid][g * 16 + pl] = oldv[g];
       }
     }
   }
   float mx = 0.f;
+  float ua[CND ? PG : 1];
+  float um = 0.f;
+  float tv = __builtin_inff();                 // DRIFT: min over the tile rows of l - ua
 #pragma unroll
   for (int g = 0; g < PG; ++g) {
     // |x|^2 by v_dot2c_f32_bf16 (two bf16 products per instruction, f32 accumulate)
-    float q = 0.f;
+    float q = 0.f, dt = 0.f;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const uint32_t w[4] = {bf[g][s].x, bf[g][s].y, bf[g][s].z, bf[g][s].w};
@@ -1835,14 +1906,46 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
         const bf16x2 h = __builtin_bit_cast(bf16x2, w[j]);
         q = __builtin_amdgcn_fdot2_f32_bf16(h, h, q, false);
       }
+      if constexpr (CND) {
+        const uint32_t cw[4] = {ca[s].x, ca[s].y, ca[s].z, ca[s].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          dt = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, w[j]), __builtin_bit_cast(bf16x2, cw[j]),
+                                               dt, false);
+      }
     }
     q += __shfl_xor(q, 16, 64);
     q += __shfl_xor(q, 32, 64);
     if (lg == 0) s_x2[wid][g * 16 + pl] = q;
     mx = fmaxf(mx, 0.5f * q);
+    if constexpr (CND) {
+      dt += __shfl_xor(dt, 16, 64);
+      dt += __shfl_xor(dt, 32, 64);
+      // |x - c_acl|^2 = |x|^2 - 2 x.c + 2 hn (f32 error far below tol: the K2 slack)
+      const float dist = fmaxf(q - 2.f * dt + 2.f * hna, 0.f);
+      ua[g] = km_up1(sqrtf(km_up1(dist + tol)));
+      if (pbase + g * 16 + pl < n) {
+        um = fmaxf(um, ua[g]);
+        if constexpr (DRIFT) tv = fminf(tv, km_dn1(lold[g] - ua[g]));
+      }
+      if (lg == 0) {
+        s_ua[wid][g * 16 + pl] = ua[g];
+        if constexpr (DRIFT) s_lold[wid][g * 16 + pl] = lold[g];
+      }
+    }
   }
   for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
   if (lane == 0) s_m[wid] = mx;
+  if constexpr (CND) {
+    for (int off = 32; off >= 1; off >>= 1) {
+      um = fmaxf(um, __shfl_xor(um, off));
+      if constexpr (DRIFT) tv = fminf(tv, __shfl_xor(tv, off));
+    }
+    if (lane == 0) {
+      s_ur[wid] = um;
+      if constexpr (DRIFT) s_tau[wid] = tv;
+    }
+  }
 
   // ---- chunk DMA (the 32x32 form's image: slot (row, jj) holds piece jj ^ (row & SWZ));
   // the global address is an SGPR base (the chunk) + a loop-invariant VGPR offset, the
@@ -1854,15 +1957,24 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   const uint32_t src_off = (uint32_t)((tid / NJ) * DP + ((tid % NJ) ^ ((tid / NJ) & SWZ)) * 8) * 2u;
   const uint32_t lds_w = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)(km_lds_void*)s_c + (uint32_t)(wid * 64 * 16));
+  // CND: chunk row r of the stream is centre s_nbl[ch * CH + r] (L2-resident Cq), same
+  // swizzled piece (the row & SWZ term does not depend on the round g)
+  const uint32_t pz = (uint32_t)(((tid % NJ) ^ ((tid / NJ) & SWZ)) * 8) * 2u;
   auto issue_to = [&](int ch, int buf) {
     const uint16_t* base = Cq + (int64_t)ch * CH * DP;
     const uint32_t dst = lds_w + (uint32_t)((buf * CHP) * 16);
 #pragma unroll
     for (int g = 0; g < GPT; ++g) {
       const uint32_t m0v = dst + (uint32_t)(g * NT * 16);
-      const uint16_t* bg = base + g * (NT / NJ) * DP;
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
-                   :: "s"(m0v), "v"(src_off), "s"(bg) : "memory");
+      if constexpr (CND) {
+        const uint32_t off = (uint32_t)s_nbl[ch * CH + g * (NT / NJ) + tid / NJ] * (uint32_t)(DP * 2) + pz;
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+                     :: "s"(m0v), "v"(off), "s"(Cq) : "memory");
+      } else {
+        const uint16_t* bg = base + g * (NT / NJ) * DP;
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+                     :: "s"(m0v), "v"(src_off), "s"(bg) : "memory");
+      }
     }
   };
   auto issue = [&](int ch) { issue_to(ch, ch % NBUF); };
@@ -1875,7 +1987,87 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   // acc = -(0.5|x - c|^2 + M - 0.5|x|^2) < 0, and for negative floats the SIGNED integer
   // order of the bits is the reverse of the value order, so the smallest key is the
   // largest acc = the nearest centre (padding centres, -1e30, have the largest keys)
-  for (int c = tid; c < kpad; c += NT) s_hn16[c] = -(hn[c] + M);
+  int nc = nchunk;                    // chunks streamed (CND: the list prefix within R)
+  float nd_first = __builtin_inff();  // CND: first distance of a pruned centre to c_acl
+  float dmp = -__builtin_inff();      // DRIFT: largest shift of a drift-pruned centre
+  if constexpr (DRIFT) {
+    float R = s_ur[0], tau = s_tau[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      R = fmaxf(R, s_ur[w]);
+      tau = fminf(tau, s_tau[w]);
+    }
+    R = km_up1(2.f * R);
+    // a dropped centre costs the rows up to tau of their l (the next filter tests
+    // l - maxd): the threshold is capped so only the slow centres are dropped
+    if (aux.tau_cap != nullptr) tau = fminf(tau, *aux.tau_cap);
+    int c = 0;
+    float dm = -__builtin_inff(), nf = __builtin_inff();
+    bool keep[KH];
+#pragma unroll
+    for (int j = 0; j < KH; ++j) {
+      const int p = tid * KH + j;
+      const bool tail = p >= CH && p < kpad;
+      const bool ball = !aux.drift_ball || ndv[j] <= R;
+      keep[j] = tail && ball && dnv[j] >= tau;
+      c += keep[j] ? 1 : 0;
+      if (tail && !keep[j]) {
+        if (dnv[j] < tau) dm = fmaxf(dm, dnv[j]);   // slow: bounds l through l - dmp
+        else nf = fminf(nf, ndv[j]);               // fast, outside the ball: nd_first - ua
+      }
+    }
+    int x = c;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+      dm = fmaxf(dm, __shfl_xor(dm, off));
+      nf = fminf(nf, __shfl_xor(nf, off));
+    }
+    if (lane == 63) s_kc[wid] = x;
+    if (lane == 0) { s_kd[wid] = dm; s_kf[wid] = nf; }
+    __syncthreads();
+    int pre = x - c, kept = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      if (w < wid) pre += s_kc[w];
+      kept += s_kc[w];
+      dmp = fmaxf(dmp, s_kd[w]);
+      nd_first = fminf(nd_first, s_kf[w]);
+    }
+    nc = 1 + (kept + CH - 1) / CH;
+    // stream order: chunk 0 as listed, the kept entries compacted behind it, then padding
+    // up to whole chunks (acl with 0.5|c|^2 = 1e30: never the nearest)
+#pragma unroll
+    for (int j = 0; j < KH; ++j) {
+      const int p = tid * KH + j;
+      int q = -1;
+      if (p < CH) q = p;
+      else if (keep[j]) q = CH + pre++;
+      if (q >= 0) {
+        s_nbl[q] = (uint16_t)nbv[j];
+        s_hn16[q] = -(hv[j] + M);
+      }
+    }
+    for (int q = CH + kept + tid; q < nc * CH; q += NT) {
+      s_nbl[q] = (uint16_t)acl;
+      s_hn16[q] = -(1e30f + M);
+    }
+    __syncthreads();                            // the stream's ids staged for the DMA
+  } else if constexpr (CND) {
+    float R = s_ur[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) R = fmaxf(R, s_ur[w]);
+    R = km_up1(2.f * R);
+    // chunk j >= 1 is needed iff its first (smallest) distance is <= R; chunk 0 always
+    nc = 1 + __popcll(__ballot(lane >= 1 && lane < nchunk && thrv <= R));
+    if (nc < nchunk) nd_first = __shfl(thrv, nc);
+    const float* hb = aux.hnb + (int64_t)acl * kpad;
+    for (int c = tid; c < kpad; c += NT) s_hn16[c] = -(hb[c] + M);
+  } else {
+    for (int c = tid; c < kpad; c += NT) s_hn16[c] = -(hn[c] + M);
+  }
   issue(0);
 
   int bkey[PG], bch[PG], cm[PG];
@@ -1981,9 +2173,9 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   float4 h4, hn4;
   km_wait_vmcnt<0>();
   __syncthreads();                             // chunk 0 landed, s_hn16 written
-  if (nchunk > 1) issue(1);
+  if (nc > 1) issue(1);
   load_frag(s_c, 0, 0, a, h4);
-  for (int ch = 0; ch < nchunk; ++ch) {
+  for (int ch = 0; ch < nc; ++ch) {
     const uint4* img = s_c + (ch % NBUF) * CHP;
     const uint4* img_next = s_c + ((ch + 1) % NBUF) * CHP;
     // sub-tile 0 under the previous chunk's sub-tile 7 argmin, then the merge of that chunk
@@ -2000,7 +2192,7 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
       h4 = hn4;
       // (branch-free: the last chunk re-reads its own first fragments, unused)
       if (sub + 1 < NSUB) load_frag(img, ch, sub + 1, an, hn4);
-      else load_frag(ch + 1 < nchunk ? img_next : img, ch + 1 < nchunk ? ch + 1 : ch, 0, an, hn4);
+      else load_frag(ch + 1 < nc ? img_next : img, ch + 1 < nc ? ch + 1 : ch, 0, an, hn4);
       mfma_sub(acc[sub & 1], a, h4);
       argmin_sub(acc[(sub - 1) & 1], sub - 1);
       pin();
@@ -2015,7 +2207,7 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
           // end the last chunk is loaded again into buffer (ch + 2) % 2, which no wave reads
           // again (chunk ch's, all of whose reads precede the barrier) or which already
           // holds those same bytes (the last chunk's own)
-          const int c2 = ch + 2 < nchunk ? ch + 2 : nchunk - 1;
+          const int c2 = ch + 2 < nc ? ch + 2 : nc - 1;
           issue_to(c2, (ch + 2) % NBUF);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -2028,7 +2220,7 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
   km_wait_vmcnt<0>();                          // the redundant last DMAs landed
   // the last chunk's sub-tile 7 and merge
   argmin_sub(acc[1], 7);
-  merge_chunk(nchunk - 1);
+  merge_chunk(nc - 1);
 
   // ---- merge the 4 lane groups of each point, write the outputs
   double my_sse = 0.0;
@@ -2039,6 +2231,7 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
     if constexpr (BND) v2 = -__int_as_float(bkey2[g] & kmask);
     const int ix = bkey[g] & 31;
     int id = bch[g] * CH + (ix >> 2) * 16 + 4 * lg + (ix & 3);
+    if constexpr (CND) id = s_nbl[id];           // list position -> centre id
 #pragma unroll
     for (int o = 16; o <= 32; o <<= 1) {
       const float pv = __shfl_xor(v, o, 64);
@@ -2057,11 +2250,16 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
       if (lg == 0 && p < n) {
         const float x2 = s_x2[wid][g * 16 + pl];
         row = s_row[wid][g * 16 + pl];
-        old_c = s_old[wid][g * 16 + pl];
+        if constexpr (CND) old_c = acl;
+        else old_c = s_old[wid][g * 16 + pl];
         const float dist = fmaxf(2.f * (v - M) + x2, 0.f);
         const float dist2 = fmaxf(2.f * (v2 - M) + x2, 0.f);
         // u rounded up, l rounded down (the keys are truncated towards smaller distances)
-        const float lo2 = km_dn1(sqrtf(fmaxf(km_dn1(dist2 - tol), 0.f)));
+        float lo2 = km_dn1(sqrtf(fmaxf(km_dn1(dist2 - tol), 0.f)));
+        // CND: every pruned centre is >= nd_first - |x - c_acl| from x
+        if constexpr (CND) lo2 = fminf(lo2, km_dn1(nd_first - s_ua[wid][g * 16 + pl]));
+        // DRIFT: every drift-pruned centre is >= l - dmp from x (dmp = -inf: none pruned)
+        if constexpr (DRIFT) lo2 = fminf(lo2, km_dn1(s_lold[wid][g * 16 + pl] - dmp));
         aux.ul[row] = make_float2(km_up1(sqrtf(km_up1(dist + tol))), fmaxf(lo2, 0.f));
         chg = id != old_c;
         if (chg) assign[row] = id;
@@ -2075,9 +2273,9 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
         base = __shfl(base, 0);
         if (chg) {
           const int slot = base + __popcll(cmk & ((1ull << lane) - 1ull));
-          s_mv[0][slot] = row;
-          s_mv[1][slot] = id;
-          s_mv[2][slot] = old_c;
+          s_mv[slot] = row;
+          s_mvn[slot] = (uint16_t)id;
+          s_mvo[slot] = (uint16_t)old_c;
         }
       }
     } else {
@@ -2101,10 +2299,10 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
       const long long b = (long long)s_mvbase;
       for (int j = tid; j < c; j += NT)
         if (b + j < aux.cap) {
-          aux.changed[b + j] = s_mv[0][j];
+          aux.changed[b + j] = s_mv[j];
           if (aux.chg_new) {
-            aux.chg_new[b + j] = s_mv[1][j];
-            aux.chg_old[b + j] = s_mv[2][j];
+            aux.chg_new[b + j] = s_mvn[j];
+            aux.chg_old[b + j] = s_mvo[j];
           }
         }
     }
@@ -2127,14 +2325,17 @@ kmeans_assign16_kernel(const uint16_t* __restrict__ X, int64_t n, int64_t ldx,
 // and runs two blocks per CU: it takes kpad <= 3456 (BND, with the per-point row /
 // previous-cluster tables and the moved-row list: <= 2304); larger k goes to the
 // pipelined form
-static bool assign16_fits(int kpad, bool bnd = false) {
-  // static: 2 chunk buffers (64 KB) + |x|^2 of the 384 points (+ BND: 5 x 384 ints) + small
-  return kpad % 128 == 0 &&
-         2 * 128 * 128 * 2 + (bnd ? 6 : 1) * 4 * 6 * 16 * 4 + (size_t)kpad * sizeof(float) + 1024 <=
+static bool assign16_fits(int kpad, bool bnd = false, bool cnd = false) {
+  // static: 2 chunk buffers (64 KB) + |x|^2 of the 384 points (+ BND: 5 x 384 words; CND:
+  // 6 x 384 words + the 1024-entry u16 list) + small
+  // (CND: the compiler's static size is 76944 B with DRIFT; 256 B of small arrays)
+  return kpad % 128 == 0 && (!cnd || kpad <= 1024) &&
+         2 * 128 * 128 * 2 + (bnd ? (cnd ? 6 : 5) : 1) * 4 * 6 * 16 * 4 + (cnd ? 2048 + 256 : 1024) +
+                 (size_t)kpad * sizeof(float) <=
              80 * 1024;
 }
 
-template <bool BND>
+template <bool BND, bool CND = false, bool DRIFT = false>
 static hipError_t launch_assign16(const void* X, int64_t n, int64_t ldx, const void* Cq,
                                   const float* hn, int kpad, int* assign, float* mind, double* sse,
                                   int sse_mask, float* xh, unsigned* xmax, hipStream_t st,
@@ -2142,7 +2343,10 @@ static hipError_t launch_assign16(const void* X, int64_t n, int64_t ldx, const v
   // (one 8-wave block per CU -- half the centre-chunk traffic per point -- measured 2 %
   // slower: 20.5-20.7 vs 20.1-20.2 ms on one box, profiles/round5/r5_22)
   constexpr int NW = 4, PG = 6, MINB = 2;
-  if (!assign16_fits(kpad, BND)) return hipErrorInvalidValue;
+  if (!assign16_fits(kpad, BND, CND)) return hipErrorInvalidValue;
+  if (CND && (aux.tiles == nullptr || aux.n_tiles == nullptr || aux.nb == nullptr || aux.hnb == nullptr ||
+              aux.nd == nullptr))
+    return hipErrorInvalidValue;
   if (BND && (idx == nullptr || aux.mcount == nullptr || aux.tol == nullptr || aux.ul == nullptr ||
               aux.changed == nullptr || aux.n_changed == nullptr ||
               (aux.chg_new == nullptr) != (aux.chg_old == nullptr)))
@@ -2152,7 +2356,7 @@ static hipError_t launch_assign16(const void* X, int64_t n, int64_t ldx, const v
   const int64_t grid = cdiv(n, (int64_t)NW * PG * 16);
   if (grid == 0) return hipSuccess;
   if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
-  auto kfn = kmeans_assign16_kernel<NW, PG, MINB, BND>;
+  auto kfn = kmeans_assign16_kernel<NW, PG, MINB, BND, CND, DRIFT>;
   static size_t attr_set = 0;
   if (dyn > attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2366,6 +2570,16 @@ hipError_t dalgo_kmeans_assign_idx(const void* X, int64_t m, int64_t ldx, int DP
       aux.nb = cand->nb; aux.nd = cand->nd; aux.extend = cand->extend;
       aux.ndb = cand->ndb; aux.dnb = cand->dnb; aux.tau_cap = cand->tau_cap;
       aux.drift_ball = cand->extend;   // (no extension chunks in the drift form)
+      if (cand->tile16) {
+        // the 16x16x32 tiling with the list prefix / the drift-compacted list (tiles of
+        // <= 384 rows)
+        if (DP != 128 || idx == nullptr) return hipErrorInvalidValue;
+        if (cand->ndb != nullptr)
+          return launch_assign16<true, true, true>(X, cand->max_tiles * 384, ldx, Cq, hn, kpad, assign, nullptr,
+                                                   sse, sse_mask, nullptr, nullptr, st, idx, aux);
+        return launch_assign16<true, true>(X, cand->max_tiles * 384, ldx, Cq, hn, kpad, assign, nullptr, sse,
+                                           sse_mask, nullptr, nullptr, st, idx, aux);
+      }
       if (cand->ndb != nullptr) {   // drift-aware candidate lists
         if (DP == 128)
           return launch_assign_pipe<128, 4, 2, 4, 2, 2, false, true, true, true, true>(

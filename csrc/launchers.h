@@ -57,6 +57,8 @@ struct DalgoKmCand {
   const float* ndb;                   // nullable: drift-aware lists (nd aligned with nb)
   const float* dnb;                   //           and each entry's centre shift
   const float* tau_cap;               // nullable (device): cap of the drift threshold
+  int tile16;                         // tiles of <= 384 rows for the 16x16x32 form (CND)
+  int64_t max_tiles;                  // capacity of the tile table (its launch grid)
 };
 
 extern "C" {

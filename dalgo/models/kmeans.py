@@ -183,7 +183,11 @@ class KMeans:
                                changed=self._changed, n_changed=self._n_changed)
         # candidate pruning (Exponion-style at tile granularity): the active rows sorted by
         # cluster, every tile's centre stream cut to a prefix of its centre's neighbour list
-        self._cand = (K.CandWorkspace(self.dev, n, k, self.cen.Cq.shape[0], self.DP, drift=self.cfg.drift)
+        # (DALGO_KM_CAND16=1: the 16x16x32 candidate form -- 384-row tiles)
+        c16 = K.cand16() and self.DP == 128
+        self._cand = (K.CandWorkspace(self.dev, n, k, self.cen.Cq.shape[0], self.DP,
+                                      drift=self.cfg.drift,
+                                      tile=K.CAND16_TILE if c16 else K.CAND_TILE)
                       if self.cfg.candidates and self.cen.Cq.shape[0] <= 1024 else None)
         if self._cand is not None:
             # the candidate K2 takes the previous cluster from its tile and writes the moved

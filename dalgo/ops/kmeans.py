@@ -237,6 +237,14 @@ def filter_rows(assign: torch.Tensor, ul: torch.Tensor, delta: torch.Tensor, s: 
 
 # ------------------------------------------------- candidate-pruned K2 (filtered iterations)
 CAND_TILE = 256          # rows per K2 block tile (4 waves x 2 point tiles x 32)
+CAND16_TILE = 384        # ... of the 16x16x32 candidate form (4 waves x 6 groups x 16)
+
+
+def cand16() -> bool:
+    """DALGO_KM_CAND16=1: the candidate-pruned K2 on the 16x16x32 tiling (plain neighbour
+    lists, tiles of CAND16_TILE rows) instead of the 32x32x16 pipelined form."""
+    import os
+    return os.environ.get("DALGO_KM_CAND16", "0") == "1"
 
 
 class CandWorkspace:
@@ -244,12 +252,14 @@ class CandWorkspace:
     padded, <= 1024): per-centre neighbour lists (nd / nb / hnb, k * kpad each), the
     cluster-sorted active rows and the tile table."""
 
-    def __init__(self, device, n: int, k: int, kpad: int, DP: int, drift: bool = False):
+    def __init__(self, device, n: int, k: int, kpad: int, DP: int, drift: bool = False,
+                 tile: int = CAND_TILE):
         i32 = dict(dtype=torch.int32, device=device)
         i64 = dict(dtype=torch.int64, device=device)
         f32 = dict(dtype=torch.float32, device=device)
         n = max(1, int(n))
         self.k, self.kpad = int(k), int(kpad)
+        self.tile = int(tile)                            # rows per tile (<=)
         self.nd = torch.empty(k * kpad, **f32)
         self.nb = torch.empty(k * kpad, **i32)
         self.hnb = torch.empty(k * kpad, **f32)
@@ -266,7 +276,7 @@ class CandWorkspace:
         self.block_counts = torch.empty(bmax * self.nkeys, **i32)
         self.cstart = torch.empty(self.nkeys + 1, **i64)
         self.seg_start = torch.empty(self.nkeys + 1, **i64)
-        tiles = (n + CAND_TILE - 1) // CAND_TILE + self.nkeys
+        tiles = (n + self.tile - 1) // self.tile + self.nkeys
         self.tiles = torch.empty(tiles * 4, **i32)      # (cluster, first, end, -) per tile
         self.n_tiles = torch.zeros(1, **i64)
 
@@ -317,7 +327,7 @@ def sort_active(idx: torch.Tensor, n_active: torch.Tensor, ws: CandWorkspace):
     cluster runs -> ws.cstart, tiles of CAND_TILE rows of one cluster -> ws.tiles /
     n_tiles (4 launches, device counts only)."""
     _ext.ops().kmeans_sort_active(ws.acl, idx, n_active, ws.nkeys, CHUNK_ROWS, ws.block_counts,
-                                  ws.cstart, ws.seg_start, ws.rows, CAND_TILE, ws.tiles,
+                                  ws.cstart, ws.seg_start, ws.rows, ws.tile, ws.tiles,
                                   ws.n_tiles)
 
 
@@ -357,7 +367,8 @@ def assign_rows(X: torch.Tensor, cen: Centers, idx: torch.Tensor | None, m: int,
                                  cand.cand() if cand is not None else [], None, None, None, None,
                                  post["m_dev"], post.get("a_prev"), post["tol"], post["ul"],
                                  post["changed"], post["n_changed"],
-                                 post.get("chg_new"), post.get("chg_old"), int(bool(extend)),
+                                 post.get("chg_new"), post.get("chg_old"),
+                                 int(bool(extend)) | (2 if cand is not None and cand.tile == CAND16_TILE else 0),
                                  post.get("acl"))
 
 

@@ -985,12 +985,13 @@ def test_kmeans_sort_active(cuda):
     assert int((th - tl).sum()) == m
 
 
-@pytest.mark.parametrize("d", [64, 128])
-def test_kmeans_assign_rows_candidates(cuda, d):
+@pytest.mark.parametrize("d,tile16", [(64, False), (128, False), (128, True)])
+def test_kmeans_assign_rows_candidates(cuda, d, tile16):
     """Candidate-pruned filtered K2 (tiles of one cluster stream only the centres within
     2 max(u) + slack of their centre): same assignment as the full pass on the active
     rows (mismatches only at kernel-rounding near-ties), the pruned centres bound l from
-    below, the changed rows are collected exactly."""
+    below, the changed rows are collected exactly. tile16: the 16x16x32 form (384-row
+    tiles, kmeans_assign16_kernel CND)."""
     torch.manual_seed(12)
     from dalgo.data.synthetic import blobs
     n, k = 120_000, 512
@@ -1007,7 +1008,7 @@ def test_kmeans_assign_rows_candidates(cuda, d):
     tol = torch.zeros(1, device=cuda)
     K.bounds_init(mind, mind2, xmax, n, torch.empty((n, 2), device=cuda), tol)
     kpad, DP = cen.Cq.shape
-    ws = K.CandWorkspace(cuda, n, k, kpad, DP)
+    ws = K.CandWorkspace(cuda, n, k, kpad, DP, tile=K.CAND16_TILE if tile16 else K.CAND_TILE)
     K.centre_nbrs(cen, cen.Cq[:k].clone(), torch.empty(k, device=cuda), torch.empty(k, device=cuda), ws)
     # active rows: a random subset; a_prev = the truth with a third of them perturbed, u =
     # a valid upper bound of the distance to c_{a_prev}
@@ -1087,6 +1088,28 @@ def test_kmeans_candidates_match_plain(cuda):
             _kmeans_step_oracle(c)
 
 
+def test_kmeans_cand16_matches_plain(cuda, monkeypatch):
+    """DALGO_KM_CAND16=1 (the candidate-pruned K2 on the 16x16x32 tiling): every filtered
+    step equals brute force from the same state, and the SSE trajectory equals the plain
+    Lloyd run's."""
+    from dalgo.data.synthetic import blobs
+    from dalgo.models.kmeans import KMeans, KMeansConfig
+    n, d, k = 300_000, 128, 1000
+    X = blobs(n, d, k, device=cuda, dtype=torch.bfloat16, seed=11)
+    plain = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5, bound_filter=False), X, 0, n)
+    plain.fit()
+    monkeypatch.setenv("DALGO_KM_CAND16", "1")
+    for kw in ({}, dict(dense="never"), dict(dense="never", drift=False)):
+        km = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5, **kw), X, 0, n)
+        assert km._cand is not None and km._cand.tile == K.CAND16_TILE
+        assert (km._cand.ndb is None) == (kw.get("drift") is False)
+        km.fit()
+        assert np.allclose(km.history.sse, plain.history.sse, rtol=2e-4)
+        c = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5, **kw), X, 0, n)
+        for _ in range(7):
+            _kmeans_step_oracle(c)
+
+
 def test_kmeans_dense_choice_on_device(cuda):
     """Filtered iterations pick the dense top-2 K2 or the pruned one on the device: right
     after the full pass always dense, later dense iff >= DENSE_FRACTION of the rows are
@@ -1118,8 +1141,8 @@ def test_kmeans_dense_choice_on_device(cuda):
             assert any(dense[i] == 0 for i in range(2, len(act))), (act, dense)
 
 
-@pytest.mark.parametrize("d", [64, 128])
-def test_kmeans_assign_rows_drift_candidates(cuda, d):
+@pytest.mark.parametrize("d,tile16", [(64, False), (128, False), (128, True)])
+def test_kmeans_assign_rows_drift_candidates(cuda, d, tile16):
     """Drift-aware candidate lists: with valid lower bounds l (below the true second-best
     distance) and small centre shifts most of every list is dropped past the first chunk;
     the assignment still equals the full pass on the active rows (near-ties aside), u / l
@@ -1140,7 +1163,7 @@ def test_kmeans_assign_rows_drift_candidates(cuda, d):
                   torch.zeros(n, device=cuda), xh=torch.zeros(n, device=cuda), xmax=xmax)
     tol = torch.zeros(1, device=cuda)
     K.bounds_init(mind, mind, xmax, n, torch.empty((n, 2), device=cuda), tol)
-    ws = K.CandWorkspace(cuda, n, k, kpad, DP, drift=True)
+    ws = K.CandWorkspace(cuda, n, k, kpad, DP, drift=True, tile=K.CAND16_TILE if tile16 else K.CAND_TILE)
     delta = torch.empty(k, device=cuda)
     K.centre_nbrs(cen, prevc.Cq[:k].clone(), delta, torch.empty(k, device=cuda), ws)
     # previous assignment / bounds vs the PREVIOUS centres: a_prev = their nearest, l = a
