@@ -241,10 +241,13 @@ CAND16_TILE = 384        # ... of the 16x16x32 candidate form (4 waves x 6 group
 
 
 def cand16() -> bool:
-    """DALGO_KM_CAND16=1: the candidate-pruned K2 on the 16x16x32 tiling (plain neighbour
-    lists, tiles of CAND16_TILE rows) instead of the 32x32x16 pipelined form."""
+    """The candidate-pruned K2 on the 16x16x32 tiling (kmeans_assign16_kernel CND: tiles of
+    CAND16_TILE rows, plain or drift-compacted neighbour lists) instead of the 32x32x16
+    pipelined form (DALGO_KM_CAND16=0). 100M x 128, k = 1024, same active rows: iterations
+    3-5 of the overlapping-blob job 18.8 / 11.1 / 9.6 -> 16.8 / 10.0 / 8.8 ms, job 95.6 ->
+    92.0 ms; separated 75.7 -> 73.8 ms (profiles/round6/r6_53)."""
     import os
-    return os.environ.get("DALGO_KM_CAND16", "0") == "1"
+    return os.environ.get("DALGO_KM_CAND16", "1") == "1"
 
 
 class CandWorkspace:
