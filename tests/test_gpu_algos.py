@@ -1088,20 +1088,22 @@ def test_kmeans_candidates_match_plain(cuda):
             _kmeans_step_oracle(c)
 
 
-def test_kmeans_cand16_matches_plain(cuda, monkeypatch):
-    """DALGO_KM_CAND16=1 (the candidate-pruned K2 on the 16x16x32 tiling): every filtered
-    step equals brute force from the same state, and the SSE trajectory equals the plain
-    Lloyd run's."""
+@pytest.mark.parametrize("c16", ["1", "0"])
+def test_kmeans_cand16_matches_plain(cuda, monkeypatch, c16):
+    """Both candidate-pruned K2 forms (DALGO_KM_CAND16=1: the 16x16x32 tiling, the default;
+    0: the 32x32x16 pipelined form): every filtered step equals brute force from the same
+    state, and the SSE trajectory equals the plain Lloyd run's."""
     from dalgo.data.synthetic import blobs
     from dalgo.models.kmeans import KMeans, KMeansConfig
     n, d, k = 300_000, 128, 1000
     X = blobs(n, d, k, device=cuda, dtype=torch.bfloat16, seed=11)
     plain = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5, bound_filter=False), X, 0, n)
     plain.fit()
-    monkeypatch.setenv("DALGO_KM_CAND16", "1")
+    monkeypatch.setenv("DALGO_KM_CAND16", c16)
     for kw in ({}, dict(dense="never"), dict(dense="never", drift=False)):
         km = KMeans(KMeansConfig(k=k, n_iterations=7, seed=5, **kw), X, 0, n)
-        assert km._cand is not None and km._cand.tile == K.CAND16_TILE
+        assert km._cand is not None
+        assert km._cand.tile == (K.CAND16_TILE if c16 == "1" else K.CAND_TILE)
         assert (km._cand.ndb is None) == (kw.get("drift") is False)
         km.fit()
         assert np.allclose(km.history.sse, plain.history.sse, rtol=2e-4)
