@@ -316,7 +316,7 @@ def run_lr(a, rt, data, layout, algo: str, steps: int, warmup: int, witness_step
         fell_back = True
     xg = getattr(getattr(model, "bucket", None), "xg", None)
     launch = "persistent" if model._persistent() else (
-        "hipgraph-replay" if model._graph_ok() else (
+        "graph" if model._graph_ok() else (   # (the calibration's names: hipGraph replay = "graph")
             "one-kernel" if model._one_kernel() else "per-step"))
     allreduce = "xgmi-oneshot (K11)" if xg is not None else (
         f"{rt.backend}" if W > 1 else "none (1 rank)")
