@@ -196,8 +196,11 @@ def test_bench_eight_ranks_on_one_gpu(cuda):
     """World size 8 (the driver's largest N), 8 ranks sharing cuda:0: sharding of the
     10M-row global set into 1.25M-row shards, the 8-peer K11 exchange (or gloo if the
     start-up race prefers it), rank-0 JSON with the whole-job aggregate."""
+    # (secondaries off: 8 spinning processes on one GPU run a step in ~90 ms, so the LR
+    # witnesses' 1500-3000 training rounds alone would take minutes, profiles/round6/r6_61;
+    # test_bench_secondary_two_ranks covers BASELINE configs #3-#5 on several ranks)
     out = _torchrun(["bench.py", "--gpus", "8", "--backend", "gloo", "--rows", "400000",
-                     "--steps", "5", "--warmup", "2"], n=8, env_extra=SPIN)
+                     "--steps", "5", "--warmup", "2", "--secondary", "off"], n=8, env_extra=SPIN)
     d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
     assert d["n_gpus"] == 8 and d["steps"] == 5 and d["config"]["parallelism"] == "dp8"
     assert d["config"]["allreduce"] in ("xgmi-oneshot (K11)", "gloo")
