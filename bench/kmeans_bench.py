@@ -48,7 +48,7 @@ def main():
     ap.add_argument("--noise", type=float, default=1.0,
                     help="blob noise (1 = well separated; 4 = overlapping clusters, the hard case "
                          "for the bound filters)")
-    ap.add_argument("--dense", default="auto", choices=["auto", "always", "never"],
+    ap.add_argument("--dense", default="auto", choices=["auto", "always", "never", "device"],
                     help="filtered iterations on the dense top-2 K2 (auto: right after the full pass)")
     ap.add_argument("--no-drift", action="store_true",
                     help="candidate lists without the centre-shift pruning")
