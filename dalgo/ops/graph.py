@@ -751,7 +751,10 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     nblk_k = max(nblk, 1)
     wu_e = max(1 << 15, E // 4096)
     n4 = (nent + 3) // 4 * 4 + PB_DUMMY
-    dloc = torch.zeros(n4, dtype=torch.int16, device=dev)
+    # every entry's bin-major place is written once below (a bijection onto [0, nent)):
+    # only the padding is cleared
+    dloc = torch.empty(n4, dtype=torch.int16, device=dev)
+    dloc[nent:].zero_()
     assert nent < (1 << 31) - 8
     if nblk_k * nbins <= CELL_CAP:
         # runs = the non-empty cells of the (block, bin) matrix (graph_build.hip gb_cell_*)
@@ -871,9 +874,13 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     it = lambda x: torch.tensor(x, **i32)
     c32 = lambda x: x.to(torch.int32).contiguous()
     splits = sorted({int(x) for x in seg_start if x > 0})
+    # entry values: phase 1 writes every entry [0, nent) before phase 2 reads it, so only
+    # the padding is cleared (a full 1.9 GB fill was 0.26 ms of the scale-26 build)
+    val = torch.empty(n4, dtype=torch.float32, device=dev)
+    val[nent:].zero_()
     lay = BlockedLayout(srcl, tile_e.contiguous(), c32(tile_ent), c32(tile_run), c32(chunk_tile),
                         c32(wu_tile), c32(wu_chunk), c32(slo), c32(ns), c32(chunk_run), c32(run_delta),
-                        torch.zeros(n4, dtype=torch.float32, device=dev), dloc,
+                        val, dloc,
                         c32(wb), wl.to(device=dev).contiguous(), c32(slab_h),
                         torch.zeros(max(nslab, 1) * bin_width, **i64),
                         c32(sp_bin), c32(sp_first), c32(sp_cnt), bin_width, nl, nch, nent, n_src,
