@@ -139,8 +139,20 @@ def persistent_used() -> bool:
 
 
 def reset_persistent_error():
+    """Clear the error words AND re-arm every device counter a failed launch can leave
+    behind: blocks that gave up on a step-release wait return without taking their
+    ticket, pool chunks or hand-off counts, so a later launch would run its tail early
+    (stale ticket) or skip pooled rows (stale pool counter). The step-release epoch
+    restarts at 0 with its host mirror. Call after the failed launch has drained (the
+    collective check synchronises) and before the next gradient launch."""
     for ws in _ws_cache.values():
         ws.perr.zero_()
+        ws.ticket.zero_()
+        ws.pool.zero_()
+        ws.cnt1.zero_()
+        ws.cnt2.zero_()
+        ws.epoch.zero_()
+        ws.epochs = 0
 
 
 def check_persistent():

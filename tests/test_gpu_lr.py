@@ -254,3 +254,35 @@ def test_lr_grad_row_pool_plain_launch(cuda, n, monkeypatch):
         assert float(C1.item()) == float(C0.item())
         assert torch.allclose(G1, G0, rtol=1e-4, atol=1e-3)
     L.check_persistent()
+
+
+@pytest.mark.gpu
+def test_lr_reset_rearms_stale_counters(cuda, monkeypatch):
+    """After a failed launch (simulated: ticket, pool and hand-off counters left part-way),
+    reset_persistent_error re-arms them: the next pooled plain launch gives the same
+    selected-row count and gradient as a launch without the pool."""
+    n = 300_000
+    Xd, yd = _data(n, 1024, torch.bfloat16, seed=17, device=cuda)
+    seg = torch.tensor([0, n], dtype=torch.int64, device=cuda)
+    w = torch.randn(1, 1025, generator=torch.Generator().manual_seed(8)).to(cuda) * 0.05
+    kw = dict(D=1024, frac=0.1, eps=0.0, seed=42)
+    monkeypatch.setattr(L, "POOL_FRAC_ONE", 0.0)
+    G0, C0 = L.lr_grad(Xd, yd, w, seg, step=3, **kw)
+    monkeypatch.setattr(L, "POOL_FRAC_ONE", 0.2)
+    monkeypatch.setattr(L, "POOL_MIN_ROWS", 0)
+    G1, C1 = L.lr_grad(Xd, yd, w, seg, step=3, **kw)      # creates the pooled workspace
+    torch.cuda.synchronize()
+    for ws in L._ws_cache.values():                       # what an aborted launch leaves
+        ws.ticket.fill_(5)
+        ws.pool.fill_(3)
+        ws.epoch.fill_(7)
+        ws.epochs = 9
+    L.reset_persistent_error()
+    for ws in L._ws_cache.values():
+        assert int(ws.ticket.item()) == 0 and int(ws.pool.abs().sum().item()) == 0
+        assert int(ws.epoch.item()) == 0 and ws.epochs == 0
+    G2, C2 = L.lr_grad(Xd, yd, w, seg, step=3, **kw)
+    torch.cuda.synchronize()
+    assert float(C1.item()) == float(C0.item()) == float(C2.item())
+    assert torch.allclose(G2, G0, rtol=1e-4, atol=1e-3)
+    L.check_persistent()
