@@ -521,8 +521,20 @@ pb_combine_kernel(const uint64_t* __restrict__ slab, const int32_t* __restrict__
   if (i < BW && base + i < n_local) {
     const uint64_t* p = slab + (int64_t)split_first[sb] * BW + i;
     const int cnt = split_count[sb];
+    // 8 independent slab loads in flight per thread (one at a time: 86 -> 77 us per
+    // iteration at scale 26, profiles/round6/r6_73; 64 destinations x 4 piece lanes per
+    // block with an LDS sum measured 92 us, and a last-arriving-piece combine inside
+    // pb_accum would leave one CU summing a hot bin's ~100 slabs)
+    uint64_t qa[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int k = 0;
+    for (; k + 8 <= cnt; k += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qa[j] += p[(int64_t)(k + j) * BW];
+    }
+    for (; k < cnt; ++k) qa[0] += p[(int64_t)k * BW];
     uint64_t q = 0;
-    for (int k = 0; k < cnt; ++k) q += p[(int64_t)k * BW];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q += qa[j];
     const int od = o.r != nullptr ? o.outdeg[base + i] : 0;
     const float dang = (o.r != nullptr && o.mode == 1 && o.dang_in) ? o.dang_in[0] : 0.f;
     dl = pb_finish(o, base + i, q, K, od, dang);
