@@ -11,6 +11,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 
 import numpy as np
+import os
+
 import torch
 
 from dalgo.ops import _ext
@@ -273,6 +275,14 @@ def _work_items(bin_cnt: torch.Tensor, bin_lo: torch.Tensor, nent: int, items: i
 SRC_SPAN = 8192          # sources per chunk: the LDS table of pb_gather (csrc/kernels/pr_binned.hip)
 CELL_CAP = 1 << 30       # largest (block, bin) cell matrix of the native build (4 B x 3 per cell)
 PB_DUMMY = 65536         # val / dloc padding after the entries (kPbDummy in pr_binned.hip)
+# phase-2 work items of the native build: a bin with more than nent / PB_ITEMS entries is
+# cut into pieces, each with its own 128 KB u64 slab that pb_combine sums. One rank at
+# scale 26 (4096 bins): 2048 -> 5662 items, 346 split bins, 2.037-2.045 ms per iteration;
+# 1024 -> 1.978-1.989; 768 -> 1.965-1.978 (4531 items, 155 split bins); 512 -> 1.994-1.999
+# (profiles/round6/r6_80). Several ranks keep 2048: a rank holds 1/W of the bins, so fewer
+# pieces would leave its phase 2 with few work items (not measured at W > 1)
+PB_ITEMS = int(os.environ.get("DALGO_PB_ITEMS", "768"))
+PB_ITEMS_MULTI = int(os.environ.get("DALGO_PB_ITEMS_MULTI", "2048"))
 
 
 @dataclass
@@ -598,7 +608,7 @@ def sort_split_bits(nbits: int) -> int:
 
 
 def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: torch.Tensor | None = None,
-                 bin_width: int = 16384, tile: int = 16384, items: int = 2048,
+                 bin_width: int = 16384, tile: int = 16384, items: int | None = None,
                  min_piece: int = 1 << 14, keep_keys: bool = False,
                  packed: torch.Tensor | None = None, packed_src_new: bool = False) -> NativeGraph:
     """``distinct().groupByKey()`` of graph_computation/pagerank.py:41 straight into the
@@ -614,6 +624,8 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     packed_src_new: their sources are already relabelled (:func:`relabel_partition_dst`)."""
     if bin_width not in (8192, 16384):
         raise ValueError("bin_width must be 8192 or 16384")
+    if items is None:
+        items = PB_ITEMS if world == 1 else PB_ITEMS_MULTI
     ops = _ext.ops()
     dev = edges[0][0].device
     N, W = n_vertices, world
