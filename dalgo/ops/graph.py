@@ -283,6 +283,10 @@ PB_DUMMY = 65536         # val / dloc padding after the entries (kPbDummy in pr_
 # pieces would leave its phase 2 with few work items (not measured at W > 1)
 PB_ITEMS = int(os.environ.get("DALGO_PB_ITEMS", "768"))
 PB_ITEMS_MULTI = int(os.environ.get("DALGO_PB_ITEMS_MULTI", "2048"))
+# phase-1 work units of the native build: a source chunk is cut every max(32K, E / PB_UNITS)
+# edges. Scale 26, one rank, 3 runs each: 2048 -> 1.986-1.990 ms per iteration, 4096 ->
+# 1.953-1.967, 8192 -> 2.024-2.027, 16384 -> 2.200-2.208 (profiles/round6/r6_82)
+PB_UNITS = int(os.environ.get("DALGO_PB_UNITS", "4096"))
 
 
 @dataclass
@@ -761,7 +765,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     bshift = bin_width.bit_length() - 1
     nbins = max(1, (nl + bin_width - 1) // bin_width)
     nblk_k = max(nblk, 1)
-    wu_e = max(1 << 15, E // 4096)
+    wu_e = max(1 << 15, E // PB_UNITS)
     n4 = (nent + 3) // 4 * 4 + PB_DUMMY
     # every entry's bin-major place is written once below (a bijection onto [0, nent)):
     # only the padding is cleared
