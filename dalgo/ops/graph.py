@@ -287,6 +287,10 @@ PB_ITEMS_MULTI = int(os.environ.get("DALGO_PB_ITEMS_MULTI", "2048"))
 # edges. Scale 26, one rank, 3 runs each: 2048 -> 1.986-1.990 ms per iteration, 4096 ->
 # 1.953-1.967, 8192 -> 2.024-2.027, 16384 -> 2.200-2.208 (profiles/round6/r6_82)
 PB_UNITS = int(os.environ.get("DALGO_PB_UNITS", "4096"))
+# wave tiles per work unit (tile length = unit edges / PB_TILES, clamped to [1024, tile]):
+# 8 -> 1.962-1.972 ms per iteration, 16 -> 1.916-1.968, 24 -> 1.990-1.995, 32 -> 1.993-2.006
+# (scale 26, one rank, profiles/round6/r6_83)
+PB_TILES = int(os.environ.get("DALGO_PB_TILES", "16"))
 
 
 @dataclass
@@ -807,7 +811,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
         ce_lo = torch.where(chunk_first > 0, ent_end[(chunk_first - 1).clamp_min(0)] + 1,
                             torch.zeros_like(chunk_first))
         ce_n = torch.diff(torch.cat([ce_lo, torch.tensor([E], **i64)]))
-        tlen = torch.clamp((torch.clamp(ce_n, max=wu_e) + 15) // 16, min=min(1024, tile), max=tile)
+        tlen = torch.clamp((torch.clamp(ce_n, max=wu_e) + PB_TILES - 1) // PB_TILES, min=min(1024, tile), max=tile)
         # tile starts: at most one per chunk start, per work-unit boundary and per tlen
         # boundary inside a unit
         cap_t = int((1 + (ce_n + wu_e - 1) // wu_e + (ce_n + tlen - 1) // tlen).sum().item())
@@ -857,7 +861,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
         ce_lo = torch.where(chunk_first > 0, ent_end[(chunk_first - 1).clamp_min(0)] + 1,
                             torch.zeros_like(chunk_first))
         ce_n = torch.diff(torch.cat([ce_lo, torch.tensor([E], **i64)]))
-        tlen = torch.clamp((torch.clamp(ce_n, max=wu_e) + 15) // 16, min=min(1024, tile), max=tile)
+        tlen = torch.clamp((torch.clamp(ce_n, max=wu_e) + PB_TILES - 1) // PB_TILES, min=min(1024, tile), max=tile)
         ts = torch.empty(nent, dtype=torch.uint8, device=dev)
         ops.gb_entry_place(ent_dst, ent_end, run_of_ent, run_delta, run_chunk, cs,
                            ce_lo, tlen, wu_e, bin_width - 1, dloc, ts)
