@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--ranks", default="0,7")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--spmv-iters", type=int, default=0,
+                    help="also time K4b (pb_spmv) over the rank's native layout, random c")
     ap.add_argument("--direct", action="store_true",
                     help="the direct shuffle (owner partition with random new_id gathers) instead "
                          "of build_rmat_sharded's source-bucketed path")
@@ -94,6 +96,25 @@ def main():
                         "degree_all_reduce_bytes": 4 * N,
                         "build_phases_ms": G.build_phase_spans()}
             G.build_marks = None
+            if a.spmv_iters and rep == a.reps and best is not None:
+                # K4b over this rank's layout (own slice + ghosts), random contributions
+                lay = ng.layout
+                c = torch.rand(ng.slice_size + ng.n_ghost, device=dev)
+                acc = torch.empty(ng.n_local, device=dev)
+                pres = torch.empty(ng.n_local, dtype=torch.int32, device=dev)
+                for _ in range(3):
+                    G.pb_spmv(lay, c, acc, pres)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                e0.record()
+                for _ in range(a.spmv_iters):
+                    G.pb_spmv(lay, c, acc, pres)
+                e1.record()
+                torch.cuda.synchronize()
+                best["k4b_ms_per_iter"] = e0.elapsed_time(e1) / a.spmv_iters
+                best["k4b_work_items"] = int(lay.wi_bin.numel())
+                best["k4b_split_bins"] = int(lay.split_bin.numel())
+                del lay, c, acc, pres
             del packed, ng, deg, nid
         res["ranks"][r] = best
         print(f"rank {r}/{W}: {best}", file=sys.stderr, flush=True)

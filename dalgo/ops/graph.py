@@ -10,6 +10,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import math
+
 import numpy as np
 import os
 
@@ -275,14 +277,18 @@ def _work_items(bin_cnt: torch.Tensor, bin_lo: torch.Tensor, nent: int, items: i
 SRC_SPAN = 8192          # sources per chunk: the LDS table of pb_gather (csrc/kernels/pr_binned.hip)
 CELL_CAP = 1 << 30       # largest (block, bin) cell matrix of the native build (4 B x 3 per cell)
 PB_DUMMY = 65536         # val / dloc padding after the entries (kPbDummy in pr_binned.hip)
-# phase-2 work items of the native build: a bin with more than nent / PB_ITEMS entries is
-# cut into pieces, each with its own 128 KB u64 slab that pb_combine sums. One rank at
-# scale 26 (4096 bins): 2048 -> 5662 items, 346 split bins, 2.037-2.045 ms per iteration;
-# 1024 -> 1.978-1.989; 768 -> 1.965-1.978 (4531 items, 155 split bins); 512 -> 1.994-1.999
-# (profiles/round6/r6_80). Several ranks keep 2048: a rank holds 1/W of the bins, so fewer
-# pieces would leave its phase 2 with few work items (not measured at W > 1)
+# phase-2 work items of the native build: a bin with more than nent / items entries is cut
+# into pieces, each with its own 128 KB u64 slab that pb_combine sums; items = PB_ITEMS /
+# sqrt(W) (a rank holds 1/W of the bins). One rank at scale 26 (4096 bins): 2048 -> 346
+# split bins, 1.99-2.05 ms per iteration; 1024 -> 1.98-1.99; 768 -> 1.96-1.97; 640 ->
+# 1.96-1.97; 512 -> 1.95-2.00 (profiles/round6/r6_80, r6_84). The W = 8 per-rank share
+# (512 bins): 2048 -> 0.48 ms, 768 -> 0.39, 384 -> 0.36, 256 -> 0.365, 192 -> 0.35,
+# 128 -> 0.37 (r6_86)
 PB_ITEMS = int(os.environ.get("DALGO_PB_ITEMS", "768"))
-PB_ITEMS_MULTI = int(os.environ.get("DALGO_PB_ITEMS_MULTI", "2048"))
+
+
+def pb_items(world: int) -> int:
+    return max(128, int(round(PB_ITEMS / math.sqrt(max(1, world)))))
 # phase-1 work units of the native build: a source chunk is cut every max(32K, E / PB_UNITS)
 # edges. Scale 26, one rank, 3 runs each: 2048 -> 1.986-1.990 ms per iteration, 4096 ->
 # 1.953-1.967, 8192 -> 2.024-2.027, 16384 -> 2.200-2.208 (profiles/round6/r6_82)
@@ -633,7 +639,7 @@ def build_native(edges: list, n_vertices: int, rank: int, world: int, new_id: to
     if bin_width not in (8192, 16384):
         raise ValueError("bin_width must be 8192 or 16384")
     if items is None:
-        items = PB_ITEMS if world == 1 else PB_ITEMS_MULTI
+        items = pb_items(world)
     ops = _ext.ops()
     dev = edges[0][0].device
     N, W = n_vertices, world
