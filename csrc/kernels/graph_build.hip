@@ -602,8 +602,10 @@ __global__ void __launch_bounds__(256) gb_keys_one_kernel(const uint64_t* __rest
 // ends at the last copy of its last key. Blocks of kDecR keys, each thread 4 consecutive
 // keys per step (coalesced), one block scan per step places the distinct edges and the
 // entries in key order.
-constexpr int kDecR = 65536;         // keys per block of the decode kernels (262144: 13.0 ->
-                                     // 14.3 ms at scale 26, profiles/round5/r5_21)
+constexpr int kDecR = 16384;         // keys per block of the decode kernels: decode phase at
+                                     // scale 26 7.4-7.8 ms (4096: 10.9-11.3, 8192: 8.4-8.6,
+                                     // 32768: 7.6, 65536: 8.5, 131072: 9.8-10.0;
+                                     // profiles/round6/r6_92)
 constexpr int kDecT = 256;
 constexpr int kDecV = 4;             // keys per thread per step (8: decode 11.3 -> 13.1 ms,
                                      // profiles/round5/r5_41)
@@ -647,6 +649,7 @@ __device__ __forceinline__ void gb_quad_flags(const GbQuad& q, int64_t ib, int64
 // per block: distinct edges, entries, and the distinct out-degree per local source (LDS
 // histogram of the block's first source block; other source blocks: global atomics)
 __global__ void __launch_bounds__(kDecT) gb_decode_count_kernel(const uint64_t* __restrict__ K, int64_t n,
+                                                                int64_t dr,
                                                                 int shift, const int64_t* __restrict__ blk_base,
                                                                 int64_t* __restrict__ counts,
                                                                 uint32_t* __restrict__ outdeg) {
@@ -655,8 +658,8 @@ __global__ void __launch_bounds__(kDecT) gb_decode_count_kernel(const uint64_t* 
   for (int j = threadIdx.x; j < kSpan; j += kDecT) hist[j] = 0u;
   if (threadIdx.x == 0) { s_d = 0; s_e = 0; }
   __syncthreads();
-  const int64_t r0 = (int64_t)blockIdx.x * kDecR;
-  const int64_t r1 = r0 + kDecR < n ? r0 + kDecR : n;
+  const int64_t r0 = (int64_t)blockIdx.x * dr;
+  const int64_t r1 = r0 + dr < n ? r0 + dr : n;
   const uint64_t blk0 = K[r0] >> shift;
   int md = 0, me = 0;
   constexpr int64_t kStep = (int64_t)kDecT * kDecV;
@@ -696,7 +699,7 @@ __global__ void __launch_bounds__(kDecT) gb_decode_count_kernel(const uint64_t* 
 
 // offsets[2 b] / [2 b + 1]: distinct edges / entries before block b
 __global__ void __launch_bounds__(kDecT) gb_decode_write_kernel(const uint64_t* __restrict__ K, int64_t n,
-                                                                int shift, int dbits,
+                                                                int64_t dr, int shift, int dbits,
                                                                 const int64_t* __restrict__ offsets,
                                                                 uint16_t* __restrict__ srcl,
                                                                 int64_t* __restrict__ ent_end,
@@ -704,8 +707,8 @@ __global__ void __launch_bounds__(kDecT) gb_decode_write_kernel(const uint64_t* 
                                                                 int32_t* __restrict__ ent_dst) {
   __shared__ int s_wd[kDecT / 64], s_we[kDecT / 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t r0 = (int64_t)blockIdx.x * kDecR;
-  const int64_t r1 = r0 + kDecR < n ? r0 + kDecR : n;
+  const int64_t r0 = (int64_t)blockIdx.x * dr;
+  const int64_t r1 = r0 + dr < n ? r0 + dr : n;
   int64_t dbase = offsets[2 * blockIdx.x], ebase = offsets[2 * blockIdx.x + 1];
   const uint64_t dmask = (1ull << dbits) - 1ull;
   constexpr int64_t kStep = (int64_t)kDecT * kDecV;
@@ -1517,7 +1520,17 @@ hipError_t dalgo_gb_pack(const int32_t* src, const int32_t* dst, int64_t n, uint
   return hipSuccess;
 }
 
-int64_t dalgo_gb_decode_blocks(int64_t n) { return cdiv(n, (int64_t)kDecR); }
+// keys per decode block: kDecR, or DALGO_GB_DEC_ROWS (a multiple of kDecT * kDecV) for A/B
+static int64_t gb_dec_rows() {
+  static int64_t v = [] {
+    const char* e = getenv("DALGO_GB_DEC_ROWS");
+    const int64_t x = e ? atoll(e) : 0;
+    return (x >= kDecT * kDecV && x % (kDecT * kDecV) == 0) ? x : (int64_t)kDecR;
+  }();
+  return v;
+}
+
+int64_t dalgo_gb_decode_blocks(int64_t n) { return cdiv(n, gb_dec_rows()); }
 
 // phase 0: counts[2 b], [2 b + 1] = distinct edges / entries of block b, outdeg += the
 // distinct out-degrees; phase 1 (offsets = exclusive scan of counts): srcl and the entries
@@ -1527,12 +1540,13 @@ hipError_t dalgo_gb_decode(const uint64_t* K, int64_t n, int shift, int dbits, c
                            hipStream_t st) {
   if (n <= 0) return hipSuccess;
   if (shift < kSpanBits || shift > 63 || dbits < 0 || dbits > 31) return hipErrorInvalidValue;
-  const int64_t g = cdiv(n, (int64_t)kDecR);
+  const int64_t dr = gb_dec_rows();
+  const int64_t g = cdiv(n, dr);
   if (phase == 0)
-    hipLaunchKernelGGL(gb_decode_count_kernel, dim3((unsigned)g), dim3(kDecT), 0, st, K, n, shift, blk_base,
+    hipLaunchKernelGGL(gb_decode_count_kernel, dim3((unsigned)g), dim3(kDecT), 0, st, K, n, dr, shift, blk_base,
                        counts, outdeg);
   else
-    hipLaunchKernelGGL(gb_decode_write_kernel, dim3((unsigned)g), dim3(kDecT), 0, st, K, n, shift, dbits,
+    hipLaunchKernelGGL(gb_decode_write_kernel, dim3((unsigned)g), dim3(kDecT), 0, st, K, n, dr, shift, dbits,
                        offsets, srcl, ent_end, ent_blk, ent_dst);
   DALGO_LAUNCH_CHECK();
   return hipSuccess;
