@@ -970,6 +970,9 @@ __global__ void __launch_bounds__(256) gb_cell_place_kernel(const int32_t* __res
   }
 }
 
+constexpr int kCellEpt = 4;          // entries per thread and step (gb_entry_cells): 4.1 ms at
+                                     // scale 26 (1: 4.9, 8: 5.2; profiles/round6/r6_93)
+
 // per entry: bin-major destination (dloc), run-start bit on the end edge of a run's first
 // entry, tile starts (a new work unit every wu_e edges of a chunk and a new tile every
 // tlen[chunk] edges of the unit, on entry boundaries; chunk starts always)
@@ -982,41 +985,77 @@ __global__ void __launch_bounds__(256) gb_entry_cells_kernel(
     int64_t ndloc, int32_t* __restrict__ tiles, unsigned long long* __restrict__ n_tiles, int64_t tile_cap,
     uint16_t* __restrict__ srcl, int64_t nsrcl) {
   const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  // (block-uniform loop: every lane reaches the ballot below)
-  for (int64_t e0 = (int64_t)blockIdx.x * 256; e0 < nent; e0 += stride) {
-    const int64_t e = e0 + threadIdx.x;
-    bool t = false;
-    if (e < nent) {
-      const int32_t b = ent_blk[e], d = ent_dst[e], bin = d >> bshift;
-      const bool okc = b >= 0 && b < nblk && bin >= 0 && bin < nbins;
-      const int64_t cell = okc ? (int64_t)b * nbins + bin : 0;
-      const int32_t q = okc ? RID[cell] : -1;
-      if (q >= 0 && q < nruns) {
-        const int64_t pos = e + run_delta[q];
-        if (pos >= 0 && pos < ndloc) dloc[pos] = (int16_t)(d & bin_mask);
-        const int64_t ee = ent_end[e];
-        if (e == CM[cell] && ee >= 0 && ee < nsrcl) srcl[ee] |= (uint16_t)0x4000;
-        const int32_t ch = CI[b];
-        t = e == RE[b];
-        if (!t && e > 0 && ch >= 0 && ch < nch) {
-          const int64_t tl = tlen[ch];
-          const int64_t a = (e > 1 ? ent_end[e - 2] + 1 : 0) - ce_lo[ch];   // entry e - 1's first edge
-          const int64_t bb = ent_end[e - 1] + 1 - ce_lo[ch];                // entry e's first edge
-          t = (a / wu_e) != (bb / wu_e) || ((a % wu_e) / tl) != ((bb % wu_e) / tl);
+  const int64_t stride = (int64_t)gridDim.x * 256 * kCellEpt;
+  // kCellEpt entries per thread and step, each level of the dependent loads (entry -> cell
+  // -> run -> chunk tables) issued for all of them before the next: one entry per thread
+  // and step left the pass latency-bound (4.7 ms at scale 26, profiles/round6/r6_48)
+  // (block-uniform loop: every lane reaches the ballots below)
+  for (int64_t e0 = (int64_t)blockIdx.x * 256 * kCellEpt; e0 < nent; e0 += stride) {
+    int64_t ev[kCellEpt], ee[kCellEpt], cell[kCellEpt];
+    int32_t bv[kCellEpt], dv[kCellEpt], q[kCellEpt], cm[kCellEpt];
+#pragma unroll
+    for (int j = 0; j < kCellEpt; ++j) {
+      ev[j] = e0 + threadIdx.x + (int64_t)j * 256;
+      const bool in = ev[j] < nent;
+      bv[j] = in ? ent_blk[ev[j]] : -1;
+      dv[j] = in ? ent_dst[ev[j]] : 0;
+      ee[j] = in ? ent_end[ev[j]] : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < kCellEpt; ++j) {
+      const int32_t bin = dv[j] >> bshift;
+      const bool okc = bv[j] >= 0 && bv[j] < nblk && bin >= 0 && bin < nbins;
+      cell[j] = okc ? (int64_t)bv[j] * nbins + bin : 0;
+      q[j] = okc ? RID[cell[j]] : -1;
+      cm[j] = okc ? CM[cell[j]] : -1;
+    }
+    bool ok[kCellEpt];
+    int32_t rd[kCellEpt], ch[kCellEpt];
+    int64_t re[kCellEpt];
+#pragma unroll
+    for (int j = 0; j < kCellEpt; ++j) {
+      ok[j] = q[j] >= 0 && q[j] < nruns;
+      rd[j] = ok[j] ? run_delta[q[j]] : 0;
+      ch[j] = ok[j] ? CI[bv[j]] : -1;
+      re[j] = ok[j] ? RE[bv[j]] : -1;
+    }
+    bool need[kCellEpt];
+    int64_t tl[kCellEpt], cl[kCellEpt], a2[kCellEpt], a1[kCellEpt];
+#pragma unroll
+    for (int j = 0; j < kCellEpt; ++j) {
+      const int64_t e = ev[j];
+      need[j] = ok[j] && e != re[j] && e > 0 && ch[j] >= 0 && ch[j] < nch;
+      tl[j] = need[j] ? tlen[ch[j]] : 1;
+      cl[j] = need[j] ? ce_lo[ch[j]] : 0;
+      a2[j] = need[j] && e > 1 ? ent_end[e - 2] : -1;
+      a1[j] = need[j] ? ent_end[e - 1] : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < kCellEpt; ++j) {
+      const int64_t e = ev[j];
+      bool t = false;
+      if (ok[j]) {
+        const int64_t pos = e + rd[j];
+        if (pos >= 0 && pos < ndloc) dloc[pos] = (int16_t)(dv[j] & bin_mask);
+        if (e == cm[j] && ee[j] >= 0 && ee[j] < nsrcl) srcl[ee[j]] |= (uint16_t)0x4000;
+        t = e == re[j];
+        if (need[j]) {
+          const int64_t a = a2[j] + 1 - cl[j];                    // entry e - 1's first edge
+          const int64_t bb = a1[j] + 1 - cl[j];                   // entry e's first edge
+          t = (a / wu_e) != (bb / wu_e) || ((a % wu_e) / tl[j]) != ((bb % wu_e) / tl[j]);
         }
       }
-    }
-    // tile starts -> an unordered list (one global atomic per wave that has any; sorted
-    // on the host side afterwards): no per-entry flag array, no compaction pass
-    const uint64_t m = __ballot(t);
-    if (m != 0ull) {
-      unsigned long long base = 0;
-      if (lane == 0) base = atomicAdd(n_tiles, (unsigned long long)__popcll(m));
-      base = __shfl(base, 0);
-      if (t) {
-        const long long slot = (long long)base + __popcll(m & ((1ull << lane) - 1ull));
-        if (slot < tile_cap) tiles[slot] = (int32_t)e;
+      // tile starts -> an unordered list (one global atomic per wave that has any; sorted
+      // on the host side afterwards): no per-entry flag array, no compaction pass
+      const uint64_t m = __ballot(t);
+      if (m != 0ull) {
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(n_tiles, (unsigned long long)__popcll(m));
+        base = __shfl(base, 0);
+        if (t) {
+          const long long slot = (long long)base + __popcll(m & ((1ull << lane) - 1ull));
+          if (slot < tile_cap) tiles[slot] = (int32_t)e;
+        }
       }
     }
   }
@@ -1625,7 +1664,7 @@ hipError_t dalgo_gb_entry_cells(const int32_t* ent_blk, const int32_t* ent_dst, 
                                 int64_t tile_cap, uint16_t* srcl, int64_t nsrcl, hipStream_t st) {
   if (nent <= 0) return hipSuccess;
   if (wu_e < 1 || nent >= (int64_t)0x7fffffffLL) return hipErrorInvalidValue;
-  const int64_t g = std::min<int64_t>(cdiv(nent, 256), 256 * 64);
+  const int64_t g = std::min<int64_t>(cdiv(nent, 256 * kCellEpt), 256 * 64);
   hipLaunchKernelGGL(gb_entry_cells_kernel, dim3((unsigned)g), dim3(256), 0, st, ent_blk, ent_dst, ent_end, nent,
                      bshift, nblk, nbins, CM, RID, run_delta, nruns, RE, CI, ce_lo, tlen, nch, wu_e, bin_mask, dloc,
                      ndloc, tiles, n_tiles, tile_cap, srcl, nsrcl);
