@@ -826,28 +826,42 @@ __global__ void __launch_bounds__(256) gb_entry_place_kernel(const int32_t* __re
 // its index, and a column-major scan gives its bin-major position -- no per-entry scans,
 // sorts or searches (nblk x nbins cells: 33.5M at R-MAT scale 26 on one rank).
 
+constexpr int kCellEpt = 4;          // entries per thread and step (gb_cell_count, gb_entry_cells): 4.1 ms at
+                                     // scale 26 (1: 4.9, 8: 5.2; profiles/round6/r6_93)
+
 // C[cell] += entries of the cell; one atomic per run of equal cells inside a wave
 __global__ void __launch_bounds__(256) gb_cell_count_kernel(const int32_t* __restrict__ ent_blk,
                                                             const int32_t* __restrict__ ent_dst, int64_t nent,
                                                             int bshift, int nblk, int nbins,
                                                             int32_t* __restrict__ C) {
   const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t e0 = (int64_t)blockIdx.x * 256; e0 < nent; e0 += stride) {
-    const int64_t e = e0 + threadIdx.x;
-    const bool in = e < nent;
-    int64_t cell = -1;
-    if (in) {
-      const int32_t b = ent_blk[e], bin = ent_dst[e] >> bshift;
-      if (b >= 0 && b < nblk && bin >= 0 && bin < nbins) cell = (int64_t)b * nbins + bin;
+  const int64_t stride = (int64_t)gridDim.x * 256 * kCellEpt;
+  // kCellEpt entries per thread and step, all loads issued first (as gb_entry_cells)
+  for (int64_t e0 = (int64_t)blockIdx.x * 256 * kCellEpt; e0 < nent; e0 += stride) {
+    int32_t bv[kCellEpt], dv[kCellEpt];
+#pragma unroll
+    for (int j = 0; j < kCellEpt; ++j) {
+      const int64_t e = e0 + threadIdx.x + (int64_t)j * 256;
+      bv[j] = e < nent ? ent_blk[e] : -1;
+      dv[j] = e < nent ? ent_dst[e] : 0;
     }
-    const int64_t prev = __shfl_up(cell, 1, 64);
-    const bool head = cell >= 0 && (lane == 0 || prev != cell);
-    const uint64_t hm = __ballot(head), vm = __ballot(in);
-    if (head) {
-      const uint64_t above = hm & ~((2ull << lane) - 1ull);   // heads after this lane
-      const int end = above ? __ffsll((long long)above) - 1 : 64 - __clzll((long long)vm);
-      atomicAdd(C + cell, end - lane);
+#pragma unroll
+    for (int j = 0; j < kCellEpt; ++j) {
+      const int64_t e = e0 + threadIdx.x + (int64_t)j * 256;
+      const bool in = e < nent;
+      int64_t cell = -1;
+      if (in) {
+        const int32_t b = bv[j], bin = dv[j] >> bshift;
+        if (b >= 0 && b < nblk && bin >= 0 && bin < nbins) cell = (int64_t)b * nbins + bin;
+      }
+      const int64_t prev = __shfl_up(cell, 1, 64);
+      const bool head = cell >= 0 && (lane == 0 || prev != cell);
+      const uint64_t hm = __ballot(head), vm = __ballot(in);
+      if (head) {
+        const uint64_t above = hm & ~((2ull << lane) - 1ull);   // heads after this lane
+        const int end = above ? __ffsll((long long)above) - 1 : 64 - __clzll((long long)vm);
+        atomicAdd(C + cell, end - lane);
+      }
     }
   }
 }
@@ -969,9 +983,6 @@ __global__ void __launch_bounds__(256) gb_cell_place_kernel(const int32_t* __res
     }
   }
 }
-
-constexpr int kCellEpt = 4;          // entries per thread and step (gb_entry_cells): 4.1 ms at
-                                     // scale 26 (1: 4.9, 8: 5.2; profiles/round6/r6_93)
 
 // per entry: bin-major destination (dloc), run-start bit on the end edge of a run's first
 // entry, tile starts (a new work unit every wu_e edges of a chunk and a new tile every
@@ -1626,7 +1637,7 @@ hipError_t dalgo_gb_cells(int phase, const int32_t* ent_blk, const int32_t* ent_
   switch (phase) {
     case 0: {   // counts
       if (nent <= 0) return hipSuccess;
-      const int64_t g = std::min<int64_t>(cdiv(nent, 256), 256 * 64);
+      const int64_t g = std::min<int64_t>(cdiv(nent, 256 * kCellEpt), 256 * 64);
       hipLaunchKernelGGL(gb_cell_count_kernel, dim3((unsigned)g), dim3(256), 0, st, ent_blk, ent_dst, nent, bshift,
                          nblk, nbins, C);
       break;
